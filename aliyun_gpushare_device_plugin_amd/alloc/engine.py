@@ -1,0 +1,296 @@
+"""The Allocate engine — the core of GPU sharing (component C5).
+
+Reference ``pkg/gpu/nvidia/allocate.go:43-201``:
+1. request size = number of fake IDs across the request (``:55-57``);
+2. under the plugin-wide mutex (``:60-61``) LIST this node's pending pods, keep "assumed"
+   ones, order by assume time (``:63-67``);
+3. pick the first whose summed container ``gpu-mem`` equals the request (``:79-89``);
+4. read the extender's GPU index from ``ALIYUN_COM_GPU_MEM_IDX`` (``:92-111``), answer with
+   env vars (``:114-129``) and PATCH the pod ``ASSIGNED=true`` (one retry, ``:132-152``);
+5. fallbacks: single-GPU node → GPU 0 without a pod (``:154-181``); otherwise an
+   error-shaped *successful* response (``:182-187``, ``buildErrResponse`` ``:25-40``).
+
+MI355X build, same protocol, different mechanics:
+* the mutex covers only the in-memory match + claim (µs); the PATCH runs outside it, with
+  a local claim set so concurrent Allocates never pick the same pod (quirk 7);
+* candidates come from a ``PodSource`` — by default a watch cache, with one fresh LIST on a
+  miss;
+* the response injects ``/dev/kfd`` + the GPU's render node as ``DeviceSpec``s and the HIP
+  quota shim as a read-only ``Mount`` + ``LD_PRELOAD`` — there is no NVIDIA runtime hook;
+* multi-container pods are matched container by container (quirk 3) after the
+  reference's pod-total rule has been tried;
+* conflicts are detected by HTTP status, not by comparing error strings (quirk 8);
+* ``--strict-allocate`` returns a gRPC error instead of the soft failure (quirk 6).
+"""
+from __future__ import annotations
+
+import dataclasses
+import os
+import threading
+import time
+
+from .. import const
+from ..api import v1beta1 as api
+from ..cluster import objects as O
+from ..cluster.client import APIClient, APIError
+from ..cluster.podcache import PodSource
+from ..device.model import DeviceModel, real_device_id
+from ..quota import ShimConfig, ledger_name
+from ..utils import log
+from ..utils.metrics import PluginMetrics
+from . import annotations as A
+
+
+class AllocationError(Exception):
+    """Raised only in strict mode; the gRPC layer maps it to FAILED_PRECONDITION."""
+
+
+@dataclasses.dataclass
+class AllocatorOptions:
+    unit: str = const.GIB
+    disable_cgpu: bool = False
+    shim: ShimConfig | None = None
+    strict: bool = False
+    expose_devices: bool = True
+    rocr_visible: bool = False
+    match_containers: bool = True
+    claim_ttl_s: float = 120.0
+
+
+@dataclasses.dataclass
+class _Claim:
+    uid: str
+    pod: dict
+    gpu_index: int
+    next_container: int
+    gpu_containers: list   # indices of containers that request gpu-mem
+    t: float
+
+
+class Allocator:
+    def __init__(self, model: DeviceModel, pods: PodSource, client: APIClient | None, node: str,
+                 opts: AllocatorOptions | None = None, metrics: PluginMetrics | None = None):
+        self.model, self.pods, self.client, self.node = model, pods, client, node
+        self.opts = opts or AllocatorOptions()
+        self.metrics = metrics or PluginMetrics()
+        self._mu = threading.Lock()
+        self._claims: dict[str, _Claim] = {}      # in-flight (multi-container or PATCH pending)
+        self._assigned: dict[str, float] = {}     # uid -> time we assigned it (stale-cache guard)
+
+    # ------------------------------------------------------------------------------------
+    # candidate selection
+    # ------------------------------------------------------------------------------------
+    def _candidates(self, fresh: bool) -> list[dict]:
+        pods = A.dedupe_by_uid(self.pods.pending_pods(fresh=fresh), self.node)
+        now = time.monotonic()
+        for u, t in list(self._assigned.items()):
+            if now - t > self.opts.claim_ttl_s:
+                del self._assigned[u]
+        out = [p for p in pods if A.is_assumed_pod(p) and O.uid(p) not in self._assigned]
+        if log.V(4):
+            for p in out:
+                log.info("candidate pod %s in ns %s with timestamp %d is found.", O.name(p), O.namespace(p),
+                         A.assume_time(p))
+        return A.order_by_assume_time(out)
+
+    def _match(self, req_units: int, fresh: bool) -> tuple[_Claim | None, bool]:
+        """Returns (claim, complete). ``complete`` = every gpu container of the pod is now
+        allocated, so the pod must be PATCHed ASSIGNED."""
+        # 1) continue a multi-container pod already in progress (container order = kubelet order)
+        for c in sorted(self._claims.values(), key=lambda c: A.assume_time(c.pod)):
+            if c.next_container < len(c.gpu_containers):
+                want = O.container_limit(O.containers(c.pod)[c.gpu_containers[c.next_container]])
+                if want == req_units:
+                    c.next_container += 1
+                    return c, c.next_container == len(c.gpu_containers)
+        cands = [p for p in self._candidates(fresh) if O.uid(p) not in self._claims]
+        # 2) the reference rule: pod-total equals the request
+        for p in cands:
+            if O.gpu_mem_of_pod(p) == req_units:
+                gc = [i for i, v in enumerate(O.gpu_mem_per_container(p)) if v > 0]
+                c = _Claim(O.uid(p), p, A.gpu_id_from_annotation(p), len(gc), gc, time.monotonic())
+                return c, True
+        # 3) multi-container pods: first gpu container's request equals this request
+        if self.opts.match_containers:
+            for p in cands:
+                per = O.gpu_mem_per_container(p)
+                gc = [i for i, v in enumerate(per) if v > 0]
+                if len(gc) > 1 and per[gc[0]] == req_units:
+                    c = _Claim(O.uid(p), p, A.gpu_id_from_annotation(p), 1, gc, time.monotonic())
+                    self._claims[c.uid] = c
+                    return c, False
+        return None, False
+
+    # ------------------------------------------------------------------------------------
+    # response building
+    # ------------------------------------------------------------------------------------
+    def _container_response(self, gpu_index: int, pod_units: int, ctr_units: int, pod_uid: str,
+                            slot: int) -> api.ContainerAllocateResponse:
+        g = self.model.gpu(gpu_index)
+        envs = {
+            const.ENV_RESOURCE_INDEX: str(gpu_index),
+            const.ENV_RESOURCE_BY_POD: str(pod_units),
+            const.ENV_RESOURCE_BY_CONTAINER: str(ctr_units),
+            const.ENV_RESOURCE_BY_DEV: str(g.units),
+            const.ENV_GPU_UUID: g.uuid,
+        }
+        r = api.ContainerAllocateResponse(envs=envs)
+        if self.opts.disable_cgpu:
+            r.envs[const.ENV_CGPU_DISABLE] = "true"
+        if self.opts.rocr_visible:
+            r.envs[const.ENV_ROCR_VISIBLE] = g.uuid
+        if self.opts.expose_devices:
+            r.devices.add(container_path=const.KFD_DEVICE, host_path=const.KFD_DEVICE, permissions="rw")
+            if g.render_node:
+                r.devices.add(container_path=g.render_node, host_path=g.render_node, permissions="rw")
+        shim = self.opts.shim
+        if shim is not None and shim.enabled and not self.opts.disable_cgpu:
+            r.mounts.add(container_path=shim.container_dir, host_path=shim.host_dir, read_only=True)
+            r.envs[const.ENV_LD_PRELOAD] = shim.container_lib
+            r.envs[const.ENV_SHIM_LEDGER] = ledger_name(pod_uid or f"{gpu_index}-{time.time_ns()}", slot)
+        return r
+
+    def _err_response(self, req, pod_units: int) -> api.AllocateResponse:
+        """``buildErrResponse`` (``allocate.go:25-40``) minus the NVIDIA env: no device node is
+        handed out, so a misallocated container cannot touch a GPU it was not given."""
+        if self.opts.strict:
+            raise AllocationError(f"no-gpu-has-{pod_units}{self.opts.unit}-to-run")
+        resp = api.AllocateResponse()
+        for creq in req.container_requests:
+            resp.container_responses.add(envs={
+                "GPUSHARE_ALLOCATION_ERROR": f"no-gpu-has-{pod_units}{self.opts.unit}-to-run",
+                const.ENV_RESOURCE_INDEX: "-1",
+                const.ENV_RESOURCE_BY_POD: str(pod_units),
+                const.ENV_RESOURCE_BY_CONTAINER: str(len(creq.devices_ids)),
+                const.ENV_RESOURCE_BY_DEV: str(self.model.dev_units()),
+            })
+        self.metrics.allocate_outcomes.inc(outcome="error")
+        return resp
+
+    # ------------------------------------------------------------------------------------
+    # RPCs
+    # ------------------------------------------------------------------------------------
+    def allocate(self, req) -> api.AllocateResponse:
+        t0 = time.perf_counter()
+        pod_units = sum(len(c.devices_ids) for c in req.container_requests)
+        log.info("----Allocating GPU for gpu mem is started---- RequestPodGPUs: %d", pod_units)
+        hist = self.metrics.allocate_latency
+        try:
+            with self._mu:
+                claim, complete = self._match(pod_units, fresh=False)
+                t1 = time.perf_counter()
+                if claim is None:
+                    # watch lag: the kubelet may see a bind before our cache does
+                    claim, complete = self._match(pod_units, fresh=True)
+                if claim is not None and complete:
+                    self._claims[claim.uid] = claim   # held across the PATCH
+                t2 = time.perf_counter()
+            hist.observe(t1 - t0, phase="lookup")
+            hist.observe(t2 - t1, phase="decide")
+        except Exception as e:  # noqa: BLE001 - pod listing failures
+            log.info("invalid allocation request: Failed to find candidate pods due to %s", e)
+            return self._err_response(req, pod_units)
+
+        if claim is None:
+            self.metrics.pending_match_failures.inc()
+            if self.model.count() == 1:
+                g = self.model.gpu(0)
+                log.info("this node has only one gpu device, skip to search pod and directly specify the "
+                         "device %d(%s) for container", 0, g.uuid)
+                resp = api.AllocateResponse()
+                for i, creq in enumerate(req.container_requests):
+                    resp.container_responses.append(self._container_response(0, pod_units, len(creq.devices_ids),
+                                                                             "", i))
+                self.metrics.allocate_outcomes.inc(outcome="single_gpu")
+                hist.observe(time.perf_counter() - t0, phase="total")
+                return resp
+            log.warning("invalid allocation request: request GPU memory %d can't be satisfied.", pod_units)
+            return self._err_response(req, pod_units)
+
+        idx = claim.gpu_index
+        if self.model.gpu(idx) is None:
+            log.warning("Failed to find the dev for pod %s because it's not able to find dev with index %d",
+                        O.name(claim.pod), idx)
+            with self._mu:
+                self._claims.pop(claim.uid, None)
+            return self._err_response(req, pod_units)
+
+        pod_total = O.gpu_mem_of_pod(claim.pod)
+        resp = api.AllocateResponse()
+        slot0 = claim.next_container - len(req.container_requests)
+        for i, creq in enumerate(req.container_requests):
+            resp.container_responses.append(self._container_response(idx, pod_total, len(creq.devices_ids),
+                                                                     claim.uid, max(0, slot0 + i)))
+        if not complete:
+            log.info("pod %s: container %d/%d of a multi-container pod allocated on GPU %d", O.name(claim.pod),
+                     claim.next_container, len(claim.gpu_containers), idx)
+            self.metrics.allocate_outcomes.inc(outcome="partial")
+            hist.observe(time.perf_counter() - t0, phase="total")
+            return resp
+
+        t3 = time.perf_counter()
+        try:
+            updated = self._patch_assigned(claim.pod)
+        except Exception as e:  # noqa: BLE001
+            log.warning("Failed due to %s", e)
+            with self._mu:
+                self._claims.pop(claim.uid, None)
+            return self._err_response(req, pod_units)
+        t4 = time.perf_counter()
+        with self._mu:
+            self._claims.pop(claim.uid, None)
+            self._assigned[claim.uid] = time.monotonic()
+        if updated:
+            self.pods.observe(updated)
+        hist.observe(t4 - t3, phase="patch")
+        hist.observe(time.perf_counter() - t0, phase="total")
+        self.metrics.allocate_outcomes.inc(outcome="assigned")
+        log.info("pod %s, new allocated GPUs info: gpu index %d uuid %s", O.name(claim.pod), idx,
+                 self.model.uuid_by_index(idx))
+        return resp
+
+    def _patch_assigned(self, pod: dict) -> dict | None:
+        if self.client is None:
+            return None
+        patch = A.assigned_patch()
+        ns, nm = O.namespace(pod), O.name(pod)
+        try:
+            return self.client.patch_pod(ns, nm, patch)
+        except APIError as e:
+            if e.conflict:  # optimistic-lock conflict: retry once (allocate.go:140-147)
+                return self.client.patch_pod(ns, nm, patch)
+            raise
+
+    def preferred(self, req) -> api.PreferredAllocationResponse:
+        """``GetPreferredAllocation`` — the reference panics (``server.go:37-40``). Here: prefer
+        fake IDs that belong to the GPU the extender chose for the oldest matching pending
+        pod, so the kubelet's device checkpoint names the physical GPU actually used."""
+        resp = api.PreferredAllocationResponse()
+        try:
+            with self._mu:
+                cands = self._candidates(fresh=False)
+        except Exception:  # noqa: BLE001
+            cands = []
+        for creq in req.container_requests:
+            size = creq.allocation_size
+            avail = list(creq.available_deviceIDs)
+            must = list(creq.must_include_deviceIDs)
+            target = None
+            for p in cands:
+                if O.gpu_mem_of_pod(p) == size or (O.gpu_mem_per_container(p) or [0])[0] == size:
+                    target = self.model.uuid_by_index(A.gpu_id_from_annotation(p))
+                    break
+            picked = list(must)
+            pool = [d for d in avail if d not in set(must)]
+            if target:
+                pool.sort(key=lambda d: real_device_id(d) != target)
+            for d in pool:
+                if len(picked) >= size:
+                    break
+                picked.append(d)
+            resp.container_responses.add(deviceIDs=picked[:max(size, len(must))])
+        return resp
+
+
+def env_shim_host_dir() -> str | None:
+    return os.environ.get("GPUSHARE_SHIM_HOST_DIR")

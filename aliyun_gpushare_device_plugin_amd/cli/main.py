@@ -1,0 +1,94 @@
+"""``gpushare-device-plugin`` entry point (components C5/C12; reference ``cmd/nvidia/main.go``).
+
+Reference flags are kept with the same names and defaults (``main.go:15-26``) so existing
+DaemonSet manifests work unchanged; glog's ``-logtostderr`` and ``--v`` are accepted.
+New flags select the SMI backend, rounding policy, pod source, quota shim, topology export
+and metrics endpoint.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+
+from .. import const
+from ..plugin.manager import PluginConfig, SharedGPUManager
+from ..utils import log, units
+
+
+def _bool(v: str) -> bool:
+    return str(v).lower() in ("1", "true", "t", "yes", "y", "")
+
+
+def build_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(prog="gpushare-device-plugin",
+                                description="MI355X GPU-sharing device plugin (aliyun.com/gpu-mem)")
+    # --- reference flags (cmd/nvidia/main.go:15-26) ---
+    p.add_argument("--mps", nargs="?", const="true", default="false", help="accepted and ignored")
+    p.add_argument("--health-check", nargs="?", const="true", default="true",
+                   help="enable GPU health monitoring (SMI events + polling)")
+    p.add_argument("--memory-unit", default=const.GIB, help="GiB or MiB")
+    p.add_argument("--query-kubelet", nargs="?", const="true", default="false",
+                   help="source pending pods from the kubelet /pods endpoint")
+    p.add_argument("--kubelet-address", default="0.0.0.0")
+    p.add_argument("--kubelet-port", type=int, default=10250)
+    p.add_argument("--client-cert", default="")
+    p.add_argument("--client-key", default="")
+    p.add_argument("--token", default="")
+    p.add_argument("--timeout", type=int, default=10, help="kubelet/apiserver HTTP timeout (s)")
+    # --- glog compatibility ---
+    p.add_argument("-logtostderr", "--logtostderr", nargs="?", const="true", default="true")
+    p.add_argument("-v", "--v", type=int, default=int(os.environ.get("GPUSHARE_V", "0")))
+    p.add_argument("--log-json", action="store_true")
+    # --- MI355X additions ---
+    p.add_argument("--smi-backend", default="auto", help="auto | rocm_smi | sysfs[:root] | fake:<N>x<SIZE> | fake:<json>")
+    p.add_argument("--round", dest="round_policy", choices=units.ROUND_POLICIES, default="nearest",
+                   help="bytes->units rounding (nearest advertises the nominal 288 GiB of an MI355X)")
+    p.add_argument("--heterogeneous", action="store_true",
+                   help="advertise each GPU's own units instead of the node minimum")
+    p.add_argument("--pod-source", choices=("watch", "list", "kubelet"), default="watch")
+    p.add_argument("--device-plugin-dir", default=const.DEVICE_PLUGIN_PATH)
+    p.add_argument("--kubeconfig", default=None)
+    p.add_argument("--apiserver", default=None, help="apiserver URL (overrides kubeconfig/in-cluster)")
+    p.add_argument("--node-name", default=os.environ.get(const.ENV_NODE_NAME, ""))
+    p.add_argument("--gpu-indices", default="", help="comma-separated subset of GPUs to manage")
+    p.add_argument("--shim-path", default=os.environ.get("GPUSHARE_SHIM_HOST_DIR", ""),
+                   help="host directory containing libgpushare_hipquota.so to inject (empty: no shim)")
+    p.add_argument("--strict-allocate", action="store_true",
+                   help="fail Allocate with a gRPC error instead of an error-shaped response")
+    p.add_argument("--no-preferred-allocation", action="store_true")
+    p.add_argument("--export-topology", nargs="?", const="true", default="true")
+    p.add_argument("--rocr-visible-devices", action="store_true",
+                   help="also set ROCR_VISIBLE_DEVICES=<uuid> in containers")
+    p.add_argument("--metrics-addr", default=None, help="host:port for /metrics and /healthz")
+    p.add_argument("--health-poll", type=float, default=5.0)
+    return p
+
+
+def config_from_args(a) -> PluginConfig:
+    return PluginConfig(
+        node_name=a.node_name, memory_unit=units.normalize_unit(a.memory_unit), round_policy=a.round_policy,
+        homogeneous=not a.heterogeneous, health_check=_bool(a.health_check), health_poll_s=a.health_poll,
+        pod_source=a.pod_source, query_kubelet=_bool(a.query_kubelet), kubelet_address=a.kubelet_address,
+        kubelet_port=a.kubelet_port, client_cert=a.client_cert, client_key=a.client_key, token=a.token,
+        timeout=float(a.timeout), smi_backend=a.smi_backend, device_plugin_dir=a.device_plugin_dir,
+        kubeconfig=a.kubeconfig, apiserver=a.apiserver,
+        gpu_indices=[int(x) for x in a.gpu_indices.split(",") if x.strip()] or None,
+        shim_host_dir=a.shim_path or None, strict_allocate=a.strict_allocate,
+        preferred_allocation=not a.no_preferred_allocation, export_topology=_bool(a.export_topology),
+        rocr_visible=a.rocr_visible_devices, metrics_addr=a.metrics_addr, mps=_bool(a.mps))
+
+
+def main(argv=None) -> int:
+    a = build_parser().parse_args(argv)
+    log.setup(verbosity=a.v, json_lines=a.log_json)
+    log.V(1).info("Start gpushare device plugin")
+    cfg = config_from_args(a)
+    if not cfg.node_name:
+        log.error("Please set env NODE_NAME (or --node-name)")
+        return 1
+    return SharedGPUManager(cfg).run()
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,193 @@
+"""Node-local pending-pod sources for Allocate (components C6 + C8 call sites).
+
+Reference: every Allocate does a fresh LIST of ``spec.nodeName=<node>,status.phase=Pending``
+pods (≤3 retries × 1 s, ``podmanager.go:227-245``) or, with ``--query-kubelet``, a GET of the
+kubelet's ``/pods`` filtered client-side (≤8 retries × 100 ms then LIST fallback,
+``podmanager.go:187-225``), dedupes by UID (``:273-291``), keeps "assumed" pods
+(``podutils.go:78-119``) and sorts by assume time (``:326-347``).
+
+``WatchCache`` is the MI355X build's main latency lever: a LIST+WATCH informer
+of this node's pods, so the per-Allocate LIST becomes an in-memory lookup and only the
+PATCH remains on the network path. Correctness under watch lag: a cache miss falls back to
+one fresh LIST (``PodSource.candidates(fresh=True)``) and locally-written pods are folded
+back into the cache from the PATCH response, so a just-assigned pod is never matched twice.
+"""
+from __future__ import annotations
+
+import threading
+import time
+
+from ..utils import log
+from . import objects as O
+from .client import APIClient, APIError
+
+
+def node_field_selector(node: str, pending_only: bool = False) -> str:
+    s = f"spec.nodeName={node}"
+    return s + ",status.phase=Pending" if pending_only else s
+
+
+class PodSource:
+    """Strategy interface: returns this node's pending pods."""
+
+    def pending_pods(self, fresh: bool = False) -> list[dict]:
+        raise NotImplementedError
+
+    def observe(self, pod: dict) -> None:
+        """Feed back an object we wrote (PATCH response)."""
+
+    def start(self):
+        return self
+
+    def stop(self):
+        pass
+
+
+class ListSource(PodSource):
+    """The reference's default path: LIST the apiserver on every call."""
+
+    def __init__(self, client: APIClient, node: str, retries: int = 3, retry_sleep: float = 1.0):
+        self.client, self.node, self.retries, self.retry_sleep = client, node, retries, retry_sleep
+
+    def pending_pods(self, fresh: bool = False) -> list[dict]:
+        sel = node_field_selector(self.node, pending_only=True)
+        err = None
+        for i in range(self.retries + 1):
+            try:
+                items, _ = self.client.list_pods(field_selector=sel)
+                return items
+            except (APIError, OSError) as e:
+                err = e
+                if i < self.retries:
+                    time.sleep(self.retry_sleep)
+        raise RuntimeError(f"failed to get Pods assigned to node {self.node}: {err}")
+
+
+class KubeletSource(PodSource):
+    """``--query-kubelet``: kubelet ``/pods`` then apiserver fallback.
+
+    Unlike the reference, "no Pending pods" is a valid answer, not an error to retry 8 × 100 ms
+    (SURVEY §2.4.9): we retry only transport errors, then fall back to the apiserver.
+    """
+
+    def __init__(self, kubelet_client, fallback: ListSource, retries: int = 8, retry_sleep: float = 0.1):
+        self.kubelet, self.fallback, self.retries, self.retry_sleep = kubelet_client, fallback, retries, retry_sleep
+
+    def pending_pods(self, fresh: bool = False) -> list[dict]:
+        for i in range(self.retries + 1):
+            try:
+                pods = self.kubelet.get_node_running_pods()
+                return [p for p in pods if O.phase(p) == "Pending"]
+            except Exception as e:  # noqa: BLE001 - transport errors of any kind
+                log.warning("failed to get pending pod list from kubelet (%s), retry", e)
+                time.sleep(self.retry_sleep)
+        log.warning("not found from kubelet /pods api, start to list apiserver")
+        return self.fallback.pending_pods(fresh=True)
+
+
+class WatchCache(PodSource):
+    """LIST+WATCH informer over ``spec.nodeName=<node>`` pods."""
+
+    def __init__(self, client: APIClient, node: str, fallback: ListSource | None = None,
+                 watch_timeout: int = 300, on_event=None):
+        self.client, self.node = client, node
+        self.fallback = fallback or ListSource(client, node, retries=1, retry_sleep=0.05)
+        self.watch_timeout = watch_timeout
+        self.on_event = on_event
+        self._pods: dict[str, dict] = {}
+        self._lock = threading.Lock()
+        self._synced = threading.Event()
+        self._stop = threading.Event()
+        self._thread = None
+        self._rv = ""
+        self.relists = 0
+        self.events = 0
+
+    # -- informer loop --------------------------------------------------------------------
+    def start(self):
+        self._thread = threading.Thread(target=self._run, name="pod-watch", daemon=True)
+        self._thread.start()
+        return self
+
+    def stop(self):
+        self._stop.set()
+
+    def wait_synced(self, timeout: float = 10.0) -> bool:
+        return self._synced.wait(timeout)
+
+    def _relist(self):
+        items, rv = self.client.list_pods(field_selector=node_field_selector(self.node))
+        with self._lock:
+            self._pods = {O.uid(p): p for p in items}
+            self._rv = rv
+        self.relists += 1
+        self._synced.set()
+
+    def _apply(self, ev: dict):
+        typ, obj = ev.get("type"), ev.get("object") or {}
+        if typ == "BOOKMARK":
+            self._rv = O.resource_version(obj) or self._rv
+            return
+        if typ == "ERROR":
+            code = obj.get("code")
+            raise APIError(code or 500, obj.get("reason", "watch error"), obj.get("message", ""), obj)
+        u = O.uid(obj)
+        with self._lock:
+            if typ == "DELETED" or O.node_name(obj) != self.node:
+                self._pods.pop(u, None)
+            else:
+                cur = self._pods.get(u)
+                if cur is None or O.rv_int(O.resource_version(obj)) >= O.rv_int(O.resource_version(cur)):
+                    self._pods[u] = obj
+            self._rv = O.resource_version(obj) or self._rv
+        self.events += 1
+        if self.on_event:
+            self.on_event(typ)
+
+    def _run(self):
+        backoff = 0.05
+        while not self._stop.is_set():
+            try:
+                if not self._synced.is_set() or not self._rv:
+                    self._relist()
+                for ev in self.client.watch_pods(node_field_selector(self.node), self._rv,
+                                                 self.watch_timeout, self._stop):
+                    self._apply(ev)
+                backoff = 0.05
+            except APIError as e:
+                if e.gone:  # resourceVersion too old: relist
+                    self._synced.clear()
+                    self._rv = ""
+                else:
+                    log.warning("pod watch error: %s", e)
+                    time.sleep(backoff)
+                    backoff = min(backoff * 2, 5.0)
+            except Exception as e:  # noqa: BLE001 - connection loss etc.
+                if self._stop.is_set():
+                    break
+                log.warning("pod watch interrupted: %s", e)
+                time.sleep(backoff)
+                backoff = min(backoff * 2, 5.0)
+
+    # -- PodSource ------------------------------------------------------------------------
+    def pending_pods(self, fresh: bool = False) -> list[dict]:
+        if fresh or not self._synced.is_set():
+            items = self.fallback.pending_pods(fresh=True)
+            for p in items:
+                self.observe(p)
+            return items
+        with self._lock:
+            return [p for p in self._pods.values() if O.phase(p) == "Pending"]
+
+    def observe(self, pod: dict) -> None:
+        if not pod or O.node_name(pod) != self.node:
+            return
+        u = O.uid(pod)
+        with self._lock:
+            cur = self._pods.get(u)
+            if cur is None or O.rv_int(O.resource_version(pod)) >= O.rv_int(O.resource_version(cur)):
+                self._pods[u] = pod
+
+    def snapshot(self) -> list[dict]:
+        with self._lock:
+            return list(self._pods.values())

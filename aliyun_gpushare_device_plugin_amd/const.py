@@ -1,0 +1,84 @@
+"""Wire contract shared with the kubelet, the gpushare-scheduler-extender and workloads.
+
+Every name here is part of the compatibility surface of the reference plugin and must not
+change spelling (reference: ``pkg/gpu/nvidia/const.go:10-36``, ``cmd/inspect/main.go:13-26``,
+``device-plugin-ds.yaml:17,23-24``). AMD-specific additions live at the bottom and are
+clearly namespaced so that an extender unaware of them keeps working.
+"""
+from __future__ import annotations
+
+import os
+
+# --- extended resources (const.go:11-12) -------------------------------------------------
+RESOURCE_NAME = "aliyun.com/gpu-mem"          # device-plugin managed: Σ GPUs × units/GPU
+RESOURCE_COUNT = "aliyun.com/gpu-count"       # node-status patched: number of physical GPUs
+
+# --- kubelet device-plugin API v1beta1 (k8s.io/kubelet v0.28, go.mod:14) ------------------
+API_VERSION = "v1beta1"
+DEVICE_PLUGIN_PATH = "/var/lib/kubelet/device-plugins/"
+KUBELET_SOCKET_NAME = "kubelet.sock"
+PLUGIN_SOCKET_NAME = "aliyungpushare.sock"    # const.go:13 (serverSock basename)
+HEALTHY = "Healthy"
+UNHEALTHY = "Unhealthy"
+
+# Fake device id "<UUID>-_-<j>" (nvidia.go:23-29)
+FAKE_ID_SEP = "-_-"
+
+# --- pod annotations written by the extender / plugin (const.go:25-31) --------------------
+ENV_RESOURCE_INDEX = "ALIYUN_COM_GPU_MEM_IDX"
+ENV_RESOURCE_BY_POD = "ALIYUN_COM_GPU_MEM_POD"
+ENV_RESOURCE_BY_CONTAINER = "ALIYUN_COM_GPU_MEM_CONTAINER"
+ENV_RESOURCE_BY_DEV = "ALIYUN_COM_GPU_MEM_DEV"
+ENV_ASSIGNED_FLAG = "ALIYUN_COM_GPU_MEM_ASSIGNED"
+ENV_RESOURCE_ASSUME_TIME = "ALIYUN_COM_GPU_MEM_ASSUME_TIME"
+ENV_RESOURCE_ASSIGN_TIME = "ALIYUN_COM_GPU_MEM_ASSIGN_TIME"
+# newer extender: {"<containerIdx>": {"<gpuIdx>": mem}} (cmd/inspect/main.go:25)
+GPUSHARE_ALLOCATION_FLAG = "scheduler.framework.gpushare.allocation"
+
+# --- node label / container env (const.go:32, allocate.go:125-127) -----------------------
+NODE_LABEL_DISABLE_CGPU = "cgpu.disable.isolation"
+ENV_CGPU_DISABLE = "CGPU_DISABLE"
+NODE_SELECTOR_LABEL = ("gpushare", "true")                 # device-plugin-ds.yaml:23-24
+PLUGIN_COMPONENT_LABEL = ("component", "gpushare-device-plugin")  # device-plugin-ds.yaml:17
+
+# --- optimistic lock message (const.go:15) -----------------------------------------------
+OPTIMISTIC_LOCK_ERROR_MSG = ("the object has been modified; please apply your changes to "
+                             "the latest version and try again")
+
+# --- memory units (const.go:34-35) -------------------------------------------------------
+GIB = "GiB"
+MIB = "MiB"
+UNIT_BYTES = {GIB: 1 << 30, MIB: 1 << 20}
+
+# --- AMD-native additions (no reference counterpart) -------------------------------------
+# Device nodes injected into every allocated container instead of an NVIDIA runtime hook.
+KFD_DEVICE = "/dev/kfd"
+DRI_RENDER_FMT = "/dev/dri/renderD{minor}"
+# HIP quota shim: host path of the .so is mounted at this container path and preloaded.
+SHIM_CONTAINER_DIR = "/usr/local/gpushare"
+SHIM_LIB_NAME = "libgpushare_hipquota.so"
+ENV_LD_PRELOAD = "LD_PRELOAD"
+ENV_SHIM_LEDGER = "GPUSHARE_LEDGER"          # shm ledger name shared by a container's processes
+ENV_SHIM_QUOTA_BYTES = "GPUSHARE_QUOTA_BYTES"  # explicit override (tests / debugging)
+ENV_SHIM_GRANULE = "GPUSHARE_ALLOC_GRANULE"    # allocation rounding granule override
+ENV_SHIM_LOG = "GPUSHARE_SHIM_LOG"
+ENV_GPU_UUID = "GPUSHARE_GPU_UUID"            # the physical GPU a container was given
+ENV_ROCR_VISIBLE = "ROCR_VISIBLE_DEVICES"
+# Node annotation carrying the exported xGMI topology (JSON, see parallel/topology.py).
+NODE_ANNOTATION_TOPOLOGY = "gpushare.amd.com/xgmi-topology"
+NODE_ANNOTATION_HEALTH = "gpushare.amd.com/gpu-health"
+
+# Environment used by the plugin itself (podmanager.go:33-58)
+ENV_NODE_NAME = "NODE_NAME"
+ENV_KUBECONFIG = "KUBECONFIG"
+
+SA_TOKEN_FILE = "/var/run/secrets/kubernetes.io/serviceaccount/token"
+SA_CA_FILE = "/var/run/secrets/kubernetes.io/serviceaccount/ca.crt"
+
+
+def plugin_socket(dir_: str | None = None) -> str:
+    return os.path.join(dir_ or DEVICE_PLUGIN_PATH, PLUGIN_SOCKET_NAME)
+
+
+def kubelet_socket(dir_: str | None = None) -> str:
+    return os.path.join(dir_ or DEVICE_PLUGIN_PATH, KUBELET_SOCKET_NAME)

@@ -1,0 +1,146 @@
+"""Live GPU health with recovery (component C3, re-designed).
+
+The reference's ``watchXIDs`` is commented out ("FIXME: re-implement for new nvml
+interface", ``nvidia.go:97-153``) so ``--health-check`` is a no-op, and a device that went
+Unhealthy could never come back (``server.go:188``). Its intended policy: fatal XID events
+mark the GPU unhealthy, application XIDs 31/43/45 are ignored (``nvidia.go:134``), an event
+without a device marks every GPU unhealthy (``:138-143``).
+
+MI355X policy, driven by the SMI event stream (rocm_smi event notification: VM fault,
+thermal throttle, GPU pre/post reset — ``rocm_smi.h:319-323``) plus periodic re-enumeration:
+
+================  ==============================================================
+event             effect
+================  ==============================================================
+VM fault          application error (≙ XID 31/43) → ignored, counted
+thermal throttle  informational → ignored, counted
+pre-reset         Unhealthy ("resetting")
+post-reset        Healthy again (unless still missing)
+unplug / missing  Unhealthy, present=False (index kept: IDX annotations stay valid)
+replug / back     Healthy, present=True
+ECC UE increase   Unhealthy until a reset
+xGMI link down    topology re-export (device stays Healthy)
+================  ==============================================================
+"""
+from __future__ import annotations
+
+import threading
+import time
+
+from ..utils import log
+from . import smi as S
+from .model import DeviceModel
+
+
+class HealthMonitor:
+    def __init__(self, smi: S.SMI, model: DeviceModel, poll_interval: float = 5.0,
+                 on_change=None, on_topology_change=None):
+        self.smi, self.model = smi, model
+        self.poll_interval = poll_interval
+        self.on_change = on_change
+        self.on_topology_change = on_topology_change
+        self._stop = threading.Event()
+        self._threads: list[threading.Thread] = []
+        self._ecc_baseline = {}
+        self.events_seen: list[S.Event] = []
+        self.ignored = 0
+        self._lock = threading.Lock()
+        for g in smi.devices():
+            self._ecc_baseline[g.uuid] = g.ecc_ue
+
+    def start(self):
+        self.smi.events_start()
+        for target, name in ((self._event_loop, "health-events"), (self._poll_loop, "health-poll")):
+            t = threading.Thread(target=target, name=name, daemon=True)
+            t.start()
+            self._threads.append(t)
+        return self
+
+    def stop(self):
+        self._stop.set()
+        for t in self._threads:
+            t.join(timeout=2.0)
+
+    # -- helpers --------------------------------------------------------------------------
+    def _set(self, index: int, healthy: bool, reason: str, present: bool | None = None):
+        if index < 0 or index >= self.model.count():
+            return
+        if self.model.set_health(index, healthy, reason, present) and self.on_change:
+            self.on_change(index, healthy, reason)
+
+    def _model_index_of_smi(self, smi_index: int) -> int:
+        try:
+            uuid = self.smi.device(smi_index).uuid
+        except S.SMIError:
+            return -1
+        g = self.model.by_uuid(uuid)
+        return g.index if g else -1
+
+    # -- event stream ---------------------------------------------------------------------
+    def handle_event(self, ev: S.Event):
+        with self._lock:
+            self.events_seen.append(ev)
+        k = ev.kind
+        if k in (S.EV_VMFAULT, S.EV_THERMAL):
+            self.ignored += 1
+            log.info("GPU event %s on %d ignored (application-level)", ev.name, ev.index)
+            return
+        if k in (S.EV_LINK_DOWN, S.EV_LINK_UP):
+            if self.on_topology_change:
+                self.on_topology_change(ev)
+            return
+        if k in (S.EV_UNPLUG, S.EV_REPLUG):
+            self.poll_once()   # membership changes are resolved by re-enumeration
+            return
+        targets = range(self.model.count()) if ev.index < 0 else [self._model_index_of_smi(ev.index)]
+        for idx in targets:
+            if k == S.EV_PRE_RESET:
+                self._set(idx, False, "GPU reset in progress")
+            elif k == S.EV_POST_RESET:
+                g = self.model.gpu(idx)
+                if g is not None:
+                    self._ecc_baseline[g.uuid] = self._current_ecc(g.uuid, self._ecc_baseline.get(g.uuid, 0))
+                    if g.present:
+                        self._set(idx, True, "recovered after reset")
+            elif k == S.EV_ECC_UE:
+                self.poll_once()
+
+    def _current_ecc(self, uuid: str, dflt: int) -> int:
+        for d in self.smi.devices():
+            if d.uuid == uuid:
+                return d.ecc_ue
+        return dflt
+
+    def _event_loop(self):
+        while not self._stop.is_set():
+            try:
+                ev = self.smi.wait_event(200)
+            except S.SMIError as e:
+                log.warning("SMI event wait failed: %s", e)
+                time.sleep(1.0)
+                continue
+            if ev is not None:
+                self.handle_event(ev)
+
+    # -- polling --------------------------------------------------------------------------
+    def poll_once(self):
+        try:
+            self.smi.refresh()
+            present = {d.uuid: d for d in self.smi.devices()}
+        except S.SMIError as e:
+            log.warning("SMI refresh failed: %s", e)
+            return
+        for g in self.model.gpus:
+            d = present.get(g.uuid)
+            if d is None:
+                self._set(g.index, False, "device missing", present=False)
+                continue
+            base = self._ecc_baseline.setdefault(g.uuid, d.ecc_ue)
+            if d.ecc_ue > base:
+                self._set(g.index, False, f"uncorrectable ECC errors {base}->{d.ecc_ue}", present=True)
+            elif not g.present:
+                self._set(g.index, True, "device back", present=True)
+
+    def _poll_loop(self):
+        while not self._stop.wait(self.poll_interval):
+            self.poll_once()

@@ -1,0 +1,68 @@
+"""xGMI topology export and TP-group placement (new capability; no reference counterpart).
+
+The reference has no topology at all (``Device.Topology`` left nil, ``nvidia.go:79-81``).
+MI355X nodes connect their 8 GPUs with point-to-point xGMI (7 links per GPU, ≈153 GB/s
+each), so on a healthy UBB every pair is one hop — but a downed link, a CPX/NPS partition
+mode or a missing GPU breaks that symmetry, and an RCCL tensor-parallel pod group placed
+across a non-xGMI pair falls back to PCIe. The plugin exports the link matrix as a node
+annotation (``gpushare.amd.com/xgmi-topology``); ``best_group`` is the placement rule a
+TP-aware extender (and ``sim/extender.py``) applies to it.
+"""
+from __future__ import annotations
+
+import itertools
+
+from ..device import smi as S
+
+
+def build_topology(smi: S.SMI, indices: list[int] | None = None) -> dict:
+    devs = smi.devices()
+    sel = [d for d in devs if indices is None or d.index in set(indices)]
+    m = smi.link_matrix()
+    idx = [d.index for d in sel]
+    return {
+        "version": 1,
+        "hive_id": format(sel[0].hive_id, "x") if sel else "0",
+        "gpus": [{"index": k, "uuid": d.uuid, "bdf": d.bdf, "numa": d.numa_node,
+                  "partition": d.compute_partition, "nps": d.memory_partition} for k, d in enumerate(sel)],
+        "link_type": [[m[i][j].type_name for j in idx] for i in idx],
+        "hops": [[m[i][j].hops for j in idx] for i in idx],
+        "weight": [[m[i][j].weight for j in idx] for i in idx],
+    }
+
+
+def xgmi_connected(topo: dict, a: int, b: int) -> bool:
+    if a == b:
+        return True
+    lt = topo.get("link_type") or []
+    try:
+        return lt[a][b] == "xgmi" and topo["hops"][a][b] == 1
+    except (IndexError, KeyError):
+        return False
+
+
+def best_group(topo: dict | None, free: list[int], size: int, request: int,
+               exclude: set[int] | None = None) -> list[int] | None:
+    """Pick ``size`` distinct GPUs, each with ``free[i] >= request``, pairwise one-hop xGMI.
+
+    Tie-break for bin-packing density: minimise the summed leftover capacity (best fit),
+    then the summed hop count (for partially connected graphs), then indices.
+    Returns None when no such group exists.
+    """
+    exclude = exclude or set()
+    ok = [i for i, f in enumerate(free) if f >= request and i not in exclude]
+    if len(ok) < size:
+        return None
+    best, best_key = None, None
+    n = len(free)
+    for combo in itertools.combinations(ok, size):
+        if topo is not None and n == len(topo.get("link_type") or []):
+            if not all(xgmi_connected(topo, a, b) for a, b in itertools.combinations(combo, 2)):
+                continue
+            hops = sum(topo["hops"][a][b] for a, b in itertools.combinations(combo, 2))
+        else:
+            hops = 0
+        key = (sum(free[i] - request for i in combo), hops, combo)
+        if best_key is None or key < best_key:
+            best, best_key = list(combo), key
+    return best

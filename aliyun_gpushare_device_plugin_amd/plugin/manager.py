@@ -1,0 +1,244 @@
+"""Lifecycle supervisor (component C9; reference ``pkg/gpu/nvidia/gpumanager.go:16-111``).
+
+Same state machine as the reference:
+* init the SMI layer; if it fails or finds no GPU, park (the reference ``select{}``s forever
+  so the DaemonSet does not crash-loop) — here parking still honours SIGTERM;
+* watch the device-plugin directory; re-creation of ``kubelet.sock`` (kubelet restart) or
+  SIGHUP rebuilds the plugin: re-enumerate, re-patch ``gpu-count``, re-register;
+* SIGQUIT dumps all stacks; SIGINT/SIGTERM stop cleanly;
+* construction failure exits 1, serve/register failure exits 2 (``:71-77``).
+Additions: topology export, the live health monitor, the metrics endpoint, and a choice of
+pod source (watch cache by default).
+"""
+from __future__ import annotations
+
+import dataclasses
+import os
+import queue
+import signal
+import threading
+
+from .. import const
+from ..alloc.engine import Allocator, AllocatorOptions
+from ..cluster import nodestatus
+from ..cluster.client import APIClient, build_client
+from ..cluster.kubelet import KubeletClient
+from ..cluster.podcache import KubeletSource, ListSource, WatchCache
+from ..device import smi as S
+from ..device.health import HealthMonitor
+from ..device.model import DeviceModel
+from ..parallel import topology as T
+from ..quota import ShimConfig
+from ..utils import log, metrics as M, stackdump
+from .server import DevicePluginServer
+from .watchers import FSWatcher, watch_signals
+
+
+@dataclasses.dataclass
+class PluginConfig:
+    node_name: str = ""
+    memory_unit: str = const.GIB
+    round_policy: str = "nearest"
+    homogeneous: bool = True
+    health_check: bool = True
+    health_poll_s: float = 5.0
+    pod_source: str = "watch"            # watch | list | kubelet
+    query_kubelet: bool = False          # reference flag; implies pod_source=kubelet
+    kubelet_address: str = "0.0.0.0"
+    kubelet_port: int = 10250
+    kubelet_scheme: str = "https"
+    client_cert: str = ""
+    client_key: str = ""
+    token: str = ""
+    timeout: float = 10.0
+    smi_backend: str = "auto"
+    device_plugin_dir: str = const.DEVICE_PLUGIN_PATH
+    kubeconfig: str | None = None
+    apiserver: str | None = None
+    gpu_indices: list | None = None
+    shim_host_dir: str | None = None     # None = do not inject the quota shim
+    strict_allocate: bool = False
+    preferred_allocation: bool = True
+    export_topology: bool = True
+    expose_devices: bool = True
+    rocr_visible: bool = False
+    metrics_addr: str | None = None
+    mps: bool = False                    # accepted for flag compatibility; ignored
+
+
+class SharedGPUManager:
+    def __init__(self, cfg: PluginConfig, client: APIClient | None = None, smi: S.SMI | None = None):
+        self.cfg = cfg
+        if cfg.query_kubelet:
+            cfg.pod_source = "kubelet"
+        if cfg.mps:
+            log.warning("--mps is accepted for compatibility and ignored (no MPS on MI355X)")
+        self.client = client
+        self.smi = smi
+        self.events: "queue.Queue" = queue.Queue()
+        self.metrics = M.PluginMetrics()
+        self.plugin: DevicePluginServer | None = None
+        self.health: HealthMonitor | None = None
+        self.pod_source = None
+        self.model: DeviceModel | None = None
+        self.started = threading.Event()
+        self.restarts = 0
+        self._metrics_srv = None
+
+    # ------------------------------------------------------------------------------------
+    def _kubelet_socket(self) -> str:
+        return os.path.join(self.cfg.device_plugin_dir, const.KUBELET_SOCKET_NAME)
+
+    def _plugin_socket(self) -> str:
+        return os.path.join(self.cfg.device_plugin_dir, const.PLUGIN_SOCKET_NAME)
+
+    def _export_topology(self):
+        if not (self.cfg.export_topology and self.client and self.smi):
+            return
+        try:
+            topo = T.build_topology(self.smi, self.cfg.gpu_indices)
+            nodestatus.export_topology(self.client, self.cfg.node_name, topo)
+        except Exception as e:  # noqa: BLE001 - best effort, never blocks Allocate
+            log.warning("topology export failed: %s", e)
+
+    def _export_health(self, *_a):
+        if not (self.client and self.model):
+            return
+        try:
+            nodestatus.export_health(self.client, self.cfg.node_name, {
+                str(g.index): {"uuid": g.uuid, "healthy": g.healthy and g.present, "reason": g.reason}
+                for g in self.model.gpus})
+        except Exception as e:  # noqa: BLE001
+            log.warning("health export failed: %s", e)
+
+    def build_plugin(self) -> DevicePluginServer:
+        """``NewNvidiaDevicePlugin`` (``server.go:43-78``)."""
+        cfg = self.cfg
+        self.smi.refresh()
+        model = DeviceModel(self.smi.devices(), cfg.memory_unit, cfg.round_policy, cfg.homogeneous,
+                            cfg.gpu_indices)
+        for g in model.gpus:
+            self.metrics.units_per_gpu.set(g.units, gpu=str(g.index))
+            self.metrics.device_health.set(1 if g.healthy else 0, gpu=str(g.index))
+        disable_cgpu = False
+        if self.client is not None:
+            nodestatus.patch_gpu_count(self.client, cfg.node_name, model.count())
+            disable_cgpu = nodestatus.cgpu_isolation_disabled(self.client, cfg.node_name)
+        if self.pod_source is not None:
+            self.pod_source.stop()
+        fallback = ListSource(self.client, cfg.node_name) if self.client else None
+        if cfg.pod_source == "watch" and self.client is not None:
+            src = WatchCache(self.client, cfg.node_name,
+                             on_event=lambda t: self.metrics.cache_events.inc(type=t)).start()
+            src.wait_synced(5.0)
+        elif cfg.pod_source == "kubelet":
+            kc = KubeletClient.from_flags(cfg.kubelet_address, cfg.kubelet_port, cfg.client_cert, cfg.client_key,
+                                          cfg.token, cfg.timeout, cfg.kubelet_scheme)
+            src = KubeletSource(kc, fallback)
+        else:
+            src = fallback
+        self.pod_source = src
+        shim = ShimConfig(cfg.shim_host_dir) if cfg.shim_host_dir else None
+        allocator = Allocator(model, src, self.client, cfg.node_name,
+                              AllocatorOptions(unit=cfg.memory_unit, disable_cgpu=disable_cgpu, shim=shim,
+                                               strict=cfg.strict_allocate, expose_devices=cfg.expose_devices,
+                                               rocr_visible=cfg.rocr_visible),
+                              self.metrics)
+        self.model = model
+        return DevicePluginServer(model, allocator, self._plugin_socket(), const.RESOURCE_NAME,
+                                  cfg.preferred_allocation, self.metrics)
+
+    def _start_health(self):
+        if self.health:
+            self.health.stop()
+            self.health = None
+        if self.cfg.health_check and self.model is not None:
+            def changed(idx, healthy, reason):
+                self.metrics.device_health.set(1 if healthy else 0, gpu=str(idx))
+                self._export_health()
+
+            self.health = HealthMonitor(self.smi, self.model, self.cfg.health_poll_s, on_change=changed,
+                                        on_topology_change=lambda ev: self._export_topology()).start()
+
+    def stop(self):
+        self.events.put(("signal", signal.SIGTERM))
+
+    def _park(self):
+        log.info("parking: no usable GPU on this node (waiting for SIGTERM)")
+        while True:
+            kind, val = self.events.get()
+            if kind == "signal" and val in (signal.SIGINT, signal.SIGTERM):
+                return 0
+
+    def run(self, install_signals: bool | None = None) -> int:
+        cfg = self.cfg
+        if install_signals is None:
+            install_signals = threading.current_thread() is threading.main_thread()
+        if install_signals:
+            watch_signals(self.events)
+        log.V(1).info("Loading SMI backend %s", cfg.smi_backend)
+        if self.smi is None:
+            try:
+                self.smi = S.SMI(cfg.smi_backend)
+            except Exception as e:  # noqa: BLE001
+                log.warning("Failed to initialize SMI: %s", e)
+                return self._park()
+        if self.smi.count() == 0:
+            log.V(1).info("No devices found. Waiting indefinitely.")
+            return self._park()
+        if self.client is None and (cfg.apiserver or cfg.kubeconfig or os.environ.get(const.ENV_KUBECONFIG)
+                                    or os.environ.get("KUBERNETES_SERVICE_HOST")):
+            self.client = build_client(cfg.kubeconfig, cfg.apiserver, cfg.timeout)
+        if cfg.metrics_addr:
+            self._metrics_srv = M.serve(self.metrics.registry, cfg.metrics_addr,
+                                        lambda: self.plugin is not None and not self.plugin.stopped.is_set())
+        os.makedirs(cfg.device_plugin_dir, exist_ok=True)
+        watcher = FSWatcher(cfg.device_plugin_dir, self.events)
+        log.V(1).info("Starting FS watcher (%s).", watcher.mode)
+        restart = True
+        rc = 0
+        try:
+            while True:
+                if restart:
+                    if self.plugin is not None:
+                        self.plugin.stop()
+                        self.restarts += 1
+                    try:
+                        self.plugin = self.build_plugin()
+                    except Exception as e:  # noqa: BLE001
+                        log.warning("Failed to get device plugin due to %s", e)
+                        return 1
+                    try:
+                        self.plugin.serve(self._kubelet_socket())
+                    except Exception as e:  # noqa: BLE001
+                        log.warning("Failed to start device plugin due to %s", e)
+                        return 2
+                    self._export_topology()
+                    self._start_health()
+                    restart = False
+                    self.started.set()
+                kind, val = self.events.get()
+                if kind == "fs":
+                    if val.name == self._kubelet_socket() and val.op == "create":
+                        log.V(1).info("inotify: %s created, restarting.", val.name)
+                        restart = True
+                elif kind == "signal":
+                    if val == signal.SIGHUP:
+                        log.V(1).info("Received SIGHUP, restarting.")
+                        restart = True
+                    elif val == signal.SIGQUIT:
+                        log.info("generate core dump: %s", stackdump.coredump())
+                    else:
+                        log.V(1).info('Received signal "%s", shutting down.', val)
+                        break
+        finally:
+            watcher.close()
+            if self.health:
+                self.health.stop()
+            if self.plugin is not None:
+                self.plugin.stop()
+            if self.pod_source is not None:
+                self.pod_source.stop()
+            if self._metrics_srv is not None:
+                self._metrics_srv.shutdown()
+        return rc

@@ -1,0 +1,198 @@
+"""Composable fake cluster: apiserver + N nodes (fake kubelet + real plugin) + extender.
+
+"Multi-node without a real cluster" (SURVEY §4): every node runs the real plugin code
+(``SharedGPUManager`` — in a thread, or as a separate ``gpushare-device-plugin`` process for
+honest IPC timing) against a shared fake apiserver, and pods flow through the same path as
+in production: create → extender filter/bind (annotations) → kubelet admission → plugin
+``Allocate`` over gRPC/UDS → ``ASSIGNED=true`` patch → Running.
+"""
+from __future__ import annotations
+
+import dataclasses
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+import threading
+import time
+
+from .. import const
+from ..cluster import objects as O
+from ..cluster.client import APIClient, KubeConfig
+from ..plugin.manager import PluginConfig, SharedGPUManager
+from ..utils import log
+from .apiserver import FakeAPIServer, make_node
+from .extender import TP_GROUP_LABEL, TP_SIZE_LABEL, ExtenderSim
+from .kubelet import Admission, FakeKubelet
+
+
+def pod_spec(name: str, gpu_mem, namespace: str = "default", labels: dict | None = None,
+             image: str = "rocm/pytorch:latest") -> dict:
+    """A pod with one container per entry of ``gpu_mem`` (int → single container)."""
+    mems = [gpu_mem] if isinstance(gpu_mem, int) else list(gpu_mem)
+    ctrs = [{"name": f"c{i}", "image": image,
+             "resources": {"limits": {const.RESOURCE_NAME: str(m)}} if m else {}} for i, m in enumerate(mems)]
+    return {"apiVersion": "v1", "kind": "Pod",
+            "metadata": {"name": name, "namespace": namespace, "labels": dict(labels or {})},
+            "spec": {"containers": ctrs, "schedulerName": "default-scheduler"}}
+
+
+@dataclasses.dataclass
+class SimNode:
+    name: str
+    smi_spec: str
+    plugin_dir: str
+    kubelet: FakeKubelet
+    manager: SharedGPUManager | None = None
+    thread: threading.Thread | None = None
+    proc: subprocess.Popen | None = None
+
+
+class SimCluster:
+    def __init__(self, nodes: list[tuple[str, str]], workdir: str | None = None, plugin_mode: str = "thread",
+                 pod_source: str = "watch", apiserver_latency_s: float = 0.0, shim_host_dir: str | None = None,
+                 gpu_indices: list[int] | None = None, health_poll_s: float = 1.0, round_policy: str = "nearest",
+                 extra_plugin_args: list[str] | None = None):
+        self.node_specs = nodes
+        self._own_dir = workdir is None
+        # short paths: UDS paths are limited to 108 bytes
+        self.workdir = workdir or tempfile.mkdtemp(prefix="gs-", dir="/tmp")
+        self.plugin_mode = plugin_mode
+        self.pod_source = pod_source
+        self.api = FakeAPIServer(latency_s=apiserver_latency_s)
+        self.client: APIClient | None = None
+        self.extender: ExtenderSim | None = None
+        self.nodes: dict[str, SimNode] = {}
+        self.shim_host_dir = shim_host_dir
+        self.gpu_indices = gpu_indices
+        self.health_poll_s = health_poll_s
+        self.round_policy = round_policy
+        self.extra_plugin_args = extra_plugin_args or []
+        self._seq = 0
+
+    # -- lifecycle ------------------------------------------------------------------------
+    def start(self, timeout: float = 30.0):
+        self.api.start()
+        self.client = APIClient(KubeConfig(self.api.url))
+        for name, spec in self.node_specs:
+            self.client.create_node(make_node(name))
+            pdir = os.path.join(self.workdir, name)
+            kl = FakeKubelet(pdir, APIClient(KubeConfig(self.api.url)), name).start()
+            node = SimNode(name, spec, pdir, kl)
+            self.nodes[name] = node
+            self._start_plugin(node)
+        for node in self.nodes.values():
+            if not node.kubelet.registered.wait(timeout):
+                raise TimeoutError(f"plugin on {node.name} did not register")
+            self._wait_capacity(node.name, timeout)
+        self.extender = ExtenderSim(self.client)
+        self.extender.sync()
+        return self
+
+    def _plugin_cfg(self, node: SimNode) -> PluginConfig:
+        return PluginConfig(node_name=node.name, smi_backend=node.smi_spec, device_plugin_dir=node.plugin_dir,
+                            apiserver=self.api.url, pod_source=self.pod_source,
+                            shim_host_dir=self.shim_host_dir, gpu_indices=self.gpu_indices,
+                            health_poll_s=self.health_poll_s, round_policy=self.round_policy)
+
+    def _start_plugin(self, node: SimNode):
+        if self.plugin_mode == "process":
+            args = [sys.executable, "-m", "aliyun_gpushare_device_plugin_amd.cli.main",
+                    "--node-name", node.name, "--smi-backend", node.smi_spec,
+                    "--device-plugin-dir", node.plugin_dir, "--apiserver", self.api.url,
+                    "--pod-source", self.pod_source, "--round", self.round_policy,
+                    "--health-poll", str(self.health_poll_s)]
+            if self.shim_host_dir:
+                args += ["--shim-path", self.shim_host_dir]
+            if self.gpu_indices:
+                args += ["--gpu-indices", ",".join(map(str, self.gpu_indices))]
+            args += self.extra_plugin_args
+            env = dict(os.environ)
+            env["PYTHONPATH"] = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))) + \
+                os.pathsep + env.get("PYTHONPATH", "")
+            node.proc = subprocess.Popen(args, env=env, stdout=subprocess.DEVNULL,
+                                         stderr=open(os.path.join(self.workdir, f"{node.name}.plugin.log"), "w"))
+        else:
+            node.manager = SharedGPUManager(self._plugin_cfg(node), client=APIClient(KubeConfig(self.api.url)))
+            node.thread = threading.Thread(target=node.manager.run, kwargs={"install_signals": False},
+                                           name=f"plugin-{node.name}", daemon=True)
+            node.thread.start()
+
+    def _wait_capacity(self, node: str, timeout: float):
+        t = time.monotonic() + timeout
+        while time.monotonic() < t:
+            n = self.client.get_node(node)
+            if O.node_allocatable(n, const.RESOURCE_COUNT) > 0 and O.node_allocatable(n, const.RESOURCE_NAME) > 0:
+                return n
+            time.sleep(0.02)
+        raise TimeoutError(f"node {node} never reported gpu capacity")
+
+    def stop(self):
+        for node in self.nodes.values():
+            if node.manager is not None:
+                node.manager.stop()
+                if node.thread is not None:
+                    node.thread.join(timeout=5)
+            if node.proc is not None:
+                node.proc.terminate()
+                try:
+                    node.proc.wait(timeout=10)
+                except subprocess.TimeoutExpired:
+                    node.proc.kill()
+            node.kubelet.stop()
+        self.api.stop()
+        if self._own_dir:
+            shutil.rmtree(self.workdir, ignore_errors=True)
+
+    def __enter__(self):
+        return self.start()
+
+    def __exit__(self, *exc):
+        self.stop()
+
+    # -- pod flow -------------------------------------------------------------------------
+    def create_pod(self, gpu_mem, name: str | None = None, labels: dict | None = None) -> dict:
+        self._seq += 1
+        return self.client.create_pod("default", pod_spec(name or f"pod-{self._seq}", gpu_mem, labels=labels))
+
+    def schedule(self, pod: dict):
+        return self.extender.schedule(pod)
+
+    def admit(self, pod: dict) -> Admission:
+        pod = self.client.get_pod(O.namespace(pod), O.name(pod))
+        node = self.nodes[O.node_name(pod)]
+        adm = node.kubelet.admit(pod)
+        if adm.error is None:
+            self.client.patch_pod_status(O.namespace(pod), O.name(pod), {"status": {"phase": "Running"}})
+        return adm
+
+    def run_pod(self, gpu_mem, name: str | None = None, labels: dict | None = None):
+        pod = self.create_pod(gpu_mem, name, labels)
+        placed = self.schedule(pod)
+        if placed is None:
+            return pod, None, None
+        return pod, placed, self.admit(pod)
+
+    def run_tp_group(self, group: str, size: int, gpu_mem: int):
+        pods = [self.create_pod(gpu_mem, labels={TP_GROUP_LABEL: group, TP_SIZE_LABEL: str(size)})
+                for _ in range(size)]
+        placed = self.extender.schedule_group(pods)
+        if placed is None:
+            return pods, None, []
+        return pods, placed, [self.admit(p) for p in pods]
+
+    def delete_pod(self, pod: dict):
+        pod = self.client.get_pod(O.namespace(pod), O.name(pod))
+        nn = O.node_name(pod)
+        if nn in self.nodes:
+            self.nodes[nn].kubelet.release(O.uid(pod))
+        self.extender.forget(pod)
+        self.client.delete_pod(O.namespace(pod), O.name(pod))
+
+    def manager(self, node: str) -> SharedGPUManager | None:
+        return self.nodes[node].manager
+
+
+def quiet():
+    log.setup(verbosity=0)

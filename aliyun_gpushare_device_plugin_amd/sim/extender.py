@@ -1,0 +1,239 @@
+"""gpushare-scheduler-extender protocol stand-in (test and bench only).
+
+The real extender is a separate Go project (linked from the reference ``README.md:14``),
+not in ``/root/reference`` and not buildable here. What the plugin relies on is inferred
+from what it consumes: per-GPU capacity = node ``allocatable[gpu-mem] /
+allocatable[gpu-count]`` (the inspect arithmetic, ``cmd/inspect/nodeinfo.go:116,146``);
+the extender picks a node and a GPU index, writes ``ALIYUN_COM_GPU_MEM_IDX/_POD/
+_ASSUME_TIME`` and ``_ASSIGNED="false"``, then binds.
+
+This simulator does exactly that with a best-fit bin-packing policy, keeps its per-GPU
+ledger like the real extender's cache, and adds the MI355X capability the north star asks
+for: pods labelled ``gpushare.amd.com/tp-group=<name>`` with ``…/tp-size=<k>`` are placed
+as a group on k distinct GPUs that are pairwise one-hop xGMI per the topology annotation
+the plugin exports (``parallel/topology.py``). It also serves the extender HTTP routes
+(``/gpushare-scheduler/filter`` and ``/bind``) for protocol-level tests.
+"""
+from __future__ import annotations
+
+import dataclasses
+import http.server
+import json
+import socketserver
+import threading
+import time
+
+from .. import const
+from ..alloc import annotations as A
+from ..cluster import nodestatus, objects as O
+from ..cluster.client import APIClient
+from ..parallel import topology as T
+
+TP_GROUP_LABEL = "gpushare.amd.com/tp-group"
+TP_SIZE_LABEL = "gpushare.amd.com/tp-size"
+
+
+@dataclasses.dataclass
+class NodeState:
+    name: str
+    gpu_count: int
+    per_gpu: int
+    used: list
+    topology: dict | None
+    healthy: list
+
+    def free(self) -> list[int]:
+        return [(self.per_gpu - u) if h else -1 for u, h in zip(self.used, self.healthy)]
+
+
+class ExtenderSim:
+    def __init__(self, client: APIClient, policy: str = "binpack"):
+        self.client = client
+        self.policy = policy
+        self.nodes: dict[str, NodeState] = {}
+        self._placed: dict[str, tuple] = {}   # pod uid -> (node, [(gpu, units)])
+        self._lock = threading.Lock()
+
+    # -- cache ----------------------------------------------------------------------------
+    def sync(self):
+        """Rebuild the ledger from the apiserver (extender cache warm-up)."""
+        with self._lock:
+            self.nodes.clear()
+            self._placed.clear()
+            for n in self.client.list_nodes():
+                cnt = O.node_allocatable(n, const.RESOURCE_COUNT)
+                mem = O.node_allocatable(n, const.RESOURCE_NAME)
+                cap = O.node_capacity(n, const.RESOURCE_NAME) or mem
+                if cnt <= 0 or cap <= 0:
+                    continue
+                health = json.loads(O.annotations(n).get(const.NODE_ANNOTATION_HEALTH, "{}") or "{}")
+                healthy = [bool((health.get(str(i)) or {}).get("healthy", True)) for i in range(cnt)]
+                self.nodes[O.name(n)] = NodeState(O.name(n), cnt, cap // cnt, [0] * cnt,
+                                                  nodestatus.read_topology(n), healthy)
+            pods, _ = self.client.list_pods()
+            for p in pods:
+                if O.is_terminated(p) or not O.node_name(p):
+                    continue
+                st = self.nodes.get(O.node_name(p))
+                if st is None or O.gpu_mem_of_pod(p) <= 0:
+                    continue
+                alloc = A.allocation_from_annotation(p) or {A.gpu_id_from_annotation(p): O.gpu_mem_of_pod(p)}
+                parts = []
+                for g, mem in alloc.items():
+                    if 0 <= g < st.gpu_count:
+                        st.used[g] += mem
+                        parts.append((g, mem))
+                self._placed[O.uid(p)] = (st.name, parts)
+
+    def forget(self, pod: dict):
+        with self._lock:
+            placed = self._placed.pop(O.uid(pod), None)
+            if placed:
+                st = self.nodes.get(placed[0])
+                if st:
+                    for g, mem in placed[1]:
+                        st.used[g] -= mem
+
+    # -- scheduling -----------------------------------------------------------------------
+    def _fits(self, st: NodeState, req: int) -> list[int]:
+        return [i for i, f in enumerate(st.free()) if f >= req]
+
+    def filter(self, pod: dict, node_names: list[str] | None = None) -> list[str]:
+        req = O.gpu_mem_of_pod(pod)
+        with self._lock:
+            names = node_names if node_names is not None else list(self.nodes)
+            return [n for n in names if n in self.nodes and self._fits(self.nodes[n], req)]
+
+    def _choose(self, req: int, node_names=None) -> tuple[str, int] | None:
+        best = None
+        for name in node_names or list(self.nodes):
+            st = self.nodes.get(name)
+            if st is None:
+                continue
+            for i, f in enumerate(st.free()):
+                if f < req:
+                    continue
+                left = f - req
+                key = (left, name, i) if self.policy == "binpack" else (-left, name, i)
+                if best is None or key < best[0]:
+                    best = (key, name, i)
+        return (best[1], best[2]) if best else None
+
+    def bind(self, pod: dict, node: str, gpu: int, assume_ns: int | None = None) -> dict:
+        req = O.gpu_mem_of_pod(pod)
+        ns, nm = O.namespace(pod), O.name(pod)
+        patched = self.client.patch_pod(ns, nm, {"metadata": {"annotations": {
+            const.ENV_RESOURCE_INDEX: str(gpu),
+            const.ENV_RESOURCE_BY_POD: str(req),
+            const.ENV_RESOURCE_ASSUME_TIME: str(assume_ns or time.time_ns()),
+            const.ENV_ASSIGNED_FLAG: "false",
+        }}})
+        self.client.bind_pod(ns, nm, node, O.uid(pod))
+        return patched
+
+    def schedule(self, pod: dict, node_names=None) -> tuple[str, int] | None:
+        """Filter + prioritize + bind one pod. Returns (node, gpu) or None if it does not fit."""
+        req = O.gpu_mem_of_pod(pod)
+        with self._lock:
+            choice = self._choose(req, node_names)
+            if choice is None:
+                return None
+            st = self.nodes[choice[0]]
+            st.used[choice[1]] += req
+            self._placed[O.uid(pod)] = (choice[0], [(choice[1], req)])
+        try:
+            self.bind(pod, choice[0], choice[1])
+        except Exception:
+            self.forget(pod)
+            raise
+        return choice
+
+    def schedule_group(self, pods: list[dict], node_names=None) -> list[tuple[str, int]] | None:
+        """Gang-place a tensor-parallel group: one pod per GPU, all GPUs pairwise xGMI."""
+        if not pods:
+            return []
+        req = max(O.gpu_mem_of_pod(p) for p in pods)
+        with self._lock:
+            best = None
+            for name in node_names or list(self.nodes):
+                st = self.nodes[name]
+                grp = T.best_group(st.topology, st.free(), len(pods), req)
+                if grp is None:
+                    continue
+                key = (sum(st.free()[g] - req for g in grp), name)
+                if best is None or key < best[0]:
+                    best = (key, name, grp)
+            if best is None:
+                return None
+            _, name, grp = best
+            st = self.nodes[name]
+            for p, g in zip(pods, grp):
+                st.used[g] += O.gpu_mem_of_pod(p)
+                self._placed[O.uid(p)] = (name, [(g, O.gpu_mem_of_pod(p))])
+        out = []
+        t = time.time_ns()
+        for k, (p, g) in enumerate(zip(pods, grp)):
+            self.bind(p, name, g, assume_ns=t + k)
+            out.append((name, g))
+        return out
+
+    def usage(self) -> dict:
+        with self._lock:
+            return {n: {"per_gpu": s.per_gpu, "used": list(s.used)} for n, s in self.nodes.items()}
+
+
+def serve_http(ext: ExtenderSim, host: str = "127.0.0.1", port: int = 0):
+    """Extender HTTP endpoints: ``POST /gpushare-scheduler/filter`` (ExtenderArgs →
+    ExtenderFilterResult) and ``POST /gpushare-scheduler/bind`` (ExtenderBindingArgs →
+    ExtenderBindingResult)."""
+
+    class H(http.server.BaseHTTPRequestHandler):
+        protocol_version = "HTTP/1.1"
+
+        def log_message(self, *a):
+            pass
+
+        def _reply(self, obj):
+            b = json.dumps(obj).encode()
+            self.send_response(200)
+            self.send_header("Content-Type", "application/json")
+            self.send_header("Content-Length", str(len(b)))
+            self.end_headers()
+            self.wfile.write(b)
+
+        def do_POST(self):
+            n = int(self.headers.get("Content-Length") or 0)
+            args = json.loads(self.rfile.read(n) or b"{}")
+            if self.path.endswith("/filter"):
+                pod = args.get("Pod") or args.get("pod") or {}
+                names = args.get("NodeNames") or args.get("nodenames") or \
+                    [O.name(x) for x in ((args.get("Nodes") or {}).get("items") or [])]
+                ok = ext.filter(pod, names)
+                failed = {x: "insufficient GPU memory in one device" for x in names if x not in ok}
+                return self._reply({"NodeNames": ok, "FailedNodes": failed, "Error": ""})
+            if self.path.endswith("/bind"):
+                try:
+                    pod = ext.client.get_pod(args.get("PodNamespace", "default"), args["PodName"])
+                    req = O.gpu_mem_of_pod(pod)
+                    with ext._lock:
+                        st = ext.nodes.get(args["Node"])
+                        fits = ext._fits(st, req) if st else []
+                        if not fits:
+                            return self._reply({"Error": "no GPU fits"})
+                        g = min(fits, key=lambda i: (st.free()[i] - req, i))
+                        st.used[g] += req
+                        ext._placed[O.uid(pod)] = (st.name, [(g, req)])
+                    ext.bind(pod, args["Node"], g)
+                    return self._reply({"Error": ""})
+                except Exception as e:  # noqa: BLE001
+                    return self._reply({"Error": str(e)})
+            self.send_response(404)
+            self.send_header("Content-Length", "0")
+            self.end_headers()
+
+    class S(socketserver.ThreadingMixIn, http.server.HTTPServer):
+        daemon_threads = True
+
+    srv = S((host, port), H)
+    threading.Thread(target=srv.serve_forever, name="extender-http", daemon=True).start()
+    return srv

@@ -1,0 +1,190 @@
+"""Fake kubelet device manager (test and bench stand-in).
+
+Plays the kubelet's side of the device-plugin API over real gRPC-on-UDS:
+* serves ``v1beta1.Registration`` on ``<dir>/kubelet.sock``;
+* on ``Register`` dials the plugin's endpoint, reads ``GetDevicePluginOptions`` and keeps a
+  ``ListAndWatch`` stream, mirroring the advertised healthy-device count into the node's
+  ``aliyun.com/gpu-mem`` capacity/allocatable (what the real kubelet reports);
+* ``admit(pod)`` does what pod admission does: for each container with a ``gpu-mem`` limit,
+  pick that many free healthy fake IDs (asking ``GetPreferredAllocation`` when offered),
+  call ``Allocate`` once per container, and remember the IDs until ``release``;
+* ``restart()`` re-creates ``kubelet.sock`` like a kubelet restart (the plugin must notice
+  and re-register, ``gpumanager.go:82-87``).
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import dataclasses
+import os
+import threading
+import time
+
+import grpc
+
+from .. import const
+from ..api import v1beta1 as api
+from ..cluster import objects as O
+from ..cluster.client import APIClient
+from ..utils import log
+
+
+@dataclasses.dataclass
+class Admission:
+    pod_uid: str
+    responses: list          # ContainerAllocateResponse per gpu container
+    latencies: list          # seconds per Allocate RPC
+    device_ids: list
+    error: str | None = None
+
+
+class FakeKubelet:
+    def __init__(self, plugin_dir: str, client: APIClient | None = None, node: str | None = None,
+                 resource: str = const.RESOURCE_NAME):
+        self.dir, self.client, self.node, self.resource = plugin_dir, client, node, resource
+        os.makedirs(plugin_dir, exist_ok=True)
+        self.sock = os.path.join(plugin_dir, const.KUBELET_SOCKET_NAME)
+        self.server = None
+        self.registrations: list = []
+        self.registered = threading.Event()
+        self.devices: dict[str, str] = {}
+        self.devices_updated = threading.Condition()
+        self.list_updates = 0
+        self.options = None
+        self._channel = None
+        self._stub = None
+        self._law_thread = None
+        self._allocated: dict[str, set] = {}
+        self._lock = threading.Lock()
+        self._stop = threading.Event()
+
+    # -- Registration service -------------------------------------------------------------
+    def Register(self, request, context):
+        self.registrations.append((request.version, request.endpoint, request.resource_name))
+        if request.version != api.VERSION:
+            context.abort(grpc.StatusCode.INVALID_ARGUMENT, f"unsupported version {request.version}")
+        threading.Thread(target=self._connect, args=(request.endpoint,), daemon=True).start()
+        return api.Empty()
+
+    def start(self):
+        self._stop.clear()
+        try:
+            os.remove(self.sock)
+        except FileNotFoundError:
+            pass
+        self.server = grpc.server(cf.ThreadPoolExecutor(max_workers=4, thread_name_prefix="kubelet"))
+        api.add_servicer(self.server, "Registration", self)
+        self.server.add_insecure_port(api.unix_target(self.sock))
+        self.server.start()
+        return self
+
+    def stop(self):
+        self._stop.set()
+        if self.server is not None:
+            self.server.stop(0.2).wait(1.0)
+            self.server = None
+        if self._channel is not None:
+            self._channel.close()
+            self._channel = None
+
+    def restart(self):
+        self.stop()
+        self.registered.clear()
+        self.start()
+
+    # -- plugin connection ----------------------------------------------------------------
+    def _connect(self, endpoint: str):
+        path = os.path.join(self.dir, endpoint)
+        if self._channel is not None:
+            self._channel.close()
+        ch = grpc.insecure_channel(api.unix_target(path))
+        grpc.channel_ready_future(ch).result(timeout=5)
+        self._channel = ch
+        self._stub = api.Stub(ch, "DevicePlugin")
+        self.options = self._stub.GetDevicePluginOptions(api.Empty(), timeout=5)
+        self._law_thread = threading.Thread(target=self._list_and_watch, args=(self._stub,), daemon=True)
+        self._law_thread.start()
+
+    def _list_and_watch(self, stub):
+        try:
+            for resp in stub.ListAndWatch(api.Empty()):
+                devs = {d.ID: d.health for d in resp.devices}
+                with self.devices_updated:
+                    self.devices = devs
+                    self.list_updates += 1
+                    self.devices_updated.notify_all()
+                self.registered.set()
+                self._report_capacity()
+                if self._stop.is_set():
+                    break
+        except grpc.RpcError as e:
+            if not self._stop.is_set():
+                log.V(2).info("fake kubelet ListAndWatch ended: %s", e.code())
+
+    def _report_capacity(self):
+        if self.client is None or not self.node:
+            return
+        healthy = sum(1 for h in self.devices.values() if h == const.HEALTHY)
+        total = len(self.devices)
+        try:
+            self.client.patch_node_status(self.node, {"status": {"capacity": {self.resource: str(total)},
+                                                                 "allocatable": {self.resource: str(healthy)}}})
+        except Exception as e:  # noqa: BLE001
+            log.warning("fake kubelet capacity report failed: %s", e)
+
+    def wait_devices(self, pred, timeout: float = 10.0) -> bool:
+        t = time.monotonic() + timeout
+        with self.devices_updated:
+            while not pred(self.devices):
+                left = t - time.monotonic()
+                if left <= 0:
+                    return False
+                self.devices_updated.wait(left)
+        return True
+
+    # -- device manager -------------------------------------------------------------------
+    def _free_healthy(self) -> list[str]:
+        used = set().union(*self._allocated.values()) if self._allocated else set()
+        return [d for d, h in self.devices.items() if h == const.HEALTHY and d not in used]
+
+    def admit(self, pod: dict, timeout: float = 10.0) -> Admission:
+        uid = O.uid(pod)
+        adm = Admission(uid, [], [], [])
+        for c in O.containers(pod):
+            n = O.container_limit(c, self.resource)
+            if n <= 0:
+                continue
+            with self._lock:
+                free = self._free_healthy()
+                if len(free) < n:
+                    adm.error = f"insufficient {self.resource}: want {n}, free {len(free)}"
+                    return adm
+                ids = free[:n]
+                if self.options is not None and self.options.get_preferred_allocation_available:
+                    pr = self._stub.GetPreferredAllocation(api.PreferredAllocationRequest(container_requests=[
+                        api.ContainerPreferredAllocationRequest(available_deviceIDs=free, allocation_size=n)]),
+                        timeout=timeout)
+                    pref = list(pr.container_responses[0].deviceIDs) if pr.container_responses else []
+                    if len(pref) == n and set(pref) <= set(free):
+                        ids = pref
+                self._allocated.setdefault(uid, set()).update(ids)
+            t0 = time.perf_counter()
+            try:
+                resp = self._stub.Allocate(api.AllocateRequest(container_requests=[
+                    api.ContainerAllocateRequest(devices_ids=ids)]), timeout=timeout)
+            except grpc.RpcError as e:
+                adm.latencies.append(time.perf_counter() - t0)
+                adm.error = f"Allocate failed: {e.code()} {e.details()}"
+                self.release(uid)
+                return adm
+            adm.latencies.append(time.perf_counter() - t0)
+            adm.responses.append(resp.container_responses[0])
+            adm.device_ids.append(ids)
+        return adm
+
+    def release(self, pod_uid: str):
+        with self._lock:
+            self._allocated.pop(pod_uid, None)
+
+    def allocated_ids(self) -> set:
+        with self._lock:
+            return set().union(*self._allocated.values()) if self._allocated else set()

@@ -1,0 +1,191 @@
+"""Metrics: Allocate phase spans, outcomes, device health — Prometheus text exposition.
+
+The reference has no metrics at all; this is the new build's observability
+layer. Kept dependency-free (a registry per plugin instance, so tests do not fight over a
+process-global registry); ``serve()`` exposes ``/metrics`` and ``/healthz``.
+"""
+from __future__ import annotations
+
+import bisect
+import http.server
+import threading
+import time
+from contextlib import contextmanager
+
+_DEFAULT_BUCKETS = (0.0001, 0.00025, 0.0005, 0.001, 0.0025, 0.005, 0.01, 0.025, 0.05, 0.1,
+                    0.25, 0.5, 1.0, 2.5, 5.0, 10.0)
+
+
+def _labels_key(labels: dict) -> tuple:
+    return tuple(sorted(labels.items()))
+
+
+def _fmt_labels(key: tuple) -> str:
+    if not key:
+        return ""
+    return "{" + ",".join(f'{k}="{v}"' for k, v in key) + "}"
+
+
+class Counter:
+    def __init__(self, name: str, help_: str):
+        self.name, self.help = name, help_
+        self._v: dict[tuple, float] = {}
+        self._lock = threading.Lock()
+
+    def inc(self, amount: float = 1.0, **labels):
+        k = _labels_key(labels)
+        with self._lock:
+            self._v[k] = self._v.get(k, 0.0) + amount
+
+    def value(self, **labels) -> float:
+        return self._v.get(_labels_key(labels), 0.0)
+
+    def render(self):
+        yield f"# HELP {self.name} {self.help}\n# TYPE {self.name} counter\n"
+        for k, v in sorted(self._v.items()):
+            yield f"{self.name}{_fmt_labels(k)} {v}\n"
+
+
+class Gauge(Counter):
+    def set(self, value: float, **labels):
+        with self._lock:
+            self._v[_labels_key(labels)] = float(value)
+
+    def render(self):
+        yield f"# HELP {self.name} {self.help}\n# TYPE {self.name} gauge\n"
+        for k, v in sorted(self._v.items()):
+            yield f"{self.name}{_fmt_labels(k)} {v}\n"
+
+
+class Histogram:
+    """Cumulative-bucket histogram plus a bounded reservoir for exact quantiles."""
+
+    def __init__(self, name: str, help_: str, buckets=_DEFAULT_BUCKETS, reservoir: int = 100_000):
+        self.name, self.help, self.buckets = name, help_, tuple(buckets)
+        self._counts: dict[tuple, list] = {}
+        self._sum: dict[tuple, float] = {}
+        self._samples: dict[tuple, list] = {}
+        self._reservoir = reservoir
+        self._lock = threading.Lock()
+
+    def observe(self, value: float, **labels):
+        k = _labels_key(labels)
+        with self._lock:
+            c = self._counts.setdefault(k, [0] * (len(self.buckets) + 1))
+            c[bisect.bisect_left(self.buckets, value)] += 1
+            self._sum[k] = self._sum.get(k, 0.0) + value
+            s = self._samples.setdefault(k, [])
+            if len(s) < self._reservoir:
+                s.append(value)
+
+    @contextmanager
+    def time(self, **labels):
+        t0 = time.perf_counter()
+        try:
+            yield
+        finally:
+            self.observe(time.perf_counter() - t0, **labels)
+
+    def samples(self, **labels) -> list:
+        return list(self._samples.get(_labels_key(labels), []))
+
+    def quantile(self, q: float, **labels) -> float | None:
+        s = sorted(self._samples.get(_labels_key(labels), []))
+        if not s:
+            return None
+        idx = min(len(s) - 1, max(0, int(round(q * (len(s) - 1)))))
+        return s[idx]
+
+    def count(self, **labels) -> int:
+        return sum(self._counts.get(_labels_key(labels), []))
+
+    def reset(self):
+        with self._lock:
+            self._counts.clear()
+            self._sum.clear()
+            self._samples.clear()
+
+    def render(self):
+        yield f"# HELP {self.name} {self.help}\n# TYPE {self.name} histogram\n"
+        for k, counts in sorted(self._counts.items()):
+            acc = 0
+            for b, c in zip(self.buckets, counts):
+                acc += c
+                lk = _fmt_labels(k + (("le", repr(b)),))
+                yield f"{self.name}_bucket{lk} {acc}\n"
+            acc += counts[-1]
+            yield f"{self.name}_bucket{_fmt_labels(k + (('le', '+Inf'),))} {acc}\n"
+            yield f"{self.name}_sum{_fmt_labels(k)} {self._sum.get(k, 0.0)}\n"
+            yield f"{self.name}_count{_fmt_labels(k)} {acc}\n"
+
+
+class Registry:
+    def __init__(self):
+        self._m: dict[str, object] = {}
+        self._lock = threading.Lock()
+
+    def _get(self, cls, name, help_, **kw):
+        with self._lock:
+            if name not in self._m:
+                self._m[name] = cls(name, help_, **kw)
+            return self._m[name]
+
+    def counter(self, name, help_=""):
+        return self._get(Counter, name, help_)
+
+    def gauge(self, name, help_=""):
+        return self._get(Gauge, name, help_)
+
+    def histogram(self, name, help_="", **kw):
+        return self._get(Histogram, name, help_, **kw)
+
+    def render(self) -> str:
+        out = []
+        for m in list(self._m.values()):
+            out.extend(m.render())
+        return "".join(out)
+
+
+class PluginMetrics:
+    """The plugin's metric set."""
+
+    def __init__(self, registry: Registry | None = None):
+        r = self.registry = registry or Registry()
+        self.allocate_latency = r.histogram("gpushare_allocate_latency_seconds",
+                                            "Allocate RPC latency by phase (lookup/decide/patch/total)")
+        self.allocate_outcomes = r.counter("gpushare_allocate_total", "Allocate outcomes")
+        self.pending_match_failures = r.counter("gpushare_pending_match_failures_total",
+                                                "Allocates with no matching assumed pod")
+        self.units_per_gpu = r.gauge("gpushare_advertised_units", "Advertised gpu-mem units per GPU")
+        self.device_health = r.gauge("gpushare_device_healthy", "1 if the GPU is healthy")
+        self.hbm_used = r.gauge("gpushare_hbm_used_bytes", "HBM in use per GPU (SMI)")
+        self.cache_events = r.counter("gpushare_pod_cache_events_total", "Pod watch-cache events")
+        self.listandwatch_sends = r.counter("gpushare_listandwatch_sends_total", "Device list sends")
+
+
+def serve(registry: Registry, addr: str, health_fn=None) -> http.server.ThreadingHTTPServer:
+    """Start ``/metrics`` + ``/healthz`` on ``host:port`` in a daemon thread."""
+    host, _, port = addr.rpartition(":")
+
+    class H(http.server.BaseHTTPRequestHandler):
+        def do_GET(self):
+            if self.path.startswith("/metrics"):
+                body, ctype, code = registry.render().encode(), "text/plain; version=0.0.4", 200
+            elif self.path.startswith("/healthz"):
+                ok = True if health_fn is None else bool(health_fn())
+                body, ctype, code = (b"ok" if ok else b"unhealthy"), "text/plain", 200 if ok else 503
+            else:
+                body, ctype, code = b"not found", "text/plain", 404
+            self.send_response(code)
+            self.send_header("Content-Type", ctype)
+            self.send_header("Content-Length", str(len(body)))
+            self.end_headers()
+            self.wfile.write(body)
+
+        def log_message(self, *a):
+            pass
+
+    srv = http.server.ThreadingHTTPServer((host or "0.0.0.0", int(port)), H)
+    srv.daemon_threads = True
+    threading.Thread(target=srv.serve_forever, name="metrics", daemon=True).start()
+    return srv

@@ -1,0 +1,54 @@
+"""Locating (and, if needed, building) the in-tree native libraries.
+
+All native artefacts live in ``<package>/_native`` so that they travel with the repository
+snapshot to the GPU box and are visibly loaded from the tree (never from a JIT cache).
+A missing library is an error, not a silent fallback: callers get ``NativeUnavailable``.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+import threading
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NATIVE_DIR = os.path.join(PKG_DIR, "_native")
+REPO_ROOT = os.path.dirname(PKG_DIR)
+BUILD_SCRIPT = os.path.join(REPO_ROOT, "native", "build.py")
+
+LIBS = {
+    "gpuinfo": "libgpushare_gpuinfo.so",
+    "hipshim": "libgpushare_hipquota.so",
+    "kernels": "libgpushare_kernels.so",
+}
+
+_lock = threading.Lock()
+
+
+class NativeUnavailable(RuntimeError):
+    pass
+
+
+def lib_path(target: str) -> str:
+    return os.path.join(NATIVE_DIR, LIBS[target])
+
+
+def ensure_built(target: str, auto_build: bool | None = None) -> str:
+    """Return the path of a native library, building it in-tree when it is missing.
+
+    ``auto_build`` defaults to on unless ``GPUSHARE_NO_AUTOBUILD=1``.
+    """
+    path = lib_path(target)
+    if os.path.exists(path):
+        return path
+    if auto_build is None:
+        auto_build = os.environ.get("GPUSHARE_NO_AUTOBUILD", "") != "1"
+    if auto_build and os.path.exists(BUILD_SCRIPT):
+        with _lock:
+            if not os.path.exists(path):
+                r = subprocess.run([sys.executable, BUILD_SCRIPT, target], capture_output=True, text=True)
+                if r.returncode != 0:
+                    raise NativeUnavailable(f"building {target} failed:\n{r.stdout}\n{r.stderr}")
+    if not os.path.exists(path):
+        raise NativeUnavailable(f"{LIBS[target]} not found in {NATIVE_DIR}; run `python native/build.py {target}`")
+    return path

@@ -1,0 +1,144 @@
+#!/usr/bin/env python3
+"""Build every native component in-tree (outputs under the package's ``_native/`` dir).
+
+Targets
+  gpuinfo   libgpushare_gpuinfo.so + gpushare-smi (C++17, host only; librocm_smi64 is dlopen'ed)
+  hipshim   libgpushare_hipquota.so  (C++17 LD_PRELOAD interposer over the HIP allocation API)
+  kernels   libgpushare_kernels.so   (hand-written HIP/CDNA4 kernels, hipcc --offload-arch=gfx950)
+
+Usage: python native/build.py [targets...] [--force] [--asan] [-j N]
+The build is incremental (mtime based) so ``__graft_entry__.build()`` stays cheap.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import shlex
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+OUT = os.path.join(ROOT, "aliyun_gpushare_device_plugin_amd", "_native")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
+
+CXX = shutil.which("g++") or "g++"
+HIPCC = os.path.join(ROCM, "bin", "hipcc") if os.path.exists(os.path.join(ROCM, "bin", "hipcc")) else "hipcc"
+
+
+def _src(*p):
+    return os.path.join(HERE, *p)
+
+
+def _newer(out, deps):
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def _run(cmd, verbose=True):
+    if verbose:
+        print("+", " ".join(shlex.quote(c) for c in cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise SystemExit(f"native build failed: {cmd[0]} exited {r.returncode}")
+    return r
+
+
+def _headers(d):
+    return [os.path.join(d, f) for f in os.listdir(d) if f.endswith((".h", ".hpp", ".inc"))]
+
+
+def build_gpuinfo(force=False, asan=False):
+    d = _src("gpuinfo")
+    lib = os.path.join(OUT, "libgpushare_gpuinfo.so")
+    deps = [_src("gpuinfo", "gpuinfo.cpp")] + _headers(d)
+    flags = ["-std=c++17", "-O2", "-fPIC", "-Wall", "-Wextra", "-Wno-unused-parameter", f"-I{d}"]
+    if asan:
+        flags += ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-O1"]
+        lib = os.path.join(OUT, "asan", "libgpushare_gpuinfo.so")
+    os.makedirs(os.path.dirname(lib), exist_ok=True)
+    if force or _newer(lib, deps):
+        _run([CXX, *flags, "-shared", "-o", lib, _src("gpuinfo", "gpuinfo.cpp"), "-ldl", "-pthread"])
+    cli = os.path.join(os.path.dirname(lib), "gpushare-smi")
+    if force or _newer(cli, [_src("gpuinfo", "smi_cli.cpp"), lib]):
+        _run([CXX, *flags, "-o", cli, _src("gpuinfo", "smi_cli.cpp"), f"-L{os.path.dirname(lib)}",
+              "-lgpushare_gpuinfo", "-Wl,-rpath,$ORIGIN", "-ldl", "-pthread"])
+    return [lib, cli]
+
+
+def build_hipshim(force=False, asan=False):
+    d = _src("hipshim")
+    src = _src("hipshim", "hipquota.cpp")
+    if not os.path.exists(src):
+        return []
+    lib = os.path.join(OUT, "libgpushare_hipquota.so")
+    flags = ["-std=c++17", "-O2", "-fPIC", "-Wall", "-Wextra", "-Wno-unused-parameter",
+             "-D__HIP_PLATFORM_AMD__", f"-I{ROCM}/include", f"-I{d}", "-fvisibility=hidden"]
+    if asan:
+        flags += ["-fsanitize=address,undefined", "-fno-omit-frame-pointer"]
+        lib = os.path.join(OUT, "asan", "libgpushare_hipquota.so")
+    os.makedirs(os.path.dirname(lib), exist_ok=True)
+    if force or _newer(lib, [src] + _headers(d)):
+        # Deliberately NOT linked against libamdhip64: the real entry points are resolved at
+        # run time from whichever HIP runtime the process loaded (PyTorch bundles its own).
+        _run([CXX, *flags, "-shared", "-o", lib, src, "-ldl", "-pthread", "-lrt"])
+    return [lib]
+
+
+def build_kernels(force=False, asan=False, jobs=4):
+    d = _src("kernels")
+    srcs = sorted(os.path.join(d, f) for f in os.listdir(d) if f.endswith(".hip")) if os.path.isdir(d) else []
+    if not srcs:
+        return []
+    lib = os.path.join(OUT, "libgpushare_kernels.so")
+    objdir = os.path.join(OUT, "obj")
+    os.makedirs(objdir, exist_ok=True)
+    hdrs = _headers(d)
+    flags = ["-std=c++17", "-O3", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
+             "-Wno-unused-result", f"-I{d}", "-D__HIP_PLATFORM_AMD__"]
+    if asan:  # host-side sanitizers only; GPU ASan is not available on the pool
+        flags += ["-Xarch_host", "-fsanitize=address", "-fno-omit-frame-pointer"]
+    objs, todo = [], []
+    for s in srcs:
+        o = os.path.join(objdir, os.path.basename(s)[:-4] + ".o")
+        objs.append(o)
+        if force or _newer(o, [s] + hdrs):
+            todo.append([HIPCC, *flags, "-c", s, "-o", o])
+    with cf.ThreadPoolExecutor(max(1, jobs)) as ex:
+        list(ex.map(_run, todo))
+    if force or todo or _newer(lib, objs):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-o", lib, *objs])
+    return [lib]
+
+
+TARGETS = {"gpuinfo": build_gpuinfo, "hipshim": build_hipshim, "kernels": build_kernels}
+
+
+def build(targets=None, force=False, asan=False, jobs=4):
+    os.makedirs(OUT, exist_ok=True)
+    built = []
+    for t in targets or list(TARGETS):
+        fn = TARGETS[t]
+        built += fn(force=force, asan=asan, jobs=jobs) if t == "kernels" else fn(force=force, asan=asan)
+    return built
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("targets", nargs="*", choices=[[], *TARGETS], default=None)
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--asan", action="store_true", help="host-side ASan/UBSan variants under _native/asan")
+    ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 4))
+    a = ap.parse_args(argv)
+    for p in build(a.targets or None, a.force, a.asan, a.jobs):
+        print("built", os.path.relpath(p, ROOT))
+
+
+if __name__ == "__main__":
+    main()
