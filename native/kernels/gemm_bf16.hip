@@ -1,0 +1,193 @@
+// bf16 GEMM on CDNA4 matrix cores: C[M,N] = epilogue(A[M,K] · B[N,K]^T)
+//
+// "NT" layout = torch.nn.functional.linear (activations [M,K], weights [N,K], both
+// K-contiguous), the shape of every projection in the demo workloads and of the bin-pack
+// traffic generator.
+//
+// Design (cdna_hip_programming.md §5, measured guidance for gfx950):
+//  * 256x256 block tile, BK = 64, 8 waves (2 along M x 4 along N), each wave 128x64 =
+//    8x4 tiles of v_mfma_f32_16x16x32_bf16 (fp32 accumulators, 128 regs/lane);
+//  * operands staged global -> LDS with global_load_lds_dwordx4 (no VGPR round trip), two
+//    64 KiB stages (128 KiB LDS, one block per CU, all LDS in ONE __shared__ array so hipcc
+//    does not drain the DMA before every ds_read);
+//  * the LDS image is lane-linear (a DMA writes base + lane*16), so the bank-conflict
+//    swizzle is applied on the SOURCE address and undone on the ds_read address: chunk c of
+//    row r lives at chunk c ^ ((r >> 1) & 7) of its 128-B row, which makes every 16-lane
+//    ds_read_b128 group hit 16 distinct 16-B slots of the 256-B bank row;
+//  * MFMA operands are swapped (weights as the "A" operand) so each lane's 4 accumulator
+//    registers are 4 consecutive output columns: 8-byte packed bf16 stores;
+//  * XCD-aware bijective block remap + GROUP_M rasterisation so the 8 blocks that share an
+//    XCD's L2 share A panels;
+//  * fused epilogue: + bias[n], SiLU, + residual[m,n] (flags), bf16 output.
+// Requirements (checked by the launcher): K % 64 == 0, lda/ldb % 8 == 0, 16-B aligned A/B,
+// N % 4 == 0, ldc % 4 == 0.
+#include "common.h"
+
+namespace {
+
+constexpr int BM = 256, BN = 256, BK = 64, NTHREADS = 512;
+constexpr int A_STAGE = BM * BK * 2;          // 32 KiB
+constexpr int B_STAGE = BN * BK * 2;          // 32 KiB
+constexpr int STAGE = A_STAGE + B_STAGE;      // 64 KiB
+constexpr int LDS_BYTES = 2 * STAGE;          // 128 KiB
+constexpr int GROUP_M = 8;
+
+enum { EP_BIAS = 1, EP_SILU = 2, EP_RESID = 4 };
+
+__device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+__device__ __forceinline__ void glds16(const void* g, void* lds) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+
+__global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_nt_256(
+    const unsigned short* __restrict__ A, const unsigned short* __restrict__ B, unsigned short* __restrict__ C,
+    const unsigned short* __restrict__ bias, const unsigned short* __restrict__ R, int M, int N, int K, int lda,
+    int ldb, int ldc, int flags) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  // ---- tile assignment: XCD-aware bijective remap, then GROUP_M rasterisation ----
+  const int nbm = (M + BM - 1) / BM, nbn = (N + BN - 1) / BN, nwg = nbm * nbn;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int per_group = GROUP_M * nbn;
+  const int first_m = (wgid / per_group) * GROUP_M;
+  const int gsz = min(nbm - first_m, GROUP_M);
+  const int tm = first_m + (wgid % per_group) % gsz;
+  const int tn = (wgid % per_group) / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+
+  // ---- DMA source pointers: 4 instructions for A, 4 for B per stage ----
+  // instruction i of wave w writes LDS bytes [(i*8 + w) * 1024, +1024) = 8 rows x 128 B;
+  // lane l lands at row (i*8+w)*8 + l/8, chunk slot l%8 which holds logical chunk swz(row, l%8).
+  const unsigned short* srcA[4];
+  const unsigned short* srcB[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (i * 8 + wave) * 8 + (lane >> 3);
+    const int c = swz(row, lane & 7);
+    const int ga = min(m0 + row, M - 1), gb = min(n0 + row, N - 1);
+    srcA[i] = A + (size_t)ga * lda + c * 8;
+    srcB[i] = B + (size_t)gb * ldb + c * 8;
+  }
+  char* const ldsA0 = smem;
+  char* const ldsB0 = smem + A_STAGE;
+
+  auto stage = [&](int buf, int kt) {
+    char* a = ldsA0 + buf * STAGE;
+    char* b = ldsB0 + buf * STAGE;
+    const int koff = kt * BK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      glds16(srcA[i] + koff, a + (i * 8 + wave) * 1024);
+      glds16(srcB[i] + koff, b + (i * 8 + wave) * 1024);
+    }
+  };
+
+  f32x4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // per-lane fragment row offsets (bytes) inside a stage
+  const int arow0 = wm * 128 + (lane & 15);
+  const int brow0 = wn * 64 + (lane & 15);
+  const int csub = lane >> 4;  // which 8-element k chunk inside a 32-wide MFMA k-step
+
+  const int KT = K / BK;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  for (int kt = 0; kt < KT; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < KT) stage(cur ^ 1, kt + 1);
+    const char* a = ldsA0 + cur * STAGE;
+    const char* b = ldsB0 + cur * STAGE;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int c = kk * 4 + csub;
+      bf16x8_t af[8], bfr[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = brow0 + j * 16;
+        bfr[j] = *(const bf16x8_t*)(b + row * 128 + (swz(row, c) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int row = arow0 + i * 16;
+        af[i] = *(const bf16x8_t*)(a + row * 128 + (swz(row, c) << 4));
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          // weights as the first operand: D[n][m] -> lane holds 4 consecutive n of one m
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+
+  // ---- epilogue: lane holds C[m][n..n+3], m = .. + (lane&15), n = .. + (lane>>4)*4 ----
+  const int mbase = m0 + wm * 128 + (lane & 15);
+  const int nbase = n0 + wn * 64 + (lane >> 4) * 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = mbase + i * 16;
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = nbase + j * 16;
+      if (n >= N) continue;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (flags & EP_BIAS) {
+        const u16x4_t bb = *(const u16x4_t*)(bias + n);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) v[t] += bf16_to_f32(bb[t]);
+      }
+      if (flags & EP_SILU) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) v[t] = silu_f32(v[t]);
+      }
+      if (flags & EP_RESID) {
+        const u16x4_t rr = *(const u16x4_t*)(R + (size_t)m * ldc + n);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) v[t] += bf16_to_f32(rr[t]);
+      }
+      u16x4_t o;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) o[t] = f32_to_bf16(v[t]);
+      *(u16x4_t*)(C + (size_t)m * ldc + n) = o;
+    }
+  }
+}
+
+}  // namespace
+
+GS_KERNEL_API int gs_gemm_bf16_nt(const void* A, const void* B, void* C, const void* bias, const void* R, int M,
+                                  int N, int K, int lda, int ldb, int ldc, int flags, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || K % BK || lda % 8 || ldb % 8 || ldc % 4 || N % 4 || lda < K || ldb < K ||
+      ldc < N || ((uintptr_t)A & 15) || ((uintptr_t)B & 15) || ((uintptr_t)C & 7))
+    return GS_EINVAL;
+  if ((flags & EP_BIAS) && !bias) return GS_EINVAL;
+  if ((flags & EP_RESID) && !R) return GS_EINVAL;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_256, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    attr_set = true;
+  }
+  const int nblocks = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  hipLaunchKernelGGL(gemm_bf16_nt_256, dim3(nblocks), dim3(NTHREADS), LDS_BYTES, stream,
+                     (const unsigned short*)A, (const unsigned short*)B, (unsigned short*)C,
+                     (const unsigned short*)bias, (const unsigned short*)R, M, N, K, lda, ldb, ldc, flags);
+  return gs_launch_status();
+}

@@ -1,0 +1,124 @@
+"""Real-MI355X tests of the native device layer and the quota shim (run with ``-m gpu``)."""
+import json
+import os
+import subprocess
+import sys
+import textwrap
+
+import pytest
+
+from aliyun_gpushare_device_plugin_amd import const
+from aliyun_gpushare_device_plugin_amd.device import smi as S
+from aliyun_gpushare_device_plugin_amd.device.model import DeviceModel
+from aliyun_gpushare_device_plugin_amd.utils import units as U
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("backend", ["auto", "rocm_smi", "sysfs"])
+def test_enumerates_mi355x(backend):
+    with S.SMI(backend) as smi:
+        assert smi.count() >= 1
+        g = smi.device(0)
+        assert g.gfx == "gfx950" or backend == "rocm_smi"
+        assert g.vram_total > 280 * (1 << 30)          # 288 GB class HBM3E
+        assert g.uuid.startswith("GPU-") and len(g.uuid) == 20
+        assert g.render_minor >= 128
+        assert os.path.exists(f"/dev/dri/renderD{g.render_minor}")
+
+
+def test_backends_agree():
+    with S.SMI("rocm_smi") as a, S.SMI("sysfs") as b:
+        da, db = a.devices(), b.devices()
+        assert [d.uuid for d in da] == [d.uuid for d in db]
+        assert [d.vram_total for d in da] == [d.vram_total for d in db]
+
+
+def test_advertised_units_mi355x():
+    with S.SMI("auto") as smi:
+        m_near = DeviceModel(smi.devices(), const.GIB, "nearest")
+        m_floor = DeviceModel(smi.devices(), const.GIB, "floor")
+    assert m_near.units_of(0) == 288        # nominal capacity
+    assert m_floor.units_of(0) in (287, 288)
+    ids = m_near.device_list()
+    assert len(ids) == 288 * m_near.count()
+
+
+def test_hip_agrees_with_smi():
+    code = "import torch;print(torch.cuda.get_device_properties(0).total_memory)"
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    with S.SMI("auto") as smi:
+        assert int(r.stdout.strip().splitlines()[-1]) == smi.device(0).vram_total
+
+
+QUOTA_SCRIPT = textwrap.dedent("""
+    import json, torch
+    free, total = torch.cuda.mem_get_info()
+    props = torch.cuda.get_device_properties(0).total_memory
+    out = {"free": free, "total": total, "props": props}
+    x = torch.empty(int(total * 0.8) // 2, dtype=torch.bfloat16, device="cuda")
+    out["ok_alloc"] = True
+    try:
+        y = torch.empty(int(total * 0.5) // 2, dtype=torch.bfloat16, device="cuda")
+        out["over_alloc"] = "allowed"
+    except torch.OutOfMemoryError:
+        out["over_alloc"] = "denied"
+    del x
+    torch.cuda.empty_cache()
+    z = torch.empty(int(total * 0.9) // 2, dtype=torch.bfloat16, device="cuda")
+    out["after_free"] = True
+    print(json.dumps(out))
+""")
+
+
+def _run_under_shim(env_extra, script=QUOTA_SCRIPT):
+    from aliyun_gpushare_device_plugin_amd.utils.native import ensure_built
+    env = dict(os.environ)
+    env.update({"LD_PRELOAD": ensure_built("hipshim"), "GPUSHARE_SHIM_LOG": "1"})
+    env.update({k: str(v) for k, v in env_extra.items()})
+    r = subprocess.run([sys.executable, "-c", script], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads(r.stdout.strip().splitlines()[-1]), r.stderr
+
+
+def test_shim_quota_under_pytorch():
+    out, err = _run_under_shim({const.ENV_RESOURCE_BY_CONTAINER: 64, const.ENV_RESOURCE_BY_DEV: 288})
+    with S.SMI("auto") as smi:
+        real = smi.device(0).vram_total
+    quota = real * 64 // 288
+    assert out["total"] == quota and out["props"] == quota
+    assert out["free"] <= quota
+    assert out["ok_alloc"] and out["over_alloc"] == "denied" and out["after_free"]
+    assert "quota" in err
+
+
+def test_shim_expandable_segments_vmm_path():
+    out, _ = _run_under_shim({const.ENV_RESOURCE_BY_CONTAINER: 32, const.ENV_RESOURCE_BY_DEV: 288,
+                              "PYTORCH_HIP_ALLOC_CONF": "expandable_segments:True"})
+    assert out["over_alloc"] == "denied"
+
+
+def test_granule_matches_hardware():
+    """hipMalloc consumes HBM in 2 MiB fragments on MI355X: the shim's default granule."""
+    code = textwrap.dedent("""
+        import ctypes, json, torch
+        torch.cuda.init()
+        hip = ctypes.CDLL("libamdhip64.so.7")
+        res = {}
+        for sz in (1, 4096, 2 << 20, (2 << 20) + 1, (64 << 20) + 4096):
+            f0, t = ctypes.c_size_t(), ctypes.c_size_t()
+            hip.hipMemGetInfo(ctypes.byref(f0), ctypes.byref(t))
+            p = ctypes.c_void_p()
+            assert hip.hipMalloc(ctypes.byref(p), ctypes.c_size_t(sz)) == 0
+            f1 = ctypes.c_size_t()
+            hip.hipMemGetInfo(ctypes.byref(f1), ctypes.byref(t))
+            res[sz] = f0.value - f1.value
+            hip.hipFree(p)
+        print(json.dumps(res))
+    """)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    res = {int(k): v for k, v in json.loads(r.stdout.strip().splitlines()[-1]).items()}
+    g = 2 << 20
+    for sz, delta in res.items():
+        assert delta == (sz + g - 1) // g * g, (sz, delta)

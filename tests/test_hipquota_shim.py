@@ -1,0 +1,128 @@
+"""CPU tests of the HIP quota shim against a stub HIP runtime (tests/native/fake_hip.c).
+
+The stub has the same soname as ROCm's runtime (libamdhip64.so.7) and a 16 GiB "device";
+the driver program is an ordinary HIP client linked against it, run with the shim in
+LD_PRELOAD — exactly how a container process sees it. Real-hardware coverage of the same
+paths lives in tests/test_gpu_quota.py (marked gpu).
+"""
+import json
+import os
+import subprocess
+import uuid
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GIB = 1 << 30
+MIB = 1 << 20
+
+
+@pytest.fixture(scope="module")
+def stub(tmp_path_factory):
+    d = tmp_path_factory.mktemp("fakehip")
+    lib = d / "libamdhip64.so.7"
+    subprocess.run(["gcc", "-shared", "-fPIC", "-O1", "-Wl,-soname,libamdhip64.so.7", "-o", str(lib),
+                    os.path.join(HERE, "native", "fake_hip.c")], check=True)
+    drv = d / "shim_driver"
+    subprocess.run(["gcc", "-O1", "-o", str(drv), os.path.join(HERE, "native", "shim_driver.c"),
+                    str(lib), f"-Wl,-rpath,{d}"], check=True)
+    return d, drv
+
+
+def run(stub, shim, args, **env):
+    d, drv = stub
+    e = dict(os.environ)
+    e.update({"LD_PRELOAD": shim, "LD_LIBRARY_PATH": str(d)})
+    e.update({k: str(v) for k, v in env.items()})
+    r = subprocess.run([str(drv), *map(str, args)], env=e, capture_output=True, text=True, timeout=30)
+    return [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")], r
+
+
+def ledger():
+    return f"/gs-test-{uuid.uuid4().hex[:12]}"
+
+
+def cleanup(name):
+    try:
+        os.unlink("/dev/shm" + name)
+    except FileNotFoundError:
+        pass
+
+
+def test_quota_from_container_share(stub, native_shim):
+    # 4 of 16 units of a 16 GiB device -> 4 GiB quota
+    out, _ = run(stub, native_shim, ["info", "alloc", 3 * GIB, "alloc", 2 * GIB, "info"],
+                 ALIYUN_COM_GPU_MEM_CONTAINER=4, ALIYUN_COM_GPU_MEM_DEV=16)
+    assert out[0]["total"] == 4 * GIB and out[0]["free"] == 4 * GIB
+    assert out[1]["err"] == 0
+    assert out[2]["err"] == 2                    # hipErrorOutOfMemory: 3 + 2 > 4
+    assert out[3]["free"] == 1 * GIB and out[3]["total"] == 4 * GIB
+
+
+def test_free_releases_charge(stub, native_shim):
+    out, _ = run(stub, native_shim, ["alloc", 3 * GIB, "free", 0, "alloc", 3 * GIB, "info"],
+                 GPUSHARE_QUOTA_BYTES=4 * GIB)
+    assert [o["err"] for o in out[:3]] == [0, 0, 0]
+    assert out[3]["free"] == 1 * GIB
+
+
+def test_cdna4_granule_rounding(stub, native_shim):
+    # 2 MiB allocation granule: a 1-byte hipMalloc costs 2 MiB, 2 MiB + 1 costs 4 MiB
+    out, _ = run(stub, native_shim, ["alloc", 1, "info", "alloc", 2 * MIB + 1, "info"],
+                 GPUSHARE_QUOTA_BYTES=64 * MIB)
+    assert out[1]["free"] == 62 * MIB
+    assert out[3]["free"] == 58 * MIB
+    out, _ = run(stub, native_shim, ["alloc", 1, "info"], GPUSHARE_QUOTA_BYTES=64 * MIB,
+                 GPUSHARE_ALLOC_GRANULE=4096)
+    assert out[1]["free"] == 64 * MIB - 4096
+
+
+def test_async_and_vmm_paths_are_charged(stub, native_shim):
+    out, _ = run(stub, native_shim, ["async", 3 * GIB, "async", 2 * GIB, "vmm", 2 * GIB, "vmm", GIB],
+                 GPUSHARE_QUOTA_BYTES=4 * GIB)
+    assert [o["err"] for o in out] == [0, 2, 2, 0]
+
+
+def test_cgpu_disable_passes_through(stub, native_shim):
+    out, _ = run(stub, native_shim, ["alloc", 10 * GIB, "info"], ALIYUN_COM_GPU_MEM_CONTAINER=1,
+                 ALIYUN_COM_GPU_MEM_DEV=16, CGPU_DISABLE="true")
+    assert out[0]["err"] == 0 and out[1]["total"] == 16 * GIB
+
+
+def test_no_quota_env_passes_through(stub, native_shim):
+    out, _ = run(stub, native_shim, ["alloc", 10 * GIB, "info"])
+    assert out[0]["err"] == 0 and out[1]["total"] == 16 * GIB
+
+
+def test_shared_ledger_across_processes(stub, native_shim):
+    name = ledger()
+    try:
+        d, drv = stub
+        env = dict(os.environ, LD_PRELOAD=native_shim, LD_LIBRARY_PATH=str(d), GPUSHARE_LEDGER=name,
+                   GPUSHARE_QUOTA_BYTES=str(4 * GIB))
+        holder = subprocess.Popen([str(drv), "alloc", str(3 * GIB), "sleep", "3"], env=env,
+                                  stdout=subprocess.PIPE, text=True)
+        first = holder.stdout.readline()
+        assert json.loads(first)["err"] == 0
+        out, _ = run(stub, native_shim, ["alloc", 2 * GIB, "alloc", GIB, "info"], GPUSHARE_LEDGER=name,
+                     GPUSHARE_QUOTA_BYTES=4 * GIB)
+        assert out[0]["err"] == 2        # the other process holds 3 of 4 GiB
+        assert out[1]["err"] == 0
+        holder.wait(timeout=10)
+        # holder exited cleanly: its charge was returned at exit
+        out, _ = run(stub, native_shim, ["alloc", 3 * GIB], GPUSHARE_LEDGER=name, GPUSHARE_QUOTA_BYTES=4 * GIB)
+        assert out[0]["err"] == 0
+    finally:
+        cleanup(name)
+
+
+def test_crashed_process_charge_is_reclaimed(stub, native_shim):
+    name = ledger()
+    try:
+        out, r = run(stub, native_shim, ["alloc", 3 * GIB, "crash"], GPUSHARE_LEDGER=name,
+                     GPUSHARE_QUOTA_BYTES=4 * GIB)
+        assert out[0]["err"] == 0 and r.returncode == 3   # _exit: no atexit cleanup ran
+        out, _ = run(stub, native_shim, ["alloc", 3 * GIB], GPUSHARE_LEDGER=name, GPUSHARE_QUOTA_BYTES=4 * GIB)
+        assert out[0]["err"] == 0                           # dead pid's 3 GiB reclaimed
+    finally:
+        cleanup(name)
