@@ -1,0 +1,62 @@
+"""``gpu-player`` for MI355X: the bin-pack demo workload (reference demo image
+``cheyang/gpu-player:v2``, ``demo/binpack-1/binpack-1.yaml:39``).
+
+A player owns an HBM share (the pod's ``aliyun.com/gpu-mem`` grant) and generates real
+matrix-core traffic in it: bf16 GEMMs on the hand-written gfx950 MFMA kernel, operands
+carved out of the share, on the player's own HIP stream so co-located players genuinely
+share the GPU. Inside a container the share is enforced by the quota shim; in the bench the
+players of one GPU run in one process and the share is allocated explicitly.
+"""
+from __future__ import annotations
+
+import torch
+
+from ..ops import gemm_nt
+
+GIB = 1 << 30
+
+
+class GemmPlayer:
+    def __init__(self, share_bytes: int, device: torch.device | int = 0, m: int = 4096, n: int = 4096,
+                 k: int = 4096, touch_fraction: float = 0.9, seed: int = 0):
+        self.device = torch.device("cuda", device) if isinstance(device, int) else device
+        self.m, self.n, self.k = m, n, k
+        self.stream = torch.cuda.Stream(self.device)
+        need = (m * k + n * k + m * n) * 2
+        self.share_bytes = int(share_bytes * touch_fraction)
+        if self.share_bytes < need:
+            raise ValueError(f"share of {share_bytes} bytes cannot hold a {m}x{n}x{k} GEMM working set")
+        # The pod's HBM share, allocated in one piece like a framework's memory pool. It is
+        # allocated on the device's default stream and recorded onto the pod stream: PyTorch's
+        # caching allocator pools blocks per allocating stream, so a share freed by a retired
+        # pod is then reusable by its replacement instead of forcing free-all + hipMalloc.
+        self.pool = torch.empty(self.share_bytes // 2, dtype=torch.bfloat16, device=self.device)
+        self.pool.record_stream(self.stream)
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self.stream):
+            off = 0
+
+            def carve(r, c):
+                nonlocal off
+                t = self.pool[off: off + r * c].view(r, c)
+                off += r * c
+                return t
+
+            self.a, self.b, self.c = carve(m, k), carve(n, k), carve(m, n)
+            g = torch.Generator(device=self.device).manual_seed(seed)
+            self.a.uniform_(-1, 1, generator=g)
+            self.b.uniform_(-1, 1, generator=g)
+        self.flops = 0.0
+
+    def run(self, iters: int):
+        with torch.cuda.stream(self.stream):
+            for _ in range(iters):
+                gemm_nt(self.a, self.b, out=self.c)
+        self.flops += 2.0 * self.m * self.n * self.k * iters
+
+    def synchronize(self):
+        self.stream.synchronize()
+
+    def release(self):
+        self.synchronize()
+        self.a = self.b = self.c = self.pool = None

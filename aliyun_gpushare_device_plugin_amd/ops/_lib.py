@@ -1,0 +1,62 @@
+"""Loader for ``libgpushare_kernels.so`` (hand-written gfx950 HIP kernels, native/kernels/).
+
+The library is loaded with ctypes into the PyTorch process; it links the same
+``libamdhip64.so.7`` soname PyTorch already loaded, so kernels run on PyTorch's streams.
+There is deliberately no eager fallback: on a GPU box a missing or failing kernel raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+
+from ..utils.native import ensure_built
+
+_lib = None
+_lock = threading.Lock()
+
+_c = ctypes
+_P, _I, _F = _c.c_void_p, _c.c_int, _c.c_float
+
+SIGNATURES = {
+    "gs_gemm_bf16_nt": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
+    "gs_rmsnorm_bf16": [_P, _P, _P, _P, _P, _I, _I, _F, _P],
+    "gs_silu_mul_bf16": [_P, _P, _I, _I, _P],
+    "gs_rope_bf16": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
+    "gs_flash_attn_fwd_bf16": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _F, _I, _P],
+}
+
+ERRORS = {1: "invalid arguments", 2: "kernel launch failed"}
+
+
+class KernelError(RuntimeError):
+    pass
+
+
+def lib():
+    global _lib
+    with _lock:
+        if _lib is None:
+            L = ctypes.CDLL(ensure_built("kernels"))
+            for name, argtypes in SIGNATURES.items():
+                fn = getattr(L, name, None)
+                if fn is None:
+                    continue
+                fn.argtypes = argtypes
+                fn.restype = _I
+            _lib = L
+    return _lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        raise KernelError(f"{what}: {ERRORS.get(rc, rc)}")
+
+
+def stream_ptr(device=None) -> int:
+    import torch
+
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def loaded_path() -> str | None:
+    return getattr(_lib, "_name", None)

@@ -1,0 +1,81 @@
+"""Fused memory-bound ops for the demo Llama workload (native/kernels/elementwise.hip)."""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+
+def _bf16_cuda(t: torch.Tensor, name: str):
+    if t.dtype != torch.bfloat16 or not t.is_cuda or not t.is_contiguous():
+        raise ValueError(f"{name}: expected a contiguous bf16 GPU tensor")
+
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float = 1e-5, residual: torch.Tensor | None = None):
+    """``rmsnorm(x [+ residual]) * w``. With ``residual`` it returns ``(y, x + residual)``
+    (the updated residual stream) from one pass over memory."""
+    _bf16_cuda(x, "x")
+    _bf16_cuda(w, "w")
+    H = x.shape[-1]
+    M = x.numel() // H
+    if w.numel() != H or H % 8 or H > 8192:
+        raise ValueError("rmsnorm needs H % 8 == 0, H <= 8192 and w of length H")
+    y = torch.empty_like(x)
+    if residual is not None:
+        _bf16_cuda(residual, "residual")
+        if residual.shape != x.shape:
+            raise ValueError("residual shape mismatch")
+        r_out = torch.empty_like(x)
+        rc = _lib.lib().gs_rmsnorm_bf16(x.data_ptr(), residual.data_ptr(), r_out.data_ptr(), w.data_ptr(),
+                                        y.data_ptr(), M, H, float(eps), _lib.stream_ptr(x.device))
+        _lib.check(rc, "gs_rmsnorm_bf16")
+        return y, r_out
+    rc = _lib.lib().gs_rmsnorm_bf16(x.data_ptr(), None, None, w.data_ptr(), y.data_ptr(), M, H, float(eps),
+                                    _lib.stream_ptr(x.device))
+    _lib.check(rc, "gs_rmsnorm_bf16")
+    return y
+
+
+def silu_mul(gu: torch.Tensor) -> torch.Tensor:
+    """``silu(gu[..., :F]) * gu[..., F:]`` for the concatenated gate|up projection."""
+    _bf16_cuda(gu, "gu")
+    F2 = gu.shape[-1]
+    if F2 % 16:
+        raise ValueError("silu_mul needs the last dim to be a multiple of 16")
+    F = F2 // 2
+    M = gu.numel() // F2
+    y = torch.empty((*gu.shape[:-1], F), dtype=gu.dtype, device=gu.device)
+    rc = _lib.lib().gs_silu_mul_bf16(gu.data_ptr(), y.data_ptr(), M, F, _lib.stream_ptr(gu.device))
+    _lib.check(rc, "gs_silu_mul_bf16")
+    return y
+
+
+def rope_tables(seq_len: int, head_dim: int, theta: float = 500000.0, device="cuda"):
+    """Host-side precomputed cos/sin tables (Appendix B: no trig on the device)."""
+    inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
+    ang = torch.outer(torch.arange(seq_len, dtype=torch.float64), inv)
+    return ang.cos().float().to(device).contiguous(), ang.sin().float().to(device).contiguous()
+
+
+def rope_(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, nheads: int, head_dim: int,
+          seq_len: int, positions: torch.Tensor | None = None) -> torch.Tensor:
+    """In-place rotate-half RoPE on ``x`` viewed as ``[T, nheads, head_dim]`` with token
+    stride ``x.stride(-2)`` (so q/k slices of a fused qkv buffer work without copies)."""
+    if x.dtype != torch.bfloat16 or not x.is_cuda or x.stride(-1) != 1:
+        raise ValueError("rope_: expected bf16 GPU tensor with contiguous last dim")
+    if head_dim % 8 or cos.shape != (seq_len, head_dim // 2) or sin.shape != cos.shape:
+        raise ValueError("rope_: table shape mismatch")
+    x2 = x.reshape(-1, x.shape[-1]) if x.dim() > 2 else x
+    T, stride = x2.shape[0], x2.stride(0)
+    if x2.shape[-1] < nheads * head_dim:
+        raise ValueError("rope_: row narrower than nheads*head_dim")
+    pos = None
+    if positions is not None:
+        positions = positions.to(torch.int32).contiguous()
+        if positions.numel() != T:
+            raise ValueError("rope_: positions must have one entry per token")
+        pos = positions.data_ptr()
+    rc = _lib.lib().gs_rope_bf16(x2.data_ptr(), cos.data_ptr(), sin.data_ptr(), pos, T, nheads, head_dim, stride,
+                                 seq_len, _lib.stream_ptr(x.device))
+    _lib.check(rc, "gs_rope_bf16")
+    return x

@@ -1,0 +1,103 @@
+"""``linear`` on the gfx950 MFMA GEMM (native/kernels/gemm_bf16.hip).
+
+``linear(x, w, bias=None, residual=None, silu=False)`` = ``epilogue(x @ w.T)`` for bf16
+tensors with fused bias / SiLU / residual-add epilogue. ``Linear`` wraps it in an autograd
+Function whose backward also runs on the same NT kernel (operands transposed once):
+``dX = dY · W`` as NT with ``Wᵀ``; ``dW = dYᵀ · X`` as NT with ``Xᵀ``.
+All shape/alignment requirements are validated on the host before any launch.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+EP_BIAS, EP_SILU, EP_RESID = 1, 2, 4
+
+
+def _check_operand(t: torch.Tensor, name: str):
+    if t.dtype != torch.bfloat16:
+        raise TypeError(f"{name}: expected bfloat16, got {t.dtype}")
+    if not t.is_cuda:
+        raise ValueError(f"{name}: expected a GPU tensor")
+    if t.stride(-1) != 1:
+        raise ValueError(f"{name}: last dimension must be contiguous")
+
+
+def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, bias: torch.Tensor | None = None,
+            residual: torch.Tensor | None = None, silu: bool = False) -> torch.Tensor:
+    """``out[M,N] = epi(a[M,K] @ b[N,K]^T)``; a and b are 2-D row-major (K contiguous)."""
+    _check_operand(a, "a")
+    _check_operand(b, "b")
+    if a.dim() != 2 or b.dim() != 2 or a.shape[1] != b.shape[1]:
+        raise ValueError(f"gemm_nt shapes {tuple(a.shape)} x {tuple(b.shape)}^T")
+    M, K = a.shape
+    N = b.shape[0]
+    if K % 64 or N % 4:
+        raise ValueError(f"gemm_nt needs K % 64 == 0 and N % 4 == 0 (K={K}, N={N})")
+    lda, ldb = a.stride(0), b.stride(0)
+    if lda % 8 or ldb % 8 or a.data_ptr() % 16 or b.data_ptr() % 16:
+        a, b = a.contiguous(), b.contiguous()
+        lda, ldb = a.stride(0), b.stride(0)
+        if lda % 8 or ldb % 8:
+            raise ValueError("gemm_nt needs 16-byte aligned rows")
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    elif out.shape != (M, N) or out.dtype != torch.bfloat16 or out.stride(1) != 1 or out.stride(0) % 4:
+        raise ValueError("bad out tensor")
+    flags = 0
+    bptr = rptr = None
+    if bias is not None:
+        if bias.numel() != N or bias.dtype != torch.bfloat16 or not bias.is_contiguous():
+            raise ValueError("bias must be a contiguous bf16 vector of length N")
+        flags |= EP_BIAS
+        bptr = bias.data_ptr()
+    if silu:
+        flags |= EP_SILU
+    if residual is not None:
+        if residual.shape != (M, N) or residual.dtype != torch.bfloat16 or residual.stride() != out.stride():
+            raise ValueError("residual must match out's shape and strides")
+        flags |= EP_RESID
+        rptr = residual.data_ptr()
+    rc = _lib.lib().gs_gemm_bf16_nt(a.data_ptr(), b.data_ptr(), out.data_ptr(), bptr, rptr, M, N, K, lda, ldb,
+                                    out.stride(0), flags, _lib.stream_ptr(a.device))
+    _lib.check(rc, "gs_gemm_bf16_nt")
+    return out
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None,
+           residual: torch.Tensor | None = None, silu: bool = False) -> torch.Tensor:
+    """``epi(x @ w.T)`` for x of any leading shape ``[..., K]``."""
+    lead = x.shape[:-1]
+    x2 = x.reshape(-1, x.shape[-1])
+    r2 = residual.reshape(-1, w.shape[0]) if residual is not None else None
+    y = gemm_nt(x2, w, bias=bias, residual=r2, silu=silu)
+    return y.reshape(*lead, w.shape[0])
+
+
+class _LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return linear(x, w)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        g2 = gy.reshape(-1, gy.shape[-1]).contiguous()
+        x2 = x.reshape(-1, x.shape[-1])
+        gx = gw = None
+        if ctx.needs_input_grad[0]:
+            gx = gemm_nt(g2, w.t().contiguous()).reshape(x.shape)          # [M,N]·[N,K]
+        if ctx.needs_input_grad[1]:
+            M = x2.shape[0]
+            pad = (-M) % 64   # the contraction (over M) must be a multiple of 64: zero rows add 0
+            if pad:
+                g2 = torch.nn.functional.pad(g2, (0, 0, 0, pad))
+                x2 = torch.nn.functional.pad(x2, (0, 0, 0, pad))
+            gw = gemm_nt(g2.t().contiguous(), x2.t().contiguous())         # [N,M]·[M,K]
+        return gx, gw
+
+
+def linear_autograd(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    return _LinearFn.apply(x, w)

@@ -197,7 +197,7 @@ class Store:
                 return None
             gone = copy.deepcopy(cur)
             self._bump(gone)
-            self._notify("DELETED", cur, None)
+            self._notify("DELETED", gone, None)   # DELETED carries the deletion's resourceVersion
             return gone
 
     def bind_pod(self, ns, name, node):
@@ -272,6 +272,7 @@ _NODE_RE = re.compile(r"^/api/v1/nodes(?:/([^/]+))?(?:/(status))?$")
 class _Handler(http.server.BaseHTTPRequestHandler):
     protocol_version = "HTTP/1.1"
     server_version = "fake-apiserver/1"
+    disable_nagle_algorithm = True   # header and body leave in one segment, no delayed-ACK stall
 
     def log_message(self, *a):
         pass
@@ -285,8 +286,8 @@ class _Handler(http.server.BaseHTTPRequestHandler):
         self.send_response(code)
         self.send_header("Content-Type", "application/json")
         self.send_header("Content-Length", str(len(body)))
-        self.end_headers()
-        self.wfile.write(body)
+        self._headers_buffer.append(b"\r\n" + body)   # one write for headers + body
+        self.flush_headers()
 
     def _status(self, code, reason, msg):
         self._send(code, {"kind": "Status", "apiVersion": "v1", "status": "Failure", "message": msg,

@@ -53,14 +53,20 @@ class SimCluster:
     def __init__(self, nodes: list[tuple[str, str]], workdir: str | None = None, plugin_mode: str = "thread",
                  pod_source: str = "watch", apiserver_latency_s: float = 0.0, shim_host_dir: str | None = None,
                  gpu_indices: list[int] | None = None, health_poll_s: float = 1.0, round_policy: str = "nearest",
-                 extra_plugin_args: list[str] | None = None):
+                 extra_plugin_args: list[str] | None = None, apiserver: str = "thread"):
         self.node_specs = nodes
         self._own_dir = workdir is None
         # short paths: UDS paths are limited to 108 bytes
         self.workdir = workdir or tempfile.mkdtemp(prefix="gs-", dir="/tmp")
         self.plugin_mode = plugin_mode
         self.pod_source = pod_source
-        self.api = FakeAPIServer(latency_s=apiserver_latency_s)
+        # apiserver: "thread" (in-process) or "process" (separate interpreter, so the
+        # control-plane latency is not inflated by this process's GIL)
+        self.api_mode = apiserver
+        self.api = FakeAPIServer(latency_s=apiserver_latency_s) if apiserver == "thread" else None
+        self.api_proc = None
+        self.api_url = None
+        self.apiserver_latency_s = apiserver_latency_s
         self.client: APIClient | None = None
         self.extender: ExtenderSim | None = None
         self.nodes: dict[str, SimNode] = {}
@@ -72,13 +78,33 @@ class SimCluster:
         self._seq = 0
 
     # -- lifecycle ------------------------------------------------------------------------
+    def _start_apiserver(self):
+        if self.api is not None:
+            self.api.start()
+            self.api_url = self.api.url
+            return
+        self.api_proc = subprocess.Popen(
+            [sys.executable, "-m", "aliyun_gpushare_device_plugin_amd.sim.apiserver", "--port", "0",
+             "--latency-ms", str(self.apiserver_latency_s * 1e3)],
+            env=self._child_env(), stdout=subprocess.PIPE, text=True)
+        self.api_url = self.api_proc.stdout.readline().strip()
+        if not self.api_url.startswith("http"):
+            raise RuntimeError("fake apiserver process failed to start")
+
+    @staticmethod
+    def _child_env():
+        env = dict(os.environ)
+        env["PYTHONPATH"] = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))) + \
+            os.pathsep + env.get("PYTHONPATH", "")
+        return env
+
     def start(self, timeout: float = 30.0):
-        self.api.start()
-        self.client = APIClient(KubeConfig(self.api.url))
+        self._start_apiserver()
+        self.client = APIClient(KubeConfig(self.api_url))
         for name, spec in self.node_specs:
             self.client.create_node(make_node(name))
             pdir = os.path.join(self.workdir, name)
-            kl = FakeKubelet(pdir, APIClient(KubeConfig(self.api.url)), name).start()
+            kl = FakeKubelet(pdir, APIClient(KubeConfig(self.api_url)), name).start()
             node = SimNode(name, spec, pdir, kl)
             self.nodes[name] = node
             self._start_plugin(node)
@@ -92,7 +118,7 @@ class SimCluster:
 
     def _plugin_cfg(self, node: SimNode) -> PluginConfig:
         return PluginConfig(node_name=node.name, smi_backend=node.smi_spec, device_plugin_dir=node.plugin_dir,
-                            apiserver=self.api.url, pod_source=self.pod_source,
+                            apiserver=self.api_url, pod_source=self.pod_source,
                             shim_host_dir=self.shim_host_dir, gpu_indices=self.gpu_indices,
                             health_poll_s=self.health_poll_s, round_policy=self.round_policy)
 
@@ -100,7 +126,7 @@ class SimCluster:
         if self.plugin_mode == "process":
             args = [sys.executable, "-m", "aliyun_gpushare_device_plugin_amd.cli.main",
                     "--node-name", node.name, "--smi-backend", node.smi_spec,
-                    "--device-plugin-dir", node.plugin_dir, "--apiserver", self.api.url,
+                    "--device-plugin-dir", node.plugin_dir, "--apiserver", self.api_url,
                     "--pod-source", self.pod_source, "--round", self.round_policy,
                     "--health-poll", str(self.health_poll_s)]
             if self.shim_host_dir:
@@ -108,13 +134,10 @@ class SimCluster:
             if self.gpu_indices:
                 args += ["--gpu-indices", ",".join(map(str, self.gpu_indices))]
             args += self.extra_plugin_args
-            env = dict(os.environ)
-            env["PYTHONPATH"] = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))) + \
-                os.pathsep + env.get("PYTHONPATH", "")
-            node.proc = subprocess.Popen(args, env=env, stdout=subprocess.DEVNULL,
+            node.proc = subprocess.Popen(args, env=self._child_env(), stdout=subprocess.DEVNULL,
                                          stderr=open(os.path.join(self.workdir, f"{node.name}.plugin.log"), "w"))
         else:
-            node.manager = SharedGPUManager(self._plugin_cfg(node), client=APIClient(KubeConfig(self.api.url)))
+            node.manager = SharedGPUManager(self._plugin_cfg(node), client=APIClient(KubeConfig(self.api_url)))
             node.thread = threading.Thread(target=node.manager.run, kwargs={"install_signals": False},
                                            name=f"plugin-{node.name}", daemon=True)
             node.thread.start()
@@ -141,7 +164,14 @@ class SimCluster:
                 except subprocess.TimeoutExpired:
                     node.proc.kill()
             node.kubelet.stop()
-        self.api.stop()
+        if self.api is not None:
+            self.api.stop()
+        if self.api_proc is not None:
+            self.api_proc.terminate()
+            try:
+                self.api_proc.wait(timeout=10)
+            except subprocess.TimeoutExpired:
+                self.api_proc.kill()
         if self._own_dir:
             shutil.rmtree(self.workdir, ignore_errors=True)
 

@@ -1,0 +1,237 @@
+"""Allocate engine (component C5) and annotation protocol (C7), without gRPC or HTTP."""
+import concurrent.futures as cf
+import json
+import threading
+import time
+
+import pytest
+
+from aliyun_gpushare_device_plugin_amd import const
+from aliyun_gpushare_device_plugin_amd.alloc import annotations as A
+from aliyun_gpushare_device_plugin_amd.alloc.engine import AllocationError, Allocator, AllocatorOptions
+from aliyun_gpushare_device_plugin_amd.api import v1beta1 as api
+from aliyun_gpushare_device_plugin_amd.cluster.podcache import PodSource
+from aliyun_gpushare_device_plugin_amd.device.model import DeviceModel
+from aliyun_gpushare_device_plugin_amd.quota import ShimConfig
+from tests.test_units_and_model import gpu
+
+NODE = "node-a"
+
+
+def mkpod(name, mems, idx=None, assume=None, assigned="false", node=NODE, phase="Pending", uid=None):
+    mems = [mems] if isinstance(mems, int) else mems
+    ann = {}
+    if idx is not None:
+        ann[const.ENV_RESOURCE_INDEX] = str(idx)
+    if assume is not None:
+        ann[const.ENV_RESOURCE_ASSUME_TIME] = str(assume)
+    if assigned is not None:
+        ann[const.ENV_ASSIGNED_FLAG] = assigned
+    return {"metadata": {"name": name, "namespace": "default", "uid": uid or f"uid-{name}", "annotations": ann,
+                         "resourceVersion": "1"},
+            "spec": {"nodeName": node, "containers": [
+                {"name": f"c{i}", "resources": {"limits": {const.RESOURCE_NAME: str(m)}} if m else {}}
+                for i, m in enumerate(mems)]},
+            "status": {"phase": phase}}
+
+
+class StaticSource(PodSource):
+    def __init__(self, pods):
+        self.pods = list(pods)
+        self.fresh_calls = 0
+        self.observed = []
+
+    def pending_pods(self, fresh=False):
+        if fresh:
+            self.fresh_calls += 1
+        return [p for p in self.pods if p["status"]["phase"] == "Pending"]
+
+    def observe(self, pod):
+        self.observed.append(pod)
+        for i, p in enumerate(self.pods):
+            if p["metadata"]["uid"] == pod["metadata"]["uid"]:
+                self.pods[i] = pod
+
+
+class FakeClient:
+    """Records PATCHes and applies them to the source's pods."""
+
+    def __init__(self, source, fail=None, delay=0.0):
+        self.source, self.fail, self.delay = source, fail, delay
+        self.patches = []
+        self.lock = threading.Lock()
+
+    def patch_pod(self, ns, name, patch, content_type=None):
+        time.sleep(self.delay)
+        if self.fail:
+            raise self.fail
+        with self.lock:
+            self.patches.append((ns, name, patch))
+            for p in self.source.pods:
+                if p["metadata"]["name"] == name:
+                    new = json.loads(json.dumps(p))
+                    new["metadata"]["annotations"].update(patch["metadata"]["annotations"])
+                    new["metadata"]["resourceVersion"] = str(int(p["metadata"]["resourceVersion"]) + 1)
+                    return new
+        return None
+
+
+def req(*sizes):
+    return api.AllocateRequest(container_requests=[
+        api.ContainerAllocateRequest(devices_ids=[f"id-{i}" for i in range(n)]) for n in sizes])
+
+
+def make(pods, ngpu=2, gib=4, **opts):
+    model = DeviceModel([gpu(i, gib << 30) for i in range(ngpu)], const.GIB)
+    src = StaticSource(pods)
+    cl = FakeClient(src)
+    return Allocator(model, src, cl, NODE, AllocatorOptions(**opts)), src, cl
+
+
+# ---- annotations -------------------------------------------------------------------------
+
+def test_assumed_pod_rules():
+    assert A.is_assumed_pod(mkpod("a", 2, 0, 10))
+    assert not A.is_assumed_pod(mkpod("a", 2, 0, 10, assigned="true"))
+    assert not A.is_assumed_pod(mkpod("a", 2, 0, None))           # no assume time
+    assert not A.is_assumed_pod(mkpod("a", 2, 0, 10, assigned=None))
+    assert not A.is_assumed_pod(mkpod("a", 0, 0, 10))             # no gpu-mem
+
+
+def test_annotation_parsing_and_order():
+    p = mkpod("a", 2, "x", "junk")
+    assert A.gpu_id_from_annotation(p) == -1 and A.assume_time(p) == 0
+    pods = [mkpod("b", 1, 0, 30), mkpod("a", 1, 0, 10), mkpod("c", 1, 0, 20)]
+    assert [x["metadata"]["name"] for x in A.order_by_assume_time(pods)] == ["a", "c", "b"]
+    patch = A.assigned_patch(123)
+    assert patch == {"metadata": {"annotations": {const.ENV_ASSIGNED_FLAG: "true",
+                                                  const.ENV_RESOURCE_ASSUME_TIME: "123"}}}
+
+
+def test_dedupe_drops_other_nodes():
+    pods = [mkpod("a", 1, 0, 1), mkpod("a", 1, 0, 1), mkpod("b", 1, 0, 1, node="other")]
+    assert [p["metadata"]["name"] for p in A.dedupe_by_uid(pods, NODE)] == ["a"]
+
+
+def test_allocation_annotation():
+    p = mkpod("a", 4, 0, 1)
+    p["metadata"]["annotations"][const.GPUSHARE_ALLOCATION_FLAG] = json.dumps({"0": {"1": 2}, "1": {"1": 1, "0": 1}})
+    assert A.allocation_from_annotation(p) == {1: 3, 0: 1}
+    p["metadata"]["annotations"][const.GPUSHARE_ALLOCATION_FLAG] = "{bad"
+    assert A.allocation_from_annotation(p) == {}
+
+
+# ---- engine ------------------------------------------------------------------------------
+
+def test_matches_oldest_equal_request_and_patches():
+    al, src, cl = make([mkpod("young", 2, 1, 200), mkpod("old", 2, 0, 100), mkpod("other", 3, 1, 50)])
+    r = al.allocate(req(2))
+    envs = dict(r.container_responses[0].envs)
+    assert envs[const.ENV_RESOURCE_INDEX] == "0"
+    assert envs[const.ENV_RESOURCE_BY_POD] == "2" and envs[const.ENV_RESOURCE_BY_CONTAINER] == "2"
+    assert envs[const.ENV_RESOURCE_BY_DEV] == "4" and envs[const.ENV_GPU_UUID] == "GPU-0000000000000000"
+    assert "NVIDIA_VISIBLE_DEVICES" not in envs
+    assert [d.host_path for d in r.container_responses[0].devices] == ["/dev/kfd", "/dev/dri/renderD128"]
+    assert cl.patches[0][1] == "old"
+    assert cl.patches[0][2]["metadata"]["annotations"][const.ENV_ASSIGNED_FLAG] == "true"
+    # the just-assigned pod is never matched again, even before a cache refresh
+    r2 = al.allocate(req(2))
+    assert dict(r2.container_responses[0].envs)[const.ENV_RESOURCE_INDEX] == "1"
+    assert [p[1] for p in cl.patches] == ["old", "young"]
+
+
+def test_no_match_multi_gpu_gives_error_response():
+    al, src, cl = make([mkpod("a", 3, 0, 1)])
+    r = al.allocate(req(2))
+    envs = dict(r.container_responses[0].envs)
+    assert envs[const.ENV_RESOURCE_INDEX] == "-1"
+    assert envs["GPUSHARE_ALLOCATION_ERROR"] == "no-gpu-has-2GiB-to-run"
+    assert len(r.container_responses[0].devices) == 0
+    assert src.fresh_calls == 1        # cache miss -> one fresh LIST before giving up
+
+
+def test_strict_mode_raises():
+    al, _, _ = make([], strict=True)
+    with pytest.raises(AllocationError):
+        al.allocate(req(2))
+
+
+def test_single_gpu_fallback_without_pod():
+    al, _, cl = make([], ngpu=1)
+    r = al.allocate(req(2))
+    envs = dict(r.container_responses[0].envs)
+    assert envs[const.ENV_RESOURCE_INDEX] == "0" and not cl.patches
+
+
+def test_bad_index_annotation_is_error():
+    al, _, cl = make([mkpod("a", 2, 7, 1)])
+    assert dict(al.allocate(req(2)).container_responses[0].envs)[const.ENV_RESOURCE_INDEX] == "-1"
+    assert not cl.patches
+
+
+def test_patch_failure_releases_claim():
+    al, src, cl = make([mkpod("a", 2, 0, 1)])
+    cl.fail = RuntimeError("apiserver down")
+    assert dict(al.allocate(req(2)).container_responses[0].envs)[const.ENV_RESOURCE_INDEX] == "-1"
+    cl.fail = None
+    assert dict(al.allocate(req(2)).container_responses[0].envs)[const.ENV_RESOURCE_INDEX] == "0"
+
+
+def test_multi_container_pod_matched_per_container():
+    # reference quirk 3: a pod with 2 gpu containers (1 + 3) never matched a per-container request
+    al, src, cl = make([mkpod("mc", [1, 0, 3], 1, 5)])
+    r1 = al.allocate(req(1))
+    assert dict(r1.container_responses[0].envs)[const.ENV_RESOURCE_INDEX] == "1"
+    assert dict(r1.container_responses[0].envs)[const.ENV_RESOURCE_BY_POD] == "4"
+    assert not cl.patches                       # not all containers allocated yet
+    r2 = al.allocate(req(3))
+    assert dict(r2.container_responses[0].envs)[const.ENV_RESOURCE_INDEX] == "1"
+    assert [p[1] for p in cl.patches] == ["mc"]
+
+
+def test_pod_total_rule_still_wins():
+    al, _, cl = make([mkpod("mc", [1, 3], 0, 5)])
+    r = al.allocate(req(4))    # kubelet sending the whole pod in one request (reference behaviour)
+    assert dict(r.container_responses[0].envs)[const.ENV_RESOURCE_INDEX] == "0"
+    assert [p[1] for p in cl.patches] == ["mc"]
+
+
+def test_concurrent_allocates_never_double_assign():
+    pods = [mkpod(f"p{i}", 2, i % 2, 100 + i) for i in range(16)]
+    al, src, cl = make(pods)
+    cl.delay = 0.005            # PATCH in flight while other Allocates run
+    with cf.ThreadPoolExecutor(8) as ex:
+        rs = list(ex.map(lambda _: al.allocate(req(2)), range(16)))
+    names = [p[1] for p in cl.patches]
+    assert sorted(names) == sorted(f"p{i}" for i in range(16))
+    assert all(dict(r.container_responses[0].envs)[const.ENV_RESOURCE_INDEX] != "-1" for r in rs)
+
+
+def test_shim_injection_and_cgpu_disable():
+    shim = ShimConfig(host_dir="/opt/gpushare/lib")
+    al, _, _ = make([mkpod("a", 2, 0, 1)], shim=shim)
+    r = al.allocate(req(2)).container_responses[0]
+    assert r.envs[const.ENV_LD_PRELOAD] == "/usr/local/gpushare/libgpushare_hipquota.so"
+    assert r.envs[const.ENV_SHIM_LEDGER].startswith("/gpushare-uida-")
+    assert r.mounts[0].host_path == "/opt/gpushare/lib" and r.mounts[0].read_only
+    al, _, _ = make([mkpod("a", 2, 0, 1)], shim=shim, disable_cgpu=True)
+    r = al.allocate(req(2)).container_responses[0]
+    assert r.envs[const.ENV_CGPU_DISABLE] == "true" and const.ENV_LD_PRELOAD not in r.envs
+    assert len(r.mounts) == 0
+
+
+def test_preferred_allocation_picks_assigned_gpu():
+    al, _, _ = make([mkpod("a", 2, 1, 1)])
+    avail = [f"GPU-{g:016x}-_-{j}" for g in (0, 1) for j in range(4)]
+    r = al.preferred(api.PreferredAllocationRequest(container_requests=[
+        api.ContainerPreferredAllocationRequest(available_deviceIDs=avail, allocation_size=2)]))
+    ids = list(r.container_responses[0].deviceIDs)
+    assert len(ids) == 2 and all(i.startswith("GPU-0000000000000001") for i in ids)
+
+
+def test_metrics_recorded():
+    al, _, _ = make([mkpod("a", 2, 0, 1)])
+    al.allocate(req(2))
+    assert al.metrics.allocate_outcomes.value(outcome="assigned") == 1
+    assert al.metrics.allocate_latency.count(phase="total") == 1
+    assert "gpushare_allocate_latency_seconds_bucket" in al.metrics.registry.render()

@@ -1,0 +1,150 @@
+"""End-to-end on CPU: fake apiserver + fake kubelet (gRPC/UDS) + real plugin + extender."""
+import os
+import signal
+import time
+
+import pytest
+
+from aliyun_gpushare_device_plugin_amd import const
+from aliyun_gpushare_device_plugin_amd.api import v1beta1 as api
+from aliyun_gpushare_device_plugin_amd.cluster import objects as O
+from aliyun_gpushare_device_plugin_amd.sim.cluster import SimCluster
+
+
+def envs(adm, i=0):
+    return dict(adm.responses[i].envs)
+
+
+def test_config1_stub_plugin_roundtrip():
+    """BASELINE config 1: 2 fake GPUs x 4 GiB, ListAndWatch/Allocate round trip."""
+    with SimCluster([("node-a", "fake:2x4G")]) as c:
+        node = c.client.get_node("node-a")
+        assert node["status"]["allocatable"][const.RESOURCE_COUNT] == "2"
+        assert node["status"]["allocatable"][const.RESOURCE_NAME] == "8"
+        kl = c.nodes["node-a"].kubelet
+        assert kl.registrations[0] == ("v1beta1", "aliyungpushare.sock", const.RESOURCE_NAME)
+        assert len(kl.devices) == 8 and set(kl.devices.values()) == {const.HEALTHY}
+        assert kl.options.get_preferred_allocation_available
+        gpus = []
+        for _ in range(4):
+            pod, where, adm = c.run_pod(2)
+            assert adm.error is None and envs(adm)[const.ENV_RESOURCE_BY_DEV] == "4"
+            gpus.append(int(envs(adm)[const.ENV_RESOURCE_INDEX]))
+            got = c.client.get_pod("default", O.name(pod))
+            assert O.annotations(got)[const.ENV_ASSIGNED_FLAG] == "true"
+            assert O.phase(got) == "Running"
+        assert sorted(gpus) == [0, 0, 1, 1]
+        # preferred allocation: kubelet's chosen fake IDs belong to the GPU actually used
+        assert {d.split("-_-")[0] for d in adm.device_ids[0]} == {c.manager("node-a").model.uuid_by_index(gpus[-1])}
+        _, where, _ = c.run_pod(1)
+        assert where is None      # node full (8 of 8 GiB)
+
+
+def test_config3_eight_mi355x_mixed_pods():
+    """BASELINE config 3: 8 x MI355X node, 32 mixed 8-128 GiB pods via the extender."""
+    sizes = [128, 64, 64, 32, 96, 96, 64, 32, 128, 96, 56, 8, 64, 64, 96, 64] * 2
+    with SimCluster([("big", "fake:8x309220868096B")]) as c:
+        assert O.node_allocatable(c.client.get_node("big"), const.RESOURCE_NAME) == 8 * 288
+        placed, lat = 0, []
+        for s in sorted(sizes, reverse=True):
+            pod, where, adm = c.run_pod(s)
+            if where is not None:
+                assert adm.error is None
+                placed += 1
+                lat += adm.latencies
+        usage = c.extender.usage()["big"]
+        assert all(u <= 288 for u in usage["used"])      # never over-committed
+        assert placed >= 31 and sum(usage["used"]) >= 0.97 * 8 * 288
+        assert sorted(lat)[len(lat) // 2] < 0.05
+
+
+def test_delete_frees_capacity_and_reuse():
+    with SimCluster([("n", "fake:1x8G")]) as c:
+        p1, _, a1 = c.run_pod(6)
+        _, w, _ = c.run_pod(4)
+        assert w is None
+        c.delete_pod(p1)
+        _, w, a = c.run_pod(4)
+        assert w == ("n", 0) and a.error is None
+
+
+def test_kubelet_restart_triggers_reregistration():
+    with SimCluster([("n", "fake:1x4G")]) as c:
+        kl = c.nodes["n"].kubelet
+        mgr = c.manager("n")
+        kl.restart()                      # re-creates kubelet.sock like a kubelet restart
+        assert kl.registered.wait(15)
+        t = time.time() + 10
+        while mgr.restarts < 1 and time.time() < t:
+            time.sleep(0.05)
+        assert mgr.restarts >= 1 and len(kl.registrations) == 2
+        _, w, adm = c.run_pod(2)
+        assert adm.error is None
+
+
+def test_sighup_restarts_plugin():
+    with SimCluster([("n", "fake:1x4G")]) as c:
+        mgr = c.manager("n")
+        mgr.events.put(("signal", signal.SIGHUP))
+        t = time.time() + 10
+        while mgr.restarts < 1 and time.time() < t:
+            time.sleep(0.05)
+        assert mgr.restarts == 1
+        assert c.nodes["n"].kubelet.registered.wait(10)
+
+
+@pytest.mark.parametrize("source", ["watch", "list"])
+def test_pod_sources(source):
+    with SimCluster([("n", "fake:2x4G")], pod_source=source) as c:
+        for _ in range(3):
+            _, w, adm = c.run_pod(2)
+            assert adm.error is None and envs(adm)[const.ENV_RESOURCE_INDEX] != "-1"
+
+
+def test_watch_cache_used_instead_of_list():
+    with SimCluster([("n", "fake:2x4G")], pod_source="watch") as c:
+        store = c.api.store
+        before = store.requests["GET pods"]
+        for _ in range(4):
+            c.run_pod(1)
+        # no per-Allocate LIST: the informer serves candidates
+        assert store.requests["GET pods"] - before == 0
+
+
+def test_plugin_as_separate_process():
+    with SimCluster([("n", "fake:2x4G")], plugin_mode="process") as c:
+        _, w, adm = c.run_pod(3)
+        assert adm.error is None and envs(adm)[const.ENV_RESOURCE_BY_CONTAINER] == "3"
+
+
+def test_multi_node_cluster():
+    with SimCluster([("a", "fake:1x4G"), ("b", "fake:1x4G")]) as c:
+        nodes = set()
+        for _ in range(4):
+            pod, where, adm = c.run_pod(2)
+            assert adm.error is None
+            nodes.add(where[0])
+        assert nodes == {"a", "b"}
+
+
+def test_cgpu_label_sets_env():
+    with SimCluster([("n", "fake:1x4G")]) as c:
+        c.client.patch_node("n", {"metadata": {"labels": {const.NODE_LABEL_DISABLE_CGPU: "true"}}})
+        c.manager("n").events.put(("signal", signal.SIGHUP))
+        time.sleep(0.5)
+        assert c.nodes["n"].kubelet.registered.wait(10)
+        t = time.time() + 10
+        while c.manager("n").restarts < 1 and time.time() < t:
+            time.sleep(0.05)
+        time.sleep(0.3)
+        _, _, adm = c.run_pod(2)
+        assert envs(adm)[const.ENV_CGPU_DISABLE] == "true"
+
+
+def test_shim_injected_end_to_end(native_shim):
+    shim_dir = os.path.dirname(native_shim)
+    with SimCluster([("n", "fake:1x4G")], shim_host_dir=shim_dir) as c:
+        _, _, adm = c.run_pod(2)
+        r = adm.responses[0]
+        assert r.envs[const.ENV_LD_PRELOAD].endswith(const.SHIM_LIB_NAME)
+        assert r.mounts[0].host_path == shim_dir

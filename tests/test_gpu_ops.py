@@ -1,0 +1,129 @@
+"""Numerics of the hand-written gfx950 kernels against plain PyTorch fp32 references."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _seed():
+    torch.manual_seed(0)
+
+
+def ref_linear(a, b, bias=None, residual=None, silu=False):
+    y = a.float() @ b.float().t()
+    if bias is not None:
+        y = y + bias.float()
+    if silu:
+        y = torch.nn.functional.silu(y)
+    if residual is not None:
+        y = y + residual.float()
+    return y
+
+
+def assert_close_bf16(out, ref, k):
+    # bf16 output rounding (2^-8 relative) + fp32 accumulation over k terms of O(1) products
+    err = (out.float() - ref).abs()
+    tol = 2e-2 * ref.abs() + 2e-3 * (k ** 0.5)
+    bad = (err > tol).sum().item()
+    assert bad == 0, f"{bad} elements out of tolerance, max err {err.max().item()}"
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 256), (4096, 4096, 4096), (1, 256, 128),
+                                   (300, 1000, 192), (8192, 1024, 512), (17, 4, 64)])
+def test_gemm_nt_matches_fp32(M, N, K):
+    from aliyun_gpushare_device_plugin_amd.ops import gemm_nt
+    a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    b = torch.randn(N, K, device="cuda", dtype=torch.bfloat16)
+    out = gemm_nt(a, b)
+    torch.cuda.synchronize()
+    assert_close_bf16(out, ref_linear(a, b), K)
+
+
+def test_gemm_identity_asymmetric():
+    """A = I with an asymmetric B catches a transposed C-write (guide §3)."""
+    from aliyun_gpushare_device_plugin_amd.ops import gemm_nt
+    K = 256
+    a = torch.eye(K, device="cuda", dtype=torch.bfloat16)
+    b = (torch.arange(512 * K, device="cuda") % 251).reshape(512, K).to(torch.bfloat16)
+    out = gemm_nt(a, b)   # = I @ b^T = b^T
+    assert torch.equal(out, b.t().contiguous())
+
+
+def test_gemm_fused_epilogues():
+    from aliyun_gpushare_device_plugin_amd.ops import gemm_nt
+    M, N, K = 384, 512, 320
+    a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    b = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.1
+    bias = torch.randn(N, device="cuda", dtype=torch.bfloat16)
+    res = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    out = gemm_nt(a, b, bias=bias, residual=res, silu=True)
+    assert_close_bf16(out, ref_linear(a, b, bias, res, silu=True), K)
+
+
+def test_gemm_strided_views():
+    from aliyun_gpushare_device_plugin_amd.ops import gemm_nt
+    big = torch.randn(512, 1024, device="cuda", dtype=torch.bfloat16)
+    a = big[:, 256:768]            # lda = 1024, K = 512
+    b = torch.randn(256, 512, device="cuda", dtype=torch.bfloat16)
+    assert_close_bf16(gemm_nt(a, b), ref_linear(a, b), 512)
+
+
+def test_gemm_rejects_bad_shapes():
+    from aliyun_gpushare_device_plugin_amd.ops import gemm_nt
+    a = torch.randn(64, 100, device="cuda", dtype=torch.bfloat16)
+    with pytest.raises(ValueError):
+        gemm_nt(a, torch.randn(64, 100, device="cuda", dtype=torch.bfloat16))
+
+
+def test_linear_autograd_backward():
+    from aliyun_gpushare_device_plugin_amd.ops import linear_autograd
+    x = torch.randn(4, 50, 256, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    w = (torch.randn(512, 256, device="cuda", dtype=torch.bfloat16) * 0.05).requires_grad_()
+    y = linear_autograd(x, w)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    xr, wr = x.detach().float().requires_grad_(), w.detach().float().requires_grad_()
+    (xr @ wr.t()).backward(gy.float())
+    assert_close_bf16(x.grad, xr.grad, 512)
+    assert_close_bf16(w.grad, wr.grad, 200)
+
+
+def test_rmsnorm_and_residual():
+    from aliyun_gpushare_device_plugin_amd.ops import rmsnorm
+    x = torch.randn(37, 4096, device="cuda", dtype=torch.bfloat16)
+    r = torch.randn(37, 4096, device="cuda", dtype=torch.bfloat16)
+    w = torch.rand(4096, device="cuda", dtype=torch.bfloat16) + 0.5
+    y = rmsnorm(x, w, 1e-5)
+    xf = x.float()
+    ref = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-5) * w.float()
+    assert torch.allclose(y.float(), ref, rtol=2e-2, atol=2e-2)
+    y2, h = rmsnorm(x, w, 1e-5, residual=r)
+    hf = (x.float() + r.float()).to(torch.bfloat16).float()
+    assert torch.equal(h, (x.float() + r.float()).to(torch.bfloat16))
+    ref2 = hf * torch.rsqrt(hf.pow(2).mean(-1, keepdim=True) + 1e-5) * w.float()
+    assert torch.allclose(y2.float(), ref2, rtol=2e-2, atol=2e-2)
+
+
+def test_silu_mul():
+    from aliyun_gpushare_device_plugin_amd.ops import silu_mul
+    gu = torch.randn(33, 2 * 1408, device="cuda", dtype=torch.bfloat16)
+    y = silu_mul(gu)
+    ref = torch.nn.functional.silu(gu[:, :1408].float()) * gu[:, 1408:].float()
+    assert torch.allclose(y.float(), ref, rtol=2e-2, atol=2e-2)
+
+
+def test_rope_matches_reference():
+    from aliyun_gpushare_device_plugin_amd.ops import rope_, rope_tables
+    T, H, D = 96, 8, 128
+    cos, sin = rope_tables(T, D)
+    qkv = torch.randn(T, (H + 2) * D, device="cuda", dtype=torch.bfloat16)
+    q = qkv[:, : H * D]
+    ref = q.float().reshape(T, H, D)
+    c, s = cos[:, None, :].float(), sin[:, None, :].float()
+    x1, x2 = ref[..., : D // 2], ref[..., D // 2:]
+    want = torch.cat([x1 * c - x2 * s, x2 * c + x1 * s], -1)
+    untouched = qkv[:, H * D:].clone()
+    rope_(q, cos, sin, H, D, T)
+    assert torch.allclose(q.float().reshape(T, H, D), want, rtol=2e-2, atol=2e-2)
+    assert torch.equal(qkv[:, H * D:], untouched)

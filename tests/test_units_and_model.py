@@ -1,0 +1,87 @@
+"""Capacity math and the fake-device model (component C2)."""
+import pytest
+
+from aliyun_gpushare_device_plugin_amd import const
+from aliyun_gpushare_device_plugin_amd.device.model import DeviceModel, fake_device_id, real_device_id
+from aliyun_gpushare_device_plugin_amd.device.smi import GPU
+from aliyun_gpushare_device_plugin_amd.utils import units as U
+
+MI355X_BYTES = 309_220_868_096   # measured on MI355X (hipMemGetInfo / mem_info_vram_total)
+
+
+def gpu(i, nbytes=MI355X_BYTES, numa=0, health=0):
+    return GPU(index=i, uuid=f"GPU-{i:016x}", bdf=f"0000:{i:02x}:00.0", name="MI355X", gfx="gfx950",
+               vram_total=nbytes, vram_used=0, numa_node=numa, render_minor=128 + i, kfd_node=2 + i,
+               unique_id=i, hive_id=1, num_xcc=8, num_cu=256, compute_partition=1, memory_partition=1,
+               ecc_ue=0, ecc_ce=0, health=health)
+
+
+def test_units_for_mi355x():
+    assert U.units_for_bytes(MI355X_BYTES, const.GIB, "nearest") == 288
+    assert U.units_for_bytes(MI355X_BYTES, const.GIB, "floor") == 287
+    assert U.units_for_bytes(MI355X_BYTES, const.MIB, "floor") == 294896
+    assert U.units_for_bytes(4 << 30, const.GIB, "floor") == 4
+
+
+def test_reference_unit_bug_not_reproduced():
+    # the reference divides NVML *bytes* by 1024 and calls it GiB (nvidia.go:31-38)
+    assert U.units_for_bytes(16 << 30, const.GIB) == 16 != (16 << 30) // 1024
+
+
+def test_quota_is_proportional():
+    assert U.quota_bytes(288, 288, MI355X_BYTES) == MI355X_BYTES
+    assert U.quota_bytes(64, 288, MI355X_BYTES) == MI355X_BYTES * 64 // 288
+    assert U.quota_bytes(0, 288, MI355X_BYTES) == 0
+
+
+def test_normalize_unit_warns_and_defaults():
+    assert U.normalize_unit("MiB") == "MiB"
+    assert U.normalize_unit("TiB") == "GiB"
+
+
+@pytest.mark.parametrize("q,v", [("2", 2), (64, 64), ("1k", 1000), ("1Ki", 1024), ("500m", 1), ("1.5", 2),
+                                 ("2e3", 2000), ("0", 0)])
+def test_parse_quantity(q, v):
+    assert U.parse_quantity(q) == v
+
+
+def test_fake_ids_roundtrip():
+    fid = fake_device_id("GPU-abc", 7)
+    assert fid == "GPU-abc-_-7" and real_device_id(fid) == "GPU-abc"
+
+
+def test_model_device_list_and_topology():
+    m = DeviceModel([gpu(0, numa=0), gpu(1, numa=1)], const.GIB, "nearest")
+    devs = m.device_list()
+    assert len(devs) == 576 and m.total_units() == 576
+    assert devs[0].ID == "GPU-0000000000000000-_-0" and devs[0].health == const.HEALTHY
+    assert devs[300].topology.nodes[0].ID == 1
+    assert m.uuid_by_index(1) == "GPU-0000000000000001" and m.uuid_by_index(5) is None
+
+
+def test_heterogeneous_uses_minimum_by_default():
+    m = DeviceModel([gpu(0, 8 << 30), gpu(1, 4 << 30)], const.GIB, "floor")
+    assert [g.units for g in m.gpus] == [4, 4]
+    m2 = DeviceModel([gpu(0, 8 << 30), gpu(1, 4 << 30)], const.GIB, "floor", homogeneous=False)
+    assert [g.units for g in m2.gpus] == [8, 4]
+
+
+def test_gpu_subset_reindexes():
+    m = DeviceModel([gpu(0), gpu(1), gpu(2)], const.GIB, gpu_indices=[1, 2])
+    assert m.count() == 2 and m.gpus[0].uuid == "GPU-0000000000000001" and m.gpus[0].index == 0
+
+
+def test_health_generation_and_recovery():
+    m = DeviceModel([gpu(0, 4 << 30)], const.GIB)
+    g0 = m.generation
+    assert m.set_health(0, False, "reset")
+    assert m.generation == g0 + 1
+    assert all(d.health == const.UNHEALTHY for d in m.device_list())
+    assert not m.set_health(0, False, "again")    # no change, no wake-up
+    assert m.set_health(0, True, "recovered")
+    assert all(d.health == const.HEALTHY for d in m.device_list())
+
+
+def test_mib_mode_limit():
+    with pytest.raises(ValueError):
+        DeviceModel([gpu(i) for i in range(8)], const.MIB)

@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""GEMM microbenchmark: our gfx950 MFMA kernel vs torch (hipBLASLt) on the same random bf16
+data, interleaved rounds in one process (cdna_hip_programming.md §5.4 rules 24/25).
+
+python tools/bench_gemm.py [--shapes 4096x4096x4096,8192x8192x8192] [--rounds 5] [--iters 20]
+Writes a JSON summary to stdout (and --out if given).
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from aliyun_gpushare_device_plugin_amd.ops import gemm_nt  # noqa: E402
+
+
+def time_fn(fn, iters):
+    start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    start.record()
+    for _ in range(iters):
+        fn()
+    end.record()
+    end.synchronize()
+    return start.elapsed_time(end) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shapes", default="4096x4096x4096,8192x8192x8192,4096x14336x4096,4096x4096x14336,"
+                                        "8192x6144x4096,16384x4096x4096")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    res = []
+    for s in a.shapes.split(","):
+        M, N, K = map(int, s.split("x"))
+        x = torch.empty(M, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)
+        w = torch.empty(N, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)
+        out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        ours = lambda: gemm_nt(x, w, out=out)  # noqa: E731
+        ref = lambda: torch.matmul(x, w.t(), out=out)  # noqa: E731
+        for f in (ours, ref):
+            for _ in range(3):
+                f()
+        torch.cuda.synchronize()
+        t_o, t_r = [], []
+        for _ in range(a.rounds):
+            t_o.append(time_fn(ours, a.iters))
+            t_r.append(time_fn(ref, a.iters))
+        flop = 2.0 * M * N * K
+        mo, mr = statistics.median(t_o), statistics.median(t_r)
+        row = {"shape": [M, N, K], "ours_ms": round(mo, 4), "torch_ms": round(mr, 4),
+               "ours_tflops": round(flop / mo / 1e9, 1), "torch_tflops": round(flop / mr / 1e9, 1),
+               "speedup": round(mr / mo, 3)}
+        res.append(row)
+        print(json.dumps(row), flush=True)
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
