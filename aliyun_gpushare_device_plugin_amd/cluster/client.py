@@ -237,13 +237,17 @@ class APIClient:
         return self.request("POST", f"/api/v1/namespaces/{namespace}/pods/{name}/binding", body=body)
 
     def watch_pods(self, field_selector: str | None = None, resource_version: str | None = None,
-                   timeout_seconds: int = 300, stop: threading.Event | None = None):
+                   timeout_seconds: int = 300, stop: threading.Event | None = None, holder: list | None = None):
         """Yields watch events (dicts with ``type`` and ``object``) until the server ends the
-        stream, the timeout passes or ``stop`` is set. Uses its own connection."""
+        stream (``timeoutSeconds``), or ``stop`` is set and the socket is shut down by
+        ``abort_watch(holder)``. Uses its own connection; reads block without a socket timeout
+        (an idle watch is normal), so stopping works by shutting the socket down."""
         q = {"watch": "1", "fieldSelector": field_selector, "resourceVersion": resource_version,
              "timeoutSeconds": str(timeout_seconds), "allowWatchBookmarks": "true"}
         url = self._prefix + "/api/v1/pods?" + urllib.parse.urlencode({k: v for k, v in q.items() if v})
-        c = self._new_conn(timeout=min(5.0, timeout_seconds))
+        c = self._new_conn()
+        if holder is not None:
+            holder[:] = [c]
         try:
             c.request("GET", url, headers=self._headers())
             r = c.getresponse()
@@ -254,13 +258,10 @@ class APIClient:
                 except ValueError:
                     obj = {}
                 raise APIError(r.status, obj.get("reason", r.reason), obj.get("message", ""), obj)
+            c.sock.settimeout(None)
             buf = b""
-            deadline = time.monotonic() + timeout_seconds + 5
-            while not (stop and stop.is_set()) and time.monotonic() < deadline:
-                try:
-                    chunk = r.read1(65536) if hasattr(r, "read1") else r.read(1)
-                except socket.timeout:
-                    continue
+            while not (stop and stop.is_set()):
+                chunk = r.read1(65536)
                 if not chunk:
                     break
                 buf += chunk
@@ -270,9 +271,19 @@ class APIClient:
                     if line:
                         yield json.loads(line)
         finally:
+            if holder is not None:
+                holder[:] = []
             try:
                 c.close()
             except Exception:
+                pass
+
+    @staticmethod
+    def abort_watch(holder: list | None):
+        for c in list(holder or []):
+            try:
+                c.sock.shutdown(socket.SHUT_RDWR)
+            except (OSError, AttributeError):
                 pass
 
     def close(self):

@@ -100,6 +100,7 @@ class WatchCache(PodSource):
         self._stop = threading.Event()
         self._thread = None
         self._rv = ""
+        self._conn: list = []
         self.relists = 0
         self.events = 0
 
@@ -111,6 +112,7 @@ class WatchCache(PodSource):
 
     def stop(self):
         self._stop.set()
+        self.client.abort_watch(self._conn)
 
     def wait_synced(self, timeout: float = 10.0) -> bool:
         return self._synced.wait(timeout)
@@ -151,7 +153,7 @@ class WatchCache(PodSource):
                 if not self._synced.is_set() or not self._rv:
                     self._relist()
                 for ev in self.client.watch_pods(node_field_selector(self.node), self._rv,
-                                                 self.watch_timeout, self._stop):
+                                                 self.watch_timeout, self._stop, self._conn):
                     self._apply(ev)
                 backoff = 0.05
             except APIError as e:

@@ -1,0 +1,79 @@
+"""Container entry point of the Llama-3-8B demo pod (BASELINE config 4).
+
+Runs inside the environment the plugin's Allocate response created (quota shim preloaded),
+loads a random-init Llama-3-8B, then runs prefill forwards for ``--seconds`` and prints JSON
+lines: the quota it sees, the weight footprint, and tokens/s per interval. ``--probe-quota``
+additionally tries to allocate past the quota and reports whether the shim refused it.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seconds", type=float, default=20.0)
+    ap.add_argument("--batch", type=int, default=4)
+    ap.add_argument("--seq", type=int, default=2048)
+    ap.add_argument("--layers", type=int, default=32)
+    ap.add_argument("--probe-quota", action="store_true")
+    ap.add_argument("--start-file", default=None, help="wait for this file before timing (sync start)")
+    ap.add_argument("--name", default="pod")
+    a = ap.parse_args(argv)
+
+    import torch
+
+    from .llama import LlamaConfig, LlamaModel
+
+    def emit(**kw):
+        kw["pod"] = a.name
+        print(json.dumps(kw), flush=True)
+
+    free, total = torch.cuda.mem_get_info()
+    emit(event="start", quota_total=total, free=free, ld_preload=os.environ.get("LD_PRELOAD", ""),
+         container_units=os.environ.get("ALIYUN_COM_GPU_MEM_CONTAINER"),
+         dev_units=os.environ.get("ALIYUN_COM_GPU_MEM_DEV"))
+    cfg = LlamaConfig.llama3_8b(n_layers=a.layers)
+    model = LlamaModel(cfg, "cuda", seed=hash(a.name) & 0xffff)
+    tok = torch.randint(0, cfg.vocab, (a.batch, a.seq), device="cuda")
+    model.forward(tok)
+    torch.cuda.synchronize()
+    emit(event="loaded", weight_bytes=model.weight_bytes(), params=cfg.n_params())
+    if a.probe_quota:
+        free, total = torch.cuda.mem_get_info()
+        try:
+            x = torch.empty(int(free * 1.5) // 2, dtype=torch.bfloat16, device="cuda")
+            emit(event="quota_probe", over_quota_alloc="allowed")
+            del x
+        except torch.OutOfMemoryError:
+            emit(event="quota_probe", over_quota_alloc="denied")
+        torch.cuda.empty_cache()
+    emit(event="ready")
+    if a.start_file:
+        while not os.path.exists(a.start_file):
+            time.sleep(0.01)
+    t0 = time.perf_counter()
+    n = 0
+    tokens = a.batch * a.seq
+    last = t0
+    while time.perf_counter() - t0 < a.seconds:
+        model.forward(tok)
+        torch.cuda.synchronize()
+        n += 1
+        now = time.perf_counter()
+        if now - last > 5.0:
+            emit(event="progress", iters=n, tokens_per_s=n * tokens / (now - t0))
+            last = now
+    dt = time.perf_counter() - t0
+    flops = model.flops_per_token(a.seq) * tokens * n
+    emit(event="done", iters=n, seconds=dt, tokens_per_s=n * tokens / dt, tflops=flops / dt / 1e12,
+         peak_mem=torch.cuda.max_memory_allocated())
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

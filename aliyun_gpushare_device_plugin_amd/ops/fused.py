@@ -63,8 +63,9 @@ def rope_(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, nheads: int, he
     stride ``x.stride(-2)`` (so q/k slices of a fused qkv buffer work without copies)."""
     if x.dtype != torch.bfloat16 or not x.is_cuda or x.stride(-1) != 1:
         raise ValueError("rope_: expected bf16 GPU tensor with contiguous last dim")
-    if head_dim % 8 or cos.shape != (seq_len, head_dim // 2) or sin.shape != cos.shape:
-        raise ValueError("rope_: table shape mismatch")
+    if head_dim % 8 or cos.dim() != 2 or cos.shape[0] < seq_len or cos.shape[1] != head_dim // 2 \
+            or sin.shape != cos.shape or not cos.is_contiguous() or not sin.is_contiguous():
+        raise ValueError("rope_: tables must be contiguous [>= seq_len, head_dim/2]")
     x2 = x.reshape(-1, x.shape[-1]) if x.dim() > 2 else x
     T, stride = x2.shape[0], x2.stride(0)
     if x2.shape[-1] < nheads * head_dim:
@@ -74,6 +75,8 @@ def rope_(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, nheads: int, he
         positions = positions.to(torch.int32).contiguous()
         if positions.numel() != T:
             raise ValueError("rope_: positions must have one entry per token")
+        if int(positions.max()) >= cos.shape[0] or int(positions.min()) < 0:
+            raise ValueError("rope_: position outside the table")
         pos = positions.data_ptr()
     rc = _lib.lib().gs_rope_bf16(x2.data_ptr(), cos.data_ptr(), sin.data_ptr(), pos, T, nheads, head_dim, stride,
                                  seq_len, _lib.stream_ptr(x.device))

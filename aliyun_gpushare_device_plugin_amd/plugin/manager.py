@@ -96,6 +96,7 @@ class SharedGPUManager:
         if not (self.cfg.export_topology and self.client and self.smi):
             return
         try:
+            self.smi.refresh()                  # link state may have changed since enumeration
             topo = T.build_topology(self.smi, self.cfg.gpu_indices)
             nodestatus.export_topology(self.client, self.cfg.node_name, topo)
         except Exception as e:  # noqa: BLE001 - best effort, never blocks Allocate

@@ -111,6 +111,8 @@ class SimCluster:
         for node in self.nodes.values():
             if not node.kubelet.registered.wait(timeout):
                 raise TimeoutError(f"plugin on {node.name} did not register")
+            if node.manager is not None and not node.manager.started.wait(timeout):
+                raise TimeoutError(f"plugin manager on {node.name} did not finish starting")
             self._wait_capacity(node.name, timeout)
         self.extender = ExtenderSim(self.client)
         self.extender.sync()

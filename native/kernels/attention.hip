@@ -21,6 +21,7 @@ namespace {
 
 constexpr int WAVES = 4, QROWS = 16 * WAVES, KT = 64;
 typedef short v4s __attribute__((ext_vector_type(4)));
+typedef short v8s __attribute__((ext_vector_type(8)));
 
 template <int D>
 struct Cfg {
@@ -34,9 +35,11 @@ struct Cfg {
 
 __device__ __forceinline__ int kswz(int row, int chunk, int nchunk) { return chunk ^ (row & (nchunk - 1)); }
 // V: 8-byte units, unit ^ ((row & 7) << 2)
-__device__ __forceinline__ int vswz_unit(int row, int unit) { return unit ^ ((row & 7) << 2); }
-
 template <int D>
+__device__ __forceinline__ int vswz(int row, int unit) { return unit ^ (((row & 7) << 2) & (D / 4 - 1)); }
+#define vswz_unit(r, u) vswz<D>(r, u)
+
+template <int D, bool TR>
 __global__ __launch_bounds__(256, 2) void flash_fwd(const unsigned short* __restrict__ Q,
                                                     const unsigned short* __restrict__ K,
                                                     const unsigned short* __restrict__ V,
@@ -162,19 +165,24 @@ __global__ __launch_bounds__(256, 2) void flash_fwd(const unsigned short* __rest
         const int q4 = (lane & 15) >> 2, p4 = lane & 3;
         const int r0 = 32 * s2 + 4 * g + q4, r1 = r0 + 16;
         const int unit = 4 * dt + p4;
-        const v4s a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) v4s*)(vb + r0 * C::ROWB + (vswz_unit(r0, unit) << 3)));
-        const v4s a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) v4s*)(vb + r1 * C::ROWB + (vswz_unit(r1, unit) << 3)));
-        bf16x8_t vf;
-        vf[0] = __builtin_bit_cast(__bf16, a0[0]);
-        vf[1] = __builtin_bit_cast(__bf16, a0[1]);
-        vf[2] = __builtin_bit_cast(__bf16, a0[2]);
-        vf[3] = __builtin_bit_cast(__bf16, a0[3]);
-        vf[4] = __builtin_bit_cast(__bf16, a1[0]);
-        vf[5] = __builtin_bit_cast(__bf16, a1[1]);
-        vf[6] = __builtin_bit_cast(__bf16, a1[2]);
-        vf[7] = __builtin_bit_cast(__bf16, a1[3]);
+        v4s a0, a1;
+        if constexpr (TR) {
+          a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) v4s*)(vb + r0 * C::ROWB + (vswz_unit(r0, unit) << 3)));
+          a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) v4s*)(vb + r1 * C::ROWB + (vswz_unit(r1, unit) << 3)));
+        } else {  // debug path: gather the same V^T fragment element by element
+          const int d = 16 * dt + ql;
+          for (int e = 0; e < 4; ++e) {
+            const int ra = 32 * s2 + 4 * g + e, rb = ra + 16;
+            a0[e] = *(const short*)(vb + ra * C::ROWB + (vswz_unit(ra, d >> 2) << 3) + (d & 3) * 2);
+            a1[e] = *(const short*)(vb + rb * C::ROWB + (vswz_unit(rb, d >> 2) << 3) + (d & 3) * 2);
+          }
+        }
+        // whole-vector reinterpretation: element-wise bf16 inserts of the shorts miscompile
+        // (hipcc emits v_perm_b32 with a repeated source register, duplicating elements)
+        const v8s both = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
+        const bf16x8_t vf = __builtin_bit_cast(bf16x8_t, both);
         o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[s2], o[dt], 0, 0, 0);
       }
     }
@@ -197,19 +205,19 @@ __global__ __launch_bounds__(256, 2) void flash_fwd(const unsigned short* __rest
   }
 }
 
-template <int D>
+template <int D, bool TR>
 int launch(const void* q, const void* k, const void* v, void* o, int B, int S, int Hq, int Hkv, int qs, int ks,
            int vs, float scale_log2, int causal, hipStream_t stream) {
   using C = Cfg<D>;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)flash_fwd<D>, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    (void)hipFuncSetAttribute((const void*)flash_fwd<D, TR>, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     attr = true;
   }
   const int nqb = (S + QROWS - 1) / QROWS;
-  hipLaunchKernelGGL(flash_fwd<D>, dim3((unsigned)(B * Hq * nqb)), dim3(256), C::LDS, stream,
+  flash_fwd<D, TR><<<dim3((unsigned)(B * Hq * nqb)), dim3(256), C::LDS, stream>>>(
                      (const unsigned short*)q, (const unsigned short*)k, (const unsigned short*)v,
-                     (unsigned short*)o, B, S, Hq, Hkv, qs, ks, vs, scale_log2, causal);
+                     (unsigned short*)o, B, S, Hq, Hkv, qs, ks, vs, scale_log2, causal & 1);
   return gs_launch_status();
 }
 
@@ -224,6 +232,10 @@ GS_KERNEL_API int gs_flash_attn_fwd_bf16(const void* q, const void* k, const voi
       ((uintptr_t)q & 15) || ((uintptr_t)k & 15) || ((uintptr_t)v & 15) || ((uintptr_t)o & 7))
     return GS_EINVAL;
   const float sl2 = scale * 1.4426950408889634f;
-  return D == 128 ? launch<128>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream)
-                  : launch<64>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
+  // flags: bit0 causal, bit1 debug path (V^T fragments gathered without ds_read_b64_tr_b16)
+  if (causal & 2)
+    return D == 128 ? launch<128, false>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream)
+                    : launch<64, false>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
+  return D == 128 ? launch<128, true>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream)
+                  : launch<64, true>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
 }

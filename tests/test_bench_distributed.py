@@ -1,0 +1,47 @@
+"""bench.py contract on CPU: single process and a 2-rank torchrun (gloo) launch."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REQUIRED = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "config"}
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def parse(out):
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+def test_bench_single_process_cpu():
+    r = subprocess.run([sys.executable, "bench.py", "--no-gpu", "--steps", "4", "--warmup", "1"], cwd=ROOT,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = parse(r.stdout)
+    assert REQUIRED <= set(d) and d["n_gpus"] == 1 and d["steps"] == 4 and d["scaling"] == "weak"
+    assert d["metric"] == json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+    assert d["pods_per_node"] == 4 and d["hbm_gib_per_node"] == 288 and d["failed_admissions"] == 0
+    assert d["allocate_p50_ms"] is not None and d["value"] > 0
+
+
+def test_bench_torchrun_two_ranks_gloo():
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", "2",
+                        "--no-gpu", "--steps", "4", "--warmup", "1"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = parse(r.stdout)           # only rank 0 prints
+    assert d["n_gpus"] == 2 and d["pods_per_node"] == 8 and d["advertised_gib_per_node"] == 576
+    assert d["config"]["parallelism"] == "node2"

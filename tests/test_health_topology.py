@@ -1,0 +1,116 @@
+"""BASELINE config 5 on CPU: health path (hot-unplug, reset, ECC) with recovery, and xGMI
+topology export + TP-pair placement reconcile, through the real plugin and fake kubelet."""
+import json
+import time
+
+from aliyun_gpushare_device_plugin_amd import const
+from aliyun_gpushare_device_plugin_amd.cluster import nodestatus, objects as O
+from aliyun_gpushare_device_plugin_amd.parallel import topology as T
+from aliyun_gpushare_device_plugin_amd.sim.cluster import SimCluster
+
+
+def health_by_gpu(kl, model):
+    out = {}
+    for g in model.gpus:
+        hs = {kl.devices.get(f"{g.uuid}-_-{j}") for j in range(g.units)}
+        out[g.index] = hs.pop() if len(hs) == 1 else "mixed"
+    return out
+
+
+def wait(pred, timeout=10.0):
+    t = time.time() + timeout
+    while time.time() < t:
+        if pred():
+            return True
+        time.sleep(0.02)
+    return False
+
+
+def test_hot_unplug_and_recovery_via_listandwatch():
+    with SimCluster([("n", "fake:4x288G")], health_poll_s=0.2) as c:
+        mgr, kl = c.manager("n"), c.nodes["n"].kubelet
+        model = mgr.model
+        assert set(health_by_gpu(kl, model).values()) == {const.HEALTHY}
+        t0 = time.time()
+        mgr.smi.inject("unplug 2")
+        assert wait(lambda: health_by_gpu(kl, model)[2] == const.UNHEALTHY)
+        time_to_unhealthy = time.time() - t0
+        assert time_to_unhealthy < 2.0
+        assert health_by_gpu(kl, model)[0] == const.HEALTHY
+        # the node's allocatable drops by one GPU's units; health exported for the extender
+        assert wait(lambda: O.node_allocatable(c.client.get_node("n"), const.RESOURCE_NAME) == 3 * 288)
+        h = json.loads(O.annotations(c.client.get_node("n"))[const.NODE_ANNOTATION_HEALTH])
+        assert h["2"]["healthy"] is False and "missing" in h["2"]["reason"]
+        # the extender no longer places pods on GPU 2
+        c.extender.sync()
+        placed = [c.run_pod(288)[1] for _ in range(4)]
+        assert sorted(g for _, g in filter(None, placed)) == [0, 1, 3] and placed.count(None) == 1
+        mgr.smi.inject("replug 2")
+        assert wait(lambda: health_by_gpu(kl, model)[2] == const.HEALTHY)
+        assert model.count() == 4 and model.gpus[2].index == 2   # index stable across unplug
+
+
+def test_reset_marks_unhealthy_then_recovers():
+    with SimCluster([("n", "fake:2x4G")], health_poll_s=0.2) as c:
+        mgr, kl = c.manager("n"), c.nodes["n"].kubelet
+        seen = []
+        orig = mgr.health.handle_event
+
+        def spy(ev):
+            seen.append(ev.name)
+            orig(ev)
+        mgr.health.handle_event = spy
+        mgr.smi.inject("reset 1")
+        assert wait(lambda: "post_reset" in seen)
+        assert wait(lambda: health_by_gpu(kl, mgr.model)[1] == const.HEALTHY)
+        assert kl.list_updates >= 3     # initial + unhealthy + healthy again
+
+
+def test_ecc_uncorrectable_marks_unhealthy_until_reset():
+    with SimCluster([("n", "fake:2x4G")], health_poll_s=0.2) as c:
+        mgr, kl = c.manager("n"), c.nodes["n"].kubelet
+        mgr.smi.inject("ecc 0 2")
+        assert wait(lambda: health_by_gpu(kl, mgr.model)[0] == const.UNHEALTHY)
+        mgr.smi.inject("reset 0")
+        assert wait(lambda: health_by_gpu(kl, mgr.model)[0] == const.HEALTHY)
+
+
+def test_vmfault_is_ignored():
+    with SimCluster([("n", "fake:1x4G")], health_poll_s=0.2) as c:
+        mgr, kl = c.manager("n"), c.nodes["n"].kubelet
+        mgr.smi.inject("vmfault 0")
+        assert wait(lambda: mgr.health.ignored >= 1)
+        assert health_by_gpu(kl, mgr.model)[0] == const.HEALTHY
+
+
+def test_topology_exported_and_tp_pair_placement_reconciles():
+    with SimCluster([("n", "fake:8x288G")], health_poll_s=0.2) as c:
+        mgr = c.manager("n")
+        topo = nodestatus.read_topology(c.client.get_node("n"))
+        assert topo and len(topo["link_type"]) == 8
+        assert topo["link_type"][0][1] == "xgmi" and topo["hops"][0][1] == 1
+        # fill GPUs 0..5 so a TP pair must use 6 and 7, then break the 6<->7 link
+        for _ in range(6):
+            c.run_pod(288)
+        mgr.smi.inject("linkdown 6 7")
+        assert wait(lambda: nodestatus.read_topology(c.client.get_node("n"))["link_type"][6][7] == "pcie")
+        c.extender.sync()
+        pods, placed, adms = c.run_tp_group("g1", 2, 64)
+        assert placed is None                      # only 6,7 have room and they are not xGMI peers
+        for p in pods:
+            c.client.delete_pod("default", O.name(p))
+        mgr.smi.inject("linkup 6 7")
+        assert wait(lambda: nodestatus.read_topology(c.client.get_node("n"))["link_type"][6][7] == "xgmi")
+        c.extender.sync()
+        pods, placed, adms = c.run_tp_group("g2", 2, 64)
+        assert sorted(g for _, g in placed) == [6, 7]
+        assert all(a.error is None for a in adms)
+
+
+def test_best_group_prefers_connected_and_tight():
+    topo = {"link_type": [["self", "xgmi", "pcie"], ["xgmi", "self", "xgmi"], ["pcie", "xgmi", "self"]],
+            "hops": [[0, 1, 3], [1, 0, 1], [3, 1, 0]]}
+    assert T.best_group(topo, [100, 100, 100], 2, 50) in ([0, 1], [1, 2])
+    assert T.best_group(topo, [60, 200, 100], 2, 50) == [0, 1]      # best fit among connected
+    assert T.best_group(topo, [100, 0, 100], 2, 50) is None          # 0-2 only over PCIe
+    assert T.best_group(None, [100, 0, 100], 2, 50) == [0, 2]        # no topology: capacity only

@@ -1,0 +1,145 @@
+#!/usr/bin/env python3
+"""BASELINE config 4: two Llama-3-8B bf16 pods co-located on one MI355X under the HIP quota shim.
+
+1. The real plugin (real SMI) admits two pods of --pod-gib GiB each through the extender and the
+   kubelet; their Allocate responses carry the env contract, /dev/kfd + render node, and the
+   quota shim (mount + LD_PRELOAD).
+2. Each pod runs as its own process with exactly that environment (the shim's container path is
+   mapped back through the response's mount) and runs Llama-3-8B prefill.
+3. Phase "solo": pod A alone. Phase "colocated": A and B together (synchronized start).
+Reports tokens/s solo vs co-located (interference), the quota each pod saw, and whether an
+over-quota allocation was refused. Output: one JSON line (and --out).
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def pod_env(resp) -> dict:
+    env = dict(os.environ)
+    envs = dict(resp.envs)
+    for m in resp.mounts:                     # container path -> host path (no container here)
+        for k, v in list(envs.items()):
+            if v.startswith(m.container_path):
+                envs[k] = m.host_path + v[len(m.container_path):]
+    env.update(envs)
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    return env
+
+
+def run_pods(specs, seconds, args, sync=True):
+    """Start one process per pod; release them together once all report ``ready``."""
+    import queue
+    import threading
+
+    start = os.path.join(tempfile.mkdtemp(prefix="coloc-"), "go")
+    procs, q = [], queue.Queue()
+    lines = {i: [] for i in range(len(specs))}
+    errs = {i: [] for i in range(len(specs))}
+    for i, (name, env, extra) in enumerate(specs):
+        cmd = [sys.executable, "-m", "aliyun_gpushare_device_plugin_amd.models.llama_pod", "--name", name,
+               "--seconds", str(seconds), "--batch", str(args.batch), "--seq", str(args.seq),
+               "--layers", str(args.layers)] + extra + (["--start-file", start] if sync else [])
+        p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+        procs.append(p)
+
+        def pump(i=i, p=p):
+            for line in p.stdout:
+                if line.startswith("{"):
+                    d = json.loads(line)
+                    lines[i].append(d)
+                    q.put((i, d))
+            q.put((i, None))
+
+        def drain(i=i, p=p):
+            for line in p.stderr:
+                errs[i].append(line)
+
+        threading.Thread(target=pump, daemon=True).start()
+        threading.Thread(target=drain, daemon=True).start()
+    ready, ended = set(), set()
+    deadline = time.time() + 900
+    while len(ready) < len(procs):
+        i, d = q.get(timeout=max(1.0, deadline - time.time()))
+        if d is None:
+            ended.add(i)
+            if i not in ready:
+                procs[i].wait()
+                raise RuntimeError(f"pod {i} exited early: {''.join(errs[i])[-3000:]}")
+        elif d["event"] == "ready":
+            ready.add(i)
+    open(start, "w").close()
+    for i, p in enumerate(procs):
+        p.wait(timeout=seconds + 600)
+        if p.returncode != 0:
+            raise RuntimeError(f"pod {i} failed: {''.join(errs[i])[-3000:]}")
+    while len(ended) < len(procs):
+        i, d = q.get(timeout=30)
+        if d is None:
+            ended.add(i)
+    return [lines[i] for i in range(len(procs))]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--pod-gib", type=int, default=64)
+    ap.add_argument("--seconds", type=float, default=20)
+    ap.add_argument("--batch", type=int, default=4)
+    ap.add_argument("--seq", type=int, default=2048)
+    ap.add_argument("--layers", type=int, default=32)
+    ap.add_argument("--smi-backend", default="auto")
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+
+    from aliyun_gpushare_device_plugin_amd.sim.cluster import SimCluster
+    from aliyun_gpushare_device_plugin_amd.utils.native import ensure_built
+
+    shim_dir = os.path.dirname(ensure_built("hipshim"))
+    with SimCluster([("mi355x", args.smi_backend)], shim_host_dir=shim_dir) as c:
+        pa, wa, adm_a = c.run_pod(args.pod_gib, name="llama-a")
+        pb, wb, adm_b = c.run_pod(args.pod_gib, name="llama-b")
+        assert adm_a.error is None and adm_b.error is None and wa[1] == wb[1]
+        env_a, env_b = pod_env(adm_a.responses[0]), pod_env(adm_b.responses[0])
+        alloc_ms = [x * 1e3 for x in adm_a.latencies + adm_b.latencies]
+
+    solo = run_pods([("llama-a", env_a, ["--probe-quota"])], args.seconds, args)[0]
+    both = run_pods([("llama-a", env_a, []), ("llama-b", env_b, [])], args.seconds, args)
+
+    def done(ls):
+        return [x for x in ls if x["event"] == "done"][0]
+
+    def start(ls):
+        return [x for x in ls if x["event"] == "start"][0]
+
+    s = done(solo)
+    ca, cb = done(both[0]), done(both[1])
+    probe = [x for x in solo if x["event"] == "quota_probe"]
+    res = {
+        "config": "2 x Llama-3-8B bf16 pods on one MI355X (BASELINE config 4)",
+        "pod_gib": args.pod_gib, "batch": args.batch, "seq": args.seq, "layers": args.layers,
+        "allocate_ms": [round(x, 3) for x in alloc_ms],
+        "quota_bytes_seen": start(solo)["quota_total"],
+        "over_quota_alloc": probe[0]["over_quota_alloc"] if probe else None,
+        "solo_tokens_per_s": round(s["tokens_per_s"], 1), "solo_tflops": round(s["tflops"], 1),
+        "colocated_tokens_per_s": [round(ca["tokens_per_s"], 1), round(cb["tokens_per_s"], 1)],
+        "colocated_sum_tokens_per_s": round(ca["tokens_per_s"] + cb["tokens_per_s"], 1),
+        "interference": round((ca["tokens_per_s"] + cb["tokens_per_s"]) / 2 / s["tokens_per_s"], 3),
+        "aggregate_speedup_vs_solo": round((ca["tokens_per_s"] + cb["tokens_per_s"]) / s["tokens_per_s"], 3),
+        "peak_mem_bytes": [ca["peak_mem"], cb["peak_mem"]],
+    }
+    line = json.dumps(res)
+    print(line)
+    if args.out:
+        with open(args.out, "w") as f:
+            f.write(line + "\n")
+
+
+if __name__ == "__main__":
+    main()

@@ -9,9 +9,10 @@ import re
 
 
 def short(name: str) -> str:
+    name = name.replace("(anonymous namespace)::", "")
     name = re.sub(r"\(.*", "", name)          # drop argument lists
     name = re.sub(r"<.*", "", name)           # drop template args
-    return name.replace("(anonymous namespace)::", "")[:70]
+    return name.replace("void ", "")[:70]
 
 
 def main():
