@@ -54,6 +54,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--gpu-indices", default="", help="comma-separated subset of GPUs to manage")
     p.add_argument("--shim-path", default=os.environ.get("GPUSHARE_SHIM_HOST_DIR", ""),
                    help="host directory containing libgpushare_hipquota.so to inject (empty: no shim)")
+    p.add_argument("--install-shim", default="",
+                   help="copy the bundled libgpushare_hipquota.so into this host directory at startup and "
+                        "inject it from there (DaemonSet hostPath, e.g. /var/lib/gpushare/lib)")
     p.add_argument("--strict-allocate", action="store_true",
                    help="fail Allocate with a gRPC error instead of an error-shaped response")
     p.add_argument("--no-preferred-allocation", action="store_true")
@@ -79,11 +82,31 @@ def config_from_args(a) -> PluginConfig:
         rocr_visible=a.rocr_visible_devices, metrics_addr=a.metrics_addr, mps=_bool(a.mps))
 
 
+def install_shim(dest_dir: str) -> str:
+    """Atomically place the quota shim where containers can bind-mount it from the host."""
+    import shutil
+    import tempfile
+
+    from ..utils.native import ensure_built
+
+    src = ensure_built("hipshim")
+    os.makedirs(dest_dir, exist_ok=True)
+    fd, tmp = tempfile.mkstemp(dir=dest_dir, prefix=".shim-")
+    os.close(fd)
+    shutil.copyfile(src, tmp)
+    os.chmod(tmp, 0o755)
+    os.replace(tmp, os.path.join(dest_dir, const.SHIM_LIB_NAME))
+    log.info("installed quota shim into %s", dest_dir)
+    return dest_dir
+
+
 def main(argv=None) -> int:
     a = build_parser().parse_args(argv)
     log.setup(verbosity=a.v, json_lines=a.log_json)
     log.V(1).info("Start gpushare device plugin")
     cfg = config_from_args(a)
+    if a.install_shim:
+        cfg.shim_host_dir = install_shim(a.install_shim)
     if not cfg.node_name:
         log.error("Please set env NODE_NAME (or --node-name)")
         return 1

@@ -45,3 +45,13 @@ def test_bench_torchrun_two_ranks_gloo():
     d = parse(r.stdout)           # only rank 0 prints
     assert d["n_gpus"] == 2 and d["pods_per_node"] == 8 and d["advertised_gib_per_node"] == 576
     assert d["config"]["parallelism"] == "node2"
+
+
+def test_tp_pair_demo_gloo():
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "-m",
+                        "aliyun_gpushare_device_plugin_amd.parallel.tp_demo", "--iters", "2"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = parse(r.stdout)
+    assert d["world"] == 2 and d["tp_block_rel_err"] < 1e-3 and d["backend"] == "gloo"

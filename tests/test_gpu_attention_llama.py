@@ -61,4 +61,5 @@ def test_llama3_8b_shapes_run():
     tok = torch.randint(0, cfg.vocab, (1, 512), device="cuda")
     out = m.forward(tok)
     assert out.shape == (1, cfg.vocab) and torch.isfinite(out.float()).all()
-    assert abs(cfg.n_params() - 8.03e9) / 8.03e9 < 0.01   # full config = Llama-3-8B size
+    full = LlamaConfig.llama3_8b().n_params()
+    assert abs(full - 8.03e9) / 8.03e9 < 0.01   # full config = Llama-3-8B size
