@@ -20,7 +20,11 @@ MI355X build, same protocol, different mechanics:
 * multi-container pods are matched container by container (quirk 3) after the
   reference's pod-total rule has been tried;
 * conflicts are detected by HTTP status, not by comparing error strings (quirk 8);
-* ``--strict-allocate`` returns a gRPC error instead of the soft failure (quirk 6).
+* ``--strict-allocate`` returns a gRPC error instead of the soft failure (quirk 6);
+* optional write-behind of the ASSIGNED patch (``async_patch``): a matched pod is claimed in
+  memory and the annotation is landed by a retrying background patcher, taking the apiserver
+  round trip off the kubelet's admission path; candidates are Pending pods only and the claim
+  is held until the patch is acknowledged, so a pod is never matched twice.
 """
 from __future__ import annotations
 
@@ -55,6 +59,10 @@ class AllocatorOptions:
     rocr_visible: bool = False
     match_containers: bool = True
     claim_ttl_s: float = 120.0
+    # Write-behind ASSIGNED=true PATCH: Allocate answers after the in-memory claim and a
+    # background patcher lands the annotation (retrying); the claim blocks re-matching until it
+    # has. False = the reference's synchronous PATCH inside Allocate (allocate.go:132-152).
+    async_patch: bool = False
 
 
 @dataclasses.dataclass
@@ -76,6 +84,12 @@ class Allocator:
         self._mu = threading.Lock()
         self._claims: dict[str, _Claim] = {}      # in-flight (multi-container or PATCH pending)
         self._assigned: dict[str, float] = {}     # uid -> time we assigned it (stale-cache guard)
+        self._unpatched: set[str] = set()         # assigned locally, PATCH not yet acknowledged
+        self._patch_q = None
+        if self.opts.async_patch:
+            import queue
+            self._patch_q = queue.Queue()
+            threading.Thread(target=self._patcher, name="assign-patcher", daemon=True).start()
 
     # ------------------------------------------------------------------------------------
     # candidate selection
@@ -84,7 +98,7 @@ class Allocator:
         pods = A.dedupe_by_uid(self.pods.pending_pods(fresh=fresh), self.node)
         now = time.monotonic()
         for u, t in list(self._assigned.items()):
-            if now - t > self.opts.claim_ttl_s:
+            if now - t > self.opts.claim_ttl_s and u not in self._unpatched:
                 del self._assigned[u]
         out = [p for p in pods if A.is_assumed_pod(p) and O.uid(p) not in self._assigned]
         if log.V(4):
@@ -229,6 +243,18 @@ class Allocator:
             return resp
 
         t3 = time.perf_counter()
+        if self._patch_q is not None:
+            with self._mu:
+                self._claims.pop(claim.uid, None)
+                self._assigned[claim.uid] = time.monotonic()
+                self._unpatched.add(claim.uid)
+            self._patch_q.put(claim.pod)
+            hist.observe(time.perf_counter() - t3, phase="patch")
+            hist.observe(time.perf_counter() - t0, phase="total")
+            self.metrics.allocate_outcomes.inc(outcome="assigned")
+            log.info("pod %s, new allocated GPUs info: gpu index %d uuid %s (patch queued)", O.name(claim.pod), idx,
+                     self.model.uuid_by_index(idx))
+            return resp
         try:
             updated = self._patch_assigned(claim.pod)
         except Exception as e:  # noqa: BLE001
@@ -248,6 +274,39 @@ class Allocator:
         log.info("pod %s, new allocated GPUs info: gpu index %d uuid %s", O.name(claim.pod), idx,
                  self.model.uuid_by_index(idx))
         return resp
+
+    def _patcher(self):
+        """Lands queued ASSIGNED=true patches; retries with backoff until the pod is gone."""
+        while True:
+            pod = self._patch_q.get()
+            delay = 0.05
+            while True:
+                try:
+                    updated = self._patch_assigned(pod)
+                    if updated:
+                        self.pods.observe(updated)
+                    break
+                except APIError as e:
+                    if e.not_found:
+                        break
+                    log.warning("assign patch for %s failed (%s); retrying", O.name(pod), e)
+                except Exception as e:  # noqa: BLE001 - transport errors
+                    log.warning("assign patch for %s failed (%s); retrying", O.name(pod), e)
+                time.sleep(delay)
+                delay = min(delay * 2, 5.0)
+            with self._mu:
+                self._unpatched.discard(O.uid(pod))
+                self._assigned[O.uid(pod)] = time.monotonic()
+
+    def flush_patches(self, timeout: float = 10.0) -> bool:
+        """Wait until every queued ASSIGNED patch has landed (tests, shutdown)."""
+        t = time.monotonic() + timeout
+        while time.monotonic() < t:
+            with self._mu:
+                if not self._unpatched:
+                    return True
+            time.sleep(0.005)
+        return False
 
     def _patch_assigned(self, pod: dict) -> dict | None:
         if self.client is None:
@@ -281,13 +340,21 @@ class Allocator:
                     target = self.model.uuid_by_index(A.gpu_id_from_annotation(p))
                     break
             picked = list(must)
-            pool = [d for d in avail if d not in set(must)]
-            if target:
-                pool.sort(key=lambda d: real_device_id(d) != target)
-            for d in pool:
+            taken = set(must)
+            if target:   # one linear pass, no sort: IDs of the target GPU first
+                prefix = target + const.FAKE_ID_SEP
+                for d in avail:
+                    if len(picked) >= size:
+                        break
+                    if d.startswith(prefix) and d not in taken:
+                        picked.append(d)
+                        taken.add(d)
+            for d in avail:
                 if len(picked) >= size:
                     break
-                picked.append(d)
+                if d not in taken:
+                    picked.append(d)
+                    taken.add(d)
             resp.container_responses.add(deviceIDs=picked[:max(size, len(must))])
         return resp
 

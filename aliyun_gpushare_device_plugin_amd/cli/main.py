@@ -59,7 +59,11 @@ def build_parser() -> argparse.ArgumentParser:
                         "inject it from there (DaemonSet hostPath, e.g. /var/lib/gpushare/lib)")
     p.add_argument("--strict-allocate", action="store_true",
                    help="fail Allocate with a gRPC error instead of an error-shaped response")
-    p.add_argument("--no-preferred-allocation", action="store_true")
+    p.add_argument("--preferred-allocation", action="store_true",
+                   help="advertise GetPreferredAllocation: the kubelet then picks fake IDs of the GPU the "
+                        "extender chose (accurate device checkpoint, one extra RPC per container)")
+    p.add_argument("--sync-patch", action="store_true",
+                   help="PATCH ASSIGNED=true inside Allocate (reference behaviour) instead of write-behind")
     p.add_argument("--export-topology", nargs="?", const="true", default="true")
     p.add_argument("--rocr-visible-devices", action="store_true",
                    help="also set ROCR_VISIBLE_DEVICES=<uuid> in containers")
@@ -78,8 +82,9 @@ def config_from_args(a) -> PluginConfig:
         kubeconfig=a.kubeconfig, apiserver=a.apiserver,
         gpu_indices=[int(x) for x in a.gpu_indices.split(",") if x.strip()] or None,
         shim_host_dir=a.shim_path or None, strict_allocate=a.strict_allocate,
-        preferred_allocation=not a.no_preferred_allocation, export_topology=_bool(a.export_topology),
-        rocr_visible=a.rocr_visible_devices, metrics_addr=a.metrics_addr, mps=_bool(a.mps))
+        preferred_allocation=a.preferred_allocation, export_topology=_bool(a.export_topology),
+        rocr_visible=a.rocr_visible_devices, metrics_addr=a.metrics_addr, mps=_bool(a.mps),
+        async_patch=not a.sync_patch)
 
 
 def install_shim(dest_dir: str) -> str:

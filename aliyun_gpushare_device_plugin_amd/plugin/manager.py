@@ -58,11 +58,12 @@ class PluginConfig:
     gpu_indices: list | None = None
     shim_host_dir: str | None = None     # None = do not inject the quota shim
     strict_allocate: bool = False
-    preferred_allocation: bool = True
+    preferred_allocation: bool = False   # opt-in: costs the kubelet one extra RPC per container
     export_topology: bool = True
     expose_devices: bool = True
     rocr_visible: bool = False
     metrics_addr: str | None = None
+    async_patch: bool = True             # write-behind ASSIGNED patch (see AllocatorOptions)
     mps: bool = False                    # accepted for flag compatibility; ignored
 
 
@@ -143,7 +144,7 @@ class SharedGPUManager:
         allocator = Allocator(model, src, self.client, cfg.node_name,
                               AllocatorOptions(unit=cfg.memory_unit, disable_cgpu=disable_cgpu, shim=shim,
                                                strict=cfg.strict_allocate, expose_devices=cfg.expose_devices,
-                                               rocr_visible=cfg.rocr_visible),
+                                               rocr_visible=cfg.rocr_visible, async_patch=cfg.async_patch),
                               self.metrics)
         self.model = model
         return DevicePluginServer(model, allocator, self._plugin_socket(), const.RESOURCE_NAME,

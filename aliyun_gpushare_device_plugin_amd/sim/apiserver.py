@@ -183,6 +183,7 @@ class Store:
             if status_only:
                 patch = {"status": (patch or {}).get("status", {})}
             new = strategic_merge(cur, patch)
+            new["metadata"] = dict(new["metadata"])   # never mutate the stored/history version
             new["metadata"]["uid"] = cur["metadata"]["uid"]
             new["metadata"]["name"], new["metadata"]["namespace"] = name, ns
             self._bump(new)
@@ -195,7 +196,8 @@ class Store:
             cur = self.pods.pop((ns, name), None)
             if cur is None:
                 return None
-            gone = copy.deepcopy(cur)
+            gone = dict(cur)
+            gone["metadata"] = dict(cur["metadata"])
             self._bump(gone)
             self._notify("DELETED", gone, None)   # DELETED carries the deletion's resourceVersion
             return gone
@@ -213,7 +215,7 @@ class Store:
 
     def list_pods(self, ns=None, fsel=None, lsel=None):
         with self.lock:
-            items = [copy.deepcopy(p) for (pns, _), p in self.pods.items()
+            items = [p for (pns, _), p in self.pods.items()
                      if (ns is None or pns == ns) and matches(p, fsel or [], lsel or [])]
             return items, str(self.rv)
 
@@ -241,6 +243,7 @@ class Store:
             else:
                 patch = {k: v for k, v in (patch or {}).items() if k != "status"}
             new = strategic_merge(cur, patch)
+            new["metadata"] = dict(new["metadata"])
             self._bump(new)
             self.nodes[name] = new
             return new
@@ -320,16 +323,15 @@ class _Handler(http.server.BaseHTTPRequestHandler):
         if m and m.group(2) and not m.group(3):
             with self.store.lock:
                 p = self.store.pods.get((m.group(1), m.group(2)))
-                p = copy.deepcopy(p) if p else None
             return self._send(200, p) if p else self._status(404, "NotFound", f'pods "{m.group(2)}" not found')
         m = _NODE_RE.match(path)
         if m:
             with self.store.lock:
                 if m.group(1):
-                    n = copy.deepcopy(self.store.nodes.get(m.group(1)))
+                    n = self.store.nodes.get(m.group(1))
                     return self._send(200, n) if n else self._status(404, "NotFound",
                                                                      f'nodes "{m.group(1)}" not found')
-                items = [copy.deepcopy(n) for n in self.store.nodes.values() if matches(n, fsel, lsel)]
+                items = [n for n in self.store.nodes.values() if matches(n, fsel, lsel)]
             return self._send(200, {"kind": "NodeList", "apiVersion": "v1",
                                     "metadata": {"resourceVersion": str(self.store.rv)}, "items": items})
         return self._status(404, "NotFound", path)

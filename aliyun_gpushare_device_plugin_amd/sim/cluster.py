@@ -9,6 +9,7 @@ in production: create → extender filter/bind (annotations) → kubelet admissi
 from __future__ import annotations
 
 import dataclasses
+import itertools
 import os
 import shutil
 import subprocess
@@ -53,7 +54,8 @@ class SimCluster:
     def __init__(self, nodes: list[tuple[str, str]], workdir: str | None = None, plugin_mode: str = "thread",
                  pod_source: str = "watch", apiserver_latency_s: float = 0.0, shim_host_dir: str | None = None,
                  gpu_indices: list[int] | None = None, health_poll_s: float = 1.0, round_policy: str = "nearest",
-                 extra_plugin_args: list[str] | None = None, apiserver: str = "thread"):
+                 extra_plugin_args: list[str] | None = None, apiserver: str = "thread",
+                 preferred_allocation: bool = False):
         self.node_specs = nodes
         self._own_dir = workdir is None
         # short paths: UDS paths are limited to 108 bytes
@@ -75,7 +77,10 @@ class SimCluster:
         self.health_poll_s = health_poll_s
         self.round_policy = round_policy
         self.extra_plugin_args = extra_plugin_args or []
-        self._seq = 0
+        self.preferred_allocation = preferred_allocation
+        self._seq = itertools.count(1)
+        import concurrent.futures as cf
+        self._bg = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="status")   # ordered
 
     # -- lifecycle ------------------------------------------------------------------------
     def _start_apiserver(self):
@@ -122,7 +127,8 @@ class SimCluster:
         return PluginConfig(node_name=node.name, smi_backend=node.smi_spec, device_plugin_dir=node.plugin_dir,
                             apiserver=self.api_url, pod_source=self.pod_source,
                             shim_host_dir=self.shim_host_dir, gpu_indices=self.gpu_indices,
-                            health_poll_s=self.health_poll_s, round_policy=self.round_policy)
+                            health_poll_s=self.health_poll_s, round_policy=self.round_policy,
+                            preferred_allocation=self.preferred_allocation)
 
     def _start_plugin(self, node: SimNode):
         if self.plugin_mode == "process":
@@ -135,6 +141,8 @@ class SimCluster:
                 args += ["--shim-path", self.shim_host_dir]
             if self.gpu_indices:
                 args += ["--gpu-indices", ",".join(map(str, self.gpu_indices))]
+            if self.preferred_allocation:
+                args += ["--preferred-allocation"]
             args += self.extra_plugin_args
             node.proc = subprocess.Popen(args, env=self._child_env(), stdout=subprocess.DEVNULL,
                                          stderr=open(os.path.join(self.workdir, f"{node.name}.plugin.log"), "w"))
@@ -154,6 +162,7 @@ class SimCluster:
         raise TimeoutError(f"node {node} never reported gpu capacity")
 
     def stop(self):
+        self._bg.shutdown(wait=True)
         for node in self.nodes.values():
             if node.manager is not None:
                 node.manager.stop()
@@ -185,19 +194,39 @@ class SimCluster:
 
     # -- pod flow -------------------------------------------------------------------------
     def create_pod(self, gpu_mem, name: str | None = None, labels: dict | None = None) -> dict:
-        self._seq += 1
-        return self.client.create_pod("default", pod_spec(name or f"pod-{self._seq}", gpu_mem, labels=labels))
+        return self.client.create_pod("default", pod_spec(name or f"pod-{next(self._seq)}", gpu_mem, labels=labels))
 
     def schedule(self, pod: dict):
         return self.extender.schedule(pod)
 
-    def admit(self, pod: dict) -> Admission:
-        pod = self.client.get_pod(O.namespace(pod), O.name(pod))
+    def admit(self, pod: dict, async_status: bool = False) -> Admission:
+        """Kubelet admission. ``pod`` may be the bound object the caller already holds (the
+        kubelet gets it from its own watch); otherwise it is fetched. With ``async_status`` the
+        Running status is posted off the admission path, as the kubelet's status manager does."""
+        if not O.node_name(pod):
+            pod = self.client.get_pod(O.namespace(pod), O.name(pod))
         node = self.nodes[O.node_name(pod)]
         adm = node.kubelet.admit(pod)
         if adm.error is None:
-            self.client.patch_pod_status(O.namespace(pod), O.name(pod), {"status": {"phase": "Running"}})
+            ns, nm = O.namespace(pod), O.name(pod)
+            if async_status:
+                self._bg.submit(self.client.patch_pod_status, ns, nm, {"status": {"phase": "Running"}})
+            else:
+                self.client.patch_pod_status(ns, nm, {"status": {"phase": "Running"}})
         return adm
+
+    def wait_assigned(self, pod: dict, timeout: float = 10.0) -> dict:
+        """Wait until the plugin's (write-behind) ASSIGNED=true patch is visible."""
+        t = time.monotonic() + timeout
+        while True:
+            got = self.client.get_pod(O.namespace(pod), O.name(pod))
+            if O.annotations(got).get(const.ENV_ASSIGNED_FLAG) == "true" or time.monotonic() > t:
+                return got
+            time.sleep(0.005)
+
+    def flush(self):
+        """Wait for asynchronous status updates."""
+        self._bg.submit(lambda: None).result()
 
     def run_pod(self, gpu_mem, name: str | None = None, labels: dict | None = None):
         pod = self.create_pod(gpu_mem, name, labels)
@@ -215,7 +244,8 @@ class SimCluster:
         return pods, placed, [self.admit(p) for p in pods]
 
     def delete_pod(self, pod: dict):
-        pod = self.client.get_pod(O.namespace(pod), O.name(pod))
+        if not O.node_name(pod):
+            pod = self.client.get_pod(O.namespace(pod), O.name(pod))
         nn = O.node_name(pod)
         if nn in self.nodes:
             self.nodes[nn].kubelet.release(O.uid(pod))

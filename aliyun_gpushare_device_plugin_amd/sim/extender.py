@@ -131,8 +131,8 @@ class ExtenderSim:
         self.client.bind_pod(ns, nm, node, O.uid(pod))
         return patched
 
-    def schedule(self, pod: dict, node_names=None) -> tuple[str, int] | None:
-        """Filter + prioritize + bind one pod. Returns (node, gpu) or None if it does not fit."""
+    def decide(self, pod: dict, node_names=None) -> tuple[str, int] | None:
+        """Filter + prioritize + reserve (the scheduling cycle; in memory)."""
         req = O.gpu_mem_of_pod(pod)
         with self._lock:
             choice = self._choose(req, node_names)
@@ -141,11 +141,25 @@ class ExtenderSim:
             st = self.nodes[choice[0]]
             st.used[choice[1]] += req
             self._placed[O.uid(pod)] = (choice[0], [(choice[1], req)])
+        return choice
+
+    def commit(self, pod: dict, choice: tuple[str, int]) -> dict:
+        """The binding cycle: write the annotations and bind (undo the reservation on error).
+        Returns the pod as the kubelet will see it (annotations + nodeName)."""
         try:
-            self.bind(pod, choice[0], choice[1])
+            patched = self.bind(pod, choice[0], choice[1])
         except Exception:
             self.forget(pod)
             raise
+        bound = dict(patched or pod)
+        bound["spec"] = dict(bound.get("spec") or {}, nodeName=choice[0])
+        return bound
+
+    def schedule(self, pod: dict, node_names=None) -> tuple[str, int] | None:
+        """Filter + prioritize + bind one pod. Returns (node, gpu) or None if it does not fit."""
+        choice = self.decide(pod, node_names)
+        if choice is not None:
+            self.commit(pod, choice)
         return choice
 
     def schedule_group(self, pods: list[dict], node_names=None) -> list[tuple[str, int]] | None:

@@ -35,7 +35,7 @@ def run_smoke(verbose: bool = True) -> dict:
         out["allocate_ms"] = round(adm.latencies[0] * 1e3, 3)
         out["envs"] = {k: v for k, v in envs.items() if k.startswith("ALIYUN")}
         out["devices"] = [d.host_path for d in adm.responses[0].devices]
-        assert O.annotations(c.client.get_pod("default", O.name(pod)))[const.ENV_ASSIGNED_FLAG] == "true"
+        assert O.annotations(c.wait_assigned(pod))[const.ENV_ASSIGNED_FLAG] == "true"
 
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)

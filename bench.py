@@ -78,9 +78,13 @@ class ControlPlane:
         if self.gpu_count != n_gpus:
             raise RuntimeError(f"plugin advertises {self.gpu_count} GPUs, expected {n_gpus}")
         self.resident: dict[int, list] = {g: [] for g in range(n_gpus)}   # gpu -> [(pod, size)] oldest first
+        import concurrent.futures as cf
+
+        self.pool = cf.ThreadPoolExecutor(max_workers=max(1, min(8, n_gpus)), thread_name_prefix="churn")
         self.alloc_lat: list[float] = []
         self.admit_lat: list[float] = []
         self.failed = 0
+        self.cp_time = 0.0
 
     def admit(self, size: int):
         t0 = time.perf_counter()
@@ -104,13 +108,34 @@ class ControlPlane:
             self.admit(s)
 
     def churn(self):
-        """Retire the oldest pod on every GPU and admit a same-size replacement."""
-        for g in range(self.n):
-            if not self.resident[g]:
+        """Retire the oldest pod on every GPU and admit a same-size replacement.
+
+        Actors as in a real cluster: pod deletion/creation (controllers) and binding (scheduler +
+        extender) proceed concurrently with each other; the kubelet admits pods one at a time
+        (its pod-addition loop is serial, so Allocate calls are too). Binds are issued in
+        best-fit-decreasing order so every replacement lands in the slot its predecessor freed.
+        """
+        olds = [(g, self.resident[g].pop(0)) for g in range(self.n) if self.resident[g]]
+        list(self.pool.map(lambda it: self.cluster.delete_pod(it[1][0]), olds))
+        news = list(self.pool.map(lambda it: (self.cluster.create_pod(it[1][1]), it[1][1]), olds))
+        news.sort(key=lambda ps: -ps[1])
+        ext = self.cluster.extender
+        decided = [(pod, size, ext.decide(pod)) for pod, size in news]            # scheduling cycles
+        bound = list(self.pool.map(lambda d: ext.commit(d[0], d[2]) if d[2] else None, decided))  # binds
+        for (pod, size, where), bpod in zip(decided, bound):
+            if where is None:
+                self.failed += 1
                 continue
-            pod, size = self.resident[g].pop(0)
-            self.cluster.delete_pod(pod)
-            self.admit(size)
+            t0 = time.perf_counter()
+            adm = self.cluster.admit(bpod, async_status=True)
+            if adm.error:
+                self.failed += 1
+                self.cluster.delete_pod(bpod)
+                continue
+            self.alloc_lat.extend(adm.latencies)
+            self.admit_lat.append(time.perf_counter() - t0)
+            gpu = int(dict(adm.responses[0].envs)["ALIYUN_COM_GPU_MEM_IDX"])
+            self.resident[gpu].append((bpod, size))
 
     def placement(self) -> dict:
         from aliyun_gpushare_device_plugin_amd.cluster import objects as O
@@ -118,6 +143,7 @@ class ControlPlane:
         return {g: [(O.uid(p), s) for p, s in pods] for g, pods in self.resident.items()}
 
     def stop(self):
+        self.pool.shutdown(wait=True)
         self.cluster.stop()
 
 
@@ -193,7 +219,10 @@ def main():
             gemm_flops += 2.0 * a.gemm ** 3 * a.burst * len(players)
         place = None
         if rank == 0:
+            tc = time.perf_counter()
             cp.churn()
+            if timed:
+                cp.cp_time += time.perf_counter() - tc
             place = cp.placement()
         place = bcast(place)
         sync_players(place)
@@ -252,6 +281,7 @@ def main():
             "allocate_p50_ms": round(pct(cp.alloc_lat, 0.5) * 1e3, 3) if cp.alloc_lat else None,
             "allocate_p99_ms": round(pct(cp.alloc_lat, 0.99) * 1e3, 3) if cp.alloc_lat else None,
             "admission_p50_ms": round(pct(cp.admit_lat, 0.5) * 1e3, 3) if cp.admit_lat else None,
+            "control_plane_ms_per_step": round(cp.cp_time / a.steps * 1e3, 3),
             "pods_per_node": pods_node,
             "hbm_gib_per_node": gib_node,
             "advertised_gib_per_node": units * n,

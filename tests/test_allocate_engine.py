@@ -235,3 +235,18 @@ def test_metrics_recorded():
     assert al.metrics.allocate_outcomes.value(outcome="assigned") == 1
     assert al.metrics.allocate_latency.count(phase="total") == 1
     assert "gpushare_allocate_latency_seconds_bucket" in al.metrics.registry.render()
+
+
+def test_async_patch_write_behind_and_retry():
+    al, src, cl = make([mkpod(f"p{i}", 2, i % 2, 10 + i) for i in range(4)], async_patch=True)
+    cl.fail = RuntimeError("apiserver flaky")
+    r = [al.allocate(req(2)) for _ in range(2)]
+    assert [dict(x.container_responses[0].envs)[const.ENV_RESOURCE_INDEX] for x in r] == ["0", "1"]
+    assert not cl.patches                      # answered before the PATCH landed
+    assert not al.flush_patches(0.2)           # still failing -> still pending, claims held
+    assert dict(al.allocate(req(2)).container_responses[0].envs)[const.ENV_RESOURCE_INDEX] == "0"  # p2, not p0
+    cl.fail = None
+    assert al.flush_patches(5.0)
+    assert sorted(p[1] for p in cl.patches) == ["p0", "p1", "p2"]
+    assert all(p["metadata"]["annotations"][const.ENV_ASSIGNED_FLAG] == "true"
+               for p in src.pods if p["metadata"]["name"] in ("p0", "p1", "p2"))

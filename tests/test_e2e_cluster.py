@@ -17,7 +17,7 @@ def envs(adm, i=0):
 
 def test_config1_stub_plugin_roundtrip():
     """BASELINE config 1: 2 fake GPUs x 4 GiB, ListAndWatch/Allocate round trip."""
-    with SimCluster([("node-a", "fake:2x4G")]) as c:
+    with SimCluster([("node-a", "fake:2x4G")], preferred_allocation=True) as c:
         node = c.client.get_node("node-a")
         assert node["status"]["allocatable"][const.RESOURCE_COUNT] == "2"
         assert node["status"]["allocatable"][const.RESOURCE_NAME] == "8"
@@ -30,7 +30,7 @@ def test_config1_stub_plugin_roundtrip():
             pod, where, adm = c.run_pod(2)
             assert adm.error is None and envs(adm)[const.ENV_RESOURCE_BY_DEV] == "4"
             gpus.append(int(envs(adm)[const.ENV_RESOURCE_INDEX]))
-            got = c.client.get_pod("default", O.name(pod))
+            got = c.wait_assigned(pod)
             assert O.annotations(got)[const.ENV_ASSIGNED_FLAG] == "true"
             assert O.phase(got) == "Running"
         assert sorted(gpus) == [0, 0, 1, 1]
@@ -112,9 +112,17 @@ def test_watch_cache_used_instead_of_list():
 
 
 def test_plugin_as_separate_process():
-    with SimCluster([("n", "fake:2x4G")], plugin_mode="process") as c:
+    with SimCluster([("n", "fake:2x4G")], plugin_mode="process", preferred_allocation=True) as c:
         _, w, adm = c.run_pod(3)
         assert adm.error is None and envs(adm)[const.ENV_RESOURCE_BY_CONTAINER] == "3"
+        assert c.nodes["n"].kubelet.options.get_preferred_allocation_available
+
+
+def test_preferred_allocation_is_opt_in():
+    with SimCluster([("n", "fake:1x4G")]) as c:
+        assert not c.nodes["n"].kubelet.options.get_preferred_allocation_available
+        _, _, adm = c.run_pod(2)
+        assert adm.error is None
 
 
 def test_multi_node_cluster():
