@@ -115,7 +115,33 @@ def main(argv=None) -> int:
     if not cfg.node_name:
         log.error("Please set env NODE_NAME (or --node-name)")
         return 1
-    return SharedGPUManager(cfg).run()
+    prof_path = os.environ.get("GPUSHARE_PROFILE")
+    if not prof_path:
+        return SharedGPUManager(cfg).run()
+    # opt-in: profile every plugin thread (gRPC handlers, informer, patcher) until shutdown
+    import cProfile
+    import threading
+
+    prof = cProfile.Profile()
+    profs = [prof]
+
+    def _thread_hook(*_a):   # first profile event of a new thread: swap in its own profiler
+        p = cProfile.Profile()
+        profs.append(p)
+        p.enable()
+
+    threading.setprofile(_thread_hook)
+    prof.enable()
+    try:
+        return SharedGPUManager(cfg).run()
+    finally:
+        prof.disable()
+        import pstats
+        st = pstats.Stats(prof)
+        for p in profs[1:]:
+            p.disable()
+            st.add(p)
+        st.dump_stats(prof_path)
 
 
 if __name__ == "__main__":

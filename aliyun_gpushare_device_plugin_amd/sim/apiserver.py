@@ -310,6 +310,9 @@ class _Handler(http.server.BaseHTTPRequestHandler):
         u = urllib.parse.urlsplit(self.path)
         q = dict(urllib.parse.parse_qsl(u.query))
         path = u.path.rstrip("/")
+        if path == "/debug/requests":      # simulator introspection: request counts by verb/kind
+            with self.store.lock:
+                return self._send(200, dict(self.store.requests))
         self.store.requests["GET " + ("watch" if q.get("watch") else path.split("/")[-1])] += 1
         fsel, lsel = parse_field_selector(q.get("fieldSelector")), parse_label_selector(q.get("labelSelector"))
         if path == "/api/v1/pods" or re.fullmatch(r"/api/v1/namespaces/[^/]+/pods", path):

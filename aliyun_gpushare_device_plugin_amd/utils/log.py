@@ -20,36 +20,58 @@ _VERBOSITY = int(os.environ.get("GPUSHARE_V", "0"))
 _JSON = os.environ.get("GPUSHARE_LOG_JSON", "") == "1"
 _lock = threading.Lock()
 
+# ``logger`` carries the level gate (tests quiet it with ``logger.setLevel``); records are
+# written by the lean emitter below instead of logging.Handler: Allocate logs two lines per
+# call, and the stdlib path (findCaller + LogRecord + handler lock) costs ~150 us a line.
 logger = logging.getLogger("gpushare")
+_stream = None
+_pid = os.getpid()
+_sec_cache = [-1, ""]
+_LEVELS = {logging.INFO: ("I", "info"), logging.WARNING: ("W", "warning"), logging.ERROR: ("E", "error")}
 
 
-class _Fmt(logging.Formatter):
-    _LVL = {"DEBUG": "D", "INFO": "I", "WARNING": "W", "ERROR": "E", "CRITICAL": "F"}
-
-    def format(self, r: logging.LogRecord) -> str:
-        if _JSON:
-            d = {"ts": round(r.created, 6), "level": r.levelname.lower(), "msg": r.getMessage(),
-                 "src": f"{r.filename}:{r.lineno}", "thread": r.threadName}
-            d.update(getattr(r, "fields", {}) or {})
-            return json.dumps(d, default=str)
-        t = time.strftime("%m%d %H:%M:%S", time.localtime(r.created))
-        us = int((r.created % 1) * 1e6)
-        return (f"{self._LVL.get(r.levelname, 'I')}{t}.{us:06d} {os.getpid():>7} "
-                f"{r.filename}:{r.lineno}] {r.getMessage()}")
+def _emit(levelno: int, msg, args, fields, depth: int = 2) -> None:
+    if levelno < logger.getEffectiveLevel():
+        return
+    if args:
+        try:
+            msg = msg % args
+        except (TypeError, ValueError):
+            msg = f"{msg} {args!r}"
+    f = sys._getframe(depth)
+    src = f"{os.path.basename(f.f_code.co_filename)}:{f.f_lineno}"
+    now = time.time()
+    code, name = _LEVELS.get(levelno, ("I", "info"))
+    if _JSON:
+        d = {"ts": round(now, 6), "level": name, "msg": str(msg), "src": src,
+             "thread": threading.current_thread().name}
+        d.update(fields or {})
+        line = json.dumps(d, default=str)
+    else:
+        sec = int(now)
+        if _sec_cache[0] != sec:
+            _sec_cache[0], _sec_cache[1] = sec, time.strftime("%m%d %H:%M:%S", time.localtime(sec))
+        line = f"{code}{_sec_cache[1]}.{int((now - sec) * 1e6):06d} {_pid:>7} {src}] {msg}"
+    st = _stream or sys.stderr
+    with _lock:
+        try:
+            st.write(line + "\n")
+            st.flush()
+        except (OSError, ValueError):
+            pass
 
 
 def setup(verbosity: int | None = None, json_lines: bool | None = None, stream=None) -> None:
-    global _VERBOSITY, _JSON
+    global _VERBOSITY, _JSON, _stream, _pid
     with _lock:
         if verbosity is not None:
             _VERBOSITY = int(verbosity)
         if json_lines is not None:
             _JSON = bool(json_lines)
-        if not logger.handlers:
-            h = logging.StreamHandler(stream or sys.stderr)
-            h.setFormatter(_Fmt())
-            logger.addHandler(h)
-            logger.propagate = False
+        if stream is not None:
+            _stream = stream
+        _pid = os.getpid()
+        logger.propagate = False
         logger.setLevel(logging.DEBUG if _VERBOSITY > 0 else logging.INFO)
 
 
@@ -68,7 +90,7 @@ class _V:
 
     def info(self, msg, *args, **fields):
         if self.on:
-            logger.info(msg, *args, stacklevel=2, extra={"fields": fields} if fields else None)
+            _emit(logging.INFO, msg, args, fields)
 
 
 def V(level: int) -> _V:
@@ -77,15 +99,15 @@ def V(level: int) -> _V:
 
 
 def info(msg, *args, **fields):
-    logger.info(msg, *args, stacklevel=2, extra={"fields": fields} if fields else None)
+    _emit(logging.INFO, msg, args, fields)
 
 
 def warning(msg, *args, **fields):
-    logger.warning(msg, *args, stacklevel=2, extra={"fields": fields} if fields else None)
+    _emit(logging.WARNING, msg, args, fields)
 
 
 def error(msg, *args, **fields):
-    logger.error(msg, *args, stacklevel=2, extra={"fields": fields} if fields else None)
+    _emit(logging.ERROR, msg, args, fields)
 
 
 setup()
