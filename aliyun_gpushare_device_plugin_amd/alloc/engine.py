@@ -24,7 +24,14 @@ MI355X build, same protocol, different mechanics:
 * optional write-behind of the ASSIGNED patch (``async_patch``): a matched pod is claimed in
   memory and the annotation is landed by a retrying background patcher, taking the apiserver
   round trip off the kubelet's admission path; candidates are Pending pods only and the claim
-  is held until the patch is acknowledged, so a pod is never matched twice.
+  is held until the patch is acknowledged, so a pod is never matched twice;
+* swap completion: AllocateRequest carries no pod identity, so when the kubelet admits two
+  equal-size pods in an order other than their assume times, the first Allocate takes the
+  other pod's reservation and its own pod turns Running with ``ASSIGNED=false``. The reference
+  then fails the second pod (``allocate.go:182-187``: no Pending candidate left); here, when no
+  Pending pod matches, an equal-size pod that is bound, un-assigned, recently assumed and never
+  allocated by this process is matched instead — the two pods simply exchange their
+  extender-reserved GPUs, so per-GPU accounting stays exact.
 """
 from __future__ import annotations
 
@@ -59,6 +66,7 @@ class AllocatorOptions:
     rocr_visible: bool = False
     match_containers: bool = True
     claim_ttl_s: float = 120.0
+    complete_swaps: bool = True
     # Write-behind ASSIGNED=true PATCH: Allocate answers after the in-memory claim and a
     # background patcher lands the annotation (retrying); the claim blocks re-matching until it
     # has. False = the reference's synchronous PATCH inside Allocate (allocate.go:132-152).
@@ -133,7 +141,29 @@ class Allocator:
                     c = _Claim(O.uid(p), p, A.gpu_id_from_annotation(p), 1, gc, time.monotonic())
                     self._claims[c.uid] = c
                     return c, False
+        # 4) swap completion (authoritative pass only): see the module docstring
+        if fresh and self.opts.complete_swaps:
+            p = self._swap_partner(req_units)
+            if p is not None:
+                gc = [i for i, v in enumerate(O.gpu_mem_per_container(p)) if v > 0]
+                self.metrics.allocate_outcomes.inc(outcome="swap")
+                log.warning("no pending pod requests %d%s: completing a swapped admission with pod %s (gpu %d)",
+                            req_units, self.opts.unit, O.name(p), A.gpu_id_from_annotation(p))
+                return _Claim(O.uid(p), p, A.gpu_id_from_annotation(p), len(gc), gc, time.monotonic()), True
         return None, False
+
+    def _swap_partner(self, req_units: int) -> dict | None:
+        now_ns = time.time_ns()
+        ttl_ns = int(self.opts.claim_ttl_s * 1e9)
+        out = []
+        for p in A.dedupe_by_uid(self.pods.node_pods(), self.node):
+            u = O.uid(p)
+            if (O.phase(p) == "Pending" or not A.is_assumed_pod(p) or u in self._assigned or u in self._claims
+                    or O.gpu_mem_of_pod(p) != req_units or now_ns - A.assume_time(p) > ttl_ns):
+                continue
+            out.append(p)
+        out = A.order_by_assume_time(out)
+        return out[0] if out else None
 
     # ------------------------------------------------------------------------------------
     # response building

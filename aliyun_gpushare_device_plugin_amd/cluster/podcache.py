@@ -33,6 +33,10 @@ class PodSource:
     def pending_pods(self, fresh: bool = False) -> list[dict]:
         raise NotImplementedError
 
+    def node_pods(self) -> list[dict]:
+        """Every non-terminated pod bound to this node, any phase (rare path: swap completion)."""
+        return [p for p in self.pending_pods(fresh=True) if not O.is_terminated(p)]
+
     def observe(self, pod: dict) -> None:
         """Feed back an object we wrote (PATCH response)."""
 
@@ -62,6 +66,10 @@ class ListSource(PodSource):
                     time.sleep(self.retry_sleep)
         raise RuntimeError(f"failed to get Pods assigned to node {self.node}: {err}")
 
+    def node_pods(self) -> list[dict]:
+        items, _ = self.client.list_pods(field_selector=node_field_selector(self.node))
+        return [p for p in items if not O.is_terminated(p)]
+
 
 class KubeletSource(PodSource):
     """``--query-kubelet``: kubelet ``/pods`` then apiserver fallback.
@@ -83,6 +91,12 @@ class KubeletSource(PodSource):
                 time.sleep(self.retry_sleep)
         log.warning("not found from kubelet /pods api, start to list apiserver")
         return self.fallback.pending_pods(fresh=True)
+
+    def node_pods(self) -> list[dict]:
+        try:
+            return [p for p in self.kubelet.get_node_running_pods() if not O.is_terminated(p)]
+        except Exception:  # noqa: BLE001
+            return self.fallback.node_pods()
 
 
 class WatchCache(PodSource):
@@ -189,6 +203,12 @@ class WatchCache(PodSource):
             cur = self._pods.get(u)
             if cur is None or O.rv_int(O.resource_version(pod)) >= O.rv_int(O.resource_version(cur)):
                 self._pods[u] = pod
+
+    def node_pods(self) -> list[dict]:
+        if not self._synced.is_set():
+            return self.fallback.node_pods()
+        with self._lock:
+            return [p for p in self._pods.values() if not O.is_terminated(p)]
 
     def snapshot(self) -> list[dict]:
         with self._lock:

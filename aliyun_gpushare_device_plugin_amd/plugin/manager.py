@@ -64,6 +64,7 @@ class PluginConfig:
     rocr_visible: bool = False
     metrics_addr: str | None = None
     async_patch: bool = True             # write-behind ASSIGNED patch (see AllocatorOptions)
+    complete_swaps: bool = True          # match a swapped equal-size pod (see alloc/engine.py)
     mps: bool = False                    # accepted for flag compatibility; ignored
 
 
@@ -144,7 +145,8 @@ class SharedGPUManager:
         allocator = Allocator(model, src, self.client, cfg.node_name,
                               AllocatorOptions(unit=cfg.memory_unit, disable_cgpu=disable_cgpu, shim=shim,
                                                strict=cfg.strict_allocate, expose_devices=cfg.expose_devices,
-                                               rocr_visible=cfg.rocr_visible, async_patch=cfg.async_patch),
+                                               rocr_visible=cfg.rocr_visible, async_patch=cfg.async_patch,
+                                               complete_swaps=cfg.complete_swaps),
                               self.metrics)
         self.model = model
         return DevicePluginServer(model, allocator, self._plugin_socket(), const.RESOURCE_NAME,

@@ -12,6 +12,7 @@ import dataclasses
 import itertools
 import os
 import shutil
+import signal
 import subprocess
 import sys
 import tempfile
@@ -91,7 +92,7 @@ class SimCluster:
         self.api_proc = subprocess.Popen(
             [sys.executable, "-m", "aliyun_gpushare_device_plugin_amd.sim.apiserver", "--port", "0",
              "--latency-ms", str(self.apiserver_latency_s * 1e3)],
-            env=self._child_env(), stdout=subprocess.PIPE, text=True)
+            env=self._child_env(), stdout=subprocess.PIPE, text=True, preexec_fn=_die_with_parent)
         self.api_url = self.api_proc.stdout.readline().strip()
         if not self.api_url.startswith("http"):
             raise RuntimeError("fake apiserver process failed to start")
@@ -144,7 +145,7 @@ class SimCluster:
             if self.preferred_allocation:
                 args += ["--preferred-allocation"]
             args += self.extra_plugin_args
-            node.proc = subprocess.Popen(args, env=self._child_env(), stdout=subprocess.DEVNULL,
+            node.proc = subprocess.Popen(args, env=self._child_env(), stdout=subprocess.DEVNULL, preexec_fn=_die_with_parent,
                                          stderr=open(os.path.join(self.workdir, f"{node.name}.plugin.log"), "w"))
         else:
             node.manager = SharedGPUManager(self._plugin_cfg(node), client=APIClient(KubeConfig(self.api_url)))
@@ -254,6 +255,14 @@ class SimCluster:
 
     def manager(self, node: str) -> SharedGPUManager | None:
         return self.nodes[node].manager
+
+
+def _die_with_parent():
+    """Child-side (between fork and exec): SIGTERM this process when the simulator dies, so a
+    killed test or bench never leaves a fake apiserver or plugin process behind."""
+    import ctypes
+
+    ctypes.CDLL(None, use_errno=True).prctl(1, signal.SIGTERM)   # PR_SET_PDEATHSIG
 
 
 def quiet():

@@ -143,11 +143,11 @@ class ExtenderSim:
             self._placed[O.uid(pod)] = (choice[0], [(choice[1], req)])
         return choice
 
-    def commit(self, pod: dict, choice: tuple[str, int]) -> dict:
+    def commit(self, pod: dict, choice: tuple[str, int], assume_ns: int | None = None) -> dict:
         """The binding cycle: write the annotations and bind (undo the reservation on error).
         Returns the pod as the kubelet will see it (annotations + nodeName)."""
         try:
-            patched = self.bind(pod, choice[0], choice[1])
+            patched = self.bind(pod, choice[0], choice[1], assume_ns)
         except Exception:
             self.forget(pod)
             raise

@@ -80,10 +80,15 @@ class ControlPlane:
         self.resident: dict[int, list] = {g: [] for g in range(n_gpus)}   # gpu -> [(pod, size)] oldest first
         import concurrent.futures as cf
 
-        self.pool = cf.ThreadPoolExecutor(max_workers=max(1, min(8, n_gpus)), thread_name_prefix="churn")
+        import threading
+
+        self.pool = cf.ThreadPoolExecutor(max_workers=max(1, n_gpus), thread_name_prefix="churn")
+        self._sched_lock = threading.Lock()
+        self._kubelet = threading.Condition()
         self.alloc_lat: list[float] = []
         self.admit_lat: list[float] = []
         self.failed = 0
+        self.fail_reasons: list[str] = []
         self.cp_time = 0.0
 
     def admit(self, size: int):
@@ -110,31 +115,60 @@ class ControlPlane:
     def churn(self):
         """Retire the oldest pod on every GPU and admit a same-size replacement.
 
-        Actors as in a real cluster: pod deletion/creation (controllers) and binding (scheduler +
-        extender) proceed concurrently with each other; the kubelet admits pods one at a time
-        (its pod-addition loop is serial, so Allocate calls are too). Binds are issued in
-        best-fit-decreasing order so every replacement lands in the slot its predecessor freed.
+        One pipeline per GPU, as in a real cluster where each replacement is independent:
+        delete (controller) -> create -> scheduling cycle (extender decide, stamps the assume
+        time) -> binding cycle (annotations + bind) -> kubelet admission. Only the scheduling
+        cycle and the kubelet are serial: the kubelet's pod worker sees pods in bind order, so
+        admissions are taken in assume-time order (a ticket per decision) and the plugin's
+        earliest-assumed match is the pod actually being admitted. Every replacement has an
+        exact-fit slot (its predecessor's), so best-fit keeps the node packed.
         """
+        import itertools
+
         olds = [(g, self.resident[g].pop(0)) for g in range(self.n) if self.resident[g]]
-        list(self.pool.map(lambda it: self.cluster.delete_pod(it[1][0]), olds))
-        news = list(self.pool.map(lambda it: (self.cluster.create_pod(it[1][1]), it[1][1]), olds))
-        news.sort(key=lambda ps: -ps[1])
         ext = self.cluster.extender
-        decided = [(pod, size, ext.decide(pod)) for pod, size in news]            # scheduling cycles
-        bound = list(self.pool.map(lambda d: ext.commit(d[0], d[2]) if d[2] else None, decided))  # binds
-        for (pod, size, where), bpod in zip(decided, bound):
-            if where is None:
+        tickets = itertools.count()
+        turn = {"next": 0}
+
+        def chain(it):
+            _, (old, size) = it
+            self.cluster.delete_pod(old)
+            pod = self.cluster.create_pod(size)
+            with self._sched_lock:                      # the scheduler's one-pod-at-a-time cycle
+                where = ext.decide(pod)
+                ticket, assume_ns = next(tickets), time.time_ns()
+            try:
+                bpod = ext.commit(pod, where, assume_ns) if where else None
+                with self._kubelet:
+                    while turn["next"] != ticket:
+                        self._kubelet.wait()
+                if bpod is None:
+                    return None, size, None, 0.0
+                t0 = time.perf_counter()
+                adm = self.cluster.admit(bpod, async_status=True)
+                return bpod, size, adm, time.perf_counter() - t0
+            finally:
+                with self._kubelet:
+                    while turn["next"] != ticket:
+                        self._kubelet.wait()
+                    turn["next"] += 1
+                    self._kubelet.notify_all()
+
+        for bpod, size, adm, dt in self.pool.map(chain, olds):
+            if adm is None or adm.error:
                 self.failed += 1
+                self.fail_reasons.append(f"{size}GiB: " + ("unschedulable" if bpod is None else f"admit: {adm and adm.error}"))
+                if bpod is not None:
+                    self.cluster.delete_pod(bpod)
                 continue
-            t0 = time.perf_counter()
-            adm = self.cluster.admit(bpod, async_status=True)
-            if adm.error:
+            gpu = int(dict(adm.responses[0].envs)["ALIYUN_COM_GPU_MEM_IDX"])
+            if gpu < 0:                                 # soft failure: no candidate matched
                 self.failed += 1
+                self.fail_reasons.append(f"{size}GiB: plugin found no candidate")
                 self.cluster.delete_pod(bpod)
                 continue
             self.alloc_lat.extend(adm.latencies)
-            self.admit_lat.append(time.perf_counter() - t0)
-            gpu = int(dict(adm.responses[0].envs)["ALIYUN_COM_GPU_MEM_IDX"])
+            self.admit_lat.append(dt)
             self.resident[gpu].append((bpod, size))
 
     def placement(self) -> dict:
@@ -242,6 +276,7 @@ def main():
         cp.alloc_lat.clear()
         cp.admit_lat.clear()
         cp.failed = 0
+        cp.fail_reasons.clear()
 
     barrier()
     t0 = time.perf_counter()
@@ -287,6 +322,7 @@ def main():
             "advertised_gib_per_node": units * n,
             "packing_efficiency": round(gib_node / (units * n), 4) if units else None,
             "failed_admissions": cp.failed,
+            "failure_reasons": cp.fail_reasons[:5],
             "gemm_tflops_node": round(gemm_flops / elapsed / 1e12, 1) if use_gpu else None,
         }
         line = json.dumps(res)

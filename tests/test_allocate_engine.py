@@ -46,6 +46,9 @@ class StaticSource(PodSource):
             self.fresh_calls += 1
         return [p for p in self.pods if p["status"]["phase"] == "Pending"]
 
+    def node_pods(self):
+        return [p for p in self.pods if p["status"]["phase"] in ("Pending", "Running")]
+
     def observe(self, pod):
         self.observed.append(pod)
         for i, p in enumerate(self.pods):
@@ -250,3 +253,26 @@ def test_async_patch_write_behind_and_retry():
     assert sorted(p[1] for p in cl.patches) == ["p0", "p1", "p2"]
     assert all(p["metadata"]["annotations"][const.ENV_ASSIGNED_FLAG] == "true"
                for p in src.pods if p["metadata"]["name"] in ("p0", "p1", "p2"))
+
+
+@pytest.mark.parametrize("complete", [True, False])
+def test_swapped_admission_order_is_completed(complete):
+    """The kubelet admits b before a (equal size): the first Allocate takes a's reservation
+    (earliest assume time), b turns Running un-assigned; a's own Allocate then gets b's GPU."""
+    now = time.time_ns()
+    a, b = mkpod("a", 2, 0, now - 2000), mkpod("b", 2, 1, now - 1000)
+    al, src, cl = make([a, b], complete_swaps=complete)
+    first = dict(al.allocate(req(2)).container_responses[0].envs)
+    assert first[const.ENV_RESOURCE_INDEX] == "0"          # reference rule: earliest assumed pod
+    b["status"]["phase"] = "Running"                       # the kubelet started b's containers
+    second = dict(al.allocate(req(2)).container_responses[0].envs)
+    if complete:
+        assert second[const.ENV_RESOURCE_INDEX] == "1"
+        assert all(A.is_assigned_pod(p) for p in src.pods)
+        assert al.metrics.allocate_outcomes.value(outcome="swap") == 1
+    else:
+        assert second[const.ENV_RESOURCE_INDEX] == "-1"   # the reference's failure
+    # a stale un-assigned running pod (assumed long ago) is never taken
+    old = mkpod("old", 2, 1, now - int(600e9), phase="Running")
+    al2, _, _ = make([old])
+    assert dict(al2.allocate(req(2)).container_responses[0].envs)[const.ENV_RESOURCE_INDEX] == "-1"
