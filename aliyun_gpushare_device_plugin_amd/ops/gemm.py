@@ -13,6 +13,13 @@ import torch
 from . import _lib
 
 EP_BIAS, EP_SILU, EP_RESID = 1, 2, 4
+GEMM_AUTO, GEMM_V1, GEMM_PINGPONG = 0, 1, 2
+
+
+def set_gemm_variant(v: int) -> None:
+    """Kernel selection (A/B measurement, tests): ``GEMM_AUTO`` = ping-pong 8-phase kernel for
+    M%256 == N%256 == K%128 == 0, the 2-stage kernel otherwise; ``GEMM_V1`` forces the latter."""
+    _lib.check(_lib.lib().gs_gemm_set_variant(int(v)), "gs_gemm_set_variant")
 
 
 def _check_operand(t: torch.Tensor, name: str):

@@ -171,6 +171,228 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_nt_256(
   }
 }
 
+
+// ---------------------------------------------------------------------------------------
+// v2: ping-pong 8-phase schedule (aligned shapes: M % 256 == 0, N % 256 == 0, K % 128 == 0)
+//
+// Same 256x256 tile / 8 waves / 16x16x32 MFMA as above; what changes is the pipeline.
+//  * LDS = 2 buffers (even / odd K-tile) x 4 quarter slots of 16 KiB. A quarter holds one
+//    operand's rows for one half of every wave's sub-tile: A-mh (rows wm*128 + mh*64 + 0..63
+//    for wm = 0, 1) and B-nh (n-rows wn*64 + nh*32 + 0..31 for wn = 0..3). Per K-tile a wave
+//    walks its 128x64 output in 4 quadrant phases (mh, nh) = (0,0), (0,1), (1,1), (1,0),
+//    reading A0+B0, B1, A1, B0 — so every quarter is last read in exactly ONE phase and can be
+//    restaged by the very next phase (its reads were retired by lgkmcnt(0) before that phase's
+//    first barrier).
+//  * one quarter (2 x global_load_lds_dwordx4 per thread) is staged per phase; the K-loop runs
+//    two K-tiles (8 phases) per iteration and waits s_waitcnt vmcnt(6) only in phases 4 and 8,
+//    keeping 3 quarters (~1500 MFMA cycles) of prefetch in flight across raw s_barriers, and a
+//    buffer is first read one barrier after the wait that retires it
+//    (cdna_hip_programming.md "Pipelining across barriers").
+//  * the two wave groups (wm = 0 / 1 — one of each on every SIMD, waves go to SIMDs
+//    cyclically) run one barrier apart: while one wave issues its ds_reads + DMA, the other
+//    wave on the SIMD issues its 16 MFMAs, so the matrix pipe alternates between them.
+// Staging order per iteration i (tiles 2i, 2i+1; buffer b = tile & 1):
+//   P1 (2i+1,B0)  P2 (2i+2,A0)  P3 (2i+2,B1)  P4 (2i+2,A1) + vmcnt(6) -> tile 2i+1 landed
+//   P5 (2i+2,B0)  P6 (2i+3,A0)  P7 (2i+3,B1)  P8 (2i+3,A1) + vmcnt(6) -> tile 2i+2 landed
+constexpr int QBYTES = 128 * BK * 2;   // 16 KiB quarter
+enum { QA0 = 0, QA1 = 1, QB0 = 2, QB1 = 3 };
+
+__device__ __forceinline__ void sched_fence() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ void raw_barrier() {
+  sched_fence();
+  __builtin_amdgcn_s_barrier();
+  sched_fence();
+}
+
+struct PPState {
+  const unsigned short* srcA[2];   // per DMA instruction, quarter h = 0 (h = 1: + 64 rows)
+  const unsigned short* srcB[2];   // per DMA instruction, quarter h = 0 (h = 1: + 32 rows)
+  size_t a_h1, b_h1;               // element offsets of the h = 1 quarter
+  char* lds;
+  int wave;
+};
+
+// DMA one quarter (q) of K-tile kt into buffer (kt & 1).
+__device__ __forceinline__ void pp_stage(const PPState& st, int q, int kt) {
+  char* slot = st.lds + ((kt & 1) * 4 + q) * QBYTES;
+  const int koff = kt * BK;
+  const bool isA = q < 2;
+  const size_t hoff = (q & 1) ? (isA ? st.a_h1 : st.b_h1) : 0;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const unsigned short* src = (isA ? st.srcA[i] : st.srcB[i]) + hoff + koff;
+    glds16(src, slot + (i * 8 + st.wave) * 1024);
+  }
+}
+
+__global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_nt_256_pp(
+    const unsigned short* __restrict__ A, const unsigned short* __restrict__ B, unsigned short* __restrict__ C,
+    const unsigned short* __restrict__ bias, const unsigned short* __restrict__ R, int M, int N, int K, int lda,
+    int ldb, int ldc, int flags) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int nbm = M / BM, nbn = N / BN, nwg = nbm * nbn;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int per_group = GROUP_M * nbn;
+  const int first_m = (wgid / per_group) * GROUP_M;
+  const int gsz = min(nbm - first_m, GROUP_M);
+  const int tm = first_m + (wgid % per_group) % gsz;
+  const int tn = (wgid % per_group) / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+
+  PPState st;
+  st.lds = smem;
+  st.wave = wave;
+  st.a_h1 = (size_t)64 * lda;
+  st.b_h1 = (size_t)32 * ldb;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    // DMA instruction i of wave w fills quarter-local rows (i*8 + w)*8 + lane/8, chunk slot lane%8
+    const int rho = (i * 8 + wave) * 8 + (lane >> 3);
+    const int c = swz(rho, lane & 7);
+    const int arow = m0 + (rho >> 6) * 128 + (rho & 63);
+    const int brow = n0 + (rho >> 5) * 64 + (rho & 31);
+    st.srcA[i] = A + (size_t)arow * lda + c * 8;
+    st.srcB[i] = B + (size_t)brow * ldb + c * 8;
+  }
+
+  f32x4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // fragment addressing inside a quarter: row rho = base + tile*16 + (lane & 15); the swizzle
+  // term ((rho >> 1) & 7) depends only on lane & 15 because base and tile*16 are multiples of 16
+  const int lr = lane & 15;
+  const int co0 = (swz(lr, 0 * 4 + (lane >> 4))) << 4;
+  const int co1 = (swz(lr, 1 * 4 + (lane >> 4))) << 4;
+  const int a_lane = (wm * 64 + lr) * 128;
+  const int b_lane = (wn * 32 + lr) * 128;
+
+  bf16x8_t af[4][2], bfr[2][2];
+
+  auto readA = [&](int buf, int h) {
+    const char* qb = smem + (buf * 4 + (h ? QA1 : QA0)) * QBYTES + a_lane;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      af[i][0] = *(const bf16x8_t*)(qb + i * 16 * 128 + co0);
+      af[i][1] = *(const bf16x8_t*)(qb + i * 16 * 128 + co1);
+    }
+  };
+  auto readB = [&](int buf, int h) {
+    const char* qb = smem + (buf * 4 + (h ? QB1 : QB0)) * QBYTES + b_lane;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      bfr[j][0] = *(const bf16x8_t*)(qb + j * 16 * 128 + co0);
+      bfr[j][1] = *(const bf16x8_t*)(qb + j * 16 * 128 + co1);
+    }
+  };
+  auto mfma_q = [&](int mh, int nh) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[mh * 4 + i][nh * 2 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][kk], af[i][kk], acc[mh * 4 + i][nh * 2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // one phase: [reads + DMA (+ counted wait)] lgkmcnt(0) barrier [16 MFMA] barrier
+#define PP_PHASE(READS, STAGE, WAIT, MH, NH)          \
+  do {                                                \
+    READS;                                            \
+    STAGE;                                            \
+    WAIT;                                             \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
+    raw_barrier();                                    \
+    mfma_q(MH, NH);                                   \
+    raw_barrier();                                    \
+  } while (0)
+
+  const int KT = K / BK;   // even, >= 2
+  // prologue: tile 0 (all quarters) into buffer 0, tile 1 minus B0 into buffer 1
+  pp_stage(st, QA0, 0);
+  pp_stage(st, QB1, 0);
+  pp_stage(st, QA1, 0);
+  pp_stage(st, QB0, 0);
+  pp_stage(st, QA0, 1);
+  pp_stage(st, QB1, 1);
+  pp_stage(st, QA1, 1);
+  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  raw_barrier();
+  if (wm == 1) raw_barrier();   // stagger: wave group 1 runs one barrier behind group 0
+
+  const int iters = KT / 2;
+  for (int it = 0; it < iters - 1; ++it) {
+    const int t0 = 2 * it;
+    PP_PHASE((readA(0, 0), readB(0, 0)), pp_stage(st, QB0, t0 + 1), (void)0, 0, 0);
+    PP_PHASE(readB(0, 1), pp_stage(st, QA0, t0 + 2), (void)0, 0, 1);
+    PP_PHASE(readA(0, 1), pp_stage(st, QB1, t0 + 2), (void)0, 1, 1);
+    PP_PHASE(readB(0, 0), pp_stage(st, QA1, t0 + 2), asm volatile("s_waitcnt vmcnt(6)" ::: "memory"), 1, 0);
+    PP_PHASE((readA(1, 0), readB(1, 0)), pp_stage(st, QB0, t0 + 2), (void)0, 0, 0);
+    PP_PHASE(readB(1, 1), pp_stage(st, QA0, t0 + 3), (void)0, 0, 1);
+    PP_PHASE(readA(1, 1), pp_stage(st, QB1, t0 + 3), (void)0, 1, 1);
+    PP_PHASE(readB(1, 0), pp_stage(st, QA1, t0 + 3), asm volatile("s_waitcnt vmcnt(6)" ::: "memory"), 1, 0);
+  }
+  {  // last iteration: only tile KT-1's B0 is still to be staged
+    const int t0 = 2 * (iters - 1);
+    PP_PHASE((readA(0, 0), readB(0, 0)), pp_stage(st, QB0, t0 + 1), (void)0, 0, 0);
+    PP_PHASE(readB(0, 1), (void)0, (void)0, 0, 1);
+    PP_PHASE(readA(0, 1), (void)0, (void)0, 1, 1);
+    PP_PHASE(readB(0, 0), (void)0, asm volatile("s_waitcnt vmcnt(0)" ::: "memory"), 1, 0);
+    PP_PHASE((readA(1, 0), readB(1, 0)), (void)0, (void)0, 0, 0);
+    PP_PHASE(readB(1, 1), (void)0, (void)0, 0, 1);
+    PP_PHASE(readA(1, 1), (void)0, (void)0, 1, 1);
+    PP_PHASE(readB(1, 0), (void)0, (void)0, 1, 0);
+  }
+#undef PP_PHASE
+  if (wm == 0) raw_barrier();   // balance the stagger barrier
+
+  const int mbase = m0 + wm * 128 + lr;
+  const int nbase = n0 + wn * 64 + (lane >> 4) * 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = mbase + i * 16;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = nbase + j * 16;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (flags & EP_BIAS) {
+        const u16x4_t bb = *(const u16x4_t*)(bias + n);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) v[t] += bf16_to_f32(bb[t]);
+      }
+      if (flags & EP_SILU) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) v[t] = silu_f32(v[t]);
+      }
+      if (flags & EP_RESID) {
+        const u16x4_t rr = *(const u16x4_t*)(R + (size_t)m * ldc + n);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) v[t] += bf16_to_f32(rr[t]);
+      }
+      u16x4_t o;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) o[t] = f32_to_bf16(v[t]);
+      *(u16x4_t*)(C + (size_t)m * ldc + n) = o;
+    }
+  }
+}
+
+int g_variant = 0;   // 0 = auto (v2 when aligned), 1 = force v1, 2 = v2 when aligned
+
 }  // namespace
 
 GS_KERNEL_API int gs_gemm_bf16_nt(const void* A, const void* B, void* C, const void* bias, const void* R, int M,
@@ -183,11 +405,27 @@ GS_KERNEL_API int gs_gemm_bf16_nt(const void* A, const void* B, void* C, const v
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_256, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_256_pp, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_BYTES);
     attr_set = true;
   }
+  const bool aligned = M % BM == 0 && N % BN == 0 && K % (2 * BK) == 0;
   const int nblocks = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  if (aligned && g_variant != 1) {
+    gemm_bf16_nt_256_pp<<<dim3(nblocks), dim3(NTHREADS), LDS_BYTES, stream>>>(
+        (const unsigned short*)A, (const unsigned short*)B, (unsigned short*)C, (const unsigned short*)bias,
+        (const unsigned short*)R, M, N, K, lda, ldb, ldc, flags);
+    return gs_launch_status();
+  }
   hipLaunchKernelGGL(gemm_bf16_nt_256, dim3(nblocks), dim3(NTHREADS), LDS_BYTES, stream,
                      (const unsigned short*)A, (const unsigned short*)B, (unsigned short*)C,
                      (const unsigned short*)bias, (const unsigned short*)R, M, N, K, lda, ldb, ldc, flags);
   return gs_launch_status();
+}
+
+// Kernel selection for A/B measurement and tests: 0 = auto, 1 = v1 only, 2 = v2 when aligned.
+GS_KERNEL_API int gs_gemm_set_variant(int v) {
+  if (v < 0 || v > 2) return GS_EINVAL;
+  g_variant = v;
+  return GS_OK;
 }

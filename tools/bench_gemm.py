@@ -16,6 +16,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from aliyun_gpushare_device_plugin_amd.ops import gemm_nt  # noqa: E402
+from aliyun_gpushare_device_plugin_amd.ops.gemm import GEMM_AUTO, GEMM_V1, set_gemm_variant  # noqa: E402
 
 
 def time_fn(fn, iters):
@@ -42,21 +43,30 @@ def main():
         x = torch.empty(M, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)
         w = torch.empty(N, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)
         out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-        ours = lambda: gemm_nt(x, w, out=out)  # noqa: E731
+        def ours():
+            set_gemm_variant(GEMM_AUTO)
+            gemm_nt(x, w, out=out)
+
+        def v1():
+            set_gemm_variant(GEMM_V1)
+            gemm_nt(x, w, out=out)
+
         ref = lambda: torch.matmul(x, w.t(), out=out)  # noqa: E731
-        for f in (ours, ref):
+        for f in (ours, v1, ref):
             for _ in range(3):
                 f()
         torch.cuda.synchronize()
-        t_o, t_r = [], []
+        t_o, t_1, t_r = [], [], []
         for _ in range(a.rounds):
             t_o.append(time_fn(ours, a.iters))
+            t_1.append(time_fn(v1, a.iters))
             t_r.append(time_fn(ref, a.iters))
+        set_gemm_variant(GEMM_AUTO)
         flop = 2.0 * M * N * K
-        mo, mr = statistics.median(t_o), statistics.median(t_r)
-        row = {"shape": [M, N, K], "ours_ms": round(mo, 4), "torch_ms": round(mr, 4),
-               "ours_tflops": round(flop / mo / 1e9, 1), "torch_tflops": round(flop / mr / 1e9, 1),
-               "speedup": round(mr / mo, 3)}
+        mo, m1, mr = statistics.median(t_o), statistics.median(t_1), statistics.median(t_r)
+        row = {"shape": [M, N, K], "ours_ms": round(mo, 4), "v1_ms": round(m1, 4), "torch_ms": round(mr, 4),
+               "ours_tflops": round(flop / mo / 1e9, 1), "v1_tflops": round(flop / m1 / 1e9, 1),
+               "torch_tflops": round(flop / mr / 1e9, 1), "speedup": round(mr / mo, 3)}
         res.append(row)
         print(json.dumps(row), flush=True)
     if a.out:
