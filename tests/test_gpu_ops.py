@@ -40,7 +40,8 @@ def test_gemm_nt_matches_fp32(M, N, K):
     assert_close_bf16(out, ref_linear(a, b), K)
 
 
-@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 768, 256), (2048, 1024, 4096), (4096, 4096, 4096)])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (256, 256, 64), (512, 768, 256), (2048, 1024, 4096),
+                                   (4096, 4096, 4096)])
 def test_gemm_pingpong_matches_v1_and_fp32(M, N, K):
     """The 8-phase ping-pong kernel (aligned shapes) against fp32 and against the 2-stage kernel."""
     from aliyun_gpushare_device_plugin_amd.ops import gemm_nt
@@ -50,14 +51,18 @@ def test_gemm_pingpong_matches_v1_and_fp32(M, N, K):
     try:
         set_gemm_variant(GEMM_V1)
         o1 = gemm_nt(a, b)
-        set_gemm_variant(GEMM_AUTO)
-        o2 = gemm_nt(a, b)
+        outs = []
+        for v in (2, 3):
+            set_gemm_variant(v)
+            outs.append(gemm_nt(a, b))
         torch.cuda.synchronize()
     finally:
         set_gemm_variant(GEMM_AUTO)
-    assert_close_bf16(o2, ref_linear(a, b), K)
-    # same fp32 accumulation order per k-step -> bitwise-identical or 1-ulp bf16 differences
-    assert (o1.float() - o2.float()).abs().max().item() <= (o1.float().abs().max().item() * 2 ** -7)
+    ref = ref_linear(a, b)
+    for o2 in outs:
+        assert_close_bf16(o2, ref, K)
+        # same fp32 accumulation order per k-step -> bitwise-identical or 1-ulp bf16 differences
+        assert (o1.float() - o2.float()).abs().max().item() <= (o1.float().abs().max().item() * 2 ** -7)
 
 
 def test_gemm_identity_asymmetric():

@@ -36,37 +36,39 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--variants", default="1,2,3", help="extra kernel variants to time besides auto")
     a = ap.parse_args()
     res = []
+    variants = [int(v) for v in a.variants.split(",") if v]
     for s in a.shapes.split(","):
         M, N, K = map(int, s.split("x"))
         x = torch.empty(M, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)
         w = torch.empty(N, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)
         out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-        def ours():
-            set_gemm_variant(GEMM_AUTO)
-            gemm_nt(x, w, out=out)
+        def run_variant(v):
+            def f():
+                set_gemm_variant(v)
+                gemm_nt(x, w, out=out)
+            return f
 
-        def v1():
-            set_gemm_variant(GEMM_V1)
-            gemm_nt(x, w, out=out)
-
-        ref = lambda: torch.matmul(x, w.t(), out=out)  # noqa: E731
-        for f in (ours, v1, ref):
+        fns = {"ours": run_variant(GEMM_AUTO), **{f"v{v}": run_variant(v) for v in variants},
+               "torch": lambda: torch.matmul(x, w.t(), out=out)}
+        for f in fns.values():
             for _ in range(3):
                 f()
         torch.cuda.synchronize()
-        t_o, t_1, t_r = [], [], []
+        times = {k: [] for k in fns}
         for _ in range(a.rounds):
-            t_o.append(time_fn(ours, a.iters))
-            t_1.append(time_fn(v1, a.iters))
-            t_r.append(time_fn(ref, a.iters))
+            for k, f in fns.items():
+                times[k].append(time_fn(f, a.iters))
         set_gemm_variant(GEMM_AUTO)
         flop = 2.0 * M * N * K
-        mo, m1, mr = statistics.median(t_o), statistics.median(t_1), statistics.median(t_r)
-        row = {"shape": [M, N, K], "ours_ms": round(mo, 4), "v1_ms": round(m1, 4), "torch_ms": round(mr, 4),
-               "ours_tflops": round(flop / mo / 1e9, 1), "v1_tflops": round(flop / m1 / 1e9, 1),
-               "torch_tflops": round(flop / mr / 1e9, 1), "speedup": round(mr / mo, 3)}
+        row = {"shape": [M, N, K]}
+        for k, t in times.items():
+            med = statistics.median(t)
+            row[f"{k}_ms"] = round(med, 4)
+            row[f"{k}_tflops"] = round(flop / med / 1e9, 1)
+        row["speedup"] = round(row["torch_ms"] / row["ours_ms"], 3)
         res.append(row)
         print(json.dumps(row), flush=True)
     if a.out:

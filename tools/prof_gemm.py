@@ -1,0 +1,31 @@
+#!/usr/bin/env python3
+"""Run each GEMM implementation a few times on fixed shapes (for rocprofv3 --pmc passes).
+
+Dispatch order per shape: v2 (ping-pong) x R, v1 (2-stage) x R, torch/hipBLASLt x R, so the
+per-dispatch counter rows can be attributed by kernel name.
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from aliyun_gpushare_device_plugin_amd.ops import gemm_nt  # noqa: E402
+from aliyun_gpushare_device_plugin_amd.ops.gemm import GEMM_AUTO, GEMM_V1, set_gemm_variant  # noqa: E402
+
+R = int(os.environ.get("PROF_REPS", "3"))
+for s in (sys.argv[1] if len(sys.argv) > 1 else "8192x8192x8192,4096x4096x4096").split(","):
+    M, N, K = map(int, s.split("x"))
+    x = torch.empty(M, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)
+    w = torch.empty(N, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)
+    out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    for variant in (GEMM_AUTO, GEMM_V1):
+        set_gemm_variant(variant)
+        for _ in range(R):
+            gemm_nt(x, w, out=out)
+    set_gemm_variant(GEMM_AUTO)
+    for _ in range(R):
+        torch.matmul(x, w.t(), out=out)
+    torch.cuda.synchronize()
+print("done")
