@@ -62,6 +62,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--preferred-allocation", action="store_true",
                    help="advertise GetPreferredAllocation: the kubelet then picks fake IDs of the GPU the "
                         "extender chose (accurate device checkpoint, one extra RPC per container)")
+    p.add_argument("--partition-aware", type=_bool, nargs="?", const=True, default=True,
+                   help="treat same-socket compute partitions (CPX/DPX/QPX under NPS1) as sharing the socket's "
+                        "HBM and advertise each its share (default true; false = every partition reports full HBM)")
     p.add_argument("--no-swap-completion", action="store_true",
                    help="reference behaviour: fail a pod whose equal-size twin was admitted first "
                         "under its reservation instead of exchanging their GPUs")
@@ -87,7 +90,8 @@ def config_from_args(a) -> PluginConfig:
         shim_host_dir=a.shim_path or None, strict_allocate=a.strict_allocate,
         preferred_allocation=a.preferred_allocation, export_topology=_bool(a.export_topology),
         rocr_visible=a.rocr_visible_devices, metrics_addr=a.metrics_addr, mps=_bool(a.mps),
-        async_patch=not a.sync_patch, complete_swaps=not a.no_swap_completion)
+        async_patch=not a.sync_patch, complete_swaps=not a.no_swap_completion,
+        partition_aware=a.partition_aware)
 
 
 def install_shim(dest_dir: str) -> str:

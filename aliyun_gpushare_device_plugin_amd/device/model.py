@@ -13,7 +13,16 @@ Differences here:
 * each fake device carries its GPU's NUMA node in ``Device.topology``;
 * health is tracked per physical GPU and can recover (the reference could not:
   ``server.go:188``); indices stay stable across hot-unplug so extender ``IDX``
-  annotations keep meaning the same GPU.
+  annotations keep meaning the same GPU;
+* partition awareness (MI355X compute partitioning, SPX/DPX/QPX/CPX x NPS1/NPS2): in a
+  non-SPX mode every partition enumerates as its own HIP device and is advertised as its own
+  GPU, but under NPS1 the partitions of one socket all report the socket's whole HBM. With
+  ``partition_aware`` (default) such a group of same-socket partitions (same unique id, or
+  same BDF) that reports identical totals is treated as sharing that HBM, and each partition
+  is advertised ``total / partitions`` — without it every partition would claim the full
+  288 GB and the node would be over-committed by the partition count. Partitions that report
+  their own (NPS-split) memory are taken as reported. Each GPU records its socket so the
+  topology export can tell partitions of one package apart from xGMI peers.
 """
 from __future__ import annotations
 
@@ -47,33 +56,62 @@ class PhysicalGPU:
     healthy: bool = True
     present: bool = True
     reason: str = ""
+    socket: int = -1        # physical package (same-socket partitions share it)
+    partition: int = 0      # partition index within the socket
 
     @property
     def render_node(self) -> str | None:
         return const.DRI_RENDER_FMT.format(minor=self.render_minor) if self.render_minor >= 0 else None
 
 
+def socket_key(g: GPU) -> str:
+    """Identity of the physical package a (possibly partitioned) device belongs to."""
+    return f"uid:{g.unique_id:x}" if g.unique_id else f"bdf:{g.bdf}" if g.bdf else f"idx:{g.index}"
+
+
+def partition_layout(gpus: list[GPU], partition_aware: bool = True) -> tuple[dict, dict, dict]:
+    """Returns ``({index: socket}, {index: partition}, {index: usable bytes})``."""
+    groups: dict[str, list[GPU]] = {}
+    for g in gpus:
+        groups.setdefault(socket_key(g), []).append(g)
+    sockets, parts, vram = {}, {}, {}
+    for s, (_, members) in enumerate(groups.items()):
+        members = sorted(members, key=lambda g: g.index)
+        shared = (partition_aware and len(members) > 1 and len({m.vram_total for m in members}) == 1
+                  and all(m.memory_partition in (0, 1) for m in members))
+        if shared:
+            log.info("socket %s: %d compute partitions share %d bytes of HBM (NPS1); %d bytes each",
+                     socket_key(members[0]), len(members), members[0].vram_total,
+                     members[0].vram_total // len(members))
+        for p, m in enumerate(members):
+            sockets[m.index], parts[m.index] = s, p
+            vram[m.index] = m.vram_total // len(members) if shared else m.vram_total
+    return sockets, parts, vram
+
+
 class DeviceModel:
     """Thread-safe device table; ``generation`` bumps on every health change."""
 
     def __init__(self, gpus: list[GPU], unit: str = const.GIB, round_policy: str = "nearest",
-                 homogeneous: bool = True, gpu_indices: list[int] | None = None):
+                 homogeneous: bool = True, gpu_indices: list[int] | None = None, partition_aware: bool = True):
         self.unit = unit
         self.round_policy = round_policy
         self._lock = threading.Lock()
         self._cond = threading.Condition(self._lock)
         self.generation = 0
         sel = [g for g in gpus if gpu_indices is None or g.index in set(gpu_indices)]
-        per = [U.units_for_bytes(g.vram_total, unit, round_policy) for g in sel]
+        sockets, part_idx, vram = partition_layout(gpus, partition_aware)
+        per = [U.units_for_bytes(vram[g.index], unit, round_policy) for g in sel]
         if homogeneous and per and len(set(per)) > 1:
             log.warning("heterogeneous GPU memory %s %s; advertising the minimum (%d) per GPU",
                         per, unit, min(per))
             per = [min(per)] * len(per)
         self.gpus: list[PhysicalGPU] = []
         for new_idx, (g, u) in enumerate(zip(sel, per)):
-            self.gpus.append(PhysicalGPU(index=new_idx, uuid=g.uuid, vram_bytes=g.vram_total, units=u,
+            self.gpus.append(PhysicalGPU(index=new_idx, uuid=g.uuid, vram_bytes=vram[g.index], units=u,
                                          numa_node=g.numa_node, render_minor=g.render_minor, bdf=g.bdf,
-                                         name=g.name, healthy=g.health == 0))
+                                         name=g.name, healthy=g.health == 0, socket=sockets[g.index],
+                                         partition=part_idx[g.index]))
         total = sum(g.units for g in self.gpus)
         if total > U.MAX_FAKE_DEVICES_PER_NODE:
             raise ValueError(f"{total} fake devices exceed the ListAndWatch limit "

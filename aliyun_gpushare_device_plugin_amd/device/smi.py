@@ -127,7 +127,14 @@ class SMIError(RuntimeError):
 
 
 class SMI:
-    """One open backend. Thread-safe (the C++ side locks its device table)."""
+    """One open backend. Thread-safe: the C++ side locks its device table, and this wrapper
+    makes ``close()`` safe against calls in flight on other threads (the health monitor
+    blocks in ``wait_event`` while the manager may shut down) — close marks the handle
+    closing, waits for in-flight calls to return, and only then frees it; later calls raise
+    ``SMIError`` instead of touching freed memory (found by the ASan run in
+    tests/test_gpuinfo_native.py)."""
+
+    CLOSE_WAIT_S = 30.0
 
     def __init__(self, spec: str = "auto"):
         self._lib = _load()
@@ -135,10 +142,43 @@ class SMI:
         if self._lib.gs_open(spec.encode(), ctypes.byref(h)) != 0:
             raise SMIError(f"gs_open({spec!r}): {self._lib.gs_last_error().decode()}")
         self._h = h
+        self._cv = threading.Condition()
+        self._active = 0
+        self._closing = False
         self.spec = spec
 
+    def _enter(self):
+        with self._cv:
+            if self._h is None or self._closing:
+                raise SMIError("SMI handle is closed")
+            self._active += 1
+            return self._h
+
+    def _exit(self):
+        with self._cv:
+            self._active -= 1
+            if self._active == 0:
+                self._cv.notify_all()
+
+    def _call(self, fn, *args):
+        h = self._enter()
+        try:
+            return fn(h, *args)
+        finally:
+            self._exit()
+
     def close(self):
-        if self._h:
+        cv = getattr(self, "_cv", None)
+        if cv is None:
+            return
+        with cv:
+            if self._h is None or self._closing:
+                return
+            self._closing = True
+            cv.wait_for(lambda: self._active == 0, timeout=self.CLOSE_WAIT_S)
+            if self._active:
+                # a native call is stuck: leak the handle rather than free it under the call
+                return
             self._lib.gs_close(self._h)
             self._h = None
 
@@ -156,26 +196,26 @@ class SMI:
 
     @property
     def backend(self) -> str:
-        return self._lib.gs_backend_name(self._h).decode()
+        return self._call(self._lib.gs_backend_name).decode()
 
     def _err(self, what):
         raise SMIError(f"{what}: {self._lib.gs_last_error().decode()}")
 
     def refresh(self) -> int:
-        n = self._lib.gs_refresh(self._h)
+        n = self._call(self._lib.gs_refresh)
         if n < 0:
             self._err("gs_refresh")
         return n
 
     def count(self) -> int:
-        return self._lib.gs_device_count(self._h)
+        return self._call(self._lib.gs_device_count)
 
     def inaccessible(self) -> int:
-        return self._lib.gs_inaccessible_count(self._h)
+        return self._call(self._lib.gs_inaccessible_count)
 
     def device(self, i: int) -> GPU:
         d = _Device()
-        if self._lib.gs_get_device(self._h, i, ctypes.byref(d)) != 0:
+        if self._call(self._lib.gs_get_device, i, ctypes.byref(d)) != 0:
             self._err(f"gs_get_device({i})")
         return GPU(index=d.index, uuid=d.uuid.decode(), bdf=d.bdf.decode(), name=d.name.decode(),
                    gfx=d.gfx.decode(), vram_total=d.vram_total, vram_used=d.vram_used, numa_node=d.numa_node,
@@ -188,7 +228,7 @@ class SMI:
 
     def link(self, i: int, j: int) -> Link:
         L = _Link()
-        if self._lib.gs_get_link(self._h, i, j, ctypes.byref(L)) != 0:
+        if self._call(self._lib.gs_get_link, i, j, ctypes.byref(L)) != 0:
             self._err(f"gs_get_link({i},{j})")
         return Link(L.type, L.hops, L.weight, L.max_bandwidth_mbps)
 
@@ -197,11 +237,11 @@ class SMI:
         return [[self.link(i, j) for j in range(n)] for i in range(n)]
 
     def events_start(self):
-        self._lib.gs_events_start(self._h)
+        self._call(self._lib.gs_events_start)
 
     def wait_event(self, timeout_ms: int) -> Event | None:
         ev = _Event()
-        rc = self._lib.gs_wait_event(self._h, int(timeout_ms), ctypes.byref(ev))
+        rc = self._call(self._lib.gs_wait_event, int(timeout_ms), ctypes.byref(ev))
         if rc < 0:
             self._err("gs_wait_event")
         if rc == 0:
@@ -209,11 +249,15 @@ class SMI:
         return Event(ev.index, ev.kind, ev.message.decode(errors="replace"))
 
     def inject(self, cmd: str):
-        if self._lib.gs_inject(self._h, cmd.encode()) != 0:
+        if self._call(self._lib.gs_inject, cmd.encode()) != 0:
             self._err(f"gs_inject({cmd!r})")
 
     def to_json(self) -> dict:
-        n = self._lib.gs_to_json(self._h, None, 0)
-        buf = ctypes.create_string_buffer(n + 1)
-        self._lib.gs_to_json(self._h, buf, n + 1)
+        h = self._enter()
+        try:
+            n = self._lib.gs_to_json(h, None, 0)
+            buf = ctypes.create_string_buffer(n + 1)
+            self._lib.gs_to_json(h, buf, n + 1)
+        finally:
+            self._exit()
         return json.loads(buf.value.decode())

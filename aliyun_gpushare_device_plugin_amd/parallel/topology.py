@@ -16,15 +16,19 @@ from ..device import smi as S
 
 
 def build_topology(smi: S.SMI, indices: list[int] | None = None) -> dict:
+    from ..device.model import partition_layout
+
     devs = smi.devices()
     sel = [d for d in devs if indices is None or d.index in set(indices)]
     m = smi.link_matrix()
     idx = [d.index for d in sel]
+    sockets, parts, _ = partition_layout(devs)
     return {
         "version": 1,
         "hive_id": format(sel[0].hive_id, "x") if sel else "0",
         "gpus": [{"index": k, "uuid": d.uuid, "bdf": d.bdf, "numa": d.numa_node,
-                  "partition": d.compute_partition, "nps": d.memory_partition} for k, d in enumerate(sel)],
+                  "partition": d.compute_partition, "nps": d.memory_partition,
+                  "socket": sockets[d.index], "partition_index": parts[d.index]} for k, d in enumerate(sel)],
         "link_type": [[m[i][j].type_name for j in idx] for i in idx],
         "hops": [[m[i][j].hops for j in idx] for i in idx],
         "weight": [[m[i][j].weight for j in idx] for i in idx],

@@ -65,6 +65,7 @@ class PluginConfig:
     metrics_addr: str | None = None
     async_patch: bool = True             # write-behind ASSIGNED patch (see AllocatorOptions)
     complete_swaps: bool = True          # match a swapped equal-size pod (see alloc/engine.py)
+    partition_aware: bool = True         # divide NPS1-shared HBM among compute partitions
     mps: bool = False                    # accepted for flag compatibility; ignored
 
 
@@ -119,7 +120,7 @@ class SharedGPUManager:
         cfg = self.cfg
         self.smi.refresh()
         model = DeviceModel(self.smi.devices(), cfg.memory_unit, cfg.round_policy, cfg.homogeneous,
-                            cfg.gpu_indices)
+                            cfg.gpu_indices, partition_aware=cfg.partition_aware)
         for g in model.gpus:
             self.metrics.units_per_gpu.set(g.units, gpu=str(g.index))
             self.metrics.device_health.set(1 if g.healthy else 0, gpu=str(g.index))

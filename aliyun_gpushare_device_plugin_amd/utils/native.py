@@ -30,6 +30,11 @@ class NativeUnavailable(RuntimeError):
 
 
 def lib_path(target: str) -> str:
+    """``GPUSHARE_NATIVE_VARIANT=asan|tsan`` selects a sanitizer build (native/build.py
+    --sanitize) from ``_native/<variant>/``; the matching runtime must be LD_PRELOADed."""
+    variant = os.environ.get("GPUSHARE_NATIVE_VARIANT", "")
+    if variant:
+        return os.path.join(NATIVE_DIR, variant, LIBS[target])
     return os.path.join(NATIVE_DIR, LIBS[target])
 
 
@@ -46,7 +51,9 @@ def ensure_built(target: str, auto_build: bool | None = None) -> str:
     if auto_build and os.path.exists(BUILD_SCRIPT):
         with _lock:
             if not os.path.exists(path):
-                r = subprocess.run([sys.executable, BUILD_SCRIPT, target], capture_output=True, text=True)
+                variant = os.environ.get("GPUSHARE_NATIVE_VARIANT", "")
+                extra = ["--sanitize", variant] if variant else []
+                r = subprocess.run([sys.executable, BUILD_SCRIPT, target, *extra], capture_output=True, text=True)
                 if r.returncode != 0:
                     raise NativeUnavailable(f"building {target} failed:\n{r.stdout}\n{r.stderr}")
     if not os.path.exists(path):

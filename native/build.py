@@ -6,7 +6,7 @@ Targets
   hipshim   libgpushare_hipquota.so  (C++17 LD_PRELOAD interposer over the HIP allocation API)
   kernels   libgpushare_kernels.so   (hand-written HIP/CDNA4 kernels, hipcc --offload-arch=gfx950)
 
-Usage: python native/build.py [targets...] [--force] [--asan] [-j N]
+Usage: python native/build.py [targets...] [--force] [--asan | --sanitize {asan,tsan}] [-j N]
 The build is incremental (mtime based) so ``__graft_entry__.build()`` stays cheap.
 """
 from __future__ import annotations
@@ -54,14 +54,29 @@ def _headers(d):
     return [os.path.join(d, f) for f in os.listdir(d) if f.endswith((".h", ".hpp", ".inc"))]
 
 
+SANITIZERS = {
+    # host-side only (GPU ASan / XNACK are not available on the pool)
+    "asan": ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-O1"],
+    "tsan": ["-fsanitize=thread", "-fno-omit-frame-pointer", "-O1"],
+}
+
+
+def _san(asan):
+    """``asan`` is False/None, True (= "asan") or a SANITIZERS key."""
+    if not asan:
+        return None
+    return "asan" if asan is True else asan
+
+
 def build_gpuinfo(force=False, asan=False):
     d = _src("gpuinfo")
     lib = os.path.join(OUT, "libgpushare_gpuinfo.so")
     deps = [_src("gpuinfo", "gpuinfo.cpp")] + _headers(d)
     flags = ["-std=c++17", "-O2", "-fPIC", "-Wall", "-Wextra", "-Wno-unused-parameter", f"-I{d}"]
-    if asan:
-        flags += ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-O1"]
-        lib = os.path.join(OUT, "asan", "libgpushare_gpuinfo.so")
+    san = _san(asan)
+    if san:
+        flags += SANITIZERS[san]
+        lib = os.path.join(OUT, san, "libgpushare_gpuinfo.so")
     os.makedirs(os.path.dirname(lib), exist_ok=True)
     if force or _newer(lib, deps):
         _run([CXX, *flags, "-shared", "-o", lib, _src("gpuinfo", "gpuinfo.cpp"), "-ldl", "-pthread"])
@@ -80,9 +95,10 @@ def build_hipshim(force=False, asan=False):
     lib = os.path.join(OUT, "libgpushare_hipquota.so")
     flags = ["-std=c++17", "-O2", "-fPIC", "-Wall", "-Wextra", "-Wno-unused-parameter",
              "-D__HIP_PLATFORM_AMD__", f"-I{ROCM}/include", f"-I{d}", "-fvisibility=hidden"]
-    if asan:
-        flags += ["-fsanitize=address,undefined", "-fno-omit-frame-pointer"]
-        lib = os.path.join(OUT, "asan", "libgpushare_hipquota.so")
+    san = _san(asan)
+    if san:
+        flags += SANITIZERS[san]
+        lib = os.path.join(OUT, san, "libgpushare_hipquota.so")
     os.makedirs(os.path.dirname(lib), exist_ok=True)
     if force or _newer(lib, [src] + _headers(d)):
         # Deliberately NOT linked against libamdhip64: the real entry points are resolved at
@@ -102,7 +118,7 @@ def build_kernels(force=False, asan=False, jobs=4):
     hdrs = _headers(d)
     flags = ["-std=c++17", "-O3", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
              "-Wno-unused-result", f"-I{d}", "-D__HIP_PLATFORM_AMD__"]
-    if asan:  # host-side sanitizers only; GPU ASan is not available on the pool
+    if _san(asan) == "asan":  # host-side sanitizers only; GPU ASan is not available on the pool
         flags += ["-Xarch_host", "-fsanitize=address", "-fno-omit-frame-pointer"]
     objs, todo = [], []
     for s in srcs:
@@ -134,9 +150,11 @@ def main(argv=None):
     ap.add_argument("targets", nargs="*", choices=[[], *TARGETS], default=None)
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--asan", action="store_true", help="host-side ASan/UBSan variants under _native/asan")
+    ap.add_argument("--sanitize", choices=sorted(SANITIZERS), default=None,
+                    help="host-side sanitizer variant under _native/<name> (asan = ASan+UBSan, tsan = TSan)")
     ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 4))
     a = ap.parse_args(argv)
-    for p in build(a.targets or None, a.force, a.asan, a.jobs):
+    for p in build(a.targets or None, a.force, a.sanitize or a.asan, a.jobs):
         print("built", os.path.relpath(p, ROOT))
 
 

@@ -556,6 +556,7 @@ class FakeBackend : public Backend {
       d.numa_node = (int32_t)jd.num_or("numa_node", d.numa_node);
       d.render_minor = (int32_t)jd.num_or("render_minor", d.render_minor);
       d.hive_id = (uint64_t)jd.num_or("hive_id", (double)d.hive_id);
+      d.unique_id = (uint64_t)jd.num_or("unique_id", (double)d.unique_id);
       d.compute_partition = (int32_t)jd.num_or("compute_partition", 1);
       d.memory_partition = (int32_t)jd.num_or("memory_partition", 1);
       d.vram_used = (uint64_t)jd.num_or("vram_used", 0);

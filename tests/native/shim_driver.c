@@ -1,5 +1,8 @@
 // Test driver: executes allocation commands against the (stub or real) HIP runtime and
 // prints one JSON line per command. Linked against libamdhip64.so.7 like any HIP program.
+#define _GNU_SOURCE
+#include <dlfcn.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -10,6 +13,17 @@ hipError_t hipMalloc(void**, size_t); hipError_t hipFree(void*);
 hipError_t hipMemGetInfo(size_t*, size_t*); hipError_t hipMallocAsync(void**, size_t, void*);
 hipError_t hipFreeAsync(void*, void*); hipError_t hipMemCreate(uint64_t*, size_t, const void*, unsigned long long);
 hipError_t hipMemRelease(uint64_t);
+// "threads N ITERS SIZE": N threads each alloc+free SIZE bytes ITERS times (quota contention)
+struct targ { int iters; size_t n; int ok, denied; };
+static void* worker(void* v) {
+  struct targ* a = (struct targ*)v;
+  for (int k = 0; k < a->iters; ++k) {
+    void* p = 0;
+    if (hipMalloc(&p, a->n) == 0) { a->ok++; hipFree(p); } else a->denied++;
+  }
+  return 0;
+}
+typedef int (*stats_fn)(uint64_t*, uint64_t*, uint64_t*, uint64_t*);
 int main(int argc, char** argv) {
   void* ptrs[4096]; int np = 0;
   for (int i = 1; i < argc; ++i) {
@@ -24,6 +38,15 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[i], "freeall")) { for (int k = 0; k < np; ++k) if (ptrs[k]) hipFree(ptrs[k]); np = 0; printf("{\"op\":\"freeall\"}\n"); }
     else if (!strcmp(argv[i], "info")) { size_t f = 0, t = 0; int e = hipMemGetInfo(&f, &t);
       printf("{\"op\":\"info\",\"free\":%zu,\"total\":%zu,\"err\":%d}\n", f, t, e); }
+    else if (!strcmp(argv[i], "threads")) { int nt = atoi(argv[++i]); int it = atoi(argv[++i]); size_t n = strtoull(argv[++i], 0, 10);
+      pthread_t th[64]; struct targ a[64]; int ok = 0, den = 0; if (nt > 64) nt = 64;
+      for (int t = 0; t < nt; ++t) { a[t].iters = it; a[t].n = n; a[t].ok = a[t].denied = 0; pthread_create(&th[t], 0, worker, &a[t]); }
+      for (int t = 0; t < nt; ++t) { pthread_join(th[t], 0); ok += a[t].ok; den += a[t].denied; }
+      printf("{\"op\":\"threads\",\"ok\":%d,\"denied\":%d}\n", ok, den); }
+    else if (!strcmp(argv[i], "stats")) { stats_fn f = (stats_fn)dlsym(RTLD_DEFAULT, "gpushare_shim_stats");
+      uint64_t u = 0, q = 0, d = 0, pk = 0; int e = f ? f(&u, &q, &d, &pk) : -1;
+      printf("{\"op\":\"stats\",\"enabled\":%d,\"used\":%llu,\"quota\":%llu,\"denied\":%llu,\"peak\":%llu}\n", e,
+             (unsigned long long)u, (unsigned long long)q, (unsigned long long)d, (unsigned long long)pk); }
     else if (!strcmp(argv[i], "sleep")) { usleep((useconds_t)(atof(argv[++i]) * 1e6)); }
     else if (!strcmp(argv[i], "crash")) { fflush(stdout); _exit(3); }
     fflush(stdout);

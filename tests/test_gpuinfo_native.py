@@ -36,6 +36,22 @@ def test_fake_json_spec(tmp_path):
         assert s.link(0, 1).type == S.LINK_PCIE
 
 
+def test_fake_json_partitions_share_socket(tmp_path):
+    """CPX-style partitions (same unique id) -> one socket in the model and the topology export."""
+    from aliyun_gpushare_device_plugin_amd import const
+    from aliyun_gpushare_device_plugin_amd.device.model import DeviceModel
+    from aliyun_gpushare_device_plugin_amd.parallel.topology import build_topology
+    devs = [{"uuid": f"GPU-p{i}", "vram_total": 288 << 30, "unique_id": 4096 + i // 2, "compute_partition": 2,
+             "memory_partition": 1} for i in range(4)]
+    p = tmp_path / "cpx.json"
+    p.write_text(json.dumps({"devices": devs}))
+    with S.SMI(f"fake:{p}") as s:
+        assert [d.unique_id for d in s.devices()] == [4096, 4096, 4097, 4097]
+        assert [g.units for g in DeviceModel(s.devices(), const.GIB).gpus] == [144] * 4
+        topo = build_topology(s)
+        assert [(g["socket"], g["partition_index"]) for g in topo["gpus"]] == [(0, 0), (0, 1), (1, 0), (1, 1)]
+
+
 def test_fault_injection_events_and_membership():
     with S.SMI("fake:4x288G") as s:
         s.inject("unplug 2")
@@ -126,3 +142,56 @@ def test_smi_cli_json(native_gpuinfo, tmp_path):
     assert d["backend"] == "fake" and len(d["devices"]) == 2 and d["links"][0][1]["type"] == S.LINK_XGMI
     r = subprocess.run([cli, "--backend", "fake:2x4G"], capture_output=True, text=True, check=True)
     assert "XGMI1" in r.stdout and "gfx950" in r.stdout
+
+
+_SAN_SCRIPT = r"""
+import threading
+from aliyun_gpushare_device_plugin_amd.device import smi as S
+with S.SMI("fake:8x288G") as s:
+    assert s.count() == 8
+    m = s.link_matrix()
+    assert m[0][1].type == S.LINK_XGMI
+    def poll():
+        for _ in range(50):
+            s.refresh()
+    t = threading.Thread(target=poll)
+    t.start()
+    for k in range(4):
+        s.inject(f"unplug {k}"); s.wait_event(1000)
+        s.inject(f"replug {k}"); s.wait_event(1000)
+        s.inject(f"reset {k}"); s.wait_event(1000); s.wait_event(1000)
+        s.inject(f"linkdown {k} {k + 1}"); s.wait_event(1000)
+    t.join()
+    # close while another thread is blocked in wait_event: must wait for it, not free under it
+    waiter = threading.Thread(target=lambda: s.wait_event(300))
+    waiter.start()
+    s.close()
+    waiter.join()
+    try:
+        s.count()
+        raise SystemExit("call after close did not raise")
+    except S.SMIError:
+        pass
+print("SAN-OK")
+"""
+
+
+@pytest.mark.parametrize("san", ["asan", "tsan"])
+def test_gpuinfo_under_sanitizers(san):
+    """libgpushare_gpuinfo built with ASan+UBSan / TSan, exercised through fault injection with
+    a concurrent refresh thread (the health monitor's pattern)."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "native", "build.py"), "gpuinfo", "--sanitize", san],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    rt = subprocess.run(["gcc", f"-print-file-name=lib{san}.so"], capture_output=True, text=True).stdout.strip()
+    if not os.path.exists(rt):
+        pytest.skip(f"lib{san}.so not installed")
+    env = dict(os.environ, LD_PRELOAD=rt, GPUSHARE_NATIVE_VARIANT=san, PYTHONPATH=root,
+               ASAN_OPTIONS="detect_leaks=0:halt_on_error=1", UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1",
+               TSAN_OPTIONS="halt_on_error=1:report_signal_unsafe=0")
+    r = subprocess.run([sys.executable, "-c", _SAN_SCRIPT], env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0 and "SAN-OK" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
+    assert "ERROR: AddressSanitizer" not in r.stderr and "WARNING: ThreadSanitizer" not in r.stderr, r.stderr[-4000:]
+    assert "runtime error" not in r.stderr, r.stderr[-4000:]

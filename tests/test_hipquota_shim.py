@@ -24,8 +24,8 @@ def stub(tmp_path_factory):
     subprocess.run(["gcc", "-shared", "-fPIC", "-O1", "-Wl,-soname,libamdhip64.so.7", "-o", str(lib),
                     os.path.join(HERE, "native", "fake_hip.c")], check=True)
     drv = d / "shim_driver"
-    subprocess.run(["gcc", "-O1", "-o", str(drv), os.path.join(HERE, "native", "shim_driver.c"),
-                    str(lib), f"-Wl,-rpath,{d}"], check=True)
+    subprocess.run(["gcc", "-O1", "-pthread", "-o", str(drv), os.path.join(HERE, "native", "shim_driver.c"),
+                    str(lib), f"-Wl,-rpath,{d}", "-ldl"], check=True)
     return d, drv
 
 
@@ -124,5 +124,50 @@ def test_crashed_process_charge_is_reclaimed(stub, native_shim):
         assert out[0]["err"] == 0 and r.returncode == 3   # _exit: no atexit cleanup ran
         out, _ = run(stub, native_shim, ["alloc", 3 * GIB], GPUSHARE_LEDGER=name, GPUSHARE_QUOTA_BYTES=4 * GIB)
         assert out[0]["err"] == 0                           # dead pid's 3 GiB reclaimed
+    finally:
+        cleanup(name)
+
+
+def test_concurrent_threads_never_exceed_quota(stub, native_shim):
+    """16 threads contend for a 64 MiB quota with 8 MiB allocations: the ledger's peak never
+    exceeds the quota, every grant is returned, and denials are counted."""
+    name = ledger()
+    try:
+        out, r = run(stub, native_shim, ["threads", 16, 400, 8 * MIB, "stats", "info"], GPUSHARE_LEDGER=name,
+                     GPUSHARE_QUOTA_BYTES=64 * MIB)
+        th, st, info = out
+        assert th["ok"] + th["denied"] == 16 * 400 and th["ok"] > 0
+        assert st["enabled"] == 1 and st["quota"] == 64 * MIB
+        assert st["peak"] <= 64 * MIB and st["used"] == 0 and st["denied"] == th["denied"]
+        assert info["free"] == 64 * MIB
+    finally:
+        cleanup(name)
+
+
+@pytest.mark.parametrize("san", ["asan", "tsan"])
+def test_shim_under_sanitizers(stub, tmp_path, san):
+    """The shim built with -fsanitize=address,undefined / -fsanitize=thread (host code; GPU
+    sanitizers are not available), run through the multi-process and multi-thread paths."""
+    import sys
+    sys.path.insert(0, os.path.join(HERE, "..", "native"))
+    import build as nb
+    lib = nb.build_hipshim(asan=san)[0]
+    rt = subprocess.run(["gcc", f"-print-file-name=lib{san}.so"], capture_output=True, text=True).stdout.strip()
+    if not os.path.exists(rt):
+        pytest.skip(f"lib{san}.so not installed")
+    d, drv = stub
+    name = ledger()
+    env = {"LD_PRELOAD": f"{rt}:{lib}", "LD_LIBRARY_PATH": str(d), "GPUSHARE_LEDGER": name,
+           "GPUSHARE_QUOTA_BYTES": str(64 * MIB), "ASAN_OPTIONS": "detect_leaks=0:halt_on_error=1",
+           "UBSAN_OPTIONS": "halt_on_error=1:print_stacktrace=1", "TSAN_OPTIONS": "halt_on_error=1:report_bugs=1"}
+    try:
+        e = dict(os.environ, **env)
+        r = subprocess.run([str(drv), "threads", "8", "200", str(8 * MIB), "alloc", str(GIB), "alloc", str(MIB),
+                            "free", "0", "stats"], env=e, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr[-3000:]
+        assert "ERROR: AddressSanitizer" not in r.stderr and "WARNING: ThreadSanitizer" not in r.stderr, r.stderr[-3000:]
+        assert "runtime error" not in r.stderr, r.stderr[-3000:]
+        out = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+        assert out[1]["err"] == 2 and out[2]["err"] == 0 and out[-1]["used"] == 0
     finally:
         cleanup(name)

@@ -85,3 +85,29 @@ def test_health_generation_and_recovery():
 def test_mib_mode_limit():
     with pytest.raises(ValueError):
         DeviceModel([gpu(i) for i in range(8)], const.MIB)
+
+
+def part(i, socket, cp=4, nps=1, nbytes=MI355X_BYTES):
+    g = gpu(i, nbytes)
+    return GPU(**{**g.__dict__, "unique_id": 0xabc0 + socket, "bdf": f"0000:{0x10 * socket:02x}:00.0",
+                  "compute_partition": cp, "memory_partition": nps})
+
+
+def test_partition_aware_divides_shared_hbm():
+    """2 sockets in QPX x NPS1: 8 HIP devices, each reporting its socket's full HBM."""
+    devs = [part(i, i // 4) for i in range(8)]
+    m = DeviceModel(devs, const.GIB)
+    assert m.count() == 8
+    assert [g.units for g in m.gpus] == [72] * 8              # 288 GiB / 4 partitions
+    assert [(g.socket, g.partition) for g in m.gpus] == [(s, p) for s in range(2) for p in range(4)]
+    assert m.total_units() == 2 * 288                        # never more than the real HBM
+    naive = DeviceModel(devs, const.GIB, partition_aware=False)
+    assert naive.total_units() == 8 * 288                    # the 4x over-commit it prevents
+
+
+def test_partition_aware_keeps_nps_split_memory():
+    """NPS2 partitions report their own half of the HBM: taken as reported."""
+    devs = [part(i, 0, cp=2, nps=2, nbytes=MI355X_BYTES // 2) for i in range(2)]
+    assert [g.units for g in DeviceModel(devs, const.GIB).gpus] == [144, 144]
+    spx = [gpu(i) for i in range(8)]                         # SPX: one device per socket
+    assert DeviceModel(spx, const.GIB).total_units() == 8 * 288
