@@ -67,6 +67,9 @@ class AllocatorOptions:
     match_containers: bool = True
     claim_ttl_s: float = 120.0
     complete_swaps: bool = True
+    # host directory for file-backed shim ledgers (mounted read-write into every shared
+    # container at const.LEDGER_CONTAINER_DIR); None = pod-private POSIX shm ledgers
+    ledger_dir: str | None = None
     # Write-behind ASSIGNED=true PATCH: Allocate answers after the in-memory claim and a
     # background patcher lands the annotation (retrying); the claim blocks re-matching until it
     # has. False = the reference's synchronous PATCH inside Allocate (allocate.go:132-152).
@@ -192,6 +195,10 @@ class Allocator:
             r.mounts.add(container_path=shim.container_dir, host_path=shim.host_dir, read_only=True)
             r.envs[const.ENV_LD_PRELOAD] = shim.container_lib
             r.envs[const.ENV_SHIM_LEDGER] = ledger_name(pod_uid or f"{gpu_index}-{time.time_ns()}", slot)
+            if self.opts.ledger_dir:
+                r.mounts.add(container_path=const.LEDGER_CONTAINER_DIR, host_path=self.opts.ledger_dir,
+                             read_only=False)
+                r.envs[const.ENV_SHIM_LEDGER_DIR] = const.LEDGER_CONTAINER_DIR
         return r
 
     def _err_response(self, req, pod_units: int) -> api.AllocateResponse:

@@ -65,6 +65,10 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--partition-aware", type=_bool, nargs="?", const=True, default=True,
                    help="treat same-socket compute partitions (CPX/DPX/QPX under NPS1) as sharing the socket's "
                         "HBM and advertise each its share (default true; false = every partition reports full HBM)")
+    p.add_argument("--ledger-dir", default=None,
+                   help="host directory for file-backed quota-shim ledgers, mounted into every shared "
+                        "container; the plugin exports per-container HBM used/peak/denials from it")
+    p.add_argument("--ledger-scan-interval", type=float, default=10.0)
     p.add_argument("--no-swap-completion", action="store_true",
                    help="reference behaviour: fail a pod whose equal-size twin was admitted first "
                         "under its reservation instead of exchanging their GPUs")
@@ -91,7 +95,7 @@ def config_from_args(a) -> PluginConfig:
         preferred_allocation=a.preferred_allocation, export_topology=_bool(a.export_topology),
         rocr_visible=a.rocr_visible_devices, metrics_addr=a.metrics_addr, mps=_bool(a.mps),
         async_patch=not a.sync_patch, complete_swaps=not a.no_swap_completion,
-        partition_aware=a.partition_aware)
+        partition_aware=a.partition_aware, ledger_dir=a.ledger_dir, ledger_scan_s=a.ledger_scan_interval)
 
 
 def install_shim(dest_dir: str) -> str:

@@ -62,6 +62,8 @@ ENV_SHIM_LEDGER = "GPUSHARE_LEDGER"          # shm ledger name shared by a conta
 ENV_SHIM_QUOTA_BYTES = "GPUSHARE_QUOTA_BYTES"  # explicit override (tests / debugging)
 ENV_SHIM_GRANULE = "GPUSHARE_ALLOC_GRANULE"    # allocation rounding granule override
 ENV_SHIM_LOG = "GPUSHARE_SHIM_LOG"
+ENV_SHIM_LEDGER_DIR = "GPUSHARE_LEDGER_DIR"    # file-backed ledgers in a host-mounted directory
+LEDGER_CONTAINER_DIR = "/run/gpushare/ledger"
 ENV_GPU_UUID = "GPUSHARE_GPU_UUID"            # the physical GPU a container was given
 ENV_ROCR_VISIBLE = "ROCR_VISIBLE_DEVICES"
 # Node annotation carrying the exported xGMI topology (JSON, see parallel/topology.py).

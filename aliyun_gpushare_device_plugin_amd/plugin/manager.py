@@ -20,7 +20,7 @@ import threading
 
 from .. import const
 from ..alloc.engine import Allocator, AllocatorOptions
-from ..cluster import nodestatus
+from ..cluster import nodestatus, objects as O
 from ..cluster.client import APIClient, build_client
 from ..cluster.kubelet import KubeletClient
 from ..cluster.podcache import KubeletSource, ListSource, WatchCache
@@ -66,6 +66,8 @@ class PluginConfig:
     async_patch: bool = True             # write-behind ASSIGNED patch (see AllocatorOptions)
     complete_swaps: bool = True          # match a swapped equal-size pod (see alloc/engine.py)
     partition_aware: bool = True         # divide NPS1-shared HBM among compute partitions
+    ledger_dir: str | None = None        # host dir for file-backed shim ledgers (usage metrics)
+    ledger_scan_s: float = 10.0
     mps: bool = False                    # accepted for flag compatibility; ignored
 
 
@@ -87,6 +89,8 @@ class SharedGPUManager:
         self.started = threading.Event()
         self.restarts = 0
         self._metrics_srv = None
+        self._ledger_thread = None
+        self._ledger_stop = threading.Event()
 
     # ------------------------------------------------------------------------------------
     def _kubelet_socket(self) -> str:
@@ -147,7 +151,8 @@ class SharedGPUManager:
                               AllocatorOptions(unit=cfg.memory_unit, disable_cgpu=disable_cgpu, shim=shim,
                                                strict=cfg.strict_allocate, expose_devices=cfg.expose_devices,
                                                rocr_visible=cfg.rocr_visible, async_patch=cfg.async_patch,
-                                               complete_swaps=cfg.complete_swaps),
+                                               complete_swaps=cfg.complete_swaps,
+                                               ledger_dir=cfg.ledger_dir if shim else None),
                               self.metrics)
         self.model = model
         return DevicePluginServer(model, allocator, self._plugin_socket(), const.RESOURCE_NAME,
@@ -164,6 +169,34 @@ class SharedGPUManager:
 
             self.health = HealthMonitor(self.smi, self.model, self.cfg.health_poll_s, on_change=changed,
                                         on_topology_change=lambda ev: self._export_topology()).start()
+
+    def _start_ledger_collector(self):
+        """Export the quota shim's per-container ledgers (--ledger-dir) every ledger_scan_s and
+        drop the ledgers of pods that no longer exist on this node."""
+        d = self.cfg.ledger_dir
+        if not d or self._ledger_thread is not None:
+            return
+        from ..quota import ledger as L
+
+        os.makedirs(d, exist_ok=True)
+        try:
+            os.chmod(d, 0o1777)     # containers may run as any uid; sticky like /tmp
+        except OSError as e:
+            log.warning("cannot chmod ledger dir %s: %s", d, e)
+
+        def loop():
+            while not self._ledger_stop.wait(self.cfg.ledger_scan_s):
+                try:
+                    live = None
+                    src = self.pod_source
+                    if isinstance(src, WatchCache) and src.wait_synced(0):
+                        live = {O.uid(p) for p in src.snapshot()}
+                    L.collect(d, self.metrics, live)
+                except Exception as e:  # noqa: BLE001
+                    log.warning("ledger scan failed: %s", e)
+
+        self._ledger_thread = threading.Thread(target=loop, name="ledger-collector", daemon=True)
+        self._ledger_thread.start()
 
     def stop(self):
         self.events.put(("signal", signal.SIGTERM))
@@ -220,6 +253,7 @@ class SharedGPUManager:
                         return 2
                     self._export_topology()
                     self._start_health()
+                    self._start_ledger_collector()
                     restart = False
                     self.started.set()
                 kind, val = self.events.get()
@@ -238,6 +272,7 @@ class SharedGPUManager:
                         break
         finally:
             watcher.close()
+            self._ledger_stop.set()
             if self.health:
                 self.health.stop()
             if self.plugin is not None:

@@ -51,6 +51,10 @@ class Gauge(Counter):
         with self._lock:
             self._v[_labels_key(labels)] = float(value)
 
+    def clear(self):
+        with self._lock:
+            self._v.clear()
+
     def render(self):
         yield f"# HELP {self.name} {self.help}\n# TYPE {self.name} gauge\n"
         for k, v in sorted(self._v.items()):
@@ -161,6 +165,11 @@ class PluginMetrics:
         self.hbm_used = r.gauge("gpushare_hbm_used_bytes", "HBM in use per GPU (SMI)")
         self.cache_events = r.counter("gpushare_pod_cache_events_total", "Pod watch-cache events")
         self.listandwatch_sends = r.counter("gpushare_listandwatch_sends_total", "Device list sends")
+        # quota shim ledgers (--ledger-dir): what each shared container actually holds
+        self.shim_used = r.gauge("gpushare_container_hbm_used_bytes", "HBM held by a container (shim ledger)")
+        self.shim_quota = r.gauge("gpushare_container_hbm_quota_bytes", "Container HBM quota (shim ledger)")
+        self.shim_peak = r.gauge("gpushare_container_hbm_peak_bytes", "Container HBM high-water mark (shim ledger)")
+        self.shim_denied = r.gauge("gpushare_container_quota_denials", "Allocations refused by the quota shim")
 
 
 def serve(registry: Registry, addr: str, health_fn=None) -> http.server.ThreadingHTTPServer:

@@ -300,7 +300,19 @@ void init() {
   const char* ln = getenv("GPUSHARE_LEDGER");
   if (ln && *ln) {
     snprintf(g.ledger_name, sizeof g.ledger_name, "%s%s", ln[0] == '/' ? "" : "/", ln);
-    int fd = shm_open(g.ledger_name, O_RDWR | O_CREAT, 0600);
+    // GPUSHARE_LEDGER_DIR: file-backed ledger in a directory the plugin mounts from the host,
+    // so the node agent can read every container's usage / peak / denials (a container's
+    // /dev/shm is private to its pod); otherwise a POSIX shm object.
+    const char* dir = getenv("GPUSHARE_LEDGER_DIR");
+    int fd = -1;
+    if (dir && *dir) {
+      char path[512];
+      snprintf(path, sizeof path, "%s%s.ledger", dir, g.ledger_name);
+      fd = open(path, O_RDWR | O_CREAT | O_CLOEXEC, 0644);
+      if (fd >= 0) snprintf(g.ledger_name, sizeof g.ledger_name, "%s", path);
+    } else {
+      fd = shm_open(g.ledger_name, O_RDWR | O_CREAT, 0600);
+    }
     if (fd >= 0 && ftruncate(fd, sizeof(LedgerShm)) == 0) {
       void* p = mmap(nullptr, sizeof(LedgerShm), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
       if (p != MAP_FAILED) {

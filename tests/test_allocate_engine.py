@@ -276,3 +276,15 @@ def test_swapped_admission_order_is_completed(complete):
     old = mkpod("old", 2, 1, now - int(600e9), phase="Running")
     al2, _, _ = make([old])
     assert dict(al2.allocate(req(2)).container_responses[0].envs)[const.ENV_RESOURCE_INDEX] == "-1"
+
+
+def test_ledger_dir_mount_and_env():
+    from aliyun_gpushare_device_plugin_amd.quota import ShimConfig
+    al, _, _ = make([mkpod("p", 2, 1, 10)], shim=ShimConfig("/opt/gpushare"), ledger_dir="/var/run/gpushare/ledgers")
+    r = al.allocate(req(2)).container_responses[0]
+    mounts = {m.container_path: (m.host_path, m.read_only) for m in r.mounts}
+    assert mounts[const.LEDGER_CONTAINER_DIR] == ("/var/run/gpushare/ledgers", False)
+    assert mounts[const.SHIM_CONTAINER_DIR] == ("/opt/gpushare", True)
+    assert r.envs[const.ENV_SHIM_LEDGER_DIR] == const.LEDGER_CONTAINER_DIR
+    al2, _, _ = make([mkpod("p", 2, 1, 10)], shim=ShimConfig("/opt/gpushare"))
+    assert const.ENV_SHIM_LEDGER_DIR not in al2.allocate(req(2)).container_responses[0].envs

@@ -171,3 +171,32 @@ def test_shim_under_sanitizers(stub, tmp_path, san):
         assert out[1]["err"] == 2 and out[2]["err"] == 0 and out[-1]["used"] == 0
     finally:
         cleanup(name)
+
+
+def test_file_backed_ledger_is_readable_by_the_plugin(stub, native_shim, tmp_path):
+    """GPUSHARE_LEDGER_DIR: the ledger is a file the node agent reads (used / peak / denials)."""
+    from aliyun_gpushare_device_plugin_amd.quota import ledger as L, ledger_name
+    from aliyun_gpushare_device_plugin_amd.utils.metrics import PluginMetrics
+    uid = "0b6f1c2e-aaaa-bbbb-cccc-0123456789ab"
+    name = ledger_name(uid, 0)
+    d, drv = stub
+    env = dict(os.environ, LD_PRELOAD=native_shim, LD_LIBRARY_PATH=str(d), GPUSHARE_LEDGER=name,
+               GPUSHARE_LEDGER_DIR=str(tmp_path), GPUSHARE_QUOTA_BYTES=str(4 * GIB))
+    holder = subprocess.Popen([str(drv), "alloc", str(3 * GIB), "alloc", str(2 * GIB), "sleep", "3"], env=env,
+                              stdout=subprocess.PIPE, text=True)
+    try:
+        assert json.loads(holder.stdout.readline())["err"] == 0
+        assert json.loads(holder.stdout.readline())["err"] == 2          # denied: 3 + 2 > 4 GiB
+        st = L.read(str(tmp_path / (name.lstrip("/") + L.SUFFIX)))
+        assert st is not None and st.pod_uid_key == L.uid_key(uid) and st.container_slot == 0
+        assert (st.used, st.quota, st.peak, st.denied, st.processes) == (3 * GIB, 4 * GIB, 3 * GIB, 1, 1)
+        m = PluginMetrics()
+        L.collect(str(tmp_path), m, live_uids={uid})
+        text = m.registry.render()
+        assert f'gpushare_container_hbm_used_bytes{{container="0",pod_uid="{L.uid_key(uid)}"}} {float(3 * GIB)}' in text
+        assert "gpushare_container_quota_denials" in text
+    finally:
+        holder.wait(timeout=10)
+    # process gone and pod gone -> the collector removes the ledger
+    L.collect(str(tmp_path), PluginMetrics(), live_uids=set())
+    assert not list(tmp_path.glob("*.ledger"))
