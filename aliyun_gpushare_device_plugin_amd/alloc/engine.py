@@ -50,6 +50,7 @@ from ..quota import ShimConfig, ledger_name
 from ..utils import log
 from ..utils.metrics import PluginMetrics
 from . import annotations as A
+from .journal import AllocJournal
 
 
 class AllocationError(Exception):
@@ -70,6 +71,9 @@ class AllocatorOptions:
     # host directory for file-backed shim ledgers (mounted read-write into every shared
     # container at const.LEDGER_CONTAINER_DIR); None = pod-private POSIX shm ledgers
     ledger_dir: str | None = None
+    # allocation journal (alloc/journal.py): in memory always, persisted when a path is given
+    journal_path: str | None = None
+    journal_ttl_s: float = 120.0
     # Write-behind ASSIGNED=true PATCH: Allocate answers after the in-memory claim and a
     # background patcher lands the annotation (retrying); the claim blocks re-matching until it
     # has. False = the reference's synchronous PATCH inside Allocate (allocate.go:132-152).
@@ -97,6 +101,7 @@ class Allocator:
         self._assigned: dict[str, float] = {}     # uid -> time we assigned it (stale-cache guard)
         self._unpatched: set[str] = set()         # assigned locally, PATCH not yet acknowledged
         self._patch_q = None
+        self.journal = AllocJournal(self.opts.journal_path, self.opts.journal_ttl_s)
         if self.opts.async_patch:
             import queue
             self._patch_q = queue.Queue()
@@ -226,6 +231,10 @@ class Allocator:
         pod_units = sum(len(c.devices_ids) for c in req.container_requests)
         log.info("----Allocating GPU for gpu mem is started---- RequestPodGPUs: %d", pod_units)
         hist = self.metrics.allocate_latency
+        replay = self._replay(req)
+        if replay is not None:
+            hist.observe(time.perf_counter() - t0, phase="total")
+            return replay
         try:
             with self._mu:
                 claim, complete = self._match(pod_units, fresh=False)
@@ -286,6 +295,7 @@ class Allocator:
                 self._assigned[claim.uid] = time.monotonic()
                 self._unpatched.add(claim.uid)
             self._patch_q.put(claim.pod)
+            self.journal.record(req, claim.uid, resp)
             hist.observe(time.perf_counter() - t3, phase="patch")
             hist.observe(time.perf_counter() - t0, phase="total")
             self.metrics.allocate_outcomes.inc(outcome="assigned")
@@ -305,12 +315,35 @@ class Allocator:
             self._assigned[claim.uid] = time.monotonic()
         if updated:
             self.pods.observe(updated)
+        self.journal.record(req, claim.uid, resp)
         hist.observe(t4 - t3, phase="patch")
         hist.observe(time.perf_counter() - t0, phase="total")
         self.metrics.allocate_outcomes.inc(outcome="assigned")
         log.info("pod %s, new allocated GPUs info: gpu index %d uuid %s", O.name(claim.pod), idx,
                  self.model.uuid_by_index(idx))
         return resp
+
+    def _replay(self, req):
+        """Idempotent retry: the same fake-ID set for a pod we already assigned that is still
+        Pending on this node gets the journaled answer (see alloc/journal.py)."""
+        if not len(self.journal):
+            return None
+        hit = self.journal.lookup(req)
+        if hit is None:
+            return None
+        uid, resp = hit
+        try:
+            pods = self.pods.node_pods()
+        except Exception:  # noqa: BLE001
+            return None
+        for p in pods:
+            if (O.uid(p) == uid and O.phase(p) == "Pending" and not (p.get("metadata") or {}).get("deletionTimestamp")
+                    and (A.is_assigned_pod(p) or uid in self._assigned)):
+                self.metrics.allocate_outcomes.inc(outcome="replay")
+                log.warning("Allocate retried for pod %s (same device IDs, still Pending): replaying the "
+                            "journaled answer", O.name(p))
+                return resp
+        return None
 
     def _patcher(self):
         """Lands queued ASSIGNED=true patches; retries with backoff until the pod is gone."""

@@ -69,6 +69,9 @@ def build_parser() -> argparse.ArgumentParser:
                    help="host directory for file-backed quota-shim ledgers, mounted into every shared "
                         "container; the plugin exports per-container HBM used/peak/denials from it")
     p.add_argument("--ledger-scan-interval", type=float, default=10.0)
+    p.add_argument("--journal-path", default=None,
+                   help="persist recent Allocate decisions (JSON lines) so a retried admission of an "
+                        "already-assigned, still-Pending pod is answered identically across plugin restarts")
     p.add_argument("--no-swap-completion", action="store_true",
                    help="reference behaviour: fail a pod whose equal-size twin was admitted first "
                         "under its reservation instead of exchanging their GPUs")
@@ -95,7 +98,8 @@ def config_from_args(a) -> PluginConfig:
         preferred_allocation=a.preferred_allocation, export_topology=_bool(a.export_topology),
         rocr_visible=a.rocr_visible_devices, metrics_addr=a.metrics_addr, mps=_bool(a.mps),
         async_patch=not a.sync_patch, complete_swaps=not a.no_swap_completion,
-        partition_aware=a.partition_aware, ledger_dir=a.ledger_dir, ledger_scan_s=a.ledger_scan_interval)
+        partition_aware=a.partition_aware, ledger_dir=a.ledger_dir, ledger_scan_s=a.ledger_scan_interval,
+        journal_path=a.journal_path)
 
 
 def install_shim(dest_dir: str) -> str:

@@ -68,6 +68,7 @@ class PluginConfig:
     partition_aware: bool = True         # divide NPS1-shared HBM among compute partitions
     ledger_dir: str | None = None        # host dir for file-backed shim ledgers (usage metrics)
     ledger_scan_s: float = 10.0
+    journal_path: str | None = None      # persisted allocation journal (alloc/journal.py)
     mps: bool = False                    # accepted for flag compatibility; ignored
 
 
@@ -152,7 +153,8 @@ class SharedGPUManager:
                                                strict=cfg.strict_allocate, expose_devices=cfg.expose_devices,
                                                rocr_visible=cfg.rocr_visible, async_patch=cfg.async_patch,
                                                complete_swaps=cfg.complete_swaps,
-                                               ledger_dir=cfg.ledger_dir if shim else None),
+                                               ledger_dir=cfg.ledger_dir if shim else None,
+                                               journal_path=cfg.journal_path),
                               self.metrics)
         self.model = model
         return DevicePluginServer(model, allocator, self._plugin_socket(), const.RESOURCE_NAME,

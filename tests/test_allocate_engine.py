@@ -1,5 +1,6 @@
 """Allocate engine (component C5) and annotation protocol (C7), without gRPC or HTTP."""
 import concurrent.futures as cf
+import itertools
 import json
 import threading
 import time
@@ -79,9 +80,13 @@ class FakeClient:
         return None
 
 
+_IDS = itertools.count()
+
+
 def req(*sizes):
+    """Like the kubelet: every admission gets fake IDs no other live pod holds."""
     return api.AllocateRequest(container_requests=[
-        api.ContainerAllocateRequest(devices_ids=[f"id-{i}" for i in range(n)]) for n in sizes])
+        api.ContainerAllocateRequest(devices_ids=[f"id-{next(_IDS)}" for _ in range(n)]) for n in sizes])
 
 
 def make(pods, ngpu=2, gib=4, **opts):
@@ -288,3 +293,25 @@ def test_ledger_dir_mount_and_env():
     assert r.envs[const.ENV_SHIM_LEDGER_DIR] == const.LEDGER_CONTAINER_DIR
     al2, _, _ = make([mkpod("p", 2, 1, 10)], shim=ShimConfig("/opt/gpushare"))
     assert const.ENV_SHIM_LEDGER_DIR not in al2.allocate(req(2)).container_responses[0].envs
+
+
+def test_journal_replays_retried_admission(tmp_path):
+    """The kubelet re-sends Allocate for a pod we already assigned (still Pending): same answer,
+    even from a new plugin instance reading the persisted journal; once the pod runs, or the
+    IDs come back for another pod, normal matching applies."""
+    path = str(tmp_path / "journal.jsonl")
+    a, b = mkpod("a", 2, 1, 10), mkpod("b", 2, 0, 20)
+    al, src, _ = make([a, b], journal_path=path)
+    r = req(2)
+    first = dict(al.allocate(r).container_responses[0].envs)
+    assert first[const.ENV_RESOURCE_INDEX] == "1"                       # a (oldest)
+    again = dict(al.allocate(r).container_responses[0].envs)
+    assert again == first and al.metrics.allocate_outcomes.value(outcome="replay") == 1
+    # a new plugin process: journal loaded from disk
+    al2 = Allocator(al.model, src, al.client, "node-a", AllocatorOptions(journal_path=path))
+    assert dict(al2.allocate(r).container_responses[0].envs) == first
+    # pod a started running: the same IDs now belong to a new admission -> b is matched
+    for p in src.pods:
+        if p["metadata"]["name"] == "a":
+            p["status"]["phase"] = "Running"
+    assert dict(al2.allocate(r).container_responses[0].envs)[const.ENV_RESOURCE_INDEX] == "0"

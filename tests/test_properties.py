@@ -60,10 +60,10 @@ def test_allocate_matches_each_pod_once_oldest_first(sizes, reqs):
     model = DeviceModel([gpu(0, 4 << 30), gpu(1, 4 << 30)], const.GIB)
     src = StaticSource(pods)
     al = Allocator(model, src, FakeClient(src), "node-a", AllocatorOptions(complete_swaps=False))
-    taken = set()
+    taken, ids = set(), itertools.count()
     for r in reqs:
-        req = api.AllocateRequest()
-        req.container_requests.add().devices_ids.extend([f"GPU-{0:016x}-_-{j}" for j in range(r)])
+        req = api.AllocateRequest()     # fresh fake IDs per admission, as the kubelet hands out
+        req.container_requests.add().devices_ids.extend([f"GPU-{0:016x}-_-{next(ids)}" for _ in range(r)])
         envs = dict(al.allocate(req).container_responses[0].envs)
         remaining = [p for p in pods if p["metadata"]["name"] not in taken and
                      int(p["spec"]["containers"][0]["resources"]["limits"][const.RESOURCE_NAME]) == r]
