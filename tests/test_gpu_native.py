@@ -122,3 +122,16 @@ def test_granule_matches_hardware():
     g = 2 << 20
     for sz, delta in res.items():
         assert delta == (sz + g - 1) // g * g, (sz, delta)
+
+
+def test_shim_charge_equals_device_consumption():
+    """tools/shim_granule_probe.py: for sizes around the granule, the shim's ledger charge equals
+    the HBM the real runtime consumed, and an over-quota request is refused by the shim
+    (evidence with the rocprofv3 memory-allocation trace: profiles/shim_granule_rocprof.md)."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "shim_granule_probe.py")], capture_output=True,
+                       text=True, timeout=300)
+    out = json.loads(r.stdout)
+    assert r.returncode == 0 and out["consistent"], out
+    assert out["over_quota"]["rc"] == 2 and out["over_quota"]["denied"] == 1
+    assert out["container_view"]["total"] == out["quota"]
