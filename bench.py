@@ -230,20 +230,26 @@ def main():
     players: dict[str, object] = {}
     gemm_flops = 0.0
 
+    arena = None
+
     def sync_players(place):
         """Make this rank's players match the pods resident on its GPU."""
         if not use_gpu:
             return
-        from aliyun_gpushare_device_plugin_amd.models.gemm_player import GemmPlayer
+        from aliyun_gpushare_device_plugin_amd.models.gemm_player import GemmPlayer, HBMArena
 
+        nonlocal arena
+        if arena is None:
+            arena = HBMArena(dev, units)          # the GPU's shareable HBM, mapped once
         mine = dict(place.get(local, []))
         for uid in [u for u in players if u not in mine]:
             players.pop(uid).release()
+            arena.free(uid)
         total = torch.cuda.get_device_properties(dev).total_memory
         for uid, size in mine.items():
             if uid not in players:
                 players[uid] = GemmPlayer(total * size // units, dev, a.gemm, a.gemm, a.gemm,
-                                          seed=hash(uid) & 0xffff)
+                                          seed=hash(uid) & 0xffff, pool=arena.alloc(uid, size))
 
     def step(timed: bool):
         nonlocal gemm_flops

@@ -29,3 +29,24 @@ def test_config2_binpack_on_real_mi355x():
         assert where is None
         _, where, adm = c.run_pod(32)
         assert where is not None and adm.error is None
+
+
+def test_hbm_arena_first_fit_and_player_on_slice():
+    """bench.py's per-GPU arena: disjoint unit ranges, reuse after free, None when fragmented."""
+    import torch
+    from aliyun_gpushare_device_plugin_amd.models.gemm_player import GemmPlayer, HBMArena
+    dev = torch.device("cuda", 0)
+    arena = HBMArena(dev, 288)
+    a = arena.alloc("a", 128)
+    b = arena.alloc("b", 64)
+    assert a.data_ptr() + a.numel() * 2 == b.data_ptr()          # contiguous, disjoint
+    assert arena.alloc("c", 128) is None                          # only 96 units left
+    arena.free("a")
+    c = arena.alloc("c", 96)
+    assert c.data_ptr() == a.data_ptr()                           # first fit reuses the hole
+    p = GemmPlayer(0, dev, 1024, 1024, 1024, pool=b)
+    p.run(3)
+    p.synchronize()
+    ref = p.a.float() @ p.b.float().t()
+    assert (p.c.float() - ref).abs().max().item() < 0.05 * ref.abs().max().item()
+    p.release()
