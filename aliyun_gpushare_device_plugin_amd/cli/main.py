@@ -32,6 +32,8 @@ def build_parser() -> argparse.ArgumentParser:
                    help="source pending pods from the kubelet /pods endpoint")
     p.add_argument("--kubelet-address", default="0.0.0.0")
     p.add_argument("--kubelet-port", type=int, default=10250)
+    p.add_argument("--kubelet-scheme", default="https", choices=("https", "http"),
+                   help="kubelet /pods scheme (http only for the read-only port or tests)")
     p.add_argument("--client-cert", default="")
     p.add_argument("--client-key", default="")
     p.add_argument("--token", default="")
@@ -90,7 +92,8 @@ def config_from_args(a) -> PluginConfig:
         node_name=a.node_name, memory_unit=units.normalize_unit(a.memory_unit), round_policy=a.round_policy,
         homogeneous=not a.heterogeneous, health_check=_bool(a.health_check), health_poll_s=a.health_poll,
         pod_source=a.pod_source, query_kubelet=_bool(a.query_kubelet), kubelet_address=a.kubelet_address,
-        kubelet_port=a.kubelet_port, client_cert=a.client_cert, client_key=a.client_key, token=a.token,
+        kubelet_port=a.kubelet_port, kubelet_scheme=a.kubelet_scheme, client_cert=a.client_cert,
+        client_key=a.client_key, token=a.token,
         timeout=float(a.timeout), smi_backend=a.smi_backend, device_plugin_dir=a.device_plugin_dir,
         kubeconfig=a.kubeconfig, apiserver=a.apiserver,
         gpu_indices=[int(x) for x in a.gpu_indices.split(",") if x.strip()] or None,

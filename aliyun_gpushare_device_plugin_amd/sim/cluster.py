@@ -111,6 +111,8 @@ class SimCluster:
             self.client.create_node(make_node(name))
             pdir = os.path.join(self.workdir, name)
             kl = FakeKubelet(pdir, APIClient(KubeConfig(self.api_url)), name).start()
+            if self.pod_source == "kubelet":
+                kl.serve_pods()
             node = SimNode(name, spec, pdir, kl)
             self.nodes[name] = node
             self._start_plugin(node)
@@ -129,7 +131,13 @@ class SimCluster:
                             apiserver=self.api_url, pod_source=self.pod_source,
                             shim_host_dir=self.shim_host_dir, gpu_indices=self.gpu_indices,
                             health_poll_s=self.health_poll_s, round_policy=self.round_policy,
-                            preferred_allocation=self.preferred_allocation)
+                            preferred_allocation=self.preferred_allocation, **self._kubelet_cfg(node))
+
+    def _kubelet_cfg(self, node: SimNode) -> dict:
+        if self.pod_source != "kubelet":
+            return {}
+        return {"kubelet_address": "127.0.0.1", "kubelet_port": node.kubelet.pods_port, "kubelet_scheme": "http",
+                "token": node.kubelet.pods_token}
 
     def _start_plugin(self, node: SimNode):
         if self.plugin_mode == "process":
@@ -144,6 +152,8 @@ class SimCluster:
                 args += ["--gpu-indices", ",".join(map(str, self.gpu_indices))]
             if self.preferred_allocation:
                 args += ["--preferred-allocation"]
+            for k, v in self._kubelet_cfg(node).items():
+                args += ["--" + k.replace("_", "-"), str(v)]
             args += self.extra_plugin_args
             node.proc = subprocess.Popen(args, env=self._child_env(), stdout=subprocess.DEVNULL, preexec_fn=_die_with_parent,
                                          stderr=open(os.path.join(self.workdir, f"{node.name}.plugin.log"), "w"))

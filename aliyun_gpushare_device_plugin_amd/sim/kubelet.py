@@ -57,6 +57,42 @@ class FakeKubelet:
         self._lock = threading.Lock()
         self._stop = threading.Event()
 
+    # -- read-only /pods endpoint (--pod-source=kubelet / --query-kubelet) ------------------
+    def serve_pods(self, token: str = "sim-kubelet-token") -> int:
+        """The kubelet's ``GET /pods/`` (``client.go:119-134``): this node's pods as a PodList,
+        bearer-token checked. Plain HTTP on 127.0.0.1 (``--kubelet-scheme http``). Returns the port."""
+        import http.server
+        import json as _json
+
+        kl = self
+
+        class H(http.server.BaseHTTPRequestHandler):
+            protocol_version = "HTTP/1.1"
+
+            def log_message(self, *a):
+                pass
+
+            def do_GET(self):
+                if self.headers.get("Authorization") != f"Bearer {token}":
+                    code, body = 401, b'{"message":"Unauthorized"}'
+                elif self.path.rstrip("/") != "/pods":
+                    code, body = 404, b"{}"
+                else:
+                    items, _ = kl.client.list_pods(field_selector=f"spec.nodeName={kl.node}")
+                    code, body = 200, _json.dumps({"kind": "PodList", "apiVersion": "v1", "items": items}).encode()
+                self.send_response(code)
+                self.send_header("Content-Type", "application/json")
+                self.send_header("Content-Length", str(len(body)))
+                self.end_headers()
+                self.wfile.write(body)
+
+        self.pods_token = token
+        self._pods_srv = http.server.ThreadingHTTPServer(("127.0.0.1", 0), H)
+        self._pods_srv.daemon_threads = True
+        threading.Thread(target=self._pods_srv.serve_forever, name="kubelet-pods", daemon=True).start()
+        self.pods_port = self._pods_srv.server_address[1]
+        return self.pods_port
+
     # -- Registration service -------------------------------------------------------------
     def Register(self, request, context):
         self.registrations.append((request.version, request.endpoint, request.resource_name))

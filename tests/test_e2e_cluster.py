@@ -93,12 +93,32 @@ def test_sighup_restarts_plugin():
         assert c.nodes["n"].kubelet.registered.wait(10)
 
 
-@pytest.mark.parametrize("source", ["watch", "list"])
-def test_pod_sources(source):
-    with SimCluster([("n", "fake:2x4G")], pod_source=source) as c:
+@pytest.mark.parametrize("source,mode", [("watch", "thread"), ("list", "thread"), ("kubelet", "thread"),
+                                         ("kubelet", "process")])
+def test_pod_sources(source, mode):
+    """Candidates from the informer, a per-Allocate LIST, or the kubelet's /pods (bearer token,
+    --kubelet-scheme http against the fake kubelet; through the CLI in process mode)."""
+    with SimCluster([("n", "fake:2x4G")], pod_source=source, plugin_mode=mode) as c:
+        gpus = []
         for _ in range(3):
             _, w, adm = c.run_pod(2)
             assert adm.error is None and envs(adm)[const.ENV_RESOURCE_INDEX] != "-1"
+            gpus.append(envs(adm)[const.ENV_RESOURCE_INDEX])
+        assert sorted(gpus) in (["0", "0", "1"], ["0", "1", "1"])
+
+
+def test_stack_dump_on_sigquit(tmp_path, monkeypatch):
+    """SIGQUIT writes every thread's stack to GPUSHARE_DUMP_DIR (coredump.go:10-30)."""
+    monkeypatch.setenv("GPUSHARE_DUMP_DIR", str(tmp_path))
+    with SimCluster([("n", "fake:1x4G")]) as c:
+        c.manager("n").events.put(("signal", signal.SIGQUIT))
+        t = time.time() + 10
+        while not list(tmp_path.glob("gpushare_*.txt")) and time.time() < t:
+            time.sleep(0.05)
+        dumps = list(tmp_path.glob("gpushare_*.txt"))
+        assert dumps and "plugin-n" in dumps[0].read_text()       # the manager thread's stack
+        _, _, adm = c.run_pod(2)                                    # and the plugin keeps serving
+        assert adm.error is None
 
 
 def test_watch_cache_used_instead_of_list():
