@@ -34,9 +34,11 @@ def coredump(path: str | None = None) -> str:
     if path is None:
         path = os.path.join(dump_dir(), "gpushare_" + time.strftime("%Y%m%d%H%M%S") + ".txt")
     os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
-    with open(path, "w") as f:
+    tmp = path + ".partial"          # written in full, then renamed: readers never see half a dump
+    with open(tmp, "w") as f:
         f.write(stack_trace())
         f.write("\n--- faulthandler (native view) ---\n")
         f.flush()
         faulthandler.dump_traceback(file=f, all_threads=True)
+    os.replace(tmp, path)
     return path
