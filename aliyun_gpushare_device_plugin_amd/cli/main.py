@@ -43,7 +43,7 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("-v", "--v", type=int, default=int(os.environ.get("GPUSHARE_V", "0")))
     p.add_argument("--log-json", action="store_true")
     # --- MI355X additions ---
-    p.add_argument("--smi-backend", default="auto", help="auto | rocm_smi | sysfs[:root] | fake:<N>x<SIZE> | fake:<json>")
+    p.add_argument("--smi-backend", default="auto", help="auto | amdsmi | rocm_smi | sysfs[:root] | fake:<N>x<SIZE> | fake:<json>")
     p.add_argument("--round", dest="round_policy", choices=units.ROUND_POLICIES, default="nearest",
                    help="bytes->units rounding (nearest advertises the nominal 288 GiB of an MI355X)")
     p.add_argument("--heterogeneous", action="store_true",

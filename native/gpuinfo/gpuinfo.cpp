@@ -507,6 +507,244 @@ class RocmSmiBackend : public Backend {
   int (*ev_stop_)(uint32_t) = nullptr;
 };
 
+// ---- amdsmi (dlopen) ---------------------------------------------------------------------
+// The newer AMD SMI library (libamd_smi, /opt/rocm/include/amd_smi/amdsmi.h). Handle-based:
+// sockets -> processors; each GPU processor is matched to its sysfs/KFD view by PCI BDF (render
+// minor, KFD node, partitions, name), then SMI values (HBM, NUMA, hive, ECC, links) override.
+// Only the types used are mirrored (amdsmi.h, ROCm 7.2: :51, :287, :668-677, :760-773,
+// :1029-1030, :1336-1341, :1362-1370, :1570, :2090-2098) so the library still builds without ROCm.
+struct amdsmi_xgmi_info {
+  uint8_t xgmi_lanes;
+  uint64_t xgmi_hive_id;
+  uint64_t xgmi_node_id;
+  uint32_t index;
+  uint32_t reserved[9];
+};
+struct amdsmi_error_count {
+  uint64_t correctable_count, uncorrectable_count, deferred_count, reserved[5];
+};
+struct amdsmi_evt_data {
+  void* processor_handle;
+  int32_t event;
+  char message[256];
+};
+
+class AmdSmiBackend : public Backend {
+ public:
+  const char* name() const override { return "amdsmi"; }
+  ~AmdSmiBackend() override {
+    if (lib_) {
+      if (events_on_ && ev_stop_)
+        for (void* h : handles_) ev_stop_(h);
+      if (shut_) shut_();
+      dlclose(lib_);
+    }
+  }
+
+  bool load() {
+    const char* names[] = {"libamd_smi.so", "libamd_smi.so.26", "/opt/rocm/lib/libamd_smi.so"};
+    for (auto nm : names)
+      if ((lib_ = dlopen(nm, RTLD_NOW | RTLD_LOCAL))) break;
+    if (!lib_) {
+      set_err(std::string("dlopen libamd_smi failed: ") + dlerror());
+      return false;
+    }
+#define SYM(var, nm)                                                   \
+  var = reinterpret_cast<decltype(var)>(dlsym(lib_, nm));              \
+  if (!var) {                                                          \
+    set_err(std::string("libamd_smi lacks ") + nm);                    \
+    return false;                                                      \
+  }
+    SYM(init_, "amdsmi_init");
+    SYM(shut_, "amdsmi_shut_down");
+    SYM(sockets_, "amdsmi_get_socket_handles");
+    SYM(procs_, "amdsmi_get_processor_handles");
+    SYM(ptype_, "amdsmi_get_processor_type");
+    SYM(bdf_, "amdsmi_get_gpu_device_bdf");
+    SYM(memtot_, "amdsmi_get_gpu_memory_total");
+#undef SYM
+    memuse_ = reinterpret_cast<decltype(memuse_)>(dlsym(lib_, "amdsmi_get_gpu_memory_usage"));
+    numa_ = reinterpret_cast<decltype(numa_)>(dlsym(lib_, "amdsmi_topo_get_numa_node_number"));
+    linktype_ = reinterpret_cast<decltype(linktype_)>(dlsym(lib_, "amdsmi_topo_get_link_type"));
+    linkw_ = reinterpret_cast<decltype(linkw_)>(dlsym(lib_, "amdsmi_topo_get_link_weight"));
+    xgmi_ = reinterpret_cast<decltype(xgmi_)>(dlsym(lib_, "amdsmi_get_xgmi_info"));
+    ecc_ = reinterpret_cast<decltype(ecc_)>(dlsym(lib_, "amdsmi_get_gpu_total_ecc_count"));
+    cpart_ = reinterpret_cast<decltype(cpart_)>(dlsym(lib_, "amdsmi_get_gpu_compute_partition"));
+    mpart_ = reinterpret_cast<decltype(mpart_)>(dlsym(lib_, "amdsmi_get_gpu_memory_partition"));
+    ev_init_ = reinterpret_cast<decltype(ev_init_)>(dlsym(lib_, "amdsmi_init_gpu_event_notification"));
+    ev_mask_ = reinterpret_cast<decltype(ev_mask_)>(dlsym(lib_, "amdsmi_set_gpu_event_notification_mask"));
+    ev_get_ = reinterpret_cast<decltype(ev_get_)>(dlsym(lib_, "amdsmi_get_gpu_event_notification"));
+    ev_stop_ = reinterpret_cast<decltype(ev_stop_)>(dlsym(lib_, "amdsmi_stop_gpu_event_notification"));
+    int rc = init_(1ull << 1 /*AMDSMI_INIT_AMD_GPUS*/);
+    if (rc != 0) {
+      set_err("amdsmi_init failed with status " + std::to_string(rc));
+      return false;
+    }
+    return true;
+  }
+
+  bool enumerate(std::vector<gs_device_t>* devs, LinkMatrix* links, int* inaccessible) override {
+    // processors of every socket, GPUs only
+    uint32_t ns = 0;
+    if (sockets_(&ns, nullptr) != 0) {
+      set_err("amdsmi_get_socket_handles failed");
+      return false;
+    }
+    std::vector<void*> socks(ns);
+    if (ns && sockets_(&ns, socks.data()) != 0) {
+      set_err("amdsmi_get_socket_handles failed");
+      return false;
+    }
+    std::vector<void*> gpus;
+    for (void* sk : socks) {
+      uint32_t np = 0;
+      if (procs_(sk, &np, nullptr) != 0 || !np) continue;
+      std::vector<void*> ps(np);
+      if (procs_(sk, &np, ps.data()) != 0) continue;
+      for (void* p : ps) {
+        int32_t t = 0;
+        if (ptype_(p, &t) == 0 && t == 1 /*AMDSMI_PROCESSOR_TYPE_AMD_GPU*/) gpus.push_back(p);
+      }
+    }
+    // sysfs detail keyed by BDF; its order (KFD / HIP ordinal order) decides device indices
+    SysfsBackend sysfs("");
+    std::vector<gs_device_t> sdevs;
+    LinkMatrix slinks;
+    int sinacc = 0;
+    std::map<std::string, gs_device_t> by_bdf;
+    *inaccessible = 0;
+    if (sysfs.enumerate(&sdevs, &slinks, &sinacc)) {
+      for (auto& d : sdevs) by_bdf[d.bdf] = d;
+      *inaccessible = sinacc;
+    }
+    struct Entry {
+      gs_device_t d;
+      void* h;
+      int order;
+    };
+    std::vector<Entry> es;
+    for (size_t k = 0; k < gpus.size(); ++k) {
+      void* h = gpus[k];
+      gs_device_t d{};
+      d.kfd_node = d.render_minor = d.numa_node = -1;
+      d.health = GS_HEALTHY;
+      uint64_t b = 0;
+      char bdf[32] = {0};
+      if (bdf_(h, &b) == 0)
+        snprintf(bdf, sizeof bdf, "%04llx:%02llx:%02llx.%llx", (unsigned long long)(b >> 16),
+                 (unsigned long long)((b >> 8) & 0xff), (unsigned long long)((b >> 3) & 0x1f),
+                 (unsigned long long)(b & 0x7));
+      int order = 1000 + (int)k;
+      auto it = by_bdf.find(bdf);
+      if (it != by_bdf.end()) {
+        d = it->second;
+        order = it->second.index;
+      } else {
+        copy_str(d.name, "AMD Instinct GPU");
+      }
+      copy_str(d.bdf, bdf);
+      uint64_t v = 0;
+      if (memtot_(h, 0 /*AMDSMI_MEM_TYPE_VRAM*/, &v) == 0) d.vram_total = v;
+      if (memuse_ && memuse_(h, 0, &v) == 0) d.vram_used = v;
+      uint32_t numa = 0;
+      if (numa_ && numa_(h, &numa) == 0) d.numa_node = (int32_t)numa;
+      amdsmi_xgmi_info xi{};
+      if (xgmi_ && xgmi_(h, &xi) == 0) d.hive_id = xi.xgmi_hive_id;
+      amdsmi_error_count ec{};
+      if (ecc_ && ecc_(h, &ec) == 0) {
+        d.ecc_ue = ec.uncorrectable_count;
+        d.ecc_ce = ec.correctable_count;
+      }
+      char part[32] = {0};
+      if (cpart_ && cpart_(h, part, sizeof part) == 0 && partition_count(part) > 0)
+        d.compute_partition = partition_count(part);
+      if (mpart_ && mpart_(h, part, sizeof part) == 0 && partition_count(part) > 0)
+        d.memory_partition = partition_count(part);
+      if (!d.uuid[0]) copy_str(d.uuid, uuid_from_unique(d.unique_id));
+      es.push_back({d, h, order});
+    }
+    std::stable_sort(es.begin(), es.end(), [](const Entry& a, const Entry& b) { return a.order < b.order; });
+    devs->clear();
+    handles_.clear();
+    for (size_t i = 0; i < es.size(); ++i) {
+      es[i].d.index = (int32_t)i;
+      devs->push_back(es[i].d);
+      handles_.push_back(es[i].h);
+    }
+    int n = (int)es.size();
+    links->resize(n);
+    for (int i = 0; i < n; ++i)
+      for (int j = 0; j < n; ++j) {
+        if (i == j) continue;
+        gs_link_t L{GS_LINK_PCIE, 3, 40, 0, 0};
+        uint64_t hops = 0, w = 0;
+        int32_t t = 0;
+        if (linktype_ && linktype_(handles_[i], handles_[j], &hops, &t) == 0) {
+          L.type = (t == 2 /*AMDSMI_LINK_TYPE_XGMI*/) ? GS_LINK_XGMI : GS_LINK_PCIE;
+          L.hops = (int32_t)hops;
+        }
+        if (linkw_ && linkw_(handles_[i], handles_[j], &w) == 0) L.weight = (int32_t)w;
+        if (L.type == GS_LINK_XGMI && i < slinks.n && j < slinks.n)
+          L.max_bandwidth_mbps = slinks.at(i, j).max_bandwidth_mbps;
+        links->at(i, j) = L;
+      }
+    return true;
+  }
+
+  bool events_start(const std::vector<gs_device_t>&) override {
+    if (!ev_init_ || !ev_mask_ || !ev_get_) return true;  // polling only
+    uint64_t mask = (1ull << 0) | (1ull << 1) | (1ull << 2) | (1ull << 3);  // events 1..4, bit = event - 1
+    bool any = false;
+    for (void* h : handles_)
+      if (ev_init_(h) == 0 && ev_mask_(h, mask) == 0) any = true;
+    events_on_ = any;
+    return true;
+  }
+
+  int wait_event(int timeout_ms, gs_event_t* ev) override {
+    if (!events_on_) return Backend::wait_event(timeout_ms, ev);
+    amdsmi_evt_data data[1];
+    uint32_t num = 1;
+    if (ev_get_(timeout_ms, &num, data) != 0 || num == 0) return 0;
+    ev->index = -1;
+    for (size_t i = 0; i < handles_.size(); ++i)
+      if (handles_[i] == data[0].processor_handle) ev->index = (int32_t)i;
+    switch (data[0].event) {
+      case 1: ev->kind = GS_EV_VMFAULT; break;
+      case 2: ev->kind = GS_EV_THERMAL; break;
+      case 3: ev->kind = GS_EV_PRE_RESET; break;
+      case 4: ev->kind = GS_EV_POST_RESET; break;
+      default: ev->kind = GS_EV_NONE; break;
+    }
+    copy_str(ev->message, std::string(data[0].message, strnlen(data[0].message, sizeof data[0].message)));
+    return 1;
+  }
+
+ private:
+  void* lib_ = nullptr;
+  std::vector<void*> handles_;
+  bool events_on_ = false;
+  int (*init_)(uint64_t) = nullptr;
+  int (*shut_)() = nullptr;
+  int (*sockets_)(uint32_t*, void**) = nullptr;
+  int (*procs_)(void*, uint32_t*, void**) = nullptr;
+  int (*ptype_)(void*, int32_t*) = nullptr;
+  int (*bdf_)(void*, uint64_t*) = nullptr;
+  int (*memtot_)(void*, int, uint64_t*) = nullptr;
+  int (*memuse_)(void*, int, uint64_t*) = nullptr;
+  int (*numa_)(void*, uint32_t*) = nullptr;
+  int (*linktype_)(void*, void*, uint64_t*, int32_t*) = nullptr;
+  int (*linkw_)(void*, void*, uint64_t*) = nullptr;
+  int (*xgmi_)(void*, amdsmi_xgmi_info*) = nullptr;
+  int (*ecc_)(void*, amdsmi_error_count*) = nullptr;
+  int (*cpart_)(void*, char*, uint32_t) = nullptr;
+  int (*mpart_)(void*, char*, uint32_t) = nullptr;
+  int (*ev_init_)(void*) = nullptr;
+  int (*ev_mask_)(void*, uint64_t) = nullptr;
+  int (*ev_get_)(int, uint32_t*, amdsmi_evt_data*) = nullptr;
+  int (*ev_stop_)(void*) = nullptr;
+};
+
 // ---- fake (tests, simulation, fault injection) -------------------------------------------
 class FakeBackend : public Backend {
  public:
@@ -752,6 +990,11 @@ int gs_open(const char* spec_c, gs_handle** out) {
   } else if (spec == "sysfs" || spec.compare(0, 6, "sysfs:") == 0) {
     be = std::make_unique<SysfsBackend>(spec.size() > 6 ? spec.substr(6) : "");
     nm = "sysfs";
+  } else if (spec == "amdsmi") {
+    auto a = std::make_unique<AmdSmiBackend>();
+    if (!a->load()) return -1;
+    be = std::move(a);
+    nm = "amdsmi";
   } else if (spec == "rocm_smi" || spec == "auto") {
     auto r = std::make_unique<RocmSmiBackend>();
     if (r->load()) {

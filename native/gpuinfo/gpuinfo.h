@@ -2,6 +2,7 @@
 //
 // Replaces the reference's NVML binding (go-nvml via cgo: pkg/gpu/nvidia/nvidia.go:17-86,
 // gpumanager.go:36-41) and its dead XID watcher (nvidia.go:97-153) with an AMD-native C ABI:
+//   * "amdsmi"    — libamd_smi (dlopen'ed at runtime), matched to sysfs by PCI BDF;
 //   * "rocm_smi"  — librocm_smi64 (dlopen'ed at runtime, so the library builds and loads on
 //                    hosts without ROCm), enriched from amdgpu/KFD sysfs;
 //   * "sysfs[:<root>]" — /sys/class/kfd topology + /sys/class/drm (root prefix for tests);

@@ -28,11 +28,21 @@ def test_enumerates_mi355x(backend):
         assert os.path.exists(f"/dev/dri/renderD{g.render_minor}")
 
 
-def test_backends_agree():
-    with S.SMI("rocm_smi") as a, S.SMI("sysfs") as b:
+@pytest.mark.parametrize("backend", ["rocm_smi", "amdsmi"])
+def test_backends_agree(backend):
+    """rocm_smi and amdsmi enumerate the same GPUs, in the same (HIP ordinal) order, with the same
+    HBM bytes, BDF, render node and link types as the sysfs/KFD view."""
+    with S.SMI(backend) as a, S.SMI("sysfs") as b:
+        assert a.backend == backend
         da, db = a.devices(), b.devices()
         assert [d.uuid for d in da] == [d.uuid for d in db]
         assert [d.vram_total for d in da] == [d.vram_total for d in db]
+        assert [(d.bdf, d.render_minor) for d in da] == [(d.bdf, d.render_minor) for d in db]
+        n = len(da)
+        assert [[a.link(i, j).type for j in range(n)] for i in range(n)] == \
+               [[b.link(i, j).type for j in range(n)] for i in range(n)]
+        a.events_start()
+        assert a.wait_event(50) is None or a.wait_event(50).kind >= 0
 
 
 def test_advertised_units_mi355x():
