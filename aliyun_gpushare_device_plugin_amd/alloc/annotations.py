@@ -71,11 +71,12 @@ def dedupe_by_uid(pods: list[dict], node: str) -> list[dict]:
     """``getPendingPodsInNode`` (``podmanager.go:273-291``): drop other nodes' pods, dedupe."""
     seen, out = set(), []
     for p in pods:
-        if O.node_name(p) != node:
+        md = p.get("metadata") or {}
+        if (p.get("spec") or {}).get("nodeName") != node:
             log.warning("Pod %s in ns %s is not assigned to node %s as expected, it's placed on node %s",
-                        O.name(p), O.namespace(p), node, O.node_name(p))
+                        md.get("name"), md.get("namespace"), node, O.node_name(p))
             continue
-        u = O.uid(p)
+        u = md.get("uid")
         if u in seen:
             continue
         seen.add(u)

@@ -50,7 +50,7 @@ from ..quota import ShimConfig, ledger_name
 from ..utils import log
 from ..utils.metrics import PluginMetrics
 from . import annotations as A
-from .journal import AllocJournal
+from .journal import AllocJournal, request_key
 
 
 class AllocationError(Exception):
@@ -100,6 +100,7 @@ class Allocator:
         self._claims: dict[str, _Claim] = {}      # in-flight (multi-container or PATCH pending)
         self._assigned: dict[str, float] = {}     # uid -> time we assigned it (stale-cache guard)
         self._unpatched: set[str] = set()         # assigned locally, PATCH not yet acknowledged
+        self._pinfo: dict[tuple, tuple] = {}      # memoised per-pod-version facts (see _info)
         self._patch_q = None
         self.journal = AllocJournal(self.opts.journal_path, self.opts.journal_ttl_s)
         if self.opts.async_patch:
@@ -110,18 +111,38 @@ class Allocator:
     # ------------------------------------------------------------------------------------
     # candidate selection
     # ------------------------------------------------------------------------------------
+    def _info(self, p: dict) -> tuple[bool, int, int]:
+        """(assumed, pod gpu-mem, assume time) of one pod version, memoised: every Allocate scans
+        all Pending pods, and re-parsing their specs dominated the handler. The
+        key carries the two annotations the plugin itself rewrites, so an object updated in
+        place (no new resourceVersion) is never served stale."""
+        ann = O.annotations(p)
+        k = (O.uid(p), O.resource_version(p), ann.get(const.ENV_ASSIGNED_FLAG),
+             ann.get(const.ENV_RESOURCE_ASSUME_TIME))
+        v = self._pinfo.get(k)
+        if v is None:
+            v = (A.is_assumed_pod(p), O.gpu_mem_of_pod(p), A.assume_time(p))
+            if len(self._pinfo) > 8192:
+                self._pinfo.clear()
+            self._pinfo[k] = v
+        return v
+
     def _candidates(self, fresh: bool) -> list[dict]:
         pods = A.dedupe_by_uid(self.pods.pending_pods(fresh=fresh), self.node)
         now = time.monotonic()
         for u, t in list(self._assigned.items()):
             if now - t > self.opts.claim_ttl_s and u not in self._unpatched:
                 del self._assigned[u]
-        out = [p for p in pods if A.is_assumed_pod(p) and O.uid(p) not in self._assigned]
+        out = []
+        for p in pods:
+            assumed, _, at = self._info(p)
+            if assumed and O.uid(p) not in self._assigned:
+                out.append((at, len(out), p))
+        out.sort(key=lambda e: (e[0], e[1]))      # assume time, then arrival order (stable)
         if log.V(4):
-            for p in out:
-                log.info("candidate pod %s in ns %s with timestamp %d is found.", O.name(p), O.namespace(p),
-                         A.assume_time(p))
-        return A.order_by_assume_time(out)
+            for at, _, p in out:
+                log.info("candidate pod %s in ns %s with timestamp %d is found.", O.name(p), O.namespace(p), at)
+        return [p for _, _, p in out]
 
     def _match(self, req_units: int, fresh: bool) -> tuple[_Claim | None, bool]:
         """Returns (claim, complete). ``complete`` = every gpu container of the pod is now
@@ -136,7 +157,7 @@ class Allocator:
         cands = [p for p in self._candidates(fresh) if O.uid(p) not in self._claims]
         # 2) the reference rule: pod-total equals the request
         for p in cands:
-            if O.gpu_mem_of_pod(p) == req_units:
+            if self._info(p)[1] == req_units:
                 gc = [i for i, v in enumerate(O.gpu_mem_per_container(p)) if v > 0]
                 c = _Claim(O.uid(p), p, A.gpu_id_from_annotation(p), len(gc), gc, time.monotonic())
                 return c, True
@@ -231,7 +252,8 @@ class Allocator:
         pod_units = sum(len(c.devices_ids) for c in req.container_requests)
         log.info("----Allocating GPU for gpu mem is started---- RequestPodGPUs: %d", pod_units)
         hist = self.metrics.allocate_latency
-        replay = self._replay(req)
+        jkey = request_key(req)
+        replay = self._replay(req, jkey)
         if replay is not None:
             hist.observe(time.perf_counter() - t0, phase="total")
             return replay
@@ -295,7 +317,7 @@ class Allocator:
                 self._assigned[claim.uid] = time.monotonic()
                 self._unpatched.add(claim.uid)
             self._patch_q.put(claim.pod)
-            self.journal.record(req, claim.uid, resp)
+            self.journal.record(req, claim.uid, resp, jkey)
             hist.observe(time.perf_counter() - t3, phase="patch")
             hist.observe(time.perf_counter() - t0, phase="total")
             self.metrics.allocate_outcomes.inc(outcome="assigned")
@@ -315,7 +337,7 @@ class Allocator:
             self._assigned[claim.uid] = time.monotonic()
         if updated:
             self.pods.observe(updated)
-        self.journal.record(req, claim.uid, resp)
+        self.journal.record(req, claim.uid, resp, jkey)
         hist.observe(t4 - t3, phase="patch")
         hist.observe(time.perf_counter() - t0, phase="total")
         self.metrics.allocate_outcomes.inc(outcome="assigned")
@@ -323,12 +345,12 @@ class Allocator:
                  self.model.uuid_by_index(idx))
         return resp
 
-    def _replay(self, req):
+    def _replay(self, req, key: str):
         """Idempotent retry: the same fake-ID set for a pod we already assigned that is still
         Pending on this node gets the journaled answer (see alloc/journal.py)."""
         if not len(self.journal):
             return None
-        hit = self.journal.lookup(req)
+        hit = self.journal.lookup(req, key)
         if hit is None:
             return None
         uid, resp = hit

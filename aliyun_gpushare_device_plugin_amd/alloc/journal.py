@@ -25,8 +25,8 @@ from ..utils import log
 
 
 def request_key(req) -> str:
-    ids = [sorted(c.devices_ids) for c in req.container_requests]
-    return hashlib.sha1(json.dumps(ids).encode()).hexdigest()
+    body = "\x1e".join("\x1f".join(sorted(c.devices_ids)) for c in req.container_requests)
+    return hashlib.sha1(body.encode()).hexdigest()
 
 
 class AllocJournal:
@@ -75,8 +75,8 @@ class AllocJournal:
         self._lines = len(self._mem)
 
     # -- API --------------------------------------------------------------------------------
-    def record(self, req, pod_uid: str, resp) -> None:
-        key, t, blob = request_key(req), time.time(), resp.SerializeToString()
+    def record(self, req, pod_uid: str, resp, key: str | None = None) -> None:
+        key, t, blob = key or request_key(req), time.time(), resp.SerializeToString()
         with self._lock:
             self._mem[key] = (pod_uid, t, blob)
             self._mem.move_to_end(key)
@@ -88,8 +88,8 @@ class AllocJournal:
                 except OSError as e:
                     log.warning("allocation journal write failed: %s", e)
 
-    def lookup(self, req) -> tuple[str, object] | None:
-        key = request_key(req)
+    def lookup(self, req, key: str | None = None) -> tuple[str, object] | None:
+        key = key or request_key(req)
         with self._lock:
             hit = self._mem.get(key)
         if hit is None or time.time() - hit[1] > self.ttl_s:

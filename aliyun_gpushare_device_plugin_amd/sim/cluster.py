@@ -100,6 +100,7 @@ class SimCluster:
     @staticmethod
     def _child_env():
         env = dict(os.environ)
+        env.setdefault("GPUSHARE_DEBUG", "1")      # simulator children: debug endpoints on
         env["PYTHONPATH"] = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))) + \
             os.pathsep + env.get("PYTHONPATH", "")
         return env

@@ -103,6 +103,20 @@ class Histogram:
     def count(self, **labels) -> int:
         return sum(self._counts.get(_labels_key(labels), []))
 
+    def summary(self, qs=(0.5, 0.9, 0.99)) -> list[dict]:
+        """Exact quantiles from the reservoir, one entry per label set."""
+        with self._lock:
+            items = [(k, sorted(v)) for k, v in self._samples.items()]
+        out = []
+        for k, s in items:
+            if not s:
+                continue
+            d = {"labels": dict(k), "count": len(s)}
+            for q in qs:
+                d[f"p{int(q * 100)}"] = s[min(len(s) - 1, max(0, int(round(q * (len(s) - 1)))))]
+            out.append(d)
+        return out
+
     def reset(self):
         with self._lock:
             self._counts.clear()
@@ -136,6 +150,10 @@ class Registry:
 
     def counter(self, name, help_=""):
         return self._get(Counter, name, help_)
+
+    def histograms(self) -> dict:
+        with self._lock:
+            return {n: m for n, m in self._m.items() if isinstance(m, Histogram)}
 
     def gauge(self, name, help_=""):
         return self._get(Gauge, name, help_)
@@ -173,13 +191,26 @@ class PluginMetrics:
 
 
 def serve(registry: Registry, addr: str, health_fn=None) -> http.server.ThreadingHTTPServer:
-    """Start ``/metrics`` + ``/healthz`` on ``host:port`` in a daemon thread."""
+    """Start ``/metrics`` + ``/healthz`` + ``/debug/latency`` on ``host:port`` in a daemon thread.
+
+    ``/debug/latency`` returns exact p50/p90/p99 of every histogram (JSON); ``?reset=1`` also
+    clears them, honoured only with ``GPUSHARE_DEBUG=1`` (benchmarks bracket a timed region)."""
+    import json as _json
+    import os as _os
+
     host, _, port = addr.rpartition(":")
 
     class H(http.server.BaseHTTPRequestHandler):
         def do_GET(self):
             if self.path.startswith("/metrics"):
                 body, ctype, code = registry.render().encode(), "text/plain; version=0.0.4", 200
+            elif self.path.startswith("/debug/latency"):
+                hs = registry.histograms()
+                body = _json.dumps({n: h.summary() for n, h in hs.items()}).encode()
+                ctype, code = "application/json", 200
+                if "reset=1" in self.path and _os.environ.get("GPUSHARE_DEBUG") == "1":
+                    for h in hs.values():
+                        h.reset()
             elif self.path.startswith("/healthz"):
                 ok = True if health_fn is None else bool(health_fn())
                 body, ctype, code = (b"ok" if ok else b"unhealthy"), "text/plain", 200 if ok else 503

@@ -60,6 +60,8 @@ def parse_quantity(q) -> int:
         raise ValueError("bad quantity")
     if isinstance(q, (int, float)):
         return int(-(-q // 1))
+    if isinstance(q, str) and q.isdigit():      # the common case for extended resources: "64"
+        return int(q)
     s = str(q).strip()
     if not s:
         return 0

@@ -66,8 +66,15 @@ class ControlPlane:
         from aliyun_gpushare_device_plugin_amd.sim.cluster import SimCluster
 
         self.n = n_gpus
+        import socket
+
+        with socket.socket() as s:              # a free port for the plugin's metrics endpoint
+            s.bind(("127.0.0.1", 0))
+            self.metrics_port = s.getsockname()[1]
+        extra = ["--metrics-addr", f"127.0.0.1:{self.metrics_port}"] if plugin_mode == "process" else []
         self.cluster = SimCluster([("mi355x-node", smi_spec)], plugin_mode=plugin_mode, pod_source=pod_source,
-                                  apiserver="process", gpu_indices=list(range(n_gpus)), health_poll_s=5.0)
+                                  apiserver="process", gpu_indices=list(range(n_gpus)), health_poll_s=5.0,
+                                  extra_plugin_args=extra)
         self.cluster.start()
         from aliyun_gpushare_device_plugin_amd import const
         from aliyun_gpushare_device_plugin_amd.cluster import objects as O
@@ -170,6 +177,21 @@ class ControlPlane:
             self.alloc_lat.extend(adm.latencies)
             self.admit_lat.append(dt)
             self.resident[gpu].append((bpod, size))
+
+    def plugin_latency(self, reset: bool = False) -> dict | None:
+        """The plugin's own (server-side) Allocate latency quantiles from its metrics endpoint."""
+        import urllib.request
+
+        try:
+            url = f"http://127.0.0.1:{self.metrics_port}/debug/latency" + ("?reset=1" if reset else "")
+            with urllib.request.urlopen(url, timeout=5) as r:
+                d = json.loads(r.read())
+        except Exception:  # noqa: BLE001 - thread mode or endpoint unavailable
+            return None
+        for e in d.get("gpushare_allocate_latency_seconds", []):
+            if e["labels"].get("phase") == "total":
+                return e
+        return None
 
     def placement(self) -> dict:
         from aliyun_gpushare_device_plugin_amd.cluster import objects as O
@@ -283,6 +305,7 @@ def main():
         cp.admit_lat.clear()
         cp.failed = 0
         cp.fail_reasons.clear()
+        cp.plugin_latency(reset=True)
 
     barrier()
     t0 = time.perf_counter()
@@ -298,6 +321,7 @@ def main():
         elapsed, gemm_flops = float(mx[0]), float(t[1])
 
     if rank == 0:
+        srv = cp.plugin_latency()
         pods_node = sum(len(v) for v in cp.resident.values())
         gib_node = sum(s for v in cp.resident.values() for _, s in v)
         admissions = a.steps * n - cp.failed
@@ -322,6 +346,8 @@ def main():
             "allocate_p50_ms": round(pct(cp.alloc_lat, 0.5) * 1e3, 3) if cp.alloc_lat else None,
             "allocate_p99_ms": round(pct(cp.alloc_lat, 0.99) * 1e3, 3) if cp.alloc_lat else None,
             "admission_p50_ms": round(pct(cp.admit_lat, 0.5) * 1e3, 3) if cp.admit_lat else None,
+            "plugin_allocate_p50_ms": round(srv["p50"] * 1e3, 3) if srv else None,
+            "plugin_allocate_p99_ms": round(srv["p99"] * 1e3, 3) if srv else None,
             "control_plane_ms_per_step": round(cp.cp_time / a.steps * 1e3, 3),
             "pods_per_node": pods_node,
             "hbm_gib_per_node": gib_node,
