@@ -16,6 +16,11 @@ EP_BIAS, EP_SILU, EP_RESID = 1, 2, 4
 GEMM_AUTO, GEMM_V1, GEMM_PINGPONG = 0, 1, 2
 
 
+def set_gemm_group_m(g: int) -> None:
+    """Tile-rasterisation group height (rows of tiles sharing an XCD's L2 walk); 0 = default."""
+    _lib.check(_lib.lib().gs_gemm_set_group_m(int(g)), "gs_gemm_set_group_m")
+
+
 def set_gemm_variant(v: int) -> None:
     """Kernel selection (A/B measurement, tests): ``GEMM_AUTO`` = ping-pong 8-phase kernel for
     M%256 == N%256 == K%128 == 0, the 2-stage kernel otherwise; ``GEMM_V1`` forces the latter."""

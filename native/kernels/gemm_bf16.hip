@@ -52,9 +52,10 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_nt_256(
   const int bid = blockIdx.x;
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  const int per_group = GROUP_M * nbn;
-  const int first_m = (wgid / per_group) * GROUP_M;
-  const int gsz = min(nbm - first_m, GROUP_M);
+  const int gm = (flags >> 8) & 0xff ? (flags >> 8) & 0xff : GROUP_M;   // rasterisation group (rows)
+  const int per_group = gm * nbn;
+  const int first_m = (wgid / per_group) * gm;
+  const int gsz = min(nbm - first_m, gm);
   const int tm = first_m + (wgid % per_group) % gsz;
   const int tn = (wgid % per_group) / gsz;
   const int m0 = tm * BM, n0 = tn * BN;
@@ -239,9 +240,10 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_nt_256_pp(
   const int bid = blockIdx.x;
   const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int per_group = GROUP_M * nbn;
-  const int first_m = (wgid / per_group) * GROUP_M;
-  const int gsz = min(nbm - first_m, GROUP_M);
+  const int gm = (flags >> 8) & 0xff ? (flags >> 8) & 0xff : GROUP_M;   // rasterisation group (rows)
+  const int per_group = gm * nbn;
+  const int first_m = (wgid / per_group) * gm;
+  const int gsz = min(nbm - first_m, gm);
   const int tm = first_m + (wgid % per_group) % gsz;
   const int tn = (wgid % per_group) / gsz;
   const int m0 = tm * BM, n0 = tn * BN;
@@ -425,9 +427,10 @@ __global__ __launch_bounds__(W4_THREADS, 1) void gemm_bf16_nt_256_w4(
   const int bid = blockIdx.x;
   const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int per_group = GROUP_M * nbn;
-  const int first_m = (wgid / per_group) * GROUP_M;
-  const int gsz = min(nbm - first_m, GROUP_M);
+  const int gm = (flags >> 8) & 0xff ? (flags >> 8) & 0xff : GROUP_M;   // rasterisation group (rows)
+  const int per_group = gm * nbn;
+  const int first_m = (wgid / per_group) * gm;
+  const int gsz = min(nbm - first_m, gm);
   const int tm = first_m + (wgid % per_group) % gsz;
   const int tn = (wgid % per_group) / gsz;
   const int m0 = tm * BM, n0 = tn * BN;
@@ -534,6 +537,7 @@ __global__ __launch_bounds__(W4_THREADS, 1) void gemm_bf16_nt_256_w4(
   }
 }
 
+int g_group_m = 0;   // 0 = GROUP_M; else tile-rasterisation group height (passed in flags bits 8..15)
 int g_variant = 0;   // 0 = auto, 1 = v1 (2-stage, 8 waves), 2 = v2 (ping-pong), 3 = v3 (4 waves)
 //   // 0 = auto (v2 when aligned), 1 = force v1, 2 = v2 when aligned
 
@@ -545,6 +549,7 @@ GS_KERNEL_API int gs_gemm_bf16_nt(const void* A, const void* B, void* C, const v
       ldc < N || ((uintptr_t)A & 15) || ((uintptr_t)B & 15) || ((uintptr_t)C & 7))
     return GS_EINVAL;
   if ((flags & EP_BIAS) && !bias) return GS_EINVAL;
+  flags = (flags & 0xff) | (g_group_m << 8);
   if ((flags & EP_RESID) && !R) return GS_EINVAL;
   static bool attr_set = false;
   if (!attr_set) {
@@ -580,5 +585,12 @@ GS_KERNEL_API int gs_gemm_bf16_nt(const void* A, const void* B, void* C, const v
 GS_KERNEL_API int gs_gemm_set_variant(int v) {
   if (v < 0 || v > 3) return GS_EINVAL;
   g_variant = v;
+  return GS_OK;
+}
+
+// Tile-rasterisation group height (1..255; 0 = default 8) for tuning sweeps.
+GS_KERNEL_API int gs_gemm_set_group_m(int g) {
+  if (g < 0 || g > 255) return GS_EINVAL;
+  g_group_m = g;
   return GS_OK;
 }
