@@ -45,7 +45,7 @@ from ..api import v1beta1 as api
 from ..cluster import objects as O
 from ..cluster.client import APIClient, APIError
 from ..cluster.podcache import PodSource
-from ..device.model import DeviceModel, real_device_id
+from ..device.model import DeviceModel
 from ..quota import ShimConfig, ledger_name
 from ..utils import log
 from ..utils.metrics import PluginMetrics

@@ -17,7 +17,6 @@ import socket
 import ssl
 import tempfile
 import threading
-import time
 import urllib.parse
 
 import yaml

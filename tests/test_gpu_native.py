@@ -10,7 +10,6 @@ import pytest
 from aliyun_gpushare_device_plugin_amd import const
 from aliyun_gpushare_device_plugin_amd.device import smi as S
 from aliyun_gpushare_device_plugin_amd.device.model import DeviceModel
-from aliyun_gpushare_device_plugin_amd.utils import units as U
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
