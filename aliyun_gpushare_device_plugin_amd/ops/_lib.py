@@ -25,6 +25,7 @@ SIGNATURES = {
     "gs_silu_mul_bf16": [_P, _P, _I, _I, _P],
     "gs_rope_bf16": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "gs_flash_attn_fwd_bf16": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _F, _I, _P],
+    "gs_attn_set_variant": [_I],
 }
 
 ERRORS = {1: "invalid arguments", 2: "kernel launch failed"}

@@ -8,6 +8,15 @@ import torch
 from . import _lib
 
 
+ATTN_AUTO, ATTN_V1 = 0, 1
+
+
+def set_attention_variant(v: int) -> None:
+    """``ATTN_AUTO``: the 8-wave 32x32-MFMA kernel for D = 128 (16x16 kernel for D = 64);
+    ``ATTN_V1``: always the 4-wave 16x16 kernel (A/B measurement, tests)."""
+    _lib.check(_lib.lib().gs_attn_set_variant(int(v)), "gs_attn_set_variant")
+
+
 def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: bool = True,
               scale: float | None = None, _debug_gather: bool = False) -> torch.Tensor:
     """``q`` [B, S, Hq, D], ``k``/``v`` [B, S, Hkv, D] (token-major; q/k/v may be strided views

@@ -205,6 +205,233 @@ __global__ __launch_bounds__(256, 2) void flash_fwd(const unsigned short* __rest
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// v2 (D = 128): 8 waves x 32 query rows on v_mfma_f32_32x32x16_bf16 (256 rows per block)
+//
+// Same algorithm, twice the rows per wave and the 32x32 MFMA, so every K / V fragment read
+// from LDS feeds twice the FLOPs of v1 (cdna_hip_programming.md "Fused attention prefill").
+//  * S^T = K Q^T (A = K rows from LDS, B = Q^T in registers): lane l holds the scores of query
+//    row l & 31 for keys (r & 3) + 8 (r >> 2) + 4 (l >> 5) of each 32-key sub-tile — the row
+//    max / sum need one exchange with lane l ^ 32;
+//  * P^T as the PV B operand: for k-step ks lane half h needs keys 16 ks + 8 h + 0..7; it holds
+//    4 of them (block 2 (ks & 1) + h) and gets the other 4 from lane l ^ 32 (block
+//    2 (ks & 1) + 1 - h), packed to bf16 pairs before the exchange;
+//  * O^T = V^T P^T: A = V^T fragments from two ds_read_b64_tr_b16 (rows 16 ks + 8 h + 0..3 and
+//    + 4..7, column 32 dt + (l & 31)); O keeps the query-row <-> lane mapping, so the online
+//    rescale is lane-local;
+//  * LDS images: K in 16-B chunks XOR (row & 15) (conflict-free ds_read_b128 groups), V in 8-B
+//    units XOR ((row & 3) << 3) (each 32-lane tr-read group covers 32 distinct units = all 64
+//    banks; 16-B staging writes stay contiguous); K/V register-staged, 2-deep ring (64 KiB);
+//  * causal: only diagonal tiles are masked; waves whose rows are all above a tile skip it.
+constexpr int KT8 = 64, ROW8 = 256, TILE8 = KT8 * ROW8, STAGE8 = 2 * TILE8, LDS8 = 2 * STAGE8;
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ int k8swz(int row, int chunk) { return chunk ^ (row & 15); }
+__device__ __forceinline__ int v8swz(int row, int unit) { return unit ^ ((row & 3) << 3); }
+
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+// one v_cvt_pk_bf16_f32 (RNE): a -> low half, b -> high half
+__device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2_t{a, b}, bf16x2_t));
+}
+
+// NW waves per block (NW x 32 query rows). NW = 4 runs two independent blocks per CU (their
+// per-tile barriers drift apart, so one block's softmax overlaps the other's MFMAs); NW = 8 is
+// one block per CU.
+template <int NW>
+__global__ __launch_bounds__(NW * 64, 8 / NW) void flash_fwd_d128_w8(const unsigned short* __restrict__ Q,
+                                                            const unsigned short* __restrict__ K,
+                                                            const unsigned short* __restrict__ V,
+                                                            unsigned short* __restrict__ O, int B, int S, int Hq,
+                                                            int Hkv, int q_stride, int k_stride, int v_stride,
+                                                            float scale_log2, int causal) {
+  constexpr int QR8 = 32 * NW, NT = NW * 64, LD = 1024 / NT;   // 16-B staging loads per thread (K or V)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nqb = (S + QR8 - 1) / QR8;
+  const int bh = blockIdx.x / nqb;
+  const int qb = causal ? (nqb - 1 - (int)(blockIdx.x % nqb)) : (int)(blockIdx.x % nqb);  // heaviest first
+  const int b = bh / Hq, h = bh % Hq;
+  const int hk = h / (Hq / Hkv);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ql = lane & 31, hh = lane >> 5;
+  const int q0 = qb * QR8 + wave * 32;
+  const int qi = q0 + ql;
+
+  // Q^T fragments (B operand): lane holds Q[qi][16 ds + 8 hh + j]
+  bf16x8_t qf[8];
+  {
+    const unsigned short* qp = Q + ((size_t)b * S + min(qi, S - 1)) * q_stride + (size_t)h * 128 + 8 * hh;
+#pragma unroll
+    for (int ds = 0; ds < 8; ++ds) qf[ds] = *(const bf16x8_t*)(qp + 16 * ds);
+  }
+  f32x16_t o[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
+  float m = -INFINITY, l = 0.f;
+
+  const int nkt_all = (S + KT8 - 1) / KT8;
+  const int nkt = causal ? min(nkt_all, (qb * QR8 + QR8 - 1) / KT8 + 1) : nkt_all;
+
+  // register staging: 1024 16-B chunks per K (or V) tile / NT threads
+  u16x8_t kreg[LD], vreg[LD];
+  auto load_tile = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < LD; ++i) {
+      const int idx = tid + i * NT, row = idx >> 4, ch = idx & 15;
+      const int key = min(t * KT8 + row, S - 1);
+      kreg[i] = *(const u16x8_t*)(K + ((size_t)b * S + key) * k_stride + (size_t)hk * 128 + ch * 8);
+      vreg[i] = *(const u16x8_t*)(V + ((size_t)b * S + key) * v_stride + (size_t)hk * 128 + ch * 8);
+    }
+  };
+  auto store_tile = [&](int buf) {
+    char* kb = smem + buf * STAGE8;
+    char* vb = kb + TILE8;
+#pragma unroll
+    for (int i = 0; i < LD; ++i) {
+      const int idx = tid + i * NT, row = idx >> 4, ch = idx & 15;
+      *(u16x8_t*)(kb + row * ROW8 + (k8swz(row, ch) << 4)) = kreg[i];
+      *(u16x8_t*)(vb + row * ROW8 + (v8swz(row, 2 * ch) << 3)) = vreg[i];
+    }
+  };
+
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+
+  for (int t = 0; t < nkt; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < nkt) load_tile(t + 1);
+    const char* kb = smem + cur * STAGE8;
+    const char* vb = kb + TILE8;
+    const int kfirst = t * KT8;
+    const bool active = !causal || kfirst <= q0 + 31;           // some key of the tile is visible
+    if (active) {
+      // ---- S^T = K Q^T, two 32-key sub-tiles ----
+      f32x16_t s[2];
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[st][r] = 0.f;
+        const int row = 32 * st + ql;
+#pragma unroll
+        for (int ds = 0; ds < 8; ++ds) {
+          const bf16x8_t kf = *(const bf16x8_t*)(kb + row * ROW8 + (k8swz(row, 2 * ds + hh) << 4));
+          s[st] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ds], s[st], 0, 0, 0);
+        }
+      }
+      // ---- online softmax (base 2); masking only on diagonal / ragged tiles ----
+      const bool need_mask = (causal && kfirst + KT8 - 1 > q0) || kfirst + KT8 > S;
+      float tmax = -INFINITY;
+      if (need_mask) {
+#pragma unroll
+        for (int st = 0; st < 2; ++st)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = kfirst + 32 * st + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            const float v = (key >= S || (causal && key > qi)) ? -INFINITY : s[st][r] * scale_log2;
+            s[st][r] = v;
+            tmax = fmaxf(tmax, v);
+          }
+      } else {
+#pragma unroll
+        for (int st = 0; st < 2; ++st)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            s[st][r] *= scale_log2;
+            tmax = fmaxf(tmax, s[st][r]);
+          }
+      }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float mnew = fmaxf(m, tmax);
+      const float alpha = __builtin_amdgcn_exp2f(m - mnew);   // raw v_exp_f32 (exp2(-inf) = 0)
+      m = mnew;
+      float psum = 0.f;
+#pragma unroll
+      for (int st = 0; st < 2; ++st)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float pv = __builtin_amdgcn_exp2f(s[st][r] - mnew);
+          s[st][r] = pv;
+          psum += pv;
+        }
+      psum += __shfl_xor(psum, 32, 64);
+      l = l * alpha + psum;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[i] *= alpha;
+
+      // ---- O^T += V^T P^T over 4 k-steps of 16 keys ----
+      const int g16 = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        // the two 4-key blocks of this k-step at compile-time register indices: lo = keys
+        // base + 4 hh + 0..3, hi = base + 8 + 4 hh + 0..3 (base = 16 (ks & 1) in the sub-tile)
+        const int st = ks >> 1, rb = 8 * (ks & 1);
+        const unsigned lo0 = pack_bf16x2(s[st][rb + 0], s[st][rb + 1]);
+        const unsigned lo1 = pack_bf16x2(s[st][rb + 2], s[st][rb + 3]);
+        const unsigned hi0 = pack_bf16x2(s[st][rb + 4], s[st][rb + 5]);
+        const unsigned hi1 = pack_bf16x2(s[st][rb + 6], s[st][rb + 7]);
+        // half hh keeps block (hh ? hi : lo) and sends the other to lane l ^ 32
+        const unsigned own0 = hh ? hi0 : lo0, own1 = hh ? hi1 : lo1;
+        const unsigned rcv0 = (unsigned)__shfl_xor((int)(hh ? lo0 : hi0), 32, 64);
+        const unsigned rcv1 = (unsigned)__shfl_xor((int)(hh ? lo1 : hi1), 32, 64);
+        typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+        const u32x4_t pw = hh ? u32x4_t{rcv0, rcv1, own0, own1} : u32x4_t{own0, own1, rcv0, rcv1};
+        const bf16x8_t pf = __builtin_bit_cast(bf16x8_t, pw);
+        // V^T fragment rows (keys) 16 ks + 8 hh + {0..3 | 4..7}; lane (4 q4 + p4) of its 16-lane
+        // group addresses row q4, columns 4 p4 .. 4 p4 + 3 of the group's 16-column block
+        const int r0 = 16 * ks + 8 * (g16 >> 1) + q4, r1 = r0 + 4;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          const int unit = 8 * dt + 4 * (g16 & 1) + p4;
+          const v4s a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) v4s*)(vb + r0 * ROW8 + (v8swz(r0, unit) << 3)));
+          const v4s a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) v4s*)(vb + r1 * ROW8 + (v8swz(r1, unit) << 3)));
+          const v8s both = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
+          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, both), pf, o[dt], 0, 0, 0);
+        }
+      }
+    }
+    if (t + 1 < nkt) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: O[qi][32 dt + 8 (r >> 2) + 4 hh + (r & 3)] = o[dt][r] / l ----
+  if (qi < S) {
+    const float inv = 1.f / l;
+    unsigned short* op = O + (((size_t)b * S + qi) * Hq + h) * 128 + 4 * hh;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        u16x4_t w;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) w[r] = f32_to_bf16(o[dt][4 * q + r] * inv);
+        *(u16x4_t*)(op + 32 * dt + 8 * q) = w;
+      }
+  }
+}
+
+int g_attn_variant = 0;   // 0 = auto, 1 = 16x16 4-wave kernel, 2 = 32x32 4-wave, 3 = 32x32 8-wave
+
+template <int NW>
+int launch_w8(const void* q, const void* k, const void* v, void* o, int B, int S, int Hq, int Hkv, int qs, int ks,
+              int vs, float scale_log2, int causal, hipStream_t stream) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)flash_fwd_d128_w8<NW>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS8);
+    attr = true;
+  }
+  const int nqb = (S + 32 * NW - 1) / (32 * NW);
+  flash_fwd_d128_w8<NW><<<dim3((unsigned)(B * Hq * nqb)), dim3(NW * 64), LDS8, stream>>>(
+      (const unsigned short*)q, (const unsigned short*)k, (const unsigned short*)v, (unsigned short*)o, B, S, Hq,
+      Hkv, qs, ks, vs, scale_log2, causal & 1);
+  return gs_launch_status();
+}
+
 template <int D, bool TR>
 int launch(const void* q, const void* k, const void* v, void* o, int B, int S, int Hq, int Hkv, int qs, int ks,
            int vs, float scale_log2, int causal, hipStream_t stream) {
@@ -236,6 +463,18 @@ GS_KERNEL_API int gs_flash_attn_fwd_bf16(const void* q, const void* k, const voi
   if (causal & 2)
     return D == 128 ? launch<128, false>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream)
                     : launch<64, false>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
+  if (D == 128 && g_attn_variant == 3)
+    return launch_w8<8>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
+  if (D == 128 && g_attn_variant != 1)
+    return launch_w8<4>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
   return D == 128 ? launch<128, true>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream)
                   : launch<64, true>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
+}
+
+// Kernel selection for A/B measurement and tests: 0 = auto (32x32-MFMA 8-wave kernel for
+// D = 128), 1 = the 16x16 4-wave kernel.
+GS_KERNEL_API int gs_attn_set_variant(int v) {
+  if (v < 0 || v > 3) return GS_EINVAL;
+  g_attn_variant = v;
+  return GS_OK;
 }
