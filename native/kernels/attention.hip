@@ -214,8 +214,8 @@ __global__ __launch_bounds__(256, 2) void flash_fwd(const unsigned short* __rest
 //    row l & 31 for keys (r & 3) + 8 (r >> 2) + 4 (l >> 5) of each 32-key sub-tile — the row
 //    max / sum need one exchange with lane l ^ 32;
 //  * P^T as the PV B operand: for k-step ks lane half h needs keys 16 ks + 8 h + 0..7; it holds
-//    4 of them (block 2 (ks & 1) + h) and gets the other 4 from lane l ^ 32 (block
-//    2 (ks & 1) + 1 - h), packed to bf16 pairs before the exchange;
+//    4 of them and gets the other 4 from lane l ^ 32 — one v_permlane32_swap per packed bf16
+//    pair, no LDS round trip (row max / sum across the pair the same way);
 //  * O^T = V^T P^T: A = V^T fragments from two ds_read_b64_tr_b16 (rows 16 ks + 8 h + 0..3 and
 //    + 4..7, column 32 dt + (l & 31)); O keeps the query-row <-> lane mapping, so the online
 //    rescale is lane-local;
@@ -232,6 +232,17 @@ __device__ __forceinline__ int v8swz(int row, int unit) { return unit ^ ((row & 
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 // one v_cvt_pk_bf16_f32 (RNE): a -> low half, b -> high half
+// v_permlane32_swap (probed on MI355X, tools/diag/permlane_probe.hip): r = swap(a, b) gives
+// r[0] = a (lanes 0-31) | b of lane l-32 (lanes 32-63), r[1] = a of lane l+32 (lanes 0-31) | b.
+__device__ __forceinline__ float pair_max(float x) {   // max over lanes l and l ^ 32
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float pair_sum(float x) {   // sum over lanes l and l ^ 32
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 __device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
   return __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2_t{a, b}, bf16x2_t));
 }
@@ -344,7 +355,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_fwd_d128_w8(const unsig
             tmax = fmaxf(tmax, s[st][r]);
           }
       }
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      tmax = pair_max(tmax);
       const float mnew = fmaxf(m, tmax);
       const float alpha = __builtin_amdgcn_exp2f(m - mnew);   // raw v_exp_f32 (exp2(-inf) = 0)
       m = mnew;
@@ -357,7 +368,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_fwd_d128_w8(const unsig
           s[st][r] = pv;
           psum += pv;
         }
-      psum += __shfl_xor(psum, 32, 64);
+      psum = pair_sum(psum);
       l = l * alpha + psum;
 #pragma unroll
       for (int i = 0; i < 4; ++i) o[i] *= alpha;
@@ -373,12 +384,12 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_fwd_d128_w8(const unsig
         const unsigned lo1 = pack_bf16x2(s[st][rb + 2], s[st][rb + 3]);
         const unsigned hi0 = pack_bf16x2(s[st][rb + 4], s[st][rb + 5]);
         const unsigned hi1 = pack_bf16x2(s[st][rb + 6], s[st][rb + 7]);
-        // half hh keeps block (hh ? hi : lo) and sends the other to lane l ^ 32
-        const unsigned own0 = hh ? hi0 : lo0, own1 = hh ? hi1 : lo1;
-        const unsigned rcv0 = (unsigned)__shfl_xor((int)(hh ? lo0 : hi0), 32, 64);
-        const unsigned rcv1 = (unsigned)__shfl_xor((int)(hh ? lo1 : hi1), 32, 64);
+        // half 0 needs {own lo, partner's lo}, half 1 {partner's hi, own hi}: swap(lo, hi) returns
+        // exactly those two words in that order on both halves — no select, no LDS round trip
+        const auto w0 = __builtin_amdgcn_permlane32_swap(lo0, hi0, false, false);
+        const auto w1 = __builtin_amdgcn_permlane32_swap(lo1, hi1, false, false);
         typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-        const u32x4_t pw = hh ? u32x4_t{rcv0, rcv1, own0, own1} : u32x4_t{own0, own1, rcv0, rcv1};
+        const u32x4_t pw = u32x4_t{w0[0], w1[0], w0[1], w1[1]};
         const bf16x8_t pf = __builtin_bit_cast(bf16x8_t, pw);
         // V^T fragment rows (keys) 16 ks + 8 hh + {0..3 | 4..7}; lane (4 q4 + p4) of its 16-lane
         // group addresses row q4, columns 4 p4 .. 4 p4 + 3 of the group's 16-column block
