@@ -229,6 +229,11 @@ typedef float f32x16_t __attribute__((ext_vector_type(16)));
 __device__ __forceinline__ int k8swz(int row, int chunk) { return chunk ^ (row & 15); }
 __device__ __forceinline__ int v8swz(int row, int unit) { return unit ^ ((row & 3) << 3); }
 
+template <bool B>
+struct BoolTag {
+  static constexpr bool value = B;
+};
+
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 // one v_cvt_pk_bf16_f32 (RNE): a -> low half, b -> high half
@@ -319,7 +324,10 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_fwd_d128_w8(const unsig
     const char* vb = kb + TILE8;
     const int kfirst = t * KT8;
     const bool active = !causal || kfirst <= q0 + 31;           // some key of the tile is visible
-    if (active) {
+    // The tile body is instantiated twice (diagonal/ragged tiles with the mask, the rest without)
+    // so each path is one basic block the scheduler can interleave (softmax VALU under MFMAs).
+    auto body = [&](auto tag) {
+      constexpr bool MASKED = decltype(tag)::value;
       // ---- S^T = K Q^T, two 32-key sub-tiles ----
       f32x16_t s[2];
 #pragma unroll
@@ -334,9 +342,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_fwd_d128_w8(const unsig
         }
       }
       // ---- online softmax (base 2); masking only on diagonal / ragged tiles ----
-      const bool need_mask = (causal && kfirst + KT8 - 1 > q0) || kfirst + KT8 > S;
       float tmax = -INFINITY;
-      if (need_mask) {
+      if constexpr (MASKED) {
 #pragma unroll
         for (int st = 0; st < 2; ++st)
 #pragma unroll
@@ -405,6 +412,12 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_fwd_d128_w8(const unsig
           o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, both), pf, o[dt], 0, 0, 0);
         }
       }
+    };
+    if (active) {
+      if ((causal && kfirst + KT8 - 1 > q0) || kfirst + KT8 > S)
+        body(BoolTag<true>{});
+      else
+        body(BoolTag<false>{});
     }
     if (t + 1 < nkt) store_tile(cur ^ 1);
     __syncthreads();
