@@ -13,7 +13,7 @@ import torch
 from . import _lib
 
 EP_BIAS, EP_SILU, EP_RESID = 1, 2, 4
-GEMM_AUTO, GEMM_V1, GEMM_PINGPONG = 0, 1, 2
+GEMM_AUTO, GEMM_V1, GEMM_PINGPONG, GEMM_W4 = 0, 1, 2, 4
 
 
 def set_gemm_group_m(g: int) -> None:
@@ -22,8 +22,10 @@ def set_gemm_group_m(g: int) -> None:
 
 
 def set_gemm_variant(v: int) -> None:
-    """Kernel selection (A/B measurement, tests): ``GEMM_AUTO`` = ping-pong 8-phase kernel for
-    M%256 == N%256 == K%128 == 0, the 2-stage kernel otherwise; ``GEMM_V1`` forces the latter."""
+    """Kernel selection (A/B measurement, tests): ``GEMM_AUTO`` = the 4-wave AGPR kernel
+    (native/kernels/gemm_bf16_w4.hip) for M%256 == N%256 == K%128 == 0 with ldc%8 == 0, else the
+    ping-pong 8-phase kernel when aligned, else the 2-stage kernel; ``GEMM_V1`` forces the 2-stage
+    kernel, ``GEMM_PINGPONG`` the ping-pong one, ``GEMM_W4`` the 4-wave one where it applies."""
     _lib.check(_lib.lib().gs_gemm_set_variant(int(v)), "gs_gemm_set_variant")
 
 

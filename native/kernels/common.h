@@ -33,3 +33,8 @@ __device__ __forceinline__ float wave_sum(float v) {
 enum { GS_OK = 0, GS_EINVAL = 1, GS_ELAUNCH = 2 };
 
 inline int gs_launch_status() { return hipGetLastError() == hipSuccess ? GS_OK : GS_ELAUNCH; }
+
+// 4-wave GEMM launcher (gemm_bf16_w4.hip); GS_EINVAL when the shape or output layout does not
+// suit it (M % 256, N % 256, K % 128, ldc % 8, 16-B aligned C).
+int gs_gemm_w4_launch(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K,
+                      int lda, int ldb, int ldc, int flags, hipStream_t stream);

@@ -21,6 +21,8 @@
 //  * fused epilogue: + bias[n], SiLU, + residual[m,n] (flags), bf16 output.
 // Requirements (checked by the launcher): K % 64 == 0, lda/ldb % 8 == 0, 16-B aligned A/B,
 // N % 4 == 0, ldc % 4 == 0.
+// Aligned shapes (M, N % 256, K % 128) run the 4-wave kernel of gemm_bf16_w4.hip (AGPR
+// accumulators, 128x128 per wave); the two 8-wave kernels here cover the rest.
 #include "common.h"
 
 namespace {
@@ -393,153 +395,8 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_nt_256_pp(
   }
 }
 
-// ---------------------------------------------------------------------------------------
-// v3: 4 waves x 128x128 (one wave per SIMD, 256 accumulator registers), register-pipelined
-// (aligned shapes: M % 256 == 0, N % 256 == 0, K % 64 == 0)
-//
-// PMC comparison of v2 against the library kernel at 8192^3 (profiles/gemm_pmc_8192.md):
-// with two waves per SIMD and 128x64 per wave, v2 parks 29 % of its wave-cycles at barriers
-// and issues 1.75x the LDS reads of a 128x128-per-wave tile. Here each SIMD runs ONE wave
-// that owns a 128x128 sub-tile (8x8 16x16 tiles, 64 MFMA per 32-wide k-step) and keeps the
-// matrix pipe fed from registers:
-//  * two LDS stages (2 x 64 KiB, global_load_lds, source-side XOR swizzle as v1);
-//  * fragments are double-buffered in registers: set0 = k-step 0 of a tile, set1 = k-step 1;
-//  * ONE raw barrier per K-tile, placed between the two MFMA halves:
-//      [64 MFMA on set0 | ds_read set1 (tile t)] vmcnt(0) lgkmcnt(0) s_barrier
-//      [DMA tile t+2 -> the buffer just released | 64 MFMA on set1 | ds_read set0 (tile t+1)]
-//    so the barrier never waits on a fragment read, the buffer being refilled was released
-//    by every wave's retired reads, and each DMA has a whole K-tile (~2k MFMA cycles) to land.
-// Status: EXPERIMENTAL (variant 3, never auto-selected). Correct, but 1.09-1.15 PF/s vs
-// v2's 1.30-1.44 (profiles/gemm_vs_hipblaslt_v3.json): hipcc runs out of AGPRs for the 256
-// accumulators + fragment sets and shuffles accumulators through VGPRs every K-tile, and the
-// 16 DMA issues (each behind a readfirstlane -> m0 chain) bunch after the barrier with the
-// matrix pipe idle. The shape is right (it is the library kernel's); the schedule needs
-// hand placement (sched_group_barrier or asm) to pay off.
-constexpr int W4_THREADS = 256;
-
-__global__ __launch_bounds__(W4_THREADS, 1) void gemm_bf16_nt_256_w4(
-    const unsigned short* __restrict__ A, const unsigned short* __restrict__ B, unsigned short* __restrict__ C,
-    const unsigned short* __restrict__ bias, const unsigned short* __restrict__ R, int M, int N, int K, int lda,
-    int ldb, int ldc, int flags) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-
-  const int nbm = M / BM, nbn = N / BN, nwg = nbm * nbn;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int gm = (flags >> 8) & 0xff ? (flags >> 8) & 0xff : GROUP_M;   // rasterisation group (rows)
-  const int per_group = gm * nbn;
-  const int first_m = (wgid / per_group) * gm;
-  const int gsz = min(nbm - first_m, gm);
-  const int tm = first_m + (wgid % per_group) % gsz;
-  const int tn = (wgid % per_group) / gsz;
-  const int m0 = tm * BM, n0 = tn * BN;
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-
-  // DMA: instruction i (0..7) of wave w writes LDS bytes [(i*4 + w) * 1024, +1024) of the
-  // operand's stage image = rows (i*4 + w)*8 + lane/8, chunk slot lane%8 <- chunk swz(row, lane%8)
-  const int drow = wave * 8 + (lane >> 3);            // + i*32
-  const int dc = swz(drow, lane & 7);                 // (i*32 >> 1) & 7 == 0: same for every i
-  const unsigned short* srcA = A + (size_t)(m0 + drow) * lda + dc * 8;
-  const unsigned short* srcB = B + (size_t)(n0 + drow) * ldb + dc * 8;
-  const size_t a32 = (size_t)32 * lda, b32 = (size_t)32 * ldb;
-
-  auto stage = [&](int buf, int kt) {
-    char* a = smem + buf * STAGE;
-    char* b = a + A_STAGE;
-    const int koff = kt * BK;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      glds16(srcA + i * a32 + koff, a + (i * 4 + wave) * 1024);
-      glds16(srcB + i * b32 + koff, b + (i * 4 + wave) * 1024);
-    }
-  };
-
-  f32x4_t acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  const int lr = lane & 15;
-  const int co[2] = {swz(lr, lane >> 4) << 4, swz(lr, 4 + (lane >> 4)) << 4};
-  const int a_lane = (wm * 128 + lr) * 128;
-  const int b_lane = (wn * 128 + lr) * 128;
-
-  bf16x8_t fa[2][8], fb[2][8];
-  auto read = [&](int set, int buf, int kk) {
-    const char* a = smem + buf * STAGE + a_lane + co[kk];
-    const char* b = smem + buf * STAGE + A_STAGE + b_lane + co[kk];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      fb[set][i] = *(const bf16x8_t*)(b + i * 16 * 128);
-      fa[set][i] = *(const bf16x8_t*)(a + i * 16 * 128);
-    }
-  };
-  auto mfma = [&](int set) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[set][j], fa[set][i], acc[i][j], 0, 0, 0);
-  };
-
-  const int KT = K / BK;
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  raw_barrier();
-  if (KT > 1) stage(1, 1);
-  read(0, 0, 0);
-
-  for (int kt = 0; kt < KT; ++kt) {
-    const int buf = kt & 1;
-    read(1, buf, 1);
-    mfma(0);
-    if (kt + 1 < KT) {
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      raw_barrier();
-      if (kt + 2 < KT) stage(buf, kt + 2);
-      read(0, buf ^ 1, 0);
-    }
-    mfma(1);
-  }
-
-  const int mbase = m0 + wm * 128 + lr;
-  const int nbase = n0 + wn * 128 + (lane >> 4) * 4;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int m = mbase + i * 16;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int n = nbase + j * 16;
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if (flags & EP_BIAS) {
-        const u16x4_t bb = *(const u16x4_t*)(bias + n);
-#pragma unroll
-        for (int t = 0; t < 4; ++t) v[t] += bf16_to_f32(bb[t]);
-      }
-      if (flags & EP_SILU) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) v[t] = silu_f32(v[t]);
-      }
-      if (flags & EP_RESID) {
-        const u16x4_t rr = *(const u16x4_t*)(R + (size_t)m * ldc + n);
-#pragma unroll
-        for (int t = 0; t < 4; ++t) v[t] += bf16_to_f32(rr[t]);
-      }
-      u16x4_t o;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) o[t] = f32_to_bf16(v[t]);
-      *(u16x4_t*)(C + (size_t)m * ldc + n) = o;
-    }
-  }
-}
-
 int g_group_m = 0;   // 0 = GROUP_M; else tile-rasterisation group height (passed in flags bits 8..15)
-int g_variant = 0;   // 0 = auto, 1 = v1 (2-stage, 8 waves), 2 = v2 (ping-pong), 3 = v3 (4 waves)
-//   // 0 = auto (v2 when aligned), 1 = force v1, 2 = v2 when aligned
+int g_variant = 0;   // 0 = auto, 1 = v1 (2-stage, 8 waves), 2 = v2 (ping-pong), 4 = 4-wave AGPR kernel
 
 }  // namespace
 
@@ -556,18 +413,14 @@ GS_KERNEL_API int gs_gemm_bf16_nt(const void* A, const void* B, void* C, const v
     (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_256, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_256_pp, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_BYTES);
-    (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_256_w4, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              LDS_BYTES);
     attr_set = true;
   }
   const bool aligned = M % BM == 0 && N % BN == 0 && K % (2 * BK) == 0;
-  const int nblocks = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  if (M % BM == 0 && N % BN == 0 && g_variant == 3) {
-    gemm_bf16_nt_256_w4<<<dim3(nblocks), dim3(W4_THREADS), LDS_BYTES, stream>>>(
-        (const unsigned short*)A, (const unsigned short*)B, (unsigned short*)C, (const unsigned short*)bias,
-        (const unsigned short*)R, M, N, K, lda, ldb, ldc, flags);
-    return gs_launch_status();
+  if (aligned && (g_variant == 0 || g_variant == 4)) {   // 4-wave kernel first when it applies
+    const int rc = gs_gemm_w4_launch(A, B, C, bias, R, M, N, K, lda, ldb, ldc, flags, stream);
+    if (rc != GS_EINVAL) return rc;
   }
+  const int nblocks = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   if (aligned && g_variant != 1) {
     gemm_bf16_nt_256_pp<<<dim3(nblocks), dim3(NTHREADS), LDS_BYTES, stream>>>(
         (const unsigned short*)A, (const unsigned short*)B, (unsigned short*)C, (const unsigned short*)bias,
@@ -580,10 +433,11 @@ GS_KERNEL_API int gs_gemm_bf16_nt(const void* A, const void* B, void* C, const v
   return gs_launch_status();
 }
 
-// Kernel selection for A/B measurement and tests: 0 = auto, 1 = v1 only, 2 = v2 when aligned,
-// 3 = v3 (4-wave) when M, N are multiples of 256.
+// Kernel selection for A/B measurement and tests: 0 = auto (4-wave kernel when it applies, else
+// ping-pong when aligned, else 2-stage), 1 = 2-stage only, 2 = ping-pong when aligned, 4 = 4-wave
+// when it applies (gemm_bf16_w4.hip), else as 2.
 GS_KERNEL_API int gs_gemm_set_variant(int v) {
-  if (v < 0 || v > 3) return GS_EINVAL;
+  if (v < 0 || v > 4 || v == 3) return GS_EINVAL;
   g_variant = v;
   return GS_OK;
 }

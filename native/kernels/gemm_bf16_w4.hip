@@ -1,0 +1,290 @@
+// bf16 GEMM, 4 waves x 128x128 per wave, accumulators pinned in AGPRs (variant 4).
+//
+// C[M,N] = epilogue(A[M,K] · B[N,K]^T), aligned shapes only (M % 256 == N % 256 == 0,
+// K % 128 == 0); the launcher in gemm_bf16.hip checks and falls back otherwise.
+//
+// Why this shape (profiles/gemm_pmc_8192.md): the 8-wave kernels give every wave a 128x64
+// output, so a CU re-reads 48 KiB of LDS per K-tile per SIMD and parks ~29 % of its wave
+// cycles at barriers. One wave per SIMD owning 128x128 reads 32 KiB per K-tile (the shape of
+// the hipBLASLt kernel) and needs no partner wave, but its 256 fp32 accumulators exceed the
+// 256-VGPR architectural file. hipcc, left alone, splits them between VGPRs and AGPRs and
+// spills (the former variant 3). Here every MFMA is an inline-asm statement whose C/D operand
+// is constrained to the accumulator file ("+a"), so the 64 f32x4 accumulators live in
+// a[0:255] for the whole kernel and the fragments, addresses and DMA pointers use ~140 VGPRs.
+//
+// Pipeline (one raw barrier per 64-deep K-tile, two LDS stages of 64 KiB):
+//   phase A(t): 64 MFMA on fragment set 0 (k 0..31 of tile t), interleaved 1 ds_read per 4
+//               MFMA filling set 1 (k 32..63 of tile t, buffer t&1)
+//   boundary  : s_waitcnt vmcnt(0) lgkmcnt(0)  (tile t+1 landed, set 1 in registers); s_barrier
+//   phase B(t): 64 MFMA on set 1, interleaved per 4 MFMA with 1 global_load_lds of tile t+2
+//               into buffer t&1 (every wave's reads of it retired before the barrier) and
+//               1 ds_read filling set 0 from tile t+1 (buffer (t+1)&1, visible after the barrier)
+// Each DMA therefore has two phases (~2k MFMA cycles) to land before its wait.
+// The last loop iteration waits for every DMA before the epilogue (s_waitcnt at its boundary).
+// LDS image and swizzle as in gemm_bf16.hip (chunk c of row r at c ^ ((r >> 1) & 7)).
+//
+// Hazards the compiler does not pad around asm (cdna_hip_programming.md §5.7): fragment VGPRs
+// are written only by ds_read (hipcc's lgkmcnt covers them — the asm names them as inputs);
+// each accumulator is rewritten 64 MFMAs after its previous write; the AGPR zero-init and the
+// epilogue's v_accvgpr_read are separated from the MFMA stream by explicit s_nop pads.
+#include "common.h"
+
+namespace {
+
+constexpr int BM = 256, BN = 256, BK = 64, NT = 256;
+constexpr int A_STAGE = BM * BK * 2;   // 32 KiB
+constexpr int STAGE = 2 * A_STAGE;     // A + B
+constexpr int LDS_BYTES = 2 * STAGE;   // 128 KiB
+constexpr int GROUP_M = 8;
+
+enum { EP_BIAS = 1, EP_SILU = 2, EP_RESID = 4 };
+
+__device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+#define MFMA_A(acc, b, a) \
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a))
+
+struct Frags {
+  bf16x8_t a[8], b[8];
+};
+
+// 64 MFMAs on fragment set `f` into acc; `extra(g, u)` runs after MFMA u (0..3) of group g
+// (0..15), each followed by a scheduling fence so the interleave is exactly the source order.
+template <typename Extra>
+__device__ __forceinline__ void mfma_phase(f32x4_t (&acc)[8][8], const Frags& f, Extra extra) {
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int idx = g * 4 + u, i = idx >> 3, j = idx & 7;
+      MFMA_A(acc[i][j], f.b[j], f.a[i]);
+      extra(g, u);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
+// Block -> output tile: XCD-aware bijective remap, then GROUP_M rasterisation (as gemm_bf16.hip).
+__device__ __forceinline__ void tile_origin(int M, int N, int flags, int& m0, int& n0) {
+  const int nbm = M / BM, nbn = N / BN, nwg = nbm * nbn;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int gm = (flags >> 8) & 0xff ? (flags >> 8) & 0xff : GROUP_M;
+  const int per_group = gm * nbn;
+  const int first_m = (wgid / per_group) * gm;
+  const int gsz = min(nbm - first_m, gm);
+  m0 = (first_m + (wgid % per_group) % gsz) * BM;
+  n0 = ((wgid % per_group) / gsz) * BN;
+}
+
+// Epilogue of a 128x128 wave tile. Lane (row r = lane & 15, quad q = lane >> 4) holds
+// C[m][n..n+3] of every 16x16 tile (i, j), m = mbase + 16 i, n = nbase + 16 j + 4 q. After
+// + bias, SiLU, + residual (by flags) and bf16 packing, one v_permlane16_swap per dword pairs
+// tiles j and j+1: quads 0/2 then hold 8 contiguous columns of tile j (4q .. 4q+7 -> cols 0-7 /
+// 8-15), quads 1/3 those of tile j+1, so each lane stores 16 B instead of 2 x 8 B
+// (cdna_hip_programming.md T21 with 16-lane rows). Needs ldc % 8 == 0 and a 16-B aligned C.
+// EPI (compile-time flags) keeps the epilogue branch-free: with runtime flags hipcc built a
+// branchy CFG per element and spilled accumulators into scratch.
+template <int EPI>
+__device__ __forceinline__ void epilogue_128x128(f32x4_t (&acc)[8][8], unsigned short* __restrict__ C,
+                                                 const unsigned short* __restrict__ bias,
+                                                 const unsigned short* __restrict__ R, int ldc, int mbase, int nbase,
+                                                 int q) {
+  const int ncol = nbase - 4 * q + 16 * (q & 1) + 8 * (q >> 1);   // store column of tile pair 0
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = mbase + i * 16;
+    // the accumulators of row i stay in AGPRs until here: hipcc otherwise copies them all to
+    // VGPRs at the loop exit and spills
+    asm volatile("" : "+a"(acc[i][0]), "+a"(acc[i][1]), "+a"(acc[i][2]), "+a"(acc[i][3]), "+a"(acc[i][4]),
+                 "+a"(acc[i][5]), "+a"(acc[i][6]), "+a"(acc[i][7]));
+#pragma unroll
+    for (int jp = 0; jp < 4; ++jp) {
+      unsigned w[2][2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int j = 2 * jp + h, n = nbase + j * 16;
+        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        if constexpr ((EPI & EP_BIAS) != 0) {
+          const u16x4_t bb = *(const u16x4_t*)(bias + n);
+#pragma unroll
+          for (int t = 0; t < 4; ++t) v[t] += bf16_to_f32(bb[t]);
+        }
+        if constexpr ((EPI & EP_SILU) != 0) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) v[t] = silu_f32(v[t]);
+        }
+        if constexpr ((EPI & EP_RESID) != 0) {
+          const u16x4_t rr = *(const u16x4_t*)(R + (size_t)m * ldc + n);
+#pragma unroll
+          for (int t = 0; t < 4; ++t) v[t] += bf16_to_f32(rr[t]);
+        }
+        w[h][0] = (unsigned)f32_to_bf16(v[0]) | ((unsigned)f32_to_bf16(v[1]) << 16);
+        w[h][1] = (unsigned)f32_to_bf16(v[2]) | ((unsigned)f32_to_bf16(v[3]) << 16);
+      }
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        const auto r = __builtin_amdgcn_permlane16_swap(w[0][d], w[1][d], false, false);
+        w[0][d] = r[0];
+        w[1][d] = r[1];
+      }
+      typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+      *(u32x4_t*)(C + (size_t)m * ldc + ncol + 32 * jp) = u32x4_t{w[0][0], w[0][1], w[1][0], w[1][1]};
+    }
+    __builtin_amdgcn_sched_barrier(0);   // one row of tiles at a time: bounds VGPR pressure
+  }
+}
+
+// DMA_GROUPS: the 16 DMA instructions of a phase B go 16 / DMA_GROUPS at a time into its first
+// DMA_GROUPS MFMA groups (earlier issue = more time to land before the next boundary's wait).
+// The 16 fragment reads of each phase go two per group into its first 8 groups, after MFMAs
+// RD_U0 and RD_U1 of the group; a DMA follows MFMA DMA_U.
+template <int DMA_GROUPS, int RD_U0, int RD_U1, int DMA_U, int EPI>
+__global__ __launch_bounds__(NT, 1) void gemm_bf16_nt_w4a(
+    const unsigned short* __restrict__ A, const unsigned short* __restrict__ B, unsigned short* __restrict__ C,
+    const unsigned short* __restrict__ bias, const unsigned short* __restrict__ R, int M, int N, int K, int lda,
+    int ldb, int ldc, int flags) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  int m0, n0;
+  tile_origin(M, N, flags, m0, n0);
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // provably uniform -> SGPR
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // ---- DMA: instruction i (0..7) of wave w fills rows (i*4 + w)*8 + lane/8 of an operand
+  // image (1 KiB per instruction); lane's chunk slot lane%8 <- logical chunk swz(row, lane%8),
+  // which is the same for every i because i*32 rows shift (row >> 1) & 7 by a multiple of 8.
+  const int drow = wave * 8 + (lane >> 3);
+  const int dc = swz(drow, lane & 7);
+  // Buffer descriptors over this block's 256 rows of A and B (base and size from kernel
+  // arguments and blockIdx only, so they stay in SGPRs); the per-lane part is one VGPR offset,
+  // the DMA index i and the K-tile go into the scalar soffset, so a DMA costs no VALU.
+  const __amdgpu_buffer_rsrc_t rA =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(A + (size_t)m0 * lda), (short)0, BM * lda * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rB =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(B + (size_t)n0 * ldb), (short)0, BN * ldb * 2, 0x00020000);
+  const unsigned voffA = (unsigned)(drow * lda + dc * 8) * 2u;
+  const unsigned voffB = (unsigned)(drow * ldb + dc * 8) * 2u;
+  const unsigned a32 = 64u * lda, b32 = 64u * ldb;   // bytes of 32 rows
+  char* const wdst = smem + wave * 1024;   // + buf*STAGE + i*4096 (+ A_STAGE for B)
+
+  // DMA instruction g (0..15) of K-tile kt into buffer buf: g < 8 -> A rows, else B rows
+  auto dma = [&](int buf, int kt, int g) {
+    const int i = g & 7;
+    const unsigned koff = (unsigned)kt * (BK * 2);
+    if (g < 8)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rA, (__attribute__((address_space(3))) void*)(wdst + buf * STAGE + i * 4096), 16, voffA, i * a32 + koff, 0, 0);
+    else
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rB, (__attribute__((address_space(3))) void*)(wdst + buf * STAGE + A_STAGE + i * 4096), 16, voffB,
+          i * b32 + koff, 0, 0);
+  };
+
+  // ---- fragment addressing: lane reads row (lane & 15) of a 16-row tile, k-chunk
+  // kk*4 + lane/16; the swizzle term depends only on lane & 15 (tile bases are multiples of 16)
+  const int lr = lane & 15;
+  const int co0 = swz(lr, lane >> 4) << 4;
+  const int co1 = swz(lr, 4 + (lane >> 4)) << 4;
+  const int a_off = (wm * 128 + lr) * 128;
+  const int b_off = A_STAGE + (wn * 128 + lr) * 128;
+  // read g (0..15) of a fragment set from buffer buf: g < 8 -> B tile g, else A tile g-8
+  auto frag_read = [&](Frags& f, int buf, int co, int g) {
+    const char* base = smem + buf * STAGE + co;
+    if (g < 8)
+      f.b[g] = *(const bf16x8_t*)(base + b_off + g * 2048);
+    else
+      f.a[g - 8] = *(const bf16x8_t*)(base + a_off + (g - 8) * 2048);
+  };
+
+  f32x4_t acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  Frags f0, f1;
+  const int KT = K / BK;   // even, >= 2
+
+  // ---- prologue: tiles 0 and 1 in flight, wait for tile 0, read set 0 of tile 0 ----
+#pragma unroll
+  for (int g = 0; g < 16; ++g) dma(0, 0, g);
+#pragma unroll
+  for (int g = 0; g < 16; ++g) dma(1, 1, g);
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int g = 0; g < 16; ++g) frag_read(f0, 0, co0, g);
+  __builtin_amdgcn_sched_barrier(0);
+
+  // One loop body for every tile, so the accumulators keep one register assignment (a peeled
+  // tail made hipcc shuffle them through VGPRs). Past the end, the DMA re-fetches tile KT-1 into
+  // the buffer just released and phase B reads a dead fragment set: both harmless.
+  for (int kt = 0; kt < KT; ++kt) {
+    const int buf = kt & 1;
+    const int kdma = min(kt + 2, KT - 1);
+    // hipcc may place the accumulators' zero-init (v_accvgpr_write) right before the loop:
+    // 2 wait states before an MFMA reads them as srcC (2 cycles per 4k-cycle iteration)
+    asm volatile("s_nop 1" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    // phase A: set-1 reads; the boundary wait sits between the last two MFMAs and the barrier
+    // after the last one, so the matrix pipe stays busy while the wave waits
+    mfma_phase(acc, f0, [&](int g, int u) {
+      if (g < 8 && u == RD_U0) frag_read(f1, buf, co1, 2 * g);
+      if (g < 8 && u == RD_U1) frag_read(f1, buf, co1, 2 * g + 1);
+      if (g == 15 && u == 2) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      if (g == 15 && u == 3) __builtin_amdgcn_s_barrier();
+    });
+    // phase B: DMA of tile kt+2 into the buffer just released, set-0 reads of tile kt+1
+    mfma_phase(acc, f1, [&](int g, int u) {
+      if (u == DMA_U && g < DMA_GROUPS) {
+#pragma unroll
+        for (int d = 0; d < 16 / DMA_GROUPS; ++d) dma(buf, kdma, g * (16 / DMA_GROUPS) + d);
+      }
+      if (g < 8 && u == RD_U0) frag_read(f0, buf ^ 1, co0, 2 * g);
+      if (g < 8 && u == RD_U1) frag_read(f0, buf ^ 1, co0, 2 * g + 1);
+    });
+    // last MFMA D -> whatever reads the accumulators next: hipcc places its AGPR copies for
+    // the epilogue on the loop-exit edge, ahead of any statement after the loop, so the pad
+    // must be inside the final iteration
+    if (kt == KT - 1) asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
+  }
+
+  epilogue_128x128<EPI>(acc, C, bias, R, ldc, m0 + wm * 128 + lr, n0 + wn * 128 + (lane >> 4) * 4, lane >> 4);
+}
+
+}  // namespace
+
+// Launch the 4-wave kernel; the caller (gs_gemm_bf16_nt) has validated pointers/strides/flags.
+// Returns GS_EINVAL when the shape or output layout does not suit it (the caller falls back).
+int gs_gemm_w4_launch(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K,
+                      int lda, int ldb, int ldc, int flags, hipStream_t stream) {
+  if (M % BM || N % BN || K % (2 * BK)) return GS_EINVAL;
+  if ((size_t)BM * lda * 2 > 0xffffffffu || (size_t)BN * ldb * 2 > 0xffffffffu) return GS_EINVAL;
+  if (ldc % 8 || ((uintptr_t)C & 15)) return GS_EINVAL;   // 16-B epilogue stores
+  // DMA after MFMA 1 of each group, the two fragment reads after MFMAs 2 and 3 of groups 0-7:
+  // the best of the placements swept on MI355X (profiles/gemm_w4_variants.md)
+  using Kern = void (*)(const unsigned short*, const unsigned short*, unsigned short*, const unsigned short*,
+                       const unsigned short*, int, int, int, int, int, int, int);
+  static const Kern kerns[8] = {gemm_bf16_nt_w4a<16, 2, 3, 1, 0>, gemm_bf16_nt_w4a<16, 2, 3, 1, 1>,
+                                gemm_bf16_nt_w4a<16, 2, 3, 1, 2>, gemm_bf16_nt_w4a<16, 2, 3, 1, 3>,
+                                gemm_bf16_nt_w4a<16, 2, 3, 1, 4>, gemm_bf16_nt_w4a<16, 2, 3, 1, 5>,
+                                gemm_bf16_nt_w4a<16, 2, 3, 1, 6>, gemm_bf16_nt_w4a<16, 2, 3, 1, 7>};
+  const Kern kern = kerns[flags & 7];
+  static bool attr_set = false;
+  if (!attr_set) {
+    for (Kern k : kerns)
+      (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    attr_set = true;
+  }
+  const int nblocks = (M / BM) * (N / BN);
+  kern<<<dim3(nblocks), dim3(NT), LDS_BYTES, stream>>>(
+      (const unsigned short*)A, (const unsigned short*)B, (unsigned short*)C, (const unsigned short*)bias,
+      (const unsigned short*)R, M, N, K, lda, ldb, ldc, flags);
+  return gs_launch_status();
+}

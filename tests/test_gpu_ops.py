@@ -43,7 +43,7 @@ def test_gemm_nt_matches_fp32(M, N, K):
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (256, 256, 64), (512, 768, 256), (2048, 1024, 4096),
                                    (4096, 4096, 4096)])
 def test_gemm_pingpong_matches_v1_and_fp32(M, N, K):
-    """The 8-phase ping-pong kernel (aligned shapes) against fp32 and against the 2-stage kernel."""
+    """The 8-phase ping-pong and 4-wave kernels (aligned shapes) against fp32 and the 2-stage kernel."""
     from aliyun_gpushare_device_plugin_amd.ops import gemm_nt
     from aliyun_gpushare_device_plugin_amd.ops.gemm import GEMM_AUTO, GEMM_V1, set_gemm_variant
     a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
@@ -52,7 +52,7 @@ def test_gemm_pingpong_matches_v1_and_fp32(M, N, K):
         set_gemm_variant(GEMM_V1)
         o1 = gemm_nt(a, b)
         outs = []
-        for v in (2, 3):
+        for v in (2, 4):
             set_gemm_variant(v)
             outs.append(gemm_nt(a, b))
         torch.cuda.synchronize()
@@ -73,6 +73,41 @@ def test_gemm_identity_asymmetric():
     b = (torch.arange(512 * K, device="cuda") % 251).reshape(512, K).to(torch.bfloat16)
     out = gemm_nt(a, b)   # = I @ b^T = b^T
     assert torch.equal(out, b.t().contiguous())
+
+
+@pytest.mark.parametrize("variant", [0, 2, 4])
+def test_gemm_identity_asymmetric_aligned(variant):
+    """Same check on an aligned shape for every kernel (auto = 4-wave, ping-pong, 4-wave forced)."""
+    from aliyun_gpushare_device_plugin_amd.ops import gemm_nt
+    from aliyun_gpushare_device_plugin_amd.ops.gemm import GEMM_AUTO, set_gemm_variant
+    K = 512
+    a = torch.eye(K, device="cuda", dtype=torch.bfloat16)
+    b = (torch.arange(768 * K, device="cuda") % 251).reshape(768, K).to(torch.bfloat16)
+    try:
+        set_gemm_variant(variant)
+        out = gemm_nt(a, b)
+        torch.cuda.synchronize()
+    finally:
+        set_gemm_variant(GEMM_AUTO)
+    assert torch.equal(out, b.t().contiguous())
+
+
+@pytest.mark.parametrize("variant", [0, 2, 4])
+def test_gemm_fused_epilogues_aligned(variant):
+    from aliyun_gpushare_device_plugin_amd.ops import gemm_nt
+    from aliyun_gpushare_device_plugin_amd.ops.gemm import GEMM_AUTO, set_gemm_variant
+    M, N, K = 512, 768, 1024
+    a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    b = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.1
+    bias = torch.randn(N, device="cuda", dtype=torch.bfloat16)
+    res = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    try:
+        set_gemm_variant(variant)
+        out = gemm_nt(a, b, bias=bias, residual=res, silu=True)
+        torch.cuda.synchronize()
+    finally:
+        set_gemm_variant(GEMM_AUTO)
+    assert_close_bf16(out, ref_linear(a, b, bias, res, silu=True), K)
 
 
 def test_gemm_fused_epilogues():

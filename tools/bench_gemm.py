@@ -36,7 +36,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--out", default=None)
-    ap.add_argument("--variants", default="1,2,3", help="extra kernel variants to time besides auto")
+    ap.add_argument("--variants", default="1,2", help="extra kernel variants to time besides auto")
     a = ap.parse_args()
     res = []
     variants = [int(v) for v in a.variants.split(",") if v]

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Run each GEMM implementation a few times on fixed shapes (for rocprofv3 --pmc passes).
 
-Dispatch order per shape: v2 (ping-pong) x R, v1 (2-stage) x R, torch/hipBLASLt x R, so the
-per-dispatch counter rows can be attributed by kernel name.
+Dispatch order per shape: each variant of PROF_VARIANTS (default "0,1": auto, 2-stage) x R, then
+torch/hipBLASLt x R; the per-dispatch counter rows are attributed by kernel name.
 """
 import os
 import sys
@@ -20,7 +20,7 @@ for s in (sys.argv[1] if len(sys.argv) > 1 else "8192x8192x8192,4096x4096x4096")
     x = torch.empty(M, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)
     w = torch.empty(N, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)
     out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-    for variant in (GEMM_AUTO, GEMM_V1):
+    for variant in [int(v) for v in os.environ.get("PROF_VARIANTS", f"{GEMM_AUTO},{GEMM_V1}").split(",")]:
         set_gemm_variant(variant)
         for _ in range(R):
             gemm_nt(x, w, out=out)
