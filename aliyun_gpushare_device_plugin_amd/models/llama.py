@@ -8,7 +8,8 @@ offline). Compute path per layer, all on hand-written gfx950 kernels except atte
   ->  RoPE in place on the q/k slices of the QKV buffer (no copies)
   ->  causal GQA attention (ops.attention: flash-style HIP kernel when built, else SDPA)
   ->  O-proj GEMM with the residual add fused into its epilogue
-  ->  rmsnorm  ->  gate|up GEMM (one fused [28672, 4096] weight)  ->  SiLU*mul
+  ->  rmsnorm  ->  gate|up GEMM (one [28672, 4096] weight, gate/up rows interleaved by 16) with
+      SiLU(gate)*up computed in its epilogue (no [T, 28672] activation round trip)
   ->  down GEMM with the residual add fused
 """
 from __future__ import annotations
@@ -72,7 +73,7 @@ class LlamaModel:
                 "wqkv": w(nq, c.d_model),
                 "wo": w(c.d_model, c.n_heads * c.head_dim, std=0.02 / math.sqrt(2 * c.n_layers)),
                 "mlp_norm": torch.ones(c.d_model, device=self.device, dtype=torch.bfloat16),
-                "wgu": w(2 * c.d_ff, c.d_model),
+                "wgu": ops.interleave_gate_up(w(2 * c.d_ff, c.d_model)),   # epilogue-SwiGLU layout
                 "wd": w(c.d_model, c.d_ff, std=0.02 / math.sqrt(2 * c.n_layers)),
             })
         self.final_norm = torch.ones(c.d_model, device=self.device, dtype=torch.bfloat16)
@@ -108,8 +109,7 @@ class LlamaModel:
                               v.view(B, S, c.n_kv_heads, c.head_dim), causal=True)
             h = ops.linear(a.reshape(T, hq), L["wo"], residual=h)   # fused residual add
             x = ops.rmsnorm(h, L["mlp_norm"], c.eps)
-            gu = ops.linear(x, L["wgu"])
-            h = ops.linear(ops.silu_mul(gu), L["wd"], residual=h)
+            h = ops.linear(ops.linear_swiglu(x, L["wgu"]), L["wd"], residual=h)
             nxt = self.layers[i + 1]["attn_norm"] if i + 1 < len(self.layers) else self.final_norm
             x = ops.rmsnorm(h, nxt, c.eps)
         if logits == "last":
@@ -156,7 +156,7 @@ def reference_forward(model: LlamaModel, tokens: torch.Tensor) -> torch.Tensor:
                                                              v.transpose(1, 2), is_causal=True)
         h = h + a.transpose(1, 2).reshape(B, S, hq) @ L["wo"].to(f).t()
         x = rms(h, L["mlp_norm"])
-        gu = x @ L["wgu"].to(f).t()
+        gu = x @ ops.deinterleave_gate_up(L["wgu"]).to(f).t()
         g_, u_ = gu[..., :c.d_ff], gu[..., c.d_ff:]
         h = h + (torch.nn.functional.silu(g_) * u_) @ L["wd"].to(f).t()
     x = rms(h, model.final_norm)

@@ -12,7 +12,7 @@ import torch
 
 from . import _lib
 
-EP_BIAS, EP_SILU, EP_RESID = 1, 2, 4
+EP_BIAS, EP_SILU, EP_RESID, EP_SWIGLU = 1, 2, 4, 8
 GEMM_AUTO, GEMM_V1, GEMM_PINGPONG, GEMM_W4 = 0, 1, 2, 4
 
 
@@ -38,9 +38,30 @@ def _check_operand(t: torch.Tensor, name: str):
         raise ValueError(f"{name}: last dimension must be contiguous")
 
 
+def interleave_gate_up(w: torch.Tensor) -> torch.Tensor:
+    """``[gate; up]`` weight rows ([2F, K], gate rows first) -> the layout the fused SwiGLU epilogue
+    reads: blocks of 16 gate rows followed by the 16 up rows of the same features."""
+    F2, K = w.shape
+    if F2 % 32:
+        raise ValueError("gate|up rows must be a multiple of 32")
+    g, u = w[: F2 // 2], w[F2 // 2:]
+    return torch.stack((g.reshape(-1, 16, K), u.reshape(-1, 16, K)), 1).reshape(F2, K).contiguous()
+
+
+def deinterleave_gate_up(w: torch.Tensor) -> torch.Tensor:
+    """Inverse of :func:`interleave_gate_up`: ``[2F, K]`` interleaved rows -> ``[gate; up]``."""
+    F2, K = w.shape
+    v = w.reshape(F2 // 32, 2, 16, K)
+    return torch.cat((v[:, 0].reshape(-1, K), v[:, 1].reshape(-1, K)), 0)
+
+
 def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, bias: torch.Tensor | None = None,
-            residual: torch.Tensor | None = None, silu: bool = False) -> torch.Tensor:
-    """``out[M,N] = epi(a[M,K] @ b[N,K]^T)``; a and b are 2-D row-major (K contiguous)."""
+            residual: torch.Tensor | None = None, silu: bool = False, swiglu: bool = False) -> torch.Tensor:
+    """``out[M,N] = epi(a[M,K] @ b[N,K]^T)``; a and b are 2-D row-major (K contiguous).
+
+    ``swiglu=True``: b holds gate/up rows interleaved by :func:`interleave_gate_up` and the result
+    is ``out[M, N/2] = silu(gate) * up`` computed in the GEMM epilogue (aligned shapes only:
+    M % 256 == N % 256 == K % 128 == 0; see :func:`linear_swiglu` for the general entry)."""
     _check_operand(a, "a")
     _check_operand(b, "b")
     if a.dim() != 2 or b.dim() != 2 or a.shape[1] != b.shape[1]:
@@ -55,11 +76,14 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, b
         lda, ldb = a.stride(0), b.stride(0)
         if lda % 8 or ldb % 8:
             raise ValueError("gemm_nt needs 16-byte aligned rows")
+    No = N // 2 if swiglu else N
+    if swiglu and (bias is not None or residual is not None or silu or M % 256 or N % 256 or K % 128):
+        raise ValueError("swiglu GEMM: no other epilogue, and M % 256 == N % 256 == K % 128 == 0")
     if out is None:
-        out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
-    elif out.shape != (M, N) or out.dtype != torch.bfloat16 or out.stride(1) != 1 or out.stride(0) % 4:
+        out = torch.empty((M, No), dtype=torch.bfloat16, device=a.device)
+    elif out.shape != (M, No) or out.dtype != torch.bfloat16 or out.stride(1) != 1 or out.stride(0) % 4:
         raise ValueError("bad out tensor")
-    flags = 0
+    flags = EP_SWIGLU if swiglu else 0
     bptr = rptr = None
     if bias is not None:
         if bias.numel() != N or bias.dtype != torch.bfloat16 or not bias.is_contiguous():
@@ -77,6 +101,24 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, b
                                     out.stride(0), flags, _lib.stream_ptr(a.device))
     _lib.check(rc, "gs_gemm_bf16_nt")
     return out
+
+
+def linear_swiglu(x: torch.Tensor, w_interleaved: torch.Tensor) -> torch.Tensor:
+    """``silu(x @ gate.T) * (x @ up.T)`` for x ``[..., K]`` and gate/up weights interleaved by
+    :func:`interleave_gate_up`; fused into the GEMM epilogue when the shape is aligned, else a
+    plain GEMM followed by the silu_mul kernel on the de-interleaved activations."""
+    from .fused import silu_mul
+
+    lead = x.shape[:-1]
+    x2 = x.reshape(-1, x.shape[-1])
+    N, K = w_interleaved.shape
+    if x2.shape[0] % 256 == 0 and N % 256 == 0 and K % 128 == 0 and x2.stride(-1) == 1:
+        y = gemm_nt(x2, w_interleaved, swiglu=True)
+    else:
+        gu = gemm_nt(x2, w_interleaved)                                  # [M, N] interleaved
+        gu = gu.view(-1, N // 32, 2, 16).permute(0, 2, 1, 3).reshape(-1, N).contiguous()
+        y = silu_mul(gu)
+    return y.reshape(*lead, N // 2)
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None,

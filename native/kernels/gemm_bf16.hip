@@ -18,7 +18,8 @@
 //    registers are 4 consecutive output columns: 8-byte packed bf16 stores;
 //  * XCD-aware bijective block remap + GROUP_M rasterisation so the 8 blocks that share an
 //    XCD's L2 share A panels;
-//  * fused epilogue: + bias[n], SiLU, + residual[m,n] (flags), bf16 output.
+//  * fused epilogue: + bias[n], SiLU, + residual[m,n] (flags), bf16 output; SwiGLU (flag 8,
+//    gate/up rows interleaved by 16) only on the 4-wave kernel of gemm_bf16_w4.hip.
 // Requirements (checked by the launcher): K % 64 == 0, lda/ldb % 8 == 0, 16-B aligned A/B,
 // N % 4 == 0, ldc % 4 == 0.
 // Aligned shapes (M, N % 256, K % 128) run the 4-wave kernel of gemm_bf16_w4.hip (AGPR
@@ -34,7 +35,7 @@ constexpr int STAGE = A_STAGE + B_STAGE;      // 64 KiB
 constexpr int LDS_BYTES = 2 * STAGE;          // 128 KiB
 constexpr int GROUP_M = 8;
 
-enum { EP_BIAS = 1, EP_SILU = 2, EP_RESID = 4 };
+enum { EP_BIAS = 1, EP_SILU = 2, EP_RESID = 4, EP_SWIGLU = 8 };
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
@@ -402,11 +403,15 @@ int g_variant = 0;   // 0 = auto, 1 = v1 (2-stage, 8 waves), 2 = v2 (ping-pong),
 
 GS_KERNEL_API int gs_gemm_bf16_nt(const void* A, const void* B, void* C, const void* bias, const void* R, int M,
                                   int N, int K, int lda, int ldb, int ldc, int flags, hipStream_t stream) {
+  const bool swiglu = flags & EP_SWIGLU;   // out[M, N/2] = silu(gate) * up, gate/up rows interleaved by 16
   if (M <= 0 || N <= 0 || K <= 0 || K % BK || lda % 8 || ldb % 8 || ldc % 4 || N % 4 || lda < K || ldb < K ||
-      ldc < N || ((uintptr_t)A & 15) || ((uintptr_t)B & 15) || ((uintptr_t)C & 7))
+      ldc < (swiglu ? N / 2 : N) || ((uintptr_t)A & 15) || ((uintptr_t)B & 15) || ((uintptr_t)C & 7))
     return GS_EINVAL;
   if ((flags & EP_BIAS) && !bias) return GS_EINVAL;
   flags = (flags & 0xff) | (g_group_m << 8);
+  if (swiglu)   // only the 4-wave kernel has the SwiGLU epilogue (aligned shapes)
+    return g_variant == 0 || g_variant == 4 ? gs_gemm_w4_launch(A, B, C, bias, R, M, N, K, lda, ldb, ldc, flags, stream)
+                                            : GS_EINVAL;
   if ((flags & EP_RESID) && !R) return GS_EINVAL;
   static bool attr_set = false;
   if (!attr_set) {

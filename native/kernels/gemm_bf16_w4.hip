@@ -37,7 +37,7 @@ constexpr int STAGE = 2 * A_STAGE;     // A + B
 constexpr int LDS_BYTES = 2 * STAGE;   // 128 KiB
 constexpr int GROUP_M = 8;
 
-enum { EP_BIAS = 1, EP_SILU = 2, EP_RESID = 4 };
+enum { EP_BIAS = 1, EP_SILU = 2, EP_RESID = 4, EP_SWIGLU = 8 };
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
@@ -133,6 +133,45 @@ __device__ __forceinline__ void epilogue_128x128(f32x4_t (&acc)[8][8], unsigned 
       *(u32x4_t*)(C + (size_t)m * ldc + ncol + 32 * jp) = u32x4_t{w[0][0], w[0][1], w[1][0], w[1][1]};
     }
     __builtin_amdgcn_sched_barrier(0);   // one row of tiles at a time: bounds VGPR pressure
+  }
+}
+
+// SwiGLU epilogue: B's rows are gate/up interleaved in blocks of 16 (rows 32b .. 32b+15 = gate
+// features 16b .., rows 32b+16 .. 32b+31 = up features 16b ..), so tiles 2jj / 2jj+1 of a wave
+// hold gate / up of the same 16 features and out[m][f] = silu(g) * u is lane-local. The wave
+// writes a 128 x 64 feature tile of the [M, N/2] output (ldc in features); pairs of feature
+// tiles are merged by v_permlane16_swap into 16-B stores as in epilogue_128x128. Saves writing
+// and re-reading the [M, N] gate|up activations (the separate silu_mul pass).
+__device__ __forceinline__ void epilogue_swiglu(f32x4_t (&acc)[8][8], unsigned short* __restrict__ C, int ldc,
+                                                int mbase, int fbase, int q) {
+  const int fcol = fbase + 16 * (q & 1) + 8 * (q >> 1);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = mbase + i * 16;
+    asm volatile("" : "+a"(acc[i][0]), "+a"(acc[i][1]), "+a"(acc[i][2]), "+a"(acc[i][3]), "+a"(acc[i][4]),
+                 "+a"(acc[i][5]), "+a"(acc[i][6]), "+a"(acc[i][7]));
+#pragma unroll
+    for (int jp = 0; jp < 2; ++jp) {
+      unsigned w[2][2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int jj = 2 * jp + h;
+        float v[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) v[t] = silu_f32(acc[i][2 * jj][t]) * acc[i][2 * jj + 1][t];
+        w[h][0] = (unsigned)f32_to_bf16(v[0]) | ((unsigned)f32_to_bf16(v[1]) << 16);
+        w[h][1] = (unsigned)f32_to_bf16(v[2]) | ((unsigned)f32_to_bf16(v[3]) << 16);
+      }
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        const auto r = __builtin_amdgcn_permlane16_swap(w[0][d], w[1][d], false, false);
+        w[0][d] = r[0];
+        w[1][d] = r[1];
+      }
+      typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+      *(u32x4_t*)(C + (size_t)m * ldc + fcol + 32 * jp) = u32x4_t{w[0][0], w[0][1], w[1][0], w[1][1]};
+    }
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 
@@ -255,7 +294,10 @@ __global__ __launch_bounds__(NT, 1) void gemm_bf16_nt_w4a(
     if (kt == KT - 1) asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
   }
 
-  epilogue_128x128<EPI>(acc, C, bias, R, ldc, m0 + wm * 128 + lr, n0 + wn * 128 + (lane >> 4) * 4, lane >> 4);
+  if constexpr ((EPI & EP_SWIGLU) != 0)
+    epilogue_swiglu(acc, C, ldc, m0 + wm * 128 + lr, (n0 + wn * 128) / 2, lane >> 4);
+  else
+    epilogue_128x128<EPI>(acc, C, bias, R, ldc, m0 + wm * 128 + lr, n0 + wn * 128 + (lane >> 4) * 4, lane >> 4);
 }
 
 }  // namespace
@@ -271,11 +313,13 @@ int gs_gemm_w4_launch(const void* A, const void* B, void* C, const void* bias, c
   // the best of the placements swept on MI355X (profiles/gemm_w4_variants.md)
   using Kern = void (*)(const unsigned short*, const unsigned short*, unsigned short*, const unsigned short*,
                        const unsigned short*, int, int, int, int, int, int, int);
-  static const Kern kerns[8] = {gemm_bf16_nt_w4a<16, 2, 3, 1, 0>, gemm_bf16_nt_w4a<16, 2, 3, 1, 1>,
+  static const Kern kerns[9] = {gemm_bf16_nt_w4a<16, 2, 3, 1, 0>, gemm_bf16_nt_w4a<16, 2, 3, 1, 1>,
                                 gemm_bf16_nt_w4a<16, 2, 3, 1, 2>, gemm_bf16_nt_w4a<16, 2, 3, 1, 3>,
                                 gemm_bf16_nt_w4a<16, 2, 3, 1, 4>, gemm_bf16_nt_w4a<16, 2, 3, 1, 5>,
-                                gemm_bf16_nt_w4a<16, 2, 3, 1, 6>, gemm_bf16_nt_w4a<16, 2, 3, 1, 7>};
-  const Kern kern = kerns[flags & 7];
+                                gemm_bf16_nt_w4a<16, 2, 3, 1, 6>, gemm_bf16_nt_w4a<16, 2, 3, 1, 7>,
+                                gemm_bf16_nt_w4a<16, 2, 3, 1, EP_SWIGLU>};
+  if ((flags & EP_SWIGLU) && (flags & 7)) return GS_EINVAL;   // SwiGLU takes no other epilogue
+  const Kern kern = kerns[(flags & EP_SWIGLU) ? 8 : (flags & 7)];
   static bool attr_set = false;
   if (!attr_set) {
     for (Kern k : kerns)

@@ -110,6 +110,22 @@ def test_gemm_fused_epilogues_aligned(variant):
     assert_close_bf16(out, ref_linear(a, b, bias, res, silu=True), K)
 
 
+@pytest.mark.parametrize("M,F,K", [(256, 128, 128), (512, 1024, 512), (8192, 2048, 4096), (300, 256, 192)])
+def test_linear_swiglu_matches_fp32(M, F, K):
+    """Fused SwiGLU epilogue (aligned) and its unfused fallback against silu(x g^T) * (x u^T)."""
+    from aliyun_gpushare_device_plugin_amd.ops import deinterleave_gate_up, interleave_gate_up, linear_swiglu
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(2 * F, K, device="cuda", dtype=torch.bfloat16) * 0.05
+    wi = interleave_gate_up(w)
+    assert torch.equal(deinterleave_gate_up(wi), w)
+    out = linear_swiglu(x, wi)
+    torch.cuda.synchronize()
+    g, u = ref_linear(x, w[:F]), ref_linear(x, w[F:])
+    ref = torch.nn.functional.silu(g) * u
+    assert out.shape == (M, F)
+    assert_close_bf16(out, ref, K)
+
+
 def test_gemm_fused_epilogues():
     from aliyun_gpushare_device_plugin_amd.ops import gemm_nt
     M, N, K = 384, 512, 320
