@@ -260,7 +260,10 @@ class APIClient:
             c.sock.settimeout(None)
             buf = b""
             while not (stop and stop.is_set()):
-                chunk = r.read1(65536)
+                try:
+                    chunk = r.read1(65536)
+                except (ValueError, http.client.IncompleteRead):   # cut mid-chunk: stream over
+                    break
                 if not chunk:
                     break
                 buf += chunk

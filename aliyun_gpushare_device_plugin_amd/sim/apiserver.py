@@ -19,11 +19,9 @@ from __future__ import annotations
 import argparse
 import collections
 import copy
-import http.server
 import json
 import queue
 import re
-import socketserver
 import sys
 import threading
 import time
@@ -110,9 +108,13 @@ def matches(obj, fsel, lsel) -> bool:
 
 
 class _Watcher:
-    def __init__(self, fsel, lsel):
+    """A watch's selectors and its sink: ``push(event)`` when given (the asyncio front end),
+    else a thread-safe queue ``q`` (direct Store users)."""
+
+    def __init__(self, fsel, lsel, push=None):
         self.fsel, self.lsel = fsel, lsel
         self.q: "queue.Queue" = queue.Queue()
+        self.put = push or self.q.put
 
 
 class Store:
@@ -142,11 +144,11 @@ class Store:
         now = new is not None and matches(new, w.fsel, w.lsel)
         if typ == "DELETED":
             if was:
-                w.q.put({"type": "DELETED", "object": old})
+                w.put({"type": "DELETED", "object": old})
         elif now:
-            w.q.put({"type": "ADDED" if (typ == "ADDED" or not was) else "MODIFIED", "object": new})
+            w.put({"type": "ADDED" if (typ == "ADDED" or not was) else "MODIFIED", "object": new})
         elif was:
-            w.q.put({"type": "DELETED", "object": new})
+            w.put({"type": "DELETED", "object": new})
 
     # -- pods -----------------------------------------------------------------------------
     def create_pod(self, ns, pod):
@@ -249,9 +251,9 @@ class Store:
             return new
 
     # -- watch ----------------------------------------------------------------------------
-    def add_watcher(self, fsel, lsel, since_rv):
+    def add_watcher(self, fsel, lsel, since_rv, push=None):
         with self.lock:
-            w = _Watcher(fsel, lsel)
+            w = _Watcher(fsel, lsel, push)
             if since_rv:
                 since = int(since_rv)
                 if self.history and since < self.history[0][0] - 1 and since < self.rv:
@@ -272,177 +274,250 @@ _POD_RE = re.compile(r"^/api/v1/namespaces/([^/]+)/pods(?:/([^/]+))?(?:/(status|
 _NODE_RE = re.compile(r"^/api/v1/nodes(?:/([^/]+))?(?:/(status))?$")
 
 
-class _Handler(http.server.BaseHTTPRequestHandler):
-    protocol_version = "HTTP/1.1"
-    server_version = "fake-apiserver/1"
-    disable_nagle_algorithm = True   # header and body leave in one segment, no delayed-ACK stall
+_REASONS = {200: "OK", 201: "Created", 404: "Not Found", 409: "Conflict", 410: "Gone", 400: "Bad Request",
+            405: "Method Not Allowed"}
 
-    def log_message(self, *a):
-        pass
 
-    @property
-    def store(self) -> Store:
-        return self.server.store
+def _status(code, reason, msg):
+    return code, {"kind": "Status", "apiVersion": "v1", "status": "Failure", "message": msg, "reason": reason,
+                  "code": code}
 
-    def _send(self, code, obj):
-        body = json.dumps(obj, separators=(",", ":")).encode()
-        self.send_response(code)
-        self.send_header("Content-Type", "application/json")
-        self.send_header("Content-Length", str(len(body)))
-        self._headers_buffer.append(b"\r\n" + body)   # one write for headers + body
-        self.flush_headers()
 
-    def _status(self, code, reason, msg):
-        self._send(code, {"kind": "Status", "apiVersion": "v1", "status": "Failure", "message": msg,
-                          "reason": reason, "code": code})
-
-    def _body(self):
-        n = int(self.headers.get("Content-Length") or 0)
-        return json.loads(self.rfile.read(n)) if n else {}
-
-    def _delay(self):
-        d = self.server.latency_s
-        if d > 0:
-            time.sleep(d)
-
-    def do_GET(self):
-        self._delay()
-        u = urllib.parse.urlsplit(self.path)
-        q = dict(urllib.parse.parse_qsl(u.query))
-        path = u.path.rstrip("/")
+def route(store: Store, method: str, target: str, body: bytes):
+    """One REST request against ``store``. Returns ``(code, obj)``, or ``("watch", fsel, lsel, rv,
+    timeout)`` for a watch (the caller streams it)."""
+    u = urllib.parse.urlsplit(target)
+    path = u.path.rstrip("/")
+    if method == "GET":
+        q = dict(urllib.parse.parse_qsl(u.query)) if u.query else {}
         if path == "/debug/requests":      # simulator introspection: request counts by verb/kind
-            with self.store.lock:
-                return self._send(200, dict(self.store.requests))
-        self.store.requests["GET " + ("watch" if q.get("watch") else path.split("/")[-1])] += 1
+            with store.lock:
+                return 200, dict(store.requests)
+        store.requests["GET " + ("watch" if q.get("watch") else path.split("/")[-1])] += 1
         fsel, lsel = parse_field_selector(q.get("fieldSelector")), parse_label_selector(q.get("labelSelector"))
         if path == "/api/v1/pods" or re.fullmatch(r"/api/v1/namespaces/[^/]+/pods", path):
             ns = None if path == "/api/v1/pods" else path.split("/")[4]
             if q.get("watch") in ("1", "true"):
-                return self._watch(fsel, lsel, q.get("resourceVersion"), float(q.get("timeoutSeconds") or 300))
-            items, rv = self.store.list_pods(ns, fsel, lsel)
-            return self._send(200, {"kind": "PodList", "apiVersion": "v1", "metadata": {"resourceVersion": rv},
-                                    "items": items})
+                return "watch", fsel, lsel, q.get("resourceVersion"), float(q.get("timeoutSeconds") or 300)
+            items, rv = store.list_pods(ns, fsel, lsel)
+            return 200, {"kind": "PodList", "apiVersion": "v1", "metadata": {"resourceVersion": rv}, "items": items}
         m = _POD_RE.match(path)
         if m and m.group(2) and not m.group(3):
-            with self.store.lock:
-                p = self.store.pods.get((m.group(1), m.group(2)))
-            return self._send(200, p) if p else self._status(404, "NotFound", f'pods "{m.group(2)}" not found')
+            with store.lock:
+                p = store.pods.get((m.group(1), m.group(2)))
+            return (200, p) if p else _status(404, "NotFound", f'pods "{m.group(2)}" not found')
         m = _NODE_RE.match(path)
         if m:
-            with self.store.lock:
+            with store.lock:
                 if m.group(1):
-                    n = self.store.nodes.get(m.group(1))
-                    return self._send(200, n) if n else self._status(404, "NotFound",
-                                                                     f'nodes "{m.group(1)}" not found')
-                items = [n for n in self.store.nodes.values() if matches(n, fsel, lsel)]
-            return self._send(200, {"kind": "NodeList", "apiVersion": "v1",
-                                    "metadata": {"resourceVersion": str(self.store.rv)}, "items": items})
-        return self._status(404, "NotFound", path)
-
-    def _watch(self, fsel, lsel, rv, timeout):
-        w = self.store.add_watcher(fsel, lsel, rv)
-        if w is None:
-            return self._status(410, "Expired", "too old resource version")
-        self.send_response(200)
-        self.send_header("Content-Type", "application/json")
-        self.send_header("Transfer-Encoding", "chunked")
-        self.end_headers()
-        deadline = time.monotonic() + timeout
-        try:
-            while time.monotonic() < deadline and not self.server.stopping.is_set():
-                try:
-                    ev = w.q.get(timeout=0.2)
-                except queue.Empty:
-                    continue
-                data = json.dumps(ev, separators=(",", ":")).encode() + b"\n"
-                self.wfile.write(b"%x\r\n%s\r\n" % (len(data), data))
-                self.wfile.flush()
-            self.wfile.write(b"0\r\n\r\n")
-        except (BrokenPipeError, ConnectionResetError, OSError):
-            pass
-        finally:
-            self.store.remove_watcher(w)
-            self.close_connection = True
-
-    def do_POST(self):
-        self._delay()
-        path = urllib.parse.urlsplit(self.path).path.rstrip("/")
-        body = self._body()
-        self.store.requests["POST " + path.split("/")[-1]] += 1
+                    n = store.nodes.get(m.group(1))
+                    return (200, n) if n else _status(404, "NotFound", f'nodes "{m.group(1)}" not found')
+                items = [n for n in store.nodes.values() if matches(n, fsel, lsel)]
+            return 200, {"kind": "NodeList", "apiVersion": "v1", "metadata": {"resourceVersion": str(store.rv)},
+                         "items": items}
+        return _status(404, "NotFound", path)
+    obj = json.loads(body) if body else {}
+    if method == "POST":
+        store.requests["POST " + path.split("/")[-1]] += 1
         m = _POD_RE.match(path)
         if m and not m.group(2):
-            p = self.store.create_pod(m.group(1), body)
-            return self._send(201, p) if p else self._status(409, "AlreadyExists", "pod already exists")
+            p = store.create_pod(m.group(1), obj)
+            return (201, p) if p else _status(409, "AlreadyExists", "pod already exists")
         if m and m.group(3) == "binding":
             try:
-                p = self.store.bind_pod(m.group(1), m.group(2), body["target"]["name"])
+                p = store.bind_pod(m.group(1), m.group(2), obj["target"]["name"])
             except ValueError:
-                return self._status(409, "Conflict", "pod is already assigned to a node")
-            return self._send(201, {"kind": "Status", "status": "Success"}) if p else \
-                self._status(404, "NotFound", "pod not found")
+                return _status(409, "Conflict", "pod is already assigned to a node")
+            return (201, {"kind": "Status", "status": "Success"}) if p else _status(404, "NotFound", "pod not found")
         if path == "/api/v1/nodes":
-            n = self.store.create_node(body)
-            return self._send(201, n) if n else self._status(409, "AlreadyExists", "node already exists")
-        return self._status(404, "NotFound", path)
-
-    def do_PATCH(self):
-        self._delay()
-        path = urllib.parse.urlsplit(self.path).path.rstrip("/")
-        body = self._body()
-        self.store.requests["PATCH " + ("status" if path.endswith("/status") else path.split("/")[3])] += 1
+            n = store.create_node(obj)
+            return (201, n) if n else _status(409, "AlreadyExists", "node already exists")
+        return _status(404, "NotFound", path)
+    if method == "PATCH":
+        store.requests["PATCH " + ("status" if path.endswith("/status") else path.split("/")[3])] += 1
         m = _POD_RE.match(path)
         if m and m.group(2):
             try:
-                p = self.store.patch_pod(m.group(1), m.group(2), body, status_only=m.group(3) == "status")
+                p = store.patch_pod(m.group(1), m.group(2), obj, status_only=m.group(3) == "status")
             except ValueError:
-                return self._status(409, "Conflict", _CONFLICT_MSG)
-            return self._send(200, p) if p else self._status(404, "NotFound", f'pods "{m.group(2)}" not found')
+                return _status(409, "Conflict", _CONFLICT_MSG)
+            return (200, p) if p else _status(404, "NotFound", f'pods "{m.group(2)}" not found')
         m = _NODE_RE.match(path)
         if m and m.group(1):
-            n = self.store.patch_node(m.group(1), body, status_only=m.group(2) == "status")
-            return self._send(200, n) if n else self._status(404, "NotFound", f'nodes "{m.group(1)}" not found')
-        return self._status(404, "NotFound", path)
-
-    def do_DELETE(self):
-        self._delay()
-        path = urllib.parse.urlsplit(self.path).path.rstrip("/")
-        self.store.requests["DELETE"] += 1
+            n = store.patch_node(m.group(1), obj, status_only=m.group(2) == "status")
+            return (200, n) if n else _status(404, "NotFound", f'nodes "{m.group(1)}" not found')
+        return _status(404, "NotFound", path)
+    if method == "DELETE":
+        store.requests["DELETE"] += 1
         m = _POD_RE.match(path)
         if m and m.group(2):
-            p = self.store.delete_pod(m.group(1), m.group(2))
-            return self._send(200, p) if p else self._status(404, "NotFound", "pod not found")
-        return self._status(404, "NotFound", path)
+            p = store.delete_pod(m.group(1), m.group(2))
+            return (200, p) if p else _status(404, "NotFound", "pod not found")
+        return _status(404, "NotFound", path)
+    return _status(405, "MethodNotAllowed", method)
 
 
-class _Server(socketserver.ThreadingMixIn, http.server.HTTPServer):
-    daemon_threads = True
-    allow_reuse_address = True
-    request_queue_size = 128
+def _response(code: int, obj) -> bytes:
+    body = json.dumps(obj, separators=(",", ":")).encode()
+    return (b"HTTP/1.1 %d %s\r\nServer: fake-apiserver/2\r\nContent-Type: application/json\r\n"
+            b"Content-Length: %d\r\n\r\n" % (code, _REASONS.get(code, "Error").encode(), len(body))) + body
 
 
 class FakeAPIServer:
+    """HTTP/1.1 front end on one asyncio event loop (its own thread, or the caller's with
+    ``serve_forever``): keep-alive request/response, chunked watch streams. Every request is
+    handled inline on the loop — no thread per connection, no ``http.server`` parsing — which
+    keeps the fake's per-request cost well below the plugin's (the N=8 bench churns ~50 requests
+    per step through it)."""
+
     def __init__(self, host: str = "127.0.0.1", port: int = 0, latency_s: float = 0.0, store: Store | None = None):
+        import asyncio
+        import socket
+
         self.store = store or Store()
-        self.httpd = _Server((host, port), _Handler)
-        self.httpd.store = self.store
-        self.httpd.latency_s = latency_s
-        self.httpd.stopping = threading.Event()
+        self.latency_s = latency_s
+        self.stopping = threading.Event()
+        self._sock = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+        self._sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+        self._sock.bind((host, port))
+        self._sock.listen(256)
+        self.loop = asyncio.new_event_loop()
         self.thread = None
+        self._server = None
 
     @property
     def url(self) -> str:
-        h, p = self.httpd.server_address[:2]
+        h, p = self._sock.getsockname()[:2]
         return f"http://{h}:{p}"
 
+    # -- connection handling ------------------------------------------------------------------
+    async def _conn(self, reader, writer):
+        import asyncio
+        import socket
+
+        sock = writer.get_extra_info("socket")
+        if sock is not None:
+            sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+        try:
+            while not self.stopping.is_set():
+                try:
+                    head = await reader.readuntil(b"\r\n\r\n")
+                except (asyncio.IncompleteReadError, asyncio.LimitOverrunError, ConnectionError):
+                    return
+                lines = head.split(b"\r\n")
+                try:
+                    method, target, _ = lines[0].decode("latin-1").split(" ", 2)
+                except ValueError:
+                    return
+                n = 0
+                for ln in lines[1:]:
+                    if ln[:15].lower() == b"content-length:":
+                        n = int(ln[15:].strip() or 0)
+                body = await reader.readexactly(n) if n else b""
+                if self.latency_s > 0:
+                    await asyncio.sleep(self.latency_s)
+                try:
+                    res = route(self.store, method, target, body)
+                except Exception as e:  # noqa: BLE001 - a malformed request must not kill the fake
+                    res = _status(400, "BadRequest", repr(e))
+                if res[0] == "watch":
+                    await self._watch(writer, *res[1:])
+                    return
+                writer.write(_response(*res))
+                if writer.transport.get_write_buffer_size() > 1 << 20:
+                    await writer.drain()
+        finally:
+            writer.close()
+
+    async def _watch(self, writer, fsel, lsel, rv, timeout):
+        import asyncio
+
+        loop = asyncio.get_running_loop()
+        aq: asyncio.Queue = asyncio.Queue()
+        loop_tid = threading.get_ident()
+
+        def push(ev):   # called under the store lock, from the loop thread or a direct Store user
+            if threading.get_ident() == loop_tid:
+                aq.put_nowait(ev)
+            else:
+                loop.call_soon_threadsafe(aq.put_nowait, ev)
+
+        w = self.store.add_watcher(fsel, lsel, rv, push=push)
+        if w is None:
+            writer.write(_response(*_status(410, "Expired", "too old resource version")))
+            return
+        writer.write(b"HTTP/1.1 200 OK\r\nContent-Type: application/json\r\nTransfer-Encoding: chunked\r\n\r\n")
+        deadline = loop.time() + timeout
+        try:
+            while not self.stopping.is_set():
+                left = deadline - loop.time()
+                if left <= 0:
+                    break
+                try:
+                    ev = await asyncio.wait_for(aq.get(), min(left, 0.5))
+                except asyncio.TimeoutError:
+                    continue
+                evs = [ev]
+                while not aq.empty():
+                    evs.append(aq.get_nowait())
+                data = b"".join(json.dumps(e, separators=(",", ":")).encode() + b"\n" for e in evs)
+                writer.write(b"%x\r\n%s\r\n" % (len(data), data))
+                await writer.drain()
+        except (ConnectionError, OSError):
+            return
+        finally:
+            self.store.remove_watcher(w)
+            if not writer.is_closing():   # end the chunked stream (also on shutdown/cancel)
+                writer.write(b"0\r\n\r\n")
+
+    # -- lifecycle ---------------------------------------------------------------------------------
+    async def _start_server(self):
+        import asyncio
+
+        self._server = await asyncio.start_server(self._conn, sock=self._sock, limit=1 << 22)
+
+    def serve_forever(self):
+        import asyncio
+
+        asyncio.set_event_loop(self.loop)
+        self.loop.run_until_complete(self._start_server())
+        try:
+            self.loop.run_forever()
+        finally:   # cancel the connection / watch tasks and let them unwind before closing
+            if self._server is not None:
+                self._server.close()
+            tasks = [t for t in asyncio.all_tasks(self.loop) if not t.done()]
+            for t in tasks:
+                t.cancel()
+            if tasks:
+                self.loop.run_until_complete(asyncio.gather(*tasks, return_exceptions=True))
+            self.loop.run_until_complete(self.loop.shutdown_asyncgens())
+            self.loop.close()
+
     def start(self):
-        self.thread = threading.Thread(target=self.httpd.serve_forever, name="fake-apiserver", daemon=True)
+        self.thread = threading.Thread(target=self.serve_forever, name="fake-apiserver", daemon=True)
         self.thread.start()
+        import time as _t
+
+        t_end = _t.monotonic() + 10
+        while self._server is None and _t.monotonic() < t_end:
+            _t.sleep(0.001)
         return self
 
     def stop(self):
-        self.httpd.stopping.set()
-        self.httpd.shutdown()
-        self.httpd.server_close()
+        self.stopping.set()
+
+        if self.loop.is_running():
+            try:
+                self.loop.call_soon_threadsafe(self.loop.stop)
+            except RuntimeError:   # loop already closed
+                pass
+        if self.thread is not None:
+            self.thread.join(timeout=5)
+        try:
+            self._sock.close()
+        except OSError:
+            pass
 
     def __enter__(self):
         return self.start()
@@ -468,7 +543,7 @@ def main(argv=None):
     s = FakeAPIServer(a.host, a.port, a.latency_ms / 1000.0)
     print(s.url, flush=True)
     try:
-        s.httpd.serve_forever()
+        s.serve_forever()
     except KeyboardInterrupt:
         pass
     return 0
