@@ -25,6 +25,9 @@ MI355X build, same protocol, different mechanics:
   memory and the annotation is landed by a retrying background patcher, taking the apiserver
   round trip off the kubelet's admission path; candidates are Pending pods only and the claim
   is held until the patch is acknowledged, so a pod is never matched twice;
+* optional compute isolation (``compute_isolation="cu"``, ``alloc/cuslots.py``): each pod also
+  gets its own run of CU slots, answered as ``HSA_CU_MASK`` / ``ROC_GLOBAL_CU_MASK`` and recorded
+  on the pod in the same ASSIGNED patch;
 * swap completion: AllocateRequest carries no pod identity, so when the kubelet admits two
   equal-size pods in an order other than their assume times, the first Allocate takes the
   other pod's reservation and its own pod turns Running with ``ASSIGNED=false``. The reference
@@ -50,6 +53,7 @@ from ..quota import ShimConfig, ledger_name
 from ..utils import log
 from ..utils.metrics import PluginMetrics
 from . import annotations as A
+from . import cuslots
 from .journal import AllocJournal, request_key
 
 
@@ -78,6 +82,8 @@ class AllocatorOptions:
     # background patcher lands the annotation (retrying); the claim blocks re-matching until it
     # has. False = the reference's synchronous PATCH inside Allocate (allocate.go:132-152).
     async_patch: bool = False
+    # "cu": per-pod CU-slot masks (alloc/cuslots.py); "none": pods time-slice the whole GPU
+    compute_isolation: str = "none"
 
 
 @dataclasses.dataclass
@@ -88,6 +94,7 @@ class _Claim:
     next_container: int
     gpu_containers: list   # indices of containers that request gpu-mem
     t: float
+    slots: cuslots.SlotRun | None = None
 
 
 class Allocator:
@@ -102,6 +109,8 @@ class Allocator:
         self._unpatched: set[str] = set()         # assigned locally, PATCH not yet acknowledged
         self._pinfo: dict[tuple, tuple] = {}      # memoised per-pod-version facts (see _info)
         self._patch_q = None
+        self._slot_mu = threading.Lock()
+        self._slot_pending: dict[str, tuple] = {}  # uid -> (gpu, SlotRun, t): chosen, not yet on the pod
         self.journal = AllocJournal(self.opts.journal_path, self.opts.journal_ttl_s)
         if self.opts.async_patch:
             import queue
@@ -198,7 +207,7 @@ class Allocator:
     # response building
     # ------------------------------------------------------------------------------------
     def _container_response(self, gpu_index: int, pod_units: int, ctr_units: int, pod_uid: str,
-                            slot: int) -> api.ContainerAllocateResponse:
+                            slot: int, cu: cuslots.SlotRun | None = None) -> api.ContainerAllocateResponse:
         g = self.model.gpu(gpu_index)
         envs = {
             const.ENV_RESOURCE_INDEX: str(gpu_index),
@@ -212,6 +221,13 @@ class Allocator:
             r.envs[const.ENV_CGPU_DISABLE] = "true"
         if self.opts.rocr_visible:
             r.envs[const.ENV_ROCR_VISIBLE] = g.uuid
+        if cu is not None:
+            # the container sees only this GPU when its render node is the one handed out
+            single = self.opts.expose_devices or self.opts.rocr_visible
+            r.envs[const.ENV_HSA_CU_MASK] = cuslots.hsa_cu_mask(cu, g.num_xcc, 0 if single else gpu_index)
+            if single:
+                r.envs[const.ENV_ROC_CU_MASK] = cuslots.roc_cu_mask(cu, g.num_xcc)
+            r.envs[const.ENV_CU_SLOTS] = cu.annotation()
         if self.opts.expose_devices:
             r.devices.add(container_path=const.KFD_DEVICE, host_path=const.KFD_DEVICE, permissions="rw")
             if g.render_node:
@@ -226,6 +242,45 @@ class Allocator:
                              read_only=False)
                 r.envs[const.ENV_SHIM_LEDGER_DIR] = const.LEDGER_CONTAINER_DIR
         return r
+
+    def _plan_slots(self, claim: _Claim, pod_units: int) -> cuslots.SlotRun | None:
+        """CU-slot run for a matched pod (compute isolation), chosen against the runs the GPU's
+        other live pods hold plus the choices not yet visible on a pod (patch in flight)."""
+        g = self.model.gpu(claim.gpu_index)
+        if (self.opts.compute_isolation != "cu" or self.opts.disable_cgpu or g is None or g.num_xcc <= 1
+                or g.num_cu < g.num_xcc):
+            return None
+        if claim.slots is not None:
+            return claim.slots
+        nslots = g.num_cu // g.num_xcc
+        req = O.annotations(claim.pod).get(const.POD_ANNOTATION_CU_SLOTS_REQUEST)
+        k = cuslots.wanted_slots(pod_units, g.units, nslots, req)
+        try:
+            pods = A.dedupe_by_uid(self.pods.node_pods(), self.node)
+        except Exception as e:  # noqa: BLE001 - a cache failure must not fail the admission
+            log.warning("compute isolation: cannot list pods (%s); pod %s shares the whole GPU", e, O.name(claim.pod))
+            return None
+        with self._slot_mu:
+            now = time.monotonic()
+            for u, (_, _, t) in list(self._slot_pending.items()):
+                if now - t > self.opts.claim_ttl_s and u not in self._unpatched:
+                    del self._slot_pending[u]
+            held = cuslots.held_runs([p for p in pods if O.uid(p) not in self._slot_pending], claim.gpu_index,
+                                     exclude_uid=claim.uid)
+            held += [r for u, (gi, r, _) in self._slot_pending.items() if gi == claim.gpu_index and u != claim.uid]
+            run, exclusive = cuslots.choose(held, k, nslots)
+            self._slot_pending[claim.uid] = (claim.gpu_index, run, now)
+        claim.slots = run
+        if not exclusive:
+            self.metrics.allocate_outcomes.inc(outcome="cu_shared")
+            log.warning("compute isolation: GPU %d has no free run of %d CU slots; pod %s shares slots %s",
+                        claim.gpu_index, k, O.name(claim.pod), run.annotation())
+        return run
+
+    def _drop_slots(self, uid: str) -> None:
+        """The pod now carries its slot annotation (or is gone): stop tracking it locally."""
+        with self._slot_mu:
+            self._slot_pending.pop(uid, None)
 
     def _err_response(self, req, pod_units: int) -> api.AllocateResponse:
         """``buildErrResponse`` (``allocate.go:25-40``) minus the NVIDIA env: no device node is
@@ -298,11 +353,12 @@ class Allocator:
             return self._err_response(req, pod_units)
 
         pod_total = O.gpu_mem_of_pod(claim.pod)
+        cu = self._plan_slots(claim, pod_total)
         resp = api.AllocateResponse()
         slot0 = claim.next_container - len(req.container_requests)
         for i, creq in enumerate(req.container_requests):
             resp.container_responses.append(self._container_response(idx, pod_total, len(creq.devices_ids),
-                                                                     claim.uid, max(0, slot0 + i)))
+                                                                     claim.uid, max(0, slot0 + i), cu))
         if not complete:
             log.info("pod %s: container %d/%d of a multi-container pod allocated on GPU %d", O.name(claim.pod),
                      claim.next_container, len(claim.gpu_containers), idx)
@@ -330,6 +386,7 @@ class Allocator:
             log.warning("Failed due to %s", e)
             with self._mu:
                 self._claims.pop(claim.uid, None)
+            self._drop_slots(claim.uid)
             return self._err_response(req, pod_units)
         t4 = time.perf_counter()
         with self._mu:
@@ -337,6 +394,7 @@ class Allocator:
             self._assigned[claim.uid] = time.monotonic()
         if updated:
             self.pods.observe(updated)
+            self._drop_slots(claim.uid)
         self.journal.record(req, claim.uid, resp, jkey)
         hist.observe(t4 - t3, phase="patch")
         hist.observe(time.perf_counter() - t0, phase="total")
@@ -377,9 +435,11 @@ class Allocator:
                     updated = self._patch_assigned(pod)
                     if updated:
                         self.pods.observe(updated)
+                        self._drop_slots(O.uid(pod))
                     break
                 except APIError as e:
                     if e.not_found:
+                        self._drop_slots(O.uid(pod))
                         break
                     log.warning("assign patch for %s failed (%s); retrying", O.name(pod), e)
                 except Exception as e:  # noqa: BLE001 - transport errors
@@ -404,6 +464,10 @@ class Allocator:
         if self.client is None:
             return None
         patch = A.assigned_patch()
+        with self._slot_mu:
+            pend = self._slot_pending.get(O.uid(pod))
+        if pend is not None:
+            patch["metadata"]["annotations"][const.POD_ANNOTATION_CU_SLOTS] = pend[1].annotation()
         ns, nm = O.namespace(pod), O.name(pod)
         try:
             return self.client.patch_pod(ns, nm, patch)

@@ -74,6 +74,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--journal-path", default=None,
                    help="persist recent Allocate decisions (JSON lines) so a retried admission of an "
                         "already-assigned, still-Pending pod is answered identically across plugin restarts")
+    p.add_argument("--compute-isolation", default="none", choices=("none", "cu"),
+                   help="cu: give every shared pod its own run of CU slots (one CU per XCD each, sized by "
+                        "its HBM share) through HSA_CU_MASK / ROC_GLOBAL_CU_MASK; none: time-slice the whole GPU")
     p.add_argument("--no-swap-completion", action="store_true",
                    help="reference behaviour: fail a pod whose equal-size twin was admitted first "
                         "under its reservation instead of exchanging their GPUs")
@@ -102,7 +105,7 @@ def config_from_args(a) -> PluginConfig:
         rocr_visible=a.rocr_visible_devices, metrics_addr=a.metrics_addr, mps=_bool(a.mps),
         async_patch=not a.sync_patch, complete_swaps=not a.no_swap_completion,
         partition_aware=a.partition_aware, ledger_dir=a.ledger_dir, ledger_scan_s=a.ledger_scan_interval,
-        journal_path=a.journal_path)
+        journal_path=a.journal_path, compute_isolation=a.compute_isolation)
 
 
 def install_shim(dest_dir: str) -> str:

@@ -66,6 +66,12 @@ ENV_SHIM_LEDGER_DIR = "GPUSHARE_LEDGER_DIR"    # file-backed ledgers in a host-m
 LEDGER_CONTAINER_DIR = "/run/gpushare/ledger"
 ENV_GPU_UUID = "GPUSHARE_GPU_UUID"            # the physical GPU a container was given
 ENV_ROCR_VISIBLE = "ROCR_VISIBLE_DEVICES"
+# Compute isolation (--compute-isolation=cu, alloc/cuslots.py): queue CU masks read by ROCr / HIP.
+ENV_HSA_CU_MASK = "HSA_CU_MASK"
+ENV_ROC_CU_MASK = "ROC_GLOBAL_CU_MASK"
+ENV_CU_SLOTS = "GPUSHARE_CU_SLOTS"              # the slot run, for the workload's information
+POD_ANNOTATION_CU_SLOTS = "gpushare.amd.com/cu-slots"                  # written by the plugin
+POD_ANNOTATION_CU_SLOTS_REQUEST = "gpushare.amd.com/cu-slots-request"  # optional, set by the user
 # Node annotation carrying the exported xGMI topology (JSON, see parallel/topology.py).
 NODE_ANNOTATION_TOPOLOGY = "gpushare.amd.com/xgmi-topology"
 NODE_ANNOTATION_HEALTH = "gpushare.amd.com/gpu-health"

@@ -58,6 +58,8 @@ class PhysicalGPU:
     reason: str = ""
     socket: int = -1        # physical package (same-socket partitions share it)
     partition: int = 0      # partition index within the socket
+    num_xcc: int = 1        # XCDs in this (partition of the) device: 8 on an SPX MI355X
+    num_cu: int = 0         # active compute units (256 on an SPX MI355X)
 
     @property
     def render_node(self) -> str | None:
@@ -111,7 +113,8 @@ class DeviceModel:
             self.gpus.append(PhysicalGPU(index=new_idx, uuid=g.uuid, vram_bytes=vram[g.index], units=u,
                                          numa_node=g.numa_node, render_minor=g.render_minor, bdf=g.bdf,
                                          name=g.name, healthy=g.health == 0, socket=sockets[g.index],
-                                         partition=part_idx[g.index]))
+                                         partition=part_idx[g.index], num_xcc=max(1, g.num_xcc),
+                                         num_cu=g.num_cu))
         total = sum(g.units for g in self.gpus)
         if total > U.MAX_FAKE_DEVICES_PER_NODE:
             raise ValueError(f"{total} fake devices exceed the ListAndWatch limit "

@@ -60,18 +60,29 @@ def main(argv=None):
     n = 0
     tokens = a.batch * a.seq
     last = t0
+    lat = []
     while time.perf_counter() - t0 < a.seconds:
+        ti = time.perf_counter()
         model.forward(tok)
         torch.cuda.synchronize()
         n += 1
         now = time.perf_counter()
+        lat.append(now - ti)
         if now - last > 5.0:
             emit(event="progress", iters=n, tokens_per_s=n * tokens / (now - t0))
             last = now
     dt = time.perf_counter() - t0
     flops = model.flops_per_token(a.seq) * tokens * n
+    lat.sort()
+
+    def q(f):
+        return round(lat[min(len(lat) - 1, int(f * (len(lat) - 1) + 0.5))] * 1e3, 2) if lat else None
+
     emit(event="done", iters=n, seconds=dt, tokens_per_s=n * tokens / dt, tflops=flops / dt / 1e12,
-         peak_mem=torch.cuda.max_memory_allocated())
+         peak_mem=torch.cuda.max_memory_allocated(), lat_p50_ms=q(0.5), lat_p99_ms=q(0.99),
+         lat_max_ms=round(lat[-1] * 1e3, 2) if lat else None,
+         cus=torch.cuda.get_device_properties(0).multi_processor_count,
+         cu_slots=os.environ.get("GPUSHARE_CU_SLOTS"))
     return 0
 
 

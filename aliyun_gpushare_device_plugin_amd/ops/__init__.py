@@ -3,3 +3,4 @@ from .gemm import (deinterleave_gate_up, gemm_nt, interleave_gate_up, linear, li
                    linear_swiglu)
 from .fused import rmsnorm, rope_, rope_tables, silu_mul  # noqa: F401
 from .attention import attention, reference_attention  # noqa: F401
+from .census import cu_census  # noqa: F401

@@ -69,6 +69,7 @@ class PluginConfig:
     ledger_dir: str | None = None        # host dir for file-backed shim ledgers (usage metrics)
     ledger_scan_s: float = 10.0
     journal_path: str | None = None      # persisted allocation journal (alloc/journal.py)
+    compute_isolation: str = "none"      # "cu": per-pod CU-slot masks (alloc/cuslots.py)
     mps: bool = False                    # accepted for flag compatibility; ignored
 
 
@@ -154,7 +155,8 @@ class SharedGPUManager:
                                                rocr_visible=cfg.rocr_visible, async_patch=cfg.async_patch,
                                                complete_swaps=cfg.complete_swaps,
                                                ledger_dir=cfg.ledger_dir if shim else None,
-                                               journal_path=cfg.journal_path),
+                                               journal_path=cfg.journal_path,
+                                               compute_isolation=cfg.compute_isolation),
                               self.metrics)
         self.model = model
         return DevicePluginServer(model, allocator, self._plugin_socket(), const.RESOURCE_NAME,

@@ -30,13 +30,14 @@ from .kubelet import Admission, FakeKubelet
 
 
 def pod_spec(name: str, gpu_mem, namespace: str = "default", labels: dict | None = None,
-             image: str = "rocm/pytorch:latest") -> dict:
+             image: str = "rocm/pytorch:latest", annotations: dict | None = None) -> dict:
     """A pod with one container per entry of ``gpu_mem`` (int → single container)."""
     mems = [gpu_mem] if isinstance(gpu_mem, int) else list(gpu_mem)
     ctrs = [{"name": f"c{i}", "image": image,
              "resources": {"limits": {const.RESOURCE_NAME: str(m)}} if m else {}} for i, m in enumerate(mems)]
     return {"apiVersion": "v1", "kind": "Pod",
-            "metadata": {"name": name, "namespace": namespace, "labels": dict(labels or {})},
+            "metadata": {"name": name, "namespace": namespace, "labels": dict(labels or {}),
+                         **({"annotations": dict(annotations)} if annotations else {})},
             "spec": {"containers": ctrs, "schedulerName": "default-scheduler"}}
 
 
@@ -56,8 +57,9 @@ class SimCluster:
                  pod_source: str = "watch", apiserver_latency_s: float = 0.0, shim_host_dir: str | None = None,
                  gpu_indices: list[int] | None = None, health_poll_s: float = 1.0, round_policy: str = "nearest",
                  extra_plugin_args: list[str] | None = None, apiserver: str = "thread",
-                 preferred_allocation: bool = False):
+                 preferred_allocation: bool = False, compute_isolation: str = "none"):
         self.node_specs = nodes
+        self.compute_isolation = compute_isolation
         self._own_dir = workdir is None
         # short paths: UDS paths are limited to 108 bytes
         self.workdir = workdir or tempfile.mkdtemp(prefix="gs-", dir="/tmp")
@@ -132,7 +134,8 @@ class SimCluster:
                             apiserver=self.api_url, pod_source=self.pod_source,
                             shim_host_dir=self.shim_host_dir, gpu_indices=self.gpu_indices,
                             health_poll_s=self.health_poll_s, round_policy=self.round_policy,
-                            preferred_allocation=self.preferred_allocation, **self._kubelet_cfg(node))
+                            preferred_allocation=self.preferred_allocation,
+                            compute_isolation=self.compute_isolation, **self._kubelet_cfg(node))
 
     def _kubelet_cfg(self, node: SimNode) -> dict:
         if self.pod_source != "kubelet":
@@ -153,6 +156,8 @@ class SimCluster:
                 args += ["--gpu-indices", ",".join(map(str, self.gpu_indices))]
             if self.preferred_allocation:
                 args += ["--preferred-allocation"]
+            if self.compute_isolation != "none":
+                args += ["--compute-isolation", self.compute_isolation]
             for k, v in self._kubelet_cfg(node).items():
                 args += ["--" + k.replace("_", "-"), str(v)]
             args += self.extra_plugin_args
@@ -205,8 +210,10 @@ class SimCluster:
         self.stop()
 
     # -- pod flow -------------------------------------------------------------------------
-    def create_pod(self, gpu_mem, name: str | None = None, labels: dict | None = None) -> dict:
-        return self.client.create_pod("default", pod_spec(name or f"pod-{next(self._seq)}", gpu_mem, labels=labels))
+    def create_pod(self, gpu_mem, name: str | None = None, labels: dict | None = None,
+                   annotations: dict | None = None) -> dict:
+        return self.client.create_pod("default", pod_spec(name or f"pod-{next(self._seq)}", gpu_mem, labels=labels,
+                                                          annotations=annotations))
 
     def schedule(self, pod: dict):
         return self.extender.schedule(pod)
@@ -240,8 +247,9 @@ class SimCluster:
         """Wait for asynchronous status updates."""
         self._bg.submit(lambda: None).result()
 
-    def run_pod(self, gpu_mem, name: str | None = None, labels: dict | None = None):
-        pod = self.create_pod(gpu_mem, name, labels)
+    def run_pod(self, gpu_mem, name: str | None = None, labels: dict | None = None,
+                annotations: dict | None = None):
+        pod = self.create_pod(gpu_mem, name, labels, annotations)
         placed = self.schedule(pod)
         if placed is None:
             return pod, None, None

@@ -7,8 +7,13 @@
 2. Each pod runs as its own process with exactly that environment (the shim's container path is
    mapped back through the response's mount) and runs Llama-3-8B prefill.
 3. Phase "solo": pod A alone. Phase "colocated": A and B together (synchronized start).
-Reports tokens/s solo vs co-located (interference), the quota each pod saw, and whether an
-over-quota allocation was refused. Output: one JSON line (and --out).
+Reports tokens/s solo vs co-located (interference), per-iteration latency p50/p99, the quota each
+pod saw, and whether an over-quota allocation was refused. Output: one JSON line (and --out).
+
+``--isolation cu`` admits the pods with the plugin's ``--compute-isolation=cu`` (each pod requests
+``--slots-a`` / ``--slots-b`` CU slots, i.e. 8 CUs per slot, one per XCD); ``both`` runs the
+experiment under time-slicing and under CU slots back to back. ``--batch-b`` makes B a heavier
+neighbour than A (A = latency-sensitive tenant).
 """
 import argparse
 import json
@@ -56,6 +61,7 @@ def run_pods(specs, seconds, args, sync=True):
                     d = json.loads(line)
                     lines[i].append(d)
                     q.put((i, d))
+                    print(f"[{specs[i][0]}] {line.strip()[:200]}", file=sys.stderr, flush=True)   # progress for long runs
             q.put((i, None))
 
         def drain(i=i, p=p):
@@ -87,30 +93,31 @@ def run_pods(specs, seconds, args, sync=True):
     return [lines[i] for i in range(len(procs))]
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--pod-gib", type=int, default=64)
-    ap.add_argument("--seconds", type=float, default=20)
-    ap.add_argument("--batch", type=int, default=4)
-    ap.add_argument("--seq", type=int, default=2048)
-    ap.add_argument("--layers", type=int, default=32)
-    ap.add_argument("--smi-backend", default="auto")
-    ap.add_argument("--out", default=None)
-    args = ap.parse_args()
-
+def admit_pair(args, isolation: str):
+    """Admit pods A and B through the real plugin; returns their pod environments + Allocate ms."""
+    from aliyun_gpushare_device_plugin_amd import const
     from aliyun_gpushare_device_plugin_amd.sim.cluster import SimCluster
     from aliyun_gpushare_device_plugin_amd.utils.native import ensure_built
 
     shim_dir = os.path.dirname(ensure_built("hipshim"))
-    with SimCluster([("mi355x", args.smi_backend)], shim_host_dir=shim_dir) as c:
-        pa, wa, adm_a = c.run_pod(args.pod_gib, name="llama-a")
-        pb, wb, adm_b = c.run_pod(args.pod_gib, name="llama-b")
+    ann = [None, None]
+    if isolation == "cu":
+        ann = [{const.POD_ANNOTATION_CU_SLOTS_REQUEST: str(args.slots_a)},
+               {const.POD_ANNOTATION_CU_SLOTS_REQUEST: str(args.slots_b)}]
+    with SimCluster([("mi355x", args.smi_backend)], shim_host_dir=shim_dir, compute_isolation=isolation) as c:
+        pa, wa, adm_a = c.run_pod(args.pod_gib, name="llama-a", annotations=ann[0])
+        pb, wb, adm_b = c.run_pod(args.pod_gib, name="llama-b", annotations=ann[1])
         assert adm_a.error is None and adm_b.error is None and wa[1] == wb[1]
-        env_a, env_b = pod_env(adm_a.responses[0]), pod_env(adm_b.responses[0])
-        alloc_ms = [x * 1e3 for x in adm_a.latencies + adm_b.latencies]
+        return (pod_env(adm_a.responses[0]), pod_env(adm_b.responses[0]),
+                [x * 1e3 for x in adm_a.latencies + adm_b.latencies])
 
+
+def run_mode(args, isolation: str) -> dict:
+    env_a, env_b, alloc_ms = admit_pair(args, isolation)
+    extra_b = ["--batch", str(args.batch_b)] if args.batch_b else []
     solo = run_pods([("llama-a", env_a, ["--probe-quota"])], args.seconds, args)[0]
-    both = run_pods([("llama-a", env_a, []), ("llama-b", env_b, [])], args.seconds, args)
+    both = run_pods([("llama-a", env_a, []), ("llama-b", env_b, extra_b)], args.seconds, args)
+    solo_b = run_pods([("llama-b", env_b, extra_b)], args.seconds, args)[0] if args.batch_b else None
 
     def done(ls):
         return [x for x in ls if x["event"] == "done"][0]
@@ -120,20 +127,58 @@ def main():
 
     s = done(solo)
     ca, cb = done(both[0]), done(both[1])
+    sb = done(solo_b) if solo_b else s
     probe = [x for x in solo if x["event"] == "quota_probe"]
-    res = {
-        "config": "2 x Llama-3-8B bf16 pods on one MI355X (BASELINE config 4)",
-        "pod_gib": args.pod_gib, "batch": args.batch, "seq": args.seq, "layers": args.layers,
+    return {
+        "isolation": isolation,
+        "cu_slots": [env_a.get("GPUSHARE_CU_SLOTS"), env_b.get("GPUSHARE_CU_SLOTS")],
+        "hsa_cu_mask": [env_a.get("HSA_CU_MASK"), env_b.get("HSA_CU_MASK")],
+        "cus_seen": [ca["cus"], cb["cus"]],
         "allocate_ms": [round(x, 3) for x in alloc_ms],
         "quota_bytes_seen": start(solo)["quota_total"],
         "over_quota_alloc": probe[0]["over_quota_alloc"] if probe else None,
         "solo_tokens_per_s": round(s["tokens_per_s"], 1), "solo_tflops": round(s["tflops"], 1),
+        "solo_b_tokens_per_s": round(sb["tokens_per_s"], 1),
+        "solo_lat_ms": [s["lat_p50_ms"], s["lat_p99_ms"]],
         "colocated_tokens_per_s": [round(ca["tokens_per_s"], 1), round(cb["tokens_per_s"], 1)],
         "colocated_sum_tokens_per_s": round(ca["tokens_per_s"] + cb["tokens_per_s"], 1),
+        "colocated_lat_ms_a": [ca["lat_p50_ms"], ca["lat_p99_ms"], ca["lat_max_ms"]],
+        "colocated_lat_ms_b": [cb["lat_p50_ms"], cb["lat_p99_ms"], cb["lat_max_ms"]],
+        # pod A's throughput with B running, relative to A alone under the same policy
+        "a_retained": round(ca["tokens_per_s"] / s["tokens_per_s"], 3),
+        "b_retained": round(cb["tokens_per_s"] / sb["tokens_per_s"], 3),
         "interference": round((ca["tokens_per_s"] + cb["tokens_per_s"]) / 2 / s["tokens_per_s"], 3),
         "aggregate_speedup_vs_solo": round((ca["tokens_per_s"] + cb["tokens_per_s"]) / s["tokens_per_s"], 3),
         "peak_mem_bytes": [ca["peak_mem"], cb["peak_mem"]],
     }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--pod-gib", type=int, default=64)
+    ap.add_argument("--seconds", type=float, default=20)
+    ap.add_argument("--batch", type=int, default=4)
+    ap.add_argument("--batch-b", type=int, default=0, help="pod B's batch (0 = same as A); B then also runs solo")
+    ap.add_argument("--seq", type=int, default=2048)
+    ap.add_argument("--layers", type=int, default=32)
+    ap.add_argument("--smi-backend", default="auto")
+    ap.add_argument("--isolation", default="none", choices=("none", "cu", "both"),
+                    help="plugin --compute-isolation for the pods; both = run the experiment under each")
+    ap.add_argument("--slots-a", type=int, default=16, help="CU slots pod A requests (cu isolation)")
+    ap.add_argument("--slots-b", type=int, default=16)
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+
+    modes = ["none", "cu"] if args.isolation == "both" else [args.isolation]
+    res = {"config": "2 x Llama-3-8B bf16 pods on one MI355X (BASELINE config 4)",
+           "pod_gib": args.pod_gib, "batch": args.batch, "batch_b": args.batch_b or args.batch, "seq": args.seq,
+           "layers": args.layers}
+    for m in modes:
+        r = run_mode(args, m)
+        print(json.dumps(r), flush=True)
+        res[m] = r
+    if len(modes) == 1:
+        res.update(res.pop(modes[0]))
     line = json.dumps(res)
     print(line)
     if args.out:
