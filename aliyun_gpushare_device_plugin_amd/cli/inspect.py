@@ -213,7 +213,30 @@ def display_topology(infos: list[NodeInfo]) -> str:
                 row += ("Healthy" if h.get("healthy", True) else f"Unhealthy({h.get('reason', '')})") + "\n"
                 w.write(row)
             out.append(w.flush())
+        slots = cu_slot_rows(info)
+        if slots:
+            out.append("CU SLOTS (--compute-isolation=cu; slot s = CU s of every XCD)\n" + slots)
     return "\n".join(out) + "\n"
+
+
+def cu_slot_rows(info: NodeInfo) -> str:
+    """Per GPU: the CU-slot run each active pod holds (``gpushare.amd.com/cu-slots``)."""
+    from ..alloc.cuslots import SlotRun
+
+    per: dict[int, list] = {}
+    for p in info.pods:
+        r = SlotRun.parse(O.annotations(p).get(const.POD_ANNOTATION_CU_SLOTS))
+        if r is None:
+            continue
+        per.setdefault(A.gpu_id_from_annotation(p), []).append((r.start, r, O.name(p)))
+    if not per:
+        return ""
+    w = TabWriter()
+    w.write("GPU\tSLOTS\tPOD\n")
+    for g in sorted(per):
+        for _, r, name in sorted(per[g]):
+            w.write(f"GPU{g}\t{r.annotation()}\t{name}\n")
+    return w.flush()
 
 
 def active_pods(pods: list[dict]) -> list[dict]:

@@ -66,3 +66,17 @@ def test_render_against_live_fake_cluster():
         topo = I.render(c.client, topology=True)
         assert "XGMI1" in topo and "Healthy" in topo
         assert I.main(["--apiserver", c.api_url]) == 0
+
+
+def test_topology_view_lists_cu_slots():
+    from aliyun_gpushare_device_plugin_amd.sim.cluster import SimCluster
+    with SimCluster([("node-a", "fake:1x309220868096B")], compute_isolation="cu") as c:
+        pa, _, _ = c.run_pod(128, name="big")
+        pb, _, _ = c.run_pod(64, name="small")
+        c.wait_assigned(pa)
+        c.wait_assigned(pb)
+        topo = I.render(c.client, topology=True)
+        assert "CU SLOTS" in topo
+        rows = [line.split() for line in topo.splitlines() if line.startswith("GPU0 ") and "-" in line]
+        assert ["GPU0", "0-13", "big"] in rows and ["GPU0", "14-20", "small"] in rows
+        assert "CU SLOTS" not in I.render(c.client, topology=False)
