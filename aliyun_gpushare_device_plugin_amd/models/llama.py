@@ -87,9 +87,11 @@ class LlamaModel:
         return 2 * n
 
     @torch.no_grad()
-    def forward(self, tokens: torch.Tensor, logits: str = "last") -> torch.Tensor:
+    def forward(self, tokens: torch.Tensor, logits: str = "last", kv_sink=None) -> torch.Tensor:
         """Prefill forward. ``tokens`` [B, S] int64. Returns logits [B, vocab] for the last
-        position (``logits="last"``) or [B, S, vocab] (``"all"``)."""
+        position (``logits="last"``) or [B, S, vocab] (``"all"``). ``kv_sink(layer, k, v)`` receives
+        each layer's post-RoPE K and V as [B, S, Hkv, D] views (the serving path fills its KV
+        cache from them)."""
         c = self.cfg
         B, S = tokens.shape
         if S > c.max_seq:
@@ -105,6 +107,8 @@ class LlamaModel:
             q, k, v = qkv[:, :hq], qkv[:, hq:hq + hk], qkv[:, hq + hk:]
             ops.rope_(q, self.cos, self.sin, c.n_heads, c.head_dim, S)
             ops.rope_(k, self.cos, self.sin, c.n_kv_heads, c.head_dim, S)
+            if kv_sink is not None:
+                kv_sink(i, k.view(B, S, c.n_kv_heads, c.head_dim), v.view(B, S, c.n_kv_heads, c.head_dim))
             a = ops.attention(q.view(B, S, c.n_heads, c.head_dim), k.view(B, S, c.n_kv_heads, c.head_dim),
                               v.view(B, S, c.n_kv_heads, c.head_dim), causal=True)
             h = ops.linear(a.reshape(T, hq), L["wo"], residual=h)   # fused residual add

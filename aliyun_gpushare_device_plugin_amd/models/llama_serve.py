@@ -1,0 +1,120 @@
+"""Serving pod workload: Llama-3-8B prefill into a KV cache, then greedy decode, one hipGraph per step.
+
+A GPU-sharing node mostly hosts inference servers, and their decode loop is the workload that
+suffers most from a noisy neighbour: every step is ~35 small launches per layer's worth of
+memory-bound work. The decode step here is built for that:
+
+* KV cache ``[B, Hkv, Smax, 128]`` per layer (``ops.kv_cache``), filled by the prefill through
+  ``LlamaModel.forward(kv_sink=...)`` and appended to by ``ops.kv_append``;
+* attention = ``ops.decode_attention`` (split-K over the cache, ``native/kernels/decode_attention.hip``);
+  RMSNorm, RoPE and SiLU·up on the hand-written kernels; the skinny projections (M = batch) on
+  hipBLASLt through ``torch.matmul`` / ``torch.addmm`` (residual folded into ``addmm``'s beta);
+* positions / lengths live in device tensors, so the whole 32-layer step is captured once in a
+  hipGraph (``torch.cuda.CUDAGraph``) and replayed: one launch per step instead of ~450.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import ops
+from .llama import LlamaModel
+
+
+class LlamaServer:
+    def __init__(self, model: LlamaModel, batch: int, max_ctx: int):
+        c = self.cfg = model.cfg
+        if max_ctx > c.max_seq:
+            raise ValueError("max_ctx exceeds the RoPE table (cfg.max_seq)")
+        self.model, self.B = model, batch
+        dev = model.device
+        self.kc, self.vc = [], []
+        for _ in range(c.n_layers):
+            k, v = ops.kv_cache(batch, c.n_kv_heads, max_ctx, c.head_dim, dev)
+            self.kc.append(k)
+            self.vc.append(v)
+        self.smax = self.kc[0].shape[2]
+        self.max_ctx = max_ctx
+        self.ws = ops.DecodeWorkspace(batch, c.n_heads, self.smax, c.head_dim, dev)
+        self.tok = torch.zeros(batch, dtype=torch.long, device=dev)      # next input token per sequence
+        self.pos = torch.zeros(batch, dtype=torch.int32, device=dev)     # its position (= cached length)
+        self.lens = torch.zeros(batch, dtype=torch.int32, device=dev)    # cached length incl. the new token
+        self.host_len = 0                                                # same, tracked on the host
+        self.graph = None
+        self.logits = None
+
+    def kv_bytes(self) -> int:
+        return 2 * sum(t.numel() for t in self.kc)
+
+    @torch.no_grad()
+    def prefill(self, tokens: torch.Tensor) -> torch.Tensor:
+        """Run the prompt ``tokens`` [B, S] through the model, fill the caches, return the last
+        logits and set up the first decode input (greedy)."""
+        B, S = tokens.shape
+        if B != self.B or S >= self.max_ctx:
+            raise ValueError("prompt does not fit the server's batch / context")
+
+        def sink(i, k, v):
+            self.kc[i][:, :, :S].copy_(k.transpose(1, 2))
+            self.vc[i][:, :, :S].copy_(v.transpose(1, 2))
+
+        logits = self.model.forward(tokens, kv_sink=sink)
+        self.tok.copy_(logits.argmax(-1))
+        self.pos.fill_(S)
+        self.host_len = S
+        return logits
+
+    @torch.no_grad()
+    def _step(self) -> torch.Tensor:
+        c, m, B = self.cfg, self.model, self.B
+        hq, hk = c.n_heads * c.head_dim, c.n_kv_heads * c.head_dim
+        torch.add(self.pos, 1, out=self.lens)
+        h = m.embed.index_select(0, self.tok)                          # residual stream [B, d]
+        x = ops.rmsnorm(h, m.layers[0]["attn_norm"], c.eps)
+        for i, L in enumerate(m.layers):
+            qkv = torch.matmul(x, L["wqkv"].t())
+            q, k, v = qkv[:, :hq], qkv[:, hq:hq + hk], qkv[:, hq + hk:]
+            ops.rope_(q, m.cos, m.sin, c.n_heads, c.head_dim, c.max_seq, positions=self.pos, validate=False)
+            ops.rope_(k, m.cos, m.sin, c.n_kv_heads, c.head_dim, c.max_seq, positions=self.pos, validate=False)
+            ops.kv_append(k, v, self.kc[i], self.vc[i], self.pos)
+            a = ops.decode_attention(q, self.kc[i], self.vc[i], self.lens, self.ws)
+            h = torch.addmm(h, a, L["wo"].t())
+            x = ops.rmsnorm(h, L["mlp_norm"], c.eps)
+            gu = torch.matmul(x, L["wgu"].t())                          # gate/up rows interleaved by 16
+            act = ops.silu_mul(gu.view(B, -1, 2, 16).transpose(1, 2).reshape(B, -1))
+            h = torch.addmm(h, act, L["wd"].t())
+            nxt = m.layers[i + 1]["attn_norm"] if i + 1 < len(m.layers) else m.final_norm
+            x = ops.rmsnorm(h, nxt, c.eps)
+        logits = torch.matmul(x, m.lm_head.t())
+        self.tok.copy_(logits.argmax(-1))
+        self.pos.add_(1)
+        return logits
+
+    def capture(self) -> None:
+        """Capture one decode step in a hipGraph (after a warm-up step on a side stream). The
+        warm-up and the capture advance nothing: positions are restored afterwards."""
+        save = (self.tok.clone(), self.pos.clone())
+        s = torch.cuda.Stream(self.model.device)
+        s.wait_stream(torch.cuda.current_stream(self.model.device))
+        with torch.cuda.stream(s):
+            self._step()
+        torch.cuda.current_stream(self.model.device).wait_stream(s)
+        self.tok.copy_(save[0])
+        self.pos.copy_(save[1])
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.logits = self._step()
+        self.tok.copy_(save[0])
+        self.pos.copy_(save[1])
+        self.graph = g
+
+    def step(self, use_graph: bool = True) -> torch.Tensor:
+        """One greedy decode step for every sequence; returns the step's logits [B, vocab]."""
+        if self.host_len + 1 > self.max_ctx:
+            raise RuntimeError("context full")
+        self.host_len += 1
+        if use_graph:
+            if self.graph is None:
+                self.capture()
+            self.graph.replay()
+            return self.logits
+        return self._step()

@@ -58,9 +58,11 @@ def rope_tables(seq_len: int, head_dim: int, theta: float = 500000.0, device="cu
 
 
 def rope_(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, nheads: int, head_dim: int,
-          seq_len: int, positions: torch.Tensor | None = None) -> torch.Tensor:
+          seq_len: int, positions: torch.Tensor | None = None, validate: bool = True) -> torch.Tensor:
     """In-place rotate-half RoPE on ``x`` viewed as ``[T, nheads, head_dim]`` with token
-    stride ``x.stride(-2)`` (so q/k slices of a fused qkv buffer work without copies)."""
+    stride ``x.stride(-2)`` (so q/k slices of a fused qkv buffer work without copies).
+    ``validate=False`` skips the host-side range check of ``positions`` (it synchronises), for
+    callers that guarantee the range themselves and capture the launch in a hipGraph."""
     if x.dtype != torch.bfloat16 or not x.is_cuda or x.stride(-1) != 1:
         raise ValueError("rope_: expected bf16 GPU tensor with contiguous last dim")
     if head_dim % 8 or cos.dim() != 2 or cos.shape[0] < seq_len or cos.shape[1] != head_dim // 2 \
@@ -72,10 +74,11 @@ def rope_(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, nheads: int, he
         raise ValueError("rope_: row narrower than nheads*head_dim")
     pos = None
     if positions is not None:
-        positions = positions.to(torch.int32).contiguous()
+        if positions.dtype != torch.int32 or not positions.is_contiguous():
+            positions = positions.to(torch.int32).contiguous()
         if positions.numel() != T:
             raise ValueError("rope_: positions must have one entry per token")
-        if int(positions.max()) >= cos.shape[0] or int(positions.min()) < 0:
+        if validate and (int(positions.max()) >= cos.shape[0] or int(positions.min()) < 0):
             raise ValueError("rope_: position outside the table")
         pos = positions.data_ptr()
     rc = _lib.lib().gs_rope_bf16(x2.data_ptr(), cos.data_ptr(), sin.data_ptr(), pos, T, nheads, head_dim, stride,

@@ -1,0 +1,228 @@
+// Decode-phase GQA attention over a KV cache (split-K, "flash-decoding"), plus the KV append.
+//
+// Serving pods decode one token per sequence per step, so attention reads the whole KV cache
+// once and does ~1 FLOP/byte: it is HBM-bound and the job is to stream K and V at full
+// bandwidth with enough workgroups in flight. Layout and schedule:
+//   * cache [B, Hkv, Smax, D=128] bf16: one (sequence, kv head) is a contiguous Smax x 256 B
+//     slab, so a chunk of positions is one contiguous stream;
+//   * grid (Smax / CHUNK, Hkv, B): a workgroup owns CHUNK = 256 positions of one (b, kv head)
+//     and all G = Hq / Hkv query heads that share it (K/V read once per group, not per head);
+//     workgroups past lens[b] exit at once, so the grid can be sized from the cache capacity
+//     and the kernel needs no host-side length (it is captured in a hipGraph once and replayed);
+//   * scores: 8 lanes per position, 16 dims (two 16-B loads) each, a wave covers 8 positions per
+//     step and the 4 waves 32: 64 lanes x 32 B = 2 KiB contiguous per wave-step; q is pre-scaled
+//     by softmax_scale * log2(e) so the softmax runs on exp2;
+//   * softmax: one wave per query head, over the CHUNK scores held in LDS;
+//   * P·V: the 4 waves take interleaved positions, 64 / G lanes per head with D * G / 64 dims each
+//     (16-B loads for G = 4), then a cross-wave LDS reduction;
+//   * partials (m, l, unnormalised o) per split go to a float workspace; a second kernel merges
+//     the splits of each (b, q head) and writes bf16.
+#include "common.h"
+
+namespace {
+
+constexpr int D = 128;
+constexpr int CHUNK = 256;
+constexpr int NT = 256;
+constexpr float LOG2E = 1.4426950408889634f;
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+template <int G>
+__global__ __launch_bounds__(NT) void decode_split(const unsigned short* __restrict__ q, int q_bstride,
+                                                   const unsigned short* __restrict__ kc,
+                                                   const unsigned short* __restrict__ vc,
+                                                   const int* __restrict__ lens, float* __restrict__ o_part,
+                                                   float* __restrict__ ml_part, int Hkv, int Smax, int nsplit,
+                                                   float qscale) {
+  constexpr int DPL = D * G / 64;         // P·V dims per lane
+  constexpr int LPH = 64 / G;             // P·V lanes per head
+  __shared__ float S[G][CHUNK];
+  __shared__ float red[4][G * D];
+  __shared__ float ML[G][2];
+
+  const int split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int len = min(lens[b], Smax);
+  const int c0 = split * CHUNK;
+  const int Hq = Hkv * G;
+  if (c0 >= len) return;                  // nothing here; the merge kernel never reads this split
+  const int n = min(CHUNK, len - c0);
+
+  const size_t slab = ((size_t)b * Hkv + kvh) * Smax;
+  const unsigned short* kp = kc + (slab + c0) * D;
+  const unsigned short* vp = vc + (slab + c0) * D;
+
+  // ---- scores ---------------------------------------------------------------------------
+  const int part = tid & 7;               // dims [16 part, 16 part + 16)
+  float qf[G][16];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const unsigned short* qh = q + (size_t)b * q_bstride + (kvh * G + g) * D + part * 16;
+    const u16x8_t q0 = *(const u16x8_t*)qh, q1 = *(const u16x8_t*)(qh + 8);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      qf[g][i] = bf16_to_f32(q0[i]) * qscale;
+      qf[g][8 + i] = bf16_to_f32(q1[i]) * qscale;
+    }
+  }
+#pragma unroll
+  for (int step = 0; step < CHUNK / 32; ++step) {
+    const int p = step * 32 + (tid >> 3);
+    float s[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) s[g] = 0.f;
+    if (p < n) {
+      const unsigned short* kr = kp + (size_t)p * D + part * 16;
+      const u16x8_t k0 = *(const u16x8_t*)kr, k1 = *(const u16x8_t*)(kr + 8);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float a = bf16_to_f32(k0[i]), c = bf16_to_f32(k1[i]);
+#pragma unroll
+        for (int g = 0; g < G; ++g) s[g] = fmaf(qf[g][i], a, fmaf(qf[g][8 + i], c, s[g]));
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      float v = s[g];
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      if (part == 0) S[g][p] = p < n ? v : -INFINITY;
+    }
+  }
+  __syncthreads();
+
+  // ---- softmax over the chunk: wave w handles heads w, w + 4, ... --------------------------
+  for (int g = wave; g < G; g += 4) {
+    float m = -INFINITY;
+#pragma unroll
+    for (int i = lane; i < CHUNK; i += 64) m = fmaxf(m, S[g][i]);
+    m = wave_max(m);
+    float l = 0.f;
+#pragma unroll
+    for (int i = lane; i < CHUNK; i += 64) {
+      const float e = i < n ? exp2f(S[g][i] - m) : 0.f;
+      S[g][i] = e;
+      l += e;
+    }
+    l = wave_sum(l);
+    if (lane == 0) {
+      ML[g][0] = m;
+      ML[g][1] = l;
+    }
+  }
+  __syncthreads();
+
+  // ---- P·V: waves take positions wave, wave + 4, ...; lane -> (head, DPL dims) --------------
+  const int g = lane / LPH, d0 = (lane % LPH) * DPL;
+  float acc[DPL];
+#pragma unroll
+  for (int i = 0; i < DPL; ++i) acc[i] = 0.f;
+#pragma unroll 4
+  for (int p = wave; p < n; p += 4) {
+    const float w = S[g][p];
+    const unsigned short* vr = vp + (size_t)p * D + d0;
+    if constexpr (DPL == 8) {
+      const u16x8_t v8 = *(const u16x8_t*)vr;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] = fmaf(w, bf16_to_f32(v8[i]), acc[i]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < DPL; ++i) acc[i] = fmaf(w, bf16_to_f32(vr[i]), acc[i]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < DPL; ++i) red[wave][g * D + d0 + i] = acc[i];
+  __syncthreads();
+  for (int e = tid; e < G * D; e += NT) {
+    const int gg = e / D, d = e % D;
+    const float o = red[0][e] + red[1][e] + red[2][e] + red[3][e];
+    const size_t row = ((size_t)b * Hq + kvh * G + gg) * nsplit + split;
+    o_part[row * D + d] = o;
+    if (d == 0) {
+      ml_part[row * 2] = ML[gg][0];
+      ml_part[row * 2 + 1] = ML[gg][1];
+    }
+  }
+}
+
+__global__ __launch_bounds__(D) void decode_merge(const float* __restrict__ o_part, const float* __restrict__ ml_part,
+                                                  const int* __restrict__ lens, unsigned short* __restrict__ out,
+                                                  int Hq, int Smax, int nsplit) {
+  const int hq = blockIdx.x, b = blockIdx.y, d = threadIdx.x;
+  const int len = min(lens[b], Smax);
+  const int ns = (len + CHUNK - 1) / CHUNK;
+  const size_t row0 = ((size_t)b * Hq + hq) * nsplit;
+  float m = -INFINITY;
+  for (int s = 0; s < ns; ++s) m = fmaxf(m, ml_part[(row0 + s) * 2]);
+  float num = 0.f, den = 0.f;
+  for (int s = 0; s < ns; ++s) {
+    const float w = exp2f(ml_part[(row0 + s) * 2] - m);
+    den = fmaf(w, ml_part[(row0 + s) * 2 + 1], den);
+    num = fmaf(w, o_part[(row0 + s) * D + d], num);
+  }
+  out[((size_t)b * Hq + hq) * D + d] = f32_to_bf16(den > 0.f ? num / den : 0.f);
+}
+
+// cache[b][h][pos[b]][:] = src[b][h * D : (h + 1) * D] for K and V; one 16-B chunk per thread.
+__global__ __launch_bounds__(256) void kv_append(const unsigned short* __restrict__ k, const unsigned short* __restrict__ v,
+                                                 int src_bstride, unsigned short* __restrict__ kc,
+                                                 unsigned short* __restrict__ vc, const int* __restrict__ pos, int B,
+                                                 int Hkv, int Smax) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;      // over B * Hkv * (D / 8) * 2
+  const int per = Hkv * (D / 8);
+  if (i >= 2 * B * per) return;
+  const int which = i / (B * per), r = i % (B * per);
+  const int b = r / per, h = (r % per) / (D / 8), c = r % (D / 8);
+  const int p = pos[b];
+  if (p < 0 || p >= Smax) return;
+  const unsigned short* src = (which ? v : k) + (size_t)b * src_bstride + h * D + c * 8;
+  unsigned short* dst = (which ? vc : kc) + ((((size_t)b * Hkv + h) * Smax + p) * D) + c * 8;
+  *(u16x8_t*)dst = *(const u16x8_t*)src;
+}
+
+}  // namespace
+
+// q: [B, Hq, D] rows at q_bstride elements per sequence (heads contiguous); caches [B, Hkv, Smax, D];
+// lens[B] (device); workspace: o_part [B, Hq, nsplit, D] f32 + ml_part [B, Hq, nsplit, 2] f32 with
+// nsplit = ceil(Smax / 256); out [B, Hq, D] bf16.
+GS_KERNEL_API int gs_decode_attn_bf16(const void* q, int q_bstride, const void* k_cache, const void* v_cache,
+                                      const int* lens, void* o_part, void* ml_part, void* out, int B, int Hq, int Hkv,
+                                      int Dh, int Smax, float scale, hipStream_t stream) {
+  if (Dh != D || B <= 0 || Hkv <= 0 || Hq % Hkv || Smax <= 0 || Smax % CHUNK || q_bstride < Hq * D || q_bstride % 8)
+    return GS_EINVAL;
+  const int G = Hq / Hkv, nsplit = Smax / CHUNK;
+  const dim3 grid(nsplit, Hkv, B);
+  const float qs = scale * LOG2E;
+  auto args = [&](auto kern) {
+    hipLaunchKernelGGL(kern, grid, dim3(NT), 0, stream, (const unsigned short*)q, q_bstride,
+                       (const unsigned short*)k_cache, (const unsigned short*)v_cache, lens, (float*)o_part,
+                       (float*)ml_part, Hkv, Smax, nsplit, qs);
+  };
+  switch (G) {
+    case 1: args(decode_split<1>); break;
+    case 2: args(decode_split<2>); break;
+    case 4: args(decode_split<4>); break;
+    case 8: args(decode_split<8>); break;
+    default: return GS_EINVAL;
+  }
+  hipLaunchKernelGGL(decode_merge, dim3(Hq, B), dim3(D), 0, stream, (const float*)o_part, (const float*)ml_part, lens,
+                     (unsigned short*)out, Hq, Smax, nsplit);
+  return gs_launch_status();
+}
+
+// k/v: [B, Hkv * D] rows at src_bstride elements (slices of the fused QKV output); pos[B] device.
+GS_KERNEL_API int gs_kv_append_bf16(const void* k, const void* v, int src_bstride, void* k_cache, void* v_cache,
+                                    const int* pos, int B, int Hkv, int Dh, int Smax, hipStream_t stream) {
+  if (Dh != D || B <= 0 || Hkv <= 0 || Smax <= 0 || src_bstride < Hkv * D || src_bstride % 8) return GS_EINVAL;
+  const int n = 2 * B * Hkv * (D / 8);
+  hipLaunchKernelGGL(kv_append, dim3((n + 255) / 256), dim3(256), 0, stream, (const unsigned short*)k,
+                     (const unsigned short*)v, src_bstride, (unsigned short*)k_cache, (unsigned short*)v_cache, pos, B,
+                     Hkv, Smax);
+  return gs_launch_status();
+}

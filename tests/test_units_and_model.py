@@ -111,3 +111,20 @@ def test_partition_aware_keeps_nps_split_memory():
     assert [g.units for g in DeviceModel(devs, const.GIB).gpus] == [144, 144]
     spx = [gpu(i) for i in range(8)]                         # SPX: one device per socket
     assert DeviceModel(spx, const.GIB).total_units() == 8 * 288
+
+
+def test_decode_ops_validate_on_host():
+    import pytest
+    import torch
+
+    from aliyun_gpushare_device_plugin_amd.ops import decode as Dm
+
+    kc = torch.zeros((2, 1, 256, 128), dtype=torch.bfloat16)
+    with pytest.raises(ValueError):
+        Dm.decode_attention(torch.zeros((2, 512), dtype=torch.bfloat16), kc, kc,
+                            torch.zeros(2, dtype=torch.int32))                      # CPU tensors
+    with pytest.raises(ValueError):
+        Dm._check_cache(kc[:, :, :100], kc[:, :, :100])                              # Smax % 256
+    with pytest.raises(ValueError):
+        Dm.kv_append(torch.zeros((2, 128), dtype=torch.bfloat16), torch.zeros((2, 128), dtype=torch.bfloat16),
+                     kc, kc, torch.zeros(2, dtype=torch.int64))

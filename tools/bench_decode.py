@@ -1,0 +1,109 @@
+#!/usr/bin/env python3
+"""Serving benchmark: Llama-3-8B bf16 greedy decode with a KV cache on one MI355X.
+
+* decode attention kernel alone vs a PyTorch SDPA decode over the same cache (effective HBM GB/s);
+* full decode step: eager launches vs one hipGraph replay per step (tokens/s, ms/step).
+Random-init weights (no checkpoints offline); synthetic prompt. Output: JSON lines (and --out).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+
+import torch  # noqa: E402
+
+from aliyun_gpushare_device_plugin_amd import ops  # noqa: E402
+
+
+def timed(fn, n, warm=3):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(n):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t) / n
+
+
+def attn_micro(B, ctx, Hq=32, Hkv=8, D=128):
+    kc, vc = ops.kv_cache(B, Hkv, ctx, D)
+    kc.normal_()
+    vc.normal_()
+    lens = torch.full((B,), ctx, dtype=torch.int32, device="cuda")
+    q = torch.randn(B, Hq * D, device="cuda", dtype=torch.bfloat16)
+    ws = ops.DecodeWorkspace(B, Hq, kc.shape[2], D)
+    out = torch.empty(B, Hq * D, device="cuda", dtype=torch.bfloat16)
+    t_ours = timed(lambda: ops.decode_attention(q, kc, vc, lens, ws, out), 50)
+    qs = q.view(B, Hq, 1, D)
+    ks, vs = kc[:, :, :ctx], vc[:, :, :ctx]
+
+    def sdpa():
+        return torch.nn.functional.scaled_dot_product_attention(qs, ks, vs, enable_gqa=True)
+
+    t_sdpa = timed(sdpa, 50)
+    nbytes = 2 * B * Hkv * ctx * D * 2
+    return {"bench": "decode_attention", "B": B, "ctx": ctx, "ours_us": round(t_ours * 1e6, 1),
+            "ours_GBps": round(nbytes / t_ours / 1e9, 1), "sdpa_us": round(t_sdpa * 1e6, 1),
+            "sdpa_GBps": round(nbytes / t_sdpa / 1e9, 1), "speedup": round(t_sdpa / t_ours, 2)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--prompt", type=int, default=1024)
+    ap.add_argument("--steps", type=int, default=64)
+    ap.add_argument("--max-ctx", type=int, default=2048)
+    ap.add_argument("--layers", type=int, default=32)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    lines = []
+
+    def emit(d):
+        print(json.dumps(d), flush=True)
+        lines.append(d)
+
+    for B, ctx in ((32, 1024), (32, 4096), (8, 8192), (64, 2048)):
+        emit(attn_micro(B, ctx))
+
+    from aliyun_gpushare_device_plugin_amd.models.llama import LlamaConfig, LlamaModel
+    from aliyun_gpushare_device_plugin_amd.models.llama_serve import LlamaServer
+
+    model = LlamaModel(LlamaConfig.llama3_8b(n_layers=a.layers), "cuda", seed=1)
+    srv = LlamaServer(model, a.batch, a.max_ctx)
+    prompt = torch.randint(0, model.cfg.vocab, (a.batch, a.prompt), device="cuda")
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    srv.prefill(prompt)
+    torch.cuda.synchronize()
+    t_prefill = time.perf_counter() - t
+    res = {"bench": "llama3_8b_decode", "batch": a.batch, "prompt": a.prompt, "layers": a.layers,
+           "kv_cache_gib": round(srv.kv_bytes() / 2**30, 2), "weights_gib": round(model.weight_bytes() / 2**30, 2),
+           "prefill_s": round(t_prefill, 3)}
+    half = a.steps // 2
+    for mode, use_graph in (("eager", False), ("graph", True)):
+        if use_graph:
+            srv.capture()
+        srv.step(use_graph)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(half):
+            srv.step(use_graph)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t) / half
+        res[f"{mode}_ms_per_step"] = round(dt * 1e3, 3)
+        res[f"{mode}_tokens_per_s"] = round(a.batch / dt, 1)
+    res["context_after"] = srv.host_len
+    res["graph_speedup"] = round(res["eager_ms_per_step"] / res["graph_ms_per_step"], 2)
+    emit(res)
+    if a.out:
+        with open(a.out, "w") as f:
+            for d in lines:
+                f.write(json.dumps(d) + "\n")
+
+
+if __name__ == "__main__":
+    main()
