@@ -4,6 +4,9 @@ Runs inside the environment the plugin's Allocate response created (quota shim p
 loads a random-init Llama-3-8B, then runs prefill forwards for ``--seconds`` and prints JSON
 lines: the quota it sees, the weight footprint, and tokens/s per interval. ``--probe-quota``
 additionally tries to allocate past the quota and reports whether the shim refused it.
+``--mode decode`` makes it a serving pod instead: a ``--seq`` token prompt is prefilled into a
+KV cache and the pod then decodes greedily (one hipGraph replay per step, models/llama_serve.py);
+a "step" is then one decode step of the whole batch and tokens/s counts generated tokens.
 """
 from __future__ import annotations
 
@@ -23,6 +26,8 @@ def main(argv=None):
     ap.add_argument("--probe-quota", action="store_true")
     ap.add_argument("--start-file", default=None, help="wait for this file before timing (sync start)")
     ap.add_argument("--name", default="pod")
+    ap.add_argument("--mode", default="prefill", choices=("prefill", "decode"))
+    ap.add_argument("--decode-window", type=int, default=256, help="decode steps before rewinding to the prompt")
     a = ap.parse_args(argv)
 
     import torch
@@ -40,7 +45,15 @@ def main(argv=None):
     cfg = LlamaConfig.llama3_8b(n_layers=a.layers)
     model = LlamaModel(cfg, "cuda", seed=hash(a.name) & 0xffff)
     tok = torch.randint(0, cfg.vocab, (a.batch, a.seq), device="cuda")
-    model.forward(tok)
+    srv = None
+    if a.mode == "decode":
+        from .llama_serve import LlamaServer
+
+        srv = LlamaServer(model, a.batch, a.seq + a.decode_window + 1)
+        srv.prefill(tok)
+        srv.capture()
+    else:
+        model.forward(tok)
     torch.cuda.synchronize()
     emit(event="loaded", weight_bytes=model.weight_bytes(), params=cfg.n_params())
     if a.probe_quota:
@@ -58,12 +71,17 @@ def main(argv=None):
             time.sleep(0.01)
     t0 = time.perf_counter()
     n = 0
-    tokens = a.batch * a.seq
+    tokens = a.batch * a.seq if srv is None else a.batch
     last = t0
     lat = []
     while time.perf_counter() - t0 < a.seconds:
         ti = time.perf_counter()
-        model.forward(tok)
+        if srv is None:
+            model.forward(tok)
+        else:
+            if srv.host_len >= srv.max_ctx:
+                srv.rewind(a.seq)
+            srv.step()
         torch.cuda.synchronize()
         n += 1
         now = time.perf_counter()
@@ -72,7 +90,8 @@ def main(argv=None):
             emit(event="progress", iters=n, tokens_per_s=n * tokens / (now - t0))
             last = now
     dt = time.perf_counter() - t0
-    flops = model.flops_per_token(a.seq) * tokens * n
+    flops = (model.flops_per_token(a.seq) * tokens * n if srv is None
+             else 2.0 * (cfg.n_params() - cfg.vocab * cfg.d_model) * tokens * n)
     lat.sort()
 
     def q(f):

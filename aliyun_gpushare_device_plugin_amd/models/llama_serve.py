@@ -107,6 +107,13 @@ class LlamaServer:
         self.pos.copy_(save[1])
         self.graph = g
 
+    def rewind(self, length: int) -> None:
+        """Continue decoding from position ``length`` (the cache beyond it is overwritten)."""
+        if not 0 < length < self.max_ctx:
+            raise ValueError("rewind length outside the cache")
+        self.pos.fill_(length)
+        self.host_len = length
+
     def step(self, use_graph: bool = True) -> torch.Tensor:
         """One greedy decode step for every sequence; returns the step's logits [B, vocab]."""
         if self.host_len + 1 > self.max_ctx:

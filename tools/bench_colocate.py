@@ -115,8 +115,9 @@ def admit_pair(args, isolation: str):
 def run_mode(args, isolation: str) -> dict:
     env_a, env_b, alloc_ms = admit_pair(args, isolation)
     extra_b = ["--batch", str(args.batch_b)] if args.batch_b else []
-    solo = run_pods([("llama-a", env_a, ["--probe-quota"])], args.seconds, args)[0]
-    both = run_pods([("llama-a", env_a, []), ("llama-b", env_b, extra_b)], args.seconds, args)
+    extra_a = ["--mode", args.mode_a] + (["--seq", str(args.seq_a)] if args.seq_a else [])
+    solo = run_pods([("llama-a", env_a, ["--probe-quota"] + extra_a)], args.seconds, args)[0]
+    both = run_pods([("llama-a", env_a, extra_a), ("llama-b", env_b, extra_b)], args.seconds, args)
     solo_b = run_pods([("llama-b", env_b, extra_b)], args.seconds, args)[0] if args.batch_b else None
 
     def done(ls):
@@ -160,6 +161,9 @@ def main():
     ap.add_argument("--batch", type=int, default=4)
     ap.add_argument("--batch-b", type=int, default=0, help="pod B's batch (0 = same as A); B then also runs solo")
     ap.add_argument("--seq", type=int, default=2048)
+    ap.add_argument("--mode-a", default="prefill", choices=("prefill", "decode"),
+                    help="decode: pod A is a serving pod (KV-cache decode, hipGraph per step)")
+    ap.add_argument("--seq-a", type=int, default=0, help="pod A's prompt length (0 = --seq)")
     ap.add_argument("--layers", type=int, default=32)
     ap.add_argument("--smi-backend", default="auto")
     ap.add_argument("--isolation", default="none", choices=("none", "cu", "both"),
@@ -170,7 +174,7 @@ def main():
     args = ap.parse_args()
 
     modes = ["none", "cu"] if args.isolation == "both" else [args.isolation]
-    res = {"config": "2 x Llama-3-8B bf16 pods on one MI355X (BASELINE config 4)",
+    res = {"config": "2 x Llama-3-8B bf16 pods on one MI355X (BASELINE config 4)", "mode_a": args.mode_a,
            "pod_gib": args.pod_gib, "batch": args.batch, "batch_b": args.batch_b or args.batch, "seq": args.seq,
            "layers": args.layers}
     for m in modes:
@@ -181,6 +185,8 @@ def main():
         res.update(res.pop(modes[0]))
     line = json.dumps(res)
     print(line)
+    if args.mode_a != "prefill":
+        res["note"] = "pod A tokens/s = generated tokens (batch per decode step); aggregate ratios mix units"
     if args.out:
         with open(args.out, "w") as f:
             f.write(line + "\n")
