@@ -7,8 +7,9 @@ memory-bound work. The decode step here is built for that:
 * KV cache ``[B, Hkv, Smax, 128]`` per layer (``ops.kv_cache``), filled by the prefill through
   ``LlamaModel.forward(kv_sink=...)`` and appended to by ``ops.kv_append``;
 * attention = ``ops.decode_attention`` (split-K over the cache, ``native/kernels/decode_attention.hip``);
-  RMSNorm, RoPE and SiLU·up on the hand-written kernels; the skinny projections (M = batch) on
-  hipBLASLt through ``torch.matmul`` / ``torch.addmm`` (residual folded into ``addmm``'s beta);
+  RMSNorm, RoPE and SiLU·up on the hand-written kernels; the projections (M = batch <= 64) on the
+  split-K skinny MFMA GEMM (``ops.skinny_linear``, residual add fused, in place) — or, for A/B
+  measurement, hipBLASLt through ``torch.matmul`` / ``torch.addmm`` (``gemm="hipblaslt"``);
 * positions / lengths live in device tensors, so the whole 32-layer step is captured once in a
   hipGraph (``torch.cuda.CUDAGraph``) and replayed: one launch per step instead of ~450.
 """
@@ -21,8 +22,11 @@ from .llama import LlamaModel
 
 
 class LlamaServer:
-    def __init__(self, model: LlamaModel, batch: int, max_ctx: int):
+    def __init__(self, model: LlamaModel, batch: int, max_ctx: int, gemm: str = "skinny"):
         c = self.cfg = model.cfg
+        if gemm not in ("skinny", "hipblaslt") or (gemm == "skinny" and batch > 64):
+            raise ValueError("gemm must be 'skinny' (batch <= 64) or 'hipblaslt'")
+        self.gemm = gemm
         if max_ctx > c.max_seq:
             raise ValueError("max_ctx exceeds the RoPE table (cfg.max_seq)")
         self.model, self.B = model, batch
@@ -63,6 +67,11 @@ class LlamaServer:
         self.host_len = S
         return logits
 
+    def _mm(self, x, w, residual=None):
+        if self.gemm == "skinny":
+            return ops.skinny_linear(x, w, residual=residual, out=residual)
+        return torch.matmul(x, w.t()) if residual is None else torch.addmm(residual, x, w.t())
+
     @torch.no_grad()
     def _step(self) -> torch.Tensor:
         c, m, B = self.cfg, self.model, self.B
@@ -71,20 +80,20 @@ class LlamaServer:
         h = m.embed.index_select(0, self.tok)                          # residual stream [B, d]
         x = ops.rmsnorm(h, m.layers[0]["attn_norm"], c.eps)
         for i, L in enumerate(m.layers):
-            qkv = torch.matmul(x, L["wqkv"].t())
+            qkv = self._mm(x, L["wqkv"])
             q, k, v = qkv[:, :hq], qkv[:, hq:hq + hk], qkv[:, hq + hk:]
             ops.rope_(q, m.cos, m.sin, c.n_heads, c.head_dim, c.max_seq, positions=self.pos, validate=False)
             ops.rope_(k, m.cos, m.sin, c.n_kv_heads, c.head_dim, c.max_seq, positions=self.pos, validate=False)
             ops.kv_append(k, v, self.kc[i], self.vc[i], self.pos)
             a = ops.decode_attention(q, self.kc[i], self.vc[i], self.lens, self.ws)
-            h = torch.addmm(h, a, L["wo"].t())
+            h = self._mm(a, L["wo"], h)
             x = ops.rmsnorm(h, L["mlp_norm"], c.eps)
-            gu = torch.matmul(x, L["wgu"].t())                          # gate/up rows interleaved by 16
+            gu = self._mm(x, L["wgu"])                                  # gate/up rows interleaved by 16
             act = ops.silu_mul(gu.view(B, -1, 2, 16).transpose(1, 2).reshape(B, -1))
-            h = torch.addmm(h, act, L["wd"].t())
+            h = self._mm(act, L["wd"], h)
             nxt = m.layers[i + 1]["attn_norm"] if i + 1 < len(m.layers) else m.final_norm
             x = ops.rmsnorm(h, nxt, c.eps)
-        logits = torch.matmul(x, m.lm_head.t())
+        logits = self._mm(x, m.lm_head)
         self.tok.copy_(logits.argmax(-1))
         self.pos.add_(1)
         return logits

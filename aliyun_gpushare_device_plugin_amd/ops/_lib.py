@@ -29,6 +29,8 @@ SIGNATURES = {
     "gs_cu_census": [_P, _I, _I, _P],
     "gs_decode_attn_bf16": [_P, _I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _F, _P],
     "gs_kv_append_bf16": [_P, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P],
+    "gs_skinny_gemm_bf16": [_P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P, _P],
+    "gs_skinny_splits": [_I, _I],
 }
 
 ERRORS = {1: "invalid arguments", 2: "kernel launch failed"}

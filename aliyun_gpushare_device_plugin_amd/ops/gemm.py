@@ -157,3 +157,37 @@ class _LinearFn(torch.autograd.Function):
 
 def linear_autograd(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     return _LinearFn.apply(x, w)
+
+
+def skinny_linear(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | None = None,
+                  out: torch.Tensor | None = None) -> torch.Tensor:
+    """Decode-shaped ``x @ w.T (+ residual)`` for ``x`` ``[M <= 64, K]`` on the split-K skinny
+    kernel (native/kernels/gemm_skinny.hip): an HBM stream over ``w`` with the batch as the MFMA's
+    16-row operand. ``out`` may be ``residual`` itself (in-place residual add)."""
+    _check_operand(x, "x")
+    _check_operand(w, "w")
+    if x.dim() != 2 or w.dim() != 2 or x.shape[1] != w.shape[1]:
+        raise ValueError("skinny_linear: x [M, K] and w [N, K] expected")
+    M, K = x.shape
+    N = w.shape[0]
+    if not 1 <= M <= 64 or N % 64 or K % 32:
+        raise ValueError("skinny_linear: needs 1 <= M <= 64, N % 64 == 0, K % 32 == 0")
+    if x.stride(0) % 8 or w.stride(0) % 8 or x.data_ptr() % 16 or w.data_ptr() % 16:
+        raise ValueError("skinny_linear: rows must be 16-byte aligned")
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
+    if out.shape != (M, N) or out.dtype != torch.bfloat16 or out.stride(1) != 1 or out.stride(0) % 4:
+        raise ValueError("skinny_linear: out must be bf16 [M, N] with contiguous rows")
+    rptr = None
+    if residual is not None:
+        if residual.shape != (M, N) or residual.dtype != torch.bfloat16 or residual.stride() != out.stride():
+            raise ValueError("skinny_linear: residual must match out's shape and strides")
+        rptr = residual.data_ptr()
+    L = _lib.lib()
+    splits = L.gs_skinny_splits(N, K)
+    part = torch.empty(splits * M * N, dtype=torch.float32, device=x.device) if splits > 1 else None
+    rc = L.gs_skinny_gemm_bf16(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), rptr,
+                               out.stride(0), M, N, K, splits, part.data_ptr() if part is not None else None,
+                               _lib.stream_ptr(x.device))
+    _lib.check(rc, "gs_skinny_gemm_bf16")
+    return out

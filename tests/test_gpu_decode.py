@@ -69,3 +69,39 @@ def test_decode_steps_match_full_recompute_and_graph_matches_eager():
         assert (lg - le).abs().max().item() < 1e-2 * scale
         assert torch.equal(graph.tok, eager.tok)
     assert graph.host_len == 43 and int(graph.pos[0]) == 43
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 256, 512), (7, 512, 4096), (16, 1024, 1024), (32, 4096, 4096),
+                                   (33, 6144, 4096), (64, 256, 14336), (32, 4096, 14336), (5, 192, 96)])
+def test_skinny_linear_matches_fp32(M, N, K):
+    torch.manual_seed(M * 7 + N)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.05
+    ref = x.float() @ w.float().t()
+    y = ops.skinny_linear(x, w)
+    assert (y.float() - ref).abs().max().item() < 2e-2 * ref.abs().max().item() + 1e-2
+    r = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    want = ref + r.float()
+    y2 = ops.skinny_linear(x, w, residual=r, out=r)            # in-place residual add
+    assert y2.data_ptr() == r.data_ptr()
+    assert (r.float() - want).abs().max().item() < 2e-2 * want.abs().max().item() + 1e-2
+
+
+def test_skinny_linear_on_strided_rows():
+    x_wide = torch.randn(8, 1024 + 64, device="cuda", dtype=torch.bfloat16)
+    x = x_wide[:, 64:]                                          # 16-B aligned slice, row stride 1088
+    w = torch.randn(512, 1024, device="cuda", dtype=torch.bfloat16) * 0.05
+    ref = x.float() @ w.float().t()
+    assert (ops.skinny_linear(x, w).float() - ref).abs().max().item() < 2e-2 * ref.abs().max().item()
+
+
+def test_decode_step_hipblaslt_and_skinny_agree():
+    from aliyun_gpushare_device_plugin_amd.models.llama_serve import LlamaServer
+
+    model = _small_model()
+    prompt = torch.randint(0, model.cfg.vocab, (4, 24), device="cuda")
+    a, b = LlamaServer(model, 4, 128, gemm="skinny"), LlamaServer(model, 4, 128, gemm="hipblaslt")
+    a.prefill(prompt)
+    b.prefill(prompt)
+    la, lb = a.step().float(), b.step().float()
+    assert (la - lb).abs().max().item() < 2e-2 * lb.abs().max().item()

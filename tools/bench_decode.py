@@ -51,6 +51,18 @@ def attn_micro(B, ctx, Hq=32, Hkv=8, D=128):
             "sdpa_GBps": round(nbytes / t_sdpa / 1e9, 1), "speedup": round(t_sdpa / t_ours, 2)}
 
 
+def gemm_micro(M, N, K):
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16)
+    out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    t_ours = timed(lambda: ops.skinny_linear(x, w, out=out), 50)
+    t_blas = timed(lambda: torch.matmul(x, w.t()), 50)
+    nbytes = N * K * 2
+    return {"bench": "skinny_gemm", "M": M, "N": N, "K": K, "ours_us": round(t_ours * 1e6, 1),
+            "ours_GBps": round(nbytes / t_ours / 1e9, 1), "hipblaslt_us": round(t_blas * 1e6, 1),
+            "hipblaslt_GBps": round(nbytes / t_blas / 1e9, 1), "speedup": round(t_blas / t_ours, 2)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=32)
@@ -68,37 +80,47 @@ def main():
 
     for B, ctx in ((32, 1024), (32, 4096), (8, 8192), (64, 2048)):
         emit(attn_micro(B, ctx))
+    for M in (8, 32, 64):
+        for N, K in ((6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336), (128256, 4096)):
+            emit(gemm_micro(M, N, K))
 
     from aliyun_gpushare_device_plugin_amd.models.llama import LlamaConfig, LlamaModel
     from aliyun_gpushare_device_plugin_amd.models.llama_serve import LlamaServer
 
     model = LlamaModel(LlamaConfig.llama3_8b(n_layers=a.layers), "cuda", seed=1)
-    srv = LlamaServer(model, a.batch, a.max_ctx)
     prompt = torch.randint(0, model.cfg.vocab, (a.batch, a.prompt), device="cuda")
-    torch.cuda.synchronize()
-    t = time.perf_counter()
-    srv.prefill(prompt)
-    torch.cuda.synchronize()
-    t_prefill = time.perf_counter() - t
-    res = {"bench": "llama3_8b_decode", "batch": a.batch, "prompt": a.prompt, "layers": a.layers,
-           "kv_cache_gib": round(srv.kv_bytes() / 2**30, 2), "weights_gib": round(model.weight_bytes() / 2**30, 2),
-           "prefill_s": round(t_prefill, 3)}
-    half = a.steps // 2
-    for mode, use_graph in (("eager", False), ("graph", True)):
-        if use_graph:
-            srv.capture()
-        srv.step(use_graph)
+    for gemm in ("hipblaslt", "skinny"):
+        srv = LlamaServer(model, a.batch, a.max_ctx, gemm=gemm)
         torch.cuda.synchronize()
         t = time.perf_counter()
-        for _ in range(half):
-            srv.step(use_graph)
+        srv.prefill(prompt)
         torch.cuda.synchronize()
-        dt = (time.perf_counter() - t) / half
-        res[f"{mode}_ms_per_step"] = round(dt * 1e3, 3)
-        res[f"{mode}_tokens_per_s"] = round(a.batch / dt, 1)
-    res["context_after"] = srv.host_len
-    res["graph_speedup"] = round(res["eager_ms_per_step"] / res["graph_ms_per_step"], 2)
-    emit(res)
+        t_prefill = time.perf_counter() - t
+        res = {"bench": "llama3_8b_decode", "gemm": gemm, "batch": a.batch, "prompt": a.prompt, "layers": a.layers,
+               "kv_cache_gib": round(srv.kv_bytes() / 2**30, 2),
+               "weights_gib": round(model.weight_bytes() / 2**30, 2), "prefill_s": round(t_prefill, 3)}
+        half = a.steps // 2
+        for mode, use_graph in (("eager", False), ("graph", True)):
+            if use_graph:
+                srv.capture()
+            srv.step(use_graph)
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            for _ in range(half):
+                srv.step(use_graph)
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t) / half
+            res[f"{mode}_ms_per_step"] = round(dt * 1e3, 3)
+            res[f"{mode}_tokens_per_s"] = round(a.batch / dt, 1)
+        res["context_after"] = srv.host_len
+        res["graph_speedup"] = round(res["eager_ms_per_step"] / res["graph_ms_per_step"], 2)
+        # bytes a step must read: weights (minus the embedding table) + the KV cache up to the context
+        kv = 2 * model.cfg.n_layers * a.batch * model.cfg.n_kv_heads * srv.host_len * model.cfg.head_dim * 2
+        step_bytes = model.weight_bytes() - model.embed.numel() * 2 + kv
+        res["graph_effective_TBps"] = round(step_bytes / (res["graph_ms_per_step"] * 1e-3) / 1e12, 2)
+        emit(res)
+        del srv
+        torch.cuda.empty_cache()
     if a.out:
         with open(a.out, "w") as f:
             for d in lines:
