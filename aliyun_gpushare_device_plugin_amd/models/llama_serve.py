@@ -7,9 +7,11 @@ memory-bound work. The decode step here is built for that:
 * KV cache ``[B, Hkv, Smax, 128]`` per layer (``ops.kv_cache``), filled by the prefill through
   ``LlamaModel.forward(kv_sink=...)`` and appended to by ``ops.kv_append``;
 * attention = ``ops.decode_attention`` (split-K over the cache, ``native/kernels/decode_attention.hip``);
-  RMSNorm, RoPE and SiLU·up on the hand-written kernels; the projections (M = batch <= 64) on the
-  split-K skinny MFMA GEMM (``ops.skinny_linear``, residual add fused, in place) — or, for A/B
-  measurement, hipBLASLt through ``torch.matmul`` / ``torch.addmm`` (``gemm="hipblaslt"``);
+  RMSNorm, RoPE and SiLU·up on the hand-written kernels; the projections (M = batch) are plain
+  library GEMMs on hipBLASLt through ``torch.matmul`` / ``torch.addmm`` (residual in addmm's beta).
+  ``gemm="skinny"`` runs them on the split-K MFMA kernel here instead (``ops.skinny_linear``):
+  1.1-1.4x hipBLASLt on the 4096- and 6144-wide projections at batch 8, but 0.4-0.7x on the
+  28672-wide gate/up and on the LM head (``profiles/decode/README.md``), hence not the default;
 * positions / lengths live in device tensors, so the whole 32-layer step is captured once in a
   hipGraph (``torch.cuda.CUDAGraph``) and replayed: one launch per step instead of ~450.
 """
@@ -22,7 +24,7 @@ from .llama import LlamaModel
 
 
 class LlamaServer:
-    def __init__(self, model: LlamaModel, batch: int, max_ctx: int, gemm: str = "skinny"):
+    def __init__(self, model: LlamaModel, batch: int, max_ctx: int, gemm: str = "hipblaslt"):
         c = self.cfg = model.cfg
         if gemm not in ("skinny", "hipblaslt") or (gemm == "skinny" and batch > 64):
             raise ValueError("gemm must be 'skinny' (batch <= 64) or 'hipblaslt'")

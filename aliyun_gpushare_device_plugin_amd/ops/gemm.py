@@ -159,6 +159,11 @@ def linear_autograd(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     return _LinearFn.apply(x, w)
 
 
+def set_skinny_nt(nt: int) -> None:
+    """Force the skinny GEMM's features-per-wave factor (1, 2 or 4 tiles of 16); 0 = heuristic."""
+    _lib.check(_lib.lib().gs_skinny_set_nt(int(nt)), "gs_skinny_set_nt")
+
+
 def skinny_linear(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | None = None,
                   out: torch.Tensor | None = None) -> torch.Tensor:
     """Decode-shaped ``x @ w.T (+ residual)`` for ``x`` ``[M <= 64, K]`` on the split-K skinny

@@ -52,15 +52,23 @@ def attn_micro(B, ctx, Hq=32, Hkv=8, D=128):
 
 
 def gemm_micro(M, N, K):
+    from aliyun_gpushare_device_plugin_amd.ops.gemm import set_skinny_nt
+
     x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
     w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16)
     out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-    t_ours = timed(lambda: ops.skinny_linear(x, w, out=out), 50)
-    t_blas = timed(lambda: torch.matmul(x, w.t()), 50)
     nbytes = N * K * 2
-    return {"bench": "skinny_gemm", "M": M, "N": N, "K": K, "ours_us": round(t_ours * 1e6, 1),
-            "ours_GBps": round(nbytes / t_ours / 1e9, 1), "hipblaslt_us": round(t_blas * 1e6, 1),
-            "hipblaslt_GBps": round(nbytes / t_blas / 1e9, 1), "speedup": round(t_blas / t_ours, 2)}
+    res = {"bench": "skinny_gemm", "M": M, "N": N, "K": K}
+    for nt in (1, 2, 4, 0):
+        set_skinny_nt(nt)
+        t = timed(lambda: ops.skinny_linear(x, w, out=out), 50)
+        res[f"nt{nt or 'auto'}_us"] = round(t * 1e6, 1)
+    set_skinny_nt(0)
+    t_ours = res["ntauto_us"] * 1e-6
+    t_blas = timed(lambda: torch.matmul(x, w.t()), 50)
+    res.update({"ours_GBps": round(nbytes / t_ours / 1e9, 1), "hipblaslt_us": round(t_blas * 1e6, 1),
+                "hipblaslt_GBps": round(nbytes / t_blas / 1e9, 1), "speedup": round(t_blas / t_ours, 2)})
+    return res
 
 
 def main():
@@ -71,6 +79,7 @@ def main():
     ap.add_argument("--max-ctx", type=int, default=2048)
     ap.add_argument("--layers", type=int, default=32)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--micro-only", action="store_true")
     a = ap.parse_args()
     lines = []
 
@@ -87,9 +96,11 @@ def main():
     from aliyun_gpushare_device_plugin_amd.models.llama import LlamaConfig, LlamaModel
     from aliyun_gpushare_device_plugin_amd.models.llama_serve import LlamaServer
 
+    if a.micro_only:
+        return
     model = LlamaModel(LlamaConfig.llama3_8b(n_layers=a.layers), "cuda", seed=1)
     prompt = torch.randint(0, model.cfg.vocab, (a.batch, a.prompt), device="cuda")
-    for gemm in ("hipblaslt", "skinny"):
+    for gemm in (["hipblaslt", "skinny"] if not a.micro_only else []):
         srv = LlamaServer(model, a.batch, a.max_ctx, gemm=gemm)
         torch.cuda.synchronize()
         t = time.perf_counter()
