@@ -50,18 +50,21 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_nt(const unsigned short* __
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[t][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  int k = k0;
-  for (; k + 32 * UNROLL <= k1; k += 32 * UNROLL) {
-    bf16x8_t w[UNROLL][NT], x[UNROLL][MT];
+  // Register double buffer: the loads of k-block i + 1 are in flight while block i's MFMAs run
+  // (the first version waited for every block's loads before its MFMAs: one exposed HBM latency
+  // per block, with only ~2 waves per SIMD to cover it).
+  bf16x8_t wa[UNROLL][NT], xa[UNROLL][MT], wb[UNROLL][NT], xb[UNROLL][MT];
+  auto load = [&](bf16x8_t (&w)[UNROLL][NT], bf16x8_t (&x)[UNROLL][MT], int kk) {
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u)
 #pragma unroll
-      for (int j = 0; j < NT; ++j) w[u][j] = *(const bf16x8_t*)(wp[j] + k + 32 * u);
+      for (int j = 0; j < NT; ++j) w[u][j] = *(const bf16x8_t*)(wp[j] + kk + 32 * u);
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u)
 #pragma unroll
-      for (int t = 0; t < MT; ++t)
-        x[u][t] = xok[t] ? *(const bf16x8_t*)(xp[t] + k + 32 * u) : bf16x8_t{};
+      for (int t = 0; t < MT; ++t) x[u][t] = xok[t] ? *(const bf16x8_t*)(xp[t] + kk + 32 * u) : bf16x8_t{};
+  };
+  auto mma = [&](const bf16x8_t (&w)[UNROLL][NT], const bf16x8_t (&x)[UNROLL][MT]) {
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u)
 #pragma unroll
@@ -69,6 +72,21 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_nt(const unsigned short* __
 #pragma unroll
         for (int j = 0; j < NT; ++j)
           acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[u][j], x[u][t], acc[t][j], 0, 0, 0);
+  };
+  constexpr int STEP = 32 * UNROLL;
+  int k = k0;
+  if (k + 2 * STEP <= k1) {
+    load(wa, xa, k);
+    for (; k + 2 * STEP <= k1; k += 2 * STEP) {
+      load(wb, xb, k + STEP);
+      mma(wa, xa);
+      if (k + 3 * STEP <= k1) load(wa, xa, k + 2 * STEP);
+      mma(wb, xb);
+    }
+    if (k + STEP <= k1) {             // an odd block: its loads were issued by the last iteration
+      mma(wa, xa);
+      k += STEP;
+    }
   }
   for (; k < k1; k += 32) {             // K tail in steps of 32 (K % 32 == 0 is required)
 #pragma unroll
@@ -158,7 +176,7 @@ GS_KERNEL_API int gs_skinny_gemm_bf16(const void* X, int ldx, const void* W, int
   int nt, planned;
   plan(N, K, nt, planned);
   int kchunk = (K + splits - 1) / splits;
-  kchunk = (kchunk + 127) / 128 * 128;
+  kchunk = (kchunk + 255) / 256 * 256;
   const int nsplit = (K + kchunk - 1) / kchunk;
   float* pp = nsplit > 1 ? (float*)part : nullptr;
   const int per_wg = 16 * nt * WAVES;
