@@ -7,11 +7,11 @@ memory-bound work. The decode step here is built for that:
 * KV cache ``[B, Hkv, Smax, 128]`` per layer (``ops.kv_cache``), filled by the prefill through
   ``LlamaModel.forward(kv_sink=...)`` and appended to by ``ops.kv_append``;
 * attention = ``ops.decode_attention`` (split-K over the cache, ``native/kernels/decode_attention.hip``);
-  RMSNorm, RoPE and SiLU·up on the hand-written kernels; the projections (M = batch) are plain
-  library GEMMs on hipBLASLt through ``torch.matmul`` / ``torch.addmm`` (residual in addmm's beta).
-  ``gemm="skinny"`` runs them on the split-K MFMA kernel here instead (``ops.skinny_linear``):
-  1.1-1.4x hipBLASLt on the 4096- and 6144-wide projections at batch 8, but 0.4-0.7x on the
-  28672-wide gate/up and on the LM head (``profiles/decode/README.md``), hence not the default;
+  RMSNorm, RoPE and SiLU·up on the hand-written kernels; the projections (M = batch <= 64) on the
+  LDS-staged skinny MFMA GEMM (``ops.skinny_linear``, residual add fused in place): 1.24-1.4x
+  hipBLASLt on the 4096/6144-wide projections, 1.03-1.08x on the LM head, 0.8-0.9x on the
+  28672-wide gate/up, 6.08 vs 6.58 ms per batch-32 step overall (``profiles/decode/README.md``);
+  ``gemm="hipblaslt"`` runs them on ``torch.matmul`` / ``torch.addmm`` for A/B measurement;
 * positions / lengths live in device tensors, so the whole 32-layer step is captured once in a
   hipGraph (``torch.cuda.CUDAGraph``) and replayed: one launch per step instead of ~450.
 """
@@ -24,7 +24,7 @@ from .llama import LlamaModel
 
 
 class LlamaServer:
-    def __init__(self, model: LlamaModel, batch: int, max_ctx: int, gemm: str = "hipblaslt"):
+    def __init__(self, model: LlamaModel, batch: int, max_ctx: int, gemm: str = "skinny"):
         c = self.cfg = model.cfg
         if gemm not in ("skinny", "hipblaslt") or (gemm == "skinny" and batch > 64):
             raise ValueError("gemm must be 'skinny' (batch <= 64) or 'hipblaslt'")

@@ -32,6 +32,8 @@ SIGNATURES = {
     "gs_skinny_gemm_bf16": [_P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P, _P],
     "gs_skinny_splits": [_I, _I],
     "gs_skinny_set_nt": [_I],
+    "gs_skinny_set_variant": [_I],
+    "gs_skinny_set_wg_target": [_I],
 }
 
 ERRORS = {1: "invalid arguments", 2: "kernel launch failed"}

@@ -164,6 +164,15 @@ def set_skinny_nt(nt: int) -> None:
     _lib.check(_lib.lib().gs_skinny_set_nt(int(nt)), "gs_skinny_set_nt")
 
 
+SKINNY_AUTO, SKINNY_REG, SKINNY_LDS = 0, 1, 2
+
+
+def set_skinny_variant(v: int) -> None:
+    """``SKINNY_AUTO``: LDS-staged kernel when K % 256 == 0, else the register kernel;
+    ``SKINNY_REG`` / ``SKINNY_LDS`` force one (A/B measurement, tests)."""
+    _lib.check(_lib.lib().gs_skinny_set_variant(int(v)), "gs_skinny_set_variant")
+
+
 def skinny_linear(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | None = None,
                   out: torch.Tensor | None = None) -> torch.Tensor:
     """Decode-shaped ``x @ w.T (+ residual)`` for ``x`` ``[M <= 64, K]`` on the split-K skinny

@@ -121,6 +121,91 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_nt(const unsigned short* __
   }
 }
 
+// LDS-staged variant: a workgroup owns 64 rows of W and stages 256-deep K slices of W and X in
+// LDS, so every global load instruction reads 8 rows x 512 contiguous bytes (the register kernel
+// above reads 16 rows x 64 B per instruction) and X is fetched once per workgroup instead of once
+// per wave. The next slice's loads are in flight (in registers) while the MFMAs consume the
+// current one. Rows are padded by 16 B in LDS to spread the 16-B fragment reads over the banks.
+constexpr int LBN = 64, LBK = 256, LROW = LBK + 8;
+
+template <int MT>
+__global__ __launch_bounds__(256) void skinny_lds(const unsigned short* __restrict__ X, int ldx,
+                                                  const unsigned short* __restrict__ W, int ldw,
+                                                  float* __restrict__ part, unsigned short* __restrict__ Y,
+                                                  const unsigned short* __restrict__ R, int ldy, int M, int N, int K,
+                                                  int kchunk) {
+  __shared__ __attribute__((aligned(16))) unsigned short sW[LBN * LROW];
+  __shared__ __attribute__((aligned(16))) unsigned short sX[MT * 16 * LROW];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n0 = blockIdx.x * LBN, split = blockIdx.y;
+  const int k0 = split * kchunk, k1 = min(K, k0 + kchunk);
+  if (k0 >= k1) return;
+  const int lr = tid >> 5, lc = (tid & 31) * 8;           // global->LDS: row group, column
+  constexpr int XI = MT * 2;                              // X row groups of 8 (M padded to 16 MT)
+  u16x8_t wr[8], xr[XI];
+  auto gload = [&](int kk) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) wr[i] = *(const u16x8_t*)(W + (size_t)(n0 + 8 * i + lr) * ldw + kk + lc);
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+      const int m = 8 * i + lr;
+      xr[i] = m < M ? *(const u16x8_t*)(X + (size_t)m * ldx + kk + lc) : u16x8_t{};
+    }
+  };
+  auto lstore = [&]() {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) *(u16x8_t*)(sW + (8 * i + lr) * LROW + lc) = wr[i];
+#pragma unroll
+    for (int i = 0; i < XI; ++i) *(u16x8_t*)(sX + (8 * i + lr) * LROW + lc) = xr[i];
+  };
+  f32x4_t acc[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int r16 = lane & 15, kof = (lane >> 4) * 8;
+  const unsigned short* wl = sW + (16 * wave + r16) * LROW + kof;
+
+  gload(k0);
+  lstore();
+  __syncthreads();
+  for (int kk = k0; kk < k1; kk += LBK) {
+    const bool more = kk + LBK < k1;
+    if (more) gload(kk + LBK);
+#pragma unroll
+    for (int ks = 0; ks < LBK / 32; ++ks) {
+      const bf16x8_t wf = *(const bf16x8_t*)(wl + ks * 32);
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        const bf16x8_t xf = *(const bf16x8_t*)(sX + (16 * t + r16) * LROW + kof + ks * 32);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, xf, acc[t], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+    if (more) {
+      lstore();
+      __syncthreads();
+    }
+  }
+
+  const int nb = n0 + 16 * wave + (lane >> 4) * 4;
+#pragma unroll
+  for (int t = 0; t < MT; ++t) {
+    const int m = t * 16 + r16;
+    if (m >= M) continue;
+    if (part) {
+      *(f32x4_t*)(part + ((size_t)split * M + m) * N + nb) = acc[t];
+    } else {
+      u16x4_t o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = acc[t][r];
+        if (R) v += bf16_to_f32(R[(size_t)m * ldy + nb + r]);
+        o[r] = f32_to_bf16(v);
+      }
+      *(u16x4_t*)(Y + (size_t)m * ldy + nb) = o;
+    }
+  }
+}
+
 // Y[m, n] = sum_s part[s, m, n] (+ R[m, n]); 4 outputs per thread.
 __global__ __launch_bounds__(256) void skinny_reduce(const float* __restrict__ part, int splits,
                                                      unsigned short* __restrict__ Y, const unsigned short* __restrict__ R,
@@ -145,6 +230,27 @@ __global__ __launch_bounds__(256) void skinny_reduce(const float* __restrict__ p
 // Features per wave (16 x NT) and split-K factor for a shape: NT = 4 once the grid has >= 1024
 // such waves, else 2, else 1; then splits double (keeping >= 256 k per split) until ~2048 waves.
 static int g_force_nt = 0;   // 0 = heuristic; 1 / 2 / 4 = forced (sweeps, tests)
+static int g_variant = 0;    // 0 = auto (LDS-staged when K % 256 == 0), 1 = register kernel, 2 = LDS
+
+static bool use_lds(int K) { return g_variant == 2 || (g_variant == 0 && K % LBK == 0); }
+
+// LDS variant: 64 features per workgroup; splits double (>= 512 k each) until the grid has
+// g_wg_target workgroups, unless W is wide enough (>= 256 workgroups) on its own. Measured on
+// MI355X over targets 256-2048 (profiles/decode/micro_lds_wg_sweep.jsonl): splitting the 28672-wide
+// gate/up projection cost 10-20 %, splitting the 4096-wide ones to 512 workgroups won 10-25 %.
+static int g_wg_target = 512;
+
+static void plan_lds(int N, int K, int& splits) {
+  splits = 1;
+  if (N / LBN >= 256) return;   // wide W: the split partials cost more than the parallelism gains
+  while ((N / LBN) * splits < g_wg_target && K / (splits * 2) >= 512) splits *= 2;
+}
+
+GS_KERNEL_API int gs_skinny_set_wg_target(int n) {
+  if (n < 1 || n > 65536) return GS_EINVAL;
+  g_wg_target = n;
+  return GS_OK;
+}
 
 static void plan(int N, int K, int& nt, int& splits) {
   nt = g_force_nt ? g_force_nt : N / 64 >= 1024 ? 4 : N / 32 >= 512 ? 2 : 1;
@@ -159,8 +265,18 @@ GS_KERNEL_API int gs_skinny_set_nt(int nt) {
   return GS_OK;
 }
 
+GS_KERNEL_API int gs_skinny_set_variant(int v) {
+  if (v < 0 || v > 2) return GS_EINVAL;
+  g_variant = v;
+  return GS_OK;
+}
+
 GS_KERNEL_API int gs_skinny_splits(int N, int K) {
   int nt, s;
+  if (use_lds(K)) {
+    plan_lds(N, K, s);
+    return s;
+  }
   plan(N, K, nt, s);
   return s;
 }
@@ -173,6 +289,31 @@ GS_KERNEL_API int gs_skinny_gemm_bf16(const void* X, int ldx, const void* W, int
   if (M < 1 || M > 64 || N % 64 || K % 32 || K <= 0 || ldx % 8 || ldw % 8 || ldy % 4 || ldx < K || ldw < K ||
       ldy < N || splits < 1 || (splits > 1 && !part))
     return GS_EINVAL;
+  const int mt = (M + 15) / 16;
+  if (use_lds(K)) {
+    if (K % LBK) return GS_EINVAL;
+    int kchunk = (K + splits - 1) / splits;
+    kchunk = (kchunk + LBK - 1) / LBK * LBK;
+    const int nsplit = (K + kchunk - 1) / kchunk;
+    float* pp = nsplit > 1 ? (float*)part : nullptr;
+    const dim3 grid(N / LBN, nsplit);
+    auto go = [&](auto kern) {
+      hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, (const unsigned short*)X, ldx, (const unsigned short*)W,
+                         ldw, pp, (unsigned short*)Y, (const unsigned short*)R, ldy, M, N, K, kchunk);
+    };
+    switch (mt) {
+      case 1: go(skinny_lds<1>); break;
+      case 2: go(skinny_lds<2>); break;
+      case 3: go(skinny_lds<3>); break;
+      default: go(skinny_lds<4>); break;
+    }
+    if (pp) {
+      const int n4 = M * N / 4;
+      hipLaunchKernelGGL(skinny_reduce, dim3((n4 + 255) / 256), dim3(256), 0, stream, (const float*)pp, nsplit,
+                         (unsigned short*)Y, (const unsigned short*)R, ldy, M, N);
+    }
+    return gs_launch_status();
+  }
   int nt, planned;
   plan(N, K, nt, planned);
   int kchunk = (K + splits - 1) / splits;
@@ -181,7 +322,6 @@ GS_KERNEL_API int gs_skinny_gemm_bf16(const void* X, int ldx, const void* W, int
   float* pp = nsplit > 1 ? (float*)part : nullptr;
   const int per_wg = 16 * nt * WAVES;
   const dim3 grid((N + per_wg - 1) / per_wg, nsplit);
-  const int mt = (M + 15) / 16;
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, grid, dim3(WAVES * 64), 0, stream, (const unsigned short*)X, ldx,
                        (const unsigned short*)W, ldw, pp, (unsigned short*)Y, (const unsigned short*)R, ldy, M, N, K,

@@ -71,9 +71,22 @@ def test_decode_steps_match_full_recompute_and_graph_matches_eager():
     assert graph.host_len == 43 and int(graph.pos[0]) == 43
 
 
+@pytest.mark.parametrize("variant", [1, 2])
 @pytest.mark.parametrize("M,N,K", [(1, 256, 512), (7, 512, 4096), (16, 1024, 1024), (32, 4096, 4096),
                                    (33, 6144, 4096), (64, 256, 14336), (32, 4096, 14336), (5, 192, 96)])
-def test_skinny_linear_matches_fp32(M, N, K):
+def test_skinny_linear_matches_fp32(M, N, K, variant):
+    from aliyun_gpushare_device_plugin_amd.ops.gemm import SKINNY_AUTO, set_skinny_variant
+
+    if variant == 2 and K % 256:
+        pytest.skip("LDS variant needs K % 256 == 0")
+    set_skinny_variant(variant)
+    try:
+        _check_skinny(M, N, K)
+    finally:
+        set_skinny_variant(SKINNY_AUTO)
+
+
+def _check_skinny(M, N, K):
     torch.manual_seed(M * 7 + N)
     x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
     w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.05

@@ -59,11 +59,24 @@ def gemm_micro(M, N, K):
     out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
     nbytes = N * K * 2
     res = {"bench": "skinny_gemm", "M": M, "N": N, "K": K}
-    for nt in (1, 2, 4, 0):
+    from aliyun_gpushare_device_plugin_amd.ops.gemm import SKINNY_AUTO, SKINNY_LDS, SKINNY_REG, set_skinny_variant
+
+    set_skinny_variant(SKINNY_REG)
+    for nt in (1, 2, 4):
         set_skinny_nt(nt)
         t = timed(lambda: ops.skinny_linear(x, w, out=out), 50)
-        res[f"nt{nt or 'auto'}_us"] = round(t * 1e6, 1)
+        res[f"reg_nt{nt}_us"] = round(t * 1e6, 1)
     set_skinny_nt(0)
+    set_skinny_variant(SKINNY_LDS)
+    from aliyun_gpushare_device_plugin_amd.ops import _lib
+
+    for tgt in (256, 512, 1024, 2048):
+        _lib.lib().gs_skinny_set_wg_target(tgt)
+        res[f"lds_wg{tgt}_us"] = round(timed(lambda: ops.skinny_linear(x, w, out=out), 50) * 1e6, 1)
+    _lib.lib().gs_skinny_set_wg_target(512)
+    res["lds_us"] = res["lds_wg512_us"]
+    set_skinny_variant(SKINNY_AUTO)
+    res["ntauto_us"] = round(timed(lambda: ops.skinny_linear(x, w, out=out), 50) * 1e6, 1)
     t_ours = res["ntauto_us"] * 1e-6
     t_blas = timed(lambda: torch.matmul(x, w.t()), 50)
     res.update({"ours_GBps": round(nbytes / t_ours / 1e9, 1), "hipblaslt_us": round(t_blas * 1e6, 1),
