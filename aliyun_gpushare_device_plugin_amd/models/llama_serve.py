@@ -7,7 +7,8 @@ memory-bound work. The decode step here is built for that:
 * KV cache ``[B, Hkv, Smax, 128]`` per layer (``ops.kv_cache``), filled by the prefill through
   ``LlamaModel.forward(kv_sink=...)`` and appended to by ``ops.kv_append``;
 * attention = ``ops.decode_attention`` (split-K over the cache, ``native/kernels/decode_attention.hip``);
-  RMSNorm, RoPE and SiLU·up on the hand-written kernels; the projections (M = batch <= 64) on the
+  RMSNorm, SiLU·up (read in the interleaved gate/up layout) and one fused RoPE(q, k) + KV-append
+  launch per layer on the hand-written kernels; the projections (M = batch <= 64) on the
   LDS-staged skinny MFMA GEMM (``ops.skinny_linear``, residual add fused in place): 1.24-1.4x
   hipBLASLt on the 4096/6144-wide projections, 1.03-1.08x on the LM head, 0.8-0.9x on the
   28672-wide gate/up, 6.08 vs 6.58 ms per batch-32 step overall (``profiles/decode/README.md``);
@@ -76,22 +77,19 @@ class LlamaServer:
 
     @torch.no_grad()
     def _step(self) -> torch.Tensor:
-        c, m, B = self.cfg, self.model, self.B
-        hq, hk = c.n_heads * c.head_dim, c.n_kv_heads * c.head_dim
+        c, m = self.cfg, self.model
+        hq = c.n_heads * c.head_dim
         torch.add(self.pos, 1, out=self.lens)
         h = m.embed.index_select(0, self.tok)                          # residual stream [B, d]
         x = ops.rmsnorm(h, m.layers[0]["attn_norm"], c.eps)
         for i, L in enumerate(m.layers):
             qkv = self._mm(x, L["wqkv"])
-            q, k, v = qkv[:, :hq], qkv[:, hq:hq + hk], qkv[:, hq + hk:]
-            ops.rope_(q, m.cos, m.sin, c.n_heads, c.head_dim, c.max_seq, positions=self.pos, validate=False)
-            ops.rope_(k, m.cos, m.sin, c.n_kv_heads, c.head_dim, c.max_seq, positions=self.pos, validate=False)
-            ops.kv_append(k, v, self.kc[i], self.vc[i], self.pos)
-            a = ops.decode_attention(q, self.kc[i], self.vc[i], self.lens, self.ws)
+            ops.rope_kv_append(qkv, m.cos, m.sin, self.pos, self.kc[i], self.vc[i], c.n_heads)
+            a = ops.decode_attention(qkv[:, :hq], self.kc[i], self.vc[i], self.lens, self.ws)
             h = self._mm(a, L["wo"], h)
             x = ops.rmsnorm(h, L["mlp_norm"], c.eps)
             gu = self._mm(x, L["wgu"])                                  # gate/up rows interleaved by 16
-            act = ops.silu_mul(gu.view(B, -1, 2, 16).transpose(1, 2).reshape(B, -1))
+            act = ops.silu_mul(gu, interleaved=True)
             h = self._mm(act, L["wd"], h)
             nxt = m.layers[i + 1]["attn_norm"] if i + 1 < len(m.layers) else m.final_norm
             x = ops.rmsnorm(h, nxt, c.eps)

@@ -4,4 +4,4 @@ from .gemm import (deinterleave_gate_up, gemm_nt, interleave_gate_up, linear, li
 from .fused import rmsnorm, rope_, rope_tables, silu_mul  # noqa: F401
 from .attention import attention, reference_attention  # noqa: F401
 from .census import cu_census  # noqa: F401
-from .decode import DecodeWorkspace, decode_attention, kv_append, kv_cache  # noqa: F401
+from .decode import DecodeWorkspace, decode_attention, kv_append, kv_cache, rope_kv_append  # noqa: F401

@@ -59,6 +59,28 @@ def kv_append(k: torch.Tensor, v: torch.Tensor, k_cache: torch.Tensor, v_cache: 
     _lib.check(rc, "gs_kv_append_bf16")
 
 
+def rope_kv_append(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, pos: torch.Tensor,
+                   k_cache: torch.Tensor, v_cache: torch.Tensor, n_heads: int) -> None:
+    """One launch for a decode step's RoPE(q), RoPE(k) (in place in the fused ``qkv`` rows
+    ``[B, (Hq + 2 Hkv) * D]``) and the append of rotated k and raw v at ``pos[b]``. Equivalent to
+    ``rope_(q); rope_(k); kv_append(k, v)``; positions are not range-checked on the host (the
+    kernel clamps table reads and skips cache writes outside it) so the call is graph-safe."""
+    _check_cache(k_cache, v_cache)
+    B, Hkv, Smax, D = k_cache.shape
+    width = (n_heads + 2 * Hkv) * D
+    qs = _rows(qkv, B, width, "qkv") if qkv.shape[1] == width else -1
+    if qs < 0:
+        raise ValueError("rope_kv_append: qkv must be [B, (Hq + 2 Hkv) * D]")
+    _ints(pos, B, "pos")
+    if (cos.dtype != torch.float32 or sin.shape != cos.shape or cos.dim() != 2 or cos.shape[1] != D // 2
+            or not cos.is_contiguous() or not sin.is_contiguous()):
+        raise ValueError("rope_kv_append: tables must be contiguous float32 [rows, D / 2]")
+    rc = _lib.lib().gs_rope_kv_append_bf16(qkv.data_ptr(), qs, cos.data_ptr(), sin.data_ptr(), cos.shape[0],
+                                           pos.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), B, n_heads, Hkv,
+                                           D, Smax, _lib.stream_ptr(qkv.device))
+    _lib.check(rc, "gs_rope_kv_append_bf16")
+
+
 class DecodeWorkspace:
     """Split partials for :func:`decode_attention` (allocated once, reused by every layer/step)."""
 

@@ -36,16 +36,19 @@ def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float = 1e-5, residual: torch
     return y
 
 
-def silu_mul(gu: torch.Tensor) -> torch.Tensor:
-    """``silu(gu[..., :F]) * gu[..., F:]`` for the concatenated gate|up projection."""
+def silu_mul(gu: torch.Tensor, interleaved: bool = False) -> torch.Tensor:
+    """``silu(gu[..., :F]) * gu[..., F:]`` for the concatenated gate|up projection, or with
+    ``interleaved=True`` for the gate/up-interleaved-by-16 layout of ``ops.interleave_gate_up``
+    weights (read in place, no de-interleave copy)."""
     _bf16_cuda(gu, "gu")
     F2 = gu.shape[-1]
-    if F2 % 16:
-        raise ValueError("silu_mul needs the last dim to be a multiple of 16")
+    if F2 % (32 if interleaved else 16) or not gu.is_contiguous():
+        raise ValueError("silu_mul needs a contiguous tensor whose last dim is a multiple of 16 (32 interleaved)")
     F = F2 // 2
     M = gu.numel() // F2
     y = torch.empty((*gu.shape[:-1], F), dtype=gu.dtype, device=gu.device)
-    rc = _lib.lib().gs_silu_mul_bf16(gu.data_ptr(), y.data_ptr(), M, F, _lib.stream_ptr(gu.device))
+    fn = _lib.lib().gs_silu_mul_il_bf16 if interleaved else _lib.lib().gs_silu_mul_bf16
+    rc = fn(gu.data_ptr(), y.data_ptr(), M, F, _lib.stream_ptr(gu.device))
     _lib.check(rc, "gs_silu_mul_bf16")
     return y
 

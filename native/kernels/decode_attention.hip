@@ -123,7 +123,7 @@ __global__ __launch_bounds__(NT) void decode_split(const unsigned short* __restr
   float acc[DPL];
 #pragma unroll
   for (int i = 0; i < DPL; ++i) acc[i] = 0.f;
-#pragma unroll 4
+#pragma unroll 16   // 16 V rows in flight per lane: the P·V loop is latency-bound at unroll 4
   for (int p = wave; p < n; p += 4) {
     const float w = S[g][p];
     const unsigned short* vr = vp + (size_t)p * D + d0;
@@ -186,7 +186,67 @@ __global__ __launch_bounds__(256) void kv_append(const unsigned short* __restric
   *(u16x8_t*)dst = *(const u16x8_t*)src;
 }
 
+// Decode-step fusion of RoPE(q), RoPE(k) and the KV append (one launch instead of three): per
+// sequence b at position pos[b], q and k heads of the fused QKV row are rotated in place (4 pairs
+// per thread, cos/sin from the host tables) and the rotated k plus the raw v are written to the
+// caches. Items per sequence: (Hq + Hkv) heads x D/8 rotation items, then Hkv x D/8 v copies.
+__global__ __launch_bounds__(256) void rope_kv_append(unsigned short* __restrict__ qkv, int bstride,
+                                                      const float* __restrict__ cosb, const float* __restrict__ sinb,
+                                                      int tab_rows, const int* __restrict__ pos,
+                                                      unsigned short* __restrict__ kc, unsigned short* __restrict__ vc,
+                                                      int B, int Hq, int Hkv, int Smax) {
+  constexpr int HALF = D / 2, NQ = HALF / 4;           // 16 rotation items per head
+  constexpr int NV = D / 8;                            // 16 copy items per v head
+  const int per = (Hq + Hkv) * NQ + Hkv * NV;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * per) return;
+  const int b = i / per, r = i % per;
+  const int p = pos[b];
+  const bool in_cache = p >= 0 && p < Smax;
+  unsigned short* row = qkv + (size_t)b * bstride;
+  if (r < (Hq + Hkv) * NQ) {
+    const int h = r / NQ, d = (r % NQ) * 4;
+    const int pt = min(max(p, 0), tab_rows - 1);
+    unsigned short* hp = row + (size_t)h * D;
+    const u16x4_t a = *(const u16x4_t*)(hp + d);
+    const u16x4_t c2 = *(const u16x4_t*)(hp + HALF + d);
+    const float4 c = *(const float4*)(cosb + (size_t)pt * HALF + d);
+    const float4 sn = *(const float4*)(sinb + (size_t)pt * HALF + d);
+    const float cc[4] = {c.x, c.y, c.z, c.w}, sc[4] = {sn.x, sn.y, sn.z, sn.w};
+    u16x4_t oa, ob;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float x1 = bf16_to_f32(a[e]), x2 = bf16_to_f32(c2[e]);
+      oa[e] = f32_to_bf16(x1 * cc[e] - x2 * sc[e]);
+      ob[e] = f32_to_bf16(x2 * cc[e] + x1 * sc[e]);
+    }
+    *(u16x4_t*)(hp + d) = oa;
+    *(u16x4_t*)(hp + HALF + d) = ob;
+    if (h >= Hq && in_cache) {
+      unsigned short* dst = kc + ((((size_t)b * Hkv + (h - Hq)) * Smax + p) * D);
+      *(u16x4_t*)(dst + d) = oa;
+      *(u16x4_t*)(dst + HALF + d) = ob;
+    }
+  } else if (in_cache) {
+    const int r2 = r - (Hq + Hkv) * NQ, h = r2 / NV, c = (r2 % NV) * 8;
+    const unsigned short* src = row + (size_t)(Hq + Hkv + h) * D + c;
+    *(u16x8_t*)(vc + ((((size_t)b * Hkv + h) * Smax + p) * D) + c) = *(const u16x8_t*)src;
+  }
+}
+
 }  // namespace
+
+GS_KERNEL_API int gs_rope_kv_append_bf16(void* qkv, int bstride, const float* cosb, const float* sinb, int tab_rows,
+                                         const int* pos, void* k_cache, void* v_cache, int B, int Hq, int Hkv, int Dh,
+                                         int Smax, hipStream_t stream) {
+  if (Dh != D || B <= 0 || Hq <= 0 || Hkv <= 0 || Smax <= 0 || tab_rows <= 0 || bstride % 8 ||
+      bstride < (Hq + 2 * Hkv) * D)
+    return GS_EINVAL;
+  const int n = B * ((Hq + Hkv) * (D / 8) + Hkv * (D / 8));
+  hipLaunchKernelGGL(rope_kv_append, dim3((n + 255) / 256), dim3(256), 0, stream, (unsigned short*)qkv, bstride, cosb,
+                     sinb, tab_rows, pos, (unsigned short*)k_cache, (unsigned short*)v_cache, B, Hq, Hkv, Smax);
+  return gs_launch_status();
+}
 
 // q: [B, Hq, D] rows at q_bstride elements per sequence (heads contiguous); caches [B, Hkv, Smax, D];
 // lens[B] (device); workspace: o_part [B, Hq, nsplit, D] f32 + ml_part [B, Hq, nsplit, 2] f32 with

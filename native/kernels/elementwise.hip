@@ -1,6 +1,7 @@
 // Memory-bound fused kernels for the demo Llama workload (bf16, 16-byte vector I/O).
 //  * gs_rmsnorm_bf16:  [h = x + r  (written to r_out)]  y = h * rsqrt(mean(h^2) + eps) * w
-//  * gs_silu_mul_bf16: y[m, f] = silu(gu[m, f]) * gu[m, F + f]   (gate|up concatenated)
+//  * gs_silu_mul_bf16: y[m, f] = silu(gu[m, f]) * gu[m, F + f]   (gate|up concatenated;
+//                      gs_silu_mul_il_bf16: the interleaved-by-16 layout)
 //  * gs_rope_bf16:     in-place rotate-half RoPE on q/k with host-precomputed cos/sin tables
 // Per cdna_hip_programming.md Appendix B: vectorised 16-B loads, f32 math, trig from a
 // table (no on-device sin/cos), one row per 256-thread block for the row reductions.
@@ -67,13 +68,16 @@ __global__ __launch_bounds__(RMS_THREADS) void rmsnorm_bf16(const unsigned short
 }
 
 __global__ __launch_bounds__(256) void silu_mul_bf16(const unsigned short* __restrict__ gu,
-                                                     unsigned short* __restrict__ y, int M, int F) {
+                                                     unsigned short* __restrict__ y, int M, int F, int il) {
   const int nvec = F / 8;
   const size_t total = (size_t)M * nvec;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
     const size_t m = i / nvec, f = (i % nvec) * 8;
-    const u16x8_t g = *(const u16x8_t*)(gu + m * 2 * F + f);
-    const u16x8_t u = *(const u16x8_t*)(gu + m * 2 * F + F + f);
+    // il: gate/up rows interleaved by 16 (ops.interleave_gate_up): feature f's gate sits at
+    // column (f / 16) * 32 + f % 16 and its up 16 columns later
+    const size_t go = il ? (f / 16) * 32 + f % 16 : f, uo = il ? go + 16 : F + f;
+    const u16x8_t g = *(const u16x8_t*)(gu + m * 2 * F + go);
+    const u16x8_t u = *(const u16x8_t*)(gu + m * 2 * F + uo);
     u16x8_t o;
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = f32_to_bf16(silu_f32(bf16_to_f32(g[e])) * bf16_to_f32(u[e]));
@@ -131,7 +135,15 @@ GS_KERNEL_API int gs_rmsnorm_bf16(const void* x, const void* resid_in, void* res
 GS_KERNEL_API int gs_silu_mul_bf16(const void* gu, void* y, int M, int F, hipStream_t stream) {
   if (M <= 0 || F <= 0 || F % 8) return GS_EINVAL;
   hipLaunchKernelGGL(silu_mul_bf16, dim3(grid_for((size_t)M * F / 8, 256)), dim3(256), 0, stream,
-                     (const unsigned short*)gu, (unsigned short*)y, M, F);
+                     (const unsigned short*)gu, (unsigned short*)y, M, F, 0);
+  return gs_launch_status();
+}
+
+// Same on the interleaved-by-16 gate/up layout the SwiGLU weights use (no de-interleave copy).
+GS_KERNEL_API int gs_silu_mul_il_bf16(const void* gu, void* y, int M, int F, hipStream_t stream) {
+  if (M <= 0 || F <= 0 || F % 16) return GS_EINVAL;
+  hipLaunchKernelGGL(silu_mul_bf16, dim3(grid_for((size_t)M * F / 8, 256)), dim3(256), 0, stream,
+                     (const unsigned short*)gu, (unsigned short*)y, M, F, 1);
   return gs_launch_status();
 }
 

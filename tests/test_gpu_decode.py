@@ -118,3 +118,29 @@ def test_decode_step_hipblaslt_and_skinny_agree():
     b.prefill(prompt)
     la, lb = a.step().float(), b.step().float()
     assert (la - lb).abs().max().item() < 2e-2 * lb.abs().max().item()
+
+
+def test_fused_rope_kv_append_equals_the_three_ops():
+    from aliyun_gpushare_device_plugin_amd.ops import rope_, rope_tables
+
+    B, Hq, Hkv, D = 3, 8, 2, 128
+    cos, sin = rope_tables(512, D, 500000.0, "cuda")
+    qkv = torch.randn(B, (Hq + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16)
+    pos = torch.tensor([0, 17, 300], dtype=torch.int32, device="cuda")
+    ka, va = ops.kv_cache(B, Hkv, 512, D)
+    kb, vb = ops.kv_cache(B, Hkv, 512, D)
+    ref = qkv.clone()
+    q, k, v = ref[:, :Hq * D], ref[:, Hq * D:(Hq + Hkv) * D], ref[:, (Hq + Hkv) * D:]
+    rope_(q, cos, sin, Hq, D, 512, positions=pos)
+    rope_(k, cos, sin, Hkv, D, 512, positions=pos)
+    ops.kv_append(k, v, ka, va, pos)
+    ops.rope_kv_append(qkv, cos, sin, pos, kb, vb, Hq)
+    torch.cuda.synchronize()
+    assert torch.equal(qkv[:, :(Hq + Hkv) * D], ref[:, :(Hq + Hkv) * D])
+    assert torch.equal(ka, kb) and torch.equal(va, vb)
+
+
+def test_silu_mul_interleaved_layout():
+    gu = torch.randn(5, 2 * 1024, device="cuda", dtype=torch.bfloat16)
+    deint = gu.view(5, -1, 2, 16).transpose(1, 2).reshape(5, -1).contiguous()
+    assert torch.equal(ops.silu_mul(gu, interleaved=True), ops.silu_mul(deint))
