@@ -13,8 +13,10 @@
 //     step and the 4 waves 32: 64 lanes x 32 B = 2 KiB contiguous per wave-step; q is pre-scaled
 //     by softmax_scale * log2(e) so the softmax runs on exp2;
 //   * softmax: one wave per query head, over the CHUNK scores held in LDS;
-//   * P·V: the 4 waves take interleaved positions, 64 / G lanes per head with D * G / 64 dims each
-//     (16-B loads for G = 4), then a cross-wave LDS reduction;
+//   * P·V: each wave instruction reads 4 whole V rows (16 lanes x 16 B per row) and every lane
+//     accumulates all G heads for its 8 dims; shuffles + an LDS pass reduce rows and waves
+//     (the first version gave each head its own 16 lanes, so an instruction fetched one 256-B
+//     row four times over: 2.85 TB/s in the model, profiles/decode/README.md);
 //   * partials (m, l, unnormalised o) per split go to a float workspace; a second kernel merges
 //     the splits of each (b, q head) and writes bf16.
 #include "common.h"
@@ -39,8 +41,6 @@ __global__ __launch_bounds__(NT) void decode_split(const unsigned short* __restr
                                                    const int* __restrict__ lens, float* __restrict__ o_part,
                                                    float* __restrict__ ml_part, int Hkv, int Smax, int nsplit,
                                                    float qscale) {
-  constexpr int DPL = D * G / 64;         // P·V dims per lane
-  constexpr int LPH = 64 / G;             // P·V lanes per head
   __shared__ float S[G][CHUNK];
   __shared__ float red[4][G * D];
   __shared__ float ML[G][2];
@@ -118,26 +118,43 @@ __global__ __launch_bounds__(NT) void decode_split(const unsigned short* __restr
   }
   __syncthreads();
 
-  // ---- P·V: waves take positions wave, wave + 4, ...; lane -> (head, DPL dims) --------------
-  const int g = lane / LPH, d0 = (lane % LPH) * DPL;
-  float acc[DPL];
+  // ---- P·V: lane -> (row r = lane / 16, dims (lane % 16) * 8); a wave instruction reads 4 whole
+  // V rows (1 KiB) and every lane accumulates all G heads for its 8 dims; the 4 row lanes of a dim
+  // group are then summed with two shuffles and the 4 waves through LDS ------------------------
+  const int rsub = lane >> 4, d0 = (lane & 15) * 8;
+  float acc[G][8];
 #pragma unroll
-  for (int i = 0; i < DPL; ++i) acc[i] = 0.f;
-#pragma unroll 16   // 16 V rows in flight per lane: the P·V loop is latency-bound at unroll 4
-  for (int p = wave; p < n; p += 4) {
-    const float w = S[g][p];
-    const unsigned short* vr = vp + (size_t)p * D + d0;
-    if constexpr (DPL == 8) {
-      const u16x8_t v8 = *(const u16x8_t*)vr;
+  for (int gg = 0; gg < G; ++gg)
 #pragma unroll
-      for (int i = 0; i < 8; ++i) acc[i] = fmaf(w, bf16_to_f32(v8[i]), acc[i]);
-    } else {
+    for (int i = 0; i < 8; ++i) acc[gg][i] = 0.f;
+#pragma unroll 8
+  for (int p = wave * 4 + rsub; p < n; p += 16) {
+    const u16x8_t v8 = *(const u16x8_t*)(vp + (size_t)p * D + d0);
+    float vf[8];
 #pragma unroll
-      for (int i = 0; i < DPL; ++i) acc[i] = fmaf(w, bf16_to_f32(vr[i]), acc[i]);
+    for (int i = 0; i < 8; ++i) vf[i] = bf16_to_f32(v8[i]);
+#pragma unroll
+    for (int gg = 0; gg < G; ++gg) {
+      const float w = S[gg][p];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[gg][i] = fmaf(w, vf[i], acc[gg][i]);
     }
   }
 #pragma unroll
-  for (int i = 0; i < DPL; ++i) red[wave][g * D + d0 + i] = acc[i];
+  for (int gg = 0; gg < G; ++gg)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float v = acc[gg][i];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      acc[gg][i] = v;
+    }
+  if (rsub == 0) {
+#pragma unroll
+    for (int gg = 0; gg < G; ++gg)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) red[wave][gg * D + d0 + i] = acc[gg][i];
+  }
   __syncthreads();
   for (int e = tid; e < G * D; e += NT) {
     const int gg = e / D, d = e % D;
