@@ -28,6 +28,7 @@ def main(argv=None):
     ap.add_argument("--name", default="pod")
     ap.add_argument("--mode", default="prefill", choices=("prefill", "decode"))
     ap.add_argument("--decode-window", type=int, default=256, help="decode steps before rewinding to the prompt")
+    ap.add_argument("--eager", action="store_true", help="decode: launch kernel by kernel instead of a hipGraph")
     a = ap.parse_args(argv)
 
     import torch
@@ -51,7 +52,8 @@ def main(argv=None):
 
         srv = LlamaServer(model, a.batch, a.seq + a.decode_window + 1)
         srv.prefill(tok)
-        srv.capture()
+        if not a.eager:
+            srv.capture()
     else:
         model.forward(tok)
     torch.cuda.synchronize()
@@ -81,7 +83,7 @@ def main(argv=None):
         else:
             if srv.host_len >= srv.max_ctx:
                 srv.rewind(a.seq)
-            srv.step()
+            srv.step(use_graph=not a.eager)
         torch.cuda.synchronize()
         n += 1
         now = time.perf_counter()

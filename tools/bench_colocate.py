@@ -115,7 +115,8 @@ def admit_pair(args, isolation: str):
 def run_mode(args, isolation: str) -> dict:
     env_a, env_b, alloc_ms = admit_pair(args, isolation)
     extra_b = ["--batch", str(args.batch_b)] if args.batch_b else []
-    extra_a = ["--mode", args.mode_a] + (["--seq", str(args.seq_a)] if args.seq_a else [])
+    extra_a = (["--mode", args.mode_a] + (["--seq", str(args.seq_a)] if args.seq_a else [])
+               + (["--eager"] if args.decode_eager else []))
     solo = run_pods([("llama-a", env_a, ["--probe-quota"] + extra_a)], args.seconds, args)[0]
     both = run_pods([("llama-a", env_a, extra_a), ("llama-b", env_b, extra_b)], args.seconds, args)
     solo_b = run_pods([("llama-b", env_b, extra_b)], args.seconds, args)[0] if args.batch_b else None
@@ -164,6 +165,7 @@ def main():
     ap.add_argument("--mode-a", default="prefill", choices=("prefill", "decode"),
                     help="decode: pod A is a serving pod (KV-cache decode, hipGraph per step)")
     ap.add_argument("--seq-a", type=int, default=0, help="pod A's prompt length (0 = --seq)")
+    ap.add_argument("--decode-eager", action="store_true", help="pod A decodes without a hipGraph")
     ap.add_argument("--layers", type=int, default=32)
     ap.add_argument("--smi-backend", default="auto")
     ap.add_argument("--isolation", default="none", choices=("none", "cu", "both"),
@@ -174,7 +176,7 @@ def main():
     args = ap.parse_args()
 
     modes = ["none", "cu"] if args.isolation == "both" else [args.isolation]
-    res = {"config": "2 x Llama-3-8B bf16 pods on one MI355X (BASELINE config 4)", "mode_a": args.mode_a,
+    res = {"config": "2 x Llama-3-8B bf16 pods on one MI355X (BASELINE config 4)", "mode_a": args.mode_a, "decode_eager": args.decode_eager,
            "pod_gib": args.pod_gib, "batch": args.batch, "batch_b": args.batch_b or args.batch, "seq": args.seq,
            "layers": args.layers}
     for m in modes:
