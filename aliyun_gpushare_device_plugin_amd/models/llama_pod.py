@@ -29,7 +29,13 @@ def main(argv=None):
     ap.add_argument("--mode", default="prefill", choices=("prefill", "decode"))
     ap.add_argument("--decode-window", type=int, default=256, help="decode steps before rewinding to the prompt")
     ap.add_argument("--eager", action="store_true", help="decode: launch kernel by kernel instead of a hipGraph")
+    ap.add_argument("--graph", action="store_true",
+                    help="decode: replay a hipGraph even under CU slots (default: eager when GPUSHARE_CU_SLOTS is "
+                         "set, since graph replay in a CU-masked pod stalls next to a busy neighbour: "
+                         "profiles/cu_mask/README.md)")
     a = ap.parse_args(argv)
+    if os.environ.get("GPUSHARE_CU_SLOTS") and not a.graph:
+        a.eager = True
 
     import torch
 
