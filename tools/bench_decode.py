@@ -84,7 +84,7 @@ def gemm_micro(M, N, K):
     set_skinny_variant(SKINNY_LDS)
     from aliyun_gpushare_device_plugin_amd.ops import _lib
 
-    for tgt in (256, 512, 1024, 2048):
+    for tgt in (1, 256, 512, 1024, 2048):
         _lib.lib().gs_skinny_set_wg_target(tgt)
         res[f"lds_wg{tgt}_us"] = round(timed(lambda: ops.skinny_linear(x, w, out=out), 50) * 1e6, 1)
     _lib.lib().gs_skinny_set_wg_target(512)
