@@ -174,10 +174,12 @@ def set_skinny_variant(v: int) -> None:
 
 
 def skinny_linear(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | None = None,
-                  out: torch.Tensor | None = None) -> torch.Tensor:
+                  out: torch.Tensor | None = None, norm_weight: torch.Tensor | None = None, eps: float = 1e-5):
     """Decode-shaped ``x @ w.T (+ residual)`` for ``x`` ``[M <= 64, K]`` on the split-K skinny
     kernel (native/kernels/gemm_skinny.hip): an HBM stream over ``w`` with the batch as the MFMA's
-    16-row operand. ``out`` may be ``residual`` itself (in-place residual add)."""
+    16-row operand. ``out`` may be ``residual`` itself (in-place residual add). With
+    ``norm_weight`` it returns ``(out, rmsnorm(out) * norm_weight)``, the norm computed in the same
+    pass that reduces the K splits (one launch less per residual projection)."""
     _check_operand(x, "x")
     _check_operand(w, "w")
     if x.dim() != 2 or w.dim() != 2 or x.shape[1] != w.shape[1]:
@@ -200,8 +202,18 @@ def skinny_linear(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | Non
     L = _lib.lib()
     splits = L.gs_skinny_splits(N, K)
     part = torch.empty(splits * M * N, dtype=torch.float32, device=x.device) if splits > 1 else None
-    rc = L.gs_skinny_gemm_bf16(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), rptr,
-                               out.stride(0), M, N, K, splits, part.data_ptr() if part is not None else None,
-                               _lib.stream_ptr(x.device))
-    _lib.check(rc, "gs_skinny_gemm_bf16")
-    return out
+    pptr = part.data_ptr() if part is not None else None
+    if norm_weight is None:
+        rc = L.gs_skinny_gemm_bf16(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), rptr,
+                                   out.stride(0), M, N, K, splits, pptr, _lib.stream_ptr(x.device))
+        _lib.check(rc, "gs_skinny_gemm_bf16")
+        return out
+    _check_operand(norm_weight, "norm_weight")
+    if norm_weight.shape != (N,) or not norm_weight.is_contiguous() or N > 8192 or out.stride(0) % 8:
+        raise ValueError("skinny_linear: norm_weight must be contiguous [N] with N <= 8192")
+    xn = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
+    rc = L.gs_skinny_gemm_norm_bf16(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), rptr,
+                                    out.stride(0), M, N, K, splits, pptr, norm_weight.data_ptr(), xn.data_ptr(),
+                                    N, float(eps), _lib.stream_ptr(x.device))
+    _lib.check(rc, "gs_skinny_gemm_norm_bf16")
+    return out, xn

@@ -225,6 +225,64 @@ __global__ __launch_bounds__(256) void skinny_reduce(const float* __restrict__ p
   *(u16x4_t*)(Y + (size_t)m * ldy + n) = o;
 }
 
+// Decode fusion of the split reduction with the RMSNorm that always follows a residual
+// projection: per row m, h = sum_s part[s, m, :] + R[m, :] (or h = Y[m, :] when the GEMM ran
+// unsplit and already wrote it), Y = bf16(h), xn = bf16(h * rsqrt(mean(h^2) + eps) * nw) with
+// the norm taken over the stored bf16 values, as ops.rmsnorm does. One workgroup per row.
+__global__ __launch_bounds__(256) void skinny_reduce_norm(const float* __restrict__ part, int splits,
+                                                          unsigned short* __restrict__ Y,
+                                                          const unsigned short* __restrict__ R, int ldy, int M, int N,
+                                                          const unsigned short* __restrict__ nw,
+                                                          unsigned short* __restrict__ xn, int ldxn, float eps) {
+  constexpr int MAXV = 4;                       // N <= 256 threads x 4 vectors x 8 = 8192
+  const int m = blockIdx.x, nvec = N / 8;
+  float v[MAXV][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int t = 0; t < MAXV; ++t) {
+    const int vi = threadIdx.x + t * 256;
+    if (vi >= nvec) continue;
+    const int n = vi * 8;
+    u16x8_t hv;
+    if (part) {
+      f32x4_t a = *(const f32x4_t*)(part + (size_t)m * N + n), b = *(const f32x4_t*)(part + (size_t)m * N + n + 4);
+      for (int p = 1; p < splits; ++p) {
+        a += *(const f32x4_t*)(part + ((size_t)p * M + m) * N + n);
+        b += *(const f32x4_t*)(part + ((size_t)p * M + m) * N + n + 4);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float h = e < 4 ? a[e] : b[e - 4];
+        if (R) h += bf16_to_f32(R[(size_t)m * ldy + n + e]);
+        hv[e] = f32_to_bf16(h);
+      }
+      *(u16x8_t*)(Y + (size_t)m * ldy + n) = hv;
+    } else {
+      hv = *(const u16x8_t*)(Y + (size_t)m * ldy + n);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      v[t][e] = bf16_to_f32(hv[e]);
+      ss += v[t][e] * v[t][e];
+    }
+  }
+  __shared__ float red[4];
+  ss = wave_sum(ss);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+  __syncthreads();
+  const float inv = rsqrtf((red[0] + red[1] + red[2] + red[3]) / (float)N + eps);
+#pragma unroll
+  for (int t = 0; t < MAXV; ++t) {
+    const int vi = threadIdx.x + t * 256;
+    if (vi >= nvec) continue;
+    const u16x8_t wv = *(const u16x8_t*)(nw + vi * 8);
+    u16x8_t o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = f32_to_bf16(v[t][e] * inv * bf16_to_f32(wv[e]));
+    *(u16x8_t*)(xn + (size_t)m * ldxn + vi * 8) = o;
+  }
+}
+
 }  // namespace
 
 // Features per wave (16 x NT) and split-K factor for a shape: NT = 4 once the grid has >= 1024
@@ -284,8 +342,23 @@ GS_KERNEL_API int gs_skinny_splits(int N, int K) {
 // X [M, K] (ldx), W [N, K] (ldw), Y [M, N] (ldy), optional residual R with Y's layout (may alias Y).
 // part: float workspace of splits * M * N (ignored when splits == 1). Requires M in [1, 64],
 // N % 64 == 0, K % 32 == 0, ldx / ldw % 8 == 0, ldy % 4 == 0, 16-B aligned X and W.
-GS_KERNEL_API int gs_skinny_gemm_bf16(const void* X, int ldx, const void* W, int ldw, void* Y, const void* R, int ldy,
-                                      int M, int N, int K, int splits, void* part, hipStream_t stream) {
+// Post-GEMM step: the plain split reduction, or (nw != null) the reduction fused with RMSNorm.
+static void finish(float* pp, int nsplit, void* Y, const void* R, int ldy, int M, int N, const void* nw, void* xn,
+                   int ldxn, float eps, hipStream_t stream) {
+  if (nw) {
+    hipLaunchKernelGGL(skinny_reduce_norm, dim3(M), dim3(256), 0, stream, (const float*)pp, nsplit,
+                       (unsigned short*)Y, (const unsigned short*)R, ldy, M, N, (const unsigned short*)nw,
+                       (unsigned short*)xn, ldxn, eps);
+  } else if (pp) {
+    const int n4 = M * N / 4;
+    hipLaunchKernelGGL(skinny_reduce, dim3((n4 + 255) / 256), dim3(256), 0, stream, (const float*)pp, nsplit,
+                       (unsigned short*)Y, (const unsigned short*)R, ldy, M, N);
+  }
+}
+
+static int skinny_launch(const void* X, int ldx, const void* W, int ldw, void* Y, const void* R, int ldy, int M, int N,
+                         int K, int splits, void* part, const void* nw, void* xn, int ldxn, float eps,
+                         hipStream_t stream) {
   if (M < 1 || M > 64 || N % 64 || K % 32 || K <= 0 || ldx % 8 || ldw % 8 || ldy % 4 || ldx < K || ldw < K ||
       ldy < N || splits < 1 || (splits > 1 && !part))
     return GS_EINVAL;
@@ -307,11 +380,7 @@ GS_KERNEL_API int gs_skinny_gemm_bf16(const void* X, int ldx, const void* W, int
       case 3: go(skinny_lds<3>); break;
       default: go(skinny_lds<4>); break;
     }
-    if (pp) {
-      const int n4 = M * N / 4;
-      hipLaunchKernelGGL(skinny_reduce, dim3((n4 + 255) / 256), dim3(256), 0, stream, (const float*)pp, nsplit,
-                         (unsigned short*)Y, (const unsigned short*)R, ldy, M, N);
-    }
+    finish(pp, nsplit, Y, R, ldy, M, N, nw, xn, ldxn, eps, stream);
     return gs_launch_status();
   }
   int nt, planned;
@@ -342,10 +411,19 @@ GS_KERNEL_API int gs_skinny_gemm_bf16(const void* X, int ldx, const void* W, int
     GS_SKINNY_NT(1)
   }
 #undef GS_SKINNY_NT
-  if (pp) {
-    const int n4 = M * N / 4;
-    hipLaunchKernelGGL(skinny_reduce, dim3((n4 + 255) / 256), dim3(256), 0, stream, (const float*)pp, nsplit,
-                       (unsigned short*)Y, (const unsigned short*)R, ldy, M, N);
-  }
+  finish(pp, nsplit, Y, R, ldy, M, N, nw, xn, ldxn, eps, stream);
   return gs_launch_status();
+}
+
+GS_KERNEL_API int gs_skinny_gemm_bf16(const void* X, int ldx, const void* W, int ldw, void* Y, const void* R, int ldy,
+                                      int M, int N, int K, int splits, void* part, hipStream_t stream) {
+  return skinny_launch(X, ldx, W, ldw, Y, R, ldy, M, N, K, splits, part, nullptr, nullptr, 0, 0.f, stream);
+}
+
+// Same GEMM, then xn = RMSNorm(Y) * nw in the reduction pass (N % 8 == 0, N <= 8192, ldxn % 8 == 0).
+GS_KERNEL_API int gs_skinny_gemm_norm_bf16(const void* X, int ldx, const void* W, int ldw, void* Y, const void* R,
+                                           int ldy, int M, int N, int K, int splits, void* part, const void* nw,
+                                           void* xn, int ldxn, float eps, hipStream_t stream) {
+  if (!nw || !xn || N > 8192 || ldy % 8 || ldxn % 8 || ldxn < N) return GS_EINVAL;
+  return skinny_launch(X, ldx, W, ldw, Y, R, ldy, M, N, K, splits, part, nw, xn, ldxn, eps, stream);
 }

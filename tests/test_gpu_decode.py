@@ -144,3 +144,19 @@ def test_silu_mul_interleaved_layout():
     gu = torch.randn(5, 2 * 1024, device="cuda", dtype=torch.bfloat16)
     deint = gu.view(5, -1, 2, 16).transpose(1, 2).reshape(5, -1).contiguous()
     assert torch.equal(ops.silu_mul(gu, interleaved=True), ops.silu_mul(deint))
+
+
+@pytest.mark.parametrize("K", [4096, 14336, 512])
+def test_skinny_linear_fused_rmsnorm(K):
+    torch.manual_seed(K)
+    M, N = 32, 4096
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.02
+    r = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    g = torch.rand(N, device="cuda", dtype=torch.bfloat16) + 0.5
+    want_h = ops.skinny_linear(x, w, residual=r.clone())
+    want_x = ops.rmsnorm(want_h, g, 1e-5)
+    h, xn = ops.skinny_linear(x, w, residual=r, out=r, norm_weight=g, eps=1e-5)
+    assert h.data_ptr() == r.data_ptr()
+    assert (h.float() - want_h.float()).abs().max().item() <= 1e-2 * want_h.float().abs().max().item()
+    assert (xn.float() - want_x.float()).abs().max().item() < 3e-2
