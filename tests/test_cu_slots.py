@@ -217,3 +217,29 @@ def test_e2e_slot_request_annotation_survives_scheduling():
             assert adm.error is None
             got.append(dict(adm.responses[0].envs)[const.ENV_HSA_CU_MASK])
         assert got == ["0:0-127", "0:128-255"]
+
+
+def test_slots_survive_a_plugin_restart():
+    """The plugin keeps no slot state of its own: after a restart (SIGHUP) it rebuilds the GPU's
+    occupied slots from the pods' annotations and hands the next pod a disjoint run."""
+    import signal
+    import time
+
+    from aliyun_gpushare_device_plugin_amd.sim.cluster import SimCluster
+
+    with SimCluster([("n", "fake:1x309220868096B")], compute_isolation="cu") as c:
+        runs = []
+        for s in (128, 64):
+            pod, _, adm = c.run_pod(s)
+            runs.append(C.SlotRun.parse(dict(adm.responses[0].envs)[const.ENV_CU_SLOTS]))
+            c.wait_assigned(pod)
+        mgr = c.manager("n")
+        mgr.events.put(("signal", signal.SIGHUP))
+        t = time.time() + 10
+        while mgr.restarts < 1 and time.time() < t:
+            time.sleep(0.05)
+        assert mgr.restarts == 1 and c.nodes["n"].kubelet.registered.wait(10)
+        _, _, adm = c.run_pod(64)
+        new = C.SlotRun.parse(dict(adm.responses[0].envs)[const.ENV_CU_SLOTS])
+        held = {s for r in runs for s in range(r.start, r.end)}
+        assert not held & set(range(new.start, new.end)), (runs, new)
