@@ -37,6 +37,7 @@ SIGNATURES = {
     "gs_skinny_set_nt": [_I],
     "gs_skinny_set_variant": [_I],
     "gs_skinny_set_wg_target": [_I],
+    "gs_skinny_set_lds_waves": [_I],
 }
 
 ERRORS = {1: "invalid arguments", 2: "kernel launch failed"}

@@ -126,37 +126,40 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_nt(const unsigned short* __
 // above reads 16 rows x 64 B per instruction) and X is fetched once per workgroup instead of once
 // per wave. The next slice's loads are in flight (in registers) while the MFMAs consume the
 // current one. Rows are padded by 16 B in LDS to spread the 16-B fragment reads over the banks.
+// NW = waves per workgroup (16 W rows each): 4; 2 (twice the workgroups) is selectable for
+// measurement.
 constexpr int LBN = 64, LBK = 256, LROW = LBK + 8;
 
-template <int MT>
-__global__ __launch_bounds__(256) void skinny_lds(const unsigned short* __restrict__ X, int ldx,
+template <int MT, int NW>
+__global__ __launch_bounds__(NW * 64) void skinny_lds(const unsigned short* __restrict__ X, int ldx,
                                                   const unsigned short* __restrict__ W, int ldw,
                                                   float* __restrict__ part, unsigned short* __restrict__ Y,
                                                   const unsigned short* __restrict__ R, int ldy, int M, int N, int K,
                                                   int kchunk) {
-  __shared__ __attribute__((aligned(16))) unsigned short sW[LBN * LROW];
+  constexpr int RPI = 2 * NW;                             // rows per global load instruction
+  __shared__ __attribute__((aligned(16))) unsigned short sW[16 * NW * LROW];
   __shared__ __attribute__((aligned(16))) unsigned short sX[MT * 16 * LROW];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int n0 = blockIdx.x * LBN, split = blockIdx.y;
+  const int n0 = blockIdx.x * 16 * NW, split = blockIdx.y;
   const int k0 = split * kchunk, k1 = min(K, k0 + kchunk);
   if (k0 >= k1) return;
   const int lr = tid >> 5, lc = (tid & 31) * 8;           // global->LDS: row group, column
-  constexpr int XI = MT * 2;                              // X row groups of 8 (M padded to 16 MT)
+  constexpr int XI = MT * 16 / RPI;                       // X row groups (M padded to 16 MT)
   u16x8_t wr[8], xr[XI];
   auto gload = [&](int kk) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) wr[i] = *(const u16x8_t*)(W + (size_t)(n0 + 8 * i + lr) * ldw + kk + lc);
+    for (int i = 0; i < 8; ++i) wr[i] = *(const u16x8_t*)(W + (size_t)(n0 + RPI * i + lr) * ldw + kk + lc);
 #pragma unroll
     for (int i = 0; i < XI; ++i) {
-      const int m = 8 * i + lr;
+      const int m = RPI * i + lr;
       xr[i] = m < M ? *(const u16x8_t*)(X + (size_t)m * ldx + kk + lc) : u16x8_t{};
     }
   };
   auto lstore = [&]() {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) *(u16x8_t*)(sW + (8 * i + lr) * LROW + lc) = wr[i];
+    for (int i = 0; i < 8; ++i) *(u16x8_t*)(sW + (RPI * i + lr) * LROW + lc) = wr[i];
 #pragma unroll
-    for (int i = 0; i < XI; ++i) *(u16x8_t*)(sX + (8 * i + lr) * LROW + lc) = xr[i];
+    for (int i = 0; i < XI; ++i) *(u16x8_t*)(sX + (RPI * i + lr) * LROW + lc) = xr[i];
   };
   f32x4_t acc[MT];
 #pragma unroll
@@ -292,6 +295,18 @@ static int g_variant = 0;    // 0 = auto (LDS-staged when K % 256 == 0), 1 = reg
 
 static bool use_lds(int K) { return g_variant == 2 || (g_variant == 0 && K % LBK == 0); }
 
+static int g_lds_waves = 0;  // 0 = default (4); 2 / 4 forced
+
+// 2-wave workgroups were measured slower on every decode shape (each workgroup re-stages X, and
+// the gate/up went 39 -> 46 us at batch 32: profiles/decode/micro_lds_waves.jsonl), so 4 it is.
+static int lds_waves(int) { return g_lds_waves ? g_lds_waves : 4; }
+
+GS_KERNEL_API int gs_skinny_set_lds_waves(int nw) {
+  if (nw != 0 && nw != 2 && nw != 4) return GS_EINVAL;
+  g_lds_waves = nw;
+  return GS_OK;
+}
+
 // LDS variant: 64 features per workgroup; splits double (>= 512 k each) until the grid has
 // g_wg_target workgroups, unless W is wide enough (>= 256 workgroups) on its own. Measured on
 // MI355X over targets 256-2048 (profiles/decode/micro_lds_wg_sweep.jsonl): splitting the 28672-wide
@@ -369,16 +384,17 @@ static int skinny_launch(const void* X, int ldx, const void* W, int ldw, void* Y
     kchunk = (kchunk + LBK - 1) / LBK * LBK;
     const int nsplit = (K + kchunk - 1) / kchunk;
     float* pp = nsplit > 1 ? (float*)part : nullptr;
-    const dim3 grid(N / LBN, nsplit);
+    const int waves = lds_waves(N);
+    const dim3 grid(N / (16 * waves), nsplit);
     auto go = [&](auto kern) {
-      hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, (const unsigned short*)X, ldx, (const unsigned short*)W,
+      hipLaunchKernelGGL(kern, grid, dim3(waves * 64), 0, stream, (const unsigned short*)X, ldx, (const unsigned short*)W,
                          ldw, pp, (unsigned short*)Y, (const unsigned short*)R, ldy, M, N, K, kchunk);
     };
     switch (mt) {
-      case 1: go(skinny_lds<1>); break;
-      case 2: go(skinny_lds<2>); break;
-      case 3: go(skinny_lds<3>); break;
-      default: go(skinny_lds<4>); break;
+      case 1: waves == 2 ? go(skinny_lds<1, 2>) : go(skinny_lds<1, 4>); break;
+      case 2: waves == 2 ? go(skinny_lds<2, 2>) : go(skinny_lds<2, 4>); break;
+      case 3: waves == 2 ? go(skinny_lds<3, 2>) : go(skinny_lds<3, 4>); break;
+      default: waves == 2 ? go(skinny_lds<4, 2>) : go(skinny_lds<4, 4>); break;
     }
     finish(pp, nsplit, Y, R, ldy, M, N, nw, xn, ldxn, eps, stream);
     return gs_launch_status();

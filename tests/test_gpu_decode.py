@@ -71,7 +71,7 @@ def test_decode_steps_match_full_recompute_and_graph_matches_eager():
     assert graph.host_len == 43 and int(graph.pos[0]) == 43
 
 
-@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("variant", [1, 2, 3])
 @pytest.mark.parametrize("M,N,K", [(1, 256, 512), (7, 512, 4096), (16, 1024, 1024), (32, 4096, 4096),
                                    (33, 6144, 4096), (64, 256, 14336), (32, 4096, 14336), (5, 192, 96)])
 def test_skinny_linear_matches_fp32(M, N, K, variant):
@@ -79,11 +79,17 @@ def test_skinny_linear_matches_fp32(M, N, K, variant):
 
     if variant == 2 and K % 256:
         pytest.skip("LDS variant needs K % 256 == 0")
-    set_skinny_variant(variant)
+    from aliyun_gpushare_device_plugin_amd.ops import _lib
+
+    if variant == 3 and K % 256:
+        pytest.skip("LDS variant needs K % 256 == 0")
+    set_skinny_variant(min(variant, 2))
+    _lib.lib().gs_skinny_set_lds_waves(2 if variant == 3 else 0)     # 3 = LDS kernel with 2-wave workgroups
     try:
         _check_skinny(M, N, K)
     finally:
         set_skinny_variant(SKINNY_AUTO)
+        _lib.lib().gs_skinny_set_lds_waves(0)
 
 
 def _check_skinny(M, N, K):

@@ -89,6 +89,10 @@ def gemm_micro(M, N, K):
         res[f"lds_wg{tgt}_us"] = round(timed(lambda: ops.skinny_linear(x, w, out=out), 50) * 1e6, 1)
     _lib.lib().gs_skinny_set_wg_target(512)
     res["lds_us"] = res["lds_wg512_us"]
+    for nw in (4, 2):
+        _lib.lib().gs_skinny_set_lds_waves(nw)
+        res[f"lds_nw{nw}_us"] = round(timed(lambda: ops.skinny_linear(x, w, out=out), 50) * 1e6, 1)
+    _lib.lib().gs_skinny_set_lds_waves(0)
     set_skinny_variant(SKINNY_AUTO)
     res["ntauto_us"] = round(timed(lambda: ops.skinny_linear(x, w, out=out), 50) * 1e6, 1)
     t_ours = res["ntauto_us"] * 1e-6
