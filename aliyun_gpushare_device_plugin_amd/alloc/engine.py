@@ -270,6 +270,7 @@ class Allocator:
             held += [r for u, (gi, r, _) in self._slot_pending.items() if gi == claim.gpu_index and u != claim.uid]
             run, exclusive = cuslots.choose(held, k, nslots)
             self._slot_pending[claim.uid] = (claim.gpu_index, run, now)
+            self.metrics.cu_slots_held.set(sum(r.count for r in held) + run.count, gpu=str(claim.gpu_index))
         claim.slots = run
         if not exclusive:
             self.metrics.allocate_outcomes.inc(outcome="cu_shared")

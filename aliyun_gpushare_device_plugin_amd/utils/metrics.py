@@ -188,6 +188,9 @@ class PluginMetrics:
         self.shim_quota = r.gauge("gpushare_container_hbm_quota_bytes", "Container HBM quota (shim ledger)")
         self.shim_peak = r.gauge("gpushare_container_hbm_peak_bytes", "Container HBM high-water mark (shim ledger)")
         self.shim_denied = r.gauge("gpushare_container_quota_denials", "Allocations refused by the quota shim")
+        self.cu_slots_held = r.gauge("gpushare_cu_slots_held",
+                                     "CU slots held by pods per GPU at the last compute-isolation decision "
+                                     "(slot = one CU on every XCD; > slots per GPU means oversubscribed)")
 
 
 def serve(registry: Registry, addr: str, health_fn=None) -> http.server.ThreadingHTTPServer:

@@ -110,6 +110,7 @@ def test_engine_gives_disjoint_runs_and_records_them_on_the_pod():
         assert e[const.ENV_ROC_CU_MASK] == C.roc_cu_mask(run, 8)
         runs.append(run)
     assert [r.count for r in runs] == [14, 7, 7, 3]
+    assert 'gpushare_cu_slots_held{gpu="0"} 31' in al.metrics.registry.render()
     slots = [s for r in runs for s in range(r.start, r.end)]
     assert len(slots) == len(set(slots))                        # exclusive
     patched = {name: p["metadata"]["annotations"] for _, name, p in cl.patches}
