@@ -54,6 +54,8 @@ class FakeKubelet:
         self._stub = None
         self._law_thread = None
         self._allocated: dict[str, set] = {}
+        self._used: set = set()                 # union of _allocated, kept incrementally
+        self._healthy: list[str] = []           # healthy IDs in advertised order, per device update
         self._lock = threading.Lock()
         self._stop = threading.Event()
 
@@ -144,8 +146,10 @@ class FakeKubelet:
         try:
             for resp in stub.ListAndWatch(api.Empty()):
                 devs = {d.ID: d.health for d in resp.devices}
+                healthy = [d for d, h in devs.items() if h == const.HEALTHY]
                 with self.devices_updated:
                     self.devices = devs
+                    self._healthy = healthy
                     self.list_updates += 1
                     self.devices_updated.notify_all()
                 self.registered.set()
@@ -179,8 +183,8 @@ class FakeKubelet:
 
     # -- device manager -------------------------------------------------------------------
     def _free_healthy(self) -> list[str]:
-        used = set().union(*self._allocated.values()) if self._allocated else set()
-        return [d for d, h in self.devices.items() if h == const.HEALTHY and d not in used]
+        used = self._used
+        return [d for d in self._healthy if d not in used]
 
     def admit(self, pod: dict, timeout: float = 10.0) -> Admission:
         uid = O.uid(pod)
@@ -203,6 +207,7 @@ class FakeKubelet:
                     if len(pref) == n and set(pref) <= set(free):
                         ids = pref
                 self._allocated.setdefault(uid, set()).update(ids)
+                self._used.update(ids)
             t0 = time.perf_counter()
             try:
                 resp = self._stub.Allocate(api.AllocateRequest(container_requests=[
@@ -219,8 +224,8 @@ class FakeKubelet:
 
     def release(self, pod_uid: str):
         with self._lock:
-            self._allocated.pop(pod_uid, None)
+            self._used.difference_update(self._allocated.pop(pod_uid, ()))
 
     def allocated_ids(self) -> set:
         with self._lock:
-            return set().union(*self._allocated.values()) if self._allocated else set()
+            return set(self._used)
