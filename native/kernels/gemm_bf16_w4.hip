@@ -201,10 +201,15 @@ __global__ __launch_bounds__(NT, 1) void gemm_bf16_nt_w4a(
   // Buffer descriptors over this block's 256 rows of A and B (base and size from kernel
   // arguments and blockIdx only, so they stay in SGPRs); the per-lane part is one VGPR offset,
   // the DMA index i and the K-tile go into the scalar soffset, so a DMA costs no VALU.
-  const __amdgpu_buffer_rsrc_t rA =
+  // In the last two K-tiles the DMA slot has no tile left to fetch: it runs on zero-size descriptors
+  // (every lane out of range, so no memory traffic and nothing for the final vmcnt wait to cover).
+  const __amdgpu_buffer_rsrc_t rA_live =
       __builtin_amdgcn_make_buffer_rsrc((void*)(A + (size_t)m0 * lda), (short)0, BM * lda * 2, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rB =
+  const __amdgpu_buffer_rsrc_t rB_live =
       __builtin_amdgcn_make_buffer_rsrc((void*)(B + (size_t)n0 * ldb), (short)0, BN * ldb * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rA_dead = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rB_dead = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, 0, 0x00020000);
+  __amdgpu_buffer_rsrc_t rA = rA_live, rB = rB_live;
   const unsigned voffA = (unsigned)(drow * lda + dc * 8) * 2u;
   const unsigned voffB = (unsigned)(drow * ldb + dc * 8) * 2u;
   const unsigned a32 = 64u * lda, b32 = 64u * ldb;   // bytes of 32 rows
@@ -262,11 +267,15 @@ __global__ __launch_bounds__(NT, 1) void gemm_bf16_nt_w4a(
   __builtin_amdgcn_sched_barrier(0);
 
   // One loop body for every tile, so the accumulators keep one register assignment (a peeled
-  // tail made hipcc shuffle them through VGPRs). Past the end, the DMA re-fetches tile KT-1 into
-  // the buffer just released and phase B reads a dead fragment set: both harmless.
+  // tail made hipcc shuffle them through VGPRs). Past the end, the DMA runs on the zero-size
+  // descriptors (zeros into the buffer just released) and phase B reads a dead fragment set.
   for (int kt = 0; kt < KT; ++kt) {
     const int buf = kt & 1;
     const int kdma = min(kt + 2, KT - 1);
+    if (kt + 2 >= KT) {
+      rA = rA_dead;
+      rB = rB_dead;
+    }
     // hipcc may place the accumulators' zero-init (v_accvgpr_write) right before the loop:
     // 2 wait states before an MFMA reads them as srcC (2 cycles per 4k-cycle iteration)
     asm volatile("s_nop 1" ::: "memory");
