@@ -37,7 +37,7 @@ constexpr int STAGE = 2 * A_STAGE;     // A + B
 constexpr int LDS_BYTES = 2 * STAGE;   // 128 KiB
 constexpr int GROUP_M = 8;
 
-enum { EP_BIAS = 1, EP_SILU = 2, EP_RESID = 4, EP_SWIGLU = 8 };
+enum { EP_BIAS = 1, EP_SILU = 2, EP_RESID = 4, EP_SWIGLU = 8, EP_STAGED = 16 };   // 16: internal only
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
@@ -133,6 +133,38 @@ __device__ __forceinline__ void epilogue_128x128(f32x4_t (&acc)[8][8], unsigned 
       *(u32x4_t*)(C + (size_t)m * ldc + ncol + 32 * jp) = u32x4_t{w[0][0], w[0][1], w[1][0], w[1][1]};
     }
     __builtin_amdgcn_sched_barrier(0);   // one row of tiles at a time: bounds VGPR pressure
+  }
+}
+
+// Plain epilogue staged through LDS (opt-in, GS_W4_STAGED_EPI=1): each wave writes its 128 x 128
+// bf16 tile into its own 32 KiB of the (by then dead) operand buffers, 16-B chunks XOR-swizzled by
+// row so the 16 rows a ds_write_b64 touches fall in distinct banks, then streams it out 4 full
+// 256-B rows per store instruction (8 whole 128-B lines) instead of 16 rows x 64 B.
+__device__ __forceinline__ void epilogue_staged(f32x4_t (&acc)[8][8], unsigned short* __restrict__ C, int ldc,
+                                                char* wsmem, int mtile, int ntile, int lane) {
+  const int lr = lane & 15, q = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    asm volatile("" : "+a"(acc[i][0]), "+a"(acc[i][1]), "+a"(acc[i][2]), "+a"(acc[i][3]), "+a"(acc[i][4]),
+                 "+a"(acc[i][5]), "+a"(acc[i][6]), "+a"(acc[i][7]));
+    const int r = lr + 16 * i;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+      const u32x2_t w = {(unsigned)f32_to_bf16(acc[i][j][0]) | ((unsigned)f32_to_bf16(acc[i][j][1]) << 16),
+                         (unsigned)f32_to_bf16(acc[i][j][2]) | ((unsigned)f32_to_bf16(acc[i][j][3]) << 16)};
+      const int chunk = 2 * j + (q >> 1);
+      *(u32x2_t*)(wsmem + r * 256 + ((chunk ^ (r & 15)) << 4) + (q & 1) * 8) = w;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+  const int chunk = lane & 15;
+#pragma unroll 8
+  for (int rb = 0; rb < 32; ++rb) {
+    const int r = rb * 4 + (lane >> 4);
+    const u32x4_t v = *(const u32x4_t*)(wsmem + r * 256 + ((chunk ^ (r & 15)) << 4));
+    *(u32x4_t*)(C + (size_t)(mtile + r) * ldc + ntile + chunk * 8) = v;
   }
 }
 
@@ -303,7 +335,13 @@ __global__ __launch_bounds__(NT, 1) void gemm_bf16_nt_w4a(
     if (kt == KT - 1) asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
   }
 
-  if constexpr ((EPI & EP_SWIGLU) != 0)
+  if constexpr ((EPI & EP_STAGED) != 0) {
+    // the operand buffers are dead once every wave is past its last fragment read and the
+    // (zero-size) tail DMAs have landed
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    epilogue_staged(acc, C, ldc, smem + wave * 32768, m0 + wm * 128, n0 + wn * 128, lane);
+  } else if constexpr ((EPI & EP_SWIGLU) != 0)
     epilogue_swiglu(acc, C, ldc, m0 + wm * 128 + lr, (n0 + wn * 128) / 2, lane >> 4);
   else
     epilogue_128x128<EPI>(acc, C, bias, R, ldc, m0 + wm * 128 + lr, n0 + wn * 128 + (lane >> 4) * 4, lane >> 4);
@@ -322,13 +360,17 @@ int gs_gemm_w4_launch(const void* A, const void* B, void* C, const void* bias, c
   // the best of the placements swept on MI355X (profiles/gemm_w4_variants.md)
   using Kern = void (*)(const unsigned short*, const unsigned short*, unsigned short*, const unsigned short*,
                        const unsigned short*, int, int, int, int, int, int, int);
-  static const Kern kerns[9] = {gemm_bf16_nt_w4a<16, 2, 3, 1, 0>, gemm_bf16_nt_w4a<16, 2, 3, 1, 1>,
+  static const Kern kerns[10] = {gemm_bf16_nt_w4a<16, 2, 3, 1, 0>, gemm_bf16_nt_w4a<16, 2, 3, 1, 1>,
                                 gemm_bf16_nt_w4a<16, 2, 3, 1, 2>, gemm_bf16_nt_w4a<16, 2, 3, 1, 3>,
                                 gemm_bf16_nt_w4a<16, 2, 3, 1, 4>, gemm_bf16_nt_w4a<16, 2, 3, 1, 5>,
                                 gemm_bf16_nt_w4a<16, 2, 3, 1, 6>, gemm_bf16_nt_w4a<16, 2, 3, 1, 7>,
-                                gemm_bf16_nt_w4a<16, 2, 3, 1, EP_SWIGLU>};
+                                gemm_bf16_nt_w4a<16, 2, 3, 1, EP_SWIGLU>, gemm_bf16_nt_w4a<16, 2, 3, 1, EP_STAGED>};
+  static const bool staged = [] {
+    const char* e = getenv("GS_W4_STAGED_EPI");
+    return e != nullptr && e[0] == '1';
+  }();
   if ((flags & EP_SWIGLU) && (flags & 7)) return GS_EINVAL;   // SwiGLU takes no other epilogue
-  const Kern kern = kerns[(flags & EP_SWIGLU) ? 8 : (flags & 7)];
+  const Kern kern = kerns[(flags & EP_SWIGLU) ? 8 : (flags & 7) ? (flags & 7) : staged ? 9 : 0];
   static bool attr_set = false;
   if (!attr_set) {
     for (Kern k : kerns)
