@@ -11,14 +11,18 @@ from __future__ import annotations
 
 import torch
 
-from ..ops import gemm_nt
+from ..ops import gemm_nt, gemm_nt_repeat
 
 GIB = 1 << 30
 
 
 class GemmPlayer:
     def __init__(self, share_bytes: int, device: torch.device | int = 0, m: int = 4096, n: int = 4096,
-                 k: int = 4096, touch_fraction: float = 0.9, seed: int = 0, pool: torch.Tensor | None = None):
+                 k: int = 4096, touch_fraction: float = 0.9, seed: int = 0, pool: torch.Tensor | None = None,
+                 fused_burst: bool = False):
+        # fused_burst: a burst is ONE dispatch of `iters` identical GEMMs (ops.gemm_nt_repeat)
+        # instead of `iters` launches, so the CUs never drain at kernel boundaries
+        self.fused_burst = fused_burst
         self.device = torch.device("cuda", device) if isinstance(device, int) else device
         self.m, self.n, self.k = m, n, k
         self.stream = torch.cuda.Stream(self.device)
@@ -52,8 +56,11 @@ class GemmPlayer:
 
     def run(self, iters: int):
         with torch.cuda.stream(self.stream):
-            for _ in range(iters):
-                gemm_nt(self.a, self.b, out=self.c)
+            if self.fused_burst:
+                gemm_nt_repeat(self.a, self.b, self.c, iters)
+            else:
+                for _ in range(iters):
+                    gemm_nt(self.a, self.b, out=self.c)
         self.flops += 2.0 * self.m * self.n * self.k * iters
 
     def synchronize(self):

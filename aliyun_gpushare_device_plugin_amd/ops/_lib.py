@@ -19,6 +19,7 @@ _P, _I, _F = _c.c_void_p, _c.c_int, _c.c_float
 
 SIGNATURES = {
     "gs_gemm_bf16_nt": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
+    "gs_gemm_bf16_nt_repeat": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
     "gs_gemm_set_variant": [_I],
     "gs_gemm_set_group_m": [_I],
     "gs_rmsnorm_bf16": [_P, _P, _P, _P, _P, _I, _I, _F, _P],

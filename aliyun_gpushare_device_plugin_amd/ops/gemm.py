@@ -55,6 +55,29 @@ def deinterleave_gate_up(w: torch.Tensor) -> torch.Tensor:
     return torch.cat((v[:, 0].reshape(-1, K), v[:, 1].reshape(-1, K)), 0)
 
 
+def gemm_nt_repeat(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, reps: int) -> torch.Tensor:
+    """``out = a @ b^T`` computed ``reps`` times in ONE dispatch of the 4-wave kernel (grid.y = reps):
+    the GEMM player's burst without a drain at every kernel boundary. Same FLOPs as ``reps`` calls of
+    :func:`gemm_nt`; every repetition stores identical values to ``out``. Falls back to a loop of
+    :func:`gemm_nt` for shapes the 4-wave kernel does not take (M, N % 256, K % 128, 16-B rows)."""
+    _check_operand(a, "a")
+    _check_operand(b, "b")
+    M, K = a.shape
+    N = b.shape[0]
+    ok = (b.shape[1] == K and out.shape == (M, N) and out.dtype == torch.bfloat16 and out.stride(1) == 1
+          and 1 <= reps <= 65535 and M % 256 == 0 and N % 256 == 0 and K % 128 == 0
+          and a.stride(1) == 1 and b.stride(1) == 1 and out.stride(0) % 8 == 0 and out.data_ptr() % 16 == 0
+          and a.stride(0) % 8 == 0 and b.stride(0) % 8 == 0 and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0)
+    if ok:
+        rc = _lib.lib().gs_gemm_bf16_nt_repeat(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, a.stride(0),
+                                               b.stride(0), out.stride(0), reps, _lib.stream_ptr(a.device))
+        _lib.check(rc, "gs_gemm_bf16_nt_repeat")   # shapes were checked above: any error is real
+        return out
+    for _ in range(reps):
+        gemm_nt(a, b, out=out)
+    return out
+
+
 def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, bias: torch.Tensor | None = None,
             residual: torch.Tensor | None = None, silu: bool = False, swiglu: bool = False) -> torch.Tensor:
     """``out[M,N] = epi(a[M,K] @ b[N,K]^T)``; a and b are 2-D row-major (K contiguous).

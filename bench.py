@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--burst", type=int, default=40, help="GEMMs per resident pod per step")
     ap.add_argument("--gemm", type=int, default=4096, help="GEMM M=N=K")
+    ap.add_argument("--burst-mode", default="loop", choices=("loop", "fused"),
+                    help="a pod's burst as one launch per GEMM, or one dispatch of all of them (same FLOPs)")
     ap.add_argument("--no-gpu", action="store_true", help="control plane only (CPU)")
     ap.add_argument("--smi-backend", default=None, help="default: auto on GPU, fake:Nx288G on CPU")
     ap.add_argument("--pod-source", default="watch", choices=("watch", "list", "kubelet"))
@@ -272,7 +274,8 @@ def main():
         for uid, size in mine.items():
             if uid not in players:
                 players[uid] = GemmPlayer(total * size // units, dev, a.gemm, a.gemm, a.gemm,
-                                          seed=hash(uid) & 0xffff, pool=arena.alloc(uid, size))
+                                          seed=hash(uid) & 0xffff, pool=arena.alloc(uid, size),
+                                          fused_burst=a.burst_mode == "fused")
 
     def step(timed: bool):
         nonlocal gemm_flops
@@ -342,7 +345,7 @@ def main():
             "data": "synthetic pod specs (mixed 8-128 GiB), random-init bf16 GEMM operands",
             "config": {"model": "gpushare-device-plugin + MFMA GEMM pods (BASELINE config 3 churn)",
                        "global_batch": 4 * n, "seq_len": None, "parallelism": f"node{n}",
-                       "pods_per_gpu": 4, "burst_gemms": a.burst, "gemm_mnk": a.gemm,
+                       "pods_per_gpu": 4, "burst_gemms": a.burst, "burst_mode": a.burst_mode, "gemm_mnk": a.gemm,
                        "pod_source": a.pod_source, "smi_backend": smi},
             "allocate_p50_ms": round(pct(cp.alloc_lat, 0.5) * 1e3, 3) if cp.alloc_lat else None,
             "allocate_p99_ms": round(pct(cp.alloc_lat, 0.99) * 1e3, 3) if cp.alloc_lat else None,

@@ -37,4 +37,4 @@ inline int gs_launch_status() { return hipGetLastError() == hipSuccess ? GS_OK :
 // 4-wave GEMM launcher (gemm_bf16_w4.hip); GS_EINVAL when the shape or output layout does not
 // suit it (M % 256, N % 256, K % 128, ldc % 8, 16-B aligned C).
 int gs_gemm_w4_launch(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K,
-                      int lda, int ldb, int ldc, int flags, hipStream_t stream);
+                      int lda, int ldb, int ldc, int flags, hipStream_t stream, int reps = 1);

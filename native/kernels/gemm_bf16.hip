@@ -401,6 +401,16 @@ int g_variant = 0;   // 0 = auto, 1 = v1 (2-stage, 8 waves), 2 = v2 (ping-pong),
 
 }  // namespace
 
+// The GEMM-player path: C = A * B^T repeated `reps` times in one dispatch of the 4-wave kernel
+// (aligned shapes, no epilogue). GS_EINVAL when the shape does not suit it (caller loops instead).
+GS_KERNEL_API int gs_gemm_bf16_nt_repeat(const void* A, const void* B, void* C, int M, int N, int K, int lda,
+                                         int ldb, int ldc, int reps, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || lda % 8 || ldb % 8 || lda < K || ldb < K || ldc < N ||
+      ((uintptr_t)A & 15) || ((uintptr_t)B & 15))
+    return GS_EINVAL;
+  return gs_gemm_w4_launch(A, B, C, nullptr, nullptr, M, N, K, lda, ldb, ldc, g_group_m << 8, stream, reps);
+}
+
 GS_KERNEL_API int gs_gemm_bf16_nt(const void* A, const void* B, void* C, const void* bias, const void* R, int M,
                                   int N, int K, int lda, int ldb, int ldc, int flags, hipStream_t stream) {
   const bool swiglu = flags & EP_SWIGLU;   // out[M, N/2] = silu(gate) * up, gate/up rows interleaved by 16

@@ -352,7 +352,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_bf16_nt_w4a(
 // Launch the 4-wave kernel; the caller (gs_gemm_bf16_nt) has validated pointers/strides/flags.
 // Returns GS_EINVAL when the shape or output layout does not suit it (the caller falls back).
 int gs_gemm_w4_launch(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K,
-                      int lda, int ldb, int ldc, int flags, hipStream_t stream) {
+                      int lda, int ldb, int ldc, int flags, hipStream_t stream, int reps) {
+  if (reps < 1 || reps > 65535) return GS_EINVAL;
   if (M % BM || N % BN || K % (2 * BK)) return GS_EINVAL;
   if ((size_t)BM * lda * 2 > 0xffffffffu || (size_t)BN * ldb * 2 > 0xffffffffu) return GS_EINVAL;
   if (ldc % 8 || ((uintptr_t)C & 15)) return GS_EINVAL;   // 16-B epilogue stores
@@ -378,7 +379,10 @@ int gs_gemm_w4_launch(const void* A, const void* B, void* C, const void* bias, c
     attr_set = true;
   }
   const int nblocks = (M / BM) * (N / BN);
-  kern<<<dim3(nblocks), dim3(NT), LDS_BYTES, stream>>>(
+  // reps > 1: the same GEMM `reps` times in one dispatch (grid.y; tile_origin reads blockIdx.x only),
+  // so back-to-back repetitions refill CUs as workgroups retire instead of draining at each kernel
+  // boundary. Every repetition computes the full product and stores identical values to C.
+  kern<<<dim3(nblocks, reps), dim3(NT), LDS_BYTES, stream>>>(
       (const unsigned short*)A, (const unsigned short*)B, (unsigned short*)C, (const unsigned short*)bias,
       (const unsigned short*)R, M, N, K, lda, ldb, ldc, flags);
   return gs_launch_status();

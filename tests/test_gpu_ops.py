@@ -40,6 +40,21 @@ def test_gemm_nt_matches_fp32(M, N, K):
     assert_close_bf16(out, ref_linear(a, b), K)
 
 
+@pytest.mark.parametrize("M,N,K,reps", [(256, 256, 128, 1), (512, 768, 256, 3), (2048, 1024, 1024, 5),
+                                        (300, 256, 192, 2)])
+def test_gemm_nt_repeat_matches_fp32(M, N, K, reps):
+    """One dispatch of `reps` identical GEMMs (grid.y) gives the single GEMM's result; the
+    unaligned shape takes the loop fallback."""
+    from aliyun_gpushare_device_plugin_amd.ops import gemm_nt, gemm_nt_repeat
+    a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    b = torch.randn(N, K, device="cuda", dtype=torch.bfloat16)
+    out = torch.full((M, N), float("nan"), device="cuda", dtype=torch.bfloat16)
+    gemm_nt_repeat(a, b, out, reps)
+    torch.cuda.synchronize()
+    assert_close_bf16(out, ref_linear(a, b), K)
+    assert torch.equal(out, gemm_nt(a, b))
+
+
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (256, 256, 64), (512, 768, 256), (2048, 1024, 4096),
                                    (4096, 4096, 4096)])
 def test_gemm_pingpong_matches_v1_and_fp32(M, N, K):
