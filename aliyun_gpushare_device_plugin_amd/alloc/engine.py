@@ -71,6 +71,12 @@ class AllocatorOptions:
     rocr_visible: bool = False
     match_containers: bool = True
     claim_ttl_s: float = 120.0
+    # a multi-container pod's containers are allocated back to back by the kubelet; a claim not
+    # continued within this window is abandoned
+    partial_claim_ttl_s: float = 10.0
+    # write-behind: how often the patcher re-checks bound pods that this plugin answered but
+    # that still read ASSIGNED=false (lost PATCH, restart) and patches them again
+    reconcile_s: float = 30.0
     complete_swaps: bool = True
     # host directory for file-backed shim ledgers (mounted read-write into every shared
     # container at const.LEDGER_CONTAINER_DIR); None = pod-private POSIX shm ledgers
@@ -91,10 +97,11 @@ class _Claim:
     uid: str
     pod: dict
     gpu_index: int
-    next_container: int
-    gpu_containers: list   # indices of containers that request gpu-mem
-    t: float
+    next_container: int    # gpu containers of ``shape`` already answered
+    shape: tuple           # the pod's gpu-mem requests, one per gpu container, in container order
+    t: float               # last time a container of this pod was answered
     slots: cuslots.SlotRun | None = None
+    swap: bool = False     # matched through swap completion (the pod is bound, not Pending)
 
 
 class Allocator:
@@ -105,32 +112,63 @@ class Allocator:
         self.metrics = metrics or PluginMetrics()
         self._mu = threading.Lock()
         self._claims: dict[str, _Claim] = {}      # in-flight (multi-container or PATCH pending)
+        self._partial: _Claim | None = None       # the multi-container pod being admitted right now
+        self._tainted: dict[str, float] = {}      # uid -> time: reservation partly used by another pod
         self._assigned: dict[str, float] = {}     # uid -> time we assigned it (stale-cache guard)
         self._unpatched: set[str] = set()         # assigned locally, PATCH not yet acknowledged
         self._pinfo: dict[tuple, tuple] = {}      # memoised per-pod-version facts (see _info)
         self._patch_q = None
         self._slot_mu = threading.Lock()
         self._slot_pending: dict[str, tuple] = {}  # uid -> (gpu, SlotRun, t): chosen, not yet on the pod
+        self._stop = threading.Event()
+        self._last_reconcile = time.monotonic()
         self.journal = AllocJournal(self.opts.journal_path, self.opts.journal_ttl_s)
         if self.opts.async_patch:
             import queue
             self._patch_q = queue.Queue()
+            # a previous instance answered these pods but never saw their PATCH land (crash,
+            # kill, apiserver outage): they stay claimed and are patched again first
+            for e in self.journal.unlanded():
+                self._assigned[e["uid"]] = time.monotonic()
+                self._unpatched.add(e["uid"])
+                self._patch_q.put(_PatchJob(e["uid"], e["ns"], e["name"], e.get("ann") or {}, recovered=True))
+                self.metrics.allocate_outcomes.inc(outcome="patch_recovered")
+                log.warning("write-behind: re-queueing the unlanded ASSIGNED patch of pod %s/%s (uid %s)",
+                            e["ns"], e["name"], e["uid"])
             threading.Thread(target=self._patcher, name="assign-patcher", daemon=True).start()
+
+    def reconfigure(self, model: DeviceModel, pods: PodSource, client: APIClient | None,
+                    opts: AllocatorOptions) -> "Allocator":
+        """Plugin rebuild (kubelet restart, SIGHUP; ``gpumanager.go:82-96``): new devices, pod
+        source and node-label options, but the same claims, assigned set, pending patches and
+        patcher — a rebuild must never forget a pod it already answered (write-behind)."""
+        with self._mu:
+            self.model, self.pods, self.client = model, pods, client
+            async_patch = self.opts.async_patch
+            self.opts = dataclasses.replace(opts, async_patch=async_patch, journal_path=self.opts.journal_path)
+            self._pinfo.clear()
+        return self
+
+    def close(self):
+        self._stop.set()
+        if self._patch_q is not None:
+            self._patch_q.put(None)
 
     # ------------------------------------------------------------------------------------
     # candidate selection
     # ------------------------------------------------------------------------------------
-    def _info(self, p: dict) -> tuple[bool, int, int]:
-        """(assumed, pod gpu-mem, assume time) of one pod version, memoised: every Allocate scans
-        all Pending pods, and re-parsing their specs dominated the handler. The
-        key carries the two annotations the plugin itself rewrites, so an object updated in
-        place (no new resourceVersion) is never served stale."""
+    def _info(self, p: dict) -> tuple[bool, int, int, tuple]:
+        """(assumed, pod gpu-mem, assume time, gpu-container shape) of one pod version,
+        memoised: every Allocate scans all Pending pods, and re-parsing their specs dominated
+        the handler. The key carries the two annotations the plugin itself
+        rewrites, so an object updated in place (no new resourceVersion) is never served stale."""
         ann = O.annotations(p)
         k = (O.uid(p), O.resource_version(p), ann.get(const.ENV_ASSIGNED_FLAG),
              ann.get(const.ENV_RESOURCE_ASSUME_TIME))
         v = self._pinfo.get(k)
         if v is None:
-            v = (A.is_assumed_pod(p), O.gpu_mem_of_pod(p), A.assume_time(p))
+            shape = tuple(x for x in O.gpu_mem_per_container(p) if x > 0)
+            v = (A.is_assumed_pod(p), sum(shape), A.assume_time(p), shape)
             if len(self._pinfo) > 8192:
                 self._pinfo.clear()
             self._pinfo[k] = v
@@ -142,10 +180,16 @@ class Allocator:
         for u, t in list(self._assigned.items()):
             if now - t > self.opts.claim_ttl_s and u not in self._unpatched:
                 del self._assigned[u]
+        if fresh and self._tainted:   # forget a withheld reservation once its pod is gone
+            live = {O.uid(p) for p in self.pods.node_pods() if not O.deleting(p)}
+            for u in [u for u in self._tainted if u not in live]:
+                del self._tainted[u]
         out = []
         for p in pods:
-            assumed, _, at = self._info(p)
-            if assumed and O.uid(p) not in self._assigned:
+            assumed, _, at, _ = self._info(p)
+            u = O.uid(p)
+            # a pod being deleted is never admitted by the kubelet
+            if assumed and u not in self._assigned and u not in self._tainted and not O.deleting(p):
                 out.append((at, len(out), p))
         out.sort(key=lambda e: (e[0], e[1]))      # assume time, then arrival order (stable)
         if log.V(4):
@@ -153,53 +197,122 @@ class Allocator:
                 log.info("candidate pod %s in ns %s with timestamp %d is found.", O.name(p), O.namespace(p), at)
         return [p for _, _, p in out]
 
-    def _match(self, req_units: int, fresh: bool) -> tuple[_Claim | None, bool]:
+    def _partial_state(self, c: _Claim, cands: list[dict], now: float) -> str:
+        """"live": the claimed pod can still be continued; "stale": it exists but the claim
+        outlived ``partial_claim_ttl_s``; "gone": deleted or being deleted."""
+        if c.swap:
+            alive = any(O.uid(p) == c.uid and not O.deleting(p) for p in self.pods.node_pods())
+        else:
+            alive = any(O.uid(p) == c.uid for p in cands)
+        if not alive:
+            return "gone"
+        return "stale" if now - c.t > self.opts.partial_claim_ttl_s else "live"
+
+    def _match(self, sizes: tuple, fresh: bool) -> tuple[_Claim | None, bool]:
         """Returns (claim, complete). ``complete`` = every gpu container of the pod is now
-        allocated, so the pod must be PATCHed ASSIGNED."""
-        # 1) continue a multi-container pod already in progress (container order = kubelet order)
-        for c in sorted(self._claims.values(), key=lambda c: A.assume_time(c.pod)):
-            if c.next_container < len(c.gpu_containers):
-                want = O.container_limit(O.containers(c.pod)[c.gpu_containers[c.next_container]])
-                if want == req_units:
-                    c.next_container += 1
-                    return c, c.next_container == len(c.gpu_containers)
-        cands = [p for p in self._candidates(fresh) if O.uid(p) not in self._claims]
-        # 2) the reference rule: pod-total equals the request
+        allocated, so the pod must be PATCHed ASSIGNED.
+
+        ``sizes`` = the request's per-container unit counts. The kubelet admits one pod at a
+        time and calls Allocate once per gpu container, back to back; an AllocateRequest names
+        no pod. So a pod only ever matches a request of its own *shape*: a single-container
+        request takes a single-container pod of that size, never a multi-container pod whose
+        total happens to be equal (the reference's pod-total rule, ``allocate.go:79-89``, is the
+        special case shape == (total,)). A multi-container pod is claimed on its first container
+        and continued only by the very next Allocate, while the pod still exists; anything else
+        abandons the claim and the pod becomes a candidate again."""
+        k = len(sizes)
+        now = time.monotonic()
+        cands = self._candidates(fresh)
+        c = self._partial
+        if c is not None:
+            state = self._partial_state(c, cands, now)
+            if state == "live" and c.shape[c.next_container:c.next_container + k] == sizes:
+                self._partial = None
+                c.next_container += k
+                c.t = now
+                done = c.next_container == len(c.shape)
+                if not done:
+                    self._partial = c
+                return c, done
+            if not fresh:
+                return None, False           # decide on an authoritative LIST, not on the cache
+            self._partial = None
+            self._claims.pop(c.uid, None)
+            if state == "gone":
+                # the claimed pod is deleted: it was the pod being admitted, nothing is in use
+                self.metrics.allocate_outcomes.inc(outcome="claim_abandoned")
+                log.warning("pod %s: deleted after %d/%d gpu containers were allocated; claim released",
+                            O.name(c.pod), c.next_container, len(c.shape))
+            else:
+                # The pod still exists but the kubelet did not continue it: the containers
+                # answered from its reservation went to another pod of the same leading shape
+                # (out-of-order admission), which may be running on them. The reservation is
+                # never handed out again while the pod lives (no double booking of its HBM);
+                # its own admission, if it comes, is matched elsewhere or refused.
+                self._tainted[c.uid] = now
+                self.metrics.allocate_outcomes.inc(outcome="claim_tainted")
+                log.warning("pod %s: %d/%d gpu containers answered from its reservation, then the kubelet moved on "
+                            "(%s); reservation withheld", O.name(c.pod), c.next_container, len(c.shape),
+                            "stale" if state == "stale" else f"next container {list(sizes)}")
+                cands = [p for p in cands if O.uid(p) != c.uid]
+                if state == "live":
+                    # the pod being admitted is another one whose gpu containers start with what
+                    # was answered: continue it when it is reserved on the same GPU
+                    done_shape = c.shape[:c.next_container] + sizes
+                    for p in cands:
+                        shape = self._info(p)[3]
+                        if (O.uid(p) not in self._claims and shape[:len(done_shape)] == done_shape
+                                and A.gpu_id_from_annotation(p) == c.gpu_index):
+                            self.metrics.allocate_outcomes.inc(outcome="claim_retargeted")
+                            log.warning("pod %s: containers answered so far fit pod %s (same GPU %d); claim moved",
+                                        O.name(c.pod), O.name(p), c.gpu_index)
+                            if len(shape) == len(done_shape):
+                                return _Claim(O.uid(p), p, c.gpu_index, len(done_shape), shape, now), True
+                            return self._start_partial(p, shape, len(done_shape), now, swap=False), False
+        cands = [p for p in cands if O.uid(p) not in self._claims]
+        # 1) the earliest-assumed pod whose gpu containers start with this request: exactly
+        #    this shape (single-container pods: the reference rule), or the first containers of
+        #    a multi-container pod (claimed, continued by the next Allocates)
         for p in cands:
-            if self._info(p)[1] == req_units:
-                gc = [i for i, v in enumerate(O.gpu_mem_per_container(p)) if v > 0]
-                c = _Claim(O.uid(p), p, A.gpu_id_from_annotation(p), len(gc), gc, time.monotonic())
-                return c, True
-        # 3) multi-container pods: first gpu container's request equals this request
-        if self.opts.match_containers:
-            for p in cands:
-                per = O.gpu_mem_per_container(p)
-                gc = [i for i, v in enumerate(per) if v > 0]
-                if len(gc) > 1 and per[gc[0]] == req_units:
-                    c = _Claim(O.uid(p), p, A.gpu_id_from_annotation(p), 1, gc, time.monotonic())
-                    self._claims[c.uid] = c
-                    return c, False
-        # 4) swap completion (authoritative pass only): see the module docstring
+            shape = self._info(p)[3]
+            if shape == sizes:
+                return _Claim(O.uid(p), p, A.gpu_id_from_annotation(p), k, sizes, now), True
+            if self.opts.match_containers and len(shape) > k and shape[:k] == sizes:
+                return self._start_partial(p, shape, k, now, swap=False), False
+        # 2) swap completion (authoritative pass only): see the module docstring
         if fresh and self.opts.complete_swaps:
-            p = self._swap_partner(req_units)
+            p = self._swap_partner(sizes)
             if p is not None:
-                gc = [i for i, v in enumerate(O.gpu_mem_per_container(p)) if v > 0]
+                shape = self._info(p)[3]
                 self.metrics.allocate_outcomes.inc(outcome="swap")
-                log.warning("no pending pod requests %d%s: completing a swapped admission with pod %s (gpu %d)",
-                            req_units, self.opts.unit, O.name(p), A.gpu_id_from_annotation(p))
-                return _Claim(O.uid(p), p, A.gpu_id_from_annotation(p), len(gc), gc, time.monotonic()), True
+                log.warning("no pending pod requests %s%s: completing a swapped admission with pod %s (gpu %d)",
+                            list(sizes), self.opts.unit, O.name(p), A.gpu_id_from_annotation(p))
+                if len(shape) > k:
+                    return self._start_partial(p, shape, k, now, swap=True), False
+                return _Claim(O.uid(p), p, A.gpu_id_from_annotation(p), k, shape, now, swap=True), True
         return None, False
 
-    def _swap_partner(self, req_units: int) -> dict | None:
+    def _start_partial(self, p: dict, shape: tuple, k: int, now: float, swap: bool) -> _Claim:
+        c = _Claim(O.uid(p), p, A.gpu_id_from_annotation(p), k, shape, now, swap=swap)
+        self._claims[c.uid] = c
+        self._partial = c
+        return c
+
+    def _swap_partner(self, sizes: tuple) -> dict | None:
+        """A bound, un-assigned pod of the request's shape whose own admission took another
+        pod's reservation (equal shapes only, so per-GPU accounting stays exact)."""
         now_ns = time.time_ns()
         ttl_ns = int(self.opts.claim_ttl_s * 1e9)
+        k = len(sizes)
         out = []
         for p in A.dedupe_by_uid(self.pods.node_pods(), self.node):
             u = O.uid(p)
-            if (O.phase(p) == "Pending" or not A.is_assumed_pod(p) or u in self._assigned or u in self._claims
-                    or O.gpu_mem_of_pod(p) != req_units or now_ns - A.assume_time(p) > ttl_ns):
+            if (O.phase(p) == "Pending" or O.deleting(p) or not A.is_assumed_pod(p) or u in self._assigned
+                    or u in self._claims or u in self._tainted or self.journal.answered(u) or now_ns - A.assume_time(p) > ttl_ns):
                 continue
-            out.append(p)
+            shape = self._info(p)[3]
+            if shape[:k] == sizes:
+                out.append(p)
         out = A.order_by_assume_time(out)
         return out[0] if out else None
 
@@ -305,7 +418,8 @@ class Allocator:
     # ------------------------------------------------------------------------------------
     def allocate(self, req) -> api.AllocateResponse:
         t0 = time.perf_counter()
-        pod_units = sum(len(c.devices_ids) for c in req.container_requests)
+        sizes = tuple(len(c.devices_ids) for c in req.container_requests)
+        pod_units = sum(sizes)
         log.info("----Allocating GPU for gpu mem is started---- RequestPodGPUs: %d", pod_units)
         hist = self.metrics.allocate_latency
         jkey = request_key(req)
@@ -315,11 +429,11 @@ class Allocator:
             return replay
         try:
             with self._mu:
-                claim, complete = self._match(pod_units, fresh=False)
+                claim, complete = self._match(sizes, fresh=False)
                 t1 = time.perf_counter()
                 if claim is None:
                     # watch lag: the kubelet may see a bind before our cache does
-                    claim, complete = self._match(pod_units, fresh=True)
+                    claim, complete = self._match(sizes, fresh=True)
                 if claim is not None and complete:
                     self._claims[claim.uid] = claim   # held across the PATCH
                 t2 = time.perf_counter()
@@ -351,6 +465,8 @@ class Allocator:
                         O.name(claim.pod), idx)
             with self._mu:
                 self._claims.pop(claim.uid, None)
+                if self._partial is claim:
+                    self._partial = None
             return self._err_response(req, pod_units)
 
         pod_total = O.gpu_mem_of_pod(claim.pod)
@@ -362,18 +478,21 @@ class Allocator:
                                                                      claim.uid, max(0, slot0 + i), cu))
         if not complete:
             log.info("pod %s: container %d/%d of a multi-container pod allocated on GPU %d", O.name(claim.pod),
-                     claim.next_container, len(claim.gpu_containers), idx)
+                     claim.next_container, len(claim.shape), idx)
             self.metrics.allocate_outcomes.inc(outcome="partial")
             hist.observe(time.perf_counter() - t0, phase="total")
             return resp
 
         t3 = time.perf_counter()
         if self._patch_q is not None:
+            job = _PatchJob(claim.uid, O.namespace(claim.pod), O.name(claim.pod), self._extra_annotations(claim.uid))
+            # journal first: a crash after the reply must not lose the pending PATCH
+            self.journal.pending(job.uid, job.ns, job.name, job.ann)
             with self._mu:
                 self._claims.pop(claim.uid, None)
                 self._assigned[claim.uid] = time.monotonic()
                 self._unpatched.add(claim.uid)
-            self._patch_q.put(claim.pod)
+            self._patch_q.put(job)
             self.journal.record(req, claim.uid, resp, jkey)
             hist.observe(time.perf_counter() - t3, phase="patch")
             hist.observe(time.perf_counter() - t0, phase="total")
@@ -427,29 +546,94 @@ class Allocator:
         return None
 
     def _patcher(self):
-        """Lands queued ASSIGNED=true patches; retries with backoff until the pod is gone."""
-        while True:
-            pod = self._patch_q.get()
+        """Lands queued ASSIGNED=true patches (retrying with backoff until the pod is gone),
+        journals each landing, and when idle reconciles pods this plugin answered that still
+        read ASSIGNED=false."""
+        import queue
+        while not self._stop.is_set():
+            try:
+                job = self._patch_q.get(timeout=1.0)
+            except queue.Empty:
+                if time.monotonic() - self._last_reconcile >= self.opts.reconcile_s:
+                    self.reconcile()
+                continue
+            if job is None:
+                break
             delay = 0.05
-            while True:
+            while not self._stop.is_set():
                 try:
-                    updated = self._patch_assigned(pod)
+                    updated = self._land(job)
                     if updated:
                         self.pods.observe(updated)
-                        self._drop_slots(O.uid(pod))
+                    self._drop_slots(job.uid)
                     break
                 except APIError as e:
                     if e.not_found:
-                        self._drop_slots(O.uid(pod))
+                        self._drop_slots(job.uid)
                         break
-                    log.warning("assign patch for %s failed (%s); retrying", O.name(pod), e)
+                    log.warning("assign patch for %s failed (%s); retrying", job.name, e)
                 except Exception as e:  # noqa: BLE001 - transport errors
-                    log.warning("assign patch for %s failed (%s); retrying", O.name(pod), e)
-                time.sleep(delay)
+                    log.warning("assign patch for %s failed (%s); retrying", job.name, e)
+                self._stop.wait(delay)
                 delay = min(delay * 2, 5.0)
+            else:
+                break
+            self.journal.landed(job.uid)
             with self._mu:
-                self._unpatched.discard(O.uid(pod))
-                self._assigned[O.uid(pod)] = time.monotonic()
+                self._unpatched.discard(job.uid)
+                self._assigned[job.uid] = time.monotonic()
+
+    def _land(self, job: "_PatchJob") -> dict | None:
+        """One ASSIGNED PATCH of a queued job. The patch carries the pod's UID, and a job
+        recovered from the journal (or a conflict) first checks that the pod of that name is
+        still the one we answered: a re-created pod with the same name is never patched."""
+        if self.client is None:
+            return None
+        if job.recovered:
+            cur = self.client.get_pod(job.ns, job.name)
+            if O.uid(cur) != job.uid:
+                log.warning("pod %s/%s was re-created (uid %s, answered %s): dropping its pending patch",
+                            job.ns, job.name, O.uid(cur), job.uid)
+                return None
+            if A.is_assigned_pod(cur):
+                return cur
+        patch = A.assigned_patch()
+        patch["metadata"]["uid"] = job.uid
+        patch["metadata"]["annotations"].update(job.ann)
+        try:
+            return self.client.patch_pod(job.ns, job.name, patch)
+        except APIError as e:
+            if e.conflict or e.status == 422:
+                job.recovered = True      # re-check the pod's identity on the next attempt
+            raise
+
+    def reconcile(self) -> int:
+        """Re-queue the ASSIGNED patch of every bound pod this plugin answered (journal) that
+        still reads ASSIGNED=false and has no patch in flight — the write-behind counterpart of
+        the reference's "answer only after the PATCH landed" (``allocate.go:132-152``)."""
+        self._last_reconcile = time.monotonic()
+        if self._patch_q is None or self.client is None:
+            return 0
+        try:
+            pods = A.dedupe_by_uid(self.pods.node_pods(), self.node)
+        except Exception as e:  # noqa: BLE001
+            log.warning("reconcile: cannot list pods: %s", e)
+            return 0
+        n = 0
+        for p in pods:
+            u = O.uid(p)
+            if O.deleting(p) or A.is_assigned_pod(p) or not A.is_assumed_pod(p) or not self.journal.answered(u):
+                continue
+            with self._mu:
+                if u in self._unpatched:
+                    continue
+                self._unpatched.add(u)
+                self._assigned[u] = time.monotonic()
+            self._patch_q.put(_PatchJob(u, O.namespace(p), O.name(p), {}, recovered=True))
+            self.metrics.allocate_outcomes.inc(outcome="patch_reconciled")
+            log.warning("reconcile: pod %s answered by this plugin still reads ASSIGNED=false; patching", O.name(p))
+            n += 1
+        return n
 
     def flush_patches(self, timeout: float = 10.0) -> bool:
         """Wait until every queued ASSIGNED patch has landed (tests, shutdown)."""
@@ -461,14 +645,16 @@ class Allocator:
             time.sleep(0.005)
         return False
 
+    def _extra_annotations(self, uid: str) -> dict:
+        with self._slot_mu:
+            pend = self._slot_pending.get(uid)
+        return {const.POD_ANNOTATION_CU_SLOTS: pend[1].annotation()} if pend is not None else {}
+
     def _patch_assigned(self, pod: dict) -> dict | None:
         if self.client is None:
             return None
         patch = A.assigned_patch()
-        with self._slot_mu:
-            pend = self._slot_pending.get(O.uid(pod))
-        if pend is not None:
-            patch["metadata"]["annotations"][const.POD_ANNOTATION_CU_SLOTS] = pend[1].annotation()
+        patch["metadata"]["annotations"].update(self._extra_annotations(O.uid(pod)))
         ns, nm = O.namespace(pod), O.name(pod)
         try:
             return self.client.patch_pod(ns, nm, patch)
@@ -493,7 +679,8 @@ class Allocator:
             must = list(creq.must_include_deviceIDs)
             target = None
             for p in cands:
-                if O.gpu_mem_of_pod(p) == size or (O.gpu_mem_per_container(p) or [0])[0] == size:
+                shape = self._info(p)[3]
+                if shape and shape[0] == size:
                     target = self.model.uuid_by_index(A.gpu_id_from_annotation(p))
                     break
             picked = list(must)
@@ -514,6 +701,15 @@ class Allocator:
                     taken.add(d)
             resp.container_responses.add(deviceIDs=picked[:max(size, len(must))])
         return resp
+
+
+@dataclasses.dataclass
+class _PatchJob:
+    uid: str
+    ns: str
+    name: str
+    ann: dict              # extra annotations landed with ASSIGNED=true (CU slots)
+    recovered: bool = False
 
 
 def env_shim_host_dir() -> str | None:

@@ -1,14 +1,25 @@
-"""Allocate decision journal: idempotent answers to a retried admission.
+"""Allocate decision journal: idempotent answers and durable write-behind.
 
-The reference keeps no state (``allocate.go``): if the kubelet re-sends an Allocate after the
-plugin already matched the pod and patched it ``ASSIGNED=true`` (an RPC deadline hit, a
-plugin restart between the PATCH and the reply), the pod is no longer a candidate and the
-retry fails with ``no-gpu-has-N``. This journal remembers recent decisions keyed by the
-request's fake-device-ID set, in memory and optionally in an append-only JSON-lines file so
-they survive a plugin restart, and the engine replays one only when its pod still exists on
-this node *and is still Pending* — i.e. the kubelet is retrying that pod's admission. The
-kubelet recycles freed fake IDs for new pods, so a key alone is never trusted: once the
-journaled pod is gone or running, the entry is ignored and normal matching runs.
+The reference keeps no state (``allocate.go``) and answers Allocate only after its
+``ASSIGNED=true`` PATCH landed (``:132-152``). This build answers first and lands the PATCH
+in the background (write-behind, ``alloc/engine.py``), so the journal carries two kinds of
+record, in memory and optionally in an append-only JSON-lines file that survives a plugin
+restart or crash:
+
+* **answers** (``{"k", "uid", "t", "resp"}``), keyed by the request's fake-device-ID set: if
+  the kubelet re-sends an Allocate after the plugin already matched the pod (an RPC deadline
+  hit, a restart between the match and the reply), the engine replays the answer — but only
+  while the journaled pod still exists on this node *and is still Pending*. The kubelet
+  recycles freed fake IDs for new pods, so a key alone is never trusted.
+* **pending patches** (``{"op": "patch", "uid", "ns", "name", "ann"}``), written *before* the
+  reply leaves the plugin, and **landings** (``{"op": "landed", "uid"}``) once the apiserver
+  acknowledged the PATCH. On start-up every pending patch without a landing is re-queued, and
+  its pod stays claimed, so a pod can neither be left ``ASSIGNED=false`` forever nor be
+  matched a second time by the next plugin instance.
+
+Writes go through the page cache (``flush`` after each record, no ``fsync``): the journal
+must survive the *process* (kill, crash, OOM, DaemonSet rollout); a node crash takes the
+pods' containers down with it.
 """
 from __future__ import annotations
 
@@ -30,11 +41,16 @@ def request_key(req) -> str:
 
 
 class AllocJournal:
-    def __init__(self, path: str | None = None, ttl_s: float = 120.0, max_entries: int = 4096):
+    def __init__(self, path: str | None = None, ttl_s: float = 120.0, max_entries: int = 4096,
+                 pending_ttl_s: float = 24 * 3600.0):
         self.path, self.ttl_s, self.max_entries = path, ttl_s, max_entries
+        self.pending_ttl_s = pending_ttl_s
         self._mem: collections.OrderedDict[str, tuple[str, float, bytes]] = collections.OrderedDict()
+        self._uids: dict[str, float] = {}                       # pod uid -> time of its answer
+        self._pending: collections.OrderedDict[str, dict] = collections.OrderedDict()  # uid -> patch
         self._lock = threading.Lock()
         self._lines = 0
+        self._f = None
         if path:
             self._load()
 
@@ -46,47 +62,74 @@ class AllocJournal:
         except FileNotFoundError:
             return
         now = time.time()
-        for line in lines[-self.max_entries:]:
+        for line in lines:
             try:
                 e = json.loads(line)
-                if now - e["t"] <= self.ttl_s:
+                op = e.get("op", "answer")
+                if op == "patch":
+                    if now - e["t"] <= self.pending_ttl_s:
+                        self._pending[e["uid"]] = e
+                elif op == "landed":
+                    self._pending.pop(e["uid"], None)
+                elif now - e["t"] <= self.ttl_s:
                     self._mem[e["k"]] = (e["uid"], e["t"], base64.b64decode(e["resp"]))
                     self._mem.move_to_end(e["k"])
-            except (ValueError, KeyError):
-                continue
+                    self._uids[e["uid"]] = e["t"]
+            except (ValueError, KeyError, TypeError):
+                continue                                          # a torn last line after a crash
+        while len(self._mem) > self.max_entries:
+            self._mem.popitem(last=False)
         self._lines = len(lines)
-        log.info("allocation journal %s: %d recent decisions loaded", self.path, len(self._mem))
+        log.info("allocation journal %s: %d recent decisions, %d unlanded patches loaded", self.path,
+                 len(self._mem), len(self._pending))
+        self._compact()
 
-    def _append(self, key: str, uid: str, t: float, blob: bytes):
-        os.makedirs(os.path.dirname(self.path) or ".", exist_ok=True)
-        line = json.dumps({"k": key, "uid": uid, "t": t, "resp": base64.b64encode(blob).decode()})
-        with open(self.path, "a") as f:
-            f.write(line + "\n")
-        self._lines += 1
-        if self._lines > 2 * self.max_entries:
-            self._compact()
+    def _write(self, rec: dict):
+        if not self.path:
+            return
+        try:
+            if self._f is None:
+                os.makedirs(os.path.dirname(self.path) or ".", exist_ok=True)
+                self._f = open(self.path, "a")
+            self._f.write(json.dumps(rec, separators=(",", ":")) + "\n")
+            self._f.flush()
+            self._lines += 1
+            if self._lines > 2 * self.max_entries + 2 * len(self._pending) + 64:
+                self._compact()
+        except OSError as e:
+            log.warning("allocation journal write failed: %s", e)
 
     def _compact(self):
+        if not self.path:
+            return
         tmp = self.path + ".tmp"
-        with open(tmp, "w") as f:
-            for k, (uid, t, blob) in self._mem.items():
-                f.write(json.dumps({"k": k, "uid": uid, "t": t, "resp": base64.b64encode(blob).decode()}) + "\n")
-        os.replace(tmp, self.path)
-        self._lines = len(self._mem)
+        try:
+            os.makedirs(os.path.dirname(self.path) or ".", exist_ok=True)
+            with open(tmp, "w") as f:
+                for k, (uid, t, blob) in self._mem.items():
+                    f.write(json.dumps({"k": k, "uid": uid, "t": t, "resp": base64.b64encode(blob).decode()},
+                                       separators=(",", ":")) + "\n")
+                for e in self._pending.values():
+                    f.write(json.dumps(e, separators=(",", ":")) + "\n")
+            if self._f is not None:
+                self._f.close()
+                self._f = None
+            os.replace(tmp, self.path)
+            self._lines = len(self._mem) + len(self._pending)
+        except OSError as e:
+            log.warning("allocation journal compaction failed: %s", e)
 
-    # -- API --------------------------------------------------------------------------------
+    # -- answers ----------------------------------------------------------------------------
     def record(self, req, pod_uid: str, resp, key: str | None = None) -> None:
         key, t, blob = key or request_key(req), time.time(), resp.SerializeToString()
         with self._lock:
             self._mem[key] = (pod_uid, t, blob)
             self._mem.move_to_end(key)
+            self._uids[pod_uid] = t
             while len(self._mem) > self.max_entries:
-                self._mem.popitem(last=False)
-            if self.path:
-                try:
-                    self._append(key, pod_uid, t, blob)
-                except OSError as e:
-                    log.warning("allocation journal write failed: %s", e)
+                _, (u, _, _) = self._mem.popitem(last=False)
+                self._uids.pop(u, None)
+            self._write({"k": key, "uid": pod_uid, "t": t, "resp": base64.b64encode(blob).decode()})
 
     def lookup(self, req, key: str | None = None) -> tuple[str, object] | None:
         key = key or request_key(req)
@@ -95,6 +138,35 @@ class AllocJournal:
         if hit is None or time.time() - hit[1] > self.ttl_s:
             return None
         return hit[0], api.AllocateResponse.FromString(hit[2])
+
+    def answered(self, uid: str) -> bool:
+        """This plugin (or a previous instance, via the file) answered an Allocate for ``uid``
+        recently, or still owes it a PATCH."""
+        with self._lock:
+            t = self._uids.get(uid)
+            return uid in self._pending or (t is not None and time.time() - t <= self.ttl_s)
+
+    # -- write-behind patches ---------------------------------------------------------------
+    def pending(self, uid: str, ns: str, name: str, ann: dict | None = None) -> None:
+        rec = {"op": "patch", "uid": uid, "ns": ns, "name": name, "ann": dict(ann or {}), "t": time.time()}
+        with self._lock:
+            self._pending[uid] = rec
+            self._write(rec)
+
+    def landed(self, uid: str) -> None:
+        with self._lock:
+            if self._pending.pop(uid, None) is not None:
+                self._write({"op": "landed", "uid": uid})
+
+    def unlanded(self) -> list[dict]:
+        with self._lock:
+            return list(self._pending.values())
+
+    def close(self):
+        with self._lock:
+            if self._f is not None:
+                self._f.close()
+                self._f = None
 
     def __len__(self):
         return len(self._mem)

@@ -99,5 +99,10 @@ def node_internal_ip(node: dict) -> str:
     return "unknown"
 
 
+def deleting(pod: dict) -> bool:
+    """Graceful deletion started (``metadata.deletionTimestamp`` set)."""
+    return bool((pod.get("metadata") or {}).get("deletionTimestamp"))
+
+
 def is_terminated(pod: dict) -> bool:
     return phase(pod) in ("Succeeded", "Failed")

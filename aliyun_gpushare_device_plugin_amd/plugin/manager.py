@@ -87,6 +87,7 @@ class SharedGPUManager:
         self.plugin: DevicePluginServer | None = None
         self.health: HealthMonitor | None = None
         self.pod_source = None
+        self.allocator: Allocator | None = None
         self.model: DeviceModel | None = None
         self.started = threading.Event()
         self.restarts = 0
@@ -149,15 +150,22 @@ class SharedGPUManager:
             src = fallback
         self.pod_source = src
         shim = ShimConfig(cfg.shim_host_dir) if cfg.shim_host_dir else None
-        allocator = Allocator(model, src, self.client, cfg.node_name,
-                              AllocatorOptions(unit=cfg.memory_unit, disable_cgpu=disable_cgpu, shim=shim,
-                                               strict=cfg.strict_allocate, expose_devices=cfg.expose_devices,
-                                               rocr_visible=cfg.rocr_visible, async_patch=cfg.async_patch,
-                                               complete_swaps=cfg.complete_swaps,
-                                               ledger_dir=cfg.ledger_dir if shim else None,
-                                               journal_path=cfg.journal_path,
-                                               compute_isolation=cfg.compute_isolation),
-                              self.metrics)
+        opts = AllocatorOptions(unit=model.unit, disable_cgpu=disable_cgpu, shim=shim,
+                                strict=cfg.strict_allocate, expose_devices=cfg.expose_devices,
+                                rocr_visible=cfg.rocr_visible, async_patch=cfg.async_patch,
+                                complete_swaps=cfg.complete_swaps,
+                                ledger_dir=cfg.ledger_dir if shim else None,
+                                journal_path=cfg.journal_path,
+                                compute_isolation=cfg.compute_isolation)
+        if self.allocator is None:
+            if cfg.async_patch and not cfg.journal_path:
+                log.warning("write-behind ASSIGNED patches without --journal-path: a patch still queued when "
+                            "the plugin process dies is lost (the reconcile pass only covers restarts in-process)")
+            self.allocator = Allocator(model, src, self.client, cfg.node_name, opts, self.metrics)
+        else:
+            # rebuild: keep claims, assigned pods, queued patches and the patcher thread
+            self.allocator.reconfigure(model, src, self.client, opts)
+        allocator = self.allocator
         self.model = model
         return DevicePluginServer(model, allocator, self._plugin_socket(), const.RESOURCE_NAME,
                                   cfg.preferred_allocation, self.metrics)
@@ -283,6 +291,9 @@ class SharedGPUManager:
                 self.plugin.stop()
             if self.pod_source is not None:
                 self.pod_source.stop()
+            if self.allocator is not None:
+                self.allocator.flush_patches(2.0)
+                self.allocator.close()
             if self._metrics_srv is not None:
                 self._metrics_srv.shutdown()
         return rc

@@ -126,6 +126,26 @@ class Store:
         self.history: collections.deque = collections.deque(maxlen=history)  # (rv, type, old, new)
         self.watchers: list[_Watcher] = []
         self.requests = collections.Counter()
+        # fault injection: kind -> (monotonic deadline, HTTP status). "pod_patch" fails every
+        # metadata PATCH of a pod (not the kubelet's /status), "assign_patch" only the plugin's
+        # ASSIGNED=true patch
+        self.faults: dict[str, tuple[float, int]] = {}
+
+    def inject(self, kind: str, seconds: float, code: int = 503):
+        with self.lock:
+            if seconds <= 0:
+                self.faults.pop(kind, None)
+            else:
+                self.faults[kind] = (time.monotonic() + seconds, code)
+
+    def fault(self, kind: str) -> int | None:
+        f = self.faults.get(kind)
+        if f is None:
+            return None
+        if time.monotonic() >= f[0]:
+            self.faults.pop(kind, None)
+            return None
+        return f[1]
 
     def _bump(self, obj):
         self.rv += 1
@@ -182,6 +202,10 @@ class Store:
             want_rv = ((patch or {}).get("metadata") or {}).get("resourceVersion")
             if want_rv and want_rv != cur["metadata"]["resourceVersion"]:
                 raise ValueError("conflict")
+            want_uid = ((patch or {}).get("metadata") or {}).get("uid")
+            if want_uid and want_uid != cur["metadata"].get("uid"):
+                # kube-apiserver: "Precondition failed: UID in precondition: …" (409)
+                raise ValueError("uid precondition")
             if status_only:
                 patch = {"status": (patch or {}).get("status", {})}
             new = strategic_merge(cur, patch)
@@ -275,7 +299,7 @@ _NODE_RE = re.compile(r"^/api/v1/nodes(?:/([^/]+))?(?:/(status))?$")
 
 
 _REASONS = {200: "OK", 201: "Created", 404: "Not Found", 409: "Conflict", 410: "Gone", 400: "Bad Request",
-            405: "Method Not Allowed"}
+            405: "Method Not Allowed", 401: "Unauthorized", 503: "Service Unavailable"}
 
 
 def _status(code, reason, msg):
@@ -318,6 +342,9 @@ def route(store: Store, method: str, target: str, body: bytes):
         return _status(404, "NotFound", path)
     obj = json.loads(body) if body else {}
     if method == "POST":
+        if path == "/debug/faults":        # simulator fault injection: {"kind", "seconds", "code"}
+            store.inject(obj["kind"], float(obj.get("seconds", 0)), int(obj.get("code", 503)))
+            return 200, {"faults": {k: v[1] for k, v in store.faults.items()}}
         store.requests["POST " + path.split("/")[-1]] += 1
         m = _POD_RE.match(path)
         if m and not m.group(2):
@@ -336,6 +363,12 @@ def route(store: Store, method: str, target: str, body: bytes):
     if method == "PATCH":
         store.requests["PATCH " + ("status" if path.endswith("/status") else path.split("/")[3])] += 1
         m = _POD_RE.match(path)
+        if m and m.group(2) and not m.group(3):
+            assigning = ((obj.get("metadata") or {}).get("annotations") or {}).get(const.ENV_ASSIGNED_FLAG) == "true"
+            code = store.fault("pod_patch") or (store.fault("assign_patch") if assigning else None)
+            if code:
+                store.requests["PATCH dropped"] += 1
+                return _status(code, "ServiceUnavailable", "injected fault")
         if m and m.group(2):
             try:
                 p = store.patch_pod(m.group(1), m.group(2), obj, status_only=m.group(3) == "status")

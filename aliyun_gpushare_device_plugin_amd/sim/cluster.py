@@ -169,6 +169,23 @@ class SimCluster:
                                            name=f"plugin-{node.name}", daemon=True)
             node.thread.start()
 
+    def kill_plugin(self, node: str, sig: int = signal.SIGKILL):
+        """Fault injection: kill a process-mode plugin outright (no shutdown path runs)."""
+        n = self.nodes[node]
+        if n.proc is None:
+            raise RuntimeError("kill_plugin needs plugin_mode='process'")
+        n.proc.send_signal(sig)
+        n.proc.wait(timeout=10)
+
+    def restart_plugin(self, node: str, timeout: float = 30.0):
+        """Start the plugin of ``node`` again (after ``kill_plugin``) and wait until it has
+        re-registered with the fake kubelet and re-opened ListAndWatch."""
+        n = self.nodes[node]
+        n.kubelet.registered.clear()
+        self._start_plugin(n)
+        if not n.kubelet.registered.wait(timeout):
+            raise TimeoutError(f"plugin on {node} did not re-register")
+
     def _wait_capacity(self, node: str, timeout: float):
         t = time.monotonic() + timeout
         while time.monotonic() < t:

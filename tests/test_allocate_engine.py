@@ -197,11 +197,96 @@ def test_multi_container_pod_matched_per_container():
     assert [p[1] for p in cl.patches] == ["mc"]
 
 
-def test_pod_total_rule_still_wins():
-    al, _, cl = make([mkpod("mc", [1, 3], 0, 5)])
-    r = al.allocate(req(4))    # kubelet sending the whole pod in one request (reference behaviour)
-    assert dict(r.container_responses[0].envs)[const.ENV_RESOURCE_INDEX] == "0"
+def test_whole_pod_request_matches_only_its_own_shape():
+    """One AllocateRequest naming every gpu container (not what the kubelet sends, but valid
+    on the wire) matches the pod whose per-container shape it is, never one with an equal
+    total but a different shape."""
+    al, _, cl = make([mkpod("other", [4], 1, 1), mkpod("mc", [1, 3], 0, 5)])
+    r = al.allocate(req(1, 3))
+    assert [dict(c.envs)[const.ENV_RESOURCE_INDEX] for c in r.container_responses] == ["0", "0"]
     assert [p[1] for p in cl.patches] == ["mc"]
+
+
+def test_single_container_request_never_takes_multi_container_pod():
+    """Regression (round-1 review): pod M [8,8] on GPU 0 assumed first, pod X [16] on GPU 1.
+    The kubelet admits X first: X must get GPU 1, M keeps its reservation for its own two
+    Allocate(8) calls."""
+    m, x = mkpod("m", [8, 8], 0, 100), mkpod("x", [16], 1, 200)
+    al, src, cl = make([m, x], gib=32)
+    rx = dict(al.allocate(req(16)).container_responses[0].envs)
+    assert rx[const.ENV_RESOURCE_INDEX] == "1"
+    assert [p[1] for p in cl.patches] == ["x"]
+    x["status"]["phase"] = "Running"
+    for _ in range(2):
+        assert dict(al.allocate(req(8)).container_responses[0].envs)[const.ENV_RESOURCE_INDEX] == "0"
+    assert [p[1] for p in cl.patches] == ["x", "m"]
+
+
+def test_partial_claim_of_deleted_pod_is_dropped():
+    """Regression (round-1 advice): M [8,8] on GPU 0 gets its first container, then M is
+    deleted. A later single-container pod Y [8] on GPU 1 must get GPU 1, and M is never
+    patched."""
+    m, y = mkpod("m", [8, 8], 0, 100), mkpod("y", [8], 1, 200)
+    al, src, cl = make([m], gib=32)
+    assert dict(al.allocate(req(8)).container_responses[0].envs)[const.ENV_RESOURCE_INDEX] == "0"
+    src.pods.remove(m)
+    src.pods.append(y)
+    assert dict(al.allocate(req(8)).container_responses[0].envs)[const.ENV_RESOURCE_INDEX] == "1"
+    assert [p[1] for p in cl.patches] == ["y"]
+    assert al.metrics.allocate_outcomes.value(outcome="claim_abandoned") == 1
+
+
+def test_stale_or_deleting_partial_claim():
+    """A claim the kubelet does not continue within partial_claim_ttl_s may have fed a pod
+    that is now running: its reservation is withheld (never double-booked). A claim whose pod
+    is being deleted is simply dropped."""
+    m, y = mkpod("m", [8, 8], 0, 100), mkpod("y", [8], 1, 200)
+    al, src, cl = make([m, y], gib=32, partial_claim_ttl_s=0.05)
+    assert dict(al.allocate(req(8)).container_responses[0].envs)[const.ENV_RESOURCE_INDEX] == "0"
+    time.sleep(0.1)
+    assert dict(al.allocate(req(8)).container_responses[0].envs)[const.ENV_RESOURCE_INDEX] == "1"
+    assert [p[1] for p in cl.patches] == ["y"]
+    assert al.metrics.allocate_outcomes.value(outcome="claim_tainted") == 1
+    assert dict(al.allocate(req(8)).container_responses[0].envs)[const.ENV_RESOURCE_INDEX] == "-1"
+    # graceful deletion (deletionTimestamp) ends a claim without withholding anything
+    m2 = mkpod("m2", [4, 4], 0, 300)
+    src.pods.append(m2)
+    assert dict(al.allocate(req(4)).container_responses[0].envs)[const.ENV_RESOURCE_INDEX] == "0"
+    m2["metadata"]["deletionTimestamp"] = "2026-01-01T00:00:00Z"
+    assert dict(al.allocate(req(4)).container_responses[0].envs)[const.ENV_RESOURCE_INDEX] == "-1"
+    assert "m2" not in [p[1] for p in cl.patches]
+    assert al.metrics.allocate_outcomes.value(outcome="claim_abandoned") == 1
+
+
+def test_mismatched_continuation_is_retargeted_or_withheld():
+    """A claim is continued only by the next Allocate. When that container does not fit the
+    claimed pod, another pod with the same first container was being admitted: the claimed
+    reservation is withheld (it feeds that pod), and the claim moves to a pod that extends
+    the answered containers on the same GPU, or the container is matched afresh."""
+    m, p2 = mkpod("m", [2, 6], 0, 100), mkpod("p2", [2, 3], 0, 150)
+    z = mkpod("z", [3], 1, 200)
+    al, src, cl = make([m, p2, z], gib=16)
+    assert dict(al.allocate(req(2)).container_responses[0].envs)[const.ENV_RESOURCE_INDEX] == "0"   # claims m
+    assert dict(al.allocate(req(3)).container_responses[0].envs)[const.ENV_RESOURCE_INDEX] == "0"   # it was p2
+    assert [p[1] for p in cl.patches] == ["p2"]
+    assert al.metrics.allocate_outcomes.value(outcome="claim_retargeted") == 1
+    # m's reservation fed p2's first container: never handed out again while m lives
+    assert dict(al.allocate(req(2)).container_responses[0].envs)[const.ENV_RESOURCE_INDEX] == "-1"
+    assert dict(al.allocate(req(3)).container_responses[0].envs)[const.ENV_RESOURCE_INDEX] == "1"
+    assert [p[1] for p in cl.patches] == ["p2", "z"]
+
+
+def test_swapped_multi_container_pods_exchange_reservations():
+    """M2 [4,4] (GPU 1) is admitted before M1 [4,4] (GPU 0, assumed first): M2 takes M1's
+    reservation container by container; M1 then completes with M2's (swap completion)."""
+    now = time.time_ns()
+    m1, m2 = mkpod("m1", [4, 4], 0, now - 2000), mkpod("m2", [4, 4], 1, now - 1000)
+    al, src, cl = make([m1, m2], gib=16)
+    first = [dict(al.allocate(req(4)).container_responses[0].envs)[const.ENV_RESOURCE_INDEX] for _ in range(2)]
+    assert first == ["0", "0"] and [p[1] for p in cl.patches] == ["m1"]
+    m2["status"]["phase"] = "Running"
+    second = [dict(al.allocate(req(4)).container_responses[0].envs)[const.ENV_RESOURCE_INDEX] for _ in range(2)]
+    assert second == ["1", "1"] and [p[1] for p in cl.patches] == ["m1", "m2"]
 
 
 def test_concurrent_allocates_never_double_assign():

@@ -1,0 +1,132 @@
+"""Write-behind durability (round-1 review item 2): an Allocate answered before its
+``ASSIGNED=true`` PATCH landed must survive an apiserver outage, a plugin kill and a restart.
+
+Reference: ``allocate.go:132-152`` answers only after the PATCH landed; this build answers
+first and journals the pending PATCH (``alloc/journal.py``).
+"""
+import time
+
+from aliyun_gpushare_device_plugin_amd import const
+from aliyun_gpushare_device_plugin_amd.alloc.engine import Allocator, AllocatorOptions
+from aliyun_gpushare_device_plugin_amd.alloc.journal import AllocJournal
+from aliyun_gpushare_device_plugin_amd.cluster import objects as O
+from aliyun_gpushare_device_plugin_amd.device.model import DeviceModel
+from aliyun_gpushare_device_plugin_amd.sim.cluster import SimCluster
+
+from .test_allocate_engine import FakeClient, StaticSource, mkpod, req
+from .test_units_and_model import gpu
+
+
+def idx(adm, i=0):
+    return int(dict(adm.responses[i].envs)[const.ENV_RESOURCE_INDEX])
+
+
+def test_killed_plugin_lands_pending_patch_after_restart(tmp_path):
+    """Apiserver drops the plugin's pod PATCHes; the plugin answers pod A (write-behind) and is
+    SIGKILLed; a new plugin process starts while PATCHes still fail and admits an equal-size pod
+    B: B gets its own GPU (A is never matched twice); when the apiserver recovers both pods end
+    ASSIGNED=true."""
+    journal = str(tmp_path / "alloc-journal.jsonl")
+    with SimCluster([("n", "fake:2x4G")], plugin_mode="process",
+                    extra_plugin_args=["--journal-path", journal]) as c:
+        c.api.store.inject("assign_patch", 60)
+        a, where_a, adm_a = c.run_pod(3, name="a")
+        assert adm_a.error is None and idx(adm_a) == where_a[1]
+        time.sleep(0.3)                     # the patcher is retrying against the outage
+        assert O.annotations(c.client.get_pod("default", "a"))[const.ENV_ASSIGNED_FLAG] == "false"
+        assert any('"op":"patch"' in ln for ln in open(journal))
+        # the kubelet has not reported A Running yet: A still looks like an assumed Pending pod
+        c.client.patch_pod_status("default", "a", {"status": {"phase": "Pending"}})
+        c.kill_plugin("n")
+        c.restart_plugin("n")
+        # the extender puts B (same size) on the other GPU (A's has 1 GiB left); the kubelet admits it
+        b, where_b, adm_b = c.run_pod(3, name="b")
+        assert where_b[1] != where_a[1]
+        assert adm_b.error is None and idx(adm_b) == where_b[1]
+        assert O.annotations(c.client.get_pod("default", "a"))[const.ENV_ASSIGNED_FLAG] == "false"
+        assert c.api.store.requests["PATCH dropped"] >= 2
+        c.api.store.inject("assign_patch", 0)
+        for name in ("a", "b"):
+            got = c.wait_assigned({"metadata": {"namespace": "default", "name": name}}, timeout=15)
+            assert O.annotations(got)[const.ENV_ASSIGNED_FLAG] == "true", name
+        # journal: every pending patch has its landing
+        j = AllocJournal(journal)
+        assert j.unlanded() == []
+
+
+def _model(n=2, gib=4):
+    return DeviceModel([gpu(i, gib << 30) for i in range(n)], const.GIB)
+
+
+def test_recovered_patch_skips_recreated_pod(tmp_path):
+    """A journaled pending patch whose pod was deleted and re-created under the same name
+    (new UID) is dropped, never applied to the new pod."""
+    path = str(tmp_path / "j.jsonl")
+    old = mkpod("web", 2, 0, 10, uid="uid-old")
+    src = StaticSource([old])
+    cl = FakeClient(src)
+    cl.fail = RuntimeError("apiserver down")
+    al = Allocator(_model(), src, cl, "node-a", AllocatorOptions(async_patch=True, journal_path=path))
+    assert dict(al.allocate(req(2)).container_responses[0].envs)[const.ENV_RESOURCE_INDEX] == "0"
+    al.close()                                   # "killed": the patch never landed
+    new = mkpod("web", 2, 1, 20, uid="uid-new")
+    src.pods[:] = [new]
+    cl.fail = None
+    cl.get_pod = lambda ns, name: next(p for p in src.pods if p["metadata"]["name"] == name)
+    al2 = Allocator(_model(), src, cl, "node-a", AllocatorOptions(async_patch=True, journal_path=path))
+    assert al2.flush_patches(5.0)
+    assert not cl.patches                         # uid-old's patch never touched uid-new
+    assert AllocJournal(path).unlanded() == []
+    # the new pod is a normal candidate
+    assert dict(al2.allocate(req(2)).container_responses[0].envs)[const.ENV_RESOURCE_INDEX] == "1"
+    assert al2.flush_patches(5.0)
+    assert [p[1] for p in cl.patches] == ["web"]
+    al2.close()
+
+
+def test_reconcile_repatches_answered_pod(tmp_path):
+    """A pod this plugin answered that reads ASSIGNED=false (its patch was lost) is patched
+    again by the reconcile pass; pods never answered are left alone."""
+    path = str(tmp_path / "j.jsonl")
+    a, other = mkpod("a", 2, 0, 10), mkpod("other", 2, 1, 20, phase="Running")
+    src = StaticSource([a, other])
+    cl = FakeClient(src)
+    al = Allocator(_model(), src, cl, "node-a", AllocatorOptions(async_patch=True, journal_path=path,
+                                                                   reconcile_s=3600))
+    al.allocate(req(2))
+    assert al.flush_patches(5.0)
+    # an operator (or a stale writer) reverts the annotation
+    for p in src.pods:
+        if p["metadata"]["name"] == "a":
+            p["metadata"]["annotations"][const.ENV_ASSIGNED_FLAG] = "false"
+            p["status"]["phase"] = "Running"
+    cl.get_pod = lambda ns, name: next(p for p in src.pods if p["metadata"]["name"] == name)
+    assert al.reconcile() == 1
+    assert al.flush_patches(5.0)
+    assert [p[1] for p in cl.patches] == ["a", "a"]
+    assert al.metrics.allocate_outcomes.value(outcome="patch_reconciled") == 1
+    al.close()
+
+
+def test_rebuild_keeps_inflight_claims(tmp_path):
+    """A kubelet restart / SIGHUP rebuilds the plugin: the Allocator (claims, assigned pods,
+    queued patches) is carried over, so a pod whose patch is still in flight is not matched
+    again by the rebuilt plugin."""
+    with SimCluster([("n", "fake:2x4G")]) as c:
+        m = c.manager("n")
+        c.api.store.inject("assign_patch", 60)
+        _, where_a, adm_a = c.run_pod(3, name="a")
+        c.client.patch_pod_status("default", "a", {"status": {"phase": "Pending"}})
+        before = m.allocator
+        m.events.put(("signal", __import__("signal").SIGHUP))
+        t = time.monotonic() + 10
+        while m.restarts == 0 and time.monotonic() < t:
+            time.sleep(0.01)
+        c.nodes["n"].kubelet.registered.wait(10)
+        assert m.allocator is before
+        _, where_b, adm_b = c.run_pod(3, name="b")
+        assert idx(adm_b) == where_b[1] != idx(adm_a)
+        c.api.store.inject("assign_patch", 0)
+        for name in ("a", "b"):
+            got = c.wait_assigned({"metadata": {"namespace": "default", "name": name}}, timeout=10)
+            assert O.annotations(got)[const.ENV_ASSIGNED_FLAG] == "true"

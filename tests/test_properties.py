@@ -132,3 +132,91 @@ def test_quota_bounded_and_monotone(dev_units, dev_bytes, c1, c2):
 def test_parse_quantity_scales(v, suffix):
     mult = {"": 1, "k": 10 ** 3, "M": 10 ** 6, "Ki": 1 << 10, "Mi": 1 << 20, "Gi": 1 << 30}[suffix]
     assert U.parse_quantity(f"{v}{suffix}") == v * mult
+
+
+def _admit_all(pods, order, ngpu, cap, strict=True):
+    """Drive the engine like the kubelet: pods one at a time in ``order``, one Allocate per gpu
+    container, back to back; a refused container fails the pod's admission (strict mode = the
+    kubelet's UnexpectedAdmissionError) and it turns Failed, an admitted pod turns Running."""
+    import time as _t
+
+    from aliyun_gpushare_device_plugin_amd.alloc.engine import AllocationError
+
+    model = DeviceModel([gpu(i, cap << 30) for i in range(ngpu)], const.GIB)
+    src = StaticSource(pods)
+    cl = FakeClient(src)
+    al = Allocator(model, src, cl, "node-a", AllocatorOptions(strict=strict))
+    ids = itertools.count()
+    granted = {}                                   # pod name -> [gpu idx per container]
+    for i in order:
+        p = pods[i]
+        shape = [int(c["resources"]["limits"][const.RESOURCE_NAME]) for c in p["spec"]["containers"]]
+        got = []
+        for size in shape:
+            req = api.AllocateRequest()
+            req.container_requests.add().devices_ids.extend([f"id-{next(ids)}" for _ in range(size)])
+            try:
+                envs = dict(al.allocate(req).container_responses[0].envs)
+            except AllocationError:
+                got = None
+                break
+            got.append(int(envs[const.ENV_RESOURCE_INDEX]))
+        p["status"]["phase"] = "Running" if got is not None else "Failed"
+        granted[p["metadata"]["name"]] = got
+        _t.sleep(0)
+    return granted, cl
+
+
+@settings(max_examples=500, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(ngpu=st.integers(1, 4), data=st.data())
+def test_admission_orders_keep_reservations_exact(ngpu, data):
+    """Round-1 review item: random mixes of single- and multi-container pods, extender-reserved
+    on N GPUs, admitted in an arbitrary kubelet order. Invariants:
+    * the GPU a container is granted is never over-committed: Σ granted per GPU over admitted
+      pods ≤ Σ reserved there ≤ capacity (every grant consumes an equal-size container of some
+      reservation, so accounting by pod annotations stays exact);
+    * a pod's containers are granted or refused cleanly (strict mode), never a bogus index;
+    * no pod is PATCHed ASSIGNED twice;
+    * all pods single-container: every pod is admitted, and the granted (size, GPU) multiset
+      equals the reserved one (equal-size pods may swap reservations, nothing else);
+    * admission in assume-time order: every container gets its own pod's reserved GPU."""
+    import time as _t
+
+    cap = 12
+    shapes = data.draw(st.lists(st.lists(st.integers(1, 5), min_size=1, max_size=3), min_size=1, max_size=10))
+    single = data.draw(st.booleans())
+    if single:
+        shapes = [s[:1] for s in shapes]
+    free = [cap] * ngpu
+    pods, reserved = [], []
+    now = _t.time_ns()
+    for i, shape in enumerate(shapes):
+        g = next((j for j in range(ngpu) if free[j] >= sum(shape)), None)   # extender first-fit
+        if g is None:
+            continue
+        free[g] -= sum(shape)
+        pods.append(mkpod(f"p{i}", shape, g, now - 10_000 + i))
+        reserved.append((tuple(shape), g))
+    in_order = data.draw(st.booleans())
+    order = list(range(len(pods))) if in_order else data.draw(st.permutations(range(len(pods))))
+    granted, cl = _admit_all(pods, order, ngpu, cap)
+
+    names = [p[1] for p in cl.patches]
+    assert len(names) == len(set(names))
+    used = [0] * ngpu
+    for p, (shape, g) in zip(pods, reserved):
+        got = granted[p["metadata"]["name"]]
+        if got is None:
+            continue
+        assert all(0 <= x < ngpu for x in got)
+        for size, x in zip(shape, got):
+            used[x] += size
+    reserved_per_gpu = [sum(sum(s) for s, g in reserved if g == j) for j in range(ngpu)]
+    assert all(u <= r <= cap for u, r in zip(used, reserved_per_gpu))
+    if single:
+        assert all(granted[p["metadata"]["name"]] is not None for p in pods)
+        got = sorted((s, granted[p["metadata"]["name"]][0]) for p, (s, _) in zip(pods, reserved))
+        assert got == sorted(reserved)
+    if in_order:
+        for p, (shape, g) in zip(pods, reserved):
+            assert granted[p["metadata"]["name"]] == [g] * len(shape)
