@@ -4,8 +4,11 @@ Reference ``cmd/inspect/{main,podinfo,nodeinfo,display}.go``: per-node, per-GPU 
 rebuilt from pod specs and annotations only (the plugin is never queried); per-GPU total is
 ``allocatable[gpu-mem] / allocatable[gpu-count]``; pods carry either the newer
 ``scheduler.framework.gpushare.allocation`` JSON or the legacy ``ALIYUN_COM_GPU_MEM_IDX``;
-pods without an index land in a PENDING column (device -1); the unit is guessed from the
-per-GPU memory (> 100 → MiB). Summary (default) and ``-d`` detail tables keep the reference
+pods without an index land in a PENDING column (device -1). The unit comes from the
+``gpushare.amd.com/memory-unit`` node annotation the plugin writes; only nodes without it fall
+back to a guess from the per-GPU units. The reference's guess (> 100 → MiB,
+``nodeinfo.go:228-244``) calls a 288 GiB MI355X "MiB", so the fallback threshold is 1024:
+every GPU between 1 GiB and 1 TiB is ≥ 1024 in MiB and < 1024 in GiB. Summary (default) and ``-d`` detail tables keep the reference
 layout byte for byte (Go tabwriter emulation). ``--topology`` adds the MI355X xGMI matrix and
 per-GPU health exported by the plugin (no reference counterpart).
 
@@ -93,11 +96,19 @@ def build_node_infos(pods: list[dict], nodes: list[dict]) -> list[NodeInfo]:
     return infos
 
 
+MIB_GUESS_THRESHOLD = 1024
+
+
 def guess_unit(infos: list[NodeInfo]) -> str:
-    """``setUnit`` (``nodeinfo.go:228-244``): the first node with GPUs decides."""
+    """``setUnit`` (``nodeinfo.go:228-244``): the first node with GPUs decides — by the unit
+    its plugin exported, else by the size heuristic (see the module docstring)."""
+    for i in infos:
+        u = O.annotations(i.node).get(const.NODE_ANNOTATION_MEMORY_UNIT)
+        if i.gpu_total > 0 and u in (const.GIB, const.MIB):
+            return u
     for i in infos:
         if i.gpu_total > 0 and i.gpu_count > 0:
-            return const.MIB if i.gpu_total // i.gpu_count > 100 else const.GIB
+            return const.MIB if i.gpu_total // i.gpu_count >= MIB_GUESS_THRESHOLD else const.GIB
     return ""
 
 

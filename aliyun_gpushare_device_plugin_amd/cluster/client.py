@@ -17,6 +17,7 @@ import socket
 import ssl
 import tempfile
 import threading
+import time
 import urllib.parse
 
 import yaml
@@ -47,22 +48,67 @@ class APIError(Exception):
 
 
 class KubeConfig:
+    """Connection settings. A bearer token read from a file (the projected service-account
+    token in a pod, or a kubeconfig ``tokenFile``) is re-read every ``TOKEN_RELOAD_S`` and on a
+    401, as client-go's in-cluster config does (``rest.InClusterConfig`` behind
+    ``podmanager.go:37-48``): bound service-account tokens rotate (≈1 h) and a plugin that
+    cached the first one would lose the apiserver after it expires."""
+
+    TOKEN_RELOAD_S = 60.0
+
     def __init__(self, server: str, token: str | None = None, ca_file: str | None = None,
-                 cert_file: str | None = None, key_file: str | None = None, insecure: bool = False):
+                 cert_file: str | None = None, key_file: str | None = None, insecure: bool = False,
+                 token_file: str | None = None):
         self.server = server.rstrip("/")
-        self.token, self.ca_file, self.cert_file, self.key_file = token, ca_file, cert_file, key_file
+        self.ca_file, self.cert_file, self.key_file = ca_file, cert_file, key_file
         self.insecure = insecure
+        self.token_file = token_file
+        self._token = token
+        self._token_read = 0.0
+        self._token_lock = threading.Lock()
+        self.token_reloads = 0
+        if token_file and token is None:
+            self.reload_token(force=True)
+
+    @property
+    def token(self) -> str | None:
+        if self.token_file and time.monotonic() - self._token_read >= self.TOKEN_RELOAD_S:
+            self.reload_token()
+        return self._token
+
+    @token.setter
+    def token(self, v: str | None):
+        self._token = v
+
+    def reload_token(self, force: bool = False) -> bool:
+        """Re-read ``token_file``; True when the token changed."""
+        if not self.token_file:
+            return False
+        with self._token_lock:
+            if not force and time.monotonic() - self._token_read < self.TOKEN_RELOAD_S:
+                return False
+            try:
+                with open(self.token_file) as f:
+                    new = f.read().strip()
+            except OSError as e:
+                log.warning("cannot read token file %s: %s", self.token_file, e)
+                self._token_read = time.monotonic()
+                return False
+            self._token_read = time.monotonic()
+            changed = new != self._token
+            if changed:
+                self._token = new
+                self.token_reloads += 1
+            return changed
 
     @classmethod
     def in_cluster(cls) -> "KubeConfig":
         host, port = os.environ.get("KUBERNETES_SERVICE_HOST"), os.environ.get("KUBERNETES_SERVICE_PORT", "443")
         if not host:
             raise RuntimeError("not running in a cluster: KUBERNETES_SERVICE_HOST unset")
-        with open(const.SA_TOKEN_FILE) as f:
-            token = f.read().strip()
         if ":" in host:
             host = f"[{host}]"
-        return cls(f"https://{host}:{port}", token=token, ca_file=const.SA_CA_FILE)
+        return cls(f"https://{host}:{port}", ca_file=const.SA_CA_FILE, token_file=const.SA_TOKEN_FILE)
 
     @classmethod
     def from_file(cls, path: str) -> "KubeConfig":
@@ -87,10 +133,8 @@ class KubeConfig:
             return None
 
         token = us.get("token")
-        if not token and us.get("tokenFile"):
-            with open(us["tokenFile"]) as f:
-                token = f.read().strip()
-        return cls(cl.get("server", "http://127.0.0.1:8080"), token=token,
+        token_file = us.get("tokenFile") if not token else None
+        return cls(cl.get("server", "http://127.0.0.1:8080"), token=token, token_file=token_file,
                    ca_file=materialize("certificate-authority-data", "certificate-authority", cl),
                    cert_file=materialize("client-certificate-data", "client-certificate", us),
                    key_file=materialize("client-key-data", "client-key", us),
@@ -163,21 +207,11 @@ class APIClient:
         if query:
             url += "?" + urllib.parse.urlencode({k: v for k, v in query.items() if v is not None})
         data = None if body is None else (body if isinstance(body, bytes) else json.dumps(body).encode())
-        for attempt in (0, 1):
-            c = self._conn()
-            try:
-                c.request(method, url, body=data, headers=self._headers(content_type if data is not None else None))
-                r = c.getresponse()
-                raw = r.read()
-                break
-            except (http.client.HTTPException, OSError):
-                # stale keep-alive connection: reconnect once
-                try:
-                    c.close()
-                finally:
-                    self._local.conn = None
-                if attempt:
-                    raise
+        r, raw = self._roundtrip(method, url, data, content_type)
+        if r.status == 401 and self.cfg.reload_token(force=True):
+            # rotated service-account token: retry once with the new one
+            log.info("apiserver answered 401; retrying with the reloaded token")
+            r, raw = self._roundtrip(method, url, data, content_type)
         self.requests += 1
         try:
             obj = json.loads(raw) if raw else {}
@@ -187,6 +221,23 @@ class APIClient:
             raise APIError(r.status, obj.get("reason", r.reason) if isinstance(obj, dict) else r.reason,
                            obj.get("message", "") if isinstance(obj, dict) else str(obj), obj)
         return obj
+
+    def _roundtrip(self, method, url, data, content_type):
+        for attempt in (0, 1):
+            c = self._conn()
+            try:
+                c.request(method, url, body=data, headers=self._headers(content_type if data is not None else None))
+                r = c.getresponse()
+                return r, r.read()
+            except (http.client.HTTPException, OSError):
+                # stale keep-alive connection: reconnect once
+                try:
+                    c.close()
+                finally:
+                    self._local.conn = None
+                if attempt:
+                    raise
+        raise AssertionError("unreachable")
 
     # -- nodes --------------------------------------------------------------------------
     def get_node(self, name: str) -> dict:
@@ -256,6 +307,8 @@ class APIClient:
                     obj = json.loads(raw)
                 except ValueError:
                     obj = {}
+                if r.status == 401:
+                    self.cfg.reload_token(force=True)     # the informer's next attempt uses it
                 raise APIError(r.status, obj.get("reason", r.reason), obj.get("message", ""), obj)
             c.sock.settimeout(None)
             buf = b""

@@ -46,6 +46,13 @@ def export_annotation(client: APIClient, node_name: str, key: str, value: dict) 
                                                                                separators=(",", ":"))}}})
 
 
+def export_memory_unit(client: APIClient, node_name: str, unit: str) -> None:
+    """Record the unit of ``aliyun.com/gpu-mem`` on the node (read by kubectl-inspect-gpushare)."""
+    node = client.get_node(node_name)
+    if O.annotations(node).get(const.NODE_ANNOTATION_MEMORY_UNIT) != unit:
+        client.patch_node(node_name, {"metadata": {"annotations": {const.NODE_ANNOTATION_MEMORY_UNIT: unit}}})
+
+
 def export_topology(client: APIClient, node_name: str, topology: dict) -> None:
     export_annotation(client, node_name, const.NODE_ANNOTATION_TOPOLOGY, topology)
 

@@ -75,6 +75,9 @@ POD_ANNOTATION_CU_SLOTS_REQUEST = "gpushare.amd.com/cu-slots-request"  # optiona
 # Node annotation carrying the exported xGMI topology (JSON, see parallel/topology.py).
 NODE_ANNOTATION_TOPOLOGY = "gpushare.amd.com/xgmi-topology"
 NODE_ANNOTATION_HEALTH = "gpushare.amd.com/gpu-health"
+# Node annotation carrying the unit of aliyun.com/gpu-mem on this node ("GiB" / "MiB"), so
+# kubectl-inspect-gpushare labels it without guessing (the reference guesses, nodeinfo.go:228-244).
+NODE_ANNOTATION_MEMORY_UNIT = "gpushare.amd.com/memory-unit"
 
 # Environment used by the plugin itself (podmanager.go:33-58)
 ENV_NODE_NAME = "NODE_NAME"

@@ -43,6 +43,7 @@ class HealthMonitor:
         self._threads: list[threading.Thread] = []
         self._ecc_baseline = {}
         self.events_seen: list[S.Event] = []
+        self.status: dict = {}
         self.ignored = 0
         self._lock = threading.Lock()
         for g in smi.devices():
@@ -50,6 +51,19 @@ class HealthMonitor:
 
     def start(self):
         self.smi.events_start()
+        try:
+            self.status = self.smi.health_status()
+        except Exception as e:  # noqa: BLE001 - an older library without the call
+            self.status = {}
+            log.warning("health status unavailable: %s", e)
+        st = self.status
+        if st and st.get("events_armed", 0) < self.smi.count():
+            log.warning("SMI event notification armed on %d/%d GPUs (status %d): resets/VM faults on the others "
+                        "are seen by polling only", st.get("events_armed", 0), self.smi.count(),
+                        st.get("events_last_status", 0))
+        if st and st.get("ecc_reads_failed", 0):
+            log.warning("ECC counters unreadable on %d GPU(s) (status %d): uncorrectable-error health is blind there",
+                        st["ecc_reads_failed"], st.get("ecc_last_status", 0))
         for target, name in ((self._event_loop, "health-events"), (self._poll_loop, "health-poll")):
             t = threading.Thread(target=target, name=name, daemon=True)
             t.start()

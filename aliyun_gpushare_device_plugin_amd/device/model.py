@@ -91,8 +91,20 @@ def partition_layout(gpus: list[GPU], partition_aware: bool = True) -> tuple[dic
     return sockets, parts, vram
 
 
+class DeviceConfigError(ValueError):
+    """The node cannot be advertised under this configuration; the supervisor parks instead of
+    exiting (an exit would only crash-loop the DaemonSet pod)."""
+
+
 class DeviceModel:
-    """Thread-safe device table; ``generation`` bumps on every health change."""
+    """Thread-safe device table; ``generation`` bumps on every health change.
+
+    ``--memory-unit=MiB`` on an MI355X would mean 294,912 fake devices per GPU (2.36 M per
+    node, a >100 MB ListAndWatch message the kubelet rejects). When the MiB count
+    exceeds ``MAX_FAKE_DEVICES_PER_NODE`` the model falls back to GiB with a warning
+    (``unit_fallback`` records why; the plugin exports the unit it actually advertises as a
+    node annotation and a metric), the same way the reference falls back to GiB for a unit it
+    cannot use (``cmd/nvidia/main.go:67-78``)."""
 
     def __init__(self, gpus: list[GPU], unit: str = const.GIB, round_policy: str = "nearest",
                  homogeneous: bool = True, gpu_indices: list[int] | None = None, partition_aware: bool = True):
@@ -101,9 +113,17 @@ class DeviceModel:
         self._lock = threading.Lock()
         self._cond = threading.Condition(self._lock)
         self.generation = 0
+        self.unit_fallback = ""
         sel = [g for g in gpus if gpu_indices is None or g.index in set(gpu_indices)]
         sockets, part_idx, vram = partition_layout(gpus, partition_aware)
         per = [U.units_for_bytes(vram[g.index], unit, round_policy) for g in sel]
+        if sum(per) > U.MAX_FAKE_DEVICES_PER_NODE and unit == const.MIB:
+            self.unit_fallback = (f"{sum(per)} MiB devices exceed the ListAndWatch limit "
+                                  f"({U.MAX_FAKE_DEVICES_PER_NODE}); advertising GiB")
+            log.warning("--memory-unit=MiB: %s. Pods must request aliyun.com/gpu-mem in GiB on this node.",
+                        self.unit_fallback)
+            unit = self.unit = const.GIB
+            per = [U.units_for_bytes(vram[g.index], unit, round_policy) for g in sel]
         if homogeneous and per and len(set(per)) > 1:
             log.warning("heterogeneous GPU memory %s %s; advertising the minimum (%d) per GPU",
                         per, unit, min(per))
@@ -117,7 +137,7 @@ class DeviceModel:
                                          num_cu=g.num_cu))
         total = sum(g.units for g in self.gpus)
         if total > U.MAX_FAKE_DEVICES_PER_NODE:
-            raise ValueError(f"{total} fake devices exceed the ListAndWatch limit "
+            raise DeviceConfigError(f"{total} fake devices exceed the ListAndWatch limit "
                              f"({U.MAX_FAKE_DEVICES_PER_NODE}); use --memory-unit=GiB on this node")
         self._by_uuid = {g.uuid: g for g in self.gpus}
         self._devs_cache = None

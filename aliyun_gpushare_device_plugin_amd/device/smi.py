@@ -40,6 +40,11 @@ class _Link(ctypes.Structure):
                 ("reserved", ctypes.c_int32), ("max_bandwidth_mbps", ctypes.c_uint64)]
 
 
+class _HealthStatus(ctypes.Structure):
+    _fields_ = [(f, ctypes.c_int32) for f in ("events_api", "events_armed", "events_last_status", "ecc_api",
+                                               "ecc_reads_ok", "ecc_reads_failed", "ecc_last_status", "refreshes")]
+
+
 class _Event(ctypes.Structure):
     _fields_ = [("index", ctypes.c_int32), ("kind", ctypes.c_int32), ("message", ctypes.c_char * 96)]
 
@@ -115,8 +120,9 @@ def _load():
             lib.gs_get_link.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_Link)]
             lib.gs_wait_event.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(_Event)]
             lib.gs_inject.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
+            lib.gs_health_status.argtypes = [ctypes.c_void_p, ctypes.POINTER(_HealthStatus)]
             lib.gs_to_json.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t]
-            if lib.gs_abi_version() != 1:
+            if lib.gs_abi_version() != 2:
                 raise RuntimeError("libgpushare_gpuinfo ABI mismatch")
             _lib = lib
     return _lib
@@ -238,6 +244,14 @@ class SMI:
 
     def events_start(self):
         self._call(self._lib.gs_events_start)
+
+    def health_status(self) -> dict:
+        """What the health path has on this backend: event notification armed on how many
+        devices, ECC counters read at the last refresh (``gs_health_status``)."""
+        st = _HealthStatus()
+        if self._call(self._lib.gs_health_status, ctypes.byref(st)) < 0:
+            self._err("gs_health_status")
+        return {f: int(getattr(st, f)) for f, _ in _HealthStatus._fields_}
 
     def wait_event(self, timeout_ms: int) -> Event | None:
         ev = _Event()

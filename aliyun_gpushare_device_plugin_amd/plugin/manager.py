@@ -26,7 +26,7 @@ from ..cluster.kubelet import KubeletClient
 from ..cluster.podcache import KubeletSource, ListSource, WatchCache
 from ..device import smi as S
 from ..device.health import HealthMonitor
-from ..device.model import DeviceModel
+from ..device.model import DeviceConfigError, DeviceModel
 from ..parallel import topology as T
 from ..quota import ShimConfig
 from ..utils import log, metrics as M, stackdump
@@ -128,12 +128,14 @@ class SharedGPUManager:
         self.smi.refresh()
         model = DeviceModel(self.smi.devices(), cfg.memory_unit, cfg.round_policy, cfg.homogeneous,
                             cfg.gpu_indices, partition_aware=cfg.partition_aware)
+        self.metrics.unit_fallback.set(1 if model.unit_fallback else 0)
         for g in model.gpus:
             self.metrics.units_per_gpu.set(g.units, gpu=str(g.index))
             self.metrics.device_health.set(1 if g.healthy else 0, gpu=str(g.index))
         disable_cgpu = False
         if self.client is not None:
             nodestatus.patch_gpu_count(self.client, cfg.node_name, model.count())
+            nodestatus.export_memory_unit(self.client, cfg.node_name, model.unit)
             disable_cgpu = nodestatus.cgpu_isolation_disabled(self.client, cfg.node_name)
         if self.pod_source is not None:
             self.pod_source.stop()
@@ -181,6 +183,9 @@ class SharedGPUManager:
 
             self.health = HealthMonitor(self.smi, self.model, self.cfg.health_poll_s, on_change=changed,
                                         on_topology_change=lambda ev: self._export_topology()).start()
+            st = self.health.status
+            self.metrics.health_events_armed.set(st.get("events_armed", 0))
+            self.metrics.health_ecc_readable.set(st.get("ecc_reads_ok", 0))
 
     def _start_ledger_collector(self):
         """Export the quota shim's per-container ledgers (--ledger-dir) every ledger_scan_s and
@@ -255,6 +260,13 @@ class SharedGPUManager:
                         self.restarts += 1
                     try:
                         self.plugin = self.build_plugin()
+                    except DeviceConfigError as e:
+                        # a configuration the node can never satisfy: exiting would only
+                        # crash-loop the DaemonSet pod
+                        log.error("cannot advertise this node: %s", e)
+                        self.metrics.config_error.set(1)
+                        self.plugin = None
+                        return self._park()
                     except Exception as e:  # noqa: BLE001
                         log.warning("Failed to get device plugin due to %s", e)
                         return 1

@@ -130,6 +130,8 @@ class Store:
         # metadata PATCH of a pod (not the kubelet's /status), "assign_patch" only the plugin's
         # ASSIGNED=true patch
         self.faults: dict[str, tuple[float, int]] = {}
+        # bearer-token authentication: None = anonymous allowed; a set = only these tokens
+        self.valid_tokens: set | None = None
 
     def inject(self, kind: str, seconds: float, code: int = 503):
         with self.lock:
@@ -443,12 +445,21 @@ class FakeAPIServer:
                 except ValueError:
                     return
                 n = 0
+                token = None
                 for ln in lines[1:]:
-                    if ln[:15].lower() == b"content-length:":
+                    low = ln[:22].lower()
+                    if low[:15] == b"content-length:":
                         n = int(ln[15:].strip() or 0)
+                    elif low[:21] == b"authorization: bearer":
+                        token = ln[21:].strip().decode("latin-1")
                 body = await reader.readexactly(n) if n else b""
                 if self.latency_s > 0:
                     await asyncio.sleep(self.latency_s)
+                valid = self.store.valid_tokens
+                if valid is not None and token not in valid:
+                    self.store.requests["401"] += 1
+                    writer.write(_response(*_status(401, "Unauthorized", "Unauthorized")))
+                    continue
                 try:
                     res = route(self.store, method, target, body)
                 except Exception as e:  # noqa: BLE001 - a malformed request must not kill the fake

@@ -75,7 +75,7 @@ class FakeKubelet:
                 pass
 
             def do_GET(self):
-                if self.headers.get("Authorization") != f"Bearer {token}":
+                if self.headers.get("Authorization") != f"Bearer {kl.pods_token}":   # rotatable
                     code, body = 401, b'{"message":"Unauthorized"}'
                 elif self.path.rstrip("/") != "/pods":
                     code, body = 404, b"{}"

@@ -179,6 +179,12 @@ class PluginMetrics:
         self.pending_match_failures = r.counter("gpushare_pending_match_failures_total",
                                                 "Allocates with no matching assumed pod")
         self.units_per_gpu = r.gauge("gpushare_advertised_units", "Advertised gpu-mem units per GPU")
+        self.unit_fallback = r.gauge("gpushare_memory_unit_fallback",
+                                     "1 if --memory-unit=MiB was replaced by GiB (fake-device limit)")
+        self.health_events_armed = r.gauge("gpushare_health_events_armed",
+                                           "GPUs with SMI event notification (reset / VM fault) armed")
+        self.health_ecc_readable = r.gauge("gpushare_health_ecc_readable", "GPUs whose ECC counters were read")
+        self.config_error = r.gauge("gpushare_config_error", "1 if the plugin parked on an impossible config")
         self.device_health = r.gauge("gpushare_device_healthy", "1 if the GPU is healthy")
         self.hbm_used = r.gauge("gpushare_hbm_used_bytes", "HBM in use per GPU (SMI)")
         self.cache_events = r.counter("gpushare_pod_cache_events_total", "Pod watch-cache events")

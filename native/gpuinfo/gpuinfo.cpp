@@ -191,6 +191,41 @@ class Backend {
     set_err(std::string("fault injection unsupported on backend ") + name() + ": " + cmd);
     return -1;
   }
+  gs_health_status_t status() const {
+    std::lock_guard<std::mutex> lk(st_mu_);
+    return st_;
+  }
+
+ protected:
+  // ECC bookkeeping of one enumeration pass: begin, one note per device, end.
+  void ecc_begin() { ecc_ok_ = ecc_fail_ = 0; }
+  void ecc_note(int rc) {
+    if (rc == 0) {
+      ++ecc_ok_;
+    } else {
+      ++ecc_fail_;
+      ecc_rc_ = rc;
+    }
+  }
+  void ecc_end(bool api) {
+    std::lock_guard<std::mutex> lk(st_mu_);
+    st_.ecc_api = api ? 1 : 0;
+    st_.ecc_reads_ok = ecc_ok_;
+    st_.ecc_reads_failed = ecc_fail_;
+    st_.ecc_last_status = ecc_rc_;
+    ++st_.refreshes;
+  }
+  void events_note(bool api, int armed, int last_rc) {
+    std::lock_guard<std::mutex> lk(st_mu_);
+    st_.events_api = api ? 1 : 0;
+    st_.events_armed = armed;
+    st_.events_last_status = last_rc;
+  }
+
+ private:
+  mutable std::mutex st_mu_;
+  gs_health_status_t st_{};
+  int ecc_ok_ = 0, ecc_fail_ = 0, ecc_rc_ = 0;
 };
 
 // ---- sysfs -------------------------------------------------------------------------------
@@ -200,8 +235,9 @@ class SysfsBackend : public Backend {
   const char* name() const override { return "sysfs"; }
 
   // Enriches a device whose render minor is known from amdgpu's DRM sysfs.
-  void enrich_from_drm(gs_device_t* d) const {
-    if (d->render_minor < 0) return;
+  // Returns true when the RAS (ECC) counters were read.
+  bool enrich_from_drm(gs_device_t* d) const {
+    if (d->render_minor < 0) return false;
     std::string dev = root_ + "/sys/class/drm/renderD" + std::to_string(d->render_minor) + "/device/";
     std::string v = read_trim(dev + "mem_info_vram_total");
     if (!v.empty()) d->vram_total = to_u64(v);
@@ -224,7 +260,9 @@ class SysfsBackend : public Backend {
       }());
       d->ecc_ue = to_u64(m["ue"]);
       d->ecc_ce = to_u64(m["ce"]);
+      return true;
     }
+    return false;
   }
 
   bool enumerate(std::vector<gs_device_t>* devs, LinkMatrix* links, int* inaccessible) override {
@@ -236,6 +274,7 @@ class SysfsBackend : public Backend {
     }
     devs->clear();
     *inaccessible = 0;
+    ecc_begin();
     std::map<int, int> node_to_idx;
     std::vector<int> gpu_nodes;
     for (int n : nodes) {
@@ -276,7 +315,7 @@ class SysfsBackend : public Backend {
         }
       }
       d.vram_total = banks;
-      enrich_from_drm(&d);
+      ecc_note(enrich_from_drm(&d) ? 0 : -1);
       if (d.name[0] == 0) copy_str(d.name, "AMD Instinct GPU");
       node_to_idx[n] = d.index;
       gpu_nodes.push_back(n);
@@ -307,6 +346,7 @@ class SysfsBackend : public Backend {
     for (int i = 0; i < links->n; ++i)
       for (int j = 0; j < links->n; ++j)
         if (i != j && links->at(i, j).type == GS_LINK_NONE) links->at(i, j) = gs_link_t{GS_LINK_PCIE, 3, 40, 0, 0};
+    ecc_end(true);
     return true;
   }
 
@@ -388,6 +428,7 @@ class RocmSmiBackend : public Backend {
     n_ = n;
     devs->clear();
     *inaccessible = 0;
+    ecc_begin();
     SysfsBackend sysfs("");
     // sysfs view for render minors / partitions / names keyed by unique id.
     std::vector<gs_device_t> sdevs;
@@ -429,7 +470,10 @@ class RocmSmiBackend : public Backend {
       uint64_t hive = 0;
       if (hive_ && hive_(i, &hive) == 0) d.hive_id = hive;
       rsmi_err_count ec{};
-      if (ecc_ && ecc_(i, 0 /*RSMI_GPU_BLOCK_UMC*/, &ec) == 0) {
+      // RSMI_GPU_BLOCK_UMC = 0x1 (rocm_smi.h rsmi_gpu_block_t): the HBM memory controllers
+      int erc = ecc_ ? ecc_(i, 0x1, &ec) : -1;
+      if (ecc_) ecc_note(erc);
+      if (erc == 0) {
         d.ecc_ue = ec.uncorrectable;
         d.ecc_ce = ec.correctable;
       }
@@ -450,6 +494,7 @@ class RocmSmiBackend : public Backend {
         if (bw_ && bw_(i, j, &bmin, &bmax) == 0) L.max_bandwidth_mbps = bmax;
         links->at((int)i, (int)j) = L;
       }
+    ecc_end(ecc_ != nullptr);
     return true;
   }
 
@@ -457,11 +502,14 @@ class RocmSmiBackend : public Backend {
     if (!ev_init_ || !ev_mask_ || !ev_get_) return true;  // polling only
     // VMFAULT(1) THERMAL_THROTTLE(2) GPU_PRE_RESET(3) GPU_POST_RESET(4), rocm_smi.h:319-323
     uint64_t mask = (1ull << 0) | (1ull << 1) | (1ull << 2) | (1ull << 3);
-    bool any = false;
+    int armed = 0, last = 0;
     for (auto& d : devs) {
-      if (ev_init_((uint32_t)d.index) == 0 && ev_mask_((uint32_t)d.index, mask) == 0) any = true;
+      int rc = ev_init_((uint32_t)d.index);
+      if (rc == 0) rc = ev_mask_((uint32_t)d.index, mask);
+      if (rc == 0) ++armed; else last = rc;
     }
-    events_on_ = any;
+    events_on_ = armed > 0;
+    events_note(true, armed, last);
     return true;
   }
 
@@ -585,6 +633,7 @@ class AmdSmiBackend : public Backend {
 
   bool enumerate(std::vector<gs_device_t>* devs, LinkMatrix* links, int* inaccessible) override {
     // processors of every socket, GPUs only
+    ecc_begin();
     uint32_t ns = 0;
     if (sockets_(&ns, nullptr) != 0) {
       set_err("amdsmi_get_socket_handles failed");
@@ -651,7 +700,9 @@ class AmdSmiBackend : public Backend {
       amdsmi_xgmi_info xi{};
       if (xgmi_ && xgmi_(h, &xi) == 0) d.hive_id = xi.xgmi_hive_id;
       amdsmi_error_count ec{};
-      if (ecc_ && ecc_(h, &ec) == 0) {
+      int erc = ecc_ ? ecc_(h, &ec) : -1;
+      if (ecc_) ecc_note(erc);
+      if (erc == 0) {
         d.ecc_ue = ec.uncorrectable_count;
         d.ecc_ce = ec.correctable_count;
       }
@@ -664,6 +715,7 @@ class AmdSmiBackend : public Backend {
       es.push_back({d, h, order});
     }
     std::stable_sort(es.begin(), es.end(), [](const Entry& a, const Entry& b) { return a.order < b.order; });
+    ecc_end(ecc_ != nullptr);
     devs->clear();
     handles_.clear();
     for (size_t i = 0; i < es.size(); ++i) {
@@ -694,10 +746,14 @@ class AmdSmiBackend : public Backend {
   bool events_start(const std::vector<gs_device_t>&) override {
     if (!ev_init_ || !ev_mask_ || !ev_get_) return true;  // polling only
     uint64_t mask = (1ull << 0) | (1ull << 1) | (1ull << 2) | (1ull << 3);  // events 1..4, bit = event - 1
-    bool any = false;
-    for (void* h : handles_)
-      if (ev_init_(h) == 0 && ev_mask_(h, mask) == 0) any = true;
-    events_on_ = any;
+    int armed = 0, last = 0;
+    for (void* h : handles_) {
+      int rc = ev_init_(h);
+      if (rc == 0) rc = ev_mask_(h, mask);
+      if (rc == 0) ++armed; else last = rc;
+    }
+    events_on_ = armed > 0;
+    events_note(true, armed, last);
     return true;
   }
 
@@ -749,6 +805,10 @@ class AmdSmiBackend : public Backend {
 class FakeBackend : public Backend {
  public:
   const char* name() const override { return "fake"; }
+  bool events_start(const std::vector<gs_device_t>& devs) override {
+    events_note(true, (int)devs.size(), 0);  // injected events are always delivered
+    return true;
+  }
 
   bool configure(const std::string& spec) {
     // "<N>x<SIZE>[G|M|B]" shorthand, e.g. "8x288G", "2x4G"; otherwise a JSON file path.
@@ -830,11 +890,14 @@ class FakeBackend : public Backend {
     std::vector<int> present;
     for (size_t i = 0; i < all_.size(); ++i)
       if (!unplugged_.count((int)i)) present.push_back((int)i);
+    ecc_begin();
     for (int k : present) {
       gs_device_t d = all_[k];
       d.index = (int32_t)devs->size();
       devs->push_back(d);
+      ecc_note(0);
     }
+    ecc_end(true);
     links->resize((int)present.size());
     for (size_t a = 0; a < present.size(); ++a)
       for (size_t b = 0; b < present.size(); ++b) {
@@ -1077,6 +1140,12 @@ int gs_wait_event(gs_handle* h, int timeout_ms, gs_event_t* ev) {
   if (!h || !ev) return -1;
   *ev = gs_event_t{};
   return h->be->wait_event(timeout_ms, ev);
+}
+
+int gs_health_status(const gs_handle* h, gs_health_status_t* out) {
+  if (!h || !out) return -1;
+  *out = h->be->status();
+  return 0;
 }
 
 int gs_inject(gs_handle* h, const char* cmd) {

@@ -17,7 +17,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 1
+#define GS_ABI_VERSION 2
 
 enum gs_health { GS_HEALTHY = 0, GS_UNHEALTHY = 1, GS_MISSING = 2 };
 enum gs_link_type { GS_LINK_NONE = 0, GS_LINK_PCIE = 1, GS_LINK_XGMI = 2, GS_LINK_SELF = 3 };
@@ -63,6 +63,19 @@ typedef struct gs_event {
   char message[96];
 } gs_event_t;
 
+// What the health path actually has on this backend (so a test on hardware can assert the
+// event stream was armed and the ECC counters were read, instead of "no event arrived").
+typedef struct gs_health_status {
+  int32_t events_api;          // 1: an event-notification API was resolved (rocm_smi / amdsmi)
+  int32_t events_armed;        // devices whose notification init + mask succeeded
+  int32_t events_last_status;  // last non-zero status from init/mask (0 = none)
+  int32_t ecc_api;             // 1: an ECC counter API (or sysfs RAS file) is available
+  int32_t ecc_reads_ok;        // devices whose ECC counters were read at the last refresh
+  int32_t ecc_reads_failed;    // devices whose ECC read failed at the last refresh
+  int32_t ecc_last_status;     // last non-zero status from the ECC read (0 = none)
+  int32_t refreshes;           // successful enumerations so far
+} gs_health_status_t;
+
 typedef struct gs_handle gs_handle;
 
 int gs_abi_version(void);
@@ -84,6 +97,8 @@ int gs_get_link(const gs_handle* h, int i, int j, gs_link_t* out);
 int gs_events_start(gs_handle* h);
 // Waits up to timeout_ms for one event. Returns 1 and fills *ev, 0 on timeout, <0 on error.
 int gs_wait_event(gs_handle* h, int timeout_ms, gs_event_t* ev);
+// Fills *out with the backend's health-path status (see gs_health_status_t).
+int gs_health_status(const gs_handle* h, gs_health_status_t* out);
 // Fault injection (fake backend only): "unplug I", "replug I", "reset I", "ecc I N",
 // "vmfault I", "linkdown I J", "linkup I J", "thermal I".
 int gs_inject(gs_handle* h, const char* cmd);

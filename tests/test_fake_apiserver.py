@@ -106,3 +106,58 @@ def test_expired_resource_version_gives_410(api):
     with pytest.raises(APIError) as e:
         list(c.watch_pods(None, "2", 1))
     assert e.value.gone
+
+
+def test_service_account_token_rotation(tmp_path, monkeypatch):
+    """Round-1 review: the in-cluster token was read once. Now it is re-read on a 401 (one
+    retry) and on a timer, for plain requests and for the pod informer's watch."""
+    tok = tmp_path / "token"
+    tok.write_text("t1\n")
+    with FakeAPIServer() as s:
+        s.store.valid_tokens = {"t1"}
+        cfg = KubeConfig(s.url, token_file=str(tok))
+        c = APIClient(cfg)
+        c.create_node(make_node("n1"))
+        # rotation: the apiserver only accepts the new token; the next call reloads and retries
+        tok.write_text("t2\n")
+        s.store.valid_tokens = {"t2"}
+        assert c.get_node("n1")["metadata"]["name"] == "n1"
+        assert cfg.token == "t2" and cfg.token_reloads == 2 and s.store.requests["401"] == 1
+        # timer: re-read without waiting for a 401
+        monkeypatch.setattr(KubeConfig, "TOKEN_RELOAD_S", 0.0)
+        tok.write_text("t3\n")
+        s.store.valid_tokens = {"t2", "t3"}
+        c.get_node("n1")
+        assert cfg.token == "t3" and s.store.requests["401"] == 1
+        # a static token (no file) that the apiserver rejects surfaces as 401
+        bad = APIClient(KubeConfig(s.url, token="nope"))
+        with pytest.raises(APIError) as e:
+            bad.get_node("n1")
+        assert e.value.status == 401
+        # the informer's watch survives a rotation
+        monkeypatch.setattr(KubeConfig, "TOKEN_RELOAD_S", 3600.0)
+        wc = WatchCache(APIClient(cfg), "n1").start()
+        assert wc.wait_synced(5)
+        tok.write_text("t4\n")
+        s.store.valid_tokens = {"t4"}
+        wc.stop()
+        wc2 = WatchCache(APIClient(cfg), "n1").start()
+        assert wc2.wait_synced(5) and cfg.token == "t4"
+        wc2.stop()
+
+
+def test_kubelet_client_token_reload(tmp_path):
+    from aliyun_gpushare_device_plugin_amd.cluster.kubelet import KubeletClient
+    from aliyun_gpushare_device_plugin_amd.sim.kubelet import FakeKubelet
+
+    tok = tmp_path / "token"
+    tok.write_text("k1")
+    with FakeAPIServer() as s:
+        kl = FakeKubelet(str(tmp_path / "dp"), APIClient(KubeConfig(s.url)), "n1")
+        port = kl.serve_pods(token="k1")
+        c = KubeletClient("127.0.0.1", port, token="k1", scheme="http", token_file=str(tok))
+        assert c.get_node_running_pods() == []
+        tok.write_text("k2")
+        kl.pods_token = "k2"
+        assert c.get_node_running_pods() == [] and c.token == "k2"
+        kl.stop()

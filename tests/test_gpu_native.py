@@ -41,7 +41,13 @@ def test_backends_agree(backend):
         assert [[a.link(i, j).type for j in range(n)] for i in range(n)] == \
                [[b.link(i, j).type for j in range(n)] for i in range(n)]
         a.events_start()
-        assert a.wait_event(50) is None or a.wait_event(50).kind >= 0
+        st = a.health_status()
+        # the health path is live on MI355X: event notification armed on every GPU and the HBM
+        # (UMC) ECC counters read on every GPU at the last refresh
+        assert st["events_api"] == 1 and st["events_armed"] == n, st
+        assert st["ecc_api"] == 1 and st["ecc_reads_ok"] == n and st["ecc_reads_failed"] == 0, st
+        ev = a.wait_event(50)                     # no fault on a healthy box: a timeout
+        assert ev is None or ev.kind in (1, 2, 3, 4), ev
 
 
 def test_advertised_units_mi355x():

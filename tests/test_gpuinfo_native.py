@@ -128,6 +128,21 @@ def test_sysfs_backend_on_synthetic_tree(tmp_path):
         assert g.compute_partition == 1 and g.memory_partition == 1 and g.ecc_ce == 2
         assert s.link(0, 1).type == S.LINK_XGMI and s.link(0, 1).hops == 1 and s.link(0, 1).weight == 15
         assert s.device(1).bdf == "0000:1a:00.0"
+        st = s.health_status()
+        assert st["ecc_api"] == 1 and st["ecc_reads_ok"] == 3 and st["ecc_reads_failed"] == 0
+        assert st["events_api"] == 0 and st["refreshes"] >= 1       # sysfs: polling only
+    os.remove(f"{tmp_path}/sys/class/drm/renderD136/device/ras/umc_err_count")
+    with S.SMI(f"sysfs:{tmp_path}") as s:
+        st = s.health_status()
+        assert st["ecc_reads_ok"] == 2 and st["ecc_reads_failed"] == 1
+
+
+def test_health_status_fake_backend():
+    with S.SMI("fake:4x288G") as s:
+        assert s.health_status()["events_armed"] == 0
+        s.events_start()
+        st = s.health_status()
+        assert st["events_api"] == 1 and st["events_armed"] == 4 and st["ecc_reads_ok"] == 4
 
 
 def test_sysfs_missing_tree_errors(tmp_path):

@@ -25,7 +25,7 @@ def test_summary_table():
     pods = [mkpod("p1", 64, 0, 1, node="n1", phase="Running"), mkpod("p2", 32, 1, 1, node="n1", phase="Running"),
             mkpod("p3", 16, None, 1, node="n1")]                                  # no index -> pending
     infos = I.build_node_infos(pods, [n])
-    assert I.guess_unit(infos) == "MiB"         # per-GPU 288 > 100: the reference's unit guess
+    assert I.guess_unit(infos) == "GiB"         # 288 units/GPU is an MI355X in GiB (the reference said MiB)
     out = I.display_summary(infos, "GiB")
     lines = out.splitlines()
     assert lines[0].split() == ["NAME", "IPADDRESS", "GPU0(Allocated/Total)", "GPU1(Allocated/Total)",
@@ -34,6 +34,16 @@ def test_summary_table():
     assert set(lines[2]) == {"-"}
     assert lines[3] == "Allocated/Total GPU Memory In Cluster:"
     assert lines[4].strip() == "112/576 (19%)"
+
+
+def test_unit_from_plugin_annotation_then_heuristic():
+    """Round-1 review: the plugin's exported unit wins; without it the fallback threshold
+    (1024) keeps an MI355X in GiB (288/GPU) and a 16 GiB card in MiB (16384/GPU)."""
+    mib_node = node("m", 1, 288, ann={const.NODE_ANNOTATION_MEMORY_UNIT: "MiB"})   # a 288 MiB slice in MiB mode
+    assert I.guess_unit(I.build_node_infos([], [mib_node])) == "MiB"
+    assert I.guess_unit(I.build_node_infos([], [node("g", 8, 8 * 288)])) == "GiB"
+    assert I.guess_unit(I.build_node_infos([], [node("old", 2, 2 * 16384)])) == "MiB"
+    assert I.guess_unit(I.build_node_infos([], [node("x", 0, 0)])) == ""
 
 
 def test_details_table_and_allocation_annotation():
@@ -62,6 +72,7 @@ def test_render_against_live_fake_cluster():
         c.run_pod(2)
         out = I.render(c.client)
         assert "node-a" in out and "5/8" in out and "GPU Memory(GiB)" in out
+        assert c.client.get_node("node-a")["metadata"]["annotations"][const.NODE_ANNOTATION_MEMORY_UNIT] == "GiB"
         assert I.render(c.client, "node-a", details=True).count("pod-") == 2
         topo = I.render(c.client, topology=True)
         assert "XGMI1" in topo and "Healthy" in topo

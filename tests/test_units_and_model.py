@@ -82,9 +82,55 @@ def test_health_generation_and_recovery():
     assert all(d.health == const.HEALTHY for d in m.device_list())
 
 
-def test_mib_mode_limit():
-    with pytest.raises(ValueError):
-        DeviceModel([gpu(i) for i in range(8)], const.MIB)
+def test_mib_mode_falls_back_to_gib_on_mi355x():
+    """Round-1 review: MiB mode on 8 x MI355X (2.36 M fake devices) used to raise, and the
+    plugin exited 1 -> DaemonSet crash loop. Now: GiB with a recorded reason; small GPUs keep MiB."""
+    m = DeviceModel([gpu(i) for i in range(8)], const.MIB)
+    assert m.unit == const.GIB and m.dev_units() == 288 and "MiB devices exceed" in m.unit_fallback
+    small = DeviceModel([gpu(i, 4 << 30) for i in range(2)], const.MIB)
+    assert small.unit == const.MIB and small.dev_units() == 4096 and not small.unit_fallback
+
+
+def test_mib_fallback_end_to_end_and_impossible_config_parks(monkeypatch):
+    """The plugin started with --memory-unit=MiB on an MI355X node registers in GiB and says so
+    on the node; a node it can never advertise parks (exit code 0 on SIGTERM), never exits 1."""
+    import dataclasses
+
+    from aliyun_gpushare_device_plugin_amd.cluster import objects as O
+    from aliyun_gpushare_device_plugin_amd.sim.cluster import SimCluster
+    from aliyun_gpushare_device_plugin_amd.utils import units as U
+
+    c = SimCluster([("n", "fake:2x309220868096B")])
+    base = c._plugin_cfg
+    c._plugin_cfg = lambda node: dataclasses.replace(base(node), memory_unit=const.MIB)
+    with c:
+        n = c.client.get_node("n")
+        assert O.node_allocatable(n, const.RESOURCE_NAME) == 2 * 288
+        assert O.annotations(n)[const.NODE_ANNOTATION_MEMORY_UNIT] == const.GIB
+        assert c.manager("n").metrics.unit_fallback.value() == 1
+
+    import signal
+    import tempfile
+    import threading
+    import time
+
+    from aliyun_gpushare_device_plugin_amd.device import smi as S
+    from aliyun_gpushare_device_plugin_amd.plugin.manager import PluginConfig, SharedGPUManager
+
+    monkeypatch.setattr(U, "MAX_FAKE_DEVICES_PER_NODE", 100)
+    d = tempfile.mkdtemp(prefix="gs-park-", dir="/tmp")
+    m = SharedGPUManager(PluginConfig(node_name="n", smi_backend="fake:1x288G", device_plugin_dir=d),
+                         smi=S.SMI("fake:1x288G"))
+    rc = []
+    t = threading.Thread(target=lambda: rc.append(m.run(install_signals=False)), daemon=True)
+    t.start()
+    t0 = time.monotonic()
+    while m.metrics.config_error.value() != 1 and time.monotonic() - t0 < 10:
+        time.sleep(0.01)
+    assert m.metrics.config_error.value() == 1 and t.is_alive()       # parked, not exited
+    m.events.put(("signal", signal.SIGTERM))
+    t.join(10)
+    assert rc == [0]
 
 
 def part(i, socket, cp=4, nps=1, nbytes=MI355X_BYTES):
