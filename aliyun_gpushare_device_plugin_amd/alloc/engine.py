@@ -50,7 +50,7 @@ from ..cluster.client import APIClient, APIError
 from ..cluster.podcache import PodSource
 from ..device.model import DeviceModel
 from ..quota import ShimConfig, ledger_name
-from ..utils import log
+from ..utils import log, units as U
 from ..utils.metrics import PluginMetrics
 from . import annotations as A
 from . import cuslots
@@ -350,6 +350,8 @@ class Allocator:
             r.mounts.add(container_path=shim.container_dir, host_path=shim.host_dir, read_only=True)
             r.envs[const.ENV_LD_PRELOAD] = shim.container_lib
             r.envs[const.ENV_SHIM_LEDGER] = ledger_name(pod_uid or f"{gpu_index}-{time.time_ns()}", slot)
+            # exact bytes from the SMI-reported HBM size, so the shim needs no device query
+            r.envs[const.ENV_SHIM_QUOTA_BYTES] = str(U.quota_bytes(ctr_units, g.units, g.vram_bytes))
             if self.opts.ledger_dir:
                 r.mounts.add(container_path=const.LEDGER_CONTAINER_DIR, host_path=self.opts.ledger_dir,
                              read_only=False)

@@ -5,6 +5,7 @@ Targets
   gpuinfo   libgpushare_gpuinfo.so + gpushare-smi (C++17, host only; librocm_smi64 is dlopen'ed)
   hipshim   libgpushare_hipquota.so  (C++17 LD_PRELOAD interposer over the HIP allocation API)
   kernels   libgpushare_kernels.so   (hand-written HIP/CDNA4 kernels, hipcc --offload-arch=gfx950)
+  probes    shim_probe               (HIP test helper run under the quota shim on hardware)
 
 Usage: python native/build.py [targets...] [--force] [--asan | --sanitize {asan,tsan}] [-j N]
 The build is incremental (mtime based) so ``__graft_entry__.build()`` stays cheap.
@@ -103,7 +104,14 @@ def build_hipshim(force=False, asan=False):
     if force or _newer(lib, [src] + _headers(d)):
         # Deliberately NOT linked against libamdhip64: the real entry points are resolved at
         # run time from whichever HIP runtime the process loaded (PyTorch bundles its own).
-        _run([CXX, *flags, "-shared", "-o", lib, src, "-ldl", "-pthread", "-lrt"])
+        # -static-libstdc++/-static-libgcc: the shim is preloaded into arbitrary tenant images,
+        # whose libstdc++ may be older than ours (or absent); only glibc stays dynamic.
+        # The shim uses no libstdc++ runtime at all (checked by tests/test_hipquota_shim.py) and
+        # pins its glibc symbol versions to the 2.2.5 baseline; libdl/librt/libpthread stay
+        # NEEDED for images whose glibc predates their merge into libc (2.34).
+        static = [] if san else ["-static-libstdc++", "-static-libgcc", "-fno-exceptions", "-fno-rtti"]
+        _run([CXX, *flags, "-shared", "-o", lib, src, *static, "-Wl,--no-as-needed", "-l:libdl.so.2", "-l:librt.so.1", "-l:libpthread.so.0",
+              "-Wl,--as-needed"])
     return [lib]
 
 
@@ -133,7 +141,24 @@ def build_kernels(force=False, asan=False, jobs=4):
     return [lib]
 
 
-TARGETS = {"gpuinfo": build_gpuinfo, "hipshim": build_hipshim, "kernels": build_kernels}
+def build_probes(force=False, asan=False):
+    """On-hardware test helpers (native/probes/*.hip): standalone HIP programs the GPU tests run
+    under the quota shim (a plain executable, so LD_PRELOAD applies exactly as in a container)."""
+    d = _src("probes")
+    out = []
+    if asan or not os.path.isdir(d):
+        return out
+    for f in sorted(os.listdir(d)):
+        if not f.endswith(".hip"):
+            continue
+        exe = os.path.join(OUT, os.path.splitext(f)[0])
+        if force or _newer(exe, [os.path.join(d, f)]):
+            _run([HIPCC, "-std=c++17", "-O2", f"--offload-arch={ARCH}", "-o", exe, os.path.join(d, f), "-ldl"])
+        out.append(exe)
+    return out
+
+
+TARGETS = {"gpuinfo": build_gpuinfo, "hipshim": build_hipshim, "kernels": build_kernels, "probes": build_probes}
 
 
 def build(targets=None, force=False, asan=False, jobs=4):

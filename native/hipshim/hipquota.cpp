@@ -1,35 +1,51 @@
-// libgpushare_hipquota.so — per-container HBM quota for HIP programs (LD_PRELOAD interposer).
+// libgpushare_hipquota.so — per-container HBM quota for GPU programs (LD_PRELOAD interposer).
 //
 // The reference plugin only *describes* a container's GPU-memory share through env vars
 // (ALIYUN_COM_GPU_MEM_CONTAINER / _DEV, allocate.go:114-129) and relies on Alibaba's closed
 // cGPU kernel module to enforce it (CGPU_DISABLE switches it off, allocate.go:125-127).
 // On MI355X the plugin mounts this library into every shared container and preloads it:
 //
-//   quota = GPUSHARE_QUOTA_BYTES                      if set, else
-//           real_HBM_bytes * CONTAINER / DEV           (unit-agnostic: GiB or MiB mode)
+//   quota = GPUSHARE_QUOTA_BYTES                      (the plugin sets it: HBM bytes * CONTAINER / DEV)
+//           else real_HBM_bytes * CONTAINER / DEV     (HBM bytes from the KFD topology / HIP)
 //
-// Every HIP device-allocation entry point is interposed: hipMalloc, hipExtMallocWithFlags,
-// hipMallocManaged, hipMallocAsync, hipMallocFromPoolAsync, hipMallocPitch, hipMalloc3D and the
-// VMM path hipMemCreate/hipMemRelease (PyTorch expandable segments); frees release the charge.
-// hipMemGetInfo / hipDeviceTotalMem / hipGetDeviceProperties report the quota as the device
-// total so frameworks size their pools to the share rather than the whole GPU.
+// Enforcement point (default, GPUSHARE_SHIM_MODE=kfd): the KFD boundary. Every byte of HBM a
+// process owns is created by one ioctl on /dev/kfd — AMDKFD_IOC_ALLOC_MEMORY_OF_GPU with the
+// VRAM flag — issued by ROCr (libhsa-runtime64 imports ioctl from libc through its PLT, so a
+// preloaded ioctl sees it) and released by AMDKFD_IOC_FREE_MEMORY_OF_GPU. Charging there
+// covers what the HIP entry points cannot see: hipMallocAsync pools that keep memory after
+// hipFreeAsync (charged until the pool trims), hipMallocArray / 3D arrays, scratch (private
+// segment) buffers, code objects, queue and staging buffers allocated inside the runtime, and
+// programs that call HSA directly. The charge is the physical allocation KFD hands out (ROCr
+// grabs 2 MiB fragments and sub-allocates), so no rounding model is needed. Over quota the
+// ioctl fails with ENOMEM, exactly as when HBM runs out: ROCr trims its caches and retries,
+// then reports HSA_STATUS_ERROR_OUT_OF_RESOURCES / hipErrorOutOfMemory.
 //
-// CDNA4 accounting: MI355X's allocator hands out memory in 2 MiB fragments — a 1-byte
-// hipMalloc consumes 2 MiB of HBM and 2 MiB + 1 B consumes 4 MiB (measured with
-// hipMemGetInfo deltas on MI355X, see profiles/). Charges are rounded to that granule so the
-// quota bounds *physical* HBM, not requested bytes (override: GPUSHARE_ALLOC_GRANULE).
+// hipMemGetInfo / hipDeviceTotalMem / hipGetDeviceProperties are also interposed so frameworks
+// see the quota as the device total and the quota's remainder as free memory.
 //
-// All processes of one container share one ledger in POSIX shared memory (GPUSHARE_LEDGER):
-// a global atomic total plus one slot per process, so a crashed process's charge is reclaimed
-// by the next allocation that needs room (its pid no longer exists).
+// GPUSHARE_SHIM_MODE=hip keeps the older HIP-API accounting (hipMalloc family + VMM, charges
+// rounded to the 2 MiB CDNA4 fragment, GPUSHARE_ALLOC_GRANULE) for runtimes whose KFD traffic
+// is not visible; the two modes never both charge.
 //
-// The library does not link libamdhip64: the real entry points are resolved at run time from
-// whichever HIP runtime the process loaded (PyTorch ships its own copy).
+// All processes of one container share one ledger in POSIX shared memory (GPUSHARE_LEDGER) or
+// a file in a host directory (GPUSHARE_LEDGER_DIR): a global atomic total plus one slot per
+// process, so a crashed process's charge is reclaimed by the next allocation that needs room.
+// A forked child starts with an empty allocation table and its own slot (a child does not
+// inherit its parent's KFD allocations).
+//
+// Limits (documented, by construction): enforcement is cooperative — a process that drops
+// LD_PRELOAD or issues the ioctl through a raw syscall is not charged. Memory imported from
+// another process (dma-buf / IPC) is charged to its exporter only.
+//
+// The library does not link libamdhip64 or libhsa-runtime64: the real entry points are
+// resolved at run time from whichever runtime the process loaded (PyTorch ships its own copy).
+// It is linked with -static-libstdc++ -static-libgcc so it loads into any tenant image.
 
 #define __HIP_PLATFORM_AMD__ 1
 #include <hip/hip_runtime_api.h>
 #include <hip/hip_deprecated.h>
 
+#include <dirent.h>
 #include <dlfcn.h>
 #include <errno.h>
 #include <fcntl.h>
@@ -45,8 +61,16 @@
 #include <unistd.h>
 
 #include <atomic>
-#include <mutex>
-#include <unordered_map>
+#include <new>
+
+// Symbol versions pinned to the x86-64 glibc baseline (2.2.5) so the shim loads into tenant
+// images with an old glibc (it is linked against this image's 2.35, where these moved into
+// libc proper under GLIBC_2.34); libdl/librt/libpthread stay NEEDED for those images.
+__asm__(".symver dlsym,dlsym@GLIBC_2.2.5");
+__asm__(".symver dlopen,dlopen@GLIBC_2.2.5");
+__asm__(".symver shm_open,shm_open@GLIBC_2.2.5");
+__asm__(".symver pthread_once,pthread_once@GLIBC_2.2.5");
+__asm__(".symver memcpy,memcpy@GLIBC_2.2.5");
 
 #undef hipGetDeviceProperties
 
@@ -57,6 +81,28 @@ namespace {
 constexpr uint64_t kMagic = 0x67707573686172ULL;  // "gpushar"
 constexpr int kSlots = 256;
 constexpr uint64_t kDefaultGranule = 2ull << 20;
+
+// ---- KFD uapi (linux/kfd_ioctl.h, stable since KFD 1.0; mirrored so the shim builds without
+// kernel headers and matches any ROCr) ----------------------------------------------------------
+struct KfdAllocArgs {   // struct kfd_ioctl_alloc_memory_of_gpu_args
+  uint64_t va_addr;
+  uint64_t size;
+  uint64_t handle;
+  uint64_t mmap_offset;
+  uint32_t gpu_id;
+  uint32_t flags;
+};
+struct KfdFreeArgs {    // struct kfd_ioctl_free_memory_of_gpu_args
+  uint64_t handle;
+};
+constexpr uint32_t kKfdVram = 1u << 0;  // KFD_IOC_ALLOC_MEM_FLAGS_VRAM
+// _IOC(dir, 'K', nr, size): dir bits 30-31 (1 write, 2 read), size bits 16-29, type 8-15, nr 0-7
+constexpr unsigned long kfd_ioc(unsigned dir, unsigned nr, unsigned size) {
+  return ((unsigned long)dir << 30) | ((unsigned long)size << 16) | ((unsigned long)'K' << 8) | nr;
+}
+constexpr unsigned long kIocAlloc = kfd_ioc(3, 0x16, sizeof(KfdAllocArgs));  // AMDKFD_IOWR(0x16)
+constexpr unsigned long kIocFree = kfd_ioc(1, 0x17, sizeof(KfdFreeArgs));    // AMDKFD_IOW(0x17)
+static_assert(sizeof(KfdAllocArgs) == 40 && sizeof(KfdFreeArgs) == 8, "KFD uapi layout");
 
 struct Slot {
   std::atomic<int32_t> pid;
@@ -73,10 +119,14 @@ struct LedgerShm {
   Slot slots[kSlots];
 };
 
+enum Mode { kModeKfd = 0, kModeHip = 1 };
+
 struct State {
   bool enabled = false;
+  int mode = kModeKfd;
   int log = 0;
-  uint64_t quota = 0;
+  std::atomic<uint64_t> quota{0};   // 0 in kfd mode until the first VRAM allocation names its GPU
+  uint64_t ctr = 0, dev = 0;        // container / device units when the quota is derived
   uint64_t granule = kDefaultGranule;
   LedgerShm* ledger = nullptr;
   LedgerShm local{};  // used when no shared ledger is configured
@@ -85,7 +135,8 @@ struct State {
 };
 
 State g;
-std::once_flag g_once;
+pthread_once_t g_once = PTHREAD_ONCE_INIT;
+std::atomic<bool> g_released{false};  // set by the atexit handler (see release_slot_at_exit)
 thread_local int t_depth = 0;  // re-entrancy guard (HIP calling itself through the PLT)
 
 void logf(int level, const char* fmt, ...) {
@@ -152,28 +203,108 @@ REAL(hipError_t, hipGetDevicePropertiesR0600, hipDeviceProp_tR0600*, int)
 REAL(hipError_t, hipGetDevicePropertiesR0000, hipDeviceProp_tR0000*, int)
 REAL(hipError_t, hipGetDeviceProperties, hipDeviceProp_tR0000*, int)
 
-// ---- pointer table (sharded) ---------------------------------------------------------------
-struct Shard {
-  std::mutex mu;
-  std::unordered_map<uintptr_t, uint64_t> m;
-};
-Shard g_shards[64];
+using ioctl_t = int (*)(int, unsigned long, ...);
+std::atomic<ioctl_t> g_real_ioctl{nullptr};
 
-Shard& shard_of(uintptr_t k) { return g_shards[(k >> 21) & 63]; }
-
-void track(uintptr_t k, uint64_t charge) {
-  Shard& s = shard_of(k);
-  std::lock_guard<std::mutex> lk(s.mu);
-  s.m[k] = charge;
+ioctl_t real_ioctl() {
+  ioctl_t f = g_real_ioctl.load(std::memory_order_acquire);
+  if (!f) {
+    f = reinterpret_cast<ioctl_t>(dlsym(RTLD_NEXT, "ioctl"));
+    g_real_ioctl.store(f, std::memory_order_release);
+  }
+  return f;
 }
 
-uint64_t untrack(uintptr_t k) {
+// ---- allocation table (sharded): pointer (hip mode) or KFD handle (kfd mode) -> charge -------
+// No libstdc++ containers: the shim must not pull libstdc++'s runtime (exception objects need a
+// newer glibc than tenant images may have). Open addressing, linear probing, key 0 = empty,
+// key ~0 = deleted; grows at 50 % load.
+struct Shard {
+  pthread_mutex_t mu = PTHREAD_MUTEX_INITIALIZER;
+  uint64_t* keys = nullptr;
+  uint64_t* vals = nullptr;
+  size_t cap = 0, used = 0;  // used counts live + deleted slots
+};
+Shard g_shards[64];
+constexpr uint64_t kEmpty = 0, kDeleted = ~0ull;
+
+Shard& shard_of(uint64_t k) { return g_shards[((k >> 21) ^ k) & 63]; }
+
+size_t slot_of(uint64_t k, size_t cap) { return (size_t)((k * 0x9E3779B97F4A7C15ull) >> 20) & (cap - 1); }
+
+bool grow(Shard& s) {
+  size_t ncap = s.cap ? s.cap * 2 : 64;
+  auto* nk = static_cast<uint64_t*>(calloc(ncap, sizeof(uint64_t)));
+  auto* nv = static_cast<uint64_t*>(calloc(ncap, sizeof(uint64_t)));
+  if (!nk || !nv) {
+    free(nk);
+    free(nv);
+    return false;
+  }
+  size_t live = 0;
+  for (size_t i = 0; i < s.cap; ++i) {
+    uint64_t k = s.keys[i];
+    if (k == kEmpty || k == kDeleted) continue;
+    size_t j = slot_of(k, ncap);
+    while (nk[j] != kEmpty) j = (j + 1) & (ncap - 1);
+    nk[j] = k;
+    nv[j] = s.vals[i];
+    ++live;
+  }
+  free(s.keys);
+  free(s.vals);
+  s.keys = nk;
+  s.vals = nv;
+  s.cap = ncap;
+  s.used = live;
+  return true;
+}
+
+void track(uint64_t k, uint64_t charge) {
+  if (k == kEmpty || k == kDeleted) return;
   Shard& s = shard_of(k);
-  std::lock_guard<std::mutex> lk(s.mu);
-  auto it = s.m.find(k);
-  if (it == s.m.end()) return 0;
-  uint64_t c = it->second;
-  s.m.erase(it);
+  pthread_mutex_lock(&s.mu);
+  if ((s.used + 1) * 2 > s.cap && !grow(s)) {
+    pthread_mutex_unlock(&s.mu);
+    return;  // out of host memory: the charge stays (conservative)
+  }
+  size_t i = slot_of(k, s.cap), tomb = (size_t)-1;
+  for (;; i = (i + 1) & (s.cap - 1)) {
+    if (s.keys[i] == k) {
+      s.vals[i] = charge;
+      break;
+    }
+    if (s.keys[i] == kDeleted && tomb == (size_t)-1) tomb = i;
+    if (s.keys[i] == kEmpty) {
+      if (tomb != (size_t)-1) {
+        i = tomb;
+      } else {
+        ++s.used;
+      }
+      s.keys[i] = k;
+      s.vals[i] = charge;
+      break;
+    }
+  }
+  pthread_mutex_unlock(&s.mu);
+}
+
+uint64_t untrack(uint64_t k) {
+  if (k == kEmpty || k == kDeleted) return 0;
+  Shard& s = shard_of(k);
+  pthread_mutex_lock(&s.mu);
+  uint64_t c = 0;
+  if (s.cap) {
+    for (size_t i = slot_of(k, s.cap), n = 0; n < s.cap; i = (i + 1) & (s.cap - 1), ++n) {
+      if (s.keys[i] == kEmpty) break;
+      if (s.keys[i] == k) {
+        c = s.vals[i];
+        s.keys[i] = kDeleted;
+        break;
+      }
+    }
+  }
+  pthread_mutex_unlock(&s.mu);
   return c;
 }
 
@@ -218,11 +349,13 @@ int acquire_slot(LedgerShm* L) {
 }
 
 bool charge(uint64_t bytes) {
+  if (g_released.load(std::memory_order_relaxed)) return true;  // process teardown
   LedgerShm* L = g.ledger;
+  uint64_t quota = g.quota.load(std::memory_order_relaxed);
   bool reclaimed = false;
   uint64_t cur = L->total.load();
   for (;;) {
-    if (cur + bytes > g.quota) {
+    if (quota && cur + bytes > quota) {
       if (!reclaimed && reclaim_dead(L) > 0) {
         reclaimed = true;
         cur = L->total.load();
@@ -241,7 +374,7 @@ bool charge(uint64_t bytes) {
 }
 
 void uncharge(uint64_t bytes) {
-  if (!bytes) return;
+  if (!bytes || g_released.load(std::memory_order_relaxed)) return;
   if (g.slot >= 0) g.ledger->slots[g.slot].used.fetch_sub(bytes);
   g.ledger->total.fetch_sub(bytes);
 }
@@ -257,8 +390,59 @@ uint64_t env_u64(const char* name, uint64_t dflt) {
   return (end && end != v) ? (uint64_t)x : dflt;
 }
 
+// HBM bytes of the GPU whose KFD gpu_id is `gpu_id`, from the KFD topology (no HIP call: this
+// runs inside ROCr's own initialisation). 0 when unknown.
+uint64_t kfd_vram_bytes(uint32_t gpu_id) {
+  char base[256];  // GPUSHARE_KFD_SYSFS: root prefix of a synthetic topology (tests)
+  const char* root = getenv("GPUSHARE_KFD_SYSFS");
+  snprintf(base, sizeof base, "%s/sys/class/kfd/kfd/topology/nodes", root ? root : "");
+  DIR* d = opendir(base);
+  if (!d) return 0;
+  uint64_t out = 0;
+  while (struct dirent* e = readdir(d)) {
+    if (e->d_name[0] < '0' || e->d_name[0] > '9') continue;
+    char path[256], buf[64];
+    snprintf(path, sizeof path, "%s/%s/gpu_id", base, e->d_name);
+    FILE* f = fopen(path, "re");
+    if (!f) continue;
+    unsigned long id = 0;
+    bool ok = fgets(buf, sizeof buf, f) && sscanf(buf, "%lu", &id) == 1;
+    fclose(f);
+    if (!ok || id != gpu_id) continue;
+    for (int bank = 0; bank < 16 && !out; ++bank) {
+      snprintf(path, sizeof path, "%s/%s/mem_banks/%d/properties", base, e->d_name, bank);
+      FILE* p = fopen(path, "re");
+      if (!p) break;
+      char line[128];
+      unsigned long long heap = 0, size = 0;
+      while (fgets(line, sizeof line, p)) {
+        sscanf(line, "heap_type %llu", &heap);
+        sscanf(line, "size_in_bytes %llu", &size);
+      }
+      fclose(p);
+      if (heap == 1 || heap == 2) out = size;  // HSA_HEAPTYPE_FRAME_BUFFER_PUBLIC / _PRIVATE
+    }
+    break;
+  }
+  closedir(d);
+  return out;
+}
+
+void set_quota_from_device_bytes(uint64_t tot) {
+  if (!tot || !g.ctr || !g.dev) return;
+  uint64_t q = (uint64_t)((__uint128_t)tot * g.ctr / g.dev);
+  if (q > tot) q = tot;
+  uint64_t zero = 0;
+  if (g.ledger->quota.compare_exchange_strong(zero, q)) logf(1, "quota %llu bytes from %llu device bytes",
+                                                            (unsigned long long)q, (unsigned long long)tot);
+  g.quota.store(g.ledger->quota.load());
+}
+
+// atexit: hand the slot back. The runtime's own teardown (later destructors) still frees its
+// allocations through the ioctl; from here on the ledger is no longer this process's to touch.
 void release_slot_at_exit() {
   if (!g.enabled || !g.ledger || g.slot < 0) return;
+  g_released.store(true);
   Slot& s = g.ledger->slots[g.slot];
   uint64_t u = s.used.exchange(0);
   g.ledger->total.fetch_sub(u);
@@ -267,7 +451,23 @@ void release_slot_at_exit() {
 }
 
 void atfork_child() {
-  if (g.enabled && g.ledger) g.slot = acquire_slot(g.ledger);  // the child is a new process
+  if (!g.enabled || !g.ledger) return;
+  // The child is a new process: it owns none of the parent's allocations (KFD allocations are
+  // per process; the parent's pointers are the parent's to free) and gets its own slot.
+  for (auto& s : g_shards) {
+    pthread_mutex_init(&s.mu, nullptr);  // a lock held by another parent thread at fork time is void here
+    if (s.cap) memset(s.keys, 0, s.cap * sizeof(uint64_t));
+    s.used = 0;
+  }
+  if (g.ledger == &g.local) {  // a process-private ledger: the copy still holds the parent's charges
+    g.local.total.store(0);
+    g.local.peak.store(0);
+    for (auto& sl : g.local.slots) {
+      sl.pid.store(0);
+      sl.used.store(0);
+    }
+  }
+  g.slot = acquire_slot(g.ledger);
 }
 
 void init() {
@@ -277,14 +477,17 @@ void init() {
     logf(1, "CGPU_DISABLE=true: quota enforcement off");
     return;
   }
-  g.granule = env_u64("GPUSHARE_ALLOC_GRANULE", kDefaultGranule);
+  const char* mode = getenv("GPUSHARE_SHIM_MODE");
+  g.mode = (mode && !strcmp(mode, "hip")) ? kModeHip : kModeKfd;
+  g.granule = g.mode == kModeHip ? env_u64("GPUSHARE_ALLOC_GRANULE", kDefaultGranule) : 1;
   uint64_t q = env_u64("GPUSHARE_QUOTA_BYTES", 0);
-  if (!q) {
-    uint64_t ctr = env_u64("ALIYUN_COM_GPU_MEM_CONTAINER", 0), dev = env_u64("ALIYUN_COM_GPU_MEM_DEV", 0);
-    if (!ctr || !dev) {
-      logf(1, "no quota configured: pass-through");
-      return;
-    }
+  g.ctr = env_u64("ALIYUN_COM_GPU_MEM_CONTAINER", 0);
+  g.dev = env_u64("ALIYUN_COM_GPU_MEM_DEV", 0);
+  if (!q && (!g.ctr || !g.dev)) {
+    logf(1, "no quota configured: pass-through");
+    return;
+  }
+  if (!q && g.mode == kModeHip) {
     size_t fr = 0, tot = 0;
     t_depth++;
     hipError_t e = real_hipMemGetInfo() ? real_hipMemGetInfo()(&fr, &tot) : hipErrorNotInitialized;
@@ -293,10 +496,11 @@ void init() {
       logf(0, "cannot read device memory (err %d): pass-through", (int)e);
       return;
     }
-    q = (uint64_t)((__uint128_t)tot * ctr / dev);
+    q = (uint64_t)((__uint128_t)tot * g.ctr / g.dev);
     if (q > tot) q = tot;
   }
-  g.quota = q;
+  // kfd mode without GPUSHARE_QUOTA_BYTES: the quota is derived at the first VRAM allocation
+  // from that GPU's HBM size (KFD topology), see kfd_alloc().
   const char* ln = getenv("GPUSHARE_LEDGER");
   if (ln && *ln) {
     snprintf(g.ledger_name, sizeof g.ledger_name, "%s%s", ln[0] == '/' ? "" : "/", ln);
@@ -318,7 +522,7 @@ void init() {
       if (p != MAP_FAILED) {
         g.ledger = static_cast<LedgerShm*>(p);
         uint64_t zero = 0;  // first process initialises; ftruncate zero-fills
-        if (g.ledger->magic.compare_exchange_strong(zero, kMagic)) g.ledger->quota.store(q);
+        if (g.ledger->magic.compare_exchange_strong(zero, kMagic) && q) g.ledger->quota.store(q);
       }
     }
     if (fd >= 0) close(fd);
@@ -329,20 +533,28 @@ void init() {
     g.local.magic.store(kMagic);
     g.local.quota.store(q);
   }
-  g.quota = g.ledger->quota.load() ? g.ledger->quota.load() : q;
+  if (q) {
+    uint64_t zero = 0;
+    g.ledger->quota.compare_exchange_strong(zero, q);
+  }
+  g.quota.store(g.ledger->quota.load());
   g.slot = acquire_slot(g.ledger);
   g.enabled = true;
   atexit(release_slot_at_exit);
   pthread_atfork(nullptr, nullptr, atfork_child);
-  logf(1, "quota %llu bytes (%.2f GiB), granule %llu, ledger %s slot %d", (unsigned long long)g.quota,
-       (double)g.quota / (1ull << 30), (unsigned long long)g.granule, g.ledger_name[0] ? g.ledger_name : "(local)",
+  logf(1, "mode %s, quota %llu bytes (%.2f GiB%s), ledger %s slot %d", g.mode == kModeKfd ? "kfd" : "hip",
+       (unsigned long long)g.quota.load(), (double)g.quota.load() / (1ull << 30),
+       g.quota.load() ? "" : ", from the first GPU allocation", g.ledger_name[0] ? g.ledger_name : "(local)",
        g.slot);
 }
 
-inline bool active() {
-  std::call_once(g_once, init);
-  return g.enabled && t_depth == 0;
+inline bool enabled() {
+  pthread_once(&g_once, init);
+  return g.enabled;
 }
+
+// HIP-API accounting applies in hip mode only (kfd mode charges below, at the ioctl).
+inline bool hip_active() { return enabled() && g.mode == kModeHip && t_depth == 0; }
 
 struct Depth {
   Depth() { ++t_depth; }
@@ -351,13 +563,13 @@ struct Depth {
 
 hipError_t deny(size_t n) {
   logf(1, "deny %zu bytes: used %llu of %llu", n, (unsigned long long)g.ledger->total.load(),
-       (unsigned long long)g.quota);
+       (unsigned long long)g.quota.load());
   return hipErrorOutOfMemory;
 }
 
 template <class F>
 hipError_t guarded_alloc(void** ptr, size_t size, F&& call) {
-  if (!active()) return call();
+  if (!hip_active()) return call();
   uint64_t c = charge_of(size);
   if (c && !charge(c)) {
     if (ptr) *ptr = nullptr;
@@ -369,15 +581,66 @@ hipError_t guarded_alloc(void** ptr, size_t size, F&& call) {
     uncharge(c);
     return e;
   }
-  track((uintptr_t)*ptr, c);
+  track((uint64_t)(uintptr_t)*ptr, c);
   logf(2, "alloc %zu -> %p (charge %llu, used %llu)", size, *ptr, (unsigned long long)c,
        (unsigned long long)g.ledger->total.load());
   return e;
 }
 
+// ---- KFD boundary --------------------------------------------------------------------------
+int kfd_alloc(ioctl_t f, int fd, unsigned long req, KfdAllocArgs* a) {
+  if (!g.quota.load(std::memory_order_relaxed)) set_quota_from_device_bytes(kfd_vram_bytes(a->gpu_id));
+  uint64_t c = a->size;
+  if (!charge(c)) {
+    logf(1, "deny VRAM %llu bytes on gpu_id %u: used %llu of %llu", (unsigned long long)c, a->gpu_id,
+         (unsigned long long)g.ledger->total.load(), (unsigned long long)g.quota.load());
+    errno = ENOMEM;
+    return -1;
+  }
+  int r = f(fd, req, a);
+  if (r != 0) {
+    int err = errno;
+    uncharge(c);
+    errno = err;
+    return r;
+  }
+  track(a->handle, c);
+  logf(2, "kfd alloc %llu bytes (flags 0x%x) -> handle 0x%llx, used %llu", (unsigned long long)c, a->flags,
+       (unsigned long long)a->handle, (unsigned long long)g.ledger->total.load());
+  return r;
+}
+
 }  // namespace
 
-// ---- interposed API ------------------------------------------------------------------------
+// ---- interposed libc ioctl (kfd mode) ------------------------------------------------------
+GS_EXPORT int ioctl(int fd, unsigned long req, ...) {
+  va_list ap;
+  va_start(ap, req);
+  void* arg = va_arg(ap, void*);
+  va_end(ap);
+  ioctl_t f = real_ioctl();
+  if (!f) {
+    errno = ENOSYS;
+    return -1;
+  }
+  if ((req != kIocAlloc && req != kIocFree) || !arg || !enabled() || g.mode != kModeKfd) return f(fd, req, arg);
+  if (req == kIocAlloc) {
+    auto* a = static_cast<KfdAllocArgs*>(arg);
+    if (!(a->flags & kKfdVram)) return f(fd, req, arg);
+    return kfd_alloc(f, fd, req, a);
+  }
+  uint64_t h = static_cast<KfdFreeArgs*>(arg)->handle;
+  int r = f(fd, req, arg);
+  if (r == 0) {
+    uint64_t c = untrack(h);
+    uncharge(c);
+    logf(2, "kfd free handle 0x%llx -> %llu bytes, used %llu", (unsigned long long)h, (unsigned long long)c,
+         (unsigned long long)g.ledger->total.load());
+  }
+  return r;
+}
+
+// ---- interposed HIP API --------------------------------------------------------------------
 GS_EXPORT hipError_t hipMalloc(void** ptr, size_t size) {
   auto f = real_hipMalloc();
   if (!f) return hipErrorNotInitialized;
@@ -411,7 +674,7 @@ GS_EXPORT hipError_t hipMallocFromPoolAsync(void** ptr, size_t size, hipMemPool_
 GS_EXPORT hipError_t hipMallocPitch(void** ptr, size_t* pitch, size_t width, size_t height) {
   auto f = real_hipMallocPitch();
   if (!f) return hipErrorNotInitialized;
-  if (!active()) return f(ptr, pitch, width, height);
+  if (!hip_active()) return f(ptr, pitch, width, height);
   hipError_t e;
   {
     Depth d;
@@ -421,18 +684,18 @@ GS_EXPORT hipError_t hipMallocPitch(void** ptr, size_t* pitch, size_t width, siz
   uint64_t c = charge_of(*pitch * height);
   if (!charge(c)) {
     Depth d;
-    if (auto fr = real_hipFree()) fr(*ptr);
+    if (auto fr = real_hipFree()) (void)fr(*ptr);
     *ptr = nullptr;
     return deny(*pitch * height);
   }
-  track((uintptr_t)*ptr, c);
+  track((uint64_t)(uintptr_t)*ptr, c);
   return e;
 }
 
 GS_EXPORT hipError_t hipMalloc3D(hipPitchedPtr* pp, hipExtent ext) {
   auto f = real_hipMalloc3D();
   if (!f) return hipErrorNotInitialized;
-  if (!active()) return f(pp, ext);
+  if (!hip_active()) return f(pp, ext);
   hipError_t e;
   {
     Depth d;
@@ -442,37 +705,37 @@ GS_EXPORT hipError_t hipMalloc3D(hipPitchedPtr* pp, hipExtent ext) {
   uint64_t c = charge_of(pp->pitch * ext.height * ext.depth);
   if (!charge(c)) {
     Depth d;
-    if (auto fr = real_hipFree()) fr(pp->ptr);
+    if (auto fr = real_hipFree()) (void)fr(pp->ptr);
     pp->ptr = nullptr;
     return deny(pp->pitch * ext.height * ext.depth);
   }
-  track((uintptr_t)pp->ptr, c);
+  track((uint64_t)(uintptr_t)pp->ptr, c);
   return e;
 }
 
 GS_EXPORT hipError_t hipFree(void* ptr) {
   auto f = real_hipFree();
   if (!f) return hipErrorNotInitialized;
-  if (!active() || !ptr) return f(ptr);
+  if (!hip_active() || !ptr) return f(ptr);
   hipError_t e;
   {
     Depth d;
     e = f(ptr);
   }
-  if (e == hipSuccess) uncharge(untrack((uintptr_t)ptr));
+  if (e == hipSuccess) uncharge(untrack((uint64_t)(uintptr_t)ptr));
   return e;
 }
 
 GS_EXPORT hipError_t hipFreeAsync(void* ptr, hipStream_t stream) {
   auto f = real_hipFreeAsync();
   if (!f) return hipErrorNotInitialized;
-  if (!active() || !ptr) return f(ptr, stream);
+  if (!hip_active() || !ptr) return f(ptr, stream);
   hipError_t e;
   {
     Depth d;
     e = f(ptr, stream);
   }
-  if (e == hipSuccess) uncharge(untrack((uintptr_t)ptr));
+  if (e == hipSuccess) uncharge(untrack((uint64_t)(uintptr_t)ptr));
   return e;
 }
 
@@ -480,7 +743,7 @@ GS_EXPORT hipError_t hipMemCreate(hipMemGenericAllocationHandle_t* handle, size_
                                   const hipMemAllocationProp* prop, unsigned long long flags) {
   auto f = real_hipMemCreate();
   if (!f) return hipErrorNotInitialized;
-  if (!active()) return f(handle, size, prop, flags);
+  if (!hip_active()) return f(handle, size, prop, flags);
   uint64_t c = charge_of(size);
   if (c && !charge(c)) return deny(size);
   hipError_t e;
@@ -492,20 +755,20 @@ GS_EXPORT hipError_t hipMemCreate(hipMemGenericAllocationHandle_t* handle, size_
     uncharge(c);
     return e;
   }
-  track((uintptr_t)*handle, c);
+  track((uint64_t)(uintptr_t)*handle, c);
   return e;
 }
 
 GS_EXPORT hipError_t hipMemRelease(hipMemGenericAllocationHandle_t handle) {
   auto f = real_hipMemRelease();
   if (!f) return hipErrorNotInitialized;
-  if (!active()) return f(handle);
+  if (!hip_active()) return f(handle);
   hipError_t e;
   {
     Depth d;
     e = f(handle);
   }
-  if (e == hipSuccess) uncharge(untrack((uintptr_t)handle));
+  if (e == hipSuccess) uncharge(untrack((uint64_t)(uintptr_t)handle));
   return e;
 }
 
@@ -517,19 +780,31 @@ GS_EXPORT hipError_t hipMemGetInfo(size_t* free_b, size_t* total_b) {
     Depth d;  // init() may call the real hipMemGetInfo itself
     e = f(free_b, total_b);
   }
-  if (e != hipSuccess || !active()) return e;
+  if (e != hipSuccess || !enabled() || t_depth) return e;
+  if (!g.quota.load() && total_b) set_quota_from_device_bytes(*total_b);
+  uint64_t quota = g.quota.load();
+  if (!quota) return e;
   uint64_t used = g.ledger->total.load();
-  uint64_t left = used >= g.quota ? 0 : g.quota - used;
+  uint64_t left = used >= quota ? 0 : quota - used;
   if (free_b && *free_b > left) *free_b = (size_t)left;
-  if (total_b) *total_b = (size_t)g.quota;
+  if (total_b) *total_b = (size_t)quota;
   return e;
 }
+
+namespace {
+uint64_t report_total(uint64_t real_total) {
+  if (!enabled()) return real_total;
+  if (!g.quota.load()) set_quota_from_device_bytes(real_total);
+  uint64_t q = g.quota.load();
+  return (q && real_total > q) ? q : real_total;
+}
+}  // namespace
 
 GS_EXPORT hipError_t hipDeviceTotalMem(size_t* bytes, hipDevice_t dev) {
   auto f = real_hipDeviceTotalMem();
   if (!f) return hipErrorNotInitialized;
   hipError_t e = f(bytes, dev);
-  if (e == hipSuccess && active() && bytes && *bytes > g.quota) *bytes = (size_t)g.quota;
+  if (e == hipSuccess && bytes) *bytes = (size_t)report_total(*bytes);
   return e;
 }
 
@@ -537,7 +812,7 @@ GS_EXPORT hipError_t hipGetDevicePropertiesR0600(hipDeviceProp_tR0600* prop, int
   auto f = real_hipGetDevicePropertiesR0600();
   if (!f) return hipErrorNotInitialized;
   hipError_t e = f(prop, dev);
-  if (e == hipSuccess && active() && prop && prop->totalGlobalMem > g.quota) prop->totalGlobalMem = g.quota;
+  if (e == hipSuccess && prop) prop->totalGlobalMem = (size_t)report_total(prop->totalGlobalMem);
   return e;
 }
 
@@ -545,7 +820,7 @@ GS_EXPORT hipError_t hipGetDevicePropertiesR0000(hipDeviceProp_tR0000* prop, int
   auto f = real_hipGetDevicePropertiesR0000();
   if (!f) return hipErrorNotInitialized;
   hipError_t e = f(prop, dev);
-  if (e == hipSuccess && active() && prop && prop->totalGlobalMem > g.quota) prop->totalGlobalMem = g.quota;
+  if (e == hipSuccess && prop) prop->totalGlobalMem = (size_t)report_total(prop->totalGlobalMem);
   return e;
 }
 
@@ -553,19 +828,22 @@ GS_EXPORT hipError_t hipGetDeviceProperties(hipDeviceProp_tR0000* prop, int dev)
   auto f = real_hipGetDeviceProperties();
   if (!f) return hipErrorNotInitialized;
   hipError_t e = f(prop, dev);
-  if (e == hipSuccess && active() && prop && prop->totalGlobalMem > g.quota) prop->totalGlobalMem = g.quota;
+  if (e == hipSuccess && prop) prop->totalGlobalMem = (size_t)report_total(prop->totalGlobalMem);
   return e;
 }
 
 // ---- introspection (tests, metrics) --------------------------------------------------------
 GS_EXPORT int gpushare_shim_stats(uint64_t* used, uint64_t* quota, uint64_t* denied, uint64_t* peak) {
-  std::call_once(g_once, init);
-  if (!g.enabled) return 0;
+  if (!enabled()) return 0;
+  reclaim_dead(g.ledger);  // report live processes' usage only
   if (used) *used = g.ledger->total.load();
-  if (quota) *quota = g.quota;
+  if (quota) *quota = g.quota.load();
   if (denied) *denied = g.ledger->denied.load();
   if (peak) *peak = g.ledger->peak.load();
   return 1;
 }
 
 GS_EXPORT uint64_t gpushare_shim_granule() { return g.granule; }
+
+// 0 = kfd (ioctl boundary), 1 = hip (HIP-API accounting), -1 = disabled / pass-through.
+GS_EXPORT int gpushare_shim_mode() { return enabled() ? g.mode : -1; }

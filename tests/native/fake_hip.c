@@ -1,22 +1,79 @@
-// Stub HIP runtime for CPU-only tests of the quota shim: host malloc stands in for HBM.
-// Exposes the exact entry points libgpushare_hipquota.so interposes (same soname as ROCm).
+// Stub HIP runtime for CPU-only tests of the quota shim (same soname as ROCm's runtime).
+// Like the real one it gets device memory from the KFD: every allocation below is an
+// AMDKFD_IOC_ALLOC_MEMORY_OF_GPU ioctl (VRAM flag) issued through libc's ioctl — which the
+// preloaded shim intercepts — and this library also exports the ioctl that emulates /dev/kfd
+// (the shim forwards to it via RTLD_NEXT), with a 16 GiB "device". Pools (hipMallocAsync)
+// keep freed blocks until trimmed, and fake_runtime_scratch() allocates behind the API's back
+// the way ROCr allocates scratch: the shapes of HBM use the HIP entry points cannot see.
+#define _GNU_SOURCE
+#include <dlfcn.h>
+#include <errno.h>
+#include <stdarg.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
 typedef int hipError_t;
+struct kfd_alloc { uint64_t va, size, handle, mmap_offset; uint32_t gpu_id, flags; };
+struct kfd_free { uint64_t handle; };
+#define KIOC(dir, nr, sz) (((unsigned long)(dir) << 30) | ((unsigned long)(sz) << 16) | ((unsigned long)'K' << 8) | (nr))
+#define KFD_ALLOC KIOC(3, 0x16, sizeof(struct kfd_alloc))
+#define KFD_FREE KIOC(1, 0x17, sizeof(struct kfd_free))
+#define MAXH (1 << 20)
 static size_t g_total = (size_t)16 << 30, g_used = 0;
-// g_used is updated atomically: the threaded driver command allocates from many threads.
-static void* take(size_t n) { char* p = malloc(16); if (!p) return 0; *(size_t*)p = n; return p + 8; }
-hipError_t hipMalloc(void** p, size_t n) {
-  size_t cur = __atomic_load_n(&g_used, __ATOMIC_RELAXED);
-  do { if (cur + n > g_total) return 2; } while (!__atomic_compare_exchange_n(&g_used, &cur, cur + n, 1, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED));
-  *p = take(n); return 0; }
+static uint64_t g_sizes[MAXH];
+static uint64_t g_next = 1;
+
+int ioctl(int fd, unsigned long req, ...) {
+  va_list ap; va_start(ap, req); void* arg = va_arg(ap, void*); va_end(ap);
+  if (req == KFD_ALLOC) {
+    struct kfd_alloc* a = (struct kfd_alloc*)arg;
+    size_t cur = __atomic_load_n(&g_used, __ATOMIC_RELAXED);
+    do { if (cur + a->size > g_total) { errno = ENOMEM; return -1; } }
+    while (!__atomic_compare_exchange_n(&g_used, &cur, cur + a->size, 1, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED));
+    uint64_t h = __atomic_fetch_add(&g_next, 1, __ATOMIC_ACQ_REL) % MAXH;
+    __atomic_store_n(&g_sizes[h], a->size, __ATOMIC_RELEASE);
+    a->handle = h; return 0;
+  }
+  if (req == KFD_FREE) {
+    uint64_t h = ((struct kfd_free*)arg)->handle;
+    __atomic_fetch_sub(&g_used, __atomic_exchange_n(&g_sizes[h], 0, __ATOMIC_ACQ_REL), __ATOMIC_ACQ_REL);
+    return 0;
+  }
+  int (*real)(int, unsigned long, ...) = (int (*)(int, unsigned long, ...))dlsym(RTLD_NEXT, "ioctl");
+  return real(fd, req, arg);
+}
+static int kfd(size_t n, uint64_t* h) {
+  struct kfd_alloc a = {0, n, 0, 0, 1, 1u /* VRAM */};
+  if (ioctl(3, KFD_ALLOC, &a)) return 2;             /* hipErrorOutOfMemory */
+  *h = a.handle; return 0;
+}
+static void kfd_release(uint64_t h) { struct kfd_free f = {h}; ioctl(3, KFD_FREE, &f); }
+#define PTR(h) ((void*)(uintptr_t)((h) << 12))
+#define HANDLE(p) ((uint64_t)(uintptr_t)(p) >> 12)
+hipError_t hipMalloc(void** p, size_t n) { uint64_t h; int e = kfd(n, &h); if (!e) *p = PTR(h); return e; }
 hipError_t hipExtMallocWithFlags(void** p, size_t n, unsigned f) { return hipMalloc(p, n); }
 hipError_t hipMallocManaged(void** p, size_t n, unsigned f) { return hipMalloc(p, n); }
-hipError_t hipMallocAsync(void** p, size_t n, void* s) { return hipMalloc(p, n); }
-hipError_t hipFree(void* p) { if (p) { char* b = (char*)p - 8; __atomic_fetch_sub(&g_used, *(size_t*)b, __ATOMIC_ACQ_REL); free(b); } return 0; }
-hipError_t hipFreeAsync(void* p, void* s) { return hipFree(p); }
+hipError_t hipFree(void* p) { if (p) kfd_release(HANDLE(p)); return 0; }
+/* stream-ordered pool: freed blocks stay cached (and charged) until hipMemPoolTrimTo */
+static struct { uint64_t h, n; } g_pool[4096];
+static int g_npool = 0;
+hipError_t hipMallocAsync(void** p, size_t n, void* s) {
+  for (int i = 0; i < g_npool; ++i) if (g_pool[i].n >= n) { *p = PTR(g_pool[i].h); g_pool[i] = g_pool[--g_npool]; return 0; }
+  return hipMalloc(p, n);
+}
+hipError_t hipFreeAsync(void* p, void* s) {
+  if (!p) return 0;
+  if (g_npool < 4096) { g_pool[g_npool].h = HANDLE(p); g_pool[g_npool].n = g_sizes[HANDLE(p)]; g_npool++; return 0; }
+  return hipFree(p);
+}
+hipError_t hipMemPoolTrimTo(void* pool, size_t keep) {
+  size_t cached = 0; for (int i = 0; i < g_npool; ++i) cached += g_pool[i].n;
+  while (g_npool && cached > keep) { --g_npool; cached -= g_pool[g_npool].n; kfd_release(g_pool[g_npool].h); }
+  return 0;
+}
 hipError_t hipMemGetInfo(size_t* f, size_t* t) { *f = g_total - __atomic_load_n(&g_used, __ATOMIC_ACQUIRE); *t = g_total; return 0; }
 hipError_t hipDeviceTotalMem(size_t* b, int d) { *b = g_total; return 0; }
-hipError_t hipMemCreate(uint64_t* h, size_t n, const void* prop, unsigned long long fl) { void* p; int e = hipMalloc(&p, n); *h = (uint64_t)p; return e; }
-hipError_t hipMemRelease(uint64_t h) { return hipFree((void*)h); }
+hipError_t hipMemCreate(uint64_t* h, size_t n, const void* prop, unsigned long long fl) { return kfd(n, h); }
+hipError_t hipMemRelease(uint64_t h) { kfd_release(h); return 0; }
+/* what ROCr does for a scratch-heavy dispatch: VRAM taken inside the runtime, no HIP call */
+int fake_runtime_scratch(size_t n) { uint64_t h; return kfd(n, &h); }

@@ -7,12 +7,13 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/wait.h>
 #include <unistd.h>
 typedef int hipError_t;
 hipError_t hipMalloc(void**, size_t); hipError_t hipFree(void*);
 hipError_t hipMemGetInfo(size_t*, size_t*); hipError_t hipMallocAsync(void**, size_t, void*);
 hipError_t hipFreeAsync(void*, void*); hipError_t hipMemCreate(uint64_t*, size_t, const void*, unsigned long long);
-hipError_t hipMemRelease(uint64_t);
+hipError_t hipMemRelease(uint64_t); hipError_t hipMemPoolTrimTo(void*, size_t); int fake_runtime_scratch(size_t);
 // "threads N ITERS SIZE": N threads each alloc+free SIZE bytes ITERS times (quota contention)
 struct targ { int iters; size_t n; int ok, denied; };
 static void* worker(void* v) {
@@ -33,6 +34,21 @@ int main(int argc, char** argv) {
       printf("{\"op\":\"async\",\"n\":%zu,\"err\":%d,\"idx\":%d}\n", n, e, e ? -1 : np); if (!e) ptrs[np++] = p; }
     else if (!strcmp(argv[i], "vmm")) { size_t n = strtoull(argv[++i], 0, 10); uint64_t h = 0; int e = hipMemCreate(&h, n, 0, 0);
       printf("{\"op\":\"vmm\",\"n\":%zu,\"err\":%d}\n", n, e); if (!e) hipMemRelease(h); }
+    else if (!strcmp(argv[i], "freeasync")) { int k = atoi(argv[++i]); int e = hipFreeAsync(ptrs[k], 0); ptrs[k] = 0;
+      printf("{\"op\":\"freeasync\",\"idx\":%d,\"err\":%d}\n", k, e); }
+    else if (!strcmp(argv[i], "trim")) { int e = hipMemPoolTrimTo(0, 0); printf("{\"op\":\"trim\",\"err\":%d}\n", e); }
+    else if (!strcmp(argv[i], "scratch")) { size_t n = strtoull(argv[++i], 0, 10); int e = fake_runtime_scratch(n);
+      printf("{\"op\":\"scratch\",\"n\":%zu,\"err\":%d}\n", n, e); }
+    else if (!strcmp(argv[i], "mode")) { int (*f)(void) = (int (*)(void))dlsym(RTLD_DEFAULT, "gpushare_shim_mode");
+      printf("{\"op\":\"mode\",\"mode\":%d}\n", f ? f() : -2); }
+    else if (!strcmp(argv[i], "fork")) { fflush(stdout); pid_t c = fork();
+      if (c == 0) { size_t n = strtoull(argv[i + 1], 0, 10); void* p = 0; int e = hipMalloc(&p, n);
+        uint64_t u = 0, q = 0, d = 0, pk = 0; stats_fn f = (stats_fn)dlsym(RTLD_DEFAULT, "gpushare_shim_stats");
+        if (f) f(&u, &q, &d, &pk); int fe = 0; for (int k = 0; k < np; ++k) if (ptrs[k]) fe |= hipFree(ptrs[k]);
+        uint64_t u2 = 0; if (f) f(&u2, &q, &d, &pk);
+        printf("{\"op\":\"child\",\"err\":%d,\"used\":%llu,\"used_after_parent_frees\":%llu}\n", e,
+               (unsigned long long)u, (unsigned long long)u2); fflush(stdout); _exit(0); }
+      int st = 0; waitpid(c, &st, 0); ++i; printf("{\"op\":\"fork\",\"status\":%d}\n", st); }
     else if (!strcmp(argv[i], "free")) { int k = atoi(argv[++i]); int e = hipFree(ptrs[k]); ptrs[k] = 0;
       printf("{\"op\":\"free\",\"idx\":%d,\"err\":%d}\n", k, e); }
     else if (!strcmp(argv[i], "freeall")) { for (int k = 0; k < np; ++k) if (ptrs[k]) hipFree(ptrs[k]); np = 0; printf("{\"op\":\"freeall\"}\n"); }

@@ -306,6 +306,7 @@ def test_shim_injection_and_cgpu_disable():
     r = al.allocate(req(2)).container_responses[0]
     assert r.envs[const.ENV_LD_PRELOAD] == "/usr/local/gpushare/libgpushare_hipquota.so"
     assert r.envs[const.ENV_SHIM_LEDGER].startswith("/gpushare-uida-")
+    assert r.envs[const.ENV_SHIM_QUOTA_BYTES] == str((4 << 30) * 2 // 4)      # 2 of 4 GiB units
     assert r.mounts[0].host_path == "/opt/gpushare/lib" and r.mounts[0].read_only
     al, _, _ = make([mkpod("a", 2, 0, 1)], shim=shim, disable_cgpu=True)
     r = al.allocate(req(2)).container_responses[0]

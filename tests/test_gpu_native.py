@@ -139,14 +139,50 @@ def test_granule_matches_hardware():
         assert delta == (sz + g - 1) // g * g, (sz, delta)
 
 
-def test_shim_charge_equals_device_consumption():
-    """tools/shim_granule_probe.py: for sizes around the granule, the shim's ledger charge equals
-    the HBM the real runtime consumed, and an over-quota request is refused by the shim
-    (evidence with the rocprofv3 memory-allocation trace: profiles/shim_granule_rocprof.md)."""
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    r = subprocess.run([sys.executable, os.path.join(root, "tools", "shim_granule_probe.py")], capture_output=True,
-                       text=True, timeout=300)
-    out = json.loads(r.stdout)
-    assert r.returncode == 0 and out["consistent"], out
-    assert out["over_quota"]["rc"] == 2 and out["over_quota"]["denied"] == 1
-    assert out["container_view"]["total"] == out["quota"]
+def _probe(args, **env):
+    """native/probes/shim_probe.hip under the shim (LD_PRELOAD, like a container process)."""
+    from aliyun_gpushare_device_plugin_amd.utils.native import ensure_built
+    exe = os.path.join(os.path.dirname(ensure_built("hipshim")), "shim_probe")
+    e = dict(os.environ, LD_PRELOAD=ensure_built("hipshim"), GPUSHARE_SHIM_LOG="1")
+    e.update({k: str(v) for k, v in env.items()})
+    r = subprocess.run([exe, *map(str, args)], env=e, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")], r.stderr
+
+
+GIB, MIB = 1 << 30, 1 << 20
+
+
+def test_shim_kfd_charge_equals_device_consumption():
+    """At the KFD boundary the charge is the HBM the runtime takes: equal to the device's own
+    accounting for every allocation of a 2 MiB fragment or more (sub-fragment buffers share a
+    fragment the ledger already holds, so their charge is never above the device's)."""
+    out, err = _probe(["granule", "smalls", 100, 4096, "smalls", 20, 3 * MIB], GPUSHARE_QUOTA_BYTES=64 * GIB)
+    assert "mode kfd" in err
+    for row in out:
+        if row.get("requested", row.get("size", 0)) >= 2 * MIB - 1:
+            assert row["shim_charge"] == row["device_bytes"], row
+        else:
+            assert row["shim_charge"] <= row["device_bytes"] <= 2 * MIB, row
+
+
+def test_shim_kfd_charges_pool_retention_and_scratch():
+    """What the HIP-level hooks could not see (round-1 review): a stream-ordered pool's block
+    stays charged until the pool trims, and a scratch-heavy kernel's private-segment buffer —
+    allocated inside the runtime, no HIP allocation call — is charged."""
+    out, _ = _probe(["pool", GIB, "scratch", 4], GPUSHARE_QUOTA_BYTES=64 * GIB)
+    pool, scratch = out
+    assert pool["rc"] == [0, 0, 0, 0]
+    assert pool["after_alloc"] - pool["used_before"] >= GIB
+    assert pool["after_trim"] <= pool["after_alloc"] - GIB
+    assert scratch["rc"] == [0, 0]
+    assert scratch["after_launch"] - scratch["used_before"] >= GIB         # ~2 GiB of scratch on 256 CUs
+    assert scratch["device_delta"] > 0
+
+
+def test_shim_kfd_denial_is_clean():
+    """Over quota the KFD allocation fails with ENOMEM, as on a full GPU: hipMalloc returns
+    hipErrorOutOfMemory and the process keeps working within its quota."""
+    out, _ = _probe(["alloc", 256 * MIB, "alloc", GIB, "alloc", 256 * MIB], GPUSHARE_QUOTA_BYTES=768 * MIB)
+    assert [o["rc"] for o in out] == [0, 2, 0]
+    assert out[1]["denied"] >= 1 and out[2]["used"] <= 768 * MIB

@@ -1,9 +1,10 @@
-"""CPU tests of the HIP quota shim against a stub HIP runtime (tests/native/fake_hip.c).
+"""CPU tests of the quota shim against a stub HIP runtime (tests/native/fake_hip.c).
 
-The stub has the same soname as ROCm's runtime (libamdhip64.so.7) and a 16 GiB "device";
-the driver program is an ordinary HIP client linked against it, run with the shim in
-LD_PRELOAD — exactly how a container process sees it. Real-hardware coverage of the same
-paths lives in tests/test_gpu_quota.py (marked gpu).
+The stub has the same soname as ROCm's runtime (libamdhip64.so.7) and a 16 GiB "device" it
+allocates from through emulated KFD ioctls, like ROCr does; the driver program is an ordinary
+HIP client linked against it, run with the shim in LD_PRELOAD — exactly how a container
+process sees it. The default mode charges at the KFD ioctl; GPUSHARE_SHIM_MODE=hip charges at
+the HIP API. Real-hardware coverage of the same paths: tests/test_gpu_native.py (marked gpu).
 """
 import json
 import os
@@ -29,6 +30,17 @@ def stub(tmp_path_factory):
     return d, drv
 
 
+@pytest.fixture(scope="module")
+def kfd_root(tmp_path_factory):
+    """A KFD topology with one GPU (gpu_id 1) of 16 GiB, for quotas derived from units."""
+    r = tmp_path_factory.mktemp("kfdroot")
+    n = r / "sys/class/kfd/kfd/topology/nodes/1"
+    (n / "mem_banks/0").mkdir(parents=True)
+    (n / "gpu_id").write_text("1\n")
+    (n / "mem_banks/0/properties").write_text(f"heap_type 1\nsize_in_bytes {16 * GIB}\n")
+    return str(r)
+
+
 def run(stub, shim, args, **env):
     d, drv = stub
     e = dict(os.environ)
@@ -49,10 +61,11 @@ def cleanup(name):
         pass
 
 
-def test_quota_from_container_share(stub, native_shim):
+@pytest.mark.parametrize("mode", ["kfd", "hip"])
+def test_quota_from_container_share(stub, native_shim, mode):
     # 4 of 16 units of a 16 GiB device -> 4 GiB quota
     out, _ = run(stub, native_shim, ["info", "alloc", 3 * GIB, "alloc", 2 * GIB, "info"],
-                 ALIYUN_COM_GPU_MEM_CONTAINER=4, ALIYUN_COM_GPU_MEM_DEV=16)
+                 ALIYUN_COM_GPU_MEM_CONTAINER=4, ALIYUN_COM_GPU_MEM_DEV=16, GPUSHARE_SHIM_MODE=mode)
     assert out[0]["total"] == 4 * GIB and out[0]["free"] == 4 * GIB
     assert out[1]["err"] == 0
     assert out[2]["err"] == 2                    # hipErrorOutOfMemory: 3 + 2 > 4
@@ -66,21 +79,88 @@ def test_free_releases_charge(stub, native_shim):
     assert out[3]["free"] == 1 * GIB
 
 
-def test_cdna4_granule_rounding(stub, native_shim):
-    # 2 MiB allocation granule: a 1-byte hipMalloc costs 2 MiB, 2 MiB + 1 costs 4 MiB
-    out, _ = run(stub, native_shim, ["alloc", 1, "info", "alloc", 2 * MIB + 1, "info"],
-                 GPUSHARE_QUOTA_BYTES=64 * MIB)
-    assert out[1]["free"] == 62 * MIB
-    assert out[3]["free"] == 58 * MIB
+def test_hip_mode_cdna4_granule_rounding(stub, native_shim):
+    # HIP-API mode: 2 MiB allocation granule, a 1-byte hipMalloc costs 2 MiB, 2 MiB + 1 costs 4 MiB
+    out, _ = run(stub, native_shim, ["mode", "alloc", 1, "info", "alloc", 2 * MIB + 1, "info"],
+                 GPUSHARE_QUOTA_BYTES=64 * MIB, GPUSHARE_SHIM_MODE="hip")
+    assert out[0]["mode"] == 1
+    assert out[2]["free"] == 62 * MIB
+    assert out[4]["free"] == 58 * MIB
     out, _ = run(stub, native_shim, ["alloc", 1, "info"], GPUSHARE_QUOTA_BYTES=64 * MIB,
-                 GPUSHARE_ALLOC_GRANULE=4096)
+                 GPUSHARE_ALLOC_GRANULE=4096, GPUSHARE_SHIM_MODE="hip")
     assert out[1]["free"] == 64 * MIB - 4096
 
 
-def test_async_and_vmm_paths_are_charged(stub, native_shim):
+@pytest.mark.parametrize("mode", ["kfd", "hip"])
+def test_async_and_vmm_paths_are_charged(stub, native_shim, mode):
     out, _ = run(stub, native_shim, ["async", 3 * GIB, "async", 2 * GIB, "vmm", 2 * GIB, "vmm", GIB],
-                 GPUSHARE_QUOTA_BYTES=4 * GIB)
+                 GPUSHARE_QUOTA_BYTES=4 * GIB, GPUSHARE_SHIM_MODE=mode)
     assert [o["err"] for o in out] == [0, 2, 2, 0]
+
+
+def test_kfd_mode_is_default_and_charges_the_ioctl(stub, native_shim):
+    out, _ = run(stub, native_shim, ["mode", "alloc", 1, "stats"], GPUSHARE_QUOTA_BYTES=64 * MIB)
+    assert out[0]["mode"] == 0
+    assert out[2]["used"] == 1          # the KFD allocation's size (the runtime rounds, not the shim)
+
+
+def test_pool_retention_is_charged_until_trim(stub, native_shim):
+    """hipMallocAsync pools keep freed blocks: HIP-level accounting forgot them at hipFreeAsync
+    (round-1 review); at the KFD boundary they stay charged until the pool trims."""
+    args = ["async", 3 * GIB, "freeasync", 0, "stats", "alloc", 2 * GIB, "trim", "stats", "alloc", 2 * GIB]
+    out, _ = run(stub, native_shim, args, GPUSHARE_QUOTA_BYTES=4 * GIB)
+    assert out[2]["used"] == 3 * GIB          # freed to the pool, still resident
+    assert out[3]["err"] == 2                 # so 2 GiB more does not fit
+    assert out[5]["used"] == 0 and out[6]["err"] == 0
+    # the HIP-level mode under-counts exactly this case
+    out, _ = run(stub, native_shim, args, GPUSHARE_QUOTA_BYTES=4 * GIB, GPUSHARE_SHIM_MODE="hip")
+    assert out[2]["used"] == 0 and out[3]["err"] == 0
+
+
+def test_runtime_internal_allocations_are_charged(stub, native_shim):
+    """Scratch / code objects / staging: VRAM the runtime takes with no HIP allocation call."""
+    out, _ = run(stub, native_shim, ["scratch", 3 * GIB, "alloc", 2 * GIB, "scratch", 2 * GIB, "stats"],
+                 GPUSHARE_QUOTA_BYTES=4 * GIB)
+    assert [o["err"] for o in out[:3]] == [0, 2, 2]
+    assert out[3]["used"] == 3 * GIB and out[3]["denied"] == 2
+
+
+def test_quota_from_units_and_kfd_topology(stub, native_shim, kfd_root):
+    # no GPUSHARE_QUOTA_BYTES: 4 of 16 units of the GPU KFD reports (16 GiB) -> 4 GiB, resolved
+    # at the first allocation (inside the runtime, before any hipMemGetInfo)
+    out, _ = run(stub, native_shim, ["alloc", 3 * GIB, "alloc", 2 * GIB, "info"],
+                 ALIYUN_COM_GPU_MEM_CONTAINER=4, ALIYUN_COM_GPU_MEM_DEV=16, GPUSHARE_KFD_SYSFS=kfd_root)
+    assert [o["err"] for o in out[:2]] == [0, 2]
+    assert out[2]["total"] == 4 * GIB and out[2]["free"] == 1 * GIB
+
+
+def test_forked_child_starts_with_empty_table(stub, native_shim):
+    """Round-1 review: the child inherited the parent's pointer map, so freeing an inherited
+    pointer uncharged the child's slot (underflow) and the shared total."""
+    name = ledger()
+    try:
+        out, r = run(stub, native_shim, ["alloc", GIB, "fork", 2 * GIB, "stats"], GPUSHARE_LEDGER=name,
+                     GPUSHARE_QUOTA_BYTES=4 * GIB)
+        child = next(o for o in out if o["op"] == "child")
+        assert child["err"] == 0 and child["used"] == 3 * GIB            # parent's 1 + child's 2 (shared ledger)
+        assert child["used_after_parent_frees"] == 3 * GIB             # inherited pointers: not the child's to uncharge
+        st = [o for o in out if o["op"] == "stats"][-1]
+        assert st["used"] == GIB                                         # child exited: its slot returned
+    finally:
+        cleanup(name)
+
+
+def test_shim_links_no_cxx_runtime_and_old_glibc(native_shim):
+    """Round-1 review: the shim is preloaded into arbitrary tenant images — no libstdc++ /
+    libgcc_s dependency, and glibc symbol versions no newer than 2.17 (CentOS 7 baseline)."""
+    dyn = subprocess.run(["readelf", "-d", native_shim], capture_output=True, text=True, check=True).stdout
+    needed = {ln.split("[")[1].rstrip("]") for ln in dyn.splitlines() if "(NEEDED)" in ln}
+    assert not {n for n in needed if n.startswith(("libstdc++", "libgcc_s"))}, needed
+    syms = subprocess.run(["objdump", "-T", native_shim], capture_output=True, text=True, check=True).stdout
+    import re
+    vers = {tuple(int(x) for x in v.split(".")) for v in re.findall(r"GLIBC_([0-9.]+)\)", syms)}
+    assert max(vers) <= (2, 17), sorted(vers)[-3:]
+    assert "GLIBCXX" not in syms and "CXXABI" not in syms
 
 
 def test_cgpu_disable_passes_through(stub, native_shim):
