@@ -1,0 +1,122 @@
+"""A pod's container process for the bench and the demos: one OS process per pod, started the
+way the container runtime starts it — with the Allocate response's env and the quota shim in
+``LD_PRELOAD`` — running bf16 MFMA GEMM traffic inside its HBM quota.
+
+Lifecycle (JSON lines on stdin/stdout):
+
+* **standby** — the interpreter is up and torch is imported, but nothing has touched the GPU
+  (the analogue of a container whose image is pulled and whose process is created). Prints
+  ``{"event": "standby"}``.
+* ``{"cmd": "start", "env": {...}, "gemm": 4096, "burst": 8, "fill": 0.85}`` — the pod was
+  admitted: the Allocate env (quota, ledger, visible GPU) is applied *before* the HIP runtime
+  initialises, so the shim (preloaded since exec, initialised lazily at the first KFD ioctl)
+  enforces this pod's quota. The worker reads its quota back through ``hipMemGetInfo``, holds
+  ``fill`` of it (the pod's resident model state) plus a GEMM working set, runs one GEMM and
+  prints ``{"event": "ready", "init_ms": ..., "quota": ..., ...}``.
+* traffic — bursts of ``burst`` GEMMs on the hand-written gfx950 kernel until told to stop;
+  ``{"cmd": "stats"}`` answers ``{"event": "stats", "gemms": n, "t": ...}`` between bursts.
+* ``{"cmd": "stop"}`` — frees everything (its HBM is back on the device when ``done`` is
+  printed, before the process exits), prints ``{"event": "done", ...}`` and exits 0.
+
+The reference's demo pod is ``cheyang/gpu-player:v2`` (``demo/binpack-1/binpack-1.yaml:39``);
+``player_main.py`` is the long-running container entry point, this is its benchable form.
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+import queue
+import sys
+import threading
+import time
+
+
+def _send(obj) -> None:
+    sys.stdout.write(json.dumps(obj) + "\n")
+    sys.stdout.flush()
+
+
+def _shim_stats() -> dict | None:
+    try:
+        f = ctypes.CDLL(None).gpushare_shim_stats
+    except AttributeError:
+        return None
+    f.argtypes = [ctypes.POINTER(ctypes.c_uint64)] * 4
+    vals = [ctypes.c_uint64() for _ in range(4)]
+    if not f(*(ctypes.byref(v) for v in vals)):
+        return None
+    return dict(zip(("used", "quota", "denied", "peak"), (v.value for v in vals)))
+
+
+def main() -> int:
+    import torch  # noqa: F401 - imported in standby: the expensive part of a process start
+
+    _send({"event": "standby", "pid": os.getpid()})
+    line = sys.stdin.readline()
+    if not line:
+        return 0
+    cmd = json.loads(line)
+    if cmd.get("cmd") != "start":
+        return 0
+    os.environ.update({k: str(v) for k, v in (cmd.get("env") or {}).items()})
+    g = int(cmd.get("gemm", 4096))
+    burst = int(cmd.get("burst", 8))
+    fill = float(cmd.get("fill", 0.0))
+
+    t0 = time.perf_counter()
+    torch.cuda.init()
+    dev = torch.device("cuda", 0)
+    free, quota = torch.cuda.mem_get_info(dev)                 # = the pod's quota under the shim
+    from .gemm_player import GemmPlayer
+
+    work = 3 * g * g * 2
+    hold_bytes = max(0, int(quota * fill) - work)
+    hold = torch.empty(hold_bytes // 2, dtype=torch.bfloat16, device=dev) if hold_bytes else None
+    player = GemmPlayer(work, dev, g, g, g, touch_fraction=1.0, seed=os.getpid() & 0xffff)
+    player.run(1)
+    player.synchronize()
+    init_ms = (time.perf_counter() - t0) * 1e3
+    _send({"event": "ready", "init_ms": round(init_ms, 3), "quota": quota, "free_at_start": free,
+           "held": hold_bytes + work, "shim": _shim_stats()})
+
+    ctl: "queue.Queue" = queue.Queue()
+
+    def reader():
+        for ln in sys.stdin:
+            try:
+                ctl.put(json.loads(ln))
+            except ValueError:
+                continue
+        ctl.put({"cmd": "stop"})                                # parent went away
+
+    threading.Thread(target=reader, daemon=True).start()
+    gemms = 1
+    t_start = time.time()
+    while True:
+        try:
+            c = ctl.get_nowait()
+        except queue.Empty:
+            c = None
+        if c is not None:
+            if c.get("cmd") == "stats":
+                _send({"event": "stats", "gemms": gemms, "t": time.time()})
+            elif c.get("cmd") == "stop":
+                break
+            continue
+        player.run(burst)
+        player.synchronize()
+        gemms += burst
+    player.release()
+    st = _shim_stats()
+    del hold, player
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()      # HBM back to the device now, not at process exit
+    after = _shim_stats()
+    _send({"event": "done", "gemms": gemms, "t": time.time(), "seconds": time.time() - t_start, "shim": st,
+           "used_after_release": (after or {}).get("used")})
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

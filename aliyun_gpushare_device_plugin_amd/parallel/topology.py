@@ -70,3 +70,57 @@ def best_group(topo: dict | None, free: list[int], size: int, request: int,
         if best_key is None or key < best_key:
             best, best_key = list(combo), key
     return best
+
+
+def bench_report(rank: int, world: int, use_gpu: bool, topo: dict | None, device=None, mib: int = 256,
+                 iters: int = 10) -> dict | None:
+    """Multi-GPU bench section (collective: every rank calls it). Rank 0 brings the topology
+    the plugin exported from SMI; the TP pair a topology-aware extender would choose for a
+    2-GPU pod group (``best_group``) runs an RCCL all-reduce (``torch.distributed`` backend
+    ``nccl`` = RCCL) over its link and reports bus bandwidth — one xGMI hop is ≈ link speed,
+    a PCIe-routed pair far lower. Returns the report on rank 0, None elsewhere."""
+    import time
+
+    import torch
+    import torch.distributed as dist
+
+    pair = None
+    if rank == 0:
+        n = len((topo or {}).get("link_type") or [])
+        pair = best_group(topo, [1] * n, 2, 1) if n >= 2 else None
+        pair = pair or [0, 1]
+    box = [pair]
+    dist.broadcast_object_list(box, src=0)
+    pair = box[0]
+    grp = dist.new_group(pair)
+    busbw = None
+    if rank in pair:
+        if use_gpu:
+            buf = torch.ones(mib * (1 << 20) // 2, dtype=torch.bfloat16, device=device)
+        else:
+            buf = torch.ones(1 << 16, dtype=torch.float32)
+        for _ in range(3):
+            dist.all_reduce(buf, group=grp)
+        if use_gpu:
+            torch.cuda.synchronize()
+        dist.barrier(group=grp)
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            dist.all_reduce(buf, group=grp)
+        if use_gpu:
+            torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / iters
+        size = buf.numel() * buf.element_size()
+        busbw = {"bytes": size, "ms": round(dt * 1e3, 3), "busbw_GBps": round(size * 2 * (len(pair) - 1) / len(pair)
+                                                                              / dt / 1e9, 2)}
+    out = [None] * world
+    dist.all_gather_object(out, busbw)
+    dist.destroy_process_group(grp)
+    if rank != 0:
+        return None
+    a, b = pair
+    rep = {"tp_pair": pair, "tp_pair_allreduce": out[a], "backend": dist.get_backend()}
+    if topo:
+        rep.update(hive_id=topo.get("hive_id"), link_type=topo.get("link_type"), hops=topo.get("hops"),
+                   pair_link=topo["link_type"][a][b], pair_hops=topo["hops"][a][b])
+    return rep

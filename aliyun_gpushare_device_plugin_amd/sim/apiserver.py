@@ -454,7 +454,9 @@ class FakeAPIServer:
                         token = ln[21:].strip().decode("latin-1")
                 body = await reader.readexactly(n) if n else b""
                 if self.latency_s > 0:
-                    await asyncio.sleep(self.latency_s)
+                    # injected network RTT: a thread sleep is accurate to ~0.1 ms, where the event
+                    # loop's own timers round up to epoll's 1 ms granularity (+~1 ms per request)
+                    await asyncio.get_running_loop().run_in_executor(None, time.sleep, self.latency_s)
                 valid = self.store.valid_tokens
                 if valid is not None and token not in valid:
                     self.store.requests["401"] += 1

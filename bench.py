@@ -5,18 +5,29 @@ Metric (BASELINE.json): "bin-packed pods + HBM-GiB/node; Allocate p50 latency at
 
 Scenario (one node with N = --gpus MI355X, one rank per GPU, rank 0 also hosts the control plane):
   * control plane = the real plugin (``gpushare-device-plugin`` in its own process, devices from
-    librocm_smi/sysfs), a fake kube-apiserver process, the extender bin-packer and the fake kubelet
-    (gRPC over UDS) — the same path pods take in production (sim/cluster.py);
+    librocm_smi/sysfs, quota shim injection, ledger dir, journal), a fake kube-apiserver, the
+    extender bin-packer and the fake kubelet (gRPC over UDS) — the path pods take in production
+    (sim/cluster.py);
+  * every admitted pod becomes its own OS process (models/pod_worker.py), started with the
+    Allocate response's env (quota, ledger, ROCR_VISIBLE_DEVICES) and the quota shim in
+    LD_PRELOAD, exactly as the container runtime would start it; it holds 85 % of its quota
+    (resident model state) and runs bf16 MFMA GEMM traffic (hand-written gfx950 kernel) until
+    retired;
   * warm-up fills every GPU with 4 pods of mixed size 8-128 GiB summing to 288 GiB (BASELINE
-    config 3: 32 pods on 8 GPUs);
-  * each timed step = one churn wave under real traffic: every resident pod launches a burst of
-    bf16 MFMA GEMMs (hand-written gfx950 kernel, 4096^3, operands inside the pod's HBM share, one
-    HIP stream per pod), and while the GPUs run, rank 0 retires the oldest pod on every GPU and
-    admits a replacement of the same size through delete -> create -> extender bind -> kubelet
-    Allocate -> Running. Per-GPU work is fixed (1 admission + 4 bursts), so scaling is weak.
-``value`` = pod admissions per second for the whole node (higher is better). Also reported: Allocate
-p50/p99 (kubelet-side gRPC round trip), pods and GiB bin-packed per node, advertised GiB per node and
-the aggregate GEMM TFLOP/s delivered to the pods.
+    config 3: 32 pods on 8 GPUs) and runs W untimed churn waves;
+  * each timed step = one churn wave on every GPU while the other pods keep the GPU busy: the
+    oldest pod's process is stopped (its HBM returns), the pod is deleted, a same-size
+    replacement is created, bin-packed by the extender, admitted by the kubelet through the
+    plugin's Allocate, and its process starts under the shim and runs its first GEMM ("pod
+    ready"). The interpreter of the replacement is pre-started (standby: torch imported, GPU
+    untouched — an image already pulled); HIP init, quota, HBM allocation and the first GEMM are
+    inside the timed step. Per-GPU work is fixed (1 admission per step), so scaling is weak.
+``value`` = pods admitted-to-ready per second for the whole node (higher is better). Also in the
+line: Allocate p50/p99 (kubelet-side gRPC round trip) and the plugin's server-side p50/p99; pod
+ready p50; pods and GiB bin-packed per node; the aggregate GEMM TFLOP/s the pod processes
+delivered during the timed window; quota denials; and a control-plane A/B at injected apiserver
+RTTs of 1 and 5 ms: this build's default (watch cache + write-behind patch) against the
+reference's cost model (LIST per Allocate + synchronous PATCH, ``allocate.go:63-152``).
 
 python bench.py --gpus N --steps K --warmup W   (N>1: launched by torch.distributed.run)
 """
@@ -25,7 +36,10 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import queue
+import subprocess
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -34,6 +48,7 @@ sys.path.insert(0, ROOT)
 METRIC = "bin-packed pods + HBM-GiB/node; Allocate p50 latency at 1/2/4/8 MI355X"
 # Per-GPU pod sizes (GiB), each pattern sums to one MI355X (288 GiB); GPU g uses pattern g % 4.
 PATTERNS = [[128, 64, 64, 32], [96, 96, 64, 32], [128, 96, 56, 8], [64, 64, 96, 64]]
+NATIVE = os.path.join(ROOT, "aliyun_gpushare_device_plugin_amd", "_native")
 
 
 def parse():
@@ -41,14 +56,16 @@ def parse():
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--burst", type=int, default=40, help="GEMMs per resident pod per step")
+    ap.add_argument("--burst", type=int, default=8, help="GEMMs between a pod process's control checks")
     ap.add_argument("--gemm", type=int, default=4096, help="GEMM M=N=K")
-    ap.add_argument("--burst-mode", default="loop", choices=("loop", "fused"),
-                    help="a pod's burst as one launch per GEMM, or one dispatch of all of them (same FLOPs)")
+    ap.add_argument("--fill", type=float, default=0.85, help="fraction of its quota a pod process holds")
+    ap.add_argument("--standby", type=int, default=2, help="pre-started pod interpreters per GPU")
     ap.add_argument("--no-gpu", action="store_true", help="control plane only (CPU)")
     ap.add_argument("--smi-backend", default=None, help="default: auto on GPU, fake:Nx288G on CPU")
     ap.add_argument("--pod-source", default="watch", choices=("watch", "list", "kubelet"))
     ap.add_argument("--plugin-mode", default="process", choices=("process", "thread"))
+    ap.add_argument("--compare-rtts", default="1,5", help="apiserver RTTs (ms) of the control-plane A/B ('' = off)")
+    ap.add_argument("--compare-pods", type=int, default=24, help="admissions per A/B configuration")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -60,10 +77,29 @@ def pct(xs, q):
     return s[min(len(s) - 1, max(0, int(round(q * (len(s) - 1)))))]
 
 
+def ms(x):
+    return None if x is None else round(x * 1e3, 3)
+
+
+def container_env(resp) -> dict:
+    """The env a container runtime would give the pod's process: the Allocate response's envs
+    with container paths (shim mount, ledger dir mount) mapped back to the host paths the
+    response's mounts name."""
+    env = dict(resp.envs)
+    mounts = sorted(((m.container_path, m.host_path) for m in resp.mounts), key=lambda m: -len(m[0]))
+    for k, v in list(env.items()):
+        for cpath, hpath in mounts:
+            if v == cpath or v.startswith(cpath.rstrip("/") + "/"):
+                env[k] = hpath + v[len(cpath.rstrip("/")):]
+                break
+    return env
+
+
 class ControlPlane:
     """Rank 0's view of the node: fake cluster + the real plugin process."""
 
-    def __init__(self, n_gpus: int, smi_spec: str, pod_source: str, plugin_mode: str):
+    def __init__(self, n_gpus: int, smi_spec: str, pod_source: str, plugin_mode: str, workdir: str,
+                 with_shim: bool):
         from aliyun_gpushare_device_plugin_amd.sim.cluster import SimCluster
 
         self.n = n_gpus
@@ -72,10 +108,15 @@ class ControlPlane:
         with socket.socket() as s:              # a free port for the plugin's metrics endpoint
             s.bind(("127.0.0.1", 0))
             self.metrics_port = s.getsockname()[1]
+        self.ledger_dir = os.path.join(workdir, "ledgers")
+        os.makedirs(self.ledger_dir, exist_ok=True)
         extra = ["--metrics-addr", f"127.0.0.1:{self.metrics_port}"] if plugin_mode == "process" else []
+        extra += ["--ledger-dir", self.ledger_dir, "--journal-path", os.path.join(workdir, "alloc-journal.jsonl")]
+        if with_shim:
+            extra += ["--rocr-visible-devices"]
         self.cluster = SimCluster([("mi355x-node", smi_spec)], plugin_mode=plugin_mode, pod_source=pod_source,
                                   apiserver="process", gpu_indices=list(range(n_gpus)), health_poll_s=5.0,
-                                  extra_plugin_args=extra)
+                                  extra_plugin_args=extra, shim_host_dir=NATIVE if with_shim else None)
         self.cluster.start()
         from aliyun_gpushare_device_plugin_amd import const
         from aliyun_gpushare_device_plugin_amd.cluster import objects as O
@@ -88,8 +129,6 @@ class ControlPlane:
         self.resident: dict[int, list] = {g: [] for g in range(n_gpus)}   # gpu -> [(pod, size)] oldest first
         import concurrent.futures as cf
 
-        import threading
-
         self.pool = cf.ThreadPoolExecutor(max_workers=max(1, n_gpus), thread_name_prefix="churn")
         self._sched_lock = threading.Lock()
         self._kubelet = threading.Condition()
@@ -99,31 +138,40 @@ class ControlPlane:
         self.fail_reasons: list[str] = []
         self.cp_time = 0.0
 
-    def admit(self, size: int):
-        t0 = time.perf_counter()
-        pod, where, adm = self.cluster.run_pod(size)
-        if where is None or adm is None or adm.error:
-            self.failed += 1
-            if where is not None:
-                self.cluster.delete_pod(pod)
-            return None
-        self.alloc_lat.extend(adm.latencies)
-        self.admit_lat.append(time.perf_counter() - t0)
-        gpu = int(dict(adm.responses[0].envs)["ALIYUN_COM_GPU_MEM_IDX"])
-        self.resident[gpu].append((pod, size))
-        return gpu
+    def _record(self, pod, size, adm) -> tuple[int, dict] | None:
+        from aliyun_gpushare_device_plugin_amd.cluster import objects as O
 
-    def fill(self):
+        gpu = int(dict(adm.responses[0].envs)["ALIYUN_COM_GPU_MEM_IDX"])
+        if gpu < 0:
+            return None
+        self.resident[gpu].append((pod, size))
+        return gpu, {"uid": O.uid(pod), "size": size, "env": container_env(adm.responses[0])}
+
+    def fill(self) -> dict:
         """Pods arrive as per-GPU-sized groups (think one StatefulSet per 288 GiB of demand), in
         pattern order. The extender's online best-fit places each group exactly onto one GPU, so
         the node packs 100 %; the same 32 pods in globally size-sorted order strand 56 GiB under
         that policy (31 of 32 placed at N = 8: its tie-break stacks two 128 GiB pods per GPU)."""
+        started: dict[int, list] = {g: [] for g in range(self.n)}
         for g in range(self.n):
             for s in PATTERNS[g % len(PATTERNS)]:
-                self.admit(s)
+                pod, where, adm = self.cluster.run_pod(s)
+                if where is None or adm is None or adm.error:
+                    self.failed += 1
+                    continue
+                rec = self._record(pod, s, adm)
+                if rec:
+                    started[rec[0]].append(rec[1])
+        return started
 
-    def churn(self):
-        """Retire the oldest pod on every GPU and admit a same-size replacement.
+    def retire_plan(self) -> dict:
+        """The oldest pod of every GPU: these processes stop before the wave's admissions."""
+        from aliyun_gpushare_device_plugin_amd.cluster import objects as O
+
+        return {g: O.uid(pods[0][0]) for g, pods in self.resident.items() if pods}
+
+    def churn(self) -> dict:
+        """Delete the retired pods and admit same-size replacements; returns {gpu: [pod record]}.
 
         One pipeline per GPU, as in a real cluster where each replacement is independent:
         delete (controller) -> create -> scheduling cycle (extender decide, stamps the assume
@@ -164,6 +212,7 @@ class ControlPlane:
                     turn["next"] += 1
                     self._kubelet.notify_all()
 
+        started: dict[int, list] = {g: [] for g in range(self.n)}
         for bpod, size, adm, dt in self.pool.map(chain, olds):
             if adm is None or adm.error:
                 self.failed += 1
@@ -171,15 +220,16 @@ class ControlPlane:
                 if bpod is not None:
                     self.cluster.delete_pod(bpod)
                 continue
-            gpu = int(dict(adm.responses[0].envs)["ALIYUN_COM_GPU_MEM_IDX"])
-            if gpu < 0:                                 # soft failure: no candidate matched
+            rec = self._record(bpod, size, adm)
+            if rec is None:                             # soft failure: no candidate matched
                 self.failed += 1
                 self.fail_reasons.append(f"{size}GiB: plugin found no candidate")
                 self.cluster.delete_pod(bpod)
                 continue
             self.alloc_lat.extend(adm.latencies)
             self.admit_lat.append(dt)
-            self.resident[gpu].append((bpod, size))
+            started[rec[0]].append(rec[1])
+        return started
 
     def plugin_latency(self, reset: bool = False) -> dict | None:
         """The plugin's own (server-side) Allocate latency quantiles from its metrics endpoint."""
@@ -196,14 +246,171 @@ class ControlPlane:
                 return e
         return None
 
-    def placement(self) -> dict:
-        from aliyun_gpushare_device_plugin_amd.cluster import objects as O
-
-        return {g: [(O.uid(p), s) for p, s in pods] for g, pods in self.resident.items()}
-
     def stop(self):
         self.pool.shutdown(wait=True)
         self.cluster.stop()
+
+
+def mode_comparison(rtts_ms: list[float], n_pods: int) -> dict:
+    """Control-plane A/B at injected apiserver RTTs: this build's default (watch cache +
+    write-behind ASSIGNED patch) vs the reference's cost model (LIST of the node's Pending pods
+    per Allocate + synchronous PATCH before answering, ``allocate.go:63-152``). Kubelet-side
+    Allocate latency over ``n_pods`` sequential admissions of 8 GiB pods per configuration."""
+    from aliyun_gpushare_device_plugin_amd.sim.cluster import SimCluster
+
+    out = {}
+    for rtt in rtts_ms:
+        for label, src, extra in (("default", "watch", []), ("reference", "list", ["--sync-patch"])):
+            lat, fails = [], 0
+            with SimCluster([("cmp", "fake:1x288G")], plugin_mode="process", pod_source=src,
+                            apiserver_latency_s=rtt / 1e3, extra_plugin_args=extra) as c:
+                req = []                                 # one apiserver round trip, as the plugin sees it
+                for _ in range(10):
+                    t = time.perf_counter()
+                    c.client.get_node("cmp")
+                    req.append(time.perf_counter() - t)
+                for _ in range(n_pods):
+                    pod, where, adm = c.run_pod(8)
+                    if adm is None or adm.error or int(dict(adm.responses[0].envs)["ALIYUN_COM_GPU_MEM_IDX"]) < 0:
+                        fails += 1
+                    else:
+                        lat += adm.latencies
+                    c.delete_pod(pod)
+            key = f"{label}@{rtt:g}ms"
+            # apiserver round trips on the Allocate path: LIST + PATCH (reference), none (default:
+            # watch-cache lookup, PATCH written behind); request_ms = one round trip through the
+            # fake apiserver at this RTT (RTT + the fake's own ~1.5 ms per-request cost)
+            out[key] = {"allocate_p50_ms": ms(pct(lat, 0.5)), "allocate_p99_ms": ms(pct(lat, 0.99)),
+                        "apiserver_round_trips_on_path": 2 if extra else 0, "request_ms": ms(pct(req, 0.5)),
+                        "pod_source": src, "patch": "sync" if extra else "write-behind", "failed": fails}
+    return out
+
+
+class PodFleet:
+    """The pod processes of this rank's GPU, plus one standby process (interpreter up, torch
+    imported, GPU untouched) that becomes the next admitted pod."""
+
+    def __init__(self, local: int, gemm: int, burst: int, fill: float, visible_by_uuid: bool, standby: int = 2):
+        self.local, self.gemm, self.burst, self.fill = local, gemm, burst, fill
+        self.visible_by_uuid = visible_by_uuid
+        self.pods: dict[str, dict] = {}       # uid -> {"proc", "q", "size", "ready"}
+        self.standby: list[dict] = []         # pre-started interpreters, oldest first
+        self.ready_ms: list[float] = []
+        self.retired_gemms = 0
+        self.denied = 0
+        self.held_bytes = 0
+        self.released_residue = 0             # shim-ledger bytes a stopped pod still held after freeing
+        self.release_ms: list[float] = []     # stop -> the device reports the pod's HBM free again
+        self._vram_used = self._vram_reader()
+        for _ in range(max(1, standby)):
+            self._spawn()
+
+    def _vram_reader(self):
+        """amdgpu's own count of used VRAM for this rank's GPU (sysfs), or None."""
+        try:
+            from aliyun_gpushare_device_plugin_amd.device.smi import SMI
+
+            with SMI("auto") as s:
+                minor = s.device(self.local).render_minor if s.count() > self.local else -1
+        except Exception:  # noqa: BLE001
+            return None
+        path = f"/sys/class/drm/renderD{minor}/device/mem_info_vram_used"
+        if minor < 0 or not os.path.exists(path):
+            return None
+
+        def read():
+            with open(path) as f:
+                return int(f.read())
+        return read
+
+    def _spawn(self):
+        env = dict(os.environ, LD_PRELOAD=os.path.join(NATIVE, "libgpushare_hipquota.so"),
+                   PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
+        for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
+                  "TORCHELASTIC_RUN_ID", "GROUP_RANK", "ROLE_RANK"):
+            env.pop(k, None)
+        p = subprocess.Popen([sys.executable, "-m", "aliyun_gpushare_device_plugin_amd.models.pod_worker"], env=env,
+                             stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, bufsize=1)
+        q: "queue.Queue" = queue.Queue()
+
+        def pump():
+            for ln in p.stdout:
+                if ln.startswith("{"):
+                    q.put(json.loads(ln))
+            q.put({"event": "eof"})
+
+        threading.Thread(target=pump, daemon=True).start()
+        self.standby.append({"proc": p, "q": q})
+
+    @staticmethod
+    def _wait(w, event, timeout=120.0):
+        while True:
+            ev = w["q"].get(timeout=timeout)
+            if ev.get("event") == event:
+                return ev
+            if ev.get("event") == "eof":
+                raise RuntimeError(f"pod process {w['proc'].pid} exited while waiting for {event!r}")
+
+    def start(self, rec: dict) -> float:
+        """Hand the oldest standby its pod's env; return the ready latency (seconds)."""
+        w = self.standby.pop(0)
+        self._spawn()                                   # replenish while this one initialises
+        self._wait(w, "standby")
+        env = dict(rec["env"])
+        env.pop("LD_PRELOAD", None)                     # preloaded since exec (same host path)
+        if not self.visible_by_uuid:                    # modelled node (fake SMI): this rank's GPU
+            env.pop("ROCR_VISIBLE_DEVICES", None)
+            env["HIP_VISIBLE_DEVICES"] = str(self.local)
+        t0 = time.perf_counter()
+        w["proc"].stdin.write(json.dumps({"cmd": "start", "env": env, "gemm": self.gemm, "burst": self.burst,
+                                          "fill": self.fill}) + "\n")
+        ev = self._wait(w, "ready")
+        dt = time.perf_counter() - t0
+        w.update(size=rec["size"], ready=ev)
+        self.pods[rec["uid"]] = w
+        self.held_bytes += ev.get("held", 0)
+        self.ready_ms.append(dt)
+        return dt
+
+    def stop(self, uid: str):
+        w = self.pods.pop(uid, None)
+        if w is None:
+            return
+        t0 = time.perf_counter()
+        before = self._vram_used() if self._vram_used else None
+        w["proc"].stdin.write('{"cmd":"stop"}\n')
+        ev = self._wait(w, "done")                      # freed through KFD at this point
+        threading.Thread(target=w["proc"].wait, daemon=True).start()   # reap the exit off the path
+        if before is not None:
+            # amdgpu returns freed VRAM asynchronously (the buffers are cleared first): the
+            # replacement pod is admitted only once the device reports the HBM free again, as
+            # a quota-sum-equals-HBM node needs (bounded wait)
+            target = before - int(0.95 * w["ready"].get("held", 0))
+            deadline = time.perf_counter() + 20.0
+            while self._vram_used() > target and time.perf_counter() < deadline:
+                time.sleep(0.005)
+            self.release_ms.append(time.perf_counter() - t0)
+        self.released_residue = max(self.released_residue, ev.get("used_after_release") or 0)
+        self.retired_gemms += ev["gemms"]
+        self.held_bytes -= w["ready"].get("held", 0)
+        self.denied += ((ev.get("shim") or {}).get("denied") or 0)
+
+    def gemms(self) -> int:
+        """Cumulative GEMMs of every pod this fleet ran (live pods asked between bursts)."""
+        live = list(self.pods.values())
+        for w in live:
+            w["proc"].stdin.write('{"cmd":"stats"}\n')
+        return self.retired_gemms + sum(self._wait(w, "stats")["gemms"] for w in live)
+
+    def close(self):
+        for uid in list(self.pods):
+            self.stop(uid)
+        for w in self.standby:
+            try:
+                w["proc"].stdin.close()
+                w["proc"].wait(30)
+            except Exception:  # noqa: BLE001
+                w["proc"].kill()
 
 
 def main():
@@ -214,6 +421,8 @@ def main():
     n = a.gpus
     if world not in (1, n):
         raise SystemExit(f"WORLD_SIZE={world} but --gpus {n}")
+
+    import tempfile
 
     import torch
     import torch.distributed as dist
@@ -232,6 +441,13 @@ def main():
         dist.broadcast_object_list(box, src=0)
         return box[0]
 
+    def gather(obj):
+        if world == 1:
+            return [obj]
+        out = [None] * world
+        dist.all_gather_object(out, obj)
+        return out
+
     def barrier():
         if world > 1:
             dist.barrier()
@@ -239,90 +455,91 @@ def main():
             torch.cuda.synchronize()
 
     smi = a.smi_backend or ("auto" if use_gpu else f"fake:{n}x288G")
+    visible_by_uuid = use_gpu
     cp = None
     info = None
+    workdir = tempfile.mkdtemp(prefix="gs-bench-", dir="/tmp")
     if rank == 0:
         if use_gpu and smi == "auto":
             from aliyun_gpushare_device_plugin_amd.device.smi import SMI
             with SMI("auto") as s:
                 if s.count() < n:          # fewer visible GPUs than ranks: model the node
                     smi = f"fake:{n}x{s.device(0).vram_total}B"
-        cp = ControlPlane(n, smi, a.pod_source, a.plugin_mode)
-        info = {"units_per_gpu": cp.units_per_gpu, "gpu_count": cp.gpu_count}
+                    visible_by_uuid = False
+        cp = ControlPlane(n, smi, a.pod_source, a.plugin_mode, workdir, with_shim=use_gpu)
+        info = {"units_per_gpu": cp.units_per_gpu, "gpu_count": cp.gpu_count, "by_uuid": visible_by_uuid}
     info = bcast(info)
     units = info["units_per_gpu"]
+    fleet = PodFleet(local, a.gemm, a.burst, a.fill, info["by_uuid"], a.standby) if use_gpu else None
+    topo_report = None
 
-    players: dict[str, object] = {}
-    gemm_flops = 0.0
+    def launch(started: dict) -> float:
+        """Start this rank's newly admitted pods; returns the slowest ready latency."""
+        worst = 0.0
+        if fleet is not None:
+            for rec in started.get(local, []):
+                worst = max(worst, fleet.start(rec))
+        return worst
 
-    arena = None
-
-    def sync_players(place):
-        """Make this rank's players match the pods resident on its GPU."""
-        if not use_gpu:
-            return
-        from aliyun_gpushare_device_plugin_amd.models.gemm_player import GemmPlayer, HBMArena
-
-        nonlocal arena
-        if arena is None:
-            arena = HBMArena(dev, units)          # the GPU's shareable HBM, mapped once
-        mine = dict(place.get(local, []))
-        for uid in [u for u in players if u not in mine]:
-            players.pop(uid).release()
-            arena.free(uid)
-        total = torch.cuda.get_device_properties(dev).total_memory
-        for uid, size in mine.items():
-            if uid not in players:
-                players[uid] = GemmPlayer(total * size // units, dev, a.gemm, a.gemm, a.gemm,
-                                          seed=hash(uid) & 0xffff, pool=arena.alloc(uid, size),
-                                          fused_burst=a.burst_mode == "fused")
-
-    def step(timed: bool):
-        nonlocal gemm_flops
-        for p in players.values():                  # traffic first: GPUs busy during admissions
-            p.run(a.burst)
-        if timed:
-            gemm_flops += 2.0 * a.gemm ** 3 * a.burst * len(players)
-        place = None
+    def step():
+        plan = bcast(cp.retire_plan() if rank == 0 else None)
+        if fleet is not None and local in plan:
+            fleet.stop(plan[local])              # HBM returned before the replacement is admitted
+        barrier()
+        started = None
         if rank == 0:
             tc = time.perf_counter()
-            cp.churn()
-            if timed:
-                cp.cp_time += time.perf_counter() - tc
-            place = cp.placement()
-        place = bcast(place)
-        sync_players(place)
-        for p in players.values():
-            p.synchronize()
+            started = cp.churn()
+            cp.cp_time += time.perf_counter() - tc
+        started = bcast(started)
+        launch(started)
 
-    # ---- warm-up: fill the node, then W untimed churn waves ----
-    place = None
-    if rank == 0:
-        cp.fill()
-        place = cp.placement()
-    place = bcast(place)
-    sync_players(place)
+    # ---- warm-up: fill the node, start its pods, then W untimed churn waves ----
+    started = bcast(cp.fill() if rank == 0 else None)
+    launch(started)
+    barrier()
     for _ in range(a.warmup):
-        step(False)
+        step()
     if rank == 0:
         cp.alloc_lat.clear()
         cp.admit_lat.clear()
+        cp.cp_time = 0.0
         cp.failed = 0
         cp.fail_reasons.clear()
         cp.plugin_latency(reset=True)
+    if fleet is not None:
+        fleet.ready_ms.clear()
+        fleet.release_ms.clear()
 
     barrier()
+    g0 = fleet.gemms() if fleet is not None else 0
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        step(True)
+        step()
     barrier()
     elapsed = time.perf_counter() - t0
+    g1 = fleet.gemms() if fleet is not None else 0
+    gemm_flops = 2.0 * a.gemm ** 3 * (g1 - g0)
     if world > 1:
         t = torch.tensor([elapsed, gemm_flops], dtype=torch.float64, device=dev if use_gpu else "cpu")
         mx = t.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         elapsed, gemm_flops = float(mx[0]), float(t[1])
+    ready = gather(fleet.ready_ms if fleet is not None else [])
+    ready_all = [x for r in ready for x in r]
+    held = gather(fleet.held_bytes if fleet is not None else 0)
+    denied = gather(fleet.denied if fleet is not None else 0)
+    residue = gather(fleet.released_residue if fleet is not None else 0)
+    release = gather(fleet.release_ms if fleet is not None else [])
+    release_all = [x for r in release for x in r]
+
+    if world > 1:
+        from aliyun_gpushare_device_plugin_amd.cluster import nodestatus
+        from aliyun_gpushare_device_plugin_amd.parallel import topology as T
+
+        topo = nodestatus.read_topology(cp.cluster.client.get_node("mi355x-node")) if rank == 0 else None
+        topo_report = T.bench_report(rank, world, use_gpu, topo, dev)
 
     if rank == 0:
         srv = cp.plugin_latency()
@@ -330,10 +547,13 @@ def main():
         gib_node = sum(s for v in cp.resident.values() for _, s in v)
         admissions = a.steps * n - cp.failed
         value = admissions / elapsed
+        cp.stop()
+        modes = mode_comparison([float(x) for x in a.compare_rtts.split(",") if x], a.compare_pods) \
+            if a.compare_rtts else {}
         res = {
             "metric": METRIC,
             "value": round(value, 3),
-            "unit": "pod admissions/s",
+            "unit": "pods admitted-to-ready/s",
             "n_gpus": n,
             "steps": a.steps,
             "warmup": a.warmup,
@@ -342,37 +562,48 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16",
-            "data": "synthetic pod specs (mixed 8-128 GiB), random-init bf16 GEMM operands",
+            "data": "synthetic pod specs (mixed 8-128 GiB), random-init bf16 GEMM operands; one OS process per pod "
+                    "under the quota shim",
             "config": {"model": "gpushare-device-plugin + MFMA GEMM pods (BASELINE config 3 churn)",
                        "global_batch": 4 * n, "seq_len": None, "parallelism": f"node{n}",
-                       "pods_per_gpu": 4, "burst_gemms": a.burst, "burst_mode": a.burst_mode, "gemm_mnk": a.gemm,
-                       "pod_source": a.pod_source, "smi_backend": smi},
-            "allocate_p50_ms": round(pct(cp.alloc_lat, 0.5) * 1e3, 3) if cp.alloc_lat else None,
-            "allocate_p99_ms": round(pct(cp.alloc_lat, 0.99) * 1e3, 3) if cp.alloc_lat else None,
-            "admission_p50_ms": round(pct(cp.admit_lat, 0.5) * 1e3, 3) if cp.admit_lat else None,
-            "plugin_allocate_p50_ms": round(srv["p50"] * 1e3, 3) if srv else None,
-            "plugin_allocate_p99_ms": round(srv["p99"] * 1e3, 3) if srv else None,
+                       "pods_per_gpu": 4, "gemm_mnk": a.gemm, "pod_fill": a.fill, "pod_source": a.pod_source,
+                       "smi_backend": smi, "pod_processes": use_gpu},
+            "allocate_p50_ms": ms(pct(cp.alloc_lat, 0.5)),
+            "allocate_p99_ms": ms(pct(cp.alloc_lat, 0.99)),
+            "plugin_allocate_p50_ms": ms(srv["p50"]) if srv else None,
+            "plugin_allocate_p99_ms": ms(srv["p99"]) if srv else None,
+            "admission_p50_ms": ms(pct(cp.admit_lat, 0.5)),
+            "pod_ready_p50_ms": ms(pct(ready_all, 0.5)),
+            "pod_ready_p99_ms": ms(pct(ready_all, 0.99)),
+            "pod_hbm_release_p50_ms": ms(pct(release_all, 0.5)),
             "control_plane_ms_per_step": round(cp.cp_time / a.steps * 1e3, 3),
+            "allocate_by_mode": modes,
             "pods_per_node": pods_node,
             "hbm_gib_per_node": gib_node,
             "advertised_gib_per_node": units * n,
             "packing_efficiency": round(gib_node / (units * n), 4) if units else None,
+            "hbm_held_by_pods_gib": round(sum(held) / (1 << 30), 1) if use_gpu else None,
+            "quota_denials": sum(denied),
+            "pod_hbm_residue_after_free_mib": round(max(residue) / (1 << 20), 1) if use_gpu else None,
             "failed_admissions": cp.failed,
             "failure_reasons": cp.fail_reasons[:5],
             "gemm_tflops_node": round(gemm_flops / elapsed / 1e12, 1) if use_gpu else None,
         }
+        if topo_report is not None:
+            res["topology"] = topo_report
         line = json.dumps(res)
         print(line, flush=True)
         if a.json_out:
             with open(a.json_out, "w") as f:
                 f.write(line + "\n")
-    for p in list(players.values()):
-        p.release()
-    if rank == 0:
-        cp.stop()
+    if fleet is not None:
+        fleet.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    import shutil
+
+    shutil.rmtree(workdir, ignore_errors=True)
 
 
 if __name__ == "__main__":
