@@ -122,6 +122,7 @@ class Allocator:
         self._slot_pending: dict[str, tuple] = {}  # uid -> (gpu, SlotRun, t): chosen, not yet on the pod
         self._stop = threading.Event()
         self._last_reconcile = time.monotonic()
+        self._last_sweep = 0.0
         self.journal = AllocJournal(self.opts.journal_path, self.opts.journal_ttl_s)
         if self.opts.async_patch:
             import queue
@@ -177,9 +178,11 @@ class Allocator:
     def _candidates(self, fresh: bool) -> list[dict]:
         pods = A.dedupe_by_uid(self.pods.pending_pods(fresh=fresh), self.node)
         now = time.monotonic()
-        for u, t in list(self._assigned.items()):
-            if now - t > self.opts.claim_ttl_s and u not in self._unpatched:
-                del self._assigned[u]
+        if now - self._last_sweep > 1.0:          # amortised: the set holds the last claim_ttl_s of pods
+            self._last_sweep = now
+            for u, t in list(self._assigned.items()):
+                if now - t > self.opts.claim_ttl_s and u not in self._unpatched:
+                    del self._assigned[u]
         if fresh and self._tainted:   # forget a withheld reservation once its pod is gone
             live = {O.uid(p) for p in self.pods.node_pods() if not O.deleting(p)}
             for u in [u for u in self._tainted if u not in live]:
@@ -488,14 +491,14 @@ class Allocator:
         t3 = time.perf_counter()
         if self._patch_q is not None:
             job = _PatchJob(claim.uid, O.namespace(claim.pod), O.name(claim.pod), self._extra_annotations(claim.uid))
-            # journal first: a crash after the reply must not lose the pending PATCH
-            self.journal.pending(job.uid, job.ns, job.name, job.ann)
+            # journal first (answer + pending PATCH, one write): a crash after the reply must
+            # not lose the PATCH
+            self.journal.record_pending(req, claim.uid, resp, job.ns, job.name, job.ann, jkey)
             with self._mu:
                 self._claims.pop(claim.uid, None)
                 self._assigned[claim.uid] = time.monotonic()
                 self._unpatched.add(claim.uid)
             self._patch_q.put(job)
-            self.journal.record(req, claim.uid, resp, jkey)
             hist.observe(time.perf_counter() - t3, phase="patch")
             hist.observe(time.perf_counter() - t0, phase="total")
             self.metrics.allocate_outcomes.inc(outcome="assigned")

@@ -17,9 +17,11 @@ restart or crash:
   its pod stays claimed, so a pod can neither be left ``ASSIGNED=false`` forever nor be
   matched a second time by the next plugin instance.
 
-Writes go through the page cache (``flush`` after each record, no ``fsync``): the journal
-must survive the *process* (kill, crash, OOM, DaemonSet rollout); a node crash takes the
-pods' containers down with it.
+Each record is one ``write(2)`` on an ``O_APPEND`` descriptor (no userspace buffering, no
+``fsync``): the journal must survive the *process* (kill, crash, OOM, DaemonSet rollout); a
+node crash takes the pods' containers down with it. A write-behind answer and its pending
+patch share one record (``{"op": "answer+patch", ...}``), so the journal costs one syscall
+on the Allocate path.
 """
 from __future__ import annotations
 
@@ -50,7 +52,7 @@ class AllocJournal:
         self._pending: collections.OrderedDict[str, dict] = collections.OrderedDict()  # uid -> patch
         self._lock = threading.Lock()
         self._lines = 0
-        self._f = None
+        self._fd = -1
         if path:
             self._load()
 
@@ -66,10 +68,12 @@ class AllocJournal:
             try:
                 e = json.loads(line)
                 op = e.get("op", "answer")
-                if op == "patch":
+                if op in ("patch", "answer+patch"):
                     if now - e["t"] <= self.pending_ttl_s:
-                        self._pending[e["uid"]] = e
-                elif op == "landed":
+                        self._pending[e["uid"]] = {k: e[k] for k in ("uid", "ns", "name", "ann", "t")} | {"op": "patch"}
+                if op == "patch":
+                    continue
+                if op == "landed":
                     self._pending.pop(e["uid"], None)
                 elif now - e["t"] <= self.ttl_s:
                     self._mem[e["k"]] = (e["uid"], e["t"], base64.b64decode(e["resp"]))
@@ -88,11 +92,10 @@ class AllocJournal:
         if not self.path:
             return
         try:
-            if self._f is None:
+            if self._fd < 0:
                 os.makedirs(os.path.dirname(self.path) or ".", exist_ok=True)
-                self._f = open(self.path, "a")
-            self._f.write(json.dumps(rec, separators=(",", ":")) + "\n")
-            self._f.flush()
+                self._fd = os.open(self.path, os.O_WRONLY | os.O_APPEND | os.O_CREAT | os.O_CLOEXEC, 0o600)
+            os.write(self._fd, (json.dumps(rec, separators=(",", ":")) + "\n").encode())
             self._lines += 1
             if self._lines > 2 * self.max_entries + 2 * len(self._pending) + 64:
                 self._compact()
@@ -111,9 +114,9 @@ class AllocJournal:
                                        separators=(",", ":")) + "\n")
                 for e in self._pending.values():
                     f.write(json.dumps(e, separators=(",", ":")) + "\n")
-            if self._f is not None:
-                self._f.close()
-                self._f = None
+            if self._fd >= 0:
+                os.close(self._fd)
+                self._fd = -1
             os.replace(tmp, self.path)
             self._lines = len(self._mem) + len(self._pending)
         except OSError as e:
@@ -147,6 +150,21 @@ class AllocJournal:
             return uid in self._pending or (t is not None and time.time() - t <= self.ttl_s)
 
     # -- write-behind patches ---------------------------------------------------------------
+    def record_pending(self, req, pod_uid: str, resp, ns: str, name: str, ann: dict | None = None,
+                       key: str | None = None) -> None:
+        """A write-behind answer and its still-pending ASSIGNED patch, in one record/syscall."""
+        key, t, blob = key or request_key(req), time.time(), resp.SerializeToString()
+        pend = {"op": "patch", "uid": pod_uid, "ns": ns, "name": name, "ann": dict(ann or {}), "t": t}
+        with self._lock:
+            self._mem[key] = (pod_uid, t, blob)
+            self._mem.move_to_end(key)
+            self._uids[pod_uid] = t
+            while len(self._mem) > self.max_entries:
+                _, (u, _, _) = self._mem.popitem(last=False)
+                self._uids.pop(u, None)
+            self._pending[pod_uid] = pend
+            self._write(pend | {"op": "answer+patch", "k": key, "resp": base64.b64encode(blob).decode()})
+
     def pending(self, uid: str, ns: str, name: str, ann: dict | None = None) -> None:
         rec = {"op": "patch", "uid": uid, "ns": ns, "name": name, "ann": dict(ann or {}), "t": time.time()}
         with self._lock:
@@ -164,9 +182,9 @@ class AllocJournal:
 
     def close(self):
         with self._lock:
-            if self._f is not None:
-                self._f.close()
-                self._f = None
+            if self._fd >= 0:
+                os.close(self._fd)
+                self._fd = -1
 
     def __len__(self):
         return len(self._mem)

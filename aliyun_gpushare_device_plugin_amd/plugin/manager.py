@@ -270,12 +270,14 @@ class SharedGPUManager:
                     except Exception as e:  # noqa: BLE001
                         log.warning("Failed to get device plugin due to %s", e)
                         return 1
+                    # the topology is on the node before the kubelet advertises capacity, so a
+                    # TP-aware extender never schedules against a node without it
+                    self._export_topology()
                     try:
                         self.plugin.serve(self._kubelet_socket())
                     except Exception as e:  # noqa: BLE001
                         log.warning("Failed to start device plugin due to %s", e)
                         return 2
-                    self._export_topology()
                     self._start_health()
                     self._start_ledger_collector()
                     restart = False

@@ -45,6 +45,14 @@ def test_bench_torchrun_two_ranks_gloo():
     d = parse(r.stdout)           # only rank 0 prints
     assert d["n_gpus"] == 2 and d["pods_per_node"] == 8 and d["advertised_gib_per_node"] == 576
     assert d["config"]["parallelism"] == "node2"
+    # N>1: the topology the plugin exported and an all-reduce on the TP pair best_group picks
+    topo = d["topology"]
+    assert topo["tp_pair"] == [0, 1] and topo["pair_link"] == "xgmi" and topo["pair_hops"] == 1
+    assert topo["tp_pair_allreduce"]["busbw_GBps"] > 0 and topo["backend"] == "gloo"
+    # the control-plane A/B is in the same line: default vs the reference's cost model
+    ab = d["allocate_by_mode"]
+    assert ab["reference@5ms"]["apiserver_round_trips_on_path"] == 2
+    assert ab["default@5ms"]["allocate_p50_ms"] < ab["reference@5ms"]["allocate_p50_ms"]
 
 
 def test_tp_pair_demo_gloo():

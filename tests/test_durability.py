@@ -34,7 +34,7 @@ def test_killed_plugin_lands_pending_patch_after_restart(tmp_path):
         assert adm_a.error is None and idx(adm_a) == where_a[1]
         time.sleep(0.3)                     # the patcher is retrying against the outage
         assert O.annotations(c.client.get_pod("default", "a"))[const.ENV_ASSIGNED_FLAG] == "false"
-        assert any('"op":"patch"' in ln for ln in open(journal))
+        assert any('"op":"answer+patch"' in ln for ln in open(journal))
         # the kubelet has not reported A Running yet: A still looks like an assumed Pending pod
         c.client.patch_pod_status("default", "a", {"status": {"phase": "Pending"}})
         c.kill_plugin("n")

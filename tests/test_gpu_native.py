@@ -186,3 +186,45 @@ def test_shim_kfd_denial_is_clean():
     out, _ = _probe(["alloc", 256 * MIB, "alloc", GIB, "alloc", 256 * MIB], GPUSHARE_QUOTA_BYTES=768 * MIB)
     assert [o["rc"] for o in out] == [0, 2, 0]
     assert out[1]["denied"] >= 1 and out[2]["used"] <= 768 * MIB
+
+
+def _gpus() -> int:
+    with S.SMI("auto") as s:
+        return s.count()
+
+
+def test_xgmi_matrix_on_multi_gpu_node():
+    """On an MI355X UBB every GPU pair is one xGMI hop; the exported matrix must say so
+    (round-1 review: only fake fixtures had been seen). Needs >= 2 visible GPUs."""
+    from aliyun_gpushare_device_plugin_amd.parallel import topology as T
+
+    if _gpus() < 2:
+        pytest.skip("needs >= 2 GPUs (runs on the 8-GPU node)")
+    with S.SMI("auto") as s:
+        topo = T.build_topology(s)
+    n = len(topo["gpus"])
+    for i in range(n):
+        for j in range(n):
+            if i != j:
+                assert topo["link_type"][i][j] == "xgmi" and topo["hops"][i][j] == 1, (i, j, topo)
+    assert T.best_group(topo, [288] * n, 2, 64) is not None
+
+
+def test_rccl_tp_pair_allreduce():
+    """The RCCL TP-pair demo on two GPUs (torch.distributed 'nccl' = RCCL over xGMI): numerics
+    of the tensor-parallel block and a non-trivial bus bandwidth. Needs >= 2 visible GPUs."""
+    if _gpus() < 2:
+        pytest.skip("needs >= 2 GPUs (runs on the 8-GPU node)")
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "-m",
+                        "aliyun_gpushare_device_plugin_amd.parallel.tp_demo", "--iters", "10"],
+                       cwd=root, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert d["backend"] == "nccl" and d["tp_block_rel_err"] < 5e-2 and d["busbw_GBps"] > 10
