@@ -32,16 +32,23 @@ def main():
         p.stdin.write(json.dumps({"cmd": "start", "env": {"GPUSHARE_QUOTA_BYTES": str(q)}, "fill": 0.85}) + "\n")
         out["ready"] = json.loads(p.stdout.readline())
         out["running"] = vram_used(s)
-        p.stdin.write('{"cmd":"stop"}\n')
+        hold_exit = os.environ.get("HOLD_EXIT", "0") == "1"
+        if hold_exit:   # keep the process alive after "done": is the HBM back without an exit?
+            p.stdin.write('{"cmd":"stop"}\n')
+        else:
+            p.stdin.write('{"cmd":"stop"}\n')
         out["done"] = json.loads(p.stdout.readline())
         t = time.perf_counter()
         out["after_done"] = vram_used(s)
         series = []
-        while p.poll() is None:
+        exit_t = None
+        while time.perf_counter() - t < 6.0:
+            if exit_t is None and p.poll() is not None:
+                exit_t = round(time.perf_counter() - t, 3)
             series.append((round(time.perf_counter() - t, 3), vram_used(s)))
-            time.sleep(0.05)
-        out["exit_s"] = round(time.perf_counter() - t, 3)
-        out["series"] = series[:40]
+            time.sleep(0.1)
+        out["exit_s"] = exit_t
+        out["series"] = series
         out["after_exit"] = vram_used(s)
     print(json.dumps(out, indent=1))
 
