@@ -128,6 +128,10 @@ def install_shim(dest_dir: str) -> str:
 
 def main(argv=None) -> int:
     a = build_parser().parse_args(argv)
+    # Allocate runs on a gRPC thread while the informer thread decodes watch events of the very
+    # pod being admitted: with CPython's default 5 ms GIL switch interval the handler can sit
+    # behind a whole decode. A 0.25 ms interval bounds that wait (the kubelet blocks on it).
+    sys.setswitchinterval(float(os.environ.get("GPUSHARE_SWITCH_INTERVAL", "0.00025")))
     log.setup(verbosity=a.v, json_lines=a.log_json)
     log.V(1).info("Start gpushare device plugin")
     cfg = config_from_args(a)

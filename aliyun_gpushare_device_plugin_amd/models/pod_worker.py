@@ -91,6 +91,10 @@ def main() -> int:
         ctl.put({"cmd": "stop"})                                # parent went away
 
     threading.Thread(target=reader, daemon=True).start()
+    # wait for each burst on a blocking-sync event: the thread sleeps until the GPU signals
+    # instead of spinning a core (HIP's default) — co-located pods and the node's control plane
+    # share the host's CPUs
+    burst_done = torch.cuda.Event(blocking=True)
     gemms = 1
     t_start = time.time()
     while True:
@@ -105,7 +109,8 @@ def main() -> int:
                 break
             continue
         player.run(burst)
-        player.synchronize()
+        burst_done.record(player.stream)
+        burst_done.synchronize()
         gemms += burst
     player.release()
     st = _shim_stats()
