@@ -64,7 +64,7 @@ def parse():
     ap.add_argument("--smi-backend", default=None, help="default: auto on GPU, fake:Nx288G on CPU")
     ap.add_argument("--pod-source", default="watch", choices=("watch", "list", "kubelet"))
     ap.add_argument("--plugin-mode", default="process", choices=("process", "thread"))
-    ap.add_argument("--compare-rtts", default="1,5", help="apiserver RTTs (ms) of the control-plane A/B ('' = off)")
+    ap.add_argument("--compare-rtts", default="0,1,5", help="apiserver RTTs (ms) of the control-plane A/B ('' = off)")
     ap.add_argument("--compare-pods", type=int, default=24, help="admissions per A/B configuration")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
