@@ -372,7 +372,7 @@ class PodFleet:
         self.ready_ms.append(dt)
         return dt
 
-    def stop(self, uid: str):
+    def stop(self, uid: str, wait_release: bool = True):
         w = self.pods.pop(uid, None)
         if w is None:
             return
@@ -381,7 +381,7 @@ class PodFleet:
         w["proc"].stdin.write('{"cmd":"stop"}\n')
         ev = self._wait(w, "done")                      # freed through KFD at this point
         threading.Thread(target=w["proc"].wait, daemon=True).start()   # reap the exit off the path
-        if before is not None:
+        if before is not None and wait_release:
             # amdgpu returns freed VRAM asynchronously (the buffers are cleared first): the
             # replacement pod is admitted only once the device reports the HBM free again, as
             # a quota-sum-equals-HBM node needs (bounded wait)
@@ -404,7 +404,7 @@ class PodFleet:
 
     def close(self):
         for uid in list(self.pods):
-            self.stop(uid)
+            self.stop(uid, wait_release=False)
         for w in self.standby:
             try:
                 w["proc"].stdin.close()
