@@ -15,13 +15,15 @@ Scenario (one node with N = --gpus MI355X, one rank per GPU, rank 0 also hosts t
     retired;
   * warm-up fills every GPU with 4 pods of mixed size 8-128 GiB summing to 288 GiB (BASELINE
     config 3: 32 pods on 8 GPUs) and runs W untimed churn waves;
-  * each timed step = one churn wave on every GPU while the other pods keep the GPU busy: the
-    oldest pod's process is stopped (its HBM returns), the pod is deleted, a same-size
-    replacement is created, bin-packed by the extender, admitted by the kubelet through the
-    plugin's Allocate, and its process starts under the shim and runs its first GEMM ("pod
-    ready"). The interpreter of the replacement is pre-started (standby: torch imported, GPU
-    untouched — an image already pulled); HIP init, quota, HBM allocation and the first GEMM are
-    inside the timed step. Per-GPU work is fixed (1 admission per step), so scaling is weak.
+  * each timed step = one churn cycle on every GPU while the other pods keep it busy: the
+    oldest pod's process is stopped (the step waits until amdgpu reports its HBM free), the pod
+    is deleted, a same-size replacement is created, bin-packed by the extender, admitted by the
+    kubelet through the plugin's Allocate, and its process starts under the shim and runs its
+    first GEMM ("pod ready"). The interpreter of the replacement is pre-started (standby: torch
+    imported, GPU untouched — an image already pulled); HIP init, quota, HBM allocation and the
+    first GEMM are inside the timed step. Each GPU cycles independently (rank 0 serves the
+    admissions, serialised like one kubelet); per-GPU work is fixed (1 admission per step), so
+    scaling is weak.
 ``value`` = pods admitted-to-ready per second for the whole node (higher is better). Also in the
 line: Allocate p50/p99 (kubelet-side gRPC round trip) and the plugin's server-side p50/p99; pod
 ready p50; pods and GiB bin-packed per node; the aggregate GEMM TFLOP/s the pod processes
@@ -164,72 +166,43 @@ class ControlPlane:
                     started[rec[0]].append(rec[1])
         return started
 
-    def retire_plan(self) -> dict:
-        """The oldest pod of every GPU: these processes stop before the wave's admissions."""
+    def churn_one(self, gpu: int, uid: str | None = None) -> tuple[int, dict] | None:
+        """Retire pod ``uid`` (default: the oldest) of ``gpu`` and admit a same-size replacement
+        through delete (controller) -> create -> extender decide + bind (assume time stamped at
+        the decision) -> kubelet admission (Allocate over gRPC). Serialised by the caller, as the
+        scheduler's cycle and the kubelet's admissions are. The replacement lands where the
+        extender's best fit puts it — the freed exact-fit hole on ``gpu``, or an equal hole
+        another GPU freed at the same time. Returns (landed gpu, pod record) or None."""
         from aliyun_gpushare_device_plugin_amd.cluster import objects as O
 
-        return {g: O.uid(pods[0][0]) for g, pods in self.resident.items() if pods}
-
-    def churn(self) -> dict:
-        """Delete the retired pods and admit same-size replacements; returns {gpu: [pod record]}.
-
-        One pipeline per GPU, as in a real cluster where each replacement is independent:
-        delete (controller) -> create -> scheduling cycle (extender decide, stamps the assume
-        time) -> binding cycle (annotations + bind) -> kubelet admission. Only the scheduling
-        cycle and the kubelet are serial: the kubelet's pod worker sees pods in bind order, so
-        admissions are taken in assume-time order (a ticket per decision) and the plugin's
-        earliest-assumed match is the pod actually being admitted. Every replacement has an
-        exact-fit slot (its predecessor's), so best-fit keeps the node packed.
-        """
-        import itertools
-
-        olds = [(g, self.resident[g].pop(0)) for g in range(self.n) if self.resident[g]]
-        ext = self.cluster.extender
-        tickets = itertools.count()
-        turn = {"next": 0}
-
-        def chain(it):
-            _, (old, size) = it
-            self.cluster.delete_pod(old)
-            pod = self.cluster.create_pod(size)
-            with self._sched_lock:                      # the scheduler's one-pod-at-a-time cycle
-                where = ext.decide(pod)
-                ticket, assume_ns = next(tickets), time.time_ns()
-            try:
-                bpod = ext.commit(pod, where, assume_ns) if where else None
-                with self._kubelet:
-                    while turn["next"] != ticket:
-                        self._kubelet.wait()
-                if bpod is None:
-                    return None, size, None, 0.0
-                t0 = time.perf_counter()
-                adm = self.cluster.admit(bpod, async_status=True)
-                return bpod, size, adm, time.perf_counter() - t0
-            finally:
-                with self._kubelet:
-                    while turn["next"] != ticket:
-                        self._kubelet.wait()
-                    turn["next"] += 1
-                    self._kubelet.notify_all()
-
-        started: dict[int, list] = {g: [] for g in range(self.n)}
-        for bpod, size, adm, dt in self.pool.map(chain, olds):
-            if adm is None or adm.error:
-                self.failed += 1
-                self.fail_reasons.append(f"{size}GiB: " + ("unschedulable" if bpod is None else f"admit: {adm and adm.error}"))
-                if bpod is not None:
-                    self.cluster.delete_pod(bpod)
-                continue
-            rec = self._record(bpod, size, adm)
-            if rec is None:                             # soft failure: no candidate matched
-                self.failed += 1
-                self.fail_reasons.append(f"{size}GiB: plugin found no candidate")
-                self.cluster.delete_pod(bpod)
-                continue
-            self.alloc_lat.extend(adm.latencies)
-            self.admit_lat.append(dt)
-            started[rec[0]].append(rec[1])
-        return started
+        pods = self.resident[gpu]
+        k = next((i for i, (p, _) in enumerate(pods) if uid is None or O.uid(p) == uid), None)
+        if k is None:
+            return None
+        old, size = pods.pop(k)
+        tc = time.perf_counter()
+        self.cluster.delete_pod(old)
+        pod = self.cluster.create_pod(size)
+        where = self.cluster.extender.decide(pod)
+        bpod = self.cluster.extender.commit(pod, where, time.time_ns()) if where else None
+        if bpod is None:
+            self.failed += 1
+            self.fail_reasons.append(f"{size}GiB: unschedulable")
+            self.cp_time += time.perf_counter() - tc
+            return None
+        t0 = time.perf_counter()
+        adm = self.cluster.admit(bpod, async_status=True)
+        dt = time.perf_counter() - t0
+        rec = self._record(bpod, size, adm) if adm.error is None else None
+        self.cp_time += time.perf_counter() - tc
+        if rec is None:
+            self.failed += 1
+            self.fail_reasons.append(f"{size}GiB: " + (f"admit: {adm.error}" if adm.error else "plugin found no candidate"))
+            self.cluster.delete_pod(bpod)
+            return None
+        self.alloc_lat.extend(adm.latencies)
+        self.admit_lat.append(dt)
+        return rec
 
     def plugin_latency(self, reset: bool = False) -> dict | None:
         """The plugin's own (server-side) Allocate latency quantiles from its metrics endpoint."""
@@ -286,6 +259,69 @@ def mode_comparison(rtts_ms: list[float], n_pods: int) -> dict:
     return out
 
 
+class AdmissionService:
+    """Rank 0's admission endpoint for the per-GPU churn pipelines: ``churn(gpu, uid)`` retires a
+    pod and admits its replacement, then returns the next pod that landed on ``gpu`` (each
+    retirement opens one exact-fit hole and each admission fills one, so every waiting GPU gets
+    a pod). Ranks > 0 reach it over a loopback TCP socket (one JSON line per request)."""
+
+    def __init__(self, cp: ControlPlane):
+        self.cp = cp
+        self.lock = threading.Lock()                        # one admission at a time, like the kubelet
+        self.mail = {g: queue.Queue() for g in range(cp.n)}
+        self.server = None
+
+    def churn(self, gpu: int, uid: str | None) -> dict | None:
+        with self.lock:
+            landed = self.cp.churn_one(gpu, uid)
+        if landed is None:
+            return None
+        self.mail[landed[0]].put(landed[1])
+        return self.mail[gpu].get(timeout=300)
+
+    def serve(self) -> int:
+        import socketserver
+
+        svc = self
+
+        class H(socketserver.StreamRequestHandler):
+            def handle(self):
+                for ln in self.rfile:
+                    req = json.loads(ln)
+                    rec = svc.churn(req["gpu"], req.get("uid"))
+                    self.wfile.write((json.dumps({"rec": rec}) + "\n").encode())
+                    self.wfile.flush()
+
+        class Srv(socketserver.ThreadingTCPServer):
+            daemon_threads = True
+            allow_reuse_address = True
+
+        self.server = Srv(("127.0.0.1", 0), H)
+        threading.Thread(target=self.server.serve_forever, daemon=True).start()
+        return self.server.server_address[1]
+
+    def stop(self):
+        if self.server is not None:
+            self.server.shutdown()
+            self.server.server_close()
+
+
+class AdmissionClient:
+    def __init__(self, port: int):
+        import socket
+
+        self.sock = socket.create_connection(("127.0.0.1", port))
+        self.f = self.sock.makefile("rw")
+
+    def churn(self, gpu: int, uid: str | None) -> dict | None:
+        self.f.write(json.dumps({"gpu": gpu, "uid": uid}) + "\n")
+        self.f.flush()
+        return json.loads(self.f.readline())["rec"]
+
+    def close(self):
+        self.sock.close()
+
+
 class PodFleet:
     """The pod processes of this rank's GPU, plus one standby process (interpreter up, torch
     imported, GPU untouched) that becomes the next admitted pod."""
@@ -301,6 +337,7 @@ class PodFleet:
         self.held_bytes = 0
         self.released_residue = 0             # shim-ledger bytes a stopped pod still held after freeing
         self.release_ms: list[float] = []     # stop -> the device reports the pod's HBM free again
+        self.release_by_size: dict[int, list] = {}
         self._vram_used = self._vram_reader()
         for _ in range(max(1, standby)):
             self._spawn()
@@ -390,10 +427,14 @@ class PodFleet:
             while self._vram_used() > target and time.perf_counter() < deadline:
                 time.sleep(0.005)
             self.release_ms.append(time.perf_counter() - t0)
+            self.release_by_size.setdefault(w["size"], []).append(time.perf_counter() - t0)
         self.released_residue = max(self.released_residue, ev.get("used_after_release") or 0)
         self.retired_gemms += ev["gemms"]
         self.held_bytes -= w["ready"].get("held", 0)
         self.denied += ((ev.get("shim") or {}).get("denied") or 0)
+
+    def oldest(self) -> str | None:
+        return next(iter(self.pods), None)
 
     def gemms(self) -> int:
         """Cumulative GEMMs of every pod this fleet ran (live pods asked between bursts)."""
@@ -481,25 +522,35 @@ def main():
                 worst = max(worst, fleet.start(rec))
         return worst
 
-    def step():
-        plan = bcast(cp.retire_plan() if rank == 0 else None)
-        if fleet is not None and local in plan:
-            fleet.stop(plan[local])              # HBM returned before the replacement is admitted
-        barrier()
-        started = None
-        if rank == 0:
-            tc = time.perf_counter()
-            started = cp.churn()
-            cp.cp_time += time.perf_counter() - tc
-        started = bcast(started)
-        launch(started)
+    # Per-GPU churn pipelines: every rank cycles its own GPU (stop the oldest pod -> its HBM is
+    # back -> ask rank 0's admission service for the replacement -> start it) without waiting for
+    # the other GPUs; rank 0 serialises the admissions themselves, as one kubelet does.
+    svc = client = None
+    port = None
+    if rank == 0:
+        svc = AdmissionService(cp)
+        port = svc.serve() if world > 1 else None
+    port = bcast(port)
+    if rank != 0:
+        client = AdmissionClient(port)
 
-    # ---- warm-up: fill the node, start its pods, then W untimed churn waves ----
+    def cycle():
+        uid = None
+        if fleet is not None:
+            uid = fleet.oldest()
+            if uid is not None:
+                fleet.stop(uid)                  # HBM returned before the replacement is admitted
+        rec = svc.churn(local, uid) if rank == 0 else client.churn(local, uid)
+        if rec is not None and fleet is not None:
+            fleet.start(rec)
+
+    # ---- warm-up: fill the node, start its pods, then W untimed churn cycles per GPU ----
     started = bcast(cp.fill() if rank == 0 else None)
     launch(started)
     barrier()
     for _ in range(a.warmup):
-        step()
+        cycle()
+    barrier()
     if rank == 0:
         cp.alloc_lat.clear()
         cp.admit_lat.clear()
@@ -510,12 +561,13 @@ def main():
     if fleet is not None:
         fleet.ready_ms.clear()
         fleet.release_ms.clear()
+        fleet.release_by_size.clear()
 
     barrier()
     g0 = fleet.gemms() if fleet is not None else 0
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        step()
+        cycle()
     barrier()
     elapsed = time.perf_counter() - t0
     g1 = fleet.gemms() if fleet is not None else 0
@@ -533,6 +585,10 @@ def main():
     residue = gather(fleet.released_residue if fleet is not None else 0)
     release = gather(fleet.release_ms if fleet is not None else [])
     release_all = [x for r in release for x in r]
+    by_size: dict = {}
+    for d in gather(fleet.release_by_size if fleet is not None else {}):
+        for k, v in d.items():
+            by_size.setdefault(k, []).extend(v)
 
     if world > 1:
         from aliyun_gpushare_device_plugin_amd.cluster import nodestatus
@@ -547,6 +603,7 @@ def main():
         gib_node = sum(s for v in cp.resident.values() for _, s in v)
         admissions = a.steps * n - cp.failed
         value = admissions / elapsed
+        svc.stop()
         cp.stop()
         modes = mode_comparison([float(x) for x in a.compare_rtts.split(",") if x], a.compare_pods) \
             if a.compare_rtts else {}
@@ -576,7 +633,8 @@ def main():
             "pod_ready_p50_ms": ms(pct(ready_all, 0.5)),
             "pod_ready_p99_ms": ms(pct(ready_all, 0.99)),
             "pod_hbm_release_p50_ms": ms(pct(release_all, 0.5)),
-            "control_plane_ms_per_step": round(cp.cp_time / a.steps * 1e3, 3),
+            "pod_hbm_release_p50_ms_by_gib": {str(k): ms(pct(v, 0.5)) for k, v in sorted(by_size.items())},
+            "control_plane_ms_per_admission": round(cp.cp_time / max(1, a.steps * n) * 1e3, 3),
             "allocate_by_mode": modes,
             "pods_per_node": pods_node,
             "hbm_gib_per_node": gib_node,
@@ -598,6 +656,8 @@ def main():
                 f.write(line + "\n")
     if fleet is not None:
         fleet.close()
+    if client is not None:
+        client.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
