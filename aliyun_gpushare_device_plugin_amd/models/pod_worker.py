@@ -72,7 +72,11 @@ def main() -> int:
 
     work = 3 * g * g * 2
     hold_bytes = max(0, int(quota * fill) - work)
-    hold = torch.empty(hold_bytes // 2, dtype=torch.bfloat16, device=dev) if hold_bytes else None
+    # resident state as a model holds it: many tensors (2 GiB each), not one block — amdgpu wipes
+    # each freed buffer before returning it, so a pod's HBM comes back piecewise on release
+    chunk = int(cmd.get("chunk", 2 << 30))
+    hold = [torch.empty(min(chunk, hold_bytes - off) // 2, dtype=torch.bfloat16, device=dev)
+            for off in range(0, hold_bytes, chunk)]
     player = GemmPlayer(work, dev, g, g, g, touch_fraction=1.0, seed=os.getpid() & 0xffff)
     player.run(1)
     player.synchronize()

@@ -16,7 +16,8 @@ Scenario (one node with N = --gpus MI355X, one rank per GPU, rank 0 also hosts t
   * warm-up fills every GPU with 4 pods of mixed size 8-128 GiB summing to 288 GiB (BASELINE
     config 3: 32 pods on 8 GPUs) and runs W untimed churn waves;
   * each timed step = one churn cycle on every GPU while the other pods keep it busy: the
-    oldest pod's process is stopped (the step waits until amdgpu reports its HBM free), the pod
+    oldest pod's process is stopped (the step waits until amdgpu, which wipes freed VRAM before
+    returning it, reports room for a same-size pod), the pod
     is deleted, a same-size replacement is created, bin-packed by the extender, admitted by the
     kubelet through the plugin's Allocate, and its process starts under the shim and runs its
     first GEMM ("pod ready"). The interpreter of the replacement is pre-started (standby: torch
@@ -336,29 +337,32 @@ class PodFleet:
         self.denied = 0
         self.held_bytes = 0
         self.released_residue = 0             # shim-ledger bytes a stopped pod still held after freeing
-        self.release_ms: list[float] = []     # stop -> the device reports the pod's HBM free again
+        self.release_ms: list[float] = []     # stop -> the GPU physically has room for the replacement
         self.release_by_size: dict[int, list] = {}
-        self._vram_used = self._vram_reader()
+        self._vram_used, self._vram_total = self._vram_reader()
         for _ in range(max(1, standby)):
             self._spawn()
 
     def _vram_reader(self):
-        """amdgpu's own count of used VRAM for this rank's GPU (sysfs), or None."""
+        """(reader of amdgpu's used-VRAM count for this rank's GPU, its total VRAM) from sysfs, or
+        (None, 0)."""
         try:
             from aliyun_gpushare_device_plugin_amd.device.smi import SMI
 
             with SMI("auto") as s:
                 minor = s.device(self.local).render_minor if s.count() > self.local else -1
         except Exception:  # noqa: BLE001
-            return None
-        path = f"/sys/class/drm/renderD{minor}/device/mem_info_vram_used"
-        if minor < 0 or not os.path.exists(path):
-            return None
+            return None, 0
+        base = f"/sys/class/drm/renderD{minor}/device/mem_info_vram_"
+        if minor < 0 or not os.path.exists(base + "used"):
+            return None, 0
+        with open(base + "total") as f:
+            total = int(f.read())
 
         def read():
-            with open(path) as f:
+            with open(base + "used") as f:
                 return int(f.read())
-        return read
+        return read, total
 
     def _spawn(self):
         env = dict(os.environ, LD_PRELOAD=os.path.join(NATIVE, "libgpushare_hipquota.so"),
@@ -414,17 +418,16 @@ class PodFleet:
         if w is None:
             return
         t0 = time.perf_counter()
-        before = self._vram_used() if self._vram_used else None
         w["proc"].stdin.write('{"cmd":"stop"}\n')
         ev = self._wait(w, "done")                      # freed through KFD at this point
         threading.Thread(target=w["proc"].wait, daemon=True).start()   # reap the exit off the path
-        if before is not None and wait_release:
-            # amdgpu returns freed VRAM asynchronously (the buffers are cleared first): the
-            # replacement pod is admitted only once the device reports the HBM free again, as
-            # a quota-sum-equals-HBM node needs (bounded wait)
-            target = before - int(0.95 * w["ready"].get("held", 0))
+        if self._vram_used is not None and wait_release:
+            # amdgpu returns freed VRAM asynchronously (it wipes it first, ~26 ms per GiB): the
+            # same-size replacement is admitted once the GPU physically has room for what it will
+            # hold plus 2 GiB of runtime slack — the quotas add up to the whole HBM (bounded wait)
+            need = w["ready"].get("held", 0) + (2 << 30)
             deadline = time.perf_counter() + 20.0
-            while self._vram_used() > target and time.perf_counter() < deadline:
+            while self._vram_total - self._vram_used() < need and time.perf_counter() < deadline:
                 time.sleep(0.005)
             self.release_ms.append(time.perf_counter() - t0)
             self.release_by_size.setdefault(w["size"], []).append(time.perf_counter() - t0)
@@ -632,8 +635,8 @@ def main():
             "admission_p50_ms": ms(pct(cp.admit_lat, 0.5)),
             "pod_ready_p50_ms": ms(pct(ready_all, 0.5)),
             "pod_ready_p99_ms": ms(pct(ready_all, 0.99)),
-            "pod_hbm_release_p50_ms": ms(pct(release_all, 0.5)),
-            "pod_hbm_release_p50_ms_by_gib": {str(k): ms(pct(v, 0.5)) for k, v in sorted(by_size.items())},
+            "pod_room_wait_p50_ms": ms(pct(release_all, 0.5)),
+            "pod_room_wait_p50_ms_by_gib": {str(k): ms(pct(v, 0.5)) for k, v in sorted(by_size.items())},
             "control_plane_ms_per_admission": round(cp.cp_time / max(1, a.steps * n) * 1e3, 3),
             "allocate_by_mode": modes,
             "pods_per_node": pods_node,
