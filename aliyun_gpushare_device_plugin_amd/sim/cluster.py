@@ -27,6 +27,7 @@ from ..utils import log
 from .apiserver import FakeAPIServer, make_node
 from .extender import TP_GROUP_LABEL, TP_SIZE_LABEL, ExtenderSim
 from .kubelet import Admission, FakeKubelet
+from .kubelet_proc import KubeletProcess
 
 
 def pod_spec(name: str, gpu_mem, namespace: str = "default", labels: dict | None = None,
@@ -46,7 +47,7 @@ class SimNode:
     name: str
     smi_spec: str
     plugin_dir: str
-    kubelet: FakeKubelet
+    kubelet: "FakeKubelet | KubeletProcess"
     manager: SharedGPUManager | None = None
     thread: threading.Thread | None = None
     proc: subprocess.Popen | None = None
@@ -57,8 +58,11 @@ class SimCluster:
                  pod_source: str = "watch", apiserver_latency_s: float = 0.0, shim_host_dir: str | None = None,
                  gpu_indices: list[int] | None = None, health_poll_s: float = 1.0, round_policy: str = "nearest",
                  extra_plugin_args: list[str] | None = None, apiserver: str = "thread",
-                 preferred_allocation: bool = False, compute_isolation: str = "none"):
+                 preferred_allocation: bool = False, compute_isolation: str = "none", kubelet: str = "thread"):
         self.node_specs = nodes
+        # kubelet: "thread" (FakeKubelet in this interpreter) or "process" (its own interpreter,
+        # sim/kubelet_proc.py, so kubelet-side Allocate timing is not inflated by this process's GIL)
+        self.kubelet_mode = kubelet
         self.compute_isolation = compute_isolation
         self._own_dir = workdir is None
         # short paths: UDS paths are limited to 108 bytes
@@ -113,9 +117,13 @@ class SimCluster:
         for name, spec in self.node_specs:
             self.client.create_node(make_node(name))
             pdir = os.path.join(self.workdir, name)
-            kl = FakeKubelet(pdir, APIClient(KubeConfig(self.api_url)), name).start()
-            if self.pod_source == "kubelet":
-                kl.serve_pods()
+            if self.kubelet_mode == "process" and self.pod_source != "kubelet":
+                kl = KubeletProcess(pdir, self.api_url, name, env=self._child_env(),
+                                    preexec_fn=_die_with_parent).start()
+            else:
+                kl = FakeKubelet(pdir, APIClient(KubeConfig(self.api_url)), name).start()
+                if self.pod_source == "kubelet":
+                    kl.serve_pods()
             node = SimNode(name, spec, pdir, kl)
             self.nodes[name] = node
             self._start_plugin(node)

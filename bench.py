@@ -138,7 +138,7 @@ class ControlPlane:
         if with_shim:
             extra += ["--rocr-visible-devices"]
         self.cluster = SimCluster([("mi355x-node", smi_spec)], plugin_mode=plugin_mode, pod_source=pod_source,
-                                  apiserver="process", gpu_indices=list(range(n_gpus)), health_poll_s=5.0,
+                                  apiserver="process", kubelet="process", gpu_indices=list(range(n_gpus)), health_poll_s=5.0,
                                   extra_plugin_args=extra, shim_host_dir=NATIVE if with_shim else None)
         self.cluster.start()
         from aliyun_gpushare_device_plugin_amd import const
@@ -246,7 +246,7 @@ def mode_comparison(rtts_ms: list[float], n_pods: int) -> dict:
             lat, fails = [], 0
             port = free_port()
             with SimCluster([("cmp", "fake:1x288G")], plugin_mode="process", pod_source=src,
-                            apiserver_latency_s=rtt / 1e3,
+                            apiserver="process", kubelet="process", apiserver_latency_s=rtt / 1e3,
                             extra_plugin_args=extra + ["--metrics-addr", f"127.0.0.1:{port}"]) as c:
                 req = []                                 # one apiserver round trip, as the plugin sees it
                 for _ in range(10):

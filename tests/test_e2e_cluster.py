@@ -140,6 +140,24 @@ def test_plugin_as_separate_process():
         assert c.nodes["n"].kubelet.options.get_preferred_allocation_available
 
 
+def test_kubelet_as_separate_process():
+    """Every component in its own interpreter (the bench's layout): apiserver, kubelet, plugin."""
+    with SimCluster([("n", "fake:2x4G")], plugin_mode="process", apiserver="process", kubelet="process",
+                    preferred_allocation=True) as c:
+        kl = c.nodes["n"].kubelet
+        assert kl.options.get_preferred_allocation_available and kl.registered.is_set()
+        pod, w, adm = c.run_pod(3)
+        assert adm.error is None and envs(adm)[const.ENV_RESOURCE_BY_CONTAINER] == "3"
+        assert len(adm.latencies) == 1 and adm.latencies[0] > 0
+        assert len(kl.allocated_ids()) == 3
+        c.delete_pod(pod)
+        assert kl.allocated_ids() == set()
+        c.kill_plugin("n")
+        c.restart_plugin("n")                    # registered.clear() + wait through the pipe
+        _, _, adm = c.run_pod(4)
+        assert adm.error is None
+
+
 def test_preferred_allocation_is_opt_in():
     with SimCluster([("n", "fake:1x4G")]) as c:
         assert not c.nodes["n"].kubelet.options.get_preferred_allocation_available
