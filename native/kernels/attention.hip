@@ -39,6 +39,26 @@ template <int D>
 __device__ __forceinline__ int vswz(int row, int unit) { return unit ^ (((row & 7) << 2) & (D / 4 - 1)); }
 #define vswz_unit(r, u) vswz<D>(r, u)
 
+// Block -> (batch*head, q-block). Workgroups are dispatched round-robin over the 8 XCDs (block i
+// on XCD i mod 8), each with its own L2. Causal: q-blocks heaviest first ACROSS the whole grid
+// (longest-processing-time order; a head-major order left heavy blocks of the last heads for the
+// tail), and within one level the heads an XCD gets are contiguous, so the query heads sharing a
+// K/V head (GQA) read it through one L2. Full attention: every XCD walks a contiguous range of
+// (head, q-block), so the blocks of one head share that XCD's L2.
+__device__ __forceinline__ void block_coords(int nqb, int BH, int causal, int& bh, int& qb) {
+  const int i = (int)blockIdx.x;
+  if (causal) {
+    const int lvl = i / BH, j = i % BH;
+    qb = nqb - 1 - lvl;
+    bh = (BH & 7) ? j : (j & 7) * (BH >> 3) + (j >> 3);
+  } else {
+    const int n = BH * nqb;
+    const int L = (n & 7) ? i : (i & 7) * (n >> 3) + (i >> 3);
+    bh = L / nqb;
+    qb = L % nqb;
+  }
+}
+
 template <int D, bool TR>
 __global__ __launch_bounds__(256, 2) void flash_fwd(const unsigned short* __restrict__ Q,
                                                     const unsigned short* __restrict__ K,
@@ -49,8 +69,8 @@ __global__ __launch_bounds__(256, 2) void flash_fwd(const unsigned short* __rest
   using C = Cfg<D>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nqb = (S + QROWS - 1) / QROWS;
-  const int bh = blockIdx.x / nqb;
-  const int qb = causal ? (nqb - 1 - (int)(blockIdx.x % nqb)) : (int)(blockIdx.x % nqb);  // heaviest first
+  int bh, qb;
+  block_coords(nqb, B * Hq, causal, bh, qb);
   const int b = bh / Hq, h = bh % Hq;
   const int hk = h / (Hq / Hkv);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -255,6 +275,8 @@ __device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
 // NW waves per block (NW x 32 query rows). NW = 4 runs two independent blocks per CU (their
 // per-tile barriers drift apart, so one block's softmax overlaps the other's MFMAs); NW = 8 is
 // one block per CU.
+constexpr float RESCALE_TAU = 8.f;   // log2 units: deferred-rescale headroom (p <= 256)
+
 template <int NW>
 __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_fwd_d128_w8(const unsigned short* __restrict__ Q,
                                                             const unsigned short* __restrict__ K,
@@ -265,8 +287,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_fwd_d128_w8(const unsig
   constexpr int QR8 = 32 * NW, NT = NW * 64, LD = 1024 / NT;   // 16-B staging loads per thread (K or V)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nqb = (S + QR8 - 1) / QR8;
-  const int bh = blockIdx.x / nqb;
-  const int qb = causal ? (nqb - 1 - (int)(blockIdx.x % nqb)) : (int)(blockIdx.x % nqb);  // heaviest first
+  int bh, qb;
+  block_coords(nqb, B * Hq, causal, bh, qb);
   const int b = bh / Hq, h = bh % Hq;
   const int hk = h / (Hq / Hkv);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -342,6 +364,12 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_fwd_d128_w8(const unsig
         }
       }
       // ---- online softmax (base 2); masking only on diagonal / ragged tiles ----
+      // The max is taken on the raw scores (scale > 0) and the scale folded into one FMA per
+      // score: p = 2^(s * scale - m). Deferred rescale (T13): the running max m moves only when
+      // a tile's max exceeds it by more than RESCALE_TAU (p then stays <= 2^TAU, harmless in
+      // fp32 and in bf16's relative precision), so the 64-register O rescale and l's multiply
+      // run only on the few tiles where some row's max really grows — the decision is
+      // wave-uniform and O, l see the same factor, before this tile's P V.
       float tmax = -INFINITY;
       if constexpr (MASKED) {
 #pragma unroll
@@ -349,7 +377,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_fwd_d128_w8(const unsig
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int key = kfirst + 32 * st + (r & 3) + 8 * (r >> 2) + 4 * hh;
-            const float v = (key >= S || (causal && key > qi)) ? -INFINITY : s[st][r] * scale_log2;
+            const float v = (key >= S || (causal && key > qi)) ? -INFINITY : s[st][r];
             s[st][r] = v;
             tmax = fmaxf(tmax, v);
           }
@@ -357,28 +385,29 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_fwd_d128_w8(const unsig
 #pragma unroll
         for (int st = 0; st < 2; ++st)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            s[st][r] *= scale_log2;
-            tmax = fmaxf(tmax, s[st][r]);
-          }
+          for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, s[st][r]);
       }
-      tmax = pair_max(tmax);
-      const float mnew = fmaxf(m, tmax);
-      const float alpha = __builtin_amdgcn_exp2f(m - mnew);   // raw v_exp_f32 (exp2(-inf) = 0)
-      m = mnew;
+      tmax = pair_max(tmax) * scale_log2;
+      const bool grow = tmax > m + RESCALE_TAU;
+      if (__builtin_amdgcn_ballot_w64(grow)) {
+        const float mnew = grow ? tmax : m;
+        const float alpha = __builtin_amdgcn_exp2f(m - mnew);   // raw v_exp_f32 (exp2(-inf) = 0)
+        m = mnew;
+        l *= alpha;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] *= alpha;
+      }
+      const float mneg = -m;
       float psum = 0.f;
 #pragma unroll
       for (int st = 0; st < 2; ++st)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float pv = __builtin_amdgcn_exp2f(s[st][r] - mnew);
+          const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(s[st][r], scale_log2, mneg));
           s[st][r] = pv;
           psum += pv;
         }
-      psum = pair_sum(psum);
-      l = l * alpha + psum;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) o[i] *= alpha;
+      l += pair_sum(psum);
 
       // ---- O^T += V^T P^T over 4 k-steps of 16 keys ----
       const int g16 = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
@@ -487,7 +516,11 @@ GS_KERNEL_API int gs_flash_attn_fwd_bf16(const void* q, const void* k, const voi
   if (causal & 2)
     return D == 128 ? launch<128, false>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream)
                     : launch<64, false>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
-  if (D == 128 && g_attn_variant == 3)
+  // auto (measured on MI355X, tools/attn_sweep.py): the 8-wave block (256 query rows, K/V tiles
+  // shared by 8 waves) wins on full attention and long causal sequences; on short causal ones
+  // the 4-wave block's finer granularity (128 rows, two blocks per CU drifting apart) wins
+  const bool w8 = g_attn_variant == 3 || (g_attn_variant == 0 && (!(causal & 1) || S >= 4096));
+  if (D == 128 && w8)
     return launch_w8<8>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
   if (D == 128 && g_attn_variant != 1)
     return launch_w8<4>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
@@ -495,8 +528,9 @@ GS_KERNEL_API int gs_flash_attn_fwd_bf16(const void* q, const void* k, const voi
                   : launch<64, true>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
 }
 
-// Kernel selection for A/B measurement and tests: 0 = auto (32x32-MFMA 8-wave kernel for
-// D = 128), 1 = the 16x16 4-wave kernel.
+// Kernel selection for A/B measurement and tests: 0 = auto (32x32-MFMA kernels for D = 128:
+// 8-wave for full attention and causal S >= 4096, else 4-wave), 1 = the 16x16 4-wave kernel,
+// 2 = 32x32 4-wave, 3 = 32x32 8-wave.
 GS_KERNEL_API int gs_attn_set_variant(int v) {
   if (v < 0 || v > 3) return GS_EINVAL;
   g_attn_variant = v;
