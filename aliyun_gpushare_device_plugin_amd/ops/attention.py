@@ -12,8 +12,8 @@ ATTN_AUTO, ATTN_V1 = 0, 1
 
 
 def set_attention_variant(v: int) -> None:
-    """``ATTN_AUTO``: the 32x32-MFMA kernels for D = 128 (8-wave block for full attention and
-    causal S >= 4096, 4-wave otherwise; 16x16 kernel for D = 64);
+    """``ATTN_AUTO``: the 32x32-MFMA kernels for D = 128 (ping-pong 8-wave block for full
+    attention and causal S >= 2048, 4-wave otherwise; 16x16 kernel for D = 64);
     ``ATTN_V1``: always the 4-wave 16x16 kernel (A/B measurement, tests)."""
     _lib.check(_lib.lib().gs_attn_set_variant(int(v)), "gs_attn_set_variant")
 

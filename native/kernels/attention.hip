@@ -277,7 +277,14 @@ __device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
 // one block per CU.
 constexpr float RESCALE_TAU = 8.f;   // log2 units: deferred-rescale headroom (p <= 256)
 
-template <int NW>
+// FLAGS bit 0 (PRIO): the younger half of an 8-wave block runs at s_setprio 1 (it loses every
+// VALU arbitration to its older SIMD partner otherwise); bit 1 (LATE): tile t+2's global loads are
+// issued after QK^T(t) and written to LDS right after the next barrier (T14 split: the staging
+// registers are not live across QK^T), instead of loads at the tile's start and the LDS write
+// before its closing barrier.
+enum { AF_PRIO = 1, AF_LATE = 2 };
+
+template <int NW, int FLAGS = 0>
 __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_fwd_d128_w8(const unsigned short* __restrict__ Q,
                                                             const unsigned short* __restrict__ K,
                                                             const unsigned short* __restrict__ V,
@@ -295,6 +302,11 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_fwd_d128_w8(const unsig
   const int ql = lane & 31, hh = lane >> 5;
   const int q0 = qb * QR8 + wave * 32;
   const int qi = q0 + ql;
+  constexpr bool LATE = (FLAGS & AF_LATE) != 0;
+  if constexpr ((FLAGS & AF_PRIO) != 0 && NW == 8) {
+    // wave-uniform branch (readfirstlane), so the scalar s_setprio is guarded per wave
+    if (__builtin_amdgcn_readfirstlane(wave) >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  }
 
   // Q^T fragments (B operand): lane holds Q[qi][16 ds + 8 hh + j]
   bf16x8_t qf[8];
@@ -337,11 +349,21 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_fwd_d128_w8(const unsig
 
   load_tile(0);
   store_tile(0);
+  if (LATE && nkt > 1) load_tile(1);
   __syncthreads();
 
   for (int t = 0; t < nkt; ++t) {
     const int cur = t & 1;
-    if (t + 1 < nkt) load_tile(t + 1);
+    if constexpr (LATE) {
+      if (t + 1 < nkt) store_tile(cur ^ 1);     // tile t+1 (loaded during t-1): its buffer was freed by the barrier
+    } else {
+      if (t + 1 < nkt) load_tile(t + 1);
+    }
+    auto prefetch = [&]() {
+      if constexpr (LATE) {
+        if (t + 2 < nkt) load_tile(t + 2);
+      }
+    };
     const char* kb = smem + cur * STAGE8;
     const char* vb = kb + TILE8;
     const int kfirst = t * KT8;
@@ -363,6 +385,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_fwd_d128_w8(const unsig
           s[st] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ds], s[st], 0, 0, 0);
         }
       }
+      prefetch();
       // ---- online softmax (base 2); masking only on diagonal / ragged tiles ----
       // The max is taken on the raw scores (scale > 0) and the scale folded into one FMA per
       // score: p = 2^(s * scale - m). Deferred rescale (T13): the running max m moves only when
@@ -447,8 +470,10 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_fwd_d128_w8(const unsig
         body(BoolTag<true>{});
       else
         body(BoolTag<false>{});
+    } else {
+      prefetch();
     }
-    if (t + 1 < nkt) store_tile(cur ^ 1);
+    if (!LATE && t + 1 < nkt) store_tile(cur ^ 1);
     __syncthreads();
   }
 
@@ -468,18 +493,370 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_fwd_d128_w8(const unsig
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Ping-pong 8-wave kernel (D = 128): the two waves that share a SIMD run in antiphase.
+//
+// In the kernels above the 8 waves of a CU meet at one barrier per K/V tile and then all do the
+// same thing: QK^T (matrix pipe contended, VALU idle), softmax (VALU busy, matrix pipe idle), PV.
+// Here each wave software-pipelines its tile loop into two segments — an MFMA segment
+// M(j) = { O += V(j-1)^T P(j-1)^T ; S(j) = K(j) Q^T } (32 MFMAs) and a VALU segment
+// V(j) = { softmax(S(j)) -> P(j), O/l rescale } — and the younger half (waves 4-7) runs one
+// segment behind the older half (waves 0-3). One workgroup barrier closes every segment, so in
+// every segment each SIMD has one wave on the matrix pipe and its partner on the VALU:
+//
+//   global segment   0      1      2      3      4   ...
+//   waves 0-3        M(0)   V(0)   M(1)   V(1)   M(2)
+//   waves 4-7        -      M(0)   V(0)   M(1)   V(1)
+//
+// K(j) and V(j-1) are read during global segments 2j and 2j+1, so a 2-deep ring for K and one for
+// V (64 KiB) suffices. K(i+1) and V(i) arrive by LDS DMA (buffer_load ... lds, 1 KiB per wave
+// instruction, 2+2 per wave per tile) issued at the start of segment 2i into the buffers K(i-1) /
+// V(i-2) left after segment 2i-1, and are waited for (vmcnt) before the barrier closing segment
+// 2i+1 — two segments of latency cover, no staging registers, no LDS store instructions. The
+// XOR swizzles are applied on the source side (lane-linear LDS image). P(j) (16 packed registers)
+// carries from V(j) to M(j+1); S(j) (32) from M(j) to V(j). Inside M(j) the 32 MFMAs run in 4
+// groups (PV k-step g with 4 of QK's), each group's 8 V^T + 4 K fragment reads issued one group
+// ahead.
+template <bool PV, bool QK>
+struct MSegTag {
+  static constexpr bool pv = PV, qk = QK;
+};
+
+__global__ __launch_bounds__(512, 1) void flash_fwd_d128_pp(const unsigned short* __restrict__ Q,
+                                                           const unsigned short* __restrict__ K,
+                                                           const unsigned short* __restrict__ V,
+                                                           unsigned short* __restrict__ O, int B, int S, int Hq,
+                                                           int Hkv, int q_stride, int k_stride, int v_stride,
+                                                           float scale_log2, int causal) {
+  constexpr int NW = 8, QR8 = 32 * NW;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* const kbuf = smem;                 // K ring: 2 x TILE8
+  char* const vbuf = smem + 2 * TILE8;     // V ring: 2 x TILE8
+  const int nqb = (S + QR8 - 1) / QR8;
+  int bh, qb;
+  block_coords(nqb, B * Hq, causal, bh, qb);
+  const int b = bh / Hq, h = bh % Hq;
+  const int hk = h / (Hq / Hkv);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int half = wave >> 2;              // 0: waves 0-3, 1: waves 4-7
+  const int ql = lane & 31, hh = lane >> 5;
+  const int q0 = qb * QR8 + wave * 32;
+  const int qi = q0 + ql;
+
+  bf16x8_t qf[8];
+  {
+    const unsigned short* qp = Q + ((size_t)b * S + min(qi, S - 1)) * q_stride + (size_t)h * 128 + 8 * hh;
+#pragma unroll
+    for (int ds = 0; ds < 8; ++ds) qf[ds] = *(const bf16x8_t*)(qp + 16 * ds);
+  }
+  f32x16_t o[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
+  float m = -INFINITY, l = 0.f;
+  f32x16_t sacc[2];
+  bf16x8_t pf[4];
+
+  const int nkt_all = (S + KT8 - 1) / KT8;
+  const int nkt = causal ? min(nkt_all, (qb * QR8 + QR8 - 1) / KT8 + 1) : nkt_all;
+
+  // ---- LDS DMA: instruction i (0, 1) of wave w fills rows 32 i + 4 w + lane / 16 of a tile;
+  // lane's 16-B slot lane & 15 receives the logical chunk the swizzle puts there (the XOR terms
+  // depend on row & 15 / row & 3 only, the same for both i). Rows past S read as zeros (buffer
+  // range check); their scores are masked and their P is 0.
+  const int prow = 4 * wave + (lane >> 4);
+  const int kch = (lane & 15) ^ (prow & 15);
+  const int vch = (lane & 15) ^ ((prow & 3) << 2);
+  const __amdgpu_buffer_rsrc_t rK = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(K + (size_t)b * S * k_stride + (size_t)hk * 128), (short)0, S * k_stride * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rV = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(V + (size_t)b * S * v_stride + (size_t)hk * 128), (short)0, S * v_stride * 2, 0x00020000);
+  const unsigned voffK = (unsigned)(prow * k_stride + kch * 8) * 2u;
+  const unsigned voffV = (unsigned)(prow * v_stride + vch * 8) * 2u;
+  auto dma_k = [&](int t, int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rK, (__attribute__((address_space(3))) void*)(kbuf + buf * TILE8 + i * 8192 + wave * 1024), 16, voffK,
+          (t * KT8 + 32 * i) * k_stride * 2, 0, 0);
+  };
+  auto dma_v = [&](int t, int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rV, (__attribute__((address_space(3))) void*)(vbuf + buf * TILE8 + i * 8192 + wave * 1024), 16, voffV,
+          (t * KT8 + 32 * i) * v_stride * 2, 0, 0);
+  };
+  // a tile is live for this wave when some key of it is visible to some row of the wave
+  auto live = [&](int t) __attribute__((always_inline)) { return !causal || t * KT8 <= q0 + 31; };
+
+  // ---- M segment: 8 sub-groups of 4 MFMAs — PV k-step g (4 V^T fragments) alternating with
+  // QK quarter g (sub-tile g >> 1, d-steps 4 (g & 1) .. +3: 4 K fragments); each sub-group's
+  // 4 fragments (16 registers) are read one sub-group ahead
+  struct Frag {
+    bf16x8_t x[4];
+  };
+  auto mseg = [&](int jp, int jq, auto tag, auto after_reads) __attribute__((always_inline)) {
+    constexpr bool DO_PV = decltype(tag)::pv, DO_QK = decltype(tag)::qk;
+    constexpr int NSUB = (DO_PV ? 4 : 0) + (DO_QK ? 4 : 0);
+    // fragment addresses are recomputed here from an opaque copy of the lane id (a few VALU on
+    // an otherwise matrix-bound segment) instead of being hoisted out of the loop: 12 per-lane
+    // XOR offsets kept live across the loop spilled, and a spill reload's vmcnt(0) also waits
+    // for the in-flight K/V DMA
+    int lx = lane;
+    asm volatile("" : "+v"(lx));
+    const int g16 = lx >> 4, q4 = (lx & 15) >> 2, p4 = lx & 3, ql = lx & 31, hh = lx >> 5;
+    const char* vb = vbuf + (jp & 1) * TILE8;
+    const char* kb = kbuf + (jq & 1) * TILE8;
+    // sub-group u: PV step when (DO_PV and (u even or !DO_QK)), else QK quarter
+    auto is_pv = [&](int u) __attribute__((always_inline)) { return DO_PV && (!DO_QK || (u & 1) == 0); };
+    auto step = [&](int u) __attribute__((always_inline)) { return (DO_PV && DO_QK) ? (u >> 1) : u; };
+    auto rd = [&](Frag& f, int u) __attribute__((always_inline)) {
+      const int g = step(u);
+      if (is_pv(u)) {
+        const int r0 = 16 * g + 8 * (g16 >> 1) + q4, r1 = r0 + 4;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          const int unit = 8 * dt + 4 * (g16 & 1) + p4;
+          const v4s a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) v4s*)(vb + r0 * ROW8 + (v8swz(r0, unit) << 3)));
+          const v4s a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) v4s*)(vb + r1 * ROW8 + (v8swz(r1, unit) << 3)));
+          f.x[dt] = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7));
+        }
+      } else {
+        const int row = 32 * (g >> 1) + ql;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const int ds = 4 * (g & 1) + d;
+          f.x[d] = *(const bf16x8_t*)(kb + row * ROW8 + (k8swz(row, 2 * ds + hh) << 4));
+        }
+      }
+    };
+    auto mm = [&](const Frag& f, int u) __attribute__((always_inline)) {
+      const int g = step(u);
+      if (is_pv(u)) {
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.x[dt], pf[g], o[dt], 0, 0, 0);
+      } else {
+        const int st = g >> 1;
+        if ((g & 1) == 0) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) sacc[st][r] = 0.f;
+        }
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+          sacc[st] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.x[d], qf[4 * (g & 1) + d], sacc[st], 0, 0, 0);
+      }
+    };
+    Frag f[2];
+    rd(f[0], 0);
+#pragma unroll
+    for (int u = 0; u < NSUB; ++u) {
+      if (u + 1 < NSUB) rd(f[(u + 1) & 1], u + 1);
+      if (u + 2 == NSUB) {
+        // after the segment's last fragment read: the compiler makes every LDS read that
+        // follows an LDS DMA wait for it (vmcnt), so DMAs are issued behind the reads
+        __builtin_amdgcn_sched_barrier(0);
+        after_reads();
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      mm(f[u & 1], u);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  auto nop = [&]() __attribute__((always_inline)) {};
+  auto softmax = [&](int j, auto tag) __attribute__((always_inline)) {
+    constexpr bool MASKED = decltype(tag)::value;
+    const int kfirst = j * KT8;
+    float tmax = -INFINITY;
+    if constexpr (MASKED) {
+#pragma unroll
+      for (int st = 0; st < 2; ++st)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = kfirst + 32 * st + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          const float v = (key >= S || (causal && key > qi)) ? -INFINITY : sacc[st][r];
+          sacc[st][r] = v;
+          tmax = fmaxf(tmax, v);
+        }
+    } else {
+#pragma unroll
+      for (int st = 0; st < 2; ++st)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, sacc[st][r]);
+    }
+    tmax = pair_max(tmax) * scale_log2;
+    const bool grow = tmax > m + RESCALE_TAU;
+    if (__builtin_amdgcn_ballot_w64(grow)) {      // O is idle here: PV(j-1) finished in M(j)
+      const float mnew = grow ? tmax : m;
+      const float alpha = __builtin_amdgcn_exp2f(m - mnew);
+      m = mnew;
+      l *= alpha;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[i] *= alpha;
+    }
+    const float mneg = -m;
+    float psum = 0.f;
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float pvv = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[st][r], scale_log2, mneg));
+        sacc[st][r] = pvv;
+        psum += pvv;
+      }
+    l += pair_sum(psum);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int st = ks >> 1, rb = 8 * (ks & 1);
+      const unsigned lo0 = pack_bf16x2(sacc[st][rb + 0], sacc[st][rb + 1]);
+      const unsigned lo1 = pack_bf16x2(sacc[st][rb + 2], sacc[st][rb + 3]);
+      const unsigned hi0 = pack_bf16x2(sacc[st][rb + 4], sacc[st][rb + 5]);
+      const unsigned hi1 = pack_bf16x2(sacc[st][rb + 6], sacc[st][rb + 7]);
+      const auto w0 = __builtin_amdgcn_permlane32_swap(lo0, hi0, false, false);
+      const auto w1 = __builtin_amdgcn_permlane32_swap(lo1, hi1, false, false);
+      typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+      pf[ks] = __builtin_bit_cast(bf16x8_t, u32x4_t{w0[0], w1[0], w0[1], w1[1]});
+    }
+  };
+
+  auto dma_pair = [&](int i) __attribute__((always_inline)) {              // K(i+1), V(i) -> the buffers freed after segment 2i-1
+    if (i + 1 < nkt) dma_k(i + 1, (i + 1) & 1);
+    if (i < nkt) dma_v(i, i & 1);
+  };
+  // Segment barrier without __syncthreads' release/acquire fences: the release fence would make
+  // every barrier wait for this wave's in-flight LDS DMA (vmcnt(0)), which must instead overlap
+  // a whole segment. LDS reads are consumed (lgkmcnt) inside their segment, so the only
+  // ordering a barrier needs is the DMA one, waited for explicitly at odd segments; the empty
+  // asm with a memory clobber keeps the compiler from moving LDS accesses across it.
+  auto bar = [&]() __attribute__((always_inline)) {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::: "memory");
+  };
+  auto wait_sync = [&]() __attribute__((always_inline)) {   // closes an odd segment: this wave's DMAs landed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar();
+  };
+  auto needmask = [&](int j) __attribute__((always_inline)) { return (causal && j * KT8 + KT8 - 1 > q0) || j * KT8 + KT8 > S; };
+  auto smax_any = [&](int j) __attribute__((always_inline)) {
+    if (needmask(j))
+      softmax(j, BoolTag<true>{});
+    else
+      softmax(j, BoolTag<false>{});
+  };
+  // tiles 0 .. nlive-1 hold a key visible to this wave; only the last of them can need the mask
+  // (causal diagonal or ragged end). Later tiles are only staged and waited for, so both halves
+  // meet 2 nkt + 2 barriers with straight-line loop bodies (no per-segment branches whose merges
+  // made the compiler shuffle O and S between register sets).
+  const int nlive = causal ? min(nkt, (q0 + 31) / KT8 + 1) : nkt;
+
+  // ---- prologue: K(0) in LDS ----
+  dma_k(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  bar();
+
+  if (half == 0) {
+    // waves 0-3: M(j) in segment 2j, V(j) in segment 2j+1; DMA issued behind M(j)'s reads
+    mseg(0, 0, MSegTag<false, true>{}, [&]() __attribute__((always_inline)) { dma_pair(0); });
+    bar();
+    smax_any(0);
+    wait_sync();
+    int j = 1;
+    for (; j < nlive - 1; ++j) {
+      mseg(j - 1, j, MSegTag<true, true>{}, [&]() __attribute__((always_inline)) { dma_pair(j); });
+      bar();
+      softmax(j, BoolTag<false>{});
+      wait_sync();
+    }
+    if (j == nlive - 1) {
+      mseg(j - 1, j, MSegTag<true, true>{}, [&]() __attribute__((always_inline)) { dma_pair(j); });
+      bar();
+      smax_any(j);
+      wait_sync();
+      ++j;
+    }
+    mseg(j - 1, 0, MSegTag<true, false>{}, [&]() __attribute__((always_inline)) { dma_pair(j); });  // j == nlive
+    bar();
+    wait_sync();
+    for (++j; j <= nkt; ++j) {
+      dma_pair(j);
+      bar();
+      wait_sync();
+    }
+  } else {
+    // waves 4-7: V(j-1) in segment 2j, M(j) in segment 2j+1
+    dma_pair(0);
+    bar();
+    mseg(0, 0, MSegTag<false, true>{}, nop);
+    wait_sync();
+    int j = 1;
+    for (; j < nlive; ++j) {
+      dma_pair(j);
+      softmax(j - 1, BoolTag<false>{});        // j - 1 < nlive - 1: never masked
+      bar();
+      mseg(j - 1, j, MSegTag<true, true>{}, nop);
+      wait_sync();
+    }
+    dma_pair(j);                              // j == nlive: V(nlive-1), the last PV
+    smax_any(j - 1);
+    bar();
+    mseg(j - 1, 0, MSegTag<true, false>{}, nop);
+    wait_sync();
+    for (++j; j <= nkt; ++j) {
+      dma_pair(j);
+      bar();
+      wait_sync();
+    }
+  }
+
+  if (qi < S) {
+    const float inv = 1.f / l;
+    unsigned short* op = O + (((size_t)b * S + qi) * Hq + h) * 128 + 4 * hh;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        u16x4_t w;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) w[r] = f32_to_bf16(o[dt][4 * q + r] * inv);
+        *(u16x4_t*)(op + 32 * dt + 8 * q) = w;
+      }
+  }
+}
+
+int launch_pp(const void* q, const void* k, const void* v, void* o, int B, int S, int Hq, int Hkv, int qs, int ks,
+              int vs, float scale_log2, int causal, hipStream_t stream) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)flash_fwd_d128_pp, hipFuncAttributeMaxDynamicSharedMemorySize, LDS8);
+    attr = true;
+  }
+  const int nqb = (S + 255) / 256;
+  flash_fwd_d128_pp<<<dim3((unsigned)(B * Hq * nqb)), dim3(512), LDS8, stream>>>(
+      (const unsigned short*)q, (const unsigned short*)k, (const unsigned short*)v, (unsigned short*)o, B, S, Hq,
+      Hkv, qs, ks, vs, scale_log2, causal & 1);
+  return gs_launch_status();
+}
+
 int g_attn_variant = 0;   // 0 = auto, 1 = 16x16 4-wave kernel, 2 = 32x32 4-wave, 3 = 32x32 8-wave
 
-template <int NW>
+template <int NW, int FLAGS = 0>
 int launch_w8(const void* q, const void* k, const void* v, void* o, int B, int S, int Hq, int Hkv, int qs, int ks,
               int vs, float scale_log2, int causal, hipStream_t stream) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)flash_fwd_d128_w8<NW>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS8);
+    (void)hipFuncSetAttribute((const void*)flash_fwd_d128_w8<NW, FLAGS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS8);
     attr = true;
   }
   const int nqb = (S + 32 * NW - 1) / (32 * NW);
-  flash_fwd_d128_w8<NW><<<dim3((unsigned)(B * Hq * nqb)), dim3(NW * 64), LDS8, stream>>>(
+  flash_fwd_d128_w8<NW, FLAGS><<<dim3((unsigned)(B * Hq * nqb)), dim3(NW * 64), LDS8, stream>>>(
       (const unsigned short*)q, (const unsigned short*)k, (const unsigned short*)v, (unsigned short*)o, B, S, Hq,
       Hkv, qs, ks, vs, scale_log2, causal & 1);
   return gs_launch_status();
@@ -516,10 +893,19 @@ GS_KERNEL_API int gs_flash_attn_fwd_bf16(const void* q, const void* k, const voi
   if (causal & 2)
     return D == 128 ? launch<128, false>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream)
                     : launch<64, false>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
-  // auto (measured on MI355X, tools/attn_sweep.py): the 8-wave block (256 query rows, K/V tiles
-  // shared by 8 waves) wins on full attention and long causal sequences; on short causal ones
-  // the 4-wave block's finer granularity (128 rows, two blocks per CU drifting apart) wins
-  const bool w8 = g_attn_variant == 3 || (g_attn_variant == 0 && (!(causal & 1) || S >= 4096));
+  // auto (measured on MI355X, tools/attn_sweep.py): the ping-pong 8-wave block wins on full
+  // attention and causal S >= 2048 (1045 / 1069 TF/s at H 64 full / causal 8192); on short causal
+  // sequences the 4-wave block's finer granularity (128 rows, two blocks per CU) wins
+  const bool pp_ok = (size_t)S * k_stride * 2 < (1ull << 31) && (size_t)S * v_stride * 2 < (1ull << 31);
+  if (D == 128 && pp_ok && (g_attn_variant == 7 || (g_attn_variant == 0 && (!(causal & 1) || S >= 2048))))
+    return launch_pp(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
+  if (D == 128 && g_attn_variant == 4)
+    return launch_w8<8, AF_PRIO>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
+  if (D == 128 && g_attn_variant == 5)
+    return launch_w8<8, AF_LATE>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
+  if (D == 128 && g_attn_variant == 6)
+    return launch_w8<4, AF_LATE>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
+  const bool w8 = g_attn_variant == 3;
   if (D == 128 && w8)
     return launch_w8<8>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
   if (D == 128 && g_attn_variant != 1)
@@ -529,10 +915,11 @@ GS_KERNEL_API int gs_flash_attn_fwd_bf16(const void* q, const void* k, const voi
 }
 
 // Kernel selection for A/B measurement and tests: 0 = auto (32x32-MFMA kernels for D = 128:
-// 8-wave for full attention and causal S >= 4096, else 4-wave), 1 = the 16x16 4-wave kernel,
-// 2 = 32x32 4-wave, 3 = 32x32 8-wave.
+// ping-pong 8-wave for full attention and causal S >= 2048, else 4-wave), 1 = the 16x16 4-wave kernel,
+// 2 = 32x32 4-wave, 3 = 32x32 8-wave; experiments: 4 = 8-wave + younger-half priority, 5 = 8-wave
+// + late (T14) loads, 6 = 4-wave + late loads, 7 = ping-pong 8-wave.
 GS_KERNEL_API int gs_attn_set_variant(int v) {
-  if (v < 0 || v > 3) return GS_EINVAL;
+  if (v < 0 || v > 7) return GS_EINVAL;
   g_attn_variant = v;
   return GS_OK;
 }
