@@ -522,6 +522,13 @@ struct MSegTag {
   static constexpr bool pv = PV, qk = QK;
 };
 
+// PP_PRIO: the wave in its MFMA segment runs at s_setprio 1, so its MFMA / LDS issue wins the
+// arbitration against the partner's softmax VALU stream.
+// PP_ILV: SIMD partners take neighbouring 32-row slices (see q0 below) instead of rows 32 w and
+// 32 w + 128.
+enum { PP_PRIO = 1, PP_ILV = 2 };
+
+template <int FLAGS = 0>
 __global__ __launch_bounds__(512, 1) void flash_fwd_d128_pp(const unsigned short* __restrict__ Q,
                                                            const unsigned short* __restrict__ K,
                                                            const unsigned short* __restrict__ V,
@@ -541,7 +548,9 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_d128_pp(const unsigned short
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int half = wave >> 2;              // 0: waves 0-3, 1: waves 4-7
   const int ql = lane & 31, hh = lane >> 5;
-  const int q0 = qb * QR8 + wave * 32;
+  // rows: the SIMD partners (wave w of each half) take neighbouring 32-row slices, so under a
+  // causal mask both have (almost) the same number of live tiles and stay in antiphase to the end
+  const int q0 = qb * QR8 + ((FLAGS & PP_ILV) ? (wave & 3) * 64 + half * 32 : wave * 32);
   const int qi = q0 + ql;
 
   bf16x8_t qf[8];
@@ -651,6 +660,7 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_d128_pp(const unsigned short
           sacc[st] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.x[d], qf[4 * (g & 1) + d], sacc[st], 0, 0, 0);
       }
     };
+    if constexpr ((FLAGS & PP_PRIO) != 0) __builtin_amdgcn_s_setprio(1);
     Frag f[2];
     rd(f[0], 0);
 #pragma unroll
@@ -666,6 +676,7 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_d128_pp(const unsigned short
       mm(f[u & 1], u);
       __builtin_amdgcn_sched_barrier(0);
     }
+    if constexpr ((FLAGS & PP_PRIO) != 0) __builtin_amdgcn_s_setprio(0);
   };
   auto nop = [&]() __attribute__((always_inline)) {};
   auto softmax = [&](int j, auto tag) __attribute__((always_inline)) {
@@ -830,15 +841,16 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_d128_pp(const unsigned short
   }
 }
 
+template <int FLAGS = 0>
 int launch_pp(const void* q, const void* k, const void* v, void* o, int B, int S, int Hq, int Hkv, int qs, int ks,
               int vs, float scale_log2, int causal, hipStream_t stream) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)flash_fwd_d128_pp, hipFuncAttributeMaxDynamicSharedMemorySize, LDS8);
+    (void)hipFuncSetAttribute((const void*)flash_fwd_d128_pp<FLAGS>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS8);
     attr = true;
   }
   const int nqb = (S + 255) / 256;
-  flash_fwd_d128_pp<<<dim3((unsigned)(B * Hq * nqb)), dim3(512), LDS8, stream>>>(
+  flash_fwd_d128_pp<FLAGS><<<dim3((unsigned)(B * Hq * nqb)), dim3(512), LDS8, stream>>>(
       (const unsigned short*)q, (const unsigned short*)k, (const unsigned short*)v, (unsigned short*)o, B, S, Hq,
       Hkv, qs, ks, vs, scale_log2, causal & 1);
   return gs_launch_status();
@@ -897,8 +909,12 @@ GS_KERNEL_API int gs_flash_attn_fwd_bf16(const void* q, const void* k, const voi
   // attention and causal S >= 2048 (1045 / 1069 TF/s at H 64 full / causal 8192); on short causal
   // sequences the 4-wave block's finer granularity (128 rows, two blocks per CU) wins
   const bool pp_ok = (size_t)S * k_stride * 2 < (1ull << 31) && (size_t)S * v_stride * 2 < (1ull << 31);
+  if (D == 128 && pp_ok && g_attn_variant == 8)
+    return launch_pp<0>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
+  if (D == 128 && pp_ok && g_attn_variant == 9)
+    return launch_pp<PP_PRIO | PP_ILV>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
   if (D == 128 && pp_ok && (g_attn_variant == 7 || (g_attn_variant == 0 && (!(causal & 1) || S >= 2048))))
-    return launch_pp(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
+    return launch_pp<PP_PRIO>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
   if (D == 128 && g_attn_variant == 4)
     return launch_w8<8, AF_PRIO>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
   if (D == 128 && g_attn_variant == 5)
@@ -917,9 +933,10 @@ GS_KERNEL_API int gs_flash_attn_fwd_bf16(const void* q, const void* k, const voi
 // Kernel selection for A/B measurement and tests: 0 = auto (32x32-MFMA kernels for D = 128:
 // ping-pong 8-wave for full attention and causal S >= 2048, else 4-wave), 1 = the 16x16 4-wave kernel,
 // 2 = 32x32 4-wave, 3 = 32x32 8-wave; experiments: 4 = 8-wave + younger-half priority, 5 = 8-wave
-// + late (T14) loads, 6 = 4-wave + late loads, 7 = ping-pong 8-wave.
+// + late (T14) loads, 6 = 4-wave + late loads, 7 = ping-pong 8-wave (MFMA-segment priority), 8 = ping-pong
+// without the priority, 9 = ping-pong + interleaved partner rows (measured 1-3 % slower).
 GS_KERNEL_API int gs_attn_set_variant(int v) {
-  if (v < 0 || v > 7) return GS_EINVAL;
+  if (v < 0 || v > 9) return GS_EINVAL;
   g_attn_variant = v;
   return GS_OK;
 }
