@@ -27,6 +27,7 @@ SIGNATURES = {
     "gs_rope_bf16": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "gs_flash_attn_fwd_bf16": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _F, _I, _P],
     "gs_attn_set_variant": [_I],
+    "gs_attn_trace": [_P, _I],
     "gs_cu_census": [_P, _I, _I, _P],
     "gs_decode_attn_bf16": [_P, _I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _F, _P],
     "gs_kv_append_bf16": [_P, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P],

@@ -526,7 +526,11 @@ struct MSegTag {
 // arbitration against the partner's softmax VALU stream.
 // PP_ILV: SIMD partners take neighbouring 32-row slices (see q0 below) instead of rows 32 w and
 // 32 w + 128.
-enum { PP_PRIO = 1, PP_ILV = 2 };
+// PP_TRACE (diagnostics, tools/attn_trace.py): block 0's waves record s_memtime before and after
+// every segment barrier into g_pp_trace (vector stores from lane 0).
+enum { PP_PRIO = 1, PP_ILV = 2, PP_TRACE = 4 };
+constexpr int PP_TRACE_SEGS = 160;
+__device__ unsigned long long g_pp_trace[8][PP_TRACE_SEGS][2];
 
 template <int FLAGS = 0>
 __global__ __launch_bounds__(512, 1) void flash_fwd_d128_pp(const unsigned short* __restrict__ Q,
@@ -709,6 +713,9 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_d128_pp(const unsigned short
 #pragma unroll
       for (int i = 0; i < 4; ++i) o[i] *= alpha;
     }
+    // the softmax segment is the long pole of the ping-pong pair (tools/attn_trace.py). Packed
+    // v_pk_fma/v_pk_add here slowed the partner's MFMA segment by ~600 cycles (measured), and
+    // 4 independent sum/max chains did not shorten the segment: plain single ops, one chain
     const float mneg = -m;
     float psum = 0.f;
 #pragma unroll
@@ -743,12 +750,21 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_d128_pp(const unsigned short
   // a whole segment. LDS reads are consumed (lgkmcnt) inside their segment, so the only
   // ordering a barrier needs is the DMA one, waited for explicitly at odd segments; the empty
   // asm with a memory clobber keeps the compiler from moving LDS accesses across it.
+  int tseg = 0;
+  const bool tracer = (FLAGS & PP_TRACE) && blockIdx.x == 0 && lane == 0;
   auto bar = [&]() __attribute__((always_inline)) {
+    if constexpr ((FLAGS & PP_TRACE) != 0) {
+      if (tracer && tseg < PP_TRACE_SEGS) g_pp_trace[wave][tseg][0] = __builtin_amdgcn_s_memtime();
+    }
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("" ::: "memory");
+    if constexpr ((FLAGS & PP_TRACE) != 0) {
+      ++tseg;
+      if (tracer && tseg < PP_TRACE_SEGS) g_pp_trace[wave][tseg][1] = __builtin_amdgcn_s_memtime();
+    }
   };
   auto wait_sync = [&]() __attribute__((always_inline)) {   // closes an odd segment: this wave's DMAs landed
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -911,6 +927,8 @@ GS_KERNEL_API int gs_flash_attn_fwd_bf16(const void* q, const void* k, const voi
   const bool pp_ok = (size_t)S * k_stride * 2 < (1ull << 31) && (size_t)S * v_stride * 2 < (1ull << 31);
   if (D == 128 && pp_ok && g_attn_variant == 8)
     return launch_pp<0>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
+  if (D == 128 && pp_ok && g_attn_variant == 10)
+    return launch_pp<PP_PRIO | PP_TRACE>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
   if (D == 128 && pp_ok && g_attn_variant == 9)
     return launch_pp<PP_PRIO | PP_ILV>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
   if (D == 128 && pp_ok && (g_attn_variant == 7 || (g_attn_variant == 0 && (!(causal & 1) || S >= 2048))))
@@ -934,9 +952,17 @@ GS_KERNEL_API int gs_flash_attn_fwd_bf16(const void* q, const void* k, const voi
 // ping-pong 8-wave for full attention and causal S >= 2048, else 4-wave), 1 = the 16x16 4-wave kernel,
 // 2 = 32x32 4-wave, 3 = 32x32 8-wave; experiments: 4 = 8-wave + younger-half priority, 5 = 8-wave
 // + late (T14) loads, 6 = 4-wave + late loads, 7 = ping-pong 8-wave (MFMA-segment priority), 8 = ping-pong
-// without the priority, 9 = ping-pong + interleaved partner rows (measured 1-3 % slower).
+// without the priority, 9 = ping-pong + interleaved partner rows (measured 1-3 % slower), 10 = ping-pong with the
+// segment trace (gs_attn_trace).
 GS_KERNEL_API int gs_attn_set_variant(int v) {
-  if (v < 0 || v > 9) return GS_EINVAL;
+  if (v < 0 || v > 10) return GS_EINVAL;
   g_attn_variant = v;
   return GS_OK;
+}
+
+// Segment trace of the last variant-10 launch: out[8 waves][PP_TRACE_SEGS][2] s_memtime stamps
+// (0: before the barrier closing segment k, 1: after the barrier opening segment k).
+GS_KERNEL_API int gs_attn_trace(unsigned long long* out, int n) {
+  if (n < 8 * PP_TRACE_SEGS * 2) return GS_EINVAL;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pp_trace), sizeof(g_pp_trace)) == hipSuccess ? GS_OK : GS_EINVAL;
 }

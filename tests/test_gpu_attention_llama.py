@@ -22,10 +22,13 @@ def test_flash_attention_matches_fp32(B, S, Hq, Hkv, D, causal):
 
 @pytest.mark.parametrize("B,S,Hq,Hkv,causal", [(1, 64, 4, 4, True), (2, 300, 8, 2, True), (1, 1000, 32, 8, True),
                                                 (2, 520, 4, 1, False), (1, 2048, 8, 8, True), (3, 17, 2, 2, True),
-                                                (1, 4160, 8, 2, True), (3, 700, 6, 3, False)])
+                                                (1, 4160, 8, 2, True), (3, 700, 6, 3, False),
+                                                (2, 1024, 8, 2, False), (1, 2048, 16, 8, False)])
 def test_attention_kernels_agree_with_fp32(B, S, Hq, Hkv, causal):
-    """D = 128: auto, the 4-wave 16x16 kernel, and the 4- and 8-wave 32x32-MFMA kernels, vs fp32
-    (head counts with and without the XCD-grouped block order: B*Hq % 8 == 0 or not)."""
+    """D = 128: auto, the 4-wave 16x16 kernel, the 4- and 8-wave 32x32-MFMA kernels and the
+    ping-pong variants, vs fp32 (head counts with and without the XCD-grouped block order:
+    B*Hq % 8 == 0 or not; S a multiple of the 64-key tile or ragged, so both the masked and the
+    unmasked path run on every kernel's last tile)."""
     from aliyun_gpushare_device_plugin_amd.ops import attention, reference_attention
     from aliyun_gpushare_device_plugin_amd.ops.attention import ATTN_AUTO, ATTN_V1, set_attention_variant
     torch.manual_seed(1)
