@@ -11,13 +11,18 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("G", [1, 2, 4, 8])
 def test_decode_attention_matches_fp32(G):
+    """vs fp32; cache rows past each sequence hold NaN (stale or never-written rows must not leak
+    into the result)."""
     torch.manual_seed(G)
     B, Hkv, D = 3, 2, 128
     kc, vc = ops.kv_cache(B, Hkv, 1000, D)                 # Smax rounds up to 1024
     assert kc.shape[2] == 1024
     kc.normal_()
     vc.normal_()
-    lens = torch.tensor([1, 300, 1024], dtype=torch.int32, device="cuda")
+    lens = torch.tensor([1, 300, 1000], dtype=torch.int32, device="cuda")
+    for b, n in enumerate(lens.tolist()):
+        kc[b, :, n:] = float("nan")
+        vc[b, :, n:] = float("nan")
     wide = torch.randn(B, G * Hkv * D + 256, device="cuda", dtype=torch.bfloat16)   # q as a strided slice
     q = wide[:, 128:128 + G * Hkv * D]
     out = ops.decode_attention(q, kc, vc, lens)
