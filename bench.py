@@ -416,6 +416,7 @@ class PodFleet:
         if not self.visible_by_uuid:                    # modelled node (fake SMI): this rank's GPU
             env.pop("ROCR_VISIBLE_DEVICES", None)
             env["HIP_VISIBLE_DEVICES"] = str(self.local)
+        self._wait_room(int(env.get("GPUSHARE_QUOTA_BYTES", 0)) * self.fill)
         t0 = time.perf_counter()
         w["proc"].stdin.write(json.dumps({"cmd": "start", "env": env, "gemm": self.gemm, "burst": self.burst,
                                           "fill": self.fill}) + "\n")
@@ -426,6 +427,16 @@ class PodFleet:
         self.held_bytes += ev.get("held", 0)
         self.ready_ms.append(dt)
         return dt
+
+    def _wait_room(self, nbytes: float, limit_s: float = 30.0) -> None:
+        """Before a pod starts: the GPU must physically have room for what it will hold. Inside the
+        churn the stop path already waited; this covers the fill, e.g. right after a previous run
+        on the same GPU whose freed HBM amdgpu is still wiping (~33 GB/s, seconds for a full GPU)."""
+        if self._vram_used is None or nbytes <= 0:
+            return
+        deadline = time.perf_counter() + limit_s
+        while self._vram_total - self._vram_used() < nbytes + (2 << 30) and time.perf_counter() < deadline:
+            time.sleep(0.01)
 
     def stop(self, uid: str, wait_release: bool = True):
         w = self.pods.pop(uid, None)
