@@ -97,8 +97,10 @@ class LlamaServer:
             ops.rope_kv_append(qkv, m.cos, m.sin, self.pos, self.kc[i], self.vc[i], c.n_heads)
             a = ops.decode_attention(qkv[:, :hq], self.kc[i], self.vc[i], self.lens, self.ws)
             h, x = self._mm_norm(a, L["wo"], h, L["mlp_norm"])
-            gu = self._mm(x, L["wgu"])                                  # gate/up rows interleaved by 16
-            act = ops.silu_mul(gu, interleaved=True)
+            act = ops.skinny_swiglu(x, L["wgu"]) if self.gemm == "skinny" else None   # SwiGLU in the epilogue
+            if act is None:
+                gu = self._mm(x, L["wgu"])                              # gate/up rows interleaved by 16
+                act = ops.silu_mul(gu, interleaved=True)
             nxt = m.layers[i + 1]["attn_norm"] if i + 1 < len(m.layers) else m.final_norm
             h, x = self._mm_norm(act, L["wd"], h, nxt)
         logits = self._mm(x, m.lm_head)

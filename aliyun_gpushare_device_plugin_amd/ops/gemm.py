@@ -240,3 +240,26 @@ def skinny_linear(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | Non
                                     N, float(eps), _lib.stream_ptr(x.device))
     _lib.check(rc, "gs_skinny_gemm_norm_bf16")
     return out, xn
+
+
+def skinny_swiglu(x: torch.Tensor, w_il: torch.Tensor) -> torch.Tensor | None:
+    """Decode MLP up-projection with the SwiGLU fused into the skinny GEMM's epilogue:
+    ``silu(x @ gate.T) * (x @ up.T)`` for ``w_il`` ``[2F, K]`` in the ``interleave_gate_up``
+    layout, one launch, ``[M, F]`` out. Returns ``None`` where the shape needs split-K (narrow
+    weights): the caller then runs ``skinny_linear`` + ``silu_mul(interleaved=True)``."""
+    _check_operand(x, "x")
+    _check_operand(w_il, "w_il")
+    if x.dim() != 2 or w_il.dim() != 2 or x.shape[1] != w_il.shape[1]:
+        raise ValueError("skinny_swiglu: x [M, K] and w_il [2F, K] expected")
+    M, K = x.shape
+    F = w_il.shape[0] // 2
+    if x.stride(0) % 8 or w_il.stride(0) % 8 or x.data_ptr() % 16 or w_il.data_ptr() % 16:
+        raise ValueError("skinny_swiglu: rows must be 16-byte aligned")
+    y = torch.empty((M, F), dtype=torch.bfloat16, device=x.device)
+    rc = _lib.lib().gs_skinny_swiglu_bf16(x.data_ptr(), x.stride(0), w_il.data_ptr(), w_il.stride(0), y.data_ptr(),
+                                          F, M, F, K, _lib.stream_ptr(x.device))
+    if rc == 1:            # GS_EINVAL: shape outside the fused path
+        return None
+    _lib.check(rc, "gs_skinny_swiglu_bf16")
+    return y
+

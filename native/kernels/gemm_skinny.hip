@@ -130,7 +130,11 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_nt(const unsigned short* __
 // measurement.
 constexpr int LBN = 64, LBK = 256, LROW = LBK + 8;
 
-template <int MT, int NW>
+// SWIGLU: W rows are gate/up interleaved by 16 (ops.interleave_gate_up), so even waves hold the
+// gate and odd waves the up projection of the same 16 features; the unsplit epilogue writes
+// Y[m, f] = silu(gate) * up (ldy = the F = N / 2 features) through LDS, and the separate
+// SiLU·up kernel (one launch and a [M, N] round trip per layer) goes away.
+template <int MT, int NW, bool SWIGLU = false>
 __global__ __launch_bounds__(NW * 64) void skinny_lds(const unsigned short* __restrict__ X, int ldx,
                                                   const unsigned short* __restrict__ W, int ldw,
                                                   float* __restrict__ part, unsigned short* __restrict__ Y,
@@ -190,6 +194,30 @@ __global__ __launch_bounds__(NW * 64) void skinny_lds(const unsigned short* __re
   }
 
   const int nb = n0 + 16 * wave + (lane >> 4) * 4;
+  if constexpr (SWIGLU) {
+    // the last k-slice's barrier has passed: sW is free. Even waves park their gate tile there.
+    float* gt = (float*)sW;                                // [NW / 2][MT * 16][16] floats
+    const int pair = wave >> 1, c = (lane >> 4) * 4;
+    if ((wave & 1) == 0) {
+#pragma unroll
+      for (int t = 0; t < MT; ++t) *(f32x4_t*)(gt + (pair * MT * 16 + t * 16 + r16) * 16 + c) = acc[t];
+    }
+    __syncthreads();
+    if (wave & 1) {
+      const int f = (n0 >> 1) + 16 * pair + c;             // output feature of this lane's 4 columns
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        const int m = t * 16 + r16;
+        if (m >= M) continue;
+        const f32x4_t g = *(const f32x4_t*)(gt + (pair * MT * 16 + t * 16 + r16) * 16 + c);
+        u16x4_t o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = f32_to_bf16(g[r] / (1.f + __expf(-g[r])) * acc[t][r]);
+        *(u16x4_t*)(Y + (size_t)m * ldy + f) = o;
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int t = 0; t < MT; ++t) {
     const int m = t * 16 + r16;
@@ -443,3 +471,30 @@ GS_KERNEL_API int gs_skinny_gemm_norm_bf16(const void* X, int ldx, const void* W
   if (!nw || !xn || N > 8192 || ldy % 8 || ldxn % 8 || ldxn < N) return GS_EINVAL;
   return skinny_launch(X, ldx, W, ldw, Y, R, ldy, M, N, K, splits, part, nw, xn, ldxn, eps, stream);
 }
+
+// Y[M, F] = silu(X W_gate^T) * (X W_up^T) for W [2F, K] gate/up interleaved by 16 rows
+// (ops.interleave_gate_up): one launch, LDS kernel, unsplit (W wide enough: 2F / 64 >= 256
+// workgroups, i.e. F >= 8192; narrower shapes return GS_EINVAL and the caller runs GEMM + SiLU·up).
+GS_KERNEL_API int gs_skinny_swiglu_bf16(const void* X, int ldx, const void* W, int ldw, void* Y, int ldy, int M,
+                                        int F, int K, hipStream_t stream) {
+  const int N = 2 * F;
+  int splits;
+  if (M < 1 || M > 64 || F % 32 || K % LBK || K <= 0 || ldx % 8 || ldw % 8 || ldy % 4 || ldx < K || ldw < K ||
+      ldy < F || !use_lds(K) || lds_waves(N) != 4)
+    return GS_EINVAL;
+  plan_lds(N, K, splits);
+  if (splits != 1) return GS_EINVAL;
+  const dim3 grid(N / 64, 1);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, (const unsigned short*)X, ldx, (const unsigned short*)W, ldw,
+                       (float*)nullptr, (unsigned short*)Y, (const unsigned short*)nullptr, ldy, M, N, K, K);
+  };
+  switch ((M + 15) / 16) {
+    case 1: go(skinny_lds<1, 4, true>); break;
+    case 2: go(skinny_lds<2, 4, true>); break;
+    case 3: go(skinny_lds<3, 4, true>); break;
+    default: go(skinny_lds<4, 4, true>); break;
+  }
+  return gs_launch_status();
+}
+

@@ -170,3 +170,21 @@ def test_skinny_linear_fused_rmsnorm(K):
     assert h.data_ptr() == r.data_ptr()
     assert (h.float() - want_h.float()).abs().max().item() <= 1e-2 * want_h.float().abs().max().item()
     assert (xn.float() - want_x.float()).abs().max().item() < 3e-2
+
+
+@pytest.mark.parametrize("M", [1, 17, 32, 64])
+def test_skinny_swiglu_matches_fp32(M):
+    """SwiGLU fused into the skinny GEMM's epilogue (interleaved gate/up weights) vs fp32."""
+    from aliyun_gpushare_device_plugin_amd.ops.gemm import interleave_gate_up
+    torch.manual_seed(M)
+    F, K = 8192, 1024
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    g = torch.randn(F, K, device="cuda", dtype=torch.bfloat16) * 0.05
+    u = torch.randn(F, K, device="cuda", dtype=torch.bfloat16) * 0.05
+    y = ops.skinny_swiglu(x, interleave_gate_up(torch.cat((g, u), 0)))
+    assert y is not None and y.shape == (M, F)
+    ref = torch.nn.functional.silu(x.float() @ g.float().t()) * (x.float() @ u.float().t())
+    err = (y.float() - ref).abs().max().item()
+    assert err < 2e-2 * ref.abs().max().item() + 1e-3, err
+    assert ops.skinny_swiglu(x, interleave_gate_up(torch.cat((g[:512], u[:512]), 0))) is None   # split-K shape
+
