@@ -31,6 +31,13 @@ class LlamaServer:
             raise ValueError("gemm must be 'skinny' (batch <= 64) or 'hipblaslt'")
         self.gemm = gemm
         self.fuse_norm = False
+        # RMSNorm folded across the projections (skinny path): the o / down projections' split
+        # reduction emits row sums of squares and the next projection normalises while staging
+        # its input, so no norm kernel runs between them
+        self.fold_norm = (gemm == "skinny" and ops.skinny_ssq_ok(c.d_model, c.n_heads * c.head_dim)
+                          and ops.skinny_ssq_ok(c.d_model, c.d_ff))
+        self.ssq = (torch.zeros((c.d_model // 1024, batch), dtype=torch.float32, device=model.device)
+                    if self.fold_norm else None)
         if max_ctx > c.max_seq:
             raise ValueError("max_ctx exceeds the RoPE table (cfg.max_seq)")
         self.model, self.B = model, batch
@@ -76,10 +83,20 @@ class LlamaServer:
             return ops.skinny_linear(x, w, residual=residual, out=residual)
         return torch.matmul(x, w.t()) if residual is None else torch.addmm(residual, x, w.t())
 
+    def _mm_in(self, x, w):
+        """Projection of a layer input that may be a deferred norm ``(h, norm_w)``."""
+        if isinstance(x, tuple):
+            h, nw = x
+            return ops.skinny_linear(h, w, norm=(self.ssq, nw, self.cfg.eps))
+        return self._mm(x, w)
+
     def _mm_norm(self, x, w, residual, norm_w):
         """``h = residual + x @ w.T`` (in place) and ``rmsnorm(h) * norm_w``. ``fuse_norm`` folds the
         norm into the skinny GEMM's split reduction; measured on MI355X it saves nothing at batch
         32 (5.62 vs 5.57 ms per step: the fused pass runs one workgroup per row), so it is off."""
+        if self.fold_norm:
+            h = ops.skinny_linear(x, w, residual=residual, out=residual, ssq_out=self.ssq)
+            return h, (h, norm_w)                      # the norm is applied by the consumer
         if self.gemm == "skinny" and self.fuse_norm:
             return ops.skinny_linear(x, w, residual=residual, out=residual, norm_weight=norm_w, eps=self.cfg.eps)
         h = self._mm(x, w, residual)
@@ -93,17 +110,20 @@ class LlamaServer:
         h = m.embed.index_select(0, self.tok)                          # residual stream [B, d]
         x = ops.rmsnorm(h, m.layers[0]["attn_norm"], c.eps)
         for i, L in enumerate(m.layers):
-            qkv = self._mm(x, L["wqkv"])
+            qkv = self._mm_in(x, L["wqkv"])
             ops.rope_kv_append(qkv, m.cos, m.sin, self.pos, self.kc[i], self.vc[i], c.n_heads)
             a = ops.decode_attention(qkv[:, :hq], self.kc[i], self.vc[i], self.lens, self.ws)
             h, x = self._mm_norm(a, L["wo"], h, L["mlp_norm"])
-            act = ops.skinny_swiglu(x, L["wgu"]) if self.gemm == "skinny" else None   # SwiGLU in the epilogue
+            act = None
+            if self.gemm == "skinny":                                   # SwiGLU in the epilogue
+                act = (ops.skinny_swiglu(x[0], L["wgu"], norm=(self.ssq, x[1], c.eps)) if isinstance(x, tuple)
+                       else ops.skinny_swiglu(x, L["wgu"]))
             if act is None:
-                gu = self._mm(x, L["wgu"])                              # gate/up rows interleaved by 16
+                gu = self._mm_in(x, L["wgu"])                           # gate/up rows interleaved by 16
                 act = ops.silu_mul(gu, interleaved=True)
             nxt = m.layers[i + 1]["attn_norm"] if i + 1 < len(m.layers) else m.final_norm
             h, x = self._mm_norm(act, L["wd"], h, nxt)
-        logits = self._mm(x, m.lm_head)
+        logits = self._mm_in(x, m.lm_head)
         self.tok.copy_(logits.argmax(-1))
         self.pos.add_(1)
         return logits

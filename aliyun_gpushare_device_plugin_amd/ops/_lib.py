@@ -34,6 +34,8 @@ SIGNATURES = {
     "gs_skinny_gemm_bf16": [_P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P, _P],
     "gs_skinny_splits": [_I, _I],
     "gs_skinny_swiglu_bf16": [_P, _I, _P, _I, _P, _I, _I, _I, _I, _P],
+    "gs_skinny_set_opts": [_P, _P, _P, _I, _F],
+    "gs_skinny_clear_opts": [],
     "gs_skinny_gemm_norm_bf16": [_P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _I, _F, _P],
     "gs_rope_kv_append_bf16": [_P, _I, _P, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "gs_silu_mul_il_bf16": [_P, _P, _I, _I, _P],

@@ -196,13 +196,59 @@ def set_skinny_variant(v: int) -> None:
     _lib.check(_lib.lib().gs_skinny_set_variant(int(v)), "gs_skinny_set_variant")
 
 
+def skinny_ssq_ok(N: int, K: int) -> bool:
+    """Whether ``skinny_linear(..., ssq_out=...)`` can emit row sums of squares for an ``[N, K]``
+    weight: the split reduction writes them, so the shape must split and N % 1024 == 0."""
+    return N % 1024 == 0 and K % 256 == 0 and _lib.lib().gs_skinny_splits(N, K) > 1
+
+
+class _SkinnyOpts:
+    """Per-launch options of the native skinny GEMM (set just before the call, cleared after)."""
+
+    def __init__(self, ssq_out=None, norm=None):
+        self.ssq_out, self.norm = ssq_out, norm
+
+    def __enter__(self):
+        if self.ssq_out is None and self.norm is None:
+            return self
+        ssq, w, eps = self.norm if self.norm is not None else (None, None, 0.0)
+        nch = ssq.shape[0] if ssq is not None else 0
+        _lib.check(_lib.lib().gs_skinny_set_opts(self.ssq_out.data_ptr() if self.ssq_out is not None else None,
+                                                 ssq.data_ptr() if ssq is not None else None,
+                                                 w.data_ptr() if w is not None else None, nch, float(eps)),
+                   "gs_skinny_set_opts")
+        return self
+
+    def __exit__(self, *exc):
+        if self.ssq_out is not None or self.norm is not None:
+            _lib.lib().gs_skinny_clear_opts()
+
+
+def _check_norm(norm, M: int, K: int):
+    if norm is None:
+        return
+    ssq, w, _ = norm
+    if ssq.dtype != torch.float32 or ssq.dim() != 2 or ssq.shape[1] != M or not ssq.is_contiguous():
+        raise ValueError("norm: ssq must be contiguous float32 [chunks, M]")
+    _check_operand(w, "norm weight")
+    if w.shape != (K,) or not w.is_contiguous():
+        raise ValueError("norm: weight must be contiguous [K]")
+
+
 def skinny_linear(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | None = None,
-                  out: torch.Tensor | None = None, norm_weight: torch.Tensor | None = None, eps: float = 1e-5):
+                  out: torch.Tensor | None = None, norm_weight: torch.Tensor | None = None, eps: float = 1e-5,
+                  ssq_out: torch.Tensor | None = None, norm: tuple | None = None):
     """Decode-shaped ``x @ w.T (+ residual)`` for ``x`` ``[M <= 64, K]`` on the split-K skinny
     kernel (native/kernels/gemm_skinny.hip): an HBM stream over ``w`` with the batch as the MFMA's
     16-row operand. ``out`` may be ``residual`` itself (in-place residual add). With
     ``norm_weight`` it returns ``(out, rmsnorm(out) * norm_weight)``, the norm computed in the same
-    pass that reduces the K splits (one launch less per residual projection)."""
+    pass that reduces the K splits (one launch less per residual projection).
+
+    Folded RMSNorm across two projections: ``ssq_out`` (float32 ``[N / 1024, M]``, see
+    ``skinny_ssq_ok``) makes this call's split reduction also write the row sums of squares of the
+    stored output; a later call with ``norm=(ssq, weight, eps)`` and ``x`` = that output multiplies
+    by ``weight`` and ``rsqrt(mean + eps)`` while staging ``x`` — ``rmsnorm(x) * weight`` without a
+    norm kernel in between."""
     _check_operand(x, "x")
     _check_operand(w, "w")
     if x.dim() != 2 or w.dim() != 2 or x.shape[1] != w.shape[1]:
@@ -226,11 +272,20 @@ def skinny_linear(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | Non
     splits = L.gs_skinny_splits(N, K)
     part = torch.empty(splits * M * N, dtype=torch.float32, device=x.device) if splits > 1 else None
     pptr = part.data_ptr() if part is not None else None
+    if ssq_out is not None:
+        if norm_weight is not None or not skinny_ssq_ok(N, K):
+            raise ValueError("skinny_linear: ssq_out needs a split shape with N % 1024 == 0 and no norm_weight")
+        if ssq_out.dtype != torch.float32 or tuple(ssq_out.shape) != (N // 1024, M) or not ssq_out.is_contiguous():
+            raise ValueError("skinny_linear: ssq_out must be contiguous float32 [N / 1024, M]")
+    _check_norm(norm, M, K)
     if norm_weight is None:
-        rc = L.gs_skinny_gemm_bf16(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), rptr,
-                                   out.stride(0), M, N, K, splits, pptr, _lib.stream_ptr(x.device))
+        with _SkinnyOpts(ssq_out, norm):
+            rc = L.gs_skinny_gemm_bf16(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), rptr,
+                                       out.stride(0), M, N, K, splits, pptr, _lib.stream_ptr(x.device))
         _lib.check(rc, "gs_skinny_gemm_bf16")
         return out
+    if norm is not None:
+        raise ValueError("skinny_linear: norm and norm_weight are exclusive")
     _check_operand(norm_weight, "norm_weight")
     if norm_weight.shape != (N,) or not norm_weight.is_contiguous() or N > 8192 or out.stride(0) % 8:
         raise ValueError("skinny_linear: norm_weight must be contiguous [N] with N <= 8192")
@@ -242,7 +297,7 @@ def skinny_linear(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | Non
     return out, xn
 
 
-def skinny_swiglu(x: torch.Tensor, w_il: torch.Tensor) -> torch.Tensor | None:
+def skinny_swiglu(x: torch.Tensor, w_il: torch.Tensor, norm: tuple | None = None) -> torch.Tensor | None:
     """Decode MLP up-projection with the SwiGLU fused into the skinny GEMM's epilogue:
     ``silu(x @ gate.T) * (x @ up.T)`` for ``w_il`` ``[2F, K]`` in the ``interleave_gate_up``
     layout, one launch, ``[M, F]`` out. Returns ``None`` where the shape needs split-K (narrow
@@ -255,9 +310,11 @@ def skinny_swiglu(x: torch.Tensor, w_il: torch.Tensor) -> torch.Tensor | None:
     F = w_il.shape[0] // 2
     if x.stride(0) % 8 or w_il.stride(0) % 8 or x.data_ptr() % 16 or w_il.data_ptr() % 16:
         raise ValueError("skinny_swiglu: rows must be 16-byte aligned")
+    _check_norm(norm, M, K)
     y = torch.empty((M, F), dtype=torch.bfloat16, device=x.device)
-    rc = _lib.lib().gs_skinny_swiglu_bf16(x.data_ptr(), x.stride(0), w_il.data_ptr(), w_il.stride(0), y.data_ptr(),
-                                          F, M, F, K, _lib.stream_ptr(x.device))
+    with _SkinnyOpts(None, norm):
+        rc = _lib.lib().gs_skinny_swiglu_bf16(x.data_ptr(), x.stride(0), w_il.data_ptr(), w_il.stride(0),
+                                              y.data_ptr(), F, M, F, K, _lib.stream_ptr(x.device))
     if rc == 1:            # GS_EINVAL: shape outside the fused path
         return None
     _lib.check(rc, "gs_skinny_swiglu_bf16")

@@ -134,12 +134,24 @@ constexpr int LBN = 64, LBK = 256, LROW = LBK + 8;
 // gate and odd waves the up projection of the same 16 features; the unsplit epilogue writes
 // Y[m, f] = silu(gate) * up (ldy = the F = N / 2 features) through LDS, and the separate
 // SiLU·up kernel (one launch and a [M, N] round trip per layer) goes away.
-template <int MT, int NW, bool SWIGLU = false>
+// NORM: X is the residual stream h and the kernel stages rmsnorm(h) * nw instead: the producer's
+// split reduction (skinny_reduce with ssq) left per-row partial sums of squares ssq[c][m] over
+// nch chunks of the row, so inv_rms[m] = rsqrt(sum_c ssq / K + eps) is known up front and the
+// scaling happens in the X staging pass (M x 256 values per k-slice): the RMSNorm kernel between
+// the two projections (one launch per norm, 64 per decode step) goes away.
+struct NormIn {
+  const float* ssq;
+  const unsigned short* w;
+  int nch;
+  float eps;
+};
+
+template <int MT, int NW, bool SWIGLU = false, bool NORM = false>
 __global__ __launch_bounds__(NW * 64) void skinny_lds(const unsigned short* __restrict__ X, int ldx,
                                                   const unsigned short* __restrict__ W, int ldw,
                                                   float* __restrict__ part, unsigned short* __restrict__ Y,
                                                   const unsigned short* __restrict__ R, int ldy, int M, int N, int K,
-                                                  int kchunk) {
+                                                  int kchunk, NormIn nrm = NormIn{}) {
   constexpr int RPI = 2 * NW;                             // rows per global load instruction
   __shared__ __attribute__((aligned(16))) unsigned short sW[16 * NW * LROW];
   __shared__ __attribute__((aligned(16))) unsigned short sX[MT * 16 * LROW];
@@ -149,7 +161,18 @@ __global__ __launch_bounds__(NW * 64) void skinny_lds(const unsigned short* __re
   if (k0 >= k1) return;
   const int lr = tid >> 5, lc = (tid & 31) * 8;           // global->LDS: row group, column
   constexpr int XI = MT * 16 / RPI;                       // X row groups (M padded to 16 MT)
-  u16x8_t wr[8], xr[XI];
+  u16x8_t wr[8], xr[XI], nwr;
+  float inv[XI];
+  if constexpr (NORM) {
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+      const int m = RPI * i + lr;
+      float ss = 0.f;
+      if (m < M)
+        for (int c = 0; c < nrm.nch; ++c) ss += nrm.ssq[(size_t)c * M + m];
+      inv[i] = rsqrtf(ss / (float)K + nrm.eps);
+    }
+  }
   auto gload = [&](int kk) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) wr[i] = *(const u16x8_t*)(W + (size_t)(n0 + RPI * i + lr) * ldw + kk + lc);
@@ -158,12 +181,20 @@ __global__ __launch_bounds__(NW * 64) void skinny_lds(const unsigned short* __re
       const int m = RPI * i + lr;
       xr[i] = m < M ? *(const u16x8_t*)(X + (size_t)m * ldx + kk + lc) : u16x8_t{};
     }
+    if constexpr (NORM) nwr = *(const u16x8_t*)(nrm.w + kk + lc);
   };
   auto lstore = [&]() {
 #pragma unroll
     for (int i = 0; i < 8; ++i) *(u16x8_t*)(sW + (RPI * i + lr) * LROW + lc) = wr[i];
 #pragma unroll
-    for (int i = 0; i < XI; ++i) *(u16x8_t*)(sX + (RPI * i + lr) * LROW + lc) = xr[i];
+    for (int i = 0; i < XI; ++i) {
+      u16x8_t xv = xr[i];
+      if constexpr (NORM) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) xv[e] = f32_to_bf16(bf16_to_f32(xv[e]) * inv[i] * bf16_to_f32(nwr[e]));
+      }
+      *(u16x8_t*)(sX + (RPI * i + lr) * LROW + lc) = xv;
+    }
   };
   f32x4_t acc[MT];
 #pragma unroll
@@ -237,23 +268,39 @@ __global__ __launch_bounds__(NW * 64) void skinny_lds(const unsigned short* __re
   }
 }
 
-// Y[m, n] = sum_s part[s, m, n] (+ R[m, n]); 4 outputs per thread.
+// Y[m, n] = sum_s part[s, m, n] (+ R[m, n]); 4 outputs per thread. With ssq (N % 1024 == 0) each
+// 1024-element workgroup also writes the sum of squares of its stored bf16 outputs to
+// ssq[chunk][m] (chunk = n / 1024): the next projection's RMSNorm, folded into its X staging.
 __global__ __launch_bounds__(256) void skinny_reduce(const float* __restrict__ part, int splits,
                                                      unsigned short* __restrict__ Y, const unsigned short* __restrict__ R,
-                                                     int ldy, int M, int N) {
+                                                     int ldy, int M, int N, float* __restrict__ ssq) {
   const int i = (blockIdx.x * 256 + threadIdx.x) * 4;
-  if (i >= M * N) return;
-  const int m = i / N, n = i % N;
-  f32x4_t s = *(const f32x4_t*)(part + i);
-  for (int p = 1; p < splits; ++p) s += *(const f32x4_t*)(part + (size_t)p * M * N + i);
-  u16x4_t o;
+  float sq = 0.f;
+  if (i < M * N) {
+    const int m = i / N, n = i % N;
+    f32x4_t s = *(const f32x4_t*)(part + i);
+    for (int p = 1; p < splits; ++p) s += *(const f32x4_t*)(part + (size_t)p * M * N + i);
+    u16x4_t o;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    float v = s[r];
-    if (R) v += bf16_to_f32(R[(size_t)m * ldy + n + r]);
-    o[r] = f32_to_bf16(v);
+    for (int r = 0; r < 4; ++r) {
+      float v = s[r];
+      if (R) v += bf16_to_f32(R[(size_t)m * ldy + n + r]);
+      o[r] = f32_to_bf16(v);
+      const float q = bf16_to_f32(o[r]);
+      sq += q * q;
+    }
+    *(u16x4_t*)(Y + (size_t)m * ldy + n) = o;
   }
-  *(u16x4_t*)(Y + (size_t)m * ldy + n) = o;
+  if (ssq) {
+    __shared__ float red[4];
+    sq = wave_sum(sq);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sq;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int e0 = blockIdx.x * 1024, m = e0 / N, c = (e0 % N) / 1024;
+      ssq[(size_t)c * M + m] = red[0] + red[1] + red[2] + red[3];
+    }
+  }
 }
 
 // Decode fusion of the split reduction with the RMSNorm that always follows a residual
@@ -386,6 +433,9 @@ GS_KERNEL_API int gs_skinny_splits(int N, int K) {
 // part: float workspace of splits * M * N (ignored when splits == 1). Requires M in [1, 64],
 // N % 64 == 0, K % 32 == 0, ldx / ldw % 8 == 0, ldy % 4 == 0, 16-B aligned X and W.
 // Post-GEMM step: the plain split reduction, or (nw != null) the reduction fused with RMSNorm.
+static float* g_ssq_out = nullptr;          // skinny_reduce writes row sums of squares here
+static NormIn g_norm_in{};                   // skinny_lds stages rmsnorm(X) when g_norm_in.ssq is set
+
 static void finish(float* pp, int nsplit, void* Y, const void* R, int ldy, int M, int N, const void* nw, void* xn,
                    int ldxn, float eps, hipStream_t stream) {
   if (nw) {
@@ -395,7 +445,7 @@ static void finish(float* pp, int nsplit, void* Y, const void* R, int ldy, int M
   } else if (pp) {
     const int n4 = M * N / 4;
     hipLaunchKernelGGL(skinny_reduce, dim3((n4 + 255) / 256), dim3(256), 0, stream, (const float*)pp, nsplit,
-                       (unsigned short*)Y, (const unsigned short*)R, ldy, M, N);
+                       (unsigned short*)Y, (const unsigned short*)R, ldy, M, N, g_ssq_out);
   }
 }
 
@@ -416,8 +466,19 @@ static int skinny_launch(const void* X, int ldx, const void* W, int ldw, void* Y
     const dim3 grid(N / (16 * waves), nsplit);
     auto go = [&](auto kern) {
       hipLaunchKernelGGL(kern, grid, dim3(waves * 64), 0, stream, (const unsigned short*)X, ldx, (const unsigned short*)W,
-                         ldw, pp, (unsigned short*)Y, (const unsigned short*)R, ldy, M, N, K, kchunk);
+                         ldw, pp, (unsigned short*)Y, (const unsigned short*)R, ldy, M, N, K, kchunk, g_norm_in);
     };
+    if (g_norm_in.ssq) {
+      if (waves != 4) return GS_EINVAL;
+      switch (mt) {
+        case 1: go(skinny_lds<1, 4, false, true>); break;
+        case 2: go(skinny_lds<2, 4, false, true>); break;
+        case 3: go(skinny_lds<3, 4, false, true>); break;
+        default: go(skinny_lds<4, 4, false, true>); break;
+      }
+      finish(pp, nsplit, Y, R, ldy, M, N, nw, xn, ldxn, eps, stream);
+      return gs_launch_status();
+    }
     switch (mt) {
       case 1: waves == 2 ? go(skinny_lds<1, 2>) : go(skinny_lds<1, 4>); break;
       case 2: waves == 2 ? go(skinny_lds<2, 2>) : go(skinny_lds<2, 4>); break;
@@ -427,6 +488,7 @@ static int skinny_launch(const void* X, int ldx, const void* W, int ldw, void* Y
     finish(pp, nsplit, Y, R, ldy, M, N, nw, xn, ldxn, eps, stream);
     return gs_launch_status();
   }
+  if (g_norm_in.ssq) return GS_EINVAL;          // folded norm: LDS kernel only
   int nt, planned;
   plan(N, K, nt, planned);
   int kchunk = (K + splits - 1) / splits;
@@ -487,14 +549,40 @@ GS_KERNEL_API int gs_skinny_swiglu_bf16(const void* X, int ldx, const void* W, i
   const dim3 grid(N / 64, 1);
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, (const unsigned short*)X, ldx, (const unsigned short*)W, ldw,
-                       (float*)nullptr, (unsigned short*)Y, (const unsigned short*)nullptr, ldy, M, N, K, K);
+                       (float*)nullptr, (unsigned short*)Y, (const unsigned short*)nullptr, ldy, M, N, K, K, g_norm_in);
   };
-  switch ((M + 15) / 16) {
-    case 1: go(skinny_lds<1, 4, true>); break;
-    case 2: go(skinny_lds<2, 4, true>); break;
-    case 3: go(skinny_lds<3, 4, true>); break;
-    default: go(skinny_lds<4, 4, true>); break;
+  if (g_norm_in.ssq) {
+    switch ((M + 15) / 16) {
+      case 1: go(skinny_lds<1, 4, true, true>); break;
+      case 2: go(skinny_lds<2, 4, true, true>); break;
+      case 3: go(skinny_lds<3, 4, true, true>); break;
+      default: go(skinny_lds<4, 4, true, true>); break;
+    }
+  } else {
+    switch ((M + 15) / 16) {
+      case 1: go(skinny_lds<1, 4, true>); break;
+      case 2: go(skinny_lds<2, 4, true>); break;
+      case 3: go(skinny_lds<3, 4, true>); break;
+      default: go(skinny_lds<4, 4, true>); break;
+    }
   }
   return gs_launch_status();
+}
+
+// Per-launch options of the next skinny call on this thread of the host: ssq_out (float
+// [N / 1024][M]) makes the split reduction emit row sums of squares (requires a split GEMM and
+// N % 1024 == 0); norm_ssq / norm_w / nch / eps make the GEMM stage rmsnorm(X) * norm_w of its
+// X rows. Both reset to off by gs_skinny_clear_opts (the Python wrapper brackets each call).
+GS_KERNEL_API int gs_skinny_set_opts(float* ssq_out, const float* norm_ssq, const void* norm_w, int nch, float eps) {
+  if ((norm_ssq == nullptr) != (norm_w == nullptr) || (norm_ssq && nch <= 0)) return GS_EINVAL;
+  g_ssq_out = ssq_out;
+  g_norm_in = NormIn{norm_ssq, (const unsigned short*)norm_w, nch, eps};
+  return GS_OK;
+}
+
+GS_KERNEL_API int gs_skinny_clear_opts() {
+  g_ssq_out = nullptr;
+  g_norm_in = NormIn{};
+  return GS_OK;
 }
 

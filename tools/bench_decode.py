@@ -111,6 +111,7 @@ def main():
     ap.add_argument("--layers", type=int, default=32)
     ap.add_argument("--out", default=None)
     ap.add_argument("--micro-only", action="store_true")
+    ap.add_argument("--no-gemm-micro", action="store_true")
     a = ap.parse_args()
     lines = []
 
@@ -120,7 +121,7 @@ def main():
 
     for B, ctx in ((32, 1024), (32, 4096), (8, 8192), (64, 2048)):
         emit(attn_micro(B, ctx))
-    for M in (8, 32, 64):
+    for M in ((8, 32, 64) if not a.no_gemm_micro else ()):
         for N, K in ((6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336), (128256, 4096)):
             emit(gemm_micro(M, N, K))
 
@@ -131,14 +132,15 @@ def main():
         return
     model = LlamaModel(LlamaConfig.llama3_8b(n_layers=a.layers), "cuda", seed=1)
     prompt = torch.randint(0, model.cfg.vocab, (a.batch, a.prompt), device="cuda")
-    for gemm in (["hipblaslt", "skinny"] if not a.micro_only else []):
+    for gemm, fold in ([("hipblaslt", False), ("skinny", False), ("skinny", True)] if not a.micro_only else []):
         srv = LlamaServer(model, a.batch, a.max_ctx, gemm=gemm)
+        srv.fold_norm = srv.fold_norm and fold
         torch.cuda.synchronize()
         t = time.perf_counter()
         srv.prefill(prompt)
         torch.cuda.synchronize()
         t_prefill = time.perf_counter() - t
-        res = {"bench": "llama3_8b_decode", "gemm": gemm, "batch": a.batch, "prompt": a.prompt, "layers": a.layers,
+        res = {"bench": "llama3_8b_decode", "gemm": gemm, "fold_norm": srv.fold_norm, "batch": a.batch, "prompt": a.prompt, "layers": a.layers,
                "kv_cache_gib": round(srv.kv_bytes() / 2**30, 2),
                "weights_gib": round(model.weight_bytes() / 2**30, 2), "prefill_s": round(t_prefill, 3)}
         half = a.steps // 2
