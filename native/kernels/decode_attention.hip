@@ -45,7 +45,7 @@ __global__ __launch_bounds__(NT) void decode_split(const unsigned short* __restr
   __shared__ float red[4][G * D];
   __shared__ float ML[G][2];
 
-  const int split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+  const int kvh = blockIdx.x, b = blockIdx.y, split = blockIdx.z;   // chunks slowest: dead ones dispatch last
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int len = min(lens[b], Smax);
   const int c0 = split * CHUNK;
@@ -274,7 +274,7 @@ GS_KERNEL_API int gs_decode_attn_bf16(const void* q, int q_bstride, const void* 
   if (Dh != D || B <= 0 || Hkv <= 0 || Hq % Hkv || Smax <= 0 || Smax % CHUNK || q_bstride < Hq * D || q_bstride % 8)
     return GS_EINVAL;
   const int G = Hq / Hkv, nsplit = Smax / CHUNK;
-  const dim3 grid(nsplit, Hkv, B);
+  const dim3 grid(Hkv, B, nsplit);
   const float qs = scale * LOG2E;
   auto args = [&](auto kern) {
     hipLaunchKernelGGL(kern, grid, dim3(NT), 0, stream, (const unsigned short*)q, q_bstride,
