@@ -416,7 +416,9 @@ class PodFleet:
         if not self.visible_by_uuid:                    # modelled node (fake SMI): this rank's GPU
             env.pop("ROCR_VISIBLE_DEVICES", None)
             env["HIP_VISIBLE_DEVICES"] = str(self.local)
-        self._wait_room(int(env.get("GPUSHARE_QUOTA_BYTES", 0)) * self.fill)
+        from aliyun_gpushare_device_plugin_amd import const
+
+        self._wait_room(int(env.get(const.ENV_SHIM_QUOTA_BYTES, 0)) * self.fill)
         t0 = time.perf_counter()
         w["proc"].stdin.write(json.dumps({"cmd": "start", "env": env, "gemm": self.gemm, "burst": self.burst,
                                           "fill": self.fill}) + "\n")

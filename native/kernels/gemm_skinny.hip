@@ -433,8 +433,8 @@ GS_KERNEL_API int gs_skinny_splits(int N, int K) {
 // part: float workspace of splits * M * N (ignored when splits == 1). Requires M in [1, 64],
 // N % 64 == 0, K % 32 == 0, ldx / ldw % 8 == 0, ldy % 4 == 0, 16-B aligned X and W.
 // Post-GEMM step: the plain split reduction, or (nw != null) the reduction fused with RMSNorm.
-static float* g_ssq_out = nullptr;          // skinny_reduce writes row sums of squares here
-static NormIn g_norm_in{};                   // skinny_lds stages rmsnorm(X) when g_norm_in.ssq is set
+static thread_local float* g_ssq_out = nullptr;   // skinny_reduce writes row sums of squares here
+static thread_local NormIn g_norm_in{};            // skinny_lds stages rmsnorm(X) when g_norm_in.ssq is set
 
 static void finish(float* pp, int nsplit, void* Y, const void* R, int ldy, int M, int N, const void* nw, void* xn,
                    int ldxn, float eps, hipStream_t stream) {
