@@ -12,7 +12,8 @@ Lifecycle (JSON lines on stdin/stdout):
   initialises, so the shim (preloaded since exec, initialised lazily at the first KFD ioctl)
   enforces this pod's quota. The worker reads its quota back through ``hipMemGetInfo``, holds
   ``fill`` of it (the pod's resident model state) plus a GEMM working set, runs one GEMM and
-  prints ``{"event": "ready", "init_ms": ..., "quota": ..., ...}``.
+  prints ``{"event": "ready", "init_ms": ..., "quota": ..., ...}``. With ``"two_phase": true``
+  it stops after the runtime is up (``{"event": "inited"}``) and allocates on ``{"cmd": "alloc"}``.
 * traffic — bursts of ``burst`` GEMMs on the hand-written gfx950 kernel until told to stop;
   ``{"cmd": "stats"}`` answers ``{"event": "stats", "gemms": n, "t": ...}`` between bursts.
 * ``{"cmd": "stop"}`` — frees everything (its HBM is back on the device when ``done`` is
@@ -67,22 +68,32 @@ def main() -> int:
     t0 = time.perf_counter()
     torch.cuda.init()
     dev = torch.device("cuda", 0)
+    torch.empty(1, device=dev)                                 # context + runtime up
     free, quota = torch.cuda.mem_get_info(dev)                 # = the pod's quota under the shim
     from .gemm_player import GemmPlayer
 
+    if cmd.get("two_phase"):
+        # the container is up before the GPU has room for its state (the driver may still be
+        # wiping the HBM a retired pod freed): report, then allocate on "alloc"
+        _send({"event": "inited", "init_ms": round((time.perf_counter() - t0) * 1e3, 3)})
+        nxt = json.loads(sys.stdin.readline() or "{}")
+        if nxt.get("cmd") != "alloc":
+            return 0
     work = 3 * g * g * 2
     hold_bytes = max(0, int(quota * fill) - work)
     # resident state as a model holds it: many tensors (2 GiB each), not one block — amdgpu wipes
     # each freed buffer before returning it, so a pod's HBM comes back piecewise on release
     chunk = int(cmd.get("chunk", 2 << 30))
+    t_hold = time.perf_counter()
     hold = [torch.empty(min(chunk, hold_bytes - off) // 2, dtype=torch.bfloat16, device=dev)
             for off in range(0, hold_bytes, chunk)]
+    hold_ms = (time.perf_counter() - t_hold) * 1e3
     player = GemmPlayer(work, dev, g, g, g, touch_fraction=1.0, seed=os.getpid() & 0xffff)
     player.run(1)
     player.synchronize()
     init_ms = (time.perf_counter() - t0) * 1e3
     _send({"event": "ready", "init_ms": round(init_ms, 3), "quota": quota, "free_at_start": free,
-           "held": hold_bytes + work, "shim": _shim_stats()})
+           "held": hold_bytes + work, "hold_ms": round(hold_ms, 3), "shim": _shim_stats()})
 
     ctl: "queue.Queue" = queue.Queue()
 

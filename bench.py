@@ -353,6 +353,8 @@ class PodFleet:
         self.released_residue = 0             # shim-ledger bytes a stopped pod still held after freeing
         self.release_ms: list[float] = []     # stop -> the GPU physically has room for the replacement
         self.release_by_size: dict[int, list] = {}
+        self._stopped_at = None                # (time, size) of the last retirement, until its room came back
+        self.phase_ms: dict[str, list] = {"stop": [], "init": [], "room": [], "alloc": [], "hold": []}
         self._vram_used, self._vram_total = self._vram_reader()
         for _ in range(max(1, standby)):
             self._spawn()
@@ -407,7 +409,9 @@ class PodFleet:
                 raise RuntimeError(f"pod process {w['proc'].pid} exited while waiting for {event!r}")
 
     def start(self, rec: dict) -> float:
-        """Hand the oldest standby its pod's env; return the ready latency (seconds)."""
+        """Hand the oldest standby its pod's env; return the ready latency (seconds). The pod's
+        runtime comes up while the GPU may still be wiping a retired pod's HBM (as a container
+        starts right after its admission); its state is allocated once the GPU has room."""
         w = self.standby.pop(0)
         self._spawn()                                   # replenish while this one initialises
         self._wait(w, "standby")
@@ -418,12 +422,23 @@ class PodFleet:
             env["HIP_VISIBLE_DEVICES"] = str(self.local)
         from aliyun_gpushare_device_plugin_amd import const
 
-        self._wait_room(int(env.get(const.ENV_SHIM_QUOTA_BYTES, 0)) * self.fill)
         t0 = time.perf_counter()
         w["proc"].stdin.write(json.dumps({"cmd": "start", "env": env, "gemm": self.gemm, "burst": self.burst,
-                                          "fill": self.fill}) + "\n")
+                                          "fill": self.fill, "two_phase": True}) + "\n")
+        self._wait(w, "inited")
+        t1 = time.perf_counter()
+        self._wait_room(int(env.get(const.ENV_SHIM_QUOTA_BYTES, 0)) * self.fill + 3 * self.gemm ** 2 * 2)
+        t2 = time.perf_counter()
+        if self._stopped_at is not None:                # retired pod's HBM back (room for this one)
+            self.release_ms.append(time.perf_counter() - self._stopped_at[0])
+            self.release_by_size.setdefault(self._stopped_at[1], []).append(time.perf_counter() - self._stopped_at[0])
+            self._stopped_at = None
+        w["proc"].stdin.write('{"cmd":"alloc"}\n')
         ev = self._wait(w, "ready")
-        dt = time.perf_counter() - t0
+        t3 = time.perf_counter()
+        dt = t3 - t0
+        for k, v in (("init", t1 - t0), ("room", t2 - t1), ("alloc", t3 - t2), ("hold", ev.get("hold_ms", 0) / 1e3)):
+            self.phase_ms[k].append(v)
         w.update(size=rec["size"], ready=ev)
         self.pods[rec["uid"]] = w
         self.held_bytes += ev.get("held", 0)
@@ -431,33 +446,31 @@ class PodFleet:
         return dt
 
     def _wait_room(self, nbytes: float, limit_s: float = 30.0) -> None:
-        """Before a pod starts: the GPU must physically have room for what it will hold. Inside the
-        churn the stop path already waited; this covers the fill, e.g. right after a previous run
-        on the same GPU whose freed HBM amdgpu is still wiping (~33 GB/s, seconds for a full GPU)."""
+        """Before a pod allocates its state: the GPU must physically have room for what it will
+        hold. In the churn that is the retired pod's HBM coming back; at the fill, e.g. right after
+        a previous run on the same GPU, amdgpu may still be wiping (~33 GB/s, seconds for a full GPU)."""
         if self._vram_used is None or nbytes <= 0:
             return
         deadline = time.perf_counter() + limit_s
         while self._vram_total - self._vram_used() < nbytes + (2 << 30) and time.perf_counter() < deadline:
             time.sleep(0.01)
 
-    def stop(self, uid: str, wait_release: bool = True):
+    def stop(self, uid: str, wait_release: bool = False):
+        """Retire a pod: it frees everything through KFD before it answers. amdgpu returns the
+        VRAM asynchronously (it wipes it first, ~26 ms per GiB); the replacement's start waits for
+        physical room (``start``), so the wipe overlaps the admission and the new pod's runtime
+        start-up. ``wait_release`` waits for that room here instead."""
         w = self.pods.pop(uid, None)
         if w is None:
             return
         t0 = time.perf_counter()
         w["proc"].stdin.write('{"cmd":"stop"}\n')
         ev = self._wait(w, "done")                      # freed through KFD at this point
+        self.phase_ms["stop"].append(time.perf_counter() - t0)
         threading.Thread(target=w["proc"].wait, daemon=True).start()   # reap the exit off the path
+        self._stopped_at = (t0, w["size"])
         if self._vram_used is not None and wait_release:
-            # amdgpu returns freed VRAM asynchronously (it wipes it first, ~26 ms per GiB): the
-            # same-size replacement is admitted once the GPU physically has room for what it will
-            # hold plus 2 GiB of runtime slack — the quotas add up to the whole HBM (bounded wait)
-            need = w["ready"].get("held", 0) + (2 << 30)
-            deadline = time.perf_counter() + 20.0
-            while self._vram_total - self._vram_used() < need and time.perf_counter() < deadline:
-                time.sleep(0.005)
-            self.release_ms.append(time.perf_counter() - t0)
-            self.release_by_size.setdefault(w["size"], []).append(time.perf_counter() - t0)
+            self._wait_room(w["ready"].get("held", 0), limit_s=20.0)
         self.released_residue = max(self.released_residue, ev.get("used_after_release") or 0)
         self.retired_gemms += ev["gemms"]
         self.held_bytes -= w["ready"].get("held", 0)
@@ -475,7 +488,7 @@ class PodFleet:
 
     def close(self):
         for uid in list(self.pods):
-            self.stop(uid, wait_release=False)
+            self.stop(uid)
         for w in self.standby:
             try:
                 w["proc"].stdin.close()
@@ -569,7 +582,7 @@ def main():
         if fleet is not None:
             uid = fleet.oldest()
             if uid is not None:
-                fleet.stop(uid)                  # HBM returned before the replacement is admitted
+                fleet.stop(uid)                  # the replacement's start waits for the HBM
         rec = svc.churn(local, uid) if rank == 0 else client.churn(local, uid)
         if rec is not None and fleet is not None:
             fleet.start(rec)
@@ -592,6 +605,8 @@ def main():
         fleet.ready_ms.clear()
         fleet.release_ms.clear()
         fleet.release_by_size.clear()
+        for v in fleet.phase_ms.values():
+            v.clear()
 
     barrier()
     g0 = fleet.gemms() if fleet is not None else 0
@@ -616,6 +631,10 @@ def main():
     release = gather(fleet.release_ms if fleet is not None else [])
     release_all = [x for r in release for x in r]
     by_size: dict = {}
+    phases: dict = {}
+    for d in gather(fleet.phase_ms if fleet is not None else {}):
+        for k, v in d.items():
+            phases.setdefault(k, []).extend(v)
     for d in gather(fleet.release_by_size if fleet is not None else {}):
         for k, v in d.items():
             by_size.setdefault(k, []).extend(v)
@@ -664,6 +683,9 @@ def main():
             "pod_ready_p99_ms": ms(pct(ready_all, 0.99)),
             "pod_room_wait_p50_ms": ms(pct(release_all, 0.5)),
             "pod_room_wait_p50_ms_by_gib": {str(k): ms(pct(v, 0.5)) for k, v in sorted(by_size.items())},
+            # one churn cycle on a GPU: stop (old pod frees) -> admission -> new pod's runtime up
+            # (init) -> physical room for its state (room) -> state allocated + first GEMM (alloc)
+            "pod_phase_p50_ms": {k: ms(pct(v, 0.5)) for k, v in phases.items()},
             "control_plane_ms_per_admission": round(cp.cp_time / max(1, a.steps * n) * 1e3, 3),
             "allocate_by_mode": modes,
             "pods_per_node": pods_node,
