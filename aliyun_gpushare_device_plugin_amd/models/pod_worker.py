@@ -85,15 +85,18 @@ def main() -> int:
     # each freed buffer before returning it, so a pod's HBM comes back piecewise on release
     chunk = int(cmd.get("chunk", 2 << 30))
     t_hold = time.perf_counter()
-    hold = [torch.empty(min(chunk, hold_bytes - off) // 2, dtype=torch.bfloat16, device=dev)
-            for off in range(0, hold_bytes, chunk)]
+    hold, chunk_ms = [], []
+    for off in range(0, hold_bytes, chunk):
+        t = time.perf_counter()
+        hold.append(torch.empty(min(chunk, hold_bytes - off) // 2, dtype=torch.bfloat16, device=dev))
+        chunk_ms.append(round((time.perf_counter() - t) * 1e3, 2))
     hold_ms = (time.perf_counter() - t_hold) * 1e3
     player = GemmPlayer(work, dev, g, g, g, touch_fraction=1.0, seed=os.getpid() & 0xffff)
     player.run(1)
     player.synchronize()
     init_ms = (time.perf_counter() - t0) * 1e3
     _send({"event": "ready", "init_ms": round(init_ms, 3), "quota": quota, "free_at_start": free,
-           "held": hold_bytes + work, "hold_ms": round(hold_ms, 3), "shim": _shim_stats()})
+           "held": hold_bytes + work, "hold_ms": round(hold_ms, 3), "hold_chunk_ms": chunk_ms, "shim": _shim_stats()})
 
     ctl: "queue.Queue" = queue.Queue()
 

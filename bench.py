@@ -69,6 +69,8 @@ def parse():
     ap.add_argument("--plugin-mode", default="process", choices=("process", "thread"))
     ap.add_argument("--compare-rtts", default="0,1,5", help="apiserver RTTs (ms) of the control-plane A/B ('' = off)")
     ap.add_argument("--compare-pods", type=int, default=24, help="admissions per A/B configuration")
+    ap.add_argument("--room-slack-gib", type=float, default=2.0,
+                    help="free HBM beyond a pod's state required before it allocates")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -341,8 +343,9 @@ class PodFleet:
     """The pod processes of this rank's GPU, plus one standby process (interpreter up, torch
     imported, GPU untouched) that becomes the next admitted pod."""
 
-    def __init__(self, local: int, gemm: int, burst: int, fill: float, visible_by_uuid: bool, standby: int = 2):
-        self.local, self.gemm, self.burst, self.fill = local, gemm, burst, fill
+    def __init__(self, local: int, gemm: int, burst: int, fill: float, visible_by_uuid: bool, standby: int = 2,
+                 slack: int = 2 << 30):
+        self.local, self.gemm, self.burst, self.fill, self.slack = local, gemm, burst, fill, slack
         self.visible_by_uuid = visible_by_uuid
         self.pods: dict[str, dict] = {}       # uid -> {"proc", "q", "size", "ready"}
         self.standby: list[dict] = []         # pre-started interpreters, oldest first
@@ -355,6 +358,7 @@ class PodFleet:
         self.release_by_size: dict[int, list] = {}
         self._stopped_at = None                # (time, size) of the last retirement, until its room came back
         self.phase_ms: dict[str, list] = {"stop": [], "init": [], "room": [], "alloc": [], "hold": []}
+        self.trace: list | None = [] if os.environ.get("GS_BENCH_POD_TRACE") else None
         self._vram_used, self._vram_total = self._vram_reader()
         for _ in range(max(1, standby)):
             self._spawn()
@@ -429,6 +433,7 @@ class PodFleet:
         t1 = time.perf_counter()
         self._wait_room(int(env.get(const.ENV_SHIM_QUOTA_BYTES, 0)) * self.fill + 3 * self.gemm ** 2 * 2)
         t2 = time.perf_counter()
+        free2 = self._vram_total - self._vram_used() if self._vram_used is not None else None
         if self._stopped_at is not None:                # retired pod's HBM back (room for this one)
             self.release_ms.append(time.perf_counter() - self._stopped_at[0])
             self.release_by_size.setdefault(self._stopped_at[1], []).append(time.perf_counter() - self._stopped_at[0])
@@ -439,6 +444,10 @@ class PodFleet:
         dt = t3 - t0
         for k, v in (("init", t1 - t0), ("room", t2 - t1), ("alloc", t3 - t2), ("hold", ev.get("hold_ms", 0) / 1e3)):
             self.phase_ms[k].append(v)
+        if self.trace is not None:
+            self.trace.append({"size": rec["size"], "init": t1 - t0, "room": t2 - t1, "alloc": t3 - t2,
+                               "hold_chunk_ms": ev.get("hold_chunk_ms"),
+                               "free_at_alloc": free2})
         w.update(size=rec["size"], ready=ev)
         self.pods[rec["uid"]] = w
         self.held_bytes += ev.get("held", 0)
@@ -452,7 +461,7 @@ class PodFleet:
         if self._vram_used is None or nbytes <= 0:
             return
         deadline = time.perf_counter() + limit_s
-        while self._vram_total - self._vram_used() < nbytes + (2 << 30) and time.perf_counter() < deadline:
+        while self._vram_total - self._vram_used() < nbytes + self.slack and time.perf_counter() < deadline:
             time.sleep(0.01)
 
     def stop(self, uid: str, wait_release: bool = False):
@@ -554,7 +563,8 @@ def main():
         info = {"units_per_gpu": cp.units_per_gpu, "gpu_count": cp.gpu_count, "by_uuid": visible_by_uuid}
     info = bcast(info)
     units = info["units_per_gpu"]
-    fleet = PodFleet(local, a.gemm, a.burst, a.fill, info["by_uuid"], a.standby) if use_gpu else None
+    fleet = PodFleet(local, a.gemm, a.burst, a.fill, info["by_uuid"], a.standby,
+                     slack=int(a.room_slack_gib * (1 << 30))) if use_gpu else None
     topo_report = None
 
     def launch(started: dict) -> float:
@@ -707,6 +717,9 @@ def main():
             with open(a.json_out, "w") as f:
                 f.write(line + "\n")
     if fleet is not None:
+        if fleet.trace is not None:              # per-pod cycle phases (GS_BENCH_POD_TRACE=<path>)
+            with open(f"{os.environ['GS_BENCH_POD_TRACE']}.{rank}", "w") as f:
+                f.writelines(json.dumps(r) + "\n" for r in fleet.trace)
         fleet.close()
     if client is not None:
         client.close()
