@@ -38,6 +38,9 @@ class LlamaServer:
                           and ops.skinny_ssq_ok(c.d_model, c.d_ff))
         self.ssq = (torch.zeros((c.d_model // 1024, batch), dtype=torch.float32, device=model.device)
                     if self.fold_norm else None)
+        # RoPE(q, k) + KV append in the QKV projection's split reduction (no rope_kv_append launch)
+        self.fuse_rope = gemm == "skinny" and ops.skinny_rope_ok((c.n_heads + 2 * c.n_kv_heads) * c.head_dim,
+                                                                 c.d_model) and c.head_dim == 128
         if max_ctx > c.max_seq:
             raise ValueError("max_ctx exceeds the RoPE table (cfg.max_seq)")
         self.model, self.B = model, batch
@@ -83,11 +86,14 @@ class LlamaServer:
             return ops.skinny_linear(x, w, residual=residual, out=residual)
         return torch.matmul(x, w.t()) if residual is None else torch.addmm(residual, x, w.t())
 
-    def _mm_in(self, x, w):
-        """Projection of a layer input that may be a deferred norm ``(h, norm_w)``."""
+    def _mm_in(self, x, w, rope=None):
+        """Projection of a layer input that may be a deferred norm ``(h, norm_w)``; ``rope`` (skinny
+        path) = ``ops.skinny_linear``'s RoPE + KV-append epilogue."""
         if isinstance(x, tuple):
             h, nw = x
-            return ops.skinny_linear(h, w, norm=(self.ssq, nw, self.cfg.eps))
+            return ops.skinny_linear(h, w, norm=(self.ssq, nw, self.cfg.eps), rope=rope)
+        if rope is not None:
+            return ops.skinny_linear(x, w, rope=rope)
         return self._mm(x, w)
 
     def _mm_norm(self, x, w, residual, norm_w):
@@ -110,8 +116,10 @@ class LlamaServer:
         h = m.embed.index_select(0, self.tok)                          # residual stream [B, d]
         x = ops.rmsnorm(h, m.layers[0]["attn_norm"], c.eps)
         for i, L in enumerate(m.layers):
-            qkv = self._mm_in(x, L["wqkv"])
-            ops.rope_kv_append(qkv, m.cos, m.sin, self.pos, self.kc[i], self.vc[i], c.n_heads)
+            rope = (m.cos, m.sin, self.pos, self.kc[i], self.vc[i], c.n_heads) if self.fuse_rope else None
+            qkv = self._mm_in(x, L["wqkv"], rope=rope)
+            if rope is None:
+                ops.rope_kv_append(qkv, m.cos, m.sin, self.pos, self.kc[i], self.vc[i], c.n_heads)
             a = ops.decode_attention(qkv[:, :hq], self.kc[i], self.vc[i], self.lens, self.ws)
             h, x = self._mm_norm(a, L["wo"], h, L["mlp_norm"])
             act = None

@@ -42,6 +42,7 @@ SIGNATURES = {
     "gs_skinny_set_nt": [_I],
     "gs_skinny_set_variant": [_I],
     "gs_skinny_set_wg_target": [_I],
+    "gs_skinny_set_rope": [_P, _P, _I, _P, _P, _P, _I, _I, _I],
     "gs_skinny_set_lds_waves": [_I],
 }
 

@@ -202,13 +202,25 @@ def skinny_ssq_ok(N: int, K: int) -> bool:
     return N % 1024 == 0 and K % 256 == 0 and _lib.lib().gs_skinny_splits(N, K) > 1
 
 
+def skinny_rope_ok(N: int, K: int) -> bool:
+    """Whether ``skinny_linear(..., rope=...)`` can apply RoPE and the KV append in its split
+    reduction for an ``[N, K]`` QKV weight (the shape must split)."""
+    return N % 128 == 0 and K % 256 == 0 and _lib.lib().gs_skinny_splits(N, K) > 1
+
+
 class _SkinnyOpts:
     """Per-launch options of the native skinny GEMM (set just before the call, cleared after)."""
 
-    def __init__(self, ssq_out=None, norm=None):
-        self.ssq_out, self.norm = ssq_out, norm
+    def __init__(self, ssq_out=None, norm=None, rope=None):
+        self.ssq_out, self.norm, self.rope = ssq_out, norm, rope
 
     def __enter__(self):
+        if self.rope is not None:
+            cos, sin, pos, kc, vc, hq = self.rope
+            B, hkv, smax, _ = kc.shape
+            _lib.check(_lib.lib().gs_skinny_set_rope(cos.data_ptr(), sin.data_ptr(), cos.shape[0], pos.data_ptr(),
+                                                     kc.data_ptr(), vc.data_ptr(), hq, hkv, smax),
+                       "gs_skinny_set_rope")
         if self.ssq_out is None and self.norm is None:
             return self
         ssq, w, eps = self.norm if self.norm is not None else (None, None, 0.0)
@@ -220,7 +232,7 @@ class _SkinnyOpts:
         return self
 
     def __exit__(self, *exc):
-        if self.ssq_out is not None or self.norm is not None:
+        if self.ssq_out is not None or self.norm is not None or self.rope is not None:
             _lib.lib().gs_skinny_clear_opts()
 
 
@@ -235,9 +247,28 @@ def _check_norm(norm, M: int, K: int):
         raise ValueError("norm: weight must be contiguous [K]")
 
 
+def _check_rope(rope, M: int, N: int, K: int, residual):
+    cos, sin, pos, kc, vc, hq = rope
+    if residual is not None or not skinny_rope_ok(N, K):
+        raise ValueError("skinny_linear: rope needs a split shape (skinny_rope_ok) and no residual")
+    if (kc.dim() != 4 or kc.shape != vc.shape or kc.dtype != torch.bfloat16 or vc.dtype != torch.bfloat16
+            or not kc.is_contiguous() or not vc.is_contiguous() or kc.shape[0] != M or kc.shape[3] != 128):
+        raise ValueError("skinny_linear: rope caches must be contiguous bf16 [M, Hkv, Smax, 128]")
+    if N != (hq + 2 * kc.shape[1]) * 128:
+        raise ValueError("skinny_linear: rope needs N = (n_heads + 2 Hkv) * 128")
+    if pos.dtype != torch.int32 or pos.shape != (M,) or not pos.is_contiguous():
+        raise ValueError("skinny_linear: rope positions must be contiguous int32 [M]")
+    if (cos.dtype != torch.float32 or sin.shape != cos.shape or cos.dim() != 2 or cos.shape[1] != 64
+            or not cos.is_contiguous() or not sin.is_contiguous()):
+        raise ValueError("skinny_linear: rope tables must be contiguous float32 [rows, 64]")
+    for t in (cos, sin, pos, kc, vc):
+        if t.device != kc.device:
+            raise ValueError("skinny_linear: rope tensors must share a device")
+
+
 def skinny_linear(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | None = None,
                   out: torch.Tensor | None = None, norm_weight: torch.Tensor | None = None, eps: float = 1e-5,
-                  ssq_out: torch.Tensor | None = None, norm: tuple | None = None):
+                  ssq_out: torch.Tensor | None = None, norm: tuple | None = None, rope: tuple | None = None):
     """Decode-shaped ``x @ w.T (+ residual)`` for ``x`` ``[M <= 64, K]`` on the split-K skinny
     kernel (native/kernels/gemm_skinny.hip): an HBM stream over ``w`` with the batch as the MFMA's
     16-row operand. ``out`` may be ``residual`` itself (in-place residual add). With
@@ -248,7 +279,11 @@ def skinny_linear(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | Non
     ``skinny_ssq_ok``) makes this call's split reduction also write the row sums of squares of the
     stored output; a later call with ``norm=(ssq, weight, eps)`` and ``x`` = that output multiplies
     by ``weight`` and ``rsqrt(mean + eps)`` while staging ``x`` — ``rmsnorm(x) * weight`` without a
-    norm kernel in between."""
+    norm kernel in between.
+
+    Decode QKV projection: ``rope=(cos, sin, pos, k_cache, v_cache, n_heads)`` makes the split
+    reduction also do ``ops.rope_kv_append``'s work (RoPE of the q and k heads at ``pos[b]``, k / v
+    appended to the caches) — one launch less per layer; see ``skinny_rope_ok``."""
     _check_operand(x, "x")
     _check_operand(w, "w")
     if x.dim() != 2 or w.dim() != 2 or x.shape[1] != w.shape[1]:
@@ -278,14 +313,16 @@ def skinny_linear(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | Non
         if ssq_out.dtype != torch.float32 or tuple(ssq_out.shape) != (N // 1024, M) or not ssq_out.is_contiguous():
             raise ValueError("skinny_linear: ssq_out must be contiguous float32 [N / 1024, M]")
     _check_norm(norm, M, K)
+    if rope is not None:
+        _check_rope(rope, M, N, K, residual)
     if norm_weight is None:
-        with _SkinnyOpts(ssq_out, norm):
+        with _SkinnyOpts(ssq_out, norm, rope):
             rc = L.gs_skinny_gemm_bf16(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), rptr,
                                        out.stride(0), M, N, K, splits, pptr, _lib.stream_ptr(x.device))
         _lib.check(rc, "gs_skinny_gemm_bf16")
         return out
-    if norm is not None:
-        raise ValueError("skinny_linear: norm and norm_weight are exclusive")
+    if norm is not None or rope is not None:
+        raise ValueError("skinny_linear: norm_weight excludes norm and rope")
     _check_operand(norm_weight, "norm_weight")
     if norm_weight.shape != (N,) or not norm_weight.is_contiguous() or N > 8192 or out.stride(0) % 8:
         raise ValueError("skinny_linear: norm_weight must be contiguous [N] with N <= 8192")

@@ -303,6 +303,73 @@ __global__ __launch_bounds__(256) void skinny_reduce(const float* __restrict__ p
   }
 }
 
+// Decode fusion of the QKV projection's split reduction with RoPE(q), RoPE(k) and the KV-cache
+// append (the rope_kv_append launch of decode_attention.hip goes away): per sequence b at
+// position pos[b], the K splits of each rotation pair (d, d + 64) of a q / k head are summed,
+// rounded to bf16 (as the reduction's stored output), rotated and written to Y, k also to the
+// cache; v heads are summed, written to Y and appended raw. Y = [B, (Hq + 2 Hkv) * 128] rows.
+struct RopeIn {
+  const float* cosb;
+  const float* sinb;
+  int tab_rows;
+  const int* pos;
+  unsigned short* kc;
+  unsigned short* vc;
+  int hq, hkv, smax;
+};
+
+__global__ __launch_bounds__(256) void skinny_reduce_rope(const float* __restrict__ part, int splits,
+                                                          unsigned short* __restrict__ Y, int ldy, int M, int N,
+                                                          RopeIn rp) {
+  constexpr int D = 128, HALF = D / 2, NQ = HALF / 4, NV = D / 8;
+  const int per = (rp.hq + rp.hkv) * NQ + rp.hkv * NV;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M * per) return;
+  const int b = i / per, r = i % per;
+  const int p = rp.pos[b];
+  const bool in_cache = p >= 0 && p < rp.smax;
+  auto sum4 = [&](int n) {
+    f32x4_t a = *(const f32x4_t*)(part + (size_t)b * N + n);
+    for (int q = 1; q < splits; ++q) a += *(const f32x4_t*)(part + ((size_t)q * M + b) * N + n);
+    return a;
+  };
+  unsigned short* row = Y + (size_t)b * ldy;
+  if (r < (rp.hq + rp.hkv) * NQ) {
+    const int h = r / NQ, d = (r % NQ) * 4, n = h * D + d;
+    const f32x4_t a = sum4(n), c2 = sum4(n + HALF);
+    const int pt = min(max(p, 0), rp.tab_rows - 1);
+    const float4 c = *(const float4*)(rp.cosb + (size_t)pt * HALF + d);
+    const float4 sn = *(const float4*)(rp.sinb + (size_t)pt * HALF + d);
+    const float cc[4] = {c.x, c.y, c.z, c.w}, sc[4] = {sn.x, sn.y, sn.z, sn.w};
+    u16x4_t oa, ob;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float x1 = bf16_to_f32(f32_to_bf16(a[e])), x2 = bf16_to_f32(f32_to_bf16(c2[e]));
+      oa[e] = f32_to_bf16(x1 * cc[e] - x2 * sc[e]);
+      ob[e] = f32_to_bf16(x2 * cc[e] + x1 * sc[e]);
+    }
+    *(u16x4_t*)(row + n) = oa;
+    *(u16x4_t*)(row + n + HALF) = ob;
+    if (h >= rp.hq && in_cache) {
+      unsigned short* dst = rp.kc + ((((size_t)b * rp.hkv + (h - rp.hq)) * rp.smax + p) * D);
+      *(u16x4_t*)(dst + d) = oa;
+      *(u16x4_t*)(dst + HALF + d) = ob;
+    }
+  } else {
+    const int r2 = r - (rp.hq + rp.hkv) * NQ, h = r2 / NV, c = (r2 % NV) * 8;
+    const int n = (rp.hq + rp.hkv + h) * D + c;
+    const f32x4_t lo = sum4(n), hi = sum4(n + 4);
+    u16x8_t o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      o[e] = f32_to_bf16(lo[e]);
+      o[e + 4] = f32_to_bf16(hi[e]);
+    }
+    *(u16x8_t*)(row + n) = o;
+    if (in_cache) *(u16x8_t*)(rp.vc + ((((size_t)b * rp.hkv + h) * rp.smax + p) * D) + c) = o;
+  }
+}
+
 // Decode fusion of the split reduction with the RMSNorm that always follows a residual
 // projection: per row m, h = sum_s part[s, m, :] + R[m, :] (or h = Y[m, :] when the GEMM ran
 // unsplit and already wrote it), Y = bf16(h), xn = bf16(h * rsqrt(mean(h^2) + eps) * nw) with
@@ -435,10 +502,15 @@ GS_KERNEL_API int gs_skinny_splits(int N, int K) {
 // Post-GEMM step: the plain split reduction, or (nw != null) the reduction fused with RMSNorm.
 static thread_local float* g_ssq_out = nullptr;   // skinny_reduce writes row sums of squares here
 static thread_local NormIn g_norm_in{};            // skinny_lds stages rmsnorm(X) when g_norm_in.ssq is set
+static thread_local RopeIn g_rope_in{};            // split reduction = skinny_reduce_rope when g_rope_in.pos is set
 
 static void finish(float* pp, int nsplit, void* Y, const void* R, int ldy, int M, int N, const void* nw, void* xn,
                    int ldxn, float eps, hipStream_t stream) {
-  if (nw) {
+  if (g_rope_in.pos) {
+    const int n = M * ((g_rope_in.hq + g_rope_in.hkv) * 16 + g_rope_in.hkv * 16);
+    hipLaunchKernelGGL(skinny_reduce_rope, dim3((n + 255) / 256), dim3(256), 0, stream, (const float*)pp, nsplit,
+                       (unsigned short*)Y, ldy, M, N, g_rope_in);
+  } else if (nw) {
     hipLaunchKernelGGL(skinny_reduce_norm, dim3(M), dim3(256), 0, stream, (const float*)pp, nsplit,
                        (unsigned short*)Y, (const unsigned short*)R, ldy, M, N, (const unsigned short*)nw,
                        (unsigned short*)xn, ldxn, eps);
@@ -462,6 +534,9 @@ static int skinny_launch(const void* X, int ldx, const void* W, int ldw, void* Y
     kchunk = (kchunk + LBK - 1) / LBK * LBK;
     const int nsplit = (K + kchunk - 1) / kchunk;
     float* pp = nsplit > 1 ? (float*)part : nullptr;
+    // the RoPE / KV-append epilogue lives in the split reduction: split, no residual, QKV width
+    if (g_rope_in.pos && (!pp || R || nw || ldy % 8 || N != (g_rope_in.hq + 2 * g_rope_in.hkv) * 128))
+      return GS_EINVAL;
     const int waves = lds_waves(N);
     const dim3 grid(N / (16 * waves), nsplit);
     auto go = [&](auto kern) {
@@ -488,7 +563,7 @@ static int skinny_launch(const void* X, int ldx, const void* W, int ldw, void* Y
     finish(pp, nsplit, Y, R, ldy, M, N, nw, xn, ldxn, eps, stream);
     return gs_launch_status();
   }
-  if (g_norm_in.ssq) return GS_EINVAL;          // folded norm: LDS kernel only
+  if (g_norm_in.ssq || g_rope_in.pos) return GS_EINVAL;   // folded norm / RoPE epilogue: LDS kernel only
   int nt, planned;
   plan(N, K, nt, planned);
   int kchunk = (K + splits - 1) / splits;
@@ -541,7 +616,7 @@ GS_KERNEL_API int gs_skinny_swiglu_bf16(const void* X, int ldx, const void* W, i
                                         int F, int K, hipStream_t stream) {
   const int N = 2 * F;
   int splits;
-  if (M < 1 || M > 64 || F % 32 || K % LBK || K <= 0 || ldx % 8 || ldw % 8 || ldy % 4 || ldx < K || ldw < K ||
+  if (g_rope_in.pos || M < 1 || M > 64 || F % 32 || K % LBK || K <= 0 || ldx % 8 || ldw % 8 || ldy % 4 || ldx < K || ldw < K ||
       ldy < F || !use_lds(K) || lds_waves(N) != 4)
     return GS_EINVAL;
   plan_lds(N, K, splits);
@@ -583,6 +658,17 @@ GS_KERNEL_API int gs_skinny_set_opts(float* ssq_out, const float* norm_ssq, cons
 GS_KERNEL_API int gs_skinny_clear_opts() {
   g_ssq_out = nullptr;
   g_norm_in = NormIn{};
+  g_rope_in = RopeIn{};
+  return GS_OK;
+}
+
+// Per-launch option: the next skinny call's split reduction applies RoPE(q, k) at pos[b] and
+// appends k / v to the caches [B, Hkv, Smax, 128] (skinny_reduce_rope); the call returns
+// GS_EINVAL unless it splits, has no residual and N = (Hq + 2 Hkv) * 128. Cleared with the rest.
+GS_KERNEL_API int gs_skinny_set_rope(const float* cosb, const float* sinb, int tab_rows, const int* pos, void* kc,
+                                     void* vc, int hq, int hkv, int smax) {
+  if (!cosb || !sinb || !pos || !kc || !vc || tab_rows <= 0 || hq <= 0 || hkv <= 0 || smax <= 0) return GS_EINVAL;
+  g_rope_in = RopeIn{cosb, sinb, tab_rows, pos, (unsigned short*)kc, (unsigned short*)vc, hq, hkv, smax};
   return GS_OK;
 }
 

@@ -110,6 +110,34 @@ def _check_skinny(M, N, K):
     assert (r.float() - want).abs().max().item() < 2e-2 * want.abs().max().item() + 1e-2
 
 
+@pytest.mark.parametrize("M,Hq,Hkv,K", [(32, 32, 8, 4096), (5, 8, 2, 1024), (64, 16, 4, 2048)])
+def test_skinny_rope_epilogue_matches_separate_launch(M, Hq, Hkv, K):
+    """QKV projection whose split reduction applies RoPE and appends k / v: bit-identical to the
+    plain projection followed by ops.rope_kv_append, including rows whose position is outside the
+    cache (rotated, not appended)."""
+    torch.manual_seed(M + Hq)
+    N, Smax, rows = (Hq + 2 * Hkv) * 128, 256, 300
+    assert ops.skinny_rope_ok(N, K)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.05
+    cos, sin = ops.rope_tables(rows, 128, 500000.0, "cuda")
+    pos = torch.randint(0, Smax, (M,), device="cuda", dtype=torch.int32)
+    pos[0] = Smax                                   # outside the cache: rotated, not appended
+    if M > 1:
+        pos[1] = -1
+    kc1, vc1 = ops.kv_cache(M, Hkv, Smax, 128, "cuda")
+    kc1.normal_()
+    vc1.normal_()
+    kc2, vc2 = kc1.clone(), vc1.clone()
+    y1 = ops.skinny_linear(x, w, rope=(cos, sin, pos, kc1, vc1, Hq))
+    y2 = ops.skinny_linear(x, w)
+    ops.rope_kv_append(y2, cos, sin, pos, kc2, vc2, Hq)
+    assert torch.equal(y1, y2)
+    assert torch.equal(kc1, kc2) and torch.equal(vc1, vc2)
+    with pytest.raises(ValueError):
+        ops.skinny_linear(x, w, residual=y2.clone(), rope=(cos, sin, pos, kc1, vc1, Hq))
+
+
 def test_skinny_linear_on_strided_rows():
     x_wide = torch.randn(8, 1024 + 64, device="cuda", dtype=torch.bfloat16)
     x = x_wide[:, 64:]                                          # 16-B aligned slice, row stride 1088
@@ -191,8 +219,9 @@ def test_skinny_swiglu_matches_fp32(M):
 
 def test_decode_step_with_folded_rmsnorm_matches_unfolded():
     """1024-wide model: the o / down projections emit row sums of squares and the next projection
-    normalises while staging its input (no RMSNorm kernels); logits match the unfolded skinny
-    step and the hipBLASLt step, through a hipGraph replay too."""
+    normalises while staging its input (no RMSNorm kernels), and the QKV reduction applies RoPE and
+    appends to the caches; logits match the unfused skinny step and the hipBLASLt step, through a
+    hipGraph replay too."""
     from aliyun_gpushare_device_plugin_amd.models.llama import LlamaConfig, LlamaModel
     from aliyun_gpushare_device_plugin_amd.models.llama_serve import LlamaServer
 
@@ -200,9 +229,9 @@ def test_decode_step_with_folded_rmsnorm_matches_unfolded():
     model = LlamaModel(cfg, "cuda", seed=3)
     prompt = torch.randint(0, cfg.vocab, (8, 40), device="cuda")
     a = LlamaServer(model, 8, 128, gemm="skinny")
-    assert a.fold_norm
+    assert a.fold_norm and a.fuse_rope
     b = LlamaServer(model, 8, 128, gemm="skinny")
-    b.fold_norm = False
+    b.fold_norm = b.fuse_rope = False
     c = LlamaServer(model, 8, 128, gemm="hipblaslt")
     for s in (a, b, c):
         s.prefill(prompt)

@@ -132,15 +132,17 @@ def main():
         return
     model = LlamaModel(LlamaConfig.llama3_8b(n_layers=a.layers), "cuda", seed=1)
     prompt = torch.randint(0, model.cfg.vocab, (a.batch, a.prompt), device="cuda")
-    for gemm, fold in ([("hipblaslt", False), ("skinny", False), ("skinny", True)] if not a.micro_only else []):
+    for gemm, fold, rope in [("hipblaslt", False, False), ("skinny", True, False), ("skinny", True, True)]:
         srv = LlamaServer(model, a.batch, a.max_ctx, gemm=gemm)
         srv.fold_norm = srv.fold_norm and fold
+        srv.fuse_rope = srv.fuse_rope and rope
         torch.cuda.synchronize()
         t = time.perf_counter()
         srv.prefill(prompt)
         torch.cuda.synchronize()
         t_prefill = time.perf_counter() - t
-        res = {"bench": "llama3_8b_decode", "gemm": gemm, "fold_norm": srv.fold_norm, "batch": a.batch, "prompt": a.prompt, "layers": a.layers,
+        res = {"bench": "llama3_8b_decode", "gemm": gemm, "fold_norm": srv.fold_norm, "fuse_rope": srv.fuse_rope,
+               "batch": a.batch, "prompt": a.prompt, "layers": a.layers,
                "kv_cache_gib": round(srv.kv_bytes() / 2**30, 2),
                "weights_gib": round(model.weight_bytes() / 2**30, 2), "prefill_s": round(t_prefill, 3)}
         half = a.steps // 2
