@@ -7,12 +7,12 @@ memory-bound work. The decode step here is built for that:
 * KV cache ``[B, Hkv, Smax, 128]`` per layer (``ops.kv_cache``), filled by the prefill through
   ``LlamaModel.forward(kv_sink=...)`` and appended to by ``ops.kv_append``;
 * attention = ``ops.decode_attention`` (split-K over the cache, ``native/kernels/decode_attention.hip``);
-  RMSNorm, SiLU·up (read in the interleaved gate/up layout) and one fused RoPE(q, k) + KV-append
-  launch per layer on the hand-written kernels; the projections (M = batch <= 64) on the
-  LDS-staged skinny MFMA GEMM (``ops.skinny_linear``, residual add fused in place): 1.24-1.4x
-  hipBLASLt on the 4096/6144-wide projections, 1.03-1.08x on the LM head, 0.8-0.9x on the
-  28672-wide gate/up, 6.08 vs 6.58 ms per batch-32 step overall (``profiles/decode/README.md``);
-  ``gemm="hipblaslt"`` runs them on ``torch.matmul`` / ``torch.addmm`` for A/B measurement;
+  the projections (M = batch <= 64) on the LDS-staged skinny MFMA GEMM (``ops.skinny_linear``,
+  residual add fused in place), with the rest folded into it: RMSNorm into the next projection's
+  X staging, SwiGLU into the gate/up epilogue, RoPE(q, k) + KV append into the QKV projection's
+  split reduction. 5.08 ms per batch-32 step against 5.75 ms with hipBLASLt projections
+  (``profiles/decode/README.md``); ``gemm="hipblaslt"`` runs them on ``torch.matmul`` /
+  ``torch.addmm`` for A/B measurement;
 * positions / lengths live in device tensors, so the whole 32-layer step is captured once in a
   hipGraph (``torch.cuda.CUDAGraph``) and replayed: one launch per step instead of ~450.
 """
