@@ -432,8 +432,10 @@ class Allocator:
         if replay is not None:
             hist.observe(time.perf_counter() - t0, phase="total")
             return replay
+        ta = time.perf_counter()
         try:
             with self._mu:
+                tb = time.perf_counter()
                 claim, complete = self._match(sizes, fresh=False)
                 t1 = time.perf_counter()
                 if claim is None:
@@ -442,7 +444,9 @@ class Allocator:
                 if claim is not None and complete:
                     self._claims[claim.uid] = claim   # held across the PATCH
                 t2 = time.perf_counter()
-            hist.observe(t1 - t0, phase="lookup")
+            hist.observe(ta - t0, phase="prelude")      # request key, journal replay check
+            hist.observe(tb - ta, phase="lock")
+            hist.observe(t1 - tb, phase="lookup")
             hist.observe(t2 - t1, phase="decide")
         except Exception as e:  # noqa: BLE001 - pod listing failures
             log.info("invalid allocation request: Failed to find candidate pods due to %s", e)

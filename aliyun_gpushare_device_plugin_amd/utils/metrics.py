@@ -174,7 +174,7 @@ class PluginMetrics:
     def __init__(self, registry: Registry | None = None):
         r = self.registry = registry or Registry()
         self.allocate_latency = r.histogram("gpushare_allocate_latency_seconds",
-                                            "Allocate RPC latency by phase (lookup/decide/patch/total)")
+                                            "Allocate RPC latency by phase (prelude/lock/lookup/decide/patch/total)")
         self.allocate_outcomes = r.counter("gpushare_allocate_total", "Allocate outcomes")
         self.pending_match_failures = r.counter("gpushare_pending_match_failures_total",
                                                 "Allocates with no matching assumed pod")

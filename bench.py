@@ -118,10 +118,11 @@ def plugin_latency(port: int, reset: bool = False) -> dict | None:
             d = json.loads(r.read())
     except Exception:  # noqa: BLE001 - thread mode or endpoint unavailable
         return None
-    for e in d.get("gpushare_allocate_latency_seconds", []):
-        if e["labels"].get("phase") == "total":
-            return e
-    return None
+    phases = {e["labels"].get("phase"): e for e in d.get("gpushare_allocate_latency_seconds", [])}
+    tot = phases.get("total")
+    if tot is not None:
+        tot = dict(tot, phases={k: v.get("p50") for k, v in phases.items()})
+    return tot
 
 
 class ControlPlane:
@@ -688,6 +689,8 @@ def main():
             "allocate_p99_ms": ms(pct(cp.alloc_lat, 0.99)),
             "plugin_allocate_p50_ms": ms(srv["p50"]) if srv else None,
             "plugin_allocate_p99_ms": ms(srv["p99"]) if srv else None,
+            "plugin_allocate_phase_p50_ms": {k: ms(v) for k, v in srv["phases"].items() if v is not None}
+            if srv else None,
             "admission_p50_ms": ms(pct(cp.admit_lat, 0.5)),
             "pod_ready_p50_ms": ms(pct(ready_all, 0.5)),
             "pod_ready_p99_ms": ms(pct(ready_all, 0.99)),
