@@ -55,6 +55,22 @@ def test_bench_torchrun_two_ranks_gloo():
     assert ab["default@5ms"]["allocate_p50_ms"] < ab["reference@5ms"]["allocate_p50_ms"]
 
 
+def test_bench_torchrun_four_ranks_gloo():
+    """N=4: ranks outside the TP pair take the non-member path of its group, and admissions from
+    four churn pipelines interleave through rank 0's admission service (the shape of the
+    driver's 8-GPU run)."""
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+                        "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", "4",
+                        "--no-gpu", "--steps", "3", "--warmup", "1", "--compare-rtts", ""],
+                       cwd=ROOT, capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = parse(r.stdout)
+    assert d["n_gpus"] == 4 and d["pods_per_node"] == 16 and d["hbm_gib_per_node"] == 4 * 288
+    assert d["failed_admissions"] == 0 and d["value"] > 0
+    assert len(d["topology"]["tp_pair"]) == 2 and d["topology"]["pair_hops"] == 1
+
+
 def test_tp_pair_demo_gloo():
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "-m",
