@@ -22,6 +22,7 @@ SIGNATURES = {
     "gs_gemm_bf16_nt_repeat": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
     "gs_gemm_set_variant": [_I],
     "gs_gemm_set_group_m": [_I],
+    "gs_gemm_w4_set_sched": [_I],
     "gs_rmsnorm_bf16": [_P, _P, _P, _P, _P, _I, _I, _F, _P],
     "gs_silu_mul_bf16": [_P, _P, _I, _I, _P],
     "gs_rope_bf16": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P],

@@ -21,6 +21,12 @@ def set_gemm_group_m(g: int) -> None:
     _lib.check(_lib.lib().gs_gemm_set_group_m(int(g)), "gs_gemm_set_group_m")
 
 
+def set_gemm_w4_sched(s: int) -> None:
+    """Phase-B placement of DMA and fragment reads in the plain 4-wave product (0 = default,
+    1..5 = the alternatives in native/kernels/gemm_bf16_w4.hip), for schedule sweeps."""
+    _lib.check(_lib.lib().gs_gemm_w4_set_sched(int(s)), "gs_gemm_w4_set_sched")
+
+
 def set_gemm_variant(v: int) -> None:
     """Kernel selection (A/B measurement, tests): ``GEMM_AUTO`` = the 4-wave AGPR kernel
     (native/kernels/gemm_bf16_w4.hip) for M%256 == N%256 == K%128 == 0 with ldc%8 == 0, else the

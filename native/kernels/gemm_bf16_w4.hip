@@ -207,11 +207,12 @@ __device__ __forceinline__ void epilogue_swiglu(f32x4_t (&acc)[8][8], unsigned s
   }
 }
 
-// DMA_GROUPS: the 16 DMA instructions of a phase B go 16 / DMA_GROUPS at a time into its first
-// DMA_GROUPS MFMA groups (earlier issue = more time to land before the next boundary's wait).
-// The 16 fragment reads of each phase go two per group into its first 8 groups, after MFMAs
+// DMA_GROUPS: the 16 DMA instructions of a phase B go 16 / DMA_GROUPS at a time into MFMA groups
+// DMA_G0 .. DMA_G0 + DMA_GROUPS - 1 (earlier issue = more time to land before the next boundary's
+// wait). The 16 fragment reads of each phase go two per group into 8 consecutive groups (phase A:
+// 0-7; phase B: RDB_G0 .. RDB_G0 + 7, so DMA and reads can be kept apart in LDS time), after MFMAs
 // RD_U0 and RD_U1 of the group; a DMA follows MFMA DMA_U.
-template <int DMA_GROUPS, int RD_U0, int RD_U1, int DMA_U, int EPI>
+template <int DMA_GROUPS, int RD_U0, int RD_U1, int DMA_U, int EPI, int DMA_G0 = 0, int RDB_G0 = 0>
 __global__ __launch_bounds__(NT, 1) void gemm_bf16_nt_w4a(
     const unsigned short* __restrict__ A, const unsigned short* __restrict__ B, unsigned short* __restrict__ C,
     const unsigned short* __restrict__ bias, const unsigned short* __restrict__ R, int M, int N, int K, int lda,
@@ -322,12 +323,12 @@ __global__ __launch_bounds__(NT, 1) void gemm_bf16_nt_w4a(
     });
     // phase B: DMA of tile kt+2 into the buffer just released, set-0 reads of tile kt+1
     mfma_phase(acc, f1, [&](int g, int u) {
-      if (u == DMA_U && g < DMA_GROUPS) {
+      if (u == DMA_U && g >= DMA_G0 && g < DMA_G0 + DMA_GROUPS) {
 #pragma unroll
-        for (int d = 0; d < 16 / DMA_GROUPS; ++d) dma(buf, kdma, g * (16 / DMA_GROUPS) + d);
+        for (int d = 0; d < 16 / DMA_GROUPS; ++d) dma(buf, kdma, (g - DMA_G0) * (16 / DMA_GROUPS) + d);
       }
-      if (g < 8 && u == RD_U0) frag_read(f0, buf ^ 1, co0, 2 * g);
-      if (g < 8 && u == RD_U1) frag_read(f0, buf ^ 1, co0, 2 * g + 1);
+      if (g >= RDB_G0 && g < RDB_G0 + 8 && u == RD_U0) frag_read(f0, buf ^ 1, co0, 2 * (g - RDB_G0));
+      if (g >= RDB_G0 && g < RDB_G0 + 8 && u == RD_U1) frag_read(f0, buf ^ 1, co0, 2 * (g - RDB_G0) + 1);
     });
     // last MFMA D -> whatever reads the accumulators next: hipcc places its AGPR copies for
     // the epilogue on the loop-exit edge, ahead of any statement after the loop, so the pad
@@ -347,7 +348,18 @@ __global__ __launch_bounds__(NT, 1) void gemm_bf16_nt_w4a(
     epilogue_128x128<EPI>(acc, C, bias, R, ldc, m0 + wm * 128 + lr, n0 + wn * 128 + (lane >> 4) * 4, lane >> 4);
 }
 
+constexpr int W4_SCHEDS = 6;
+int g_w4_sched = 0;
+
 }  // namespace
+
+// Phase-B schedule of the plain 4-wave product (0 = default; 1..5 = the alternatives listed in
+// gs_gemm_w4_launch) for A/B sweeps (tools/gemm_sched_sweep.py).
+GS_KERNEL_API int gs_gemm_w4_set_sched(int s) {
+  if (s < 0 || s >= W4_SCHEDS) return GS_EINVAL;
+  g_w4_sched = s;
+  return GS_OK;
+}
 
 // Launch the 4-wave kernel; the caller (gs_gemm_bf16_nt) has validated pointers/strides/flags.
 // Returns GS_EINVAL when the shape or output layout does not suit it (the caller falls back).
@@ -366,15 +378,28 @@ int gs_gemm_w4_launch(const void* A, const void* B, void* C, const void* bias, c
                                 gemm_bf16_nt_w4a<16, 2, 3, 1, 4>, gemm_bf16_nt_w4a<16, 2, 3, 1, 5>,
                                 gemm_bf16_nt_w4a<16, 2, 3, 1, 6>, gemm_bf16_nt_w4a<16, 2, 3, 1, 7>,
                                 gemm_bf16_nt_w4a<16, 2, 3, 1, EP_SWIGLU>, gemm_bf16_nt_w4a<16, 2, 3, 1, EP_STAGED>};
+  // Alternative placements of phase B's DMA and fragment reads for the plain product (schedule
+  // sweeps, gs_gemm_w4_set_sched): <DMA groups, first DMA group, first read group of phase B>
+  static const Kern sched[W4_SCHEDS] = {
+      gemm_bf16_nt_w4a<16, 2, 3, 1, 0, 0, 0>,   // 0: default (DMA spread over 16 groups, reads 0-7)
+      gemm_bf16_nt_w4a<8, 2, 3, 1, 0, 0, 8>,    // 1: DMA in groups 0-7, reads 8-15
+      gemm_bf16_nt_w4a<16, 2, 3, 1, 0, 0, 4>,   // 2: DMA spread, reads 4-11
+      gemm_bf16_nt_w4a<8, 2, 3, 1, 0, 0, 4>,    // 3: DMA in groups 0-7, reads 4-11
+      gemm_bf16_nt_w4a<8, 2, 3, 1, 0, 8, 0>,    // 4: reads 0-7, DMA in groups 8-15
+      gemm_bf16_nt_w4a<16, 2, 3, 1, 0, 0, 8>,   // 5: DMA spread, reads 8-15
+  };
   static const bool staged = [] {
     const char* e = getenv("GS_W4_STAGED_EPI");
     return e != nullptr && e[0] == '1';
   }();
   if ((flags & EP_SWIGLU) && (flags & 7)) return GS_EINVAL;   // SwiGLU takes no other epilogue
-  const Kern kern = kerns[(flags & EP_SWIGLU) ? 8 : (flags & 7) ? (flags & 7) : staged ? 9 : 0];
+  Kern kern = kerns[(flags & EP_SWIGLU) ? 8 : (flags & 7) ? (flags & 7) : staged ? 9 : 0];
+  if (kern == kerns[0] && g_w4_sched > 0) kern = sched[g_w4_sched];
   static bool attr_set = false;
   if (!attr_set) {
     for (Kern k : kerns)
+      (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    for (Kern k : sched)
       (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     attr_set = true;
   }

@@ -80,6 +80,27 @@ def test_gemm_pingpong_matches_v1_and_fp32(M, N, K):
         assert (o1.float() - o2.float()).abs().max().item() <= (o1.float().abs().max().item() * 2 ** -7)
 
 
+@pytest.mark.parametrize("sched", range(6))
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 768, 512), (2048, 1024, 1024)])
+def test_gemm_w4_schedules_bitwise_equal(sched, M, N, K):
+    """Every phase-B schedule of the 4-wave kernel moves only where DMA and fragment reads issue,
+    not the accumulation order: bitwise-equal to the default schedule and within fp32 tolerance."""
+    from aliyun_gpushare_device_plugin_amd.ops import gemm_nt
+    from aliyun_gpushare_device_plugin_amd.ops.gemm import set_gemm_w4_sched
+    a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    b = torch.randn(N, K, device="cuda", dtype=torch.bfloat16)
+    try:
+        set_gemm_w4_sched(0)
+        o0 = gemm_nt(a, b)
+        set_gemm_w4_sched(sched)
+        o = gemm_nt(a, b)
+        torch.cuda.synchronize()
+    finally:
+        set_gemm_w4_sched(0)
+    assert torch.equal(o, o0)
+    assert_close_bf16(o, ref_linear(a, b), K)
+
+
 def test_gemm_identity_asymmetric():
     """A = I with an asymmetric B catches a transposed C-write (guide §3)."""
     from aliyun_gpushare_device_plugin_amd.ops import gemm_nt
