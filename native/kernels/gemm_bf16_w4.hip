@@ -37,7 +37,7 @@ constexpr int STAGE = 2 * A_STAGE;     // A + B
 constexpr int LDS_BYTES = 2 * STAGE;   // 128 KiB
 constexpr int GROUP_M = 8;
 
-enum { EP_BIAS = 1, EP_SILU = 2, EP_RESID = 4, EP_SWIGLU = 8, EP_STAGED = 16 };   // 16: internal only
+enum { EP_BIAS = 1, EP_SILU = 2, EP_RESID = 4, EP_SWIGLU = 8, EP_STAGED = 16, EP_NT = 32, EP_WT = 64 };   // 16-64: internal only
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
@@ -76,6 +76,25 @@ __device__ __forceinline__ void tile_origin(int M, int N, int flags, int& m0, in
   const int gsz = min(nbm - first_m, gm);
   m0 = (first_m + (wgid % per_group) % gsz) * BM;
   n0 = ((wgid % per_group) / gsz) * BN;
+}
+
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+
+// One 16-B C store. EP_WT | EP_NT (the default of every epilogue): device scope + streamed, so C is
+// written through L2 instead of sitting dirty there until the kernel-end release writes it back
+// (4096^3 back to back: 93.8 -> 91.5 us, 8192^3: 698 -> 679 us; profiles/gemm_store_policy_r2.md).
+// The s_nop covers the store-data hazard hipcc does not see through asm (a VALU overwriting a
+// >8-B store's data VGPRs right after issue).
+template <int EPI>
+__device__ __forceinline__ void store16(u32x4_t* dst, u32x4_t val) {
+  if constexpr ((EPI & EP_WT) != 0 && (EPI & EP_NT) != 0)
+    asm volatile("global_store_dwordx4 %0, %1, off sc1 nt\n\ts_nop 1" ::"v"(dst), "v"(val) : "memory");
+  else if constexpr ((EPI & EP_WT) != 0)
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(dst), "v"(val) : "memory");
+  else if constexpr ((EPI & EP_NT) != 0)
+    __builtin_nontemporal_store(val, dst);
+  else
+    *dst = val;
 }
 
 // Epilogue of a 128x128 wave tile. Lane (row r = lane & 15, quad q = lane >> 4) holds
@@ -129,8 +148,7 @@ __device__ __forceinline__ void epilogue_128x128(f32x4_t (&acc)[8][8], unsigned 
         w[0][d] = r[0];
         w[1][d] = r[1];
       }
-      typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-      *(u32x4_t*)(C + (size_t)m * ldc + ncol + 32 * jp) = u32x4_t{w[0][0], w[0][1], w[1][0], w[1][1]};
+      store16<EPI>((u32x4_t*)(C + (size_t)m * ldc + ncol + 32 * jp), u32x4_t{w[0][0], w[0][1], w[1][0], w[1][1]});
     }
     __builtin_amdgcn_sched_barrier(0);   // one row of tiles at a time: bounds VGPR pressure
   }
@@ -158,7 +176,6 @@ __device__ __forceinline__ void epilogue_staged(f32x4_t (&acc)[8][8], unsigned s
     }
     __builtin_amdgcn_sched_barrier(0);
   }
-  typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
   const int chunk = lane & 15;
 #pragma unroll 8
   for (int rb = 0; rb < 32; ++rb) {
@@ -174,6 +191,7 @@ __device__ __forceinline__ void epilogue_staged(f32x4_t (&acc)[8][8], unsigned s
 // writes a 128 x 64 feature tile of the [M, N/2] output (ldc in features); pairs of feature
 // tiles are merged by v_permlane16_swap into 16-B stores as in epilogue_128x128. Saves writing
 // and re-reading the [M, N] gate|up activations (the separate silu_mul pass).
+template <int EPI>
 __device__ __forceinline__ void epilogue_swiglu(f32x4_t (&acc)[8][8], unsigned short* __restrict__ C, int ldc,
                                                 int mbase, int fbase, int q) {
   const int fcol = fbase + 16 * (q & 1) + 8 * (q >> 1);
@@ -200,8 +218,7 @@ __device__ __forceinline__ void epilogue_swiglu(f32x4_t (&acc)[8][8], unsigned s
         w[0][d] = r[0];
         w[1][d] = r[1];
       }
-      typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-      *(u32x4_t*)(C + (size_t)m * ldc + fcol + 32 * jp) = u32x4_t{w[0][0], w[0][1], w[1][0], w[1][1]};
+      store16<EPI>((u32x4_t*)(C + (size_t)m * ldc + fcol + 32 * jp), u32x4_t{w[0][0], w[0][1], w[1][0], w[1][1]});
     }
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -343,17 +360,17 @@ __global__ __launch_bounds__(NT, 1) void gemm_bf16_nt_w4a(
     __builtin_amdgcn_s_barrier();
     epilogue_staged(acc, C, ldc, smem + wave * 32768, m0 + wm * 128, n0 + wn * 128, lane);
   } else if constexpr ((EPI & EP_SWIGLU) != 0)
-    epilogue_swiglu(acc, C, ldc, m0 + wm * 128 + lr, (n0 + wn * 128) / 2, lane >> 4);
+    epilogue_swiglu<EPI>(acc, C, ldc, m0 + wm * 128 + lr, (n0 + wn * 128) / 2, lane >> 4);
   else
     epilogue_128x128<EPI>(acc, C, bias, R, ldc, m0 + wm * 128 + lr, n0 + wn * 128 + (lane >> 4) * 4, lane >> 4);
 }
 
-constexpr int W4_SCHEDS = 6;
+constexpr int W4_SCHEDS = 10;
 int g_w4_sched = 0;
 
 }  // namespace
 
-// Phase-B schedule of the plain 4-wave product (0 = default; 1..5 = the alternatives listed in
+// Phase-B schedule of the plain 4-wave product (0 = default; 1..9 = the alternatives listed in
 // gs_gemm_w4_launch) for A/B sweeps (tools/gemm_sched_sweep.py).
 GS_KERNEL_API int gs_gemm_w4_set_sched(int s) {
   if (s < 0 || s >= W4_SCHEDS) return GS_EINVAL;
@@ -373,20 +390,25 @@ int gs_gemm_w4_launch(const void* A, const void* B, void* C, const void* bias, c
   // the best of the placements swept on MI355X (profiles/gemm_w4_variants.md)
   using Kern = void (*)(const unsigned short*, const unsigned short*, unsigned short*, const unsigned short*,
                        const unsigned short*, int, int, int, int, int, int, int);
-  static const Kern kerns[10] = {gemm_bf16_nt_w4a<16, 2, 3, 1, 0>, gemm_bf16_nt_w4a<16, 2, 3, 1, 1>,
-                                gemm_bf16_nt_w4a<16, 2, 3, 1, 2>, gemm_bf16_nt_w4a<16, 2, 3, 1, 3>,
-                                gemm_bf16_nt_w4a<16, 2, 3, 1, 4>, gemm_bf16_nt_w4a<16, 2, 3, 1, 5>,
-                                gemm_bf16_nt_w4a<16, 2, 3, 1, 6>, gemm_bf16_nt_w4a<16, 2, 3, 1, 7>,
-                                gemm_bf16_nt_w4a<16, 2, 3, 1, EP_SWIGLU>, gemm_bf16_nt_w4a<16, 2, 3, 1, EP_STAGED>};
+  constexpr int ST = EP_WT | EP_NT;   // C store policy of every default kernel (store16)
+  static const Kern kerns[10] = {gemm_bf16_nt_w4a<16, 2, 3, 1, ST>, gemm_bf16_nt_w4a<16, 2, 3, 1, 1 | ST>,
+                                gemm_bf16_nt_w4a<16, 2, 3, 1, 2 | ST>, gemm_bf16_nt_w4a<16, 2, 3, 1, 3 | ST>,
+                                gemm_bf16_nt_w4a<16, 2, 3, 1, 4 | ST>, gemm_bf16_nt_w4a<16, 2, 3, 1, 5 | ST>,
+                                gemm_bf16_nt_w4a<16, 2, 3, 1, 6 | ST>, gemm_bf16_nt_w4a<16, 2, 3, 1, 7 | ST>,
+                                gemm_bf16_nt_w4a<16, 2, 3, 1, EP_SWIGLU | ST>, gemm_bf16_nt_w4a<16, 2, 3, 1, EP_STAGED>};
   // Alternative placements of phase B's DMA and fragment reads for the plain product (schedule
   // sweeps, gs_gemm_w4_set_sched): <DMA groups, first DMA group, first read group of phase B>
   static const Kern sched[W4_SCHEDS] = {
-      gemm_bf16_nt_w4a<16, 2, 3, 1, 0, 0, 0>,   // 0: default (DMA spread over 16 groups, reads 0-7)
+      gemm_bf16_nt_w4a<16, 2, 3, 1, ST, 0, 0>,  // 0: default (DMA spread over 16 groups, reads 0-7, ST stores)
       gemm_bf16_nt_w4a<8, 2, 3, 1, 0, 0, 8>,    // 1: DMA in groups 0-7, reads 8-15
       gemm_bf16_nt_w4a<16, 2, 3, 1, 0, 0, 4>,   // 2: DMA spread, reads 4-11
       gemm_bf16_nt_w4a<8, 2, 3, 1, 0, 0, 4>,    // 3: DMA in groups 0-7, reads 4-11
       gemm_bf16_nt_w4a<8, 2, 3, 1, 0, 8, 0>,    // 4: reads 0-7, DMA in groups 8-15
       gemm_bf16_nt_w4a<16, 2, 3, 1, 0, 0, 8>,   // 5: DMA spread, reads 8-15
+      gemm_bf16_nt_w4a<16, 2, 3, 1, EP_NT, 0, 0>,   // 6: 0 with non-temporal C stores
+      gemm_bf16_nt_w4a<16, 2, 3, 1, EP_NT, 0, 8>,   // 7: 5 with non-temporal C stores
+      gemm_bf16_nt_w4a<16, 2, 3, 1, EP_WT, 0, 0>,   // 8: 0 with device-scope (write-through) C stores
+      gemm_bf16_nt_w4a<16, 2, 3, 1, 0, 0, 0>,   // 9: 0 with plain (write-back) C stores
   };
   static const bool staged = [] {
     const char* e = getenv("GS_W4_STAGED_EPI");
