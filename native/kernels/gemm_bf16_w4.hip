@@ -229,7 +229,12 @@ __device__ __forceinline__ void epilogue_swiglu(f32x4_t (&acc)[8][8], unsigned s
 // wait). The 16 fragment reads of each phase go two per group into 8 consecutive groups (phase A:
 // 0-7; phase B: RDB_G0 .. RDB_G0 + 7, so DMA and reads can be kept apart in LDS time), after MFMAs
 // RD_U0 and RD_U1 of the group; a DMA follows MFMA DMA_U.
-template <int DMA_GROUPS, int RD_U0, int RD_U1, int DMA_U, int EPI, int DMA_G0 = 0, int RDB_G0 = 0>
+// NSTG (0, 4 or 8): the last NSTG of the 16 pieces of a K-tile (B rows) skip the LDS DMA: they are
+// loaded into VGPRs during phase A (buffer_load_dwordx4, one per group from group 0) and written
+// to the same LDS image in phase B (ds_write_b128, lane-linear like the DMA, conflict-free), in
+// the groups between the remaining DMA pieces. The boundary wait then leaves those NSTG loads in
+// flight (vmcnt(NSTG)).
+template <int DMA_GROUPS, int RD_U0, int RD_U1, int DMA_U, int EPI, int DMA_G0 = 0, int RDB_G0 = 0, int NSTG = 0>
 __global__ __launch_bounds__(NT, 1) void gemm_bf16_nt_w4a(
     const unsigned short* __restrict__ A, const unsigned short* __restrict__ B, unsigned short* __restrict__ C,
     const unsigned short* __restrict__ bias, const unsigned short* __restrict__ R, int M, int N, int K, int lda,
@@ -276,6 +281,18 @@ __global__ __launch_bounds__(NT, 1) void gemm_bf16_nt_w4a(
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           rB, (__attribute__((address_space(3))) void*)(wdst + buf * STAGE + A_STAGE + i * 4096), 16, voffB,
           i * b32 + koff, 0, 0);
+  };
+
+  static_assert(NSTG == 0 || NSTG == 4 || NSTG == 8, "NSTG: 0, 4 or 8 staged B pieces");
+  u32x4_t stg[NSTG > 0 ? NSTG : 1];
+  // staged piece s = DMA piece 16 - NSTG + s (B rows i = that & 7), same global bytes and LDS slot
+  auto stage_load = [&](int kt, int s) {
+    const int i = (16 - NSTG + s) & 7;
+    stg[s] = __builtin_amdgcn_raw_buffer_load_b128(rB, (int)voffB, (int)(i * b32 + (unsigned)kt * (BK * 2)), 0);
+  };
+  auto stage_write = [&](int buf, int s) {
+    const int i = (16 - NSTG + s) & 7;
+    *(u32x4_t*)(wdst + buf * STAGE + A_STAGE + i * 4096 + lane * 16) = stg[s];
   };
 
   // ---- fragment addressing: lane reads row (lane & 15) of a 16-row tile, k-chunk
@@ -333,14 +350,26 @@ __global__ __launch_bounds__(NT, 1) void gemm_bf16_nt_w4a(
     // phase A: set-1 reads; the boundary wait sits between the last two MFMAs and the barrier
     // after the last one, so the matrix pipe stays busy while the wave waits
     mfma_phase(acc, f0, [&](int g, int u) {
+      if (NSTG > 0 && g < NSTG && u == 0) stage_load(kdma, g);
       if (g < 8 && u == RD_U0) frag_read(f1, buf, co1, 2 * g);
       if (g < 8 && u == RD_U1) frag_read(f1, buf, co1, 2 * g + 1);
-      if (g == 15 && u == 2) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      if (g == 15 && u == 2) {
+        if constexpr (NSTG == 8)
+          asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+        else if constexpr (NSTG == 4)
+          asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      }
       if (g == 15 && u == 3) __builtin_amdgcn_s_barrier();
     });
     // phase B: DMA of tile kt+2 into the buffer just released, set-0 reads of tile kt+1
     mfma_phase(acc, f1, [&](int g, int u) {
-      if (u == DMA_U && g >= DMA_G0 && g < DMA_G0 + DMA_GROUPS) {
+      if constexpr (NSTG > 0) {
+        constexpr int step = 16 / NSTG;   // every step-th group writes a staged piece
+        if (u == DMA_U && g % step == step - 1) stage_write(buf, g / step);
+        else if (u == DMA_U) dma(buf, kdma, g - g / step);
+      } else if (u == DMA_U && g >= DMA_G0 && g < DMA_G0 + DMA_GROUPS) {
 #pragma unroll
         for (int d = 0; d < 16 / DMA_GROUPS; ++d) dma(buf, kdma, (g - DMA_G0) * (16 / DMA_GROUPS) + d);
       }
@@ -365,12 +394,12 @@ __global__ __launch_bounds__(NT, 1) void gemm_bf16_nt_w4a(
     epilogue_128x128<EPI>(acc, C, bias, R, ldc, m0 + wm * 128 + lr, n0 + wn * 128 + (lane >> 4) * 4, lane >> 4);
 }
 
-constexpr int W4_SCHEDS = 10;
+constexpr int W4_SCHEDS = 12;
 int g_w4_sched = 0;
 
 }  // namespace
 
-// Phase-B schedule of the plain 4-wave product (0 = default; 1..9 = the alternatives listed in
+// Phase-B schedule of the plain 4-wave product (0 = default; 1..11 = the alternatives listed in
 // gs_gemm_w4_launch) for A/B sweeps (tools/gemm_sched_sweep.py).
 GS_KERNEL_API int gs_gemm_w4_set_sched(int s) {
   if (s < 0 || s >= W4_SCHEDS) return GS_EINVAL;
@@ -409,6 +438,8 @@ int gs_gemm_w4_launch(const void* A, const void* B, void* C, const void* bias, c
       gemm_bf16_nt_w4a<16, 2, 3, 1, EP_NT, 0, 8>,   // 7: 5 with non-temporal C stores
       gemm_bf16_nt_w4a<16, 2, 3, 1, EP_WT, 0, 0>,   // 8: 0 with device-scope (write-through) C stores
       gemm_bf16_nt_w4a<16, 2, 3, 1, 0, 0, 0>,   // 9: 0 with plain (write-back) C stores
+      gemm_bf16_nt_w4a<16, 2, 3, 1, ST, 0, 0, 8>,   // 10: 0 with B staged through VGPRs (A by DMA)
+      gemm_bf16_nt_w4a<16, 2, 3, 1, ST, 0, 0, 4>,   // 11: 0 with half of B staged through VGPRs
   };
   static const bool staged = [] {
     const char* e = getenv("GS_W4_STAGED_EPI");

@@ -32,7 +32,7 @@ def time_fn(fn, iters=20):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shapes", default="4096x4096x4096,4096x4096x1024,8192x8192x8192,4096x4096x14336")
-    ap.add_argument("--scheds", default="0,9,6,8")
+    ap.add_argument("--scheds", default="0,10,11")
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
