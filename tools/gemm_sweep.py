@@ -29,17 +29,19 @@ for shape in sys.argv[1].split(",") if len(sys.argv) > 1 else ["4096x4096x4096",
     w = torch.empty(N, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)
     out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
     row = {"shape": shape}
-    gms = [1, 2, 4, 8, 16, 32]
+    gms = [int(g) for g in os.environ.get("GMS", "1,2,4,8,16,32").split(",")]
     times = {g: [] for g in gms}
+    times["torch"] = []
     for g in gms:
         set_gemm_group_m(g)
         gemm_nt(x, w, out=out)
-    for _ in range(5):
+    for _ in range(int(os.environ.get("ROUNDS", "5"))):
         for g in gms:
             set_gemm_group_m(g)
             times[g].append(t(lambda: gemm_nt(x, w, out=out)))
+        times["torch"].append(t(lambda: torch.matmul(x, w.t(), out=out)))
     set_gemm_group_m(0)
-    for g in gms:
-        row[f"gm{g}_tflops"] = round(2.0 * M * N * K / statistics.median(times[g]) / 1e9, 1)
+    for g in times:
+        row[f"gm{g}_tflops" if g != "torch" else "torch_tflops"] = round(2.0 * M * N * K / statistics.median(times[g]) / 1e9, 1)
     print(json.dumps(row), flush=True)
     res.append(row)
