@@ -35,7 +35,10 @@ constexpr int BM = 256, BN = 256, BK = 64, NT = 256;
 constexpr int A_STAGE = BM * BK * 2;   // 32 KiB
 constexpr int STAGE = 2 * A_STAGE;     // A + B
 constexpr int LDS_BYTES = 2 * STAGE;   // 128 KiB
-constexpr int GROUP_M = 8;
+// Tile rasterisation group height. 4 over 8 for the 4-wave kernel with streamed stores, interleaved
+// on one box (profiles/gemm_group_m_ab_w4_r2.jsonl): 4096^3 +1.9 %, 4096x4096x1024 +5.3 %,
+// 8192^3 +0.8 %, 16384x4096x4096 +0.5 %, 4096x4096x14336 +0.4 %, 4096x14336x4096 -1.2 %.
+constexpr int GROUP_M = 4;
 
 enum { EP_BIAS = 1, EP_SILU = 2, EP_RESID = 4, EP_SWIGLU = 8, EP_STAGED = 16, EP_NT = 32, EP_WT = 64 };   // 16-64: internal only
 
