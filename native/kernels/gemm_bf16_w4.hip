@@ -237,7 +237,12 @@ __device__ __forceinline__ void epilogue_swiglu(f32x4_t (&acc)[8][8], unsigned s
 // to the same LDS image in phase B (ds_write_b128, lane-linear like the DMA, conflict-free), in
 // the groups between the remaining DMA pieces. The boundary wait then leaves those NSTG loads in
 // flight (vmcnt(NSTG)).
-template <int DMA_GROUPS, int RD_U0, int RD_U1, int DMA_U, int EPI, int DMA_G0 = 0, int RDB_G0 = 0, int NSTG = 0>
+// KV (schedule 12 only): the K-tile offset goes into the per-lane VGPR offset (one v_add per operand
+// and tile) and the scalar offset is the loop-invariant row offset i * 32 rows, instead of an s_add
+// per DMA piece: 14 fewer SALU per K-tile, yet measured 0.6 % faster at 4096^3 and 1-2 % slower at
+// 8192^3, long K and N = 14336 (order-rotated sweep, profiles/gemm_kv_offset_r2_rotated.json).
+template <int DMA_GROUPS, int RD_U0, int RD_U1, int DMA_U, int EPI, int DMA_G0 = 0, int RDB_G0 = 0, int NSTG = 0,
+          int KV = 0>
 __global__ __launch_bounds__(NT, 1) void gemm_bf16_nt_w4a(
     const unsigned short* __restrict__ A, const unsigned short* __restrict__ B, unsigned short* __restrict__ C,
     const unsigned short* __restrict__ bias, const unsigned short* __restrict__ R, int M, int N, int K, int lda,
@@ -277,13 +282,14 @@ __global__ __launch_bounds__(NT, 1) void gemm_bf16_nt_w4a(
   auto dma = [&](int buf, int kt, int g) {
     const int i = g & 7;
     const unsigned koff = (unsigned)kt * (BK * 2);
+    const unsigned va = KV ? voffA + koff : voffA, vb = KV ? voffB + koff : voffB;
+    const unsigned sa = KV ? i * a32 : i * a32 + koff, sb = KV ? i * b32 : i * b32 + koff;
     if (g < 8)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rA, (__attribute__((address_space(3))) void*)(wdst + buf * STAGE + i * 4096), 16, voffA, i * a32 + koff, 0, 0);
+          rA, (__attribute__((address_space(3))) void*)(wdst + buf * STAGE + i * 4096), 16, va, sa, 0, 0);
     else
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rB, (__attribute__((address_space(3))) void*)(wdst + buf * STAGE + A_STAGE + i * 4096), 16, voffB,
-          i * b32 + koff, 0, 0);
+          rB, (__attribute__((address_space(3))) void*)(wdst + buf * STAGE + A_STAGE + i * 4096), 16, vb, sb, 0, 0);
   };
 
   static_assert(NSTG == 0 || NSTG == 4 || NSTG == 8, "NSTG: 0, 4 or 8 staged B pieces");
@@ -397,12 +403,12 @@ __global__ __launch_bounds__(NT, 1) void gemm_bf16_nt_w4a(
     epilogue_128x128<EPI>(acc, C, bias, R, ldc, m0 + wm * 128 + lr, n0 + wn * 128 + (lane >> 4) * 4, lane >> 4);
 }
 
-constexpr int W4_SCHEDS = 12;
+constexpr int W4_SCHEDS = 13;
 int g_w4_sched = 0;
 
 }  // namespace
 
-// Phase-B schedule of the plain 4-wave product (0 = default; 1..11 = the alternatives listed in
+// Phase-B schedule of the plain 4-wave product (0 = default; 1..12 = the alternatives listed in
 // gs_gemm_w4_launch) for A/B sweeps (tools/gemm_sched_sweep.py).
 GS_KERNEL_API int gs_gemm_w4_set_sched(int s) {
   if (s < 0 || s >= W4_SCHEDS) return GS_EINVAL;
@@ -423,15 +429,20 @@ int gs_gemm_w4_launch(const void* A, const void* B, void* C, const void* bias, c
   using Kern = void (*)(const unsigned short*, const unsigned short*, unsigned short*, const unsigned short*,
                        const unsigned short*, int, int, int, int, int, int, int);
   constexpr int ST = EP_WT | EP_NT;   // C store policy of every default kernel (store16)
-  static const Kern kerns[10] = {gemm_bf16_nt_w4a<16, 2, 3, 1, ST>, gemm_bf16_nt_w4a<16, 2, 3, 1, 1 | ST>,
-                                gemm_bf16_nt_w4a<16, 2, 3, 1, 2 | ST>, gemm_bf16_nt_w4a<16, 2, 3, 1, 3 | ST>,
-                                gemm_bf16_nt_w4a<16, 2, 3, 1, 4 | ST>, gemm_bf16_nt_w4a<16, 2, 3, 1, 5 | ST>,
-                                gemm_bf16_nt_w4a<16, 2, 3, 1, 6 | ST>, gemm_bf16_nt_w4a<16, 2, 3, 1, 7 | ST>,
-                                gemm_bf16_nt_w4a<16, 2, 3, 1, EP_SWIGLU | ST>, gemm_bf16_nt_w4a<16, 2, 3, 1, EP_STAGED>};
+  static const Kern kerns[10] = {gemm_bf16_nt_w4a<16, 2, 3, 1, ST, 0, 0, 0, 0>,
+                                gemm_bf16_nt_w4a<16, 2, 3, 1, 1 | ST, 0, 0, 0, 0>,
+                                gemm_bf16_nt_w4a<16, 2, 3, 1, 2 | ST, 0, 0, 0, 0>,
+                                gemm_bf16_nt_w4a<16, 2, 3, 1, 3 | ST, 0, 0, 0, 0>,
+                                gemm_bf16_nt_w4a<16, 2, 3, 1, 4 | ST, 0, 0, 0, 0>,
+                                gemm_bf16_nt_w4a<16, 2, 3, 1, 5 | ST, 0, 0, 0, 0>,
+                                gemm_bf16_nt_w4a<16, 2, 3, 1, 6 | ST, 0, 0, 0, 0>,
+                                gemm_bf16_nt_w4a<16, 2, 3, 1, 7 | ST, 0, 0, 0, 0>,
+                                gemm_bf16_nt_w4a<16, 2, 3, 1, EP_SWIGLU | ST, 0, 0, 0, 0>,
+                                gemm_bf16_nt_w4a<16, 2, 3, 1, EP_STAGED, 0, 0, 0, 0>};
   // Alternative placements of phase B's DMA and fragment reads for the plain product (schedule
   // sweeps, gs_gemm_w4_set_sched): <DMA groups, first DMA group, first read group of phase B>
   static const Kern sched[W4_SCHEDS] = {
-      gemm_bf16_nt_w4a<16, 2, 3, 1, ST, 0, 0>,  // 0: default (DMA spread over 16 groups, reads 0-7, ST stores)
+      gemm_bf16_nt_w4a<16, 2, 3, 1, ST, 0, 0, 0, 0>,   // 0: default (DMA spread over 16 groups, reads 0-7, ST stores)
       gemm_bf16_nt_w4a<8, 2, 3, 1, 0, 0, 8>,    // 1: DMA in groups 0-7, reads 8-15
       gemm_bf16_nt_w4a<16, 2, 3, 1, 0, 0, 4>,   // 2: DMA spread, reads 4-11
       gemm_bf16_nt_w4a<8, 2, 3, 1, 0, 0, 4>,    // 3: DMA in groups 0-7, reads 4-11
@@ -440,9 +451,10 @@ int gs_gemm_w4_launch(const void* A, const void* B, void* C, const void* bias, c
       gemm_bf16_nt_w4a<16, 2, 3, 1, EP_NT, 0, 0>,   // 6: 0 with non-temporal C stores
       gemm_bf16_nt_w4a<16, 2, 3, 1, EP_NT, 0, 8>,   // 7: 5 with non-temporal C stores
       gemm_bf16_nt_w4a<16, 2, 3, 1, EP_WT, 0, 0>,   // 8: 0 with device-scope (write-through) C stores
-      gemm_bf16_nt_w4a<16, 2, 3, 1, 0, 0, 0>,   // 9: 0 with plain (write-back) C stores
+      gemm_bf16_nt_w4a<16, 2, 3, 1, 0, 0, 0>,   // 9: plain (write-back) C stores, scalar K offsets
       gemm_bf16_nt_w4a<16, 2, 3, 1, ST, 0, 0, 8>,   // 10: 0 with B staged through VGPRs (A by DMA)
       gemm_bf16_nt_w4a<16, 2, 3, 1, ST, 0, 0, 4>,   // 11: 0 with half of B staged through VGPRs
+      gemm_bf16_nt_w4a<16, 2, 3, 1, ST, 0, 0, 0, 1>,   // 12: 0 with the K offset in the VGPR offset (KV)
   };
   static const bool staged = [] {
     const char* e = getenv("GS_W4_STAGED_EPI");

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Phase-B schedule sweep of the 4-wave GEMM (placement of the LDS DMA and the fragment reads,
-``set_gemm_w4_sched``) against torch.matmul (hipBLASLt), interleaved rounds in one process, event
-timing of 20 back-to-back launches. Each schedule's output is checked against torch's first.
+``set_gemm_w4_sched``) against torch.matmul (hipBLASLt), interleaved rounds in one process (order
+rotated every round), event timing of 20 back-to-back launches. Each schedule's output is checked against torch's first.
 
 python tools/gemm_sched_sweep.py [--shapes 4096x4096x4096,...] [--scheds 0,1,2,3,4,5]
 """
@@ -64,9 +64,10 @@ def main():
         for f in fns.values():
             time_fn(f, 5)
         t = {k: [] for k in fns}
-        for _ in range(a.rounds):
-            for k, f in fns.items():
-                t[k].append(time_fn(f))
+        names = list(fns)
+        for r in range(a.rounds):   # rotate the order every round: a fixed order biases by position
+            for k in names[r % len(names):] + names[:r % len(names)]:
+                t[k].append(time_fn(fns[k]))
         set_gemm_w4_sched(0)
         flop = 2.0 * M * N * K
         for k, v in t.items():
