@@ -52,9 +52,10 @@ def main():
                                                              is_causal=causal, enable_gqa=True)
         torch.cuda.synchronize()
         times = {k_: [] for k_ in fns}
-        for _ in range(5):
-            for k_, f in fns.items():
-                times[k_].append(timed(f))
+        names = list(fns)
+        for r in range(5):   # order rotated every round (a fixed order biases by slot)
+            for k_ in names[r % len(names):] + names[:r % len(names)]:
+                times[k_].append(timed(fns[k_]))
         for k_, t in times.items():
             med = statistics.median(t)
             row[f"{k_}_tflops"] = round(flop / med / 1e9, 1)

@@ -58,9 +58,10 @@ def main():
                 f()
         torch.cuda.synchronize()
         times = {k: [] for k in fns}
-        for _ in range(a.rounds):
-            for k, f in fns.items():
-                times[k].append(time_fn(f, a.iters))
+        names = list(fns)
+        for r in range(a.rounds):   # order rotated every round (a fixed order biases by slot)
+            for k in names[r % len(names):] + names[:r % len(names)]:
+                times[k].append(time_fn(fns[k], a.iters))
         set_gemm_variant(GEMM_AUTO)
         flop = 2.0 * M * N * K
         row = {"shape": [M, N, K]}
