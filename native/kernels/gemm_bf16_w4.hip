@@ -403,12 +403,12 @@ __global__ __launch_bounds__(NT, 1) void gemm_bf16_nt_w4a(
     epilogue_128x128<EPI>(acc, C, bias, R, ldc, m0 + wm * 128 + lr, n0 + wn * 128 + (lane >> 4) * 4, lane >> 4);
 }
 
-constexpr int W4_SCHEDS = 13;
+constexpr int W4_SCHEDS = 16;
 int g_w4_sched = 0;
 
 }  // namespace
 
-// Phase-B schedule of the plain 4-wave product (0 = default; 1..12 = the alternatives listed in
+// Phase-B schedule of the plain 4-wave product (0 = default; 1..15 = the alternatives listed in
 // gs_gemm_w4_launch) for A/B sweeps (tools/gemm_sched_sweep.py).
 GS_KERNEL_API int gs_gemm_w4_set_sched(int s) {
   if (s < 0 || s >= W4_SCHEDS) return GS_EINVAL;
@@ -455,6 +455,9 @@ int gs_gemm_w4_launch(const void* A, const void* B, void* C, const void* bias, c
       gemm_bf16_nt_w4a<16, 2, 3, 1, ST, 0, 0, 8>,   // 10: 0 with B staged through VGPRs (A by DMA)
       gemm_bf16_nt_w4a<16, 2, 3, 1, ST, 0, 0, 4>,   // 11: 0 with half of B staged through VGPRs
       gemm_bf16_nt_w4a<16, 2, 3, 1, ST, 0, 0, 0, 1>,   // 12: 0 with the K offset in the VGPR offset (KV)
+      gemm_bf16_nt_w4a<16, 2, 3, 0, ST>,   // 13: 0 with the DMA after MFMA 0 of its group
+      gemm_bf16_nt_w4a<16, 1, 2, 3, ST>,   // 14: reads after MFMAs 1 / 2, DMA after MFMA 3
+      gemm_bf16_nt_w4a<16, 0, 1, 2, ST>,   // 15: reads after MFMAs 0 / 1, DMA after MFMA 2
   };
   static const bool staged = [] {
     const char* e = getenv("GS_W4_STAGED_EPI");

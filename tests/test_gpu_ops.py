@@ -80,7 +80,7 @@ def test_gemm_pingpong_matches_v1_and_fp32(M, N, K):
         assert (o1.float() - o2.float()).abs().max().item() <= (o1.float().abs().max().item() * 2 ** -7)
 
 
-@pytest.mark.parametrize("sched", range(13))
+@pytest.mark.parametrize("sched", range(16))
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 768, 512), (2048, 1024, 1024)])
 def test_gemm_w4_schedules_bitwise_equal(sched, M, N, K):
     """Every phase-B schedule of the 4-wave kernel moves only where DMA and fragment reads issue,
