@@ -34,7 +34,14 @@ MI355X build, same protocol, different mechanics:
   then fails the second pod (``allocate.go:182-187``: no Pending candidate left); here, when no
   Pending pod matches, an equal-size pod that is bound, un-assigned, recently assumed and never
   allocated by this process is matched instead — the two pods simply exchange their
-  extender-reserved GPUs, so per-GPU accounting stays exact.
+  extender-reserved GPUs;
+* placement truth (``alloc/placement.py``): every answered container is recorded in a grant
+  book (fake-ID set → GPU); with the kubelet's pod-resources API configured, the plugin asks
+  for ``PreStartContainer`` and, before each container starts (and every ``placement_s``),
+  joins the book with which pod holds which IDs and rewrites ``IDX`` / the allocation JSON /
+  CU slots to where the containers really run — a swapped admission never leaves the
+  extender's ledger pointing at the wrong GPU, so deleting one of the pods frees the GPU it
+  actually used.
 """
 from __future__ import annotations
 
@@ -54,6 +61,7 @@ from ..utils import log, units as U
 from ..utils.metrics import PluginMetrics
 from . import annotations as A
 from . import cuslots
+from . import placement as PL
 from .journal import AllocJournal, request_key
 
 
@@ -90,6 +98,10 @@ class AllocatorOptions:
     async_patch: bool = False
     # "cu": per-pod CU-slot masks (alloc/cuslots.py); "none": pods time-slice the whole GPU
     compute_isolation: str = "none"
+    # placement truth (alloc/placement.py): periodic pass interval, and how long an answer whose
+    # fake IDs no pod holds yet counts as "in flight" (kubelet checkpoint not visible yet)
+    placement_s: float = 2.0
+    in_flight_s: float = 30.0
 
 
 @dataclasses.dataclass
@@ -124,6 +136,18 @@ class Allocator:
         self._last_reconcile = time.monotonic()
         self._last_sweep = 0.0
         self.journal = AllocJournal(self.opts.journal_path, self.opts.journal_ttl_s)
+        # placement truth: answered containers, the kubelet's pod-resources view, and the
+        # annotation changes this plugin has queued but the pod cache may not show yet
+        self.grants = PL.GrantBook()
+        self.podres = None
+        self._overlay: dict[str, dict] = {}       # uid -> annotations written, not yet landed
+        self._overlay_gen: dict[str, int] = {}
+        self._revoked: set[str] = set()           # reservation re-armed: its assign job must not re-claim
+        self._place_mu = threading.Lock()
+        self._place_thread = None
+        for k, uid, t, resp in self.journal.answers():   # grants of a previous instance (journal TTL)
+            if len(resp.container_responses) == 1:
+                self.grants.record(k, self._grant_from(resp.container_responses[0], uid, t))
         if self.opts.async_patch:
             import queue
             self._patch_q = queue.Queue()
@@ -175,8 +199,29 @@ class Allocator:
             self._pinfo[k] = v
         return v
 
+    def _view(self, pods: list[dict]) -> list[dict]:
+        """Pods as they will read once this plugin's queued placement patches have landed."""
+        ov = self._overlay
+        if not ov:
+            return pods
+        out = []
+        for p in pods:
+            a = ov.get(O.uid(p))
+            if a is not None:
+                md = dict(p.get("metadata") or {})
+                ann = dict(md.get("annotations") or {})
+                for k, v in a.items():
+                    if v is None:
+                        ann.pop(k, None)
+                    else:
+                        ann[k] = v
+                md["annotations"] = ann
+                p = dict(p, metadata=md)
+            out.append(p)
+        return out
+
     def _candidates(self, fresh: bool) -> list[dict]:
-        pods = A.dedupe_by_uid(self.pods.pending_pods(fresh=fresh), self.node)
+        pods = self._view(A.dedupe_by_uid(self.pods.pending_pods(fresh=fresh), self.node))
         now = time.monotonic()
         if now - self._last_sweep > 1.0:          # amortised: the set holds the last claim_ttl_s of pods
             self._last_sweep = now
@@ -308,7 +353,7 @@ class Allocator:
         ttl_ns = int(self.opts.claim_ttl_s * 1e9)
         k = len(sizes)
         out = []
-        for p in A.dedupe_by_uid(self.pods.node_pods(), self.node):
+        for p in self._view(A.dedupe_by_uid(self.pods.node_pods(), self.node)):
             u = O.uid(p)
             if (O.phase(p) == "Pending" or O.deleting(p) or not A.is_assumed_pod(p) or u in self._assigned
                     or u in self._claims or u in self._tainted or self.journal.answered(u) or now_ns - A.assume_time(p) > ttl_ns):
@@ -441,8 +486,10 @@ class Allocator:
                 if claim is None:
                     # watch lag: the kubelet may see a bind before our cache does
                     claim, complete = self._match(sizes, fresh=True)
-                if claim is not None and complete:
-                    self._claims[claim.uid] = claim   # held across the PATCH
+                if claim is not None:
+                    self._revoked.discard(claim.uid)
+                    if complete:
+                        self._claims[claim.uid] = claim   # held across the PATCH
                 t2 = time.perf_counter()
             hist.observe(ta - t0, phase="prelude")      # request key, journal replay check
             hist.observe(tb - ta, phase="lock")
@@ -462,6 +509,7 @@ class Allocator:
                 for i, creq in enumerate(req.container_requests):
                     resp.container_responses.append(self._container_response(0, pod_units, len(creq.devices_ids),
                                                                              "", i))
+                self._record_grants(req, resp, "", jkey)
                 self.metrics.allocate_outcomes.inc(outcome="single_gpu")
                 hist.observe(time.perf_counter() - t0, phase="total")
                 return resp
@@ -485,6 +533,7 @@ class Allocator:
         for i, creq in enumerate(req.container_requests):
             resp.container_responses.append(self._container_response(idx, pod_total, len(creq.devices_ids),
                                                                      claim.uid, max(0, slot0 + i), cu))
+        self._record_grants(req, resp, claim.uid, jkey)
         if not complete:
             log.info("pod %s: container %d/%d of a multi-container pod allocated on GPU %d", O.name(claim.pod),
                      claim.next_container, len(claim.shape), idx)
@@ -495,13 +544,15 @@ class Allocator:
         t3 = time.perf_counter()
         if self._patch_q is not None:
             job = _PatchJob(claim.uid, O.namespace(claim.pod), O.name(claim.pod), self._extra_annotations(claim.uid))
-            # journal first (answer + pending PATCH, one write): a crash after the reply must
-            # not lose the PATCH
-            self.journal.record_pending(req, claim.uid, resp, job.ns, job.name, job.ann, jkey)
+            # claimed as unpatched before the journal says "answered", so the reconcile pass
+            # never queues a second, annotation-less patch for it in between
             with self._mu:
                 self._claims.pop(claim.uid, None)
                 self._assigned[claim.uid] = time.monotonic()
                 self._unpatched.add(claim.uid)
+            # journal before the reply (answer + pending PATCH, one write): a crash after the
+            # reply must not lose the PATCH
+            self.journal.record_pending(req, claim.uid, resp, job.ns, job.name, job.ann, jkey)
             self._patch_q.put(job)
             hist.observe(time.perf_counter() - t3, phase="patch")
             hist.observe(time.perf_counter() - t0, phase="total")
@@ -531,6 +582,19 @@ class Allocator:
         log.info("pod %s, new allocated GPUs info: gpu index %d uuid %s", O.name(claim.pod), idx,
                  self.model.uuid_by_index(idx))
         return resp
+
+    @staticmethod
+    def _grant_from(cresp, uid: str, t: float) -> PL.Grant:
+        e = cresp.envs
+        return PL.Grant(gpu=int(e.get(const.ENV_RESOURCE_INDEX, "-1")), units=int(e.get(const.ENV_RESOURCE_BY_CONTAINER, "0")),
+                        claimed=uid, t=t, cu=e.get(const.ENV_CU_SLOTS), ledger=e.get(const.ENV_SHIM_LEDGER, ""))
+
+    def _record_grants(self, req, resp, uid: str, jkey: str) -> None:
+        t = time.time()
+        crs = req.container_requests
+        for i, cresp in enumerate(resp.container_responses):
+            key = jkey if len(crs) == 1 else PL.ids_key(crs[i].devices_ids)
+            self.grants.record(key, self._grant_from(cresp, uid, t))
 
     def _replay(self, req, key: str):
         """Idempotent retry: the same fake-ID set for a pod we already assigned that is still
@@ -587,9 +651,19 @@ class Allocator:
                 delay = min(delay * 2, 5.0)
             else:
                 break
-            self.journal.landed(job.uid)
+            self._landed(job)
+
+    def _landed(self, job: "_PatchJob") -> None:
+        if job.kind == "placement":
             with self._mu:
-                self._unpatched.discard(job.uid)
+                if self._overlay_gen.get(job.uid) == job.gen:
+                    self._overlay.pop(job.uid, None)
+                    self._overlay_gen.pop(job.uid, None)
+            return
+        self.journal.landed(job.uid)
+        with self._mu:
+            self._unpatched.discard(job.uid)
+            if job.uid not in self._revoked:
                 self._assigned[job.uid] = time.monotonic()
 
     def _land(self, job: "_PatchJob") -> dict | None:
@@ -604,11 +678,14 @@ class Allocator:
                 log.warning("pod %s/%s was re-created (uid %s, answered %s): dropping its pending patch",
                             job.ns, job.name, O.uid(cur), job.uid)
                 return None
-            if A.is_assigned_pod(cur):
+            if job.kind == "assign" and A.is_assigned_pod(cur):
                 return cur
-        patch = A.assigned_patch()
+        if job.kind == "placement":
+            patch = {"metadata": {"annotations": dict(job.ann)}}
+        else:
+            patch = A.assigned_patch()
+            patch["metadata"]["annotations"].update(job.ann)
         patch["metadata"]["uid"] = job.uid
-        patch["metadata"]["annotations"].update(job.ann)
         try:
             return self.client.patch_pod(job.ns, job.name, patch)
         except APIError as e:
@@ -638,18 +715,101 @@ class Allocator:
                     continue
                 self._unpatched.add(u)
                 self._assigned[u] = time.monotonic()
-            self._patch_q.put(_PatchJob(u, O.namespace(p), O.name(p), {}, recovered=True))
+            self._patch_q.put(_PatchJob(u, O.namespace(p), O.name(p), self._extra_annotations(u), recovered=True))
             self.metrics.allocate_outcomes.inc(outcome="patch_reconciled")
             log.warning("reconcile: pod %s answered by this plugin still reads ASSIGNED=false; patching", O.name(p))
             n += 1
         return n
+
+    # ------------------------------------------------------------------------------------
+    # placement truth (alloc/placement.py)
+    # ------------------------------------------------------------------------------------
+    def set_pod_resources(self, src) -> None:
+        """Attach the kubelet's pod-resources view (``api.podresources.PodResourcesClient`` or
+        any object with ``list() -> [PodDevices]``) and start the periodic placement pass."""
+        self.podres = src
+        if src is not None and self._place_thread is None and self.opts.placement_s > 0:
+            def loop():
+                while not self._stop.wait(self.opts.placement_s):
+                    try:
+                        self.reconcile_placement()
+                    except Exception as e:  # noqa: BLE001 - kubelet restarting, apiserver down
+                        log.V(2).info("placement pass failed: %s", e)
+            self._place_thread = threading.Thread(target=loop, name="placement", daemon=True)
+            self._place_thread.start()
+
+    def prestart(self, req) -> None:
+        """``PreStartContainer``: the kubelet checkpointed this container's fake IDs and is
+        about to start it — make the pod annotations tell the truth first."""
+        if self.podres is None:
+            return
+        try:
+            self.reconcile_placement()
+        except Exception as e:  # noqa: BLE001 - never block a container start on bookkeeping
+            log.warning("placement check before container start failed: %s", e)
+
+    def reconcile_placement(self) -> list:
+        """One placement pass: join the grant book with the kubelet's pod-resources view and
+        queue (write-behind) or apply (sync) the annotation fixes ``placement.plan`` returns."""
+        src = self.podres
+        if src is None:
+            return []
+        with self._place_mu:
+            held = src.list()
+            pods = self._view(A.dedupe_by_uid(self.pods.node_pods(), self.node))
+            now = time.time()
+            fixes = PL.plan(pods, held, self.grants, now, self.opts.in_flight_s)
+            for f in fixes:
+                self._apply_fix(f)
+            live = {O.uid(p) for p in pods}
+            self.grants.prune({PL.ids_key(ids) for pd in held for _, ids in pd.containers}, live, now,
+                              self.opts.in_flight_s)
+            return fixes
+
+    def _apply_fix(self, f: PL.Fix) -> None:
+        ann = dict(f.ann)
+        if f.assigned is True:
+            ann.update(A.assigned_patch()["metadata"]["annotations"])
+        elif f.assigned is False:
+            ann[const.ENV_ASSIGNED_FLAG] = "false"
+        self.metrics.allocate_outcomes.inc(outcome=f"placement_{f.reason}")
+        log.warning("placement: pod %s/%s %s -> %s", f.ns, f.name,
+                    "holds its containers' grants" if f.reason == "holder" else "reservation re-homed",
+                    {k: v for k, v in ann.items() if k != const.ENV_RESOURCE_ASSUME_TIME})
+        with self._mu:
+            gen = self._overlay_gen.get(f.uid, 0) + 1
+            self._overlay_gen[f.uid] = gen
+            self._overlay[f.uid] = dict(self._overlay.get(f.uid) or {}, **ann)
+            if f.assigned is True:
+                self._assigned[f.uid] = time.monotonic()
+                self._revoked.discard(f.uid)
+            elif f.assigned is False:
+                # its reservation was consumed by another pod: match it again on admission
+                self._assigned.pop(f.uid, None)
+                self._revoked.add(f.uid)
+                self._claims.pop(f.uid, None)
+        if f.assigned is False:
+            self.journal.forget(f.uid)
+            self._drop_slots(f.uid)
+        job = _PatchJob(f.uid, f.ns, f.name, ann, kind="placement", gen=gen)
+        if self._patch_q is not None:
+            self._patch_q.put(job)
+            return
+        try:
+            updated = self._land(job)
+            if updated:
+                self.pods.observe(updated)
+        except APIError as e:
+            if not e.not_found:
+                raise
+        self._landed(job)
 
     def flush_patches(self, timeout: float = 10.0) -> bool:
         """Wait until every queued ASSIGNED patch has landed (tests, shutdown)."""
         t = time.monotonic() + timeout
         while time.monotonic() < t:
             with self._mu:
-                if not self._unpatched:
+                if not self._unpatched and not self._overlay:
                     return True
             time.sleep(0.005)
         return False
@@ -717,8 +877,10 @@ class _PatchJob:
     uid: str
     ns: str
     name: str
-    ann: dict              # extra annotations landed with ASSIGNED=true (CU slots)
+    ann: dict              # extra annotations landed with ASSIGNED=true (CU slots); placement: all
     recovered: bool = False
+    kind: str = "assign"   # "assign" (ASSIGNED=true after an answer) | "placement" (truth fix)
+    gen: int = 0           # placement: overlay generation this job lands
 
 
 def env_shim_host_dir() -> str | None:

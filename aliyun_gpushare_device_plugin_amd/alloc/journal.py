@@ -149,6 +149,18 @@ class AllocJournal:
             t = self._uids.get(uid)
             return uid in self._pending or (t is not None and time.time() - t <= self.ttl_s)
 
+    def forget(self, uid: str) -> None:
+        """``uid``'s answer went to another pod (placement truth): it is no longer answered."""
+        with self._lock:
+            self._uids.pop(uid, None)
+
+    def answers(self) -> list[tuple[str, str, float, object]]:
+        """(key, uid, time, AllocateResponse) of the answers still within the TTL."""
+        now = time.time()
+        with self._lock:
+            items = [(k, u, t, b) for k, (u, t, b) in self._mem.items() if now - t <= self.ttl_s]
+        return [(k, u, t, api.AllocateResponse.FromString(b)) for k, u, t, b in items]
+
     # -- write-behind patches ---------------------------------------------------------------
     def record_pending(self, req, pod_uid: str, resp, ns: str, name: str, ann: dict | None = None,
                        key: str | None = None) -> None:

@@ -10,14 +10,11 @@ identical (golden-byte tests in ``tests/test_api_wire.py``).
 """
 from __future__ import annotations
 
-from google.protobuf import descriptor_pb2, descriptor_pool, message_factory
+from . import _proto
+from ._proto import BOOL as _BOOL, I32 as _I32, I64 as _I64, MSG as _MSG, OPT as _OPT, REP as _REP, STR as _STR
 
 PACKAGE = "v1beta1"
 VERSION = "v1beta1"
-
-_F = descriptor_pb2.FieldDescriptorProto
-_OPT, _REP = _F.LABEL_OPTIONAL, _F.LABEL_REPEATED
-_STR, _BOOL, _I64, _I32, _MSG = _F.TYPE_STRING, _F.TYPE_BOOL, _F.TYPE_INT64, _F.TYPE_INT32, _F.TYPE_MESSAGE
 
 # (message name, [(field name, number, label, type, type_name or None, json_name or None)])
 _MESSAGES = [
@@ -78,31 +75,10 @@ SERVICES = {
 }
 
 
-def _build_file() -> descriptor_pb2.FileDescriptorProto:
-    fdp = descriptor_pb2.FileDescriptorProto(name="deviceplugin/v1beta1/api.proto",
-                                             package=PACKAGE, syntax="proto3")
-    for name, fields in _MESSAGES:
-        m = fdp.message_type.add(name=name)
-        for entry in _MAP_ENTRIES.get(name, []):
-            e = m.nested_type.add(name=entry)
-            e.options.map_entry = True
-            e.field.add(name="key", number=1, label=_OPT, type=_STR, json_name="key")
-            e.field.add(name="value", number=2, label=_OPT, type=_STR, json_name="value")
-        for fname, num, label, ftype, tname in fields:
-            f = m.field.add(name=fname, number=num, label=label, type=ftype)
-            if tname:
-                f.type_name = f".{PACKAGE}.{tname}"
-    for svc, methods in SERVICES.items():
-        s = fdp.service.add(name=svc)
-        for meth, inp, out, stream in methods:
-            s.method.add(name=meth, input_type=f".{PACKAGE}.{inp}", output_type=f".{PACKAGE}.{out}",
-                         server_streaming=stream)
-    return fdp
-
-
-_POOL = descriptor_pool.DescriptorPool()
-_CLASSES = message_factory.GetMessages([_build_file()], pool=_POOL)
-FILE_DESCRIPTOR = _POOL.FindFileByName("deviceplugin/v1beta1/api.proto")
+PROTO = _proto.ProtoFile("deviceplugin/v1beta1/api.proto", PACKAGE, _MESSAGES, SERVICES, _MAP_ENTRIES)
+FILE_DESCRIPTOR = PROTO.descriptor
+_BY_NAME = PROTO.by_name
+_CLASSES = {f"{PACKAGE}.{k}": v for k, v in _BY_NAME.items()}
 
 DevicePluginOptions = _CLASSES["v1beta1.DevicePluginOptions"]
 RegisterRequest = _CLASSES["v1beta1.RegisterRequest"]
@@ -125,8 +101,6 @@ ContainerAllocateResponse = _CLASSES["v1beta1.ContainerAllocateResponse"]
 Mount = _CLASSES["v1beta1.Mount"]
 DeviceSpec = _CLASSES["v1beta1.DeviceSpec"]
 
-_BY_NAME = {k.split(".", 1)[1]: v for k, v in _CLASSES.items() if k.count(".") == 1}
-
 
 def message_class(name: str):
     return _BY_NAME[name]
@@ -147,31 +121,15 @@ def add_servicer(server, service: str, impl) -> None:
     Equivalent of the generated ``RegisterDevicePluginServer`` / ``RegisterRegistrationServer``
     (``server.go:125-126``).
     """
-    import grpc
-
-    handlers = {}
-    for meth, inp, out, stream in SERVICES[service]:
-        fn = getattr(impl, meth)
-        req_cls, resp_cls = _BY_NAME[inp], _BY_NAME[out]
-        factory = grpc.unary_stream_rpc_method_handler if stream else grpc.unary_unary_rpc_method_handler
-        handlers[meth] = factory(fn, request_deserializer=req_cls.FromString,
-                                 response_serializer=resp_cls.SerializeToString)
-    server.add_generic_rpc_handlers((grpc.method_handlers_generic_handler(f"{PACKAGE}.{service}", handlers),))
+    PROTO.add_servicer(server, service, impl)
 
 
-class Stub:
+def Stub(channel, service: str):
     """Client stub for one service over an existing ``grpc.Channel``.
 
     ``Stub(channel, "DevicePlugin").Allocate(req)`` mirrors the generated Go client.
     """
-
-    def __init__(self, channel, service: str):
-        for meth, inp, out, stream in SERVICES[service]:
-            make = channel.unary_stream if stream else channel.unary_unary
-            setattr(self, meth, make(method_path(service, meth),
-                                     request_serializer=_BY_NAME[inp].SerializeToString,
-                                     response_deserializer=_BY_NAME[out].FromString))
+    return PROTO.stub(channel, service)
 
 
-def unix_target(path: str) -> str:
-    return "unix://" + path if not path.startswith("unix:") else path
+unix_target = _proto.unix_target

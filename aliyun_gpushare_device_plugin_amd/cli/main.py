@@ -80,6 +80,13 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--no-swap-completion", action="store_true",
                    help="reference behaviour: fail a pod whose equal-size twin was admitted first "
                         "under its reservation instead of exchanging their GPUs")
+    p.add_argument("--pod-resources-socket", default="auto",
+                   help="kubelet pod-resources socket (v1.PodResourcesLister); with it the plugin requests "
+                        "PreStartContainer and rewrites IDX/allocation annotations to the GPU each container "
+                        "really got (swapped admissions). 'auto' = /var/lib/kubelet/pod-resources/kubelet.sock "
+                        "when present; 'none' disables placement truth")
+    p.add_argument("--placement-interval", type=float, default=2.0,
+                   help="seconds between periodic placement-truth passes (besides PreStartContainer)")
     p.add_argument("--sync-patch", action="store_true",
                    help="PATCH ASSIGNED=true inside Allocate (reference behaviour) instead of write-behind")
     p.add_argument("--export-topology", nargs="?", const="true", default="true")
@@ -105,7 +112,8 @@ def config_from_args(a) -> PluginConfig:
         rocr_visible=a.rocr_visible_devices, metrics_addr=a.metrics_addr, mps=_bool(a.mps),
         async_patch=not a.sync_patch, complete_swaps=not a.no_swap_completion,
         partition_aware=a.partition_aware, ledger_dir=a.ledger_dir, ledger_scan_s=a.ledger_scan_interval,
-        journal_path=a.journal_path, compute_isolation=a.compute_isolation)
+        journal_path=a.journal_path, compute_isolation=a.compute_isolation,
+        pod_resources_socket=a.pod_resources_socket, placement_s=a.placement_interval)
 
 
 def install_shim(dest_dir: str) -> str:

@@ -221,6 +221,15 @@ class _SkinnyOpts:
         self.ssq_out, self.norm, self.rope = ssq_out, norm, rope
 
     def __enter__(self):
+        try:
+            return self._arm()
+        except BaseException:
+            # a partly armed state (RoPE/KV pointers set, opts refused) must never leak into the
+            # next unrelated skinny_linear on this thread
+            _lib.lib().gs_skinny_clear_opts()
+            raise
+
+    def _arm(self):
         if self.rope is not None:
             cos, sin, pos, kc, vc, hq = self.rope
             B, hkv, smax, _ = kc.shape

@@ -70,6 +70,10 @@ class PluginConfig:
     ledger_scan_s: float = 10.0
     journal_path: str | None = None      # persisted allocation journal (alloc/journal.py)
     compute_isolation: str = "none"      # "cu": per-pod CU-slot masks (alloc/cuslots.py)
+    # kubelet pod-resources socket for placement truth (alloc/placement.py): "auto" = the
+    # standard path when it exists, "none"/"" = off
+    pod_resources_socket: str = "auto"
+    placement_s: float = 2.0
     mps: bool = False                    # accepted for flag compatibility; ignored
 
 
@@ -158,7 +162,7 @@ class SharedGPUManager:
                                 complete_swaps=cfg.complete_swaps,
                                 ledger_dir=cfg.ledger_dir if shim else None,
                                 journal_path=cfg.journal_path,
-                                compute_isolation=cfg.compute_isolation)
+                                compute_isolation=cfg.compute_isolation, placement_s=cfg.placement_s)
         if self.allocator is None:
             if cfg.async_patch and not cfg.journal_path:
                 log.warning("write-behind ASSIGNED patches without --journal-path: a patch still queued when "
@@ -168,9 +172,26 @@ class SharedGPUManager:
             # rebuild: keep claims, assigned pods, queued patches and the patcher thread
             self.allocator.reconfigure(model, src, self.client, opts)
         allocator = self.allocator
+        if allocator.podres is None:
+            allocator.set_pod_resources(self._pod_resources())
         self.model = model
         return DevicePluginServer(model, allocator, self._plugin_socket(), const.RESOURCE_NAME,
                                   cfg.preferred_allocation, self.metrics)
+
+    def _pod_resources(self):
+        from ..api.podresources import SOCKET, PodResourcesClient
+
+        path = self.cfg.pod_resources_socket
+        if not path or path == "none":
+            return None
+        if path == "auto":
+            path = SOCKET
+            if not os.path.exists(path):
+                log.warning("kubelet pod-resources socket %s not found: placement truth is off, so a swapped "
+                            "admission of two equal-size pods leaves their IDX annotations crossed", path)
+                return None
+        log.info("placement truth from the kubelet pod-resources API at %s", path)
+        return PodResourcesClient(path, const.RESOURCE_NAME)
 
     def _start_health(self):
         if self.health:

@@ -10,6 +10,9 @@ Fixed here:
   blocks when no stream is attached;
 * devices can go back to Healthy (``server.go:188`` FIXME);
 * ``GetPreferredAllocation`` is implemented and advertised when enabled (it panicked);
+* ``PreStartContainer`` (a no-op there, ``:199-201``) is requested when the kubelet's
+  pod-resources API is available: before each container starts, the plugin makes the pod's
+  placement annotations match the GPU the container was really given (alloc/placement.py);
 * the Allocate RPC is not serialized behind one plugin-wide lock (see alloc/engine.py).
 """
 from __future__ import annotations
@@ -45,8 +48,7 @@ class _Servicer:
         self.p = plugin
 
     def GetDevicePluginOptions(self, request, context):
-        return api.DevicePluginOptions(pre_start_required=False,
-                                       get_preferred_allocation_available=self.p.preferred_allocation)
+        return self.p.options()
 
     def ListAndWatch(self, request, context):
         p = self.p
@@ -70,6 +72,7 @@ class _Servicer:
         return self.p.allocator.preferred(request)
 
     def PreStartContainer(self, request, context):
+        self.p.allocator.prestart(request)
         return api.PreStartContainerResponse()
 
 
@@ -85,6 +88,10 @@ class DevicePluginServer:
         self.max_workers = max_workers
         self.server: grpc.Server | None = None
         self.stopped = threading.Event()
+
+    def options(self) -> api.DevicePluginOptions:
+        return api.DevicePluginOptions(pre_start_required=self.allocator.podres is not None,
+                                       get_preferred_allocation_available=self.preferred_allocation)
 
     def _cleanup(self):
         try:
@@ -121,8 +128,9 @@ class DevicePluginServer:
             stub = api.Stub(ch, "Registration")
             req = api.RegisterRequest(version=api.VERSION, endpoint=os.path.basename(self.socket),
                                       resource_name=self.resource_name)
-            if self.preferred_allocation:
-                req.options.get_preferred_allocation_available = True
+            opts = self.options()
+            if opts.pre_start_required or opts.get_preferred_allocation_available:
+                req.options.CopyFrom(opts)     # the kubelet reads the options from Register
             stub.Register(req, timeout=timeout)
         finally:
             ch.close()

@@ -58,11 +58,14 @@ class SimCluster:
                  pod_source: str = "watch", apiserver_latency_s: float = 0.0, shim_host_dir: str | None = None,
                  gpu_indices: list[int] | None = None, health_poll_s: float = 1.0, round_policy: str = "nearest",
                  extra_plugin_args: list[str] | None = None, apiserver: str = "thread",
-                 preferred_allocation: bool = False, compute_isolation: str = "none", kubelet: str = "thread"):
+                 preferred_allocation: bool = False, compute_isolation: str = "none", kubelet: str = "thread",
+                 placement_truth: bool = True):
         self.node_specs = nodes
         # kubelet: "thread" (FakeKubelet in this interpreter) or "process" (its own interpreter,
         # sim/kubelet_proc.py, so kubelet-side Allocate timing is not inflated by this process's GIL)
         self.kubelet_mode = kubelet
+        # the fake kubelet serves pod-resources; the plugin uses it for placement truth
+        self.placement_truth = placement_truth
         self.compute_isolation = compute_isolation
         self._own_dir = workdir is None
         # short paths: UDS paths are limited to 108 bytes
@@ -143,7 +146,11 @@ class SimCluster:
                             shim_host_dir=self.shim_host_dir, gpu_indices=self.gpu_indices,
                             health_poll_s=self.health_poll_s, round_policy=self.round_policy,
                             preferred_allocation=self.preferred_allocation,
-                            compute_isolation=self.compute_isolation, **self._kubelet_cfg(node))
+                            compute_isolation=self.compute_isolation, pod_resources_socket=self._podres(node),
+                            **self._kubelet_cfg(node))
+
+    def _podres(self, node: SimNode) -> str:
+        return os.path.join(node.plugin_dir, "pod-resources.sock") if self.placement_truth else "none"
 
     def _kubelet_cfg(self, node: SimNode) -> dict:
         if self.pod_source != "kubelet":
@@ -166,6 +173,7 @@ class SimCluster:
                 args += ["--preferred-allocation"]
             if self.compute_isolation != "none":
                 args += ["--compute-isolation", self.compute_isolation]
+            args += ["--pod-resources-socket", self._podres(node)]
             for k, v in self._kubelet_cfg(node).items():
                 args += ["--" + k.replace("_", "-"), str(v)]
             args += self.extra_plugin_args
@@ -205,6 +213,8 @@ class SimCluster:
 
     def stop(self):
         self._bg.shutdown(wait=True)
+        if self.extender is not None:
+            self.extender.stop_watch()
         for node in self.nodes.values():
             if node.manager is not None:
                 node.manager.stop()

@@ -13,6 +13,11 @@ for: pods labelled ``gpushare.amd.com/tp-group=<name>`` with ``…/tp-size=<k>``
 as a group on k distinct GPUs that are pairwise one-hop xGMI per the topology annotation
 the plugin exports (``parallel/topology.py``). It also serves the extender HTTP routes
 (``/gpushare-scheduler/filter`` and ``/bind``) for protocol-level tests.
+
+Like the real extender's pod informer, ``update(pod)`` re-accounts a pod whose annotations
+changed (the plugin's placement-truth rewrite of ``IDX`` / the allocation JSON, see
+``alloc/placement.py``) and ``forget`` drops a deleted or finished one; ``watch()`` drives both
+from an apiserver pod watch.
 """
 from __future__ import annotations
 
@@ -87,12 +92,71 @@ class ExtenderSim:
 
     def forget(self, pod: dict):
         with self._lock:
-            placed = self._placed.pop(O.uid(pod), None)
-            if placed:
-                st = self.nodes.get(placed[0])
-                if st:
-                    for g, mem in placed[1]:
-                        st.used[g] -= mem
+            self._forget_locked(O.uid(pod))
+
+    def _forget_locked(self, uid: str):
+        placed = self._placed.pop(uid, None)
+        if placed:
+            st = self.nodes.get(placed[0])
+            if st:
+                for g, mem in placed[1]:
+                    st.used[g] -= mem
+
+    @staticmethod
+    def _parts_from_annotations(pod: dict, st: NodeState) -> list | None:
+        if A.is_assumed_pod(pod) or A.is_assigned_pod(pod) or A.allocation_from_annotation(pod):
+            alloc = A.allocation_from_annotation(pod) or {A.gpu_id_from_annotation(pod): O.gpu_mem_of_pod(pod)}
+            return [(g, mem) for g, mem in alloc.items() if 0 <= g < st.gpu_count]
+        return None
+
+    def update(self, pod: dict):
+        """Pod informer update: re-account the pod from its (possibly rewritten) annotations."""
+        with self._lock:
+            u = O.uid(pod)
+            if O.is_terminated(pod) or O.deleting(pod):
+                self._forget_locked(u)
+                return
+            st = self.nodes.get(O.node_name(pod))
+            if st is None or O.gpu_mem_of_pod(pod) <= 0:
+                return
+            parts = self._parts_from_annotations(pod, st)
+            if parts is None or (u in self._placed and self._placed[u] == (st.name, parts)):
+                return
+            self._forget_locked(u)
+            for g, mem in parts:
+                st.used[g] += mem
+            self._placed[u] = (st.name, parts)
+
+    def watch(self) -> "ExtenderSim":
+        """Follow pod updates and deletions from the apiserver (background thread)."""
+        self._watch_stop = threading.Event()
+        self._watch_holder: list = []
+
+        def loop():
+            rv = None
+            while not self._watch_stop.is_set():
+                try:
+                    if rv is None:
+                        _, rv = self.client.list_pods()
+                    for ev in self.client.watch_pods(resource_version=rv, stop=self._watch_stop,
+                                                     holder=self._watch_holder):
+                        obj = ev.get("object") or {}
+                        rv = (obj.get("metadata") or {}).get("resourceVersion", rv)
+                        if ev.get("type") == "DELETED":
+                            self.forget(obj)
+                        elif ev.get("type") == "MODIFIED":
+                            self.update(obj)
+                except Exception:  # noqa: BLE001 - expired RV, apiserver restart: re-list
+                    rv = None
+                    self._watch_stop.wait(0.1)
+
+        threading.Thread(target=loop, name="extender-watch", daemon=True).start()
+        return self
+
+    def stop_watch(self):
+        if getattr(self, "_watch_stop", None) is not None:
+            self._watch_stop.set()
+            self.client.abort_watch(self._watch_holder)
 
     # -- scheduling -----------------------------------------------------------------------
     def _fits(self, st: NodeState, req: int) -> list[int]:

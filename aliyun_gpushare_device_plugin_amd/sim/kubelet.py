@@ -9,7 +9,12 @@ Plays the kubelet's side of the device-plugin API over real gRPC-on-UDS:
   pick that many free healthy fake IDs (asking ``GetPreferredAllocation`` when offered),
   call ``Allocate`` once per container, and remember the IDs until ``release``;
 * ``restart()`` re-creates ``kubelet.sock`` like a kubelet restart (the plugin must notice
-  and re-register, ``gpumanager.go:82-87``).
+  and re-register, ``gpumanager.go:82-87``);
+* serves the pod-resources API (``v1.PodResourcesLister``) on ``<dir>/pod-resources.sock``:
+  every admitted pod's containers with the fake IDs checkpointed for them, exactly what the
+  real kubelet publishes on ``/var/lib/kubelet/pod-resources/kubelet.sock``;
+* when the plugin registered with ``pre_start_required``, calls ``PreStartContainer`` for each
+  gpu container after the pod's admission, before "starting" it.
 """
 from __future__ import annotations
 
@@ -22,6 +27,7 @@ import time
 import grpc
 
 from .. import const
+from ..api import podresources as podres
 from ..api import v1beta1 as api
 from ..cluster import objects as O
 from ..cluster.client import APIClient
@@ -58,6 +64,10 @@ class FakeKubelet:
         self._healthy: list[str] = []           # healthy IDs in advertised order, per device update
         self._lock = threading.Lock()
         self._stop = threading.Event()
+        self._holdings: dict[str, tuple] = {}    # uid -> (ns, name, [(container, ids)])
+        self.podres_sock = os.path.join(plugin_dir, "pod-resources.sock")
+        self.prestart_calls = 0
+        self.reg_options = None
 
     # -- read-only /pods endpoint (--pod-source=kubelet / --query-kubelet) ------------------
     def serve_pods(self, token: str = "sim-kubelet-token") -> int:
@@ -96,8 +106,38 @@ class FakeKubelet:
         return self.pods_port
 
     # -- Registration service -------------------------------------------------------------
+    # -- pod-resources service (v1.PodResourcesLister) ----------------------------------
+    def _pod_resources(self, uid_filter=None) -> list:
+        with self._lock:
+            items = list(self._holdings.items())
+        out = []
+        for uid, (ns, name, ctrs) in items:
+            if uid_filter is not None and not uid_filter(ns, name):
+                continue
+            out.append(podres.PodResources(name=name, namespace=ns, containers=[
+                podres.ContainerResources(name=cn, devices=[
+                    podres.ContainerDevices(resource_name=self.resource, device_ids=[i]) for i in ids])
+                for cn, ids in ctrs]))
+        return out
+
+    def List(self, request, context):
+        return podres.ListPodResourcesResponse(pod_resources=self._pod_resources())
+
+    def Get(self, request, context):
+        got = self._pod_resources(lambda ns, n: (ns, n) == (request.pod_namespace, request.pod_name))
+        if not got:
+            context.abort(grpc.StatusCode.NOT_FOUND, "pod not found")
+        return podres.GetPodResourcesResponse(pod_resources=got[0])
+
+    def GetAllocatableResources(self, request, context):
+        with self.devices_updated:
+            healthy = list(self._healthy)
+        return podres.AllocatableResourcesResponse(devices=[
+            podres.ContainerDevices(resource_name=self.resource, device_ids=[i]) for i in healthy])
+
     def Register(self, request, context):
         self.registrations.append((request.version, request.endpoint, request.resource_name))
+        self.reg_options = request.options if request.HasField("options") else None
         if request.version != api.VERSION:
             context.abort(grpc.StatusCode.INVALID_ARGUMENT, f"unsupported version {request.version}")
         threading.Thread(target=self._connect, args=(request.endpoint,), daemon=True).start()
@@ -109,9 +149,15 @@ class FakeKubelet:
             os.remove(self.sock)
         except FileNotFoundError:
             pass
+        try:
+            os.remove(self.podres_sock)
+        except FileNotFoundError:
+            pass
         self.server = grpc.server(cf.ThreadPoolExecutor(max_workers=4, thread_name_prefix="kubelet"))
         api.add_servicer(self.server, "Registration", self)
+        podres.PROTO.add_servicer(self.server, "PodResourcesLister", self)
         self.server.add_insecure_port(api.unix_target(self.sock))
+        self.server.add_insecure_port(api.unix_target(self.podres_sock))
         self.server.start()
         return self
 
@@ -189,6 +235,7 @@ class FakeKubelet:
     def admit(self, pod: dict, timeout: float = 10.0) -> Admission:
         uid = O.uid(pod)
         adm = Admission(uid, [], [], [])
+        started = []
         for c in O.containers(pod):
             n = O.container_limit(c, self.resource)
             if n <= 0:
@@ -220,11 +267,28 @@ class FakeKubelet:
             adm.latencies.append(time.perf_counter() - t0)
             adm.responses.append(resp.container_responses[0])
             adm.device_ids.append(ids)
+            # the device manager checkpoints the container's IDs (pod-resources shows them)
+            started.append((c.get("name", ""), tuple(ids)))
+            with self._lock:
+                self._holdings[uid] = (O.namespace(pod), O.name(pod), list(started))
+        if self._pre_start_required():
+            for _, ids in started:     # container start: PreStartContainer per gpu container
+                self.prestart_calls += 1
+                try:
+                    self._stub.PreStartContainer(api.PreStartContainerRequest(devices_ids=list(ids)),
+                                                 timeout=timeout)
+                except grpc.RpcError as e:
+                    adm.error = f"PreStartContainer failed: {e.code()} {e.details()}"
         return adm
+
+    def _pre_start_required(self) -> bool:
+        o = self.reg_options if self.reg_options is not None else self.options
+        return bool(o is not None and o.pre_start_required)
 
     def release(self, pod_uid: str):
         with self._lock:
             self._used.difference_update(self._allocated.pop(pod_uid, ()))
+            self._holdings.pop(pod_uid, None)
 
     def allocated_ids(self) -> set:
         with self._lock:

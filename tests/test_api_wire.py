@@ -68,3 +68,27 @@ def test_method_paths():
                                                                  "ListAndWatchResponse", True)]
     svc = api.FILE_DESCRIPTOR.services_by_name["DevicePlugin"]
     assert svc.full_name == "v1beta1.DevicePlugin"
+
+
+def test_podresources_golden_bytes_and_paths():
+    """k8s.io/kubelet/pkg/apis/podresources/v1/api.proto: PodResources{name=1, namespace=2,
+    containers=3{name=1, devices=2{resource_name=1, device_ids=2}}}; unknown fields (DRA's
+    dynamic_resources) are skipped by the parser."""
+    from aliyun_gpushare_device_plugin_amd.api import podresources as pr
+
+    d = pr.ContainerDevices(resource_name="r", device_ids=["a"])
+    assert d.SerializeToString() == bytes.fromhex("0a0172" "120161")
+    c = pr.ContainerResources(name="c", devices=[d])
+    assert c.SerializeToString() == bytes.fromhex("0a0163" "1206") + d.SerializeToString()
+    p = pr.PodResources(name="p", namespace="n", containers=[c])
+    assert p.SerializeToString() == bytes.fromhex("0a0170" "12016e" "1a0b") + c.SerializeToString()
+    # the same container with a DRA dynamic_resources entry (field 5) the plugin does not model
+    c_dra = c.SerializeToString() + bytes.fromhex("2a00")
+    raw = bytes.fromhex("0a0170" "12016e" "1a0d") + c_dra
+    resp = pr.ListPodResourcesResponse.FromString(bytes([0x0a, len(raw)]) + raw)
+    assert pr.pod_devices(resp, "r") == [pr.PodDevices("n", "p", (("c", ("a",)),))]
+    assert pr.pod_devices(resp, "other") == []
+    assert pr.PROTO.method_path("PodResourcesLister", "List") == "/v1.PodResourcesLister/List"
+    assert pr.FILE_DESCRIPTOR.services_by_name["PodResourcesLister"].full_name == "v1.PodResourcesLister"
+    g = pr.GetPodResourcesRequest(pod_name="p", pod_namespace="n")
+    assert g.SerializeToString() == bytes.fromhex("0a0170" "12016e")
