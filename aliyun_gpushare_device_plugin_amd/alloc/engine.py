@@ -139,6 +139,7 @@ class Allocator:
         # placement truth: answered containers, the kubelet's pod-resources view, and the
         # annotation changes this plugin has queued but the pod cache may not show yet
         self.grants = PL.GrantBook()
+        self._ledgers = self._ledger_dir(self.opts)
         self.podres = None
         self._overlay: dict[str, dict] = {}       # uid -> annotations written, not yet landed
         self._overlay_gen: dict[str, int] = {}
@@ -162,6 +163,18 @@ class Allocator:
                             e["ns"], e["name"], e["uid"])
             threading.Thread(target=self._patcher, name="assign-patcher", daemon=True).start()
 
+    @staticmethod
+    def _ledger_dir(opts: AllocatorOptions):
+        if not (opts.ledger_dir and opts.shim is not None):
+            return None
+        from ..quota.ledger import LedgerDir
+        ld = LedgerDir(opts.ledger_dir)
+        try:
+            ld.prepare()
+        except OSError as e:
+            log.warning("ledger dir %s: %s", opts.ledger_dir, e)
+        return ld
+
     def reconfigure(self, model: DeviceModel, pods: PodSource, client: APIClient | None,
                     opts: AllocatorOptions) -> "Allocator":
         """Plugin rebuild (kubelet restart, SIGHUP; ``gpumanager.go:82-96``): new devices, pod
@@ -170,7 +183,10 @@ class Allocator:
         with self._mu:
             self.model, self.pods, self.client = model, pods, client
             async_patch = self.opts.async_patch
+            ledger_dir = self.opts.ledger_dir
             self.opts = dataclasses.replace(opts, async_patch=async_patch, journal_path=self.opts.journal_path)
+            if opts.ledger_dir != ledger_dir:
+                self._ledgers = self._ledger_dir(self.opts)
             self._pinfo.clear()
         return self
 
@@ -400,10 +416,18 @@ class Allocator:
             r.envs[const.ENV_SHIM_LEDGER] = ledger_name(pod_uid or f"{gpu_index}-{time.time_ns()}", slot)
             # exact bytes from the SMI-reported HBM size, so the shim needs no device query
             r.envs[const.ENV_SHIM_QUOTA_BYTES] = str(U.quota_bytes(ctr_units, g.units, g.vram_bytes))
-            if self.opts.ledger_dir:
-                r.mounts.add(container_path=const.LEDGER_CONTAINER_DIR, host_path=self.opts.ledger_dir,
-                             read_only=False)
-                r.envs[const.ENV_SHIM_LEDGER_DIR] = const.LEDGER_CONTAINER_DIR
+            if self._ledgers is not None:
+                # this container's own ledger directory (quota/ledger.py): a tenant never sees
+                # another container's ledger
+                lkey = self._ledgers.new_key(pod_uid or f"gpu{gpu_index}", slot)
+                try:
+                    host = self._ledgers.create(lkey, pod_uid)
+                except OSError as e:
+                    log.warning("ledger dir for pod %s: %s (pod-private shm ledger instead)", pod_uid, e)
+                else:
+                    r.mounts.add(container_path=const.LEDGER_CONTAINER_DIR, host_path=host, read_only=False)
+                    r.envs[const.ENV_SHIM_LEDGER_DIR] = const.LEDGER_CONTAINER_DIR
+                    r.annotations[const.CTR_ANNOTATION_LEDGER] = lkey
         return r
 
     def _plan_slots(self, claim: _Claim, pod_units: int) -> cuslots.SlotRun | None:
@@ -587,7 +611,8 @@ class Allocator:
     def _grant_from(cresp, uid: str, t: float) -> PL.Grant:
         e = cresp.envs
         return PL.Grant(gpu=int(e.get(const.ENV_RESOURCE_INDEX, "-1")), units=int(e.get(const.ENV_RESOURCE_BY_CONTAINER, "0")),
-                        claimed=uid, t=t, cu=e.get(const.ENV_CU_SLOTS), ledger=e.get(const.ENV_SHIM_LEDGER, ""))
+                        claimed=uid, t=t, cu=e.get(const.ENV_CU_SLOTS),
+                        ledger=cresp.annotations.get(const.CTR_ANNOTATION_LEDGER, ""))
 
     def _record_grants(self, req, resp, uid: str, jkey: str) -> None:
         t = time.time()
@@ -791,6 +816,14 @@ class Allocator:
         if f.assigned is False:
             self.journal.forget(f.uid)
             self._drop_slots(f.uid)
+        if self._ledgers is not None:
+            for k in f.holder_of:          # the holder's containers write these ledgers
+                g = self.grants.get(k)
+                if g is not None and g.ledger and g.claimed != f.uid:
+                    try:
+                        self._ledgers.add_owner(g.ledger, f.uid)
+                    except OSError as e:
+                        log.warning("ledger owner record %s: %s", g.ledger, e)
         job = _PatchJob(f.uid, f.ns, f.name, ann, kind="placement", gen=gen)
         if self._patch_q is not None:
             self._patch_q.put(job)

@@ -64,6 +64,9 @@ ENV_SHIM_GRANULE = "GPUSHARE_ALLOC_GRANULE"    # allocation rounding granule ove
 ENV_SHIM_LOG = "GPUSHARE_SHIM_LOG"
 ENV_SHIM_LEDGER_DIR = "GPUSHARE_LEDGER_DIR"    # file-backed ledgers in a host-mounted directory
 LEDGER_CONTAINER_DIR = "/run/gpushare/ledger"
+# container annotation (ContainerAllocateResponse.annotations): the host ledger directory key
+# of this container, so the plugin can map an answer back to its ledger (quota/ledger.py)
+CTR_ANNOTATION_LEDGER = "gpushare.amd.com/ledger"
 ENV_GPU_UUID = "GPUSHARE_GPU_UUID"            # the physical GPU a container was given
 ENV_ROCR_VISIBLE = "ROCR_VISIBLE_DEVICES"
 # Compute isolation (--compute-isolation=cu, alloc/cuslots.py): queue CU masks read by ROCr / HIP.

@@ -210,17 +210,18 @@ class SharedGPUManager:
 
     def _start_ledger_collector(self):
         """Export the quota shim's per-container ledgers (--ledger-dir) every ledger_scan_s and
-        drop the ledgers of pods that no longer exist on this node."""
+        remove the ledger directories of containers whose pods no longer exist on this node."""
         d = self.cfg.ledger_dir
         if not d or self._ledger_thread is not None:
             return
         from ..quota import ledger as L
 
-        os.makedirs(d, exist_ok=True)
+        # layout and permissions: quota/ledger.py (the root stays plugin-owned, 0755; each
+        # container gets its own subdirectory)
         try:
-            os.chmod(d, 0o1777)     # containers may run as any uid; sticky like /tmp
+            L.LedgerDir(d).prepare()
         except OSError as e:
-            log.warning("cannot chmod ledger dir %s: %s", d, e)
+            log.warning("cannot prepare ledger dir %s: %s", d, e)
 
         def loop():
             while not self._ledger_stop.wait(self.cfg.ledger_scan_s):

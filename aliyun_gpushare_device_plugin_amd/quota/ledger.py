@@ -1,20 +1,37 @@
-"""Reader for the quota shim's per-container ledgers (native/hipshim/hipquota.cpp).
+"""Per-container quota-shim ledgers on the host: isolation, usage export, garbage collection.
 
-With ``--ledger-dir`` the plugin mounts a host directory into every shared container and
-the shim keeps its ledger there as a file (``<dir>/gpushare-<pod-uid>-<slot>.ledger``) instead
-of a POSIX shm object in the pod-private ``/dev/shm``. The node agent can then read what each
-container actually holds, its peak and how many allocations the quota refused — the "shim-
-reported per-container usage and quota denials" of SURVEY §5.5 — and garbage-collect the
-ledgers of pods that are gone.
+With ``--ledger-dir`` the quota shim (native/hipshim/hipquota.cpp) keeps each container's
+ledger as a file the node agent can read — what the container holds, its peak and how many
+allocations the quota refused (the "shim-reported per-container usage and quota denials" of
+SURVEY §5.5) — instead of a POSIX shm object in the pod-private ``/dev/shm``.
 
-Layout (``struct LedgerShm``, little-endian): magic, quota, total, denied, peak (u64 each),
-then 256 slots of {i32 pid, i32 pad, u64 used}.
+Layout (host side)::
+
+    <root>/                      0755, plugin-owned, never mounted
+    <root>/<lkey>/               0777, bind-mounted read-write into exactly ONE container at
+                                 const.LEDGER_CONTAINER_DIR (Allocate ``Mount``)
+    <root>/<lkey>/gpushare-<pod-uid-key>-<slot>.ledger    written by the shim
+    <root>/.owners/<lkey>        0600 JSON {"pods": [uid, ...], "t": ...}, plugin-only
+
+A container sees only its own ledger directory, so no tenant can read a neighbour's usage or
+rewrite its ``total``/``quota``. ``lkey`` is unique per answered container (pod-uid key,
+container slot, random suffix), so a recycled set of fake IDs or a re-answered pod never
+lands on an old ledger. The owner record names the pod the answer was matched to and — after
+placement truth (``alloc/placement.py``) found that another pod's container holds it — that
+pod too; a directory is garbage once none of its owners is alive on the node, whatever the
+ledger says is used (a SIGKILLed or OOM-killed container never releases its slot).
+
+Ledger file format (``struct LedgerShm``, little-endian): magic, quota, total, denied, peak
+(u64 each), then 256 slots of {i32 pid, i32 pad, u64 used}.
 """
 from __future__ import annotations
 
 import dataclasses
+import json
 import os
+import shutil
 import struct
+import time
 
 MAGIC = 0x67707573686172          # "gpushar"
 N_SLOTS = 256
@@ -22,6 +39,7 @@ _HDR = struct.Struct("<5Q")
 _SLOT = struct.Struct("<iiQ")
 LEDGER_BYTES = _HDR.size + N_SLOTS * _SLOT.size
 SUFFIX = ".ledger"
+OWNERS = ".owners"
 
 
 @dataclasses.dataclass(frozen=True)
@@ -34,9 +52,10 @@ class LedgerStats:
     denied: int
     peak: int
     processes: int      # slots with a live (non-zero) pid
+    lkey: str = ""      # the per-container directory it lives in ("" = legacy flat layout)
 
 
-def parse(buf: bytes, name: str = "") -> LedgerStats | None:
+def parse(buf: bytes, name: str = "", lkey: str = "") -> LedgerStats | None:
     if len(buf) < LEDGER_BYTES:
         return None
     magic, quota, total, denied, peak = _HDR.unpack_from(buf, 0)
@@ -49,30 +68,17 @@ def parse(buf: bytes, name: str = "") -> LedgerStats | None:
         k, _, s = body.rpartition("-")
         if s.isdigit():
             key, slot = k, int(s)
-    return LedgerStats(name, key, slot, quota, total, denied, peak, procs)
+    return LedgerStats(name, key, slot, quota, total, denied, peak, procs, lkey)
 
 
-def read(path: str) -> LedgerStats | None:
+def read(path: str, lkey: str = "") -> LedgerStats | None:
     try:
         with open(path, "rb") as f:
             buf = f.read(LEDGER_BYTES)
     except OSError:
         return None
-    return parse(buf, os.path.basename(path)[: -len(SUFFIX)] if path.endswith(SUFFIX) else os.path.basename(path))
-
-
-def scan(directory: str) -> list[LedgerStats]:
-    out = []
-    try:
-        names = sorted(os.listdir(directory))
-    except OSError:
-        return out
-    for n in names:
-        if n.endswith(SUFFIX):
-            st = read(os.path.join(directory, n))
-            if st is not None:
-                out.append(st)
-    return out
+    base = os.path.basename(path)
+    return parse(buf, base[: -len(SUFFIX)] if base.endswith(SUFFIX) else base, lkey)
 
 
 def uid_key(pod_uid: str) -> str:
@@ -80,25 +86,129 @@ def uid_key(pod_uid: str) -> str:
     return "".join(ch for ch in pod_uid if ch.isalnum())[:40] or "anon"
 
 
-def collect(directory: str, metrics, live_uids: set[str] | None = None, gc: bool = True) -> list[LedgerStats]:
-    """Export every ledger's numbers as gauges; with ``live_uids`` (this node's pods), remove
-    ledgers whose pod no longer exists and whose processes have all exited."""
-    stats = scan(directory)
+class LedgerDir:
+    """The plugin's side of ``<root>``: per-container directories and their owner records."""
+
+    def __init__(self, root: str):
+        self.root = root
+        self._owners = os.path.join(root, OWNERS)
+
+    def prepare(self) -> None:
+        os.makedirs(self._owners, exist_ok=True)
+        os.chmod(self.root, 0o755)        # tenants never see the root, only their own subdir
+        os.chmod(self._owners, 0o700)
+
+    def new_key(self, pod_uid: str, slot: int) -> str:
+        return f"{uid_key(pod_uid)[:32]}-{slot}-{os.urandom(4).hex()}"
+
+    def create(self, lkey: str, owner_uid: str) -> str:
+        """Create ``<root>/<lkey>`` (writable by any container uid) and its owner record;
+        returns the host path to mount."""
+        path = os.path.join(self.root, lkey)
+        os.makedirs(path, exist_ok=True)
+        os.chmod(path, 0o777)
+        self._write_owners(lkey, [owner_uid] if owner_uid else [])
+        return path
+
+    def _write_owners(self, lkey: str, pods: list) -> None:
+        tmp = os.path.join(self._owners, f".{lkey}.tmp")
+        with open(tmp, "w") as f:
+            json.dump({"pods": pods, "t": time.time()}, f)
+        os.replace(tmp, os.path.join(self._owners, lkey))
+
+    def owners(self, lkey: str) -> tuple[list, float]:
+        try:
+            with open(os.path.join(self._owners, lkey)) as f:
+                d = json.load(f)
+            return list(d.get("pods") or []), float(d.get("t") or 0.0)
+        except (OSError, ValueError):
+            return [], 0.0
+
+    def add_owner(self, lkey: str, uid: str) -> None:
+        """Placement truth: ``uid``'s container holds the grant this ledger was made for."""
+        pods, _ = self.owners(lkey)
+        if uid and uid not in pods:
+            self._write_owners(lkey, pods + [uid])
+
+    def keys(self) -> list[str]:
+        try:
+            return sorted(n for n in os.listdir(self.root)
+                          if n != OWNERS and not n.startswith(".") and os.path.isdir(os.path.join(self.root, n)))
+        except OSError:
+            return []
+
+    def remove(self, lkey: str) -> None:
+        shutil.rmtree(os.path.join(self.root, lkey), ignore_errors=True)
+        try:
+            os.unlink(os.path.join(self._owners, lkey))
+        except OSError:
+            pass
+
+
+def scan(directory: str) -> list[LedgerStats]:
+    """Every ledger under ``directory``: per-container subdirectories, plus ledger files left
+    in the root by the legacy flat layout."""
+    out = []
+    ld = LedgerDir(directory)
+    for lkey in ld.keys():
+        sub = os.path.join(directory, lkey)
+        try:
+            names = sorted(os.listdir(sub))
+        except OSError:
+            continue
+        for n in names:
+            if n.endswith(SUFFIX):
+                st = read(os.path.join(sub, n), lkey)
+                if st is not None:
+                    out.append(st)
+    try:
+        flat = sorted(n for n in os.listdir(directory) if n.endswith(SUFFIX))
+    except OSError:
+        flat = []
+    for n in flat:
+        st = read(os.path.join(directory, n))
+        if st is not None:
+            out.append(st)
+    return out
+
+
+def collect(directory: str, metrics, live_uids: set[str] | None = None, gc: bool = True,
+            grace_s: float = 60.0) -> list[LedgerStats]:
+    """Export every live ledger's numbers as gauges (labelled with the pod that holds it); with
+    ``live_uids`` (this node's pods) remove the ledgers of containers whose pods are all gone —
+    regardless of the ``used`` they still show (a killed process never releases its slot).
+    A directory younger than ``grace_s`` is kept: its pod may not be in the cache yet."""
+    ld = LedgerDir(directory)
+    now = time.time()
     live_keys = {uid_key(u) for u in live_uids} if live_uids is not None else None
+    removed: set[str] = set()
+    holder: dict[str, str] = {}
+    for lkey in ld.keys():
+        pods, t = ld.owners(lkey)
+        alive = [u for u in pods if live_uids is None or u in live_uids]
+        if alive:
+            holder[lkey] = uid_key(alive[-1])   # the latest owner: the pod really running it
+        elif gc and live_uids is not None and now - t > grace_s:
+            ld.remove(lkey)
+            removed.add(lkey)
     metrics.shim_used.clear()
     metrics.shim_quota.clear()
     metrics.shim_peak.clear()
     metrics.shim_denied.clear()
-    for st in stats:
-        if gc and live_keys is not None and st.pod_uid_key not in live_keys and st.used == 0:
-            try:
+    out = []
+    for st in scan(directory):
+        if st.lkey in removed:
+            continue
+        if not st.lkey and gc and live_keys is not None and st.pod_uid_key not in live_keys:
+            try:                                # legacy flat ledger of a gone pod
                 os.unlink(os.path.join(directory, st.name + SUFFIX))
             except OSError:
                 pass
             continue
-        labels = {"pod_uid": st.pod_uid_key, "container": str(st.container_slot)}
+        out.append(st)
+        labels = {"pod_uid": holder.get(st.lkey, st.pod_uid_key), "container": str(st.container_slot)}
         metrics.shim_used.set(st.used, **labels)
         metrics.shim_quota.set(st.quota, **labels)
         metrics.shim_peak.set(st.peak, **labels)
         metrics.shim_denied.set(st.denied, **labels)
-    return stats
+    return out

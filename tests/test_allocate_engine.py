@@ -2,6 +2,7 @@
 import concurrent.futures as cf
 import itertools
 import json
+import os
 import threading
 import time
 
@@ -369,14 +370,31 @@ def test_swapped_admission_order_is_completed(complete):
     assert dict(al2.allocate(req(2)).container_responses[0].envs)[const.ENV_RESOURCE_INDEX] == "-1"
 
 
-def test_ledger_dir_mount_and_env():
+def test_ledger_dir_mount_and_env(tmp_path):
+    """Round-2 review: every shared container used to get the node-wide ledger directory
+    read-write. Now each answered container gets its own subdirectory (root 0755, plugin-owned;
+    owner records outside any mount), so a tenant can neither read nor rewrite a neighbour's
+    ledger."""
     from aliyun_gpushare_device_plugin_amd.quota import ShimConfig
-    al, _, _ = make([mkpod("p", 2, 1, 10)], shim=ShimConfig("/opt/gpushare"), ledger_dir="/var/run/gpushare/ledgers")
-    r = al.allocate(req(2)).container_responses[0]
-    mounts = {m.container_path: (m.host_path, m.read_only) for m in r.mounts}
-    assert mounts[const.LEDGER_CONTAINER_DIR] == ("/var/run/gpushare/ledgers", False)
-    assert mounts[const.SHIM_CONTAINER_DIR] == ("/opt/gpushare", True)
-    assert r.envs[const.ENV_SHIM_LEDGER_DIR] == const.LEDGER_CONTAINER_DIR
+    from aliyun_gpushare_device_plugin_amd.quota import ledger as L
+    root = tmp_path / "ledgers"
+    al, _, _ = make([mkpod("p", 2, 1, 10), mkpod("q", 2, 0, 20)], shim=ShimConfig("/opt/gpushare"),
+                    ledger_dir=str(root))
+    rp, rq = (al.allocate(req(2)).container_responses[0] for _ in range(2))
+    mp, mq = ({m.container_path: (m.host_path, m.read_only) for m in r.mounts} for r in (rp, rq))
+    assert mp[const.SHIM_CONTAINER_DIR] == ("/opt/gpushare", True)
+    hp, hq = mp[const.LEDGER_CONTAINER_DIR][0], mq[const.LEDGER_CONTAINER_DIR][0]
+    assert mp[const.LEDGER_CONTAINER_DIR][1] is False
+    assert hp != hq and os.path.dirname(hp) == os.path.dirname(hq) == str(root)
+    assert os.path.basename(hp) == rp.annotations[const.CTR_ANNOTATION_LEDGER]
+    assert rp.envs[const.ENV_SHIM_LEDGER_DIR] == const.LEDGER_CONTAINER_DIR
+    assert oct(os.stat(root).st_mode & 0o7777) == "0o755"
+    assert oct(os.stat(hp).st_mode & 0o777) == "0o777"
+    ld = L.LedgerDir(str(root))
+    assert ld.owners(os.path.basename(hp))[0] == ["uid-p"] and ld.owners(os.path.basename(hq))[0] == ["uid-q"]
+    # nothing of q's is reachable below p's mount (the only host path p's container sees)
+    (tmp_path / "ledgers" / os.path.basename(hq) / "gpushare-uidq-0.ledger").write_bytes(b"x")
+    assert os.listdir(hp) == []
     al2, _, _ = make([mkpod("p", 2, 1, 10)], shim=ShimConfig("/opt/gpushare"))
     assert const.ENV_SHIM_LEDGER_DIR not in al2.allocate(req(2)).container_responses[0].envs
 

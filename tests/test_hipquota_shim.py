@@ -280,3 +280,53 @@ def test_file_backed_ledger_is_readable_by_the_plugin(stub, native_shim, tmp_pat
     # process gone and pod gone -> the collector removes the ledger
     L.collect(str(tmp_path), PluginMetrics(), live_uids=set())
     assert not list(tmp_path.glob("*.ledger"))
+
+
+def test_per_container_ledger_dirs_and_gc_after_sigkill(stub, native_shim, tmp_path):
+    """Round-2 review item 2: each container's shim writes into its own ledger directory (the
+    only one mounted into it), and a SIGKILLed container's ledger — still showing its bytes as
+    used — is removed once its pod is gone, not exported forever."""
+    import signal
+    import time
+
+    from aliyun_gpushare_device_plugin_amd.quota import ledger as L, ledger_name
+    from aliyun_gpushare_device_plugin_amd.utils.metrics import PluginMetrics
+    root = tmp_path / "ledgers"
+    ld = L.LedgerDir(str(root))
+    ld.prepare()
+    d, drv = stub
+    procs, keys = [], {}
+    for uid in ("uid-a", "uid-b"):
+        lkey = ld.new_key(uid, 0)
+        keys[uid] = lkey
+        env = dict(os.environ, LD_PRELOAD=native_shim, LD_LIBRARY_PATH=str(d), GPUSHARE_LEDGER=ledger_name(uid, 0),
+                   GPUSHARE_LEDGER_DIR=ld.create(lkey, uid), GPUSHARE_QUOTA_BYTES=str(4 * GIB))
+        procs.append(subprocess.Popen([str(drv), "alloc", str(1 * GIB), "sleep", "30"], env=env,
+                                      stdout=subprocess.PIPE, text=True))
+    try:
+        for p in procs:
+            assert json.loads(p.stdout.readline())["err"] == 0
+        # each directory holds exactly its own container's ledger
+        for uid, lkey in keys.items():
+            assert [n for n in os.listdir(root / lkey)] == [ledger_name(uid, 0).lstrip("/") + L.SUFFIX]
+        m = PluginMetrics()
+        got = {st.lkey: st for st in L.collect(str(root), m, live_uids={"uid-a", "uid-b"})}
+        assert got[keys["uid-a"]].used == got[keys["uid-b"]].used == 1 * GIB
+        procs[0].send_signal(signal.SIGKILL)         # OOM-kill: the slot is never released
+        procs[0].wait(timeout=10)
+        st = L.read(str(root / keys["uid-a"] / (ledger_name("uid-a", 0).lstrip("/") + L.SUFFIX)))
+        assert st.used == 1 * GIB
+        # pod a deleted: its directory goes (after the grace period), b's stays
+        left = {s.lkey for s in L.collect(str(root), m, live_uids={"uid-b"}, grace_s=0.0)}
+        assert left == {keys["uid-b"]} and not (root / keys["uid-a"]).exists()
+        assert 'pod_uid="uida"' not in m.registry.render()
+        # placement truth: b's ledger is also owned by c (the pod really running it); b gone, c alive
+        ld.add_owner(keys["uid-b"], "uid-c")
+        time.sleep(0.01)
+        left = {s.lkey for s in L.collect(str(root), m, live_uids={"uid-c"}, grace_s=0.0)}
+        assert left == {keys["uid-b"]} and 'pod_uid="uidc"' in m.registry.render()
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+            p.wait(timeout=10)
