@@ -34,11 +34,15 @@ from .model import DeviceModel
 
 class HealthMonitor:
     def __init__(self, smi: S.SMI, model: DeviceModel, poll_interval: float = 5.0,
-                 on_change=None, on_topology_change=None):
+                 on_change=None, on_topology_change=None, on_sample=None):
         self.smi, self.model = smi, model
         self.poll_interval = poll_interval
         self.on_change = on_change
         self.on_topology_change = on_topology_change
+        # on_sample(model_index, smi_device) after every poll: per-GPU HBM used for the
+        # gpushare_hbm_used_bytes gauge
+        self.on_sample = on_sample
+        self.degraded: str = ""            # why health detection is weaker than it should be
         self._stop = threading.Event()
         self._threads: list[threading.Thread] = []
         self._ecc_baseline = {}
@@ -58,9 +62,12 @@ class HealthMonitor:
             log.warning("health status unavailable: %s", e)
         st = self.status
         if st and st.get("events_armed", 0) < self.smi.count():
-            log.warning("SMI event notification armed on %d/%d GPUs (status %d): resets/VM faults on the others "
-                        "are seen by polling only", st.get("events_armed", 0), self.smi.count(),
-                        st.get("events_last_status", 0))
+            # typically the plugin container cannot open /dev/kfd (not privileged / no device
+            # cgroup grant): resets are then only seen by the poll, seconds late
+            self.degraded = (f"SMI event notification armed on {st.get('events_armed', 0)}/{self.smi.count()} GPUs "
+                             f"(status {st.get('events_last_status', 0)})")
+            log.error("%s: resets/VM faults on the others are seen by polling only; check that the plugin "
+                      "container can open /dev/kfd (privileged DaemonSet)", self.degraded)
         if st and st.get("ecc_reads_failed", 0):
             log.warning("ECC counters unreadable on %d GPU(s) (status %d): uncorrectable-error health is blind there",
                         st["ecc_reads_failed"], st.get("ecc_last_status", 0))
@@ -68,12 +75,21 @@ class HealthMonitor:
             t = threading.Thread(target=target, name=name, daemon=True)
             t.start()
             self._threads.append(t)
+        if self.on_sample is not None:
+            for g in self.model.gpus:           # first sample now, not one poll interval later
+                d = next((x for x in self.smi.devices() if x.uuid == g.uuid), None)
+                if d is not None:
+                    self.on_sample(g.index, d)
         return self
 
     def stop(self):
         self._stop.set()
         for t in self._threads:
             t.join(timeout=2.0)
+
+    @property
+    def ready(self) -> bool:
+        return not self.degraded
 
     # -- helpers --------------------------------------------------------------------------
     def _set(self, index: int, healthy: bool, reason: str, present: bool | None = None):
@@ -149,6 +165,8 @@ class HealthMonitor:
             if d is None:
                 self._set(g.index, False, "device missing", present=False)
                 continue
+            if self.on_sample is not None:
+                self.on_sample(g.index, d)
             base = self._ecc_baseline.setdefault(g.uuid, d.ecc_ue)
             if d.ecc_ue > base:
                 self._set(g.index, False, f"uncorrectable ECC errors {base}->{d.ecc_ue}", present=True)

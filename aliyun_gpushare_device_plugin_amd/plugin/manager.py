@@ -178,6 +178,16 @@ class SharedGPUManager:
         return DevicePluginServer(model, allocator, self._plugin_socket(), const.RESOURCE_NAME,
                                   cfg.preferred_allocation, self.metrics)
 
+    def readiness(self) -> tuple[bool, str]:
+        """``/readyz``: serving and registered, with health detection at full strength (SMI
+        event notification armed on every GPU). A DaemonSet pod that cannot open /dev/kfd shows
+        NotReady instead of silently degrading to polling."""
+        if self.plugin is None or self.plugin.stopped.is_set():
+            return False, "device plugin not serving"
+        if self.health is not None and not self.health.ready:
+            return False, self.health.degraded
+        return True, "ok"
+
     def _pod_resources(self):
         from ..api.podresources import SOCKET, PodResourcesClient
 
@@ -202,11 +212,16 @@ class SharedGPUManager:
                 self.metrics.device_health.set(1 if healthy else 0, gpu=str(idx))
                 self._export_health()
 
+            def sample(idx, d):
+                self.metrics.hbm_used.set(d.vram_used, gpu=str(idx))
+
             self.health = HealthMonitor(self.smi, self.model, self.cfg.health_poll_s, on_change=changed,
-                                        on_topology_change=lambda ev: self._export_topology()).start()
+                                        on_topology_change=lambda ev: self._export_topology(),
+                                        on_sample=sample).start()
             st = self.health.status
             self.metrics.health_events_armed.set(st.get("events_armed", 0))
             self.metrics.health_ecc_readable.set(st.get("ecc_reads_ok", 0))
+            self.metrics.health_degraded.set(0 if self.health.ready else 1)
 
     def _start_ledger_collector(self):
         """Export the quota shim's per-container ledgers (--ledger-dir) every ledger_scan_s and
@@ -268,7 +283,8 @@ class SharedGPUManager:
             self.client = build_client(cfg.kubeconfig, cfg.apiserver, cfg.timeout)
         if cfg.metrics_addr:
             self._metrics_srv = M.serve(self.metrics.registry, cfg.metrics_addr,
-                                        lambda: self.plugin is not None and not self.plugin.stopped.is_set())
+                                        lambda: self.plugin is not None and not self.plugin.stopped.is_set(),
+                                        ready_fn=self.readiness)
         os.makedirs(cfg.device_plugin_dir, exist_ok=True)
         watcher = FSWatcher(cfg.device_plugin_dir, self.events)
         log.V(1).info("Starting FS watcher (%s).", watcher.mode)

@@ -184,6 +184,9 @@ class PluginMetrics:
         self.health_events_armed = r.gauge("gpushare_health_events_armed",
                                            "GPUs with SMI event notification (reset / VM fault) armed")
         self.health_ecc_readable = r.gauge("gpushare_health_ecc_readable", "GPUs whose ECC counters were read")
+        self.health_degraded = r.gauge("gpushare_health_degraded",
+                                       "1 if SMI event notification is not armed on every GPU (alert: /dev/kfd "
+                                       "not accessible; resets seen by polling only)")
         self.config_error = r.gauge("gpushare_config_error", "1 if the plugin parked on an impossible config")
         self.device_health = r.gauge("gpushare_device_healthy", "1 if the GPU is healthy")
         self.hbm_used = r.gauge("gpushare_hbm_used_bytes", "HBM in use per GPU (SMI)")
@@ -199,8 +202,9 @@ class PluginMetrics:
                                      "(slot = one CU on every XCD; > slots per GPU means oversubscribed)")
 
 
-def serve(registry: Registry, addr: str, health_fn=None) -> http.server.ThreadingHTTPServer:
-    """Start ``/metrics`` + ``/healthz`` + ``/debug/latency`` on ``host:port`` in a daemon thread.
+def serve(registry: Registry, addr: str, health_fn=None, ready_fn=None) -> http.server.ThreadingHTTPServer:
+    """Start ``/metrics`` + ``/healthz`` + ``/readyz`` + ``/debug/latency`` on ``host:port`` in a
+    daemon thread. ``ready_fn() -> (ok, reason)`` backs ``/readyz`` (503 + reason when not ready).
 
     ``/debug/latency`` returns exact p50/p90/p99 of every histogram (JSON); ``?reset=1`` also
     clears them, honoured only with ``GPUSHARE_DEBUG=1`` (benchmarks bracket a timed region)."""
@@ -220,6 +224,9 @@ def serve(registry: Registry, addr: str, health_fn=None) -> http.server.Threadin
                 if "reset=1" in self.path and _os.environ.get("GPUSHARE_DEBUG") == "1":
                     for h in hs.values():
                         h.reset()
+            elif self.path.startswith("/readyz"):
+                ok, why = (True, "ok") if ready_fn is None else ready_fn()
+                body, ctype, code = why.encode(), "text/plain", 200 if ok else 503
             elif self.path.startswith("/healthz"):
                 ok = True if health_fn is None else bool(health_fn())
                 body, ctype, code = (b"ok" if ok else b"unhealthy"), "text/plain", 200 if ok else 503

@@ -924,7 +924,7 @@ class FakeBackend : public Backend {
     std::string op;
     int a = -1, b = -1;
     is >> op >> a;
-    if (op == "linkdown" || op == "linkup" || op == "ecc") is >> b;
+    if (op == "linkdown" || op == "linkup" || op == "ecc" || op == "vram") is >> b;
     std::lock_guard<std::mutex> lk(mu_);
     if (a < 0 || a >= (int)all_.size()) {
       set_err("inject: bad device index in '" + cmd + "'");
@@ -949,6 +949,8 @@ class FakeBackend : public Backend {
     } else if (op == "ecc") {
       all_[a].ecc_ue += (uint64_t)(b > 0 ? b : 1);
       push(a, GS_EV_ECC_UE, "uncorrectable ECC error");
+    } else if (op == "vram") {  // "vram <idx> <MiB>": the HBM use the backend reports (no event)
+      all_[a].vram_used = (uint64_t)(b > 0 ? b : 0) << 20;
     } else if (op == "vmfault") {
       push(a, GS_EV_VMFAULT, "VM fault");
     } else if (op == "thermal") {

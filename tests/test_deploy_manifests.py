@@ -57,3 +57,47 @@ def test_demo_pods_use_the_plugin_contract():
                 if k.startswith("gpushare.amd.com/"):
                     assert k == const.POD_ANNOTATION_CU_SLOTS_REQUEST, (path, k)
     assert seen >= 4
+
+
+def _ds():
+    ds = [d for _, d in _docs() if d["kind"] == "DaemonSet"]
+    assert len(ds) == 1
+    return ds[0]["spec"]["template"]["spec"]
+
+
+def test_daemonset_can_open_kfd_and_render_nodes():
+    """Round-2 review item 3: a hostPath mount of /dev/kfd without a device-cgroup grant is
+    refused at open(), so SMI event notification could never arm in a cluster. The plugin
+    container must be privileged (AMD's own device plugin does the same) — and then the
+    security context must not contradict it — and /readyz must gate readiness on it."""
+    spec = _ds()
+    c = spec["containers"][0]
+    sc = c.get("securityContext") or {}
+    assert sc.get("privileged") is True
+    # the API server rejects privileged + allowPrivilegeEscalation=false; dropping all
+    # capabilities would also defeat the KFD SMI-event ioctl
+    assert sc.get("allowPrivilegeEscalation") is not False
+    assert "ALL" not in ((sc.get("capabilities") or {}).get("drop") or [])
+    assert c["readinessProbe"]["httpGet"]["path"] == "/readyz"
+    assert c["livenessProbe"]["httpGet"]["path"] == "/healthz"
+    port = int(next(a for a in c["command"] if a.startswith("--metrics-addr=")).rsplit(":", 1)[1])
+    assert c["readinessProbe"]["httpGet"]["port"] == port
+
+
+def test_daemonset_mounts_match_the_flags():
+    """Every host path a flag names is mounted: the device-plugin dir (kubelet.sock + our
+    socket), the kubelet pod-resources socket (placement truth), the shim/ledger/journal dir
+    and /sys (read-only, SMI + KFD topology)."""
+    spec = _ds()
+    c = spec["containers"][0]
+    mounts = {m["mountPath"]: m for m in c["volumeMounts"]}
+    vols = {v["name"]: v for v in spec["volumes"]}
+    for path in ("/var/lib/kubelet/device-plugins", "/var/lib/kubelet/pod-resources", "/var/lib/gpushare", "/sys"):
+        assert path in mounts, path
+        assert vols[mounts[path]["name"]]["hostPath"]["path"] == path
+    assert mounts["/sys"].get("readOnly") is True
+    cfg = config_from_args(build_parser().parse_args([a for a in c["command"][1:] if a.startswith("--")]))
+    assert os.path.dirname(cfg.pod_resources_socket) == "/var/lib/kubelet/pod-resources"
+    for p in (cfg.ledger_dir, cfg.journal_path):
+        assert p.startswith("/var/lib/gpushare/")
+    assert spec.get("hostNetwork") is True and spec["nodeSelector"] == {"gpushare": "true"}

@@ -228,3 +228,32 @@ def test_rccl_tp_pair_allreduce():
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert d["backend"] == "nccl" and d["tp_block_rel_err"] < 5e-2 and d["busbw_GBps"] > 10
+
+
+def test_hbm_used_gauge_matches_sysfs():
+    """gpushare_hbm_used_bytes{gpu} (set from the health poll's SMI sample) tracks amdgpu's
+    mem_info_vram_used while this process holds 8 GiB on GPU 0."""
+    import time
+
+    import torch
+
+    from aliyun_gpushare_device_plugin_amd.device.health import HealthMonitor
+    from aliyun_gpushare_device_plugin_amd.utils.metrics import PluginMetrics
+
+    m = PluginMetrics()
+    with S.SMI("auto") as smi:
+        model = DeviceModel(smi.devices(), const.GIB, "nearest")
+        card = f"/sys/bus/pci/devices/{smi.device(0).bdf}/mem_info_vram_used"
+        mon = HealthMonitor(smi, model, 0.2, on_sample=lambda i, d: m.hbm_used.set(d.vram_used, gpu=str(i)))
+        mon.start()
+        try:
+            held = torch.empty(8 << 30, dtype=torch.uint8, device="cuda:0")
+            torch.cuda.synchronize()
+            time.sleep(0.6)
+            sysfs = int(open(card).read())
+            got = m.hbm_used.value(gpu="0")
+            assert sysfs >= 8 << 30 and got >= 8 << 30
+            assert abs(got - sysfs) < (1 << 30), (got, sysfs)   # same counter, sampled ~0.2 s apart
+            del held
+        finally:
+            mon.stop()

@@ -114,3 +114,45 @@ def test_best_group_prefers_connected_and_tight():
     assert T.best_group(topo, [60, 200, 100], 2, 50) == [0, 1]      # best fit among connected
     assert T.best_group(topo, [100, 0, 100], 2, 50) is None          # 0-2 only over PCIe
     assert T.best_group(None, [100, 0, 100], 2, 50) == [0, 2]        # no topology: capacity only
+
+
+def test_hbm_used_gauge_follows_smi():
+    """SURVEY §5.5 "SMI HBM used per GPU": gpushare_hbm_used_bytes{gpu} is set from the health
+    poll (round-2 review: the gauge was declared but never set)."""
+    with SimCluster([("n", "fake:2x8G")], health_poll_s=0.1) as c:
+        mgr = c.manager("n")
+        m = mgr.metrics.hbm_used
+        assert m.value(gpu="0") == 0 and m.value(gpu="1") == 0
+        mgr.smi.inject("vram 1 3072")
+        assert wait(lambda: m.value(gpu="1") == 3 << 30)
+        assert m.value(gpu="0") == 0
+        assert 'gpushare_hbm_used_bytes{gpu="1"} 3221225472' in mgr.metrics.registry.render()
+
+
+def test_unarmed_events_make_the_plugin_not_ready():
+    """Round-2 review item 3: when SMI event notification is not armed on every GPU (the
+    container cannot open /dev/kfd) the plugin logs at error level, sets
+    gpushare_health_degraded and /readyz answers 503 with the reason."""
+    import urllib.error
+    import urllib.request
+
+    from aliyun_gpushare_device_plugin_amd.utils import metrics as M
+
+    with SimCluster([("n", "fake:2x8G")], health_poll_s=0.5) as c:
+        mgr = c.manager("n")
+        assert mgr.readiness() == (True, "ok") and mgr.metrics.health_degraded.value() == 0
+        orig = mgr.smi.health_status
+        mgr.smi.health_status = lambda: dict(orig(), events_armed=0, events_last_status=13)
+        mgr._start_health()
+        ok, why = mgr.readiness()
+        assert not ok and "armed on 0/2" in why and mgr.metrics.health_degraded.value() == 1
+        srv = M.serve(mgr.metrics.registry, "127.0.0.1:0", ready_fn=mgr.readiness)
+        try:
+            port = srv.server_address[1]
+            try:
+                urllib.request.urlopen(f"http://127.0.0.1:{port}/readyz", timeout=5)
+                raise AssertionError("expected 503")
+            except urllib.error.HTTPError as e:
+                assert e.code == 503 and b"armed on 0/2" in e.read()
+        finally:
+            srv.shutdown()
