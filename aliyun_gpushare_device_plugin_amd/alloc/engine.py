@@ -173,7 +173,7 @@ class Allocator:
             ld.prepare()
         except OSError as e:
             log.warning("ledger dir %s: %s", opts.ledger_dir, e)
-        return ld
+        return ld.start()
 
     def reconfigure(self, model: DeviceModel, pods: PodSource, client: APIClient | None,
                     opts: AllocatorOptions) -> "Allocator":
@@ -419,9 +419,9 @@ class Allocator:
             if self._ledgers is not None:
                 # this container's own ledger directory (quota/ledger.py): a tenant never sees
                 # another container's ledger
-                lkey = self._ledgers.new_key(pod_uid or f"gpu{gpu_index}", slot)
                 try:
-                    host = self._ledgers.create(lkey, pod_uid)
+                    lkey = self._ledgers.take(pod_uid)
+                    host = self._ledgers.path(lkey)
                 except OSError as e:
                     log.warning("ledger dir for pod %s: %s (pod-private shm ledger instead)", pod_uid, e)
                 else:
@@ -630,17 +630,18 @@ class Allocator:
         if hit is None:
             return None
         uid, resp = hit
+        # the kubelet recycles freed fake IDs, so under churn most key hits belong to pods that
+        # are gone: one O(1) cache lookup decides (round 2 scanned every node pod here)
         try:
-            pods = self.pods.node_pods()
+            p = self.pods.get(uid)
         except Exception:  # noqa: BLE001
             return None
-        for p in pods:
-            if (O.uid(p) == uid and O.phase(p) == "Pending" and not (p.get("metadata") or {}).get("deletionTimestamp")
-                    and (A.is_assigned_pod(p) or uid in self._assigned)):
-                self.metrics.allocate_outcomes.inc(outcome="replay")
-                log.warning("Allocate retried for pod %s (same device IDs, still Pending): replaying the "
-                            "journaled answer", O.name(p))
-                return resp
+        if (p is not None and O.phase(p) == "Pending" and not O.deleting(p)
+                and (A.is_assigned_pod(p) or uid in self._assigned)):
+            self.metrics.allocate_outcomes.inc(outcome="replay")
+            log.warning("Allocate retried for pod %s (same device IDs, still Pending): replaying the "
+                        "journaled answer", O.name(p))
+            return resp()
         return None
 
     def _patcher(self):

@@ -17,11 +17,14 @@ restart or crash:
   its pod stays claimed, so a pod can neither be left ``ASSIGNED=false`` forever nor be
   matched a second time by the next plugin instance.
 
-Each record is one ``write(2)`` on an ``O_APPEND`` descriptor (no userspace buffering, no
-``fsync``): the journal must survive the *process* (kill, crash, OOM, DaemonSet rollout); a
-node crash takes the pods' containers down with it. A write-behind answer and its pending
-patch share one record (``{"op": "answer+patch", ...}``), so the journal costs one syscall
-on the Allocate path.
+The journal must survive the *process* (kill, crash, OOM, DaemonSet rollout), not the node:
+a node crash takes the pods' containers down with it. Records are JSON lines appended into a
+``MAP_SHARED`` mapping of a pre-sized file (zero bytes mark the end): a store into the page
+cache survives the process exactly like a ``write(2)`` without ``fsync`` does, and costs no
+system call on the Allocate path — a syscall there hands the GIL to whichever plugin thread is
+busy (the informer decoding the very pod's watch events) and the kubelet waits for it. A
+write-behind answer and its pending patch share one record (``{"op": "answer+patch", ...}``).
+When the mapping is full the live records are compacted into a fresh file (atomic rename).
 """
 from __future__ import annotations
 
@@ -29,6 +32,7 @@ import base64
 import collections
 import hashlib
 import json
+import mmap
 import os
 import threading
 import time
@@ -44,25 +48,29 @@ def request_key(req) -> str:
 
 class AllocJournal:
     def __init__(self, path: str | None = None, ttl_s: float = 120.0, max_entries: int = 4096,
-                 pending_ttl_s: float = 24 * 3600.0):
+                 pending_ttl_s: float = 24 * 3600.0, map_bytes: int = 16 << 20):
         self.path, self.ttl_s, self.max_entries = path, ttl_s, max_entries
         self.pending_ttl_s = pending_ttl_s
+        self.map_bytes = map_bytes
+        self._mm: mmap.mmap | None = None
+        self._off = 0
         self._mem: collections.OrderedDict[str, tuple[str, float, bytes]] = collections.OrderedDict()
         self._uids: dict[str, float] = {}                       # pod uid -> time of its answer
         self._pending: collections.OrderedDict[str, dict] = collections.OrderedDict()  # uid -> patch
         self._lock = threading.Lock()
         self._lines = 0
-        self._fd = -1
         if path:
             self._load()
 
     # -- persistence ------------------------------------------------------------------------
     def _load(self):
         try:
-            with open(self.path) as f:
-                lines = f.readlines()
+            with open(self.path, "rb") as f:
+                raw = f.read()
         except FileNotFoundError:
             return
+        end = raw.find(b"\0")                 # the mapped file's unused tail is zero
+        lines = (raw if end < 0 else raw[:end]).decode(errors="replace").splitlines()
         now = time.time()
         for line in lines:
             try:
@@ -88,38 +96,58 @@ class AllocJournal:
                  len(self._mem), len(self._pending))
         self._compact()
 
+    def _map(self):
+        """Map the journal file (grown to ``map_bytes``) and find the end of its records."""
+        os.makedirs(os.path.dirname(self.path) or ".", exist_ok=True)
+        fd = os.open(self.path, os.O_RDWR | os.O_CREAT | os.O_CLOEXEC, 0o600)
+        try:
+            size = max(self.map_bytes, os.fstat(fd).st_size)
+            os.ftruncate(fd, size)
+            self._mm = mmap.mmap(fd, size, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
+        finally:
+            os.close(fd)
+        end = self._mm.find(b"\0")
+        self._off = len(self._mm) if end < 0 else end
+
     def _write(self, rec: dict):
         if not self.path:
             return
+        data = (json.dumps(rec, separators=(",", ":")) + "\n").encode()
         try:
-            if self._fd < 0:
-                os.makedirs(os.path.dirname(self.path) or ".", exist_ok=True)
-                self._fd = os.open(self.path, os.O_WRONLY | os.O_APPEND | os.O_CREAT | os.O_CLOEXEC, 0o600)
-            os.write(self._fd, (json.dumps(rec, separators=(",", ":")) + "\n").encode())
+            if self._mm is None:
+                self._map()
+            if self._off + len(data) > len(self._mm):
+                self._compact(extra=data)
+                return
+            self._mm[self._off:self._off + len(data)] = data
+            self._off += len(data)
             self._lines += 1
-            if self._lines > 2 * self.max_entries + 2 * len(self._pending) + 64:
-                self._compact()
-        except OSError as e:
+        except (OSError, ValueError) as e:
             log.warning("allocation journal write failed: %s", e)
 
-    def _compact(self):
+    def _compact(self, extra: bytes = b""):
+        """Rewrite the live records (+ ``extra``) into a fresh mapped file, atomically."""
         if not self.path:
             return
         tmp = self.path + ".tmp"
         try:
             os.makedirs(os.path.dirname(self.path) or ".", exist_ok=True)
-            with open(tmp, "w") as f:
-                for k, (uid, t, blob) in self._mem.items():
-                    f.write(json.dumps({"k": k, "uid": uid, "t": t, "resp": base64.b64encode(blob).decode()},
-                                       separators=(",", ":")) + "\n")
-                for e in self._pending.values():
-                    f.write(json.dumps(e, separators=(",", ":")) + "\n")
-            if self._fd >= 0:
-                os.close(self._fd)
-                self._fd = -1
+            parts = [json.dumps({"k": k, "uid": uid, "t": t, "resp": base64.b64encode(blob).decode()},
+                                separators=(",", ":")).encode() + b"\n" for k, (uid, t, blob) in self._mem.items()]
+            parts += [json.dumps(e, separators=(",", ":")).encode() + b"\n" for e in self._pending.values()]
+            body = b"".join(parts) + extra
+            if len(body) * 2 > self.map_bytes:      # keep room for the next records
+                self.map_bytes = len(body) * 2
+            with open(tmp, "wb") as f:
+                f.write(body)
+                f.truncate(self.map_bytes)
+            if self._mm is not None:
+                self._mm.close()
+                self._mm = None
             os.replace(tmp, self.path)
-            self._lines = len(self._mem) + len(self._pending)
-        except OSError as e:
+            self._map()
+            self._lines = len(self._mem) + len(self._pending) + (1 if extra else 0)
+        except (OSError, ValueError) as e:
             log.warning("allocation journal compaction failed: %s", e)
 
     # -- answers ----------------------------------------------------------------------------
@@ -135,12 +163,15 @@ class AllocJournal:
             self._write({"k": key, "uid": pod_uid, "t": t, "resp": base64.b64encode(blob).decode()})
 
     def lookup(self, req, key: str | None = None) -> tuple[str, object] | None:
+        """(pod uid, the journaled answer) for this request's fake-ID set, or None. The answer
+        is returned as a zero-argument callable: parsing it is only worth it on a replay."""
         key = key or request_key(req)
         with self._lock:
             hit = self._mem.get(key)
         if hit is None or time.time() - hit[1] > self.ttl_s:
             return None
-        return hit[0], api.AllocateResponse.FromString(hit[2])
+        blob = hit[2]
+        return hit[0], lambda: api.AllocateResponse.FromString(blob)
 
     def answered(self, uid: str) -> bool:
         """This plugin (or a previous instance, via the file) answered an Allocate for ``uid``
@@ -194,9 +225,9 @@ class AllocJournal:
 
     def close(self):
         with self._lock:
-            if self._fd >= 0:
-                os.close(self._fd)
-                self._fd = -1
+            if self._mm is not None:
+                self._mm.close()
+                self._mm = None
 
     def __len__(self):
         return len(self._mem)

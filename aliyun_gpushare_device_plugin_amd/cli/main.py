@@ -140,7 +140,7 @@ def main(argv=None) -> int:
     # pod being admitted: with CPython's default 5 ms GIL switch interval the handler can sit
     # behind a whole decode. A 0.25 ms interval bounds that wait (the kubelet blocks on it).
     sys.setswitchinterval(float(os.environ.get("GPUSHARE_SWITCH_INTERVAL", "0.00025")))
-    log.setup(verbosity=a.v, json_lines=a.log_json)
+    log.setup(verbosity=a.v, json_lines=a.log_json, buffered=os.environ.get("GPUSHARE_LOG_UNBUFFERED") != "1")
     log.V(1).info("Start gpushare device plugin")
     cfg = config_from_args(a)
     if a.install_shim:

@@ -40,6 +40,10 @@ class PodSource:
     def observe(self, pod: dict) -> None:
         """Feed back an object we wrote (PATCH response)."""
 
+    def get(self, uid: str) -> dict | None:
+        """This node's live pod with ``uid`` (O(1) in the watch cache; a scan elsewhere)."""
+        return next((p for p in self.node_pods() if O.uid(p) == uid), None)
+
     def start(self):
         return self
 
@@ -109,6 +113,7 @@ class WatchCache(PodSource):
         self.watch_timeout = watch_timeout
         self.on_event = on_event
         self._pods: dict[str, dict] = {}
+        self._pending: dict[str, dict] = {}     # the Pending subset, so Allocate never scans Running pods
         self._lock = threading.Lock()
         self._synced = threading.Event()
         self._stop = threading.Event()
@@ -135,6 +140,7 @@ class WatchCache(PodSource):
         items, rv = self.client.list_pods(field_selector=node_field_selector(self.node))
         with self._lock:
             self._pods = {O.uid(p): p for p in items}
+            self._pending = {u: p for u, p in self._pods.items() if O.phase(p) == "Pending"}
             self._rv = rv
         self.relists += 1
         self._synced.set()
@@ -151,10 +157,11 @@ class WatchCache(PodSource):
         with self._lock:
             if typ == "DELETED" or O.node_name(obj) != self.node:
                 self._pods.pop(u, None)
+                self._pending.pop(u, None)
             else:
                 cur = self._pods.get(u)
                 if cur is None or O.rv_int(O.resource_version(obj)) >= O.rv_int(O.resource_version(cur)):
-                    self._pods[u] = obj
+                    self._put(u, obj)
             self._rv = O.resource_version(obj) or self._rv
         self.events += 1
         if self.on_event:
@@ -193,7 +200,14 @@ class WatchCache(PodSource):
                 self.observe(p)
             return items
         with self._lock:
-            return [p for p in self._pods.values() if O.phase(p) == "Pending"]
+            return list(self._pending.values())
+
+    def _put(self, u: str, pod: dict) -> None:
+        self._pods[u] = pod
+        if O.phase(pod) == "Pending":
+            self._pending[u] = pod
+        else:
+            self._pending.pop(u, None)
 
     def observe(self, pod: dict) -> None:
         if not pod or O.node_name(pod) != self.node:
@@ -202,7 +216,14 @@ class WatchCache(PodSource):
         with self._lock:
             cur = self._pods.get(u)
             if cur is None or O.rv_int(O.resource_version(pod)) >= O.rv_int(O.resource_version(cur)):
-                self._pods[u] = pod
+                self._put(u, pod)
+
+    def get(self, uid: str) -> dict | None:
+        if not self._synced.is_set():
+            return super().get(uid)
+        with self._lock:
+            p = self._pods.get(uid)
+        return None if p is None or O.is_terminated(p) else p
 
     def node_pods(self) -> list[dict]:
         if not self._synced.is_set():

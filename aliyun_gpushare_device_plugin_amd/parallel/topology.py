@@ -72,6 +72,22 @@ def best_group(topo: dict | None, free: list[int], size: int, request: int,
     return best
 
 
+def verdict(topo: dict | None, n: int, healthy: list | None = None) -> tuple[bool, list[str]]:
+    """Pass/fail of the topology the plugin exported for an ``n``-GPU node: present, ``n × n``,
+    and — on a healthy UBB (every GPU healthy) — every pair one-hop xGMI. Returns (ok, reasons)."""
+    why = []
+    lt = (topo or {}).get("link_type")
+    if not lt:
+        return False, ["no xGMI topology annotation on the node"]
+    if len(lt) != n or any(len(r) != n for r in lt) or len((topo or {}).get("hops") or []) != n:
+        return False, [f"topology matrix is {len(lt)}x{len(lt[0]) if lt else 0}, expected {n}x{n}"]
+    if healthy is None or all(healthy):
+        bad = [(a, b, lt[a][b], topo["hops"][a][b]) for a, b in itertools.combinations(range(n), 2)
+               if not xgmi_connected(topo, a, b)]
+        why += [f"GPU pair {a}-{b}: {t}, {h} hop(s) (healthy UBB: one-hop xGMI expected)" for a, b, t, h in bad]
+    return not why, why
+
+
 def bench_report(rank: int, world: int, use_gpu: bool, topo: dict | None, device=None, mib: int = 256,
                  iters: int = 10) -> dict | None:
     """Multi-GPU bench section (collective: every rank calls it). Rank 0 brings the topology

@@ -31,6 +31,7 @@ import json
 import os
 import shutil
 import struct
+import threading
 import time
 
 MAGIC = 0x67707573686172          # "gpushar"
@@ -87,45 +88,129 @@ def uid_key(pod_uid: str) -> str:
 
 
 class LedgerDir:
-    """The plugin's side of ``<root>``: per-container directories and their owner records."""
+    """The plugin's side of ``<root>``: per-container directories and their owner records.
 
-    def __init__(self, root: str):
+    Directory creation costs a few filesystem syscalls (≈0.1-1 ms on an overlay root), too
+    much for the Allocate path, so ``take`` hands out a directory made ahead of time by a
+    background thread (a *pool* entry: owner record ``{"pods": [], "pool": true}``, which the
+    garbage collector leaves alone) and its owner record is written behind the answer. A pool
+    left by a previous plugin instance is adopted on ``prepare``."""
+
+    def __init__(self, root: str, pool_size: int = 32):
         self.root = root
         self._owners = os.path.join(root, OWNERS)
+        self.pool_size = pool_size
+        self._pool: list[str] = []
+        self._pending: list[tuple[str, list]] = []     # owner records to write behind
+        self._cv = threading.Condition()
+        self._thread = None
 
     def prepare(self) -> None:
         os.makedirs(self._owners, exist_ok=True)
         os.chmod(self.root, 0o755)        # tenants never see the root, only their own subdir
         os.chmod(self._owners, 0o700)
+        for lkey in self.keys():
+            rec = self._record(lkey)
+            if rec.get("pool") and not rec.get("pods"):
+                self._pool.append(lkey)
 
-    def new_key(self, pod_uid: str, slot: int) -> str:
-        return f"{uid_key(pod_uid)[:32]}-{slot}-{os.urandom(4).hex()}"
+    def start(self) -> "LedgerDir":
+        """Background pool refill + owner-record writer."""
+        if self._thread is None:
+            self._thread = threading.Thread(target=self._run, name="ledger-pool", daemon=True)
+            self._thread.start()
+        return self
 
-    def create(self, lkey: str, owner_uid: str) -> str:
-        """Create ``<root>/<lkey>`` (writable by any container uid) and its owner record;
-        returns the host path to mount."""
+    def _run(self):
+        while True:
+            with self._cv:
+                while not self._pending and len(self._pool) >= self.pool_size:
+                    self._cv.wait()
+                todo, self._pending = self._pending, []
+                short = self.pool_size - len(self._pool)
+            for lkey, pods in todo:
+                try:
+                    self._write_owners(lkey, pods)
+                except OSError:
+                    pass
+            for _ in range(max(0, short)):
+                lkey = self.new_key()
+                try:
+                    self._mkdir(lkey)
+                    self._write_owners(lkey, [], pool=True)
+                except OSError:
+                    break
+                with self._cv:
+                    self._pool.append(lkey)
+
+    def new_key(self, pod_uid: str = "", slot: int | None = None) -> str:
+        head = f"{uid_key(pod_uid)[:32]}-{slot}-" if pod_uid else "c-"
+        return head + os.urandom(6).hex()
+
+    def _mkdir(self, lkey: str) -> str:
         path = os.path.join(self.root, lkey)
         os.makedirs(path, exist_ok=True)
-        os.chmod(path, 0o777)
+        os.chmod(path, 0o777)             # containers may run as any uid; only one sees it
+        return path
+
+    def take(self, owner_uid: str) -> str:
+        """A fresh per-container directory for ``owner_uid``'s container: its key. Pool hit =
+        no syscall on the caller's path; the owner record follows on the background thread."""
+        with self._cv:
+            lkey = self._pool.pop() if self._pool else None
+            if lkey is not None:
+                self._pending.append((lkey, [owner_uid] if owner_uid else []))
+                self._cv.notify()
+                return lkey
+        lkey = self.new_key(owner_uid, 0)
+        self.create(lkey, owner_uid)
+        with self._cv:
+            self._cv.notify()
+        return lkey
+
+    def path(self, lkey: str) -> str:
+        return os.path.join(self.root, lkey)
+
+    def create(self, lkey: str, owner_uid: str) -> str:
+        """Create ``<root>/<lkey>`` (writable by any container uid) and its owner record now;
+        returns the host path to mount."""
+        path = self._mkdir(lkey)
         self._write_owners(lkey, [owner_uid] if owner_uid else [])
         return path
 
-    def _write_owners(self, lkey: str, pods: list) -> None:
+    def _write_owners(self, lkey: str, pods: list, pool: bool = False) -> None:
         tmp = os.path.join(self._owners, f".{lkey}.tmp")
+        rec = {"pods": pods, "t": time.time()}
+        if pool:
+            rec["pool"] = True
         with open(tmp, "w") as f:
-            json.dump({"pods": pods, "t": time.time()}, f)
+            json.dump(rec, f)
         os.replace(tmp, os.path.join(self._owners, lkey))
 
-    def owners(self, lkey: str) -> tuple[list, float]:
+    def _record(self, lkey: str) -> dict:
         try:
             with open(os.path.join(self._owners, lkey)) as f:
-                d = json.load(f)
-            return list(d.get("pods") or []), float(d.get("t") or 0.0)
+                return json.load(f)
         except (OSError, ValueError):
-            return [], 0.0
+            return {}
+
+    def owners(self, lkey: str) -> tuple[list, float]:
+        d = self._record(lkey)
+        return list(d.get("pods") or []), float(d.get("t") or 0.0)
+
+    def flush(self, timeout: float = 5.0) -> bool:
+        """Wait until the queued owner records are written (tests, shutdown)."""
+        t = time.monotonic() + timeout
+        while time.monotonic() < t:
+            with self._cv:
+                if not self._pending:
+                    return True
+            time.sleep(0.005)
+        return False
 
     def add_owner(self, lkey: str, uid: str) -> None:
         """Placement truth: ``uid``'s container holds the grant this ledger was made for."""
+        self.flush()
         pods, _ = self.owners(lkey)
         if uid and uid not in pods:
             self._write_owners(lkey, pods + [uid])
@@ -184,7 +269,10 @@ def collect(directory: str, metrics, live_uids: set[str] | None = None, gc: bool
     removed: set[str] = set()
     holder: dict[str, str] = {}
     for lkey in ld.keys():
-        pods, t = ld.owners(lkey)
+        rec = ld._record(lkey)
+        if rec.get("pool") and not rec.get("pods"):
+            continue                            # made ahead, not handed out yet
+        pods, t = list(rec.get("pods") or []), float(rec.get("t") or 0.0)
         alive = [u for u in pods if live_uids is None or u in live_uids]
         if alive:
             holder[lkey] = uid_key(alive[-1])   # the latest owner: the pod really running it

@@ -59,11 +59,14 @@ class SimCluster:
                  gpu_indices: list[int] | None = None, health_poll_s: float = 1.0, round_policy: str = "nearest",
                  extra_plugin_args: list[str] | None = None, apiserver: str = "thread",
                  preferred_allocation: bool = False, compute_isolation: str = "none", kubelet: str = "thread",
-                 placement_truth: bool = True):
+                 placement_truth: bool = True, node_overrides: dict | None = None):
         self.node_specs = nodes
         # kubelet: "thread" (FakeKubelet in this interpreter) or "process" (its own interpreter,
         # sim/kubelet_proc.py, so kubelet-side Allocate timing is not inflated by this process's GIL)
         self.kubelet_mode = kubelet
+        # per-node plugin settings: {node: {"pod_source": ..., "extra_args": [...]}} (e.g. a second
+        # node running the reference's cost model next to the default one, bench.py)
+        self.node_overrides = node_overrides or {}
         # the fake kubelet serves pod-resources; the plugin uses it for placement truth
         self.placement_truth = placement_truth
         self.compute_isolation = compute_isolation
@@ -140,9 +143,12 @@ class SimCluster:
         self.extender.sync()
         return self
 
+    def _pod_source(self, node: SimNode) -> str:
+        return self.node_overrides.get(node.name, {}).get("pod_source", self.pod_source)
+
     def _plugin_cfg(self, node: SimNode) -> PluginConfig:
         return PluginConfig(node_name=node.name, smi_backend=node.smi_spec, device_plugin_dir=node.plugin_dir,
-                            apiserver=self.api_url, pod_source=self.pod_source,
+                            apiserver=self.api_url, pod_source=self._pod_source(node),
                             shim_host_dir=self.shim_host_dir, gpu_indices=self.gpu_indices,
                             health_poll_s=self.health_poll_s, round_policy=self.round_policy,
                             preferred_allocation=self.preferred_allocation,
@@ -163,7 +169,7 @@ class SimCluster:
             args = [sys.executable, "-m", "aliyun_gpushare_device_plugin_amd.cli.main",
                     "--node-name", node.name, "--smi-backend", node.smi_spec,
                     "--device-plugin-dir", node.plugin_dir, "--apiserver", self.api_url,
-                    "--pod-source", self.pod_source, "--round", self.round_policy,
+                    "--pod-source", self._pod_source(node), "--round", self.round_policy,
                     "--health-poll", str(self.health_poll_s)]
             if self.shim_host_dir:
                 args += ["--shim-path", self.shim_host_dir]
@@ -176,7 +182,8 @@ class SimCluster:
             args += ["--pod-resources-socket", self._podres(node)]
             for k, v in self._kubelet_cfg(node).items():
                 args += ["--" + k.replace("_", "-"), str(v)]
-            args += self.extra_plugin_args
+            ov = self.node_overrides.get(node.name, {})
+            args += ov["extra_args"] if "extra_args" in ov else self.extra_plugin_args
             node.proc = subprocess.Popen(args, env=self._child_env(), stdout=subprocess.DEVNULL, preexec_fn=_die_with_parent,
                                          stderr=open(os.path.join(self.workdir, f"{node.name}.plugin.log"), "w"))
         else:
@@ -250,8 +257,8 @@ class SimCluster:
         return self.client.create_pod("default", pod_spec(name or f"pod-{next(self._seq)}", gpu_mem, labels=labels,
                                                           annotations=annotations))
 
-    def schedule(self, pod: dict):
-        return self.extender.schedule(pod)
+    def schedule(self, pod: dict, node_names: list | None = None):
+        return self.extender.schedule(pod, node_names)
 
     def admit(self, pod: dict, async_status: bool = False) -> Admission:
         """Kubelet admission. ``pod`` may be the bound object the caller already holds (the
@@ -283,9 +290,9 @@ class SimCluster:
         self._bg.submit(lambda: None).result()
 
     def run_pod(self, gpu_mem, name: str | None = None, labels: dict | None = None,
-                annotations: dict | None = None):
+                annotations: dict | None = None, node_names: list | None = None):
         pod = self.create_pod(gpu_mem, name, labels, annotations)
-        placed = self.schedule(pod)
+        placed = self.schedule(pod, node_names)
         if placed is None:
             return pod, None, None
         return pod, placed, self.admit(pod)

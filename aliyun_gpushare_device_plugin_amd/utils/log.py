@@ -52,17 +52,67 @@ def _emit(levelno: int, msg, args, fields, depth: int = 2) -> None:
         if _sec_cache[0] != sec:
             _sec_cache[0], _sec_cache[1] = sec, time.strftime("%m%d %H:%M:%S", time.localtime(sec))
         line = f"{code}{_sec_cache[1]}.{int((now - sec) * 1e6):06d} {_pid:>7} {src}] {msg}"
-    st = _stream or sys.stderr
     with _lock:
-        try:
-            st.write(line + "\n")
-            st.flush()
-        except (OSError, ValueError):
-            pass
+        if _flusher is not None and levelno < logging.WARNING:
+            # buffered INFO (like glog's): no write(2) on the caller's path — a syscall there
+            # hands the GIL to whichever thread is busy (Allocate's latency); the flusher
+            # thread writes within _FLUSH_S, and WARNING+ flushes everything at once
+            _buf.append(line)
+            _buf_bytes[0] += len(line)
+            if _buf_bytes[0] < _BUF_MAX:
+                return
+        else:
+            _buf.append(line)
+        _flush_locked()
 
 
-def setup(verbosity: int | None = None, json_lines: bool | None = None, stream=None) -> None:
-    global _VERBOSITY, _JSON, _stream, _pid
+_buf: list[str] = []
+_buf_bytes = [0]
+_BUF_MAX = 1 << 16
+_FLUSH_S = 0.05
+_flusher = None
+
+
+def _flush_locked() -> None:
+    if not _buf:
+        return
+    st = _stream or sys.stderr
+    data = "\n".join(_buf) + "\n"
+    _buf.clear()
+    _buf_bytes[0] = 0
+    try:
+        st.write(data)
+        st.flush()
+    except (OSError, ValueError):
+        pass
+
+
+def flush() -> None:
+    with _lock:
+        _flush_locked()
+
+
+def _flush_loop(stop: threading.Event) -> None:
+    while not stop.wait(_FLUSH_S):
+        flush()
+    flush()
+
+
+def setup(verbosity: int | None = None, json_lines: bool | None = None, stream=None,
+          buffered: bool | None = None) -> None:
+    """``buffered``: INFO lines are written by a background thread every 50 ms (WARNING and
+    above, and process exit, flush at once) — the plugin daemon turns it on."""
+    global _VERBOSITY, _JSON, _stream, _pid, _flusher
+    if buffered and _flusher is None:
+        import atexit
+
+        stop = threading.Event()
+        _flusher = threading.Thread(target=_flush_loop, args=(stop,), name="log-flush", daemon=True)
+        _flusher.start()
+        atexit.register(lambda: (stop.set(), flush()))
+    elif buffered is False and _flusher is not None:
+        flush()
+        _flusher = None
     with _lock:
         if verbosity is not None:
             _VERBOSITY = int(verbosity)

@@ -49,6 +49,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "bin-packed pods + HBM-GiB/node; Allocate p50 latency at 1/2/4/8 MI355X"
+MAIN_NODE, REF_NODE = "mi355x-node", "ref-node"
 # Per-GPU pod sizes (GiB), each pattern sums to one MI355X (288 GiB); GPU g uses pattern g % 4.
 PATTERNS = [[128, 64, 64, 32], [96, 96, 64, 32], [128, 96, 56, 8], [64, 64, 96, 64]]
 NATIVE = os.path.join(ROOT, "aliyun_gpushare_device_plugin_amd", "_native")
@@ -69,6 +70,10 @@ def parse():
     ap.add_argument("--plugin-mode", default="process", choices=("process", "thread"))
     ap.add_argument("--compare-rtts", default="0,1,5", help="apiserver RTTs (ms) of the control-plane A/B ('' = off)")
     ap.add_argument("--compare-pods", type=int, default=24, help="admissions per A/B configuration")
+    ap.add_argument("--no-ref-churn", action="store_true",
+                    help="skip the reference-model node churned in lock-step with the real one")
+    ap.add_argument("--fill-orders", default="grouped,random,size_desc,size_asc",
+                    help="bin-pack stress: arrival orders of the node's mixed pods through the extender ('' = off)")
     ap.add_argument("--room-slack-gib", type=float, default=2.0,
                     help="free HBM beyond a pod's state required before it allocates")
     ap.add_argument("--json-out", default=None)
@@ -129,7 +134,7 @@ class ControlPlane:
     """Rank 0's view of the node: fake cluster + the real plugin process."""
 
     def __init__(self, n_gpus: int, smi_spec: str, pod_source: str, plugin_mode: str, workdir: str,
-                 with_shim: bool):
+                 with_shim: bool, ref_spec: str | None = None):
         from aliyun_gpushare_device_plugin_amd.sim.cluster import SimCluster
 
         self.n = n_gpus
@@ -140,14 +145,26 @@ class ControlPlane:
         extra += ["--ledger-dir", self.ledger_dir, "--journal-path", os.path.join(workdir, "alloc-journal.jsonl")]
         if with_shim:
             extra += ["--rocr-visible-devices"]
-        self.cluster = SimCluster([("mi355x-node", smi_spec)], plugin_mode=plugin_mode, pod_source=pod_source,
+        nodes = [(MAIN_NODE, smi_spec)]
+        overrides = {}
+        # the reference's cost model (LIST per Allocate + synchronous PATCH, allocate.go:63-152)
+        # on a second, modelled node of the same shape, churned in lock-step with the real one so
+        # both plugins are measured under the same pod load (control plane only: no processes)
+        self.ref_port = None
+        if ref_spec and plugin_mode == "process":
+            self.ref_port = free_port()
+            nodes.append((REF_NODE, ref_spec))
+            overrides[REF_NODE] = {"pod_source": "list", "extra_args": [
+                "--sync-patch", "--metrics-addr", f"127.0.0.1:{self.ref_port}", "--pod-resources-socket", "none"]}
+        self.cluster = SimCluster(nodes, plugin_mode=plugin_mode, pod_source=pod_source,
                                   apiserver="process", kubelet="process", gpu_indices=list(range(n_gpus)), health_poll_s=5.0,
-                                  extra_plugin_args=extra, shim_host_dir=NATIVE if with_shim else None)
+                                  extra_plugin_args=extra, shim_host_dir=NATIVE if with_shim else None,
+                                  node_overrides=overrides)
         self.cluster.start()
         from aliyun_gpushare_device_plugin_amd import const
         from aliyun_gpushare_device_plugin_amd.cluster import objects as O
 
-        node = self.cluster.client.get_node("mi355x-node")
+        node = self.cluster.client.get_node(MAIN_NODE)
         self.gpu_count = O.node_allocatable(node, const.RESOURCE_COUNT)
         self.units_per_gpu = O.node_allocatable(node, const.RESOURCE_NAME) // max(1, self.gpu_count)
         if self.gpu_count != n_gpus:
@@ -159,6 +176,10 @@ class ControlPlane:
         self._sched_lock = threading.Lock()
         self._kubelet = threading.Condition()
         self.alloc_lat: list[float] = []
+        self.alloc_lat_by_gpu: dict[int, list] = {g: [] for g in range(n_gpus)}
+        self.ref_resident: dict[int, list] = {g: [] for g in range(n_gpus)}
+        self.ref_lat: list[float] = []
+        self.ref_failed = 0
         self.admit_lat: list[float] = []
         self.failed = 0
         self.fail_reasons: list[str] = []
@@ -181,14 +202,45 @@ class ControlPlane:
         started: dict[int, list] = {g: [] for g in range(self.n)}
         for g in range(self.n):
             for s in PATTERNS[g % len(PATTERNS)]:
-                pod, where, adm = self.cluster.run_pod(s)
+                pod, where, adm = self.cluster.run_pod(s, node_names=[MAIN_NODE])
                 if where is None or adm is None or adm.error:
                     self.failed += 1
                     continue
                 rec = self._record(pod, s, adm)
                 if rec:
                     started[rec[0]].append(rec[1])
+                if self.ref_port:
+                    rpod, rwhere, radm = self.cluster.run_pod(s, node_names=[REF_NODE])
+                    if rwhere is not None and radm is not None and not radm.error:
+                        rg = int(dict(radm.responses[0].envs)["ALIYUN_COM_GPU_MEM_IDX"])
+                        if rg >= 0:
+                            self.ref_resident[rg].append((rpod, s))
         return started
+
+    def _mirror(self, gpu: int, size: int) -> None:
+        """The same churn step on the reference-model node: retire its oldest ``size`` pod
+        (preferring GPU ``gpu``) and admit a same-size replacement through its plugin."""
+        cands = [(g, i) for g in [gpu] + [x for x in range(self.n) if x != gpu]
+                 for i, (_, sz) in enumerate(self.ref_resident[g]) if sz == size]
+        if not cands:
+            return
+        g, i = cands[0]
+        old, _ = self.ref_resident[g].pop(i)
+        self.cluster.delete_pod(old)
+        pod = self.cluster.create_pod(size)
+        where = self.cluster.extender.decide(pod, [REF_NODE])
+        bpod = self.cluster.extender.commit(pod, where, time.time_ns()) if where else None
+        if bpod is None:
+            self.ref_failed += 1
+            return
+        adm = self.cluster.admit(bpod, async_status=True)
+        rg = int(dict(adm.responses[0].envs)["ALIYUN_COM_GPU_MEM_IDX"]) if adm.error is None and adm.responses else -1
+        if rg < 0:
+            self.ref_failed += 1
+            self.cluster.delete_pod(bpod)
+            return
+        self.ref_lat.extend(adm.latencies)
+        self.ref_resident[rg].append((bpod, size))
 
     def churn_one(self, gpu: int, uid: str | None = None) -> tuple[int, dict] | None:
         """Retire pod ``uid`` (default: the oldest) of ``gpu`` and admit a same-size replacement
@@ -207,7 +259,7 @@ class ControlPlane:
         tc = time.perf_counter()
         self.cluster.delete_pod(old)
         pod = self.cluster.create_pod(size)
-        where = self.cluster.extender.decide(pod)
+        where = self.cluster.extender.decide(pod, [MAIN_NODE])
         bpod = self.cluster.extender.commit(pod, where, time.time_ns()) if where else None
         if bpod is None:
             self.failed += 1
@@ -225,7 +277,10 @@ class ControlPlane:
             self.cluster.delete_pod(bpod)
             return None
         self.alloc_lat.extend(adm.latencies)
+        self.alloc_lat_by_gpu[rec[0]].extend(adm.latencies)
         self.admit_lat.append(dt)
+        if self.ref_port:
+            self._mirror(gpu, size)          # alternating admissions, same pod load
         return rec
 
     def plugin_latency(self, reset: bool = False) -> dict | None:
@@ -274,6 +329,46 @@ def mode_comparison(rtts_ms: list[float], n_pods: int) -> dict:
                         "plugin_allocate_p50_ms": ms(srv.get("p50")), "plugin_allocate_p99_ms": ms(srv.get("p99")),
                         "apiserver_round_trips_on_path": 2 if extra else 0, "request_ms": ms(pct(req, 0.5)),
                         "pod_source": src, "patch": "sync" if extra else "write-behind", "failed": fails}
+    return out
+
+
+def fill_orders(orders: list[str], n_gpus: int, units: int, seed: int = 0) -> dict:
+    """Bin-pack stress (BASELINE config 3, control plane only): the node's 4·N mixed pods
+    (``PATTERNS``, 8-128 GiB, summing to exactly the node's HBM) arrive in a given order
+    through the extender's online best fit and the plugin's Allocate. ``grouped`` = per-GPU
+    groups (the churn's fill: packs by construction); ``random`` = one seeded shuffle;
+    ``size_desc`` / ``size_asc`` = sorted. Reports pods and GiB placed, the node's HBM left
+    stranded when a pod could not be placed, and failed placements."""
+    import random
+
+    from aliyun_gpushare_device_plugin_amd.sim.cluster import SimCluster
+
+    sizes = [s for g in range(n_gpus) for s in PATTERNS[g % len(PATTERNS)]]
+    out = {}
+    for order in orders:
+        seq = list(sizes)
+        if order == "random":
+            random.Random(seed).shuffle(seq)
+        elif order == "size_desc":
+            seq.sort(reverse=True)
+        elif order == "size_asc":
+            seq.sort()
+        placed, failed, admit_fail = [], 0, 0
+        with SimCluster([("fill", f"fake:{n_gpus}x288G")], plugin_mode="thread", apiserver="thread",
+                        kubelet="thread") as c:
+            for sz in seq:
+                pod, where, adm = c.run_pod(sz)
+                if where is None:
+                    failed += 1
+                elif adm is None or adm.error or int(dict(adm.responses[0].envs)["ALIYUN_COM_GPU_MEM_IDX"]) < 0:
+                    admit_fail += 1
+                else:
+                    placed.append(sz)
+        gib = sum(placed)
+        out[order] = {"pods_placed": len(placed), "pods_total": len(seq), "gib_placed": gib,
+                      "packing_efficiency": round(gib / (units * n_gpus), 4) if units else None,
+                      "stranded_gib": units * n_gpus - gib if failed or admit_fail else 0,
+                      "failed_placements": failed, "failed_admissions": admit_fail}
     return out
 
 
@@ -554,19 +649,23 @@ def main():
     info = None
     workdir = tempfile.mkdtemp(prefix="gs-bench-", dir="/tmp")
     if rank == 0:
+        ref_spec = smi if smi.startswith("fake:") else None
         if use_gpu and smi == "auto":
             from aliyun_gpushare_device_plugin_amd.device.smi import SMI
             with SMI("auto") as s:
+                ref_spec = f"fake:{n}x{s.device(0).vram_total}B"
                 if s.count() < n:          # fewer visible GPUs than ranks: model the node
-                    smi = f"fake:{n}x{s.device(0).vram_total}B"
+                    smi = ref_spec
                     visible_by_uuid = False
-        cp = ControlPlane(n, smi, a.pod_source, a.plugin_mode, workdir, with_shim=use_gpu)
+        cp = ControlPlane(n, smi, a.pod_source, a.plugin_mode, workdir, with_shim=use_gpu,
+                          ref_spec=None if a.no_ref_churn else ref_spec)
         info = {"units_per_gpu": cp.units_per_gpu, "gpu_count": cp.gpu_count, "by_uuid": visible_by_uuid}
     info = bcast(info)
     units = info["units_per_gpu"]
     fleet = PodFleet(local, a.gemm, a.burst, a.fill, info["by_uuid"], a.standby,
                      slack=int(a.room_slack_gib * (1 << 30))) if use_gpu else None
     topo_report = None
+    topo_failed = False
 
     def launch(started: dict) -> float:
         """Start this rank's newly admitted pods; returns the slowest ready latency."""
@@ -607,11 +706,17 @@ def main():
     barrier()
     if rank == 0:
         cp.alloc_lat.clear()
+        for v in cp.alloc_lat_by_gpu.values():
+            v.clear()
         cp.admit_lat.clear()
+        cp.ref_lat.clear()
+        cp.ref_failed = 0
         cp.cp_time = 0.0
         cp.failed = 0
         cp.fail_reasons.clear()
         cp.plugin_latency(reset=True)
+        if cp.ref_port:
+            plugin_latency(cp.ref_port, reset=True)
     if fleet is not None:
         fleet.ready_ms.clear()
         fleet.release_ms.clear()
@@ -654,19 +759,47 @@ def main():
         from aliyun_gpushare_device_plugin_amd.cluster import nodestatus
         from aliyun_gpushare_device_plugin_amd.parallel import topology as T
 
-        topo = nodestatus.read_topology(cp.cluster.client.get_node("mi355x-node")) if rank == 0 else None
+        topo = healthy = None
+        if rank == 0:
+            node = cp.cluster.client.get_node(MAIN_NODE)
+            topo = nodestatus.read_topology(node)
+            hmap = json.loads((node.get("metadata", {}).get("annotations") or {}).get(
+                "gpushare.amd.com/gpu-health", "{}") or "{}")
+            healthy = [bool((hmap.get(str(i)) or {}).get("healthy", True)) for i in range(n)]
         topo_report = T.bench_report(rank, world, use_gpu, topo, dev)
+        if rank == 0:
+            ok, why = T.verdict(topo, n, healthy)
+            topo_report["verdict"] = "pass" if ok else "fail"
+            topo_report["reasons"] = why
+            topo_failed = not ok
 
     if rank == 0:
         srv = cp.plugin_latency()
+        ref_srv = plugin_latency(cp.ref_port) if cp.ref_port else None
         pods_node = sum(len(v) for v in cp.resident.values())
         gib_node = sum(s for v in cp.resident.values() for _, s in v)
         admissions = a.steps * n - cp.failed
         value = admissions / elapsed
+        under_churn = {"default": {
+            "allocate_p50_ms": ms(pct(cp.alloc_lat, 0.5)), "allocate_p99_ms": ms(pct(cp.alloc_lat, 0.99)),
+            "plugin_allocate_p50_ms": ms(srv["p50"]) if srv else None,
+            "plugin_allocate_p99_ms": ms(srv["p99"]) if srv else None,
+            "admissions": len(cp.alloc_lat), "pod_source": a.pod_source, "patch": "write-behind",
+            "apiserver_round_trips_on_path": 0}}
+        if cp.ref_port:
+            under_churn["reference"] = {
+                "allocate_p50_ms": ms(pct(cp.ref_lat, 0.5)), "allocate_p99_ms": ms(pct(cp.ref_lat, 0.99)),
+                "plugin_allocate_p50_ms": ms(ref_srv["p50"]) if ref_srv else None,
+                "plugin_allocate_p99_ms": ms(ref_srv["p99"]) if ref_srv else None,
+                "plugin_allocate_phase_p50_ms": {k: ms(v) for k, v in ref_srv["phases"].items() if v is not None}
+                if ref_srv else None,
+                "admissions": len(cp.ref_lat), "failed": cp.ref_failed, "pod_source": "list", "patch": "sync",
+                "apiserver_round_trips_on_path": 2}
         svc.stop()
         cp.stop()
         modes = mode_comparison([float(x) for x in a.compare_rtts.split(",") if x], a.compare_pods) \
             if a.compare_rtts else {}
+        fills = fill_orders([x for x in a.fill_orders.split(",") if x], n, units) if a.fill_orders else {}
         res = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -700,7 +833,12 @@ def main():
             # (init) -> physical room for its state (room) -> state allocated + first GEMM (alloc)
             "pod_phase_p50_ms": {k: ms(pct(v, 0.5)) for k, v in phases.items()},
             "control_plane_ms_per_admission": round(cp.cp_time / max(1, a.steps * n) * 1e3, 3),
+            "allocate_p50_ms_by_gpu": {str(g): ms(pct(v, 0.5)) for g, v in cp.alloc_lat_by_gpu.items()},
+            # both plugins during the same timed churn (alternating admissions, same pod load)
+            "allocate_under_churn": under_churn,
+            # the same A/B on a quiet cluster at injected apiserver RTTs
             "allocate_by_mode": modes,
+            "fill_orders": fills,
             "pods_per_node": pods_node,
             "hbm_gib_per_node": gib_node,
             "advertised_gib_per_node": units * n,
@@ -732,6 +870,10 @@ def main():
     import shutil
 
     shutil.rmtree(workdir, ignore_errors=True)
+    if topo_failed:
+        # a broken topology export must not pass as a successful multi-GPU run
+        sys.stderr.write("bench: topology verdict FAIL: " + "; ".join(topo_report["reasons"]) + "\n")
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -118,11 +118,12 @@ def test_rebuild_keeps_inflight_claims(tmp_path):
         _, where_a, adm_a = c.run_pod(3, name="a")
         c.client.patch_pod_status("default", "a", {"status": {"phase": "Pending"}})
         before = m.allocator
+        c.nodes["n"].kubelet.registered.clear()      # wait for the *re*-registration below
         m.events.put(("signal", __import__("signal").SIGHUP))
         t = time.monotonic() + 10
         while m.restarts == 0 and time.monotonic() < t:
             time.sleep(0.01)
-        c.nodes["n"].kubelet.registered.wait(10)
+        assert c.nodes["n"].kubelet.registered.wait(10)
         assert m.allocator is before
         _, where_b, adm_b = c.run_pod(3, name="b")
         assert idx(adm_b) == where_b[1] != idx(adm_a)
@@ -130,3 +131,30 @@ def test_rebuild_keeps_inflight_claims(tmp_path):
         for name in ("a", "b"):
             got = c.wait_assigned({"metadata": {"namespace": "default", "name": name}}, timeout=10)
             assert O.annotations(got)[const.ENV_ASSIGNED_FLAG] == "true"
+
+
+def test_mapped_journal_reload_and_compaction(tmp_path):
+    """The journal is a MAP_SHARED file with a zero tail: records written by one instance are
+    read back by the next (no close, as after a SIGKILL), and a full mapping compacts into a
+    fresh file that keeps every live answer and unlanded patch."""
+    from aliyun_gpushare_device_plugin_amd.alloc.journal import AllocJournal
+    from aliyun_gpushare_device_plugin_amd.api import v1beta1 as api
+
+    path = str(tmp_path / "j.jsonl")
+    j = AllocJournal(path, map_bytes=4096)
+    resp = api.AllocateResponse()
+    resp.container_responses.add(envs={"ALIYUN_COM_GPU_MEM_IDX": "1"})
+    for i in range(40):                                   # ~4x the mapping: several compactions
+        req = api.AllocateRequest(container_requests=[api.ContainerAllocateRequest(devices_ids=[f"d{i}"])])
+        j.record_pending(req, f"u{i}", resp, "default", f"p{i}", {"a": "b"})
+        if i % 2:
+            j.landed(f"u{i}")
+    with open(path, "rb") as f:
+        raw = f.read()
+    assert raw.rstrip(b"\0").endswith(b"\n") and len(raw) >= 4096
+    j2 = AllocJournal(path)                               # no close(): the writer was "killed"
+    assert sorted(e["uid"] for e in j2.unlanded()) == sorted(f"u{i}" for i in range(0, 40, 2))
+    assert all(j2.answered(f"u{i}") for i in range(40))
+    req = api.AllocateRequest(container_requests=[api.ContainerAllocateRequest(devices_ids=["d7"])])
+    uid, got = j2.lookup(req)
+    assert uid == "u7" and got().container_responses[0].envs["ALIYUN_COM_GPU_MEM_IDX"] == "1"
