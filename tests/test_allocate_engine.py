@@ -390,6 +390,7 @@ def test_ledger_dir_mount_and_env(tmp_path):
     assert rp.envs[const.ENV_SHIM_LEDGER_DIR] == const.LEDGER_CONTAINER_DIR
     assert oct(os.stat(root).st_mode & 0o7777) == "0o755"
     assert oct(os.stat(hp).st_mode & 0o777) == "0o777"
+    assert al._ledgers.flush()                   # owner records are written behind the answer
     ld = L.LedgerDir(str(root))
     assert ld.owners(os.path.basename(hp))[0] == ["uid-p"] and ld.owners(os.path.basename(hq))[0] == ["uid-q"]
     # nothing of q's is reachable below p's mount (the only host path p's container sees)
