@@ -35,6 +35,13 @@ MI355X build, same protocol, different mechanics:
   Pending pod matches, an equal-size pod that is bound, un-assigned, recently assumed and never
   allocated by this process is matched instead — the two pods simply exchange their
   extender-reserved GPUs;
+* prepared answers (fast path): a background thread keeps, for every candidate pod in the
+  watch cache, its single-container answer already serialized plus its journal record; when
+  the cache has not changed since, Allocate only picks the first eligible candidate of the
+  request's size (same order and rules as the full match), appends the record to the mapped
+  journal and returns the prepared bytes — grants and the replay index follow off the hot
+  path. Anything unusual (multi-container pod first in line, possible replay, cache changed,
+  CU isolation, sync patch) takes the full path;
 * placement truth (``alloc/placement.py``): every answered container is recorded in a grant
   book (fake-ID set → GPU); with the kubelet's pod-resources API configured, the plugin asks
   for ``PreStartContainer`` and, before each container starts (and every ``placement_s``),
@@ -45,6 +52,7 @@ MI355X build, same protocol, different mechanics:
 """
 from __future__ import annotations
 
+import collections
 import dataclasses
 import os
 import threading
@@ -102,6 +110,11 @@ class AllocatorOptions:
     # fake IDs no pod holds yet counts as "in flight" (kubelet checkpoint not visible yet)
     placement_s: float = 2.0
     in_flight_s: float = 30.0
+    # prepared answers for the common admission (see module docstring); write-behind only
+    fast_path: bool = True
+    # admission identity from the kubelet's pod-resources List when the request's size is
+    # ambiguous or a multi-container admission is in progress (see _identify)
+    identify: bool = True
 
 
 @dataclasses.dataclass
@@ -114,6 +127,26 @@ class _Claim:
     t: float               # last time a container of this pod was answered
     slots: cuslots.SlotRun | None = None
     swap: bool = False     # matched through swap completion (the pod is bound, not Pending)
+
+
+@dataclasses.dataclass(frozen=True)
+class _Prepared:
+    uid: str
+    ns: str
+    name: str
+    size: int              # single-container pods: its units; multi: the first container's
+    multi: bool            # multi-container pod: the full path must handle it
+    gpu: int
+    body: bytes = b""      # serialized AllocateResponse (one container)
+    head: bytes = b""      # journal record prefix (AllocJournal.fast_head)
+    lkey: str = ""
+
+
+@dataclasses.dataclass(frozen=True)
+class _Fast:
+    version: int           # pod-cache version the candidates were read at
+    gen: int               # engine state generation (overlays, taints, rebuilds)
+    cands: tuple           # _Prepared in the full match's order
 
 
 class Allocator:
@@ -146,6 +179,12 @@ class Allocator:
         self._revoked: set[str] = set()           # reservation re-armed: its assign job must not re-claim
         self._place_mu = threading.Lock()
         self._place_thread = None
+        # fast path: prepared answers, engine-state generation, answers awaiting bookkeeping
+        self._fast: _Fast | None = None
+        self._gen = 0
+        self._prep_cache: dict[tuple, _Prepared] = {}
+        self._post: "collections.deque" = collections.deque()
+        self._post_mu = threading.Lock()
         for k, uid, t, resp in self.journal.answers():   # grants of a previous instance (journal TTL)
             if len(resp.container_responses) == 1:
                 self.grants.record(k, self._grant_from(resp.container_responses[0], uid, t))
@@ -162,6 +201,7 @@ class Allocator:
                 log.warning("write-behind: re-queueing the unlanded ASSIGNED patch of pod %s/%s (uid %s)",
                             e["ns"], e["name"], e["uid"])
             threading.Thread(target=self._patcher, name="assign-patcher", daemon=True).start()
+            threading.Thread(target=self._prepare_loop, name="prepare-answers", daemon=True).start()
 
     @staticmethod
     def _ledger_dir(opts: AllocatorOptions):
@@ -188,6 +228,9 @@ class Allocator:
             if opts.ledger_dir != ledger_dir:
                 self._ledgers = self._ledger_dir(self.opts)
             self._pinfo.clear()
+            self._gen += 1
+            self._fast = None
+            self._prep_cache.clear()
         return self
 
     def close(self):
@@ -263,11 +306,19 @@ class Allocator:
 
     def _partial_state(self, c: _Claim, cands: list[dict], now: float) -> str:
         """"live": the claimed pod can still be continued; "stale": it exists but the claim
-        outlived ``partial_claim_ttl_s``; "gone": deleted or being deleted."""
+        outlived ``partial_claim_ttl_s`` — or, not matched through swap completion, it is no
+        longer Pending (it started: some of its containers ran on answers from other
+        reservations, and the ones answered from its own may be in use); "gone": deleted or
+        being deleted."""
         if c.swap:
             alive = any(O.uid(p) == c.uid and not O.deleting(p) for p in self.pods.node_pods())
+        elif any(O.uid(p) == c.uid for p in cands):
+            alive = True
         else:
-            alive = any(O.uid(p) == c.uid for p in cands)
+            p = self.pods.get(c.uid)
+            if p is None or O.deleting(p) or O.is_terminated(p):
+                return "gone"
+            return "stale"
         if not alive:
             return "gone"
         return "stale" if now - c.t > self.opts.partial_claim_ttl_s else "live"
@@ -287,6 +338,11 @@ class Allocator:
         k = len(sizes)
         now = time.monotonic()
         cands = self._candidates(fresh)
+        if self.podres is not None and self.opts.identify and (
+                self._partial is not None or self._ambiguous(cands, sizes)):
+            ident = self._identify(cands, sizes)
+            if ident is not None:
+                return self._match_identified(ident, sizes, now)
         c = self._partial
         if c is not None:
             state = self._partial_state(c, cands, now)
@@ -314,6 +370,7 @@ class Allocator:
                 # never handed out again while the pod lives (no double booking of its HBM);
                 # its own admission, if it comes, is matched elsewhere or refused.
                 self._tainted[c.uid] = now
+                self._gen += 1
                 self.metrics.allocate_outcomes.inc(outcome="claim_tainted")
                 log.warning("pod %s: %d/%d gpu containers answered from its reservation, then the kubelet moved on "
                             "(%s); reservation withheld", O.name(c.pod), c.next_container, len(c.shape),
@@ -355,6 +412,88 @@ class Allocator:
                     return self._start_partial(p, shape, k, now, swap=True), False
                 return _Claim(O.uid(p), p, A.gpu_id_from_annotation(p), k, shape, now, swap=True), True
         return None, False
+
+    def _ambiguous(self, cands: list[dict], sizes: tuple) -> bool:
+        """More than one candidate could be the pod this request belongs to."""
+        n = 0
+        for p in cands:
+            if O.uid(p) in self._claims:
+                continue
+            shape = self._info(p)[3]
+            if shape[:len(sizes)] == sizes:
+                n += 1
+                if n > 1:
+                    return True
+        return False
+
+    def _identify(self, cands: list[dict], sizes: tuple) -> tuple[dict, int] | None:
+        """Admission identity: the kubelet adds a pod to its pod manager right before admitting
+        it and checkpoints each container's fake IDs as soon as that container's Allocate
+        returns, so in the pod-resources List the pod being admitted is the one Pending pod
+        of this node whose gpu containers do not all hold IDs yet. Returns (pod, number of its
+        gpu containers already allocated), or None when that is not exactly one pod."""
+        try:
+            held = self.podres.list(include_empty=True)
+        except Exception as e:  # noqa: BLE001 - kubelet restarting: fall back to the heuristic
+            log.V(2).info("admission identity unavailable: %s", e)
+            return None
+        pending = {(O.namespace(p), O.name(p)): p for p in self._view(A.dedupe_by_uid(
+            self.pods.pending_pods(fresh=False), self.node))}
+        for p in cands:
+            pending.setdefault((O.namespace(p), O.name(p)), p)
+        found = []
+        for pd in held:
+            p = pending.get((pd.namespace, pd.name))
+            if p is None or O.deleting(p):
+                continue
+            have = {cn for cn, ids in pd.containers if ids}
+            gpu_ctrs = [name for _, name, _ in PL._gpu_containers(p)]
+            done = sum(1 for cn in gpu_ctrs if cn in have)
+            if gpu_ctrs and done < len(gpu_ctrs):
+                found.append((p, done))
+        if len(found) != 1:
+            return None
+        p, done = found[0]
+        if self._info(p)[3][done:done + len(sizes)] != sizes:
+            log.warning("admission identity: pod %s is being admitted but its next gpu containers are not %s; "
+                        "falling back to matching by size", O.name(p), list(sizes))
+            return None
+        return p, done
+
+    def _match_identified(self, ident: tuple[dict, int], sizes: tuple, now: float) -> tuple[_Claim | None, bool]:
+        """Match the pod the kubelet is admitting (``_identify``): its own reservation, never
+        another pod's — no swap, no stray partial claim."""
+        p, done = ident
+        u = O.uid(p)
+        shape = self._info(p)[3]
+        c = self._partial
+        if c is not None and c.uid == u and c.next_container == done:
+            self._partial = None
+            c.next_container += len(sizes)
+            c.t = now
+            if c.next_container < len(c.shape):
+                self._partial = c
+                return c, False
+            return c, True
+        if c is not None:
+            # a claim started by size matching belongs to another pod: its answered containers
+            # went to the pods admitted since, so its reservation is withheld (see _match)
+            self._partial = None
+            self._claims.pop(c.uid, None)
+            if self.pods.get(c.uid) is not None:
+                self._tainted[c.uid] = now
+                self._gen += 1
+                self.metrics.allocate_outcomes.inc(outcome="claim_tainted")
+        if u in self._tainted or u in self._claims or (u in self._assigned and done == 0):
+            log.warning("admission identity: pod %s is being admitted but its reservation is no longer whole", O.name(p))
+            return None, False
+        self.metrics.allocate_outcomes.inc(outcome="identified")
+        claim = _Claim(u, p, A.gpu_id_from_annotation(p), done + len(sizes), shape, now)
+        if claim.next_container == len(shape):
+            return claim, True
+        self._claims[u] = claim
+        self._partial = claim
+        return claim, False
 
     def _start_partial(self, p: dict, shape: tuple, k: int, now: float, swap: bool) -> _Claim:
         c = _Claim(O.uid(p), p, A.gpu_id_from_annotation(p), k, shape, now, swap=swap)
@@ -491,11 +630,132 @@ class Allocator:
     # RPCs
     # ------------------------------------------------------------------------------------
     def allocate(self, req) -> api.AllocateResponse:
+        r = self.allocate_raw(req)
+        return api.AllocateResponse.FromString(r) if isinstance(r, bytes) else r
+
+    def allocate_raw(self, req, defer=None):
+        """The Allocate RPC: the prepared answer's wire bytes (fast path) or a message.
+        ``defer(fn)`` runs ``fn`` once the reply is on its way (gRPC ``context.add_callback``):
+        the fast path wakes the patcher there, so that thread never competes with the reply
+        for the interpreter."""
         t0 = time.perf_counter()
+        fast = self._fast
+        if fast is not None:
+            body = self._allocate_fast(req, fast, t0, defer)
+            if body is not None:
+                return body
+        return self._allocate_full(req, t0)
+
+    def _allocate_fast(self, req, fast: "_Fast", t0: float, defer=None) -> bytes | None:
+        crs = req.container_requests
+        if len(crs) != 1 or self._partial is not None:
+            return None
+        ids = crs[0].devices_ids
+        n = len(ids)
+        if n == 0 or self.journal.maybe_replay(ids[0]) or fast.version != getattr(self.pods, "version", -1):
+            return None
+        with self._mu:
+            if fast.gen != self._gen or self._partial is not None:
+                return None
+            el = [c for c in fast.cands if c.size == n and c.uid not in self._assigned
+                  and c.uid not in self._claims and c.uid not in self._tainted]
+            # a multi-container pod first in line (partial claims), or — with pod-resources —
+            # more than one candidate of this size (which one the kubelet is admitting is for
+            # admission identity to say): the full path decides
+            if not el or el[0].multi or (len(el) > 1 and self.podres is not None):
+                return None
+            pick = self._take(el[0])
+        rb = req.SerializeToString()
+        t = self.journal.record_fast(pick.uid, pick.ns, pick.name, pick.head, rb)
+        self._post.append((rb, pick, t))
+        job = _PatchJob(pick.uid, pick.ns, pick.name, {})
+        # the reference logs the request and the outcome (allocate.go:47-58,193-194): one record here
+        log.info("----Allocating GPU for gpu mem is started---- RequestPodGPUs: %d; pod %s, new allocated GPUs info: "
+                 "gpu index %d uuid %s (patch queued)", n, pick.name, pick.gpu, self.model.uuid_by_index(pick.gpu))
+        self.metrics.allocate_outcomes.inc(outcome="assigned")
+        dt = time.perf_counter() - t0
+        self.metrics.allocate_latency.observe(dt, phase="total")
+        self.metrics.allocate_latency.observe(dt, phase="fast")
+        if defer is None or not defer(lambda: self._patch_q.put(job)):
+            self._patch_q.put(job)
+        return pick.body
+
+    def _take(self, c: "_Prepared") -> "_Prepared":
+        """Claim a prepared candidate (caller holds ``_mu``)."""
+        self._assigned[c.uid] = time.monotonic()
+        self._unpatched.add(c.uid)
+        self._revoked.discard(c.uid)
+        return c
+
+    def _drain_post(self) -> None:
+        """Bookkeeping of fast-path answers, off the hot path: grant book + journal index."""
+        with self._post_mu:
+            while self._post:
+                rb, c, t = self._post.popleft()
+                ids = tuple(api.AllocateRequest.FromString(rb).container_requests[0].devices_ids)
+                key = PL.ids_key(ids)
+                self.journal.index_answer(key, c.uid, t, c.body, ids)
+                self.grants.record(key, PL.Grant(gpu=c.gpu, units=len(ids), claimed=c.uid, t=t, ledger=c.lkey))
+            self.journal.prefault()
+
+    def _prepare_loop(self):
+        """Keep ``self._fast`` current: woken by every pod-cache change."""
+        while not self._stop.is_set():
+            src = self.pods
+            ev = getattr(src, "changed", None)
+            if ev is None or not self.opts.fast_path or self.opts.compute_isolation == "cu":
+                self._fast = None
+                self._stop.wait(1.0)
+                continue
+            ev.wait(0.5)
+            ev.clear()
+            try:
+                self._prepare(src)
+            except Exception as e:  # noqa: BLE001 - the full path still answers
+                self._fast = None
+                log.V(2).info("prepare answers: %s", e)
+
+    def _prepare(self, src) -> None:
+        version = src.version
+        with self._mu:
+            gen = self._gen
+            cands = self._candidates(fresh=False)
+            cands = [p for p in cands if O.uid(p) not in self._claims]
+        out, keep = [], {}
+        for p in cands:
+            shape = self._info(p)[3]
+            if not shape:
+                continue
+            u, g = O.uid(p), A.gpu_id_from_annotation(p)
+            if len(shape) > 1:
+                out.append(_Prepared(u, O.namespace(p), O.name(p), shape[0], True, g))
+                continue
+            k = (u, g, shape[0])
+            c = self._prep_cache.get(k)
+            if c is None:
+                if self.model.gpu(g) is None:
+                    continue
+                cr = self._container_response(g, shape[0], shape[0], u, 0, None)
+                r = api.AllocateResponse()
+                r.container_responses.append(cr)
+                body = r.SerializeToString()
+                c = _Prepared(u, O.namespace(p), O.name(p), shape[0], False, g, body,
+                              AllocJournal.fast_head(u, O.namespace(p), O.name(p), body),
+                              cr.annotations.get(const.CTR_ANNOTATION_LEDGER, ""))
+            keep[k] = c
+            out.append(c)
+        self._prep_cache = keep
+        self._fast = _Fast(version, gen, tuple(out))
+        if self.journal.indexed_uids():         # replay index: only pods that can still be retried
+            pend = {O.uid(p) for p in src.pending_pods()}
+            self.journal.prune_index(pend)
+
+    def _allocate_full(self, req, t0: float):
         sizes = tuple(len(c.devices_ids) for c in req.container_requests)
         pod_units = sum(sizes)
         log.info("----Allocating GPU for gpu mem is started---- RequestPodGPUs: %d", pod_units)
         hist = self.metrics.allocate_latency
+        self._drain_post()
         jkey = request_key(req)
         replay = self._replay(req, jkey)
         if replay is not None:
@@ -658,6 +918,7 @@ class Allocator:
                 continue
             if job is None:
                 break
+            self._drain_post()
             delay = 0.05
             while not self._stop.is_set():
                 try:
@@ -685,6 +946,7 @@ class Allocator:
                 if self._overlay_gen.get(job.uid) == job.gen:
                     self._overlay.pop(job.uid, None)
                     self._overlay_gen.pop(job.uid, None)
+                    self._gen += 1
             return
         self.journal.landed(job.uid)
         with self._mu:
@@ -780,6 +1042,7 @@ class Allocator:
         src = self.podres
         if src is None:
             return []
+        self._drain_post()
         with self._place_mu:
             held = src.list()
             pods = self._view(A.dedupe_by_uid(self.pods.node_pods(), self.node))
@@ -806,6 +1069,7 @@ class Allocator:
             gen = self._overlay_gen.get(f.uid, 0) + 1
             self._overlay_gen[f.uid] = gen
             self._overlay[f.uid] = dict(self._overlay.get(f.uid) or {}, **ann)
+            self._gen += 1
             if f.assigned is True:
                 self._assigned[f.uid] = time.monotonic()
                 self._revoked.discard(f.uid)

@@ -46,6 +46,11 @@ def request_key(req) -> str:
     return hashlib.sha1(body.encode()).hexdigest()
 
 
+def ids_key(ids) -> str:
+    """``request_key`` of a one-container request with these fake IDs."""
+    return hashlib.sha1("\x1f".join(sorted(ids)).encode()).hexdigest()
+
+
 class AllocJournal:
     def __init__(self, path: str | None = None, ttl_s: float = 120.0, max_entries: int = 4096,
                  pending_ttl_s: float = 24 * 3600.0, map_bytes: int = 16 << 20):
@@ -54,11 +59,17 @@ class AllocJournal:
         self.map_bytes = map_bytes
         self._mm: mmap.mmap | None = None
         self._off = 0
+        self._touched = 0
         self._mem: collections.OrderedDict[str, tuple[str, float, bytes]] = collections.OrderedDict()
         self._uids: dict[str, float] = {}                       # pod uid -> time of its answer
         self._pending: collections.OrderedDict[str, dict] = collections.OrderedDict()  # uid -> patch
         self._lock = threading.Lock()
         self._lines = 0
+        # fake ID -> key of the journaled answer that holds it, for answers whose pod may still
+        # be retried (Pending): lets the Allocate fast path rule a replay out with one dict probe
+        self._by_id: dict[str, str] = {}
+        self._ids_of: dict[str, tuple[str, tuple]] = {}       # uid -> (key, ids)
+        self._legacy_until = 0.0       # answers loaded without their IDs: probe says "maybe"
         if path:
             self._load()
 
@@ -84,9 +95,18 @@ class AllocJournal:
                 if op == "landed":
                     self._pending.pop(e["uid"], None)
                 elif now - e["t"] <= self.ttl_s:
-                    self._mem[e["k"]] = (e["uid"], e["t"], base64.b64decode(e["resp"]))
-                    self._mem.move_to_end(e["k"])
+                    ids = tuple(e["ids"].split(",")) if e.get("ids") else None
+                    if e.get("req"):
+                        r = api.AllocateRequest.FromString(base64.b64decode(e["req"]))
+                        ids = tuple(i for c in r.container_requests for i in c.devices_ids)
+                    k = e.get("k") or ids_key(ids)
+                    self._mem[k] = (e["uid"], e["t"], base64.b64decode(e["resp"]))
+                    self._mem.move_to_end(k)
                     self._uids[e["uid"]] = e["t"]
+                    if ids:
+                        self._index(k, e["uid"], ids)
+                    else:
+                        self._legacy_until = max(self._legacy_until, e["t"] + self.ttl_s)
             except (ValueError, KeyError, TypeError):
                 continue                                          # a torn last line after a crash
         while len(self._mem) > self.max_entries:
@@ -103,11 +123,32 @@ class AllocJournal:
         try:
             size = max(self.map_bytes, os.fstat(fd).st_size)
             os.ftruncate(fd, size)
+            try:
+                os.posix_fallocate(fd, 0, size)   # blocks reserved now, not at a page's first store
+            except OSError:
+                pass
             self._mm = mmap.mmap(fd, size, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
         finally:
             os.close(fd)
         end = self._mm.find(b"\0")
         self._off = len(self._mm) if end < 0 else end
+        self._touched = self._off
+        self.prefault()
+
+    def prefault(self, ahead: int = 256 << 10) -> None:
+        """Fault in the pages the next records will land on (off the Allocate path: the
+        patcher calls it), so an answer's store never takes the first-write page fault."""
+        mm = self._mm
+        if mm is None:
+            return
+        end = min(len(mm), self._off + ahead)
+        pos = max(self._touched, self._off)
+        pos -= pos % mmap.PAGESIZE
+        while pos < end:
+            if pos >= self._off:
+                mm[pos] = mm[pos]          # a store: write fault now (the byte is still zero)
+            pos += mmap.PAGESIZE
+        self._touched = max(self._touched, end)
 
     def _write(self, rec: dict):
         if not self.path:
@@ -132,7 +173,8 @@ class AllocJournal:
         tmp = self.path + ".tmp"
         try:
             os.makedirs(os.path.dirname(self.path) or ".", exist_ok=True)
-            parts = [json.dumps({"k": k, "uid": uid, "t": t, "resp": base64.b64encode(blob).decode()},
+            parts = [json.dumps({"k": k, "uid": uid, "t": t, "resp": base64.b64encode(blob).decode(),
+                                 **({"ids": ",".join(self._ids_of[uid][1])} if uid in self._ids_of else {})},
                                 separators=(",", ":")).encode() + b"\n" for k, (uid, t, blob) in self._mem.items()]
             parts += [json.dumps(e, separators=(",", ":")).encode() + b"\n" for e in self._pending.values()]
             body = b"".join(parts) + extra
@@ -150,17 +192,90 @@ class AllocJournal:
         except (OSError, ValueError) as e:
             log.warning("allocation journal compaction failed: %s", e)
 
+    # -- replay index -----------------------------------------------------------------------
+    def _index(self, key: str, uid: str, ids) -> None:
+        old = self._ids_of.pop(uid, None)
+        if old is not None:
+            for i in old[1]:
+                if self._by_id.get(i) == old[0]:
+                    del self._by_id[i]
+        self._ids_of[uid] = (key, tuple(ids))
+        for i in ids:
+            self._by_id[i] = key
+
+    def maybe_replay(self, device_id: str) -> bool:
+        """False = no journaled answer of a possibly-retried pod holds this fake ID (so the
+        request is not a replay); True = check properly (``lookup``)."""
+        return device_id in self._by_id or time.time() < self._legacy_until
+
+    def prune_index(self, keep_uids) -> None:
+        """Forget the IDs of answers whose pod can no longer be retried (not Pending any more,
+        or gone): the kubelet recycles those IDs for new pods at once."""
+        with self._lock:
+            for u in [u for u in self._ids_of if u not in keep_uids]:
+                key, ids = self._ids_of.pop(u)
+                for i in ids:
+                    if self._by_id.get(i) == key:
+                        del self._by_id[i]
+
+    def indexed_uids(self) -> list[str]:
+        with self._lock:
+            return list(self._ids_of)
+
     # -- answers ----------------------------------------------------------------------------
     def record(self, req, pod_uid: str, resp, key: str | None = None) -> None:
         key, t, blob = key or request_key(req), time.time(), resp.SerializeToString()
+        ids = [i for c in req.container_requests for i in c.devices_ids]
         with self._lock:
             self._mem[key] = (pod_uid, t, blob)
             self._mem.move_to_end(key)
             self._uids[pod_uid] = t
+            self._index(key, pod_uid, ids)
             while len(self._mem) > self.max_entries:
                 _, (u, _, _) = self._mem.popitem(last=False)
                 self._uids.pop(u, None)
             self._write({"k": key, "uid": pod_uid, "t": t, "resp": base64.b64encode(blob).decode()})
+
+    def record_fast(self, pod_uid: str, ns: str, name: str, head: bytes, req_bytes: bytes) -> float:
+        """Allocate fast path: the answer + pending-patch record from its prepared ``head``
+        (everything but the time and the request) — one store into the mapping. The request
+        goes in as its wire bytes (no per-ID Python strings on the hot path); the in-memory
+        answer index follows off the hot path (``index_answer``). Returns the record's time."""
+        t = time.time()
+        pend = {"op": "patch", "uid": pod_uid, "ns": ns, "name": name, "ann": {}, "t": t}
+        data = b"".join((head, repr(t).encode(), b',"req":"', base64.b64encode(req_bytes), b'"}\n'))
+        with self._lock:
+            self._uids[pod_uid] = t
+            self._pending[pod_uid] = pend
+            if self.path:
+                try:
+                    if self._mm is None:
+                        self._map()
+                    if self._off + len(data) <= len(self._mm):
+                        self._mm[self._off:self._off + len(data)] = data
+                        self._off += len(data)
+                        self._lines += 1
+                    else:
+                        self._compact(extra=data)
+                except (OSError, ValueError) as e:
+                    log.warning("allocation journal write failed: %s", e)
+        return t
+
+    @staticmethod
+    def fast_head(pod_uid: str, ns: str, name: str, resp_bytes: bytes) -> bytes:
+        """The constant part of a fast-path record (see ``record_fast``)."""
+        return (json.dumps({"op": "answer+patch", "uid": pod_uid, "ns": ns, "name": name, "ann": {},
+                            "resp": base64.b64encode(resp_bytes).decode()}, separators=(",", ":"))[:-1]
+                + ',"t":').encode()
+
+    def index_answer(self, key: str, pod_uid: str, t: float, blob: bytes, ids) -> None:
+        with self._lock:
+            self._mem[key] = (pod_uid, t, blob)
+            self._mem.move_to_end(key)
+            self._index(key, pod_uid, ids)
+            while len(self._mem) > self.max_entries:
+                _, (u, _, _) = self._mem.popitem(last=False)
+                self._uids.pop(u, None)
 
     def lookup(self, req, key: str | None = None) -> tuple[str, object] | None:
         """(pod uid, the journaled answer) for this request's fake-ID set, or None. The answer
@@ -202,6 +317,7 @@ class AllocJournal:
             self._mem[key] = (pod_uid, t, blob)
             self._mem.move_to_end(key)
             self._uids[pod_uid] = t
+            self._index(key, pod_uid, [i for c in req.container_requests for i in c.devices_ids])
             while len(self._mem) > self.max_entries:
                 _, (u, _, _) = self._mem.popitem(last=False)
                 self._uids.pop(u, None)

@@ -61,13 +61,23 @@ class ProtoFile:
             fn = getattr(impl, meth)
             factory = grpc.unary_stream_rpc_method_handler if stream else grpc.unary_unary_rpc_method_handler
             handlers[meth] = factory(fn, request_deserializer=self.by_name[inp].FromString,
-                                     response_serializer=self.by_name[out].SerializeToString)
+                                     response_serializer=_serializer(self.by_name[out]))
         server.add_generic_rpc_handlers((grpc.method_handlers_generic_handler(f"{self.package}.{service}",
                                                                               handlers),))
 
     def stub(self, channel, service: str):
         """Client stub over an existing ``grpc.Channel`` (generated Go client equivalent)."""
         return _Stub(self, channel, service)
+
+
+def _serializer(cls):
+    """A handler may return the message or its wire bytes already serialized (the Allocate
+    fast path answers with bytes prepared before the request arrived)."""
+    ser = cls.SerializeToString
+
+    def f(r):
+        return r if isinstance(r, bytes) else ser(r)
+    return f
 
 
 class _Stub:

@@ -82,13 +82,17 @@ class PodDevices:
     containers: tuple
 
 
-def pod_devices(resp, resource: str) -> list[PodDevices]:
+def pod_devices(resp, resource: str, include_empty: bool = False) -> list[PodDevices]:
+    """Per pod, its containers' IDs of ``resource``. ``include_empty``: also list pods and
+    containers holding none yet — the kubelet adds a pod to its pod manager right before
+    admitting it, so a Pending pod whose gpu containers hold no (or only some) IDs is the one
+    whose ``Allocate`` calls are in progress (``alloc/engine.py`` admission identity)."""
     out = []
     for pr in resp.pod_resources:
         ctrs = []
         for c in pr.containers:
             ids = [i for d in c.devices if d.resource_name == resource for i in d.device_ids]
-            if ids:
+            if ids or include_empty:
                 ctrs.append((c.name, tuple(ids)))
         if ctrs:
             out.append(PodDevices(pr.namespace, pr.name, tuple(ctrs)))
@@ -115,7 +119,7 @@ class PodResourcesClient:
             self._stub = PROTO.stub(self._ch, "PodResourcesLister")
         return self._stub
 
-    def list(self) -> list[PodDevices]:
+    def list(self, include_empty: bool = False) -> list[PodDevices]:
         import grpc
 
         try:
@@ -123,7 +127,7 @@ class PodResourcesClient:
         except grpc.RpcError:
             self.close()        # the kubelet restarted: re-dial on the next call
             raise
-        return pod_devices(resp, self.resource)
+        return pod_devices(resp, self.resource, include_empty)
 
     def available(self) -> bool:
         import os

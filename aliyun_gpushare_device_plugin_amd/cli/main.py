@@ -85,6 +85,10 @@ def build_parser() -> argparse.ArgumentParser:
                         "PreStartContainer and rewrites IDX/allocation annotations to the GPU each container "
                         "really got (swapped admissions). 'auto' = /var/lib/kubelet/pod-resources/kubelet.sock "
                         "when present; 'none' disables placement truth")
+    p.add_argument("--admission-identity", type=_bool, nargs="?", const=True, default=True,
+                   help="when several pending pods could own an Allocate request, ask the kubelet's "
+                        "pod-resources List which pod is being admitted (it holds no IDs yet) instead of "
+                        "guessing by assume time (default true; needs --pod-resources-socket)")
     p.add_argument("--placement-interval", type=float, default=2.0,
                    help="seconds between periodic placement-truth passes (besides PreStartContainer)")
     p.add_argument("--sync-patch", action="store_true",
@@ -113,7 +117,8 @@ def config_from_args(a) -> PluginConfig:
         async_patch=not a.sync_patch, complete_swaps=not a.no_swap_completion,
         partition_aware=a.partition_aware, ledger_dir=a.ledger_dir, ledger_scan_s=a.ledger_scan_interval,
         journal_path=a.journal_path, compute_isolation=a.compute_isolation,
-        pod_resources_socket=a.pod_resources_socket, placement_s=a.placement_interval)
+        pod_resources_socket=a.pod_resources_socket, placement_s=a.placement_interval,
+        admission_identity=a.admission_identity)
 
 
 def install_shim(dest_dir: str) -> str:

@@ -115,6 +115,10 @@ class WatchCache(PodSource):
         self._pods: dict[str, dict] = {}
         self._pending: dict[str, dict] = {}     # the Pending subset, so Allocate never scans Running pods
         self._lock = threading.Lock()
+        # bumped on every change of the cached set; ``changed`` wakes consumers that precompute
+        # from the cache (the Allocate engine's prepared answers)
+        self.version = 0
+        self.changed = threading.Event()
         self._synced = threading.Event()
         self._stop = threading.Event()
         self._thread = None
@@ -142,6 +146,8 @@ class WatchCache(PodSource):
             self._pods = {O.uid(p): p for p in items}
             self._pending = {u: p for u, p in self._pods.items() if O.phase(p) == "Pending"}
             self._rv = rv
+            self.version += 1
+        self.changed.set()
         self.relists += 1
         self._synced.set()
 
@@ -158,11 +164,13 @@ class WatchCache(PodSource):
             if typ == "DELETED" or O.node_name(obj) != self.node:
                 self._pods.pop(u, None)
                 self._pending.pop(u, None)
+                self.version += 1
             else:
                 cur = self._pods.get(u)
                 if cur is None or O.rv_int(O.resource_version(obj)) >= O.rv_int(O.resource_version(cur)):
                     self._put(u, obj)
             self._rv = O.resource_version(obj) or self._rv
+        self.changed.set()
         self.events += 1
         if self.on_event:
             self.on_event(typ)
@@ -203,6 +211,7 @@ class WatchCache(PodSource):
             return list(self._pending.values())
 
     def _put(self, u: str, pod: dict) -> None:
+        self.version += 1
         self._pods[u] = pod
         if O.phase(pod) == "Pending":
             self._pending[u] = pod
@@ -217,6 +226,7 @@ class WatchCache(PodSource):
             cur = self._pods.get(u)
             if cur is None or O.rv_int(O.resource_version(pod)) >= O.rv_int(O.resource_version(cur)):
                 self._put(u, pod)
+        self.changed.set()
 
     def get(self, uid: str) -> dict | None:
         if not self._synced.is_set():

@@ -74,6 +74,7 @@ class PluginConfig:
     # standard path when it exists, "none"/"" = off
     pod_resources_socket: str = "auto"
     placement_s: float = 2.0
+    admission_identity: bool = True      # which pod is being admitted, from pod-resources (engine)
     mps: bool = False                    # accepted for flag compatibility; ignored
 
 
@@ -162,7 +163,8 @@ class SharedGPUManager:
                                 complete_swaps=cfg.complete_swaps,
                                 ledger_dir=cfg.ledger_dir if shim else None,
                                 journal_path=cfg.journal_path,
-                                compute_isolation=cfg.compute_isolation, placement_s=cfg.placement_s)
+                                compute_isolation=cfg.compute_isolation, placement_s=cfg.placement_s,
+                                identify=cfg.admission_identity)
         if self.allocator is None:
             if cfg.async_patch and not cfg.journal_path:
                 log.warning("write-behind ASSIGNED patches without --journal-path: a patch still queued when "

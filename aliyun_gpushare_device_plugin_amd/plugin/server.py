@@ -64,7 +64,8 @@ class _Servicer:
 
     def Allocate(self, request, context):
         try:
-            return self.p.allocator.allocate(request)
+            # message, or prepared wire bytes; follow-up work runs after the reply is sent
+            return self.p.allocator.allocate_raw(request, defer=context.add_callback)
         except AllocationError as e:
             context.abort(grpc.StatusCode.FAILED_PRECONDITION, str(e))
 

@@ -59,7 +59,8 @@ class SimCluster:
                  gpu_indices: list[int] | None = None, health_poll_s: float = 1.0, round_policy: str = "nearest",
                  extra_plugin_args: list[str] | None = None, apiserver: str = "thread",
                  preferred_allocation: bool = False, compute_isolation: str = "none", kubelet: str = "thread",
-                 placement_truth: bool = True, node_overrides: dict | None = None):
+                 placement_truth: bool = True, node_overrides: dict | None = None,
+                 admission_identity: bool = True):
         self.node_specs = nodes
         # kubelet: "thread" (FakeKubelet in this interpreter) or "process" (its own interpreter,
         # sim/kubelet_proc.py, so kubelet-side Allocate timing is not inflated by this process's GIL)
@@ -69,6 +70,7 @@ class SimCluster:
         self.node_overrides = node_overrides or {}
         # the fake kubelet serves pod-resources; the plugin uses it for placement truth
         self.placement_truth = placement_truth
+        self.admission_identity = admission_identity
         self.compute_isolation = compute_isolation
         self._own_dir = workdir is None
         # short paths: UDS paths are limited to 108 bytes
@@ -153,6 +155,7 @@ class SimCluster:
                             health_poll_s=self.health_poll_s, round_policy=self.round_policy,
                             preferred_allocation=self.preferred_allocation,
                             compute_isolation=self.compute_isolation, pod_resources_socket=self._podres(node),
+                            admission_identity=self.admission_identity,
                             **self._kubelet_cfg(node))
 
     def _podres(self, node: SimNode) -> str:
@@ -179,7 +182,8 @@ class SimCluster:
                 args += ["--preferred-allocation"]
             if self.compute_isolation != "none":
                 args += ["--compute-isolation", self.compute_isolation]
-            args += ["--pod-resources-socket", self._podres(node)]
+            args += ["--pod-resources-socket", self._podres(node),
+                     "--admission-identity", "true" if self.admission_identity else "false"]
             for k, v in self._kubelet_cfg(node).items():
                 args += ["--" + k.replace("_", "-"), str(v)]
             ov = self.node_overrides.get(node.name, {})

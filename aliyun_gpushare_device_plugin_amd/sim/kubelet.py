@@ -65,6 +65,7 @@ class FakeKubelet:
         self._lock = threading.Lock()
         self._stop = threading.Event()
         self._holdings: dict[str, tuple] = {}    # uid -> (ns, name, [(container, ids)])
+        self._specs: dict[str, list] = {}        # uid -> container names (all listed, like the kubelet)
         self.podres_sock = os.path.join(plugin_dir, "pod-resources.sock")
         self.prestart_calls = 0
         self.reg_options = None
@@ -110,14 +111,17 @@ class FakeKubelet:
     def _pod_resources(self, uid_filter=None) -> list:
         with self._lock:
             items = list(self._holdings.items())
+            specs = dict(self._specs)
         out = []
         for uid, (ns, name, ctrs) in items:
             if uid_filter is not None and not uid_filter(ns, name):
                 continue
+            got = dict(ctrs)
+            names = specs.get(uid) or [cn for cn, _ in ctrs]
             out.append(podres.PodResources(name=name, namespace=ns, containers=[
                 podres.ContainerResources(name=cn, devices=[
-                    podres.ContainerDevices(resource_name=self.resource, device_ids=[i]) for i in ids])
-                for cn, ids in ctrs]))
+                    podres.ContainerDevices(resource_name=self.resource, device_ids=[i]) for i in got.get(cn, ())])
+                for cn in names]))
         return out
 
     def List(self, request, context):
@@ -236,6 +240,11 @@ class FakeKubelet:
         uid = O.uid(pod)
         adm = Admission(uid, [], [], [])
         started = []
+        # like the kubelet's HandlePodAdditions: the pod joins the pod manager (and so the
+        # pod-resources List, holding nothing yet) right before it is admitted
+        with self._lock:
+            self._holdings[uid] = (O.namespace(pod), O.name(pod), [])
+            self._specs[uid] = [c.get("name", "") for c in O.containers(pod)]
         for c in O.containers(pod):
             n = O.container_limit(c, self.resource)
             if n <= 0:
@@ -244,6 +253,9 @@ class FakeKubelet:
                 free = self._free_healthy()
                 if len(free) < n:
                     adm.error = f"insufficient {self.resource}: want {n}, free {len(free)}"
+                    self._holdings.pop(uid, None)      # rejected: no longer an active pod
+                    self._specs.pop(uid, None)
+                    self._used.difference_update(self._allocated.pop(uid, ()))
                     return adm
                 ids = free[:n]
                 if self.options is not None and self.options.get_preferred_allocation_available:
@@ -289,6 +301,7 @@ class FakeKubelet:
         with self._lock:
             self._used.difference_update(self._allocated.pop(pod_uid, ()))
             self._holdings.pop(pod_uid, None)
+            self._specs.pop(pod_uid, None)
 
     def allocated_ids(self) -> set:
         with self._lock:

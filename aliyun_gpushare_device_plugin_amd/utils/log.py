@@ -73,13 +73,20 @@ _FLUSH_S = 0.05
 _flusher = None
 
 
-def _flush_locked() -> None:
+_wlock = threading.Lock()      # orders writes; never held by a caller of _emit's fast branch
+
+
+def _take_locked() -> str:
     if not _buf:
-        return
-    st = _stream or sys.stderr
+        return ""
     data = "\n".join(_buf) + "\n"
     _buf.clear()
     _buf_bytes[0] = 0
+    return data
+
+
+def _write(data: str) -> None:
+    st = _stream or sys.stderr
     try:
         st.write(data)
         st.flush()
@@ -87,9 +94,21 @@ def _flush_locked() -> None:
         pass
 
 
+def _flush_locked() -> None:
+    data = _take_locked()
+    if data:
+        with _wlock:
+            _write(data)
+
+
 def flush() -> None:
-    with _lock:
-        _flush_locked()
+    """Write buffered lines. The buffer is swapped under the emit lock and written outside
+    it, so a logging caller never waits for the flusher's write(2)."""
+    with _wlock:
+        with _lock:
+            data = _take_locked()
+        if data:
+            _write(data)
 
 
 def _flush_loop(stop: threading.Event) -> None:

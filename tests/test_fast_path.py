@@ -1,0 +1,92 @@
+"""Allocate fast path (prepared answers) — same decisions as the full match, less work.
+
+The engine keeps every candidate pod's single-container answer serialized ahead of time;
+when the watch cache has not changed since, Allocate only picks the first eligible candidate
+of the request's size, appends its journal record to the mapped file and returns the bytes.
+"""
+import time
+
+from aliyun_gpushare_device_plugin_amd import const
+from aliyun_gpushare_device_plugin_amd.alloc.journal import AllocJournal
+from aliyun_gpushare_device_plugin_amd.api import v1beta1 as api
+from aliyun_gpushare_device_plugin_amd.cluster import objects as O
+from aliyun_gpushare_device_plugin_amd.sim.cluster import SimCluster
+
+
+def _settle(al, timeout=5.0):
+    """Wait until the prepared answers match the pod cache."""
+    t = time.monotonic() + timeout
+    while time.monotonic() < t:
+        f = al._fast
+        if f is not None and f.version == al.pods.version and f.gen == al._gen:
+            return True
+        time.sleep(0.005)
+    return False
+
+
+def _envs(r):
+    e = dict(r.envs)
+    e.pop(const.ENV_SHIM_LEDGER, None)
+    return e
+
+
+def test_fast_path_answers_like_the_full_path(tmp_path):
+    with SimCluster([("n", "fake:2x16G")], shim_host_dir=str(tmp_path)) as c:
+        al = c.manager("n").allocator
+        pods = [c.create_pod(s, name=f"p{i}") for i, s in enumerate((4, 8))]
+        places = [c.schedule(p) for p in pods]
+        assert _settle(al)
+        adm = c.admit(pods[0])
+        assert adm.error is None
+        assert al.metrics.allocate_latency.count(phase="fast") == 1
+        env = _envs(adm.responses[0])
+        assert env[const.ENV_RESOURCE_INDEX] == str(places[0][1])
+        assert env[const.ENV_RESOURCE_BY_CONTAINER] == env[const.ENV_RESOURCE_BY_POD] == "4"
+        assert {d.container_path for d in adm.responses[0].devices} >= {"/dev/kfd"}
+        got = c.wait_assigned(pods[0])
+        assert O.annotations(got)[const.ENV_ASSIGNED_FLAG] == "true"
+        # the same pod answered by the full path (fast path off) carries the same envs
+        al.opts.fast_path = False
+        al._fast = None
+        adm2 = c.admit(pods[1])
+        assert al.metrics.allocate_latency.count(phase="fast") == 1
+        assert _envs(adm2.responses[0])[const.ENV_RESOURCE_INDEX] == str(places[1][1])
+        assert set(_envs(adm2.responses[0])) == set(env)
+
+
+def test_fast_path_defers_to_identity_on_ambiguity():
+    """Two pending pods of the same size: the fast path steps aside and admission identity
+    (pod-resources) gives the kubelet's pod its own reservation."""
+    with SimCluster([("n", "fake:2x8G")]) as c:
+        al = c.manager("n").allocator
+        a, b = c.create_pod(8, name="a"), c.create_pod(8, name="b")
+        assert c.schedule(a)[1] == 0 and c.schedule(b)[1] == 1
+        assert _settle(al)
+        adm = c.admit(b)
+        assert int(adm.responses[0].envs[const.ENV_RESOURCE_INDEX]) == 1
+        assert al.metrics.allocate_latency.count(phase="fast") == 0
+        assert al.metrics.allocate_outcomes.value(outcome="identified") == 1
+        assert _settle(al)
+        adm = c.admit(a)                       # now unambiguous: fast
+        assert int(adm.responses[0].envs[const.ENV_RESOURCE_INDEX]) == 0
+        assert al.metrics.allocate_latency.count(phase="fast") == 1
+
+
+def test_fast_records_survive_a_crash(tmp_path):
+    """A fast-path record (answer + pending patch, request as wire bytes) is recovered by the
+    next plugin instance: the patch is re-queued and a retried Allocate replays the answer."""
+    path = str(tmp_path / "j.jsonl")
+    j = AllocJournal(path)
+    ids = [f"GPU-0-_-{i}" for i in range(5)]
+    req = api.AllocateRequest(container_requests=[api.ContainerAllocateRequest(devices_ids=ids)])
+    resp = api.AllocateResponse()
+    resp.container_responses.add(envs={const.ENV_RESOURCE_INDEX: "1"})
+    body = resp.SerializeToString()
+    j.record_fast("uid-a", "default", "a", AllocJournal.fast_head("uid-a", "default", "a", body),
+                  req.SerializeToString())
+    j2 = AllocJournal(path)                                  # no close(): killed
+    assert [e["uid"] for e in j2.unlanded()] == ["uid-a"]
+    shuffled = api.AllocateRequest(container_requests=[api.ContainerAllocateRequest(devices_ids=ids[::-1])])
+    uid, got = j2.lookup(shuffled)
+    assert uid == "uid-a" and got().container_responses[0].envs[const.ENV_RESOURCE_INDEX] == "1"
+    assert j2.maybe_replay(ids[3])
