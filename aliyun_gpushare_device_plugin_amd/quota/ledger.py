@@ -103,6 +103,7 @@ class LedgerDir:
         self._pool: list[str] = []
         self._pending: list[tuple[str, list]] = []     # owner records to write behind
         self._cv = threading.Condition()
+        self._writing = 0                      # owner records taken from _pending, not yet on disk
         self._thread = None
 
     def prepare(self) -> None:
@@ -127,12 +128,15 @@ class LedgerDir:
                 while not self._pending and len(self._pool) >= self.pool_size:
                     self._cv.wait()
                 todo, self._pending = self._pending, []
+                self._writing = len(todo)
                 short = self.pool_size - len(self._pool)
             for lkey, pods in todo:
                 try:
                     self._write_owners(lkey, pods)
                 except OSError:
                     pass
+            with self._cv:
+                self._writing = 0
             for _ in range(max(0, short)):
                 lkey = self.new_key()
                 try:
@@ -203,7 +207,7 @@ class LedgerDir:
         t = time.monotonic() + timeout
         while time.monotonic() < t:
             with self._cv:
-                if not self._pending:
+                if not self._pending and not self._writing:
                     return True
             time.sleep(0.005)
         return False

@@ -33,9 +33,16 @@
 // A forked child starts with an empty allocation table and its own slot (a child does not
 // inherit its parent's KFD allocations).
 //
+// The render node is the second way to HBM: a container is handed /dev/dri/renderD<n> (for
+// libdrm / Mesa / video) and DRM_IOCTL_AMDGPU_GEM_CREATE with the VRAM domain allocates HBM
+// there, outside KFD. In kfd mode those buffer objects are charged too (per render-node fd and
+// GEM handle) and released on DRM_IOCTL_GEM_CLOSE or when that fd is closed.
+//
 // Limits (documented, by construction): enforcement is cooperative — a process that drops
 // LD_PRELOAD or issues the ioctl through a raw syscall is not charged. Memory imported from
-// another process (dma-buf / IPC) is charged to its exporter only.
+// another process (dma-buf / IPC) is charged to its exporter only. KFD allocations issued
+// while the shim itself is initialising (the runtime's own start-up, reached from init) pass
+// uncharged.
 //
 // The library does not link libamdhip64 or libhsa-runtime64: the real entry points are
 // resolved at run time from whichever runtime the process loaded (PyTorch ships its own copy).
@@ -58,6 +65,8 @@
 #include <string.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
+#include <sys/syscall.h>
+#include <sys/sysmacros.h>
 #include <unistd.h>
 
 #include <atomic>
@@ -104,6 +113,28 @@ constexpr unsigned long kIocAlloc = kfd_ioc(3, 0x16, sizeof(KfdAllocArgs));  // 
 constexpr unsigned long kIocFree = kfd_ioc(1, 0x17, sizeof(KfdFreeArgs));    // AMDKFD_IOW(0x17)
 static_assert(sizeof(KfdAllocArgs) == 40 && sizeof(KfdFreeArgs) == 8, "KFD uapi layout");
 
+// ---- amdgpu DRM uapi (drm/amdgpu_drm.h, drm/drm.h) -----------------------------------------
+struct DrmGemCreateIn {   // union drm_amdgpu_gem_create: in {bo_size, alignment, domains, domain_flags}
+  uint64_t bo_size;       //                              out {u32 handle, u32 _pad} (overlays bo_size)
+  uint64_t alignment;
+  uint64_t domains;
+  uint64_t domain_flags;
+};
+struct DrmGemClose {      // struct drm_gem_close
+  uint32_t handle;
+  uint32_t pad;
+};
+constexpr unsigned long drm_ioc(unsigned dir, unsigned nr, unsigned size) {
+  return ((unsigned long)dir << 30) | ((unsigned long)size << 16) | ((unsigned long)'d' << 8) | nr;
+}
+constexpr unsigned long kDrmGemCreate = drm_ioc(3, 0x40 + 0x00, sizeof(DrmGemCreateIn));  // DRM_IOCTL_AMDGPU_GEM_CREATE
+constexpr unsigned long kDrmGemClose = drm_ioc(1, 0x09, sizeof(DrmGemClose));              // DRM_IOCTL_GEM_CLOSE
+constexpr uint64_t kAmdgpuDomainVram = 0x4;                                               // AMDGPU_GEM_DOMAIN_VRAM
+static_assert(sizeof(DrmGemCreateIn) == 32 && sizeof(DrmGemClose) == 8, "DRM uapi layout");
+constexpr int kMaxDrmFd = 4096;
+// table key of a GEM handle: bit 63 set (KFD handles are gpu_id << 32 | idr, bit 63 clear)
+inline uint64_t gem_key(int fd, uint32_t h) { return (1ull << 63) | ((uint64_t)(uint32_t)fd << 32) | h; }
+
 struct Slot {
   std::atomic<int32_t> pid;
   int32_t pad;
@@ -136,6 +167,11 @@ struct State {
 
 State g;
 pthread_once_t g_once = PTHREAD_ONCE_INIT;
+// init() in progress (any thread): an ioctl reached from it (the runtime starting up under a
+// HIP call the shim makes) must not wait on the once-control held by that same init
+std::atomic<bool> g_initializing{false};
+std::atomic<int> g_env_mode{-1};          // GPUSHARE_SHIM_MODE read without initialising
+std::atomic<uint8_t> g_drm_fd[kMaxDrmFd];  // 1 = this fd holds charged GEM handles
 std::atomic<bool> g_released{false};  // set by the atexit handler (see release_slot_at_exit)
 thread_local int t_depth = 0;  // re-entrancy guard (HIP calling itself through the PLT)
 
@@ -428,6 +464,22 @@ uint64_t kfd_vram_bytes(uint32_t gpu_id) {
   return out;
 }
 
+// HBM bytes of the GPU behind render-node fd ``fd`` (amdgpu sysfs), 0 when unknown.
+uint64_t render_vram_bytes(int fd) {
+  struct stat st;   // raw syscall: glibc's fstat is versioned GLIBC_2.33, newer than tenant images'
+  if (syscall(SYS_fstat, fd, &st) != 0 || !S_ISCHR(st.st_mode)) return 0;
+  char path[256], buf[64];
+  const char* root = getenv("GPUSHARE_KFD_SYSFS");
+  snprintf(path, sizeof path, "%s/sys/dev/char/%u:%u/device/mem_info_vram_total", root ? root : "",
+           (unsigned)major(st.st_rdev), (unsigned)minor(st.st_rdev));
+  FILE* f = fopen(path, "re");
+  if (!f) return 0;
+  unsigned long long v = 0;
+  if (!fgets(buf, sizeof buf, f) || sscanf(buf, "%llu", &v) != 1) v = 0;
+  fclose(f);
+  return v;
+}
+
 void set_quota_from_device_bytes(uint64_t tot) {
   if (!tot || !g.ctr || !g.dev) return;
   uint64_t q = (uint64_t)((__uint128_t)tot * g.ctr / g.dev);
@@ -467,10 +519,31 @@ void atfork_child() {
       sl.used.store(0);
     }
   }
+  for (auto& fl : g_drm_fd) fl.store(0, std::memory_order_relaxed);   // the parent's GEM handles are the parent's
   g.slot = acquire_slot(g.ledger);
 }
 
+// The accounting mode from the environment, without running init(): the ioctl interposer
+// must know whether it charges at all before it may touch the once-control.
+int env_mode() {
+  int m = g_env_mode.load(std::memory_order_relaxed);
+  if (m < 0) {
+    const char* v = getenv("GPUSHARE_SHIM_MODE");
+    m = (v && !strcmp(v, "hip")) ? kModeHip : kModeKfd;
+    g_env_mode.store(m, std::memory_order_relaxed);
+  }
+  return m;
+}
+
+void init_body();
+
 void init() {
+  g_initializing.store(true);
+  init_body();
+  g_initializing.store(false);
+}
+
+void init_body() {
   g.log = (int)env_u64("GPUSHARE_SHIM_LOG", 0);
   const char* dis = getenv("CGPU_DISABLE");
   if (dis && !strcmp(dis, "true")) {
@@ -610,6 +683,54 @@ int kfd_alloc(ioctl_t f, int fd, unsigned long req, KfdAllocArgs* a) {
   return r;
 }
 
+// ---- render node (amdgpu GEM) ---------------------------------------------------------------
+int gem_create(ioctl_t f, int fd, unsigned long req, DrmGemCreateIn* a) {
+  if (!(a->domains & kAmdgpuDomainVram) || fd < 0 || fd >= kMaxDrmFd) return f(fd, req, a);
+  uint64_t c = round_up(a->bo_size, 4096);
+  if (!g.quota.load(std::memory_order_relaxed)) set_quota_from_device_bytes(render_vram_bytes(fd));
+  if (!g.quota.load(std::memory_order_relaxed)) {
+    logf(1, "GEM VRAM %llu bytes before the quota is known: not charged", (unsigned long long)c);
+    return f(fd, req, a);
+  }
+  if (!charge(c)) {
+    logf(1, "deny GEM VRAM %llu bytes on fd %d: used %llu of %llu", (unsigned long long)c, fd,
+         (unsigned long long)g.ledger->total.load(), (unsigned long long)g.quota.load());
+    errno = ENOMEM;
+    return -1;
+  }
+  int r = f(fd, req, a);
+  if (r != 0) {
+    int err = errno;
+    uncharge(c);
+    errno = err;
+    return r;
+  }
+  uint32_t h = reinterpret_cast<DrmGemClose*>(a)->handle;   // out.handle overlays bo_size
+  g_drm_fd[fd].store(1, std::memory_order_relaxed);
+  track(gem_key(fd, h), c);
+  logf(2, "gem create %llu bytes VRAM on fd %d -> handle %u, used %llu", (unsigned long long)c, fd, h,
+       (unsigned long long)g.ledger->total.load());
+  return r;
+}
+
+// A closed render-node fd drops every GEM handle it held: uncharge them all.
+void gem_fd_closed(int fd) {
+  uint64_t freed = 0;
+  for (auto& s : g_shards) {
+    pthread_mutex_lock(&s.mu);
+    for (size_t i = 0; i < s.cap; ++i) {
+      uint64_t k = s.keys[i];
+      if (k != kEmpty && k != kDeleted && (k >> 63) && (uint32_t)(k >> 32 & 0x7fffffff) == (uint32_t)fd) {
+        freed += s.vals[i];
+        s.keys[i] = kDeleted;
+      }
+    }
+    pthread_mutex_unlock(&s.mu);
+  }
+  uncharge(freed);
+  logf(2, "render fd %d closed: %llu GEM bytes released", fd, (unsigned long long)freed);
+}
+
 }  // namespace
 
 // ---- interposed libc ioctl (kfd mode) ------------------------------------------------------
@@ -623,12 +744,25 @@ GS_EXPORT int ioctl(int fd, unsigned long req, ...) {
     errno = ENOSYS;
     return -1;
   }
-  if ((req != kIocAlloc && req != kIocFree) || !arg || !enabled() || g.mode != kModeKfd) return f(fd, req, arg);
-  if (req == kIocAlloc) {
-    auto* a = static_cast<KfdAllocArgs*>(arg);
-    if (!(a->flags & kKfdVram)) return f(fd, req, arg);
-    return kfd_alloc(f, fd, req, a);
+  // Cheap filters first, and never the once-control while init() runs (the runtime may start
+  // up underneath it and allocate through here: waiting on that init would deadlock).
+  if ((req != kIocAlloc && req != kIocFree && req != kDrmGemCreate && req != kDrmGemClose) || !arg ||
+      env_mode() != kModeKfd || g_initializing.load(std::memory_order_acquire))
+    return f(fd, req, arg);
+  if (req == kIocAlloc && !(static_cast<KfdAllocArgs*>(arg)->flags & kKfdVram)) return f(fd, req, arg);
+  if (!enabled()) return f(fd, req, arg);
+  if (req == kDrmGemCreate) return gem_create(f, fd, req, static_cast<DrmGemCreateIn*>(arg));
+  if (req == kDrmGemClose) {
+    uint32_t gh = static_cast<DrmGemClose*>(arg)->handle;
+    int r = f(fd, req, arg);
+    if (r == 0 && fd >= 0 && fd < kMaxDrmFd && g_drm_fd[fd].load(std::memory_order_relaxed)) {
+      uint64_t c = untrack(gem_key(fd, gh));
+      uncharge(c);
+      if (c) logf(2, "gem close fd %d handle %u -> %llu bytes", fd, gh, (unsigned long long)c);
+    }
+    return r;
   }
+  if (req == kIocAlloc) return kfd_alloc(f, fd, req, static_cast<KfdAllocArgs*>(arg));
   uint64_t h = static_cast<KfdFreeArgs*>(arg)->handle;
   int r = f(fd, req, arg);
   if (r == 0) {
@@ -638,6 +772,27 @@ GS_EXPORT int ioctl(int fd, unsigned long req, ...) {
          (unsigned long long)g.ledger->total.load());
   }
   return r;
+}
+
+// ---- interposed libc close (render-node fds with charged GEM handles) ----------------------
+using close_t = int (*)(int);
+
+GS_EXPORT int close(int fd) {
+  static std::atomic<close_t> real{nullptr};
+  close_t f = real.load(std::memory_order_acquire);
+  if (!f) {
+    f = reinterpret_cast<close_t>(dlsym(RTLD_NEXT, "close"));
+    real.store(f, std::memory_order_release);
+  }
+  if (fd >= 0 && fd < kMaxDrmFd && g_drm_fd[fd].load(std::memory_order_relaxed)) {
+    int r = f(fd);
+    if (r == 0) {
+      g_drm_fd[fd].store(0, std::memory_order_relaxed);
+      gem_fd_closed(fd);
+    }
+    return r;
+  }
+  return f ? f(fd) : (errno = ENOSYS, -1);
 }
 
 // ---- interposed HIP API --------------------------------------------------------------------

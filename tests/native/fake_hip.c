@@ -23,8 +23,32 @@ static size_t g_total = (size_t)16 << 30, g_used = 0;
 static uint64_t g_sizes[MAXH];
 static uint64_t g_next = 1;
 
+/* amdgpu render node: DRM_IOCTL_AMDGPU_GEM_CREATE / DRM_IOCTL_GEM_CLOSE */
+struct gem_create { uint64_t bo_size, alignment, domains, domain_flags; };
+struct gem_close { uint32_t handle, pad; };
+#define DIOC(dir, nr, sz) (((unsigned long)(dir) << 30) | ((unsigned long)(sz) << 16) | ((unsigned long)'d' << 8) | (nr))
+#define GEM_CREATE DIOC(3, 0x40, sizeof(struct gem_create))
+#define GEM_CLOSE DIOC(1, 0x09, sizeof(struct gem_close))
+static uint64_t g_gem_sizes[4096];
+static uint32_t g_gem_next = 1;
+
 int ioctl(int fd, unsigned long req, ...) {
   va_list ap; va_start(ap, req); void* arg = va_arg(ap, void*); va_end(ap);
+  if (req == GEM_CREATE) {
+    struct gem_create* a = (struct gem_create*)arg;
+    uint64_t n = a->bo_size, vram = a->domains & 0x4;
+    if (vram && __atomic_add_fetch(&g_used, n, __ATOMIC_ACQ_REL) > g_total) {
+      __atomic_fetch_sub(&g_used, n, __ATOMIC_ACQ_REL); errno = ENOMEM; return -1;
+    }
+    uint32_t h = __atomic_fetch_add(&g_gem_next, 1, __ATOMIC_ACQ_REL) % 4096;
+    g_gem_sizes[h] = vram ? n : 0;
+    memset(a, 0, sizeof *a); *(uint32_t*)a = h; return 0;
+  }
+  if (req == GEM_CLOSE) {
+    uint32_t h = ((struct gem_close*)arg)->handle % 4096;
+    __atomic_fetch_sub(&g_used, __atomic_exchange_n(&g_gem_sizes[h], 0, __ATOMIC_ACQ_REL), __ATOMIC_ACQ_REL);
+    return 0;
+  }
   if (req == KFD_ALLOC) {
     struct kfd_alloc* a = (struct kfd_alloc*)arg;
     size_t cur = __atomic_load_n(&g_used, __ATOMIC_RELAXED);
@@ -71,7 +95,15 @@ hipError_t hipMemPoolTrimTo(void* pool, size_t keep) {
   while (g_npool && cached > keep) { --g_npool; cached -= g_pool[g_npool].n; kfd_release(g_pool[g_npool].h); }
   return 0;
 }
-hipError_t hipMemGetInfo(size_t* f, size_t* t) { *f = g_total - __atomic_load_n(&g_used, __ATOMIC_ACQUIRE); *t = g_total; return 0; }
+/* FAKE_HIP_INIT_KFD=1: the first call initialises the "runtime", which allocates VRAM through
+   the KFD ioctl the way ROCr does while the shim may still be inside its own init */
+static int g_inited = 0;
+static void runtime_init(void) {
+  if (__atomic_exchange_n(&g_inited, 1, __ATOMIC_ACQ_REL)) return;
+  const char* v = getenv("FAKE_HIP_INIT_KFD");
+  if (v && *v == '1') { uint64_t h; kfd((size_t)2 << 20, &h); }
+}
+hipError_t hipMemGetInfo(size_t* f, size_t* t) { runtime_init(); *f = g_total - __atomic_load_n(&g_used, __ATOMIC_ACQUIRE); *t = g_total; return 0; }
 hipError_t hipDeviceTotalMem(size_t* b, int d) { *b = g_total; return 0; }
 hipError_t hipMemCreate(uint64_t* h, size_t n, const void* prop, unsigned long long fl) { return kfd(n, h); }
 hipError_t hipMemRelease(uint64_t h) { kfd_release(h); return 0; }

@@ -7,8 +7,12 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <sys/ioctl.h>
 #include <sys/wait.h>
 #include <unistd.h>
+static int g_render_fd = -1;
 typedef int hipError_t;
 hipError_t hipMalloc(void**, size_t); hipError_t hipFree(void*);
 hipError_t hipMemGetInfo(size_t*, size_t*); hipError_t hipMallocAsync(void**, size_t, void*);
@@ -63,6 +67,17 @@ int main(int argc, char** argv) {
       uint64_t u = 0, q = 0, d = 0, pk = 0; int e = f ? f(&u, &q, &d, &pk) : -1;
       printf("{\"op\":\"stats\",\"enabled\":%d,\"used\":%llu,\"quota\":%llu,\"denied\":%llu,\"peak\":%llu}\n", e,
              (unsigned long long)u, (unsigned long long)q, (unsigned long long)d, (unsigned long long)pk); }
+    else if (!strcmp(argv[i], "gem")) {   /* "gem BYTES DOMAINS": amdgpu GEM_CREATE on the render fd */
+      static int rfd = -1; if (rfd < 0) rfd = open("/dev/null", O_RDWR);
+      struct { uint64_t size, align, domains, flags; } a = {strtoull(argv[i + 1], 0, 10), 4096, strtoull(argv[i + 2], 0, 10), 0};
+      unsigned long req = ((unsigned long)3 << 30) | ((unsigned long)32 << 16) | ((unsigned long)'d' << 8) | 0x40;
+      int r = ioctl(rfd, req, &a); i += 2; g_render_fd = rfd;
+      printf("{\"op\":\"gem\",\"err\":%d,\"handle\":%u,\"fd\":%d}\n", r ? errno : 0, r ? 0u : *(uint32_t*)&a, rfd); }
+    else if (!strcmp(argv[i], "gemclose")) { struct { uint32_t h, pad; } c = {(uint32_t)atoi(argv[++i]), 0};
+      unsigned long req = ((unsigned long)1 << 30) | ((unsigned long)8 << 16) | ((unsigned long)'d' << 8) | 0x09;
+      int r = ioctl(g_render_fd, req, &c); printf("{\"op\":\"gemclose\",\"err\":%d}\n", r); }
+    else if (!strcmp(argv[i], "closefd")) { int r = close(g_render_fd); g_render_fd = -1;
+      printf("{\"op\":\"closefd\",\"err\":%d}\n", r); }
     else if (!strcmp(argv[i], "sleep")) { usleep((useconds_t)(atof(argv[++i]) * 1e6)); }
     else if (!strcmp(argv[i], "crash")) { fflush(stdout); _exit(3); }
     fflush(stdout);

@@ -257,3 +257,70 @@ def test_hbm_used_gauge_matches_sysfs():
             del held
         finally:
             mon.stop()
+
+
+_GEM_CHILD = r'''
+import ctypes, json, os, sys, time
+minor, sizes = int(sys.argv[1]), [int(x) for x in sys.argv[2:]]
+libc = ctypes.CDLL(None, use_errno=True)          # global lookup: the preloaded shim's ioctl
+fd = os.open(f"/dev/dri/renderD{minor}", os.O_RDWR)
+used_path = f"/sys/class/drm/renderD{minor}/device/mem_info_vram_used"
+class Create(ctypes.Structure):
+    _fields_ = [("bo_size", ctypes.c_uint64), ("alignment", ctypes.c_uint64), ("domains", ctypes.c_uint64),
+                ("domain_flags", ctypes.c_uint64)]
+class Close(ctypes.Structure):
+    _fields_ = [("handle", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
+CREATE = (3 << 30) | (32 << 16) | (ord("d") << 8) | 0x40     # DRM_IOCTL_AMDGPU_GEM_CREATE
+CLOSE = (1 << 30) | (8 << 16) | (ord("d") << 8) | 0x09       # DRM_IOCTL_GEM_CLOSE
+libc.ioctl.argtypes = [ctypes.c_int, ctypes.c_ulong, ctypes.c_void_p]
+stats = libc.gpushare_shim_stats
+stats.argtypes = [ctypes.POINTER(ctypes.c_uint64)] * 4
+def ledger():
+    u, q, d, p = (ctypes.c_uint64() for _ in range(4))
+    stats(ctypes.byref(u), ctypes.byref(q), ctypes.byref(d), ctypes.byref(p))
+    return u.value, d.value
+def dev():
+    return int(open(used_path).read())
+handles = []
+for n in sizes:
+    before, dev0 = ledger()[0], dev()
+    a = Create(n, 4096, 0x4, 0)                               # AMDGPU_GEM_DOMAIN_VRAM
+    r = libc.ioctl(fd, CREATE, ctypes.addressof(a))
+    err = ctypes.get_errno() if r else 0
+    time.sleep(0.05)
+    after, denied = ledger()
+    h = ctypes.cast(ctypes.pointer(a), ctypes.POINTER(ctypes.c_uint32))[0] if r == 0 else None
+    if h is not None:
+        handles.append(h)
+    print(json.dumps({"size": n, "rc": r, "errno": err, "charge": after - before, "device_delta": dev() - dev0,
+                      "denied": denied}), flush=True)
+for h in handles:
+    before = ledger()[0]
+    c = Close(h, 0)
+    libc.ioctl(fd, CLOSE, ctypes.addressof(c))
+    print(json.dumps({"closed": h, "released": before - ledger()[0]}), flush=True)
+os.close(fd)
+'''
+
+
+def test_shim_charges_render_node_gem_vram():
+    """Round-2 review item 5: HBM allocated on the container's render node (amdgpu GEM_CREATE,
+    VRAM domain; a raw ioctl through ctypes, no HIP) is charged to the container's quota: within
+    quota the charge equals the device's VRAM delta, over quota it is refused with ENOMEM, and
+    GEM_CLOSE releases it."""
+    from aliyun_gpushare_device_plugin_amd.utils.native import lib_path
+
+    with S.SMI("auto") as smi:
+        minor = smi.device(0).render_minor
+    env = dict(os.environ, LD_PRELOAD=lib_path("hipshim"), GPUSHARE_QUOTA_BYTES=str(4 * GIB),
+               GPUSHARE_SHIM_LOG="1")
+    r = subprocess.run([sys.executable, "-c", _GEM_CHILD, str(minor), str(2 * GIB), str(3 * GIB), str(GIB)],
+                       env=env, capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rows = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    ok2, over, ok1 = rows[:3]
+    assert ok2["rc"] == 0 and ok2["charge"] == 2 * GIB
+    assert abs(ok2["device_delta"] - 2 * GIB) <= 64 * MIB, ok2         # the device saw the same 2 GiB
+    assert over["rc"] != 0 and over["errno"] == 12 and over["denied"] >= 1 and over["charge"] == 0
+    assert ok1["rc"] == 0 and ok1["charge"] == GIB
+    assert [x["released"] for x in rows[3:]] == [2 * GIB, GIB]

@@ -330,3 +330,38 @@ def test_per_container_ledger_dirs_and_gc_after_sigkill(stub, native_shim, tmp_p
             if p.poll() is None:
                 p.kill()
             p.wait(timeout=10)
+
+
+def test_render_node_gem_vram_is_charged(stub, native_shim):
+    """Round-2 review item 5: VRAM allocated on the container's render node
+    (DRM_IOCTL_AMDGPU_GEM_CREATE, VRAM domain) is charged like KFD allocations: over quota it
+    is refused with ENOMEM, GEM_CLOSE releases it, closing the render fd releases the rest;
+    GTT-only buffer objects are not charged."""
+    vram, gtt = 4, 2
+    out, r = run(stub, native_shim, ["alloc", 1 * GIB, "gem", 2 * GIB, vram, "stats", "gem", 2 * GIB, vram,
+                                     "gem", 8 * GIB, gtt, "stats", "gemclose", 1, "stats", "gem", 1 * GIB, vram,
+                                     "closefd", "stats"],
+                 GPUSHARE_QUOTA_BYTES=4 * GIB)
+    assert out[0]["err"] == 0
+    assert out[1]["err"] == 0 and out[2]["used"] == 3 * GIB
+    assert out[3]["err"] == 12                               # ENOMEM: 3 + 2 > 4 GiB
+    assert out[4]["err"] == 0 and out[5]["used"] == 3 * GIB  # GTT: not HBM, not charged
+    assert out[6]["err"] == 0 and out[7]["used"] == 1 * GIB  # GEM_CLOSE of the 2 GiB VRAM object
+    assert out[8]["err"] == 0 and out[9]["err"] == 0
+    assert out[10]["used"] == 1 * GIB                        # fd closed: its GEM objects are gone
+
+
+def test_hip_mode_runtime_init_under_shim_init_does_not_deadlock(stub, native_shim):
+    """ADVICE (round 2): in hip mode without GPUSHARE_QUOTA_BYTES the shim's init calls the real
+    hipMemGetInfo; if that starts the runtime, which allocates VRAM through the (interposed)
+    KFD ioctl on the same thread, the ioctl must not wait on the shim's own once-control."""
+    out, r = run(stub, native_shim, ["alloc", 1 * GIB, "info"], ALIYUN_COM_GPU_MEM_CONTAINER=4,
+                 ALIYUN_COM_GPU_MEM_DEV=16, GPUSHARE_SHIM_MODE="hip", FAKE_HIP_INIT_KFD=1)
+    assert r.returncode == 0, r.stderr
+    assert out[0]["err"] == 0 and out[1]["total"] == 4 * GIB
+
+
+def test_kfd_mode_allocation_during_shim_init_passes(stub, native_shim):
+    out, r = run(stub, native_shim, ["info", "alloc", 1 * GIB, "stats"], GPUSHARE_QUOTA_BYTES=4 * GIB,
+                 FAKE_HIP_INIT_KFD=1)
+    assert r.returncode == 0 and out[1]["err"] == 0 and out[2]["used"] >= 1 * GIB
