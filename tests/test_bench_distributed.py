@@ -48,6 +48,12 @@ def test_bench_torchrun_two_ranks_gloo():
     # N>1: the topology the plugin exported and an all-reduce on the TP pair best_group picks
     topo = d["topology"]
     assert topo["tp_pair"] == [0, 1] and topo["pair_link"] == "xgmi" and topo["pair_hops"] == 1
+    assert topo["verdict"] == "pass" and topo["reasons"] == []
+    # both plugins measured under the same churn, in the same line
+    uc = d["allocate_under_churn"]
+    assert uc["default"]["admissions"] == uc["reference"]["admissions"] == 8
+    assert uc["reference"]["apiserver_round_trips_on_path"] == 2
+    assert set(d["allocate_p50_ms_by_gpu"]) == {"0", "1"}
     assert topo["tp_pair_allreduce"]["busbw_GBps"] > 0 and topo["backend"] == "gloo"
     # the control-plane A/B is in the same line: default vs the reference's cost model
     ab = d["allocate_by_mode"]
@@ -79,3 +85,33 @@ def test_tp_pair_demo_gloo():
     assert r.returncode == 0, r.stderr[-3000:]
     d = parse(r.stdout)
     assert d["world"] == 2 and d["tp_block_rel_err"] < 1e-3 and d["backend"] == "gloo"
+
+
+def test_bench_fails_loudly_on_a_broken_topology(tmp_path):
+    """Round-2 review item 7: with N>1 a topology export that is not one-hop xGMI on a healthy
+    node (here: a fake 2-GPU node whose pair is PCIe) fails the run (exit 3) while still
+    printing its measurement line with the verdict."""
+    spec = tmp_path / "pcie.json"
+    spec.write_text(json.dumps({"devices": [{"vram_total": 288 << 30}, {"vram_total": 288 << 30}], "xgmi": "none"}))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", "2",
+                        "--no-gpu", "--steps", "2", "--warmup", "0", "--smi-backend", f"fake:{spec}",
+                        "--compare-rtts", "", "--fill-orders", ""],
+                       cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode != 0
+    d = parse(r.stdout)
+    assert d["topology"]["verdict"] == "fail" and "pcie" in d["topology"]["reasons"][0]
+    assert "topology verdict FAIL" in r.stderr
+
+
+def test_topology_verdict_rules():
+    from aliyun_gpushare_device_plugin_amd.parallel import topology as T
+
+    full = {"link_type": [["self", "xgmi"], ["xgmi", "self"]], "hops": [[0, 1], [1, 0]]}
+    assert T.verdict(full, 2) == (True, [])
+    assert not T.verdict(None, 2)[0]
+    assert "expected 4x4" in T.verdict(full, 4)[1][0]
+    pcie = {"link_type": [["self", "pcie"], ["pcie", "self"]], "hops": [[0, 3], [3, 0]]}
+    assert not T.verdict(pcie, 2)[0]
+    assert T.verdict(pcie, 2, healthy=[True, False]) == (True, [])     # a sick GPU excuses its links
