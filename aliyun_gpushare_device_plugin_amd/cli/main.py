@@ -89,6 +89,13 @@ def build_parser() -> argparse.ArgumentParser:
                    help="when several pending pods could own an Allocate request, ask the kubelet's "
                         "pod-resources List which pod is being admitted (it holds no IDs yet) instead of "
                         "guessing by assume time (default true; needs --pod-resources-socket)")
+    p.add_argument("--quota-enforcement", default="report", choices=("off", "report", "kill"),
+                   help="node-side quota watchdog over the kernel's per-process HBM (DRM fdinfo): report "
+                        "pods above their share, or also SIGKILL their largest GPU process (the shim cannot be "
+                        "bypassed this way; needs hostPID)")
+    p.add_argument("--quota-watch-interval", type=float, default=10.0)
+    p.add_argument("--quota-slack-mib", type=int, default=256,
+                   help="HBM above a pod's share tolerated by the watchdog (runtime overhead)")
     p.add_argument("--placement-interval", type=float, default=2.0,
                    help="seconds between periodic placement-truth passes (besides PreStartContainer)")
     p.add_argument("--sync-patch", action="store_true",
@@ -118,7 +125,8 @@ def config_from_args(a) -> PluginConfig:
         partition_aware=a.partition_aware, ledger_dir=a.ledger_dir, ledger_scan_s=a.ledger_scan_interval,
         journal_path=a.journal_path, compute_isolation=a.compute_isolation,
         pod_resources_socket=a.pod_resources_socket, placement_s=a.placement_interval,
-        admission_identity=a.admission_identity)
+        admission_identity=a.admission_identity, quota_enforcement=a.quota_enforcement,
+        quota_watch_s=a.quota_watch_interval, quota_slack_mib=a.quota_slack_mib)
 
 
 def install_shim(dest_dir: str) -> str:

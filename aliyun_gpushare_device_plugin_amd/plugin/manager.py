@@ -75,6 +75,9 @@ class PluginConfig:
     pod_resources_socket: str = "auto"
     placement_s: float = 2.0
     admission_identity: bool = True      # which pod is being admitted, from pod-resources (engine)
+    quota_enforcement: str = "report"    # quota/watchdog.py: off | report | kill
+    quota_watch_s: float = 10.0
+    quota_slack_mib: int = 256
     mps: bool = False                    # accepted for flag compatibility; ignored
 
 
@@ -99,6 +102,8 @@ class SharedGPUManager:
         self._metrics_srv = None
         self._ledger_thread = None
         self._ledger_stop = threading.Event()
+        self.watchdog = None
+        self._cgpu_disabled = False
 
     # ------------------------------------------------------------------------------------
     def _kubelet_socket(self) -> str:
@@ -173,6 +178,7 @@ class SharedGPUManager:
         else:
             # rebuild: keep claims, assigned pods, queued patches and the patcher thread
             self.allocator.reconfigure(model, src, self.client, opts)
+        self._cgpu_disabled = disable_cgpu
         allocator = self.allocator
         if allocator.podres is None:
             allocator.set_pod_resources(self._pod_resources())
@@ -224,6 +230,21 @@ class SharedGPUManager:
             self.metrics.health_events_armed.set(st.get("events_armed", 0))
             self.metrics.health_ecc_readable.set(st.get("ecc_reads_ok", 0))
             self.metrics.health_degraded.set(0 if self.health.ready else 1)
+
+    def _start_watchdog(self):
+        """The node-side quota watchdog (quota/watchdog.py), re-pointed at the current device
+        model and pod source after every rebuild."""
+        from ..quota.watchdog import QuotaWatchdog
+
+        cfg = self.cfg
+        if cfg.quota_enforcement == "off" or self.model is None or self.pod_source is None:
+            return
+        if self.watchdog is None:
+            self.watchdog = QuotaWatchdog(self.model, self.pod_source, self.metrics, cfg.quota_enforcement,
+                                          cfg.quota_watch_s, cfg.quota_slack_mib << 20,
+                                          disabled=lambda: self._cgpu_disabled).start()
+        else:
+            self.watchdog.model, self.watchdog.pods = self.model, self.pod_source
 
     def _start_ledger_collector(self):
         """Export the quota shim's per-container ledgers (--ledger-dir) every ledger_scan_s and
@@ -320,6 +341,7 @@ class SharedGPUManager:
                         return 2
                     self._start_health()
                     self._start_ledger_collector()
+                    self._start_watchdog()
                     restart = False
                     self.started.set()
                 kind, val = self.events.get()
@@ -339,6 +361,8 @@ class SharedGPUManager:
         finally:
             watcher.close()
             self._ledger_stop.set()
+            if self.watchdog is not None:
+                self.watchdog.stop()
             if self.health:
                 self.health.stop()
             if self.plugin is not None:

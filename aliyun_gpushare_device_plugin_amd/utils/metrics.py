@@ -197,6 +197,13 @@ class PluginMetrics:
         self.shim_quota = r.gauge("gpushare_container_hbm_quota_bytes", "Container HBM quota (shim ledger)")
         self.shim_peak = r.gauge("gpushare_container_hbm_peak_bytes", "Container HBM high-water mark (shim ledger)")
         self.shim_denied = r.gauge("gpushare_container_quota_denials", "Allocations refused by the quota shim")
+        # quota watchdog (quota/watchdog.py): kernel-reported HBM per pod vs its share
+        self.quota_violation = r.gauge("gpushare_quota_violation_bytes",
+                                       "HBM a pod holds on a GPU beyond its share (DRM fdinfo), per pod and GPU")
+        self.quota_violations_total = r.counter("gpushare_quota_violations_total", "Quota violations detected")
+        self.quota_kills = r.counter("gpushare_quota_kills_total", "Processes killed by the quota watchdog")
+        self.unaccounted_hbm = r.gauge("gpushare_unaccounted_hbm_bytes",
+                                       "HBM held on a GPU by processes of no pod on this node")
         self.cu_slots_held = r.gauge("gpushare_cu_slots_held",
                                      "CU slots held by pods per GPU at the last compute-isolation decision "
                                      "(slot = one CU on every XCD; > slots per GPU means oversubscribed)")

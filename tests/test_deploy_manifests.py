@@ -101,3 +101,5 @@ def test_daemonset_mounts_match_the_flags():
     for p in (cfg.ledger_dir, cfg.journal_path):
         assert p.startswith("/var/lib/gpushare/")
     assert spec.get("hostNetwork") is True and spec["nodeSelector"] == {"gpushare": "true"}
+    # the quota watchdog reads every GPU process's DRM fdinfo and pod cgroup
+    assert spec.get("hostPID") is True and cfg.quota_enforcement in ("report", "kill")

@@ -324,3 +324,41 @@ def test_shim_charges_render_node_gem_vram():
     assert over["rc"] != 0 and over["errno"] == 12 and over["denied"] >= 1 and over["charge"] == 0
     assert ok1["rc"] == 0 and ok1["charge"] == GIB
     assert [x["released"] for x in rows[3:]] == [2 * GIB, GIB]
+
+
+def test_quota_watchdog_catches_a_process_without_the_shim():
+    """Round-2 review, isolation: a tenant process that drops the quota shim is still seen by
+    the node-side watchdog (amdgpu DRM fdinfo, kernel-reported) and, in kill mode, ended."""
+    import time
+
+    from aliyun_gpushare_device_plugin_amd.quota.watchdog import QuotaWatchdog
+    from aliyun_gpushare_device_plugin_amd.utils.metrics import PluginMetrics
+    from tests.test_allocate_engine import StaticSource, mkpod
+
+    code = ("import torch, sys, time\nx = torch.empty(6 << 30, dtype=torch.uint8, device='cuda')\n"
+            "torch.cuda.synchronize()\nprint('held', flush=True)\ntime.sleep(60)\n")
+    env = {k: v for k, v in os.environ.items() if k != "LD_PRELOAD"}
+    child = subprocess.Popen([sys.executable, "-c", code], env=env, stdout=subprocess.PIPE, text=True)
+    try:
+        assert child.stdout.readline().strip() == "held"
+        with S.SMI("auto") as smi:
+            model = DeviceModel(smi.devices(), const.GIB, "nearest")
+        pod = mkpod("tenant", 4, 0, 10, assigned="true", phase="Running", uid="uid-tenant")   # 4 GiB share
+        m = PluginMetrics()
+        wd = QuotaWatchdog(model, StaticSource([pod]), m, mode="report", slack_bytes=256 << 20,
+                           pid_pod=lambda pid: "uid-tenant" if pid == child.pid else None)
+        v = wd.scan()
+        assert len(v) == 1 and v[0].gpu == 0, v
+        assert 6 * GIB <= v[0].used <= 6 * GIB + 512 * MIB and v[0].allowed < 4.1 * GIB
+        assert m.quota_violation.value(pod_uid="uid-tenant", gpu="0") > 1.5 * GIB
+        wd.mode = "kill"
+        v = wd.scan()
+        assert v[0].killed == [child.pid]
+        child.wait(timeout=20)
+        assert child.returncode == -9
+        time.sleep(0.5)
+        assert wd.scan() == []
+    finally:
+        if child.poll() is None:
+            child.kill()
+            child.wait(timeout=20)
