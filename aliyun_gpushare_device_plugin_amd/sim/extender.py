@@ -52,11 +52,15 @@ class NodeState:
 
 
 class ExtenderSim:
-    def __init__(self, client: APIClient, policy: str = "binpack"):
+    def __init__(self, client: APIClient, policy: str = "binpack", group_ttl_s: float = 300.0):
         self.client = client
         self.policy = policy
         self.nodes: dict[str, NodeState] = {}
         self._placed: dict[str, tuple] = {}   # pod uid -> (node, [(gpu, units)])
+        # TP groups bound one member at a time through the HTTP bind route: the whole group's
+        # xGMI clique is reserved when its first member binds (group -> reservation)
+        self._groups: dict[str, dict] = {}
+        self.group_ttl_s = group_ttl_s
         self._lock = threading.Lock()
 
     # -- cache ----------------------------------------------------------------------------
@@ -89,6 +93,10 @@ class ExtenderSim:
                         st.used[g] += mem
                         parts.append((g, mem))
                 self._placed[O.uid(p)] = (st.name, parts)
+            for r in self._groups.values():      # reserved slots of TP groups still binding
+                st = self.nodes.get(r["node"])
+                for g in (r["free"] if st else []):
+                    st.used[g] += r["req"]
 
     def forget(self, pod: dict):
         with self._lock:
@@ -166,6 +174,9 @@ class ExtenderSim:
         req = O.gpu_mem_of_pod(pod)
         with self._lock:
             names = node_names if node_names is not None else list(self.nodes)
+            if self._group_of(pod) is not None:
+                self._expire_groups_locked(time.monotonic())
+                return [n for n in names if self.group_fits(pod, n)]
             return [n for n in names if n in self.nodes and self._fits(self.nodes[n], req)]
 
     def _choose(self, req: int, node_names=None) -> tuple[str, int] | None:
@@ -255,9 +266,69 @@ class ExtenderSim:
             out.append((name, g))
         return out
 
+    # -- TP groups over the scheduler's one-pod-at-a-time extender protocol ----------------
+    def _expire_groups_locked(self, now: float):
+        for name, r in list(self._groups.items()):
+            if now - r["t"] > self.group_ttl_s:
+                st = self.nodes.get(r["node"])
+                for g in r["free"]:           # reserved for members that never came
+                    if st:
+                        st.used[g] -= r["req"]
+                del self._groups[name]
+
+    def _group_of(self, pod: dict) -> tuple[str, int] | None:
+        labels = (pod.get("metadata") or {}).get("labels") or {}
+        grp = labels.get(TP_GROUP_LABEL)
+        if not grp:
+            return None
+        try:
+            return f"{O.namespace(pod)}/{grp}", max(1, int(labels.get(TP_SIZE_LABEL, "1")))
+        except ValueError:
+            return f"{O.namespace(pod)}/{grp}", 1
+
+    def group_fits(self, pod: dict, node: str) -> bool:
+        """Filter for a TP-group member: the node holds its group's reservation with a slot
+        left, or has a pairwise one-hop xGMI set of GPUs for the whole group."""
+        gk = self._group_of(pod)
+        st = self.nodes.get(node)
+        if gk is None or st is None:
+            return False
+        r = self._groups.get(gk[0])
+        if r is not None:
+            return r["node"] == node and bool(r["free"])
+        return T.best_group(st.topology, st.free(), gk[1], O.gpu_mem_of_pod(pod)) is not None
+
+    def bind_member(self, pod: dict, node: str) -> int | None:
+        """Bind one member of a TP group: reserve the group's clique on ``node`` at the first
+        member (best fit, ``best_group``), hand each member the next GPU of it."""
+        gk = self._group_of(pod)
+        req = O.gpu_mem_of_pod(pod)
+        with self._lock:
+            self._expire_groups_locked(time.monotonic())
+            st = self.nodes.get(node)
+            if st is None:
+                return None
+            r = self._groups.get(gk[0])
+            if r is None or r["node"] != node or not r["free"]:
+                grp = T.best_group(st.topology, st.free(), gk[1], req)
+                if grp is None:
+                    return None
+                for g in grp:
+                    st.used[g] += req
+                r = self._groups[gk[0]] = {"node": node, "free": list(grp), "req": req, "t": time.monotonic()}
+            g = r["free"].pop(0)
+            self._placed[O.uid(pod)] = (node, [(g, req)])
+            if not r["free"]:
+                del self._groups[gk[0]]       # every member placed
+        self.bind(pod, node, g)
+        return g
+
     def usage(self) -> dict:
         with self._lock:
             return {n: {"per_gpu": s.per_gpu, "used": list(s.used)} for n, s in self.nodes.items()}
+
+
+Extender = ExtenderSim          # the deployable name (cli/extender.py); the class is the same
 
 
 def serve_http(ext: ExtenderSim, host: str = "127.0.0.1", port: int = 0):
@@ -293,6 +364,9 @@ def serve_http(ext: ExtenderSim, host: str = "127.0.0.1", port: int = 0):
                 try:
                     pod = ext.client.get_pod(args.get("PodNamespace", "default"), args["PodName"])
                     req = O.gpu_mem_of_pod(pod)
+                    if ext._group_of(pod) is not None:
+                        g = ext.bind_member(pod, args["Node"])
+                        return self._reply({"Error": "" if g is not None else "no xGMI-connected GPU set fits"})
                     with ext._lock:
                         st = ext.nodes.get(args["Node"])
                         fits = ext._fits(st, req) if st else []

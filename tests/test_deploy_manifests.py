@@ -153,3 +153,26 @@ def test_dockerfile_recipe_builds_and_installs(tmp_path):
                        capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stderr[-2000:]
     assert r.stdout.strip().startswith(str(site)) and os.path.exists(r.stdout.strip())
+
+
+def test_scheduler_extender_manifest_matches_the_cli():
+    """The extender Deployment's flags parse, its Service port is the one it listens on, and
+    the KubeSchedulerConfiguration points filter/bind at the routes it serves."""
+    import yaml as _yaml
+
+    from aliyun_gpushare_device_plugin_amd.cli import extender as X
+
+    docs = [d for p, d in _docs() if p.endswith("scheduler-extender.yaml")]
+    dep = next(d for d in docs if d["kind"] == "Deployment")
+    cmd = dep["spec"]["template"]["spec"]["containers"][0]["command"]
+    a = X.build_parser().parse_args(cmd[1:])
+    svc = next(d for d in docs if d["kind"] == "Service")
+    assert svc["spec"]["ports"][0]["targetPort"] == a.port
+    cm = next(d for d in docs if d["kind"] == "ConfigMap")
+    cfg = _yaml.safe_load(cm["data"]["scheduler-config.yaml"])
+    ext = cfg["extenders"][0]
+    assert ext["urlPrefix"].endswith(f":{a.port}/gpushare-scheduler")
+    assert (ext["filterVerb"], ext["bindVerb"]) == ("filter", "bind")
+    assert ext["managedResources"][0]["name"] == const.RESOURCE_NAME
+    rules = next(d for d in docs if d["kind"] == "ClusterRole")["rules"]
+    assert any("pods/binding" in r["resources"] and "create" in r["verbs"] for r in rules)
