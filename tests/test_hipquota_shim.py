@@ -243,12 +243,14 @@ def test_shim_under_sanitizers(stub, tmp_path, san):
     try:
         e = dict(os.environ, **env)
         r = subprocess.run([str(drv), "threads", "8", "200", str(8 * MIB), "alloc", str(GIB), "alloc", str(MIB),
-                            "free", "0", "stats"], env=e, capture_output=True, text=True, timeout=120)
+                            "free", "0", "gem", str(8 * MIB), "4", "gem", str(8 * MIB), "4", "gemclose", "1",
+                            "closefd", "stats"], env=e, capture_output=True, text=True, timeout=120)
         assert r.returncode == 0, r.stderr[-3000:]
         assert "ERROR: AddressSanitizer" not in r.stderr and "WARNING: ThreadSanitizer" not in r.stderr, r.stderr[-3000:]
         assert "runtime error" not in r.stderr, r.stderr[-3000:]
         out = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
         assert out[1]["err"] == 2 and out[2]["err"] == 0 and out[-1]["used"] == 0
+        assert [o["err"] for o in out if o["op"] in ("gem", "gemclose", "closefd")] == [0, 0, 0, 0]
     finally:
         cleanup(name)
 
