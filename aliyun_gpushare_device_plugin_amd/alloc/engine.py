@@ -106,6 +106,10 @@ class AllocatorOptions:
     async_patch: bool = False
     # "cu": per-pod CU-slot masks (alloc/cuslots.py); "none": pods time-slice the whole GPU
     compute_isolation: str = "none"
+    # CDI: also (or instead of DeviceSpecs, expose_devices=False) name the GPU as a CDI device
+    # "<kind>=<index>" — the spec AMD's container toolkit generates (e.g. amd.com/gpu=3) carries
+    # /dev/kfd and the GPU's render node; None = no CDI devices
+    cdi_kind: str | None = None
     # placement truth (alloc/placement.py): periodic pass interval, and how long an answer whose
     # fake IDs no pod holds yet counts as "in flight" (kubelet checkpoint not visible yet)
     placement_s: float = 2.0
@@ -548,6 +552,8 @@ class Allocator:
             r.devices.add(container_path=const.KFD_DEVICE, host_path=const.KFD_DEVICE, permissions="rw")
             if g.render_node:
                 r.devices.add(container_path=g.render_node, host_path=g.render_node, permissions="rw")
+        if self.opts.cdi_kind:
+            r.cdi_devices.add(name=f"{self.opts.cdi_kind}={gpu_index}")
         shim = self.opts.shim
         if shim is not None and shim.enabled and not self.opts.disable_cgpu:
             r.mounts.add(container_path=shim.container_dir, host_path=shim.host_dir, read_only=True)

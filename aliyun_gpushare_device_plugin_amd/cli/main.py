@@ -89,6 +89,11 @@ def build_parser() -> argparse.ArgumentParser:
                    help="when several pending pods could own an Allocate request, ask the kubelet's "
                         "pod-resources List which pod is being admitted (it holds no IDs yet) instead of "
                         "guessing by assume time (default true; needs --pod-resources-socket)")
+    p.add_argument("--cdi-kind", default="",
+                   help="also answer the GPU as a CDI device '<kind>=<index>' (e.g. amd.com/gpu, the spec AMD's "
+                        "container toolkit generates); empty = DeviceSpecs only")
+    p.add_argument("--device-specs", type=_bool, nargs="?", const=True, default=True,
+                   help="answer /dev/kfd and the GPU's render node as DeviceSpecs (false with --cdi-kind: CDI only)")
     p.add_argument("--quota-enforcement", default="report", choices=("off", "report", "kill"),
                    help="node-side quota watchdog over the kernel's per-process HBM (DRM fdinfo): report "
                         "pods above their share, or also SIGKILL their largest GPU process (the shim cannot be "
@@ -126,6 +131,7 @@ def config_from_args(a) -> PluginConfig:
         journal_path=a.journal_path, compute_isolation=a.compute_isolation,
         pod_resources_socket=a.pod_resources_socket, placement_s=a.placement_interval,
         admission_identity=a.admission_identity, quota_enforcement=a.quota_enforcement,
+        cdi_kind=a.cdi_kind, expose_devices=a.device_specs,
         quota_watch_s=a.quota_watch_interval, quota_slack_mib=a.quota_slack_mib)
 
 

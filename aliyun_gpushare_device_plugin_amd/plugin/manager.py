@@ -60,7 +60,8 @@ class PluginConfig:
     strict_allocate: bool = False
     preferred_allocation: bool = False   # opt-in: costs the kubelet one extra RPC per container
     export_topology: bool = True
-    expose_devices: bool = True
+    expose_devices: bool = True          # DeviceSpecs for /dev/kfd + the GPU's render node
+    cdi_kind: str = ""                   # e.g. "amd.com/gpu": also answer CDI device names
     rocr_visible: bool = False
     metrics_addr: str | None = None
     async_patch: bool = True             # write-behind ASSIGNED patch (see AllocatorOptions)
@@ -164,6 +165,7 @@ class SharedGPUManager:
         shim = ShimConfig(cfg.shim_host_dir) if cfg.shim_host_dir else None
         opts = AllocatorOptions(unit=model.unit, disable_cgpu=disable_cgpu, shim=shim,
                                 strict=cfg.strict_allocate, expose_devices=cfg.expose_devices,
+                                cdi_kind=cfg.cdi_kind or None,
                                 rocr_visible=cfg.rocr_visible, async_patch=cfg.async_patch,
                                 complete_swaps=cfg.complete_swaps,
                                 ledger_dir=cfg.ledger_dir if shim else None,

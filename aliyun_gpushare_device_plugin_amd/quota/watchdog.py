@@ -184,6 +184,9 @@ class QuotaWatchdog:
         out = []
         if self.metrics is not None:
             self.metrics.quota_violation.clear()
+            self.metrics.pod_hbm_used.clear()
+            for (uid, gi), procs in usage.items():
+                self.metrics.pod_hbm_used.set(sum(n for _, n in procs), pod_uid=uid, gpu=str(gi))
             for g in self.model.gpus:
                 self.metrics.unaccounted_hbm.set(unaccounted.get(g.index, 0), gpu=str(g.index))
         for (uid, gi), procs in usage.items():

@@ -200,6 +200,8 @@ class PluginMetrics:
         # quota watchdog (quota/watchdog.py): kernel-reported HBM per pod vs its share
         self.quota_violation = r.gauge("gpushare_quota_violation_bytes",
                                        "HBM a pod holds on a GPU beyond its share (DRM fdinfo), per pod and GPU")
+        self.pod_hbm_used = r.gauge("gpushare_pod_hbm_used_bytes",
+                                    "HBM a pod's processes hold on a GPU (kernel-reported, DRM fdinfo)")
         self.quota_violations_total = r.counter("gpushare_quota_violations_total", "Quota violations detected")
         self.quota_kills = r.counter("gpushare_quota_kills_total", "Processes killed by the quota watchdog")
         self.unaccounted_hbm = r.gauge("gpushare_unaccounted_hbm_bytes",

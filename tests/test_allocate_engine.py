@@ -420,3 +420,14 @@ def test_journal_replays_retried_admission(tmp_path):
         if p["metadata"]["name"] == "a":
             p["status"]["phase"] = "Running"
     assert dict(al2.allocate(r).container_responses[0].envs)[const.ENV_RESOURCE_INDEX] == "0"
+
+
+def test_cdi_device_names():
+    """--cdi-kind: the GPU is also named as a CDI device (the spec AMD's container toolkit
+    generates carries /dev/kfd and its render node); with DeviceSpecs off it is the only one."""
+    al, _, _ = make([mkpod("p", 2, 1, 10)], cdi_kind="amd.com/gpu")
+    r = al.allocate(req(2)).container_responses[0]
+    assert [c.name for c in r.cdi_devices] == ["amd.com/gpu=1"] and len(r.devices) >= 1
+    al2, _, _ = make([mkpod("p", 2, 0, 10)], cdi_kind="amd.com/gpu", expose_devices=False)
+    r2 = al2.allocate(req(2)).container_responses[0]
+    assert [c.name for c in r2.cdi_devices] == ["amd.com/gpu=0"] and len(r2.devices) == 0

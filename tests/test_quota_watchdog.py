@@ -57,6 +57,8 @@ def test_within_share_is_quiet_and_foreign_use_is_exported(tmp_path):
     wd, m = _setup(tmp_path, 3 * GIB)
     assert wd.scan() == []
     assert m.unaccounted_hbm.value(gpu="1") == GIB and m.unaccounted_hbm.value(gpu="0") == 0
+    assert m.pod_hbm_used.value(pod_uid=UID_A, gpu="1") == 3 * GIB
+    assert m.pod_hbm_used.value(pod_uid=UID_B, gpu="1") == 6 * GIB
 
 
 def test_over_share_is_reported(tmp_path):
