@@ -258,8 +258,11 @@ class SimCluster:
     # -- pod flow -------------------------------------------------------------------------
     def create_pod(self, gpu_mem, name: str | None = None, labels: dict | None = None,
                    annotations: dict | None = None) -> dict:
-        return self.client.create_pod("default", pod_spec(name or f"pod-{next(self._seq)}", gpu_mem, labels=labels,
-                                                          annotations=annotations))
+        pod = self.client.create_pod("default", pod_spec(name or f"pod-{next(self._seq)}", gpu_mem, labels=labels,
+                                                         annotations=annotations))
+        if self.extender is not None:
+            self.extender.note_pending(pod)       # what the extender's pod informer sees
+        return pod
 
     def schedule(self, pod: dict, node_names: list | None = None):
         return self.extender.schedule(pod, node_names)

@@ -7,7 +7,9 @@ allocatable[gpu-count]`` (the inspect arithmetic, ``cmd/inspect/nodeinfo.go:116,
 the extender picks a node and a GPU index, writes ``ALIYUN_COM_GPU_MEM_IDX/_POD/
 _ASSUME_TIME`` and ``_ASSIGNED="false"``, then binds.
 
-This simulator does exactly that with a best-fit bin-packing policy, keeps its per-GPU
+It places pods with a best-fit bin-packing policy — jointly for the queue of unscheduled pods
+it knows about (``sim/packing.py``: online best fit strands HBM when mixed sizes arrive in an
+unlucky order, the joint plan does not) — keeps its per-GPU
 ledger like the real extender's cache, and adds the MI355X capability the north star asks
 for: pods labelled ``gpushare.amd.com/tp-group=<name>`` with ``…/tp-size=<k>`` are placed
 as a group on k distinct GPUs that are pairwise one-hop xGMI per the topology annotation
@@ -61,6 +63,11 @@ class ExtenderSim:
         # xGMI clique is reserved when its first member binds (group -> reservation)
         self._groups: dict[str, dict] = {}
         self.group_ttl_s = group_ttl_s
+        # the pending queue (unscheduled gpu-mem pods, not TP groups) and its joint placement
+        self._pending: dict[str, dict] = {}
+        self._plan: dict[str, tuple[str, int]] = {}
+        self.plan_budget = 50_000
+        self.plan_enabled = True
         self._lock = threading.Lock()
 
     # -- cache ----------------------------------------------------------------------------
@@ -98,8 +105,56 @@ class ExtenderSim:
                 for g in (r["free"] if st else []):
                     st.used[g] += r["req"]
 
+    # -- the pending queue and its joint plan -----------------------------------------------
+    def note_pending(self, pod: dict) -> None:
+        """An unscheduled pod asking for gpu-mem (pod informer ADDED / MODIFIED, or the
+        simulator's create): it joins the queue the next placement plans for."""
+        if (O.node_name(pod) or O.gpu_mem_of_pod(pod) <= 0 or O.is_terminated(pod) or O.deleting(pod)
+                or self._group_of(pod) is not None):
+            return
+        with self._lock:
+            if O.uid(pod) not in self._pending:
+                self._pending[O.uid(pod)] = pod
+                self._plan.clear()            # the queue changed: plan it again as a whole
+
+    def _drop_pending_locked(self, uid: str) -> None:
+        if self._pending.pop(uid, None) is not None:
+            self._plan.pop(uid, None)
+
+    def _replan_locked(self) -> None:
+        """Joint best placement of every queued pod onto the GPUs' free HBM (sim/packing.py)."""
+        if (not self.plan_enabled or self.policy != "binpack" or not self._pending
+                or all(u in self._plan for u in self._pending)):
+            return
+        from .packing import pack
+
+        bins, free = [], []
+        for name, st in sorted(self.nodes.items()):
+            for i, f in enumerate(st.free()):
+                if f > 0:
+                    bins.append((name, i))
+                    free.append(f)
+        uids = list(self._pending)
+        sizes = [O.gpu_mem_of_pod(self._pending[u]) for u in uids]
+        assign = pack(free, sizes, self.plan_budget)
+        self._plan = {u: bins[a] for u, a in zip(uids, assign) if a is not None}
+
+    def _planned_locked(self, pod: dict, node_names=None) -> tuple[str, int] | None:
+        u = O.uid(pod)
+        if u not in self._pending:
+            return None
+        self._replan_locked()
+        choice = self._plan.get(u)
+        if choice is None or (node_names is not None and choice[0] not in node_names):
+            return None
+        st = self.nodes.get(choice[0])
+        if st is None or st.free()[choice[1]] < O.gpu_mem_of_pod(pod):
+            return None
+        return choice
+
     def forget(self, pod: dict):
         with self._lock:
+            self._drop_pending_locked(O.uid(pod))
             self._forget_locked(O.uid(pod))
 
     def _forget_locked(self, uid: str):
@@ -119,8 +174,12 @@ class ExtenderSim:
 
     def update(self, pod: dict):
         """Pod informer update: re-account the pod from its (possibly rewritten) annotations."""
+        if not O.node_name(pod):
+            self.note_pending(pod)
+            return
         with self._lock:
             u = O.uid(pod)
+            self._drop_pending_locked(u)
             if O.is_terminated(pod) or O.deleting(pod):
                 self._forget_locked(u)
                 return
@@ -152,7 +211,7 @@ class ExtenderSim:
                         rv = (obj.get("metadata") or {}).get("resourceVersion", rv)
                         if ev.get("type") == "DELETED":
                             self.forget(obj)
-                        elif ev.get("type") == "MODIFIED":
+                        elif ev.get("type") in ("MODIFIED", "ADDED"):
                             self.update(obj)
                 except Exception:  # noqa: BLE001 - expired RV, apiserver restart: re-list
                     rv = None
@@ -177,6 +236,9 @@ class ExtenderSim:
             if self._group_of(pod) is not None:
                 self._expire_groups_locked(time.monotonic())
                 return [n for n in names if self.group_fits(pod, n)]
+            planned = self._planned_locked(pod, names)
+            if planned is not None:
+                return [planned[0]]          # the queue's joint plan put it there
             return [n for n in names if n in self.nodes and self._fits(self.nodes[n], req)]
 
     def _choose(self, req: int, node_names=None) -> tuple[str, int] | None:
@@ -210,7 +272,8 @@ class ExtenderSim:
         """Filter + prioritize + reserve (the scheduling cycle; in memory)."""
         req = O.gpu_mem_of_pod(pod)
         with self._lock:
-            choice = self._choose(req, node_names)
+            choice = self._planned_locked(pod, node_names) or self._choose(req, node_names)
+            self._drop_pending_locked(O.uid(pod))
             if choice is None:
                 return None
             st = self.nodes[choice[0]]
@@ -372,7 +435,9 @@ def serve_http(ext: ExtenderSim, host: str = "127.0.0.1", port: int = 0):
                         fits = ext._fits(st, req) if st else []
                         if not fits:
                             return self._reply({"Error": "no GPU fits"})
-                        g = min(fits, key=lambda i: (st.free()[i] - req, i))
+                        planned = ext._planned_locked(pod, [args["Node"]])
+                        ext._drop_pending_locked(O.uid(pod))
+                        g = planned[1] if planned else min(fits, key=lambda i: (st.free()[i] - req, i))
                         st.used[g] += req
                         ext._placed[O.uid(pod)] = (st.name, [(g, req)])
                     ext.bind(pod, args["Node"], g)

@@ -72,8 +72,9 @@ def parse():
     ap.add_argument("--compare-pods", type=int, default=24, help="admissions per A/B configuration")
     ap.add_argument("--no-ref-churn", action="store_true",
                     help="skip the reference-model node churned in lock-step with the real one")
-    ap.add_argument("--fill-orders", default="grouped,random,size_desc,size_asc",
-                    help="bin-pack stress: arrival orders of the node's mixed pods through the extender ('' = off)")
+    ap.add_argument("--fill-orders", default="grouped,random,size_desc,size_asc,burst_random,burst_size_asc",
+                    help="bin-pack stress: arrival orders of the node's mixed pods through the extender; burst_* = "
+                         "all pods queued first, placed jointly ('' = off)")
     ap.add_argument("--room-slack-gib", type=float, default=2.0,
                     help="free HBM beyond a pod's state required before it allocates")
     ap.add_argument("--json-out", default=None)
@@ -337,8 +338,10 @@ def fill_orders(orders: list[str], n_gpus: int, units: int, seed: int = 0) -> di
     (``PATTERNS``, 8-128 GiB, summing to exactly the node's HBM) arrive in a given order
     through the extender's online best fit and the plugin's Allocate. ``grouped`` = per-GPU
     groups (the churn's fill: packs by construction); ``random`` = one seeded shuffle;
-    ``size_desc`` / ``size_asc`` = sorted. Reports pods and GiB placed, the node's HBM left
-    stranded when a pod could not be placed, and failed placements."""
+    ``size_desc`` / ``size_asc`` = sorted — each pod scheduled as it arrives (online best fit);
+    ``burst_<order>`` = the same arrival order, but all pods are queued before the scheduler
+    runs, so the extender places the queue jointly (``sim/packing.py``). Reports pods and GiB
+    placed, the node's HBM left stranded when a pod could not be placed, and failed placements."""
     import random
 
     from aliyun_gpushare_device_plugin_amd.sim.cluster import SimCluster
@@ -347,17 +350,27 @@ def fill_orders(orders: list[str], n_gpus: int, units: int, seed: int = 0) -> di
     out = {}
     for order in orders:
         seq = list(sizes)
-        if order == "random":
+        burst = order.startswith("burst_")
+        base = order[len("burst_"):] if burst else order
+        if base == "random":
             random.Random(seed).shuffle(seq)
-        elif order == "size_desc":
+        elif base == "size_desc":
             seq.sort(reverse=True)
-        elif order == "size_asc":
+        elif base == "size_asc":
             seq.sort()
+        elif base != "grouped":
+            raise ValueError(f"fill order {order!r}")
         placed, failed, admit_fail = [], 0, 0
         with SimCluster([("fill", f"fake:{n_gpus}x288G")], plugin_mode="thread", apiserver="thread",
                         kubelet="thread") as c:
-            for sz in seq:
-                pod, where, adm = c.run_pod(sz)
+            queued = [c.create_pod(sz) for sz in seq] if burst else []
+            for k, sz in enumerate(seq):
+                if burst:
+                    pod = queued[k]
+                    where = c.schedule(pod)
+                    adm = c.admit(pod) if where else None
+                else:
+                    pod, where, adm = c.run_pod(sz)
                 if where is None:
                     failed += 1
                 elif adm is None or adm.error or int(dict(adm.responses[0].envs)["ALIYUN_COM_GPU_MEM_IDX"]) < 0:

@@ -220,3 +220,41 @@ def test_admission_orders_keep_reservations_exact(ngpu, data):
     if in_order:
         for p, (shape, g) in zip(pods, reserved):
             assert granted[p["metadata"]["name"]] == [g] * len(shape)
+
+
+@settings(max_examples=200, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(nbins=st.integers(1, 8), data=st.data())
+def test_joint_packing_is_feasible_and_beats_best_fit(nbins, data):
+    """sim/packing.py: the joint plan never over-fills a GPU, is never worse than best fit (in
+    arrival order or decreasing), and packs everything when a perfect packing exists (items cut
+    from the bins themselves, then shuffled)."""
+    from aliyun_gpushare_device_plugin_amd.sim.packing import best_fit, pack
+
+    cap = data.draw(st.sampled_from([64, 288]))
+    free = [cap] * nbins
+    items = []
+    for _ in range(nbins):                      # cut every bin into 1-5 pieces: a perfect packing
+        left, cuts = cap, data.draw(st.integers(1, 5))
+        for _ in range(cuts - 1):
+            piece = data.draw(st.integers(1, max(1, left - 1))) if left > 1 else 0
+            if piece <= 0 or piece >= left:
+                break
+            items.append(piece)
+            left -= piece
+        items.append(left)
+    extra = data.draw(st.lists(st.integers(1, cap), max_size=4))  # over-subscription
+    sizes = data.draw(st.permutations(items + extra))
+    got = pack(free, sizes, budget=20_000)
+    used = [0] * nbins
+    for a, s in zip(got, sizes):
+        if a is not None:
+            used[a] += s
+    assert all(u <= cap for u in used)
+
+    def score(x):
+        return sum(a is not None for a in x), sum(s for a, s in zip(x, sizes) if a is not None)
+
+    assert score(got) >= score(best_fit(free, sizes, list(range(len(sizes)))))
+    assert score(got) >= score(best_fit(free, sizes, sorted(range(len(sizes)), key=lambda k: -sizes[k])))
+    if not extra:
+        assert score(got)[0] == len(sizes), (free, sizes, got)
