@@ -230,6 +230,26 @@ def test_rccl_tp_pair_allreduce():
     assert d["backend"] == "nccl" and d["tp_block_rel_err"] < 5e-2 and d["busbw_GBps"] > 10
 
 
+def test_rccl_single_rank_tp_block_on_mi355x():
+    """The RCCL path on the 1-GPU box: the TP demo as one rank (torch.distributed 'nccl' = RCCL
+    on ROCm; communicator init, the all-reduce kernels, the MFMA GEMM block) — the 2-GPU pair
+    test above needs the 8-GPU node."""
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "-m",
+                        "aliyun_gpushare_device_plugin_amd.parallel.tp_demo", "--iters", "5"],
+                       cwd=root, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert d["backend"] == "nccl" and d["world"] == 1 and d["tp_block_rel_err"] < 5e-2
+    assert d["allreduce_bytes"] == 256 << 20 and d["allreduce_ms"] > 0
+
+
 def test_hbm_used_gauge_matches_sysfs():
     """gpushare_hbm_used_bytes{gpu} (set from the health poll's SMI sample) tracks amdgpu's
     mem_info_vram_used while this process holds 8 GiB on GPU 0."""
