@@ -183,6 +183,7 @@ class Allocator:
         self._revoked: set[str] = set()           # reservation re-armed: its assign job must not re-claim
         self._place_mu = threading.Lock()
         self._place_thread = None
+        self._last_grant = 0.0
         # fast path: prepared answers, engine-state generation, answers awaiting bookkeeping
         self._fast: _Fast | None = None
         self._gen = 0
@@ -702,6 +703,7 @@ class Allocator:
                 key = PL.ids_key(ids)
                 self.journal.index_answer(key, c.uid, t, c.body, ids)
                 self.grants.record(key, PL.Grant(gpu=c.gpu, units=len(ids), claimed=c.uid, t=t, ledger=c.lkey))
+                self._last_grant = time.monotonic()
             self.journal.prefault()
 
     def _prepare_loop(self):
@@ -881,6 +883,7 @@ class Allocator:
                         ledger=cresp.annotations.get(const.CTR_ANNOTATION_LEDGER, ""))
 
     def _record_grants(self, req, resp, uid: str, jkey: str) -> None:
+        self._last_grant = time.monotonic()
         t = time.time()
         crs = req.container_requests
         for i, cresp in enumerate(resp.container_responses):
@@ -1024,7 +1027,16 @@ class Allocator:
         self.podres = src
         if src is not None and self._place_thread is None and self.opts.placement_s > 0:
             def loop():
+                last = 0.0
                 while not self._stop.wait(self.opts.placement_s):
+                    # every placement_s while answers are in flight (the kubelet has not shown
+                    # who holds them yet), otherwise a slow safety pass: a List of every pod's
+                    # devices is not free on a busy node
+                    now = time.monotonic()
+                    busy = now - self._last_grant < self.opts.in_flight_s
+                    if not busy and now - last < 15 * self.opts.placement_s:
+                        continue
+                    last = now
                     try:
                         self.reconcile_placement()
                     except Exception as e:  # noqa: BLE001 - kubelet restarting, apiserver down
