@@ -156,6 +156,7 @@ struct State {
   bool enabled = false;
   int mode = kModeKfd;
   int log = 0;
+  int diag = 0;
   std::atomic<uint64_t> quota{0};   // 0 in kfd mode until the first VRAM allocation names its GPU
   uint64_t ctr = 0, dev = 0;        // container / device units when the quota is derived
   uint64_t granule = kDefaultGranule;
@@ -384,9 +385,31 @@ int acquire_slot(LedgerShm* L) {
   return -1;
 }
 
+// GPUSHARE_SHIM_DIAG=1: before each charge, check that the ledger page is still mapped; if it
+// is not, print the process's mappings around it and abort (field diagnosis of a lost ledger).
+void diag_check(LedgerShm* L) {
+  unsigned char v;
+  void* page = reinterpret_cast<void*>(reinterpret_cast<uintptr_t>(L) & ~uintptr_t(4095));
+  if (mincore(page, 4096, &v) == 0 || errno != ENOMEM) return;
+  fprintf(stderr, "[gpushare-hipquota %d] ledger %p (%s) is no longer mapped\n", (int)getpid(), (void*)L,
+          g.ledger_name);
+  FILE* f = fopen("/proc/self/maps", "re");
+  if (f) {
+    char ln[512];
+    uintptr_t a = reinterpret_cast<uintptr_t>(L);
+    while (fgets(ln, sizeof ln, f)) {
+      unsigned long lo = 0, hi = 0;
+      if (sscanf(ln, "%lx-%lx", &lo, &hi) == 2 && hi + (64ul << 20) > a && lo < a + (64ul << 20)) fputs(ln, stderr);
+    }
+    fclose(f);
+  }
+  abort();
+}
+
 bool charge(uint64_t bytes) {
   if (g_released.load(std::memory_order_relaxed)) return true;  // process teardown
   LedgerShm* L = g.ledger;
+  if (g.diag) diag_check(L);
   uint64_t quota = g.quota.load(std::memory_order_relaxed);
   bool reclaimed = false;
   uint64_t cur = L->total.load();
@@ -537,6 +560,16 @@ int env_mode() {
 
 void init_body();
 
+// Address range for the ledger, reserved when the library loads — before the runtime (or
+// anything else) starts mapping and unmapping — so no one else can believe it is theirs.
+constexpr size_t kLedgerMapBytes = (sizeof(LedgerShm) + 4095) & ~size_t(4095);
+void* g_ledger_va = nullptr;
+
+__attribute__((constructor)) void reserve_ledger_va() {
+  void* p = mmap(nullptr, kLedgerMapBytes, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+  if (p != MAP_FAILED) g_ledger_va = p;
+}
+
 void init() {
   g_initializing.store(true);
   init_body();
@@ -545,6 +578,7 @@ void init() {
 
 void init_body() {
   g.log = (int)env_u64("GPUSHARE_SHIM_LOG", 0);
+  g.diag = (int)env_u64("GPUSHARE_SHIM_DIAG", 0);
   const char* dis = getenv("CGPU_DISABLE");
   if (dis && !strcmp(dis, "true")) {
     logf(1, "CGPU_DISABLE=true: quota enforcement off");
@@ -591,7 +625,11 @@ void init_body() {
       fd = shm_open(g.ledger_name, O_RDWR | O_CREAT, 0600);
     }
     if (fd >= 0 && ftruncate(fd, sizeof(LedgerShm)) == 0) {
-      void* p = mmap(nullptr, sizeof(LedgerShm), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+      // Onto the range reserved at load time: this runs inside the runtime's first VRAM ioctl,
+      // and ROCr maps ranges it probed free just before that ioctl MAP_FIXED right after it —
+      // a fresh mapping placed there would be replaced under us (measured on MI355X).
+      void* p = g_ledger_va ? mmap(g_ledger_va, sizeof(LedgerShm), PROT_READ | PROT_WRITE, MAP_SHARED | MAP_FIXED, fd, 0)
+                            : mmap(nullptr, sizeof(LedgerShm), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
       if (p != MAP_FAILED) {
         g.ledger = static_cast<LedgerShm*>(p);
         uint64_t zero = 0;  // first process initialises; ftruncate zero-fills
@@ -615,6 +653,7 @@ void init_body() {
   g.enabled = true;
   atexit(release_slot_at_exit);
   pthread_atfork(nullptr, nullptr, atfork_child);
+  if (g.diag) fprintf(stderr, "[gpushare-hipquota %d] ledger %s mapped at %p\n", (int)getpid(), g.ledger_name, (void*)g.ledger);
   logf(1, "mode %s, quota %llu bytes (%.2f GiB%s), ledger %s slot %d", g.mode == kModeKfd ? "kfd" : "hip",
        (unsigned long long)g.quota.load(), (double)g.quota.load() / (1ull << 30),
        g.quota.load() ? "" : ", from the first GPU allocation", g.ledger_name[0] ? g.ledger_name : "(local)",

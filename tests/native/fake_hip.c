@@ -12,6 +12,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 typedef int hipError_t;
 struct kfd_alloc { uint64_t va, size, handle, mmap_offset; uint32_t gpu_id, flags; };
 struct kfd_free { uint64_t handle; };
@@ -66,9 +67,24 @@ int ioctl(int fd, unsigned long req, ...) {
   int (*real)(int, unsigned long, ...) = (int (*)(int, unsigned long, ...))dlsym(RTLD_NEXT, "ioctl");
   return real(fd, req, arg);
 }
+/* FAKE_HIP_PROBE_FIXED=1: the runtime's address-space habit measured on MI355X — it finds a
+   free range (map + unmap), issues the allocation ioctl, then maps that range MAP_FIXED and
+   trims it. Whatever the process mapped inside the range meanwhile (the shim initialising
+   inside that ioctl) is silently replaced. */
 static int kfd(size_t n, uint64_t* h) {
   struct kfd_alloc a = {0, n, 0, 0, 1, 1u /* VRAM */};
-  if (ioctl(3, KFD_ALLOC, &a)) return 2;             /* hipErrorOutOfMemory */
+  const char* pf = getenv("FAKE_HIP_PROBE_FIXED");
+  void* probe = NULL;
+  if (pf && *pf == '1') {
+    probe = mmap(NULL, 2 * 4096, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (probe == MAP_FAILED) probe = NULL; else munmap(probe, 2 * 4096);
+  }
+  int r = ioctl(3, KFD_ALLOC, &a);
+  if (probe) {
+    mmap(probe, 2 * 4096, PROT_READ, MAP_PRIVATE | MAP_ANONYMOUS | MAP_FIXED, -1, 0);
+    munmap((char*)probe + 4096, 4096);
+  }
+  if (r) return 2;                                   /* hipErrorOutOfMemory */
   *h = a.handle; return 0;
 }
 static void kfd_release(uint64_t h) { struct kfd_free f = {h}; ioctl(3, KFD_FREE, &f); }

@@ -367,3 +367,23 @@ def test_kfd_mode_allocation_during_shim_init_passes(stub, native_shim):
     out, r = run(stub, native_shim, ["info", "alloc", 1 * GIB, "stats"], GPUSHARE_QUOTA_BYTES=4 * GIB,
                  FAKE_HIP_INIT_KFD=1)
     assert r.returncode == 0 and out[1]["err"] == 0 and out[2]["used"] >= 1 * GIB
+
+
+@pytest.mark.parametrize("backing", ["file", "shm"])
+def test_ledger_survives_runtime_map_fixed_during_shim_init(stub, native_shim, tmp_path, backing):
+    """Measured on MI355X (bench pod processes): the shim initialised inside ROCr's first VRAM
+    ioctl, mapped its ledger into the range ROCr had just probed and unmapped, and ROCr then
+    mapped that range MAP_FIXED and trimmed it — the ledger page vanished and the next charge
+    faulted. The shim reserves the ledger's address range when it is loaded, before any runtime
+    runs, and maps the ledger onto that reservation."""
+    name = ledger()
+    env = dict(GPUSHARE_LEDGER=name, GPUSHARE_QUOTA_BYTES=4 * GIB, FAKE_HIP_PROBE_FIXED=1, GPUSHARE_SHIM_DIAG=1)
+    if backing == "file":
+        env["GPUSHARE_LEDGER_DIR"] = str(tmp_path)
+    try:
+        out, r = run(stub, native_shim, ["scratch", 1 * GIB, "alloc", 2 * GIB, "alloc", 2 * GIB, "stats"], **env)
+    finally:
+        cleanup(name)
+    assert r.returncode == 0, r.stderr
+    assert [o["err"] for o in out[:3]] == [0, 0, 2]
+    assert out[3]["used"] == 3 * GIB and out[3]["denied"] == 1
