@@ -272,6 +272,29 @@ __device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
   return __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2_t{a, b}, bf16x2_t));
 }
 
+// Epilogue of the 32x32-MFMA kernels: lane (ql, hh) holds o[dt][4q + r] = O[row][32 dt + 8 q + 4 hh + r].
+// Column group k = 4 dt + q covers columns 8k .. 8k+7, split across the half-waves; for each pair
+// (2c, 2c+1) one v_permlane32_swap per dword leaves the lower half-wave with columns 16c .. 16c+7
+// of its row and the upper half with 16c+8 .. 16c+15, so each lane stores 16 B per instruction
+// (8 dwordx4 instead of 16 dwordx2: the store tail of the last waves is issue-bound — guide T21,
+// measured +1.5-10 % on the ping-pong kernel). The swaps need all 64 lanes active: only the
+// stores are predicated. `row` points at the row's first element (any valid row when !store).
+__device__ __forceinline__ void store_o_wide(const f32x16_t (&o)[4], float inv, unsigned short* row, int hh,
+                                             bool store) {
+  typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+  char* const p = (char*)row + 16 * hh;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const f32x16_t& x0 = o[c >> 1];        // groups 2c and 2c+1 share dt = c >> 1
+    const int r0 = 8 * (c & 1), r1 = r0 + 4;
+    const auto w0 = __builtin_amdgcn_permlane32_swap(pack_bf16x2(x0[r0] * inv, x0[r0 + 1] * inv),
+                                                     pack_bf16x2(x0[r1] * inv, x0[r1 + 1] * inv), false, false);
+    const auto w1 = __builtin_amdgcn_permlane32_swap(pack_bf16x2(x0[r0 + 2] * inv, x0[r0 + 3] * inv),
+                                                     pack_bf16x2(x0[r1 + 2] * inv, x0[r1 + 3] * inv), false, false);
+    if (store) *(u32x4_t*)(p + 32 * c) = u32x4_t{w0[0], w1[0], w0[1], w1[1]};
+  }
+}
+
 // NW waves per block (NW x 32 query rows). NW = 4 runs two independent blocks per CU (their
 // per-tile barriers drift apart, so one block's softmax overlaps the other's MFMAs); NW = 8 is
 // one block per CU.
@@ -282,7 +305,9 @@ constexpr float RESCALE_TAU = 8.f;   // log2 units: deferred-rescale headroom (p
 // issued after QK^T(t) and written to LDS right after the next barrier (T14 split: the staging
 // registers are not live across QK^T), instead of loads at the tile's start and the LDS write
 // before its closing barrier.
-enum { AF_PRIO = 1, AF_LATE = 2 };
+// AF_WIDE: the widened epilogue (store_o_wide) on the 4-wave block; the 8-wave block always uses
+// it. On the 4-wave block at the 256-register budget it costs 3 spilled registers (A/B: variant 13).
+enum { AF_PRIO = 1, AF_LATE = 2, AF_WIDE = 4 };
 
 template <int NW, int FLAGS = 0>
 __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_fwd_d128_w8(const unsigned short* __restrict__ Q,
@@ -478,7 +503,9 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_fwd_d128_w8(const unsig
   }
 
   // ---- epilogue: O[qi][32 dt + 8 (r >> 2) + 4 hh + (r & 3)] = o[dt][r] / l ----
-  if (qi < S) {
+  if constexpr (NW == 8 || (FLAGS & AF_WIDE) != 0) {
+    store_o_wide(o, 1.f / l, O + (((size_t)b * S + min(qi, S - 1)) * Hq + h) * 128, hh, qi < S);
+  } else if (qi < S) {
     const float inv = 1.f / l;
     unsigned short* op = O + (((size_t)b * S + qi) * Hq + h) * 128 + 4 * hh;
 #pragma unroll
@@ -528,7 +555,12 @@ struct MSegTag {
 // 32 w + 128.
 // PP_TRACE (diagnostics, tools/attn_trace.py): block 0's waves record s_memtime before and after
 // every segment barrier into g_pp_trace (vector stores from lane 0).
-enum { PP_PRIO = 1, PP_ILV = 2, PP_TRACE = 4 };
+// PP_WIDE: the epilogue pairs column groups across the half-waves (v_permlane32_swap) so each
+// lane stores 16 B per instruction: 8 dwordx4 stores per lane instead of 16 dwordx2 (the store
+// tail of the last-finishing waves is issue-bound, not HBM-bound).
+// PP_SPRIO: static priority instead of PP_PRIO's per-segment flips — the younger half (waves
+// 4-7, which lose VALU arbitration to the older half by age) runs at s_setprio 1 throughout.
+enum { PP_PRIO = 1, PP_ILV = 2, PP_TRACE = 4, PP_WIDE = 8, PP_SPRIO = 16 };
 constexpr int PP_TRACE_SEGS = 160;
 __device__ unsigned long long g_pp_trace[8][PP_TRACE_SEGS][2];
 
@@ -783,6 +815,9 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_d128_pp(const unsigned short
   // made the compiler shuffle O and S between register sets).
   const int nlive = causal ? min(nkt, (q0 + 31) / KT8 + 1) : nkt;
 
+  if constexpr ((FLAGS & PP_SPRIO) != 0) {
+    if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);   // wave-uniform guard
+  }
   // ---- prologue: K(0) in LDS ----
   dma_k(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -842,7 +877,9 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_d128_pp(const unsigned short
     }
   }
 
-  if (qi < S) {
+  if constexpr ((FLAGS & PP_WIDE) != 0) {
+    store_o_wide(o, 1.f / l, O + (((size_t)b * S + min(qi, S - 1)) * Hq + h) * 128, hh, qi < S);
+  } else if (qi < S) {
     const float inv = 1.f / l;
     unsigned short* op = O + (((size_t)b * S + qi) * Hq + h) * 128 + 4 * hh;
 #pragma unroll
@@ -922,17 +959,24 @@ GS_KERNEL_API int gs_flash_attn_fwd_bf16(const void* q, const void* k, const voi
     return D == 128 ? launch<128, false>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream)
                     : launch<64, false>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
   // auto (measured on MI355X, tools/attn_sweep.py): the ping-pong 8-wave block wins on full
-  // attention and causal S >= 2048 (1045 / 1069 TF/s at H 64 full / causal 8192); on short causal
-  // sequences the 4-wave block's finer granularity (128 rows, two blocks per CU) wins
+  // attention and causal S >= 2048 (1080-1110 / 1065-1095 TF/s at H 64 full / causal 8192 with the
+  // widened store tail, profiles/r3/attn_sweep_wide_*.jsonl); on short causal sequences the
+  // 4-wave block's finer granularity (128 rows, two blocks per CU) wins
   const bool pp_ok = (size_t)S * k_stride * 2 < (1ull << 31) && (size_t)S * v_stride * 2 < (1ull << 31);
   if (D == 128 && pp_ok && g_attn_variant == 8)
     return launch_pp<0>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
   if (D == 128 && pp_ok && g_attn_variant == 10)
     return launch_pp<PP_PRIO | PP_TRACE>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
+  if (D == 128 && pp_ok && g_attn_variant == 12)
+    return launch_pp<PP_SPRIO | PP_WIDE>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
+  if (D == 128 && (g_attn_variant == 13 || g_attn_variant == 0))
+    return launch_w8<4, AF_WIDE>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
   if (D == 128 && pp_ok && g_attn_variant == 9)
     return launch_pp<PP_PRIO | PP_ILV>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
-  if (D == 128 && pp_ok && (g_attn_variant == 7 || (g_attn_variant == 0 && (!(causal & 1) || S >= 2048))))
+  if (D == 128 && pp_ok && g_attn_variant == 7)
     return launch_pp<PP_PRIO>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
+  if (D == 128 && pp_ok && (g_attn_variant == 11 || (g_attn_variant == 0 && (!(causal & 1) || S >= 2048))))
+    return launch_pp<PP_PRIO | PP_WIDE>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
   if (D == 128 && g_attn_variant == 4)
     return launch_w8<8, AF_PRIO>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
   if (D == 128 && g_attn_variant == 5)
@@ -953,9 +997,10 @@ GS_KERNEL_API int gs_flash_attn_fwd_bf16(const void* q, const void* k, const voi
 // 2 = 32x32 4-wave, 3 = 32x32 8-wave; experiments: 4 = 8-wave + younger-half priority, 5 = 8-wave
 // + late (T14) loads, 6 = 4-wave + late loads, 7 = ping-pong 8-wave (MFMA-segment priority), 8 = ping-pong
 // without the priority, 9 = ping-pong + interleaved partner rows (measured 1-3 % slower), 10 = ping-pong with the
-// segment trace (gs_attn_trace).
+// segment trace (gs_attn_trace), 11 = ping-pong + widened store tail, 12 = ping-pong with static
+// younger-half priority + widened store tail, 13 = 4-wave 32x32 + widened store tail.
 GS_KERNEL_API int gs_attn_set_variant(int v) {
-  if (v < 0 || v > 10) return GS_EINVAL;
+  if (v < 0 || v > 13) return GS_EINVAL;
   g_attn_variant = v;
   return GS_OK;
 }
