@@ -6,8 +6,9 @@ node's mixed pod sizes do not arrive in a convenient order: at 8 MI355X with BAS
 though all 32 fit. The extender sees the whole queue of unscheduled ``aliyun.com/gpu-mem``
 pods, so it can place them jointly: ``pack`` assigns items to bins maximising the number of
 pods placed, then the HBM placed — a depth-first search over items in decreasing size with
-best-fit as the starting incumbent, bins with equal free space tried once per level, and a
-bound on what the remaining items could still add. The search stops after ``budget`` node
+best-fit as the starting incumbent, bins with equal free space tried once per level, an exact
+fit taken without alternatives, and a bound on what the remaining items could still add (free
+space smaller than the smallest item is waste; items larger than every free space are out). The search stops after ``budget`` node
 expansions and keeps the best assignment found (never worse than best fit).
 """
 from __future__ import annotations
@@ -29,11 +30,92 @@ def _score(assign: list[int | None], sizes: list[int]) -> tuple[int, int]:
     return sum(1 for a in assign if a is not None), sum(s for a, s in zip(assign, sizes) if a is not None)
 
 
+class _Budget(Exception):
+    pass
+
+
+def place_all(free: list[int], sizes: list[int], budget: int = 200_000) -> list[int] | None:
+    """A bin per item with every item placed, or None (none exists, or the budget ran out).
+
+    Bin completion (Korf's algorithm, for bins of different sizes): bins are filled one at a
+    time, smallest first, each with a *maximal* subset of the remaining items (one no remaining
+    item could still join: a non-maximal fill is never better). The total space the bins may
+    leave empty is the slack, free space minus item size, so with little slack — the hard
+    case for item-by-item search, a node whose pods exactly fill its GPUs — only fills that
+    waste almost nothing are tried. Subsets are enumerated over items in decreasing size,
+    fuller fills first, and equal sizes are tried once per level; when the bins left all have
+    the same size, the largest item left goes into the current one."""
+    n = len(sizes)
+    slack = sum(free) - sum(sizes)
+    if n == 0:
+        return []
+    if slack < 0:
+        return None
+    order = sorted(range(n), key=lambda k: -sizes[k])
+    bins = sorted(range(len(free)), key=lambda b: (free[b], b))
+    assign: list[int | None] = [None] * n
+    steps = 0
+
+    def fill(bi: int, left_items: list[int], waste_left: int) -> bool:
+        if not left_items:
+            return True
+        if bi == len(bins) or sizes[left_items[0]] > max(free[b] for b in bins[bi:]):
+            return False
+        cap = free[bins[bi]]
+        lo = cap - waste_left                 # this bin must hold at least this much
+        chosen: list[int] = []
+
+        def sub(j0: int, total: int) -> bool:
+            nonlocal steps
+            steps += 1
+            if steps > budget:
+                raise _Budget
+            tried = set()
+            for j in range(j0, len(left_items)):
+                k = left_items[j]
+                sz = sizes[k]
+                if total + sz > cap or sz in tried:
+                    continue
+                tried.add(sz)
+                chosen.append(k)
+                if sub(j + 1, total + sz):
+                    return True
+                chosen.pop()
+            if total < lo:
+                return False
+            cs = set(chosen)
+            rest = [k for k in left_items if k not in cs]
+            if rest and sizes[rest[-1]] <= cap - total:
+                return False                  # not maximal: the smallest remaining item still fits
+            for k in chosen:
+                assign[k] = bins[bi]
+            if fill(bi + 1, rest, waste_left - (cap - total)):
+                return True
+            for k in chosen:
+                assign[k] = None
+            return False
+
+        if all(free[b] == cap for b in bins[bi:]):
+            # the remaining bins are interchangeable: the largest remaining item may as well be
+            # in this one (removes the bin-order symmetry)
+            chosen.append(left_items[0])
+            return sub(1, sizes[left_items[0]])
+        return sub(0, 0)
+
+    try:
+        ok = fill(0, order, slack)
+    except _Budget:
+        return None
+    return [a for a in assign] if ok else None   # type: ignore[misc]
+
+
 def pack(free: list[int], sizes: list[int], budget: int = 200_000) -> list[int | None]:
     """Bin index per item (None = not placed) maximising (items placed, size placed)."""
     n = len(sizes)
     if n == 0:
         return []
+    if not free:
+        return [None] * n
     order = sorted(range(n), key=lambda k: -sizes[k])
     # incumbent: the better of best fit in arrival order (what the online extender would do)
     # and in decreasing size order
@@ -42,12 +124,17 @@ def pack(free: list[int], sizes: list[int], budget: int = 200_000) -> list[int |
     best_score = _score(best, sizes)
     if best_score[0] == n:
         return best
+    if sum(sizes) <= sum(free):
+        full = place_all(free, sizes, budget // 2)
+        if full is not None:
+            return full
     suffix_cnt = [0] * (n + 1)
     suffix_sz = [0] * (n + 1)
     for i in range(n - 1, -1, -1):
         suffix_cnt[i] = suffix_cnt[i + 1] + 1
         suffix_sz[i] = suffix_sz[i + 1] + sizes[order[i]]
     left = list(free)
+    smallest = min(sizes)
     cur: list[int | None] = [None] * n
     expansions = 0
 
@@ -62,14 +149,23 @@ def pack(free: list[int], sizes: list[int], budget: int = 200_000) -> list[int |
                 return True
         if i == n or expansions > budget:
             return False
-        room = sum(left)
-        if (cnt + suffix_cnt[i], sz + min(suffix_sz[i], room)) <= best_score:
+        # bound: space in a bin smaller than the smallest remaining item is wasted, and items
+        # larger than the largest free space cannot be placed any more
+        usable = sum(f for f in left if f >= smallest)
+        big = max(left)
+        fit_cnt = suffix_cnt[i] - sum(1 for j in range(i, n) if sizes[order[j]] > big)
+        if (cnt + fit_cnt, sz + min(suffix_sz[i], usable)) <= best_score:
             return False
         k = order[i]
         s = sizes[k]
         if s != skipped:
             tried = set()
-            for b in sorted(range(len(left)), key=lambda b: (left[b] - s, b)):
+            cand = sorted(range(len(left)), key=lambda b: (left[b] - s, b))
+            # an item that exactly fills a bin goes there: any solution placing it elsewhere can
+            # swap it with that bin's remaining contents (same count, same size placed)
+            if left[cand[0]] == s:
+                cand = cand[:1]
+            for b in cand:
                 f = left[b]
                 if f < s or f in tried:
                     continue

@@ -8,6 +8,8 @@
 """
 import itertools
 
+import pytest
+
 from hypothesis import HealthCheck, given, settings, strategies as st
 
 from aliyun_gpushare_device_plugin_amd import const
@@ -258,3 +260,23 @@ def test_joint_packing_is_feasible_and_beats_best_fit(nbins, data):
     assert score(got) >= score(best_fit(free, sizes, sorted(range(len(sizes)), key=lambda k: -sizes[k])))
     if not extra:
         assert score(got)[0] == len(sizes), (free, sizes, got)
+
+
+@pytest.mark.parametrize("nbins,cap,sizes", [
+    (7, 288, [288, 288, 178, 154, 133, 125, 98, 94, 90, 86, 76, 69, 58, 54, 41, 38, 35, 27, 23, 20, 13, 9, 8, 6, 5]),
+    (7, 64, [59, 50, 43, 41, 34, 29, 22, 22, 18, 17, 16, 14, 13, 11, 11, 8, 7, 7, 6, 5, 5, 4, 3, 3]),
+    (8, 288, [255, 210, 203, 191, 150, 149, 139, 134, 124, 119, 109, 102, 70, 55, 46, 45, 33, 23, 20, 19, 15, 13,
+              13, 12, 10, 10, 9, 8, 8, 6, 4]),
+])
+def test_zero_slack_perfect_packings_are_found(nbins, cap, sizes):
+    """Pods that exactly fill every GPU (no slack): item-by-item search missed these within
+    200k expansions; bin completion (sim/packing.py place_all) finds them in a few hundred."""
+    from aliyun_gpushare_device_plugin_amd.sim.packing import pack, place_all
+
+    assert sum(sizes) == nbins * cap
+    for got in (place_all([cap] * nbins, sizes, budget=2_000), pack([cap] * nbins, sizes, budget=4_000)):
+        assert got is not None and None not in got
+        used = [0] * nbins
+        for a, s in zip(got, sizes):
+            used[a] += s
+        assert used == [cap] * nbins
