@@ -245,3 +245,30 @@ def test_decode_step_with_folded_rmsnorm_matches_unfolded():
         ga, gb = a.step().float(), b.step().float()
         assert (ga - gb).abs().max().item() < 2e-2 * scale
 
+
+
+def test_refused_skinny_options_leave_no_armed_state():
+    """ADVICE (round 2): when the native side refuses a call's options after RoPE was armed, the
+    wrapper must clear them, or the next unrelated skinny_linear on this thread would rotate its
+    output and write into the stale cache pointers."""
+    from aliyun_gpushare_device_plugin_amd.ops.gemm import _SkinnyOpts
+
+    torch.manual_seed(7)
+    M, Hq, Hkv, K, Smax = 8, 8, 2, 1024, 64
+    N = (Hq + 2 * Hkv) * 128
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.05
+    cos, sin = ops.rope_tables(128, 128, 500000.0, "cuda")
+    pos = torch.arange(M, device="cuda", dtype=torch.int32)
+    kc, vc = ops.kv_cache(M, Hkv, Smax, 128, "cuda")
+    kc0, vc0 = kc.clone(), vc.clone()
+    bad_norm = (torch.empty(0, M, device="cuda"), torch.ones(K, device="cuda", dtype=torch.bfloat16), 1e-5)
+    with pytest.raises(Exception):
+        with _SkinnyOpts(None, bad_norm, (cos, sin, pos, kc, vc, Hq)):   # nch = 0: refused after RoPE armed
+            pass
+    y = ops.skinny_linear(x, w)
+    assert torch.equal(y, ops.skinny_linear(x, w))
+    want = x.float() @ w.float().T
+    assert (y.float() - want).abs().max().item() < 2e-2 * want.abs().max().item() + 1e-2
+    torch.cuda.synchronize()
+    assert torch.equal(kc, kc0) and torch.equal(vc, vc0)
