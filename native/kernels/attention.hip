@@ -909,6 +909,473 @@ int launch_pp(const void* q, const void* k, const void* v, void* o, int B, int S
   return gs_launch_status();
 }
 
+// ---------------------------------------------------------------------------------------------
+// One wave per SIMD, 64 query rows per wave (D = 128): flash_fwd_d128_w64.
+//
+// The ping-pong kernel above pairs two 32-row waves per SIMD in antiphase; its softmax segment
+// (~1800 cycles, VALU-issue bound) sets the pace while the partner's 32 MFMAs take ~1300, so the
+// matrix pipe idles a third of the time (profiles/attention_r2.md). Here a single wave per SIMD
+// owns 64 rows and interleaves its own softmax of tile j into the issue gaps of its MFMA stream
+// {P·V(j-1), QK^T(j+1)}: a v_mfma_f32_32x32x16_bf16 holds the SIMD's vector issue for 8 of its
+// 32 cycles (MI355X_MICROARCH.md, issue-cost row), so ~24 cycles of VALU per MFMA ride along.
+//
+// Tiles are 32 keys: per tile a wave issues 32 MFMAs (16 P·V + 16 QK^T, 1024 matrix cycles)
+// beside ~700 cycles of softmax issue for its 64 x 32 scores. Registers (512 per lane at one
+// wave per SIMD): Q^T (16 bf16x8 fragments, 64) and P (16) live in AGPRs and are read by the
+// MFMAs from there (every MFMA is inline asm with "a" B operands); O^T (8 tiles of 32x32 fp32,
+// 128), S^T of the tile being softmaxed and of the tile being produced (2 x 32), one fragment set
+// and the 12 per-lane LDS offsets are VGPRs. O stays out of the AGPRs on purpose: the rare
+// online-softmax rescale is a branch, and an accumulator whose value merges at a branch join was
+// copied AGPR -> VGPR by the allocator on every iteration (measured in the .s); 64-key tiles
+// (2 x 64 S registers) spilled Q to scratch. The two S buffers alternate by name (the loop is
+// unrolled by two), never by a runtime index; one P buffer suffices (P(j-1) is consumed in the
+// first half of iteration j, P(j) produced in its second half).
+//
+// Lane mapping (swapped QK^T, as the other 32x32 kernels): lane (ql, hh) holds query rows
+// q0 + ql (block c = 0) and q0 + 32 + ql (c = 1); S^T tile c register r is key
+// 8 (r >> 2) + 4 hh + (r & 3) of the tile; O^T tile (c, dt) register r is dim 32 dt + 8 (r >> 2) +
+// 4 hh + (r & 3).
+//
+// K/V tiles arrive by LDS DMA issued from inline asm (the compiler would otherwise make every
+// later LDS read of the iteration wait for the DMA, vmcnt): K(j+2) and V(j) at the start of
+// iteration j into the slots iteration j-1 finished reading, waited for (vmcnt(0)) before the one
+// raw barrier that opens iteration j+1 — a whole iteration of latency cover. Hazards the compiler
+// does not see around asm are padded by hand: MFMA results are read by VALU only an iteration
+// later or after explicit s_nop, and AGPR writes are padded before the next MFMA reads them.
+constexpr int W64_QR = 256;                 // rows per block: 4 waves x 64
+// diagnostics: compiler-issued LDS DMA (waits for it at every LDS read); a 64-cycle pad after every
+// MFMA group
+enum { W64_BUILTIN_DMA = 1, W64_PAD = 2 };
+constexpr int W64_KT = 32, W64_TILE = W64_KT * ROW8, W64_LDS = 4 * W64_TILE;
+
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+
+template <int I>
+struct W64Int {
+  static constexpr int value = I;
+};
+template <int B, int E, typename F>
+__device__ __forceinline__ void w64_static_for(F&& f) {
+  if constexpr (B < E) {
+    f(W64Int<B>{});
+    w64_static_for<B + 1, E>(f);
+  }
+}
+
+template <bool PV, bool SM, bool QK, bool MASK>
+struct W64Tag {
+  static constexpr bool pv = PV, sm = SM, qk = QK, mask = MASK;
+};
+
+// Inline asm (operands in the register files chosen here), so the compiler does not see the MFMA
+// latency: a copy of an accumulator tuple placed right after the MFMA that writes it would read
+// rows the MFMA has not written yet (measured: stale upper halves of O tiles). Every place the
+// allocator may copy — block boundaries — is therefore preceded by a pad: the end of each step
+// and the start of each iteration (open), and no branch sits between MFMAs.
+#define W64_MFMA_QK0(d, k, q) \
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(d) : "v"(k), "a"(q))
+#define W64_MFMA_QK(d, k, q) \
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(d) : "v"(k), "a"(q))
+#define W64_MFMA_PV(o, v, p) \
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(o) : "v"(v), "a"(p))
+
+template <int FLAGS = 0>
+__global__ __launch_bounds__(256, 1) void flash_fwd_d128_w64(const unsigned short* __restrict__ Q,
+                                                            const unsigned short* __restrict__ K,
+                                                            const unsigned short* __restrict__ V,
+                                                            unsigned short* __restrict__ O, int B, int S, int Hq,
+                                                            int Hkv, int q_stride, int k_stride, int v_stride,
+                                                            float scale_log2, int causal) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* const kbuf = smem;                   // K ring: 2 x W64_TILE
+  char* const vbuf = smem + 2 * W64_TILE;    // V ring: 2 x W64_TILE
+  const int nqb = (S + W64_QR - 1) / W64_QR;
+  int bh, qb;
+  block_coords(nqb, B * Hq, causal, bh, qb);
+  const int b = bh / Hq, h = bh % Hq;
+  const int hk = h / (Hq / Hkv);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ql = lane & 31, hh = lane >> 5;
+  const int q0 = qb * W64_QR + wave * 64;
+
+  // ---- Q^T fragments (B operand), pinned in AGPRs: qf[c][ds] = Q[q0 + 32 c + ql][16 ds + 8 hh ..]
+  bf16x8_t qf[2][8];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const unsigned short* qp =
+        Q + ((size_t)b * S + min(q0 + 32 * c + ql, S - 1)) * q_stride + (size_t)h * 128 + 8 * hh;
+#pragma unroll
+    for (int ds = 0; ds < 8; ++ds) qf[c][ds] = *(const bf16x8_t*)(qp + 16 * ds);
+  }
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int ds = 0; ds < 8; ++ds) asm volatile("" : "+a"(qf[c][ds]));
+  f32x16_t o[2][4];
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[c][dt][r] = 0.f;
+      asm volatile("" : "+a"(o[c][dt]));
+    }
+  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+  f32x16_t sA[2], sB[2];
+  bf16x8_t pP[2][2];                          // [c][g]: P^T of 16-key step g
+
+  const int nkt_all = (S + W64_KT - 1) / W64_KT;
+  const int nkt = causal ? min(nkt_all, (qb * W64_QR + W64_QR - 1) / W64_KT + 1) : nkt_all;
+  // tiles 0 .. nlive-1 hold a key visible to this wave; causal: the last two straddle the
+  // diagonal, ragged S: the last one is partial
+  const int nlive = causal ? min(nkt, (q0 + 63) / W64_KT + 1) : nkt;
+  const int mask_from = causal ? nlive - 2 : ((S % W64_KT) ? nlive - 1 : nlive);
+
+  // ---- LDS DMA (inline asm: invisible to the compiler's vmcnt tracking). Instruction i (0, 1) of
+  // wave w fills rows 16 i + 4 w + lane / 16 of a tile; the swizzle XOR terms depend on row & 15
+  // (K) and row & 3 (V) only, the same for both i. Rows past S read as zeros (range check).
+  const int prow = 4 * wave + (lane >> 4);
+  const int kch = (lane & 15) ^ (prow & 15);
+  const int vch = (lane & 15) ^ ((prow & 3) << 2);
+  auto rsrc = [&](const unsigned short* base, int stride) __attribute__((always_inline)) {
+    const unsigned long long a = (unsigned long long)(uintptr_t)(base + (size_t)b * S * stride + (size_t)hk * 128);
+    return i32x4_t{__builtin_amdgcn_readfirstlane((int)(unsigned)a), __builtin_amdgcn_readfirstlane((int)(a >> 32)),
+                   __builtin_amdgcn_readfirstlane(S * stride * 2), 0x00020000};
+  };
+  const i32x4_t rK = rsrc(K, k_stride), rV = rsrc(V, v_stride);
+  const unsigned voffK = (unsigned)(prow * k_stride + kch * 8) * 2u;
+  const unsigned voffV = (unsigned)(prow * v_stride + vch * 8) * 2u;
+  const unsigned lds_base = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  const __amdgpu_buffer_rsrc_t bK = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(K + (size_t)b * S * k_stride + (size_t)hk * 128), (short)0, S * k_stride * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t bV = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(V + (size_t)b * S * v_stride + (size_t)hk * 128), (short)0, S * v_stride * 2, 0x00020000);
+  auto dma = [&](const i32x4_t& r, unsigned voff, int stride, int t, unsigned lds) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int soff = __builtin_amdgcn_readfirstlane((t * W64_KT + 16 * i) * stride * 2);
+      const unsigned dst = __builtin_amdgcn_readfirstlane(lds + i * 4096 + wave * 1024);
+      if constexpr ((FLAGS & W64_BUILTIN_DMA) != 0) {   // diagnostics: the compiler's own LDS DMA
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(&r == &rK ? bK : bV,
+                                                 (__attribute__((address_space(3))) void*)(uintptr_t)dst, 16, voff,
+                                                 soff, 0, 0);
+      } else {
+        // one wait state between the M0 write and the DMA that reads it (hipcc emits the same
+        // s_nop for its own LDS DMA; without it the DMA used the previous M0: tiles landed in
+        // the wrong slot)
+        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                     :
+                     : "s"(dst), "v"(voff), "s"(r), "s"(soff)
+                     : "memory", "m0");
+      }
+    }
+  };
+  auto dma_tiles = [&](int j) __attribute__((always_inline)) {   // K(j+2), V(j) -> slot j & 1
+    if (j + 2 < nkt) dma(rK, voffK, k_stride, j + 2, lds_base + (j & 1) * W64_TILE);
+    if (j < nkt) dma(rV, voffV, v_stride, j, lds_base + 2 * W64_TILE + (j & 1) * W64_TILE);
+  };
+  auto sync = [&]() __attribute__((always_inline)) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::: "memory");
+  };
+
+  // ---- fragments. K (A operand of QK^T) for d-step ds; V^T (A operand of P·V) for dim block dt,
+  // 16-key step g (ds_read_b64_tr_b16 pair, as the ping-pong kernel). The swizzle makes the
+  // per-lane part depend on ds (K) and dt (V) only: the key-step term is an immediate offset, so
+  // 8 + 4 lane offsets serve every read of the loop.
+  int kofs[8], vofs[4];
+  {
+    const int row = lane & 31, g16 = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+#pragma unroll
+    for (int ds = 0; ds < 8; ++ds) kofs[ds] = row * ROW8 + (k8swz(row, 2 * ds + hh) << 4);
+    const int r0 = 8 * (g16 >> 1) + q4;                  // + 16 g; (r0 & 3) = q4 for every g
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) vofs[dt] = r0 * ROW8 + (v8swz(r0, 8 * dt + 4 * (g16 & 1) + p4) << 3);
+  }
+  auto kfrag = [&](const char* kb_, int ds) __attribute__((always_inline)) {
+    return *(const bf16x8_t*)(kb_ + kofs[ds]);
+  };
+  auto vfrag = [&](const char* vb_, int dt, int g) __attribute__((always_inline)) {
+    const char* a = vb_ + vofs[dt] + g * 16 * ROW8;
+    const v4s a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(a));
+    const v4s a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(a + 4 * ROW8));
+    return __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
+
+  // ---- softmax pieces on one S buffer -> the P buffer (per query block c)
+  auto tile_max = [&](f32x16_t (&s)[2], int c) __attribute__((always_inline)) {
+    float t = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) t = fmaxf(t, s[c][r]);
+    return pair_max(t) * scale_log2;
+  };
+  // keys of tile j visible to row block c: register r is key j * 32 + 4 hh + (8 (r >> 2) + (r & 3));
+  // rows see keys < lim (causal: their own position + 1). A tile no row of the wave may see
+  // (past the diagonal, or past S) is masked whole, so its P is 0.
+  auto mask = [&](f32x16_t (&s)[2], int j) __attribute__((always_inline)) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int qi = q0 + 32 * c + ql;
+      const int rel = (causal ? min(qi + 1, S) : S) - (j * W64_KT + 4 * hh);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[c][r] = (8 * (r >> 2) + (r & 3)) < rel ? s[c][r] : -INFINITY;
+    }
+  };
+  auto exps = [&](f32x16_t (&s)[2], int c, int r0, float mneg) __attribute__((always_inline)) {
+    float ps = 0.f;
+#pragma unroll
+    for (int r = r0; r < r0 + 8; ++r) {
+      const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(s[c][r], scale_log2, mneg));
+      s[c][r] = pv;
+      ps += pv;
+    }
+    return ps;
+  };
+  auto pack = [&](f32x16_t (&s)[2], int c) __attribute__((always_inline)) {
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      const int rb = 8 * g;
+      const unsigned lo0 = pack_bf16x2(s[c][rb + 0], s[c][rb + 1]);
+      const unsigned lo1 = pack_bf16x2(s[c][rb + 2], s[c][rb + 3]);
+      const unsigned hi0 = pack_bf16x2(s[c][rb + 4], s[c][rb + 5]);
+      const unsigned hi1 = pack_bf16x2(s[c][rb + 6], s[c][rb + 7]);
+      const auto w0 = __builtin_amdgcn_permlane32_swap(lo0, hi0, false, false);
+      const auto w1 = __builtin_amdgcn_permlane32_swap(lo1, hi1, false, false);
+      typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+      pP[c][g] = __builtin_bit_cast(bf16x8_t, u32x4_t{w0[0], w1[0], w0[1], w1[1]});
+      asm volatile("" : "+a"(pP[c][g]));   // P waits for its P·V in AGPRs
+    }
+  };
+  // online-softmax rescale of O, decided in step j (the row max grew by more than RESCALE_TAU:
+  // rare, and once at the first tile, where O is still zero) and applied at the start of step
+  // j + 1, after open()'s pad (every MFMA writing O has retired) and before P·V(j), the first
+  // contribution at the new scale
+  float pend_alpha[2] = {1.f, 1.f};
+  bool pend = false;
+
+  // ---- one step j: 32 MFMAs, each followed by its share of the step's other work (one work
+  // slot per MFMA, fenced with sched_barrier so the compiler keeps the interleave): MFMAs 0-15
+  // are P·V(j-1) (fragment fk = k >> 1: V^T of dims 32 (fk & 3) .., keys 16 (fk >> 2) ..; row
+  // block c = k & 1), MFMAs 16-31 QK^T(j+1) (fragment fk = 8 + d-step; c = k & 1). Fragments
+  // stream through a 3-deep ring, two fragments ahead. The work slots carry this step's DMA
+  // (K(j+2), V(j)) and the softmax of tile j: row maxima, the rescale decision, 32 exponentials
+  // two per slot, row sums, P packing. Branches (wave-uniform) only at the step's start —
+  // before its first MFMA — and the step ends with a pad, so the allocator's copies at block
+  // boundaries never read an unfinished MFMA.
+  auto step = [&](int j, f32x16_t (&sc)[2], f32x16_t (&sn)[2]) __attribute__((always_inline)) {
+    if (pend) {                 // one O tile at a time through VGPRs, back into its AGPRs
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          __builtin_amdgcn_sched_barrier(0);
+          o[c][dt] *= pend_alpha[c];
+          asm volatile("" : "+a"(o[c][dt]));
+        }
+      __builtin_amdgcn_sched_barrier(0);
+      pend = false;
+    }
+    if (j >= mask_from) mask(sc, j);
+    asm volatile("s_nop 4" ::: "memory");          // VALU writes of O / S before the MFMAs read them
+    const char* vb = vbuf + ((j - 1) & 1) * W64_TILE;
+    const char* kb_ = kbuf + ((j + 1) & 1) * W64_TILE;
+    // this step's DMA is unconditional (no branch between MFMAs): a tile past S reads as zeros
+    const unsigned lk = lds_base + (j & 1) * W64_TILE, lv = lds_base + 2 * W64_TILE + (j & 1) * W64_TILE;
+    float t[2] = {-INFINITY, -INFINITY}, ps[2] = {0.f, 0.f};
+    bf16x8_t ring[3];
+    bf16x8_t (&qv)[2][8] = qf;   // named here: clang does not capture qf through the asm operands below
+    auto load = [&](int fk) __attribute__((always_inline)) {
+      ring[fk % 3] = fk < 8 ? vfrag(vb, fk & 3, fk >> 2) : kfrag(kb_, fk - 8);
+    };
+    auto mfma = [&](int k) __attribute__((always_inline)) {
+      const int fk = k >> 1, c = k & 1;
+      if (k < 16) {
+        W64_MFMA_PV(o[c][fk & 3], ring[fk % 3], pP[c][fk >> 2]);
+      } else if (fk == 8) {
+        W64_MFMA_QK0(sn[c], ring[fk % 3], qv[c][0]);
+      } else {
+        W64_MFMA_QK(sn[c], ring[fk % 3], qv[c][fk - 8]);
+      }
+    };
+    auto dma1 = [&](const i32x4_t& r, unsigned voff, int stride, int tt, unsigned lds, int i) __attribute__((always_inline)) {
+      const int soff = __builtin_amdgcn_readfirstlane((tt * W64_KT + 16 * i) * stride * 2);
+      const unsigned dst = __builtin_amdgcn_readfirstlane(lds + i * 4096 + wave * 1024);
+      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                   :
+                   : "s"(dst), "v"(voff), "s"(r), "s"(soff)
+                   : "memory", "m0");
+    };
+    auto mx = [&](int c, int r0) __attribute__((always_inline)) {
+#pragma unroll
+      for (int r = r0; r < r0 + 8; ++r) t[c] = fmaxf(t[c], sc[c][r]);
+    };
+    auto ex = [&](int e) __attribute__((always_inline)) {      // 2 exponentials: row block e >> 3, regs 2 (e & 7) ..
+      const int c = e >> 3, r = 2 * (e & 7);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) sc[c][r + i] = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[c][r + i], scale_log2, -m[c]));
+    };
+    auto sm = [&](int c, int q) __attribute__((always_inline)) {   // row sum of regs 4 q .. 4 q + 3
+#pragma unroll
+      for (int r = 4 * q; r < 4 * q + 4; ++r) ps[c] += sc[c][r];
+    };
+    auto pk = [&](int c, int g) __attribute__((always_inline)) {
+      const int rb = 8 * g;
+      const unsigned lo0 = pack_bf16x2(sc[c][rb + 0], sc[c][rb + 1]);
+      const unsigned lo1 = pack_bf16x2(sc[c][rb + 2], sc[c][rb + 3]);
+      const unsigned hi0 = pack_bf16x2(sc[c][rb + 4], sc[c][rb + 5]);
+      const unsigned hi1 = pack_bf16x2(sc[c][rb + 6], sc[c][rb + 7]);
+      const auto w0 = __builtin_amdgcn_permlane32_swap(lo0, hi0, false, false);
+      const auto w1 = __builtin_amdgcn_permlane32_swap(lo1, hi1, false, false);
+      typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+      pP[c][g] = __builtin_bit_cast(bf16x8_t, u32x4_t{w0[0], w1[0], w0[1], w1[1]});
+      asm volatile("" : "+a"(pP[c][g]));   // P waits for its P·V in AGPRs
+    };
+    auto work = [&](int k) __attribute__((always_inline)) {
+      switch (k) {
+        case 0: dma1(rK, voffK, k_stride, j + 2, lk, 0); mx(0, 0); break;
+        case 1: dma1(rK, voffK, k_stride, j + 2, lk, 1); mx(0, 8); break;
+        case 2: dma1(rV, voffV, v_stride, j, lv, 0); mx(1, 0); break;
+        case 3: dma1(rV, voffV, v_stride, j, lv, 1); mx(1, 8); break;
+        case 4:
+          t[0] = pair_max(t[0]) * scale_log2;
+          t[1] = pair_max(t[1]) * scale_log2;
+          break;
+        case 5: {
+          const bool g0 = t[0] > m[0] + RESCALE_TAU, g1 = t[1] > m[1] + RESCALE_TAU;
+          const float m0n = g0 ? t[0] : m[0], m1n = g1 ? t[1] : m[1];
+          const float a0 = __builtin_amdgcn_exp2f(m[0] - m0n), a1 = __builtin_amdgcn_exp2f(m[1] - m1n);
+          pend = __builtin_amdgcn_ballot_w64(g0 || g1) != 0;
+          pend_alpha[0] = a0;
+          pend_alpha[1] = a1;
+          m[0] = m0n;
+          m[1] = m1n;
+          l[0] *= a0;
+          l[1] *= a1;
+          break;
+        }
+        case 22: sm(0, 0); sm(0, 1); break;
+        case 23: sm(0, 2); sm(0, 3); break;
+        case 24: sm(1, 0); sm(1, 1); break;
+        case 25: sm(1, 2); sm(1, 3); break;
+        case 26: pk(0, 0); break;
+        case 27: pk(0, 1); break;
+        case 28: pk(1, 0); break;
+        case 29: pk(1, 1); break;
+        case 30:
+          l[0] += pair_sum(ps[0]);
+          l[1] += pair_sum(ps[1]);
+          break;
+        default:
+          if (k >= 6 && k < 22) ex(k - 6);
+          break;
+      }
+    };
+    load(0);
+    load(1);
+    // 32 slots, expanded at compile time (a rolled loop would index the fragment ring at run time)
+    w64_static_for<0, 32>([&](auto kc) __attribute__((always_inline)) {
+      constexpr int k = decltype(kc)::value;
+      __builtin_amdgcn_sched_barrier(0);
+      mfma(k);
+      if constexpr ((k & 1) == 0 && (k >> 1) + 2 < 16) load((k >> 1) + 2);
+      work(k);
+    });
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");   // this step's MFMAs retire before any copy
+  };
+
+  // ---- prologue: zero P and the V ring (step 0's P·V(-1) then adds 0), K(0), K(1); S(0) = K(0) Q^T
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      pP[c][g] = bf16x8_t{};
+      asm volatile("" : "+a"(pP[c][g]));
+    }
+#pragma unroll
+  for (int i = 0; i < 2 * W64_TILE / (256 * 16); ++i)
+    *(u16x8_t*)(vbuf + (i * 256 + tid) * 16) = u16x8_t{};
+  if (0 < nkt) dma(rK, voffK, k_stride, 0, lds_base);
+  if (1 < nkt) dma(rK, voffK, k_stride, 1, lds_base + W64_TILE);
+  asm volatile("s_nop 4" ::: "memory");        // Q / P AGPR writes before their first MFMA read
+  __syncthreads();                             // the V ring's zeros (LDS stores) before any read
+  sync();
+#pragma unroll
+  for (int ds = 0; ds < 8; ++ds) {
+    const bf16x8_t f = kfrag(kbuf, ds);
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      if (ds == 0)
+        W64_MFMA_QK0(sA[c], f, qf[c][0]);
+      else
+        W64_MFMA_QK(sA[c], f, qf[c][ds]);
+    }
+  }
+  asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
+
+  // ---- iterations j = 0, 1, ... (barriers and DMAs are collective: every wave runs the same
+  // count, nkt + 1 rounded up to even): open() = wait for this wave's DMAs, barrier, DMA K(j+2)
+  // and V(j) into the slots iteration j-1 finished reading. A wave computes steps j <= nlive
+  // (step nlive is the last P·V; its softmax sees a fully masked tile and QK^T(nlive + 1) is
+  // never used) and only stages tiles after that. S(j) is in sA for even j, sB for odd j.
+  auto open = [&]() __attribute__((always_inline)) {
+    sync();
+    asm volatile("s_nop 15\n\ts_nop 3" ::: "memory");   // AGPR writes / MFMA results of the last step
+  };
+  // steps 0 .. nlive in pairs (no branch around a step inside the loop: a join there made the
+  // allocator keep O in VGPRs and copy it into AGPRs every iteration), then the odd last step,
+  // then staging-only iterations up to the block's common count
+  int j = 0;
+  for (; j + 1 <= nlive; j += 2) {
+    open();
+    step(j, sA, sB);
+    open();
+    step(j + 1, sB, sA);
+  }
+  if (j <= nlive) {
+    open();
+    step(j, sA, sB);
+    ++j;
+  }
+  for (; j <= nkt; ++j) {            // every wave opens nkt + 1 iterations in all
+    open();
+    dma_tiles(j);
+  }
+
+  // ---- epilogue: O^T (AGPR) / l -> bf16 rows, widened stores
+  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int qi = q0 + 32 * c + ql;
+    // O stays in AGPRs until here (pinned), so the loop's exit value is not copied to VGPRs early
+    asm volatile("" : "+a"(o[c][0]), "+a"(o[c][1]), "+a"(o[c][2]), "+a"(o[c][3]));
+    f32x16_t oc[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) oc[dt] = o[c][dt];
+    store_o_wide(oc, 1.f / l[c], O + (((size_t)b * S + min(qi, S - 1)) * Hq + h) * 128, hh, qi < S);
+  }
+}
+
+template <int FLAGS = 0>
+int launch_w64(const void* q, const void* k, const void* v, void* o, int B, int S, int Hq, int Hkv, int qs, int ks,
+               int vs, float scale_log2, int causal, hipStream_t stream) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)flash_fwd_d128_w64<FLAGS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              W64_LDS);
+    attr = true;
+  }
+  const int nqb = (S + W64_QR - 1) / W64_QR;
+  flash_fwd_d128_w64<FLAGS><<<dim3((unsigned)(B * Hq * nqb)), dim3(256), W64_LDS, stream>>>(
+      (const unsigned short*)q, (const unsigned short*)k, (const unsigned short*)v, (unsigned short*)o, B, S, Hq,
+      Hkv, qs, ks, vs, scale_log2, causal & 1);
+  return gs_launch_status();
+}
+
 int g_attn_variant = 0;   // 0 = auto, 1 = 16x16 4-wave kernel, 2 = 32x32 4-wave, 3 = 32x32 8-wave
 
 template <int NW, int FLAGS = 0>
@@ -969,6 +1436,12 @@ GS_KERNEL_API int gs_flash_attn_fwd_bf16(const void* q, const void* k, const voi
     return launch_pp<PP_PRIO | PP_TRACE>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
   if (D == 128 && pp_ok && g_attn_variant == 12)
     return launch_pp<PP_SPRIO | PP_WIDE>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
+  if (D == 128 && pp_ok && g_attn_variant == 14)
+    return launch_w64<0>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
+  if (D == 128 && pp_ok && g_attn_variant == 16)
+    return launch_w64<W64_PAD>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
+  if (D == 128 && pp_ok && g_attn_variant == 15)
+    return launch_w64<W64_BUILTIN_DMA>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
   if (D == 128 && (g_attn_variant == 13 || g_attn_variant == 0))
     return launch_w8<4, AF_WIDE>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
   if (D == 128 && pp_ok && g_attn_variant == 9)
@@ -998,9 +1471,10 @@ GS_KERNEL_API int gs_flash_attn_fwd_bf16(const void* q, const void* k, const voi
 // + late (T14) loads, 6 = 4-wave + late loads, 7 = ping-pong 8-wave (MFMA-segment priority), 8 = ping-pong
 // without the priority, 9 = ping-pong + interleaved partner rows (measured 1-3 % slower), 10 = ping-pong with the
 // segment trace (gs_attn_trace), 11 = ping-pong + widened store tail, 12 = ping-pong with static
-// younger-half priority + widened store tail, 13 = 4-wave 32x32 + widened store tail.
+// younger-half priority + widened store tail, 13 = 4-wave 32x32 + widened store tail, 14 = one wave
+// per SIMD with 64 rows (flash_fwd_d128_w64), 15 = the same with compiler-issued LDS DMA (diagnostics).
 GS_KERNEL_API int gs_attn_set_variant(int v) {
-  if (v < 0 || v > 13) return GS_EINVAL;
+  if (v < 0 || v > 16) return GS_EINVAL;
   g_attn_variant = v;
   return GS_OK;
 }
