@@ -1178,9 +1178,9 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_d128_w64(const unsigned shor
         }
       __builtin_amdgcn_sched_barrier(0);
       pend = false;
+      asm volatile("s_nop 4" ::: "memory");        // VALU writes of O before the MFMAs read it
     }
     if (j >= mask_from) mask(sc, j);
-    asm volatile("s_nop 4" ::: "memory");          // VALU writes of O / S before the MFMAs read them
     const char* vb = vbuf + ((j - 1) & 1) * W64_TILE;
     const char* kb_ = kbuf + ((j + 1) & 1) * W64_TILE;
     // this step's DMA is unconditional (no branch between MFMAs): a tile past S reads as zeros
@@ -1281,11 +1281,12 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_d128_w64(const unsigned shor
       constexpr int k = decltype(kc)::value;
       __builtin_amdgcn_sched_barrier(0);
       mfma(k);
+      __builtin_amdgcn_sched_barrier(0);       // the slot's work stays behind its MFMA
       if constexpr ((k & 1) == 0 && (k >> 1) + 2 < 16) load((k >> 1) + 2);
       work(k);
     });
     __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");   // this step's MFMAs retire before any copy
+    if constexpr ((FLAGS & W64_PAD) != 0) asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
   };
 
   // ---- prologue: zero P and the V ring (step 0's P·V(-1) then adds 0), K(0), K(1); S(0) = K(0) Q^T
@@ -1324,7 +1325,7 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_d128_w64(const unsigned shor
   // never used) and only stages tiles after that. S(j) is in sA for even j, sB for odd j.
   auto open = [&]() __attribute__((always_inline)) {
     sync();
-    asm volatile("s_nop 15\n\ts_nop 3" ::: "memory");   // AGPR writes / MFMA results of the last step
+    asm volatile("s_nop 2" ::: "memory");   // P's AGPR writes (last step) before the P·V MFMAs read them
   };
   // steps 0 .. nlive in pairs (no branch around a step inside the loop: a join there made the
   // allocator keep O in VGPRs and copy it into AGPRs every iteration), then the odd last step,
