@@ -945,7 +945,11 @@ int launch_pp(const void* q, const void* k, const void* v, void* o, int B, int S
 constexpr int W64_QR = 256;                 // rows per block: 4 waves x 64
 // diagnostics: compiler-issued LDS DMA (waits for it at every LDS read); a 64-cycle pad after every
 // MFMA group
-enum { W64_BUILTIN_DMA = 1, W64_PAD = 2 };
+// timing-only diagnostics (wrong results): no iteration barrier / no in-step DMA
+// W64_REGSTAGE: the step's K/V tiles come through AGPRs (buffer_load into AGPRs in the first work
+// slots, ds_write_b128 from them at the step's end) instead of LDS DMA, whose issue costs ~60
+// cycles a piece beside MFMAs (measured: the in-step DMA was 15 % of the kernel's time)
+enum { W64_BUILTIN_DMA = 1, W64_PAD = 2, W64_T_NOBAR = 4, W64_T_NODMA = 8, W64_REGSTAGE = 16 };
 constexpr int W64_KT = 32, W64_TILE = W64_KT * ROW8, W64_LDS = 4 * W64_TILE;
 
 typedef int i32x4_t __attribute__((ext_vector_type(4)));
@@ -1078,7 +1082,7 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_d128_w64(const unsigned shor
   auto sync = [&]() __attribute__((always_inline)) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
+    if constexpr ((FLAGS & W64_T_NOBAR) == 0) __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("" ::: "memory");
   };
@@ -1201,13 +1205,20 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_d128_w64(const unsigned shor
         W64_MFMA_QK(sn[c], ring[fk % 3], qv[c][fk - 8]);
       }
     };
+    bf16x8_t stg[4];                           // W64_REGSTAGE: K rows (0, 1), V rows (2, 3) in flight
     auto dma1 = [&](const i32x4_t& r, unsigned voff, int stride, int tt, unsigned lds, int i) __attribute__((always_inline)) {
       const int soff = __builtin_amdgcn_readfirstlane((tt * W64_KT + 16 * i) * stride * 2);
-      const unsigned dst = __builtin_amdgcn_readfirstlane(lds + i * 4096 + wave * 1024);
-      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
-                   :
-                   : "s"(dst), "v"(voff), "s"(r), "s"(soff)
-                   : "memory", "m0");
+      if constexpr ((FLAGS & W64_REGSTAGE) != 0) {
+        // the load's destination is written when it lands: read only after the explicit vmcnt(0)
+        asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=a"(stg[(&r == &rK ? 0 : 2) + i])
+                     : "v"(voff), "s"(r), "s"(soff) : "memory");
+      } else {
+        const unsigned dst = __builtin_amdgcn_readfirstlane(lds + i * 4096 + wave * 1024);
+        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                     :
+                     : "s"(dst), "v"(voff), "s"(r), "s"(soff)
+                     : "memory", "m0");
+      }
     };
     auto mx = [&](int c, int r0) __attribute__((always_inline)) {
 #pragma unroll
@@ -1236,10 +1247,10 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_d128_w64(const unsigned shor
     };
     auto work = [&](int k) __attribute__((always_inline)) {
       switch (k) {
-        case 0: dma1(rK, voffK, k_stride, j + 2, lk, 0); mx(0, 0); break;
-        case 1: dma1(rK, voffK, k_stride, j + 2, lk, 1); mx(0, 8); break;
-        case 2: dma1(rV, voffV, v_stride, j, lv, 0); mx(1, 0); break;
-        case 3: dma1(rV, voffV, v_stride, j, lv, 1); mx(1, 8); break;
+        case 0: if constexpr ((FLAGS & W64_T_NODMA) == 0) dma1(rK, voffK, k_stride, j + 2, lk, 0); mx(0, 0); break;
+        case 1: if constexpr ((FLAGS & W64_T_NODMA) == 0) dma1(rK, voffK, k_stride, j + 2, lk, 1); mx(0, 8); break;
+        case 2: if constexpr ((FLAGS & W64_T_NODMA) == 0) dma1(rV, voffV, v_stride, j, lv, 0); mx(1, 0); break;
+        case 3: if constexpr ((FLAGS & W64_T_NODMA) == 0) dma1(rV, voffV, v_stride, j, lv, 1); mx(1, 8); break;
         case 4:
           t[0] = pair_max(t[0]) * scale_log2;
           t[1] = pair_max(t[1]) * scale_log2;
@@ -1287,6 +1298,17 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_d128_w64(const unsigned shor
     });
     __builtin_amdgcn_sched_barrier(0);
     if constexpr ((FLAGS & W64_PAD) != 0) asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
+    if constexpr ((FLAGS & W64_REGSTAGE) != 0) {
+      // the staged rows into this step's K / V slots (free since the barrier that opened the
+      // step), at the lane-linear positions the DMA would have written
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const unsigned base = (i < 2 ? lk : lv) + (unsigned)((i & 1) * 4096 + wave * 1024 + lane * 16);
+        asm volatile("ds_write_b128 %0, %1" ::"v"(base), "a"(stg[i]) : "memory");
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
   };
 
   // ---- prologue: zero P and the V ring (step 0's P·V(-1) then adds 0), K(0), K(1); S(0) = K(0) Q^T
@@ -1439,6 +1461,14 @@ GS_KERNEL_API int gs_flash_attn_fwd_bf16(const void* q, const void* k, const voi
     return launch_pp<PP_SPRIO | PP_WIDE>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
   if (D == 128 && pp_ok && g_attn_variant == 14)
     return launch_w64<0>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
+  if (D == 128 && pp_ok && g_attn_variant == 17)
+    return launch_w64<W64_T_NOBAR>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
+  if (D == 128 && pp_ok && g_attn_variant == 18)
+    return launch_w64<W64_T_NODMA>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
+  if (D == 128 && pp_ok && g_attn_variant == 19)
+    return launch_w64<W64_T_NODMA | W64_T_NOBAR>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
+  if (D == 128 && pp_ok && g_attn_variant == 20)
+    return launch_w64<W64_REGSTAGE>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
   if (D == 128 && pp_ok && g_attn_variant == 16)
     return launch_w64<W64_PAD>(q, k, v, o, B, S, Hq, Hkv, q_stride, k_stride, v_stride, sl2, causal, stream);
   if (D == 128 && pp_ok && g_attn_variant == 15)
@@ -1475,7 +1505,7 @@ GS_KERNEL_API int gs_flash_attn_fwd_bf16(const void* q, const void* k, const voi
 // younger-half priority + widened store tail, 13 = 4-wave 32x32 + widened store tail, 14 = one wave
 // per SIMD with 64 rows (flash_fwd_d128_w64), 15 = the same with compiler-issued LDS DMA (diagnostics).
 GS_KERNEL_API int gs_attn_set_variant(int v) {
-  if (v < 0 || v > 16) return GS_EINVAL;
+  if (v < 0 || v > 20) return GS_EINVAL;
   g_attn_variant = v;
   return GS_OK;
 }

@@ -37,7 +37,7 @@ def test_attention_kernels_agree_with_fp32(B, S, Hq, Hkv, causal):
     v = torch.randn(B, S, Hkv, 128, device="cuda", dtype=torch.bfloat16)
     ref = reference_attention(q, k, v, causal=causal)
     try:
-        for var in (ATTN_AUTO, ATTN_V1, 2, 3, 7, 8, 9, 11, 12, 13, 14):
+        for var in (ATTN_AUTO, ATTN_V1, 2, 3, 7, 8, 9, 11, 12, 13, 14, 20):
             set_attention_variant(var)
             out = attention(q, k, v, causal=causal)
             torch.cuda.synchronize()
