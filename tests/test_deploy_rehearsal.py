@@ -1,0 +1,150 @@
+"""The shipped manifests, run as a node would run them (sim/deploy.py): the DaemonSet's container
+and the scheduler extender's Deployment start from their own commands, env and hostPath volumes;
+kube-scheduler's side follows the extender ConfigMap; the reference's bin-pack demo
+(deploy/demo/binpack-1) is scheduled and admitted; the probes the manifests declare answer; and
+``kubectl-inspect-gpushare`` reports the result. Overrides (no GPU, no cluster) are listed in the
+module docstring of sim/deploy.py and asserted below to be nothing else."""
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+
+import pytest
+
+from aliyun_gpushare_device_plugin_amd import const
+from aliyun_gpushare_device_plugin_amd.cluster import objects as O
+from aliyun_gpushare_device_plugin_amd.cluster.client import APIClient, KubeConfig
+from aliyun_gpushare_device_plugin_amd.sim import deploy as D
+from aliyun_gpushare_device_plugin_amd.sim.apiserver import FakeAPIServer, make_node
+from aliyun_gpushare_device_plugin_amd.sim.kubelet import FakeKubelet
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NODE = "mi355x-0"
+
+
+@pytest.fixture
+def hostroot():
+    d = tempfile.mkdtemp(prefix="gsd-", dir="/tmp")       # short: unix socket paths are limited
+    yield d
+    shutil.rmtree(d, ignore_errors=True)
+
+
+def _stop(p):
+    if p is not None and p.poll() is None:
+        p.terminate()
+        try:
+            p.wait(timeout=10)
+        except subprocess.TimeoutExpired:
+            p.kill()
+
+
+def test_shipped_manifests_run_a_node(hostroot):
+    api = FakeAPIServer()
+    api.start()
+    client = APIClient(KubeConfig(api.url))
+    client.create_node(make_node(NODE))
+    plugin = ext = None
+    kubelet = FakeKubelet(os.path.join(hostroot, "device-plugin"), APIClient(KubeConfig(api.url)), NODE).start()
+    try:
+        # ---- the DaemonSet, as the kubelet would start it on NODE
+        ds = next(d for d in D.load(os.path.join(ROOT, "deploy", "device-plugin-ds.yaml")) if d["kind"] == "DaemonSet")
+        assert ds["spec"]["template"]["spec"]["nodeSelector"] == {"gpushare": "true"}
+        assert make_node(NODE)["metadata"]["labels"]["gpushare"] == "true"
+        mport = D.free_port()
+        overrides = {"--smi-backend": "fake:2x288G", "--metrics-addr": f"127.0.0.1:{mport}", "--apiserver": api.url}
+        ct = D.resolve(ds, hostroot, {"spec.nodeName": NODE}, overrides, skip_volumes=("sys",))
+        # the kubelet socket directory is the binary's default (not written in the manifest): the
+        # container sees it at that path through the device-plugin mount
+        ct.argv.append("--device-plugin-dir=" + ct.host_path(const.DEVICE_PLUGIN_PATH))
+        # the pod-resources socket the manifest names is the kubelet's (hostPath mount)
+        podres = ct.host_path("/var/lib/kubelet/pod-resources/kubelet.sock")
+        os.symlink(kubelet.podres_sock, podres)
+        assert ct.host_path("/var/lib/kubelet/device-plugins") == kubelet.dir
+        assert ct.env["NODE_NAME"] == NODE
+        plugin = D.start(ct, os.path.join(hostroot, "plugin.log"))
+        assert kubelet.registered.wait(60), open(os.path.join(hostroot, "plugin.log")).read()[-3000:]
+        assert D.wait_for(lambda: O.node_allocatable(client.get_node(NODE), const.RESOURCE_NAME) == 576, 30)
+        # the probes the manifest declares (port remapped from 9400)
+        probes = ds["spec"]["template"]["spec"]["containers"][0]
+        for probe in ("livenessProbe", "readinessProbe"):
+            path = probes[probe]["httpGet"]["path"]
+            assert D.wait_for(lambda: D.http_get(f"http://127.0.0.1:{mport}{path}")[0] == 200, 20), path
+        # --install-shim put the quota shim into the gpushare-lib hostPath
+        shim = ct.host_path(os.path.join("/var/lib/gpushare/lib", const.SHIM_LIB_NAME))
+        assert os.path.isfile(shim)
+
+        # ---- the scheduler extender Deployment and kube-scheduler's config for it
+        docs = D.load(os.path.join(ROOT, "deploy", "scheduler-extender.yaml"))
+        dep = next(d for d in docs if d["kind"] == "Deployment")
+        ect = D.resolve(dep, hostroot, {}, {"--apiserver": api.url, "--port": "0", "--host": "127.0.0.1",
+                                            "--resync": "0.5"})
+        ext = D.start(ect, os.path.join(hostroot, "extender.log"))
+        eport = int(ext.stdout.readline().split()[1])
+        cm = next(d for d in docs if d["kind"] == "ConfigMap")
+        sched = D.Scheduler(cm["data"]["scheduler-config.yaml"], f"127.0.0.1:{eport}")
+        assert sched.managed == [const.RESOURCE_NAME]
+
+        # ---- the reference's bin-pack demo: StatefulSet (3 replicas) + Job, 2 GiB each
+        demo = D.load(os.path.join(ROOT, "deploy", "demo", "binpack-1", "binpack-1.yaml")) + \
+            D.load(os.path.join(ROOT, "deploy", "demo", "binpack-1", "job.yaml"))
+        pods = []
+        for d in demo:
+            if d["kind"] not in ("StatefulSet", "Job"):
+                continue
+            tpl = D.pod_template(d)
+            for i in range(d["spec"].get("replicas", 1)):
+                pod = {"apiVersion": "v1", "kind": "Pod",
+                       "metadata": {"name": f"{d['metadata']['name']}-{i}", "namespace": "default",
+                                    "labels": dict(tpl.get("metadata", {}).get("labels", {}))},
+                       "spec": {**tpl["spec"], "schedulerName": "default-scheduler"}}
+                pods.append(client.create_pod("default", pod))
+        assert len(pods) == 4
+        for pod in pods:
+            placed = []                                        # the extender's informer catches up
+            assert D.wait_for(lambda: placed.append(sched.schedule(pod, [NODE])) or placed[-1] == NODE, 10, 0.1), \
+                O.name(pod)
+            bound = client.get_pod("default", O.name(pod))
+            adm = kubelet.admit(bound)
+            assert adm.error is None, adm.error
+            envs = adm.responses[0].envs
+            assert envs[const.ENV_RESOURCE_INDEX] == O.annotations(bound)[const.ENV_RESOURCE_INDEX]
+            assert int(envs["ALIYUN_COM_GPU_MEM_CONTAINER"]) == 2
+            # the shim the DaemonSet installed is what the container gets mounted and preloaded
+            mounts = {m.container_path: m.host_path for m in adm.responses[0].mounts}
+            assert any(h.startswith(ct.host_path("/var/lib/gpushare/lib")) for h in mounts.values()), mounts
+            assert "LD_PRELOAD" in envs
+        # best fit packs all four 2 GiB pods onto one GPU
+        gpus = {O.annotations(client.get_pod("default", O.name(p)))[const.ENV_RESOURCE_INDEX] for p in pods}
+        assert len(gpus) == 1
+
+        # ---- kubectl-inspect-gpushare against the same apiserver
+        r = subprocess.run([sys.executable, "-m", D.ENTRY_POINTS["kubectl-inspect-gpushare"], "--apiserver", api.url],
+                           capture_output=True, text=True, timeout=60,
+                           env=dict(os.environ, PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", "")))
+        assert r.returncode == 0, r.stdout + r.stderr
+        assert NODE in r.stdout and "8/576" in r.stdout.replace(" ", ""), r.stdout
+    finally:
+        _stop(ext)
+        _stop(plugin)
+        kubelet.stop()
+        api.stop()
+
+
+def test_rehearsal_overrides_are_only_the_documented_ones():
+    """Nothing but the SMI backend, the apiserver and the listening address/port differs from the
+    manifests: every other flag reaches the process as written (paths remapped)."""
+    ds = next(d for d in D.load(os.path.join(ROOT, "deploy", "device-plugin-ds.yaml")) if d["kind"] == "DaemonSet")
+    root = tempfile.mkdtemp(prefix="gsd-", dir="/tmp")
+    try:
+        ct = D.resolve(ds, root, {"spec.nodeName": NODE},
+                       {"--smi-backend": "fake:2x288G", "--metrics-addr": "127.0.0.1:1", "--apiserver": "http://x"},
+                       skip_volumes=("sys",))
+        cmd = ds["spec"]["template"]["spec"]["containers"][0]["command"]
+        want = [D._rewrite(a, ct.mounts) for a in cmd[1:]
+                if a.partition("=")[0] not in ("--smi-backend", "--metrics-addr")]
+        got = ct.argv[3:]
+        assert [a for a in got if a.partition("=")[0] not in ("--smi-backend", "--metrics-addr", "--apiserver")] == want
+        assert all(not a.startswith("/var/lib/gpushare") for a in got)   # every hostPath remapped
+    finally:
+        shutil.rmtree(root, ignore_errors=True)
