@@ -465,7 +465,9 @@ class PodFleet:
         self.released_residue = 0             # shim-ledger bytes a stopped pod still held after freeing
         self.release_ms: list[float] = []     # stop -> the GPU physically has room for the replacement
         self.release_by_size: dict[int, list] = {}
-        self._stopped_at = None                # (time, size) of the last retirement, until its room came back
+        self.release_gbps: list[float] = []    # retired pod's bytes / (stop -> room back): amdgpu's wipe rate
+        self.retired_bytes = 0                 # HBM the retired pods held (turned over by amdgpu)
+        self._stopped_at = None                # (time, size, held bytes) of the last retirement, until its room came back
         self.phase_ms: dict[str, list] = {"stop": [], "init": [], "room": [], "alloc": [], "hold": []}
         self.trace: list | None = [] if os.environ.get("GS_BENCH_POD_TRACE") else None
         self._vram_used, self._vram_total = self._vram_reader()
@@ -544,8 +546,11 @@ class PodFleet:
         t2 = time.perf_counter()
         free2 = self._vram_total - self._vram_used() if self._vram_used is not None else None
         if self._stopped_at is not None:                # retired pod's HBM back (room for this one)
-            self.release_ms.append(time.perf_counter() - self._stopped_at[0])
-            self.release_by_size.setdefault(self._stopped_at[1], []).append(time.perf_counter() - self._stopped_at[0])
+            dt_rel = time.perf_counter() - self._stopped_at[0]
+            self.release_ms.append(dt_rel)
+            self.release_by_size.setdefault(self._stopped_at[1], []).append(dt_rel)
+            if self._stopped_at[2] > 0:
+                self.release_gbps.append(self._stopped_at[2] / dt_rel / 1e9)
             self._stopped_at = None
         w["proc"].stdin.write('{"cmd":"alloc"}\n')
         ev = self._wait(w, "ready")
@@ -586,7 +591,8 @@ class PodFleet:
         ev = self._wait(w, "done")                      # freed through KFD at this point
         self.phase_ms["stop"].append(time.perf_counter() - t0)
         threading.Thread(target=w["proc"].wait, daemon=True).start()   # reap the exit off the path
-        self._stopped_at = (t0, w["size"])
+        self._stopped_at = (t0, w["size"], w["ready"].get("held", 0))
+        self.retired_bytes += w["ready"].get("held", 0)
         if self._vram_used is not None and wait_release:
             self._wait_room(w["ready"].get("held", 0), limit_s=20.0)
         self.released_residue = max(self.released_residue, ev.get("used_after_release") or 0)
@@ -734,6 +740,8 @@ def main():
         fleet.ready_ms.clear()
         fleet.release_ms.clear()
         fleet.release_by_size.clear()
+        fleet.release_gbps.clear()
+        fleet.retired_bytes = 0
         for v in fleet.phase_ms.values():
             v.clear()
 
@@ -759,6 +767,8 @@ def main():
     residue = gather(fleet.released_residue if fleet is not None else 0)
     release = gather(fleet.release_ms if fleet is not None else [])
     release_all = [x for r in release for x in r]
+    retired = gather(fleet.retired_bytes if fleet is not None else 0)
+    rel_rate = [x for r in gather(fleet.release_gbps if fleet is not None else []) for x in r]
     by_size: dict = {}
     phases: dict = {}
     for d in gather(fleet.phase_ms if fleet is not None else {}):
@@ -862,6 +872,11 @@ def main():
             "failed_admissions": cp.failed,
             "failure_reasons": cp.fail_reasons[:5],
             "gemm_tflops_node": round(gemm_flops / elapsed / 1e12, 1) if use_gpu else None,
+            # the churn's physical bound: every cycle turns a retired pod's HBM over, and amdgpu wipes
+            # freed VRAM before it returns it. Turnover per GPU near the wipe rate = the step is at
+            # that bound, not in the plugin (control_plane_ms_per_admission is the plugin's share).
+            "hbm_turnover_GBps_per_gpu": round(sum(retired) / n / elapsed / 1e9, 1) if use_gpu else None,
+            "amdgpu_release_GBps_p50": round(pct(rel_rate, 0.5), 1) if rel_rate else None,
         }
         if topo_report is not None:
             res["topology"] = topo_report
