@@ -45,6 +45,8 @@ SIGNATURES = {
     "gs_skinny_set_wg_target": [_I],
     "gs_skinny_set_rope": [_P, _P, _I, _P, _P, _P, _I, _I, _I],
     "gs_skinny_set_lds_waves": [_I],
+    "gs_skinny_set_prefetch": [_I],
+    "gs_skinny_get_prefetch": [],
 }
 
 ERRORS = {1: "invalid arguments", 2: "kernel launch failed"}

@@ -146,7 +146,11 @@ struct NormIn {
   float eps;
 };
 
-template <int MT, int NW, bool SWIGLU = false, bool NORM = false>
+// PF = 2: two k-slices in flight per workgroup instead of one. A register ring of two slices
+// (buffer loads; a slice past the workgroup's K range goes through a zero-size descriptor, so it
+// costs no memory traffic and the load stream stays branch-free for the compiler's vmcnt
+// accounting) — the next-but-one slice is requested before the current one is multiplied.
+template <int MT, int NW, bool SWIGLU = false, bool NORM = false, int PF = 1>
 __global__ __launch_bounds__(NW * 64) void skinny_lds(const unsigned short* __restrict__ X, int ldx,
                                                   const unsigned short* __restrict__ W, int ldw,
                                                   float* __restrict__ part, unsigned short* __restrict__ Y,
@@ -202,12 +206,7 @@ __global__ __launch_bounds__(NW * 64) void skinny_lds(const unsigned short* __re
   const int r16 = lane & 15, kof = (lane >> 4) * 8;
   const unsigned short* wl = sW + (16 * wave + r16) * LROW + kof;
 
-  gload(k0);
-  lstore();
-  __syncthreads();
-  for (int kk = k0; kk < k1; kk += LBK) {
-    const bool more = kk + LBK < k1;
-    if (more) gload(kk + LBK);
+  auto mma = [&]() {
 #pragma unroll
     for (int ks = 0; ks < LBK / 32; ++ks) {
       const bf16x8_t wf = *(const bf16x8_t*)(wl + ks * 32);
@@ -217,10 +216,85 @@ __global__ __launch_bounds__(NW * 64) void skinny_lds(const unsigned short* __re
         acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, xf, acc[t], 0, 0, 0);
       }
     }
+  };
+
+  if constexpr (PF == 2) {
+    typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+    // descriptors: this workgroup's W rows, all of X (rows >= M read as zero), the norm weight
+    const __amdgpu_buffer_rsrc_t rW =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(W + (size_t)n0 * ldw), (short)0, 16 * NW * ldw * 2, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, M * ldx * 2, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rN =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(NORM ? nrm.w : X), (short)0, NORM ? K * 2 : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rD = __builtin_amdgcn_make_buffer_rsrc((void*)W, (short)0, 0, 0x00020000);
+    // the bounds check sees the VGPR offset only: rows go there, the k-slice into the SGPR offset
+    const int vW = (lr * ldw + lc) * 2;
+    u32x4_t w2[2][8], x2[2][XI], n2[2];
+    auto gl = [&](u32x4_t(&wv)[8], u32x4_t(&xv)[XI], u32x4_t& nv, int kk) {
+      const bool live = kk < k1;
+      const __amdgpu_buffer_rsrc_t rw = live ? rW : rD, rx = live ? rX : rD, rn = live ? rN : rD;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) wv[i] = __builtin_amdgcn_raw_buffer_load_b128(rw, vW, (RPI * i * ldw + kk) * 2, 0);
+#pragma unroll
+      for (int i = 0; i < XI; ++i)
+        xv[i] = __builtin_amdgcn_raw_buffer_load_b128(rx, ((RPI * i + lr) * ldx + lc) * 2, kk * 2, 0);
+      if constexpr (NORM) nv = __builtin_amdgcn_raw_buffer_load_b128(rn, lc * 2, kk * 2, 0);
+    };
+    auto ls = [&](const u32x4_t(&wv)[8], const u32x4_t(&xv)[XI], const u32x4_t& nv) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) *(u32x4_t*)(sW + (RPI * i + lr) * LROW + lc) = wv[i];
+#pragma unroll
+      for (int i = 0; i < XI; ++i) {
+        u16x8_t xs = __builtin_bit_cast(u16x8_t, xv[i]);
+        if constexpr (NORM) {
+          const u16x8_t nw8 = __builtin_bit_cast(u16x8_t, nv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) xs[e] = f32_to_bf16(bf16_to_f32(xs[e]) * inv[i] * bf16_to_f32(nw8[e]));
+        }
+        *(u16x8_t*)(sX + (RPI * i + lr) * LROW + lc) = xs;
+      }
+    };
+    // straight-line body (no mid-loop exit): every path into the loop head has exactly one
+    // slice's loads (set 1) outstanding, so the compiler's vmcnt waits stay per-set
+    const int S = (k1 - k0) / LBK;
+    gl(w2[0], x2[0], n2[0], k0);
+    gl(w2[1], x2[1], n2[1], k0 + LBK);
+    ls(w2[0], x2[0], n2[0]);
     __syncthreads();
-    if (more) {
-      lstore();
+    int it = 0;
+    for (; it + 2 < S; it += 2) {                 // LDS: slice it; set 1: slice it + 1
+      gl(w2[0], x2[0], n2[0], k0 + (it + 2) * LBK);
+      mma();
       __syncthreads();
+      ls(w2[1], x2[1], n2[1]);
+      __syncthreads();
+      gl(w2[1], x2[1], n2[1], k0 + (it + 3) * LBK);
+      mma();
+      __syncthreads();
+      ls(w2[0], x2[0], n2[0]);
+      __syncthreads();
+    }
+    mma();                                        // slice it (S - 2 or S - 1)
+    if (it + 1 < S) {
+      __syncthreads();
+      ls(w2[1], x2[1], n2[1]);
+      __syncthreads();
+      mma();
+    }
+    __syncthreads();
+  } else {
+    gload(k0);
+    lstore();
+    __syncthreads();
+    for (int kk = k0; kk < k1; kk += LBK) {
+      const bool more = kk + LBK < k1;
+      if (more) gload(kk + LBK);
+      mma();
+      __syncthreads();
+      if (more) {
+        lstore();
+        __syncthreads();
+      }
     }
   }
 
@@ -438,6 +512,15 @@ static int g_variant = 0;    // 0 = auto (LDS-staged when K % 256 == 0), 1 = reg
 static bool use_lds(int K) { return g_variant == 2 || (g_variant == 0 && K % LBK == 0); }
 
 static int g_lds_waves = 0;  // 0 = default (4); 2 / 4 forced
+static int g_pf = 1;         // k-slices in flight per 4-wave LDS workgroup (1 or 2)
+
+GS_KERNEL_API int gs_skinny_set_prefetch(int pf) {
+  if (pf != 1 && pf != 2) return GS_EINVAL;
+  g_pf = pf;
+  return GS_OK;
+}
+
+GS_KERNEL_API int gs_skinny_get_prefetch() { return g_pf; }
 
 // 2-wave workgroups were measured slower on every decode shape (each workgroup re-stages X, and
 // the gate/up went 39 -> 46 us at batch 32: profiles/decode/micro_lds_waves.jsonl), so 4 it is.
@@ -546,19 +629,19 @@ static int skinny_launch(const void* X, int ldx, const void* W, int ldw, void* Y
     if (g_norm_in.ssq) {
       if (waves != 4) return GS_EINVAL;
       switch (mt) {
-        case 1: go(skinny_lds<1, 4, false, true>); break;
-        case 2: go(skinny_lds<2, 4, false, true>); break;
-        case 3: go(skinny_lds<3, 4, false, true>); break;
-        default: go(skinny_lds<4, 4, false, true>); break;
+        case 1: (g_pf == 2 ? go(skinny_lds<1, 4, false, true, 2>) : go(skinny_lds<1, 4, false, true>)); break;
+        case 2: (g_pf == 2 ? go(skinny_lds<2, 4, false, true, 2>) : go(skinny_lds<2, 4, false, true>)); break;
+        case 3: (g_pf == 2 ? go(skinny_lds<3, 4, false, true, 2>) : go(skinny_lds<3, 4, false, true>)); break;
+        default: (g_pf == 2 ? go(skinny_lds<4, 4, false, true, 2>) : go(skinny_lds<4, 4, false, true>)); break;
       }
       finish(pp, nsplit, Y, R, ldy, M, N, nw, xn, ldxn, eps, stream);
       return gs_launch_status();
     }
     switch (mt) {
-      case 1: waves == 2 ? go(skinny_lds<1, 2>) : go(skinny_lds<1, 4>); break;
-      case 2: waves == 2 ? go(skinny_lds<2, 2>) : go(skinny_lds<2, 4>); break;
-      case 3: waves == 2 ? go(skinny_lds<3, 2>) : go(skinny_lds<3, 4>); break;
-      default: waves == 2 ? go(skinny_lds<4, 2>) : go(skinny_lds<4, 4>); break;
+      case 1: waves == 2 ? go(skinny_lds<1, 2>) : (g_pf == 2 ? go(skinny_lds<1, 4, false, false, 2>) : go(skinny_lds<1, 4>)); break;
+      case 2: waves == 2 ? go(skinny_lds<2, 2>) : (g_pf == 2 ? go(skinny_lds<2, 4, false, false, 2>) : go(skinny_lds<2, 4>)); break;
+      case 3: waves == 2 ? go(skinny_lds<3, 2>) : (g_pf == 2 ? go(skinny_lds<3, 4, false, false, 2>) : go(skinny_lds<3, 4>)); break;
+      default: waves == 2 ? go(skinny_lds<4, 2>) : (g_pf == 2 ? go(skinny_lds<4, 4, false, false, 2>) : go(skinny_lds<4, 4>)); break;
     }
     finish(pp, nsplit, Y, R, ldy, M, N, nw, xn, ldxn, eps, stream);
     return gs_launch_status();
@@ -628,17 +711,17 @@ GS_KERNEL_API int gs_skinny_swiglu_bf16(const void* X, int ldx, const void* W, i
   };
   if (g_norm_in.ssq) {
     switch ((M + 15) / 16) {
-      case 1: go(skinny_lds<1, 4, true, true>); break;
-      case 2: go(skinny_lds<2, 4, true, true>); break;
-      case 3: go(skinny_lds<3, 4, true, true>); break;
-      default: go(skinny_lds<4, 4, true, true>); break;
+      case 1: (g_pf == 2 ? go(skinny_lds<1, 4, true, true, 2>) : go(skinny_lds<1, 4, true, true>)); break;
+      case 2: (g_pf == 2 ? go(skinny_lds<2, 4, true, true, 2>) : go(skinny_lds<2, 4, true, true>)); break;
+      case 3: (g_pf == 2 ? go(skinny_lds<3, 4, true, true, 2>) : go(skinny_lds<3, 4, true, true>)); break;
+      default: (g_pf == 2 ? go(skinny_lds<4, 4, true, true, 2>) : go(skinny_lds<4, 4, true, true>)); break;
     }
   } else {
     switch ((M + 15) / 16) {
-      case 1: go(skinny_lds<1, 4, true>); break;
-      case 2: go(skinny_lds<2, 4, true>); break;
-      case 3: go(skinny_lds<3, 4, true>); break;
-      default: go(skinny_lds<4, 4, true>); break;
+      case 1: (g_pf == 2 ? go(skinny_lds<1, 4, true, false, 2>) : go(skinny_lds<1, 4, true>)); break;
+      case 2: (g_pf == 2 ? go(skinny_lds<2, 4, true, false, 2>) : go(skinny_lds<2, 4, true>)); break;
+      case 3: (g_pf == 2 ? go(skinny_lds<3, 4, true, false, 2>) : go(skinny_lds<3, 4, true>)); break;
+      default: (g_pf == 2 ? go(skinny_lds<4, 4, true, false, 2>) : go(skinny_lds<4, 4, true>)); break;
     }
   }
   return gs_launch_status();

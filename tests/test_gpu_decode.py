@@ -247,6 +247,69 @@ def test_decode_step_with_folded_rmsnorm_matches_unfolded():
 
 
 
+@pytest.fixture
+def skinny_prefetch():
+    """Set the 4-wave LDS kernel's k-slices in flight (1 or 2) for one test; restore the default."""
+    from aliyun_gpushare_device_plugin_amd.ops import _lib
+
+    lib = _lib.lib()
+    before = lib.gs_skinny_get_prefetch()
+    yield lambda pf: _lib.check(lib.gs_skinny_set_prefetch(pf), "gs_skinny_set_prefetch")
+    lib.gs_skinny_set_prefetch(before)
+
+
+@pytest.mark.parametrize("M,N,K", [(32, 4096, 4096), (33, 6144, 4096), (64, 256, 14336), (7, 512, 4096),
+                                   (32, 16384, 1024), (1, 4096, 14336)])
+def test_skinny_prefetch_depths_agree_bitwise(M, N, K, skinny_prefetch):
+    """Two k-slices in flight (register ring, zero-size descriptors past the K range) change only
+    when bytes arrive, not the arithmetic: outputs equal the one-slice kernel bit for bit, and both
+    match fp32."""
+    torch.manual_seed(M + N + K)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.05
+    r = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    outs = []
+    for pf in (1, 2):
+        skinny_prefetch(pf)
+        outs.append((ops.skinny_linear(x, w), ops.skinny_linear(x, w, residual=r.clone())))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    ref = x.float() @ w.float().t()
+    assert (outs[1][0].float() - ref).abs().max().item() < 2e-2 * ref.abs().max().item() + 1e-2
+
+
+@pytest.mark.parametrize("M", [1, 32, 64])
+def test_skinny_swiglu_prefetch_depths_agree_bitwise(M, skinny_prefetch):
+    from aliyun_gpushare_device_plugin_amd.ops.gemm import interleave_gate_up
+    torch.manual_seed(100 + M)
+    F, K = 8192, 2048
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = interleave_gate_up(torch.randn(2 * F, K, device="cuda", dtype=torch.bfloat16) * 0.05)
+    ys = []
+    for pf in (1, 2):
+        skinny_prefetch(pf)
+        ys.append(ops.skinny_swiglu(x, w))
+    assert ys[0] is not None and torch.equal(ys[0], ys[1])
+
+
+def test_decode_step_prefetch_depths_agree_bitwise(skinny_prefetch):
+    """Folded RMSNorm staging (norm weight through its own descriptor), the RoPE/KV-append
+    reduction and the residual projections, one decode step per depth: identical logits."""
+    from aliyun_gpushare_device_plugin_amd.models.llama import LlamaConfig, LlamaModel
+    from aliyun_gpushare_device_plugin_amd.models.llama_serve import LlamaServer
+
+    cfg = LlamaConfig.tiny(d_model=1024, n_heads=8, n_kv_heads=2, head_dim=128, d_ff=2048, vocab=2048)
+    model = LlamaModel(cfg, "cuda", seed=5)
+    prompt = torch.randint(0, cfg.vocab, (8, 40), device="cuda")
+    logits = []
+    for pf in (1, 2):
+        skinny_prefetch(pf)
+        s = LlamaServer(model, 8, 128, gemm="skinny")
+        assert s.fold_norm and s.fuse_rope
+        s.prefill(prompt)
+        logits.append(s.step(use_graph=False))
+    assert torch.equal(logits[0], logits[1])
+
+
 def test_refused_skinny_options_leave_no_armed_state():
     """ADVICE (round 2): when the native side refuses a call's options after RoPE was armed, the
     wrapper must clear them, or the next unrelated skinny_linear on this thread would rotate its

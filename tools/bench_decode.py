@@ -93,6 +93,22 @@ def gemm_micro(M, N, K):
         _lib.lib().gs_skinny_set_lds_waves(nw)
         res[f"lds_nw{nw}_us"] = round(timed(lambda: ops.skinny_linear(x, w, out=out), 50) * 1e6, 1)
     _lib.lib().gs_skinny_set_lds_waves(0)
+    pf0 = _lib.lib().gs_skinny_get_prefetch()
+    for rnd in range(2):                   # k-slices in flight, order rotated per round
+        for pf in ((1, 2) if rnd == 0 else (2, 1)):
+            _lib.lib().gs_skinny_set_prefetch(pf)
+            t = timed(lambda: ops.skinny_linear(x, w, out=out), 50) * 1e6
+            res[f"lds_pf{pf}_us"] = round(min(t, res.get(f"lds_pf{pf}_us", t)), 1)
+    _lib.lib().gs_skinny_set_prefetch(pf0)
+    if N % 64 == 0 and (N // 2) % 32 == 0 and N // 64 >= 256:    # fused SwiGLU (gate/up shape)
+        from aliyun_gpushare_device_plugin_amd.ops.gemm import interleave_gate_up
+        wil = interleave_gate_up(w)
+        for rnd in range(2):
+            for pf in ((1, 2) if rnd == 0 else (2, 1)):
+                _lib.lib().gs_skinny_set_prefetch(pf)
+                t = timed(lambda: ops.skinny_swiglu(x, wil), 50) * 1e6
+                res[f"swiglu_pf{pf}_us"] = round(min(t, res.get(f"swiglu_pf{pf}_us", t)), 1)
+        _lib.lib().gs_skinny_set_prefetch(pf0)
     set_skinny_variant(SKINNY_AUTO)
     res["ntauto_us"] = round(timed(lambda: ops.skinny_linear(x, w, out=out), 50) * 1e6, 1)
     t_ours = res["ntauto_us"] * 1e-6
@@ -112,14 +128,21 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--micro-only", action="store_true")
     ap.add_argument("--no-gemm-micro", action="store_true")
+    ap.add_argument("--no-attn-micro", action="store_true")
+    ap.add_argument("--prefetch", type=int, default=0, help="skinny k-slices in flight (0 = library default)")
+    ap.add_argument("--gemms", default="hipblaslt,skinny,skinny_rope",
+                    help="decode-step configurations to time")
     a = ap.parse_args()
+    if a.prefetch:
+        from aliyun_gpushare_device_plugin_amd.ops import _lib
+        _lib.check(_lib.lib().gs_skinny_set_prefetch(a.prefetch), "gs_skinny_set_prefetch")
     lines = []
 
     def emit(d):
         print(json.dumps(d), flush=True)
         lines.append(d)
 
-    for B, ctx in ((32, 1024), (32, 4096), (8, 8192), (64, 2048)):
+    for B, ctx in (((32, 1024), (32, 4096), (8, 8192), (64, 2048)) if not a.no_attn_micro else ()):
         emit(attn_micro(B, ctx))
     for M in ((8, 32, 64) if not a.no_gemm_micro else ()):
         for N, K in ((6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336), (128256, 4096)):
@@ -132,7 +155,9 @@ def main():
         return
     model = LlamaModel(LlamaConfig.llama3_8b(n_layers=a.layers), "cuda", seed=1)
     prompt = torch.randint(0, model.cfg.vocab, (a.batch, a.prompt), device="cuda")
-    for gemm, fold, rope in [("hipblaslt", False, False), ("skinny", True, False), ("skinny", True, True)]:
+    cfgs = {"hipblaslt": ("hipblaslt", False, False), "skinny": ("skinny", True, False),
+            "skinny_rope": ("skinny", True, True)}
+    for gemm, fold, rope in [cfgs[k] for k in a.gemms.split(",") if k]:
         srv = LlamaServer(model, a.batch, a.max_ctx, gemm=gemm)
         srv.fold_norm = srv.fold_norm and fold
         srv.fuse_rope = srv.fuse_rope and rope
@@ -141,7 +166,7 @@ def main():
         srv.prefill(prompt)
         torch.cuda.synchronize()
         t_prefill = time.perf_counter() - t
-        res = {"bench": "llama3_8b_decode", "gemm": gemm, "fold_norm": srv.fold_norm, "fuse_rope": srv.fuse_rope,
+        res = {"bench": "llama3_8b_decode", "gemm": gemm, "prefetch": a.prefetch or None, "fold_norm": srv.fold_norm, "fuse_rope": srv.fuse_rope,
                "batch": a.batch, "prompt": a.prompt, "layers": a.layers,
                "kv_cache_gib": round(srv.kv_bytes() / 2**30, 2),
                "weights_gib": round(model.weight_bytes() / 2**30, 2), "prefill_s": round(t_prefill, 3)}
