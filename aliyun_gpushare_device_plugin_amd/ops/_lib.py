@@ -47,6 +47,7 @@ SIGNATURES = {
     "gs_skinny_set_lds_waves": [_I],
     "gs_skinny_set_prefetch": [_I],
     "gs_skinny_get_prefetch": [],
+    "gs_decode_attn_set_nt": [_I],
 }
 
 ERRORS = {1: "invalid arguments", 2: "kernel launch failed"}

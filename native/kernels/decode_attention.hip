@@ -34,7 +34,8 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
-template <int G>
+// NTL: K and V rows are loaded non-temporal (the cache is streamed once per step).
+template <int G, bool NTL = false>
 __global__ __launch_bounds__(NT) void decode_split(const unsigned short* __restrict__ q, int q_bstride,
                                                    const unsigned short* __restrict__ kc,
                                                    const unsigned short* __restrict__ vc,
@@ -78,7 +79,14 @@ __global__ __launch_bounds__(NT) void decode_split(const unsigned short* __restr
     for (int g = 0; g < G; ++g) s[g] = 0.f;
     if (p < n) {
       const unsigned short* kr = kp + (size_t)p * D + part * 16;
-      const u16x8_t k0 = *(const u16x8_t*)kr, k1 = *(const u16x8_t*)(kr + 8);
+      u16x8_t k0, k1;
+      if constexpr (NTL) {
+        k0 = __builtin_nontemporal_load((const u16x8_t*)kr);
+        k1 = __builtin_nontemporal_load((const u16x8_t*)(kr + 8));
+      } else {
+        k0 = *(const u16x8_t*)kr;
+        k1 = *(const u16x8_t*)(kr + 8);
+      }
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const float a = bf16_to_f32(k0[i]), c = bf16_to_f32(k1[i]);
@@ -129,7 +137,12 @@ __global__ __launch_bounds__(NT) void decode_split(const unsigned short* __restr
     for (int i = 0; i < 8; ++i) acc[gg][i] = 0.f;
 #pragma unroll 8
   for (int p = wave * 4 + rsub; p < n; p += 16) {
-    const u16x8_t v8 = *(const u16x8_t*)(vp + (size_t)p * D + d0);
+    const u16x8_t* vsrc = (const u16x8_t*)(vp + (size_t)p * D + d0);
+    u16x8_t v8;
+    if constexpr (NTL)
+      v8 = __builtin_nontemporal_load(vsrc);
+    else
+      v8 = *vsrc;
     float vf[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) vf[i] = bf16_to_f32(v8[i]);
@@ -265,6 +278,15 @@ GS_KERNEL_API int gs_rope_kv_append_bf16(void* qkv, int bstride, const float* co
   return gs_launch_status();
 }
 
+// K/V load policy of the split kernel (0 plain, 1 non-temporal); A/B switch for measurement.
+static int g_dec_nt = 0;
+
+GS_KERNEL_API int gs_decode_attn_set_nt(int on) {
+  if (on != 0 && on != 1) return GS_EINVAL;
+  g_dec_nt = on;
+  return GS_OK;
+}
+
 // q: [B, Hq, D] rows at q_bstride elements per sequence (heads contiguous); caches [B, Hkv, Smax, D];
 // lens[B] (device); workspace: o_part [B, Hq, nsplit, D] f32 + ml_part [B, Hq, nsplit, 2] f32 with
 // nsplit = ceil(Smax / 256); out [B, Hq, D] bf16.
@@ -281,11 +303,15 @@ GS_KERNEL_API int gs_decode_attn_bf16(const void* q, int q_bstride, const void* 
                        (const unsigned short*)k_cache, (const unsigned short*)v_cache, lens, (float*)o_part,
                        (float*)ml_part, Hkv, Smax, nsplit, qs);
   };
-  switch (G) {
-    case 1: args(decode_split<1>); break;
-    case 2: args(decode_split<2>); break;
-    case 4: args(decode_split<4>); break;
-    case 8: args(decode_split<8>); break;
+  switch (G * 2 + (g_dec_nt ? 1 : 0)) {
+    case 2: args(decode_split<1>); break;
+    case 3: args(decode_split<1, true>); break;
+    case 4: args(decode_split<2>); break;
+    case 5: args(decode_split<2, true>); break;
+    case 8: args(decode_split<4>); break;
+    case 9: args(decode_split<4, true>); break;
+    case 16: args(decode_split<8>); break;
+    case 17: args(decode_split<8, true>); break;
     default: return GS_EINVAL;
   }
   hipLaunchKernelGGL(decode_merge, dim3(Hq, B), dim3(D), 0, stream, (const float*)o_part, (const float*)ml_part, lens,

@@ -150,6 +150,11 @@ struct NormIn {
 // (buffer loads; a slice past the workgroup's K range goes through a zero-size descriptor, so it
 // costs no memory traffic and the load stream stays branch-free for the compiler's vmcnt
 // accounting) — the next-but-one slice is requested before the current one is multiplied.
+// PF = 3 (wave-level K split): every wave multiplies all 16 NW rows of the slice over its own
+// quarter of the slice's K (LBK / NW) instead of its 16 rows over the whole slice, so each X
+// fragment is read from LDS by one wave instead of all of them (per slice at M = 32: 48 instead
+// of 96 KiB of fragment reads; M = 64: 64 instead of 160), and the NW partial tiles are summed
+// through LDS once at the end; the epilogue then sees the usual tile-per-wave layout.
 template <int MT, int NW, bool SWIGLU = false, bool NORM = false, int PF = 1>
 __global__ __launch_bounds__(NW * 64) void skinny_lds(const unsigned short* __restrict__ X, int ldx,
                                                   const unsigned short* __restrict__ W, int ldw,
@@ -157,8 +162,11 @@ __global__ __launch_bounds__(NW * 64) void skinny_lds(const unsigned short* __re
                                                   const unsigned short* __restrict__ R, int ldy, int M, int N, int K,
                                                   int kchunk, NormIn nrm = NormIn{}) {
   constexpr int RPI = 2 * NW;                             // rows per global load instruction
-  __shared__ __attribute__((aligned(16))) unsigned short sW[16 * NW * LROW];
-  __shared__ __attribute__((aligned(16))) unsigned short sX[MT * 16 * LROW];
+  // one LDS object (W image, then X image; reused for the wave-split reduction and the epilogue)
+  __shared__ __attribute__((aligned(16))) unsigned short smem[(16 * NW + MT * 16) * LROW];
+  unsigned short* const sW = smem;
+  unsigned short* const sX = smem + 16 * NW * LROW;
+  static_assert(PF != 3 || NW * NW * MT * 64 * 4 * 4 <= (16 * NW + MT * 16) * LROW * 2, "reduction fits LDS");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n0 = blockIdx.x * 16 * NW, split = blockIdx.y;
   const int k0 = split * kchunk, k1 = min(K, k0 + kchunk);
@@ -179,7 +187,13 @@ __global__ __launch_bounds__(NW * 64) void skinny_lds(const unsigned short* __re
   }
   auto gload = [&](int kk) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) wr[i] = *(const u16x8_t*)(W + (size_t)(n0 + RPI * i + lr) * ldw + kk + lc);
+    for (int i = 0; i < 8; ++i) {
+      const u16x8_t* src = (const u16x8_t*)(W + (size_t)(n0 + RPI * i + lr) * ldw + kk + lc);
+      if constexpr (PF == 4)
+        wr[i] = __builtin_nontemporal_load(src);     // streamed W: keep X resident in L2
+      else
+        wr[i] = *src;
+    }
 #pragma unroll
     for (int i = 0; i < XI; ++i) {
       const int m = RPI * i + lr;
@@ -206,7 +220,32 @@ __global__ __launch_bounds__(NW * 64) void skinny_lds(const unsigned short* __re
   const int r16 = lane & 15, kof = (lane >> 4) * 8;
   const unsigned short* wl = sW + (16 * wave + r16) * LROW + kof;
 
+  constexpr int KW = LBK / NW;                           // PF 3: k per wave per slice
+  f32x4_t accw[PF == 3 ? NW : 1][MT];
+  if constexpr (PF == 3) {
+#pragma unroll
+    for (int tt = 0; tt < NW; ++tt)
+#pragma unroll
+      for (int t = 0; t < MT; ++t) accw[tt][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  }
   auto mma = [&]() {
+    if constexpr (PF == 3) {
+#pragma unroll
+      for (int ks = 0; ks < KW / 32; ++ks) {
+        const int kc = wave * KW + ks * 32 + kof;
+        bf16x8_t xf[MT];
+#pragma unroll
+        for (int t = 0; t < MT; ++t) xf[t] = *(const bf16x8_t*)(sX + (16 * t + r16) * LROW + kc);
+#pragma unroll
+        for (int tt = 0; tt < NW; ++tt) {
+          const bf16x8_t wf = *(const bf16x8_t*)(sW + (16 * tt + r16) * LROW + kc);
+#pragma unroll
+          for (int t = 0; t < MT; ++t)
+            accw[tt][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, xf[t], accw[tt][t], 0, 0, 0);
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int ks = 0; ks < LBK / 32; ++ks) {
       const bf16x8_t wf = *(const bf16x8_t*)(wl + ks * 32);
@@ -282,7 +321,7 @@ __global__ __launch_bounds__(NW * 64) void skinny_lds(const unsigned short* __re
       mma();
     }
     __syncthreads();
-  } else {
+  } else {                                       // PF 1 (and 4: the same with streamed W loads)
     gload(k0);
     lstore();
     __syncthreads();
@@ -298,6 +337,23 @@ __global__ __launch_bounds__(NW * 64) void skinny_lds(const unsigned short* __re
     }
   }
 
+  if constexpr (PF == 3) {
+    // the last slice's barrier has passed: sum the NW waves' partial tiles, wave w gets tile w
+    float* red = (float*)smem;                               // [wave][tile][MT][64 lanes] f32x4
+#pragma unroll
+    for (int tt = 0; tt < NW; ++tt)
+#pragma unroll
+      for (int t = 0; t < MT; ++t) *(f32x4_t*)(red + (((wave * NW + tt) * MT + t) * 64 + lane) * 4) = accw[tt][t];
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      f32x4_t a = *(const f32x4_t*)(red + ((wave * MT + t) * 64 + lane) * 4);   // wave 0's tile `wave`
+#pragma unroll
+      for (int v = 1; v < NW; ++v) a += *(const f32x4_t*)(red + (((v * NW + wave) * MT + t) * 64 + lane) * 4);
+      acc[t] = a;
+    }
+    __syncthreads();                                         // smem is the epilogue's again
+  }
   const int nb = n0 + 16 * wave + (lane >> 4) * 4;
   if constexpr (SWIGLU) {
     // the last k-slice's barrier has passed: sW is free. Even waves park their gate tile there.
@@ -512,15 +568,31 @@ static int g_variant = 0;    // 0 = auto (LDS-staged when K % 256 == 0), 1 = reg
 static bool use_lds(int K) { return g_variant == 2 || (g_variant == 0 && K % LBK == 0); }
 
 static int g_lds_waves = 0;  // 0 = default (4); 2 / 4 forced
-static int g_pf = 1;         // k-slices in flight per 4-wave LDS workgroup (1 or 2)
+// 4-wave LDS schedule: 0 = auto, 1 = one k-slice in flight, 2 = two, 3 = wave-level K split,
+// 4 = one slice with W loaded non-temporal. Auto streams W non-temporal when it is >= 64 MiB and
+// loads it plainly otherwise. Measured with weights streamed from HBM, as in a decode step
+// (profiles/decode/skinny_nt_r3_micro.jsonl): nt keeps the W stream from evicting X in L2 and runs
+// the gate/up, down and LM-head projections 4-9 % faster; the 34-50 MB qkv / o weights lose 0-8 %.
+static int g_pf = 0;
 
 GS_KERNEL_API int gs_skinny_set_prefetch(int pf) {
-  if (pf != 1 && pf != 2) return GS_EINVAL;
+  if (pf < 0 || pf > 4) return GS_EINVAL;
   g_pf = pf;
   return GS_OK;
 }
 
 GS_KERNEL_API int gs_skinny_get_prefetch() { return g_pf; }
+
+// Launch the 4-wave LDS kernel <MT, SWIGLU, NORM> with the schedule g_pf selects.
+template <int MT, bool SWIGLU, bool NORM, typename Go>
+static void go_lds4(Go&& go, size_t wbytes) {
+  switch (g_pf ? g_pf : wbytes >= (64u << 20) ? 4 : 1) {
+    case 2: go(skinny_lds<MT, 4, SWIGLU, NORM, 2>); break;
+    case 3: go(skinny_lds<MT, 4, SWIGLU, NORM, 3>); break;
+    case 4: go(skinny_lds<MT, 4, SWIGLU, NORM, 4>); break;
+    default: go(skinny_lds<MT, 4, SWIGLU, NORM, 1>); break;
+  }
+}
 
 // 2-wave workgroups were measured slower on every decode shape (each workgroup re-stages X, and
 // the gate/up went 39 -> 46 us at batch 32: profiles/decode/micro_lds_waves.jsonl), so 4 it is.
@@ -629,19 +701,19 @@ static int skinny_launch(const void* X, int ldx, const void* W, int ldw, void* Y
     if (g_norm_in.ssq) {
       if (waves != 4) return GS_EINVAL;
       switch (mt) {
-        case 1: (g_pf == 2 ? go(skinny_lds<1, 4, false, true, 2>) : go(skinny_lds<1, 4, false, true>)); break;
-        case 2: (g_pf == 2 ? go(skinny_lds<2, 4, false, true, 2>) : go(skinny_lds<2, 4, false, true>)); break;
-        case 3: (g_pf == 2 ? go(skinny_lds<3, 4, false, true, 2>) : go(skinny_lds<3, 4, false, true>)); break;
-        default: (g_pf == 2 ? go(skinny_lds<4, 4, false, true, 2>) : go(skinny_lds<4, 4, false, true>)); break;
+        case 1: go_lds4<1, false, true>(go, (size_t)N * K * 2); break;
+        case 2: go_lds4<2, false, true>(go, (size_t)N * K * 2); break;
+        case 3: go_lds4<3, false, true>(go, (size_t)N * K * 2); break;
+        default: go_lds4<4, false, true>(go, (size_t)N * K * 2); break;
       }
       finish(pp, nsplit, Y, R, ldy, M, N, nw, xn, ldxn, eps, stream);
       return gs_launch_status();
     }
     switch (mt) {
-      case 1: waves == 2 ? go(skinny_lds<1, 2>) : (g_pf == 2 ? go(skinny_lds<1, 4, false, false, 2>) : go(skinny_lds<1, 4>)); break;
-      case 2: waves == 2 ? go(skinny_lds<2, 2>) : (g_pf == 2 ? go(skinny_lds<2, 4, false, false, 2>) : go(skinny_lds<2, 4>)); break;
-      case 3: waves == 2 ? go(skinny_lds<3, 2>) : (g_pf == 2 ? go(skinny_lds<3, 4, false, false, 2>) : go(skinny_lds<3, 4>)); break;
-      default: waves == 2 ? go(skinny_lds<4, 2>) : (g_pf == 2 ? go(skinny_lds<4, 4, false, false, 2>) : go(skinny_lds<4, 4>)); break;
+      case 1: waves == 2 ? go(skinny_lds<1, 2>) : go_lds4<1, false, false>(go, (size_t)N * K * 2); break;
+      case 2: waves == 2 ? go(skinny_lds<2, 2>) : go_lds4<2, false, false>(go, (size_t)N * K * 2); break;
+      case 3: waves == 2 ? go(skinny_lds<3, 2>) : go_lds4<3, false, false>(go, (size_t)N * K * 2); break;
+      default: waves == 2 ? go(skinny_lds<4, 2>) : go_lds4<4, false, false>(go, (size_t)N * K * 2); break;
     }
     finish(pp, nsplit, Y, R, ldy, M, N, nw, xn, ldxn, eps, stream);
     return gs_launch_status();
@@ -711,17 +783,17 @@ GS_KERNEL_API int gs_skinny_swiglu_bf16(const void* X, int ldx, const void* W, i
   };
   if (g_norm_in.ssq) {
     switch ((M + 15) / 16) {
-      case 1: (g_pf == 2 ? go(skinny_lds<1, 4, true, true, 2>) : go(skinny_lds<1, 4, true, true>)); break;
-      case 2: (g_pf == 2 ? go(skinny_lds<2, 4, true, true, 2>) : go(skinny_lds<2, 4, true, true>)); break;
-      case 3: (g_pf == 2 ? go(skinny_lds<3, 4, true, true, 2>) : go(skinny_lds<3, 4, true, true>)); break;
-      default: (g_pf == 2 ? go(skinny_lds<4, 4, true, true, 2>) : go(skinny_lds<4, 4, true, true>)); break;
+      case 1: go_lds4<1, true, true>(go, (size_t)N * K * 2); break;
+      case 2: go_lds4<2, true, true>(go, (size_t)N * K * 2); break;
+      case 3: go_lds4<3, true, true>(go, (size_t)N * K * 2); break;
+      default: go_lds4<4, true, true>(go, (size_t)N * K * 2); break;
     }
   } else {
     switch ((M + 15) / 16) {
-      case 1: (g_pf == 2 ? go(skinny_lds<1, 4, true, false, 2>) : go(skinny_lds<1, 4, true>)); break;
-      case 2: (g_pf == 2 ? go(skinny_lds<2, 4, true, false, 2>) : go(skinny_lds<2, 4, true>)); break;
-      case 3: (g_pf == 2 ? go(skinny_lds<3, 4, true, false, 2>) : go(skinny_lds<3, 4, true>)); break;
-      default: (g_pf == 2 ? go(skinny_lds<4, 4, true, false, 2>) : go(skinny_lds<4, 4, true>)); break;
+      case 1: go_lds4<1, true, false>(go, (size_t)N * K * 2); break;
+      case 2: go_lds4<2, true, false>(go, (size_t)N * K * 2); break;
+      case 3: go_lds4<3, true, false>(go, (size_t)N * K * 2); break;
+      default: go_lds4<4, true, false>(go, (size_t)N * K * 2); break;
     }
   }
   return gs_launch_status();

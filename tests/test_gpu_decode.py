@@ -29,6 +29,10 @@ def test_decode_attention_matches_fp32(G):
     ref = reference_decode_attention(q, kc, vc, lens)
     err = (out.float() - ref).abs().max().item()
     assert err < 2e-2, err
+    from aliyun_gpushare_device_plugin_amd.ops import _lib
+    for ntl in (1, 0):                              # K/V load policy: same arithmetic, same bits
+        _lib.check(_lib.lib().gs_decode_attn_set_nt(ntl), "gs_decode_attn_set_nt")
+        assert torch.equal(ops.decode_attention(q, kc, vc, lens), out)
 
 
 def test_kv_append_writes_exactly_the_new_rows():
@@ -249,7 +253,8 @@ def test_decode_step_with_folded_rmsnorm_matches_unfolded():
 
 @pytest.fixture
 def skinny_prefetch():
-    """Set the 4-wave LDS kernel's k-slices in flight (1 or 2) for one test; restore the default."""
+    """Set the 4-wave LDS kernel's schedule (0 auto, 1 / 2 k-slices in flight, 3 wave-level K split,
+    4 non-temporal W) for one test; restore the previous one."""
     from aliyun_gpushare_device_plugin_amd.ops import _lib
 
     lib = _lib.lib()
@@ -269,12 +274,15 @@ def test_skinny_prefetch_depths_agree_bitwise(M, N, K, skinny_prefetch):
     w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.05
     r = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
     outs = []
-    for pf in (1, 2):
+    for pf in (1, 2, 3, 4, 0):
         skinny_prefetch(pf)
         outs.append((ops.skinny_linear(x, w), ops.skinny_linear(x, w, residual=r.clone())))
-    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    for o in (outs[1], outs[3], outs[4]):      # 2 / 4 / auto: same arithmetic, other loads
+        assert torch.equal(outs[0][0], o[0]) and torch.equal(outs[0][1], o[1])
     ref = x.float() @ w.float().t()
-    assert (outs[1][0].float() - ref).abs().max().item() < 2e-2 * ref.abs().max().item() + 1e-2
+    for y, yr in (outs[1], outs[2]):           # 3 = wave-level K split: same sums, another order
+        assert (y.float() - ref).abs().max().item() < 2e-2 * ref.abs().max().item() + 1e-2
+        assert (yr.float() - ref - r.float()).abs().max().item() < 2e-2 * ref.abs().max().item() + 2e-2
 
 
 @pytest.mark.parametrize("M", [1, 32, 64])
@@ -285,10 +293,12 @@ def test_skinny_swiglu_prefetch_depths_agree_bitwise(M, skinny_prefetch):
     x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
     w = interleave_gate_up(torch.randn(2 * F, K, device="cuda", dtype=torch.bfloat16) * 0.05)
     ys = []
-    for pf in (1, 2):
+    for pf in (1, 2, 3, 4, 0):
         skinny_prefetch(pf)
         ys.append(ops.skinny_swiglu(x, w))
-    assert ys[0] is not None and torch.equal(ys[0], ys[1])
+    assert ys[0] is not None and all(torch.equal(ys[0], ys[i]) for i in (1, 3, 4))
+    scale = ys[0].float().abs().max().item()
+    assert (ys[2].float() - ys[0].float()).abs().max().item() < 1e-2 * scale + 1e-3
 
 
 def test_decode_step_prefetch_depths_agree_bitwise(skinny_prefetch):
@@ -301,13 +311,15 @@ def test_decode_step_prefetch_depths_agree_bitwise(skinny_prefetch):
     model = LlamaModel(cfg, "cuda", seed=5)
     prompt = torch.randint(0, cfg.vocab, (8, 40), device="cuda")
     logits = []
-    for pf in (1, 2):
+    for pf in (1, 2, 3, 4, 0):
         skinny_prefetch(pf)
         s = LlamaServer(model, 8, 128, gemm="skinny")
         assert s.fold_norm and s.fuse_rope
         s.prefill(prompt)
         logits.append(s.step(use_graph=False))
-    assert torch.equal(logits[0], logits[1])
+    assert all(torch.equal(logits[0], logits[i]) for i in (1, 3, 4))
+    scale = logits[0].float().abs().max().item()
+    assert (logits[2].float() - logits[0].float()).abs().max().item() < 2e-2 * scale
 
 
 def test_refused_skinny_options_leave_no_armed_state():

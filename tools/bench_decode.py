@@ -6,6 +6,7 @@
 Random-init weights (no checkpoints offline); synthetic prompt. Output: JSON lines (and --out).
 """
 import argparse
+import itertools
 import json
 import os
 import sys
@@ -50,6 +51,14 @@ def attn_micro(B, ctx, Hq=32, Hkv=8, D=128, layers=8):
         return ops.decode_attention(q, kc, vc, lens, ws, out)
 
     t_ours = timed(ours, 8 * layers)
+    from aliyun_gpushare_device_plugin_amd.ops import _lib
+    t_pol = {}
+    for rnd in range(2):                       # K/V load policy A/B (plain / non-temporal), rotated
+        for ntl in ((0, 1) if rnd == 0 else (1, 0)):
+            _lib.lib().gs_decode_attn_set_nt(ntl)
+            t = timed(ours, 8 * layers)
+            t_pol[ntl] = min(t, t_pol.get(ntl, t))
+    _lib.lib().gs_decode_attn_set_nt(0)
     qs = q.view(B, Hq, 1, D)
 
     def sdpa():
@@ -61,24 +70,40 @@ def attn_micro(B, ctx, Hq=32, Hkv=8, D=128, layers=8):
     del caches
     nbytes = 2 * B * Hkv * ctx * D * 2
     return {"bench": "decode_attention", "B": B, "ctx": ctx, "ours_us": round(t_ours * 1e6, 1),
+            "plain_us": round(t_pol[0] * 1e6, 1), "nt_us": round(t_pol[1] * 1e6, 1),
             "ours_GBps": round(nbytes / t_ours / 1e9, 1), "sdpa_us": round(t_sdpa * 1e6, 1),
             "sdpa_GBps": round(nbytes / t_sdpa / 1e9, 1), "speedup": round(t_sdpa / t_ours, 2)}
+
+
+class _Rot:
+    """``copies`` weights of one shape, handed out round-robin: together > 1 GiB, so a timed loop
+    streams W from HBM as a decode step does (one 235 MB weight re-read back to back stays in the
+    256 MB Infinity Cache and flatters every kernel, most of all one that loads W cached)."""
+
+    def __init__(self, N, K):
+        n = -(-(1 << 30) // (N * K * 2)) + 1
+        self.ws = [torch.randn(N, K, device="cuda", dtype=torch.bfloat16) for _ in range(n)]
+        self.i = 0
+
+    def next(self):
+        self.i += 1
+        return self.ws[self.i % len(self.ws)]
 
 
 def gemm_micro(M, N, K):
     from aliyun_gpushare_device_plugin_amd.ops.gemm import set_skinny_nt
 
     x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
-    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16)
+    rot = _Rot(N, K)
     out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
     nbytes = N * K * 2
-    res = {"bench": "skinny_gemm", "M": M, "N": N, "K": K}
+    res = {"bench": "skinny_gemm", "M": M, "N": N, "K": K, "w_copies": len(rot.ws)}
     from aliyun_gpushare_device_plugin_amd.ops.gemm import SKINNY_AUTO, SKINNY_LDS, SKINNY_REG, set_skinny_variant
 
     set_skinny_variant(SKINNY_REG)
     for nt in (1, 2, 4):
         set_skinny_nt(nt)
-        t = timed(lambda: ops.skinny_linear(x, w, out=out), 50)
+        t = timed(lambda: ops.skinny_linear(x, rot.next(), out=out), 50)
         res[f"reg_nt{nt}_us"] = round(t * 1e6, 1)
     set_skinny_nt(0)
     set_skinny_variant(SKINNY_LDS)
@@ -86,33 +111,34 @@ def gemm_micro(M, N, K):
 
     for tgt in (1, 256, 512, 1024, 2048):
         _lib.lib().gs_skinny_set_wg_target(tgt)
-        res[f"lds_wg{tgt}_us"] = round(timed(lambda: ops.skinny_linear(x, w, out=out), 50) * 1e6, 1)
+        res[f"lds_wg{tgt}_us"] = round(timed(lambda: ops.skinny_linear(x, rot.next(), out=out), 50) * 1e6, 1)
     _lib.lib().gs_skinny_set_wg_target(512)
     res["lds_us"] = res["lds_wg512_us"]
     for nw in (4, 2):
         _lib.lib().gs_skinny_set_lds_waves(nw)
-        res[f"lds_nw{nw}_us"] = round(timed(lambda: ops.skinny_linear(x, w, out=out), 50) * 1e6, 1)
+        res[f"lds_nw{nw}_us"] = round(timed(lambda: ops.skinny_linear(x, rot.next(), out=out), 50) * 1e6, 1)
     _lib.lib().gs_skinny_set_lds_waves(0)
     pf0 = _lib.lib().gs_skinny_get_prefetch()
     for rnd in range(2):                   # k-slices in flight, order rotated per round
-        for pf in ((1, 2) if rnd == 0 else (2, 1)):
+        for pf in ((0, 1, 2, 3, 4) if rnd == 0 else (4, 3, 2, 1, 0)):
             _lib.lib().gs_skinny_set_prefetch(pf)
-            t = timed(lambda: ops.skinny_linear(x, w, out=out), 50) * 1e6
+            t = timed(lambda: ops.skinny_linear(x, rot.next(), out=out), 50) * 1e6
             res[f"lds_pf{pf}_us"] = round(min(t, res.get(f"lds_pf{pf}_us", t)), 1)
     _lib.lib().gs_skinny_set_prefetch(pf0)
     if N % 64 == 0 and (N // 2) % 32 == 0 and N // 64 >= 256:    # fused SwiGLU (gate/up shape)
         from aliyun_gpushare_device_plugin_amd.ops.gemm import interleave_gate_up
-        wil = interleave_gate_up(w)
+        wils = [interleave_gate_up(v) for v in rot.ws]
+        wi = itertools.count()
         for rnd in range(2):
-            for pf in ((1, 2) if rnd == 0 else (2, 1)):
+            for pf in ((1, 2, 3, 4) if rnd == 0 else (4, 3, 2, 1)):
                 _lib.lib().gs_skinny_set_prefetch(pf)
-                t = timed(lambda: ops.skinny_swiglu(x, wil), 50) * 1e6
+                t = timed(lambda: ops.skinny_swiglu(x, wils[next(wi) % len(wils)]), 50) * 1e6
                 res[f"swiglu_pf{pf}_us"] = round(min(t, res.get(f"swiglu_pf{pf}_us", t)), 1)
         _lib.lib().gs_skinny_set_prefetch(pf0)
     set_skinny_variant(SKINNY_AUTO)
-    res["ntauto_us"] = round(timed(lambda: ops.skinny_linear(x, w, out=out), 50) * 1e6, 1)
+    res["ntauto_us"] = round(timed(lambda: ops.skinny_linear(x, rot.next(), out=out), 50) * 1e6, 1)
     t_ours = res["ntauto_us"] * 1e-6
-    t_blas = timed(lambda: torch.matmul(x, w.t()), 50)
+    t_blas = timed(lambda: torch.matmul(x, rot.next().t()), 50)
     res.update({"ours_GBps": round(nbytes / t_ours / 1e9, 1), "hipblaslt_us": round(t_blas * 1e6, 1),
                 "hipblaslt_GBps": round(nbytes / t_blas / 1e9, 1), "speedup": round(t_blas / t_ours, 2)})
     return res
@@ -129,10 +155,15 @@ def main():
     ap.add_argument("--micro-only", action="store_true")
     ap.add_argument("--no-gemm-micro", action="store_true")
     ap.add_argument("--no-attn-micro", action="store_true")
-    ap.add_argument("--prefetch", type=int, default=0, help="skinny k-slices in flight (0 = library default)")
+    ap.add_argument("--attn-nt", type=int, default=-1, help="decode attention K/V loads: 0 plain, 1 nt")
+    ap.add_argument("--prefetch", type=int, default=0,
+                    help="skinny schedule: 0 auto, 1 one k-slice in flight, 2 two, 3 wave K split, 4 nt W")
     ap.add_argument("--gemms", default="hipblaslt,skinny,skinny_rope",
                     help="decode-step configurations to time")
     a = ap.parse_args()
+    if a.attn_nt >= 0:
+        from aliyun_gpushare_device_plugin_amd.ops import _lib
+        _lib.check(_lib.lib().gs_decode_attn_set_nt(a.attn_nt), "gs_decode_attn_set_nt")
     if a.prefetch:
         from aliyun_gpushare_device_plugin_amd.ops import _lib
         _lib.check(_lib.lib().gs_skinny_set_prefetch(a.prefetch), "gs_skinny_set_prefetch")
@@ -166,7 +197,8 @@ def main():
         srv.prefill(prompt)
         torch.cuda.synchronize()
         t_prefill = time.perf_counter() - t
-        res = {"bench": "llama3_8b_decode", "gemm": gemm, "prefetch": a.prefetch or None, "fold_norm": srv.fold_norm, "fuse_rope": srv.fuse_rope,
+        res = {"bench": "llama3_8b_decode", "gemm": gemm, "skinny_schedule": a.prefetch or "auto", "attn_nt": a.attn_nt,
+               "fold_norm": srv.fold_norm, "fuse_rope": srv.fuse_rope,
                "batch": a.batch, "prompt": a.prompt, "layers": a.layers,
                "kv_cache_gib": round(srv.kv_bytes() / 2**30, 2),
                "weights_gib": round(model.weight_bytes() / 2**30, 2), "prefill_s": round(t_prefill, 3)}
