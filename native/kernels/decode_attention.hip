@@ -278,8 +278,10 @@ GS_KERNEL_API int gs_rope_kv_append_bf16(void* qkv, int bstride, const float* co
   return gs_launch_status();
 }
 
-// K/V load policy of the split kernel (0 plain, 1 non-temporal); A/B switch for measurement.
-static int g_dec_nt = 0;
+// K/V load policy of the split kernel (0 plain, 1 non-temporal, the default): the cache is read once
+// per step, so it is streamed non-temporal; 1.5-5 % faster with caches streamed from HBM and the
+// batch-32 decode step 0.6 % (profiles/decode/decode_nt_r3_*.jsonl).
+static int g_dec_nt = 1;
 
 GS_KERNEL_API int gs_decode_attn_set_nt(int on) {
   if (on != 0 && on != 1) return GS_EINVAL;

@@ -30,9 +30,12 @@ def test_decode_attention_matches_fp32(G):
     err = (out.float() - ref).abs().max().item()
     assert err < 2e-2, err
     from aliyun_gpushare_device_plugin_amd.ops import _lib
-    for ntl in (1, 0):                              # K/V load policy: same arithmetic, same bits
-        _lib.check(_lib.lib().gs_decode_attn_set_nt(ntl), "gs_decode_attn_set_nt")
-        assert torch.equal(ops.decode_attention(q, kc, vc, lens), out)
+    try:
+        for ntl in (0, 1):                          # K/V load policy: same arithmetic, same bits
+            _lib.check(_lib.lib().gs_decode_attn_set_nt(ntl), "gs_decode_attn_set_nt")
+            assert torch.equal(ops.decode_attention(q, kc, vc, lens), out)
+    finally:
+        _lib.lib().gs_decode_attn_set_nt(1)
 
 
 def test_kv_append_writes_exactly_the_new_rows():

@@ -58,7 +58,7 @@ def attn_micro(B, ctx, Hq=32, Hkv=8, D=128, layers=8):
             _lib.lib().gs_decode_attn_set_nt(ntl)
             t = timed(ours, 8 * layers)
             t_pol[ntl] = min(t, t_pol.get(ntl, t))
-    _lib.lib().gs_decode_attn_set_nt(0)
+    _lib.lib().gs_decode_attn_set_nt(1)
     qs = q.view(B, Hq, 1, D)
 
     def sdpa():
