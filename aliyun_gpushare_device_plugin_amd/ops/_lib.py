@@ -48,6 +48,7 @@ SIGNATURES = {
     "gs_skinny_set_prefetch": [_I],
     "gs_skinny_get_prefetch": [],
     "gs_decode_attn_set_nt": [_I],
+    "gs_skinny_set_reduce_static": [_I],
 }
 
 ERRORS = {1: "invalid arguments", 2: "kernel launch failed"}

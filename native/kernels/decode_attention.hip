@@ -184,17 +184,40 @@ __global__ __launch_bounds__(NT) void decode_split(const unsigned short* __restr
 __global__ __launch_bounds__(D) void decode_merge(const float* __restrict__ o_part, const float* __restrict__ ml_part,
                                                   const int* __restrict__ lens, unsigned short* __restrict__ out,
                                                   int Hq, int Smax, int nsplit) {
+  // a latency kernel: lane s < ns fetches split s's (max, sum) pair, and every thread issues its o
+  // loads 8 at a time before using them; the combine order (split 0, 1, ...) is unchanged
+  __shared__ float2 MLs[D];
   const int hq = blockIdx.x, b = blockIdx.y, d = threadIdx.x;
   const int len = min(lens[b], Smax);
   const int ns = (len + CHUNK - 1) / CHUNK;
   const size_t row0 = ((size_t)b * Hq + hq) * nsplit;
   float m = -INFINITY;
-  for (int s = 0; s < ns; ++s) m = fmaxf(m, ml_part[(row0 + s) * 2]);
+  for (int s0 = 0; s0 < ns; s0 += D) {
+    const int s = s0 + d;
+    const float2 v = s < ns ? *(const float2*)(ml_part + (row0 + s) * 2) : make_float2(-INFINITY, 0.f);
+    if (s0 == 0) MLs[d] = v;
+    m = fmaxf(m, v.x);
+  }
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  __shared__ float wmax[D / 64];
+  if ((d & 63) == 0) wmax[d >> 6] = m;
+  __syncthreads();
+#pragma unroll
+  for (int w = 0; w < D / 64; ++w) m = fmaxf(m, wmax[w]);
   float num = 0.f, den = 0.f;
-  for (int s = 0; s < ns; ++s) {
-    const float w = exp2f(ml_part[(row0 + s) * 2] - m);
-    den = fmaf(w, ml_part[(row0 + s) * 2 + 1], den);
-    num = fmaf(w, o_part[(row0 + s) * D + d], num);
+  for (int s0 = 0; s0 < ns; s0 += 8) {
+    float ov[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ov[j] = s0 + j < ns ? o_part[(row0 + s0 + j) * D + d] : 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int s = s0 + j;
+      if (s >= ns) break;
+      const float2 ml = s < D ? MLs[s] : *(const float2*)(ml_part + (row0 + s) * 2);
+      const float w = exp2f(ml.x - m);
+      den = fmaf(w, ml.y, den);
+      num = fmaf(w, ov[j], num);
+    }
   }
   out[((size_t)b * Hq + hq) * D + d] = f32_to_bf16(den > 0.f ? num / den : 0.f);
 }

@@ -398,9 +398,31 @@ __global__ __launch_bounds__(NW * 64) void skinny_lds(const unsigned short* __re
   }
 }
 
+// Sum of the S split partials of 4 consecutive outputs at element offset i (stride MN between
+// splits), added in split order. SPLITS > 0: a compile-time count, so all S loads are issued before
+// the first add (one memory latency per thread instead of S in a row: the reductions are latency
+// kernels, ~5 us each with the runtime loop); SPLITS = 0: the runtime count, in a loop.
+template <int SPLITS>
+__device__ __forceinline__ f32x4_t sum_splits(const float* __restrict__ part, int splits, size_t MN, size_t i) {
+  if constexpr (SPLITS > 0) {
+    f32x4_t v[SPLITS];
+#pragma unroll
+    for (int p = 0; p < SPLITS; ++p) v[p] = *(const f32x4_t*)(part + (size_t)p * MN + i);
+    f32x4_t a = v[0];
+#pragma unroll
+    for (int p = 1; p < SPLITS; ++p) a += v[p];
+    return a;
+  } else {
+    f32x4_t a = *(const f32x4_t*)(part + i);
+    for (int p = 1; p < splits; ++p) a += *(const f32x4_t*)(part + (size_t)p * MN + i);
+    return a;
+  }
+}
+
 // Y[m, n] = sum_s part[s, m, n] (+ R[m, n]); 4 outputs per thread. With ssq (N % 1024 == 0) each
 // 1024-element workgroup also writes the sum of squares of its stored bf16 outputs to
 // ssq[chunk][m] (chunk = n / 1024): the next projection's RMSNorm, folded into its X staging.
+template <int SPLITS>
 __global__ __launch_bounds__(256) void skinny_reduce(const float* __restrict__ part, int splits,
                                                      unsigned short* __restrict__ Y, const unsigned short* __restrict__ R,
                                                      int ldy, int M, int N, float* __restrict__ ssq) {
@@ -408,8 +430,7 @@ __global__ __launch_bounds__(256) void skinny_reduce(const float* __restrict__ p
   float sq = 0.f;
   if (i < M * N) {
     const int m = i / N, n = i % N;
-    f32x4_t s = *(const f32x4_t*)(part + i);
-    for (int p = 1; p < splits; ++p) s += *(const f32x4_t*)(part + (size_t)p * M * N + i);
+    const f32x4_t s = sum_splits<SPLITS>(part, splits, (size_t)M * N, i);
     u16x4_t o;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -448,6 +469,7 @@ struct RopeIn {
   int hq, hkv, smax;
 };
 
+template <int SPLITS>
 __global__ __launch_bounds__(256) void skinny_reduce_rope(const float* __restrict__ part, int splits,
                                                           unsigned short* __restrict__ Y, int ldy, int M, int N,
                                                           RopeIn rp) {
@@ -458,11 +480,7 @@ __global__ __launch_bounds__(256) void skinny_reduce_rope(const float* __restric
   const int b = i / per, r = i % per;
   const int p = rp.pos[b];
   const bool in_cache = p >= 0 && p < rp.smax;
-  auto sum4 = [&](int n) {
-    f32x4_t a = *(const f32x4_t*)(part + (size_t)b * N + n);
-    for (int q = 1; q < splits; ++q) a += *(const f32x4_t*)(part + ((size_t)q * M + b) * N + n);
-    return a;
-  };
+  auto sum4 = [&](int n) { return sum_splits<SPLITS>(part, splits, (size_t)M * N, (size_t)b * N + n); };
   unsigned short* row = Y + (size_t)b * ldy;
   if (r < (rp.hq + rp.hkv) * NQ) {
     const int h = r / NQ, d = (r % NQ) * 4, n = h * D + d;
@@ -655,6 +673,14 @@ GS_KERNEL_API int gs_skinny_splits(int N, int K) {
 // part: float workspace of splits * M * N (ignored when splits == 1). Requires M in [1, 64],
 // N % 64 == 0, K % 32 == 0, ldx / ldw % 8 == 0, ldy % 4 == 0, 16-B aligned X and W.
 // Post-GEMM step: the plain split reduction, or (nw != null) the reduction fused with RMSNorm.
+static int g_reduce_static = 1;   // split reductions with compile-time split counts (0: runtime loop, A/B)
+
+GS_KERNEL_API int gs_skinny_set_reduce_static(int on) {
+  if (on != 0 && on != 1) return GS_EINVAL;
+  g_reduce_static = on;
+  return GS_OK;
+}
+
 static thread_local float* g_ssq_out = nullptr;   // skinny_reduce writes row sums of squares here
 static thread_local NormIn g_norm_in{};            // skinny_lds stages rmsnorm(X) when g_norm_in.ssq is set
 static thread_local RopeIn g_rope_in{};            // split reduction = skinny_reduce_rope when g_rope_in.pos is set
@@ -663,16 +689,34 @@ static void finish(float* pp, int nsplit, void* Y, const void* R, int ldy, int M
                    int ldxn, float eps, hipStream_t stream) {
   if (g_rope_in.pos) {
     const int n = M * ((g_rope_in.hq + g_rope_in.hkv) * 16 + g_rope_in.hkv * 16);
-    hipLaunchKernelGGL(skinny_reduce_rope, dim3((n + 255) / 256), dim3(256), 0, stream, (const float*)pp, nsplit,
-                       (unsigned short*)Y, ldy, M, N, g_rope_in);
+    auto go = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3((n + 255) / 256), dim3(256), 0, stream, (const float*)pp, nsplit,
+                         (unsigned short*)Y, ldy, M, N, g_rope_in);
+    };
+    switch (g_reduce_static ? nsplit : 0) {
+      case 2: go(skinny_reduce_rope<2>); break;
+      case 4: go(skinny_reduce_rope<4>); break;
+      case 8: go(skinny_reduce_rope<8>); break;
+      case 16: go(skinny_reduce_rope<16>); break;
+      default: go(skinny_reduce_rope<0>); break;
+    }
   } else if (nw) {
     hipLaunchKernelGGL(skinny_reduce_norm, dim3(M), dim3(256), 0, stream, (const float*)pp, nsplit,
                        (unsigned short*)Y, (const unsigned short*)R, ldy, M, N, (const unsigned short*)nw,
                        (unsigned short*)xn, ldxn, eps);
   } else if (pp) {
     const int n4 = M * N / 4;
-    hipLaunchKernelGGL(skinny_reduce, dim3((n4 + 255) / 256), dim3(256), 0, stream, (const float*)pp, nsplit,
-                       (unsigned short*)Y, (const unsigned short*)R, ldy, M, N, g_ssq_out);
+    auto go = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3((n4 + 255) / 256), dim3(256), 0, stream, (const float*)pp, nsplit,
+                         (unsigned short*)Y, (const unsigned short*)R, ldy, M, N, g_ssq_out);
+    };
+    switch (g_reduce_static ? nsplit : 0) {
+      case 2: go(skinny_reduce<2>); break;
+      case 4: go(skinny_reduce<4>); break;
+      case 8: go(skinny_reduce<8>); break;
+      case 16: go(skinny_reduce<16>); break;
+      default: go(skinny_reduce<0>); break;
+    }
   }
 }
 

@@ -325,6 +325,40 @@ def test_decode_step_prefetch_depths_agree_bitwise(skinny_prefetch):
     assert (logits[2].float() - logits[0].float()).abs().max().item() < 2e-2 * scale
 
 
+@pytest.mark.parametrize("K,rope", [(4096, False), (14336, False), (4096, True)])
+def test_static_split_reductions_equal_the_loop(K, rope):
+    """The split reductions with compile-time split counts (all partial loads issued at once) add
+    the splits in the same order as the runtime loop: bit-identical outputs, plain and RoPE/KV."""
+    from aliyun_gpushare_device_plugin_amd.ops import _lib
+
+    torch.manual_seed(K)
+    M, Hq, Hkv = 32, 32, 8
+    N = (Hq + 2 * Hkv) * 128 if rope else 4096
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.03
+    assert _lib.lib().gs_skinny_splits(N, K) > 1
+    r0 = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    cos, sin = torch.randn(512, 64, device="cuda"), torch.randn(512, 64, device="cuda")
+    pos = torch.arange(M, dtype=torch.int32, device="cuda") * 3
+    outs = []
+    try:
+        for st in (0, 1):
+            _lib.check(_lib.lib().gs_skinny_set_reduce_static(st), "gs_skinny_set_reduce_static")
+            if rope:
+                kc, vc = ops.kv_cache(M, Hkv, 256, 128)
+                y = ops.skinny_linear(x, w, rope=(cos, sin, pos, kc, vc, Hq))
+                outs.append((y, kc, vc))
+            else:
+                r = r0.clone()
+                ssq = torch.zeros(N // 1024, M, device="cuda")
+                y = ops.skinny_linear(x, w, residual=r, out=r, ssq_out=ssq)
+                outs.append((y, ssq))
+    finally:
+        _lib.lib().gs_skinny_set_reduce_static(1)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 def test_refused_skinny_options_leave_no_armed_state():
     """ADVICE (round 2): when the native side refuses a call's options after RoPE was armed, the
     wrapper must clear them, or the next unrelated skinny_linear on this thread would rotate its

@@ -156,11 +156,15 @@ def main():
     ap.add_argument("--no-gemm-micro", action="store_true")
     ap.add_argument("--no-attn-micro", action="store_true")
     ap.add_argument("--attn-nt", type=int, default=-1, help="decode attention K/V loads: 0 plain, 1 nt")
+    ap.add_argument("--reduce-static", type=int, default=-1, help="skinny split reductions: 1 static counts, 0 loop")
     ap.add_argument("--prefetch", type=int, default=0,
                     help="skinny schedule: 0 auto, 1 one k-slice in flight, 2 two, 3 wave K split, 4 nt W")
     ap.add_argument("--gemms", default="hipblaslt,skinny,skinny_rope",
                     help="decode-step configurations to time")
     a = ap.parse_args()
+    if a.reduce_static >= 0:
+        from aliyun_gpushare_device_plugin_amd.ops import _lib
+        _lib.check(_lib.lib().gs_skinny_set_reduce_static(a.reduce_static), "gs_skinny_set_reduce_static")
     if a.attn_nt >= 0:
         from aliyun_gpushare_device_plugin_amd.ops import _lib
         _lib.check(_lib.lib().gs_decode_attn_set_nt(a.attn_nt), "gs_decode_attn_set_nt")
@@ -198,6 +202,7 @@ def main():
         torch.cuda.synchronize()
         t_prefill = time.perf_counter() - t
         res = {"bench": "llama3_8b_decode", "gemm": gemm, "skinny_schedule": a.prefetch or "auto", "attn_nt": a.attn_nt,
+               "reduce_static": a.reduce_static,
                "fold_norm": srv.fold_norm, "fuse_rope": srv.fuse_rope,
                "batch": a.batch, "prompt": a.prompt, "layers": a.layers,
                "kv_cache_gib": round(srv.kv_bytes() / 2**30, 2),
