@@ -132,7 +132,7 @@ class LlamaServer:
             nxt = m.layers[i + 1]["attn_norm"] if i + 1 < len(m.layers) else m.final_norm
             h, x = self._mm_norm(act, L["wd"], h, nxt)
         logits = self._mm_in(x, m.lm_head)
-        self.tok.copy_(logits.argmax(-1))
+        ops.argmax_rows(logits, out=self.tok)                          # greedy, one launch
         self.pos.add_(1)
         return logits
 

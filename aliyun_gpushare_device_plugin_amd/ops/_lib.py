@@ -49,6 +49,7 @@ SIGNATURES = {
     "gs_skinny_get_prefetch": [],
     "gs_decode_attn_set_nt": [_I],
     "gs_skinny_set_reduce_static": [_I],
+    "gs_argmax_rows_bf16": [_P, _I, _I, _I, _P, _P],
 }
 
 ERRORS = {1: "invalid arguments", 2: "kernel launch failed"}

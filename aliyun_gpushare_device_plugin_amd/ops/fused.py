@@ -88,3 +88,20 @@ def rope_(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, nheads: int, he
                                  seq_len, _lib.stream_ptr(x.device))
     _lib.check(rc, "gs_rope_bf16")
     return x
+
+
+def argmax_rows(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Greedy sampling: ``torch.argmax(x, -1)`` for bf16 ``x`` ``[B, V]`` (rows may be strided;
+    first index of the maximum, NaN counted as the maximum) into int64 ``out`` ``[B]``, one
+    launch (torch's argmax is a generic reduction plus a copy into the token buffer)."""
+    if x.dtype != torch.bfloat16 or not x.is_cuda or x.dim() != 2 or x.stride(1) != 1:
+        raise ValueError("argmax_rows: expected a bf16 GPU [B, V] tensor with contiguous rows")
+    B, V = x.shape
+    if x.stride(0) % 8 or x.data_ptr() % 16:
+        raise ValueError("argmax_rows: rows must be 16-byte aligned")
+    out = torch.empty(B, dtype=torch.long, device=x.device) if out is None else out
+    if out.dtype != torch.long or out.shape != (B,) or not out.is_contiguous() or out.device != x.device:
+        raise ValueError("argmax_rows: out must be a contiguous int64 [B] tensor on x's device")
+    rc = _lib.lib().gs_argmax_rows_bf16(x.data_ptr(), x.stride(0), B, V, out.data_ptr(), _lib.stream_ptr(x.device))
+    _lib.check(rc, "gs_argmax_rows_bf16")
+    return out

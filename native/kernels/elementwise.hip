@@ -3,6 +3,8 @@
 //  * gs_silu_mul_bf16: y[m, f] = silu(gu[m, f]) * gu[m, F + f]   (gate|up concatenated;
 //                      gs_silu_mul_il_bf16: the interleaved-by-16 layout)
 //  * gs_rope_bf16:     in-place rotate-half RoPE on q/k with host-precomputed cos/sin tables
+//  * gs_argmax_rows_bf16: greedy sampling, out[b] = argmax_v x[b, v] as torch.argmax defines it
+//                      (first index of the maximum; NaN counts as the maximum)
 // Per cdna_hip_programming.md Appendix B: vectorised 16-B loads, f32 math, trig from a
 // table (no on-device sin/cos), one row per 256-thread block for the row reductions.
 #include "common.h"
@@ -121,7 +123,71 @@ inline int grid_for(size_t work, int threads) {
   return (int)(b < 2048 * 8 ? (b ? b : 1) : 2048 * 8);
 }
 
+// Order-preserving 32-bit key of a bf16 value (NaN above +inf); with the index complemented in the
+// low half, the max of (key << 32 | ~idx) is the first index of the maximum.
+__device__ __forceinline__ unsigned long long argmax_key(unsigned short h, int idx) {
+  unsigned u = ((unsigned)h) << 16;
+  const bool nan = (u & 0x7fffffffu) > 0x7f800000u;
+  u = nan ? 0xffffffffu : (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  return ((unsigned long long)u << 32) | (unsigned)~idx;
+}
+
+// One 1024-thread workgroup per row: the decode step's logits row (128256 entries for Llama 3) is
+// read with 16-B loads, 4 in flight per thread, and reduced in registers, then across the waves.
+constexpr int AM_THREADS = 1024;
+__global__ __launch_bounds__(AM_THREADS) void argmax_rows_bf16(const unsigned short* __restrict__ x, int ld, int V,
+                                                               long long* __restrict__ out) {
+  const unsigned short* r = x + (size_t)blockIdx.x * ld;
+  const int tid = threadIdx.x, v8 = V / 8;
+  unsigned long long best = 0;
+  int v = tid;
+  for (; v + 3 * AM_THREADS < v8; v += 4 * AM_THREADS) {
+    u16x8_t q[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) q[j] = *(const u16x8_t*)(r + (size_t)(v + j * AM_THREADS) * 8);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const unsigned long long k = argmax_key(q[j][e], (v + j * AM_THREADS) * 8 + e);
+        best = k > best ? k : best;
+      }
+  }
+  for (; v < v8; v += AM_THREADS) {
+    const u16x8_t q = *(const u16x8_t*)(r + (size_t)v * 8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const unsigned long long k = argmax_key(q[e], v * 8 + e);
+      best = k > best ? k : best;
+    }
+  }
+  for (int t = v8 * 8 + tid; t < V; t += AM_THREADS) {
+    const unsigned long long k = argmax_key(r[t], t);
+    best = k > best ? k : best;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long k = __shfl_xor(best, o, 64);
+    best = k > best ? k : best;
+  }
+  __shared__ unsigned long long red[AM_THREADS / 64];
+  if ((tid & 63) == 0) red[tid >> 6] = best;
+  __syncthreads();
+  if (tid == 0) {
+#pragma unroll
+    for (int w = 1; w < AM_THREADS / 64; ++w) best = red[w] > best ? red[w] : best;
+    out[blockIdx.x] = (long long)(unsigned)~(unsigned)(best & 0xffffffffu);
+  }
+}
+
 }  // namespace
+
+GS_KERNEL_API int gs_argmax_rows_bf16(const void* x, int ld, int B, int V, void* out, hipStream_t stream) {
+  if (B <= 0 || V <= 0 || ld < V || ld % 8 || ((uintptr_t)x & 15)) return GS_EINVAL;
+  hipLaunchKernelGGL(argmax_rows_bf16, dim3(B), dim3(AM_THREADS), 0, stream, (const unsigned short*)x, ld, V,
+                     (long long*)out);
+  return gs_launch_status();
+}
 
 GS_KERNEL_API int gs_rmsnorm_bf16(const void* x, const void* resid_in, void* resid_out, const void* w, void* y,
                                   int M, int H, float eps, hipStream_t stream) {

@@ -176,12 +176,26 @@ __global__ __launch_bounds__(NW * 64) void skinny_lds(const unsigned short* __re
   u16x8_t wr[8], xr[XI], nwr;
   float inv[XI];
   if constexpr (NORM) {
+    // up to 8 chunks (K <= 8192): every row's chunk sums are loaded at once (clamped addresses, masked
+    // adds in chunk order), not one dependent load per chunk at the kernel's start
+    constexpr int NCH = 8;
+    float cs[XI][NCH];
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+      const int m = min(RPI * i + lr, M - 1);
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) cs[i][c] = nrm.ssq[(size_t)min(c, nrm.nch - 1) * M + m];
+    }
 #pragma unroll
     for (int i = 0; i < XI; ++i) {
       const int m = RPI * i + lr;
       float ss = 0.f;
-      if (m < M)
+      if (nrm.nch <= NCH) {
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) ss += c < nrm.nch ? cs[i][c] : 0.f;
+      } else if (m < M) {
         for (int c = 0; c < nrm.nch; ++c) ss += nrm.ssq[(size_t)c * M + m];
+      }
       inv[i] = rsqrtf(ss / (float)K + nrm.eps);
     }
   }

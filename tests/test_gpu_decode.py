@@ -359,6 +359,23 @@ def test_static_split_reductions_equal_the_loop(K, rope):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("B,V", [(32, 128256), (3, 1001), (1, 7), (64, 4096)])
+def test_argmax_rows_matches_torch(B, V):
+    """Greedy sampling kernel vs torch.argmax: bf16 ties resolved to the first index, strided rows,
+    a V that is not a multiple of 8, -inf rows and NaN (counted as the maximum, as torch does)."""
+    torch.manual_seed(V)
+    ld = -(-V // 8) * 8 + 16                                    # 16-B aligned rows wider than V
+    wide = (torch.randn(B, ld, device="cuda") * 4).round().to(torch.bfloat16)   # many exact ties
+    x = wide[:, 8:8 + V]
+    assert torch.equal(ops.argmax_rows(x), torch.argmax(x, -1))
+    y = wide.clone()[:, 8:8 + V]
+    y[0] = float("-inf")
+    if B > 1:
+        y[1, V // 2] = float("nan")
+        y[1, V - 1] = float("nan")
+    assert torch.equal(ops.argmax_rows(y), torch.argmax(y, -1))
+
+
 def test_refused_skinny_options_leave_no_armed_state():
     """ADVICE (round 2): when the native side refuses a call's options after RoPE was armed, the
     wrapper must clear them, or the next unrelated skinny_linear on this thread would rotate its

@@ -1,0 +1,12 @@
+#!/bin/bash
+# Greedy-sampling kernel: decode tests (argmax vs torch), then the batch-32 decode step.
+set -o pipefail
+O=gpurun_out/am
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest tests/test_gpu_decode.py -x -v -m gpu --timeout 120 --timeout-method thread > $O/tests.log 2>&1 \
+ && timeout -k 10 300 python -u tools/bench_decode.py --no-attn-micro --no-gemm-micro --gemms skinny_rope,hipblaslt > $O/step.log 2>&1 \
+ && timeout -k 10 300 python -u tools/bench_decode.py --no-attn-micro --no-gemm-micro --gemms skinny_rope >> $O/step.log 2>&1
+rc=$?
+echo "rc=$rc"
+exit $rc
