@@ -175,30 +175,35 @@ __global__ __launch_bounds__(NW * 64) void skinny_lds(const unsigned short* __re
   constexpr int XI = MT * 16 / RPI;                       // X row groups (M padded to 16 MT)
   u16x8_t wr[8], xr[XI], nwr;
   float inv[XI];
+  // NORM: up to 8 chunks (K <= 8192) of every row's sums of squares are loaded at once (clamped
+  // addresses, masked adds in chunk order) before the first k-slice is requested, and summed after
+  // it: one memory latency for both at the kernel's start instead of the sums' and then the slice's
+  constexpr int NCH = 8;
+  float cs[NORM ? XI : 1][NCH];
   if constexpr (NORM) {
-    // up to 8 chunks (K <= 8192): every row's chunk sums are loaded at once (clamped addresses, masked
-    // adds in chunk order), not one dependent load per chunk at the kernel's start
-    constexpr int NCH = 8;
-    float cs[XI][NCH];
 #pragma unroll
     for (int i = 0; i < XI; ++i) {
       const int m = min(RPI * i + lr, M - 1);
 #pragma unroll
       for (int c = 0; c < NCH; ++c) cs[i][c] = nrm.ssq[(size_t)min(c, nrm.nch - 1) * M + m];
     }
-#pragma unroll
-    for (int i = 0; i < XI; ++i) {
-      const int m = RPI * i + lr;
-      float ss = 0.f;
-      if (nrm.nch <= NCH) {
-#pragma unroll
-        for (int c = 0; c < NCH; ++c) ss += c < nrm.nch ? cs[i][c] : 0.f;
-      } else if (m < M) {
-        for (int c = 0; c < nrm.nch; ++c) ss += nrm.ssq[(size_t)c * M + m];
-      }
-      inv[i] = rsqrtf(ss / (float)K + nrm.eps);
-    }
   }
+  auto norm_init = [&]() {
+    if constexpr (NORM) {
+#pragma unroll
+      for (int i = 0; i < XI; ++i) {
+        const int m = RPI * i + lr;
+        float ss = 0.f;
+        if (nrm.nch <= NCH) {
+#pragma unroll
+          for (int c = 0; c < NCH; ++c) ss += c < nrm.nch ? cs[i][c] : 0.f;
+        } else if (m < M) {
+          for (int c = 0; c < nrm.nch; ++c) ss += nrm.ssq[(size_t)c * M + m];
+        }
+        inv[i] = rsqrtf(ss / (float)K + nrm.eps);
+      }
+    }
+  };
   auto gload = [&](int kk) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -312,6 +317,7 @@ __global__ __launch_bounds__(NW * 64) void skinny_lds(const unsigned short* __re
     const int S = (k1 - k0) / LBK;
     gl(w2[0], x2[0], n2[0], k0);
     gl(w2[1], x2[1], n2[1], k0 + LBK);
+    norm_init();
     ls(w2[0], x2[0], n2[0]);
     __syncthreads();
     int it = 0;
@@ -337,6 +343,7 @@ __global__ __launch_bounds__(NW * 64) void skinny_lds(const unsigned short* __re
     __syncthreads();
   } else {                                       // PF 1 (and 4: the same with streamed W loads)
     gload(k0);
+    norm_init();
     lstore();
     __syncthreads();
     for (int kk = k0; kk < k1; kk += LBK) {
