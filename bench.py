@@ -465,7 +465,7 @@ class PodFleet:
         self.released_residue = 0             # shim-ledger bytes a stopped pod still held after freeing
         self.release_ms: list[float] = []     # stop -> the GPU physically has room for the replacement
         self.release_by_size: dict[int, list] = {}
-        self.release_gbps: list[float] = []    # retired pod's bytes / (stop -> room back): amdgpu's wipe rate
+        self.release_bytes_s: list[tuple] = [] # (retired pod's bytes, stop -> room back seconds)
         self.retired_bytes = 0                 # HBM the retired pods held (turned over by amdgpu)
         self._stopped_at = None                # (time, size, held bytes) of the last retirement, until its room came back
         self.phase_ms: dict[str, list] = {"stop": [], "init": [], "room": [], "alloc": [], "hold": []}
@@ -550,7 +550,7 @@ class PodFleet:
             self.release_ms.append(dt_rel)
             self.release_by_size.setdefault(self._stopped_at[1], []).append(dt_rel)
             if self._stopped_at[2] > 0:
-                self.release_gbps.append(self._stopped_at[2] / dt_rel / 1e9)
+                self.release_bytes_s.append((self._stopped_at[2], dt_rel))
             self._stopped_at = None
         w["proc"].stdin.write('{"cmd":"alloc"}\n')
         ev = self._wait(w, "ready")
@@ -740,7 +740,7 @@ def main():
         fleet.ready_ms.clear()
         fleet.release_ms.clear()
         fleet.release_by_size.clear()
-        fleet.release_gbps.clear()
+        fleet.release_bytes_s.clear()
         fleet.retired_bytes = 0
         for v in fleet.phase_ms.values():
             v.clear()
@@ -768,7 +768,7 @@ def main():
     release = gather(fleet.release_ms if fleet is not None else [])
     release_all = [x for r in release for x in r]
     retired = gather(fleet.retired_bytes if fleet is not None else 0)
-    rel_rate = [x for r in gather(fleet.release_gbps if fleet is not None else []) for x in r]
+    rel = [x for r in gather(fleet.release_bytes_s if fleet is not None else []) for x in r]
     by_size: dict = {}
     phases: dict = {}
     for d in gather(fleet.phase_ms if fleet is not None else {}):
@@ -876,7 +876,8 @@ def main():
             # freed VRAM before it returns it. Turnover per GPU near the wipe rate = the step is at
             # that bound, not in the plugin (control_plane_ms_per_admission is the plugin's share).
             "hbm_turnover_GBps_per_gpu": round(sum(retired) / n / elapsed / 1e9, 1) if use_gpu else None,
-            "amdgpu_release_GBps_p50": round(pct(rel_rate, 0.5), 1) if rel_rate else None,
+            # bytes-weighted over the retirements: sum(bytes held) / sum(stop -> GPU has room again)
+            "amdgpu_release_GBps": round(sum(b for b, _ in rel) / sum(t for _, t in rel) / 1e9, 1) if rel else None,
         }
         if topo_report is not None:
             res["topology"] = topo_report
