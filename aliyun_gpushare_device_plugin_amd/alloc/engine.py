@@ -176,6 +176,7 @@ class Allocator:
         # placement truth: answered containers, the kubelet's pod-resources view, and the
         # annotation changes this plugin has queued but the pod cache may not show yet
         self.grants = PL.GrantBook()
+        self.prestart_hooks: list = []          # run at PreStartContainer (after the placement pass)
         self._ledgers = self._ledger_dir(self.opts)
         self.podres = None
         self._overlay: dict[str, dict] = {}       # uid -> annotations written, not yet landed
@@ -1046,13 +1047,18 @@ class Allocator:
 
     def prestart(self, req) -> None:
         """``PreStartContainer``: the kubelet checkpointed this container's fake IDs and is
-        about to start it — make the pod annotations tell the truth first."""
-        if self.podres is None:
-            return
-        try:
-            self.reconcile_placement()
-        except Exception as e:  # noqa: BLE001 - never block a container start on bookkeeping
-            log.warning("placement check before container start failed: %s", e)
+        about to start it — make the pod annotations tell the truth first, then run the
+        ``prestart_hooks`` (kernel HBM limits on the pod cgroup, quota/dmem.py)."""
+        if self.podres is not None:
+            try:
+                self.reconcile_placement()
+            except Exception as e:  # noqa: BLE001 - never block a container start on bookkeeping
+                log.warning("placement check before container start failed: %s", e)
+        for hook in list(self.prestart_hooks):
+            try:
+                hook()
+            except Exception as e:  # noqa: BLE001
+                log.warning("pre-start hook failed: %s", e)
 
     def reconcile_placement(self) -> list:
         """One placement pass: join the grant book with the kubelet's pod-resources view and

@@ -98,6 +98,11 @@ def build_parser() -> argparse.ArgumentParser:
                    help="node-side quota watchdog over the kernel's per-process HBM (DRM fdinfo): report "
                         "pods above their share, or also SIGKILL their largest GPU process (the shim cannot be "
                         "bypassed this way; needs hostPID)")
+    p.add_argument("--dmem-limits", default="auto", choices=("auto", "off"),
+                   help="kernel-enforced HBM shares: write each shared pod's share as dmem.max on its cgroup "
+                        "when the kernel has the dmem cgroup controller with amdgpu VRAM regions (auto), else "
+                        "rely on the shim and the watchdog")
+    p.add_argument("--cgroup-root", default="/sys/fs/cgroup", help="cgroup v2 mount (dmem limits)")
     p.add_argument("--quota-watch-interval", type=float, default=10.0)
     p.add_argument("--quota-slack-mib", type=int, default=256,
                    help="HBM above a pod's share tolerated by the watchdog (runtime overhead)")
@@ -132,7 +137,8 @@ def config_from_args(a) -> PluginConfig:
         pod_resources_socket=a.pod_resources_socket, placement_s=a.placement_interval,
         admission_identity=a.admission_identity, quota_enforcement=a.quota_enforcement,
         cdi_kind=a.cdi_kind, expose_devices=a.device_specs,
-        quota_watch_s=a.quota_watch_interval, quota_slack_mib=a.quota_slack_mib)
+        quota_watch_s=a.quota_watch_interval, quota_slack_mib=a.quota_slack_mib,
+        dmem_limits=a.dmem_limits, cgroup_root=a.cgroup_root)
 
 
 def install_shim(dest_dir: str) -> str:

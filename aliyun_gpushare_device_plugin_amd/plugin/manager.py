@@ -79,6 +79,8 @@ class PluginConfig:
     quota_enforcement: str = "report"    # quota/watchdog.py: off | report | kill
     quota_watch_s: float = 10.0
     quota_slack_mib: int = 256
+    dmem_limits: str = "auto"            # quota/dmem.py: kernel dmem.max per pod cgroup when available | off
+    cgroup_root: str = "/sys/fs/cgroup"
     mps: bool = False                    # accepted for flag compatibility; ignored
 
 
@@ -104,6 +106,7 @@ class SharedGPUManager:
         self._ledger_thread = None
         self._ledger_stop = threading.Event()
         self.watchdog = None
+        self.dmem = None
         self._cgpu_disabled = False
 
     # ------------------------------------------------------------------------------------
@@ -248,6 +251,34 @@ class SharedGPUManager:
         else:
             self.watchdog.model, self.watchdog.pods = self.model, self.pod_source
 
+    def _start_dmem(self):
+        """Kernel HBM limits (quota/dmem.py): applied before each container start and on the
+        watchdog's period, so they follow re-homed placements."""
+        from ..quota.dmem import DmemLimits
+
+        cfg = self.cfg
+        if cfg.dmem_limits == "off" or self.model is None or self.pod_source is None or self.allocator is None:
+            return
+        if self.dmem is None:
+            self.dmem = DmemLimits(self.model, self.pod_source, self.metrics, cfg.cgroup_root, cfg.dmem_limits,
+                                   disabled=lambda: self._cgpu_disabled)
+
+            def loop():
+                while not self._ledger_stop.wait(cfg.quota_watch_s):
+                    try:
+                        self.dmem.sync()
+                    except Exception as e:  # noqa: BLE001 - never take the plugin down
+                        log.warning("dmem limit pass failed: %s", e)
+            threading.Thread(target=loop, name="dmem-limits", daemon=True).start()
+        else:
+            self.dmem.model, self.dmem.pods = self.model, self.pod_source
+        if self.dmem.available():
+            log.info("dmem cgroup controller present: shared pods get a kernel HBM limit (dmem.max) on their cgroup")
+            if self.dmem.sync not in self.allocator.prestart_hooks:
+                self.allocator.prestart_hooks.append(self.dmem.sync)
+        else:
+            self.dmem.sync()                        # logs once that it is inactive
+
     def _start_ledger_collector(self):
         """Export the quota shim's per-container ledgers (--ledger-dir) every ledger_scan_s and
         remove the ledger directories of containers whose pods no longer exist on this node."""
@@ -344,6 +375,7 @@ class SharedGPUManager:
                     self._start_health()
                     self._start_ledger_collector()
                     self._start_watchdog()
+                    self._start_dmem()
                     restart = False
                     self.started.set()
                 kind, val = self.events.get()

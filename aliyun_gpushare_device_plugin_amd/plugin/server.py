@@ -91,7 +91,8 @@ class DevicePluginServer:
         self.stopped = threading.Event()
 
     def options(self) -> api.DevicePluginOptions:
-        return api.DevicePluginOptions(pre_start_required=self.allocator.podres is not None,
+        return api.DevicePluginOptions(pre_start_required=self.allocator.podres is not None
+                                       or bool(self.allocator.prestart_hooks),
                                        get_preferred_allocation_available=self.preferred_allocation)
 
     def _cleanup(self):

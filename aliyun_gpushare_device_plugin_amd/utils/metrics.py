@@ -206,6 +206,8 @@ class PluginMetrics:
         self.quota_kills = r.counter("gpushare_quota_kills_total", "Processes killed by the quota watchdog")
         self.unaccounted_hbm = r.gauge("gpushare_unaccounted_hbm_bytes",
                                        "HBM held on a GPU by processes of no pod on this node")
+        self.dmem_limited_pods = r.gauge("gpushare_dmem_limited_pods",
+                                         "Shared pods whose HBM share is a kernel dmem.max limit on their cgroup")
         self.cu_slots_held = r.gauge("gpushare_cu_slots_held",
                                      "CU slots held by pods per GPU at the last compute-isolation decision "
                                      "(slot = one CU on every XCD; > slots per GPU means oversubscribed)")

@@ -103,6 +103,9 @@ def test_daemonset_mounts_match_the_flags():
     assert spec.get("hostNetwork") is True and spec["nodeSelector"] == {"gpushare": "true"}
     # the quota watchdog reads every GPU process's DRM fdinfo and pod cgroup
     assert spec.get("hostPID") is True and cfg.quota_enforcement in ("report", "kill")
+    # kernel dmem limits write the HOST cgroup hierarchy (the container's own is namespaced)
+    assert cfg.dmem_limits == "auto" and cfg.cgroup_root in mounts and not mounts[cfg.cgroup_root].get("readOnly")
+    assert vols[mounts[cfg.cgroup_root]["name"]]["hostPath"]["path"] == "/sys/fs/cgroup"
 
 
 def test_dockerfile_recipe_builds_and_installs(tmp_path):
