@@ -2,7 +2,7 @@
 # Round-3 validation of the final tree: smoke, the whole GPU suite (one process, per-test limits),
 # then the 1-GPU headline bench with the driver's step counts.
 set -o pipefail
-O=gpurun_out/final
+O=gpurun_out/${1:-final}
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 \
