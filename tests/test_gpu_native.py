@@ -382,3 +382,26 @@ def test_quota_watchdog_catches_a_process_without_the_shim():
         if child.poll() is None:
             child.kill()
             child.wait(timeout=20)
+
+
+def test_dmem_limits_read_the_box_kernel_truthfully():
+    """quota/dmem.py on the real cgroup v2 tree: it reports the dmem controller exactly when the
+    kernel lists it, finds a VRAM region for every GPU when it does, and otherwise stays inactive
+    (the test boxes' 6.18 kernel has no dmem controller: profiles/r3/dmem_probe.txt)."""
+    from aliyun_gpushare_device_plugin_amd.quota.dmem import DmemLimits
+
+    from .test_allocate_engine import StaticSource
+
+    with S.SMI("auto") as smi:
+        model = DeviceModel(smi.devices(), const.GIB, "nearest")
+    try:
+        with open("/sys/fs/cgroup/cgroup.controllers") as f:
+            ctrl = "dmem" in f.read().split()
+    except OSError:
+        ctrl = False
+    d = DmemLimits(model, StaticSource([]))
+    assert d.controller_present() == ctrl
+    if ctrl and d.regions():
+        assert set(d.regions()) == {g.index for g in model.gpus}
+    else:
+        assert not d.available() and d.sync() == 0
