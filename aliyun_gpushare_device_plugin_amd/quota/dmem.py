@@ -12,7 +12,9 @@ This module applies each shared pod's HBM share as ``dmem.max`` on the pod's cgr
 
 * the share per GPU comes from the pod's (truthful, ``alloc/placement.py``) placement annotations,
   converted exactly as the quota shim and the watchdog convert units to bytes (``units.quota_bytes``);
-  the node's other GPUs' regions are set to 0 for that pod;
+  the pod's other regions are left at the kernel default (``max``; the device cgroup already keeps
+  it off GPUs it was not given, and a pod may hold whole GPUs from another plugin), and a region
+  whose share moved away with a re-homed placement goes back to ``max``;
 * the pod's cgroup is found under the kubelet's hierarchy (cgroupfs ``kubepods/<qos>/pod<uid>`` or
   systemd ``kubepods-<qos>-pod<uid_with_underscores>.slice``); the controller is switched on down
   the path (``+dmem`` in every ancestor's ``cgroup.subtree_control``), which the kubelet does not
@@ -111,13 +113,13 @@ class DmemLimits:
 
     # ---- the limits -------------------------------------------------------------------------------
     def limits_for(self, pod: dict, regions: dict[int, str]) -> dict[str, int]:
-        """Region -> bytes the pod may hold: its share on the GPUs it is placed on, 0 elsewhere."""
-        share = {}
+        """Region -> bytes the pod may hold, for the GPUs it is placed on."""
+        out = {}
         for gi, units in PL.annotated_usage(pod).items():
             g = self.model.gpu(gi)
-            if g is not None:
-                share[gi] = U.quota_bytes(units, g.units, g.vram_bytes)
-        return {name: share.get(gi, 0) for gi, name in regions.items()}
+            if g is not None and gi in regions:
+                out[regions[gi]] = U.quota_bytes(units, g.units, g.vram_bytes)
+        return out
 
     def apply(self, pod: dict, regions: dict[int, str] | None = None) -> bool:
         """Write the pod's limits to its cgroup's ``dmem.max`` (only what changed). False when the
@@ -127,16 +129,21 @@ class DmemLimits:
         if not regions or not PL.annotated_usage(pod):
             return False
         want = self.limits_for(pod, regions)
+        if not want:
+            return False
         with self._mu:
-            if self.applied.get(uid) == want:
+            before = self.applied.get(uid, {})
+            if before == want:
                 return True
             cg = self.pod_cgroup(uid)
             if cg is None:
                 return False
+            lines = [f"{name} {nbytes}" for name, nbytes in sorted(want.items())]
+            lines += [f"{name} max" for name in sorted(before) if name not in want]    # share moved away
             try:
                 self._enable_down_to(cg)
-                with open(os.path.join(cg, "dmem.max"), "w") as f:    # one "region bytes" line each
-                    f.write("\n".join(f"{name} {nbytes}" for name, nbytes in sorted(want.items())) + "\n")
+                with open(os.path.join(cg, "dmem.max"), "w") as f:    # one "region limit" line each
+                    f.write("\n".join(lines) + "\n")
             except OSError as e:
                 log.warning("dmem limit for pod %s/%s not applied: %s", O.namespace(pod), O.name(pod), e)
                 return False

@@ -42,7 +42,11 @@ def _model():
 
 
 def _limits(path):
-    return dict((ln.split()[0], int(ln.split()[1])) for ln in (path / "dmem.max").read_text().splitlines())
+    out = {}
+    for ln in (path / "dmem.max").read_text().splitlines():
+        name, v = ln.split()
+        out[name] = v if v == "max" else int(v)
+    return out
 
 
 def test_shares_become_dmem_max_on_both_cgroup_layouts(tmp_path):
@@ -56,7 +60,7 @@ def test_shares_become_dmem_max_on_both_cgroup_layouts(tmp_path):
     assert d.regions() == {0: f"drm/{model.gpu(0).bdf}/vram0", 1: f"drm/{model.gpu(1).bdf}/vram0"}
     assert d.sync() == 2
     r0, r1 = d.regions()[0], d.regions()[1]
-    assert _limits(a) == {r0: 0, r1: 4 * GIB} and _limits(b) == {r0: 8 * GIB, r1: 0}
+    assert _limits(a) == {r1: 4 * GIB} and _limits(b) == {r0: 8 * GIB}     # other GPUs: kernel default
     for anc in (root, root / "kubepods.slice", root / "kubepods.slice" / "kubepods-burstable.slice",
                 root / "kubepods", root / "kubepods" / "besteffort"):
         assert "dmem" in (anc / "cgroup.subtree_control").read_text()
@@ -75,7 +79,7 @@ def test_limits_follow_a_rehomed_placement_and_forget_gone_pods(tmp_path):
     assert (a / "dmem.max").read_text() == ""
     pa["metadata"]["annotations"][const.ENV_RESOURCE_INDEX] = "0"            # placement truth moved it
     d.sync()
-    assert _limits(a) == {d.regions()[0]: 4 * GIB, d.regions()[1]: 0}
+    assert _limits(a) == {d.regions()[0]: 4 * GIB, d.regions()[1]: "max"}   # old region back to max
     src.pods = []
     d.sync()
     assert d.applied == {}
