@@ -13,4 +13,26 @@ Layer map (re-designed for MI355X):
   parallel/                xGMI topology export, TP-group placement, RCCL demo
   sim/                     fake apiserver / kubelet / extender for CPU-only end-to-end runs
 """
+import os as _os
+
 __version__ = "0.1.0"
+
+
+def _lifeline() -> None:
+    """Simulator children (``sim/cluster.py``: fake apiserver, kubelet, plugin processes) die with
+    the process that started them. Armed here, after exec: in a ``preexec_fn`` (between fork and
+    exec) the child imports ctypes and dlopens, and a loader or import lock another thread of the
+    multi-threaded parent (gRPC pollers) held at fork time deadlocks it (seen as a plugin process
+    that never registered)."""
+    ppid = _os.environ.pop("GPUSHARE_DIE_WITH_PARENT", None)      # not inherited any further
+    if not ppid:
+        return
+    import ctypes
+    import signal
+
+    ctypes.CDLL(None, use_errno=True).prctl(1, signal.SIGTERM)    # PR_SET_PDEATHSIG
+    if _os.getppid() != int(ppid):                                # the parent is already gone
+        _os._exit(0)
+
+
+_lifeline()

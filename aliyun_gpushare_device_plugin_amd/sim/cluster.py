@@ -106,7 +106,7 @@ class SimCluster:
         self.api_proc = subprocess.Popen(
             [sys.executable, "-m", "aliyun_gpushare_device_plugin_amd.sim.apiserver", "--port", "0",
              "--latency-ms", str(self.apiserver_latency_s * 1e3)],
-            env=self._child_env(), stdout=subprocess.PIPE, text=True, preexec_fn=_die_with_parent)
+            env=self._child_env(), stdout=subprocess.PIPE, text=True)
         self.api_url = self.api_proc.stdout.readline().strip()
         if not self.api_url.startswith("http"):
             raise RuntimeError("fake apiserver process failed to start")
@@ -115,6 +115,9 @@ class SimCluster:
     def _child_env():
         env = dict(os.environ)
         env.setdefault("GPUSHARE_DEBUG", "1")      # simulator children: debug endpoints on
+        # SIGTERM the child when the simulator dies (a killed test or bench leaves no fake
+        # apiserver / kubelet / plugin behind); armed by the package import, after exec
+        env["GPUSHARE_DIE_WITH_PARENT"] = str(os.getpid())
         env["PYTHONPATH"] = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))) + \
             os.pathsep + env.get("PYTHONPATH", "")
         return env
@@ -126,8 +129,7 @@ class SimCluster:
             self.client.create_node(make_node(name))
             pdir = os.path.join(self.workdir, name)
             if self.kubelet_mode == "process" and self.pod_source != "kubelet":
-                kl = KubeletProcess(pdir, self.api_url, name, env=self._child_env(),
-                                    preexec_fn=_die_with_parent).start()
+                kl = KubeletProcess(pdir, self.api_url, name, env=self._child_env()).start()
             else:
                 kl = FakeKubelet(pdir, APIClient(KubeConfig(self.api_url)), name).start()
                 if self.pod_source == "kubelet":
@@ -137,7 +139,7 @@ class SimCluster:
             self._start_plugin(node)
         for node in self.nodes.values():
             if not node.kubelet.registered.wait(timeout):
-                raise TimeoutError(f"plugin on {node.name} did not register")
+                raise TimeoutError(f"plugin on {node.name} did not register{self._plugin_log_tail(node)}")
             if node.manager is not None and not node.manager.started.wait(timeout):
                 raise TimeoutError(f"plugin manager on {node.name} did not finish starting")
             self._wait_capacity(node.name, timeout)
@@ -188,7 +190,7 @@ class SimCluster:
                 args += ["--" + k.replace("_", "-"), str(v)]
             ov = self.node_overrides.get(node.name, {})
             args += ov["extra_args"] if "extra_args" in ov else self.extra_plugin_args
-            node.proc = subprocess.Popen(args, env=self._child_env(), stdout=subprocess.DEVNULL, preexec_fn=_die_with_parent,
+            node.proc = subprocess.Popen(args, env=self._child_env(), stdout=subprocess.DEVNULL,
                                          stderr=open(os.path.join(self.workdir, f"{node.name}.plugin.log"), "w"))
         else:
             node.manager = SharedGPUManager(self._plugin_cfg(node), client=APIClient(KubeConfig(self.api_url)))
@@ -211,7 +213,15 @@ class SimCluster:
         n.kubelet.registered.clear()
         self._start_plugin(n)
         if not n.kubelet.registered.wait(timeout):
-            raise TimeoutError(f"plugin on {node} did not re-register")
+            raise TimeoutError(f"plugin on {node} did not re-register{self._plugin_log_tail(n)}")
+
+    def _plugin_log_tail(self, node, n: int = 3000) -> str:
+        """The end of a process-mode plugin's log, for timeout messages."""
+        try:
+            with open(os.path.join(self.workdir, f"{node.name}.plugin.log")) as f:
+                return "; plugin log tail:\n" + f.read()[-n:]
+        except OSError:
+            return ""
 
     def _wait_capacity(self, node: str, timeout: float):
         t = time.monotonic() + timeout
@@ -323,14 +333,6 @@ class SimCluster:
 
     def manager(self, node: str) -> SharedGPUManager | None:
         return self.nodes[node].manager
-
-
-def _die_with_parent():
-    """Child-side (between fork and exec): SIGTERM this process when the simulator dies, so a
-    killed test or bench never leaves a fake apiserver or plugin process behind."""
-    import ctypes
-
-    ctypes.CDLL(None, use_errno=True).prctl(1, signal.SIGTERM)   # PR_SET_PDEATHSIG
 
 
 def quiet():
