@@ -196,3 +196,21 @@ def test_shim_injected_end_to_end(native_shim):
         r = adm.responses[0]
         assert r.envs[const.ENV_LD_PRELOAD].endswith(const.SHIM_LIB_NAME)
         assert r.mounts[0].host_path == shim_dir
+
+
+def test_children_arm_their_lifeline_after_exec():
+    """The simulator's children set PR_SET_PDEATHSIG from the package import (no preexec_fn between
+    fork and exec of the threaded parent): the variable is consumed so grandchildren do not inherit
+    it, and a child whose parent is not the one named exits at once."""
+    import subprocess
+    import sys
+
+    code = ("import os, aliyun_gpushare_device_plugin_amd; "
+            "print(os.environ.get('GPUSHARE_DIE_WITH_PARENT', 'consumed'))")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, GPUSHARE_DIE_WITH_PARENT=str(os.getpid()), PYTHONPATH=root)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and r.stdout.strip() == "consumed"
+    env["GPUSHARE_DIE_WITH_PARENT"] = "1"                     # not our parent: the child leaves quietly
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and r.stdout == ""
