@@ -453,8 +453,9 @@ class PodFleet:
     imported, GPU untouched) that becomes the next admitted pod."""
 
     def __init__(self, local: int, gemm: int, burst: int, fill: float, visible_by_uuid: bool, standby: int = 2,
-                 slack: int = 2 << 30):
+                 slack: int = 2 << 30, ordinal: int | None = None):
         self.local, self.gemm, self.burst, self.fill, self.slack = local, gemm, burst, fill, slack
+        self.ordinal = local if ordinal is None else ordinal     # this GPU's HIP ordinal (bind_device)
         self.visible_by_uuid = visible_by_uuid
         self.pods: dict[str, dict] = {}       # uid -> {"proc", "q", "size", "ready"}
         self.standby: list[dict] = []         # pre-started interpreters, oldest first
@@ -534,7 +535,7 @@ class PodFleet:
         env.pop("LD_PRELOAD", None)                     # preloaded since exec (same host path)
         if not self.visible_by_uuid:                    # modelled node (fake SMI): this rank's GPU
             env.pop("ROCR_VISIBLE_DEVICES", None)
-            env["HIP_VISIBLE_DEVICES"] = str(self.local)
+            env["HIP_VISIBLE_DEVICES"] = str(self.ordinal)
         from aliyun_gpushare_device_plugin_amd import const
 
         t0 = time.perf_counter()
@@ -621,14 +622,48 @@ class PodFleet:
                 w["proc"].kill()
 
 
+def relaunch(n: int) -> int:
+    """``bench.py --gpus N`` started without a launcher (no ``WORLD_SIZE``): run the same command
+    as N ranks under ``torch.distributed.run`` in a child process and return its exit code. Called
+    before anything touches the GPU (no torch import yet), so the parent never holds a device."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    sys.stderr.write(f"bench: --gpus {n} without a launcher: running {n} ranks under torch.distributed.run\n")
+    sys.stderr.flush()
+    return subprocess.call(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
+
+
+def bind_device(smi_index: int) -> tuple[int, dict]:
+    """The HIP ordinal of the plugin's GPU ``smi_index`` (the plugin enumerates SMI devices and
+    this rank churns that GPU), matched by PCI address — HIP and SMI orders are not promised to
+    agree. Returns (ordinal, binding record); exits when no visible HIP device has that address."""
+    import torch
+
+    from aliyun_gpushare_device_plugin_amd.device.smi import SMI
+
+    with SMI("auto") as s:
+        if s.count() <= smi_index:
+            raise SystemExit(f"bench: rank for plugin GPU {smi_index} but SMI sees {s.count()} GPU(s)")
+        g = s.device(smi_index)
+    dom, bus, rest = g.bdf.split(":")
+    want = (int(dom, 16), int(bus, 16), int(rest.split(".")[0], 16))
+    for i in range(torch.cuda.device_count()):
+        p = torch.cuda.get_device_properties(i)
+        if (p.pci_domain_id, p.pci_bus_id, p.pci_device_id) == want:
+            return i, {"smi_index": smi_index, "uuid": g.uuid, "bdf": g.bdf, "hip_ordinal": i}
+    raise SystemExit(f"bench: no HIP device at {g.bdf} (plugin GPU {smi_index}, {g.uuid})")
+
+
 def main():
     a = parse()
+    n = a.gpus
+    if "WORLD_SIZE" not in os.environ and n > 1:
+        sys.exit(relaunch(n))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    n = a.gpus
-    if world not in (1, n):
-        raise SystemExit(f"WORLD_SIZE={world} but --gpus {n}")
+    if world != n:
+        raise SystemExit(f"WORLD_SIZE={world} but --gpus {n}: one rank per GPU")
 
     import tempfile
 
@@ -636,9 +671,12 @@ def main():
     import torch.distributed as dist
 
     use_gpu = torch.cuda.is_available() and not a.no_gpu
+    binding = None
+    ordinal = local
     if use_gpu:
-        torch.cuda.set_device(local)
-    dev = torch.device("cuda", local) if use_gpu else None
+        ordinal, binding = bind_device(local)
+        torch.cuda.set_device(ordinal)
+    dev = torch.device("cuda", ordinal) if use_gpu else None
     if world > 1:
         dist.init_process_group("nccl" if use_gpu else "gloo", device_id=dev if use_gpu else None)
 
@@ -663,7 +701,6 @@ def main():
             torch.cuda.synchronize()
 
     smi = a.smi_backend or ("auto" if use_gpu else f"fake:{n}x288G")
-    visible_by_uuid = use_gpu
     cp = None
     info = None
     workdir = tempfile.mkdtemp(prefix="gs-bench-", dir="/tmp")
@@ -672,19 +709,19 @@ def main():
         if use_gpu and smi == "auto":
             from aliyun_gpushare_device_plugin_amd.device.smi import SMI
             with SMI("auto") as s:
+                # every rank bound its plugin GPU above (bind_device), so the node has >= n GPUs
                 ref_spec = f"fake:{n}x{s.device(0).vram_total}B"
-                if s.count() < n:          # fewer visible GPUs than ranks: model the node
-                    smi = ref_spec
-                    visible_by_uuid = False
         cp = ControlPlane(n, smi, a.pod_source, a.plugin_mode, workdir, with_shim=use_gpu,
                           ref_spec=None if a.no_ref_churn else ref_spec)
-        info = {"units_per_gpu": cp.units_per_gpu, "gpu_count": cp.gpu_count, "by_uuid": visible_by_uuid}
+        info = {"units_per_gpu": cp.units_per_gpu, "gpu_count": cp.gpu_count}
     info = bcast(info)
     units = info["units_per_gpu"]
-    fleet = PodFleet(local, a.gemm, a.burst, a.fill, info["by_uuid"], a.standby,
-                     slack=int(a.room_slack_gib * (1 << 30))) if use_gpu else None
-    topo_report = None
+    # pod processes see their GPU through the Allocate response's ROCR_VISIBLE_DEVICES (UUID)
+    fleet = PodFleet(local, a.gemm, a.burst, a.fill, not smi.startswith("fake:"), a.standby,
+                     slack=int(a.room_slack_gib * (1 << 30)), ordinal=ordinal) if use_gpu else None
+    topo_report = cp_topo = None
     topo_failed = False
+    problems: list = []
 
     def launch(started: dict) -> float:
         """Start this rank's newly admitted pods; returns the slowest ready latency."""
@@ -706,15 +743,24 @@ def main():
     if rank != 0:
         client = AdmissionClient(port)
 
+    done = {"churned": 0, "started": 0}          # this rank's GPU, timed region only (reset below)
+
+    idle = os.environ.get("GS_BENCH_IDLE_RANK")   # test hook: this rank's pipeline does nothing
+
     def cycle():
+        if idle is not None and int(idle) == rank:
+            return
         uid = None
         if fleet is not None:
             uid = fleet.oldest()
             if uid is not None:
                 fleet.stop(uid)                  # the replacement's start waits for the HBM
         rec = svc.churn(local, uid) if rank == 0 else client.churn(local, uid)
-        if rec is not None and fleet is not None:
-            fleet.start(rec)
+        if rec is not None:
+            done["churned"] += 1
+            if fleet is not None:
+                fleet.start(rec)
+                done["started"] += 1
 
     # ---- warm-up: fill the node, start its pods, then W untimed churn cycles per GPU ----
     started = bcast(cp.fill() if rank == 0 else None)
@@ -745,6 +791,7 @@ def main():
         for v in fleet.phase_ms.values():
             v.clear()
 
+    done.update(churned=0, started=0)
     barrier()
     g0 = fleet.gemms() if fleet is not None else 0
     t0 = time.perf_counter()
@@ -769,6 +816,8 @@ def main():
     release_all = [x for r in release for x in r]
     retired = gather(fleet.retired_bytes if fleet is not None else 0)
     rel = [x for r in gather(fleet.release_bytes_s if fleet is not None else []) for x in r]
+    per_rank = gather(dict(done, rank=rank, gpu=local, binding=binding,
+                           pods_live=len(fleet.pods) if fleet is not None else None))
     by_size: dict = {}
     phases: dict = {}
     for d in gather(fleet.phase_ms if fleet is not None else {}):
@@ -785,7 +834,7 @@ def main():
         topo = healthy = None
         if rank == 0:
             node = cp.cluster.client.get_node(MAIN_NODE)
-            topo = nodestatus.read_topology(node)
+            topo = cp_topo = nodestatus.read_topology(node)
             hmap = json.loads((node.get("metadata", {}).get("annotations") or {}).get(
                 "gpushare.amd.com/gpu-health", "{}") or "{}")
             healthy = [bool((hmap.get(str(i)) or {}).get("healthy", True)) for i in range(n)]
@@ -801,8 +850,18 @@ def main():
         ref_srv = plugin_latency(cp.ref_port) if cp.ref_port else None
         pods_node = sum(len(v) for v in cp.resident.values())
         gib_node = sum(s for v in cp.resident.values() for _, s in v)
-        admissions = a.steps * n - cp.failed
+        # real admissions of the timed region (every churn_one that admitted a replacement),
+        # never steps x n: a GPU whose pipeline did not run contributes nothing
+        admissions = len(cp.admit_lat)
         value = admissions / elapsed
+        problems = []
+        for r in per_rank:
+            if r["churned"] == 0:
+                problems.append(f"GPU {r['gpu']} (rank {r['rank']}): no admissions in the timed region")
+            if use_gpu and (r["started"] == 0 or not r["pods_live"]):
+                problems.append(f"GPU {r['gpu']} (rank {r['rank']}): no pod processes started")
+        if n > 1 and (topo_report is None or "verdict" not in topo_report):
+            problems.append("no topology verdict for a multi-GPU node")
         under_churn = {"default": {
             "allocate_p50_ms": ms(pct(cp.alloc_lat, 0.5)), "allocate_p99_ms": ms(pct(cp.alloc_lat, 0.99)),
             "plugin_allocate_p50_ms": ms(srv["p50"]) if srv else None,
@@ -855,7 +914,7 @@ def main():
             # one churn cycle on a GPU: stop (old pod frees) -> admission -> new pod's runtime up
             # (init) -> physical room for its state (room) -> state allocated + first GEMM (alloc)
             "pod_phase_p50_ms": {k: ms(pct(v, 0.5)) for k, v in phases.items()},
-            "control_plane_ms_per_admission": round(cp.cp_time / max(1, a.steps * n) * 1e3, 3),
+            "control_plane_ms_per_admission": round(cp.cp_time / max(1, admissions) * 1e3, 3),
             "allocate_p50_ms_by_gpu": {str(g): ms(pct(v, 0.5)) for g, v in cp.alloc_lat_by_gpu.items()},
             # both plugins during the same timed churn (alternating admissions, same pod load)
             "allocate_under_churn": under_churn,
@@ -869,6 +928,9 @@ def main():
             "hbm_held_by_pods_gib": round(sum(held) / (1 << 30), 1) if use_gpu else None,
             "quota_denials": sum(denied),
             "pod_hbm_residue_after_free_mib": round(max(residue) / (1 << 20), 1) if use_gpu else None,
+            "admissions": admissions,
+            "admissions_by_gpu": {str(r["gpu"]): r["churned"] for r in per_rank},
+            "pods_started_by_gpu": {str(r["gpu"]): r["started"] for r in per_rank} if use_gpu else None,
             "failed_admissions": cp.failed,
             "failure_reasons": cp.fail_reasons[:5],
             "gemm_tflops_node": round(gemm_flops / elapsed / 1e12, 1) if use_gpu else None,
@@ -881,6 +943,17 @@ def main():
         }
         if topo_report is not None:
             res["topology"] = topo_report
+            if use_gpu:
+                # each rank's device, bound by PCI address, against the plugin's matrix row
+                binds = {str(r["gpu"]): r["binding"] for r in per_rank}
+                topo_report["device_binding"] = binds
+                rows = {str(k): g for k, g in enumerate((cp_topo or {}).get("gpus") or [])}
+                for k, b in binds.items():
+                    row = rows.get(k)
+                    if b is None or row is None or row.get("bdf") != b["bdf"]:
+                        problems.append(f"rank of GPU {k} bound {b} but the plugin's topology row is {row}")
+        if problems:
+            res["run_problems"] = problems
         line = json.dumps(res)
         print(line, flush=True)
         if a.json_out:
@@ -903,6 +976,10 @@ def main():
         # a broken topology export must not pass as a successful multi-GPU run
         sys.stderr.write("bench: topology verdict FAIL: " + "; ".join(topo_report["reasons"]) + "\n")
         sys.exit(3)
+    if problems:
+        # a GPU that did no work must not pass as an N-GPU measurement
+        sys.stderr.write("bench: run FAILED: " + "; ".join(problems) + "\n")
+        sys.exit(4)
 
 
 if __name__ == "__main__":

@@ -115,3 +115,35 @@ def test_topology_verdict_rules():
     pcie = {"link_type": [["self", "pcie"], ["pcie", "self"]], "hops": [[0, 3], [3, 0]]}
     assert not T.verdict(pcie, 2)[0]
     assert T.verdict(pcie, 2, healthy=[True, False]) == (True, [])     # a sick GPU excuses its links
+
+
+def test_bench_plain_multi_gpu_runs_every_gpu():
+    """Round-3 review item 1: ``bench.py --gpus 4`` without a launcher re-launches itself as 4
+    ranks (before touching any GPU), so every GPU churns: 4 x steps real admissions, a p50 per
+    GPU and a topology verdict — not one pipeline divided by 4x the admissions."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "4", "--no-gpu", "--steps", "4", "--warmup", "1",
+                        "--compare-rtts", "", "--fill-orders", ""],
+                       cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "torch.distributed.run" in r.stderr
+    d = parse(r.stdout)
+    assert d["n_gpus"] == 4 and d["admissions"] == 16
+    assert d["admissions_by_gpu"] == {"0": 4, "1": 4, "2": 4, "3": 4}
+    assert all(d["allocate_p50_ms_by_gpu"][str(g)] is not None for g in range(4))
+    assert d["topology"]["verdict"] == "pass" and "run_problems" not in d
+    assert abs(d["value"] - d["admissions"] / (d["ms_per_step"] * d["steps"] / 1e3)) < 0.05 * d["value"]
+
+
+def test_bench_fails_when_a_gpu_does_no_work():
+    """A rank whose pipeline never churns makes the run fail (exit 4) and is named in the line;
+    the value counts only the admissions that happened."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["GS_BENCH_IDLE_RANK"] = "1"
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--no-gpu", "--steps", "3", "--warmup", "0",
+                        "--compare-rtts", "", "--fill-orders", "", "--no-ref-churn"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode != 0
+    d = parse(r.stdout)
+    assert d["admissions"] == 3 and d["admissions_by_gpu"] == {"0": 3, "1": 0}
+    assert any("GPU 1" in p for p in d["run_problems"]) and "run FAILED" in r.stderr
