@@ -185,6 +185,7 @@ class Allocator:
         self._place_mu = threading.Lock()
         self._place_thread = None
         self._last_grant = 0.0
+        self._placed_at = 0.0                     # start of the last completed placement pass
         # fast path: prepared answers, engine-state generation, answers awaiting bookkeeping
         self._fast: _Fast | None = None
         self._gen = 0
@@ -674,7 +675,7 @@ class Allocator:
                 return None
             pick = self._take(el[0])
         rb = req.SerializeToString()
-        t = self.journal.record_fast(pick.uid, pick.ns, pick.name, pick.head, rb)
+        t = self.journal.record_fast(pick.uid, pick.ns, pick.name, pick.head, rb, ids)
         self._post.append((rb, pick, t))
         job = _PatchJob(pick.uid, pick.ns, pick.name, {})
         # the reference logs the request and the outcome (allocate.go:47-58,193-194): one record here
@@ -753,8 +754,11 @@ class Allocator:
                               cr.annotations.get(const.CTR_ANNOTATION_LEDGER, ""))
             keep[k] = c
             out.append(c)
-        self._prep_cache = keep
-        self._fast = _Fast(version, gen, tuple(out))
+        with self._mu:
+            if gen != self._gen:          # reconfigured meanwhile: answers built from the old model
+                return
+            self._prep_cache = keep
+            self._fast = _Fast(version, gen, tuple(out))
         if self.journal.indexed_uids():         # replay index: only pods that can still be retried
             pend = {O.uid(p) for p in src.pending_pods()}
             self.journal.prune_index(pend)
@@ -928,7 +932,10 @@ class Allocator:
                 continue
             if job is None:
                 break
-            self._drain_post()
+            try:
+                self._drain_post()
+            except Exception as e:  # noqa: BLE001 - bookkeeping must never stop the patcher
+                log.warning("fast-path bookkeeping failed: %s", e)
             delay = 0.05
             while not self._stop.is_set():
                 try:
@@ -1068,6 +1075,7 @@ class Allocator:
             return []
         self._drain_post()
         with self._place_mu:
+            t_pass = time.monotonic()
             held = src.list()
             pods = self._view(A.dedupe_by_uid(self.pods.node_pods(), self.node))
             now = time.time()
@@ -1077,7 +1085,23 @@ class Allocator:
             live = {O.uid(p) for p in pods}
             self.grants.prune({PL.ids_key(ids) for pd in held for _, ids in pd.containers}, live, now,
                               self.opts.in_flight_s)
+            self._placed_at = t_pass
             return fixes
+
+    def settled(self, uid: str) -> bool:
+        """The pod's annotations are known to tell where it runs: placement truth is on, a
+        placement pass has run since the last answer of this node, and nothing of the pod (its
+        answer's PATCH, a placement fix, a multi-container claim) is in flight. The quota
+        watchdog kills only settled pods (quota/watchdog.py)."""
+        if self.podres is None or self._post or self._placed_at < self._last_grant:
+            return False
+        with self._mu:
+            return uid not in self._overlay and uid not in self._unpatched and uid not in self._claims
+
+    def view(self, pods: list[dict]) -> list[dict]:
+        """``pods`` as they read once this plugin's queued annotation fixes have landed."""
+        with self._mu:
+            return self._view(pods)
 
     def _apply_fix(self, f: PL.Fix) -> None:
         ann = dict(f.ann)

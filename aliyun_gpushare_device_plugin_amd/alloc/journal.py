@@ -133,11 +133,19 @@ class AllocJournal:
         end = self._mm.find(b"\0")
         self._off = len(self._mm) if end < 0 else end
         self._touched = self._off
-        self.prefault()
+        self._prefault()
 
     def prefault(self, ahead: int = 256 << 10) -> None:
         """Fault in the pages the next records will land on (off the Allocate path: the
-        patcher calls it), so an answer's store never takes the first-write page fault."""
+        patcher calls it), so an answer's store never takes the first-write page fault. Under
+        the journal lock: a compaction on a gRPC thread replaces the mapping."""
+        with self._lock:
+            try:
+                self._prefault(ahead)
+            except ValueError:           # mapping closed by a failed compaction: next write remaps
+                pass
+
+    def _prefault(self, ahead: int = 256 << 10) -> None:
         mm = self._mm
         if mm is None:
             return
@@ -236,15 +244,20 @@ class AllocJournal:
                 self._uids.pop(u, None)
             self._write({"k": key, "uid": pod_uid, "t": t, "resp": base64.b64encode(blob).decode()})
 
-    def record_fast(self, pod_uid: str, ns: str, name: str, head: bytes, req_bytes: bytes) -> float:
+    def record_fast(self, pod_uid: str, ns: str, name: str, head: bytes, req_bytes: bytes, ids=()) -> float:
         """Allocate fast path: the answer + pending-patch record from its prepared ``head``
         (everything but the time and the request) — one store into the mapping. The request
-        goes in as its wire bytes (no per-ID Python strings on the hot path); the in-memory
-        answer index follows off the hot path (``index_answer``). Returns the record's time."""
+        goes in as its wire bytes; the answer itself is indexed off the hot path
+        (``index_answer``), but its fake ``ids`` are marked at once, so a kubelet retry of the
+        same set that arrives before that sees "maybe a replay" and takes the full path (which
+        indexes first). Returns the record's time."""
         t = time.time()
         pend = {"op": "patch", "uid": pod_uid, "ns": ns, "name": name, "ann": {}, "t": t}
         data = b"".join((head, repr(t).encode(), b',"req":"', base64.b64encode(req_bytes), b'"}\n'))
         with self._lock:
+            mark = self._by_id
+            for i in ids:
+                mark[i] = ""             # placeholder key: index_answer overwrites it
             self._uids[pod_uid] = t
             self._pending[pod_uid] = pend
             if self.path:

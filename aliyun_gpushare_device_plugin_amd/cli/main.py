@@ -94,10 +94,12 @@ def build_parser() -> argparse.ArgumentParser:
                         "container toolkit generates); empty = DeviceSpecs only")
     p.add_argument("--device-specs", type=_bool, nargs="?", const=True, default=True,
                    help="answer /dev/kfd and the GPU's render node as DeviceSpecs (false with --cdi-kind: CDI only)")
-    p.add_argument("--quota-enforcement", default="report", choices=("off", "report", "kill"),
+    p.add_argument("--quota-enforcement", default="auto", choices=("auto", "off", "report", "kill"),
                    help="node-side quota watchdog over the kernel's per-process HBM (DRM fdinfo): report "
                         "pods above their share, or also SIGKILL their largest GPU process (the shim cannot be "
-                        "bypassed this way; needs hostPID)")
+                        "bypassed this way; needs hostPID). auto = kill when the kernel has no dmem limits and "
+                        "the kubelet pod-resources API is available, else report; kill without pod-resources "
+                        "is downgraded to report")
     p.add_argument("--dmem-limits", default="auto", choices=("auto", "off"),
                    help="kernel-enforced HBM shares: write each shared pod's share as dmem.max on its cgroup "
                         "when the kernel has the dmem cgroup controller with amdgpu VRAM regions (auto), else "

@@ -76,7 +76,9 @@ class PluginConfig:
     pod_resources_socket: str = "auto"
     placement_s: float = 2.0
     admission_identity: bool = True      # which pod is being admitted, from pod-resources (engine)
-    quota_enforcement: str = "report"    # quota/watchdog.py: off | report | kill
+    # quota/watchdog.py: off | report | kill | auto (kill where the kernel has no dmem limits
+    # and placement truth is on, so the share holds for a tenant that drops the shim)
+    quota_enforcement: str = "auto"
     quota_watch_s: float = 10.0
     quota_slack_mib: int = 256
     dmem_limits: str = "auto"            # quota/dmem.py: kernel dmem.max per pod cgroup when available | off
@@ -107,6 +109,7 @@ class SharedGPUManager:
         self._ledger_stop = threading.Event()
         self.watchdog = None
         self.dmem = None
+        self.enforcement = "off"             # effective HBM-share enforcement (see _enforcement)
         self._cgpu_disabled = False
 
     # ------------------------------------------------------------------------------------
@@ -199,7 +202,34 @@ class SharedGPUManager:
             return False, "device plugin not serving"
         if self.health is not None and not self.health.ready:
             return False, self.health.degraded
+        if self.enforcement in ("report", "off") and not self._cgpu_disabled and self.cfg.shim_host_dir:
+            return False, (f"HBM shares are not enforced on a tenant that drops the quota shim: no dmem cgroup "
+                           f"controller and the watchdog is in {self.enforcement!r} mode")
         return True, "ok"
+
+    def _enforcement(self) -> str:
+        """Effective enforcement of the HBM shares on non-cooperative tenants: "dmem" (kernel
+        limit per pod cgroup), "kill" (watchdog SIGKILL), "report" or "off". ``auto`` picks
+        kill when the kernel cannot limit; kill needs placement truth (pod-resources), because
+        without it a swapped admission leaves the annotations crossed and a pod inside its real
+        share would be killed — it is downgraded to report then."""
+        mode = self.cfg.quota_enforcement
+        dmem_on = self.dmem is not None and self.dmem.available()
+        podres = self.allocator is not None and self.allocator.podres is not None
+        if mode == "auto":
+            mode = "report" if dmem_on else "kill" if podres else "report"
+        elif mode == "kill" and not podres:
+            log.warning("--quota-enforcement=kill needs the kubelet pod-resources API (placement truth): without "
+                        "it pod annotations can be crossed after a swapped admission; reporting only")
+            mode = "report"
+        eff = "dmem" if dmem_on and mode != "off" else mode
+        for m in ("dmem", "kill", "report", "off"):
+            self.metrics.enforcement_mode.set(1 if m == eff else 0, mode=m)
+        if eff in ("report", "off") and self.cfg.shim_host_dir:
+            log.warning("HBM shares are enforced by the quota shim only (%s): a tenant that drops LD_PRELOAD is "
+                        "not limited", eff)
+        self.enforcement = eff
+        return mode
 
     def _pod_resources(self):
         from ..api.podresources import SOCKET, PodResourcesClient
@@ -242,14 +272,18 @@ class SharedGPUManager:
         from ..quota.watchdog import QuotaWatchdog
 
         cfg = self.cfg
-        if cfg.quota_enforcement == "off" or self.model is None or self.pod_source is None:
+        mode = self._enforcement()
+        if mode == "off" or self.model is None or self.pod_source is None:
             return
+        alloc = self.allocator
         if self.watchdog is None:
-            self.watchdog = QuotaWatchdog(self.model, self.pod_source, self.metrics, cfg.quota_enforcement,
+            self.watchdog = QuotaWatchdog(self.model, self.pod_source, self.metrics, mode,
                                           cfg.quota_watch_s, cfg.quota_slack_mib << 20,
-                                          disabled=lambda: self._cgpu_disabled).start()
+                                          disabled=lambda: self._cgpu_disabled,
+                                          view=alloc.view if alloc else None,
+                                          settled=alloc.settled if alloc else None).start()
         else:
-            self.watchdog.model, self.watchdog.pods = self.model, self.pod_source
+            self.watchdog.model, self.watchdog.pods, self.watchdog.mode = self.model, self.pod_source, mode
 
     def _start_dmem(self):
         """Kernel HBM limits (quota/dmem.py): applied before each container start and on the
@@ -374,8 +408,8 @@ class SharedGPUManager:
                         return 2
                     self._start_health()
                     self._start_ledger_collector()
-                    self._start_watchdog()
                     self._start_dmem()
+                    self._start_watchdog()
                     restart = False
                     self.started.set()
                 kind, val = self.events.get()

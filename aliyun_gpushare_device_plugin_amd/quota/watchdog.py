@@ -21,8 +21,15 @@ plus ``slack_bytes`` (runtime overhead the quota does not model). A violation is
 (``gpushare_quota_violation_bytes{pod_uid,gpu}``), logged, and — with ``mode="kill"`` — ended
 the way the kernel ends a cgroup over its memory limit: the pod's largest GPU process on that
 GPU is SIGKILLed, then the next, until the pod is back within its share. ``mode="report"``
-(default) only reports. Processes on a GPU that belong to no pod are exported as
+only reports. Processes on a GPU that belong to no pod are exported as
 ``gpushare_unaccounted_hbm_bytes{gpu}``.
+
+Kill mode acts only on a settled placement, so a pod that stays within its real share is never
+killed for a stale annotation: the pods are read through the allocator's view (placement
+fixes queued but not landed yet, ``view``), a pod whose answer or placement patch is still in
+flight is reported but not killed (``settled``), and a violation must be seen on
+``confirm_scans`` consecutive scans (the placement pass runs every 2 s while answers are in
+flight, the watchdog every 10 s) before the first SIGKILL.
 """
 from __future__ import annotations
 
@@ -129,9 +136,11 @@ class Violation:
 class QuotaWatchdog:
     def __init__(self, model, pods, metrics=None, mode: str = "report", period_s: float = 10.0,
                  slack_bytes: int = 256 << 20, proc: str = "/proc", kfd_proc: str = "/sys/class/kfd/kfd/proc",
-                 pid_pod=None, pids=None, disabled=lambda: False):
+                 pid_pod=None, pids=None, disabled=lambda: False, view=None, settled=None,
+                 confirm_scans: int = 2):
         """``pods``: a PodSource (this node's pods). ``pid_pod`` / ``pids`` override the
-        cgroup lookup / process discovery (tests, the simulator)."""
+        cgroup lookup / process discovery (tests, the simulator). ``view(pods)`` /
+        ``settled(uid)``: the allocator's annotation overlay and in-flight test (see above)."""
         if mode not in ("off", "report", "kill"):
             raise ValueError(f"quota enforcement mode {mode!r}")
         self.model, self.pods, self.metrics = model, pods, metrics
@@ -140,6 +149,10 @@ class QuotaWatchdog:
         self.pid_pod = pid_pod or (lambda pid: pod_of_pid(pid, self.proc))
         self.pids = pids or (lambda: gpu_pids(self.proc, self.kfd_proc))
         self.disabled = disabled          # node label cgpu.disable.isolation=true
+        self.view = view or (lambda pods: pods)
+        self.settled = settled or (lambda uid: True)
+        self.confirm_scans = max(1, confirm_scans)
+        self._strikes: dict[tuple[str, int], int] = {}   # (pod uid, gpu) -> consecutive violating scans
         self.violations_total = 0
         self._stop = threading.Event()
         self._thread = None
@@ -160,7 +173,7 @@ class QuotaWatchdog:
         if self.mode == "off" or self.disabled():
             return []
         by_bdf = self._gpu_of_bdf()
-        pods = {O.uid(p): p for p in self.pods.node_pods()}
+        pods = {O.uid(p): p for p in self.view(self.pods.node_pods())}
         usage: dict[tuple[str, int], list] = {}
         unaccounted: dict[int, int] = {}
         seen: set[str] = set()           # a DRM client inherited across fork is counted once
@@ -189,6 +202,7 @@ class QuotaWatchdog:
                 self.metrics.pod_hbm_used.set(sum(n for _, n in procs), pod_uid=uid, gpu=str(gi))
             for g in self.model.gpus:
                 self.metrics.unaccounted_hbm.set(unaccounted.get(g.index, 0), gpu=str(g.index))
+        strikes: dict[tuple[str, int], int] = {}
         for (uid, gi), procs in usage.items():
             pod = pods[uid]
             if O.gpu_mem_of_pod(pod) <= 0:
@@ -200,13 +214,17 @@ class QuotaWatchdog:
             procs.sort(key=lambda x: -x[1])
             v = Violation(uid, O.name(pod), gi, used, allowed, procs)
             self.violations_total += 1
+            strikes[(uid, gi)] = n_seen = self._strikes.get((uid, gi), 0) + 1
             if self.metrics is not None:
                 self.metrics.quota_violation.set(used - allowed, pod_uid=uid, gpu=str(gi))
                 self.metrics.quota_violations_total.inc()
+            act = self.mode == "kill" and n_seen >= self.confirm_scans and self.settled(uid)
             log.warning("quota violation: pod %s/%s holds %.2f GiB on GPU %d, its share is %.2f GiB (%s)",
                         O.namespace(pod), O.name(pod), used / (1 << 30), gi, allowed / (1 << 30),
-                        "killing its largest process" if self.mode == "kill" else "report only")
-            if self.mode == "kill":
+                        "killing its largest process" if act else
+                        "report only" if self.mode != "kill" else
+                        f"seen {n_seen}/{self.confirm_scans} scans" if self.settled(uid) else "placement in flight")
+            if act:
                 left = used
                 for pid, n in procs:
                     if left <= allowed + self.slack:
@@ -220,6 +238,7 @@ class QuotaWatchdog:
                     except OSError as e:
                         log.warning("quota enforcement: cannot kill pid %d: %s", pid, e)
             out.append(v)
+        self._strikes = strikes
         return out
 
     def start(self) -> "QuotaWatchdog":

@@ -206,6 +206,9 @@ class PluginMetrics:
         self.quota_kills = r.counter("gpushare_quota_kills_total", "Processes killed by the quota watchdog")
         self.unaccounted_hbm = r.gauge("gpushare_unaccounted_hbm_bytes",
                                        "HBM held on a GPU by processes of no pod on this node")
+        self.enforcement_mode = r.gauge("gpushare_enforcement_mode",
+                                        "1 on the effective HBM-share enforcement for tenants without the shim: "
+                                        "dmem (kernel limit), kill (watchdog), report or off")
         self.dmem_limited_pods = r.gauge("gpushare_dmem_limited_pods",
                                          "Shared pods whose HBM share is a kernel dmem.max limit on their cgroup")
         self.cu_slots_held = r.gauge("gpushare_cu_slots_held",

@@ -431,3 +431,59 @@ def test_cdi_device_names():
     al2, _, _ = make([mkpod("p", 2, 0, 10)], cdi_kind="amd.com/gpu", expose_devices=False)
     r2 = al2.allocate(req(2)).container_responses[0]
     assert [c.name for c in r2.cdi_devices] == ["amd.com/gpu=0"] and len(r2.devices) == 0
+
+
+class VersionedSource(StaticSource):
+    """A StaticSource with the watch cache's change signal (enables the fast path)."""
+
+    def __init__(self, pods):
+        super().__init__(pods)
+        self.version = 1
+        self.changed = threading.Event()
+
+
+def test_fast_path_retry_before_bookkeeping_replays():
+    """a fast-path answer is indexed for replay off the hot path. A kubelet retry of
+    the same fake-ID set that arrives before that bookkeeping must still replay the answer, not
+    take the next candidate's reservation (one pod matched twice)."""
+    model = DeviceModel([gpu(i, 4 << 30) for i in range(2)], const.GIB)
+    src = VersionedSource([mkpod("a", 2, 1, 10), mkpod("b", 2, 0, 20)])
+    al = Allocator(model, src, FakeClient(src), NODE, AllocatorOptions(async_patch=True))
+    try:
+        held = []
+        al._patch_q = type("Q", (), {"put": lambda self, j: held.append(j)})()   # patcher never drains
+        al._prepare(src)
+        assert al._fast is not None
+        r = req(2)
+        first = al.allocate(r)
+        assert al.metrics.allocate_latency.count(phase="fast") == 1 and al._post     # not indexed yet
+        again = al.allocate(r)
+        assert dict(again.container_responses[0].envs) == dict(first.container_responses[0].envs)
+        assert dict(first.container_responses[0].envs)[const.ENV_RESOURCE_INDEX] == "1"
+        assert al.metrics.allocate_outcomes.value(outcome="replay") == 1
+        # b is still free for its own admission
+        assert dict(al.allocate(req(2)).container_responses[0].envs)[const.ENV_RESOURCE_INDEX] == "0"
+    finally:
+        al.close()
+
+
+def test_prepare_discards_answers_built_before_a_reconfigure():
+    """a _prepare that raced a reconfigure must not install answers built from the
+    old device model."""
+    model = DeviceModel([gpu(i, 4 << 30) for i in range(2)], const.GIB)
+    src = VersionedSource([mkpod("a", 2, 1, 10)])
+    al = Allocator(model, src, FakeClient(src), NODE, AllocatorOptions(async_patch=True))
+    try:
+        orig = al._candidates
+
+        def racing(fresh):
+            out = orig(fresh)
+            al._gen += 1                  # a reconfigure lands while answers are being built
+            return out
+        al._candidates = racing
+        al._fast = None
+        al._prep_cache.clear()
+        al._prepare(src)
+        assert al._fast is None and not al._prep_cache
+    finally:
+        al.close()

@@ -102,7 +102,10 @@ def test_daemonset_mounts_match_the_flags():
         assert p.startswith("/var/lib/gpushare/")
     assert spec.get("hostNetwork") is True and spec["nodeSelector"] == {"gpushare": "true"}
     # the quota watchdog reads every GPU process's DRM fdinfo and pod cgroup
-    assert spec.get("hostPID") is True and cfg.quota_enforcement in ("report", "kill")
+    assert spec.get("hostPID") is True
+    # round-3 review item 4: non-cooperative tenants are enforced by default — kill where the
+    # kernel has no dmem controller (the pod-resources mount above is what kill mode needs)
+    assert cfg.quota_enforcement in ("auto", "kill")
     # kernel dmem limits write the HOST cgroup hierarchy (the container's own is namespaced)
     assert cfg.dmem_limits == "auto" and cfg.cgroup_root in mounts and not mounts[cfg.cgroup_root].get("readOnly")
     assert vols[mounts[cfg.cgroup_root]["name"]]["hostPath"]["path"] == "/sys/fs/cgroup"

@@ -158,3 +158,38 @@ def test_mapped_journal_reload_and_compaction(tmp_path):
     req = api.AllocateRequest(container_requests=[api.ContainerAllocateRequest(devices_ids=["d7"])])
     uid, got = j2.lookup(req)
     assert uid == "u7" and got().container_responses[0].envs["ALIYUN_COM_GPU_MEM_IDX"] == "1"
+
+
+def test_prefault_survives_a_concurrent_compaction(tmp_path):
+    """prefault (patcher thread) and a compaction (gRPC thread, journal full) used to
+    race on the mapping: prefault raised ValueError('mmap closed') and killed the patcher."""
+    import threading
+
+    from aliyun_gpushare_device_plugin_amd.alloc.journal import AllocJournal
+    from aliyun_gpushare_device_plugin_amd.api import v1beta1 as api
+
+    j = AllocJournal(str(tmp_path / "j.jsonl"), map_bytes=64 << 10)
+    resp = api.AllocateResponse()
+    resp.container_responses.add(envs={"K": "v" * 200})
+    stop = threading.Event()
+    errors = []
+
+    def prefaulter():
+        while not stop.is_set():
+            try:
+                j.prefault(ahead=64 << 10)
+            except Exception as e:  # noqa: BLE001
+                errors.append(e)
+                return
+
+    t = threading.Thread(target=prefaulter)
+    t.start()
+    try:
+        for i in range(3000):             # ~1 KB records into a 64 KiB map: many compactions
+            r = api.AllocateRequest(container_requests=[api.ContainerAllocateRequest(devices_ids=[f"d{i}"])])
+            j.record(r, f"uid-{i % 50}", resp)
+    finally:
+        stop.set()
+        t.join()
+    assert errors == []
+    j.close()

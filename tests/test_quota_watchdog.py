@@ -76,6 +76,8 @@ def test_kill_mode_ends_the_largest_process(tmp_path):
         wd, m = _setup(tmp_path, 5 * GIB, mode="kill")
         os.rename(tmp_path / "proc" / "100", tmp_path / "proc" / str(victim.pid))
         wd.pids = lambda: {victim.pid, 200, 300}
+        v = wd.scan()                          # first sighting: confirmed on the next scan
+        assert v[0].killed == [] and victim.poll() is None
         v = wd.scan()
         assert v[0].killed == [victim.pid] and m.quota_kills.value() == 1
         victim.wait(timeout=5)
@@ -94,3 +96,33 @@ def test_cgpu_disable_label_turns_it_off(tmp_path):
 def test_bad_mode_rejected():
     with pytest.raises(ValueError):
         W.QuotaWatchdog(None, None, mode="evict")
+
+
+def test_kill_mode_spares_a_pod_whose_placement_is_not_settled(tmp_path):
+    """after a swapped equal-size admission the pod annotations are crossed until the
+    placement patch lands. Kill mode reads the allocator's overlay (the truth already decided)
+    and never kills a pod whose placement is still in flight."""
+    victim = subprocess.Popen(["sleep", "30"])
+    try:
+        wd, m = _setup(tmp_path, 5 * GIB, mode="kill")
+        os.rename(tmp_path / "proc" / "100", tmp_path / "proc" / str(victim.pid))
+        wd.pids = lambda: {victim.pid, 200, 300}
+        # pod a really holds an 8 GiB reservation on GPU 1 (the annotations still say 4 GiB):
+        # the overlay of the queued placement fix makes the share right, so no violation at all
+        wd.view = lambda pods: [p if p["metadata"]["uid"] != UID_A else
+                                dict(p, spec={"containers": [{"name": "c", "resources": {"limits": {
+                                    const.RESOURCE_NAME: "8"}}}]}) for p in pods]
+        assert wd.scan() == [] and wd.scan() == []
+        # a pod whose answer / placement patch is still in flight is reported, never killed
+        wd.view = lambda pods: pods
+        wd.settled = lambda uid: uid != UID_A
+        for _ in range(3):
+            v = wd.scan()
+            assert len(v) == 1 and v[0].killed == []
+        assert victim.poll() is None and m.quota_kills.value() == 0
+        wd.settled = lambda uid: True          # settled and still over: killed
+        assert wd.scan()[0].killed == [victim.pid]
+        victim.wait(timeout=5)
+    finally:
+        if victim.poll() is None:
+            victim.kill()
