@@ -21,6 +21,16 @@ replug / back     Healthy, present=True
 ECC UE increase   Unhealthy until a reset
 xGMI link down    topology re-export (device stays Healthy)
 ================  ==============================================================
+
+Recovery never depends on one event arriving (the reference's "no way to recover",
+``server.go:188``; one lost POST_RESET would strand a whole 288 GiB GPU). The poll also ends
+a mark when it sees the reset itself:
+
+* "GPU reset in progress" (a pre-reset without its post-reset): Healthy again once the GPU is
+  present and answering SMI on ``settle_polls`` consecutive polls;
+* an ECC uncorrectable-error mark clears on an *observed* reset: a pre-reset event (then as
+  above), the GPU leaving and re-joining the enumeration, or its UE counters going backwards
+  (a reset cleared them) — the UE baseline restarts from the value read then.
 """
 from __future__ import annotations
 
@@ -34,9 +44,15 @@ from .model import DeviceModel
 
 class HealthMonitor:
     def __init__(self, smi: S.SMI, model: DeviceModel, poll_interval: float = 5.0,
-                 on_change=None, on_topology_change=None, on_sample=None):
+                 on_change=None, on_topology_change=None, on_sample=None, settle_polls: int = 2):
         self.smi, self.model = smi, model
         self.poll_interval = poll_interval
+        self.settle_polls = max(1, settle_polls)
+        # uuid -> "reset" (pre-reset seen, waiting for post-reset or settle_polls good polls,
+        # counted in _settle) | "gone" (left the enumeration: its return is a reset)
+        self._marks: dict[str, str] = {}
+        self._settle: dict[str, int] = {}
+        self._ecc_last: dict[str, int] = {}      # uuid -> UE count at the previous poll
         self.on_change = on_change
         self.on_topology_change = on_topology_change
         # on_sample(model_index, smi_device) after every poll: per-GPU HBM used for the
@@ -124,11 +140,17 @@ class HealthMonitor:
             return
         targets = range(self.model.count()) if ev.index < 0 else [self._model_index_of_smi(ev.index)]
         for idx in targets:
+            g = self.model.gpu(idx)
             if k == S.EV_PRE_RESET:
+                if g is not None:
+                    with self._lock:
+                        self._marks[g.uuid] = "reset"
+                        self._settle[g.uuid] = 0
                 self._set(idx, False, "GPU reset in progress")
             elif k == S.EV_POST_RESET:
-                g = self.model.gpu(idx)
                 if g is not None:
+                    with self._lock:
+                        self._marks.pop(g.uuid, None)
                     self._ecc_baseline[g.uuid] = self._current_ecc(g.uuid, self._ecc_baseline.get(g.uuid, 0))
                     if g.present:
                         self._set(idx, True, "recovered after reset")
@@ -162,14 +184,43 @@ class HealthMonitor:
             return
         for g in self.model.gpus:
             d = present.get(g.uuid)
+            with self._lock:
+                if d is None:
+                    self._marks[g.uuid] = "gone"
+                    self._settle.pop(g.uuid, None)
+                    mark, settled = "gone", 0
+                else:
+                    mark = self._marks.get(g.uuid)
+                    settled = self._settle.get(g.uuid, 0) + 1 if mark == "reset" else 0
+                    if mark == "reset":
+                        self._settle[g.uuid] = settled
             if d is None:
                 self._set(g.index, False, "device missing", present=False)
                 continue
             if self.on_sample is not None:
                 self.on_sample(g.index, d)
             base = self._ecc_baseline.setdefault(g.uuid, d.ecc_ue)
+            last = self._ecc_last.get(g.uuid, d.ecc_ue)
+            self._ecc_last[g.uuid] = d.ecc_ue
+            why = None
+            if d.ecc_ue < last:
+                why = f"uncorrectable ECC counters went back ({last}->{d.ecc_ue}): reset observed"
+            elif mark == "gone":
+                why = "device back"
+            elif mark == "reset" and settled >= self.settle_polls:
+                why = f"answering SMI on {settled} polls after a reset (post-reset event not seen)"
+            if why is not None:
+                # an observed reset: the UE baseline restarts from what the GPU reports now
+                with self._lock:
+                    self._marks.pop(g.uuid, None)
+                    self._settle.pop(g.uuid, None)
+                self._ecc_baseline[g.uuid] = base = d.ecc_ue
             if d.ecc_ue > base:
                 self._set(g.index, False, f"uncorrectable ECC errors {base}->{d.ecc_ue}", present=True)
+            elif why is not None:
+                self._set(g.index, True, why, present=True)
+            elif mark is None and not g.healthy and g.reason.startswith("uncorrectable ECC"):
+                pass                      # stays marked until a reset is observed
             elif not g.present:
                 self._set(g.index, True, "device back", present=True)
 

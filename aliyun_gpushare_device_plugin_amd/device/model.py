@@ -200,6 +200,7 @@ class DeviceModel:
             g = self.gpus[index]
             new_present = g.present if present is None else present
             if g.healthy == healthy and g.present == new_present:
+                g.reason = reason or g.reason   # e.g. an ECC mark now waiting for its reset
                 return False
             g.healthy, g.present, g.reason = healthy, new_present, reason
             self._devs_cache = None

@@ -946,6 +946,10 @@ class FakeBackend : public Backend {
     } else if (op == "reset") {
       push(a, GS_EV_PRE_RESET, "GPU pre-reset");
       push(a, GS_EV_POST_RESET, "GPU post-reset");
+    } else if (op == "prereset") {  // a reset whose post-reset event is lost
+      push(a, GS_EV_PRE_RESET, "GPU pre-reset");
+    } else if (op == "silentreset") {  // a completed reset with no event at all: counters cleared
+      all_[a].ecc_ue = 0;
     } else if (op == "ecc") {
       all_[a].ecc_ue += (uint64_t)(b > 0 ? b : 1);
       push(a, GS_EV_ECC_UE, "uncorrectable ECC error");

@@ -156,3 +156,48 @@ def test_unarmed_events_make_the_plugin_not_ready():
                 assert e.code == 503 and b"armed on 0/2" in e.read()
         finally:
             srv.shutdown()
+
+
+def test_lost_post_reset_recovers_by_polling():
+    """Round-3 review item 5: a pre-reset whose post-reset event never arrives used to strand
+    the GPU Unhealthy. The poll returns it to Healthy once it answers SMI on settle_polls (2)
+    consecutive polls, and ListAndWatch re-sends both transitions."""
+    with SimCluster([("n", "fake:2x4G")], health_poll_s=0.2) as c:
+        mgr, kl = c.manager("n"), c.nodes["n"].kubelet
+        sends = kl.list_updates
+        mgr.smi.inject("prereset 1")
+        assert wait(lambda: health_by_gpu(kl, mgr.model)[1] == const.UNHEALTHY)
+        t0 = time.time()
+        assert wait(lambda: health_by_gpu(kl, mgr.model)[1] == const.HEALTHY, timeout=5.0)
+        assert time.time() - t0 <= 3 * 0.2 + 0.5        # within settle_polls (+1) poll intervals
+        assert "post-reset event not seen" in mgr.model.gpu(1).reason
+        assert kl.list_updates >= sends + 2
+        assert health_by_gpu(kl, mgr.model)[0] == const.HEALTHY
+
+
+def test_ecc_mark_clears_on_a_silent_reset():
+    """An ECC uncorrectable-error mark followed by a reset that emits no event at all: the UE
+    counters going backwards is the observed reset; the GPU returns and a later UE marks it again."""
+    with SimCluster([("n", "fake:2x4G")], health_poll_s=0.2) as c:
+        mgr, kl = c.manager("n"), c.nodes["n"].kubelet
+        mgr.smi.inject("ecc 0 2")
+        assert wait(lambda: health_by_gpu(kl, mgr.model)[0] == const.UNHEALTHY)
+        time.sleep(0.5)                                 # stays marked across polls
+        assert health_by_gpu(kl, mgr.model)[0] == const.UNHEALTHY
+        mgr.smi.inject("silentreset 0")
+        assert wait(lambda: health_by_gpu(kl, mgr.model)[0] == const.HEALTHY, timeout=3.0)
+        assert "reset observed" in mgr.model.gpu(0).reason
+        mgr.smi.inject("ecc 0 1")                       # a new UE after the reset marks it again
+        assert wait(lambda: health_by_gpu(kl, mgr.model)[0] == const.UNHEALTHY)
+
+
+def test_ecc_mark_clears_on_a_pre_reset_without_post_reset():
+    with SimCluster([("n", "fake:2x4G")], health_poll_s=0.2) as c:
+        mgr, kl = c.manager("n"), c.nodes["n"].kubelet
+        mgr.smi.inject("ecc 1 3")
+        assert wait(lambda: health_by_gpu(kl, mgr.model)[1] == const.UNHEALTHY)
+        mgr.smi.inject("prereset 1")                   # the UE counter is NOT cleared here
+        assert wait(lambda: "reset in progress" in mgr.model.gpu(1).reason)
+        assert wait(lambda: health_by_gpu(kl, mgr.model)[1] == const.HEALTHY, timeout=3.0)
+        time.sleep(0.6)                                 # re-baselined: the old UEs do not re-mark it
+        assert health_by_gpu(kl, mgr.model)[1] == const.HEALTHY
