@@ -117,8 +117,12 @@ class AllocatorOptions:
     # prepared answers for the common admission (see module docstring); write-behind only
     fast_path: bool = True
     # admission identity from the kubelet's pod-resources List when the request's size is
-    # ambiguous or a multi-container admission is in progress (see _identify)
+    # ambiguous or a multi-container admission is in progress (see _identify). The List runs
+    # outside the engine lock with this timeout; after a timeout or error identity is skipped
+    # (size matching) for identify_backoff_s
     identify: bool = True
+    identify_timeout_s: float = 0.2
+    identify_backoff_s: float = 5.0
 
 
 @dataclasses.dataclass
@@ -186,6 +190,9 @@ class Allocator:
         self._place_thread = None
         self._last_grant = 0.0
         self._placed_at = 0.0                     # start of the last completed placement pass
+        self._answer_seq = 0                      # answers given (invalidates the identity List)
+        self._ident_cache = None                  # (monotonic, answer_seq, pod-resources List)
+        self._ident_off_until = 0.0
         # fast path: prepared answers, engine-state generation, answers awaiting bookkeeping
         self._fast: _Fast | None = None
         self._gen = 0
@@ -330,7 +337,7 @@ class Allocator:
             return "gone"
         return "stale" if now - c.t > self.opts.partial_claim_ttl_s else "live"
 
-    def _match(self, sizes: tuple, fresh: bool) -> tuple[_Claim | None, bool]:
+    def _match(self, sizes: tuple, fresh: bool, held=None) -> tuple[_Claim | None, bool]:
         """Returns (claim, complete). ``complete`` = every gpu container of the pod is now
         allocated, so the pod must be PATCHed ASSIGNED.
 
@@ -345,9 +352,8 @@ class Allocator:
         k = len(sizes)
         now = time.monotonic()
         cands = self._candidates(fresh)
-        if self.podres is not None and self.opts.identify and (
-                self._partial is not None or self._ambiguous(cands, sizes)):
-            ident = self._identify(cands, sizes)
+        if held is not None and (self._partial is not None or self._ambiguous(cands, sizes)):
+            ident = self._identify(cands, sizes, held)
             if ident is not None:
                 return self._match_identified(ident, sizes, now)
         c = self._partial
@@ -433,17 +439,45 @@ class Allocator:
                     return True
         return False
 
-    def _identify(self, cands: list[dict], sizes: tuple) -> tuple[dict, int] | None:
+    def _identity_list(self, sizes: tuple):
+        """The kubelet's pod-resources List for admission identity (``_identify``), or None.
+        Fetched only when the request is ambiguous, and never under the engine lock: a slow or
+        rate-limited kubelet must not stall every Allocate of the node (the reference's global
+        lock, quirk 7). Short timeout; after a failure identity is off for a while (size
+        matching decides, placement truth repairs a swap afterwards). One List serves a
+        retried or concurrent request until the next answer is given."""
+        src = self.podres
+        if src is None or not self.opts.identify or time.monotonic() < self._ident_off_until:
+            return None
+        with self._mu:
+            need = self._partial is not None or self._ambiguous(self._candidates(False), sizes)
+            seq = self._answer_seq
+        if not need:
+            return None
+        c = self._ident_cache
+        if c is not None and c[1] == seq and time.monotonic() - c[0] < 0.5:
+            return c[2]
+        t = time.monotonic()
+        try:
+            try:
+                held = src.list(include_empty=True, timeout=self.opts.identify_timeout_s)
+            except TypeError:                     # a pod-resources view without a timeout argument
+                held = src.list(include_empty=True)
+        except Exception as e:  # noqa: BLE001 - kubelet restarting or overloaded
+            self._ident_off_until = time.monotonic() + self.opts.identify_backoff_s
+            self.metrics.allocate_outcomes.inc(outcome="identity_unavailable")
+            log.warning("admission identity unavailable (%s): size matching for %.0f s", e,
+                        self.opts.identify_backoff_s)
+            return None
+        self._ident_cache = (t, seq, held)
+        return held
+
+    def _identify(self, cands: list[dict], sizes: tuple, held) -> tuple[dict, int] | None:
         """Admission identity: the kubelet adds a pod to its pod manager right before admitting
         it and checkpoints each container's fake IDs as soon as that container's Allocate
-        returns, so in the pod-resources List the pod being admitted is the one Pending pod
-        of this node whose gpu containers do not all hold IDs yet. Returns (pod, number of its
-        gpu containers already allocated), or None when that is not exactly one pod."""
-        try:
-            held = self.podres.list(include_empty=True)
-        except Exception as e:  # noqa: BLE001 - kubelet restarting: fall back to the heuristic
-            log.V(2).info("admission identity unavailable: %s", e)
-            return None
+        returns, so in the pod-resources List (``held``) the pod being admitted is the one
+        Pending pod of this node whose gpu containers do not all hold IDs yet. Returns (pod,
+        number of its gpu containers already allocated), or None when that is not exactly one pod."""
         pending = {(O.namespace(p), O.name(p)): p for p in self._view(A.dedupe_by_uid(
             self.pods.pending_pods(fresh=False), self.node))}
         for p in cands:
@@ -691,6 +725,7 @@ class Allocator:
 
     def _take(self, c: "_Prepared") -> "_Prepared":
         """Claim a prepared candidate (caller holds ``_mu``)."""
+        self._answer_seq += 1
         self._assigned[c.uid] = time.monotonic()
         self._unpatched.add(c.uid)
         self._revoked.discard(c.uid)
@@ -776,20 +811,23 @@ class Allocator:
             return replay
         ta = time.perf_counter()
         try:
+            held = self._identity_list(sizes)          # outside the lock (kubelet RPC)
+            tl = time.perf_counter()
             with self._mu:
                 tb = time.perf_counter()
-                claim, complete = self._match(sizes, fresh=False)
+                claim, complete = self._match(sizes, fresh=False, held=held)
                 t1 = time.perf_counter()
                 if claim is None:
                     # watch lag: the kubelet may see a bind before our cache does
-                    claim, complete = self._match(sizes, fresh=True)
+                    claim, complete = self._match(sizes, fresh=True, held=held)
                 if claim is not None:
                     self._revoked.discard(claim.uid)
                     if complete:
                         self._claims[claim.uid] = claim   # held across the PATCH
                 t2 = time.perf_counter()
             hist.observe(ta - t0, phase="prelude")      # request key, journal replay check
-            hist.observe(tb - ta, phase="lock")
+            hist.observe(tl - ta, phase="identity")     # pod-resources List (ambiguous requests only)
+            hist.observe(tb - tl, phase="lock")
             hist.observe(t1 - tb, phase="lookup")
             hist.observe(t2 - t1, phase="decide")
         except Exception as e:  # noqa: BLE001 - pod listing failures
@@ -888,6 +926,7 @@ class Allocator:
                         ledger=cresp.annotations.get(const.CTR_ANNOTATION_LEDGER, ""))
 
     def _record_grants(self, req, resp, uid: str, jkey: str) -> None:
+        self._answer_seq += 1
         self._last_grant = time.monotonic()
         t = time.time()
         crs = req.container_requests

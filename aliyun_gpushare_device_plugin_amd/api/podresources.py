@@ -119,11 +119,11 @@ class PodResourcesClient:
             self._stub = PROTO.stub(self._ch, "PodResourcesLister")
         return self._stub
 
-    def list(self, include_empty: bool = False) -> list[PodDevices]:
+    def list(self, include_empty: bool = False, timeout: float | None = None) -> list[PodDevices]:
         import grpc
 
         try:
-            resp = self._connect().List(ListPodResourcesRequest(), timeout=self.timeout)
+            resp = self._connect().List(ListPodResourcesRequest(), timeout=timeout or self.timeout)
         except grpc.RpcError:
             self.close()        # the kubelet restarted: re-dial on the next call
             raise

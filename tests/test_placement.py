@@ -290,3 +290,68 @@ def test_admissions_deletions_replacements_never_overcommit(ngpu, identify, data
             phys.pop(p["metadata"]["uid"], None)
             kl.held.pop(p["metadata"]["uid"], None)
         src.pods = [p for p in src.pods if p["status"]["phase"] in ("Pending", "Running")]
+
+
+class SlowKubelet(Kubelet):
+    """A pod-resources server that answers after ``delay`` seconds (hung: a long delay)."""
+
+    def __init__(self, delay):
+        super().__init__()
+        self.delay = delay
+        self.calls = 0
+
+    def list(self, include_empty=False, timeout=None):
+        self.calls += 1
+        if timeout is not None and self.delay > timeout:
+            time.sleep(timeout)
+            raise TimeoutError("deadline exceeded")
+        time.sleep(self.delay)
+        return super().list(include_empty)
+
+
+def test_hung_pod_resources_never_stalls_allocate():
+    """Round-3 review item 6: the identity List ran under the engine lock with a 2 s timeout, so
+    a hung kubelet stalled every Allocate of the node. Now it runs outside the lock with a
+    200 ms timeout, and after a failure identity is skipped (size matching) for a while."""
+    now = time.time_ns()
+    pods = [mkpod(f"p{i}", 2, i % 2, now - 1000 * (10 - i)) for i in range(6)]
+    src, cl, al, _ = _engine(pods, 2, 8)
+    kl = SlowKubelet(30.0)
+    al.set_pod_resources(kl)
+    t0 = time.perf_counter()
+    assert kl.admit(al, pods[0]) is not None
+    first = time.perf_counter() - t0
+    assert first < 0.5 and kl.calls == 1
+    assert al.metrics.allocate_outcomes.value(outcome="identity_unavailable") == 1
+    t0 = time.perf_counter()
+    for p in pods[1:3]:
+        assert kl.admit(al, p) is not None
+    assert time.perf_counter() - t0 < 0.1 and kl.calls == 1       # backed off: no more waits
+
+
+def test_slow_pod_resources_does_not_serialize_allocates():
+    """Two Allocates of an ambiguous size with a slow (150 ms) but answering kubelet run their
+    Lists concurrently: the engine lock is not held across the RPC."""
+    import threading
+
+    now = time.time_ns()
+    pods = [mkpod(f"p{i}", 2, i % 2, now - 1000 * (10 - i)) for i in range(4)]
+    src, cl, al, _ = _engine(pods, 2, 8)
+    kl = SlowKubelet(0.15)
+    al.set_pod_resources(kl)
+    for p in pods[:2]:                        # both pods are being admitted (listed, no IDs yet)
+        kl.held[p["metadata"]["uid"]] = ("default", p["metadata"]["name"], [("c0", ())])
+    out = []
+
+    def one():
+        r = api.AllocateRequest()
+        r.container_requests.add().devices_ids.extend([f"x-{threading.get_ident()}-{i}" for i in range(2)])
+        out.append(dict(al.allocate(r).container_responses[0].envs)[const.ENV_RESOURCE_INDEX])
+    ts = [threading.Thread(target=one) for _ in range(2)]
+    t0 = time.perf_counter()
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert time.perf_counter() - t0 < 0.28, "Lists ran one after the other"
+    assert sorted(out) == ["0", "1"] and kl.calls == 2
