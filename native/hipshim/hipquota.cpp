@@ -35,14 +35,24 @@
 //
 // The render node is the second way to HBM: a container is handed /dev/dri/renderD<n> (for
 // libdrm / Mesa / video) and DRM_IOCTL_AMDGPU_GEM_CREATE with the VRAM domain allocates HBM
-// there, outside KFD. In kfd mode those buffer objects are charged too (per render-node fd and
-// GEM handle) and released on DRM_IOCTL_GEM_CLOSE or when that fd is closed.
+// there, outside KFD. In kfd mode those buffer objects are charged too. GEM handles belong to
+// the DRM *file* (one open file description, shared by dup'ed and inherited fds), not to an
+// fd number, so charges are keyed by the file's DRM client id (amdgpu fdinfo
+// "drm-client-id") and a handle: DRM_IOCTL_GEM_CLOSE on any fd of that file releases one;
+// closing an fd releases the file's charges only when no fd of any process this shim can see
+// (/proc: the container's processes) still refers to that client — otherwise the client
+// lingers and is re-checked when another fd of it closes and before any denial. A charged
+// VRAM handle cannot be exported as a dma-buf (DRM_IOCTL_PRIME_HANDLE_TO_FD fails with EACCES),
+// because the dma-buf would keep the HBM alive after GEM_CLOSE; GPUSHARE_SHIM_PRIME=keep
+// allows the export and keeps the handle charged until its DRM file is gone.
 //
 // Limits (documented, by construction): enforcement is cooperative — a process that drops
 // LD_PRELOAD or issues the ioctl through a raw syscall is not charged. Memory imported from
 // another process (dma-buf / IPC) is charged to its exporter only. KFD allocations issued
 // while the shim itself is initialising (the runtime's own start-up, reached from init) pass
-// uncharged.
+// uncharged. A GEM buffer still CPU-mapped after its GEM_CLOSE (the mapping holds it), and a
+// DRM file held only by a process the shim cannot read in /proc, are not followed; the node's
+// quota watchdog (amdgpu fdinfo / VRAM usage, quota/watchdog.py) is the backstop there.
 //
 // The library does not link libamdhip64 or libhsa-runtime64: the real entry points are
 // resolved at run time from whichever runtime the process loaded (PyTorch ships its own copy).
@@ -131,9 +141,20 @@ constexpr unsigned long kDrmGemCreate = drm_ioc(3, 0x40 + 0x00, sizeof(DrmGemCre
 constexpr unsigned long kDrmGemClose = drm_ioc(1, 0x09, sizeof(DrmGemClose));              // DRM_IOCTL_GEM_CLOSE
 constexpr uint64_t kAmdgpuDomainVram = 0x4;                                               // AMDGPU_GEM_DOMAIN_VRAM
 static_assert(sizeof(DrmGemCreateIn) == 32 && sizeof(DrmGemClose) == 8, "DRM uapi layout");
+struct DrmPrimeHandle {    // struct drm_prime_handle
+  uint32_t handle, flags;
+  int32_t fd;
+};
+constexpr unsigned long kDrmPrimeHandleToFd = drm_ioc(3, 0x2d, sizeof(DrmPrimeHandle));  // DRM_IOCTL_PRIME_HANDLE_TO_FD
+static_assert(sizeof(DrmPrimeHandle) == 12, "DRM uapi layout");
 constexpr int kMaxDrmFd = 4096;
-// table key of a GEM handle: bit 63 set (KFD handles are gpu_id << 32 | idr, bit 63 clear)
-inline uint64_t gem_key(int fd, uint32_t h) { return (1ull << 63) | ((uint64_t)(uint32_t)fd << 32) | h; }
+// Table key of a GEM handle: bit 63 set (KFD handles are gpu_id << 32 | idr, bit 63 clear),
+// bit 62 = kept after a dma-buf export (GEM_CLOSE does not release it), bits 32-61 = the DRM
+// client key (client id, or kFdClient | fd when the kernel reports none), bits 0-31 = handle.
+constexpr uint64_t kGemBit = 1ull << 63, kStickyBit = 1ull << 62;
+constexpr uint64_t kClientMask = (1ull << 30) - 1, kFdClient = 1ull << 29;
+inline uint64_t gem_key(uint64_t client, uint32_t h) { return kGemBit | (client & kClientMask) << 32 | h; }
+inline uint64_t client_of_key(uint64_t k) { return k >> 32 & kClientMask; }
 
 struct Slot {
   std::atomic<int32_t> pid;
@@ -172,7 +193,14 @@ pthread_once_t g_once = PTHREAD_ONCE_INIT;
 // HIP call the shim makes) must not wait on the once-control held by that same init
 std::atomic<bool> g_initializing{false};
 std::atomic<int> g_env_mode{-1};          // GPUSHARE_SHIM_MODE read without initialising
-std::atomic<uint8_t> g_drm_fd[kMaxDrmFd];  // 1 = this fd holds charged GEM handles
+std::atomic<uint64_t> g_drm_client[kMaxDrmFd];  // fd -> its DRM client key + 1 (0: no charged GEM handles)
+std::atomic<int> g_gem_live{0};                  // charged GEM handles in this process (fast path skip)
+struct Lingering {                               // clients whose charged fd closed while still referred to
+  pthread_mutex_t mu = PTHREAD_MUTEX_INITIALIZER;
+  uint64_t client[64];
+  int n = 0;
+};
+Lingering g_linger;
 std::atomic<bool> g_released{false};  // set by the atexit handler (see release_slot_at_exit)
 thread_local int t_depth = 0;  // re-entrancy guard (HIP calling itself through the PLT)
 
@@ -406,12 +434,14 @@ void diag_check(LedgerShm* L) {
   abort();
 }
 
+int linger_gc();
+
 bool charge(uint64_t bytes) {
   if (g_released.load(std::memory_order_relaxed)) return true;  // process teardown
   LedgerShm* L = g.ledger;
   if (g.diag) diag_check(L);
   uint64_t quota = g.quota.load(std::memory_order_relaxed);
-  bool reclaimed = false;
+  bool reclaimed = false, gced = false;
   uint64_t cur = L->total.load();
   for (;;) {
     if (quota && cur + bytes > quota) {
@@ -419,6 +449,13 @@ bool charge(uint64_t bytes) {
         reclaimed = true;
         cur = L->total.load();
         continue;
+      }
+      if (!gced) {  // GEM files that were still referred to when their fd closed may be gone now
+        gced = true;
+        if (linger_gc() > 0) {
+          cur = L->total.load();
+          continue;
+        }
       }
       L->denied.fetch_add(1);
       return false;
@@ -542,7 +579,10 @@ void atfork_child() {
       sl.used.store(0);
     }
   }
-  for (auto& fl : g_drm_fd) fl.store(0, std::memory_order_relaxed);   // the parent's GEM handles are the parent's
+  for (auto& fl : g_drm_client) fl.store(0, std::memory_order_relaxed);   // the parent's GEM handles are the parent's
+  g_gem_live.store(0);
+  pthread_mutex_init(&g_linger.mu, nullptr);
+  g_linger.n = 0;
   g.slot = acquire_slot(g.ledger);
 }
 
@@ -723,6 +763,133 @@ int kfd_alloc(ioctl_t f, int fd, unsigned long req, KfdAllocArgs* a) {
 }
 
 // ---- render node (amdgpu GEM) ---------------------------------------------------------------
+// /proc, or GPUSHARE_SHIM_PROC_ROOT (tests: a synthetic tree of <pid>/fd and <pid>/fdinfo)
+const char* proc_root() {
+  static const char* r = nullptr;
+  if (!r) {
+    const char* v = getenv("GPUSHARE_SHIM_PROC_ROOT");
+    r = (v && *v) ? v : "/proc";
+  }
+  return r;
+}
+
+// "drm-client-id" of <root>/<pid>/fdinfo/<fd> (0 = none: not a DRM file, or an old kernel).
+uint64_t read_client_id(const char* path) {
+  int f = open(path, O_RDONLY | O_CLOEXEC);
+  if (f < 0) return 0;
+  char buf[2048];
+  ssize_t n = read(f, buf, sizeof buf - 1);
+  syscall(SYS_close, f);  // not through the interposed close (it may call back in here)
+  if (n <= 0) return 0;
+  buf[n] = 0;
+  const char* p = strstr(buf, "drm-client-id:");
+  return p ? strtoull(p + 14, nullptr, 10) : 0;
+}
+
+// The DRM client key of this process's fd: the kernel's client id (shared by every fd of one
+// open file description), or kFdClient | fd when the kernel does not report one.
+uint64_t client_key_of(int fd) {
+  char path[96];
+  snprintf(path, sizeof path, "%s/%d/fdinfo/%d", proc_root(), (int)getpid(), fd);
+  uint64_t id = read_client_id(path);
+  return id ? (id & kClientMask & ~kFdClient) : (kFdClient | (uint64_t)fd);
+}
+
+// Does any fd of any process visible in /proc still refer to DRM client `key`?
+bool client_alive(uint64_t key) {
+  if (key & kFdClient) return false;  // no client ids on this kernel: the fd was the file
+  DIR* d = opendir(proc_root());
+  if (!d) return true;  // cannot tell: keep the charge
+  bool alive = false;
+  char path[160], link[64];
+  while (!alive) {
+    struct dirent* e = readdir(d);
+    if (!e) break;
+    if (e->d_name[0] < '0' || e->d_name[0] > '9') continue;
+    snprintf(path, sizeof path, "%s/%s/fd", proc_root(), e->d_name);
+    DIR* fds = opendir(path);
+    if (!fds) continue;  // exited, or not ours to read
+    while (!alive) {
+      struct dirent* f = readdir(fds);
+      if (!f) break;
+      if (f->d_name[0] < '0' || f->d_name[0] > '9') continue;
+      snprintf(path, sizeof path, "%s/%s/fd/%s", proc_root(), e->d_name, f->d_name);
+      ssize_t n = readlink(path, link, sizeof link - 1);
+      if (n <= 0) continue;
+      link[n] = 0;
+      if (strncmp(link, "/dev/dri/", 9) != 0) continue;
+      snprintf(path, sizeof path, "%s/%s/fdinfo/%s", proc_root(), e->d_name, f->d_name);
+      uint64_t id = read_client_id(path);
+      alive = id && (id & kClientMask & ~kFdClient) == key;
+    }
+    closedir(fds);
+  }
+  closedir(d);
+  return alive;
+}
+
+// Release every charged GEM handle (sticky ones included) of DRM client `key`.
+uint64_t release_client(uint64_t key) {
+  uint64_t freed = 0;
+  int handles = 0;
+  for (auto& s : g_shards) {
+    pthread_mutex_lock(&s.mu);
+    for (size_t i = 0; i < s.cap; ++i) {
+      uint64_t k = s.keys[i];
+      if (k != kEmpty && k != kDeleted && (k & kGemBit) && client_of_key(k) == key) {
+        freed += s.vals[i];
+        s.keys[i] = kDeleted;
+        ++handles;
+      }
+    }
+    pthread_mutex_unlock(&s.mu);
+  }
+  g_gem_live.fetch_sub(handles);
+  uncharge(freed);
+  logf(2, "DRM client %llu gone: %llu GEM bytes released", (unsigned long long)key, (unsigned long long)freed);
+  return freed;
+}
+
+void linger_add(uint64_t key) {
+  pthread_mutex_lock(&g_linger.mu);
+  bool have = false;
+  for (int i = 0; i < g_linger.n; ++i) have |= g_linger.client[i] == key;
+  if (!have && g_linger.n < 64) g_linger.client[g_linger.n++] = key;
+  pthread_mutex_unlock(&g_linger.mu);
+  if (!have) logf(1, "DRM client %llu still referred to after its fd closed: GEM charges kept", (unsigned long long)key);
+}
+
+// Re-check lingering clients; returns how many were released.
+bool linger_has(uint64_t key) {
+  pthread_mutex_lock(&g_linger.mu);
+  bool have = false;
+  for (int i = 0; i < g_linger.n; ++i) have |= g_linger.client[i] == key;
+  pthread_mutex_unlock(&g_linger.mu);
+  return have;
+}
+
+int linger_gc() {
+  pthread_mutex_lock(&g_linger.mu);
+  int n = g_linger.n, released = 0;
+  uint64_t keys[64];
+  memcpy(keys, g_linger.client, sizeof(uint64_t) * (size_t)n);
+  pthread_mutex_unlock(&g_linger.mu);
+  if (!n) return 0;
+  for (int i = 0; i < n; ++i) {
+    if (client_alive(keys[i])) continue;
+    release_client(keys[i]);
+    ++released;
+    pthread_mutex_lock(&g_linger.mu);
+    for (int j = 0; j < g_linger.n; ++j)
+      if (g_linger.client[j] == keys[i]) {
+        g_linger.client[j] = g_linger.client[--g_linger.n];
+        break;
+      }
+    pthread_mutex_unlock(&g_linger.mu);
+  }
+  return released;
+}
+
 int gem_create(ioctl_t f, int fd, unsigned long req, DrmGemCreateIn* a) {
   if (!(a->domains & kAmdgpuDomainVram) || fd < 0 || fd >= kMaxDrmFd) return f(fd, req, a);
   uint64_t c = round_up(a->bo_size, 4096);
@@ -745,29 +912,70 @@ int gem_create(ioctl_t f, int fd, unsigned long req, DrmGemCreateIn* a) {
     return r;
   }
   uint32_t h = reinterpret_cast<DrmGemClose*>(a)->handle;   // out.handle overlays bo_size
-  g_drm_fd[fd].store(1, std::memory_order_relaxed);
-  track(gem_key(fd, h), c);
-  logf(2, "gem create %llu bytes VRAM on fd %d -> handle %u, used %llu", (unsigned long long)c, fd, h,
-       (unsigned long long)g.ledger->total.load());
+  uint64_t key = client_key_of(fd);                          // read each time: fd numbers are reused
+  g_drm_client[fd].store(key + 1, std::memory_order_relaxed);
+  g_gem_live.fetch_add(1);
+  track(gem_key(key, h), c);
+  logf(2, "gem create %llu bytes VRAM on fd %d (client %llu) -> handle %u, used %llu", (unsigned long long)c, fd,
+       (unsigned long long)key, h, (unsigned long long)g.ledger->total.load());
   return r;
 }
 
-// A closed render-node fd drops every GEM handle it held: uncharge them all.
-void gem_fd_closed(int fd) {
-  uint64_t freed = 0;
-  for (auto& s : g_shards) {
-    pthread_mutex_lock(&s.mu);
-    for (size_t i = 0; i < s.cap; ++i) {
-      uint64_t k = s.keys[i];
-      if (k != kEmpty && k != kDeleted && (k >> 63) && (uint32_t)(k >> 32 & 0x7fffffff) == (uint32_t)fd) {
-        freed += s.vals[i];
-        s.keys[i] = kDeleted;
-      }
+// The DRM client key of a render fd a GEM ioctl names (recorded at create, else read).
+uint64_t gem_client(int fd) {
+  uint64_t k = fd >= 0 && fd < kMaxDrmFd ? g_drm_client[fd].load(std::memory_order_relaxed) : 0;
+  return k ? k - 1 : client_key_of(fd);
+}
+
+int gem_close(ioctl_t f, int fd, unsigned long req, DrmGemClose* a) {
+  uint32_t gh = a->handle;
+  int r = f(fd, req, a);
+  if (r == 0 && g_gem_live.load(std::memory_order_relaxed) > 0) {
+    uint64_t c = untrack(gem_key(gem_client(fd), gh));
+    if (c) {
+      g_gem_live.fetch_sub(1);
+      uncharge(c);
+      logf(2, "gem close fd %d handle %u -> %llu bytes", fd, gh, (unsigned long long)c);
     }
-    pthread_mutex_unlock(&s.mu);
   }
-  uncharge(freed);
-  logf(2, "render fd %d closed: %llu GEM bytes released", fd, (unsigned long long)freed);
+  return r;
+}
+
+// Exporting a charged VRAM handle as a dma-buf would let the HBM outlive GEM_CLOSE uncharged:
+// refused (EACCES), or with GPUSHARE_SHIM_PRIME=keep exported and kept charged until the DRM
+// file is gone.
+int prime_export(ioctl_t f, int fd, unsigned long req, DrmPrimeHandle* a) {
+  if (g_gem_live.load(std::memory_order_relaxed) <= 0) return f(fd, req, a);
+  uint64_t k = gem_key(gem_client(fd), a->handle);
+  uint64_t c = untrack(k);
+  if (!c) return f(fd, req, a);
+  const char* mode = getenv("GPUSHARE_SHIM_PRIME");
+  if (!(mode && !strcmp(mode, "keep"))) {
+    track(k, c);
+    logf(1, "refused dma-buf export of charged VRAM handle %u on fd %d (GPUSHARE_SHIM_PRIME=keep allows it)",
+         a->handle, fd);
+    errno = EACCES;
+    return -1;
+  }
+  int r = f(fd, req, a);
+  track(r == 0 ? (k | kStickyBit) : k, c);
+  if (r == 0) logf(2, "dma-buf export of handle %u: charge kept until its DRM file is gone", a->handle);
+  return r;
+}
+
+// A closed render fd: the DRM file's GEM handles die with the file, which may still be open
+// through a dup'ed or inherited fd — released now if not, else once it is (linger_gc).
+void gem_fd_closed(int fd, uint64_t key) {
+  for (int i = 0; i < kMaxDrmFd; ++i)
+    if (i != fd && g_drm_client[i].load(std::memory_order_relaxed) == key + 1) {
+      logf(2, "render fd %d closed: DRM client %llu still open as fd %d", fd, (unsigned long long)key, i);
+      return;
+    }
+  if (client_alive(key)) {
+    linger_add(key);
+    return;
+  }
+  release_client(key);
 }
 
 }  // namespace
@@ -785,22 +993,16 @@ GS_EXPORT int ioctl(int fd, unsigned long req, ...) {
   }
   // Cheap filters first, and never the once-control while init() runs (the runtime may start
   // up underneath it and allocate through here: waiting on that init would deadlock).
-  if ((req != kIocAlloc && req != kIocFree && req != kDrmGemCreate && req != kDrmGemClose) || !arg ||
-      env_mode() != kModeKfd || g_initializing.load(std::memory_order_acquire))
+  if ((req != kIocAlloc && req != kIocFree && req != kDrmGemCreate && req != kDrmGemClose &&
+       req != kDrmPrimeHandleToFd) || !arg || env_mode() != kModeKfd || g_initializing.load(std::memory_order_acquire))
     return f(fd, req, arg);
   if (req == kIocAlloc && !(static_cast<KfdAllocArgs*>(arg)->flags & kKfdVram)) return f(fd, req, arg);
+  if ((req == kDrmGemClose || req == kDrmPrimeHandleToFd) && g_gem_live.load(std::memory_order_relaxed) <= 0)
+    return f(fd, req, arg);
   if (!enabled()) return f(fd, req, arg);
   if (req == kDrmGemCreate) return gem_create(f, fd, req, static_cast<DrmGemCreateIn*>(arg));
-  if (req == kDrmGemClose) {
-    uint32_t gh = static_cast<DrmGemClose*>(arg)->handle;
-    int r = f(fd, req, arg);
-    if (r == 0 && fd >= 0 && fd < kMaxDrmFd && g_drm_fd[fd].load(std::memory_order_relaxed)) {
-      uint64_t c = untrack(gem_key(fd, gh));
-      uncharge(c);
-      if (c) logf(2, "gem close fd %d handle %u -> %llu bytes", fd, gh, (unsigned long long)c);
-    }
-    return r;
-  }
+  if (req == kDrmGemClose) return gem_close(f, fd, req, static_cast<DrmGemClose*>(arg));
+  if (req == kDrmPrimeHandleToFd) return prime_export(f, fd, req, static_cast<DrmPrimeHandle*>(arg));
   if (req == kIocAlloc) return kfd_alloc(f, fd, req, static_cast<KfdAllocArgs*>(arg));
   uint64_t h = static_cast<KfdFreeArgs*>(arg)->handle;
   int r = f(fd, req, arg);
@@ -823,11 +1025,30 @@ GS_EXPORT int close(int fd) {
     f = reinterpret_cast<close_t>(dlsym(RTLD_NEXT, "close"));
     real.store(f, std::memory_order_release);
   }
-  if (fd >= 0 && fd < kMaxDrmFd && g_drm_fd[fd].load(std::memory_order_relaxed)) {
+  if (fd >= 0 && fd < kMaxDrmFd && g_drm_client[fd].load(std::memory_order_relaxed)) {
+    // forget the fd before the real close: once closed, another thread may get the same number
+    // for a new render fd and charge handles under it
+    uint64_t ck = g_drm_client[fd].exchange(0, std::memory_order_acq_rel);
     int r = f(fd);
-    if (r == 0) {
-      g_drm_fd[fd].store(0, std::memory_order_relaxed);
-      gem_fd_closed(fd);
+    if (r != 0 && errno == EBADF) {
+      g_drm_client[fd].store(ck, std::memory_order_relaxed);
+      return r;
+    }
+    if (ck) {
+      int err = errno;
+      gem_fd_closed(fd, ck - 1);
+      errno = err;
+    }
+    return r;
+  }
+  if (f && fd >= 0 && __atomic_load_n(&g_linger.n, __ATOMIC_RELAXED) > 0) {
+    // the last fd of a lingering DRM file (a dup the shim never saw used) may be this one
+    uint64_t k = client_key_of(fd);
+    int r = f(fd);
+    if (r == 0 && !(k & kFdClient) && linger_has(k)) {
+      int err = errno;
+      linger_gc();
+      errno = err;
     }
     return r;
   }

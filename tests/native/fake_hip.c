@@ -13,6 +13,9 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/mman.h>
+#include <stdio.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 typedef int hipError_t;
 struct kfd_alloc { uint64_t va, size, handle, mmap_offset; uint32_t gpu_id, flags; };
 struct kfd_free { uint64_t handle; };
@@ -33,6 +36,18 @@ struct gem_close { uint32_t handle, pad; };
 static uint64_t g_gem_sizes[4096];
 static uint32_t g_gem_next = 1;
 
+/* The kernel's view of a closed fd: with a synthetic /proc (GPUSHARE_SHIM_PROC_ROOT, the shim
+   tests) its fd and fdinfo entries disappear when the fd really closes. */
+int close(int fd) {
+  const char* root = getenv("GPUSHARE_SHIM_PROC_ROOT");
+  if (root && fd >= 0) {
+    char p[512];
+    snprintf(p, sizeof p, "%s/%d/fd/%d", root, (int)getpid(), fd); unlink(p);
+    snprintf(p, sizeof p, "%s/%d/fdinfo/%d", root, (int)getpid(), fd); unlink(p);
+  }
+  return (int)syscall(SYS_close, fd);
+}
+
 int ioctl(int fd, unsigned long req, ...) {
   va_list ap; va_start(ap, req); void* arg = va_arg(ap, void*); va_end(ap);
   if (req == GEM_CREATE) {
@@ -44,6 +59,9 @@ int ioctl(int fd, unsigned long req, ...) {
     uint32_t h = __atomic_fetch_add(&g_gem_next, 1, __ATOMIC_ACQ_REL) % 4096;
     g_gem_sizes[h] = vram ? n : 0;
     memset(a, 0, sizeof *a); *(uint32_t*)a = h; return 0;
+  }
+  if (req == DIOC(3, 0x2d, 12)) {           /* DRM_IOCTL_PRIME_HANDLE_TO_FD: a dma-buf fd */
+    ((int32_t*)arg)[2] = dup(fd); return 0;
   }
   if (req == GEM_CLOSE) {
     uint32_t h = ((struct gem_close*)arg)->handle % 4096;

@@ -10,9 +10,35 @@
 #include <errno.h>
 #include <fcntl.h>
 #include <sys/ioctl.h>
+#include <sys/stat.h>
 #include <sys/wait.h>
 #include <unistd.h>
-static int g_render_fd = -1;
+static int g_render_fd = -1, g_dup_fd = -1, g_hold_pipe = -1;
+static pid_t g_hold_pid = -1;
+static int g_hold_fd = -1;
+static unsigned long long g_cid = 0;
+/* synthetic /proc entries (GPUSHARE_SHIM_PROC_ROOT) for fd of pid: <root>/<pid>/fd/<fd> -> a
+   render node, <root>/<pid>/fdinfo/<fd> with drm-client-id; cid 0 removes them */
+static void fake_fd(pid_t pid, int fd, unsigned long long cid) {
+  const char* root = getenv("GPUSHARE_SHIM_PROC_ROOT");
+  if (!root || fd < 0) return;
+  char p[512], q[512];
+  snprintf(p, sizeof p, "%s/%d", root, (int)pid); mkdir(p, 0755);
+  snprintf(p, sizeof p, "%s/%d/fd", root, (int)pid); mkdir(p, 0755);
+  snprintf(p, sizeof p, "%s/%d/fdinfo", root, (int)pid); mkdir(p, 0755);
+  snprintf(p, sizeof p, "%s/%d/fd/%d", root, (int)pid, fd);
+  snprintf(q, sizeof q, "%s/%d/fdinfo/%d", root, (int)pid, fd);
+  unlink(p); unlink(q);
+  if (!cid) return;
+  if (symlink("/dev/dri/renderD128", p)) return;
+  FILE* f = fopen(q, "w");
+  if (f) { fprintf(f, "pos:\t0\nflags:\t02100002\ndrm-driver:\tamdgpu\ndrm-client-id:\t%llu\n", cid); fclose(f); }
+}
+static int fake_exists(pid_t pid, int fd) {
+  const char* root = getenv("GPUSHARE_SHIM_PROC_ROOT");
+  char q[512]; snprintf(q, sizeof q, "%s/%d/fdinfo/%d", root ? root : "/nonexistent", (int)pid, fd);
+  return access(q, F_OK) == 0;
+}
 typedef int hipError_t;
 hipError_t hipMalloc(void**, size_t); hipError_t hipFree(void*);
 hipError_t hipMemGetInfo(size_t*, size_t*); hipError_t hipMallocAsync(void**, size_t, void*);
@@ -68,7 +94,7 @@ int main(int argc, char** argv) {
       printf("{\"op\":\"stats\",\"enabled\":%d,\"used\":%llu,\"quota\":%llu,\"denied\":%llu,\"peak\":%llu}\n", e,
              (unsigned long long)u, (unsigned long long)q, (unsigned long long)d, (unsigned long long)pk); }
     else if (!strcmp(argv[i], "gem")) {   /* "gem BYTES DOMAINS": amdgpu GEM_CREATE on the render fd */
-      static int rfd = -1; if (rfd < 0) rfd = open("/dev/null", O_RDWR);
+      int rfd = g_render_fd >= 0 ? g_render_fd : open("/dev/null", O_RDWR);
       struct { uint64_t size, align, domains, flags; } a = {strtoull(argv[i + 1], 0, 10), 4096, strtoull(argv[i + 2], 0, 10), 0};
       unsigned long req = ((unsigned long)3 << 30) | ((unsigned long)32 << 16) | ((unsigned long)'d' << 8) | 0x40;
       int r = ioctl(rfd, req, &a); i += 2; g_render_fd = rfd;
@@ -76,8 +102,30 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[i], "gemclose")) { struct { uint32_t h, pad; } c = {(uint32_t)atoi(argv[++i]), 0};
       unsigned long req = ((unsigned long)1 << 30) | ((unsigned long)8 << 16) | ((unsigned long)'d' << 8) | 0x09;
       int r = ioctl(g_render_fd, req, &c); printf("{\"op\":\"gemclose\",\"err\":%d}\n", r); }
-    else if (!strcmp(argv[i], "closefd")) { int r = close(g_render_fd); g_render_fd = -1;
-      printf("{\"op\":\"closefd\",\"err\":%d}\n", r); }
+    else if (!strcmp(argv[i], "closefd")) { int fd = g_render_fd; int r = close(fd);
+      g_render_fd = -1; printf("{\"op\":\"closefd\",\"err\":%d}\n", r); }
+    /* DRM file identity through a synthetic /proc (GPUSHARE_SHIM_PROC_ROOT): "drmfile CID" gives
+       the render fd the kernel's drm-client-id CID; "dup" duplicates it (same file, same id) */
+    else if (!strcmp(argv[i], "drmfile")) { if (g_render_fd < 0) g_render_fd = open("/dev/null", O_RDWR);
+      g_cid = strtoull(argv[++i], 0, 10); fake_fd(getpid(), g_render_fd, g_cid);
+      printf("{\"op\":\"drmfile\",\"fd\":%d}\n", g_render_fd); }
+    else if (!strcmp(argv[i], "dup")) { g_dup_fd = dup(g_render_fd); fake_fd(getpid(), g_dup_fd, g_cid);
+      printf("{\"op\":\"dup\",\"fd\":%d}\n", g_dup_fd); }
+    else if (!strcmp(argv[i], "swapdup")) { int t = g_render_fd; g_render_fd = g_dup_fd; g_dup_fd = t;
+      printf("{\"op\":\"swapdup\"}\n"); }
+    else if (!strcmp(argv[i], "closedup")) { int fd = g_dup_fd; int r = close(fd);
+      g_dup_fd = -1; printf("{\"op\":\"closedup\",\"err\":%d}\n", r); }
+    /* "forkhold": a child inherits the render fd and keeps it open until "killhold" */
+    else if (!strcmp(argv[i], "forkhold")) { int pp[2]; if (pipe(pp)) return 9; fflush(stdout); pid_t c = fork();
+      if (c == 0) { close(pp[1]); fake_fd(getpid(), g_render_fd, g_cid); char b; ssize_t n = read(pp[0], &b, 1); (void)n; _exit(0); }
+      close(pp[0]); g_hold_pid = c; g_hold_pipe = pp[1]; g_hold_fd = g_render_fd;
+      for (int k = 0; k < 200 && !fake_exists(c, g_render_fd); ++k) usleep(5000);
+      printf("{\"op\":\"forkhold\",\"pid\":%d}\n", (int)c); }
+    else if (!strcmp(argv[i], "killhold")) { close(g_hold_pipe); int st = 0; waitpid(g_hold_pid, &st, 0);
+      fake_fd(g_hold_pid, g_hold_fd, 0); printf("{\"op\":\"killhold\",\"status\":%d}\n", st); }
+    else if (!strcmp(argv[i], "prime")) { struct { uint32_t h, flags; int32_t fd; } a = {(uint32_t)atoi(argv[++i]), 0, -1};
+      unsigned long req = ((unsigned long)3 << 30) | ((unsigned long)12 << 16) | ((unsigned long)'d' << 8) | 0x2d;
+      int r = ioctl(g_render_fd, req, &a); printf("{\"op\":\"prime\",\"err\":%d,\"fd\":%d}\n", r ? errno : 0, a.fd); }
     else if (!strcmp(argv[i], "sleep")) { usleep((useconds_t)(atof(argv[++i]) * 1e6)); }
     else if (!strcmp(argv[i], "crash")) { fflush(stdout); _exit(3); }
     fflush(stdout);

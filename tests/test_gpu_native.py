@@ -346,6 +346,110 @@ def test_shim_charges_render_node_gem_vram():
     assert [x["released"] for x in rows[3:]] == [2 * GIB, GIB]
 
 
+_GEM_ESCAPES = r'''
+import ctypes, json, os, sys, time
+minor = int(sys.argv[1])
+GIB = 1 << 30
+libc = ctypes.CDLL(None, use_errno=True)
+used_path = f"/sys/class/drm/renderD{minor}/device/mem_info_vram_used"
+class Create(ctypes.Structure):
+    _fields_ = [("bo_size", ctypes.c_uint64), ("alignment", ctypes.c_uint64), ("domains", ctypes.c_uint64),
+                ("domain_flags", ctypes.c_uint64)]
+class Close(ctypes.Structure):
+    _fields_ = [("handle", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
+class Prime(ctypes.Structure):
+    _fields_ = [("handle", ctypes.c_uint32), ("flags", ctypes.c_uint32), ("fd", ctypes.c_int32)]
+CREATE = (3 << 30) | (32 << 16) | (ord("d") << 8) | 0x40
+CLOSE = (1 << 30) | (8 << 16) | (ord("d") << 8) | 0x09
+PRIME = (3 << 30) | (12 << 16) | (ord("d") << 8) | 0x2d
+libc.ioctl.argtypes = [ctypes.c_int, ctypes.c_ulong, ctypes.c_void_p]
+libc.close.argtypes = [ctypes.c_int]
+stats = libc.gpushare_shim_stats
+stats.argtypes = [ctypes.POINTER(ctypes.c_uint64)] * 4
+def ledger():
+    u, q, d, p = (ctypes.c_uint64() for _ in range(4))
+    stats(ctypes.byref(u), ctypes.byref(q), ctypes.byref(d), ctypes.byref(p))
+    return u.value
+def dev():
+    time.sleep(0.3)                       # amdgpu returns freed VRAM asynchronously
+    return int(open(used_path).read())
+def create(fd, n):
+    a = Create(n, 4096, 0x4, 0)
+    r = libc.ioctl(fd, CREATE, ctypes.addressof(a))
+    return (ctypes.cast(ctypes.pointer(a), ctypes.POINTER(ctypes.c_uint32))[0] if r == 0 else None), \
+        (ctypes.get_errno() if r else 0)
+def out(**k):
+    print(json.dumps(k), flush=True)
+def fresh():
+    return os.open(f"/dev/dri/renderD{minor}", os.O_RDWR)
+# 1) dup + close: the DRM file lives on through the dup, so does the charge
+base = dev()
+a = fresh()
+h, e = create(a, GIB)
+b = os.dup(a)
+libc.close(a)
+out(case="dup", err=e, charge=ledger(), held=dev() - base)
+libc.ioctl(b, CLOSE, ctypes.addressof(Close(h, 0)))
+out(case="dup_gemclose", charge=ledger(), held=dev() - base)
+# 2) PRIME export of a charged VRAM handle
+h2, e2 = create(b, GIB)
+pr = Prime(h2, 0, -1)
+r = libc.ioctl(b, PRIME, ctypes.addressof(pr))
+out(case="prime", rc=r, errno=ctypes.get_errno() if r else 0, charge=ledger())
+libc.close(b)
+out(case="closed", charge=ledger(), held=dev() - base)
+# 3) a child inherits the render fd; the parent closes its copy
+c = fresh()
+h3, e3 = create(c, 2 * GIB)
+rp, wp = os.pipe()
+pid = os.fork()
+if pid == 0:
+    os.close(wp)
+    os.read(rp, 1)
+    os._exit(0)
+os.close(rp)
+libc.close(c)
+out(case="inherited", charge=ledger(), held=dev() - base)
+d = fresh()
+h4, e4 = create(d, 3 * GIB)                  # quota 4 GiB: 2 (lingering, child alive) + 3 > 4
+out(case="over_while_child", errno=e4)
+os.close(wp)
+os.waitpid(pid, 0)
+h5, e5 = create(d, 3 * GIB)                  # the child is gone: its file's 2 GiB were freed
+out(case="after_child", errno=e5, charge=ledger(), held=dev() - base)
+libc.close(d)
+out(case="end", charge=ledger(), held=dev() - base)
+'''
+
+
+def test_shim_gem_escapes_are_closed():
+    """Round-3 review item 3 on the real render node: dup + close keeps the charge while the DRM
+    file (and the device's VRAM) lives; a charged VRAM handle cannot be exported as a dma-buf;
+    a parent closing an inherited fd leaves the charge until the child holding the file exits.
+    Throughout, the ledger follows the device's own VRAM count."""
+    from aliyun_gpushare_device_plugin_amd.utils.native import lib_path
+
+    with S.SMI("auto") as smi:
+        minor = smi.device(0).render_minor
+    env = dict(os.environ, LD_PRELOAD=lib_path("hipshim"), GPUSHARE_QUOTA_BYTES=str(4 * GIB),
+               GPUSHARE_SHIM_LOG="1")
+    r = subprocess.run([sys.executable, "-c", _GEM_ESCAPES, str(minor)], env=env, capture_output=True, text=True,
+                       timeout=90)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rows = {x["case"]: x for x in (json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{"))}
+    tol = 128 * MIB
+    assert rows["dup"]["err"] == 0 and rows["dup"]["charge"] == GIB
+    assert abs(rows["dup"]["held"] - GIB) <= tol, rows           # the VRAM really is still allocated
+    assert rows["dup_gemclose"]["charge"] == 0 and rows["dup_gemclose"]["held"] <= tol
+    assert rows["prime"]["rc"] != 0 and rows["prime"]["errno"] == 13 and rows["prime"]["charge"] == GIB
+    assert rows["closed"]["charge"] == 0 and rows["closed"]["held"] <= tol
+    assert rows["inherited"]["charge"] == 2 * GIB and abs(rows["inherited"]["held"] - 2 * GIB) <= tol
+    assert rows["over_while_child"]["errno"] == 12
+    assert rows["after_child"]["errno"] == 0 and rows["after_child"]["charge"] == 3 * GIB
+    assert abs(rows["after_child"]["held"] - 3 * GIB) <= tol
+    assert rows["end"]["charge"] == 0 and rows["end"]["held"] <= tol
+
+
 def test_quota_watchdog_catches_a_process_without_the_shim():
     """Round-2 review, isolation: a tenant process that drops the quota shim is still seen by
     the node-side watchdog (amdgpu DRM fdinfo, kernel-reported) and, in kill mode, ended."""

@@ -387,3 +387,65 @@ def test_ledger_survives_runtime_map_fixed_during_shim_init(stub, native_shim, t
     assert r.returncode == 0, r.stderr
     assert [o["err"] for o in out[:3]] == [0, 0, 2]
     assert out[3]["used"] == 3 * GIB and out[3]["denied"] == 1
+
+
+def _proc(tmp_path):
+    root = tmp_path / "proc"
+    root.mkdir(parents=True)
+    return str(root)
+
+
+def test_gem_charge_survives_dup_and_close(stub, native_shim, tmp_path):
+    """Round-3 review item 3: GEM handles belong to the DRM file, not the fd number. dup(fd) +
+    close(fd) leaves the file (and its VRAM) alive through the dup, so the charge stays; it is
+    released when the last fd closes, and GEM_CLOSE through the dup releases a handle."""
+    vram = 4
+    out, r = run(stub, native_shim, ["drmfile", 71, "gem", GIB, vram, "gem", GIB, vram, "dup", "closefd", "stats",
+                                     "swapdup", "gemclose", 2, "stats", "closefd", "stats"],
+                 GPUSHARE_QUOTA_BYTES=4 * GIB, GPUSHARE_SHIM_PROC_ROOT=_proc(tmp_path))
+    assert r.returncode == 0, r.stderr
+    ops = {o["op"]: o for o in out}
+    st = [o for o in out if o["op"] == "stats"]
+    assert out[1]["err"] == out[2]["err"] == 0 and ops["closefd"]["err"] == 0
+    assert st[0]["used"] == 2 * GIB              # the original fd closed, the dup holds the file
+    assert st[1]["used"] == GIB                  # GEM_CLOSE through the dup: same DRM file
+    assert st[2]["used"] == 0                    # the last fd closed: the file and its BOs are gone
+
+
+def test_gem_charge_survives_a_parent_closing_an_inherited_fd(stub, native_shim, tmp_path):
+    """A child inherits the render fd; the parent closing its copy does not free the file, so
+    the charge lingers; once the child is gone it is released at the next re-check (before a
+    denial, or when another fd of the file closes)."""
+    vram = 4
+    out, r = run(stub, native_shim, ["drmfile", 72, "gem", 2 * GIB, vram, "forkhold", "closefd", "stats",
+                                     "drmfile", 73, "gem", 3 * GIB, vram, "killhold", "gem", 3 * GIB, vram, "stats"],
+                 GPUSHARE_QUOTA_BYTES=4 * GIB, GPUSHARE_SHIM_PROC_ROOT=_proc(tmp_path))
+    assert r.returncode == 0, r.stderr
+    gems = [o for o in out if o["op"] == "gem"]
+    st = [o for o in out if o["op"] == "stats"]
+    assert gems[0]["err"] == 0
+    assert st[0]["used"] == 2 * GIB              # the child still holds the DRM file
+    assert gems[1]["err"] == 12                  # 2 + 3 > 4 GiB: the lingering file is still alive
+    assert gems[2]["err"] == 0                   # child gone: re-checked before denying, released
+    assert st[1]["used"] == 3 * GIB
+
+
+def test_prime_export_of_charged_vram_is_refused(stub, native_shim, tmp_path):
+    """A dma-buf export would keep the BO alive after GEM_CLOSE: refused for charged VRAM
+    handles (EACCES); GTT handles export normally; GPUSHARE_SHIM_PRIME=keep exports and keeps the
+    charge until the DRM file is gone."""
+    vram, gtt = 4, 2
+    args = ["drmfile", 74, "gem", GIB, vram, "gem", GIB, gtt, "prime", 1, "prime", 2, "gemclose", 1, "stats",
+            "closefd", "stats"]
+    out, r = run(stub, native_shim, args, GPUSHARE_QUOTA_BYTES=4 * GIB, GPUSHARE_SHIM_PROC_ROOT=_proc(tmp_path))
+    assert r.returncode == 0, r.stderr
+    pr = [o for o in out if o["op"] == "prime"]
+    st = [o for o in out if o["op"] == "stats"]
+    assert pr[0]["err"] == 13 and pr[1]["err"] == 0      # EACCES for VRAM; GTT is not HBM
+    assert st[0]["used"] == 0                            # not exported: GEM_CLOSE released it
+    out, r = run(stub, native_shim, args, GPUSHARE_QUOTA_BYTES=4 * GIB, GPUSHARE_SHIM_PRIME="keep",
+                 GPUSHARE_SHIM_PROC_ROOT=_proc(tmp_path / "k"))
+    pr = [o for o in out if o["op"] == "prime"]
+    st = [o for o in out if o["op"] == "stats"]
+    assert pr[0]["err"] == 0 and st[0]["used"] == GIB  # exported: GEM_CLOSE keeps the charge
+    assert st[1]["used"] == 0                            # the DRM file closed: released
