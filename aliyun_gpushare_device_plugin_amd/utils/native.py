@@ -38,19 +38,35 @@ def lib_path(target: str) -> str:
     return os.path.join(NATIVE_DIR, LIBS[target])
 
 
+SOURCES = {"gpuinfo": "gpuinfo", "hipshim": "hipshim", "kernels": "kernels"}   # native/<dir>
+
+
+def stale(target: str, path: str) -> bool:
+    """The library is older than a source file of its ``native/<dir>`` (a test must never run
+    a build of code that has since changed)."""
+    src = os.path.join(REPO_ROOT, "native", SOURCES[target])
+    try:
+        built = os.path.getmtime(path)
+        return any(os.path.getmtime(os.path.join(src, f)) > built for f in os.listdir(src)
+                   if f.endswith((".cpp", ".h", ".hip", ".hpp")))
+    except OSError:
+        return False
+
+
 def ensure_built(target: str, auto_build: bool | None = None) -> str:
-    """Return the path of a native library, building it in-tree when it is missing.
+    """Return the path of a native library, building it in-tree when it is missing or older
+    than its sources.
 
     ``auto_build`` defaults to on unless ``GPUSHARE_NO_AUTOBUILD=1``.
     """
     path = lib_path(target)
-    if os.path.exists(path):
-        return path
     if auto_build is None:
         auto_build = os.environ.get("GPUSHARE_NO_AUTOBUILD", "") != "1"
+    if os.path.exists(path) and not (auto_build and stale(target, path)):
+        return path
     if auto_build and os.path.exists(BUILD_SCRIPT):
         with _lock:
-            if not os.path.exists(path):
+            if not os.path.exists(path) or stale(target, path):
                 variant = os.environ.get("GPUSHARE_NATIVE_VARIANT", "")
                 extra = ["--sanitize", variant] if variant else []
                 r = subprocess.run([sys.executable, BUILD_SCRIPT, target, *extra], capture_output=True, text=True)
