@@ -53,6 +53,7 @@ MI355X build, same protocol, different mechanics:
 from __future__ import annotations
 
 import collections
+import contextlib
 import dataclasses
 import os
 import threading
@@ -719,6 +720,7 @@ class Allocator:
         dt = time.perf_counter() - t0
         self.metrics.allocate_latency.observe(dt, phase="total")
         self.metrics.allocate_latency.observe(dt, phase="fast")
+        self.metrics.allocate_requests.observe(0)
         if defer is None or not defer(lambda: self._patch_q.put(job)):
             self._patch_q.put(job)
         return pick.body
@@ -799,6 +801,19 @@ class Allocator:
             self.journal.prune_index(pend)
 
     def _allocate_full(self, req, t0: float):
+        """The full Allocate path, counting the apiserver round trips it makes (the handler
+        thread's requests; write-behind patches run on the patcher thread)."""
+        count = getattr(self.client, "thread_requests", None)
+        n0 = count() if count else 0
+        try:
+            view = getattr(self.pods, "allocate_view", None)
+            with view() if view else contextlib.nullcontext():   # per-call sources: one LIST per Allocate
+                return self._allocate_full_in(req, t0)
+        finally:
+            if count:
+                self.metrics.allocate_requests.observe(count() - n0)
+
+    def _allocate_full_in(self, req, t0: float):
         sizes = tuple(len(c.devices_ids) for c in req.container_requests)
         pod_units = sum(sizes)
         log.info("----Allocating GPU for gpu mem is started---- RequestPodGPUs: %d", pod_units)
@@ -818,7 +833,8 @@ class Allocator:
                 claim, complete = self._match(sizes, fresh=False, held=held)
                 t1 = time.perf_counter()
                 if claim is None:
-                    # watch lag: the kubelet may see a bind before our cache does
+                    # watch lag: the kubelet may see a bind before our cache does (per-call
+                    # sources: the view is already an authoritative LIST)
                     claim, complete = self._match(sizes, fresh=True, held=held)
                 if claim is not None:
                     self._revoked.discard(claim.uid)
@@ -944,9 +960,10 @@ class Allocator:
             return None
         uid, resp = hit
         # the kubelet recycles freed fake IDs, so under churn most key hits belong to pods that
-        # are gone: one O(1) cache lookup decides (round 2 scanned every node pod here)
+        # are gone: one O(1) cache lookup decides (round 2 scanned every node pod here); a
+        # per-call source answers from the Allocate's one LIST of Pending pods (allocate_view)
         try:
-            p = self.pods.get(uid)
+            p = self.pods.get_pending(uid)
         except Exception:  # noqa: BLE001
             return None
         if (p is not None and O.phase(p) == "Pending" and not O.deleting(p)

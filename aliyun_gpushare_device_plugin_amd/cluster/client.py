@@ -173,6 +173,11 @@ class APIClient:
         self._local = threading.local()
         self.requests = 0
 
+    def thread_requests(self) -> int:
+        """apiserver requests made so far by the calling thread (the Allocate handler counts
+        the round trips on its own path with it)."""
+        return getattr(self._local, "n", 0)
+
     # -- transport ----------------------------------------------------------------------
     def _new_conn(self, timeout=None):
         t = self.timeout if timeout is None else timeout
@@ -213,6 +218,7 @@ class APIClient:
             log.info("apiserver answered 401; retrying with the reloaded token")
             r, raw = self._roundtrip(method, url, data, content_type)
         self.requests += 1
+        self._local.n = getattr(self._local, "n", 0) + 1
         try:
             obj = json.loads(raw) if raw else {}
         except ValueError:

@@ -14,6 +14,7 @@ back into the cache from the PATCH response, so a just-assigned pod is never mat
 """
 from __future__ import annotations
 
+import contextlib
 import threading
 import time
 
@@ -44,6 +45,19 @@ class PodSource:
         """This node's live pod with ``uid`` (O(1) in the watch cache; a scan elsewhere)."""
         return next((p for p in self.node_pods() if O.uid(p) == uid), None)
 
+    def get_pending(self, uid: str) -> dict | None:
+        """This node's pod ``uid`` if it is Pending, else None."""
+        p = self.get(uid)
+        return p if p is not None and O.phase(p) == "Pending" else None
+
+    @contextlib.contextmanager
+    def allocate_view(self):
+        """One Allocate's view: sources that fetch per call (LIST, kubelet GET) answer every
+        ``pending_pods`` / ``get_pending`` inside the block from a single fetch — the
+        reference's cost model is one LIST per Allocate (``allocate.go:63``), not one per
+        lookup. A no-op for the watch cache."""
+        yield
+
     def start(self):
         return self
 
@@ -51,13 +65,46 @@ class PodSource:
         pass
 
 
-class ListSource(PodSource):
+class _PerCallSource(PodSource):
+    """A source that fetches on every call, with a per-thread memo inside ``allocate_view``."""
+
+    def __init__(self):
+        self._memo = threading.local()
+
+    @contextlib.contextmanager
+    def allocate_view(self):
+        m = self._memo
+        outer = getattr(m, "on", False)
+        m.on = True
+        try:
+            yield
+        finally:
+            if not outer:
+                m.on, m.items = False, None
+
+    def pending_pods(self, fresh: bool = False) -> list[dict]:
+        m = self._memo
+        if getattr(m, "on", False):
+            if getattr(m, "items", None) is None:
+                m.items = self._fetch_pending()
+            return m.items
+        return self._fetch_pending()
+
+    def get_pending(self, uid: str) -> dict | None:
+        return next((p for p in self.pending_pods() if O.uid(p) == uid), None)
+
+    def _fetch_pending(self) -> list[dict]:
+        raise NotImplementedError
+
+
+class ListSource(_PerCallSource):
     """The reference's default path: LIST the apiserver on every call."""
 
     def __init__(self, client: APIClient, node: str, retries: int = 3, retry_sleep: float = 1.0):
+        super().__init__()
         self.client, self.node, self.retries, self.retry_sleep = client, node, retries, retry_sleep
 
-    def pending_pods(self, fresh: bool = False) -> list[dict]:
+    def _fetch_pending(self) -> list[dict]:
         sel = node_field_selector(self.node, pending_only=True)
         err = None
         for i in range(self.retries + 1):
@@ -75,7 +122,7 @@ class ListSource(PodSource):
         return [p for p in items if not O.is_terminated(p)]
 
 
-class KubeletSource(PodSource):
+class KubeletSource(_PerCallSource):
     """``--query-kubelet``: kubelet ``/pods`` then apiserver fallback.
 
     Unlike the reference, "no Pending pods" is a valid answer, not an error to retry 8 × 100 ms
@@ -83,9 +130,10 @@ class KubeletSource(PodSource):
     """
 
     def __init__(self, kubelet_client, fallback: ListSource, retries: int = 8, retry_sleep: float = 0.1):
+        super().__init__()
         self.kubelet, self.fallback, self.retries, self.retry_sleep = kubelet_client, fallback, retries, retry_sleep
 
-    def pending_pods(self, fresh: bool = False) -> list[dict]:
+    def _fetch_pending(self) -> list[dict]:
         for i in range(self.retries + 1):
             try:
                 pods = self.kubelet.get_node_running_pods()
@@ -94,7 +142,7 @@ class KubeletSource(PodSource):
                 log.warning("failed to get pending pod list from kubelet (%s), retry", e)
                 time.sleep(self.retry_sleep)
         log.warning("not found from kubelet /pods api, start to list apiserver")
-        return self.fallback.pending_pods(fresh=True)
+        return self.fallback._fetch_pending()
 
     def node_pods(self) -> list[dict]:
         try:

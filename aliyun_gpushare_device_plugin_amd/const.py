@@ -96,3 +96,6 @@ def plugin_socket(dir_: str | None = None) -> str:
 
 def kubelet_socket(dir_: str | None = None) -> str:
     return os.path.join(dir_ or DEVICE_PLUGIN_PATH, KUBELET_SOCKET_NAME)
+
+# Allocate reply trailing metadata: "<handler entry ns>,<handler exit ns>" (CLOCK_MONOTONIC)
+HANDLER_STAMP_KEY = "gpushare-handler-ns"

@@ -63,11 +63,16 @@ class _Servicer:
                 p.metrics.listandwatch_sends.inc()
 
     def Allocate(self, request, context):
+        t_in = time.monotonic_ns()
         try:
             # message, or prepared wire bytes; follow-up work runs after the reply is sent
-            return self.p.allocator.allocate_raw(request, defer=context.add_callback)
+            out = self.p.allocator.allocate_raw(request, defer=context.add_callback)
         except AllocationError as e:
             context.abort(grpc.StatusCode.FAILED_PRECONDITION, str(e))
+        # handler entry/exit (CLOCK_MONOTONIC, ns) in the trailing metadata: a caller splits its
+        # round trip into transport-in, handler and transport-out (bench.py); the kubelet ignores it
+        context.set_trailing_metadata(((const.HANDLER_STAMP_KEY, f"{t_in},{time.monotonic_ns()}"),))
+        return out
 
     def GetPreferredAllocation(self, request, context):
         return self.p.allocator.preferred(request)

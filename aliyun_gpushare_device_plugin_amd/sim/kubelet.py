@@ -41,6 +41,10 @@ class Admission:
     latencies: list          # seconds per Allocate RPC
     device_ids: list
     error: str | None = None
+    # per Allocate RPC: (kubelet -> handler entry, handler, handler exit -> kubelet) seconds,
+    # from the handler's own timestamps in the reply's trailing metadata (one system-wide
+    # CLOCK_MONOTONIC for both processes)
+    splits: list = dataclasses.field(default_factory=list)
 
 
 class FakeKubelet:
@@ -267,16 +271,22 @@ class FakeKubelet:
                         ids = pref
                 self._allocated.setdefault(uid, set()).update(ids)
                 self._used.update(ids)
+            areq = api.AllocateRequest(container_requests=[api.ContainerAllocateRequest(devices_ids=ids)])
+            t0n = time.monotonic_ns()
             t0 = time.perf_counter()
             try:
-                resp = self._stub.Allocate(api.AllocateRequest(container_requests=[
-                    api.ContainerAllocateRequest(devices_ids=ids)]), timeout=timeout)
+                resp, call = self._stub.Allocate.with_call(areq, timeout=timeout)
             except grpc.RpcError as e:
                 adm.latencies.append(time.perf_counter() - t0)
                 adm.error = f"Allocate failed: {e.code()} {e.details()}"
                 self.release(uid)
                 return adm
             adm.latencies.append(time.perf_counter() - t0)
+            t1n = time.monotonic_ns()
+            stamp = dict(call.trailing_metadata() or ()).get(const.HANDLER_STAMP_KEY)
+            if stamp:
+                a, b = (int(x) for x in stamp.split(","))
+                adm.splits.append(((a - t0n) / 1e9, (b - a) / 1e9, (t1n - b) / 1e9))
             adm.responses.append(resp.container_responses[0])
             adm.device_ids.append(ids)
             # the device manager checkpoints the container's IDs (pod-resources shows them)

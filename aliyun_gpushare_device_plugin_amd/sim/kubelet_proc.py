@@ -89,7 +89,8 @@ class KubeletProcess:
     def admit(self, pod: dict, timeout: float = 10.0) -> Admission:
         r = self._call({"op": "admit", "pod": pod, "timeout": timeout})
         return Admission(r["uid"], [api.ContainerAllocateResponse.FromString(base64.b64decode(b))
-                                    for b in r["responses"]], r["latencies"], r["device_ids"], r["error"])
+                                    for b in r["responses"]], r["latencies"], r["device_ids"], r["error"],
+                         [tuple(x) for x in r.get("splits", [])])
 
     def release(self, pod_uid: str):
         self._call({"op": "release", "uid": pod_uid})
@@ -141,7 +142,7 @@ def main(argv=None) -> int:
             if op == "admit":
                 adm = kl.admit(req["pod"], timeout=req.get("timeout", 10.0))
                 send({"uid": adm.pod_uid, "latencies": adm.latencies, "device_ids": adm.device_ids,
-                      "error": adm.error,
+                      "error": adm.error, "splits": adm.splits,
                       "responses": [base64.b64encode(r.SerializeToString()).decode() for r in adm.responses]})
             elif op == "release":
                 kl.release(req["uid"])

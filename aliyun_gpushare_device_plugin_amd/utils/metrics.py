@@ -176,6 +176,9 @@ class PluginMetrics:
         self.allocate_latency = r.histogram("gpushare_allocate_latency_seconds",
                                             "Allocate RPC latency by phase (prelude/lock/lookup/decide/patch/total)")
         self.allocate_outcomes = r.counter("gpushare_allocate_total", "Allocate outcomes")
+        self.allocate_requests = r.histogram("gpushare_allocate_apiserver_requests",
+                                             "apiserver requests made on the Allocate path (counted by the handler "
+                                             "thread; write-behind patches excluded)", buckets=(0, 1, 2, 3, 4, 8))
         self.pending_match_failures = r.counter("gpushare_pending_match_failures_total",
                                                 "Allocates with no matching assumed pod")
         self.units_per_gpu = r.gauge("gpushare_advertised_units", "Advertised gpu-mem units per GPU")

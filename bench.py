@@ -128,7 +128,37 @@ def plugin_latency(port: int, reset: bool = False) -> dict | None:
     tot = phases.get("total")
     if tot is not None:
         tot = dict(tot, phases={k: v.get("p50") for k, v in phases.items()})
+        # apiserver round trips the handler itself made, per Allocate (measured, not assumed)
+        rq = (d.get("gpushare_allocate_apiserver_requests") or [{}])[0]
+        tot["requests"] = {"p50": rq.get("p50"), "p99": rq.get("p99"), "count": rq.get("count")}
     return tot
+
+
+def transport_floor() -> float | None:
+    """Kubelet-side round trip of an Allocate whose handler returns a prepared answer at once."""
+    try:
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "grpc_server_probe.py"), "--models", "sync",
+                            "--busy-threads", "0", "--calls", "200", "--gap-ms", "5"],
+                           capture_output=True, text=True, timeout=120)
+        return json.loads(r.stdout.strip().splitlines()[-1])["sync"]["p50_ms"]
+    except Exception:  # noqa: BLE001 - a calibration, never fatal
+        return None
+
+
+def breakdown(splits) -> dict | None:
+    """p50 of each leg of the kubelet-side Allocate round trip (ms): kubelet -> handler entry
+    (gRPC client, transport, server dispatch), the handler, handler exit -> kubelet (reply
+    serialisation, transport, client wake-up) — from the handler's own timestamps."""
+    if not splits:
+        return None
+    return {k: ms(pct([x[i] for x in splits], 0.5))
+            for i, k in enumerate(("kubelet_to_handler", "handler", "handler_to_kubelet"))}
+
+
+def round_trips(srv) -> dict | None:
+    """The plugin's own count of apiserver requests on its Allocate path (p50 / p99)."""
+    rq = (srv or {}).get("requests") or {}
+    return None if rq.get("p50") is None else {"p50": rq["p50"], "p99": rq["p99"]}
 
 
 class ControlPlane:
@@ -180,6 +210,9 @@ class ControlPlane:
         self.alloc_lat_by_gpu: dict[int, list] = {g: [] for g in range(n_gpus)}
         self.ref_resident: dict[int, list] = {g: [] for g in range(n_gpus)}
         self.ref_lat: list[float] = []
+        self.ref_splits: list = []
+        self.splits: list = []
+        self.steps_done = 0                     # alternates which node is admitted first
         self.ref_failed = 0
         self.admit_lat: list[float] = []
         self.failed = 0
@@ -241,6 +274,7 @@ class ControlPlane:
             self.cluster.delete_pod(bpod)
             return
         self.ref_lat.extend(adm.latencies)
+        self.ref_splits.extend(adm.splits)
         self.ref_resident[rg].append((bpod, size))
 
     def churn_one(self, gpu: int, uid: str | None = None) -> tuple[int, dict] | None:
@@ -257,6 +291,12 @@ class ControlPlane:
         if k is None:
             return None
         old, size = pods.pop(k)
+        # the same churn step on the reference-model node, first on every other step: neither
+        # node always admits right after a retired pod's teardown started
+        self.steps_done += 1
+        mirror_first = self.ref_port and self.steps_done % 2 == 0
+        if mirror_first:
+            self._mirror(gpu, size)
         tc = time.perf_counter()
         self.cluster.delete_pod(old)
         pod = self.cluster.create_pod(size)
@@ -279,8 +319,9 @@ class ControlPlane:
             return None
         self.alloc_lat.extend(adm.latencies)
         self.alloc_lat_by_gpu[rec[0]].extend(adm.latencies)
+        self.splits.extend(adm.splits)
         self.admit_lat.append(dt)
-        if self.ref_port:
+        if self.ref_port and not mirror_first:
             self._mirror(gpu, size)          # alternating admissions, same pod load
         return rec
 
@@ -302,7 +343,7 @@ def mode_comparison(rtts_ms: list[float], n_pods: int) -> dict:
     out = {}
     for rtt in rtts_ms:
         for label, src, extra in (("default", "watch", []), ("reference", "list", ["--sync-patch"])):
-            lat, fails = [], 0
+            lat, fails, splits = [], 0, []
             port = free_port()
             with SimCluster([("cmp", "fake:1x288G")], plugin_mode="process", pod_source=src,
                             apiserver="process", kubelet="process", apiserver_latency_s=rtt / 1e3,
@@ -318,6 +359,7 @@ def mode_comparison(rtts_ms: list[float], n_pods: int) -> dict:
                         fails += 1
                     else:
                         lat += adm.latencies
+                        splits += adm.splits
                     c.delete_pod(pod)
                 srv = plugin_latency(port) or {}
             key = f"{label}@{rtt:g}ms"
@@ -328,7 +370,8 @@ def mode_comparison(rtts_ms: list[float], n_pods: int) -> dict:
             # kubelet-side number is gRPC transport and the harness's processes sharing the CPUs
             out[key] = {"allocate_p50_ms": ms(pct(lat, 0.5)), "allocate_p99_ms": ms(pct(lat, 0.99)),
                         "plugin_allocate_p50_ms": ms(srv.get("p50")), "plugin_allocate_p99_ms": ms(srv.get("p99")),
-                        "apiserver_round_trips_on_path": 2 if extra else 0, "request_ms": ms(pct(req, 0.5)),
+                        "allocate_breakdown_p50_ms": breakdown(splits),
+                        "apiserver_round_trips_on_path": round_trips(srv), "request_ms": ms(pct(req, 0.5)),
                         "pod_source": src, "patch": "sync" if extra else "write-behind", "failed": fails}
     return out
 
@@ -775,6 +818,8 @@ def main():
             v.clear()
         cp.admit_lat.clear()
         cp.ref_lat.clear()
+        cp.ref_splits.clear()
+        cp.splits.clear()
         cp.ref_failed = 0
         cp.cp_time = 0.0
         cp.failed = 0
@@ -866,8 +911,9 @@ def main():
             "allocate_p50_ms": ms(pct(cp.alloc_lat, 0.5)), "allocate_p99_ms": ms(pct(cp.alloc_lat, 0.99)),
             "plugin_allocate_p50_ms": ms(srv["p50"]) if srv else None,
             "plugin_allocate_p99_ms": ms(srv["p99"]) if srv else None,
+            "allocate_breakdown_p50_ms": breakdown(cp.splits),
             "admissions": len(cp.alloc_lat), "pod_source": a.pod_source, "patch": "write-behind",
-            "apiserver_round_trips_on_path": 0}}
+            "apiserver_round_trips_on_path": round_trips(srv)}}
         if cp.ref_port:
             under_churn["reference"] = {
                 "allocate_p50_ms": ms(pct(cp.ref_lat, 0.5)), "allocate_p99_ms": ms(pct(cp.ref_lat, 0.99)),
@@ -875,13 +921,15 @@ def main():
                 "plugin_allocate_p99_ms": ms(ref_srv["p99"]) if ref_srv else None,
                 "plugin_allocate_phase_p50_ms": {k: ms(v) for k, v in ref_srv["phases"].items() if v is not None}
                 if ref_srv else None,
+                "allocate_breakdown_p50_ms": breakdown(cp.ref_splits),
                 "admissions": len(cp.ref_lat), "failed": cp.ref_failed, "pod_source": "list", "patch": "sync",
-                "apiserver_round_trips_on_path": 2}
+                "apiserver_round_trips_on_path": round_trips(ref_srv)}
         svc.stop()
         cp.stop()
         modes = mode_comparison([float(x) for x in a.compare_rtts.split(",") if x], a.compare_pods) \
             if a.compare_rtts else {}
         fills = fill_orders([x for x in a.fill_orders.split(",") if x], n, units) if a.fill_orders else {}
+        floor = transport_floor() if a.compare_rtts else None
         res = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -902,6 +950,7 @@ def main():
                        "smi_backend": smi, "pod_processes": use_gpu},
             "allocate_p50_ms": ms(pct(cp.alloc_lat, 0.5)),
             "allocate_p99_ms": ms(pct(cp.alloc_lat, 0.99)),
+            "allocate_breakdown_p50_ms": breakdown(cp.splits),
             "plugin_allocate_p50_ms": ms(srv["p50"]) if srv else None,
             "plugin_allocate_p99_ms": ms(srv["p99"]) if srv else None,
             "plugin_allocate_phase_p50_ms": {k: ms(v) for k, v in srv["phases"].items() if v is not None}
@@ -920,6 +969,10 @@ def main():
             "allocate_under_churn": under_churn,
             # the same A/B on a quiet cluster at injected apiserver RTTs
             "allocate_by_mode": modes,
+            # what the two transport legs cost with a handler that does nothing: a Python gRPC
+            # client (the fake kubelet; the real one is Go) calling a grpcio server like the
+            # plugin's, every 5 ms, nothing else running (tools/grpc_server_probe.py)
+            "allocate_transport_floor_p50_ms": floor,
             "fill_orders": fills,
             "pods_per_node": pods_node,
             "hbm_gib_per_node": gib_node,

@@ -52,12 +52,15 @@ def test_bench_torchrun_two_ranks_gloo():
     # both plugins measured under the same churn, in the same line
     uc = d["allocate_under_churn"]
     assert uc["default"]["admissions"] == uc["reference"]["admissions"] == 8
-    assert uc["reference"]["apiserver_round_trips_on_path"] == 2
+    # measured by the plugins themselves: LIST + PATCH for the reference model, none by default
+    assert uc["reference"]["apiserver_round_trips_on_path"]["p50"] == 2
+    assert uc["default"]["apiserver_round_trips_on_path"]["p99"] == 0
+    assert set(uc["default"]["allocate_breakdown_p50_ms"]) == {"kubelet_to_handler", "handler", "handler_to_kubelet"}
     assert set(d["allocate_p50_ms_by_gpu"]) == {"0", "1"}
     assert topo["tp_pair_allreduce"]["busbw_GBps"] > 0 and topo["backend"] == "gloo"
     # the control-plane A/B is in the same line: default vs the reference's cost model
     ab = d["allocate_by_mode"]
-    assert ab["reference@5ms"]["apiserver_round_trips_on_path"] == 2
+    assert ab["reference@5ms"]["apiserver_round_trips_on_path"]["p50"] == 2
     assert ab["default@5ms"]["allocate_p50_ms"] < ab["reference@5ms"]["allocate_p50_ms"]
 
 

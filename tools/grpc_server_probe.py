@@ -95,12 +95,16 @@ def main():
     ap.add_argument("--calls", type=int, default=400)
     ap.add_argument("--gap-ms", type=float, default=20.0)
     ap.add_argument("--busy-threads", type=int, default=1, help="CPU-bound threads inside the server process")
+    ap.add_argument("--models", default="sync,aio", help="server models to measure")
+    ap.add_argument("--switch-interval", type=float, default=0.00025,
+                    help="server process GIL switch interval (the plugin's default)")
     a = ap.parse_args()
     out = {}
-    for name, fn in (("sync", serve_sync), ("aio", serve_aio)):
+    models = {"sync": serve_sync, "aio": serve_aio}
+    for name, fn in ((m, models[m]) for m in a.models.split(",")):
         path = os.path.join(tempfile.mkdtemp(prefix="gsp-"), "s.sock")
         ready = mp.Event()
-        srv = mp.Process(target=_with_burners, args=(fn, path, ready, a.busy_threads), daemon=True)
+        srv = mp.Process(target=_with_burners, args=(fn, path, ready, a.busy_threads, a.switch_interval), daemon=True)
         srv.start()
         ready.wait(20)
         q = mp.Queue()
@@ -112,7 +116,8 @@ def main():
     print(json.dumps({"gap_ms": a.gap_ms, "busy_threads": a.busy_threads, **out}))
 
 
-def _with_burners(fn, path, ready, n):
+def _with_burners(fn, path, ready, n, switch_interval):
+    sys.setswitchinterval(switch_interval)
     stop = threading.Event()
     for _ in range(n):
         threading.Thread(target=burner, args=(stop,), daemon=True).start()
