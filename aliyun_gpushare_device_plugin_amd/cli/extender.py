@@ -8,7 +8,7 @@ the same annotations) plus what MI355X needs:
 
 * TP groups (pods labelled ``gpushare.amd.com/tp-group`` / ``tp-size``) get GPUs that are
   pairwise one-hop xGMI per the topology the plugin exports, reserved for the whole group when
-  its first member binds (``sim/extender.py`` ``bind_member``);
+  its first member binds (``extender/core.py`` ``bind_member``);
 * unhealthy GPUs (the plugin's health annotation) are never chosen;
 * placement follows the plugin's placement-truth rewrites (pod informer, ``update``).
 
@@ -24,7 +24,7 @@ import sys
 import threading
 
 from ..cluster.client import build_client
-from ..sim.extender import Extender, serve_http
+from ..extender import Extender, serve_http
 from ..utils import log
 
 

@@ -1,25 +1,28 @@
-"""gpushare-scheduler-extender protocol stand-in (test and bench only).
+"""gpushare-scheduler-extender protocol implementation for MI355X nodes (deployable: ``cli/extender.py``,
+``deploy/scheduler-extender.yaml``; the simulator drives the same class in-process).
 
-The real extender is a separate Go project (linked from the reference ``README.md:14``),
-not in ``/root/reference`` and not buildable here. What the plugin relies on is inferred
-from what it consumes: per-GPU capacity = node ``allocatable[gpu-mem] /
-allocatable[gpu-count]`` (the inspect arithmetic, ``cmd/inspect/nodeinfo.go:116,146``);
-the extender picks a node and a GPU index, writes ``ALIYUN_COM_GPU_MEM_IDX/_POD/
-_ASSUME_TIME`` and ``_ASSIGNED="false"``, then binds.
+The reference plugin's partner extender is a separate Go project (linked from the reference
+``README.md:14``), not in ``/root/reference`` and not buildable here. What the plugin relies on
+is inferred from what it consumes: per-GPU capacity = node ``allocatable[gpu-mem]
+/ allocatable[gpu-count]`` (the inspect arithmetic, ``cmd/inspect/nodeinfo.go:116,146``); the
+extender picks a node and a GPU index, writes ``ALIYUN_COM_GPU_MEM_IDX/_POD/_ASSUME_TIME`` and
+``_ASSIGNED="false"``, then binds.
 
 It places pods with a best-fit bin-packing policy — jointly for the queue of unscheduled pods
-it knows about (``sim/packing.py``: online best fit strands HBM when mixed sizes arrive in an
-unlucky order, the joint plan does not) — keeps its per-GPU
-ledger like the real extender's cache, and adds the MI355X capability the north star asks
-for: pods labelled ``gpushare.amd.com/tp-group=<name>`` with ``…/tp-size=<k>`` are placed
-as a group on k distinct GPUs that are pairwise one-hop xGMI per the topology annotation
-the plugin exports (``parallel/topology.py``). It also serves the extender HTTP routes
-(``/gpushare-scheduler/filter`` and ``/bind``) for protocol-level tests.
+it knows about (``extender/packing.py``: online best fit strands HBM when mixed sizes arrive in
+an unlucky order, the joint plan does not; a pod the plan leaves out only uses room the plan
+does not hold for the others) — keeps its per-GPU ledger like the real extender's cache, and
+adds the MI355X capability the north star asks for: pods labelled
+``gpushare.amd.com/tp-group=<name>`` with ``…/tp-size=<k>`` are placed as a group on k distinct
+GPUs that are pairwise one-hop xGMI per the topology annotation the plugin exports
+(``parallel/topology.py``). It serves the extender HTTP routes (``/gpushare-scheduler/filter``
+and ``/bind``).
 
 Like the real extender's pod informer, ``update(pod)`` re-accounts a pod whose annotations
 changed (the plugin's placement-truth rewrite of ``IDX`` / the allocation JSON, see
 ``alloc/placement.py``) and ``forget`` drops a deleted or finished one; ``watch()`` drives both
-from an apiserver pod watch.
+from an apiserver pod watch. The ledger holds no state of its own: a restarted extender
+rebuilds it from the pods' annotations (``sync``), placement-truth rewrites included.
 """
 from __future__ import annotations
 
@@ -53,7 +56,7 @@ class NodeState:
         return [(self.per_gpu - u) if h else -1 for u, h in zip(self.used, self.healthy)]
 
 
-class ExtenderSim:
+class Extender:
     def __init__(self, client: APIClient, policy: str = "binpack", group_ttl_s: float = 300.0):
         self.client = client
         self.policy = policy
@@ -122,7 +125,7 @@ class ExtenderSim:
             self._plan.pop(uid, None)
 
     def _replan_locked(self) -> None:
-        """Joint best placement of every queued pod onto the GPUs' free HBM (sim/packing.py)."""
+        """Joint best placement of every queued pod onto the GPUs' free HBM (extender/packing.py)."""
         if (not self.plan_enabled or self.policy != "binpack" or not self._pending
                 or all(u in self._plan for u in self._pending)):
             return
@@ -194,7 +197,7 @@ class ExtenderSim:
                 st.used[g] += mem
             self._placed[u] = (st.name, parts)
 
-    def watch(self) -> "ExtenderSim":
+    def watch(self) -> "Extender":
         """Follow pod updates and deletions from the apiserver (background thread)."""
         self._watch_stop = threading.Event()
         self._watch_holder: list = []
@@ -239,15 +242,33 @@ class ExtenderSim:
             planned = self._planned_locked(pod, names)
             if planned is not None:
                 return [planned[0]]          # the queue's joint plan put it there
-            return [n for n in names if n in self.nodes and self._fits(self.nodes[n], req)]
+            res = self._reserved_locked(O.uid(pod))
+            return [n for n in names if n in self.nodes
+                    and any(f - res.get((n, i), 0) >= req for i, f in enumerate(self.nodes[n].free()))]
 
-    def _choose(self, req: int, node_names=None) -> tuple[str, int] | None:
+    def _reserved_locked(self, uid: str) -> dict:
+        """(node, gpu) -> HBM the queue's joint plan holds for the *other* pending pods. A pod
+        the plan left out may only use what the plan leaves free: placing it by best fit into
+        a planned pod's room would undo the joint placement (and strand that pod)."""
+        if uid not in self._pending:
+            return {}
+        self._replan_locked()
+        if uid in self._plan:
+            return {}
+        out: dict = {}
+        for u, where in self._plan.items():
+            if u != uid and u in self._pending:
+                out[where] = out.get(where, 0) + O.gpu_mem_of_pod(self._pending[u])
+        return out
+
+    def _choose(self, req: int, node_names=None, reserved: dict | None = None) -> tuple[str, int] | None:
         best = None
         for name in node_names or list(self.nodes):
             st = self.nodes.get(name)
             if st is None:
                 continue
             for i, f in enumerate(st.free()):
+                f -= (reserved or {}).get((name, i), 0)
                 if f < req:
                     continue
                 left = f - req
@@ -272,7 +293,8 @@ class ExtenderSim:
         """Filter + prioritize + reserve (the scheduling cycle; in memory)."""
         req = O.gpu_mem_of_pod(pod)
         with self._lock:
-            choice = self._planned_locked(pod, node_names) or self._choose(req, node_names)
+            choice = (self._planned_locked(pod, node_names)
+                      or self._choose(req, node_names, self._reserved_locked(O.uid(pod))))
             self._drop_pending_locked(O.uid(pod))
             if choice is None:
                 return None
@@ -391,10 +413,9 @@ class ExtenderSim:
             return {n: {"per_gpu": s.per_gpu, "used": list(s.used)} for n, s in self.nodes.items()}
 
 
-Extender = ExtenderSim          # the deployable name (cli/extender.py); the class is the same
 
 
-def serve_http(ext: ExtenderSim, host: str = "127.0.0.1", port: int = 0):
+def serve_http(ext: Extender, host: str = "127.0.0.1", port: int = 0):
     """Extender HTTP endpoints: ``POST /gpushare-scheduler/filter`` (ExtenderArgs →
     ExtenderFilterResult) and ``POST /gpushare-scheduler/bind`` (ExtenderBindingArgs →
     ExtenderBindingResult)."""

@@ -6,7 +6,7 @@ each), so on a healthy UBB every pair is one hop — but a downed link, a CPX/NP
 mode or a missing GPU breaks that symmetry, and an RCCL tensor-parallel pod group placed
 across a non-xGMI pair falls back to PCIe. The plugin exports the link matrix as a node
 annotation (``gpushare.amd.com/xgmi-topology``); ``best_group`` is the placement rule a
-TP-aware extender (and ``sim/extender.py``) applies to it.
+TP-aware extender (and ``extender/core.py``) applies to it.
 """
 from __future__ import annotations
 

@@ -25,7 +25,7 @@ from ..cluster.client import APIClient, KubeConfig
 from ..plugin.manager import PluginConfig, SharedGPUManager
 from ..utils import log
 from .apiserver import FakeAPIServer, make_node
-from .extender import TP_GROUP_LABEL, TP_SIZE_LABEL, ExtenderSim
+from ..extender import TP_GROUP_LABEL, TP_SIZE_LABEL, Extender
 from .kubelet import Admission, FakeKubelet
 from .kubelet_proc import KubeletProcess
 
@@ -85,7 +85,7 @@ class SimCluster:
         self.api_url = None
         self.apiserver_latency_s = apiserver_latency_s
         self.client: APIClient | None = None
-        self.extender: ExtenderSim | None = None
+        self.extender: Extender | None = None
         self.nodes: dict[str, SimNode] = {}
         self.shim_host_dir = shim_host_dir
         self.gpu_indices = gpu_indices
@@ -143,7 +143,7 @@ class SimCluster:
             if node.manager is not None and not node.manager.started.wait(timeout):
                 raise TimeoutError(f"plugin manager on {node.name} did not finish starting")
             self._wait_capacity(node.name, timeout)
-        self.extender = ExtenderSim(self.client)
+        self.extender = Extender(self.client)
         self.extender.sync()
         return self
 

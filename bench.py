@@ -52,6 +52,7 @@ METRIC = "bin-packed pods + HBM-GiB/node; Allocate p50 latency at 1/2/4/8 MI355X
 MAIN_NODE, REF_NODE = "mi355x-node", "ref-node"
 # Per-GPU pod sizes (GiB), each pattern sums to one MI355X (288 GiB); GPU g uses pattern g % 4.
 PATTERNS = [[128, 64, 64, 32], [96, 96, 64, 32], [128, 96, 56, 8], [64, 64, 96, 64]]
+OVERSUB_SIZES = [8, 16, 32, 56, 64, 96, 128]     # GiB, the oversubscribed fill's size menu
 NATIVE = os.path.join(ROOT, "aliyun_gpushare_device_plugin_amd", "_native")
 
 
@@ -72,7 +73,8 @@ def parse():
     ap.add_argument("--compare-pods", type=int, default=24, help="admissions per A/B configuration")
     ap.add_argument("--no-ref-churn", action="store_true",
                     help="skip the reference-model node churned in lock-step with the real one")
-    ap.add_argument("--fill-orders", default="grouped,random,size_desc,size_asc,burst_random,burst_size_asc",
+    ap.add_argument("--fill-orders", default="grouped,random,size_desc,size_asc,burst_random,burst_size_asc,"
+                                             "oversub,burst_oversub",
                     help="bin-pack stress: arrival orders of the node's mixed pods through the extender; burst_* = "
                          "all pods queued first, placed jointly ('' = off)")
     ap.add_argument("--room-slack-gib", type=float, default=2.0,
@@ -383,19 +385,30 @@ def fill_orders(orders: list[str], n_gpus: int, units: int, seed: int = 0) -> di
     groups (the churn's fill: packs by construction); ``random`` = one seeded shuffle;
     ``size_desc`` / ``size_asc`` = sorted — each pod scheduled as it arrives (online best fit);
     ``burst_<order>`` = the same arrival order, but all pods are queued before the scheduler
-    runs, so the extender places the queue jointly (``sim/packing.py``). Reports pods and GiB
+    runs, so the extender places the queue jointly (``extender/packing.py``). Reports pods and GiB
     placed, the node's HBM left stranded when a pod could not be placed, and failed placements."""
     import random
 
     from aliyun_gpushare_device_plugin_amd.sim.cluster import SimCluster
 
+    import random as _random
+
     sizes = [s for g in range(n_gpus) for s in PATTERNS[g % len(PATTERNS)]]
+    cap = units * n_gpus
+    # oversubscribed mix: seeded sizes that do not sum to an exact fit, drawn until the demand
+    # is 125 % of the node's HBM (the demo's bin-pack workload at MI355X scale)
+    rng = _random.Random(seed + 1)
+    over: list[int] = []
+    while sum(over) < 1.25 * cap:
+        over.append(rng.choice(OVERSUB_SIZES))
     out = {}
     for order in orders:
-        seq = list(sizes)
         burst = order.startswith("burst_")
         base = order[len("burst_"):] if burst else order
-        if base == "random":
+        seq = list(over if base == "oversub" else sizes)
+        if base == "oversub":
+            pass                                      # arrival order = the seeded draw order
+        elif base == "random":
             random.Random(seed).shuffle(seq)
         elif base == "size_desc":
             seq.sort(reverse=True)
@@ -422,9 +435,11 @@ def fill_orders(orders: list[str], n_gpus: int, units: int, seed: int = 0) -> di
                     placed.append(sz)
         gib = sum(placed)
         out[order] = {"pods_placed": len(placed), "pods_total": len(seq), "gib_placed": gib,
-                      "packing_efficiency": round(gib / (units * n_gpus), 4) if units else None,
-                      "stranded_gib": units * n_gpus - gib if failed or admit_fail else 0,
+                      "packing_efficiency": round(gib / cap, 4) if units else None,
+                      "stranded_gib": cap - gib if failed or admit_fail else 0,
                       "failed_placements": failed, "failed_admissions": admit_fail}
+        if base == "oversub":
+            out[order]["demand_gib"] = sum(seq)
     return out
 
 
@@ -978,6 +993,10 @@ def main():
             "hbm_gib_per_node": gib_node,
             "advertised_gib_per_node": units * n,
             "packing_efficiency": round(gib_node / (units * n), 4) if units else None,
+            # the same node under 125 % demand of seeded mixed sizes (no exact fit): HBM placed /
+            # HBM advertised, online (one pod at a time) and burst (queue placed jointly)
+            "oversub_packing_efficiency": {k: (fills.get(o) or {}).get("packing_efficiency")
+                                           for k, o in (("online", "oversub"), ("burst", "burst_oversub"))},
             "hbm_held_by_pods_gib": round(sum(held) / (1 << 30), 1) if use_gpu else None,
             "quota_denials": sum(denied),
             "pod_hbm_residue_after_free_mib": round(max(residue) / (1 << 20), 1) if use_gpu else None,

@@ -11,7 +11,7 @@ import urllib.request
 from aliyun_gpushare_device_plugin_amd import const
 from aliyun_gpushare_device_plugin_amd.cluster import nodestatus, objects as O
 from aliyun_gpushare_device_plugin_amd.sim.cluster import SimCluster
-from aliyun_gpushare_device_plugin_amd.sim.extender import TP_GROUP_LABEL, TP_SIZE_LABEL
+from aliyun_gpushare_device_plugin_amd.extender import TP_GROUP_LABEL, TP_SIZE_LABEL
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 

@@ -17,7 +17,7 @@ from aliyun_gpushare_device_plugin_amd.alloc.engine import Allocator, AllocatorO
 from aliyun_gpushare_device_plugin_amd.api import v1beta1 as api
 from aliyun_gpushare_device_plugin_amd.device.model import DeviceModel
 from aliyun_gpushare_device_plugin_amd.parallel import topology as T
-from aliyun_gpushare_device_plugin_amd.sim.extender import ExtenderSim, NodeState
+from aliyun_gpushare_device_plugin_amd.extender import Extender, NodeState
 from aliyun_gpushare_device_plugin_amd.utils import units as U
 
 from .test_allocate_engine import FakeClient, StaticSource, mkpod
@@ -36,7 +36,7 @@ def _pod(uid, size):
 @given(ngpu=st.integers(1, 8), cap=st.sampled_from([8, 64, 288]),
        ops=st.lists(st.tuples(st.booleans(), st.integers(1, 160)), min_size=1, max_size=80))
 def test_extender_never_overcommits(ngpu, cap, ops):
-    ext = ExtenderSim(client=None)
+    ext = Extender(client=None)
     ext.nodes["n"] = NodeState("n", ngpu, cap, [0] * ngpu, None, [True] * ngpu)
     live, seq = [], itertools.count()
     for create, size in ops:
@@ -227,10 +227,10 @@ def test_admission_orders_keep_reservations_exact(ngpu, data):
 @settings(max_examples=200, deadline=None, suppress_health_check=[HealthCheck.too_slow])
 @given(nbins=st.integers(1, 8), data=st.data())
 def test_joint_packing_is_feasible_and_beats_best_fit(nbins, data):
-    """sim/packing.py: the joint plan never over-fills a GPU, is never worse than best fit (in
+    """extender/packing.py: the joint plan never over-fills a GPU, is never worse than best fit (in
     arrival order or decreasing), and packs everything when a perfect packing exists (items cut
     from the bins themselves, then shuffled)."""
-    from aliyun_gpushare_device_plugin_amd.sim.packing import best_fit, pack
+    from aliyun_gpushare_device_plugin_amd.extender.packing import best_fit, pack
 
     cap = data.draw(st.sampled_from([64, 288]))
     free = [cap] * nbins
@@ -270,8 +270,8 @@ def test_joint_packing_is_feasible_and_beats_best_fit(nbins, data):
 ])
 def test_zero_slack_perfect_packings_are_found(nbins, cap, sizes):
     """Pods that exactly fill every GPU (no slack): item-by-item search missed these within
-    200k expansions; bin completion (sim/packing.py place_all) finds them in a few hundred."""
-    from aliyun_gpushare_device_plugin_amd.sim.packing import pack, place_all
+    200k expansions; bin completion (extender/packing.py place_all) finds them in a few hundred."""
+    from aliyun_gpushare_device_plugin_amd.extender.packing import pack, place_all
 
     assert sum(sizes) == nbins * cap
     for got in (place_all([cap] * nbins, sizes, budget=2_000), pack([cap] * nbins, sizes, budget=4_000)):
