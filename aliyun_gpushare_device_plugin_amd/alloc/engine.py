@@ -200,6 +200,12 @@ class Allocator:
         self._prep_cache: dict[tuple, _Prepared] = {}
         self._post: "collections.deque" = collections.deque()
         self._post_mu = threading.Lock()
+        # native fast path (plugin/native_server.py): the server answers from the published
+        # table; its claims come back through _native_taken
+        self.native = None
+        self._native_prep: dict[str, _Prepared] = {}
+        self._native_hold = False                 # a block kept while a multi-container claim is open
+        self._published = (-1, -1)                # (pending version, gen) of the last native table
         for k, uid, t, resp in self.journal.answers():   # grants of a previous instance (journal TTL)
             if len(resp.container_responses) == 1:
                 self.grants.record(k, self._grant_from(resp.container_responses[0], uid, t))
@@ -243,15 +249,28 @@ class Allocator:
             if opts.ledger_dir != ledger_dir:
                 self._ledgers = self._ledger_dir(self.opts)
             self._pinfo.clear()
-            self._gen += 1
+            self._bump_gen()
             self._fast = None
             self._prep_cache.clear()
+        if self.native is not None:
+            self._hook_pods(self.native)
         return self
 
     def close(self):
         self._stop.set()
         if self._patch_q is not None:
             self._patch_q.put(None)
+
+    def _bump_gen(self) -> None:
+        """A change of engine state the prepared answers depend on (caller holds ``_mu``): the
+        native table built before it is no longer served, and the prepare loop rebuilds."""
+        self._gen += 1
+        nat = self.native
+        if nat is not None:
+            nat.set_gen(self._gen)
+        ev = getattr(self.pods, "changed", None)
+        if ev is not None:
+            ev.set()
 
     # ------------------------------------------------------------------------------------
     # candidate selection
@@ -384,7 +403,7 @@ class Allocator:
                 # never handed out again while the pod lives (no double booking of its HBM);
                 # its own admission, if it comes, is matched elsewhere or refused.
                 self._tainted[c.uid] = now
-                self._gen += 1
+                self._bump_gen()
                 self.metrics.allocate_outcomes.inc(outcome="claim_tainted")
                 log.warning("pod %s: %d/%d gpu containers answered from its reservation, then the kubelet moved on "
                             "(%s); reservation withheld", O.name(c.pod), c.next_container, len(c.shape),
@@ -524,7 +543,7 @@ class Allocator:
             self._claims.pop(c.uid, None)
             if self.pods.get(c.uid) is not None:
                 self._tainted[c.uid] = now
-                self._gen += 1
+                self._bump_gen()
                 self.metrics.allocate_outcomes.inc(outcome="claim_tainted")
         if u in self._tainted or u in self._claims or (u in self._assigned and done == 0):
             log.warning("admission identity: pod %s is being admitted but its reservation is no longer whole", O.name(p))
@@ -684,7 +703,7 @@ class Allocator:
         for the interpreter."""
         t0 = time.perf_counter()
         fast = self._fast
-        if fast is not None:
+        if fast is not None and self.native is None:
             body = self._allocate_fast(req, fast, t0, defer)
             if body is not None:
                 return body
@@ -696,7 +715,8 @@ class Allocator:
             return None
         ids = crs[0].devices_ids
         n = len(ids)
-        if n == 0 or self.journal.maybe_replay(ids[0]) or fast.version != getattr(self.pods, "version", -1):
+        if n == 0 or self.journal.maybe_replay(ids[0]) or fast.version != getattr(
+                self.pods, "pending_version", getattr(self.pods, "version", -1)):
             return None
         with self._mu:
             if fast.gen != self._gen or self._partial is not None:
@@ -735,6 +755,8 @@ class Allocator:
 
     def _drain_post(self) -> None:
         """Bookkeeping of fast-path answers, off the hot path: grant book + journal index."""
+        if self.native is not None:
+            self._drain_native()
         with self._post_mu:
             while self._post:
                 rb, c, t = self._post.popleft()
@@ -752,6 +774,8 @@ class Allocator:
             ev = getattr(src, "changed", None)
             if ev is None or not self.opts.fast_path or self.opts.compute_isolation == "cu":
                 self._fast = None
+                if self.native is not None:
+                    self.native.publish(_native_blob(0, 0, 0, [], []))   # never valid: every Allocate to the engine
                 self._stop.wait(1.0)
                 continue
             ev.wait(0.5)
@@ -763,7 +787,7 @@ class Allocator:
                 log.V(2).info("prepare answers: %s", e)
 
     def _prepare(self, src) -> None:
-        version = src.version
+        version = getattr(src, "pending_version", src.version)
         with self._mu:
             gen = self._gen
             cands = self._candidates(fresh=False)
@@ -791,20 +815,42 @@ class Allocator:
                               cr.annotations.get(const.CTR_ANNOTATION_LEDGER, ""))
             keep[k] = c
             out.append(c)
+        nat = self.native
         with self._mu:
             if gen != self._gen:          # reconfigured meanwhile: answers built from the old model
                 return
             self._prep_cache = keep
-            self._fast = _Fast(version, gen, tuple(out))
+            if nat is None:
+                self._fast = _Fast(version, gen, tuple(out))
+        if nat is not None:
+            # the native server answers from this table while the cache and the engine are still
+            # at (version, gen); a possible replay (IDs of journaled answers) goes to the engine
+            self._fast = None
+            prep = self._native_prep
+            for c in out:
+                prep[c.uid] = c
+            if len(prep) > 4096:          # only recent candidates can still come back as claims
+                for u in list(prep)[:len(prep) - 2048]:
+                    del prep[u]
+            legacy = time.time() < self.journal._legacy_until
+            nat.publish(_native_blob(version, gen, 1 if self.podres is not None else 0,
+                                     [] if legacy else out, self.journal.replay_ids()))
+            self._published = (version, gen)
         if self.journal.indexed_uids():         # replay index: only pods that can still be retried
             pend = {O.uid(p) for p in src.pending_pods()}
             self.journal.prune_index(pend)
 
     def _allocate_full(self, req, t0: float):
         """The full Allocate path, counting the apiserver round trips it makes (the handler
-        thread's requests; write-behind patches run on the patcher thread)."""
+        thread's requests; write-behind patches run on the patcher thread). With the native
+        server, its answers are blocked meanwhile and its claims taken in first, so the two
+        never hand out the same pod."""
         count = getattr(self.client, "thread_requests", None)
         n0 = count() if count else 0
+        nat = self.native
+        if nat is not None:
+            nat.block()
+            self._drain_native()
         try:
             view = getattr(self.pods, "allocate_view", None)
             with view() if view else contextlib.nullcontext():   # per-call sources: one LIST per Allocate
@@ -812,6 +858,22 @@ class Allocator:
         finally:
             if count:
                 self.metrics.allocate_requests.observe(count() - n0)
+            if nat is not None:
+                self._native_release(nat)
+
+    def _native_release(self, nat) -> None:
+        """End of a full-path Allocate: unblock the native answers — unless a multi-container
+        claim is now open, whose next containers the engine must answer (one block is kept
+        until that claim ends)."""
+        with self._mu:
+            open_claim = self._partial is not None
+        if open_claim and not self._native_hold:
+            self._native_hold = True
+            return
+        nat.unblock()
+        if not open_claim and self._native_hold:
+            self._native_hold = False
+            nat.unblock()
 
     def _allocate_full_in(self, req, t0: float):
         sizes = tuple(len(c.devices_ids) for c in req.container_requests)
@@ -840,6 +902,8 @@ class Allocator:
                     self._revoked.discard(claim.uid)
                     if complete:
                         self._claims[claim.uid] = claim   # held across the PATCH
+                    if self.native is not None:
+                        self.native.take(claim.uid)      # never answered from the table again
                 t2 = time.perf_counter()
             hist.observe(ta - t0, phase="prelude")      # request key, journal replay check
             hist.observe(tl - ta, phase="identity")     # pod-resources List (ambiguous requests only)
@@ -1019,7 +1083,7 @@ class Allocator:
                 if self._overlay_gen.get(job.uid) == job.gen:
                     self._overlay.pop(job.uid, None)
                     self._overlay_gen.pop(job.uid, None)
-                    self._gen += 1
+                    self._bump_gen()
             return
         self.journal.landed(job.uid)
         with self._mu:
@@ -1076,6 +1140,8 @@ class Allocator:
                     continue
                 self._unpatched.add(u)
                 self._assigned[u] = time.monotonic()
+                if self.native is not None:
+                    self.native.take(u)
             self._patch_q.put(_PatchJob(u, O.namespace(p), O.name(p), self._extra_annotations(u), recovered=True))
             self.metrics.allocate_outcomes.inc(outcome="patch_reconciled")
             log.warning("reconcile: pod %s answered by this plugin still reads ASSIGNED=false; patching", O.name(p))
@@ -1085,6 +1151,99 @@ class Allocator:
     # ------------------------------------------------------------------------------------
     # placement truth (alloc/placement.py)
     # ------------------------------------------------------------------------------------
+    # ------------------------------------------------------------------------------------
+    # native fast path (plugin/native_server.py, native/dpserver)
+    # ------------------------------------------------------------------------------------
+    def attach_native(self, nat) -> None:
+        """Serve the fast path from the native server ``nat``: the prepare loop publishes its
+        table there instead of answering here, and the server's claims come back through
+        ``_native_taken``. Its journal records go to ``<journal>.fast`` (loaded with the journal)."""
+        self.native = nat
+        with self._mu:
+            self._fast = None
+            nat.set_gen(self._gen)
+        self._hook_pods(nat)
+        if self.journal.path:
+            # loaded and compacted into the main journal at start-up: the fast file starts empty
+            nat.journal_open(self.journal.fast_path(), 32 << 20)
+            nat.journal_rotate()
+        threading.Thread(target=self._native_loop, args=(nat,), name="native-claims", daemon=True).start()
+        ev = getattr(self.pods, "changed", None)
+        if ev is not None:
+            ev.set()
+
+    def detach_native(self) -> None:
+        nat, self.native = self.native, None
+        if nat is not None:
+            self._drain_native(nat)
+            src = self.pods
+            if getattr(src, "on_pending_change", None) is not None:
+                src.on_pending_change = None
+            if self._native_hold:
+                self._native_hold = False
+
+    def _hook_pods(self, nat) -> None:
+        src = self.pods
+        if hasattr(src, "on_pending_change"):
+            with src._lock:
+                src.on_pending_change = nat.set_version
+                nat.set_version(src.pending_version)
+
+    def _native_loop(self, nat) -> None:
+        """Takes in the native server's claims as they happen; rotates its journal file once
+        the engine's own journal holds everything it has."""
+        while not self._stop.is_set() and self.native is nat:
+            rec = nat.taken_next(200)
+            if rec is None:
+                break
+            if rec:
+                self._native_taken(rec)
+            if self.journal.path and nat.journal_used() > (16 << 20):
+                nat.block()
+                try:
+                    self._drain_native(nat)
+                    self._drain_post()
+                    self.journal.compact()
+                    nat.journal_rotate()
+                finally:
+                    nat.unblock()
+
+    def _drain_native(self, nat=None) -> None:
+        nat = nat or self.native
+        if nat is None:
+            return
+        while True:
+            rec = nat.taken_next(0)
+            if not rec:
+                return
+            self._native_taken(rec)
+
+    def _native_taken(self, rec) -> None:
+        """One native answer: the same claim and bookkeeping as the engine's fast path."""
+        uid, rb, t, hns = rec
+        pick = self._native_prep.get(uid)
+        with self._mu:
+            self._assigned[uid] = time.monotonic()
+            self._unpatched.add(uid)
+            self._revoked.discard(uid)
+            self._answer_seq += 1
+        if pick is None:     # never: the server only answers from a table the engine published
+            log.error("native fast path answered pod uid %s that no published table holds", uid)
+            return
+        req = api.AllocateRequest.FromString(rb)
+        ids = req.container_requests[0].devices_ids
+        self.journal.note_fast(uid, pick.ns, pick.name, t, ids)
+        self._post.append((rb, pick, t))
+        log.info("----Allocating GPU for gpu mem is started---- RequestPodGPUs: %d; pod %s, new allocated GPUs info: "
+                 "gpu index %d uuid %s (patch queued, native)", len(ids), pick.name, pick.gpu,
+                 self.model.uuid_by_index(pick.gpu))
+        self.metrics.allocate_outcomes.inc(outcome="assigned")
+        self.metrics.allocate_latency.observe(hns / 1e9, phase="total")
+        self.metrics.allocate_latency.observe(hns / 1e9, phase="native")
+        self.metrics.allocate_requests.observe(0)
+        if self._patch_q is not None:
+            self._patch_q.put(_PatchJob(uid, pick.ns, pick.name, {}))
+
     def set_pod_resources(self, src) -> None:
         """Attach the kubelet's pod-resources view (``api.podresources.PodResourcesClient`` or
         any object with ``list() -> [PodDevices]``) and start the periodic placement pass."""
@@ -1151,6 +1310,8 @@ class Allocator:
         watchdog kills only settled pods (quota/watchdog.py)."""
         if self.podres is None or self._post or self._placed_at < self._last_grant:
             return False
+        if self.native is not None and self.native.pending():
+            return False
         with self._mu:
             return uid not in self._overlay and uid not in self._unpatched and uid not in self._claims
 
@@ -1173,7 +1334,7 @@ class Allocator:
             gen = self._overlay_gen.get(f.uid, 0) + 1
             self._overlay_gen[f.uid] = gen
             self._overlay[f.uid] = dict(self._overlay.get(f.uid) or {}, **ann)
-            self._gen += 1
+            self._bump_gen()
             if f.assigned is True:
                 self._assigned[f.uid] = time.monotonic()
                 self._revoked.discard(f.uid)
@@ -1283,6 +1444,21 @@ class _PatchJob:
     recovered: bool = False
     kind: str = "assign"   # "assign" (ASSIGNED=true after an answer) | "placement" (truth fix)
     gen: int = 0           # placement: overlay generation this job lands
+
+
+def _native_blob(version: int, gen: int, flags: int, cands, replay_ids) -> bytes:
+    """The fast table in the native server's format (native/dpserver/dpserver.cpp "table
+    blob"): the prepared candidates in match order, then the fake IDs of possible replays."""
+    import struct
+
+    def s(b):
+        b = b if isinstance(b, bytes) else b.encode()
+        return struct.pack("<I", len(b)) + b
+    parts = [struct.pack("<QQIII", version, gen, flags, len(cands), len(replay_ids))]
+    for c in cands:
+        parts += [struct.pack("<IB", c.size, 1 if c.multi else 0), s(c.uid), s(c.body), s(c.head)]
+    parts += [s(i) for i in replay_ids]
+    return b"".join(parts)
 
 
 def env_shim_host_dir() -> str | None:

@@ -74,14 +74,28 @@ class AllocJournal:
             self._load()
 
     # -- persistence ------------------------------------------------------------------------
-    def _load(self):
+    def fast_path(self) -> str:
+        """The native server's journal file (native/dpserver): its Allocate answers, in the
+        same record format, written before each reply."""
+        return self.path + ".fast"
+
+    @staticmethod
+    def _read_records(path: str) -> list[str] | None:
         try:
-            with open(self.path, "rb") as f:
+            with open(path, "rb") as f:
                 raw = f.read()
         except FileNotFoundError:
-            return
+            return None
         end = raw.find(b"\0")                 # the mapped file's unused tail is zero
-        lines = (raw if end < 0 else raw[:end]).decode(errors="replace").splitlines()
+        return (raw if end < 0 else raw[:end]).decode(errors="replace").splitlines()
+
+    def _load(self):
+        main = self._read_records(self.path)
+        fast = self._read_records(self.fast_path())
+        if main is None and fast is None:
+            return
+        # the native answers first: a "landed" record in the main file then closes their patch
+        lines = (fast or []) + (main or [])
         now = time.time()
         for line in lines:
             try:
@@ -229,6 +243,26 @@ class AllocJournal:
     def indexed_uids(self) -> list[str]:
         with self._lock:
             return list(self._ids_of)
+
+    def replay_ids(self) -> list[str]:
+        """Every fake ID ``maybe_replay`` answers True for (the native fast table's replay set)."""
+        with self._lock:
+            return list(self._by_id)
+
+    def note_fast(self, pod_uid: str, ns: str, name: str, t: float, ids) -> None:
+        """A native-server answer (its record is already in the fast file): the in-memory state
+        ``record_fast`` would have set."""
+        pend = {"op": "patch", "uid": pod_uid, "ns": ns, "name": name, "ann": {}, "t": t}
+        with self._lock:
+            for i in ids:
+                self._by_id.setdefault(i, "")
+            self._uids[pod_uid] = t
+            self._pending[pod_uid] = pend
+
+    def compact(self) -> None:
+        """Rewrite the live records now (the native fast file is then redundant)."""
+        with self._lock:
+            self._compact()
 
     # -- answers ----------------------------------------------------------------------------
     def record(self, req, pod_uid: str, resp, key: str | None = None) -> None:

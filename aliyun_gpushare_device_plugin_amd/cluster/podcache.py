@@ -166,6 +166,12 @@ class WatchCache(PodSource):
         # bumped on every change of the cached set; ``changed`` wakes consumers that precompute
         # from the cache (the Allocate engine's prepared answers)
         self.version = 0
+        # bumped only when the Pending subset changes (what Allocate candidates are made of);
+        # ``on_pending_change(version)`` runs under the cache lock at every bump, so a consumer
+        # that answers from precomputed state (the native Allocate fast path) never sees the
+        # cache ahead of the version it was told
+        self.pending_version = 0
+        self.on_pending_change = None
         self.changed = threading.Event()
         self._synced = threading.Event()
         self._stop = threading.Event()
@@ -195,6 +201,7 @@ class WatchCache(PodSource):
             self._pending = {u: p for u, p in self._pods.items() if O.phase(p) == "Pending"}
             self._rv = rv
             self.version += 1
+            self._pending_bump()
         self.changed.set()
         self.relists += 1
         self._synced.set()
@@ -211,7 +218,8 @@ class WatchCache(PodSource):
         with self._lock:
             if typ == "DELETED" or O.node_name(obj) != self.node:
                 self._pods.pop(u, None)
-                self._pending.pop(u, None)
+                if self._pending.pop(u, None) is not None:
+                    self._pending_bump()
                 self.version += 1
             else:
                 cur = self._pods.get(u)
@@ -258,13 +266,21 @@ class WatchCache(PodSource):
         with self._lock:
             return list(self._pending.values())
 
+    def _pending_bump(self) -> None:
+        """Caller holds the cache lock."""
+        self.pending_version += 1
+        hook = self.on_pending_change
+        if hook is not None:
+            hook(self.pending_version)
+
     def _put(self, u: str, pod: dict) -> None:
         self.version += 1
         self._pods[u] = pod
         if O.phase(pod) == "Pending":
             self._pending[u] = pod
-        else:
-            self._pending.pop(u, None)
+            self._pending_bump()
+        elif self._pending.pop(u, None) is not None:
+            self._pending_bump()
 
     def observe(self, pod: dict) -> None:
         if not pod or O.node_name(pod) != self.node:

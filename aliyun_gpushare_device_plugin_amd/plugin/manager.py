@@ -84,6 +84,9 @@ class PluginConfig:
     dmem_limits: str = "auto"            # quota/dmem.py: kernel dmem.max per pod cgroup when available | off
     cgroup_root: str = "/sys/fs/cgroup"
     mps: bool = False                    # accepted for flag compatibility; ignored
+    # DevicePlugin gRPC server: "native" (libgpushare_dpserver, Allocate fast path in C++),
+    # "python" (grpcio), "auto" = native when the library loads
+    grpc_server: str = "auto"
 
 
 class SharedGPUManager:
@@ -191,8 +194,23 @@ class SharedGPUManager:
         if allocator.podres is None:
             allocator.set_pod_resources(self._pod_resources())
         self.model = model
-        return DevicePluginServer(model, allocator, self._plugin_socket(), const.RESOURCE_NAME,
-                                  cfg.preferred_allocation, self.metrics)
+        return self._server_class()(model, allocator, self._plugin_socket(), const.RESOURCE_NAME,
+                                    cfg.preferred_allocation, self.metrics)
+
+    def _server_class(self):
+        mode = self.cfg.grpc_server
+        if mode == "python":
+            return DevicePluginServer
+        from .native_server import NativeDevicePluginServer, load
+
+        try:
+            load()
+        except Exception as e:  # noqa: BLE001
+            if mode == "native":
+                raise
+            log.warning("native device-plugin server unavailable (%s): serving with grpcio", e)
+            return DevicePluginServer
+        return NativeDevicePluginServer
 
     def readiness(self) -> tuple[bool, str]:
         """``/readyz``: serving and registered, with health detection at full strength (SMI

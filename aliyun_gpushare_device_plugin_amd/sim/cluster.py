@@ -60,7 +60,7 @@ class SimCluster:
                  extra_plugin_args: list[str] | None = None, apiserver: str = "thread",
                  preferred_allocation: bool = False, compute_isolation: str = "none", kubelet: str = "thread",
                  placement_truth: bool = True, node_overrides: dict | None = None,
-                 admission_identity: bool = True):
+                 admission_identity: bool = True, grpc_server: str = "auto"):
         self.node_specs = nodes
         # kubelet: "thread" (FakeKubelet in this interpreter) or "process" (its own interpreter,
         # sim/kubelet_proc.py, so kubelet-side Allocate timing is not inflated by this process's GIL)
@@ -68,6 +68,7 @@ class SimCluster:
         # per-node plugin settings: {node: {"pod_source": ..., "extra_args": [...]}} (e.g. a second
         # node running the reference's cost model next to the default one, bench.py)
         self.node_overrides = node_overrides or {}
+        self.grpc_server = grpc_server
         # the fake kubelet serves pod-resources; the plugin uses it for placement truth
         self.placement_truth = placement_truth
         self.admission_identity = admission_identity
@@ -157,7 +158,7 @@ class SimCluster:
                             health_poll_s=self.health_poll_s, round_policy=self.round_policy,
                             preferred_allocation=self.preferred_allocation,
                             compute_isolation=self.compute_isolation, pod_resources_socket=self._podres(node),
-                            admission_identity=self.admission_identity,
+                            admission_identity=self.admission_identity, grpc_server=self.grpc_server,
                             **self._kubelet_cfg(node))
 
     def _podres(self, node: SimNode) -> str:
@@ -185,7 +186,8 @@ class SimCluster:
             if self.compute_isolation != "none":
                 args += ["--compute-isolation", self.compute_isolation]
             args += ["--pod-resources-socket", self._podres(node),
-                     "--admission-identity", "true" if self.admission_identity else "false"]
+                     "--admission-identity", "true" if self.admission_identity else "false",
+                     "--grpc-server", self.grpc_server]
             for k, v in self._kubelet_cfg(node).items():
                 args += ["--" + k.replace("_", "-"), str(v)]
             ov = self.node_overrides.get(node.name, {})
@@ -284,6 +286,7 @@ class SimCluster:
         if not O.node_name(pod):
             pod = self.client.get_pod(O.namespace(pod), O.name(pod))
         node = self.nodes[O.node_name(pod)]
+        self._watch_delivered(node, pod)
         adm = node.kubelet.admit(pod)
         if adm.error is None:
             ns, nm = O.namespace(pod), O.name(pod)
@@ -292,6 +295,25 @@ class SimCluster:
             else:
                 self.client.patch_pod_status(ns, nm, {"status": {"phase": "Running"}})
         return adm
+
+    @staticmethod
+    def _watch_delivered(node, pod: dict, timeout: float = 2.0) -> None:
+        """The kubelet admits a pod once its own apiserver watch delivered the binding — the
+        same event stream the plugin's pod informer reads, so the plugin has (nearly always)
+        seen it too. The harness hands the kubelet the bound object straight from the bind
+        call; with the plugin in this process, wait until its informer has the binding as well
+        (a kubelet that outruns the informer is the watch-lag case, covered by the full path's
+        fresh LIST and by placement truth)."""
+        src = getattr(getattr(node.manager, "allocator", None), "pods", None)
+        if src is None or not hasattr(src, "pending_version"):
+            return
+        u = O.uid(pod)
+        t = time.monotonic() + timeout
+        while time.monotonic() < t:
+            p = src.get(u)
+            if p is not None and O.node_name(p):
+                return
+            time.sleep(0.0005)
 
     def wait_assigned(self, pod: dict, timeout: float = 10.0) -> dict:
         """Wait until the plugin's (write-behind) ASSIGNED=true patch is visible."""

@@ -19,6 +19,7 @@ BUILD_SCRIPT = os.path.join(REPO_ROOT, "native", "build.py")
 LIBS = {
     "gpuinfo": "libgpushare_gpuinfo.so",
     "hipshim": "libgpushare_hipquota.so",
+    "dpserver": "libgpushare_dpserver.so",
     "kernels": "libgpushare_kernels.so",
 }
 
@@ -38,7 +39,7 @@ def lib_path(target: str) -> str:
     return os.path.join(NATIVE_DIR, LIBS[target])
 
 
-SOURCES = {"gpuinfo": "gpuinfo", "hipshim": "hipshim", "kernels": "kernels"}   # native/<dir>
+SOURCES = {"gpuinfo": "gpuinfo", "hipshim": "hipshim", "dpserver": "dpserver", "kernels": "kernels"}   # native/<dir>
 
 
 def stale(target: str, path: str) -> bool:

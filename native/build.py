@@ -4,6 +4,7 @@
 Targets
   gpuinfo   libgpushare_gpuinfo.so + gpushare-smi (C++17, host only; librocm_smi64 is dlopen'ed)
   hipshim   libgpushare_hipquota.so  (C++17 LD_PRELOAD interposer over the HIP allocation API)
+  dpserver  libgpushare_dpserver.so  (C++17 DevicePlugin gRPC server over libnghttp2, native Allocate fast path)
   kernels   libgpushare_kernels.so   (hand-written HIP/CDNA4 kernels, hipcc --offload-arch=gfx950)
   probes    shim_probe               (HIP test helper run under the quota shim on hardware)
 
@@ -115,6 +116,39 @@ def build_hipshim(force=False, asan=False):
     return [lib]
 
 
+def _nghttp2_include():
+    """Directory holding nghttp2/nghttp2.h (the dev headers, or the copy a Python distribution
+    ships); the library itself is the system's libnghttp2.so.14."""
+    for d in (os.environ.get("NGHTTP2_INCLUDE", ""), "/usr/include", "/usr/local/include", "/opt/conda/include"):
+        if d and os.path.exists(os.path.join(d, "nghttp2", "nghttp2.h")):
+            return d
+    return None
+
+
+def build_dpserver(force=False, asan=False):
+    """libgpushare_dpserver.so: the DevicePlugin gRPC server with the native Allocate fast path
+    (C++17 over libnghttp2)."""
+    d = _src("dpserver")
+    src = _src("dpserver", "dpserver.cpp")
+    inc = _nghttp2_include()
+    if not os.path.exists(src):
+        return []
+    if inc is None:
+        print("dpserver: nghttp2/nghttp2.h not found (set NGHTTP2_INCLUDE); skipped", flush=True)
+        return []
+    lib = os.path.join(OUT, "libgpushare_dpserver.so")
+    flags = ["-std=c++17", "-O2", "-fPIC", "-Wall", "-Wextra", "-Wno-unused-parameter", f"-I{d}",
+             f"-I{inc}", "-fvisibility=hidden", "-fvisibility-inlines-hidden"]
+    san = _san(asan)
+    if san:
+        flags += SANITIZERS[san]
+        lib = os.path.join(OUT, san, "libgpushare_dpserver.so")
+    os.makedirs(os.path.dirname(lib), exist_ok=True)
+    if force or _newer(lib, [src] + _headers(d)):
+        _run([CXX, *flags, "-shared", "-o", lib, src, "-l:libnghttp2.so.14", "-pthread"])
+    return [lib]
+
+
 def build_kernels(force=False, asan=False, jobs=4):
     d = _src("kernels")
     srcs = sorted(os.path.join(d, f) for f in os.listdir(d) if f.endswith(".hip")) if os.path.isdir(d) else []
@@ -158,7 +192,8 @@ def build_probes(force=False, asan=False):
     return out
 
 
-TARGETS = {"gpuinfo": build_gpuinfo, "hipshim": build_hipshim, "kernels": build_kernels, "probes": build_probes}
+TARGETS = {"gpuinfo": build_gpuinfo, "hipshim": build_hipshim, "dpserver": build_dpserver, "kernels": build_kernels,
+           "probes": build_probes}
 
 
 def build(targets=None, force=False, asan=False, jobs=4):

@@ -4,6 +4,7 @@
 Reference: ``allocate.go:132-152`` answers only after the PATCH landed; this build answers
 first and journals the pending PATCH (``alloc/journal.py``).
 """
+import os
 import time
 
 from aliyun_gpushare_device_plugin_amd import const
@@ -34,7 +35,10 @@ def test_killed_plugin_lands_pending_patch_after_restart(tmp_path):
         assert adm_a.error is None and idx(adm_a) == where_a[1]
         time.sleep(0.3)                     # the patcher is retrying against the outage
         assert O.annotations(c.client.get_pod("default", "a"))[const.ENV_ASSIGNED_FLAG] == "false"
-        assert any('"op":"answer+patch"' in ln for ln in open(journal))
+        # the answer + pending patch record: in the journal, or (native server) in its fast file
+        recs = [ln for f in (journal, journal + ".fast") if os.path.exists(f)
+                for ln in open(f, errors="replace")]
+        assert any('"op":"answer+patch"' in ln for ln in recs)
         # the kubelet has not reported A Running yet: A still looks like an assumed Pending pod
         c.client.patch_pod_status("default", "a", {"status": {"phase": "Pending"}})
         c.kill_plugin("n")

@@ -6,6 +6,8 @@ of the request's size, appends its journal record to the mapped file and returns
 """
 import time
 
+import pytest
+
 from aliyun_gpushare_device_plugin_amd import const
 from aliyun_gpushare_device_plugin_amd.alloc.journal import AllocJournal
 from aliyun_gpushare_device_plugin_amd.api import v1beta1 as api
@@ -13,15 +15,27 @@ from aliyun_gpushare_device_plugin_amd.cluster import objects as O
 from aliyun_gpushare_device_plugin_amd.sim.cluster import SimCluster
 
 
+SERVERS = ["python", "native"]    # grpcio + the engine's fast path; libgpushare_dpserver's table
+
+
 def _settle(al, timeout=5.0):
-    """Wait until the prepared answers match the pod cache."""
+    """Wait until the prepared answers match the pod cache (the engine's own table, or the one
+    published to the native server)."""
     t = time.monotonic() + timeout
     while time.monotonic() < t:
-        f = al._fast
-        if f is not None and f.version == al.pods.version and f.gen == al._gen:
-            return True
+        if al.native is not None:
+            if al._published == (al.pods.pending_version, al._gen):
+                return True
+        else:
+            f = al._fast
+            if f is not None and f.version == al.pods.pending_version and f.gen == al._gen:
+                return True
         time.sleep(0.005)
     return False
+
+
+def _fast_count(al):
+    return al.metrics.allocate_latency.count(phase="native" if al.native is not None else "fast")
 
 
 def _envs(r):
@@ -30,15 +44,16 @@ def _envs(r):
     return e
 
 
-def test_fast_path_answers_like_the_full_path(tmp_path):
-    with SimCluster([("n", "fake:2x16G")], shim_host_dir=str(tmp_path)) as c:
+@pytest.mark.parametrize("server", SERVERS)
+def test_fast_path_answers_like_the_full_path(tmp_path, server):
+    with SimCluster([("n", "fake:2x16G")], shim_host_dir=str(tmp_path), grpc_server=server) as c:
         al = c.manager("n").allocator
         pods = [c.create_pod(s, name=f"p{i}") for i, s in enumerate((4, 8))]
         places = [c.schedule(p) for p in pods]
         assert _settle(al)
         adm = c.admit(pods[0])
         assert adm.error is None
-        assert al.metrics.allocate_latency.count(phase="fast") == 1
+        assert _fast_count(al) == 1
         env = _envs(adm.responses[0])
         assert env[const.ENV_RESOURCE_INDEX] == str(places[0][1])
         assert env[const.ENV_RESOURCE_BY_CONTAINER] == env[const.ENV_RESOURCE_BY_POD] == "4"
@@ -48,28 +63,30 @@ def test_fast_path_answers_like_the_full_path(tmp_path):
         # the same pod answered by the full path (fast path off) carries the same envs
         al.opts.fast_path = False
         al._fast = None
+        time.sleep(1.2)                        # the prepare loop publishes an empty native table
         adm2 = c.admit(pods[1])
-        assert al.metrics.allocate_latency.count(phase="fast") == 1
+        assert _fast_count(al) == 1
         assert _envs(adm2.responses[0])[const.ENV_RESOURCE_INDEX] == str(places[1][1])
         assert set(_envs(adm2.responses[0])) == set(env)
 
 
-def test_fast_path_defers_to_identity_on_ambiguity():
+@pytest.mark.parametrize("server", SERVERS)
+def test_fast_path_defers_to_identity_on_ambiguity(server):
     """Two pending pods of the same size: the fast path steps aside and admission identity
     (pod-resources) gives the kubelet's pod its own reservation."""
-    with SimCluster([("n", "fake:2x8G")]) as c:
+    with SimCluster([("n", "fake:2x8G")], grpc_server=server) as c:
         al = c.manager("n").allocator
         a, b = c.create_pod(8, name="a"), c.create_pod(8, name="b")
         assert c.schedule(a)[1] == 0 and c.schedule(b)[1] == 1
         assert _settle(al)
         adm = c.admit(b)
         assert int(adm.responses[0].envs[const.ENV_RESOURCE_INDEX]) == 1
-        assert al.metrics.allocate_latency.count(phase="fast") == 0
+        assert _fast_count(al) == 0
         assert al.metrics.allocate_outcomes.value(outcome="identified") == 1
         assert _settle(al)
         adm = c.admit(a)                       # now unambiguous: fast
         assert int(adm.responses[0].envs[const.ENV_RESOURCE_INDEX]) == 0
-        assert al.metrics.allocate_latency.count(phase="fast") == 1
+        assert _fast_count(al) == 1
 
 
 def test_fast_records_survive_a_crash(tmp_path):

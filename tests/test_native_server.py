@@ -1,0 +1,299 @@
+"""The native DevicePlugin server (native/dpserver, plugin/native_server.py).
+
+A grpcio client (the same HTTP/2 + gRPC stack the fake kubelet uses; the real kubelet's is
+grpc-go) drives every RPC; the Allocate fast table is exercised directly with published tables
+to pin each rule under which the server must leave an Allocate to the engine, and under load
+(every prepared answer handed out at most once)."""
+import collections
+import json
+import os
+import subprocess
+import sys
+import threading
+import time
+
+import grpc
+import pytest
+
+from aliyun_gpushare_device_plugin_amd import const
+from aliyun_gpushare_device_plugin_amd.alloc.engine import Allocator, AllocatorOptions, _native_blob
+from aliyun_gpushare_device_plugin_amd.alloc.journal import AllocJournal
+from aliyun_gpushare_device_plugin_amd.api import v1beta1 as api
+from aliyun_gpushare_device_plugin_amd.device.model import DeviceModel
+from aliyun_gpushare_device_plugin_amd.plugin.native_server import NativeDevicePluginServer
+
+from .test_allocate_engine import FakeClient, StaticSource, mkpod
+from .test_units_and_model import gpu
+
+Cand = collections.namedtuple("Cand", "size multi uid body head")
+
+
+class VSource(StaticSource):
+    def __init__(self, pods):
+        super().__init__(pods)
+        self.version = self.pending_version = 1
+        self.changed = threading.Event()
+        self.on_pending_change = None
+        self._lock = threading.Lock()
+
+
+def _server(tmp_path, pods=(), strict=False, journal=True, **opts):
+    model = DeviceModel([gpu(i, 8 << 30) for i in range(2)], const.GIB)
+    src = VSource(list(pods))
+    o = AllocatorOptions(async_patch=True, strict=strict, fast_path=False,
+                         journal_path=str(tmp_path / "j.jsonl") if journal else None, **opts)
+    al = Allocator(model, src, FakeClient(src), "node-a", o)
+    srv = NativeDevicePluginServer(model, al, str(tmp_path / "dp.sock"))
+    srv.start()
+    return srv, al, src
+
+
+def _stub(srv):
+    ch = grpc.insecure_channel(api.unix_target(srv.socket))
+    return ch, api.Stub(ch, "DevicePlugin")
+
+
+def _req(*ids):
+    return api.AllocateRequest(container_requests=[api.ContainerAllocateRequest(devices_ids=list(ids))])
+
+
+def _resp(gpu_idx, tag=""):
+    r = api.AllocateResponse()
+    r.container_responses.add(envs={const.ENV_RESOURCE_INDEX: str(gpu_idx), "TAG": tag})
+    return r.SerializeToString()
+
+
+def _table(srv, cands, version=1, gen=0, flags=0, replay=()):
+    nat = srv.fast
+    nat.set_version(version)
+    nat.set_gen(gen)
+    nat.publish(_native_blob(version, gen, flags, [Cand(*c) for c in cands], list(replay)))
+
+
+def _cand(uid, size, g=0, multi=False):
+    body = _resp(g, uid)
+    return (size, multi, uid, body, AllocJournal.fast_head(uid, "default", uid, body))
+
+
+def test_every_rpc_over_the_native_server(tmp_path):
+    srv, al, src = _server(tmp_path, [mkpod("p", 2, 1, 10)])
+    ch, stub = _stub(srv)
+    try:
+        opts = stub.GetDevicePluginOptions(api.Empty())
+        assert opts == srv.options()
+        law = stub.ListAndWatch(api.Empty())
+        first = next(law)
+        assert len(first.devices) == 16 and {d.health for d in first.devices} == {const.HEALTHY}
+        srv.model.set_health(1, False, "test")                   # re-sent on a health change
+        second = next(law)
+        assert sum(d.health == const.UNHEALTHY for d in second.devices) == 8
+        law.cancel()
+        # an Allocate no table answers goes to the engine (full path) and comes back
+        resp, call = stub.Allocate.with_call(_req("GPU-x-_-0", "GPU-x-_-1"))
+        assert resp.container_responses[0].envs[const.ENV_RESOURCE_INDEX] == "1"
+        stamp = dict(call.trailing_metadata())[const.HANDLER_STAMP_KEY]
+        t_in, t_out = (int(x) for x in stamp.split(","))
+        assert 0 < t_out - t_in < 5e9
+        assert stub.PreStartContainer(api.PreStartContainerRequest(devices_ids=["GPU-x-_-0"])) == \
+            api.PreStartContainerResponse()
+        pr = stub.GetPreferredAllocation(api.PreferredAllocationRequest(container_requests=[
+            api.ContainerPreferredAllocationRequest(available_deviceIDs=["a", "b", "c"], allocation_size=2)]))
+        assert len(pr.container_responses[0].deviceIDs) == 2
+        bad = ch.unary_unary("/v1beta1.DevicePlugin/NoSuchMethod", request_serializer=lambda b: b,
+                             response_deserializer=lambda b: b)
+        with pytest.raises(grpc.RpcError) as e:
+            bad(b"")
+        assert e.value.code() == grpc.StatusCode.UNIMPLEMENTED
+        st = srv.stats()
+        assert st["forwarded"] >= 3 and st["connections"] >= 1 and st["law_sends"] >= 2
+    finally:
+        ch.close()
+        srv.stop()
+
+
+def test_strict_failure_is_failed_precondition(tmp_path):
+    srv, al, src = _server(tmp_path, [], strict=True)
+    ch, stub = _stub(srv)
+    try:
+        with pytest.raises(grpc.RpcError) as e:
+            stub.Allocate(_req("GPU-x-_-0"))
+        assert e.value.code() == grpc.StatusCode.FAILED_PRECONDITION and "no-gpu-has-1" in e.value.details()
+    finally:
+        ch.close()
+        srv.stop()
+
+
+def test_fast_table_rules(tmp_path):
+    """The server answers from the table only when the engine would: current version and
+    generation, no possible replay, unblocked, the first unclaimed candidate of the size a
+    single-container pod, and — with admission identity — the only one."""
+    srv, al, src = _server(tmp_path)
+    ch, stub = _stub(srv)
+    al.detach_native()                 # drive the table by hand; claims are read below
+    time.sleep(0.3)                    # the engine's claim reader has noticed
+    nat = srv.fast
+    nat.lib.gs_dp_set_fast_wait_us(nat.h, 0)
+
+    def tag(r):
+        return r.container_responses[0].envs["TAG"]
+
+    def engine(r):                       # the handler threads answer what the table declines
+        return r.container_responses[0].envs.get("TAG") is None
+
+    try:
+        _table(srv, [_cand("a", 2, 0), _cand("b", 2, 1), _cand("c", 3, 1)])
+        assert tag(stub.Allocate(_req("i1", "i2"))) == "a"             # first of its size
+        assert tag(stub.Allocate(_req("i3", "i4"))) == "b"             # a is claimed now
+        assert tag(stub.Allocate(_req("j1", "j2", "j3"))) == "c"
+        assert engine(stub.Allocate(_req("k1", "k2")))                 # none left of size 2
+        # a kubelet retry of answered IDs is a replay: the engine decides
+        _table(srv, [_cand("d", 2, 0)], version=2)
+        assert engine(stub.Allocate(_req("i2", "i1")))
+        assert tag(stub.Allocate(_req("m1", "m2"))) == "d"
+        # the table's cache version / engine generation moved on
+        _table(srv, [_cand("e", 1)], version=3)
+        nat.set_version(4)
+        assert engine(stub.Allocate(_req("n1")))
+        nat.set_gen(1)
+        _table(srv, [_cand("e", 1)], version=4, gen=1)
+        nat.block()
+        assert engine(stub.Allocate(_req("n2")))                       # a full-path Allocate runs
+        nat.unblock()
+        nat.take("e")                                                  # the engine claimed e itself
+        assert engine(stub.Allocate(_req("n3")))
+        # journaled answers' IDs (replay set published with the table)
+        _table(srv, [_cand("f", 1)], version=5, gen=1, replay=["z1"])
+        assert engine(stub.Allocate(_req("z1")))
+        # a multi-container pod first in line; identity ambiguity
+        _table(srv, [_cand("g", 1, multi=True), _cand("h", 1)], version=6, gen=1)
+        assert engine(stub.Allocate(_req("q1")))
+        _table(srv, [_cand("h", 1), _cand("i", 1)], version=7, gen=1, flags=1)
+        assert engine(stub.Allocate(_req("q2")))
+        _table(srv, [_cand("h", 1), _cand("i", 1)], version=8, gen=1, flags=0)
+        assert tag(stub.Allocate(_req("q3"))) == "h"
+        # two containers in one request: the engine
+        two = api.AllocateRequest(container_requests=[api.ContainerAllocateRequest(devices_ids=["r1"]),
+                                                      api.ContainerAllocateRequest(devices_ids=["r2"])])
+        assert engine(stub.Allocate(two))
+        st = srv.stats()
+        assert st["fast"] == 5
+        d = st["declined"]
+        assert d["nomatch"] >= 1 and d["replay"] == 2 and d["stale"] == 1 and d["blocked"] == 1
+        assert d["multi"] == 1 and d["ambiguous"] == 1 and d["shape"] == 1
+        # every native answer reported for the engine's bookkeeping, in order, with its request
+        got = []
+        while True:
+            rec = nat.taken_next(0)
+            if not rec:
+                break
+            got.append((rec[0], list(api.AllocateRequest.FromString(rec[1]).container_requests[0].devices_ids)))
+        assert got == [("a", ["i1", "i2"]), ("b", ["i3", "i4"]), ("c", ["j1", "j2", "j3"]), ("d", ["m1", "m2"]),
+                       ("h", ["q3"])]
+        # journal records (written before each reply) load like the engine's own fast records
+        j = AllocJournal(str(tmp_path / "j.jsonl"))
+        assert sorted(e["uid"] for e in j.unlanded()) == ["a", "b", "c", "d", "h"]
+        uid, body = j.lookup(_req("i2", "i1"))
+        assert uid == "a" and body().container_responses[0].envs["TAG"] == "a"
+    finally:
+        ch.close()
+        srv.stop()
+
+
+def test_each_prepared_answer_is_handed_out_once_under_load(tmp_path):
+    srv, al, src = _server(tmp_path)
+    al.detach_native()
+    n_cands = 400
+    _table(srv, [_cand(f"u{i}", 1 + i % 3) for i in range(n_cands)])
+    answers, errors = [], []
+    lock = threading.Lock()
+
+    def worker(w):
+        ch, stub = _stub(srv)
+        try:
+            for k in range(60):
+                size = 1 + (w + k) % 3
+                r = stub.Allocate(_req(*[f"w{w}-{k}-{x}" for x in range(size)]))
+                t = r.container_responses[0].envs.get("TAG")
+                with lock:
+                    answers.append((size, t))
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+        finally:
+            ch.close()
+    ts = [threading.Thread(target=worker, args=(w,)) for w in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    srv.stop()
+    assert not errors
+    native = [t for _, t in answers if t is not None]
+    assert len(native) == len(set(native)) == n_cands                  # each candidate exactly once
+    assert all(int(t[1:]) % 3 + 1 == s for s, t in answers if t is not None)
+
+
+@pytest.mark.parametrize("san", ["asan", "tsan"])
+def test_native_server_under_sanitizers(tmp_path, san):
+    """libgpushare_dpserver built with ASan+UBSan / TSan, driven by concurrent clients (fast
+    answers, forwarded requests, ListAndWatch, table publishes) in a separate interpreter."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "native", "build.py"), "dpserver", "--sanitize", san],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    rt = subprocess.run(["gcc", f"-print-file-name=lib{san}.so"], capture_output=True, text=True).stdout.strip()
+    if not os.path.exists(rt):
+        pytest.skip(f"lib{san}.so not installed")
+    script = f"""
+import sys, threading
+sys.path.insert(0, {root!r})
+import pathlib, tests.test_native_server as T
+tmp = pathlib.Path({str(tmp_path)!r})
+srv, al, src = T._server(tmp, [T.mkpod("p", 1, 0, 10)])
+stubs = [T._stub(srv) for _ in range(4)]
+law = stubs[0][1].ListAndWatch(T.api.Empty())
+next(law)
+def work(i):
+    ch, stub = stubs[i]
+    for k in range(40):
+        if k % 10 == 0:
+            srv.model.set_health(i % 2, k % 20 == 0, "x")
+        stub.Allocate(T._req(f"s{{i}}-{{k}}"))
+ts = [threading.Thread(target=work, args=(i,)) for i in range(4)]
+[t.start() for t in ts]
+[t.join() for t in ts]
+law.cancel()
+for ch, _ in stubs:
+    ch.close()
+print(srv.stats()["fast"] + srv.stats()["forwarded"])
+srv.stop()
+print("SAN-OK")
+"""
+    env = dict(os.environ, LD_PRELOAD=rt, GPUSHARE_NATIVE_VARIANT=san, PYTHONPATH=root,
+               ASAN_OPTIONS="detect_leaks=0:halt_on_error=1", UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1",
+               TSAN_OPTIONS="halt_on_error=1:report_signal_unsafe=0:ignore_noninstrumented_modules=1")
+    r = subprocess.run([sys.executable, "-c", script], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "SAN-OK" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
+    assert "ERROR: AddressSanitizer" not in r.stderr and "WARNING: ThreadSanitizer" not in r.stderr, r.stderr[-4000:]
+    assert "runtime error" not in r.stderr, r.stderr[-4000:]
+    assert int(r.stdout.split()[0]) >= 160
+
+
+def test_manager_serves_natively_by_default():
+    from aliyun_gpushare_device_plugin_amd.sim.cluster import SimCluster
+
+    with SimCluster([("n", "fake:1x8G")]) as c:
+        assert type(c.manager("n").plugin).__name__ == "NativeDevicePluginServer"
+        pod, where, adm = c.run_pod(2)
+        assert adm.error is None
+    with SimCluster([("n", "fake:1x8G")], grpc_server="python") as c:
+        assert type(c.manager("n").plugin).__name__ == "DevicePluginServer"
+
+
+def test_stats_json_is_well_formed(tmp_path):
+    srv, al, src = _server(tmp_path, journal=False)
+    try:
+        st = srv.stats()
+        assert json.loads(json.dumps(st)) == st and st["fast"] == 0 and st["journal_used"] == 0
+    finally:
+        srv.stop()
+    time.sleep(0.05)
