@@ -775,7 +775,7 @@ class Allocator:
             if ev is None or not self.opts.fast_path or self.opts.compute_isolation == "cu":
                 self._fast = None
                 if self.native is not None:
-                    self.native.publish(_native_blob(0, 0, 0, [], []))   # never valid: every Allocate to the engine
+                    self.native.publish(_native_blob(0, 0, NATIVE_NO_TABLE, [], []))   # every Allocate to the engine
                 self._stop.wait(1.0)
                 continue
             ev.wait(0.5)
@@ -1444,6 +1444,9 @@ class _PatchJob:
     recovered: bool = False
     kind: str = "assign"   # "assign" (ASSIGNED=true after an answer) | "placement" (truth fix)
     gen: int = 0           # placement: overlay generation this job lands
+
+
+NATIVE_NO_TABLE = 1 << 31
 
 
 def _native_blob(version: int, gen: int, flags: int, cands, replay_ids) -> bytes:

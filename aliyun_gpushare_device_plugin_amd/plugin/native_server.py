@@ -32,6 +32,28 @@ from .server import DevicePluginServer, dial
 
 _lib = None
 _lib_mu = threading.Lock()
+# Calls that wait (for a request, for a claim) release the interpreter lock while they do; the
+# quick ones (reply, publish, version hooks, block/take) keep it: a ctypes call that drops the
+# GIL has to queue behind whichever Python thread took it meanwhile to get it back (measured:
+# ~0.3 ms per reply under load), which is longer than the call itself
+_WAITING = {"gs_dp_start", "gs_dp_stop", "gs_dp_next", "gs_dp_taken_next", "gs_dp_fast_journal_open"}
+
+
+class _Lib:
+    """The library bound twice: ``ctypes.CDLL`` (GIL released) for the waiting calls,
+    ``ctypes.PyDLL`` (GIL kept) for the rest."""
+
+    def __init__(self, path: str):
+        free, held = ctypes.CDLL(path), ctypes.PyDLL(path)
+        P, I, I64, U64, B = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_char_p
+        for name, res, args in _SIGNATURES(P, I, I64, U64, B):
+            fn = getattr(free if name in _WAITING else held, name)
+            fn.restype, fn.argtypes = res, args
+            setattr(self, name, fn)
+            if name == "gs_dp_taken_next":           # the non-blocking drain keeps the GIL
+                poll = held.gs_dp_taken_next
+                poll.restype, poll.argtypes = res, args
+                self.gs_dp_taken_poll = poll
 
 
 def load():
@@ -39,32 +61,30 @@ def load():
     global _lib
     with _lib_mu:
         if _lib is None:
-            lib = ctypes.CDLL(ensure_built("dpserver"))
-            P, I, I64, U64, B = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_char_p
-            for name, res, args in (
-                    ("gs_dp_start", P, [B, ctypes.c_char_p, I]),
-                    ("gs_dp_stop", None, [P]),
-                    ("gs_dp_next", I64, [P, I, ctypes.c_char_p, I, ctypes.c_char_p, I, ctypes.POINTER(I),
-                                         ctypes.POINTER(I64)]),
-                    ("gs_dp_reply", I, [P, I64, I, B, ctypes.c_char_p, I]),
-                    ("gs_dp_set_devices", I, [P, ctypes.c_char_p, I]),
-                    ("gs_dp_fast_publish", I, [P, ctypes.c_char_p, I]),
-                    ("gs_dp_set_version", None, [P, U64]),
-                    ("gs_dp_set_gen", None, [P, U64]),
-                    ("gs_dp_fast_block", None, [P]),
-                    ("gs_dp_fast_unblock", None, [P]),
-                    ("gs_dp_fast_take", None, [P, B]),
-                    ("gs_dp_set_fast_wait_us", None, [P, I]),
-                    ("gs_dp_taken_next", I, [P, I, ctypes.c_char_p, I]),
-                    ("gs_dp_taken_pending", I, [P]),
-                    ("gs_dp_fast_journal_open", I, [P, B, U64]),
-                    ("gs_dp_fast_journal_used", U64, [P]),
-                    ("gs_dp_fast_journal_rotate", I, [P]),
-                    ("gs_dp_stats", I, [P, ctypes.c_char_p, I])):
-                fn = getattr(lib, name)
-                fn.restype, fn.argtypes = res, args
-            _lib = lib
+            _lib = _Lib(ensure_built("dpserver"))
     return _lib
+
+
+def _SIGNATURES(P, I, I64, U64, B):
+    C = ctypes.c_char_p
+    return (("gs_dp_start", P, [B, C, I]),
+            ("gs_dp_stop", None, [P]),
+            ("gs_dp_next", I64, [P, I, C, I, C, I, ctypes.POINTER(I), ctypes.POINTER(I64)]),
+            ("gs_dp_reply", I, [P, I64, I, B, C, I]),
+            ("gs_dp_set_devices", I, [P, C, I]),
+            ("gs_dp_fast_publish", I, [P, C, I]),
+            ("gs_dp_set_version", None, [P, U64]),
+            ("gs_dp_set_gen", None, [P, U64]),
+            ("gs_dp_fast_block", None, [P]),
+            ("gs_dp_fast_unblock", None, [P]),
+            ("gs_dp_fast_take", None, [P, B]),
+            ("gs_dp_set_fast_wait_us", None, [P, I]),
+            ("gs_dp_taken_next", I, [P, I, C, I]),
+            ("gs_dp_taken_pending", I, [P]),
+            ("gs_dp_fast_journal_open", I, [P, B, U64]),
+            ("gs_dp_fast_journal_used", U64, [P]),
+            ("gs_dp_fast_journal_rotate", I, [P]),
+            ("gs_dp_stats", I, [P, C, I]))
 
 
 class NativeFast:
@@ -98,7 +118,8 @@ class NativeFast:
 
     def taken_next(self, timeout_ms: int):
         """(uid, AllocateRequest bytes, wall time, handler ns); () on timeout; None once stopped."""
-        n = self.lib.gs_dp_taken_next(self.h, timeout_ms, self._buf, len(self._buf))
+        fn = self.lib.gs_dp_taken_poll if timeout_ms <= 0 else self.lib.gs_dp_taken_next
+        n = fn(self.h, timeout_ms, self._buf, len(self._buf))
         if n == 0:
             return ()
         if n < 0:
@@ -106,7 +127,7 @@ class NativeFast:
                 self._buf = ctypes.create_string_buffer(len(self._buf) * 4)
                 return ()
             return None
-        b = self._buf.raw[:n]
+        b = ctypes.string_at(self._buf, n)
         (lu,) = struct.unpack_from("<I", b, 0)
         uid = b[4:4 + lu].decode()
         (lr,) = struct.unpack_from("<I", b, 4 + lu)
@@ -138,7 +159,9 @@ class _Ctx:
 
 
 class NativeDevicePluginServer(DevicePluginServer):
-    def __init__(self, *a, handler_threads: int = 4, fast_wait_us: int = 1000, **kw):
+    # fast_wait_us: how long an Allocate that finds the table one pod-cache change behind waits
+    # for the engine to republish it before going to the engine's full path (~0.3 ms itself)
+    def __init__(self, *a, handler_threads: int = 4, fast_wait_us: int = 300, **kw):
         super().__init__(*a, **kw)
         self.handler_threads = handler_threads
         self.fast_wait_us = fast_wait_us
@@ -218,7 +241,8 @@ class NativeDevicePluginServer(DevicePluginServer):
                 continue
             if rid < 0:
                 return
-            self._handle(rid, meth.value.decode(), body.raw[:n.value])
+            # string_at copies the request only (``.raw`` would copy the whole 8 MiB buffer)
+            self._handle(rid, meth.value.decode(), ctypes.string_at(body, n.value))
 
     def _handle(self, rid: int, method: str, raw: bytes) -> None:
         lib, h = self._lib, self._h

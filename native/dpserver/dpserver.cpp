@@ -159,7 +159,7 @@ bool parse_allocate(const uint8_t* p, const uint8_t* e, std::vector<std::vector<
 
 // ---- the fast table ---------------------------------------------------------------------
 // blob: u64 version, u64 gen, u32 flags (bit 0: admission identity on — an answer needs the
-// only unclaimed candidate of its size), u32 entries, u32 replay ids, then per entry
+// only unclaimed candidate of its size; bit 31: no table, every Allocate to the engine), u32 entries, u32 replay ids, then per entry
 // {u32 size, u8 multi, u32 len + uid, u32 len + response bytes, u32 len + journal head}, then
 // per replay id {u32 len + id} (fake IDs of journaled answers whose pod may still be retried).
 struct Entry {
@@ -285,7 +285,7 @@ struct gs_dp {
   Table table;
   uint64_t cur_version = 0, cur_gen = 0;
   int blocked = 0;
-  int fast_wait_us = 1000;
+  int fast_wait_us = 300;
   // fake IDs of native answers -> when: a kubelet retry of them is for the engine (replay),
   // kept until a published replay set covers them (or for 30 s, by when the engine has)
   std::unordered_map<std::string, int64_t> answered_ids;
@@ -319,6 +319,7 @@ struct Conn {
   int efd;
   std::weak_ptr<Conn> self;
   std::atomic<bool> done{false};     // the connection ended (its thread exits)
+  bool wake_taken = false;           // a native answer went out this turn (conn thread only)
   nghttp2_session* sess = nullptr;
   std::map<int32_t, Stream> streams;
   std::mutex out_mu;                 // replies from Python threads
@@ -459,6 +460,10 @@ bool fast_allocate(Conn* c, int32_t sid, const std::string& body, int64_t t_in) 
     return false;
   }
   std::unique_lock<std::mutex> lk(s->mu);
+  if (!s->table.valid) {                    // no table (the engine serves every Allocate itself)
+    s->n.stale++;
+    return false;
+  }
   if (!table_current(s)) {
     // the pod cache or the engine moved since the table was built: the engine republishes
     // within a few hundred microseconds (its prepare loop wakes on the same change)
@@ -485,7 +490,9 @@ bool fast_allocate(Conn* c, int32_t sid, const std::string& body, int64_t t_in) 
   std::string resp = en->body;
   s->n.fast++;
   lk.unlock();
-  s->taken_cv.notify_all();
+  // the engine's claim reader is woken once the reply is on the wire (serve_conn): its
+  // bookkeeping and the write-behind PATCH it starts must not compete with the reply
+  c->wake_taken = true;
   respond(c, sid, 0, "", resp, true);
   return true;
 }
@@ -661,6 +668,11 @@ void serve_conn(std::shared_ptr<Conn> cp) {
     wbuf.clear();
     while ((n = nghttp2_session_mem_send(c->sess, &data)) > 0) wbuf.append((const char*)data, (size_t)n);
     if (!wbuf.empty() && !write_all(c->fd, (const uint8_t*)wbuf.data(), wbuf.size())) break;
+    if (c->wake_taken) {
+      c->wake_taken = false;
+      std::lock_guard<std::mutex> lk(c->srv->mu);   // pairs with gs_dp_taken_next's wait
+      c->srv->taken_cv.notify_all();
+    }
     if (n < 0) break;
     if (!nghttp2_session_want_read(c->sess) && !nghttp2_session_want_write(c->sess)) break;
     pollfd fds[2] = {{c->fd, POLLIN, 0}, {c->efd, POLLIN, 0}};
@@ -865,7 +877,7 @@ int gs_dp_set_devices(gs_dp* s, const uint8_t* body, int len) {
 int gs_dp_fast_publish(gs_dp* s, const uint8_t* blob, int len) {
   Table t;
   if (!parse_table(blob, len, &t)) return -1;
-  t.valid = true;
+  t.valid = !(t.flags & 0x80000000u);       // flag 31: no table (fast path off)
   {
     std::lock_guard<std::mutex> lk(s->mu);
     // A claim stays a claim while the new table still lists the pod (the engine built it
