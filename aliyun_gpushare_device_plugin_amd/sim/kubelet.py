@@ -32,6 +32,9 @@ from ..api import v1beta1 as api
 from ..cluster import objects as O
 from ..cluster.client import APIClient
 from ..utils import log
+from .h2client import NativeUnaryClient, UnaryError
+
+_STATUS = {s.value[0]: s for s in grpc.StatusCode}
 
 
 @dataclasses.dataclass
@@ -71,6 +74,8 @@ class FakeKubelet:
         self._holdings: dict[str, tuple] = {}    # uid -> (ns, name, [(container, ids)])
         self._specs: dict[str, list] = {}        # uid -> container names (all listed, like the kubelet)
         self.podres_sock = os.path.join(plugin_dir, "pod-resources.sock")
+        self._h2 = None                           # NativeUnaryClient for Allocate (see _connect)
+        self._watch = None                        # this node's pods, as the kubelet's own watch sees them
         self.prestart_calls = 0
         self.reg_options = None
 
@@ -167,16 +172,26 @@ class FakeKubelet:
         self.server.add_insecure_port(api.unix_target(self.sock))
         self.server.add_insecure_port(api.unix_target(self.podres_sock))
         self.server.start()
+        if self.client is not None and self.node and self._watch is None:
+            from ..cluster.podcache import WatchCache
+
+            self._watch = WatchCache(self.client, self.node).start()
         return self
 
     def stop(self):
         self._stop.set()
+        if self._watch is not None:
+            self._watch.stop()
+            self._watch = None
         if self.server is not None:
             self.server.stop(0.2).wait(1.0)
             self.server = None
         if self._channel is not None:
             self._channel.close()
             self._channel = None
+        if self._h2 is not None:
+            self._h2.close()
+            self._h2 = None
 
     def restart(self):
         self.stop()
@@ -193,6 +208,12 @@ class FakeKubelet:
         self._channel = ch
         self._stub = api.Stub(ch, "DevicePlugin")
         self.options = self._stub.GetDevicePluginOptions(api.Empty(), timeout=5)
+        if self._h2 is not None:
+            self._h2.close()
+            self._h2 = None
+        if NativeUnaryClient.wanted():
+            # Allocate the way the real kubelet calls it: compiled client code (sim/h2client.py)
+            self._h2 = NativeUnaryClient(path)
         self._law_thread = threading.Thread(target=self._list_and_watch, args=(self._stub,), daemon=True)
         self._law_thread.start()
 
@@ -240,8 +261,22 @@ class FakeKubelet:
         used = self._used
         return [d for d in self._healthy if d not in used]
 
+    def _await_watch(self, uid: str, limit: float = 2.0) -> None:
+        """The kubelet admits a pod its own apiserver watch delivered (bound to this node) —
+        the event the plugin's informer reads too; a harness handing it the bind response
+        directly would always outrun the plugin's cache."""
+        w = self._watch
+        if w is None or not w.wait_synced(limit):
+            return
+        t = time.monotonic() + limit
+        while time.monotonic() < t:
+            if w.get(uid) is not None:
+                return
+            time.sleep(0.0002)
+
     def admit(self, pod: dict, timeout: float = 10.0) -> Admission:
         uid = O.uid(pod)
+        self._await_watch(uid)
         adm = Admission(uid, [], [], [])
         started = []
         # like the kubelet's HandlePodAdditions: the pod joins the pod manager (and so the
@@ -272,18 +307,34 @@ class FakeKubelet:
                 self._allocated.setdefault(uid, set()).update(ids)
                 self._used.update(ids)
             areq = api.AllocateRequest(container_requests=[api.ContainerAllocateRequest(devices_ids=ids)])
-            t0n = time.monotonic_ns()
-            t0 = time.perf_counter()
-            try:
-                resp, call = self._stub.Allocate.with_call(areq, timeout=timeout)
-            except grpc.RpcError as e:
+            h2 = self._h2
+            if h2 is not None:
+                try:
+                    raw, stamp, t0n, t1n = h2.unary("/v1beta1.DevicePlugin/Allocate", areq.SerializeToString(),
+                                                    timeout)
+                except UnaryError as e:
+                    adm.error = f"Allocate failed: {_STATUS.get(e.status, e.status)} {e.message}"
+                    self.release(uid)
+                    return adm
+                except ConnectionError as e:
+                    adm.error = f"Allocate failed: {e}"
+                    self.release(uid)
+                    return adm
+                resp = api.AllocateResponse.FromString(raw)
+                adm.latencies.append((t1n - t0n) / 1e9)
+            else:
+                t0n = time.monotonic_ns()
+                t0 = time.perf_counter()
+                try:
+                    resp, call = self._stub.Allocate.with_call(areq, timeout=timeout)
+                except grpc.RpcError as e:
+                    adm.latencies.append(time.perf_counter() - t0)
+                    adm.error = f"Allocate failed: {e.code()} {e.details()}"
+                    self.release(uid)
+                    return adm
                 adm.latencies.append(time.perf_counter() - t0)
-                adm.error = f"Allocate failed: {e.code()} {e.details()}"
-                self.release(uid)
-                return adm
-            adm.latencies.append(time.perf_counter() - t0)
-            t1n = time.monotonic_ns()
-            stamp = dict(call.trailing_metadata() or ()).get(const.HANDLER_STAMP_KEY)
+                t1n = time.monotonic_ns()
+                stamp = dict(call.trailing_metadata() or ()).get(const.HANDLER_STAMP_KEY)
             if stamp:
                 a, b = (int(x) for x in stamp.split(","))
                 adm.splits.append(((a - t0n) / 1e9, (b - a) / 1e9, (t1n - b) / 1e9))

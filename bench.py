@@ -343,38 +343,46 @@ def mode_comparison(rtts_ms: list[float], n_pods: int) -> dict:
     from aliyun_gpushare_device_plugin_amd.sim.cluster import SimCluster
 
     out = {}
-    for rtt in rtts_ms:
-        for label, src, extra in (("default", "watch", []), ("reference", "list", ["--sync-patch"])):
-            lat, fails, splits = [], 0, []
-            port = free_port()
-            with SimCluster([("cmp", "fake:1x288G")], plugin_mode="process", pod_source=src,
-                            apiserver="process", kubelet="process", apiserver_latency_s=rtt / 1e3,
-                            extra_plugin_args=extra + ["--metrics-addr", f"127.0.0.1:{port}"]) as c:
-                req = []                                 # one apiserver round trip, as the plugin sees it
-                for _ in range(10):
-                    t = time.perf_counter()
-                    c.client.get_node("cmp")
-                    req.append(time.perf_counter() - t)
-                for _ in range(n_pods):
-                    pod, where, adm = c.run_pod(8)
-                    if adm is None or adm.error or int(dict(adm.responses[0].envs)["ALIYUN_COM_GPU_MEM_IDX"]) < 0:
-                        fails += 1
-                    else:
-                        lat += adm.latencies
-                        splits += adm.splits
-                    c.delete_pod(pod)
-                srv = plugin_latency(port) or {}
-            key = f"{label}@{rtt:g}ms"
-            # apiserver round trips on the Allocate path: LIST + PATCH (reference), none (default:
-            # watch-cache lookup, PATCH written behind); request_ms = one round trip through the
-            # fake apiserver at this RTT (RTT + the fake's own ~1.5 ms per-request cost)
-            # plugin_* = the plugin's own handler time (its metrics endpoint): the rest of the
-            # kubelet-side number is gRPC transport and the harness's processes sharing the CPUs
-            out[key] = {"allocate_p50_ms": ms(pct(lat, 0.5)), "allocate_p99_ms": ms(pct(lat, 0.99)),
-                        "plugin_allocate_p50_ms": ms(srv.get("p50")), "plugin_allocate_p99_ms": ms(srv.get("p99")),
-                        "allocate_breakdown_p50_ms": breakdown(splits),
-                        "apiserver_round_trips_on_path": round_trips(srv), "request_ms": ms(pct(req, 0.5)),
-                        "pod_source": src, "patch": "sync" if extra else "write-behind", "failed": fails}
+    runs = [(rtt, label, src, extra, "native") for rtt in rtts_ms
+            for label, src, extra in (("default", "watch", []), ("reference", "list", ["--sync-patch"]))]
+    if 0.0 in rtts_ms:
+        # calibration: the same quiet A/B measured by a Python grpcio kubelet client (the client
+        # of rounds 1-3; the real kubelet's is compiled grpc-go)
+        runs += [(0.0, label + "+grpcio_client", src, extra, "python")
+                 for label, src, extra in (("default", "watch", []), ("reference", "list", ["--sync-patch"]))]
+    for rtt, label, src, extra, client in runs:
+        lat, fails, splits = [], 0, []
+        port = free_port()
+        os.environ["GS_SIM_KUBELET_CLIENT"] = client          # inherited by the kubelet process
+        with SimCluster([("cmp", "fake:1x288G")], plugin_mode="process", pod_source=src,
+                        apiserver="process", kubelet="process", apiserver_latency_s=rtt / 1e3,
+                        extra_plugin_args=extra + ["--metrics-addr", f"127.0.0.1:{port}"]) as c:
+            req = []                                 # one apiserver round trip, as the plugin sees it
+            for _ in range(10):
+                t = time.perf_counter()
+                c.client.get_node("cmp")
+                req.append(time.perf_counter() - t)
+            for _ in range(n_pods):
+                pod, where, adm = c.run_pod(8)
+                if adm is None or adm.error or int(dict(adm.responses[0].envs)["ALIYUN_COM_GPU_MEM_IDX"]) < 0:
+                    fails += 1
+                else:
+                    lat += adm.latencies
+                    splits += adm.splits
+                c.delete_pod(pod)
+            srv = plugin_latency(port) or {}
+        os.environ.pop("GS_SIM_KUBELET_CLIENT", None)
+        key = f"{label}@{rtt:g}ms"
+        # apiserver round trips on the Allocate path: LIST + PATCH (reference), none (default:
+        # watch-cache lookup, PATCH written behind); request_ms = one round trip through the
+        # fake apiserver at this RTT (RTT + the fake's own ~1.5 ms per-request cost)
+        # plugin_* = the plugin's own handler time (its metrics endpoint): the rest of the
+        # kubelet-side number is gRPC transport and the harness's processes sharing the CPUs
+        out[key] = {"allocate_p50_ms": ms(pct(lat, 0.5)), "allocate_p99_ms": ms(pct(lat, 0.99)),
+                    "plugin_allocate_p50_ms": ms(srv.get("p50")), "plugin_allocate_p99_ms": ms(srv.get("p99")),
+                    "allocate_breakdown_p50_ms": breakdown(splits),
+                    "apiserver_round_trips_on_path": round_trips(srv), "request_ms": ms(pct(req, 0.5)),
+                    "pod_source": src, "patch": "sync" if extra else "write-behind", "failed": fails}
     return out
 
 
@@ -906,6 +914,9 @@ def main():
             topo_failed = not ok
 
     if rank == 0:
+        from aliyun_gpushare_device_plugin_amd.plugin import native_server
+        from aliyun_gpushare_device_plugin_amd.sim.h2client import NativeUnaryClient
+
         srv = cp.plugin_latency()
         ref_srv = plugin_latency(cp.ref_port) if cp.ref_port else None
         pods_node = sum(len(v) for v in cp.resident.values())
@@ -962,7 +973,10 @@ def main():
             "config": {"model": "gpushare-device-plugin + MFMA GEMM pods (BASELINE config 3 churn)",
                        "global_batch": 4 * n, "seq_len": None, "parallelism": f"node{n}",
                        "pods_per_gpu": 4, "gemm_mnk": a.gemm, "pod_fill": a.fill, "pod_source": a.pod_source,
-                       "smi_backend": smi, "pod_processes": use_gpu},
+                       "smi_backend": smi, "pod_processes": use_gpu,
+                       # the plugin's gRPC server and the simulated kubelet's Allocate client
+                       "grpc_server": "native" if native_server.available() else "python",
+                       "kubelet_client": "native" if NativeUnaryClient.wanted() else "grpcio"},
             "allocate_p50_ms": ms(pct(cp.alloc_lat, 0.5)),
             "allocate_p99_ms": ms(pct(cp.alloc_lat, 0.99)),
             "allocate_breakdown_p50_ms": breakdown(cp.splits),

@@ -144,8 +144,9 @@ def build_dpserver(force=False, asan=False):
         flags += SANITIZERS[san]
         lib = os.path.join(OUT, san, "libgpushare_dpserver.so")
     os.makedirs(os.path.dirname(lib), exist_ok=True)
-    if force or _newer(lib, [src] + _headers(d)):
-        _run([CXX, *flags, "-shared", "-o", lib, src, "-l:libnghttp2.so.14", "-pthread"])
+    srcs = [src, _src("dpserver", "h2client.cpp")]
+    if force or _newer(lib, srcs + _headers(d)):
+        _run([CXX, *flags, "-shared", "-o", lib, *srcs, "-l:libnghttp2.so.14", "-pthread"])
     return [lib]
 
 

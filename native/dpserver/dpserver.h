@@ -64,6 +64,14 @@ GS_DP_API int gs_dp_fast_journal_rotate(gs_dp* s);
 // Counters as a JSON object (NUL-terminated); returns its length or -1.
 GS_DP_API int gs_dp_stats(gs_dp* s, char* buf, int cap);
 
+// ---- gRPC unary client (h2client.cpp): the simulated kubelet's device-manager calls ---------
+typedef struct gs_h2c gs_h2c;
+GS_DP_API gs_h2c* gs_h2c_connect(const char* socket_path);
+GS_DP_API int gs_h2c_unary(gs_h2c* h, const char* path, const uint8_t* req, int len, uint8_t* out, int cap,
+                           int* out_len, int* status, char* message, int mcap, char* stamp, int scap,
+                           int timeout_ms, int64_t* t_send, int64_t* t_recv);
+GS_DP_API void gs_h2c_close(gs_h2c* h);
+
 #ifdef __cplusplus
 }
 #endif

@@ -297,3 +297,32 @@ def test_stats_json_is_well_formed(tmp_path):
     finally:
         srv.stop()
     time.sleep(0.05)
+
+
+def test_native_kubelet_client(tmp_path):
+    """The simulated kubelet's compiled Allocate client (sim/h2client.py): replies, gRPC error
+    statuses, the handler's timestamps, and a re-dial after the plugin's server restarted."""
+    from aliyun_gpushare_device_plugin_amd.sim.h2client import NativeUnaryClient, UnaryError
+
+    srv, al, src = _server(tmp_path, [mkpod("p", 2, 1, 10)])
+    cl = NativeUnaryClient(srv.socket)
+    try:
+        raw, stamp, t0, t1 = cl.unary("/v1beta1.DevicePlugin/Allocate", _req("a", "b").SerializeToString())
+        r = api.AllocateResponse.FromString(raw)
+        assert r.container_responses[0].envs[const.ENV_RESOURCE_INDEX] == "1"
+        t_in, t_out = (int(x) for x in stamp.split(","))
+        assert t0 <= t_in <= t_out <= t1
+        with pytest.raises(UnaryError) as e:
+            cl.unary("/v1beta1.DevicePlugin/Nope", b"")
+        assert e.value.status == 12
+        srv.stop()                                     # plugin restart: a new server on the socket
+        srv2 = NativeDevicePluginServer(srv.model, al, srv.socket)
+        srv2.start()
+        try:
+            raw, _, _, _ = cl.unary("/v1beta1.DevicePlugin/GetDevicePluginOptions", b"")
+            assert api.DevicePluginOptions.FromString(raw) == srv2.options()
+        finally:
+            srv2.stop()
+    finally:
+        cl.close()
+        srv.stop()
