@@ -97,6 +97,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--grpc-server", default="auto", choices=("auto", "native", "python"),
                    help="DevicePlugin gRPC server: native = libgpushare_dpserver (HTTP/2 in C++, the common "
                         "Allocate answered without entering Python), python = grpcio; auto = native when it loads")
+    p.add_argument("--native-fast-wait-us", type=int, default=300,
+                   help="native server: how long an Allocate that finds the prepared answers one pod-cache "
+                        "change behind waits for them to be rebuilt before the engine's full path answers it")
     p.add_argument("--quota-enforcement", default="auto", choices=("auto", "off", "report", "kill"),
                    help="node-side quota watchdog over the kernel's per-process HBM (DRM fdinfo): report "
                         "pods above their share, or also SIGKILL their largest GPU process (the shim cannot be "
@@ -141,7 +144,7 @@ def config_from_args(a) -> PluginConfig:
         journal_path=a.journal_path, compute_isolation=a.compute_isolation,
         pod_resources_socket=a.pod_resources_socket, placement_s=a.placement_interval,
         admission_identity=a.admission_identity, quota_enforcement=a.quota_enforcement,
-        grpc_server=a.grpc_server,
+        grpc_server=a.grpc_server, native_fast_wait_us=a.native_fast_wait_us,
         cdi_kind=a.cdi_kind, expose_devices=a.device_specs,
         quota_watch_s=a.quota_watch_interval, quota_slack_mib=a.quota_slack_mib,
         dmem_limits=a.dmem_limits, cgroup_root=a.cgroup_root)

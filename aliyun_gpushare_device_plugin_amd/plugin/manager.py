@@ -87,6 +87,7 @@ class PluginConfig:
     # DevicePlugin gRPC server: "native" (libgpushare_dpserver, Allocate fast path in C++),
     # "python" (grpcio), "auto" = native when the library loads
     grpc_server: str = "auto"
+    native_fast_wait_us: int = 300       # native server: wait for a republished table (see native_server.py)
 
 
 class SharedGPUManager:
@@ -194,8 +195,10 @@ class SharedGPUManager:
         if allocator.podres is None:
             allocator.set_pod_resources(self._pod_resources())
         self.model = model
-        return self._server_class()(model, allocator, self._plugin_socket(), const.RESOURCE_NAME,
-                                    cfg.preferred_allocation, self.metrics)
+        cls = self._server_class()
+        kw = {"fast_wait_us": cfg.native_fast_wait_us} if cls is not DevicePluginServer else {}
+        return cls(model, allocator, self._plugin_socket(), const.RESOURCE_NAME, cfg.preferred_allocation,
+                   self.metrics, **kw)
 
     def _server_class(self):
         mode = self.cfg.grpc_server
@@ -248,6 +251,10 @@ class SharedGPUManager:
                         "not limited", eff)
         self.enforcement = eff
         return mode
+
+    def _debug_view(self) -> dict:
+        stats = getattr(self.plugin, "stats", None)
+        return {"native_server": stats()} if stats else {}
 
     def _pod_resources(self):
         from ..api.podresources import SOCKET, PodResourcesClient
@@ -392,7 +399,7 @@ class SharedGPUManager:
         if cfg.metrics_addr:
             self._metrics_srv = M.serve(self.metrics.registry, cfg.metrics_addr,
                                         lambda: self.plugin is not None and not self.plugin.stopped.is_set(),
-                                        ready_fn=self.readiness)
+                                        ready_fn=self.readiness, debug_fn=self._debug_view)
         os.makedirs(cfg.device_plugin_dir, exist_ok=True)
         watcher = FSWatcher(cfg.device_plugin_dir, self.events)
         log.V(1).info("Starting FS watcher (%s).", watcher.mode)

@@ -219,12 +219,14 @@ class PluginMetrics:
                                      "(slot = one CU on every XCD; > slots per GPU means oversubscribed)")
 
 
-def serve(registry: Registry, addr: str, health_fn=None, ready_fn=None) -> http.server.ThreadingHTTPServer:
+def serve(registry: Registry, addr: str, health_fn=None, ready_fn=None,
+          debug_fn=None) -> http.server.ThreadingHTTPServer:
     """Start ``/metrics`` + ``/healthz`` + ``/readyz`` + ``/debug/latency`` on ``host:port`` in a
     daemon thread. ``ready_fn() -> (ok, reason)`` backs ``/readyz`` (503 + reason when not ready).
 
-    ``/debug/latency`` returns exact p50/p90/p99 of every histogram (JSON); ``?reset=1`` also
-    clears them, honoured only with ``GPUSHARE_DEBUG=1`` (benchmarks bracket a timed region)."""
+    ``/debug/latency`` returns exact p50/p90/p99 of every histogram (JSON), plus whatever
+    ``debug_fn()`` returns (the native server's counters); ``?reset=1`` also clears the
+    histograms, honoured only with ``GPUSHARE_DEBUG=1`` (benchmarks bracket a timed region)."""
     import json as _json
     import os as _os
 
@@ -236,7 +238,13 @@ def serve(registry: Registry, addr: str, health_fn=None, ready_fn=None) -> http.
                 body, ctype, code = registry.render().encode(), "text/plain; version=0.0.4", 200
             elif self.path.startswith("/debug/latency"):
                 hs = registry.histograms()
-                body = _json.dumps({n: h.summary() for n, h in hs.items()}).encode()
+                d = {n: h.summary() for n, h in hs.items()}
+                if debug_fn is not None:
+                    try:
+                        d.update(debug_fn())
+                    except Exception:  # noqa: BLE001 - a debug view never fails the endpoint
+                        pass
+                body = _json.dumps(d).encode()
                 ctype, code = "application/json", 200
                 if "reset=1" in self.path and _os.environ.get("GPUSHARE_DEBUG") == "1":
                     for h in hs.values():

@@ -136,6 +136,29 @@ def plugin_latency(port: int, reset: bool = False) -> dict | None:
     return tot
 
 
+def native_stats(port: int) -> dict | None:
+    """The native server's counters (plugin metrics endpoint)."""
+    import urllib.request
+
+    try:
+        with urllib.request.urlopen(f"http://127.0.0.1:{port}/debug/latency", timeout=5) as r:
+            return json.loads(r.read()).get("native_server")
+    except Exception:  # noqa: BLE001
+        return None
+
+
+def native_share(before: dict | None, after: dict | None) -> dict | None:
+    """Allocates the native server answered from the prepared table vs handed to the engine,
+    between two readings of its counters, and why it declined."""
+    b, a = before or {}, after or {}
+    if not a:
+        return None
+    fast = a.get("fast", 0) - b.get("fast", 0)
+    eng = a.get("forwarded_allocate", 0) - b.get("forwarded_allocate", 0)
+    why = {k: v - (b.get("declined") or {}).get(k, 0) for k, v in (a.get("declined") or {}).items()}
+    return {"native": fast, "engine": eng, "declined": {k: v for k, v in why.items() if v}}
+
+
 def transport_floor() -> float | None:
     """Kubelet-side round trip of an Allocate whose handler returns a prepared answer at once."""
     try:
@@ -847,6 +870,7 @@ def main():
         cp.cp_time = 0.0
         cp.failed = 0
         cp.fail_reasons.clear()
+        cp.native_before = native_stats(cp.metrics_port)
         cp.plugin_latency(reset=True)
         if cp.ref_port:
             plugin_latency(cp.ref_port, reset=True)
@@ -938,6 +962,7 @@ def main():
             "plugin_allocate_p50_ms": ms(srv["p50"]) if srv else None,
             "plugin_allocate_p99_ms": ms(srv["p99"]) if srv else None,
             "allocate_breakdown_p50_ms": breakdown(cp.splits),
+            "answered_by": native_share(getattr(cp, "native_before", None), native_stats(cp.metrics_port)),
             "admissions": len(cp.alloc_lat), "pod_source": a.pod_source, "patch": "write-behind",
             "apiserver_round_trips_on_path": round_trips(srv)}}
         if cp.ref_port:

@@ -252,7 +252,7 @@ struct Taken {
 };
 
 struct Counters {
-  std::atomic<uint64_t> fast{0}, forwarded{0}, stale{0}, blocked{0}, replay{0}, nomatch{0}, multi{0},
+  std::atomic<uint64_t> fast{0}, forwarded{0}, forwarded_allocate{0}, stale{0}, blocked{0}, replay{0}, nomatch{0}, multi{0},
       ambiguous{0}, shape{0}, journal{0}, waited{0}, law_sends{0}, conns{0}, unknown{0};
 };
 
@@ -550,7 +550,10 @@ void request_done(Conn* c, int32_t sid) {
     respond(c, sid, 12, "unknown method " + st.path, "", false);
     return;
   }
-  if (st.path == kAllocate && fast_allocate(c, sid, msg, st.t_in)) return;
+  if (st.path == kAllocate) {
+    if (fast_allocate(c, sid, msg, st.t_in)) return;
+    s->n.forwarded_allocate++;
+  }
   auto f = std::make_shared<Fwd>();
   f->conn = c->self;
   f->stream = sid;
@@ -1015,11 +1018,12 @@ int gs_dp_stats(gs_dp* s, char* buf, int cap) {
     pend = s->taken.size();
   }
   int n = snprintf(buf, (size_t)cap,
-                   "{\"fast\":%llu,\"forwarded\":%llu,\"declined\":{\"stale\":%llu,\"blocked\":%llu,\"replay\":%llu,"
+                   "{\"fast\":%llu,\"forwarded\":%llu,\"forwarded_allocate\":%llu,\"declined\":{\"stale\":%llu,\"blocked\":%llu,\"replay\":%llu,"
                    "\"nomatch\":%llu,\"multi\":%llu,\"ambiguous\":%llu,\"shape\":%llu,\"journal\":%llu},"
                    "\"waited\":%llu,\"law_sends\":%llu,\"connections\":%llu,\"unknown\":%llu,"
                    "\"journal_used\":%llu,\"taken_pending\":%llu}",
-                   (unsigned long long)s->n.fast, (unsigned long long)s->n.forwarded, (unsigned long long)s->n.stale,
+                   (unsigned long long)s->n.fast, (unsigned long long)s->n.forwarded,
+                   (unsigned long long)s->n.forwarded_allocate, (unsigned long long)s->n.stale,
                    (unsigned long long)s->n.blocked, (unsigned long long)s->n.replay, (unsigned long long)s->n.nomatch,
                    (unsigned long long)s->n.multi, (unsigned long long)s->n.ambiguous, (unsigned long long)s->n.shape,
                    (unsigned long long)s->n.journal, (unsigned long long)s->n.waited,
