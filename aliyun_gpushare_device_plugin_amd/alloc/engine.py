@@ -206,6 +206,7 @@ class Allocator:
         self._native_prep: dict[str, _Prepared] = {}
         self._native_hold = False                 # a block kept while a multi-container claim is open
         self._published = (-1, -1)                # (pending version, gen) of the last native table
+        self.native_rotate_bytes = 16 << 20       # rotate the native journal file past this
         for k, uid, t, resp in self.journal.answers():   # grants of a previous instance (journal TTL)
             if len(resp.container_responses) == 1:
                 self.grants.record(k, self._grant_from(resp.container_responses[0], uid, t))
@@ -1198,7 +1199,7 @@ class Allocator:
                 break
             if rec:
                 self._native_taken(rec)
-            if self.journal.path and nat.journal_used() > (16 << 20):
+            if self.journal.path and nat.journal_used() > self.native_rotate_bytes:
                 nat.block()
                 try:
                     self._drain_native(nat)

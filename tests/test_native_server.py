@@ -326,3 +326,38 @@ def test_native_kubelet_client(tmp_path):
     finally:
         cl.close()
         srv.stop()
+
+
+def test_native_journal_rotates_without_losing_a_pending_patch(tmp_path):
+    """Native answers are journaled in <journal>.fast before each reply. Past a size the engine
+    compacts its own journal (which then holds every answer and pending patch) and zeroes the
+    fast file; a plugin restarted after that still re-queues every unlanded patch."""
+    pods = [mkpod(f"p{i}", 1, i % 2, 10 + i) for i in range(12)]
+    srv, al, src = _server(tmp_path, pods)
+    al.native_rotate_bytes = 4096
+    al.client.fail = RuntimeError("apiserver down")          # PATCHes never land
+    al.opts.fast_path = True
+    ch, stub = _stub(srv)
+    try:
+        src.changed.set()
+        fast = 0
+        for k in range(10):
+            t = time.monotonic() + 5
+            while al._published != (src.pending_version, al._gen) and time.monotonic() < t:
+                time.sleep(0.002)
+            r = stub.Allocate(_req(f"r{k}"))
+            assert r.container_responses[0].envs[const.ENV_RESOURCE_INDEX] in ("0", "1")
+            fast = srv.stats()["fast"]
+        assert fast >= 5
+        t = time.monotonic() + 5
+        while (al.native.pending() or al._post) and time.monotonic() < t:
+            time.sleep(0.01)
+        time.sleep(0.5)                                      # the claim reader's rotation check
+        used = srv.fast.journal_used()
+        assert used < 4096, used                             # rotated at least once
+    finally:
+        ch.close()
+        srv.stop()
+        al.close()
+    j = AllocJournal(str(tmp_path / "j.jsonl"))
+    assert len(j.unlanded()) == 10                           # every answered pod still owes its PATCH
