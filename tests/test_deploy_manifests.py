@@ -140,6 +140,7 @@ def test_dockerfile_recipe_builds_and_installs(tmp_path):
     native = src / "aliyun_gpushare_device_plugin_amd" / "_native"
     assert (native / "libgpushare_gpuinfo.so").exists() and (native / "libgpushare_hipquota.so").exists()
     assert (native / "gpushare-smi").exists()
+    assert (native / "libgpushare_dpserver.so").exists()       # the native DevicePlugin server
     site = tmp_path / "site"
     r = subprocess.run([sys.executable, "-m", "pip", "install", "--no-deps", "--no-build-isolation", "--no-index",
                         "--target", str(site), str(src)], capture_output=True, text=True, timeout=600)
