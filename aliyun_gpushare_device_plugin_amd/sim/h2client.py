@@ -33,9 +33,10 @@ class NativeUnaryClient:
                 lib = ctypes.CDLL(ensure_built("dpserver"))      # calls wait on the socket: GIL released
                 lib.gs_h2c_connect.restype, lib.gs_h2c_connect.argtypes = ctypes.c_void_p, [ctypes.c_char_p]
                 I, C, I64 = ctypes.c_int, ctypes.c_char_p, ctypes.c_int64
-                lib.gs_h2c_unary.restype = I
-                lib.gs_h2c_unary.argtypes = [ctypes.c_void_p, C, C, I, C, I, ctypes.POINTER(I), ctypes.POINTER(I),
-                                             C, I, C, I, I, ctypes.POINTER(I64), ctypes.POINTER(I64)]
+                for fn in (lib.gs_h2c_unary, lib.gs_h2c_call):
+                    fn.restype = I
+                    fn.argtypes = [ctypes.c_void_p, C, C, I, C, I, ctypes.POINTER(I), ctypes.POINTER(I),
+                                   C, I, C, I, I, ctypes.POINTER(I64), ctypes.POINTER(I64)]
                 lib.gs_h2c_close.restype, lib.gs_h2c_close.argtypes = None, [ctypes.c_void_p]
                 cls._lib = lib
         return cls._lib
@@ -66,22 +67,24 @@ class NativeUnaryClient:
         if not self.h:
             raise ConnectionError(f"cannot connect to {self.path}")
 
-    def unary(self, path: str, request: bytes, timeout: float = 10.0):
+    def unary(self, path: str, request: bytes, timeout: float = 10.0, framed: bool = False):
         """(reply bytes, handler stamp "in,out" or "", t_send ns, t_recv ns); UnaryError on a
         non-OK status, ConnectionError on a transport failure. A connection the plugin closed
-        (restart) is re-dialled once, as a grpc channel reconnects to its socket."""
+        (restart) is re-dialled once, as a grpc channel reconnects to its socket. ``framed``:
+        ``request`` is the whole DATA payload, sent without adding the gRPC length prefix."""
         try:
-            return self._unary(path, request, timeout)
+            return self._unary(path, request, timeout, framed)
         except ConnectionError:
             self._connect()
-            return self._unary(path, request, timeout)
+            return self._unary(path, request, timeout, framed)
 
-    def _unary(self, path: str, request: bytes, timeout: float):
+    def _unary(self, path: str, request: bytes, timeout: float, framed: bool = False):
         if not self.h:
             self._connect()
         n, st = ctypes.c_int(), ctypes.c_int()
         ts, tr = ctypes.c_int64(), ctypes.c_int64()
-        rc = self.l.gs_h2c_unary(self.h, path.encode(), request, len(request), self._out, len(self._out),
+        fn = self.l.gs_h2c_call if framed else self.l.gs_h2c_unary
+        rc = fn(self.h, path.encode(), request, len(request), self._out, len(self._out),
                                  ctypes.byref(n), ctypes.byref(st), self._msg, len(self._msg), self._stamp,
                                  len(self._stamp), int(timeout * 1000), ctypes.byref(ts), ctypes.byref(tr))
         if rc != 0:

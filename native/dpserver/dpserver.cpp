@@ -264,8 +264,7 @@ struct gs_dp {
   std::atomic<bool> stopping{false};
   std::thread acceptor;
   std::mutex conns_mu;
-  std::vector<std::shared_ptr<Conn>> conns;
-  std::vector<std::thread> conn_threads;
+  std::vector<std::shared_ptr<Conn>> conns;   // live ones; ended ones are joined and dropped at the next accept
 
   // requests for Python
   std::mutex q_mu;
@@ -311,12 +310,17 @@ struct Stream {
   std::string message;
   int64_t t_in = 0, t_out = 0;
   bool stamp = false;
+  bool too_big = false;     // the request passed kMaxRequest: its bytes are dropped, answered RESOURCE_EXHAUSTED
 };
+
+// Larger requests are refused (gRPC's default receive limit is 4 MiB; Python's handler buffer is 8)
+constexpr size_t kMaxRequest = (8u << 20) + 5;
 
 struct Conn {
   gs_dp* srv;
   int fd;
-  int efd;
+  int efd = -1;                      // wakes the thread; open while any reference (a reply in flight) lives
+  std::thread th;                    // serve_conn; joined by the acceptor once done, or at stop
   std::weak_ptr<Conn> self;
   std::atomic<bool> done{false};     // the connection ended (its thread exits)
   bool wake_taken = false;           // a native answer went out this turn (conn thread only)
@@ -326,6 +330,9 @@ struct Conn {
   std::vector<Reply> outbox;
   uint64_t sent_dev_gen = 0;
   std::atomic<bool> closing{false};
+  ~Conn() {
+    if (efd >= 0) close(efd);
+  }
 };
 
 void wake(Conn* c) {
@@ -385,6 +392,23 @@ ssize_t read_cb(nghttp2_session* sess, int32_t sid, uint8_t* buf, size_t len, ui
 }
 
 // A unary answer: headers, one message, trailers (status 0); or trailers-only on an error.
+// grpc-message is percent-encoded (gRPC over HTTP/2 spec): an exception text with a newline
+// would otherwise be an invalid header value that grpc-go rejects, losing the status
+std::string pct_encode(const std::string& m) {
+  static const char* hex = "0123456789ABCDEF";
+  std::string o;
+  for (unsigned char ch : m) {
+    if (ch >= 0x20 && ch <= 0x7e && ch != '%') {
+      o += (char)ch;
+    } else {
+      o += '%';
+      o += hex[ch >> 4];
+      o += hex[ch & 15];
+    }
+  }
+  return o;
+}
+
 void respond(Conn* c, int32_t sid, int status, const std::string& message, const std::string& body, bool stamp) {
   auto it = c->streams.find(sid);
   if (it == c->streams.end()) return;  // the client went away
@@ -392,9 +416,9 @@ void respond(Conn* c, int32_t sid, int status, const std::string& message, const
   st.t_out = mono_ns();
   st.stamp = stamp;
   if (status != 0) {
-    std::string code = std::to_string(status);
+    std::string code = std::to_string(status), msg = pct_encode(message);
     std::vector<nghttp2_nv> h{nv(":status", kStatus200), nv("content-type", kCtype), nv("grpc-status", code)};
-    if (!message.empty()) h.push_back(nv("grpc-message", message));
+    if (!msg.empty()) h.push_back(nv("grpc-message", msg));
     nghttp2_submit_response(c->sess, sid, h.data(), h.size(), nullptr);
     return;
   }
@@ -528,6 +552,10 @@ void request_done(Conn* c, int32_t sid) {
   Stream& st = it->second;
   st.t_in = mono_ns();
   const std::string& b = st.body;
+  if (st.too_big) {
+    respond(c, sid, 8, "request larger than " + std::to_string(kMaxRequest - 5) + " bytes", "", false);
+    return;
+  }
   if (b.size() < 5 || b[0] != 0) {
     respond(c, sid, b.size() >= 5 ? 12 : 13, b.size() >= 5 ? "compressed messages are not supported"
                                                             : "malformed gRPC message", "", false);
@@ -590,8 +618,13 @@ int on_data_chunk(nghttp2_session*, uint8_t, int32_t sid, const uint8_t* d, size
   Conn* c = static_cast<Conn*>(ud);
   auto it = c->streams.find(sid);
   if (it == c->streams.end()) return 0;
-  if (it->second.body.size() + l > (64u << 20)) return NGHTTP2_ERR_TEMPORAL_CALLBACK_FAILURE;
-  it->second.body.append((const char*)d, l);
+  Stream& st = it->second;
+  if (st.too_big || st.body.size() + l > kMaxRequest) {
+    st.too_big = true;
+    std::string().swap(st.body);
+    return 0;
+  }
+  st.body.append((const char*)d, l);
   return 0;
 }
 
@@ -728,15 +761,25 @@ void accept_loop(gs_dp* s) {
     c->fd = fd;
     c->self = c;
     c->efd = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
+    if (c->efd < 0) {
+      close(fd);
+      continue;
+    }
     s->n.conns++;
     std::lock_guard<std::mutex> lk(s->conns_mu);
-    // connections that ended are dropped from the list (their threads are joined at stop)
+    // connections that ended are joined and dropped (a client that reconnects over and over
+    // costs nothing that stays); the eventfd goes with the last reference
     std::vector<std::shared_ptr<Conn>> live;
-    for (auto& x : s->conns)
-      if (!x->done.load()) live.push_back(x);
+    for (auto& x : s->conns) {
+      if (x->done.load()) {
+        if (x->th.joinable()) x->th.join();
+      } else {
+        live.push_back(x);
+      }
+    }
+    c->th = std::thread(serve_conn, c);
     live.push_back(c);
     s->conns.swap(live);
-    s->conn_threads.emplace_back(serve_conn, c);
   }
 }
 
@@ -784,18 +827,15 @@ void gs_dp_stop(gs_dp* s) {
   shutdown(s->lfd, SHUT_RDWR);
   close(s->lfd);
   if (s->acceptor.joinable()) s->acceptor.join();
+  std::vector<std::shared_ptr<Conn>> conns;
   {
     std::lock_guard<std::mutex> lk(s->conns_mu);
-    for (auto& c : s->conns)
-      if (c->efd >= 0) wake(c.get());
+    conns.swap(s->conns);
   }
-  for (auto& t : s->conn_threads)
-    if (t.joinable()) t.join();
-  {
-    std::lock_guard<std::mutex> lk(s->conns_mu);
-    for (auto& c : s->conns)
-      if (c->efd >= 0) close(c->efd), c->efd = -1;
-  }
+  for (auto& c : conns) wake(c.get());
+  for (auto& c : conns)
+    if (c->th.joinable()) c->th.join();
+  conns.clear();
   s->q_cv.notify_all();
   {
     std::lock_guard<std::mutex> lk(s->mu);

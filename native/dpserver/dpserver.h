@@ -70,6 +70,10 @@ GS_DP_API gs_h2c* gs_h2c_connect(const char* socket_path);
 GS_DP_API int gs_h2c_unary(gs_h2c* h, const char* path, const uint8_t* req, int len, uint8_t* out, int cap,
                            int* out_len, int* status, char* message, int mcap, char* stamp, int scap,
                            int timeout_ms, int64_t* t_send, int64_t* t_recv);
+// gs_h2c_unary with the DATA payload sent as given (no gRPC length prefix added).
+GS_DP_API int gs_h2c_call(gs_h2c* h, const char* path, const uint8_t* body, int len, uint8_t* out, int cap,
+                          int* out_len, int* status, char* message, int mcap, char* stamp, int scap,
+                          int timeout_ms, int64_t* t_send, int64_t* t_recv);
 GS_DP_API void gs_h2c_close(gs_h2c* h);
 
 #ifdef __cplusplus

@@ -5,10 +5,12 @@
 // round trip. This client sends the call and reads the reply in C++, and stamps both ends
 // itself (CLOCK_MONOTONIC), so the kubelet-side latency the bench reports is the plugin's plus
 // the transport's, as the real kubelet sees it. One connection, one call at a time.
+#include <ctype.h>
 #include <errno.h>
 #include <nghttp2/nghttp2.h>
 #include <poll.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <sys/socket.h>
 #include <sys/un.h>
@@ -58,13 +60,26 @@ ssize_t req_read(nghttp2_session*, int32_t, uint8_t* buf, size_t len, uint32_t* 
   return (ssize_t)n;
 }
 
+std::string pct_decode(const std::string& v) {
+  std::string o;
+  for (size_t i = 0; i < v.size(); i++) {
+    if (v[i] == '%' && i + 2 < v.size() && isxdigit((unsigned char)v[i + 1]) && isxdigit((unsigned char)v[i + 2])) {
+      o += (char)strtol(v.substr(i + 1, 2).c_str(), nullptr, 16);
+      i += 2;
+    } else {
+      o += v[i];
+    }
+  }
+  return o;
+}
+
 int on_header(nghttp2_session*, const nghttp2_frame* f, const uint8_t* name, size_t nl, const uint8_t* value,
               size_t vl, uint8_t, void* ud) {
   Call* c = static_cast<gs_h2c*>(ud)->cur;
   if (!c || f->hd.stream_id != c->sid) return 0;
   std::string n((const char*)name, nl), v((const char*)value, vl);
   if (n == "grpc-status") c->status = v;
-  else if (n == "grpc-message") c->message = v;
+  else if (n == "grpc-message") c->message = pct_decode(v);
   else if (n == "gpushare-handler-ns") c->stamp = v;
   return 0;
 }
@@ -143,12 +158,23 @@ GS_DP_API gs_h2c* gs_h2c_connect(const char* socket_path) {
 GS_DP_API int gs_h2c_unary(gs_h2c* h, const char* path, const uint8_t* req, int len, uint8_t* out, int cap,
                            int* out_len, int* status, char* message, int mcap, char* stamp, int scap,
                            int timeout_ms, int64_t* t_send, int64_t* t_recv) {
+  std::string framed(5, '\0');
+  uint32_t l = (uint32_t)len;
+  framed[1] = (char)(l >> 24), framed[2] = (char)(l >> 16), framed[3] = (char)(l >> 8), framed[4] = (char)l;
+  framed.append((const char*)req, (size_t)len);
+  return gs_h2c_call(h, path, (const uint8_t*)framed.data(), (int)framed.size(), out, cap, out_len, status,
+                     message, mcap, stamp, scap, timeout_ms, t_send, t_recv);
+}
+
+// The same call with the request body sent as given (`body` is the whole DATA payload: gRPC
+// length-prefixed messages, or anything else) — how the tests send what a broken or hostile
+// client would.
+GS_DP_API int gs_h2c_call(gs_h2c* h, const char* path, const uint8_t* body, int len, uint8_t* out, int cap,
+                          int* out_len, int* status, char* message, int mcap, char* stamp, int scap,
+                          int timeout_ms, int64_t* t_send, int64_t* t_recv) {
   std::lock_guard<std::mutex> lk(h->mu);
   Call c;
-  c.req.assign(5, '\0');
-  uint32_t l = (uint32_t)len;
-  c.req[1] = (char)(l >> 24), c.req[2] = (char)(l >> 16), c.req[3] = (char)(l >> 8), c.req[4] = (char)l;
-  c.req.append((const char*)req, (size_t)len);
+  c.req.assign((const char*)body, (size_t)len);
   h->cur = &c;
   std::string p = path;
   auto nv = [](const char* n, const std::string& v) {

@@ -234,8 +234,9 @@ def test_each_prepared_answer_is_handed_out_once_under_load(tmp_path):
 
 @pytest.mark.parametrize("san", ["asan", "tsan"])
 def test_native_server_under_sanitizers(tmp_path, san):
-    """libgpushare_dpserver built with ASan+UBSan / TSan, driven by concurrent clients (fast
-    answers, forwarded requests, ListAndWatch, table publishes) in a separate interpreter."""
+    """libgpushare_dpserver built with ASan+UBSan / TSan, driven by the hostile-client sequence
+    and then by concurrent clients (fast answers, forwarded requests, ListAndWatch, table
+    publishes) in a separate interpreter."""
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     r = subprocess.run([sys.executable, os.path.join(root, "native", "build.py"), "dpserver", "--sanitize", san],
                        capture_output=True, text=True)
@@ -249,6 +250,7 @@ sys.path.insert(0, {root!r})
 import pathlib, tests.test_native_server as T
 tmp = pathlib.Path({str(tmp_path)!r})
 srv, al, src = T._server(tmp, [T.mkpod("p", 1, 0, 10)])
+T._hostile(srv, n_random=20)
 stubs = [T._stub(srv) for _ in range(4)]
 law = stubs[0][1].ListAndWatch(T.api.Empty())
 next(law)
@@ -361,3 +363,149 @@ def test_native_journal_rotates_without_losing_a_pending_patch(tmp_path):
         al.close()
     j = AllocJournal(str(tmp_path / "j.jsonl"))
     assert len(j.unlanded()) == 10                           # every answered pod still owes its PATCH
+
+
+# ---- a broken or hostile client ---------------------------------------------------------------
+_PREFACE = b"PRI * HTTP/2.0\r\n\r\nSM\r\n\r\n"
+
+
+def _frame(typ, flags, sid, payload=b""):
+    return len(payload).to_bytes(3, "big") + bytes([typ, flags]) + sid.to_bytes(4, "big") + payload
+
+
+def _hpack(path):
+    # literal header fields without indexing, new names, no Huffman (RFC 7541 6.2.2)
+    def lit(k, v):
+        return b"\x00" + bytes([len(k)]) + k + bytes([len(v)]) + v
+
+    return b"".join(lit(k, v) for k, v in ((b":method", b"POST"), (b":scheme", b"http"), (b":path", path),
+                                            (b":authority", b"x"), (b"content-type", b"application/grpc"),
+                                            (b"te", b"trailers")))
+
+
+def _raw(sock_path, data, read_s=0.2):
+    """Send raw bytes on a fresh connection, read what comes back for read_s, hang up."""
+    import socket
+
+    s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+    s.connect(sock_path)
+    got = b""
+    try:
+        s.sendall(data)
+        s.settimeout(read_s)
+        while True:
+            b = s.recv(65536)
+            if not b:
+                break
+            got += b
+    except OSError:                                    # timeout, reset, would block
+        pass
+    finally:
+        s.close()
+    return got
+
+
+def _hostile(srv, seed=0, n_random=60):
+    """Everything a broken client can send; returns the number of forwarded requests it left
+    for the handlers (each must still be answered without harm)."""
+    import random
+
+    from aliyun_gpushare_device_plugin_amd.sim.h2client import NativeUnaryClient, UnaryError
+
+    alloc = b"/v1beta1.DevicePlugin/Allocate"
+    msg = _req("h-0").SerializeToString()
+    pre = len(msg).to_bytes(4, "big")
+    cl = NativeUnaryClient(srv.socket)
+    try:
+        for body, want in ((b"", 13), (b"\x00\x00\x00", 13),                 # truncated prefix
+                           (b"\x01" + pre + msg, 12),                          # compressed flag
+                           (b"\x00" + (len(msg) + 1).to_bytes(4, "big") + msg, 13),
+                           (b"\x00\xff\xff\xff\xff" + msg, 13),
+                           (b"\x00" + pre + msg + b"\x00" + pre + msg, 13),    # two messages on a unary call
+                           (b"\x00" + pre + msg, 0)):
+            if want == 0:
+                raw, _, _, _ = cl.unary(alloc.decode(), body, framed=True)
+                assert api.AllocateResponse.FromString(raw).container_responses
+                continue
+            with pytest.raises(UnaryError) as e:
+                cl.unary(alloc.decode(), body, framed=True)
+            assert e.value.status == want, (body[:8], e.value)
+        big = b"\x00" + (9 << 20).to_bytes(4, "big") + bytes(9 << 20)      # over the request limit
+        with pytest.raises(UnaryError) as e:
+            cl.unary(alloc.decode(), big, framed=True)
+        assert e.value.status == 8
+    finally:
+        cl.close()
+    settings = _frame(4, 0, 0)
+    hdr = _frame(1, 4, 1, _hpack(alloc))                                    # HEADERS, END_HEADERS
+    data = _frame(0, 1, 1, b"\x00" + pre + msg)                             # DATA, END_STREAM
+    forwarded = 0
+    assert _raw(srv.socket, b"GET / HTTP/1.1\r\nHost: x\r\n\r\n") is not None  # not HTTP/2
+    _raw(srv.socket, _PREFACE + settings + hdr + data + _frame(3, 0, 1, (8).to_bytes(4, "big")))  # RST_STREAM
+    forwarded += 1
+    _raw(srv.socket, _PREFACE + settings + hdr + data, read_s=0)            # hang up before the reply
+    forwarded += 1
+    _raw(srv.socket, _PREFACE + settings + _frame(0, 1, 3, b"\x00" * 9))    # DATA on an idle stream
+    _raw(srv.socket, _PREFACE + settings + hdr)                             # a request never finished
+    _raw(srv.socket, _PREFACE + settings + _frame(1, 5, 1, _hpack(b"/v1beta1.DevicePlugin/ListAndWatch")),
+         read_s=0.05)                                                        # a watch dropped mid-stream
+    _raw(srv.socket, _PREFACE + settings + _frame(1, 4, 1, b"\xff\xff\xff\xff"))  # HPACK garbage
+    rnd = random.Random(seed)
+    for _ in range(n_random):                                                # random frames after the preface
+        frames = b"".join(_frame(rnd.choice([0, 1, 2, 3, 4, 5, 6, 7, 8, 9, rnd.randrange(256)]), rnd.randrange(256),
+                                 rnd.choice([0, 1, 3, rnd.randrange(1 << 31)]),
+                                 bytes(rnd.randrange(256) for _ in range(rnd.randrange(40))))
+                          for _ in range(rnd.randrange(1, 6)))
+        _raw(srv.socket, _PREFACE + settings + (hdr if rnd.random() < 0.5 else b"") + frames, read_s=0.01)
+    return forwarded
+
+
+def test_broken_and_hostile_clients_leave_the_server_serving(tmp_path):
+    """Malformed gRPC messages get the gRPC status grpc-go would give; protocol garbage, resets
+    and hang-ups with requests in flight end that connection only; the server keeps answering,
+    and ended connections leave no thread or descriptor behind."""
+    srv, al, src = _server(tmp_path, [mkpod(f"p{i}", 1, i % 2, 10 + i) for i in range(4)])
+    try:
+        fds0 = len(os.listdir("/proc/self/fd"))
+        _hostile(srv)
+        ch, stub = _stub(srv)
+        try:
+            r = stub.Allocate(_req("after-0"))
+            assert r.container_responses[0].envs[const.ENV_RESOURCE_INDEX] in ("0", "1")
+            assert stub.GetDevicePluginOptions(api.Empty()) == srv.options()
+        finally:
+            ch.close()
+        st = srv.stats()
+        assert st["connections"] >= 60 and st["unknown"] == 0
+        _raw(srv.socket, _PREFACE)                     # the next accept joins every ended connection
+        time.sleep(0.1)
+        assert len(os.listdir("/proc/self/fd")) <= fds0 + 4       # no eventfd per ended connection
+    finally:
+        srv.stop()
+        al.close()
+
+
+def test_error_messages_survive_the_trailer(tmp_path):
+    """A handler error whose text has a newline or a '%' still reaches the client intact
+    (grpc-message is percent-encoded; a raw newline is an invalid header value for grpc-go)."""
+    from aliyun_gpushare_device_plugin_amd.sim.h2client import NativeUnaryClient, UnaryError
+
+    srv, al, src = _server(tmp_path, [])
+
+    def boom(*a, **kw):
+        raise RuntimeError("line one\nline two 100% é")
+
+    al.allocate_raw = boom
+    cl = NativeUnaryClient(srv.socket)
+    ch, stub = _stub(srv)
+    try:
+        with pytest.raises(UnaryError) as e:
+            cl.unary("/v1beta1.DevicePlugin/Allocate", _req("x").SerializeToString())
+        assert e.value.status == 2 and "line one\nline two 100% é" in e.value.message
+        with pytest.raises(grpc.RpcError) as g:
+            stub.Allocate(_req("x"))
+        assert g.value.code() == grpc.StatusCode.UNKNOWN and "line one\nline two 100% é" in g.value.details()
+    finally:
+        ch.close()
+        cl.close()
+        srv.stop()
