@@ -7,13 +7,13 @@ JOBS ?= 8
 
 all: build test
 
-build:                      ## native libs: SMI library + CLI, HIP quota shim, gfx950 kernels (cross-compiles)
+build:                      ## native libs: SMI library + CLI, HIP quota shim, DevicePlugin server, gfx950 kernels
 	PYTORCH_ROCM_ARCH=$(ARCH) $(PY) native/build.py -j $(JOBS)
 	$(PY) -c "import __graft_entry__ as g; g.build()"
 
 build-san:                  ## host-side ASan+UBSan and TSan variants (_native/asan, _native/tsan)
-	$(PY) native/build.py gpuinfo hipshim --sanitize asan
-	$(PY) native/build.py gpuinfo hipshim --sanitize tsan
+	$(PY) native/build.py gpuinfo hipshim dpserver --sanitize asan
+	$(PY) native/build.py gpuinfo hipshim dpserver --sanitize tsan
 
 lint:                       ## byte-compile everything; reject tabs / trailing whitespace in sources
 	$(PY) -m compileall -q aliyun_gpushare_device_plugin_amd tests tools bench.py __graft_entry__.py
