@@ -430,12 +430,33 @@ def _hostile(srv, seed=0, n_random=60):
             with pytest.raises(UnaryError) as e:
                 cl.unary(alloc.decode(), body, framed=True)
             assert e.value.status == want, (body[:8], e.value)
+        rnd = random.Random(seed)
+        for k in range(40):                       # well-framed, random or mangled protobuf bodies
+            body = bytearray(_req(f"z{k}", f"z{k}b").SerializeToString())
+            if k % 2:
+                body = bytearray(rnd.randrange(256) for _ in range(rnd.randrange(1, 48)))
+            else:
+                for _ in range(rnd.randrange(1, 4)):
+                    body[rnd.randrange(len(body))] = rnd.randrange(256)
+            try:
+                cl.unary(alloc.decode(), bytes(body))
+            except UnaryError as e:               # the engine's verdict on a bad request
+                assert e.status in (2, 9), e
         big = b"\x00" + (9 << 20).to_bytes(4, "big") + bytes(9 << 20)      # over the request limit
         with pytest.raises(UnaryError) as e:
             cl.unary(alloc.decode(), big, framed=True)
         assert e.value.status == 8
     finally:
         cl.close()
+    good = _native_blob(1, 0, 0, [Cand(*_cand("t0", 1))], ["r0"])
+    for k in range(200):                          # truncated and corrupted fast tables are refused whole
+        blob = bytearray(good[:rnd.randrange(len(good))] if k % 2 else good)
+        if not k % 2:
+            for _ in range(rnd.randrange(1, 4)):
+                blob[rnd.randrange(len(blob))] = rnd.randrange(256)
+        b = bytes(blob)
+        assert srv._lib.gs_dp_fast_publish(srv._h, b, len(b)) in (0, -1)
+    srv.fast.publish(_native_blob(0, 0, 1 << 31, [], []))                 # back to "no table"
     settings = _frame(4, 0, 0)
     hdr = _frame(1, 4, 1, _hpack(alloc))                                    # HEADERS, END_HEADERS
     data = _frame(0, 1, 1, b"\x00" + pre + msg)                             # DATA, END_STREAM
@@ -450,7 +471,6 @@ def _hostile(srv, seed=0, n_random=60):
     _raw(srv.socket, _PREFACE + settings + _frame(1, 5, 1, _hpack(b"/v1beta1.DevicePlugin/ListAndWatch")),
          read_s=0.05)                                                        # a watch dropped mid-stream
     _raw(srv.socket, _PREFACE + settings + _frame(1, 4, 1, b"\xff\xff\xff\xff"))  # HPACK garbage
-    rnd = random.Random(seed)
     for _ in range(n_random):                                                # random frames after the preface
         frames = b"".join(_frame(rnd.choice([0, 1, 2, 3, 4, 5, 6, 7, 8, 9, rnd.randrange(256)]), rnd.randrange(256),
                                  rnd.choice([0, 1, 3, rnd.randrange(1 << 31)]),
