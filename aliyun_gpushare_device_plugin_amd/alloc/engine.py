@@ -207,6 +207,7 @@ class Allocator:
         self._native_hold = False                 # a block kept while a multi-container claim is open
         self._published = (-1, -1)                # (pending version, gen) of the last native table
         self.native_rotate_bytes = 16 << 20       # rotate the native journal file past this
+        self.native_prep_keep = 4096              # prepared answers kept for native claims past the current table
         for k, uid, t, resp in self.journal.answers():   # grants of a previous instance (journal TTL)
             if len(resp.container_responses) == 1:
                 self.grants.record(k, self._grant_from(resp.container_responses[0], uid, t))
@@ -827,11 +828,14 @@ class Allocator:
             # the native server answers from this table while the cache and the engine are still
             # at (version, gen); a possible replay (IDs of journaled answers) goes to the engine
             self._fast = None
+            # every answer a published table holds must stay resolvable when its claim comes
+            # back: the current table's entries always; of the older ones, the most recent
             prep = self._native_prep
             for c in out:
-                prep[c.uid] = c
-            if len(prep) > 4096:          # only recent candidates can still come back as claims
-                for u in list(prep)[:len(prep) - 2048]:
+                prep.pop(c.uid, None)
+                prep[c.uid] = c           # (re)inserted last: the oldest entries are the stale ones
+            if len(prep) > self.native_prep_keep + len(out):
+                for u in list(prep)[:len(prep) - len(out) - self.native_prep_keep // 2]:
                     del prep[u]
             legacy = time.time() < self.journal._legacy_until
             nat.publish(_native_blob(version, gen, 1 if self.podres is not None else 0,

@@ -529,3 +529,28 @@ def test_error_messages_survive_the_trailer(tmp_path):
         ch.close()
         cl.close()
         srv.stop()
+
+
+def test_prepared_answers_of_the_current_table_are_never_pruned(tmp_path):
+    """The engine keeps every published candidate resolvable for the native server's claims:
+    a pod that stays pending while thousands of others come and go is never pruned (it was,
+    by first insertion, once more than 4096 candidates had been seen)."""
+    class Nat:                                    # the engine's side of the server: publish only
+        def publish(self, blob):
+            self.blob = blob
+
+    model = DeviceModel([gpu(i, 8 << 30) for i in range(2)], const.GIB)
+    src = VSource([mkpod("old", 1, 0, 1)])
+    al = Allocator(model, src, FakeClient(src), "node-a", AllocatorOptions(async_patch=False, fast_path=False))
+    al.native = Nat()
+    al.native_prep_keep = 4
+    try:
+        for r in range(12):
+            src.pods = [mkpod("old", 1, 0, 1)] + [mkpod(f"p{r}-{i}", 2, i % 2, 10 + i) for i in range(5)]
+            al._prepare(src)
+            assert "uid-old" in al._native_prep
+            assert all(f"uid-p{r}-{i}" in al._native_prep for i in range(5))
+            assert len(al._native_prep) <= 6 + al.native_prep_keep
+    finally:
+        al.native = None
+        al.close()
