@@ -808,13 +808,7 @@ class Allocator:
             if c is None:
                 if self.model.gpu(g) is None:
                     continue
-                cr = self._container_response(g, shape[0], shape[0], u, 0, None)
-                r = api.AllocateResponse()
-                r.container_responses.append(cr)
-                body = r.SerializeToString()
-                c = _Prepared(u, O.namespace(p), O.name(p), shape[0], False, g, body,
-                              AllocJournal.fast_head(u, O.namespace(p), O.name(p), body),
-                              cr.annotations.get(const.CTR_ANNOTATION_LEDGER, ""))
+                c = self._prepared(p, u, g, shape[0])
             keep[k] = c
             out.append(c)
         nat = self.native
@@ -844,6 +838,16 @@ class Allocator:
         if self.journal.indexed_uids():         # replay index: only pods that can still be retried
             pend = {O.uid(p) for p in src.pending_pods()}
             self.journal.prune_index(pend)
+
+    def _prepared(self, p: dict, u: str, g: int, units: int) -> "_Prepared":
+        """The answer to a single-container pod's Allocate, serialized ahead of the request."""
+        cr = self._container_response(g, units, units, u, 0, None)
+        r = api.AllocateResponse()
+        r.container_responses.append(cr)
+        body = r.SerializeToString()
+        return _Prepared(u, O.namespace(p), O.name(p), units, False, g, body,
+                         AllocJournal.fast_head(u, O.namespace(p), O.name(p), body),
+                         cr.annotations.get(const.CTR_ANNOTATION_LEDGER, ""))
 
     def _allocate_full(self, req, t0: float):
         """The full Allocate path, counting the apiserver round trips it makes (the handler
@@ -1232,9 +1236,17 @@ class Allocator:
             self._unpatched.add(uid)
             self._revoked.discard(uid)
             self._answer_seq += 1
-        if pick is None:     # never: the server only answers from a table the engine published
-            log.error("native fast path answered pod uid %s that no published table holds", uid)
-            return
+        if pick is None:
+            # not expected (every entry of a published table stays in _native_prep): the
+            # answer went out, so the pod still owes its ASSIGNED patch — take it from the cache
+            p = self.pods.get(uid)
+            log.error("native fast path answered pod uid %s outside the prepared answers%s", uid,
+                      "" if p is not None else "; the pod is gone from the cache, no patch")
+            if p is None:
+                with self._mu:
+                    self._unpatched.discard(uid)
+                return
+            pick = self._prepared(p, uid, A.gpu_id_from_annotation(p), self._info(p)[3][0])
         req = api.AllocateRequest.FromString(rb)
         ids = req.container_requests[0].devices_ids
         self.journal.note_fast(uid, pick.ns, pick.name, t, ids)

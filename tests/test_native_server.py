@@ -554,3 +554,23 @@ def test_prepared_answers_of_the_current_table_are_never_pruned(tmp_path):
     finally:
         al.native = None
         al.close()
+
+
+def test_a_native_claim_outside_the_prepared_answers_still_gets_its_patch(tmp_path):
+    """Defensive path: a claim whose answer the engine no longer holds is rebuilt from the pod
+    cache (PATCH, grant), or — the pod gone — is not left owing a PATCH forever."""
+    src = VSource([mkpod("p", 2, 1, 10)])
+    model = DeviceModel([gpu(i, 8 << 30) for i in range(2)], const.GIB)
+    al = Allocator(model, src, FakeClient(src), "node-a", AllocatorOptions(async_patch=True, fast_path=False))
+    try:
+        al._native_taken(("uid-p", _req("a", "b").SerializeToString(), time.time(), 1000))
+        t = time.monotonic() + 5
+        while not al.client.patches and time.monotonic() < t:
+            time.sleep(0.01)
+        assert [n for _, n, _ in al.client.patches] == ["p"]
+        al._drain_post()
+        assert [(g.gpu, g.claimed) for _, g in al.grants.items()] == [(1, "uid-p")]
+        al._native_taken(("uid-gone", _req("c").SerializeToString(), time.time(), 1000))
+        assert "uid-gone" not in al._unpatched
+    finally:
+        al.close()
