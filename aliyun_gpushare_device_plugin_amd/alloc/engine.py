@@ -1205,17 +1205,21 @@ class Allocator:
             rec = nat.taken_next(200)
             if rec is None:
                 break
-            if rec:
-                self._native_taken(rec)
-            if self.journal.path and nat.journal_used() > self.native_rotate_bytes:
-                nat.block()
-                try:
-                    self._drain_native(nat)
-                    self._drain_post()
-                    self.journal.compact()
-                    nat.journal_rotate()
-                finally:
-                    nat.unblock()
+            try:
+                if rec:
+                    self._native_taken(rec)
+                if self.journal.path and nat.journal_used() > self.native_rotate_bytes:
+                    nat.block()
+                    try:
+                        self._drain_native(nat)
+                        self._drain_post()
+                        self.journal.compact()
+                        nat.journal_rotate()
+                    finally:
+                        nat.unblock()
+            except Exception as e:  # noqa: BLE001 - one bad record must not stop every later claim's bookkeeping
+                log.error("native claim bookkeeping failed: %s", e)
+                self._stop.wait(0.05)
 
     def _drain_native(self, nat=None) -> None:
         nat = nat or self.native

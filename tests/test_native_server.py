@@ -574,3 +574,35 @@ def test_a_native_claim_outside_the_prepared_answers_still_gets_its_patch(tmp_pa
         assert "uid-gone" not in al._unpatched
     finally:
         al.close()
+
+
+def test_claim_reader_survives_a_bookkeeping_error(tmp_path):
+    pods = [mkpod(f"p{i}", 1, i % 2, 10 + i) for i in range(3)]
+    srv, al, src = _server(tmp_path, pods)
+    al.opts.fast_path = True
+    src.changed.set()
+    ch, stub = _stub(srv)
+    real, calls = al._native_taken, []
+
+    def flaky(rec):
+        calls.append(rec[0])
+        if len(calls) == 1:
+            raise RuntimeError("injected")
+        return real(rec)
+
+    al._native_taken = flaky
+    try:
+        for k in range(3):
+            t = time.monotonic() + 5
+            while al._published != (src.pending_version, al._gen) and time.monotonic() < t:
+                time.sleep(0.002)
+            stub.Allocate(_req(f"q{k}"))
+        t = time.monotonic() + 5
+        while len(al.client.patches) < 2 and time.monotonic() < t:
+            time.sleep(0.01)
+        assert srv.stats()["fast"] == 3 and len(calls) == 3
+        assert len(al.client.patches) == 2          # the reader went on after the failure
+    finally:
+        ch.close()
+        srv.stop()
+        al.close()
