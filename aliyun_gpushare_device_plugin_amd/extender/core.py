@@ -72,6 +72,12 @@ class Extender:
         self.plan_budget = 50_000
         self.plan_enabled = True
         self._lock = threading.Lock()
+        self.elector = None                   # extender/leader.py LeaderElector with --leader-elect
+
+    def serving(self) -> bool:
+        """Whether this replica answers filter / bind: always without leader election, else
+        only while it holds the lease."""
+        return self.elector is None or self.elector.is_leader()
 
     # -- cache ----------------------------------------------------------------------------
     def sync(self):
@@ -418,7 +424,8 @@ class Extender:
 def serve_http(ext: Extender, host: str = "127.0.0.1", port: int = 0):
     """Extender HTTP endpoints: ``POST /gpushare-scheduler/filter`` (ExtenderArgs →
     ExtenderFilterResult) and ``POST /gpushare-scheduler/bind`` (ExtenderBindingArgs →
-    ExtenderBindingResult)."""
+    ExtenderBindingResult); ``GET /healthz`` (alive) and ``GET /readyz`` (serving: 503 on a
+    replica that is not the leader, which answers the POSTs 503 too)."""
 
     class H(http.server.BaseHTTPRequestHandler):
         protocol_version = "HTTP/1.1"
@@ -434,9 +441,33 @@ def serve_http(ext: Extender, host: str = "127.0.0.1", port: int = 0):
             self.end_headers()
             self.wfile.write(b)
 
+        def _plain(self, code: int, text: str):
+            b = text.encode()
+            self.send_response(code)
+            self.send_header("Content-Type", "text/plain")
+            self.send_header("Content-Length", str(len(b)))
+            self.end_headers()
+            self.wfile.write(b)
+
+        def do_GET(self):
+            if self.path == "/healthz":
+                return self._plain(200, "ok")
+            if self.path == "/readyz":
+                return self._plain(200, "leader" if ext.elector else "ok") if ext.serving() else \
+                    self._plain(503, "not the leader")
+            return self._plain(404, "not found")
+
         def do_POST(self):
             n = int(self.headers.get("Content-Length") or 0)
             args = json.loads(self.rfile.read(n) or b"{}")
+            if not ext.serving():
+                # another replica holds the lease: its ledger, not this one's, decides
+                b = json.dumps({"Error": "not the leader"}).encode()
+                self.send_response(503)
+                self.send_header("Content-Type", "application/json")
+                self.send_header("Content-Length", str(len(b)))
+                self.end_headers()
+                return self.wfile.write(b)
             if self.path.endswith("/filter"):
                 pod = args.get("Pod") or args.get("pod") or {}
                 names = args.get("NodeNames") or args.get("nodenames") or \

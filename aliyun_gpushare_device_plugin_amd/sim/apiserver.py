@@ -10,7 +10,9 @@ exercised end to end:
 * WATCH ``/api/v1/pods?watch=1`` as a chunked JSON-lines stream, replaying from
   ``resourceVersion`` (410 Gone when the history window has moved past it) and emitting
   DELETED when an object stops matching the watch's selector (watch-cache semantics);
-* optimistic concurrency: a PATCH carrying a stale ``metadata.resourceVersion`` gets 409.
+* optimistic concurrency: a PATCH carrying a stale ``metadata.resourceVersion`` gets 409;
+* ``coordination.k8s.io/v1`` Leases: GET, POST, PUT (compare-and-swap on ``resourceVersion``,
+  409 on a stale one) — the extender's leader election.
 
 Run standalone: ``python -m aliyun_gpushare_device_plugin_amd.sim.apiserver --port 0``.
 """
@@ -123,6 +125,7 @@ class Store:
         self.rv = 1
         self.pods: dict[tuple, dict] = {}
         self.nodes: dict[str, dict] = {}
+        self.leases: dict[tuple, dict] = {}
         self.history: collections.deque = collections.deque(maxlen=history)  # (rv, type, old, new)
         self.watchers: list[_Watcher] = []
         self.requests = collections.Counter()
@@ -276,6 +279,34 @@ class Store:
             self.nodes[name] = new
             return new
 
+    # -- leases ---------------------------------------------------------------------------
+    def create_lease(self, ns, obj):
+        with self.lock:
+            obj = copy.deepcopy(obj)
+            md = obj.setdefault("metadata", {})
+            md["namespace"] = ns
+            key = (ns, md.get("name"))
+            if key in self.leases:
+                return None
+            md.setdefault("uid", str(uuidlib.uuid4()))
+            self._bump(obj)
+            self.leases[key] = obj
+            return copy.deepcopy(obj)
+
+    def replace_lease(self, ns, name, obj):
+        """PUT: the stored object's ``resourceVersion`` must match the one sent (ValueError)."""
+        with self.lock:
+            cur = self.leases.get((ns, name))
+            if cur is None:
+                return None
+            if (obj.get("metadata") or {}).get("resourceVersion") != cur["metadata"]["resourceVersion"]:
+                raise ValueError("conflict")
+            new = copy.deepcopy(obj)
+            new["metadata"] = dict(new.get("metadata") or {}, name=name, namespace=ns, uid=cur["metadata"]["uid"])
+            self._bump(new)
+            self.leases[(ns, name)] = new
+            return copy.deepcopy(new)
+
     # -- watch ----------------------------------------------------------------------------
     def add_watcher(self, fsel, lsel, since_rv, push=None):
         with self.lock:
@@ -298,6 +329,7 @@ class Store:
 
 _POD_RE = re.compile(r"^/api/v1/namespaces/([^/]+)/pods(?:/([^/]+))?(?:/(status|binding))?$")
 _NODE_RE = re.compile(r"^/api/v1/nodes(?:/([^/]+))?(?:/(status))?$")
+_LEASE_RE = re.compile(r"^/apis/coordination\.k8s\.io/v1/namespaces/([^/]+)/leases(?:/([^/]+))?$")
 
 
 _REASONS = {200: "OK", 201: "Created", 404: "Not Found", 409: "Conflict", 410: "Gone", 400: "Bad Request",
@@ -309,11 +341,37 @@ def _status(code, reason, msg):
                   "code": code}
 
 
+def _lease_route(store: Store, method: str, m, body: bytes):
+    store.requests[f"{method} lease"] += 1
+    code = store.fault("lease")
+    if code:
+        return _status(code, "ServiceUnavailable", "injected fault")
+    ns, name = m.group(1), m.group(2)
+    if method == "GET" and name:
+        with store.lock:
+            obj = copy.deepcopy(store.leases.get((ns, name)))
+        return (200, obj) if obj else _status(404, "NotFound", f'leases.coordination.k8s.io "{name}" not found')
+    obj = json.loads(body) if body else {}
+    if method == "POST" and not name:
+        made = store.create_lease(ns, obj)
+        return (201, made) if made else _status(409, "AlreadyExists", "lease already exists")
+    if method == "PUT" and name:
+        try:
+            new = store.replace_lease(ns, name, obj)
+        except ValueError:
+            return _status(409, "Conflict", _CONFLICT_MSG)
+        return (200, new) if new else _status(404, "NotFound", f'leases.coordination.k8s.io "{name}" not found')
+    return _status(405, "MethodNotAllowed", method)
+
+
 def route(store: Store, method: str, target: str, body: bytes):
     """One REST request against ``store``. Returns ``(code, obj)``, or ``("watch", fsel, lsel, rv,
     timeout)`` for a watch (the caller streams it)."""
     u = urllib.parse.urlsplit(target)
     path = u.path.rstrip("/")
+    m = _LEASE_RE.match(path)
+    if m:
+        return _lease_route(store, method, m, body)
     if method == "GET":
         q = dict(urllib.parse.parse_qsl(u.query)) if u.query else {}
         if path == "/debug/requests":      # simulator introspection: request counts by verb/kind

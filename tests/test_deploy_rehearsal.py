@@ -77,10 +77,15 @@ def test_shipped_manifests_run_a_node(hostroot):
         # ---- the scheduler extender Deployment and kube-scheduler's config for it
         docs = D.load(os.path.join(ROOT, "deploy", "scheduler-extender.yaml"))
         dep = next(d for d in docs if d["kind"] == "Deployment")
-        ect = D.resolve(dep, hostroot, {}, {"--apiserver": api.url, "--port": "0", "--host": "127.0.0.1",
-                                            "--resync": "0.5"})
+        ect = D.resolve(dep, hostroot, {"metadata.name": "gpushare-scheduler-extender-0"},
+                        {"--apiserver": api.url, "--port": "0", "--host": "127.0.0.1", "--resync": "0.5"})
+        assert "--leader-elect" in ect.argv and ect.env["POD_NAME"] == "gpushare-scheduler-extender-0"
         ext = D.start(ect, os.path.join(hostroot, "extender.log"))
         eport = int(ext.stdout.readline().split()[1])
+        # the Service routes kube-scheduler to a ready replica: the Lease holder
+        assert D.wait_for(lambda: D.http_get(f"http://127.0.0.1:{eport}/readyz")[0] == 200, 10.0)
+        lease = api.store.leases[("kube-system", "gpushare-scheduler-extender")]
+        assert lease["spec"]["holderIdentity"].startswith("gpushare-scheduler-extender-0_")
         cm = next(d for d in docs if d["kind"] == "ConfigMap")
         sched = D.Scheduler(cm["data"]["scheduler-config.yaml"], f"127.0.0.1:{eport}")
         assert sched.managed == [const.RESOURCE_NAME]
