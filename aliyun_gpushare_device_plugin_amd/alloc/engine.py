@@ -124,6 +124,10 @@ class AllocatorOptions:
     identify: bool = True
     identify_timeout_s: float = 0.2
     identify_backoff_s: float = 5.0
+    # an Allocate for a pod the pod watch has not delivered yet (the kubelet's own watch can be
+    # ahead of the plugin's) waits up to this long for the watch before it falls back to a LIST
+    # (a round trip to the apiserver on the kubelet's path)
+    watch_grace_s: float = 0.005
 
 
 @dataclasses.dataclass
@@ -839,6 +843,27 @@ class Allocator:
             pend = {O.uid(p) for p in src.pending_pods()}
             self.journal.prune_index(pend)
 
+    def _hold(self, claim, complete: bool) -> None:
+        """A full-path match (caller holds ``_mu``): keep the pod claimed across its PATCH."""
+        if claim is None:
+            return
+        self._revoked.discard(claim.uid)
+        if complete:
+            self._claims[claim.uid] = claim
+        if self.native is not None:
+            self.native.take(claim.uid)          # never answered from the table again
+
+    def _await_watch(self, v0) -> bool:
+        """Wait up to ``watch_grace_s`` for the pod watch to change the Pending set since
+        ``v0``; True if it did (a retry of the cache match may now find the pod)."""
+        wait = getattr(self.pods, "wait_pending_change", None)
+        if wait is None or v0 is None or self.opts.watch_grace_s <= 0:
+            return False
+        t = time.perf_counter()
+        changed = wait(v0, self.opts.watch_grace_s)
+        self.metrics.allocate_latency.observe(time.perf_counter() - t, phase="watch_wait")
+        return changed
+
     def _prepared(self, p: dict, u: str, g: int, units: int) -> "_Prepared":
         """The answer to a single-container pod's Allocate, serialized ahead of the request."""
         cr = self._container_response(g, units, units, u, 0, None)
@@ -899,21 +924,24 @@ class Allocator:
         try:
             held = self._identity_list(sizes)          # outside the lock (kubelet RPC)
             tl = time.perf_counter()
+            v0 = getattr(self.pods, "pending_version", None)
             with self._mu:
                 tb = time.perf_counter()
                 claim, complete = self._match(sizes, fresh=False, held=held)
                 t1 = time.perf_counter()
-                if claim is None:
-                    # watch lag: the kubelet may see a bind before our cache does (per-call
-                    # sources: the view is already an authoritative LIST)
+                self._hold(claim, complete)
+            if claim is None and self._await_watch(v0):
+                # watch lag: the kubelet saw the bind first; the pod watch delivered within the grace
+                with self._mu:
+                    claim, complete = self._match(sizes, fresh=False, held=held)
+                    self._hold(claim, complete)
+            if claim is None:
+                # still not in the cache: an authoritative LIST (per-call sources: the view
+                # already is one)
+                with self._mu:
                     claim, complete = self._match(sizes, fresh=True, held=held)
-                if claim is not None:
-                    self._revoked.discard(claim.uid)
-                    if complete:
-                        self._claims[claim.uid] = claim   # held across the PATCH
-                    if self.native is not None:
-                        self.native.take(claim.uid)      # never answered from the table again
-                t2 = time.perf_counter()
+                    self._hold(claim, complete)
+            t2 = time.perf_counter()
             hist.observe(ta - t0, phase="prelude")      # request key, journal replay check
             hist.observe(tl - ta, phase="identity")     # pod-resources List (ambiguous requests only)
             hist.observe(tb - tl, phase="lock")

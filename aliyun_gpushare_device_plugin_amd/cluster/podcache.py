@@ -172,6 +172,7 @@ class WatchCache(PodSource):
         # cache ahead of the version it was told
         self.pending_version = 0
         self.on_pending_change = None
+        self._pending_cv = threading.Condition(self._lock)
         self.changed = threading.Event()
         self._synced = threading.Event()
         self._stop = threading.Event()
@@ -272,6 +273,12 @@ class WatchCache(PodSource):
         hook = self.on_pending_change
         if hook is not None:
             hook(self.pending_version)
+        self._pending_cv.notify_all()
+
+    def wait_pending_change(self, version: int, timeout: float) -> bool:
+        """Wait until the Pending set changed since ``version`` (or ``timeout``); True if it did."""
+        with self._lock:
+            return self._pending_cv.wait_for(lambda: self.pending_version != version, timeout)
 
     def _put(self, u: str, pod: dict) -> None:
         self.version += 1

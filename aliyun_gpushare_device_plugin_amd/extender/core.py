@@ -69,7 +69,16 @@ class Extender:
         # the pending queue (unscheduled gpu-mem pods, not TP groups) and its joint placement
         self._pending: dict[str, dict] = {}
         self._plan: dict[str, tuple[str, int]] = {}
+        self._plan_res: dict[tuple[str, int], int] = {}   # (node, gpu) -> HBM the plan holds there
+        self._unplanned: dict[str, None] = {}             # queued since the last plan (arrival order)
+        self._plan_at = 0.0
         self.plan_budget = 50_000
+        self.plan_deadline_s = 0.05
+        # queues up to joint_max pods are re-planned jointly on every arrival; a longer queue at
+        # most every replan_interval_s, arrivals in between going best fit into the room the
+        # plan leaves (a full plan of a long queue is best fit anyway: packing.EXACT_MAX_ITEMS)
+        self.joint_max = 128
+        self.replan_interval_s = 1.0
         self.plan_enabled = True
         self._lock = threading.Lock()
         self.elector = None                   # extender/leader.py LeaderElector with --leader-elect
@@ -124,18 +133,27 @@ class Extender:
         with self._lock:
             if O.uid(pod) not in self._pending:
                 self._pending[O.uid(pod)] = pod
-                self._plan.clear()            # the queue changed: plan it again as a whole
+                self._unplanned[O.uid(pod)] = None
 
     def _drop_pending_locked(self, uid: str) -> None:
-        if self._pending.pop(uid, None) is not None:
-            self._plan.pop(uid, None)
+        pod = self._pending.pop(uid, None)
+        if pod is not None:
+            self._unplanned.pop(uid, None)
+            where = self._plan.pop(uid, None)
+            if where is not None:
+                left = self._plan_res.get(where, 0) - O.gpu_mem_of_pod(pod)
+                if left > 0:
+                    self._plan_res[where] = left
+                else:
+                    self._plan_res.pop(where, None)
 
     def _replan_locked(self) -> None:
-        """Joint best placement of every queued pod onto the GPUs' free HBM (extender/packing.py)."""
-        if (not self.plan_enabled or self.policy != "binpack" or not self._pending
-                or all(u in self._plan for u in self._pending)):
+        """Joint best placement of the queued pods onto the GPUs' free HBM (extender/packing.py).
+        Runs only when pods joined the queue since the last plan; a pod the plan left out does
+        not trigger another one."""
+        if not self.plan_enabled or self.policy != "binpack" or not self._unplanned:
             return
-        from .packing import pack
+        from .packing import _Buckets, pack
 
         bins, free = [], []
         for name, st in sorted(self.nodes.items()):
@@ -143,23 +161,50 @@ class Extender:
                 if f > 0:
                     bins.append((name, i))
                     free.append(f)
-        uids = list(self._pending)
-        sizes = [O.gpu_mem_of_pod(self._pending[u]) for u in uids]
-        assign = pack(free, sizes, self.plan_budget)
-        self._plan = {u: bins[a] for u, a in zip(uids, assign) if a is not None}
+        now = time.monotonic()
+        if len(self._pending) <= self.joint_max or now - self._plan_at >= self.replan_interval_s:
+            uids = list(self._pending)
+            sizes = [O.gpu_mem_of_pod(self._pending[u]) for u in uids]
+            assign = pack(free, sizes, self.plan_budget, self.plan_deadline_s)
+            self._plan, self._plan_res = {}, {}
+            for u, a, sz in zip(uids, assign, sizes):
+                if a is not None:
+                    self._plan[u] = bins[a]
+                    self._plan_res[bins[a]] = self._plan_res.get(bins[a], 0) + sz
+            self._plan_at = now
+        else:
+            # the newcomers, best fit into what the current plan leaves free
+            bk = _Buckets([f - self._plan_res.get(b, 0) for b, f in zip(bins, free)])
+            for u in self._unplanned:
+                sz = O.gpu_mem_of_pod(self._pending[u])
+                f = bk.best(sz)
+                if f is None or sz <= 0:
+                    continue
+                a = bk.take(f)
+                bk.put(f - sz, a)
+                self._plan[u] = bins[a]
+                self._plan_res[bins[a]] = self._plan_res.get(bins[a], 0) + sz
+        self._unplanned.clear()
 
     def _planned_locked(self, pod: dict, node_names=None) -> tuple[str, int] | None:
         u = O.uid(pod)
         if u not in self._pending:
             return None
         self._replan_locked()
-        choice = self._plan.get(u)
-        if choice is None or (node_names is not None and choice[0] not in node_names):
-            return None
-        st = self.nodes.get(choice[0])
-        if st is None or st.free()[choice[1]] < O.gpu_mem_of_pod(pod):
-            return None
-        return choice
+        for attempt in (0, 1):
+            choice = self._plan.get(u)
+            if choice is None or (node_names is not None and choice[0] not in node_names):
+                return None
+            st = self.nodes.get(choice[0])
+            if st is not None and st.free()[choice[1]] >= O.gpu_mem_of_pod(pod):
+                return choice
+            if attempt == 0:
+                # the room the plan counted on went elsewhere (a pod placed outside the queue,
+                # a node re-synced): plan the whole queue again now
+                self._unplanned.update(dict.fromkeys(self._pending))
+                self._plan_at = 0.0
+                self._replan_locked()
+        return None
 
     def forget(self, pod: dict):
         with self._lock:
@@ -261,11 +306,7 @@ class Extender:
         self._replan_locked()
         if uid in self._plan:
             return {}
-        out: dict = {}
-        for u, where in self._plan.items():
-            if u != uid and u in self._pending:
-                out[where] = out.get(where, 0) + O.gpu_mem_of_pod(self._pending[u])
-        return out
+        return self._plan_res                 # maintained with the plan (read only here)
 
     def _choose(self, req: int, node_names=None, reserved: dict | None = None) -> tuple[str, int] | None:
         best = None

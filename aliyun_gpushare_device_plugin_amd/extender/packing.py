@@ -9,20 +9,66 @@ pods placed, then the HBM placed — a depth-first search over items in decreasi
 best-fit as the starting incumbent, bins with equal free space tried once per level, an exact
 fit taken without alternatives, and a bound on what the remaining items could still add (free
 space smaller than the smallest item is waste; items larger than every free space are out). The search stops after ``budget`` node
-expansions and keeps the best assignment found (never worse than best fit).
+expansions (or ``deadline_s``) and keeps the best assignment found (never worse than best fit).
+
+Scale: bins are kept as buckets of equal free space (a heap of bin indices per value, the
+values sorted), so best fit is O(log) per item and the search branches over *distinct* free
+values — a cluster's thousands of GPUs have a few hundred distinct free amounts at most. The
+exact search runs for queues and bin sets up to ``EXACT_MAX_ITEMS`` / ``EXACT_MAX_VALUES``;
+beyond that the better best fit (arrival order or decreasing size) is the plan.
 """
 from __future__ import annotations
 
+import bisect
+import time
+
+EXACT_MAX_ITEMS = 160        # the search recurses once per item
+EXACT_MAX_VALUES = 320       # distinct free amounts it branches over
+PLACE_ALL_MAX_BINS = 128     # bin completion recurses once per bin
+
+
+class _Buckets:
+    """Bins grouped by free space: value -> sorted bin indices, plus the sorted values."""
+
+    def __init__(self, free: list[int]):
+        self.by: dict[int, list[int]] = {}
+        for b, f in enumerate(free):
+            self.by.setdefault(f, []).append(b)      # appended in index order: already sorted
+        self.keys = sorted(self.by)
+
+    def take(self, f: int, b: int | None = None) -> int:
+        """Remove bin ``b`` (default: the lowest-index one) from the bins with free space ``f``."""
+        lst = self.by[f]
+        b = lst.pop(0) if b is None else lst.pop(bisect.bisect_left(lst, b))
+        if not lst:
+            del self.by[f]
+            self.keys.pop(bisect.bisect_left(self.keys, f))
+        return b
+
+    def put(self, f: int, b: int) -> None:
+        lst = self.by.get(f)
+        if lst is None:
+            self.by[f] = [b]
+            bisect.insort(self.keys, f)
+        else:
+            bisect.insort(lst, b)
+
+    def best(self, s: int) -> int | None:
+        """The smallest free value that holds ``s`` (best fit), or None."""
+        i = bisect.bisect_left(self.keys, s)
+        return self.keys[i] if i < len(self.keys) else None
+
 
 def best_fit(free: list[int], sizes: list[int], order: list[int]) -> list[int | None]:
-    left = list(free)
+    """Each item in ``order`` to the bin it fills most tightly (lowest index on ties)."""
+    bk = _Buckets(free)
     out: list[int | None] = [None] * len(sizes)
     for k in order:
-        fits = [b for b, f in enumerate(left) if f >= sizes[k]]
-        if fits:
-            b = min(fits, key=lambda b: (left[b] - sizes[k], b))
+        f = bk.best(sizes[k])
+        if f is not None:
+            b = bk.take(f)
             out[k] = b
-            left[b] -= sizes[k]
+            bk.put(f - sizes[k], b)
     return out
 
 
@@ -109,7 +155,8 @@ def place_all(free: list[int], sizes: list[int], budget: int = 200_000) -> list[
     return [a for a in assign] if ok else None   # type: ignore[misc]
 
 
-def pack(free: list[int], sizes: list[int], budget: int = 200_000) -> list[int | None]:
+def pack(free: list[int], sizes: list[int], budget: int = 200_000,
+         deadline_s: float | None = None) -> list[int | None]:
     """Bin index per item (None = not placed) maximising (items placed, size placed)."""
     n = len(sizes)
     if n == 0:
@@ -122,21 +169,22 @@ def pack(free: list[int], sizes: list[int], budget: int = 200_000) -> list[int |
     best = max((best_fit(free, sizes, list(range(n))), best_fit(free, sizes, order)),
                key=lambda a: _score(a, sizes))
     best_score = _score(best, sizes)
-    if best_score[0] == n:
+    if best_score[0] == n or n > EXACT_MAX_ITEMS or len(set(free)) > EXACT_MAX_VALUES:
         return best
-    if sum(sizes) <= sum(free):
+    if sum(sizes) <= sum(free) and len(free) <= PLACE_ALL_MAX_BINS:
         full = place_all(free, sizes, budget // 2)
         if full is not None:
             return full
-    suffix_cnt = [0] * (n + 1)
+    desc = [sizes[k] for k in order]                 # sizes in search order (non-increasing)
+    neg = [-x for x in desc]                         # ascending, for bisect
     suffix_sz = [0] * (n + 1)
     for i in range(n - 1, -1, -1):
-        suffix_cnt[i] = suffix_cnt[i + 1] + 1
-        suffix_sz[i] = suffix_sz[i + 1] + sizes[order[i]]
-    left = list(free)
-    smallest = min(sizes)
+        suffix_sz[i] = suffix_sz[i + 1] + desc[i]
+    bk = _Buckets(free)
+    smallest = desc[-1]
     cur: list[int | None] = [None] * n
     expansions = 0
+    stop_at = None if deadline_s is None else time.monotonic() + deadline_s
 
     def dfs(i: int, cnt: int, sz: int, skipped: int) -> bool:
         """``skipped``: size of the last item left out — equal items are interchangeable, so
@@ -149,32 +197,36 @@ def pack(free: list[int], sizes: list[int], budget: int = 200_000) -> list[int |
                 return True
         if i == n or expansions > budget:
             return False
+        if stop_at is not None and not expansions & 255 and time.monotonic() > stop_at:
+            expansions = budget + 1
+            return False
         # bound: space in a bin smaller than the smallest remaining item is wasted, and items
         # larger than the largest free space cannot be placed any more
-        usable = sum(f for f in left if f >= smallest)
-        big = max(left)
-        fit_cnt = suffix_cnt[i] - sum(1 for j in range(i, n) if sizes[order[j]] > big)
+        keys = bk.keys
+        if not keys:
+            return False
+        lo = bisect.bisect_left(keys, smallest)
+        usable = sum(f * len(bk.by[f]) for f in keys[lo:])
+        big = keys[-1]
+        first_fit = max(i, bisect.bisect_left(neg, -big))   # items i.. before this are > big
+        fit_cnt = n - first_fit
         if (cnt + fit_cnt, sz + min(suffix_sz[i], usable)) <= best_score:
             return False
+        s = desc[i]
         k = order[i]
-        s = sizes[k]
         if s != skipped:
-            tried = set()
-            cand = sorted(range(len(left)), key=lambda b: (left[b] - s, b))
-            # an item that exactly fills a bin goes there: any solution placing it elsewhere can
-            # swap it with that bin's remaining contents (same count, same size placed)
-            if left[cand[0]] == s:
-                cand = cand[:1]
-            for b in cand:
-                f = left[b]
-                if f < s or f in tried:
-                    continue
-                tried.add(f)
-                left[b] -= s
+            j = bisect.bisect_left(keys, s)
+            # best fit first; an item that exactly fills a bin goes there: any solution placing
+            # it elsewhere can swap it with that bin's remaining contents
+            cands = list(keys[j:j + 1]) if j < len(keys) and keys[j] == s else list(keys[j:])
+            for f in cands:
+                b = bk.take(f)
+                bk.put(f - s, b)
                 cur[k] = b
                 if dfs(i + 1, cnt + 1, sz + s, 0):
                     return True
-                left[b] += s
+                bk.take(f - s, b)
+                bk.put(f, b)
                 cur[k] = None
         return dfs(i + 1, cnt, sz, s)        # leave this one out
 

@@ -487,3 +487,61 @@ def test_prepare_discards_answers_built_before_a_reconfigure():
         assert al._fast is None and not al._prep_cache
     finally:
         al.close()
+
+
+class LaggingWatch(StaticSource):
+    """A watch-backed source whose pod watch delivers a bound pod after the kubelet asked."""
+
+    def __init__(self, pods):
+        super().__init__(pods)
+        self.pending_version = 1
+        self.cv = threading.Condition()
+        self.watched = {p["metadata"]["uid"] for p in pods}
+
+    def pending_pods(self, fresh=False):
+        got = super().pending_pods(fresh)
+        return got if fresh else [p for p in got if p["metadata"]["uid"] in self.watched]
+
+    def deliver(self, pod):
+        with self.cv:
+            self.pods.append(pod)
+            self.watched.add(pod["metadata"]["uid"])
+            self.pending_version += 1
+            self.cv.notify_all()
+
+    def wait_pending_change(self, version, timeout):
+        with self.cv:
+            return self.cv.wait_for(lambda: self.pending_version != version, timeout)
+
+
+def _lag_engine(src, grace):
+    model = DeviceModel([gpu(i, 8 << 30) for i in range(2)], const.GIB)
+    return Allocator(model, src, FakeClient(src), NODE,
+                     AllocatorOptions(async_patch=True, fast_path=False, watch_grace_s=grace))
+
+
+def test_allocate_waits_for_a_lagging_watch_instead_of_listing():
+    """The kubelet's watch delivered the bind before the plugin's: the Allocate waits (up to
+    watch_grace_s) for the pod watch and answers from the cache, with no LIST on its path."""
+    src = LaggingWatch([])
+    al = _lag_engine(src, 0.2)
+    try:
+        threading.Timer(0.005, src.deliver, args=(mkpod("late", 3, 1, 10),)).start()
+        t = time.perf_counter()
+        r = al.allocate(req(3))
+        assert r.container_responses[0].envs[const.ENV_RESOURCE_INDEX] == "1"
+        assert src.fresh_calls == 0 and time.perf_counter() - t < 0.15
+    finally:
+        al.close()
+
+
+def test_allocate_lists_once_the_watch_grace_runs_out():
+    src = LaggingWatch([])
+    al = _lag_engine(src, 0.02)
+    try:
+        src.pods.append(mkpod("unseen", 3, 0, 10))          # in the apiserver, never in the watch
+        r = al.allocate(req(3))
+        assert r.container_responses[0].envs[const.ENV_RESOURCE_INDEX] == "0"
+        assert src.fresh_calls == 1
+    finally:
+        al.close()

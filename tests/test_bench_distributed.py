@@ -54,7 +54,9 @@ def test_bench_torchrun_two_ranks_gloo():
     assert uc["default"]["admissions"] == uc["reference"]["admissions"] == 8
     # measured by the plugins themselves: LIST + PATCH for the reference model, none by default
     assert uc["reference"]["apiserver_round_trips_on_path"]["p50"] == 2
-    assert uc["default"]["apiserver_round_trips_on_path"]["p99"] == 0
+    # (a LIST only when the plugin's pod watch lagged the kubelet's past watch_grace_s: rare)
+    assert uc["default"]["apiserver_round_trips_on_path"]["p50"] == 0
+    assert uc["default"]["apiserver_round_trips_on_path"]["p99"] <= 1
     assert set(uc["default"]["allocate_breakdown_p50_ms"]) == {"kubelet_to_handler", "handler", "handler_to_kubelet"}
     assert set(d["allocate_p50_ms_by_gpu"]) == {"0", "1"}
     assert topo["tp_pair_allreduce"]["busbw_GBps"] > 0 and topo["backend"] == "gloo"
