@@ -82,6 +82,7 @@ class Extender:
         self.plan_enabled = True
         self._lock = threading.Lock()
         self.elector = None                   # extender/leader.py LeaderElector with --leader-elect
+        self._touched: dict[str, float] = {}  # pod uid -> when the ledger entry last changed here
 
     def serving(self) -> bool:
         """Whether this replica answers filter / bind: always without leader election, else
@@ -89,12 +90,24 @@ class Extender:
         return self.elector is None or self.elector.is_leader()
 
     # -- cache ----------------------------------------------------------------------------
+    def _touch(self, uid: str) -> None:
+        """A ledger change made here (caller holds the lock): a re-sync whose LIST started
+        earlier keeps it instead of the LIST's older view of that pod."""
+        self._touched[uid] = time.monotonic()
+
     def sync(self):
-        """Rebuild the ledger from the apiserver (extender cache warm-up)."""
+        """Rebuild the ledger from the apiserver (extender cache warm-up, periodic resync). The
+        LISTs run outside the lock, so filter / bind keep going meanwhile; what changed here
+        after they started (binds, informer updates, deletions) wins over what they returned."""
+        t_fetch = time.monotonic()
+        node_list = self.client.list_nodes()
+        pods, _ = self.client.list_pods()
         with self._lock:
+            recent = {u for u, t in self._touched.items() if t >= t_fetch}
+            old_placed = self._placed
             self.nodes.clear()
-            self._placed.clear()
-            for n in self.client.list_nodes():
+            self._placed = {}
+            for n in node_list:
                 cnt = O.node_allocatable(n, const.RESOURCE_COUNT)
                 mem = O.node_allocatable(n, const.RESOURCE_NAME)
                 cap = O.node_capacity(n, const.RESOURCE_NAME) or mem
@@ -104,9 +117,8 @@ class Extender:
                 healthy = [bool((health.get(str(i)) or {}).get("healthy", True)) for i in range(cnt)]
                 self.nodes[O.name(n)] = NodeState(O.name(n), cnt, cap // cnt, [0] * cnt,
                                                   nodestatus.read_topology(n), healthy)
-            pods, _ = self.client.list_pods()
             for p in pods:
-                if O.is_terminated(p) or not O.node_name(p):
+                if O.is_terminated(p) or not O.node_name(p) or O.uid(p) in recent:
                     continue
                 st = self.nodes.get(O.node_name(p))
                 if st is None or O.gpu_mem_of_pod(p) <= 0:
@@ -118,6 +130,16 @@ class Extender:
                         st.used[g] += mem
                         parts.append((g, mem))
                 self._placed[O.uid(p)] = (st.name, parts)
+            for u in recent:                     # newer than the LIST: as this replica has it
+                node, parts = old_placed.get(u, (None, ()))
+                st = self.nodes.get(node)
+                if st is None:
+                    continue
+                for g, mem in parts:
+                    if 0 <= g < st.gpu_count:
+                        st.used[g] += mem
+                self._placed[u] = (node, list(parts))
+            self._touched = {u: t for u, t in self._touched.items() if t >= t_fetch}
             for r in self._groups.values():      # reserved slots of TP groups still binding
                 st = self.nodes.get(r["node"])
                 for g in (r["free"] if st else []):
@@ -212,6 +234,7 @@ class Extender:
             self._forget_locked(O.uid(pod))
 
     def _forget_locked(self, uid: str):
+        self._touch(uid)
         placed = self._placed.pop(uid, None)
         if placed:
             st = self.nodes.get(placed[0])
@@ -247,6 +270,7 @@ class Extender:
             for g, mem in parts:
                 st.used[g] += mem
             self._placed[u] = (st.name, parts)
+            self._touch(u)
 
     def watch(self) -> "Extender":
         """Follow pod updates and deletions from the apiserver (background thread)."""
@@ -348,6 +372,7 @@ class Extender:
             st = self.nodes[choice[0]]
             st.used[choice[1]] += req
             self._placed[O.uid(pod)] = (choice[0], [(choice[1], req)])
+            self._touch(O.uid(pod))
         return choice
 
     def commit(self, pod: dict, choice: tuple[str, int], assume_ns: int | None = None) -> dict:
@@ -391,6 +416,7 @@ class Extender:
             for p, g in zip(pods, grp):
                 st.used[g] += O.gpu_mem_of_pod(p)
                 self._placed[O.uid(p)] = (name, [(g, O.gpu_mem_of_pod(p))])
+                self._touch(O.uid(p))
         out = []
         t = time.time_ns()
         for k, (p, g) in enumerate(zip(pods, grp)):
@@ -450,6 +476,7 @@ class Extender:
                 r = self._groups[gk[0]] = {"node": node, "free": list(grp), "req": req, "t": time.monotonic()}
             g = r["free"].pop(0)
             self._placed[O.uid(pod)] = (node, [(g, req)])
+            self._touch(O.uid(pod))
             if not r["free"]:
                 del self._groups[gk[0]]       # every member placed
         self.bind(pod, node, g)
@@ -533,6 +560,7 @@ def serve_http(ext: Extender, host: str = "127.0.0.1", port: int = 0):
                         g = planned[1] if planned else min(fits, key=lambda i: (st.free()[i] - req, i))
                         st.used[g] += req
                         ext._placed[O.uid(pod)] = (st.name, [(g, req)])
+                        ext._touch(O.uid(pod))
                     ext.bind(pod, args["Node"], g)
                     return self._reply({"Error": ""})
                 except Exception as e:  # noqa: BLE001

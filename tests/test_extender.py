@@ -129,3 +129,36 @@ def test_extender_scales_to_a_large_oversubscribed_queue():
     used = [u for st in e.nodes.values() for u in st.used]
     assert max(used) <= 288 and placed > 0.6 * len(pods)
     assert total < 20.0 and worst < 1.0, (total, worst, len(pods))
+
+
+def test_resync_runs_outside_the_lock_and_keeps_binds_made_meanwhile():
+    """kube-scheduler is not stalled by the periodic re-sync's LISTs (seconds on a large cluster),
+    and a bind made while they were in flight survives the rebuild from their older view."""
+    import threading
+
+    with SimCluster([("n", "fake:2x8G")]) as c:
+        ext = c.extender
+        real = ext.client.list_pods
+
+        class SlowList:
+            def __getattr__(self, k):
+                return getattr(c.client, k)
+
+            def list_pods(self, *a, **k):
+                got = real(*a, **k)                 # the LIST's view is taken now...
+                time.sleep(0.3)                     # ...and arrives later
+                return got
+
+        ext.client = SlowList()
+        t = threading.Thread(target=ext.sync)
+        t.start()
+        time.sleep(0.05)
+        p = c.create_pod(6, name="meanwhile")
+        t0 = time.perf_counter()
+        where = c.schedule(p)                       # not blocked by the sync in flight
+        assert where is not None and time.perf_counter() - t0 < 0.2
+        t.join()
+        used = ext.usage()["n"]["used"]
+        assert sum(used) == 6 and used[where[1]] == 6   # the bind survived the rebuild
+        q = c.create_pod(6, name="next")
+        assert c.schedule(q)[1] == 1 - where[1]         # and still counts: no double booking
