@@ -101,6 +101,7 @@ class SharedGPUManager:
         self.smi = smi
         self.events: "queue.Queue" = queue.Queue()
         self.metrics = M.PluginMetrics()
+        self.metrics.registry.add_collector(lambda: M.native_server_exposition(self._debug_view().get("native_server")))
         self.plugin: DevicePluginServer | None = None
         self.health: HealthMonitor | None = None
         self.pod_source = None

@@ -141,6 +141,7 @@ class Registry:
     def __init__(self):
         self._m: dict[str, object] = {}
         self._lock = threading.Lock()
+        self._collectors: list = []     # fn() -> exposition text, read at scrape time
 
     def _get(self, cls, name, help_, **kw):
         with self._lock:
@@ -161,11 +162,45 @@ class Registry:
     def histogram(self, name, help_="", **kw):
         return self._get(Histogram, name, help_, **kw)
 
+    def add_collector(self, fn) -> None:
+        self._collectors.append(fn)
+
     def render(self) -> str:
         out = []
         for m in list(self._m.values()):
             out.extend(m.render())
+        for fn in list(self._collectors):
+            try:
+                out.append(fn())
+            except Exception:  # noqa: BLE001 - a collector never fails the scrape
+                pass
         return "".join(out)
+
+
+def native_server_exposition(st: dict) -> str:
+    """The native DevicePlugin server's counters (``gs_dp_stats``) as Prometheus text."""
+    if not st:
+        return ""
+    lines = [
+        "# HELP gpushare_native_allocate_total Allocates the native server answered from the prepared table "
+        "(native) or handed to the engine (forwarded)\n# TYPE gpushare_native_allocate_total counter\n",
+        f'gpushare_native_allocate_total{{path="native"}} {st.get("fast", 0)}\n',
+        f'gpushare_native_allocate_total{{path="forwarded"}} {st.get("forwarded_allocate", 0)}\n',
+        "# HELP gpushare_native_declined_total Why an Allocate was left to the engine\n"
+        "# TYPE gpushare_native_declined_total counter\n"]
+    lines += [f'gpushare_native_declined_total{{reason="{k}"}} {v}\n'
+              for k, v in sorted((st.get("declined") or {}).items())]
+    for name, key, kind, help_ in (
+            ("gpushare_native_forwarded_requests_total", "forwarded", "counter", "Requests handed to Python handlers"),
+            ("gpushare_native_table_waits_total", "waited", "counter",
+             "Allocates that waited for the table to catch up with the pod cache"),
+            ("gpushare_native_connections_total", "connections", "counter", "Kubelet connections accepted"),
+            ("gpushare_native_listandwatch_sends_total", "law_sends", "counter", "ListAndWatch messages sent"),
+            ("gpushare_native_journal_used_bytes", "journal_used", "gauge", "Bytes in the native answers' journal"),
+            ("gpushare_native_claims_pending", "taken_pending", "gauge",
+             "Native answers not yet taken in by the engine's bookkeeping")):
+        lines.append(f"# HELP {name} {help_}\n# TYPE {name} {kind}\n{name} {st.get(key, 0)}\n")
+    return "".join(lines)
 
 
 class PluginMetrics:

@@ -284,9 +284,14 @@ def test_manager_serves_natively_by_default():
     from aliyun_gpushare_device_plugin_amd.sim.cluster import SimCluster
 
     with SimCluster([("n", "fake:1x8G")]) as c:
-        assert type(c.manager("n").plugin).__name__ == "NativeDevicePluginServer"
+        m = c.manager("n")
+        assert type(m.plugin).__name__ == "NativeDevicePluginServer"
         pod, where, adm = c.run_pod(2)
         assert adm.error is None
+        text = m.metrics.registry.render()                 # the native counters are scraped too
+        n = sum(float(ln.split()[-1]) for ln in text.splitlines()
+                if ln.startswith("gpushare_native_allocate_total{"))
+        assert n >= 1 and "gpushare_native_connections_total" in text
     with SimCluster([("n", "fake:1x8G")], grpc_server="python") as c:
         assert type(c.manager("n").plugin).__name__ == "DevicePluginServer"
 
