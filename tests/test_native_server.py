@@ -611,3 +611,26 @@ def test_claim_reader_survives_a_bookkeeping_error(tmp_path):
         ch.close()
         srv.stop()
         al.close()
+
+
+def test_listandwatch_of_a_full_node_crosses_flow_control(tmp_path):
+    """8 x 288 GiB = 2304 fake devices (~130 KB per message, twice the HTTP/2 initial window):
+    the native server streams it under flow control, and again after a health change."""
+    model = DeviceModel([gpu(i, 288 << 30) for i in range(8)], const.GIB)
+    src = VSource([])
+    al = Allocator(model, src, FakeClient(src), "node-a", AllocatorOptions(async_patch=True, fast_path=False))
+    srv = NativeDevicePluginServer(model, al, str(tmp_path / "dp.sock"))
+    srv.start()
+    ch, stub = _stub(srv)
+    try:
+        law = stub.ListAndWatch(api.Empty())
+        first = next(law)
+        assert len(first.devices) == 2304 and len(first.SerializeToString()) > 65535
+        model.set_health(3, False, "test")
+        second = next(law)
+        assert sum(d.health == const.UNHEALTHY for d in second.devices) == 288
+        law.cancel()
+    finally:
+        ch.close()
+        srv.stop()
+        al.close()
