@@ -52,6 +52,7 @@ MI355X build, same protocol, different mechanics:
 """
 from __future__ import annotations
 
+import bisect
 import collections
 import contextlib
 import dataclasses
@@ -153,6 +154,8 @@ class _Prepared:
     body: bytes = b""      # serialized AllocateResponse (one container)
     head: bytes = b""      # journal record prefix (AllocJournal.fast_head)
     lkey: str = ""
+    # this entry in the native table's wire format, encoded once (_native_blob)
+    frag: bytes = dataclasses.field(default=b"", compare=False, repr=False)
 
 
 @dataclasses.dataclass(frozen=True)
@@ -210,6 +213,10 @@ class Allocator:
         self._native_prep: dict[str, _Prepared] = {}
         self._native_hold = False                 # a block kept while a multi-container claim is open
         self._published = (-1, -1)                # (pending version, gen) of the last native table
+        # the last native table: (version, gen, entries, their assume times) — a pod the watch
+        # adds is published into it at once from the cache hook (_publish_added)
+        self._last_table: tuple | None = None
+        self._table_mu = threading.Lock()
         self.native_rotate_bytes = 16 << 20       # rotate the native journal file past this
         self.native_prep_keep = 4096              # prepared answers kept for native claims past the current table
         for k, uid, t, resp in self.journal.answers():   # grants of a previous instance (journal TTL)
@@ -793,19 +800,21 @@ class Allocator:
                 log.V(2).info("prepare answers: %s", e)
 
     def _prepare(self, src) -> None:
+        tp = time.perf_counter()
         version = getattr(src, "pending_version", src.version)
         with self._mu:
             gen = self._gen
             cands = self._candidates(fresh=False)
             cands = [p for p in cands if O.uid(p) not in self._claims]
-        out, keep = [], {}
+        out, ats, keep = [], [], {}
         for p in cands:
-            shape = self._info(p)[3]
+            _, _, at, shape = self._info(p)
             if not shape:
                 continue
             u, g = O.uid(p), A.gpu_id_from_annotation(p)
             if len(shape) > 1:
                 out.append(_Prepared(u, O.namespace(p), O.name(p), shape[0], True, g))
+                ats.append(at)
                 continue
             k = (u, g, shape[0])
             c = self._prep_cache.get(k)
@@ -815,6 +824,7 @@ class Allocator:
                 c = self._prepared(p, u, g, shape[0])
             keep[k] = c
             out.append(c)
+            ats.append(at)
         nat = self.native
         with self._mu:
             if gen != self._gen:          # reconfigured meanwhile: answers built from the old model
@@ -836,9 +846,15 @@ class Allocator:
                 for u in list(prep)[:len(prep) - len(out) - self.native_prep_keep // 2]:
                     del prep[u]
             legacy = time.time() < self.journal._legacy_until
-            nat.publish(_native_blob(version, gen, 1 if self.podres is not None else 0,
-                                     [] if legacy else out, self.journal.replay_ids()))
-            self._published = (version, gen)
+            with self._table_mu:
+                last = self._last_table
+                # the cache hook may have published a newer table meanwhile: never go back
+                if last is None or (gen, version) >= (last[1], last[0]):
+                    nat.publish(_native_blob(version, gen, 1 if self.podres is not None else 0,
+                                             [] if legacy else out, self.journal.replay_ids()))
+                    self._last_table = (version, gen, () if legacy else tuple(out), () if legacy else tuple(ats))
+                    self._published = (version, gen)
+                    self.metrics.table_publish.observe(time.perf_counter() - tp, path="prepare")
         if self.journal.indexed_uids():         # replay index: only pods that can still be retried
             pend = {O.uid(p) for p in src.pending_pods()}
             self.journal.prune_index(pend)
@@ -1223,8 +1239,71 @@ class Allocator:
         src = self.pods
         if hasattr(src, "on_pending_change"):
             with src._lock:
-                src.on_pending_change = nat.set_version
+                src.on_pending_change = self._on_pending
                 nat.set_version(src.pending_version)
+
+    def _on_pending(self, version: int, pod: dict | None = None, gone: bool = False) -> None:
+        """Pod-cache hook (the watch thread, cache lock held), at every change of the Pending
+        set: the native server learns the version first, so it never answers from a table
+        older than the cache. The change itself (one pod joined, changed or left the set) is
+        then applied to the last table right here, so the kubelet's Allocate — usually arriving
+        right after the same watch event — finds a current table instead of waiting for the
+        prepare loop."""
+        nat = self.native
+        if nat is None:
+            return
+        nat.set_version(version)
+        if pod is not None:
+            t = time.perf_counter()
+            try:
+                if self._publish_change(nat, version, pod, gone):
+                    self.metrics.table_publish.observe(time.perf_counter() - t, path="hook")
+            except Exception as e:  # noqa: BLE001 - the prepare loop republishes anyway
+                log.V(2).info("incremental native table: %s", e)
+
+    def _publish_change(self, nat, version: int, pod: dict, gone: bool) -> bool:
+        """The table at ``version`` = the table at ``version - 1`` with ``pod`` removed and, if
+        it is a candidate now, placed in candidate order (assume time, then arrival) — what
+        ``_prepare`` would build: anything else that changes candidates (a taint, a placement
+        overlay, a reconfigure) bumps the engine generation, and claims made since are marked
+        taken in the server."""
+        if not self.opts.fast_path or self.opts.compute_isolation == "cu" or time.time() < self.journal._legacy_until:
+            return False
+        with self._table_mu:
+            last = self._last_table
+            gen = self._gen
+            if last is None or last[0] != version - 1 or last[1] != gen:
+                self.metrics.table_publish_skipped.inc(why="gen" if last is not None and last[1] != gen else "version")
+                return False
+            _, _, out, ats = last
+            u = O.uid(pod)
+            idx = next((i for i, c in enumerate(out) if c.uid == u), None)
+            c = at = None
+            if not gone:
+                p = self._view([pod])[0]
+                assumed, _, at, shape = self._info(p)
+                if (assumed and shape and not O.deleting(p) and u not in self._assigned and u not in self._claims
+                        and u not in self._tainted):
+                    g = A.gpu_id_from_annotation(p)
+                    if len(shape) > 1:
+                        c = _Prepared(u, O.namespace(p), O.name(p), shape[0], True, g)
+                    elif self.model.gpu(g) is not None:
+                        k = (u, g, shape[0])
+                        c = self._prep_cache.get(k) or self._prepared(p, u, g, shape[0])
+                        self._prep_cache[k] = c
+            keep_at = idx is not None and c is not None and ats[idx] == at
+            if idx is not None:
+                out, ats = out[:idx] + out[idx + 1:], ats[:idx] + ats[idx + 1:]
+            if c is not None:
+                i = idx if keep_at else bisect.bisect_right(ats, at)   # same place, or after its equals
+                out, ats = out[:i] + (c,) + out[i:], ats[:i] + (at,) + ats[i:]
+                self._native_prep.pop(u, None)
+                self._native_prep[u] = c
+            nat.publish(_native_blob(version, gen, 1 if self.podres is not None else 0, list(out),
+                                     self.journal.replay_ids()))
+            self._last_table = (version, gen, out, ats)
+            self._published = (version, gen)
+        return True
 
     def _native_loop(self, nat) -> None:
         """Takes in the native server's claims as they happen; rotates its journal file once
@@ -1508,7 +1587,12 @@ def _native_blob(version: int, gen: int, flags: int, cands, replay_ids) -> bytes
         return struct.pack("<I", len(b)) + b
     parts = [struct.pack("<QQIII", version, gen, flags, len(cands), len(replay_ids))]
     for c in cands:
-        parts += [struct.pack("<IB", c.size, 1 if c.multi else 0), s(c.uid), s(c.body), s(c.head)]
+        f = getattr(c, "frag", None)
+        if not f:
+            f = struct.pack("<IB", c.size, 1 if c.multi else 0) + s(c.uid) + s(c.body) + s(c.head)
+            if isinstance(c, _Prepared):
+                object.__setattr__(c, "frag", f)      # the entry is immutable: encode it once
+        parts.append(f)
     parts += [s(i) for i in replay_ids]
     return b"".join(parts)
 

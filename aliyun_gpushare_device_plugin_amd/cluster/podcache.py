@@ -167,9 +167,10 @@ class WatchCache(PodSource):
         # from the cache (the Allocate engine's prepared answers)
         self.version = 0
         # bumped only when the Pending subset changes (what Allocate candidates are made of);
-        # ``on_pending_change(version)`` runs under the cache lock at every bump, so a consumer
-        # that answers from precomputed state (the native Allocate fast path) never sees the
-        # cache ahead of the version it was told
+        # ``on_pending_change(version, pod, gone)`` runs under the cache lock at every bump (``pod``:
+        # the one pod that joined, changed in or left (``gone``) the set; None after a relist),
+        # so a consumer that answers from precomputed state (the native Allocate fast path)
+        # never sees the cache ahead of the version it was told
         self.pending_version = 0
         self.on_pending_change = None
         self._pending_cv = threading.Condition(self._lock)
@@ -220,7 +221,7 @@ class WatchCache(PodSource):
             if typ == "DELETED" or O.node_name(obj) != self.node:
                 self._pods.pop(u, None)
                 if self._pending.pop(u, None) is not None:
-                    self._pending_bump()
+                    self._pending_bump(obj, gone=True)
                 self.version += 1
             else:
                 cur = self._pods.get(u)
@@ -267,12 +268,12 @@ class WatchCache(PodSource):
         with self._lock:
             return list(self._pending.values())
 
-    def _pending_bump(self) -> None:
+    def _pending_bump(self, pod: dict | None = None, gone: bool = False) -> None:
         """Caller holds the cache lock."""
         self.pending_version += 1
         hook = self.on_pending_change
         if hook is not None:
-            hook(self.pending_version)
+            hook(self.pending_version, pod, gone)
         self._pending_cv.notify_all()
 
     def wait_pending_change(self, version: int, timeout: float) -> bool:
@@ -285,9 +286,9 @@ class WatchCache(PodSource):
         self._pods[u] = pod
         if O.phase(pod) == "Pending":
             self._pending[u] = pod
-            self._pending_bump()
+            self._pending_bump(pod)
         elif self._pending.pop(u, None) is not None:
-            self._pending_bump()
+            self._pending_bump(pod, gone=True)
 
     def observe(self, pod: dict) -> None:
         if not pod or O.node_name(pod) != self.node:

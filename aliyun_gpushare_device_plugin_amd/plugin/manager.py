@@ -255,7 +255,10 @@ class SharedGPUManager:
 
     def _debug_view(self) -> dict:
         stats = getattr(self.plugin, "stats", None)
-        return {"native_server": stats()} if stats else {}
+        if not stats:
+            return {}
+        skipped = {dict(k).get("why", ""): v for k, v in self.metrics.table_publish_skipped._v.items()}
+        return {"native_server": dict(stats(), table_hook_skipped=skipped)}
 
     def _pod_resources(self):
         from ..api.podresources import SOCKET, PodResourcesClient

@@ -79,6 +79,7 @@ def _SIGNATURES(P, I, I64, U64, B):
             ("gs_dp_fast_unblock", None, [P]),
             ("gs_dp_fast_take", None, [P, B]),
             ("gs_dp_set_fast_wait_us", None, [P, I]),
+            ("gs_dp_set_watch_wait_us", None, [P, I]),
             ("gs_dp_taken_next", I, [P, I, C, I]),
             ("gs_dp_taken_pending", I, [P]),
             ("gs_dp_fast_journal_open", I, [P, B, U64]),
@@ -160,11 +161,14 @@ class _Ctx:
 
 class NativeDevicePluginServer(DevicePluginServer):
     # fast_wait_us: how long an Allocate that finds the table one pod-cache change behind waits
-    # for the engine to republish it before going to the engine's full path (~0.3 ms itself)
-    def __init__(self, *a, handler_threads: int = 4, fast_wait_us: int = 300, **kw):
+    # for the engine to republish it before going to the engine's full path (~0.3 ms itself);
+    # watch_wait_us: how long one that no candidate matches waits for the plugin's pod watch
+    # to deliver the pod (the kubelet's watch can be ahead) before the engine's path
+    def __init__(self, *a, handler_threads: int = 4, fast_wait_us: int = 300, watch_wait_us: int = 2000, **kw):
         super().__init__(*a, **kw)
         self.handler_threads = handler_threads
         self.fast_wait_us = fast_wait_us
+        self.watch_wait_us = watch_wait_us
         self._h = None
         self._lib = None
         self._threads: list[threading.Thread] = []
@@ -183,6 +187,7 @@ class NativeDevicePluginServer(DevicePluginServer):
             raise RuntimeError(f"native device-plugin server: {err.value.decode()}")
         self._h = h
         lib.gs_dp_set_fast_wait_us(h, self.fast_wait_us)
+        lib.gs_dp_set_watch_wait_us(h, self.watch_wait_us)
         self._push_devices()
         self.fast = NativeFast(lib, h)
         self.allocator.attach_native(self.fast)

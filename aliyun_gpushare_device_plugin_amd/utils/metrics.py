@@ -211,6 +211,12 @@ class PluginMetrics:
         self.allocate_latency = r.histogram("gpushare_allocate_latency_seconds",
                                             "Allocate RPC latency by phase (prelude/lock/lookup/decide/patch/total)")
         self.allocate_outcomes = r.counter("gpushare_allocate_total", "Allocate outcomes")
+        self.table_publish = r.histogram("gpushare_native_table_publish_seconds",
+                                         "Time to build and publish the native Allocate table: from the pod-cache "
+                                         "hook (one pod changed) or the prepare loop (full rebuild)")
+        self.table_publish_skipped = r.counter("gpushare_native_table_hook_skipped_total",
+                                               "Pod-cache changes the hook left to the prepare loop (its last table "
+                                               "was not at the previous version / engine generation)")
         self.allocate_requests = r.histogram("gpushare_allocate_apiserver_requests",
                                              "apiserver requests made on the Allocate path (counted by the handler "
                                              "thread; write-behind patches excluded)", buckets=(0, 1, 2, 3, 4, 8))

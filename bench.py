@@ -133,6 +133,10 @@ def plugin_latency(port: int, reset: bool = False) -> dict | None:
         # apiserver round trips the handler itself made, per Allocate (measured, not assumed)
         rq = (d.get("gpushare_allocate_apiserver_requests") or [{}])[0]
         tot["requests"] = {"p50": rq.get("p50"), "p99": rq.get("p99"), "count": rq.get("count")}
+    pub = {e["labels"].get("path"): e for e in d.get("gpushare_native_table_publish_seconds", [])}
+    if tot is not None and pub:
+        # the native table: how long the watch-thread hook (one pod) and a full rebuild take
+        tot["table_publish"] = {k: {"p50_ms": round(v["p50"] * 1e3, 3), "count": v["count"]} for k, v in pub.items()}
     return tot
 
 
@@ -156,7 +160,11 @@ def native_share(before: dict | None, after: dict | None) -> dict | None:
     fast = a.get("fast", 0) - b.get("fast", 0)
     eng = a.get("forwarded_allocate", 0) - b.get("forwarded_allocate", 0)
     why = {k: v - (b.get("declined") or {}).get(k, 0) for k, v in (a.get("declined") or {}).items()}
-    return {"native": fast, "engine": eng, "declined": {k: v for k, v in why.items() if v}}
+    return {"native": fast, "engine": eng, "declined": {k: v for k, v in why.items() if v},
+            "waited_for_table": a.get("waited", 0) - b.get("waited", 0),
+            "waited_for_watch": a.get("watch_waits", 0) - b.get("watch_waits", 0),
+            "table_hook_skipped": {k: v - (b.get("table_hook_skipped") or {}).get(k, 0)
+                                   for k, v in (a.get("table_hook_skipped") or {}).items()}}
 
 
 def transport_floor() -> float | None:
@@ -963,6 +971,7 @@ def main():
             "plugin_allocate_p99_ms": ms(srv["p99"]) if srv else None,
             "allocate_breakdown_p50_ms": breakdown(cp.splits),
             "answered_by": native_share(getattr(cp, "native_before", None), native_stats(cp.metrics_port)),
+            "native_table_publish": (srv or {}).get("table_publish"),
             "admissions": len(cp.alloc_lat), "pod_source": a.pod_source, "patch": "write-behind",
             "apiserver_round_trips_on_path": round_trips(srv)}}
         if cp.ref_port:

@@ -253,7 +253,7 @@ struct Taken {
 
 struct Counters {
   std::atomic<uint64_t> fast{0}, forwarded{0}, forwarded_allocate{0}, stale{0}, blocked{0}, replay{0}, nomatch{0}, multi{0},
-      ambiguous{0}, shape{0}, journal{0}, waited{0}, law_sends{0}, conns{0}, unknown{0};
+      ambiguous{0}, shape{0}, journal{0}, waited{0}, law_sends{0}, conns{0}, unknown{0}, older{0}, watch_waits{0};
 };
 
 }  // namespace
@@ -285,6 +285,7 @@ struct gs_dp {
   uint64_t cur_version = 0, cur_gen = 0;
   int blocked = 0;
   int fast_wait_us = 300;
+  int watch_wait_us = 2000;   // an Allocate with no candidate yet waits this long for the pod watch
   // fake IDs of native answers -> when: a kubelet retry of them is for the engine (replay),
   // kept until a published replay set covers them (or for 30 s, by when the engine has)
   std::unordered_map<std::string, int64_t> answered_ids;
@@ -449,25 +450,38 @@ bool journal_append(gs_dp* s, const Entry& en, const std::string& req, double t)
   return true;
 }
 
-// Caller holds s->mu. Returns the entry to answer, or null (the reason counted).
-const Entry* pick(gs_dp* s, const std::vector<std::string>& ids) {
+enum Decline { kOk = 0, kReplay, kMulti, kAmbiguous, kNoMatch };
+
+// Caller holds s->mu. The entry to answer (kOk), or why the engine must decide.
+Decline pick(gs_dp* s, const std::vector<std::string>& ids, const Entry** out) {
   Table& t = s->table;
   size_t n = ids.size();
   for (const auto& id : ids)
-    if (t.replay.count(id) || s->answered_ids.count(id)) return s->n.replay++, nullptr;
+    if (t.replay.count(id) || s->answered_ids.count(id)) return kReplay;
   Entry* first = nullptr;
   for (auto& en : t.entries) {
     if (en.size != n || en.taken || s->taken_uids.count(en.uid)) continue;
     if (!first) {
       first = &en;
-      if (en.multi) return s->n.multi++, nullptr;   // a multi-container pod first in line
+      if (en.multi) return kMulti;                  // a multi-container pod first in line
       if (!(t.flags & 1)) break;
     } else {
-      return s->n.ambiguous++, nullptr;             // which one is for admission identity to say
+      return kAmbiguous;                            // which one is for admission identity to say
     }
   }
-  if (!first) return s->n.nomatch++, nullptr;
-  return first;
+  if (!first) return kNoMatch;
+  *out = first;
+  return kOk;
+}
+
+void count_decline(gs_dp* s, Decline d) {
+  switch (d) {
+    case kReplay: s->n.replay++; break;
+    case kMulti: s->n.multi++; break;
+    case kAmbiguous: s->n.ambiguous++; break;
+    case kNoMatch: s->n.nomatch++; break;
+    default: break;
+  }
 }
 
 bool table_current(gs_dp* s) {
@@ -499,8 +513,23 @@ bool fast_allocate(Conn* c, int32_t sid, const std::string& body, int64_t t_in) 
       return false;
     }
   }
-  const Entry* en = pick(s, crs[0]);
-  if (!en) return false;
+  const Entry* en = nullptr;
+  Decline d = pick(s, crs[0], &en);
+  if (d == kNoMatch && s->watch_wait_us > 0) {
+    // no candidate of this size yet: the kubelet's own pod watch can deliver the bind before
+    // the plugin's does; the engine's cache hook publishes the pod the moment it arrives, so
+    // wait for the next table (a LIST on the engine's path is the alternative)
+    s->n.watch_waits++;
+    uint64_t v = s->cur_version;
+    s->cv.wait_until(lk, deadline_us(s->watch_wait_us), [&] {
+      return (s->cur_version != v && table_current(s)) || s->blocked > 0 || s->stopping.load();
+    });
+    if (table_current(s)) d = pick(s, crs[0], &en);
+  }
+  if (d != kOk) {
+    count_decline(s, d);
+    return false;
+  }
   double t = wall_s();
   if (!journal_append(s, *en, body, t)) {  // journal before the reply
     s->n.journal++;
@@ -923,6 +952,13 @@ int gs_dp_fast_publish(gs_dp* s, const uint8_t* blob, int len) {
   t.valid = !(t.flags & 0x80000000u);       // flag 31: no table (fast path off)
   {
     std::lock_guard<std::mutex> lk(s->mu);
+    // two publishers (the engine's prepare loop and its pod-cache hook) may finish out of
+    // order: a table older than the one held is dropped, never installed over it
+    if (t.valid && s->table.valid &&
+        (t.gen < s->table.gen || (t.gen == s->table.gen && t.version < s->table.version))) {
+      s->n.older++;
+      return 0;
+    }
     // A claim stays a claim while the new table still lists the pod (the engine built it
     // before it processed the claim) or the engine has not taken the claim's record yet.
     std::unordered_set<std::string> keep;
@@ -982,6 +1018,11 @@ void gs_dp_fast_take(gs_dp* s, const char* uid) {
 void gs_dp_set_fast_wait_us(gs_dp* s, int us) {
   std::lock_guard<std::mutex> lk(s->mu);
   s->fast_wait_us = us < 0 ? 0 : us;
+}
+
+void gs_dp_set_watch_wait_us(gs_dp* s, int us) {
+  std::lock_guard<std::mutex> lk(s->mu);
+  s->watch_wait_us = us < 0 ? 0 : us;
 }
 
 int gs_dp_taken_next(gs_dp* s, int timeout_ms, uint8_t* buf, int cap) {
@@ -1060,7 +1101,7 @@ int gs_dp_stats(gs_dp* s, char* buf, int cap) {
   int n = snprintf(buf, (size_t)cap,
                    "{\"fast\":%llu,\"forwarded\":%llu,\"forwarded_allocate\":%llu,\"declined\":{\"stale\":%llu,\"blocked\":%llu,\"replay\":%llu,"
                    "\"nomatch\":%llu,\"multi\":%llu,\"ambiguous\":%llu,\"shape\":%llu,\"journal\":%llu},"
-                   "\"waited\":%llu,\"law_sends\":%llu,\"connections\":%llu,\"unknown\":%llu,"
+                   "\"waited\":%llu,\"law_sends\":%llu,\"connections\":%llu,\"unknown\":%llu,\"older_tables\":%llu,\"watch_waits\":%llu,"
                    "\"journal_used\":%llu,\"taken_pending\":%llu}",
                    (unsigned long long)s->n.fast, (unsigned long long)s->n.forwarded,
                    (unsigned long long)s->n.forwarded_allocate, (unsigned long long)s->n.stale,
@@ -1068,7 +1109,8 @@ int gs_dp_stats(gs_dp* s, char* buf, int cap) {
                    (unsigned long long)s->n.multi, (unsigned long long)s->n.ambiguous, (unsigned long long)s->n.shape,
                    (unsigned long long)s->n.journal, (unsigned long long)s->n.waited,
                    (unsigned long long)s->n.law_sends, (unsigned long long)s->n.conns,
-                   (unsigned long long)s->n.unknown, (unsigned long long)used, (unsigned long long)pend);
+                   (unsigned long long)s->n.unknown, (unsigned long long)s->n.older, (unsigned long long)s->n.watch_waits, (unsigned long long)used,
+                   (unsigned long long)pend);
   return n < cap ? n : -1;
 }
 

@@ -49,6 +49,9 @@ GS_DP_API void gs_dp_fast_unblock(gs_dp* s);
 GS_DP_API void gs_dp_fast_take(gs_dp* s, const char* uid);
 // How long an Allocate may wait for a table matching the current version/generation.
 GS_DP_API void gs_dp_set_fast_wait_us(gs_dp* s, int us);
+// How long an Allocate no candidate matches may wait for the pod watch (a newer table) before
+// it goes to the engine.
+GS_DP_API void gs_dp_set_watch_wait_us(gs_dp* s, int us);
 // Next native answer for the engine's bookkeeping: record = u32 uid_len, uid, u32 req_len,
 // AllocateRequest bytes, f64 wall time (the journal record's "t"), u64 handler ns. Returns the
 // record size, 0 on timeout, -1 once stopped, -2 if `cap` is too small (record kept).
