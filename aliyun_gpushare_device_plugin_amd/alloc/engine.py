@@ -794,6 +794,11 @@ class Allocator:
             ev.wait(0.5)
             ev.clear()
             try:
+                if self.native is not None and self._published == (getattr(src, "pending_version", None), self._gen):
+                    # the cache hook already applied the change to the native table: a full
+                    # rebuild now would only compete with the Allocate it made the table for
+                    self._prune_replay_index(src)
+                    continue
                 self._prepare(src)
             except Exception as e:  # noqa: BLE001 - the full path still answers
                 self._fast = None
@@ -842,9 +847,7 @@ class Allocator:
             for c in out:
                 prep.pop(c.uid, None)
                 prep[c.uid] = c           # (re)inserted last: the oldest entries are the stale ones
-            if len(prep) > self.native_prep_keep + len(out):
-                for u in list(prep)[:len(prep) - len(out) - self.native_prep_keep // 2]:
-                    del prep[u]
+            self._trim_native_prep(len(out))
             legacy = time.time() < self.journal._legacy_until
             with self._table_mu:
                 last = self._last_table
@@ -855,6 +858,17 @@ class Allocator:
                     self._last_table = (version, gen, () if legacy else tuple(out), () if legacy else tuple(ats))
                     self._published = (version, gen)
                     self.metrics.table_publish.observe(time.perf_counter() - tp, path="prepare")
+        self._prune_replay_index(src)
+
+    def _trim_native_prep(self, n_current: int) -> None:
+        """Bound the prepared answers kept for native claims (the current table's entries are
+        the last ``n_current`` inserted and always stay)."""
+        prep = self._native_prep
+        if len(prep) > self.native_prep_keep + n_current:
+            for u in list(prep)[:len(prep) - n_current - self.native_prep_keep // 2]:
+                del prep[u]
+
+    def _prune_replay_index(self, src) -> None:
         if self.journal.indexed_uids():         # replay index: only pods that can still be retried
             pend = {O.uid(p) for p in src.pending_pods()}
             self.journal.prune_index(pend)
@@ -1293,12 +1307,21 @@ class Allocator:
                         self._prep_cache[k] = c
             keep_at = idx is not None and c is not None and ats[idx] == at
             if idx is not None:
+                old = out[idx]
+                if c is None or (old.gpu, old.size) != (c.gpu, c.size):
+                    self._prep_cache.pop((old.uid, old.gpu, old.size), None)   # left the table
                 out, ats = out[:idx] + out[idx + 1:], ats[:idx] + ats[idx + 1:]
             if c is not None:
                 i = idx if keep_at else bisect.bisect_right(ats, at)   # same place, or after its equals
                 out, ats = out[:i] + (c,) + out[i:], ats[:i] + (at,) + ats[i:]
                 self._native_prep.pop(u, None)
                 self._native_prep[u] = c
+                # the current entries must be the newest: re-append them after the new one
+                for e in out:
+                    if e.uid != u:
+                        self._native_prep.pop(e.uid, None)
+                        self._native_prep[e.uid] = e
+                self._trim_native_prep(len(out))
             nat.publish(_native_blob(version, gen, 1 if self.podres is not None else 0, list(out),
                                      self.journal.replay_ids()))
             self._last_table = (version, gen, out, ats)

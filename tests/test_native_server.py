@@ -671,3 +671,40 @@ def test_a_pod_the_watch_adds_is_in_the_table_before_the_kubelet_asks(tmp_path):
         ch.close()
         srv.stop()
         al.close()
+
+
+def test_the_table_hook_keeps_its_caches_bounded(tmp_path):
+    """With every change applied by the cache hook (no full rebuild), the per-pod caches of
+    prepared answers still shrink as pods leave: a long churn does not grow them."""
+    from aliyun_gpushare_device_plugin_amd.cluster.podcache import WatchCache
+
+    class Nat:
+        def publish(self, blob):
+            pass
+
+        def set_version(self, v):
+            pass
+
+    cache = WatchCache(client=None, node="node-a")
+    cache._synced.set()
+    model = DeviceModel([gpu(i, 8 << 30) for i in range(2)], const.GIB)
+    al = Allocator(model, cache, FakeClient(cache), "node-a", AllocatorOptions(async_patch=True, fast_path=False))
+    al.opts.fast_path = True
+    al.native = Nat()
+    al.native_prep_keep = 8
+    cache.on_pending_change = al._on_pending
+    al._prepare(cache)
+    try:
+        for i in range(300):
+            p = mkpod(f"c{i}", 1 + i % 3, i % 2, 10 + i)
+            cache._apply({"type": "ADDED", "object": p})
+            running = json.loads(json.dumps(p))
+            running["status"]["phase"] = "Running"
+            running["metadata"]["resourceVersion"] = "2"
+            cache._apply({"type": "MODIFIED", "object": running})      # admitted: leaves Pending
+            assert al._published == (cache.pending_version, al._gen)   # every change by the hook
+        assert len(al._last_table[2]) == 0
+        assert len(al._prep_cache) <= 2 and len(al._native_prep) <= 8 + 1
+    finally:
+        al.native = None
+        al.close()
