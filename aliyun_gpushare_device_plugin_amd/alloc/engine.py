@@ -217,6 +217,8 @@ class Allocator:
         # adds is published into it at once from the cache hook (_publish_added)
         self._last_table: tuple | None = None
         self._table_mu = threading.Lock()
+        self._resp_tmpl: dict[tuple, api.ContainerAllocateResponse] = {}   # _container_response
+        self._tmpl_bytes: dict[tuple, bytes] = {}                          # _prepared
         self.native_rotate_bytes = 16 << 20       # rotate the native journal file past this
         self.native_prep_keep = 4096              # prepared answers kept for native claims past the current table
         for k, uid, t, resp in self.journal.answers():   # grants of a previous instance (journal TTL)
@@ -598,6 +600,41 @@ class Allocator:
     # ------------------------------------------------------------------------------------
     def _container_response(self, gpu_index: int, pod_units: int, ctr_units: int, pod_uid: str,
                             slot: int, cu: cuslots.SlotRun | None = None) -> api.ContainerAllocateResponse:
+        """One container's answer: what depends only on (GPU, sizes, configuration) comes from a
+        cached template (a copy in C), then the per-pod quota-ledger parts are added — this runs
+        on the watch thread for every newly bound pod (``_publish_change``)."""
+        if cu is not None:
+            r = self._container_base(gpu_index, pod_units, ctr_units, cu)
+        else:
+            key = (self._gen, gpu_index, pod_units, ctr_units)
+            base = self._resp_tmpl.get(key)
+            if base is None:
+                base = self._container_base(gpu_index, pod_units, ctr_units, None)
+                if len(self._resp_tmpl) > 512:
+                    self._resp_tmpl.clear()
+                self._resp_tmpl[key] = base
+            r = api.ContainerAllocateResponse()
+            r.CopyFrom(base)
+        shim = self.opts.shim
+        if shim is not None and shim.enabled and not self.opts.disable_cgpu:
+            r.envs[const.ENV_SHIM_LEDGER] = ledger_name(pod_uid or f"{gpu_index}-{time.time_ns()}", slot)
+            if self._ledgers is not None:
+                # this container's own ledger directory (quota/ledger.py): a tenant never sees
+                # another container's ledger
+                try:
+                    lkey = self._ledgers.take(pod_uid)
+                    host = self._ledgers.path(lkey)
+                except OSError as e:
+                    log.warning("ledger dir for pod %s: %s (pod-private shm ledger instead)", pod_uid, e)
+                else:
+                    r.mounts.add(container_path=const.LEDGER_CONTAINER_DIR, host_path=host, read_only=False)
+                    r.envs[const.ENV_SHIM_LEDGER_DIR] = const.LEDGER_CONTAINER_DIR
+                    r.annotations[const.CTR_ANNOTATION_LEDGER] = lkey
+        return r
+
+    def _container_base(self, gpu_index: int, pod_units: int, ctr_units: int,
+                        cu: cuslots.SlotRun | None) -> api.ContainerAllocateResponse:
+        """The container answer without its per-pod ledger parts."""
         g = self.model.gpu(gpu_index)
         envs = {
             const.ENV_RESOURCE_INDEX: str(gpu_index),
@@ -628,21 +665,8 @@ class Allocator:
         if shim is not None and shim.enabled and not self.opts.disable_cgpu:
             r.mounts.add(container_path=shim.container_dir, host_path=shim.host_dir, read_only=True)
             r.envs[const.ENV_LD_PRELOAD] = shim.container_lib
-            r.envs[const.ENV_SHIM_LEDGER] = ledger_name(pod_uid or f"{gpu_index}-{time.time_ns()}", slot)
             # exact bytes from the SMI-reported HBM size, so the shim needs no device query
             r.envs[const.ENV_SHIM_QUOTA_BYTES] = str(U.quota_bytes(ctr_units, g.units, g.vram_bytes))
-            if self._ledgers is not None:
-                # this container's own ledger directory (quota/ledger.py): a tenant never sees
-                # another container's ledger
-                try:
-                    lkey = self._ledgers.take(pod_uid)
-                    host = self._ledgers.path(lkey)
-                except OSError as e:
-                    log.warning("ledger dir for pod %s: %s (pod-private shm ledger instead)", pod_uid, e)
-                else:
-                    r.mounts.add(container_path=const.LEDGER_CONTAINER_DIR, host_path=host, read_only=False)
-                    r.envs[const.ENV_SHIM_LEDGER_DIR] = const.LEDGER_CONTAINER_DIR
-                    r.annotations[const.CTR_ANNOTATION_LEDGER] = lkey
         return r
 
     def _plan_slots(self, claim: _Claim, pod_units: int) -> cuslots.SlotRun | None:
@@ -895,14 +919,36 @@ class Allocator:
         return changed
 
     def _prepared(self, p: dict, u: str, g: int, units: int) -> "_Prepared":
-        """The answer to a single-container pod's Allocate, serialized ahead of the request."""
-        cr = self._container_response(g, units, units, u, 0, None)
-        r = api.AllocateResponse()
-        r.container_responses.append(cr)
-        body = r.SerializeToString()
+        """The answer to a single-container pod's Allocate, serialized ahead of the request:
+        the cached wire bytes of its (GPU, size) template followed by its per-pod ledger
+        fields, encoded directly (protobuf: appended records of repeated / map fields merge
+        into the message) — the same message ``_container_response`` builds, at a fraction of
+        the cost on the watch thread (``tests/test_allocate_engine.py`` pins the equality)."""
+        key = (self._gen, g, units)
+        base = self._tmpl_bytes.get(key)
+        if base is None:
+            base = self._container_base(g, units, units, None).SerializeToString()
+            if len(self._tmpl_bytes) > 512:
+                self._tmpl_bytes.clear()
+            self._tmpl_bytes[key] = base
+        extra, lkey = b"", ""
+        shim = self.opts.shim
+        if shim is not None and shim.enabled and not self.opts.disable_cgpu:
+            extra = _pb_map_entry(0x0a, const.ENV_SHIM_LEDGER, ledger_name(u or f"{g}-{time.time_ns()}", 0))
+            if self._ledgers is not None:
+                try:
+                    lkey = self._ledgers.take(u)
+                    host = self._ledgers.path(lkey)
+                except OSError as e:
+                    log.warning("ledger dir for pod %s: %s (pod-private shm ledger instead)", u, e)
+                    lkey = ""
+                else:
+                    extra += (_pb_ld(0x12, _pb_ld(0x0a, const.LEDGER_CONTAINER_DIR.encode()) + _pb_ld(0x12, host.encode()))
+                              + _pb_map_entry(0x0a, const.ENV_SHIM_LEDGER_DIR, const.LEDGER_CONTAINER_DIR)
+                              + _pb_map_entry(0x22, const.CTR_ANNOTATION_LEDGER, lkey))
+        body = _pb_ld(0x0a, base + extra)            # AllocateResponse.container_responses[0]
         return _Prepared(u, O.namespace(p), O.name(p), units, False, g, body,
-                         AllocJournal.fast_head(u, O.namespace(p), O.name(p), body),
-                         cr.annotations.get(const.CTR_ANNOTATION_LEDGER, ""))
+                         AllocJournal.fast_head(u, O.namespace(p), O.name(p), body), lkey)
 
     def _allocate_full(self, req, t0: float):
         """The full Allocate path, counting the apiserver round trips it makes (the handler
@@ -1270,25 +1316,26 @@ class Allocator:
         if pod is not None:
             t = time.perf_counter()
             try:
-                if self._publish_change(nat, version, pod, gone):
-                    self.metrics.table_publish.observe(time.perf_counter() - t, path="hook")
+                kind = self._publish_change(nat, version, pod, gone)
+                if kind:
+                    self.metrics.table_publish.observe(time.perf_counter() - t, path=f"hook_{kind}")
             except Exception as e:  # noqa: BLE001 - the prepare loop republishes anyway
                 log.V(2).info("incremental native table: %s", e)
 
-    def _publish_change(self, nat, version: int, pod: dict, gone: bool) -> bool:
+    def _publish_change(self, nat, version: int, pod: dict, gone: bool) -> str:
         """The table at ``version`` = the table at ``version - 1`` with ``pod`` removed and, if
         it is a candidate now, placed in candidate order (assume time, then arrival) — what
         ``_prepare`` would build: anything else that changes candidates (a taint, a placement
         overlay, a reconfigure) bumps the engine generation, and claims made since are marked
         taken in the server."""
         if not self.opts.fast_path or self.opts.compute_isolation == "cu" or time.time() < self.journal._legacy_until:
-            return False
+            return ""
         with self._table_mu:
             last = self._last_table
             gen = self._gen
             if last is None or last[0] != version - 1 or last[1] != gen:
                 self.metrics.table_publish_skipped.inc(why="gen" if last is not None and last[1] != gen else "version")
-                return False
+                return ""
             _, _, out, ats = last
             u = O.uid(pod)
             idx = next((i for i, c in enumerate(out) if c.uid == u), None)
@@ -1326,7 +1373,7 @@ class Allocator:
                                      self.journal.replay_ids()))
             self._last_table = (version, gen, out, ats)
             self._published = (version, gen)
-        return True
+        return "add" if idx is None and c is not None else "other"
 
     def _native_loop(self, nat) -> None:
         """Takes in the native server's claims as they happen; rotates its journal file once
@@ -1598,6 +1645,26 @@ class _PatchJob:
 
 
 NATIVE_NO_TABLE = 1 << 31
+
+
+# protobuf wire encoding of the few fields _prepared appends (field tags precomputed:
+# ContainerAllocateResponse envs = 1, mounts = 2, annotations = 4; entry key = 1, value = 2;
+# Mount container_path = 1, host_path = 2)
+def _pb_varint(n: int) -> bytes:
+    out = bytearray()
+    while n >= 0x80:
+        out.append((n & 0x7F) | 0x80)
+        n >>= 7
+    out.append(n)
+    return bytes(out)
+
+
+def _pb_ld(tag: int, b: bytes) -> bytes:
+    return bytes((tag,)) + _pb_varint(len(b)) + b
+
+
+def _pb_map_entry(tag: int, k: str, v: str) -> bytes:
+    return _pb_ld(tag, _pb_ld(0x0A, k.encode()) + _pb_ld(0x12, v.encode()))
 
 
 def _native_blob(version: int, gen: int, flags: int, cands, replay_ids) -> bytes:

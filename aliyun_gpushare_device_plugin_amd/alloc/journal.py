@@ -311,9 +311,11 @@ class AllocJournal:
     @staticmethod
     def fast_head(pod_uid: str, ns: str, name: str, resp_bytes: bytes) -> bytes:
         """The constant part of a fast-path record (see ``record_fast``)."""
-        return (json.dumps({"op": "answer+patch", "uid": pod_uid, "ns": ns, "name": name, "ann": {},
-                            "resp": base64.b64encode(resp_bytes).decode()}, separators=(",", ":"))[:-1]
-                + ',"t":').encode()
+        # the same bytes json.dumps(..., separators=(",", ":")) writes, without its dict walk
+        # (this runs on the pod watch thread for every newly bound pod)
+        q = json.encoder.encode_basestring_ascii
+        return (f'{{"op":"answer+patch","uid":{q(pod_uid)},"ns":{q(ns)},"name":{q(name)},"ann":{{}},'
+                f'"resp":"{base64.b64encode(resp_bytes).decode()}","t":').encode()
 
     def index_answer(self, key: str, pod_uid: str, t: float, blob: bytes, ids) -> None:
         with self._lock:

@@ -163,6 +163,8 @@ def native_share(before: dict | None, after: dict | None) -> dict | None:
     return {"native": fast, "engine": eng, "declined": {k: v for k, v in why.items() if v},
             "waited_for_table": a.get("waited", 0) - b.get("waited", 0),
             "waited_for_watch": a.get("watch_waits", 0) - b.get("watch_waits", 0),
+            "table_wait_mean_ms": round((a.get("wait_ns", 0) - b.get("wait_ns", 0)) / 1e6
+                                        / max(1, a.get("waited", 0) - b.get("waited", 0)), 3),
             "table_hook_skipped": {k: v - (b.get("table_hook_skipped") or {}).get(k, 0)
                                    for k, v in (a.get("table_hook_skipped") or {}).items()}}
 

@@ -253,7 +253,7 @@ struct Taken {
 
 struct Counters {
   std::atomic<uint64_t> fast{0}, forwarded{0}, forwarded_allocate{0}, stale{0}, blocked{0}, replay{0}, nomatch{0}, multi{0},
-      ambiguous{0}, shape{0}, journal{0}, waited{0}, law_sends{0}, conns{0}, unknown{0}, older{0}, watch_waits{0};
+      ambiguous{0}, shape{0}, journal{0}, waited{0}, law_sends{0}, conns{0}, unknown{0}, older{0}, watch_waits{0}, wait_ns{0};
 };
 
 }  // namespace
@@ -507,7 +507,9 @@ bool fast_allocate(Conn* c, int32_t sid, const std::string& body, int64_t t_in) 
     // within a few hundred microseconds (its prepare loop wakes on the same change)
     s->n.waited++;
     auto until = deadline_us(s->fast_wait_us);
+    int64_t w0 = mono_ns();
     s->cv.wait_until(lk, until, [&] { return table_current(s) || s->blocked > 0 || s->stopping.load(); });
+    s->n.wait_ns += (uint64_t)(mono_ns() - w0);
     if (!table_current(s)) {
       (s->blocked > 0 ? s->n.blocked : s->n.stale)++;
       return false;
@@ -1101,7 +1103,7 @@ int gs_dp_stats(gs_dp* s, char* buf, int cap) {
   int n = snprintf(buf, (size_t)cap,
                    "{\"fast\":%llu,\"forwarded\":%llu,\"forwarded_allocate\":%llu,\"declined\":{\"stale\":%llu,\"blocked\":%llu,\"replay\":%llu,"
                    "\"nomatch\":%llu,\"multi\":%llu,\"ambiguous\":%llu,\"shape\":%llu,\"journal\":%llu},"
-                   "\"waited\":%llu,\"law_sends\":%llu,\"connections\":%llu,\"unknown\":%llu,\"older_tables\":%llu,\"watch_waits\":%llu,"
+                   "\"waited\":%llu,\"law_sends\":%llu,\"connections\":%llu,\"unknown\":%llu,\"older_tables\":%llu,\"watch_waits\":%llu,\"wait_ns\":%llu,"
                    "\"journal_used\":%llu,\"taken_pending\":%llu}",
                    (unsigned long long)s->n.fast, (unsigned long long)s->n.forwarded,
                    (unsigned long long)s->n.forwarded_allocate, (unsigned long long)s->n.stale,
@@ -1109,7 +1111,8 @@ int gs_dp_stats(gs_dp* s, char* buf, int cap) {
                    (unsigned long long)s->n.multi, (unsigned long long)s->n.ambiguous, (unsigned long long)s->n.shape,
                    (unsigned long long)s->n.journal, (unsigned long long)s->n.waited,
                    (unsigned long long)s->n.law_sends, (unsigned long long)s->n.conns,
-                   (unsigned long long)s->n.unknown, (unsigned long long)s->n.older, (unsigned long long)s->n.watch_waits, (unsigned long long)used,
+                   (unsigned long long)s->n.unknown, (unsigned long long)s->n.older, (unsigned long long)s->n.watch_waits,
+                   (unsigned long long)s->n.wait_ns, (unsigned long long)used,
                    (unsigned long long)pend);
   return n < cap ? n : -1;
 }

@@ -545,3 +545,36 @@ def test_allocate_lists_once_the_watch_grace_runs_out():
         assert src.fresh_calls == 1
     finally:
         al.close()
+
+
+@pytest.mark.parametrize("shim,ledgers,disable_cgpu,cdi,rocr", [
+    (False, False, False, None, False), (True, False, False, None, False), (True, True, False, None, False),
+    (True, True, True, None, False), (True, True, False, "amd.com/gpu", True)])
+def test_prepared_body_is_the_container_response(tmp_path, shim, ledgers, disable_cgpu, cdi, rocr):
+    """The hand-encoded prepared answer (template bytes + per-pod ledger fields) parses to the
+    same AllocateResponse the engine builds field by field."""
+    model = DeviceModel([gpu(i, 8 << 30) for i in range(2)], const.GIB)
+    src = StaticSource([])
+    opts = AllocatorOptions(shim=ShimConfig(host_dir=str(tmp_path / "shim")) if shim else None,
+                            ledger_dir=str(tmp_path / "ledgers") if ledgers else None,
+                            disable_cgpu=disable_cgpu, cdi_kind=cdi, rocr_visible=rocr)
+    al = Allocator(model, src, FakeClient(src), NODE, opts)
+    try:
+        for i in range(3):
+            pod = mkpod(f"b{i}", 3, 1, 10)
+            c = al._prepared(pod, f"uid-b{i}", 1, 3)
+            got = api.AllocateResponse.FromString(c.body)
+            want_cr = al._container_response(1, 3, 3, f"uid-b{i}", 0, None)
+            # the ledger directory differs per call (a fresh key each time): compare the rest
+            for cr in (got.container_responses[0], want_cr):
+                if const.CTR_ANNOTATION_LEDGER in cr.annotations:
+                    assert cr.annotations[const.CTR_ANNOTATION_LEDGER]
+                    del cr.annotations[const.CTR_ANNOTATION_LEDGER]
+                for m in [m for m in cr.mounts if m.container_path == const.LEDGER_CONTAINER_DIR]:
+                    m.host_path = "<ledger>"
+            want = api.AllocateResponse()
+            want.container_responses.append(want_cr)
+            assert got == want
+            assert (c.lkey != "") == (ledgers and shim and not disable_cgpu)
+    finally:
+        al.close()
