@@ -1312,6 +1312,10 @@ class Allocator:
         nat = self.native
         if nat is None:
             return
+        if pod is not None and not gone and getattr(nat, "spin_us", 0) > 0 and O.uid(pod) not in self._native_prep:
+            # a pod joined the Pending set: the kubelet's Allocate for it is on its way — keep
+            # the server's threads hot from now until it has come (``gs_dp_spin``)
+            nat.spin(nat.spin_us)
         nat.set_version(version)
         if pod is not None:
             t = time.perf_counter()
@@ -1378,6 +1382,7 @@ class Allocator:
     def _native_loop(self, nat) -> None:
         """Takes in the native server's claims as they happen; rotates its journal file once
         the engine's own journal holds everything it has."""
+        last_prefault = 0.0
         while not self._stop.is_set() and self.native is nat:
             rec = nat.taken_next(200)
             if rec is None:
@@ -1385,6 +1390,13 @@ class Allocator:
             try:
                 if rec:
                     self._native_taken(rec)
+                now = time.monotonic()
+                if self.journal.path and (rec or now - last_prefault > 5.0):
+                    # keep the pages the next native answers journal into writable (after each
+                    # answer, and every few seconds against writeback), so the answer never
+                    # takes a page fault
+                    nat.journal_prefault()
+                    last_prefault = now
                 if self.journal.path and nat.journal_used() > self.native_rotate_bytes:
                     nat.block()
                     try:
@@ -1519,6 +1531,15 @@ class Allocator:
             return self._view(pods)
 
     def _apply_fix(self, f: PL.Fix) -> None:
+        if f.reason == "rehomed" and f.assigned is None:
+            # this plugin claimed the pod (its ASSIGNED patch may still be queued, so the pod
+            # can read ASSIGNED=false) but another pod consumed the reservation: re-arm it, and
+            # make its annotation say so once the queued patch has landed — else the pod's own
+            # Allocate finds it claimed (and, after that patch, assigned) and fails
+            with self._mu:
+                claimed = f.uid in self._assigned or f.uid in self._unpatched or f.uid in self._claims
+            if claimed:
+                f = dataclasses.replace(f, assigned=False)
         ann = dict(f.ann)
         if f.assigned is True:
             ann.update(A.assigned_patch()["metadata"]["annotations"])

@@ -80,10 +80,12 @@ def _SIGNATURES(P, I, I64, U64, B):
             ("gs_dp_fast_take", None, [P, B]),
             ("gs_dp_set_fast_wait_us", None, [P, I]),
             ("gs_dp_set_watch_wait_us", None, [P, I]),
+            ("gs_dp_spin", None, [P, I]),
             ("gs_dp_taken_next", I, [P, I, C, I]),
             ("gs_dp_taken_pending", I, [P]),
             ("gs_dp_fast_journal_open", I, [P, B, U64]),
             ("gs_dp_fast_journal_used", U64, [P]),
+            ("gs_dp_fast_journal_prefault", None, [P]),
             ("gs_dp_fast_journal_rotate", I, [P]),
             ("gs_dp_stats", I, [P, C, I]))
 
@@ -93,6 +95,7 @@ class NativeFast:
 
     def __init__(self, lib, h):
         self.lib, self.h = lib, h
+        self.spin_us = 0
         self._buf = ctypes.create_string_buffer(1 << 20)
 
     def publish(self, blob: bytes) -> None:
@@ -144,6 +147,12 @@ class NativeFast:
     def journal_used(self) -> int:
         return self.lib.gs_dp_fast_journal_used(self.h)
 
+    def spin(self, us: int) -> None:
+        self.lib.gs_dp_spin(self.h, us)
+
+    def journal_prefault(self) -> None:
+        self.lib.gs_dp_fast_journal_prefault(self.h)
+
     def journal_rotate(self) -> None:
         self.lib.gs_dp_fast_journal_rotate(self.h)
 
@@ -164,11 +173,15 @@ class NativeDevicePluginServer(DevicePluginServer):
     # for the engine to republish it before going to the engine's full path (~0.3 ms itself);
     # watch_wait_us: how long one that no candidate matches waits for the plugin's pod watch
     # to deliver the pod (the kubelet's watch can be ahead) before the engine's path
-    def __init__(self, *a, handler_threads: int = 4, fast_wait_us: int = 300, watch_wait_us: int = 2000, **kw):
+    # spin_us: after a pod was published into the table, the connection threads busy-poll this
+    # long for the kubelet's Allocate instead of sleeping (0 = never)
+    def __init__(self, *a, handler_threads: int = 4, fast_wait_us: int = 300, watch_wait_us: int = 2000,
+                 spin_us: int = 5000, **kw):
         super().__init__(*a, **kw)
         self.handler_threads = handler_threads
         self.fast_wait_us = fast_wait_us
         self.watch_wait_us = watch_wait_us
+        self.spin_us = spin_us
         self._h = None
         self._lib = None
         self._threads: list[threading.Thread] = []
@@ -190,6 +203,7 @@ class NativeDevicePluginServer(DevicePluginServer):
         lib.gs_dp_set_watch_wait_us(h, self.watch_wait_us)
         self._push_devices()
         self.fast = NativeFast(lib, h)
+        self.fast.spin_us = self.spin_us
         self.allocator.attach_native(self.fast)
         for i in range(self.handler_threads):
             t = threading.Thread(target=self._handle_loop, name=f"dp-native-{i}", daemon=True)

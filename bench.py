@@ -165,6 +165,10 @@ def native_share(before: dict | None, after: dict | None) -> dict | None:
             "waited_for_watch": a.get("watch_waits", 0) - b.get("watch_waits", 0),
             "table_wait_mean_ms": round((a.get("wait_ns", 0) - b.get("wait_ns", 0)) / 1e6
                                         / max(1, a.get("waited", 0) - b.get("waited", 0)), 3),
+            # inside a native answer (mean over the answers): taking the server lock, the journal
+            # record, and request-complete -> reply (all of the server's own time)
+            "native_answer_mean_us": {k: round((a.get(f"{k}_ns", 0) - b.get(f"{k}_ns", 0)) / 1e3 / max(1, fast), 1)
+                                      for k in ("lock", "journal", "answer")},
             "table_hook_skipped": {k: v - (b.get("table_hook_skipped") or {}).get(k, 0)
                                    for k, v in (a.get("table_hook_skipped") or {}).items()}}
 

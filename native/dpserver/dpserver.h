@@ -52,6 +52,9 @@ GS_DP_API void gs_dp_set_fast_wait_us(gs_dp* s, int us);
 // How long an Allocate no candidate matches may wait for the pod watch (a newer table) before
 // it goes to the engine.
 GS_DP_API void gs_dp_set_watch_wait_us(gs_dp* s, int us);
+// Busy-poll the kubelet connections for the next `us` microseconds (an Allocate is expected:
+// a pod was just published) instead of sleeping in poll.
+GS_DP_API void gs_dp_spin(gs_dp* s, int us);
 // Next native answer for the engine's bookkeeping: record = u32 uid_len, uid, u32 req_len,
 // AllocateRequest bytes, f64 wall time (the journal record's "t"), u64 handler ns. Returns the
 // record size, 0 on timeout, -1 once stopped, -2 if `cap` is too small (record kept).
@@ -62,6 +65,8 @@ GS_DP_API int gs_dp_taken_pending(gs_dp* s);
 // its own journal with everything in it.
 GS_DP_API int gs_dp_fast_journal_open(gs_dp* s, const char* path, uint64_t bytes);
 GS_DP_API uint64_t gs_dp_fast_journal_used(gs_dp* s);
+// Re-dirty the next pages the journal appends will write (off the Allocate path).
+GS_DP_API void gs_dp_fast_journal_prefault(gs_dp* s);
 GS_DP_API int gs_dp_fast_journal_rotate(gs_dp* s);
 
 // Counters as a JSON object (NUL-terminated); returns its length or -1.

@@ -355,3 +355,30 @@ def test_slow_pod_resources_does_not_serialize_allocates():
         t.join()
     assert time.perf_counter() - t0 < 0.28, "Lists ran one after the other"
     assert sorted(out) == ["0", "1"] and kl.calls == 2
+
+
+def test_rehoming_a_claimed_pod_whose_patch_has_not_landed_rearms_it():
+    """The race behind a flaky end-to-end run: B's admission took A's reservation (size match,
+    no identity), and the placement pass re-homes A *before* A's queued ASSIGNED=true patch has
+    landed, so A still reads ASSIGNED=false. A must be re-armed anyway (not left claimed), its
+    annotation must end ASSIGNED=false, and A's own Allocate must get the re-homed reservation."""
+    from .test_allocate_engine import NODE, req
+
+    class Down(Client):
+        def patch_pod(self, *a, **k):                        # the ASSIGNED patch stays queued
+            raise RuntimeError("apiserver unreachable")
+
+    src = StaticSource([mkpod("a", 4, 0, 1)])
+    al = Allocator(DeviceModel([gpu(0, 8 << 30), gpu(1, 8 << 30)], const.GIB), src, Down(src), NODE,
+                   AllocatorOptions(async_patch=True, fast_path=False))
+    try:
+        r = al.allocate(req(4))                              # B's admission takes A's reservation
+        assert r.container_responses[0].envs[const.ENV_RESOURCE_INDEX] == "0"
+        assert "uid-a" in al._assigned and _ann(src, "a")[const.ENV_ASSIGNED_FLAG] == "false"
+        al._apply_fix(PL.Fix("uid-a", "default", "a", {const.ENV_RESOURCE_INDEX: "1"}, None, [], "rehomed"))
+        assert "uid-a" not in al._assigned and "uid-a" in al._revoked
+        assert al._overlay["uid-a"][const.ENV_ASSIGNED_FLAG] == "false"
+        r = al.allocate(req(4))                              # A's own admission
+        assert r.container_responses[0].envs[const.ENV_RESOURCE_INDEX] == "1"
+    finally:
+        al.close()
