@@ -280,3 +280,95 @@ def test_zero_slack_perfect_packings_are_found(nbins, cap, sizes):
         for a, s in zip(got, sizes):
             used[a] += s
         assert used == [cap] * nbins
+
+
+@settings(max_examples=150, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(ops=st.lists(st.tuples(st.sampled_from(["add", "add", "add", "run", "delete", "assign", "claim", "taint"]),
+                              st.integers(0, 7), st.integers(1, 3), st.integers(0, 1), st.integers(0, 40)),
+                    min_size=1, max_size=25))
+def test_table_hook_equals_a_full_rebuild(ops):
+    """alloc/engine.py ``_publish_change``: after any sequence of pod-cache changes (pods bound,
+    admitted, deleted, assigned by a patch) and engine-side changes (claims, taints), the table
+    the watch-thread hook published is entry for entry the one a full ``_prepare`` builds."""
+    import json as _json
+    import time
+
+    from aliyun_gpushare_device_plugin_amd import const as C
+    from aliyun_gpushare_device_plugin_amd.alloc.engine import Allocator, AllocatorOptions
+    from aliyun_gpushare_device_plugin_amd.cluster.podcache import WatchCache
+    from aliyun_gpushare_device_plugin_amd.device.model import DeviceModel
+    from tests.test_allocate_engine import FakeClient, mkpod
+    from tests.test_units_and_model import gpu
+
+    class Nat:
+        spin_us = 0
+
+        def publish(self, blob):
+            pass
+
+        def set_version(self, v):
+            pass
+
+        def set_gen(self, g):
+            pass
+
+    cache = WatchCache(client=None, node="node-a")
+    cache._synced.set()
+    al = Allocator(DeviceModel([gpu(0, 8 << 30), gpu(1, 8 << 30)], C.GIB), cache, FakeClient(cache), "node-a",
+                   AllocatorOptions(async_patch=True, fast_path=False))
+    al.native = Nat()
+    al.opts.fast_path = True
+    cache.on_pending_change = al._on_pending
+    al._prepare(cache)
+    pods: dict = {}
+    rv = [1]
+
+    def put(p, typ="MODIFIED"):
+        rv[0] += 1
+        p = _json.loads(_json.dumps(p))
+        p["metadata"]["resourceVersion"] = str(rv[0])
+        cache._apply({"type": typ, "object": p})
+        return p
+
+    def expected():
+        with al._mu:
+            cands = [p for p in al._candidates(fresh=False) if p["metadata"]["uid"] not in al._claims]
+        out = []
+        for p in cands:
+            shape = al._info(p)[3]
+            if shape and (len(shape) > 1 or al.model.gpu(int(p["metadata"]["annotations"][C.ENV_RESOURCE_INDEX])) is not None):
+                out.append(p["metadata"]["uid"])
+        return out
+
+    try:
+        for op, k, size, g, at in ops:
+            name = f"p{k}"
+            cur = pods.get(name)
+            if op == "add" and cur is None:
+                pods[name] = put(mkpod(name, size, g, 100 + at), "ADDED")
+            elif op == "run" and cur is not None:
+                cur["status"]["phase"] = "Running"
+                pods[name] = put(cur)
+            elif op == "delete" and cur is not None:
+                put(cur, "DELETED")
+                del pods[name]
+            elif op == "assign" and cur is not None:
+                cur["metadata"]["annotations"][C.ENV_ASSIGNED_FLAG] = "true"
+                pods[name] = put(cur)
+            elif op == "claim" and cur is not None:
+                with al._mu:                                   # a native answer taken in
+                    al._assigned[cur["metadata"]["uid"]] = time.monotonic()
+            elif op == "taint" and cur is not None:
+                with al._mu:
+                    al._tainted[cur["metadata"]["uid"]] = time.monotonic()
+                    al._bump_gen()
+                al._prepare(cache)                             # a generation change: the full path
+            v, gen, out, _ = al._last_table
+            assert (v, gen) == (cache.pending_version, al._gen)
+            got = [c.uid for c in out]
+            # claims taken after the table was built stay in it (the server marks them taken)
+            want = expected()
+            assert [u for u in got if u not in al._assigned] == want, (op, name, got, want)
+    finally:
+        al.native = None
+        al.close()
