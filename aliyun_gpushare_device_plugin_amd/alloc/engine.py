@@ -218,6 +218,8 @@ class Allocator:
         self._last_table: tuple | None = None
         self._table_mu = threading.Lock()
         self._resp_tmpl: dict[tuple, api.ContainerAllocateResponse] = {}   # _container_response
+        # answers prepared before the bind (PrebindWatch -> precompute), by (uid, gpu, units)
+        self._precomputed: collections.OrderedDict = collections.OrderedDict()
         self._tmpl_bytes: dict[tuple, bytes] = {}                          # _prepared
         self.native_rotate_bytes = 16 << 20       # rotate the native journal file past this
         self.native_prep_keep = 4096              # prepared answers kept for native claims past the current table
@@ -296,8 +298,10 @@ class Allocator:
         the handler. The key carries the two annotations the plugin itself
         rewrites, so an object updated in place (no new resourceVersion) is never served stale."""
         ann = O.annotations(p)
-        k = (O.uid(p), O.resource_version(p), ann.get(const.ENV_ASSIGNED_FLAG),
-             ann.get(const.ENV_RESOURCE_ASSUME_TIME))
+        # a pod's gpu-mem requests cannot change (extended resources are not resizable in
+        # place), so the key is the pod plus the two annotations the result depends on — not
+        # its resourceVersion: the bind (a new version) hits what the pre-bind pass parsed
+        k = (O.uid(p), ann.get(const.ENV_ASSIGNED_FLAG), ann.get(const.ENV_RESOURCE_ASSUME_TIME))
         v = self._pinfo.get(k)
         if v is None:
             shape = tuple(x for x in O.gpu_mem_per_container(p) if x > 0)
@@ -846,7 +850,7 @@ class Allocator:
                 ats.append(at)
                 continue
             k = (u, g, shape[0])
-            c = self._prep_cache.get(k)
+            c = self._prep_cache.get(k) or self._precomputed.pop(k, None)
             if c is None:
                 if self.model.gpu(g) is None:
                     continue
@@ -891,6 +895,25 @@ class Allocator:
         if len(prep) > self.native_prep_keep + n_current:
             for u in list(prep)[:len(prep) - n_current - self.native_prep_keep // 2]:
                 del prep[u]
+
+    def precompute(self, pod: dict) -> None:
+        """A pod placed on this node but not bound yet (``cluster/podcache.py`` PrebindWatch):
+        prepare its Allocate answer now, so the watch-thread hook only has to insert it when
+        the bind arrives — the kubelet's Allocate follows the same watch event."""
+        if self.native is None or not self.opts.fast_path or self.opts.compute_isolation == "cu":
+            return
+        assumed, _, _, shape = self._info(pod)
+        if not assumed or len(shape) != 1:
+            return
+        u, g = O.uid(pod), A.gpu_id_from_annotation(pod)
+        k = (u, g, shape[0])
+        if self.model.gpu(g) is None or k in self._precomputed or k in self._prep_cache:
+            return
+        c = self._prepared(pod, u, g, shape[0])
+        _native_blob(0, 0, 0, [c], [])                # fills c.frag: the table entry, encoded once
+        self._precomputed[k] = c
+        while len(self._precomputed) > 1024:
+            self._precomputed.popitem(last=False)
 
     def _prune_replay_index(self, src) -> None:
         if self.journal.indexed_uids():         # replay index: only pods that can still be retried
@@ -1354,7 +1377,8 @@ class Allocator:
                         c = _Prepared(u, O.namespace(p), O.name(p), shape[0], True, g)
                     elif self.model.gpu(g) is not None:
                         k = (u, g, shape[0])
-                        c = self._prep_cache.get(k) or self._prepared(p, u, g, shape[0])
+                        c = (self._prep_cache.get(k) or self._precomputed.pop(k, None)
+                             or self._prepared(p, u, g, shape[0]))
                         self._prep_cache[k] = c
             keep_at = idx is not None and c is not None and ats[idx] == at
             if idx is not None:

@@ -100,6 +100,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--native-fast-wait-us", type=int, default=300,
                    help="native server: how long an Allocate that finds the prepared answers one pod-cache "
                         "change behind waits for them to be rebuilt before the engine's full path answers it")
+    p.add_argument("--prebind-watch", default="true",
+                   help="watch pods the scheduler extender placed on this node (label gpushare.amd.com/node) "
+                        "and prepare their Allocate answers before the bind reaches the node")
     p.add_argument("--quota-enforcement", default="auto", choices=("auto", "off", "report", "kill"),
                    help="node-side quota watchdog over the kernel's per-process HBM (DRM fdinfo): report "
                         "pods above their share, or also SIGKILL their largest GPU process (the shim cannot be "
@@ -144,7 +147,7 @@ def config_from_args(a) -> PluginConfig:
         journal_path=a.journal_path, compute_isolation=a.compute_isolation,
         pod_resources_socket=a.pod_resources_socket, placement_s=a.placement_interval,
         admission_identity=a.admission_identity, quota_enforcement=a.quota_enforcement,
-        grpc_server=a.grpc_server, native_fast_wait_us=a.native_fast_wait_us,
+        grpc_server=a.grpc_server, native_fast_wait_us=a.native_fast_wait_us, prebind_watch=_bool(a.prebind_watch),
         cdi_kind=a.cdi_kind, expose_devices=a.device_specs,
         quota_watch_s=a.quota_watch_interval, quota_slack_mib=a.quota_slack_mib,
         dmem_limits=a.dmem_limits, cgroup_root=a.cgroup_root)

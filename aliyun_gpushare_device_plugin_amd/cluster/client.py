@@ -293,12 +293,14 @@ class APIClient:
         return self.request("POST", f"/api/v1/namespaces/{namespace}/pods/{name}/binding", body=body)
 
     def watch_pods(self, field_selector: str | None = None, resource_version: str | None = None,
-                   timeout_seconds: int = 300, stop: threading.Event | None = None, holder: list | None = None):
+                   timeout_seconds: int = 300, stop: threading.Event | None = None, holder: list | None = None,
+                   label_selector: str | None = None):
         """Yields watch events (dicts with ``type`` and ``object``) until the server ends the
         stream (``timeoutSeconds``), or ``stop`` is set and the socket is shut down by
         ``abort_watch(holder)``. Uses its own connection; reads block without a socket timeout
         (an idle watch is normal), so stopping works by shutting the socket down."""
-        q = {"watch": "1", "fieldSelector": field_selector, "resourceVersion": resource_version,
+        q = {"watch": "1", "fieldSelector": field_selector, "labelSelector": label_selector,
+             "resourceVersion": resource_version,
              "timeoutSeconds": str(timeout_seconds), "allowWatchBookmarks": "true"}
         url = self._prefix + "/api/v1/pods?" + urllib.parse.urlencode({k: v for k, v in q.items() if v})
         c = self._new_conn()

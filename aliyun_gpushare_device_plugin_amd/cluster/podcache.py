@@ -18,6 +18,7 @@ import contextlib
 import threading
 import time
 
+from .. import const
 from ..utils import log
 from . import objects as O
 from .client import APIClient, APIError
@@ -149,6 +150,50 @@ class KubeletSource(_PerCallSource):
             return [p for p in self.kubelet.get_node_running_pods() if not O.is_terminated(p)]
         except Exception:  # noqa: BLE001
             return self.fallback.node_pods()
+
+
+class PrebindWatch:
+    """Pods the extender has placed on this node but not bound yet (label
+    ``gpushare.amd.com/node=<node>``, ``spec.nodeName`` empty): ``on_pod(pod)`` for each, so the
+    Allocate engine can prepare the pod's answer before the bind reaches the node's pod watch
+    and, right behind it, the kubelet's Allocate. Pods placed by an extender that does not set
+    the label are simply never seen here (the answer is prepared at the bind, as before)."""
+
+    def __init__(self, client: APIClient, node: str, on_pod, watch_timeout: int = 300):
+        self.client, self.node, self.on_pod, self.watch_timeout = client, node, on_pod, watch_timeout
+        self._stop = threading.Event()
+        self._conn: list = []
+        self._thread = None
+        self.events = 0
+
+    def start(self) -> "PrebindWatch":
+        self._thread = threading.Thread(target=self._run, name="pod-prebind-watch", daemon=True)
+        self._thread.start()
+        return self
+
+    def stop(self) -> None:
+        self._stop.set()
+        self.client.abort_watch(self._conn)
+
+    def _run(self) -> None:
+        backoff = 0.1
+        while not self._stop.is_set():
+            try:
+                for ev in self.client.watch_pods("spec.nodeName=", None, self.watch_timeout, self._stop, self._conn,
+                                                 label_selector=f"{const.POD_LABEL_NODE}={self.node}"):
+                    if ev.get("type") in ("ADDED", "MODIFIED") and not O.node_name(ev.get("object") or {}):
+                        self.events += 1
+                        try:
+                            self.on_pod(ev["object"])
+                        except Exception as e:  # noqa: BLE001 - preparing ahead is an optimisation
+                            log.V(2).info("prebind: %s", e)
+                backoff = 0.1
+            except Exception as e:  # noqa: BLE001 - apiserver restart, expired watch
+                if self._stop.is_set():
+                    break
+                log.V(2).info("prebind watch: %s", e)
+                self._stop.wait(backoff)
+                backoff = min(backoff * 2, 5.0)
 
 
 class WatchCache(PodSource):

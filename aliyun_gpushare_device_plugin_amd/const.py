@@ -74,6 +74,9 @@ ENV_HSA_CU_MASK = "HSA_CU_MASK"
 ENV_ROC_CU_MASK = "ROC_GLOBAL_CU_MASK"
 ENV_CU_SLOTS = "GPUSHARE_CU_SLOTS"              # the slot run, for the workload's information
 POD_ANNOTATION_CU_SLOTS = "gpushare.amd.com/cu-slots"                  # written by the plugin
+# label the MI355X extender sets with its annotations, before the bind: the node's plugin sees the
+# pod coming (a label-selected watch) and prepares its Allocate answer ahead of the bind
+POD_LABEL_NODE = "gpushare.amd.com/node"
 POD_ANNOTATION_CU_SLOTS_REQUEST = "gpushare.amd.com/cu-slots-request"  # optional, set by the user
 # Node annotation carrying the exported xGMI topology (JSON, see parallel/topology.py).
 NODE_ANNOTATION_TOPOLOGY = "gpushare.amd.com/xgmi-topology"

@@ -356,7 +356,7 @@ class Extender:
             const.ENV_RESOURCE_BY_POD: str(req),
             const.ENV_RESOURCE_ASSUME_TIME: str(assume_ns or time.time_ns()),
             const.ENV_ASSIGNED_FLAG: "false",
-        }}})
+        }, "labels": {const.POD_LABEL_NODE: node}}})   # the node's plugin prepares ahead of the bind
         self.client.bind_pod(ns, nm, node, O.uid(pod))
         return patched
 

@@ -23,7 +23,7 @@ from ..alloc.engine import Allocator, AllocatorOptions
 from ..cluster import nodestatus, objects as O
 from ..cluster.client import APIClient, build_client
 from ..cluster.kubelet import KubeletClient
-from ..cluster.podcache import KubeletSource, ListSource, WatchCache
+from ..cluster.podcache import KubeletSource, ListSource, PrebindWatch, WatchCache
 from ..device import smi as S
 from ..device.health import HealthMonitor
 from ..device.model import DeviceConfigError, DeviceModel
@@ -88,6 +88,7 @@ class PluginConfig:
     # "python" (grpcio), "auto" = native when the library loads
     grpc_server: str = "auto"
     native_fast_wait_us: int = 300       # native server: wait for a republished table (see native_server.py)
+    prebind_watch: bool = True           # prepare answers of pods the extender placed here, before their bind
 
 
 class SharedGPUManager:
@@ -101,6 +102,7 @@ class SharedGPUManager:
         self.smi = smi
         self.events: "queue.Queue" = queue.Queue()
         self.metrics = M.PluginMetrics()
+        self._prebind = None
         self.metrics.registry.add_collector(lambda: M.native_server_exposition(self._debug_view().get("native_server")))
         self.plugin: DevicePluginServer | None = None
         self.health: HealthMonitor | None = None
@@ -161,6 +163,9 @@ class SharedGPUManager:
             disable_cgpu = nodestatus.cgpu_isolation_disabled(self.client, cfg.node_name)
         if self.pod_source is not None:
             self.pod_source.stop()
+        if self._prebind is not None:
+            self._prebind.stop()
+            self._prebind = None
         fallback = ListSource(self.client, cfg.node_name) if self.client else None
         if cfg.pod_source == "watch" and self.client is not None:
             src = WatchCache(self.client, cfg.node_name,
@@ -195,6 +200,8 @@ class SharedGPUManager:
         allocator = self.allocator
         if allocator.podres is None:
             allocator.set_pod_resources(self._pod_resources())
+        if cfg.prebind_watch and cfg.pod_source == "watch" and self.client is not None:
+            self._prebind = PrebindWatch(self.client, cfg.node_name, allocator.precompute).start()
         self.model = model
         cls = self._server_class()
         kw = {"fast_wait_us": cfg.native_fast_wait_us} if cls is not DevicePluginServer else {}
@@ -466,6 +473,8 @@ class SharedGPUManager:
                 self.plugin.stop()
             if self.pod_source is not None:
                 self.pod_source.stop()
+            if self._prebind is not None:
+                self._prebind.stop()
             if self.allocator is not None:
                 self.allocator.flush_patches(2.0)
                 self.allocator.close()

@@ -176,7 +176,7 @@ class NativeDevicePluginServer(DevicePluginServer):
     # spin_us: after a pod was published into the table, the connection threads busy-poll this
     # long for the kubelet's Allocate instead of sleeping (0 = never)
     def __init__(self, *a, handler_threads: int = 4, fast_wait_us: int = 300, watch_wait_us: int = 2000,
-                 spin_us: int = 5000, **kw):
+                 spin_us: int = 0, **kw):
         super().__init__(*a, **kw)
         self.handler_threads = handler_threads
         self.fast_wait_us = fast_wait_us

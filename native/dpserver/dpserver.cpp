@@ -27,6 +27,7 @@
 #include <fcntl.h>
 #include <nghttp2/nghttp2.h>
 #include <poll.h>
+#include <sched.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -268,7 +269,10 @@ struct gs_dp {
   // a pod the kubelet is about to admit was published (gs_dp_spin). A core that slept pays
   // tens of microseconds of wake-up and cold caches on the Allocate path (measured: building
   // one journal record takes 1 us hot, 30 us on a core idle for 300 ms)
-  std::atomic<int64_t> spin_until{0};   // an Allocate with no candidate yet waits this long for the pod watch
+  std::atomic<int64_t> spin_until{0};
+  // bumped (under mu) by everything a table wait depends on: a spinning waiter watches it
+  // without the lock, so it never contends with the publisher it is waiting for
+  std::atomic<uint64_t> table_seq{0};   // an Allocate with no candidate yet waits this long for the pod watch
   // fake IDs of native answers -> when: a kubelet retry of them is for the engine (replay),
   // kept until a published replay set covers them (or for 30 s, by when the engine has)
   std::unordered_map<std::string, int64_t> answered_ids;
@@ -497,8 +501,10 @@ void wait_for_table(gs_dp* s, std::unique_lock<std::mutex>& lk, int us, Pred pre
   if (s->spin_until.load(std::memory_order_relaxed) > mono_ns()) {
     int64_t dl = mono_ns() + (int64_t)us * 1000;
     while (!pred() && mono_ns() < dl) {
+      uint64_t seq = s->table_seq.load(std::memory_order_acquire);
       lk.unlock();
-      for (int i = 0; i < 32; ++i) __builtin_ia32_pause();
+      while (s->table_seq.load(std::memory_order_acquire) == seq && mono_ns() < dl && !s->stopping.load())
+        sched_yield();
       lk.lock();
     }
     return;
@@ -778,7 +784,9 @@ void serve_conn(std::shared_ptr<Conn> cp) {
       break;
     }
     if (pr == 0) {                             // spinning, nothing yet
-      for (int i = 0; i < 32; ++i) __builtin_ia32_pause();
+      // yield, not pause: a thread that shares this CPU (the kubelet's, the plugin's pod
+      // watch) must run at once, not after a scheduler time slice (~ms) of our spinning
+      sched_yield();
       continue;
     }
     if (fds[1].revents & POLLIN) {
@@ -1007,6 +1015,7 @@ int gs_dp_fast_publish(gs_dp* s, const uint8_t* blob, int len) {
     for (auto it = s->answered_ids.begin(); it != s->answered_ids.end();)
       it = (t.replay.count(it->first) || now - it->second > 30 * 1000000000LL) ? s->answered_ids.erase(it) : ++it;
     s->table = std::move(t);
+    s->table_seq++;
   }
   s->cv.notify_all();
   return 0;
@@ -1016,6 +1025,7 @@ void gs_dp_set_version(gs_dp* s, uint64_t version) {
   {
     std::lock_guard<std::mutex> lk(s->mu);
     s->cur_version = std::max(s->cur_version, version);   // versions only grow
+    s->table_seq++;
   }
   s->cv.notify_all();
 }
@@ -1024,6 +1034,7 @@ void gs_dp_set_gen(gs_dp* s, uint64_t gen) {
   {
     std::lock_guard<std::mutex> lk(s->mu);
     s->cur_gen = std::max(s->cur_gen, gen);
+    s->table_seq++;
   }
   s->cv.notify_all();
 }
@@ -1032,6 +1043,7 @@ void gs_dp_fast_block(gs_dp* s) {
   {
     std::lock_guard<std::mutex> lk(s->mu);   // an answer in progress holds mu: it completes first
     s->blocked++;
+    s->table_seq++;
   }
   s->cv.notify_all();
 }
@@ -1040,6 +1052,7 @@ void gs_dp_fast_unblock(gs_dp* s) {
   {
     std::lock_guard<std::mutex> lk(s->mu);
     if (s->blocked > 0) s->blocked--;
+    s->table_seq++;
   }
   s->cv.notify_all();
 }

@@ -708,3 +708,39 @@ def test_the_table_hook_keeps_its_caches_bounded(tmp_path):
     finally:
         al.native = None
         al.close()
+
+
+def test_answers_are_prepared_before_the_bind():
+    """The extender labels a pod with its node together with its annotations, before binding
+    it; the node's plugin sees it on a label-selected watch of unbound pods and prepares the
+    Allocate answer then, so at the bind the watch-thread hook only inserts it."""
+    from aliyun_gpushare_device_plugin_amd.sim.cluster import SimCluster
+
+    with SimCluster([("n", "fake:1x8G")]) as c:
+        m = c.manager("n")
+        al = m.allocator
+        built = []
+        real = al._prepared
+
+        def counting(p, u, g, units):
+            built.append((u, threading.current_thread().name))
+            return real(p, u, g, units)
+
+        al._prepared = counting
+        pod = c.create_pod(2)
+        c.extender.note_pending(pod)
+        ns, nm = pod["metadata"]["namespace"], pod["metadata"]["name"]
+        # the extender's annotation + label patch, then (a moment later) the bind
+        c.client.patch_pod(ns, nm, {"metadata": {"annotations": {
+            const.ENV_RESOURCE_INDEX: "0", const.ENV_RESOURCE_BY_POD: "2",
+            const.ENV_RESOURCE_ASSUME_TIME: str(time.time_ns()), const.ENV_ASSIGNED_FLAG: "false"},
+            "labels": {const.POD_LABEL_NODE: "n"}}})
+        t = time.monotonic() + 5
+        while not any(u == pod["metadata"]["uid"] for u, _ in built) and time.monotonic() < t:
+            time.sleep(0.01)
+        assert built and built[0][1] == "pod-prebind-watch"     # prepared on the pre-bind watch
+        c.client.bind_pod(ns, nm, "n", pod["metadata"]["uid"])
+        adm = c.admit(c.client.get_pod(ns, nm))
+        assert adm.error is None and adm.responses[0].envs[const.ENV_RESOURCE_INDEX] == "0"
+        assert [n for u, n in built if u == pod["metadata"]["uid"]] == ["pod-prebind-watch"]   # not again
+        assert m.plugin.stats()["fast"] >= 1
