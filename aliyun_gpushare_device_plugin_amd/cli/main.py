@@ -100,6 +100,10 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--native-fast-wait-us", type=int, default=300,
                    help="native server: how long an Allocate that finds the prepared answers one pod-cache "
                         "change behind waits for them to be rebuilt before the engine's full path answers it")
+    p.add_argument("--native-spin-us", type=int, default=0,
+                   help="native server: busy-poll the kubelet connection this long after a pod joined the "
+                        "Pending set (keeps the answering core awake; costs a core meanwhile and, on a "
+                        "small VM, can delay the kubelet itself: off by default)")
     p.add_argument("--prebind-watch", default="true",
                    help="watch pods the scheduler extender placed on this node (label gpushare.amd.com/node) "
                         "and prepare their Allocate answers before the bind reaches the node")
@@ -148,6 +152,7 @@ def config_from_args(a) -> PluginConfig:
         pod_resources_socket=a.pod_resources_socket, placement_s=a.placement_interval,
         admission_identity=a.admission_identity, quota_enforcement=a.quota_enforcement,
         grpc_server=a.grpc_server, native_fast_wait_us=a.native_fast_wait_us, prebind_watch=_bool(a.prebind_watch),
+        native_spin_us=a.native_spin_us,
         cdi_kind=a.cdi_kind, expose_devices=a.device_specs,
         quota_watch_s=a.quota_watch_interval, quota_slack_mib=a.quota_slack_mib,
         dmem_limits=a.dmem_limits, cgroup_root=a.cgroup_root)

@@ -89,6 +89,7 @@ class PluginConfig:
     grpc_server: str = "auto"
     native_fast_wait_us: int = 300       # native server: wait for a republished table (see native_server.py)
     prebind_watch: bool = True           # prepare answers of pods the extender placed here, before their bind
+    native_spin_us: int = 0              # native server: busy-poll this long after a pod is published (0 = off)
 
 
 class SharedGPUManager:
@@ -204,7 +205,8 @@ class SharedGPUManager:
             self._prebind = PrebindWatch(self.client, cfg.node_name, allocator.precompute).start()
         self.model = model
         cls = self._server_class()
-        kw = {"fast_wait_us": cfg.native_fast_wait_us} if cls is not DevicePluginServer else {}
+        kw = ({"fast_wait_us": cfg.native_fast_wait_us, "spin_us": cfg.native_spin_us}
+              if cls is not DevicePluginServer else {})
         return cls(model, allocator, self._plugin_socket(), const.RESOURCE_NAME, cfg.preferred_allocation,
                    self.metrics, **kw)
 
