@@ -850,7 +850,7 @@ class Allocator:
                 ats.append(at)
                 continue
             k = (u, g, shape[0])
-            c = self._prep_cache.get(k) or self._precomputed.pop(k, None)
+            c = self._prep_cache.get(k) or self._take_precomputed(k)
             if c is None:
                 if self.model.gpu(g) is None:
                     continue
@@ -911,9 +911,19 @@ class Allocator:
             return
         c = self._prepared(pod, u, g, shape[0])
         _native_blob(0, 0, 0, [c], [])                # fills c.frag: the table entry, encoded once
-        self._precomputed[k] = c
+        self._precomputed[k] = (c, time.monotonic())
         while len(self._precomputed) > 1024:
             self._precomputed.popitem(last=False)
+
+    # the ledger directory a prepared answer names is kept for a grace period without a pod on
+    # this node (quota/ledger.py collect, 60 s): a bind later than this gets a fresh answer
+    PRECOMPUTED_TTL_S = 30.0
+
+    def _take_precomputed(self, k) -> "_Prepared | None":
+        e = self._precomputed.pop(k, None)
+        if e is None or time.monotonic() - e[1] > self.PRECOMPUTED_TTL_S:
+            return None
+        return e[0]
 
     def _prune_replay_index(self, src) -> None:
         if self.journal.indexed_uids():         # replay index: only pods that can still be retried
@@ -1377,7 +1387,7 @@ class Allocator:
                         c = _Prepared(u, O.namespace(p), O.name(p), shape[0], True, g)
                     elif self.model.gpu(g) is not None:
                         k = (u, g, shape[0])
-                        c = (self._prep_cache.get(k) or self._precomputed.pop(k, None)
+                        c = (self._prep_cache.get(k) or self._take_precomputed(k)
                              or self._prepared(p, u, g, shape[0]))
                         self._prep_cache[k] = c
             keep_at = idx is not None and c is not None and ats[idx] == at

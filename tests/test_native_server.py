@@ -744,3 +744,32 @@ def test_answers_are_prepared_before_the_bind():
         assert adm.error is None and adm.responses[0].envs[const.ENV_RESOURCE_INDEX] == "0"
         assert [n for u, n in built if u == pod["metadata"]["uid"]] == ["pod-prebind-watch"]   # not again
         assert m.plugin.stats()["fast"] >= 1
+
+
+def test_a_stale_prebind_answer_is_not_used():
+    """An answer prepared before the bind names a ledger directory the collector removes after
+    a grace period with no pod on the node; a bind that comes later gets a fresh answer."""
+    model = DeviceModel([gpu(i, 8 << 30) for i in range(2)], const.GIB)
+    src = VSource([])
+
+    class Nat:
+        spin_us = 0
+
+        def publish(self, blob):
+            pass
+
+    al = Allocator(model, src, FakeClient(src), "node-a", AllocatorOptions(async_patch=True))
+    al.native = Nat()
+    try:
+        p = mkpod("late", 2, 1, 5)
+        al.precompute(p)
+        k = ("uid-late", 1, 2)
+        assert k in al._precomputed
+        c, t = al._precomputed[k]
+        al._precomputed[k] = (c, t - al.PRECOMPUTED_TTL_S - 1)   # the bind comes too late
+        assert al._take_precomputed(k) is None and k not in al._precomputed
+        al.precompute(p)
+        assert al._take_precomputed(k) is not None
+    finally:
+        al.native = None
+        al.close()
