@@ -91,3 +91,19 @@ def test_topology_view_lists_cu_slots():
         rows = [line.split() for line in topo.splitlines() if line.startswith("GPU0 ") and "-" in line]
         assert ["GPU0", "0-13", "big"] in rows and ["GPU0", "14-20", "small"] in rows
         assert "CU SLOTS" not in I.render(c.client, topology=False)
+
+
+def test_podgetter_lists_the_kubelets_pods(capsys):
+    """``podgetter`` (C15, ``cmd/podgetter/main.go``): the kubelet's /pods, one line per pod."""
+    from aliyun_gpushare_device_plugin_amd.cli import podgetter
+    from aliyun_gpushare_device_plugin_amd.sim.cluster import SimCluster
+
+    with SimCluster([("n", "fake:1x8G")]) as c:
+        pod, where, adm = c.run_pod(2)
+        assert adm.error is None
+        kl = c.nodes["n"].kubelet
+        port = kl.serve_pods()
+        rc = podgetter.main(["--kubelet-address", "127.0.0.1", "--kubelet-port", str(port), "--scheme", "http",
+                             "--token", kl.pods_token])
+        out, err = capsys.readouterr()
+        assert rc == 0 and f"default/{pod['metadata']['name']}\t" in out and '"items": 1' in err
