@@ -1,0 +1,322 @@
+"""The native Allocate table: the engine's side of the native DevicePlugin server.
+
+``plugin/native_server.py`` serves the kubelet from ``libgpushare_dpserver.so`` (native/dpserver),
+which answers the common Allocate from a table of prepared answers without entering Python.
+This mixin of ``alloc/engine.py``'s ``Allocator`` keeps that table equal to what the engine's
+own candidate rules give (``docs/ALLOCATE_PATH.md``):
+
+* the pod-cache hook (``_on_pending`` / ``_publish_change``, on the watch thread) applies each
+  change of the Pending set to the last table at once; a full rebuild (``Allocator._prepare``)
+  covers everything else (engine generation changes, relists);
+* answers of pods the extender placed here are prepared before their bind (``precompute``,
+  fed by ``cluster/podcache.py`` PrebindWatch);
+* the server's claims come back through ``_native_loop`` / ``_native_taken`` for the same
+  bookkeeping as the engine's own answers (claimed set, grants, replay index, write-behind
+  PATCH), and its journal file is compacted into the engine's.
+
+Wire formats: the table blob (``_native_blob``, parsed by ``dpserver.cpp`` ``parse_table``) and
+the few protobuf records prepared answers append (``_pb_*``).
+"""
+from __future__ import annotations
+
+import bisect
+import dataclasses
+import threading
+import time
+
+from ..api import v1beta1 as api
+from ..cluster import objects as O
+from ..utils import log
+from . import annotations as A
+
+
+@dataclasses.dataclass(frozen=True)
+class _Prepared:
+    uid: str
+    ns: str
+    name: str
+    size: int              # single-container pods: its units; multi: the first container's
+    multi: bool            # multi-container pod: the full path must handle it
+    gpu: int
+    body: bytes = b""      # serialized AllocateResponse (one container)
+    head: bytes = b""      # journal record prefix (AllocJournal.fast_head)
+    lkey: str = ""
+    # this entry in the native table's wire format, encoded once (_native_blob)
+    frag: bytes = dataclasses.field(default=b"", compare=False, repr=False)
+
+
+NATIVE_NO_TABLE = 1 << 31
+
+
+# protobuf wire encoding of the few fields _prepared appends (field tags precomputed:
+# ContainerAllocateResponse envs = 1, mounts = 2, annotations = 4; entry key = 1, value = 2;
+# Mount container_path = 1, host_path = 2)
+def _pb_varint(n: int) -> bytes:
+    out = bytearray()
+    while n >= 0x80:
+        out.append((n & 0x7F) | 0x80)
+        n >>= 7
+    out.append(n)
+    return bytes(out)
+
+
+def _pb_ld(tag: int, b: bytes) -> bytes:
+    return bytes((tag,)) + _pb_varint(len(b)) + b
+
+
+def _pb_map_entry(tag: int, k: str, v: str) -> bytes:
+    return _pb_ld(tag, _pb_ld(0x0A, k.encode()) + _pb_ld(0x12, v.encode()))
+
+
+def _native_blob(version: int, gen: int, flags: int, cands, replay_ids) -> bytes:
+    """The fast table in the native server's format (native/dpserver/dpserver.cpp "table
+    blob"): the prepared candidates in match order, then the fake IDs of possible replays."""
+    import struct
+
+    def s(b):
+        b = b if isinstance(b, bytes) else b.encode()
+        return struct.pack("<I", len(b)) + b
+    parts = [struct.pack("<QQIII", version, gen, flags, len(cands), len(replay_ids))]
+    for c in cands:
+        f = getattr(c, "frag", None)
+        if not f:
+            f = struct.pack("<IB", c.size, 1 if c.multi else 0) + s(c.uid) + s(c.body) + s(c.head)
+            if isinstance(c, _Prepared):
+                object.__setattr__(c, "frag", f)      # the entry is immutable: encode it once
+        parts.append(f)
+    parts += [s(i) for i in replay_ids]
+    return b"".join(parts)
+
+
+class NativeTable:
+    """Mixin of ``Allocator``: the native server's table and claims (see the module docstring)."""
+
+    # ------------------------------------------------------------------------------------
+    # native fast path (plugin/native_server.py, native/dpserver)
+    # ------------------------------------------------------------------------------------
+    def attach_native(self, nat) -> None:
+        """Serve the fast path from the native server ``nat``: the prepare loop publishes its
+        table there instead of answering here, and the server's claims come back through
+        ``_native_taken``. Its journal records go to ``<journal>.fast`` (loaded with the journal)."""
+        self.native = nat
+        with self._mu:
+            self._fast = None
+            nat.set_gen(self._gen)
+        self._hook_pods(nat)
+        if self.journal.path:
+            # loaded and compacted into the main journal at start-up: the fast file starts empty
+            nat.journal_open(self.journal.fast_path(), 32 << 20)
+            nat.journal_rotate()
+        threading.Thread(target=self._native_loop, args=(nat,), name="native-claims", daemon=True).start()
+        ev = getattr(self.pods, "changed", None)
+        if ev is not None:
+            ev.set()
+
+    def detach_native(self) -> None:
+        nat, self.native = self.native, None
+        if nat is not None:
+            self._drain_native(nat)
+            src = self.pods
+            if getattr(src, "on_pending_change", None) is not None:
+                src.on_pending_change = None
+            if self._native_hold:
+                self._native_hold = False
+
+    def _hook_pods(self, nat) -> None:
+        src = self.pods
+        if hasattr(src, "on_pending_change"):
+            with src._lock:
+                src.on_pending_change = self._on_pending
+                nat.set_version(src.pending_version)
+
+    def _on_pending(self, version: int, pod: dict | None = None, gone: bool = False) -> None:
+        """Pod-cache hook (the watch thread, cache lock held), at every change of the Pending
+        set: the native server learns the version first, so it never answers from a table
+        older than the cache. The change itself (one pod joined, changed or left the set) is
+        then applied to the last table right here, so the kubelet's Allocate — usually arriving
+        right after the same watch event — finds a current table instead of waiting for the
+        prepare loop."""
+        nat = self.native
+        if nat is None:
+            return
+        if pod is not None and not gone and getattr(nat, "spin_us", 0) > 0 and O.uid(pod) not in self._native_prep:
+            # a pod joined the Pending set: the kubelet's Allocate for it is on its way — keep
+            # the server's threads hot from now until it has come (``gs_dp_spin``)
+            nat.spin(nat.spin_us)
+        nat.set_version(version)
+        if pod is not None:
+            t = time.perf_counter()
+            try:
+                kind = self._publish_change(nat, version, pod, gone)
+                if kind:
+                    self.metrics.table_publish.observe(time.perf_counter() - t, path=f"hook_{kind}")
+            except Exception as e:  # noqa: BLE001 - the prepare loop republishes anyway
+                log.V(2).info("incremental native table: %s", e)
+
+    def _publish_change(self, nat, version: int, pod: dict, gone: bool) -> str:
+        """The table at ``version`` = the table at ``version - 1`` with ``pod`` removed and, if
+        it is a candidate now, placed in candidate order (assume time, then arrival) — what
+        ``_prepare`` would build: anything else that changes candidates (a taint, a placement
+        overlay, a reconfigure) bumps the engine generation, and claims made since are marked
+        taken in the server."""
+        if not self.opts.fast_path or self.opts.compute_isolation == "cu" or time.time() < self.journal._legacy_until:
+            return ""
+        with self._table_mu:
+            last = self._last_table
+            gen = self._gen
+            if last is None or last[0] != version - 1 or last[1] != gen:
+                self.metrics.table_publish_skipped.inc(why="gen" if last is not None and last[1] != gen else "version")
+                return ""
+            _, _, out, ats = last
+            u = O.uid(pod)
+            idx = next((i for i, c in enumerate(out) if c.uid == u), None)
+            c = at = None
+            if not gone:
+                p = self._view([pod])[0]
+                assumed, _, at, shape = self._info(p)
+                if (assumed and shape and not O.deleting(p) and u not in self._assigned and u not in self._claims
+                        and u not in self._tainted):
+                    g = A.gpu_id_from_annotation(p)
+                    if len(shape) > 1:
+                        c = _Prepared(u, O.namespace(p), O.name(p), shape[0], True, g)
+                    elif self.model.gpu(g) is not None:
+                        k = (u, g, shape[0])
+                        c = (self._prep_cache.get(k) or self._take_precomputed(k)
+                             or self._prepared(p, u, g, shape[0]))
+                        self._prep_cache[k] = c
+            keep_at = idx is not None and c is not None and ats[idx] == at
+            if idx is not None:
+                old = out[idx]
+                if c is None or (old.gpu, old.size) != (c.gpu, c.size):
+                    self._prep_cache.pop((old.uid, old.gpu, old.size), None)   # left the table
+                out, ats = out[:idx] + out[idx + 1:], ats[:idx] + ats[idx + 1:]
+            if c is not None:
+                i = idx if keep_at else bisect.bisect_right(ats, at)   # same place, or after its equals
+                out, ats = out[:i] + (c,) + out[i:], ats[:i] + (at,) + ats[i:]
+                self._native_prep.pop(u, None)
+                self._native_prep[u] = c
+                # the current entries must be the newest: re-append them after the new one
+                for e in out:
+                    if e.uid != u:
+                        self._native_prep.pop(e.uid, None)
+                        self._native_prep[e.uid] = e
+                self._trim_native_prep(len(out))
+            nat.publish(_native_blob(version, gen, 1 if self.podres is not None else 0, list(out),
+                                     self.journal.replay_ids()))
+            self._last_table = (version, gen, out, ats)
+            self._published = (version, gen)
+        return "add" if idx is None and c is not None else "other"
+
+    def _native_loop(self, nat) -> None:
+        """Takes in the native server's claims as they happen; rotates its journal file once
+        the engine's own journal holds everything it has."""
+        last_prefault = 0.0
+        while not self._stop.is_set() and self.native is nat:
+            rec = nat.taken_next(200)
+            if rec is None:
+                break
+            try:
+                if rec:
+                    self._native_taken(rec)
+                now = time.monotonic()
+                if self.journal.path and (rec or now - last_prefault > 5.0):
+                    # keep the pages the next native answers journal into writable (after each
+                    # answer, and every few seconds against writeback), so the answer never
+                    # takes a page fault
+                    nat.journal_prefault()
+                    last_prefault = now
+                if self.journal.path and nat.journal_used() > self.native_rotate_bytes:
+                    nat.block()
+                    try:
+                        self._drain_native(nat)
+                        self._drain_post()
+                        self.journal.compact()
+                        nat.journal_rotate()
+                    finally:
+                        nat.unblock()
+            except Exception as e:  # noqa: BLE001 - one bad record must not stop every later claim's bookkeeping
+                log.error("native claim bookkeeping failed: %s", e)
+                self._stop.wait(0.05)
+
+    def _drain_native(self, nat=None) -> None:
+        nat = nat or self.native
+        if nat is None:
+            return
+        while True:
+            rec = nat.taken_next(0)
+            if not rec:
+                return
+            self._native_taken(rec)
+
+    def _native_taken(self, rec) -> None:
+        """One native answer: the same claim and bookkeeping as the engine's fast path."""
+        uid, rb, t, hns = rec
+        pick = self._native_prep.get(uid)
+        with self._mu:
+            self._assigned[uid] = time.monotonic()
+            self._unpatched.add(uid)
+            self._revoked.discard(uid)
+            self._answer_seq += 1
+        if pick is None:
+            # not expected (every entry of a published table stays in _native_prep): the
+            # answer went out, so the pod still owes its ASSIGNED patch — take it from the cache
+            p = self.pods.get(uid)
+            log.error("native fast path answered pod uid %s outside the prepared answers%s", uid,
+                      "" if p is not None else "; the pod is gone from the cache, no patch")
+            if p is None:
+                with self._mu:
+                    self._unpatched.discard(uid)
+                return
+            pick = self._prepared(p, uid, A.gpu_id_from_annotation(p), self._info(p)[3][0])
+        req = api.AllocateRequest.FromString(rb)
+        ids = req.container_requests[0].devices_ids
+        self.journal.note_fast(uid, pick.ns, pick.name, t, ids)
+        self._post.append((rb, pick, t))
+        log.info("----Allocating GPU for gpu mem is started---- RequestPodGPUs: %d; pod %s, new allocated GPUs info: "
+                 "gpu index %d uuid %s (patch queued, native)", len(ids), pick.name, pick.gpu,
+                 self.model.uuid_by_index(pick.gpu))
+        self.metrics.allocate_outcomes.inc(outcome="assigned")
+        self.metrics.allocate_latency.observe(hns / 1e9, phase="total")
+        self.metrics.allocate_latency.observe(hns / 1e9, phase="native")
+        self.metrics.allocate_requests.observe(0)
+        if self._patch_q is not None:
+            from .engine import _PatchJob             # the engine's patcher job (engine imports this module)
+
+            self._patch_q.put(_PatchJob(uid, pick.ns, pick.name, {}))
+
+    def _trim_native_prep(self, n_current: int) -> None:
+        """Bound the prepared answers kept for native claims (the current table's entries are
+        the last ``n_current`` inserted and always stay)."""
+        prep = self._native_prep
+        if len(prep) > self.native_prep_keep + n_current:
+            for u in list(prep)[:len(prep) - n_current - self.native_prep_keep // 2]:
+                del prep[u]
+
+    def precompute(self, pod: dict) -> None:
+        """A pod placed on this node but not bound yet (``cluster/podcache.py`` PrebindWatch):
+        prepare its Allocate answer now, so the watch-thread hook only has to insert it when
+        the bind arrives — the kubelet's Allocate follows the same watch event."""
+        if self.native is None or not self.opts.fast_path or self.opts.compute_isolation == "cu":
+            return
+        assumed, _, _, shape = self._info(pod)
+        if not assumed or len(shape) != 1:
+            return
+        u, g = O.uid(pod), A.gpu_id_from_annotation(pod)
+        k = (u, g, shape[0])
+        if self.model.gpu(g) is None or k in self._precomputed or k in self._prep_cache:
+            return
+        c = self._prepared(pod, u, g, shape[0])
+        _native_blob(0, 0, 0, [c], [])                # fills c.frag: the table entry, encoded once
+        self._precomputed[k] = (c, time.monotonic())
+        while len(self._precomputed) > 1024:
+            self._precomputed.popitem(last=False)
+
+    # the ledger directory a prepared answer names is kept for a grace period without a pod on
+    # this node (quota/ledger.py collect, 60 s): a bind later than this gets a fresh answer
+    PRECOMPUTED_TTL_S = 30.0
+
+    def _take_precomputed(self, k) -> "_Prepared | None":
+        e = self._precomputed.pop(k, None)
+        if e is None or time.monotonic() - e[1] > self.PRECOMPUTED_TTL_S:
+            return None
+        return e[0]

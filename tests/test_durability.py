@@ -4,6 +4,7 @@
 Reference: ``allocate.go:132-152`` answers only after the PATCH landed; this build answers
 first and journals the pending PATCH (``alloc/journal.py``).
 """
+import json
 import os
 import time
 
@@ -53,9 +54,31 @@ def test_killed_plugin_lands_pending_patch_after_restart(tmp_path):
         for name in ("a", "b"):
             got = c.wait_assigned({"metadata": {"namespace": "default", "name": name}}, timeout=15)
             assert O.annotations(got)[const.ENV_ASSIGNED_FLAG] == "true", name
-        # journal: every pending patch has its landing
-        j = AllocJournal(journal)
-        assert j.unlanded() == []
+        # journal: every pending patch has its landing (written right after the PATCH returned:
+        # the plugin process may still be at it when the annotation is already visible). Read
+        # the files as they are: opening an AllocJournal would compact them under the plugin.
+        def unlanded():                         # answers live in .fast, landings in the journal
+            pend, landed = set(), set()
+            for f in (journal, journal + ".fast"):
+                if not os.path.exists(f):
+                    continue
+                for ln in open(f, "rb").read().split(b"\n"):
+                    try:
+                        e = json.loads(ln)
+                    except ValueError:
+                        continue
+                    if e.get("op") in ("patch", "answer+patch"):
+                        pend.add(e["uid"])
+                    elif e.get("op") == "landed":
+                        landed.add(e["uid"])
+            return pend - landed
+
+        t = time.monotonic() + 5
+        while unlanded() and time.monotonic() < t:
+            time.sleep(0.05)
+        assert unlanded() == set()
+    j = AllocJournal(journal)                   # the plugin is gone: the journal reader agrees
+    assert j.unlanded() == []
 
 
 def _model(n=2, gib=4):
