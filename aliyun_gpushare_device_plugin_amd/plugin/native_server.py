@@ -7,7 +7,7 @@ interpreter lock — while the engine's prepared answer took ~0.1 ms (``bench.py
 ``allocate_breakdown_p50_ms``). Here the HTTP/2 + gRPC framing runs in C++ (libnghttp2), and:
 
 * the common Allocate is answered in the library from the engine's published table of
-  prepared answers (``alloc/engine.py`` ``attach_native``): claim, journal record, reply — the
+  prepared answers (``alloc/native_table.py`` ``attach_native``): claim, journal record, reply — the
   interpreter is not entered; the claim reaches the engine right after for the write-behind
   PATCH;
 * every other request (the options, PreStartContainer, GetPreferredAllocation, and each
