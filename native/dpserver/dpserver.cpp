@@ -221,6 +221,7 @@ struct Fwd {
   int32_t stream;
   std::string method, body;
   int64_t t_in;
+  int64_t deadline = 0;     // CLOCK_MONOTONIC ns from the client's grpc-timeout; 0 = none
 };
 
 struct Taken {
@@ -231,7 +232,7 @@ struct Taken {
 
 struct Counters {
   std::atomic<uint64_t> fast{0}, forwarded{0}, forwarded_allocate{0}, stale{0}, blocked{0}, replay{0}, nomatch{0}, multi{0},
-      ambiguous{0}, shape{0}, journal{0}, waited{0}, law_sends{0}, conns{0}, unknown{0}, older{0}, watch_waits{0}, wait_ns{0},
+      ambiguous{0}, shape{0}, journal{0}, waited{0}, law_sends{0}, conns{0}, unknown{0}, older{0}, watch_waits{0}, wait_ns{0}, expired{0},
       lock_ns{0}, journal_ns{0}, answer_ns{0};
 };
 
@@ -299,7 +300,27 @@ struct Stream {
   int64_t t_in = 0, t_out = 0;
   bool stamp = false;
   bool too_big = false;     // the request passed kMaxRequest: its bytes are dropped, answered RESOURCE_EXHAUSTED
+  int64_t deadline = 0;     // grpc-timeout, as CLOCK_MONOTONIC ns
 };
+
+// gRPC "grpc-timeout": up to 8 digits and a unit (H, M, S, m, u, n). 0 when absent or malformed.
+int64_t parse_grpc_timeout_ns(const uint8_t* v, size_t n) {
+  if (n < 2 || n > 9) return 0;
+  int64_t x = 0;
+  for (size_t i = 0; i + 1 < n; ++i) {
+    if (v[i] < '0' || v[i] > '9') return 0;
+    x = x * 10 + (v[i] - '0');
+  }
+  switch (v[n - 1]) {
+    case 'H': return x * 3600 * 1000000000LL;
+    case 'M': return x * 60 * 1000000000LL;
+    case 'S': return x * 1000000000LL;
+    case 'm': return x * 1000000LL;
+    case 'u': return x * 1000LL;
+    case 'n': return x;
+    default: return 0;
+  }
+}
 
 // Larger requests are refused (gRPC's default receive limit is 4 MiB; Python's handler buffer is 8)
 constexpr size_t kMaxRequest = (8u << 20) + 5;
@@ -653,6 +674,7 @@ void request_done(Conn* c, int32_t sid) {
   f->method = st.path;
   f->body = std::move(msg);
   f->t_in = st.t_in;
+  f->deadline = st.deadline;
   {
     std::lock_guard<std::mutex> lk(s->q_mu);
     f->id = s->next_id++;
@@ -675,6 +697,10 @@ int on_header(nghttp2_session*, const nghttp2_frame* f, const uint8_t* name, siz
   if (nl == 5 && !memcmp(name, ":path", 5)) {
     auto it = static_cast<Conn*>(ud)->streams.find(f->hd.stream_id);
     if (it != static_cast<Conn*>(ud)->streams.end()) it->second.path.assign((const char*)value, vl);
+  } else if (nl == 12 && !memcmp(name, "grpc-timeout", 12)) {
+    auto it = static_cast<Conn*>(ud)->streams.find(f->hd.stream_id);
+    int64_t t = parse_grpc_timeout_ns(value, vl);
+    if (it != static_cast<Conn*>(ud)->streams.end() && t > 0) it->second.deadline = mono_ns() + t;
   }
   return 0;
 }
@@ -940,6 +966,23 @@ int64_t gs_dp_next(gs_dp* s, int timeout_ms, char* method, int method_cap, uint8
       s->queue.pop_front();
       if ((int)f->body.size() <= body_cap && (int)f->method.size() < method_cap) s->inflight[f->id] = f;
     }
+    if (f->deadline && mono_ns() > f->deadline) {
+      // the client gave up while the request waited for a handler (the kubelet's admission of
+      // that pod already failed): running it would only claim a pod for nobody
+      {
+        std::lock_guard<std::mutex> lk(s->q_mu);
+        s->inflight.erase(f->id);
+      }
+      s->n.expired++;
+      if (auto c = f->conn.lock()) {
+        {
+          std::lock_guard<std::mutex> lk(c->out_mu);
+          c->outbox.push_back(Reply{f->stream, 4, "deadline exceeded before a handler took the request", ""});
+        }
+        wake(c.get());
+      }
+      continue;
+    }
     if ((int)f->body.size() > body_cap || (int)f->method.size() >= method_cap) {
       if (auto c = f->conn.lock()) {
         {
@@ -1173,7 +1216,7 @@ int gs_dp_stats(gs_dp* s, char* buf, int cap) {
   int n = snprintf(buf, (size_t)cap,
                    "{\"fast\":%llu,\"forwarded\":%llu,\"forwarded_allocate\":%llu,\"declined\":{\"stale\":%llu,\"blocked\":%llu,\"replay\":%llu,"
                    "\"nomatch\":%llu,\"multi\":%llu,\"ambiguous\":%llu,\"shape\":%llu,\"journal\":%llu},"
-                   "\"waited\":%llu,\"law_sends\":%llu,\"connections\":%llu,\"unknown\":%llu,\"older_tables\":%llu,\"watch_waits\":%llu,\"wait_ns\":%llu,\"lock_ns\":%llu,\"journal_ns\":%llu,\"answer_ns\":%llu,"
+                   "\"waited\":%llu,\"law_sends\":%llu,\"connections\":%llu,\"unknown\":%llu,\"older_tables\":%llu,\"expired\":%llu,\"watch_waits\":%llu,\"wait_ns\":%llu,\"lock_ns\":%llu,\"journal_ns\":%llu,\"answer_ns\":%llu,"
                    "\"journal_used\":%llu,\"taken_pending\":%llu}",
                    (unsigned long long)s->n.fast, (unsigned long long)s->n.forwarded,
                    (unsigned long long)s->n.forwarded_allocate, (unsigned long long)s->n.stale,
@@ -1181,7 +1224,7 @@ int gs_dp_stats(gs_dp* s, char* buf, int cap) {
                    (unsigned long long)s->n.multi, (unsigned long long)s->n.ambiguous, (unsigned long long)s->n.shape,
                    (unsigned long long)s->n.journal, (unsigned long long)s->n.waited,
                    (unsigned long long)s->n.law_sends, (unsigned long long)s->n.conns,
-                   (unsigned long long)s->n.unknown, (unsigned long long)s->n.older, (unsigned long long)s->n.watch_waits,
+                   (unsigned long long)s->n.unknown, (unsigned long long)s->n.older, (unsigned long long)s->n.expired, (unsigned long long)s->n.watch_waits,
                    (unsigned long long)s->n.wait_ns, (unsigned long long)s->n.lock_ns,
                    (unsigned long long)s->n.journal_ns, (unsigned long long)s->n.answer_ns, (unsigned long long)used,
                    (unsigned long long)pend);

@@ -773,3 +773,40 @@ def test_a_stale_prebind_answer_is_not_used():
     finally:
         al.native = None
         al.close()
+
+
+def test_a_request_past_its_deadline_is_not_run(tmp_path):
+    """A forwarded request whose client deadline (grpc-timeout) passed while it waited for a
+    handler is answered DEADLINE_EXCEEDED without running: an Allocate the kubelet gave up on
+    would only claim a pod for nobody."""
+    model = DeviceModel([gpu(i, 8 << 30) for i in range(2)], const.GIB)
+    src = VSource([mkpod("p", 2, 1, 10)])
+    al = Allocator(model, src, FakeClient(src), "node-a", AllocatorOptions(async_patch=True, fast_path=False))
+    srv = NativeDevicePluginServer(model, al, str(tmp_path / "dp.sock"), handler_threads=1)
+    srv.start()
+    calls = []
+    real = al.allocate_raw
+
+    def slow(req, defer=None):
+        calls.append(time.monotonic())
+        time.sleep(0.4)
+        return real(req, defer=defer)
+
+    al.allocate_raw = slow
+    ch, stub = _stub(srv)
+    try:
+        first = stub.Allocate.future(_req("a", "b"))             # occupies the only handler
+        time.sleep(0.05)
+        with pytest.raises(grpc.RpcError) as e:
+            stub.Allocate(_req("c", "d"), timeout=0.1)          # waits behind it, past its deadline
+        assert e.value.code() == grpc.StatusCode.DEADLINE_EXCEEDED
+        first.result(timeout=5)
+        t = time.monotonic() + 2
+        while srv.stats()["expired"] < 1 and time.monotonic() < t:
+            time.sleep(0.01)
+        assert srv.stats()["expired"] == 1 and len(calls) == 1
+        assert stub.GetDevicePluginOptions(api.Empty()) == srv.options()   # still serving
+    finally:
+        ch.close()
+        srv.stop()
+        al.close()
