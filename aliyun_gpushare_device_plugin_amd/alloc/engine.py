@@ -317,14 +317,20 @@ class Allocator(NativeTable):
             out.append(p)
         return out
 
-    def _candidates(self, fresh: bool) -> list[dict]:
-        pods = self._view(A.dedupe_by_uid(self.pods.pending_pods(fresh=fresh), self.node))
-        now = time.monotonic()
-        if now - self._last_sweep > 1.0:          # amortised: the set holds the last claim_ttl_s of pods
+    def _sweep_assigned(self, now: float) -> None:
+        """Forget claims older than claim_ttl_s whose patch has landed (caller holds ``_mu``;
+        amortised to once a second). The full path sweeps before matching; with the native
+        server answering, the claim reader does (``native_table.py`` ``_native_loop``)."""
+        if now - self._last_sweep > 1.0:
             self._last_sweep = now
             for u, t in list(self._assigned.items()):
                 if now - t > self.opts.claim_ttl_s and u not in self._unpatched:
                     del self._assigned[u]
+
+    def _candidates(self, fresh: bool) -> list[dict]:
+        pods = self._view(A.dedupe_by_uid(self.pods.pending_pods(fresh=fresh), self.node))
+        now = time.monotonic()
+        self._sweep_assigned(now)
         if fresh and self._tainted:   # forget a withheld reservation once its pod is gone
             live = {O.uid(p) for p in self.pods.node_pods() if not O.deleting(p)}
             for u in [u for u in self._tainted if u not in live]:

@@ -219,6 +219,9 @@ class NativeTable:
                 if rec:
                     self._native_taken(rec)
                 now = time.monotonic()
+                if now - self._last_sweep > 1.0:
+                    with self._mu:
+                        self._sweep_assigned(now)
                 if self.journal.path and (rec or now - last_prefault > 5.0):
                     # keep the pages the next native answers journal into writable (after each
                     # answer, and every few seconds against writeback), so the answer never
@@ -303,8 +306,8 @@ class NativeTable:
             return
         u, g = O.uid(pod), A.gpu_id_from_annotation(pod)
         k = (u, g, shape[0])
-        if self.model.gpu(g) is None or k in self._precomputed or k in self._prep_cache:
-            return
+        if self.model.gpu(g) is None or k in self._precomputed or k in self._prep_cache or u in self._native_prep:
+            return                                    # prepared already (the bind came first)
         c = self._prepared(pod, u, g, shape[0])
         _native_blob(0, 0, 0, [c], [])                # fills c.frag: the table entry, encoded once
         self._precomputed[k] = (c, time.monotonic())

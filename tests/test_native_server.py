@@ -810,3 +810,21 @@ def test_a_request_past_its_deadline_is_not_run(tmp_path):
         ch.close()
         srv.stop()
         al.close()
+
+
+def test_claims_are_swept_with_the_native_server_answering(tmp_path):
+    """With the native server answering, the engine's full match (which used to sweep expired
+    claims) may never run: the claim reader sweeps them, so the claimed set stays bounded."""
+    srv, al, src = _server(tmp_path, [])
+    try:
+        al.opts.claim_ttl_s = 0.1
+        with al._mu:
+            for i in range(50):
+                al._assigned[f"old-{i}"] = time.monotonic() - 10
+        t = time.monotonic() + 3
+        while al._assigned and time.monotonic() < t:
+            time.sleep(0.05)
+        assert not al._assigned
+    finally:
+        srv.stop()
+        al.close()
