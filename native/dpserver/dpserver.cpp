@@ -311,15 +311,19 @@ int64_t parse_grpc_timeout_ns(const uint8_t* v, size_t n) {
     if (v[i] < '0' || v[i] > '9') return 0;
     x = x * 10 + (v[i] - '0');
   }
+  int64_t unit;
   switch (v[n - 1]) {
-    case 'H': return x * 3600 * 1000000000LL;
-    case 'M': return x * 60 * 1000000000LL;
-    case 'S': return x * 1000000000LL;
-    case 'm': return x * 1000000LL;
-    case 'u': return x * 1000LL;
-    case 'n': return x;
+    case 'H': unit = 3600 * 1000000000LL; break;
+    case 'M': unit = 60 * 1000000000LL; break;
+    case 'S': unit = 1000000000LL; break;
+    case 'm': unit = 1000000LL; break;
+    case 'u': unit = 1000LL; break;
+    case 'n': unit = 1; break;
     default: return 0;
   }
+  int64_t ns;
+  if (__builtin_mul_overflow(x, unit, &ns) || ns > (int64_t)1 << 61) return 0;   // years: no deadline
+  return ns;
 }
 
 // Larger requests are refused (gRPC's default receive limit is 4 MiB; Python's handler buffer is 8)
