@@ -8,6 +8,8 @@ import json
 import os
 import time
 
+import pytest
+
 from aliyun_gpushare_device_plugin_amd import const
 from aliyun_gpushare_device_plugin_amd.alloc.engine import Allocator, AllocatorOptions
 from aliyun_gpushare_device_plugin_amd.alloc.journal import AllocJournal
@@ -220,3 +222,56 @@ def test_prefault_survives_a_concurrent_compaction(tmp_path):
         t.join()
     assert errors == []
     j.close()
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_chaos_churn_never_overcommits_and_every_patch_lands(tmp_path, seed):
+    """Randomised churn through the whole stack (extender, native server, engine, journal,
+    placement truth) with faults mixed in: the plugin SIGKILLed and restarted, the apiserver
+    dropping the plugin's PATCHes for a while. Invariants: no GPU is ever given more than it
+    has (by what the admitted containers were really answered), and once the faults stop every
+    admitted pod ends ASSIGNED=true with nothing left unlanded in the journal."""
+    import random
+
+    rnd = random.Random(seed)
+    journal = str(tmp_path / "j.jsonl")
+    cap = 16
+    with SimCluster([("n", "fake:2x16G")], plugin_mode="process",
+                    extra_plugin_args=["--journal-path", journal]) as c:
+        c.extender.watch()
+        live: dict = {}                                        # name -> (gpu answered, size)
+        faults = {"kill": 0, "patch_outage": 0}
+        for step in range(60):
+            r = rnd.random()
+            if step in (10, 35):
+                r = 0.0                                        # at least two kills per run
+            elif step in (5, 25):
+                r = 0.1                                        # and two PATCH outages
+            if r < 0.08:
+                faults["kill"] += 1
+                c.kill_plugin("n")
+                c.restart_plugin("n")
+            elif r < 0.16:
+                faults["patch_outage"] += 1
+                c.api.store.inject("assign_patch", rnd.uniform(0.2, 1.0))
+            elif r < 0.40 and live:
+                name = rnd.choice(sorted(live))
+                c.delete_pod(c.client.get_pod("default", name))
+                del live[name]
+            else:
+                size = rnd.choice([1, 2, 4, 8])
+                pod, where, adm = c.run_pod(size)
+                if where is None:
+                    continue                                   # the extender found no room
+                assert adm.error is None, adm.error
+                g = int(adm.responses[0].envs[const.ENV_RESOURCE_INDEX])
+                live[pod["metadata"]["name"]] = (g, size)
+                used = {0: 0, 1: 0}
+                for gg, s in live.values():
+                    used[gg] += s
+                assert max(used.values()) <= cap, (step, used)
+        assert faults["kill"] >= 2 and faults["patch_outage"] >= 2 and len(live) >= 1
+        c.api.store.inject("assign_patch", 0)
+        for name in live:
+            got = c.wait_assigned({"metadata": {"namespace": "default", "name": name}}, timeout=20)
+            assert O.annotations(got)[const.ENV_ASSIGNED_FLAG] == "true", name
