@@ -183,6 +183,12 @@ def main(argv=None) -> int:
     # behind a whole decode. A 0.25 ms interval bounds that wait (the kubelet blocks on it).
     sys.setswitchinterval(float(os.environ.get("GPUSHARE_SWITCH_INTERVAL", "0.00025")))
     log.setup(verbosity=a.v, json_lines=a.log_json, buffered=os.environ.get("GPUSHARE_LOG_UNBUFFERED") != "1")
+    # SIGUSR2: every thread's stack to stderr straight from the signal handler — works even when
+    # the interpreter is wedged (SIGQUIT's dump needs the main thread to run Python)
+    import faulthandler
+    import signal as _signal
+
+    faulthandler.register(_signal.SIGUSR2, all_threads=True)
     log.V(1).info("Start gpushare device plugin")
     cfg = config_from_args(a)
     if a.install_shim:

@@ -215,7 +215,10 @@ class SimCluster:
         n.kubelet.registered.clear()
         self._start_plugin(n)
         if not n.kubelet.registered.wait(timeout):
-            raise TimeoutError(f"plugin on {node} did not re-register{self._plugin_log_tail(n)}")
+            if n.proc is not None and n.proc.poll() is None:
+                n.proc.send_signal(signal.SIGUSR2)       # every thread's stack into its log
+                time.sleep(1.0)
+            raise TimeoutError(f"plugin on {node} did not re-register{self._plugin_log_tail(n, 20000)}")
 
     def _plugin_log_tail(self, node, n: int = 3000) -> str:
         """The end of a process-mode plugin's log, for timeout messages."""

@@ -63,7 +63,9 @@ def _emit(levelno: int, msg, args, fields, depth: int = 2) -> None:
                 return
         else:
             _buf.append(line)
-        _flush_locked()
+    # outside _lock: flush() takes _wlock, then _lock — the only order either lock is nested in
+    # (taking _wlock while holding _lock deadlocked against the flusher thread)
+    flush()
 
 
 _buf: list[str] = []
@@ -73,7 +75,7 @@ _FLUSH_S = 0.05
 _flusher = None
 
 
-_wlock = threading.Lock()      # orders writes; never held by a caller of _emit's fast branch
+_wlock = threading.Lock()      # orders writes; taken before _lock, never while holding it
 
 
 def _take_locked() -> str:
@@ -92,13 +94,6 @@ def _write(data: str) -> None:
         st.flush()
     except (OSError, ValueError):
         pass
-
-
-def _flush_locked() -> None:
-    data = _take_locked()
-    if data:
-        with _wlock:
-            _write(data)
 
 
 def flush() -> None:

@@ -224,11 +224,12 @@ def test_prefault_survives_a_concurrent_compaction(tmp_path):
     j.close()
 
 
-@pytest.mark.parametrize("seed", [1, 2, 3])
-def test_chaos_churn_never_overcommits_and_every_patch_lands(tmp_path, seed):
+@pytest.mark.parametrize("seed,identity", [(s, False) for s in range(3, 7)] + [(1, True), (2, True)])
+def test_chaos_churn_never_overcommits_and_every_patch_lands(tmp_path, seed, identity):
     """Randomised churn through the whole stack (extender, native server, engine, journal,
     placement truth) with faults mixed in: the plugin SIGKILLed and restarted, the apiserver
-    dropping the plugin's PATCHes for a while. Invariants: no GPU is ever given more than it
+    dropping the plugin's PATCHes for a while; without admission identity equal-size pods also
+    swap reservations and placement truth repairs them. Invariants: no GPU is ever given more than it
     has (by what the admitted containers were really answered), and once the faults stop every
     admitted pod ends ASSIGNED=true with nothing left unlanded in the journal."""
     import random
@@ -236,7 +237,7 @@ def test_chaos_churn_never_overcommits_and_every_patch_lands(tmp_path, seed):
     rnd = random.Random(seed)
     journal = str(tmp_path / "j.jsonl")
     cap = 16
-    with SimCluster([("n", "fake:2x16G")], plugin_mode="process",
+    with SimCluster([("n", "fake:2x16G")], plugin_mode="process", admission_identity=identity,
                     extra_plugin_args=["--journal-path", journal]) as c:
         c.extender.watch()
         live: dict = {}                                        # name -> (gpu answered, size)
