@@ -50,6 +50,18 @@ def _shim_stats() -> dict | None:
     return dict(zip(("used", "quota", "denied", "peak"), (v.value for v in vals)))
 
 
+def _arena_release():
+    """With an HBM broker arena (quota shim + GPUSHARE_HBM_BROKER), hand its granules back now
+    that everything is freed, rather than at process exit. None without an arena."""
+    try:
+        f = ctypes.CDLL(None).gpushare_shim_arena_release
+    except AttributeError:
+        return None
+    f.restype = ctypes.c_int
+    r = f()
+    return None if r == 0 else r == 1
+
+
 def main() -> int:
     import torch  # noqa: F401 - imported in standby: the expensive part of a process start
 
@@ -137,7 +149,7 @@ def main() -> int:
     torch.cuda.empty_cache()      # HBM back to the device now, not at process exit
     after = _shim_stats()
     _send({"event": "done", "gemms": gemms, "t": time.time(), "seconds": time.time() - t_start, "shim": st,
-           "used_after_release": (after or {}).get("used")})
+           "used_after_release": (after or {}).get("used"), "arena_released": _arena_release()})
     return 0
 
 

@@ -21,6 +21,7 @@ LIBS = {
     "hipshim": "libgpushare_hipquota.so",
     "dpserver": "libgpushare_dpserver.so",
     "kernels": "libgpushare_kernels.so",
+    "hbmbroker": "gpushare-hbm-broker",
 }
 
 _lock = threading.Lock()
@@ -39,7 +40,8 @@ def lib_path(target: str) -> str:
     return os.path.join(NATIVE_DIR, LIBS[target])
 
 
-SOURCES = {"gpuinfo": "gpuinfo", "hipshim": "hipshim", "dpserver": "dpserver", "kernels": "kernels"}   # native/<dir>
+SOURCES = {"gpuinfo": "gpuinfo", "hipshim": "hipshim", "dpserver": "dpserver", "kernels": "kernels",
+           "hbmbroker": "hbmbroker"}   # native/<dir>
 
 
 def stale(target: str, path: str) -> bool:

@@ -22,7 +22,10 @@ Scenario (one node with N = --gpus MI355X, one rank per GPU, rank 0 also hosts t
     kubelet through the plugin's Allocate, and its process starts under the shim and runs its
     first GEMM ("pod ready"). The interpreter of the replacement is pre-started (standby: torch
     imported, GPU untouched — an image already pulled); HIP init, quota, HBM allocation and the
-    first GEMM are inside the timed step. Each GPU cycles independently (rank 0 serves the
+    first GEMM are inside the timed step. By default pods take their HBM from the GPU's HBM
+    broker (native/hbmbroker, docs/HBM_TURNOVER.md): VMM granules lent per pod and scrubbed
+    between pods, so an admission does not wait for amdgpu's wipe of the retired pod's HBM
+    (--no-hbm-broker: fresh driver allocations, the wipe-bound path). Each GPU cycles independently (rank 0 serves the
     admissions, serialised like one kubelet); per-GPU work is fixed (1 admission per step), so
     scaling is weak.
 ``value`` = pods admitted-to-ready per second for the whole node (higher is better). Also in the
@@ -64,7 +67,9 @@ def parse():
     ap.add_argument("--burst", type=int, default=8, help="GEMMs between a pod process's control checks")
     ap.add_argument("--gemm", type=int, default=4096, help="GEMM M=N=K")
     ap.add_argument("--fill", type=float, default=0.85, help="fraction of its quota a pod process holds")
-    ap.add_argument("--standby", type=int, default=2, help="pre-started pod interpreters per GPU")
+    ap.add_argument("--standby", type=int, default=6,
+                    help="pre-started pod interpreters per GPU (images pulled, processes created, torch imported; "
+                         "each takes ~1.5 s of CPU, so the pool must cover the admission rate)")
     ap.add_argument("--no-gpu", action="store_true", help="control plane only (CPU)")
     ap.add_argument("--smi-backend", default=None, help="default: auto on GPU, fake:Nx288G on CPU")
     ap.add_argument("--pod-source", default="watch", choices=("watch", "list", "kubelet"))
@@ -79,6 +84,12 @@ def parse():
                          "all pods queued first, placed jointly ('' = off)")
     ap.add_argument("--room-slack-gib", type=float, default=2.0,
                     help="free HBM beyond a pod's state required before it allocates")
+    ap.add_argument("--hbm-broker", action=argparse.BooleanOptionalAction, default=True,
+                    help="pods take their HBM from a per-GPU broker (native/hbmbroker) instead of fresh driver "
+                         "allocations: no wait for amdgpu's wipe of a retired pod's HBM (--no-hbm-broker: the "
+                         "driver path; if the broker cannot start, the run falls back to it and says why)")
+    ap.add_argument("--hbm-broker-reserve-gib", type=float, default=16.0,
+                    help="HBM the broker leaves to the driver (runtimes' own allocations)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -556,8 +567,9 @@ class PodFleet:
     imported, GPU untouched) that becomes the next admitted pod."""
 
     def __init__(self, local: int, gemm: int, burst: int, fill: float, visible_by_uuid: bool, standby: int = 2,
-                 slack: int = 2 << 30, ordinal: int | None = None):
+                 slack: int = 2 << 30, ordinal: int | None = None, broker=None):
         self.local, self.gemm, self.burst, self.fill, self.slack = local, gemm, burst, fill, slack
+        self.broker = broker                  # HBMBroker: pods' HBM comes from it (no driver wipe on the path)
         self.ordinal = local if ordinal is None else ordinal     # this GPU's HIP ordinal (bind_device)
         self.visible_by_uuid = visible_by_uuid
         self.pods: dict[str, dict] = {}       # uid -> {"proc", "q", "size", "ready"}
@@ -575,6 +587,8 @@ class PodFleet:
         self.phase_ms: dict[str, list] = {"stop": [], "init": [], "room": [], "alloc": [], "hold": []}
         self.trace: list | None = [] if os.environ.get("GS_BENCH_POD_TRACE") else None
         self._vram_used, self._vram_total = self._vram_reader()
+        if broker is not None:
+            self._vram_used = None            # the broker's TAKE waits for the granules, not for the driver
         for _ in range(max(1, standby)):
             self._spawn()
 
@@ -641,6 +655,16 @@ class PodFleet:
             env["HIP_VISIBLE_DEVICES"] = str(self.ordinal)
         from aliyun_gpushare_device_plugin_amd import const
 
+        if self.broker is not None:
+            # the granter's part (the plugin's Allocate in a deployment): the pod's state + its
+            # GEMM working set + 1 GiB for the caching allocator's rounding, under a one-time token
+            from aliyun_gpushare_device_plugin_amd.quota import hbmbroker
+
+            token = hbmbroker.new_token()
+            quota = int(env.get(const.ENV_SHIM_QUOTA_BYTES, 0))
+            self.broker.grant(token, int(quota * self.fill) + 3 * self.gemm ** 2 * 2 + (1 << 30))
+            env[hbmbroker.ENV_SOCKET] = self.broker.socket_path
+            env[hbmbroker.ENV_TOKEN] = token
         t0 = time.perf_counter()
         w["proc"].stdin.write(json.dumps({"cmd": "start", "env": env, "gemm": self.gemm, "burst": self.burst,
                                           "fill": self.fill, "two_phase": True}) + "\n")
@@ -819,9 +843,22 @@ def main():
         info = {"units_per_gpu": cp.units_per_gpu, "gpu_count": cp.gpu_count}
     info = bcast(info)
     units = info["units_per_gpu"]
+    broker = None
+    broker_error = None
+    if use_gpu and a.hbm_broker:
+        from aliyun_gpushare_device_plugin_amd.quota.hbmbroker import HBMBroker
+
+        broker = HBMBroker(os.path.join(workdir, f"hbm{local}.sock"), device=ordinal,
+                           reserve_gib=a.hbm_broker_reserve_gib)
+        try:
+            broker.start()
+        except Exception as e:  # noqa: BLE001 - reported in the line; the churn runs on the driver path
+            broker_error = f"{type(e).__name__}: {e}"[:500]
+            sys.stderr.write(f"bench: hbm broker unavailable, pods allocate from the driver: {broker_error}\n")
+            broker = None
     # pod processes see their GPU through the Allocate response's ROCR_VISIBLE_DEVICES (UUID)
     fleet = PodFleet(local, a.gemm, a.burst, a.fill, not smi.startswith("fake:"), a.standby,
-                     slack=int(a.room_slack_gib * (1 << 30)), ordinal=ordinal) if use_gpu else None
+                     slack=int(a.room_slack_gib * (1 << 30)), ordinal=ordinal, broker=broker) if use_gpu else None
     topo_report = cp_topo = None
     topo_failed = False
     problems: list = []
@@ -1013,7 +1050,8 @@ def main():
             "config": {"model": "gpushare-device-plugin + MFMA GEMM pods (BASELINE config 3 churn)",
                        "global_batch": 4 * n, "seq_len": None, "parallelism": f"node{n}",
                        "pods_per_gpu": 4, "gemm_mnk": a.gemm, "pod_fill": a.fill, "pod_source": a.pod_source,
-                       "smi_backend": smi, "pod_processes": use_gpu,
+                       "smi_backend": smi, "pod_processes": use_gpu, "hbm_broker": broker is not None,
+                       "standby_interpreters_per_gpu": a.standby,
                        # the plugin's gRPC server and the simulated kubelet's Allocate client
                        "grpc_server": "native" if native_server.available() else "python",
                        "kubelet_client": "native" if NativeUnaryClient.wanted() else "grpcio"},
@@ -1067,6 +1105,10 @@ def main():
             # bytes-weighted over the retirements: sum(bytes held) / sum(stop -> GPU has room again)
             "amdgpu_release_GBps": round(sum(b for b, _ in rel) / sum(t for _, t in rel) / 1e9, 1) if rel else None,
         }
+        # pods' HBM from the per-GPU broker (--hbm-broker): rank 0's broker counters
+        res["hbm_broker"] = broker.stat() if broker is not None else None
+        if broker_error:
+            res["hbm_broker_error"] = broker_error
         if topo_report is not None:
             res["topology"] = topo_report
             if use_gpu:
@@ -1090,6 +1132,8 @@ def main():
             with open(f"{os.environ['GS_BENCH_POD_TRACE']}.{rank}", "w") as f:
                 f.writelines(json.dumps(r) + "\n" for r in fleet.trace)
         fleet.close()
+    if broker is not None:
+        broker.stop()
     if client is not None:
         client.close()
     if world > 1:

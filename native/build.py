@@ -5,6 +5,7 @@ Targets
   gpuinfo   libgpushare_gpuinfo.so + gpushare-smi (C++17, host only; librocm_smi64 is dlopen'ed)
   hipshim   libgpushare_hipquota.so  (C++17 LD_PRELOAD interposer over the HIP allocation API)
   dpserver  libgpushare_dpserver.so  (C++17 DevicePlugin gRPC server over libnghttp2, native Allocate fast path)
+  hbmbroker gpushare-hbm-broker     (C++17 per-GPU HBM broker daemon over HIP VMM, host only)
   kernels   libgpushare_kernels.so   (hand-written HIP/CDNA4 kernels, hipcc --offload-arch=gfx950)
   probes    shim_probe               (HIP test helper run under the quota shim on hardware)
 
@@ -150,6 +151,25 @@ def build_dpserver(force=False, asan=False):
     return [lib]
 
 
+def build_hbmbroker(force=False, asan=False):
+    """gpushare-hbm-broker: lends each pod VMM granules of HBM it holds, scrubbed between pods
+    (docs/HBM_TURNOVER.md). Host code only: the scrub is hipMemsetAsync."""
+    src = _src("hbmbroker", "hbmbroker.cpp")
+    if not os.path.exists(src):
+        return []
+    exe = os.path.join(OUT, "gpushare-hbm-broker")
+    flags = ["-std=c++17", "-O2", "-Wall", "-Wextra", "-Wno-unused-parameter", "-D__HIP_PLATFORM_AMD__",
+             f"-I{ROCM}/include"]
+    san = _san(asan)
+    if san:
+        flags += SANITIZERS[san]
+        exe = os.path.join(OUT, san, "gpushare-hbm-broker")
+    os.makedirs(os.path.dirname(exe), exist_ok=True)
+    if force or _newer(exe, [src]):
+        _run([CXX, *flags, "-o", exe, src, f"-L{ROCM}/lib", "-lamdhip64", f"-Wl,-rpath,{ROCM}/lib", "-pthread"])
+    return [exe]
+
+
 def build_kernels(force=False, asan=False, jobs=4):
     d = _src("kernels")
     srcs = sorted(os.path.join(d, f) for f in os.listdir(d) if f.endswith(".hip")) if os.path.isdir(d) else []
@@ -193,7 +213,8 @@ def build_probes(force=False, asan=False):
     return out
 
 
-TARGETS = {"gpuinfo": build_gpuinfo, "hipshim": build_hipshim, "dpserver": build_dpserver, "kernels": build_kernels,
+TARGETS = {"gpuinfo": build_gpuinfo, "hipshim": build_hipshim, "dpserver": build_dpserver,
+           "hbmbroker": build_hbmbroker, "kernels": build_kernels,
            "probes": build_probes}
 
 

@@ -74,6 +74,8 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/mman.h>
+#include <sys/socket.h>
+#include <sys/un.h>
 #include <sys/stat.h>
 #include <sys/syscall.h>
 #include <sys/sysmacros.h>
@@ -1055,11 +1057,350 @@ GS_EXPORT int close(int fd) {
   return f ? f(fd) : (errno = ENOSYS, -1);
 }
 
+// ---- HBM broker arena ------------------------------------------------------------------------
+// GPUSHARE_HBM_BROKER=<socket> + GPUSHARE_HBM_TOKEN=<token>: the pod's HBM comes from the node's
+// HBM broker (native/hbmbroker) instead of fresh driver allocations, so it never waits for
+// amdgpu's wipe of a retired pod's memory. At the first hipMalloc the shim takes its grant (the
+// fds of its granules, and only those), imports and maps them contiguously, and serves
+// hipMalloc/hipFree from that range. The broker connection stays open for the process lifetime:
+// its end returns the granules (scrubbed) to the broker. gpushare_shim_arena_release() hands them
+// back early, once nothing in the arena is live.
+namespace {
+REAL(hipError_t, hipMemImportFromShareableHandle, hipMemGenericAllocationHandle_t*, void*,
+     hipMemAllocationHandleType)
+REAL(hipError_t, hipMemAddressReserve, void**, size_t, size_t, void*, unsigned long long)
+REAL(hipError_t, hipMemAddressFree, void*, size_t)
+REAL(hipError_t, hipMemMap, void*, size_t, size_t, hipMemGenericAllocationHandle_t, unsigned long long)
+REAL(hipError_t, hipMemUnmap, void*, size_t)
+REAL(hipError_t, hipMemSetAccess, void*, size_t, const hipMemAccessDesc*, size_t)
+REAL(hipError_t, hipGetDevice, int*)
+REAL(hipError_t, hipDeviceSynchronize)
+
+constexpr int kArenaMaxGranules = 1024;
+constexpr int kArenaMaxExt = 1 << 16;     // free extents
+constexpr int kArenaLiveCap = 1 << 17;    // live allocations (open addressing, power of two)
+
+struct Ext {
+  uint64_t off, len;
+};
+struct Live {
+  uint64_t off1;  // offset + 1 (0 = empty slot)
+  uint64_t len;
+  bool tomb;
+};
+
+struct Arena {
+  pthread_mutex_t mu = PTHREAD_MUTEX_INITIALIZER;
+  std::atomic<int> state{0};  // 0 untried, 1 active, -1 off (no broker configured, failed or released)
+  int sock = -1;
+  char* base = nullptr;
+  uint64_t size = 0, gran = 0, used = 0;
+  int n = 0;
+  hipMemGenericAllocationHandle_t h[kArenaMaxGranules];
+  Ext* ext = nullptr;
+  int next = 0;
+  Live* live = nullptr;
+  uint64_t nlive = 0;
+};
+Arena g_arena;
+
+bool arena_configured() {
+  static std::atomic<int> c{-1};
+  int v = c.load(std::memory_order_relaxed);
+  if (v < 0) {
+    v = getenv("GPUSHARE_HBM_BROKER") && getenv("GPUSHARE_HBM_TOKEN") ? 1 : 0;
+    c.store(v, std::memory_order_relaxed);
+  }
+  return v == 1;
+}
+
+bool recv_line(int s, char* buf, size_t cap) {
+  size_t i = 0;
+  while (i + 1 < cap) {
+    char ch;
+    ssize_t r = recv(s, &ch, 1, 0);
+    if (r <= 0) return false;
+    if (ch == '\n') break;
+    buf[i++] = ch;
+  }
+  buf[i] = 0;
+  return true;
+}
+
+// fds of one SCM_RIGHTS message into out[*got...]
+bool recv_fd_batch(int s, int* out, int* got, int want) {
+  char byte;
+  iovec io{&byte, 1};
+  alignas(cmsghdr) char ctl[CMSG_SPACE(200 * sizeof(int))];
+  msghdr m;
+  memset(&m, 0, sizeof m);
+  m.msg_iov = &io;
+  m.msg_iovlen = 1;
+  m.msg_control = ctl;
+  m.msg_controllen = sizeof ctl;
+  if (recvmsg(s, &m, MSG_CMSG_CLOEXEC) != 1) return false;
+  cmsghdr* c = CMSG_FIRSTHDR(&m);
+  if (!c || c->cmsg_level != SOL_SOCKET || c->cmsg_type != SCM_RIGHTS) return false;
+  int k = int((c->cmsg_len - CMSG_LEN(0)) / sizeof(int));
+  const int* p = reinterpret_cast<const int*>(CMSG_DATA(c));
+  for (int i = 0; i < k; ++i) {
+    if (*got < want) out[(*got)++] = p[i];
+    else close(p[i]);
+  }
+  return true;
+}
+
+// called with g_arena.mu held, at the first allocation
+void arena_take() {
+  Arena& a = g_arena;
+  a.state.store(-1, std::memory_order_relaxed);
+  const char* path = getenv("GPUSHARE_HBM_BROKER");
+  const char* tok = getenv("GPUSHARE_HBM_TOKEN");
+  int s = socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  sockaddr_un sa;
+  memset(&sa, 0, sizeof sa);
+  sa.sun_family = AF_UNIX;
+  snprintf(sa.sun_path, sizeof sa.sun_path, "%s", path);
+  char line[256];
+  int fds[kArenaMaxGranules];
+  int got = 0;
+  unsigned long long want = 0, gran = 0;
+  int dev = 0;
+  auto import_f = real_hipMemImportFromShareableHandle();
+  auto reserve_f = real_hipMemAddressReserve();
+  auto map_f = real_hipMemMap();
+  auto access_f = real_hipMemSetAccess();
+  auto getdev_f = real_hipGetDevice();
+  if (s < 0 || !import_f || !reserve_f || !map_f || !access_f || !getdev_f) goto fail;
+  if (connect(s, reinterpret_cast<sockaddr*>(&sa), sizeof sa) != 0) goto fail;
+  {
+    int n = snprintf(line, sizeof line, "TAKE %s\n", tok);
+    if (send(s, line, n, MSG_NOSIGNAL) != n) goto fail;
+  }
+  if (!recv_line(s, line, sizeof line) || sscanf(line, "FDS %llu %llu", &want, &gran) != 2 || want == 0 ||
+      want > (unsigned long long)kArenaMaxGranules || gran == 0) {
+    logf(1, "hbm broker %s refused the grant: %s", path, line);
+    goto fail;
+  }
+  while (got < (int)want)
+    if (!recv_fd_batch(s, fds, &got, (int)want)) goto fail;
+  logf(2, "hbm broker: %d fds of %llu bytes received", got, gran);
+  {
+    Depth d;
+    if (getdev_f(&dev) != hipSuccess) goto fail;
+    void* base = nullptr;
+    uint64_t size = want * gran;
+    if (reserve_f(&base, size, 0, nullptr, 0) != hipSuccess) goto fail;
+    logf(2, "hbm broker: reserved %p + %llu", base, (unsigned long long)size);
+    for (int i = 0; i < got; ++i) {
+      logf(2, "hbm broker: import granule %d (fd %d)", i, fds[i]);
+      // The HIP 7.0 runtime (PyTorch's) reads the fd through the pointer, dies on a bare fd; the
+      // 7.2 runtime takes the fd as the pointer's value and refuses an address (invalid value).
+      hipError_t ie = import_f(&a.h[i], &fds[i], hipMemHandleTypePosixFileDescriptor);
+      if (ie == hipErrorInvalidValue)
+        ie = import_f(&a.h[i], reinterpret_cast<void*>(static_cast<intptr_t>(fds[i])),
+                      hipMemHandleTypePosixFileDescriptor);
+      if (ie != hipSuccess ||
+          map_f(static_cast<char*>(base) + uint64_t(i) * gran, gran, 0, a.h[i], 0) != hipSuccess) {
+        logf(1, "hbm broker: import/map of granule %d failed", i);
+        goto fail;  // the process keeps what it mapped until exit; the broker reclaims at close
+      }
+      logf(2, "hbm broker: mapped granule %d", i);
+      close(fds[i]);
+      fds[i] = -1;
+      a.n = i + 1;
+    }
+    hipMemAccessDesc acc;
+    memset(&acc, 0, sizeof acc);
+    acc.location.type = hipMemLocationTypeDevice;
+    acc.location.id = dev;
+    acc.flags = hipMemAccessFlagsProtReadWrite;
+    if (access_f(base, size, &acc, 1) != hipSuccess) goto fail;
+    a.base = static_cast<char*>(base);
+    a.size = size;
+    a.gran = gran;
+  }
+  a.ext = static_cast<Ext*>(calloc(kArenaMaxExt, sizeof(Ext)));
+  a.live = static_cast<Live*>(calloc(kArenaLiveCap, sizeof(Live)));
+  if (!a.ext || !a.live) goto fail;
+  a.ext[0] = {0, a.size};
+  a.next = 1;
+  a.sock = s;
+  a.state.store(1, std::memory_order_release);  // base/size published before the state
+  logf(1, "hbm broker: %d granules of %llu bytes mapped at %p", a.n, gran, a.base);
+  return;
+fail:
+  for (int i = 0; i < got; ++i)
+    if (fds[i] >= 0) close(fds[i]);
+  if (s >= 0) close(s);
+}
+
+uint64_t live_slot(uint64_t off) { return (off * 0x9E3779B97F4A7C15ull >> 20) & (kArenaLiveCap - 1); }
+
+bool live_put(uint64_t off, uint64_t len) {
+  Arena& a = g_arena;
+  if (a.nlive * 2 >= kArenaLiveCap) return false;
+  for (uint64_t i = live_slot(off);; i = (i + 1) & (kArenaLiveCap - 1))
+    if (!a.live[i].off1) {
+      a.live[i] = {off + 1, len, false};
+      ++a.nlive;
+      return true;
+    }
+}
+
+bool live_take(uint64_t off, uint64_t* len) {
+  Arena& a = g_arena;
+  for (uint64_t i = live_slot(off);; i = (i + 1) & (kArenaLiveCap - 1)) {
+    Live& l = a.live[i];
+    if (!l.off1 && !l.tomb) return false;
+    if (l.off1 == off + 1) {
+      *len = l.len;
+      l.off1 = 0;
+      l.tomb = true;
+      --a.nlive;
+      return true;
+    }
+  }
+}
+
+// first fit; large blocks on 2 MiB boundaries (the CDNA4 TLB fragment), small ones on 4 KiB
+bool arena_alloc(uint64_t size, void** ptr) {
+  Arena& a = g_arena;
+  uint64_t align = size >= (2ull << 20) ? (2ull << 20) : 4096;
+  uint64_t len = (size + 4095) & ~uint64_t(4095);
+  for (int i = 0; i < a.next; ++i) {
+    Ext e = a.ext[i];
+    uint64_t start = (e.off + align - 1) & ~(align - 1);
+    if (start + len > e.off + e.len) continue;
+    uint64_t head = start - e.off, tail = e.off + e.len - (start + len);
+    if (head && tail && a.next >= kArenaMaxExt) return false;
+    if (!live_put(start, len)) return false;
+    if (head && tail) {  // split in two: shift the rest up by one
+      memmove(&a.ext[i + 2], &a.ext[i + 1], sizeof(Ext) * (a.next - i - 1));
+      a.ext[i] = {e.off, head};
+      a.ext[i + 1] = {start + len, tail};
+      ++a.next;
+    } else if (head) {
+      a.ext[i] = {e.off, head};
+    } else if (tail) {
+      a.ext[i] = {start + len, tail};
+    } else {
+      memmove(&a.ext[i], &a.ext[i + 1], sizeof(Ext) * (a.next - i - 1));
+      --a.next;
+    }
+    a.used += len;
+    *ptr = a.base + start;
+    return true;
+  }
+  return false;
+}
+
+void arena_free(uint64_t off) {
+  Arena& a = g_arena;
+  uint64_t len = 0;
+  if (!live_take(off, &len)) return;
+  a.used -= len;
+  int lo = 0, hi = a.next;  // first extent after off
+  while (lo < hi) {
+    int mid = (lo + hi) / 2;
+    if (a.ext[mid].off < off) lo = mid + 1;
+    else hi = mid;
+  }
+  bool join_prev = lo > 0 && a.ext[lo - 1].off + a.ext[lo - 1].len == off;
+  bool join_next = lo < a.next && off + len == a.ext[lo].off;
+  if (join_prev && join_next) {
+    a.ext[lo - 1].len += len + a.ext[lo].len;
+    memmove(&a.ext[lo], &a.ext[lo + 1], sizeof(Ext) * (a.next - lo - 1));
+    --a.next;
+  } else if (join_prev) {
+    a.ext[lo - 1].len += len;
+  } else if (join_next) {
+    a.ext[lo].off = off;
+    a.ext[lo].len += len;
+  } else if (a.next < kArenaMaxExt) {
+    memmove(&a.ext[lo + 1], &a.ext[lo], sizeof(Ext) * (a.next - lo));
+    a.ext[lo] = {off, len};
+    ++a.next;
+  }  // else: the extent list is full and these bytes stay unusable until release (never seen)
+}
+
+// 1: served from the arena (*e set), 0: not the arena's (pass through)
+int arena_try_alloc(void** ptr, size_t size, hipError_t* e) {
+  if (!arena_configured() || size == 0 || t_depth) return 0;
+  Arena& a = g_arena;
+  pthread_mutex_lock(&a.mu);
+  if (a.state == 0) arena_take();
+  if (a.state != 1) {
+    pthread_mutex_unlock(&a.mu);
+    return 0;
+  }
+  bool ok = arena_alloc(size, ptr);
+  pthread_mutex_unlock(&a.mu);
+  if (!ok) {
+    if (ptr) *ptr = nullptr;
+    logf(1, "hbm broker arena: deny %zu bytes (used %llu of %llu)", size, (unsigned long long)a.used,
+         (unsigned long long)a.size);
+    *e = hipErrorOutOfMemory;
+  } else {
+    *e = hipSuccess;
+  }
+  return 1;
+}
+
+bool arena_owns(void* p) {
+  Arena& a = g_arena;
+  return a.state.load(std::memory_order_acquire) == 1 && static_cast<char*>(p) >= a.base &&
+         static_cast<char*>(p) < a.base + a.size;
+}
+}  // namespace
+
 // ---- interposed HIP API --------------------------------------------------------------------
 GS_EXPORT hipError_t hipMalloc(void** ptr, size_t size) {
   auto f = real_hipMalloc();
   if (!f) return hipErrorNotInitialized;
+  hipError_t ae;
+  if (arena_try_alloc(ptr, size, &ae)) return ae;
   return guarded_alloc(ptr, size, [&] { return f(ptr, size); });
+}
+
+// Hand the arena back to the broker now (the pod is retiring and freed everything). Returns 1 if
+// released, 0 if there is no arena, -1 if allocations are still live in it.
+GS_EXPORT int gpushare_shim_arena_release() {
+  Arena& a = g_arena;
+  pthread_mutex_lock(&a.mu);
+  if (a.state != 1) {
+    pthread_mutex_unlock(&a.mu);
+    return 0;
+  }
+  if (a.nlive) {
+    pthread_mutex_unlock(&a.mu);
+    return -1;
+  }
+  {
+    Depth d;
+    if (auto dev_sync = real_hipDeviceSynchronize()) (void)dev_sync();
+    if (auto un = real_hipMemUnmap()) (void)un(a.base, a.size);
+    if (auto rel = real_hipMemRelease())
+      for (int i = 0; i < a.n; ++i) (void)rel(a.h[i]);
+    if (auto fr = real_hipMemAddressFree()) (void)fr(a.base, a.size);
+  }
+  close(a.sock);
+  a.sock = -1;
+  a.state.store(-1, std::memory_order_release);
+  a.n = 0;
+  pthread_mutex_unlock(&a.mu);
+  return 1;
+}
+
+// (size, used) of the arena; 0 when there is none
+GS_EXPORT int gpushare_shim_arena_stats(uint64_t* size, uint64_t* used) {
+  Arena& a = g_arena;
+  pthread_mutex_lock(&a.mu);
+  int on = a.state == 1;
+  if (size) *size = on ? a.size : 0;
+  if (used) *used = on ? a.used : 0;
+  pthread_mutex_unlock(&a.mu);
+  return on;
 }
 
 GS_EXPORT hipError_t hipExtMallocWithFlags(void** ptr, size_t size, unsigned int flags) {
@@ -1131,6 +1472,16 @@ GS_EXPORT hipError_t hipMalloc3D(hipPitchedPtr* pp, hipExtent ext) {
 GS_EXPORT hipError_t hipFree(void* ptr) {
   auto f = real_hipFree();
   if (!f) return hipErrorNotInitialized;
+  if (ptr && arena_configured() && arena_owns(ptr)) {
+    // the caching allocator frees after its streams' work; a plain hipFree synchronises the
+    // device first, so do the same before the range can be handed out again
+    Depth d;
+    if (auto dev_sync = real_hipDeviceSynchronize()) (void)dev_sync();
+    pthread_mutex_lock(&g_arena.mu);
+    arena_free(uint64_t(static_cast<char*>(ptr) - g_arena.base));
+    pthread_mutex_unlock(&g_arena.mu);
+    return hipSuccess;
+  }
   if (!hip_active() || !ptr) return f(ptr);
   hipError_t e;
   {
@@ -1203,6 +1554,9 @@ GS_EXPORT hipError_t hipMemGetInfo(size_t* free_b, size_t* total_b) {
   uint64_t left = used >= quota ? 0 : quota - used;
   if (free_b && *free_b > left) *free_b = (size_t)left;
   if (total_b) *total_b = (size_t)quota;
+  uint64_t asz = 0, aused = 0;
+  if (free_b && arena_configured() && gpushare_shim_arena_stats(&asz, &aused) && *free_b > asz - aused)
+    *free_b = (size_t)(asz - aused);  // with a broker arena, what the pod can still get is the arena's rest
   return e;
 }
 

@@ -140,6 +140,31 @@ static void runtime_init(void) {
 hipError_t hipMemGetInfo(size_t* f, size_t* t) { runtime_init(); *f = g_total - __atomic_load_n(&g_used, __ATOMIC_ACQUIRE); *t = g_total; return 0; }
 hipError_t hipDeviceTotalMem(size_t* b, int d) { *b = g_total; return 0; }
 hipError_t hipMemCreate(uint64_t* h, size_t n, const void* prop, unsigned long long fl) { return kfd(n, h); }
-hipError_t hipMemRelease(uint64_t h) { kfd_release(h); return 0; }
+hipError_t hipMemRelease_imported(uint64_t h);
+hipError_t hipMemRelease(uint64_t h) { if (h & (1ull << 62)) return hipMemRelease_imported(h); kfd_release(h); return 0; }
 /* what ROCr does for a scratch-heavy dispatch: VRAM taken inside the runtime, no HIP call */
 int fake_runtime_scratch(size_t n) { uint64_t h; return kfd(n, &h); }
+/* HIP VMM for the shim's HBM-broker arena: imported handles keep a dup of the broker's fd (the
+   high bit marks them); the address range is a host reservation. Import follows the 7.2
+   runtime: the fd is the pointer's value, and an address (a pointer to the fd) is refused
+   with hipErrorInvalidValue. */
+#define IMPORTED (1ull << 62)
+hipError_t hipMemImportFromShareableHandle(uint64_t* h, void* os, int type) {
+  uintptr_t fd = (uintptr_t)os;
+  if (fd > (1u << 20)) return 1;                     /* hipErrorInvalidValue */
+  int d = dup((int)fd);
+  if (d < 0) return 1;
+  *h = IMPORTED | (uint64_t)d; return 0;
+}
+hipError_t hipMemRelease_imported(uint64_t h) { close((int)(h & 0xffffffff)); return 0; }
+hipError_t hipMemAddressReserve(void** p, size_t n, size_t al, void* addr, unsigned long long fl) {
+  void* m = mmap(0, n, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+  if (m == MAP_FAILED) return 2;
+  *p = m; return 0;
+}
+hipError_t hipMemAddressFree(void* p, size_t n) { munmap(p, n); return 0; }
+hipError_t hipMemMap(void* p, size_t n, size_t off, uint64_t h, unsigned long long fl) { return (h & IMPORTED) ? 0 : 1; }
+hipError_t hipMemUnmap(void* p, size_t n) { return 0; }
+hipError_t hipMemSetAccess(void* p, size_t n, const void* d, size_t c) { return 0; }
+hipError_t hipGetDevice(int* d) { *d = 0; return 0; }
+hipError_t hipDeviceSynchronize(void) { return 0; }

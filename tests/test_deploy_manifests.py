@@ -141,6 +141,7 @@ def test_dockerfile_recipe_builds_and_installs(tmp_path):
     assert (native / "libgpushare_gpuinfo.so").exists() and (native / "libgpushare_hipquota.so").exists()
     assert (native / "gpushare-smi").exists()
     assert (native / "libgpushare_dpserver.so").exists()       # the native DevicePlugin server
+    assert (native / "gpushare-hbm-broker").exists()           # the per-GPU HBM broker
     site = tmp_path / "site"
     r = subprocess.run([sys.executable, "-m", "pip", "install", "--no-deps", "--no-build-isolation", "--no-index",
                         "--target", str(site), str(src)], capture_output=True, text=True, timeout=600)

@@ -1,0 +1,115 @@
+"""The per-GPU HBM broker (native/hbmbroker) and the quota shim's broker arena, on MI355X.
+
+A pod under the shim with ``GPUSHARE_HBM_BROKER``/``GPUSHARE_HBM_TOKEN`` takes its granted
+granules at its first allocation and serves every ``hipMalloc`` from them. Checked here:
+the next pod sees only zeros (the broker scrubbed), a pod waits for granules a retiring pod still
+holds instead of failing, and a pod with an unknown token gets no arena.
+"""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+import time
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+GIB = 1 << 30
+
+TENANT = r"""
+import ctypes, faulthandler, json, sys, time
+faulthandler.enable()
+import torch
+mode = sys.argv[1]
+t0 = time.perf_counter()
+x = torch.empty(5 * (1 << 30), dtype=torch.uint8, device="cuda")      # inside the arena
+t1 = time.perf_counter()
+lib = ctypes.CDLL(None)
+size, used = ctypes.c_uint64(), ctypes.c_uint64()
+on = lib.gpushare_shim_arena_stats(ctypes.byref(size), ctypes.byref(used))
+out = {"arena": on, "arena_size": size.value, "arena_used": used.value, "alloc_ms": (t1 - t0) * 1e3,
+       "free_total": list(torch.cuda.mem_get_info())}
+if mode == "check":
+    out["nonzero"] = int(x.max().item())                               # a reduction: no full-size temporary
+x.fill_(7)
+torch.cuda.synchronize()
+if mode == "hold":
+    print(json.dumps(out), flush=True)
+    sys.stdin.readline()                                               # hold until told to exit
+else:
+    print(json.dumps(out), flush=True)
+"""
+
+
+@pytest.fixture
+def broker(tmp_path):
+    from aliyun_gpushare_device_plugin_amd.quota.hbmbroker import HBMBroker
+
+    b = HBMBroker(str(tmp_path / "hbm.sock"), device=0, gib=8, wait_s=20)
+    b.start()
+    yield b
+    b.stop()
+
+
+def _tenant(broker, token, mode, **kw):
+    from aliyun_gpushare_device_plugin_amd.utils.native import ensure_built
+
+    env = dict(os.environ, LD_PRELOAD=ensure_built("hipshim"), GPUSHARE_QUOTA_BYTES=str(8 * GIB),
+               GPUSHARE_HBM_BROKER=broker.socket_path, GPUSHARE_HBM_TOKEN=token, GPUSHARE_SHIM_LOG="1",
+               PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    return subprocess.Popen([sys.executable, "-c", TENANT, mode], env=env, stdin=subprocess.PIPE,
+                            stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, **kw)
+
+
+def _result(p, timeout=120):
+    out, err = p.communicate(timeout=timeout)
+    assert p.returncode == 0, err[-3000:]
+    return json.loads(out.strip().splitlines()[-1])
+
+
+def test_the_next_pod_sees_only_zeros(broker):
+    assert broker.grant("a" * 32, 6 * GIB) == 6
+    a = _result(_tenant(broker, "a" * 32, "write"))
+    assert a["arena"] == 1 and a["arena_size"] == 6 * GIB and a["arena_used"] >= 5 * GIB
+    # what the pod sees as free is the arena's rest, under a total of its quota
+    assert a["free_total"][1] == 8 * GIB and a["free_total"][0] <= GIB
+    assert broker.grant("b" * 32, 6 * GIB) == 6
+    b = _result(_tenant(broker, "b" * 32, "check"))
+    assert b["arena"] == 1 and b["nonzero"] == 0
+    st = broker.stat()
+    assert st["takes"] == 2 and st["releases"] == 2 and st["free"] == st["granules"]
+    assert st["scrubbed_bytes"] >= 12 * GIB
+
+
+def test_a_pod_waits_for_granules_a_retiring_pod_holds(broker):
+    broker.grant("c" * 32, 6 * GIB)
+    holder = _tenant(broker, "c" * 32, "hold")
+    first = json.loads(holder.stdout.readline())
+    assert first["arena"] == 1
+    broker.grant("d" * 32, 6 * GIB)                       # 6 + 6 > 8: must wait for the holder
+    waiter = _tenant(broker, "d" * 32, "check")
+    time.sleep(3.0)
+    assert waiter.poll() is None and broker.stat()["waiting"] == 1
+    holder.stdin.write("\n")
+    holder.stdin.flush()
+    holder.wait(60)
+    r = _result(waiter)
+    assert r["arena"] == 1 and r["nonzero"] == 0
+
+
+def test_an_unknown_token_gets_no_arena(tmp_path):
+    from aliyun_gpushare_device_plugin_amd.quota.hbmbroker import HBMBroker
+
+    b = HBMBroker(str(tmp_path / "hbm.sock"), device=0, gib=4, wait_s=1)
+    b.start()
+    try:
+        r = _result(_tenant(b, "never-granted", "write"))
+        assert r["arena"] == 0                           # refused: the pod's allocations go to the driver
+        assert b.stat()["timeouts"] == 1
+    finally:
+        b.stop()

@@ -449,3 +449,122 @@ def test_prime_export_of_charged_vram_is_refused(stub, native_shim, tmp_path):
     st = [o for o in out if o["op"] == "stats"]
     assert pr[0]["err"] == 0 and st[0]["used"] == GIB  # exported: GEM_CLOSE keeps the charge
     assert st[1]["used"] == 0                            # the DRM file closed: released
+
+
+class FakeBroker:
+    """The HBM broker's pod side (native/hbmbroker): answers one TAKE with ``granules`` fds, then
+    records when the pod's connection ends (its granules would be scrubbed and lent again)."""
+
+    def __init__(self, path, granules=4, gran=GIB, refuse=False):
+        import socket
+        import threading
+
+        self.granules, self.gran, self.refuse = granules, gran, refuse
+        self.took = None
+        self.closed_at = None
+        self.ls = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        self.ls.bind(path)
+        self.ls.listen(1)
+        threading.Thread(target=self._serve, daemon=True).start()
+
+    def _serve(self):
+        import socket
+        import time
+
+        conn, _ = self.ls.accept()
+        buf = b""
+        while not buf.endswith(b"\n"):
+            buf += conn.recv(1)
+        self.took = buf.decode().strip()
+        if self.refuse:
+            conn.sendall(b"ERR timeout\n")
+            conn.close()
+            return
+        fds = [os.open("/dev/null", os.O_RDONLY) for _ in range(self.granules)]
+        conn.sendall(f"FDS {self.granules} {self.gran}\n".encode())
+        socket.send_fds(conn, [b"f"], fds)
+        for fd in fds:
+            os.close(fd)
+        while conn.recv(1):
+            pass
+        self.closed_at = time.monotonic()
+        conn.close()
+
+
+def test_broker_arena_serves_hipmalloc_from_the_granted_granules(stub, native_shim, tmp_path):
+    """The pod's hipMalloc/hipFree come from its granted granules (first fit, coalescing), the
+    pod sees the arena's rest as free, nothing is charged at the KFD for them, and the arena is
+    handed back only once nothing in it is live; allocations after that go to the driver."""
+    import time
+
+    sock = str(tmp_path / "hbm.sock")
+    b = FakeBroker(sock, granules=4)
+    name = ledger()
+    try:
+        t0 = time.monotonic()
+        out, r = run(stub, native_shim, ["alloc", 3 * GIB, "alloc", 512 * MIB, "arena", "free", 0, "alloc", 2 * GIB,
+                                         "alloc", GIB, "alloc", GIB, "info", "stats", "arenarelease", "freeall",
+                                         "arenarelease", "arena", "sleep", 600, "alloc", MIB, "stats"],
+                     GPUSHARE_QUOTA_BYTES=8 * GIB, GPUSHARE_LEDGER=name, GPUSHARE_HBM_BROKER=sock,
+                     GPUSHARE_HBM_TOKEN="tok123")
+        t_end = time.monotonic()
+        assert r.returncode == 0, r.stderr
+        assert b.took == "TAKE tok123"
+        a3, b512, arena, _, c2, d1, e1, info, st, rel_live, _, rel, arena_after, late, st_after = out
+        assert a3["err"] == 0 and b512["err"] == 0
+        assert arena == {"op": "arena", "on": 1, "size": 4 * GIB, "used": 3 * GIB + 512 * MIB}
+        assert c2["err"] == 0 and c2["p"] == a3["p"]             # first fit reuses the freed range
+        assert d1["err"] == 0 and d1["p"] == a3["p"] + 2 * GIB   # coalesced rest of it
+        assert e1["err"] == 2                                    # 4 GiB arena full: out of memory
+        assert info["total"] == 8 * GIB and info["free"] == 512 * MIB
+        assert st["used"] == 0                                   # no KFD charge for broker granules
+        assert rel_live["r"] == -1 and rel["r"] == 1             # released only once nothing is live
+        assert arena_after["on"] == 0
+        assert b.closed_at is not None and b.closed_at < t_end - 0.4   # handed back before exit
+        assert late["err"] == 0 and st_after["used"] >= MIB      # afterwards: the driver, charged
+    finally:
+        cleanup(name)
+
+
+def test_broker_refusal_leaves_the_pod_on_the_driver(stub, native_shim, tmp_path):
+    sock = str(tmp_path / "hbm.sock")
+    b = FakeBroker(sock, refuse=True)
+    name = ledger()
+    try:
+        out, r = run(stub, native_shim, ["alloc", GIB, "arena", "stats"], GPUSHARE_QUOTA_BYTES=4 * GIB,
+                     GPUSHARE_LEDGER=name, GPUSHARE_HBM_BROKER=sock, GPUSHARE_HBM_TOKEN="nope")
+        assert r.returncode == 0, r.stderr
+        assert b.took == "TAKE nope"
+        assert out[0]["err"] == 0 and out[1]["on"] == 0 and out[2]["used"] == GIB   # quota shim as before
+    finally:
+        cleanup(name)
+
+
+@pytest.mark.parametrize("san", ["asan", "tsan"])
+def test_broker_arena_under_sanitizers(stub, tmp_path, san):
+    """8 threads allocating and freeing from the broker arena at once, under ASan+UBSan / TSan."""
+    import sys
+    sys.path.insert(0, os.path.join(HERE, "..", "native"))
+    import build as nb
+    lib = nb.build_hipshim(asan=san)[0]
+    rt = subprocess.run(["gcc", f"-print-file-name=lib{san}.so"], capture_output=True, text=True).stdout.strip()
+    if not os.path.exists(rt):
+        pytest.skip(f"lib{san}.so not installed")
+    d, drv = stub
+    sock = str(tmp_path / "hbm.sock")
+    b = FakeBroker(sock, granules=2)
+    name = ledger()
+    env = dict(os.environ, LD_PRELOAD=f"{rt}:{lib}", LD_LIBRARY_PATH=str(d), GPUSHARE_LEDGER=name,
+               GPUSHARE_QUOTA_BYTES=str(4 * GIB), GPUSHARE_HBM_BROKER=sock, GPUSHARE_HBM_TOKEN="t",
+               ASAN_OPTIONS="detect_leaks=0:halt_on_error=1", UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1",
+               TSAN_OPTIONS="halt_on_error=1:report_bugs=1")
+    try:
+        r = subprocess.run([str(drv), "threads", "8", "300", str(64 * MIB), "arena", "arenarelease"], env=env,
+                           capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr[-3000:]
+        out = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+        assert out[0]["ok"] == 8 * 300 and out[0]["denied"] == 0
+        assert out[1] == {"op": "arena", "on": 1, "size": 2 * GIB, "used": 0}
+        assert out[2]["r"] == 1 and b.took == "TAKE t"
+    finally:
+        cleanup(name)

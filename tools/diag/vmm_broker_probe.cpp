@@ -203,8 +203,14 @@ static int tenant(const char* path) {
   double t2 = now_ms();
   size_t total = gran * fds.size();
   std::vector<hipMemGenericAllocationHandle_t> h(fds.size());
+  // VMM_IMPORT_BY_PTR=1: pass the address of the fd (what some HIP releases dereference)
+  const bool by_ptr = getenv("VMM_IMPORT_BY_PTR") && getenv("VMM_IMPORT_BY_PTR")[0] == '1';
+  int rtv = 0;
+  CK(hipRuntimeGetVersion(&rtv));
   for (size_t i = 0; i < fds.size(); ++i)
-    CK(hipMemImportFromShareableHandle(&h[i], reinterpret_cast<void*>(static_cast<intptr_t>(fds[i])),
+    CK(hipMemImportFromShareableHandle(&h[i],
+                                       by_ptr ? static_cast<void*>(&fds[i])
+                                              : reinterpret_cast<void*>(static_cast<intptr_t>(fds[i])),
                                        hipMemHandleTypePosixFileDescriptor));
   double t3 = now_ms();
   void* base = nullptr;
@@ -225,10 +231,10 @@ static int tenant(const char* path) {
   CK(hipMemset(base, 7, total));
   CK(hipDeviceSynchronize());
   double t6 = now_ms();
-  std::printf("{\"tenant_gib\": %.1f, \"hip_init_ms\": %.1f, \"recv_ms\": %.2f, \"import_ms\": %.2f, "
+  std::printf("{\"runtime_version\": %d, \"by_ptr\": %d, \"tenant_gib\": %.1f, \"hip_init_ms\": %.1f, \"recv_ms\": %.2f, \"import_ms\": %.2f, "
               "\"map_ms\": %.2f, \"write_ms\": %.1f, \"write_GBps\": %.0f, "
               "\"nonzero_granules_seen\": %u, \"ready_ms\": %.1f}\n",
-              total / double(1ull << 30), t1 - t0, t2 - t1, t3 - t2, t4 - t3, t6 - t5,
+              rtv, int(by_ptr), total / double(1ull << 30), t1 - t0, t2 - t1, t3 - t2, t4 - t3, t6 - t5,
               total / ((t6 - t5) / 1e3) / 1e9, nonzero, (t4 - t1));
   std::fflush(stdout);
   return 0;  // exit: the mappings go with the process, the broker's handles keep the memory

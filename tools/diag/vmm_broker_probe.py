@@ -23,6 +23,8 @@ def main(argv=None) -> int:
     ap.add_argument("--granule-mib", type=int, default=1024)
     ap.add_argument("--tenants", type=int, default=3)
     ap.add_argument("--timeout", type=float, default=120.0)
+    ap.add_argument("--tenant-env", action="append", default=[], metavar="K=V",
+                    help="extra env of the tenant processes (e.g. LD_PRELOAD of the quota shim)")
     a = ap.parse_args(argv)
     sock = os.path.join(tempfile.mkdtemp(prefix="vmmbroker"), "b.sock")
     br = subprocess.Popen([BIN, "broker", sock, str(a.granules), str(a.granule_mib), str(a.tenants)],
@@ -35,7 +37,8 @@ def main(argv=None) -> int:
             print(json.dumps(out), flush=True)
             return 1
         for _ in range(a.tenants):
-            t = subprocess.run([BIN, "tenant", sock], capture_output=True, text=True, timeout=a.timeout)
+            tenv = dict(os.environ, **dict(kv.split("=", 1) for kv in a.tenant_env))
+            t = subprocess.run([BIN, "tenant", sock], capture_output=True, text=True, timeout=a.timeout, env=tenv)
             rec = json.loads(t.stdout.strip().splitlines()[-1]) if t.stdout.strip() else {}
             rec["rc"] = t.returncode
             if t.returncode:
