@@ -63,6 +63,11 @@ def _arena_release():
 
 
 def main() -> int:
+    nice = int(os.environ.get("GS_POD_NICE", "0") or 0)
+    if nice > 0:
+        # a node runs its daemons (kubelet, device plugin) ahead of container workloads
+        # (system-reserved CPU); the pod's start-up must not starve the plugin's watch
+        os.nice(nice)
     import torch  # noqa: F401 - imported in standby: the expensive part of a process start
 
     _send({"event": "standby", "pid": os.getpid()})

@@ -615,7 +615,7 @@ class PodFleet:
 
     def _spawn(self):
         env = dict(os.environ, LD_PRELOAD=os.path.join(NATIVE, "libgpushare_hipquota.so"),
-                   PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
+                   PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""), GS_POD_NICE="5")
         for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
                   "TORCHELASTIC_RUN_ID", "GROUP_RANK", "ROLE_RANK"):
             env.pop(k, None)

@@ -66,7 +66,7 @@ int main(int argc, char** argv) {
       printf("{\"op\":\"arena\",\"on\":%d,\"size\":%llu,\"used\":%llu}\n", on, (unsigned long long)sz, (unsigned long long)used); }
     else if (!strcmp(argv[i], "arenarelease")) { int (*f)(void) = (int (*)(void))dlsym(RTLD_DEFAULT, "gpushare_shim_arena_release");
       printf("{\"op\":\"arenarelease\",\"r\":%d}\n", f ? f() : -2); fflush(stdout); }
-    else if (!strcmp(argv[i], "sleep")) { fflush(stdout); usleep((useconds_t)atoi(argv[++i]) * 1000); }
+    else if (!strcmp(argv[i], "sleepms")) { fflush(stdout); usleep((useconds_t)atoi(argv[++i]) * 1000); }
     else if (!strcmp(argv[i], "async")) { size_t n = strtoull(argv[++i], 0, 10); void* p = 0; int e = hipMallocAsync(&p, n, 0);
       printf("{\"op\":\"async\",\"n\":%zu,\"err\":%d,\"idx\":%d}\n", n, e, e ? -1 : np); if (!e) ptrs[np++] = p; }
     else if (!strcmp(argv[i], "vmm")) { size_t n = strtoull(argv[++i], 0, 10); uint64_t h = 0; int e = hipMemCreate(&h, n, 0, 0);

@@ -504,7 +504,7 @@ def test_broker_arena_serves_hipmalloc_from_the_granted_granules(stub, native_sh
         t0 = time.monotonic()
         out, r = run(stub, native_shim, ["alloc", 3 * GIB, "alloc", 512 * MIB, "arena", "free", 0, "alloc", 2 * GIB,
                                          "alloc", GIB, "alloc", GIB, "info", "stats", "arenarelease", "freeall",
-                                         "arenarelease", "arena", "sleep", 600, "alloc", MIB, "stats"],
+                                         "arenarelease", "arena", "sleepms", 600, "alloc", MIB, "stats"],
                      GPUSHARE_QUOTA_BYTES=8 * GIB, GPUSHARE_LEDGER=name, GPUSHARE_HBM_BROKER=sock,
                      GPUSHARE_HBM_TOKEN="tok123")
         t_end = time.monotonic()
