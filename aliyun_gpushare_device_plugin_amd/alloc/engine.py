@@ -129,6 +129,10 @@ class AllocatorOptions:
     # ahead of the plugin's) waits up to this long for the watch before it falls back to a LIST
     # (a round trip to the apiserver on the kubelet's path)
     watch_grace_s: float = 0.005
+    # per-GPU HBM brokers (native/hbmbroker): their socket directory on the host, and the share of
+    # a container's quota granted as broker granules (quota/hbmbroker.py HBMGranter); None = off
+    hbm_broker_dir: str | None = None
+    hbm_broker_fraction: float = 0.94
 
 
 @dataclasses.dataclass
@@ -175,6 +179,7 @@ class Allocator(NativeTable):
         self.grants = PL.GrantBook()
         self.prestart_hooks: list = []          # run at PreStartContainer (after the placement pass)
         self._ledgers = self._ledger_dir(self.opts)
+        self._hbm = self._hbm_granter(self.opts)
         self.podres = None
         self._overlay: dict[str, dict] = {}       # uid -> annotations written, not yet landed
         self._overlay_gen: dict[str, int] = {}
@@ -227,6 +232,13 @@ class Allocator(NativeTable):
             threading.Thread(target=self._prepare_loop, name="prepare-answers", daemon=True).start()
 
     @staticmethod
+    def _hbm_granter(opts: AllocatorOptions, secret: bytes | None = None):
+        if not (opts.hbm_broker_dir and opts.shim is not None and opts.shim.enabled and not opts.disable_cgpu):
+            return None
+        from ..quota.hbmbroker import HBMGranter
+        return HBMGranter(opts.hbm_broker_dir, opts.hbm_broker_fraction, secret=secret)
+
+    @staticmethod
     def _ledger_dir(opts: AllocatorOptions):
         if not (opts.ledger_dir and opts.shim is not None):
             return None
@@ -250,6 +262,8 @@ class Allocator(NativeTable):
             self.opts = dataclasses.replace(opts, async_patch=async_patch, journal_path=self.opts.journal_path)
             if opts.ledger_dir != ledger_dir:
                 self._ledgers = self._ledger_dir(self.opts)
+            # same secret across rebuilds: a re-prepared answer keeps its pod's token
+            self._hbm = self._hbm_granter(self.opts, self._hbm.secret if self._hbm is not None else None)
             self._pinfo.clear()
             self._bump_gen()
             self._fast = None
@@ -625,6 +639,12 @@ class Allocator(NativeTable):
                     r.mounts.add(container_path=const.LEDGER_CONTAINER_DIR, host_path=host, read_only=False)
                     r.envs[const.ENV_SHIM_LEDGER_DIR] = const.LEDGER_CONTAINER_DIR
                     r.annotations[const.CTR_ANNOTATION_LEDGER] = lkey
+            hbm = self._hbm
+            if hbm is not None:
+                g = self.model.gpu(gpu_index)
+                tok = hbm.token(pod_uid or f"{gpu_index}-{time.time_ns()}", slot)
+                if hbm.grant(gpu_index, tok, U.quota_bytes(ctr_units, g.units, g.vram_bytes)):
+                    r.envs[const.ENV_HBM_TOKEN] = tok
         return r
 
     def _container_base(self, gpu_index: int, pod_units: int, ctr_units: int,
@@ -662,6 +682,11 @@ class Allocator(NativeTable):
             r.envs[const.ENV_LD_PRELOAD] = shim.container_lib
             # exact bytes from the SMI-reported HBM size, so the shim needs no device query
             r.envs[const.ENV_SHIM_QUOTA_BYTES] = str(U.quota_bytes(ctr_units, g.units, g.vram_bytes))
+            if self._hbm is not None:
+                # the GPU's HBM broker; the pod's token is per pod (_container_response / _prepared)
+                r.mounts.add(container_path=const.HBM_BROKER_CONTAINER_DIR, host_path=self._hbm.host_dir,
+                             read_only=False)
+                r.envs[const.ENV_HBM_BROKER] = self._hbm.container_socket(gpu_index)
         return r
 
     def _plan_slots(self, claim: _Claim, pod_units: int) -> cuslots.SlotRun | None:
@@ -933,6 +958,12 @@ class Allocator(NativeTable):
                     extra += (_pb_ld(0x12, _pb_ld(0x0a, const.LEDGER_CONTAINER_DIR.encode()) + _pb_ld(0x12, host.encode()))
                               + _pb_map_entry(0x0a, const.ENV_SHIM_LEDGER_DIR, const.LEDGER_CONTAINER_DIR)
                               + _pb_map_entry(0x22, const.CTR_ANNOTATION_LEDGER, lkey))
+            hbm = self._hbm
+            if hbm is not None:
+                gg = self.model.gpu(g)
+                tok = hbm.token(u or f"{g}-{time.time_ns()}", 0)
+                if hbm.grant(g, tok, U.quota_bytes(units, gg.units, gg.vram_bytes)):
+                    extra += _pb_map_entry(0x0a, const.ENV_HBM_TOKEN, tok)
         body = _pb_ld(0x0a, base + extra)            # AllocateResponse.container_responses[0]
         return _Prepared(u, O.namespace(p), O.name(p), units, False, g, body,
                          AllocJournal.fast_head(u, O.namespace(p), O.name(p), body), lkey)

@@ -64,6 +64,11 @@ ENV_SHIM_GRANULE = "GPUSHARE_ALLOC_GRANULE"    # allocation rounding granule ove
 ENV_SHIM_LOG = "GPUSHARE_SHIM_LOG"
 ENV_SHIM_LEDGER_DIR = "GPUSHARE_LEDGER_DIR"    # file-backed ledgers in a host-mounted directory
 LEDGER_CONTAINER_DIR = "/run/gpushare/ledger"
+# per-GPU HBM broker (native/hbmbroker): the socket directory mounted into shared containers,
+# the GPU's socket and the pod's one-time grant token
+ENV_HBM_BROKER = "GPUSHARE_HBM_BROKER"
+ENV_HBM_TOKEN = "GPUSHARE_HBM_TOKEN"
+HBM_BROKER_CONTAINER_DIR = "/run/gpushare/hbm"
 # container annotation (ContainerAllocateResponse.annotations): the host ledger directory key
 # of this container, so the plugin can map an answer back to its ledger (quota/ledger.py)
 CTR_ANNOTATION_LEDGER = "gpushare.amd.com/ledger"

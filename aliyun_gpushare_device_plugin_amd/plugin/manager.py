@@ -68,6 +68,8 @@ class PluginConfig:
     complete_swaps: bool = True          # match a swapped equal-size pod (see alloc/engine.py)
     partition_aware: bool = True         # divide NPS1-shared HBM among compute partitions
     ledger_dir: str | None = None        # host dir for file-backed shim ledgers (usage metrics)
+    hbm_broker_dir: str | None = None    # host dir of the per-GPU HBM broker sockets (quota/hbmbroker.py)
+    hbm_broker_fraction: float = 0.94
     ledger_scan_s: float = 10.0
     journal_path: str | None = None      # persisted allocation journal (alloc/journal.py)
     compute_isolation: str = "none"      # "cu": per-pod CU-slot masks (alloc/cuslots.py)
@@ -186,6 +188,8 @@ class SharedGPUManager:
                                 rocr_visible=cfg.rocr_visible, async_patch=cfg.async_patch,
                                 complete_swaps=cfg.complete_swaps,
                                 ledger_dir=cfg.ledger_dir if shim else None,
+                                hbm_broker_dir=cfg.hbm_broker_dir if shim else None,
+                                hbm_broker_fraction=cfg.hbm_broker_fraction,
                                 journal_path=cfg.journal_path,
                                 compute_isolation=cfg.compute_isolation, placement_s=cfg.placement_s,
                                 identify=cfg.admission_identity)

@@ -12,17 +12,24 @@ No counterpart in the reference: there a pod's memory is whatever cGPU lets the 
 """
 from __future__ import annotations
 
+import collections
+import hashlib
+import hmac
 import json
 import os
 import secrets
 import socket
 import subprocess
 import threading
+import time
 
+from .. import const
+from ..utils import log
 from ..utils.native import ensure_built
 
-ENV_SOCKET = "GPUSHARE_HBM_BROKER"
-ENV_TOKEN = "GPUSHARE_HBM_TOKEN"
+ENV_SOCKET = const.ENV_HBM_BROKER
+ENV_TOKEN = const.ENV_HBM_TOKEN
+GRANULE = 1 << 30
 
 
 def broker_exe() -> str:
@@ -31,6 +38,11 @@ def broker_exe() -> str:
 
 def new_token() -> str:
     return secrets.token_hex(16)
+
+
+def socket_name(gpu_index: int) -> str:
+    """The broker socket of GPU ``gpu_index`` inside the broker directory."""
+    return f"hbm{gpu_index}.sock"
 
 
 def _request(path: str, line: str, timeout: float = 10.0) -> str:
@@ -119,3 +131,66 @@ class HBMBroker:
                 p.kill()
                 p.wait()
         self.proc = None
+
+
+class HBMGranter:
+    """The device plugin's side (``--hbm-broker-dir``): grants each shared container its HBM on
+    its GPU's broker while the plugin prepares the container's Allocate answer (before the bind
+    when the extender labelled the pod, so off the kubelet's path), under a token derived from
+    the pod UID and the container slot with a per-process secret. The same pod always gets the
+    same token, so a re-prepared or replayed answer is byte-identical.
+
+    The grant is ``fraction`` of the container's quota, rounded down to whole 1 GiB granules
+    (the shim charges it to the container's ledger, and what the runtime still takes from the
+    driver is charged on top, within the quota). Below 2 granules there is no arena. A broker
+    that cannot be reached is skipped for ``backoff_s``: the answer then carries no token and the
+    pod allocates from the driver as without a broker."""
+
+    def __init__(self, host_dir: str, fraction: float = 0.94, secret: bytes | None = None,
+                 timeout_s: float = 0.2, backoff_s: float = 5.0):
+        self.host_dir = host_dir
+        self.fraction = fraction
+        self.secret = secret or os.urandom(32)
+        self.timeout_s, self.backoff_s = timeout_s, backoff_s
+        self._mu = threading.Lock()
+        self._granted: collections.OrderedDict = collections.OrderedDict()   # token -> bytes
+        self._down_until: dict[int, float] = {}
+        self.grants = self.failures = 0
+
+    def container_socket(self, gpu_index: int) -> str:
+        return f"{const.HBM_BROKER_CONTAINER_DIR}/{socket_name(gpu_index)}"
+
+    def token(self, pod_uid: str, slot: int) -> str:
+        return hmac.new(self.secret, f"{pod_uid}/{slot}".encode(), hashlib.sha256).hexdigest()[:32]
+
+    def arena_bytes(self, quota_bytes: int) -> int:
+        n = int(quota_bytes * self.fraction) // GRANULE
+        return n * GRANULE if n >= 2 else 0
+
+    def grant(self, gpu_index: int, token: str, quota_bytes: int) -> bool:
+        nbytes = self.arena_bytes(quota_bytes)
+        if not nbytes:
+            return False
+        with self._mu:
+            if self._granted.get(token) == nbytes:
+                return True
+            if self._down_until.get(gpu_index, 0.0) > time.monotonic():
+                return False
+        path = os.path.join(self.host_dir, socket_name(gpu_index)) + ".admin"
+        try:
+            r = _request(path, f"GRANT {token} {nbytes}", timeout=self.timeout_s)
+            ok = r.startswith("OK ")
+        except OSError as e:
+            r, ok = str(e), False
+        with self._mu:
+            if ok:
+                self.grants += 1
+                self._granted[token] = nbytes
+                while len(self._granted) > 8192:
+                    self._granted.popitem(last=False)
+                return True
+            self.failures += 1
+            self._down_until[gpu_index] = time.monotonic() + self.backoff_s
+        log.warning("hbm broker of GPU %d: no grant (%s); its pods allocate from the driver for %.0f s",
+                    gpu_index, r, self.backoff_s)
+        return False

@@ -88,8 +88,9 @@ def parse():
                     help="pods take their HBM from a per-GPU broker (native/hbmbroker) instead of fresh driver "
                          "allocations: no wait for amdgpu's wipe of a retired pod's HBM (--no-hbm-broker: the "
                          "driver path; if the broker cannot start, the run falls back to it and says why)")
-    ap.add_argument("--hbm-broker-reserve-gib", type=float, default=16.0,
-                    help="HBM the broker leaves to the driver (runtimes' own allocations)")
+    ap.add_argument("--hbm-broker-reserve-gib", type=float, default=12.0,
+                    help="HBM the broker leaves to the driver (runtimes' own allocations); the plugin grants each "
+                         "pod 94 %% of its quota in whole GiB, 269-270 GiB for a GPU's 4 pods")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -215,7 +216,7 @@ class ControlPlane:
     """Rank 0's view of the node: fake cluster + the real plugin process."""
 
     def __init__(self, n_gpus: int, smi_spec: str, pod_source: str, plugin_mode: str, workdir: str,
-                 with_shim: bool, ref_spec: str | None = None):
+                 with_shim: bool, ref_spec: str | None = None, hbm_dir: str | None = None):
         from aliyun_gpushare_device_plugin_amd.sim.cluster import SimCluster
 
         self.n = n_gpus
@@ -226,6 +227,9 @@ class ControlPlane:
         extra += ["--ledger-dir", self.ledger_dir, "--journal-path", os.path.join(workdir, "alloc-journal.jsonl")]
         if with_shim:
             extra += ["--rocr-visible-devices"]
+        if hbm_dir:
+            # the plugin grants every pod its broker granules while it prepares the pod's answer
+            extra += ["--hbm-broker-dir", hbm_dir]
         nodes = [(MAIN_NODE, smi_spec)]
         overrides = {}
         # the reference's cost model (LIST per Allocate + synchronous PATCH, allocate.go:63-152)
@@ -655,16 +659,8 @@ class PodFleet:
             env["HIP_VISIBLE_DEVICES"] = str(self.ordinal)
         from aliyun_gpushare_device_plugin_amd import const
 
-        if self.broker is not None:
-            # the granter's part (the plugin's Allocate in a deployment): the pod's state + its
-            # GEMM working set + 1 GiB for the caching allocator's rounding, under a one-time token
-            from aliyun_gpushare_device_plugin_amd.quota import hbmbroker
-
-            token = hbmbroker.new_token()
-            quota = int(env.get(const.ENV_SHIM_QUOTA_BYTES, 0))
-            self.broker.grant(token, int(quota * self.fill) + 3 * self.gemm ** 2 * 2 + (1 << 30))
-            env[hbmbroker.ENV_SOCKET] = self.broker.socket_path
-            env[hbmbroker.ENV_TOKEN] = token
+        # with an HBM broker the plugin granted the pod its granules while it prepared the answer:
+        # the env carries the broker socket (host path, container_env) and the pod's token
         t0 = time.perf_counter()
         w["proc"].stdin.write(json.dumps({"cmd": "start", "env": env, "gemm": self.gemm, "burst": self.burst,
                                           "fill": self.fill, "two_phase": True}) + "\n")
@@ -838,17 +834,19 @@ def main():
             with SMI("auto") as s:
                 # every rank bound its plugin GPU above (bind_device), so the node has >= n GPUs
                 ref_spec = f"fake:{n}x{s.device(0).vram_total}B"
+        hbm_dir = tempfile.mkdtemp(prefix="gs-hbm-", dir="/tmp") if use_gpu and a.hbm_broker else None
         cp = ControlPlane(n, smi, a.pod_source, a.plugin_mode, workdir, with_shim=use_gpu,
-                          ref_spec=None if a.no_ref_churn else ref_spec)
-        info = {"units_per_gpu": cp.units_per_gpu, "gpu_count": cp.gpu_count}
+                          ref_spec=None if a.no_ref_churn else ref_spec, hbm_dir=hbm_dir)
+        info = {"units_per_gpu": cp.units_per_gpu, "gpu_count": cp.gpu_count, "hbm_dir": hbm_dir}
     info = bcast(info)
     units = info["units_per_gpu"]
     broker = None
     broker_error = None
-    if use_gpu and a.hbm_broker:
-        from aliyun_gpushare_device_plugin_amd.quota.hbmbroker import HBMBroker
+    if use_gpu and info.get("hbm_dir"):
+        from aliyun_gpushare_device_plugin_amd.quota.hbmbroker import HBMBroker, socket_name
 
-        broker = HBMBroker(os.path.join(workdir, f"hbm{local}.sock"), device=ordinal,
+        # the broker of the plugin's GPU <local> (this rank's device, bound by PCI address)
+        broker = HBMBroker(os.path.join(info["hbm_dir"], socket_name(local)), device=ordinal,
                            reserve_gib=a.hbm_broker_reserve_gib)
         try:
             broker.start()

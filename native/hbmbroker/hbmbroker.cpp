@@ -23,7 +23,7 @@
 // is gone, as it does on a node.
 //
 //   gpushare-hbm-broker --socket /run/gpushare/hbm0.sock [--device 0] [--gib N | --reserve-gib R]
-//                       [--granule-mib 1024] [--wait-s 30]
+//                       [--granule-mib 1024] [--wait-s 30] [--grant-ttl-s 600]
 #include <hip/hip_runtime.h>
 
 #include <poll.h>
@@ -101,7 +101,13 @@ struct Broker {
   char* base = nullptr;  // every granule mapped here, for the scrub
   hipStream_t stream = nullptr;
   std::deque<int> free_list;
-  std::map<std::string, int> grants;  // token -> granules
+  struct Grant {
+    int granules;
+    double at;
+  };
+  std::map<std::string, Grant> grants;  // token -> granules; dropped after grant_ttl_s untaken
+  double grant_ttl_s = 600.0;
+  unsigned long long expired = 0;
   std::map<int, Client> clients;
   // stats
   unsigned long long takes = 0, releases = 0, refused = 0, timeouts = 0;
@@ -197,9 +203,9 @@ struct Broker {
       Client& c = clients[o.second];
       auto g = grants.find(c.waiting);
       if (g == grants.end()) continue;           // grant not here yet
-      if (size_t(g->second) > free_list.size()) break;  // keep arrival order: no overtaking
+      if (size_t(g->second.granules) > free_list.size()) break;  // keep arrival order: no overtaking
       std::vector<int> idx;
-      for (int i = 0; i < g->second; ++i) {
+      for (int i = 0; i < g->second.granules; ++i) {
         idx.push_back(free_list.front());
         free_list.pop_front();
       }
@@ -233,10 +239,10 @@ struct Broker {
     std::snprintf(b, sizeof b,
                   "{\"device\": %d, \"granule_bytes\": %zu, \"granules\": %d, \"free\": %zu, \"held\": %zu, "
                   "\"waiting\": %zu, \"grants\": %zu, \"takes\": %llu, \"releases\": %llu, \"refused\": %llu, "
-                  "\"timeouts\": %llu, \"scrubbed_bytes\": %llu, \"scrub_ms_total\": %.3f, \"scrub_ms_last\": %.3f, "
+                  "\"timeouts\": %llu, \"expired\": %llu, \"scrubbed_bytes\": %llu, \"scrub_ms_total\": %.3f, \"scrub_ms_last\": %.3f, "
                   "\"setup_ms\": %.1f}\n",
                   device, gran, count, free_list.size(), held, waiting, grants.size(), takes, releases, refused,
-                  timeouts, scrubbed_bytes, scrub_s_total * 1e3, scrub_s_last * 1e3, setup_s * 1e3);
+                  timeouts, expired, scrubbed_bytes, scrub_s_total * 1e3, scrub_s_last * 1e3, setup_s * 1e3);
     return b;
   }
 
@@ -251,7 +257,7 @@ struct Broker {
         reply(fd, "ERR size\n");
         return;
       }
-      grants[tok] = n;
+      grants[tok] = Grant{n, now_s()};  // a repeated grant (a re-prepared answer) refreshes it
       reply(fd, "OK " + std::to_string(n) + "\n");
       serve_waiting();
     } else if (c.admin && line == "STAT") {
@@ -283,6 +289,7 @@ int main(int argc, char** argv) {
     else if (k == "--reserve-gib") reserve_gib = std::atof(v);
     else if (k == "--granule-mib") gran_mib = std::strtoull(v, nullptr, 10);
     else if (k == "--wait-s") b.wait_s = std::atof(v);
+    else if (k == "--grant-ttl-s") b.grant_ttl_s = std::atof(v);
     else {
       std::fprintf(stderr, "gpushare-hbm-broker: unknown flag %s\n", k.c_str());
       return 2;
@@ -351,6 +358,15 @@ int main(int argc, char** argv) {
       ++b.timeouts;
       Broker::reply(fd, "ERR timeout\n");
       b.drop(fd);
+    }
+    // grants of pods that never started (deleted before admission) do not pile up
+    for (auto it = b.grants.begin(); it != b.grants.end();) {
+      if (t - it->second.at > b.grant_ttl_s) {
+        it = b.grants.erase(it);
+        ++b.expired;
+      } else {
+        ++it;
+      }
     }
   }
   for (auto it = b.clients.begin(); it != b.clients.end();) close((it++)->first);

@@ -1101,6 +1101,7 @@ struct Arena {
   int next = 0;
   Live* live = nullptr;
   uint64_t nlive = 0;
+  bool charged = false;  // the arena's size is on the pod's ledger
 };
 Arena g_arena;
 
@@ -1148,6 +1149,21 @@ bool recv_fd_batch(int s, int* out, int* got, int want) {
     else close(p[i]);
   }
   return true;
+}
+
+// unmap and release whatever of the arena is mapped (g_arena.mu held)
+void arena_unmap_locked() {
+  Arena& a = g_arena;
+  Depth d;
+  if (auto dev_sync = real_hipDeviceSynchronize()) (void)dev_sync();
+  if (a.base) {
+    if (auto un = real_hipMemUnmap()) (void)un(a.base, a.size);
+    if (auto fr = real_hipMemAddressFree()) (void)fr(a.base, a.size);
+  }
+  if (auto rel = real_hipMemRelease())
+    for (int i = 0; i < a.n; ++i) (void)rel(a.h[i]);
+  a.n = 0;
+  a.base = nullptr;
 }
 
 // called with g_arena.mu held, at the first allocation
@@ -1220,6 +1236,15 @@ void arena_take() {
     a.size = size;
     a.gran = gran;
   }
+  // the arena counts against the pod's quota like any other HBM it holds: what the runtime
+  // still takes from the driver (code objects, scratch) is charged on top of it
+  if (enabled() && !charge(a.size)) {
+    logf(1, "hbm broker: arena of %llu bytes exceeds the quota (%llu): not used",
+         (unsigned long long)a.size, (unsigned long long)g.quota.load());
+    arena_unmap_locked();
+    goto fail;
+  }
+  a.charged = enabled();
   a.ext = static_cast<Ext*>(calloc(kArenaMaxExt, sizeof(Ext)));
   a.live = static_cast<Live*>(calloc(kArenaLiveCap, sizeof(Live)));
   if (!a.ext || !a.live) goto fail;
@@ -1376,18 +1401,12 @@ GS_EXPORT int gpushare_shim_arena_release() {
     pthread_mutex_unlock(&a.mu);
     return -1;
   }
-  {
-    Depth d;
-    if (auto dev_sync = real_hipDeviceSynchronize()) (void)dev_sync();
-    if (auto un = real_hipMemUnmap()) (void)un(a.base, a.size);
-    if (auto rel = real_hipMemRelease())
-      for (int i = 0; i < a.n; ++i) (void)rel(a.h[i]);
-    if (auto fr = real_hipMemAddressFree()) (void)fr(a.base, a.size);
-  }
+  arena_unmap_locked();
+  if (a.charged) uncharge(a.size);
+  a.charged = false;
   close(a.sock);
   a.sock = -1;
   a.state.store(-1, std::memory_order_release);
-  a.n = 0;
   pthread_mutex_unlock(&a.mu);
   return 1;
 }
@@ -1555,8 +1574,8 @@ GS_EXPORT hipError_t hipMemGetInfo(size_t* free_b, size_t* total_b) {
   if (free_b && *free_b > left) *free_b = (size_t)left;
   if (total_b) *total_b = (size_t)quota;
   uint64_t asz = 0, aused = 0;
-  if (free_b && arena_configured() && gpushare_shim_arena_stats(&asz, &aused) && *free_b > asz - aused)
-    *free_b = (size_t)(asz - aused);  // with a broker arena, what the pod can still get is the arena's rest
+  if (free_b && arena_configured() && gpushare_shim_arena_stats(&asz, &aused))
+    *free_b = (size_t)(asz - aused);  // with a broker arena, hipMalloc is served from the arena's rest
   return e;
 }
 

@@ -578,3 +578,73 @@ def test_prepared_body_is_the_container_response(tmp_path, shim, ledgers, disabl
             assert (c.lkey != "") == (ledgers and shim and not disable_cgpu)
     finally:
         al.close()
+
+
+class _FakeBrokerAdmin:
+    """The admin socket of one GPU's HBM broker: records GRANTs and answers OK."""
+
+    def __init__(self, path, ok=True):
+        import socket as _s
+
+        self.grants = []
+        self.ok = ok
+        self.ls = _s.socket(_s.AF_UNIX, _s.SOCK_STREAM)
+        self.ls.bind(path)
+        self.ls.listen(16)
+        threading.Thread(target=self._serve, daemon=True).start()
+
+    def _serve(self):
+        while True:
+            try:
+                c, _ = self.ls.accept()
+            except OSError:
+                return
+            buf = b""
+            while not buf.endswith(b"\n"):
+                chunk = c.recv(256)
+                if not chunk:
+                    break
+                buf += chunk
+            _, tok, nbytes = buf.decode().split()
+            self.grants.append((tok, int(nbytes)))
+            c.sendall(f"OK {int(nbytes) >> 30}\n".encode() if self.ok else b"ERR size\n")
+            c.close()
+
+
+def test_hbm_broker_grant_rides_in_the_prepared_answer(tmp_path):
+    """With --hbm-broker-dir the answer mounts the broker directory, names the GPU's socket and
+    carries the pod's token, granted on that GPU's broker while the answer is prepared; the
+    hand-encoded prepared answer and the field-by-field one stay equal, and a re-prepared answer
+    grants nothing new. An unreachable broker leaves the token out (the pod uses the driver)."""
+    from aliyun_gpushare_device_plugin_amd.quota import hbmbroker
+
+    model = DeviceModel([gpu(i, 64 << 30) for i in range(2)], const.GIB)
+    src = StaticSource([])
+    hdir = tmp_path / "hbm"
+    hdir.mkdir()
+    admin = _FakeBrokerAdmin(str(hdir / (hbmbroker.socket_name(1) + ".admin")))
+    opts = AllocatorOptions(shim=ShimConfig(host_dir=str(tmp_path / "shim")), hbm_broker_dir=str(hdir))
+    al = Allocator(model, src, FakeClient(src), NODE, opts)
+    try:
+        pod = mkpod("h0", 16, 1, 10)
+        c = al._prepared(pod, "uid-h0", 1, 16)
+        got = api.AllocateResponse.FromString(c.body).container_responses[0]
+        want = al._container_response(1, 16, 16, "uid-h0", 0, None)
+        assert got == want
+        tok = got.envs[const.ENV_HBM_TOKEN]
+        assert got.envs[const.ENV_HBM_BROKER] == f"{const.HBM_BROKER_CONTAINER_DIR}/hbm1.sock"
+        assert any(m.container_path == const.HBM_BROKER_CONTAINER_DIR and m.host_path == str(hdir) for m in got.mounts)
+        # 16 of 64 GiB -> a 16 GiB quota; 94 % of it in whole granules = 15 GiB, granted once
+        assert admin.grants == [(tok, 15 << 30)]
+        assert al._prepared(pod, "uid-h0", 1, 16).body == c.body and len(admin.grants) == 1
+        # GPU 0 has no broker: no token, and the failure is not retried on every answer
+        r0 = al._container_response(0, 16, 16, "uid-h1", 0, None)
+        assert const.ENV_HBM_TOKEN not in r0.envs and r0.envs[const.ENV_HBM_BROKER].endswith("hbm0.sock")
+        assert al._hbm.failures == 1
+        al._container_response(0, 16, 16, "uid-h2", 0, None)
+        assert al._hbm.failures == 1       # backed off: no second connect
+        # too small for two granules: no arena, no grant
+        small = al._container_response(1, 1, 1, "uid-h3", 0, None)
+        assert const.ENV_HBM_TOKEN not in small.envs and len(admin.grants) == 1
+    finally:
+        al.close()

@@ -493,7 +493,7 @@ class FakeBroker:
 
 def test_broker_arena_serves_hipmalloc_from_the_granted_granules(stub, native_shim, tmp_path):
     """The pod's hipMalloc/hipFree come from its granted granules (first fit, coalescing), the
-    pod sees the arena's rest as free, nothing is charged at the KFD for them, and the arena is
+    pod sees the arena's rest as free, the arena counts against its quota, and the arena is
     handed back only once nothing in it is live; allocations after that go to the driver."""
     import time
 
@@ -517,11 +517,11 @@ def test_broker_arena_serves_hipmalloc_from_the_granted_granules(stub, native_sh
         assert d1["err"] == 0 and d1["p"] == a3["p"] + 2 * GIB   # coalesced rest of it
         assert e1["err"] == 2                                    # 4 GiB arena full: out of memory
         assert info["total"] == 8 * GIB and info["free"] == 512 * MIB
-        assert st["used"] == 0                                   # no KFD charge for broker granules
+        assert st["used"] == 4 * GIB                             # the arena is on the pod's ledger
         assert rel_live["r"] == -1 and rel["r"] == 1             # released only once nothing is live
         assert arena_after["on"] == 0
         assert b.closed_at is not None and b.closed_at < t_end - 0.4   # handed back before exit
-        assert late["err"] == 0 and st_after["used"] >= MIB      # afterwards: the driver, charged
+        assert late["err"] == 0 and MIB <= st_after["used"] < GIB   # arena uncharged; the driver, charged
     finally:
         cleanup(name)
 
@@ -566,5 +566,27 @@ def test_broker_arena_under_sanitizers(stub, tmp_path, san):
         assert out[0]["ok"] == 8 * 300 and out[0]["denied"] == 0
         assert out[1] == {"op": "arena", "on": 1, "size": 2 * GIB, "used": 0}
         assert out[2]["r"] == 1 and b.took == "TAKE t"
+    finally:
+        cleanup(name)
+
+
+def test_broker_arena_larger_than_the_quota_is_not_used(stub, native_shim, tmp_path):
+    """A grant bigger than the pod's quota (a misconfigured granter) must not lift the quota: the
+    shim hands the granules back and the pod allocates from the driver under its quota."""
+    sock = str(tmp_path / "hbm.sock")
+    b = FakeBroker(sock, granules=4)
+    name = ledger()
+    try:
+        out, r = run(stub, native_shim, ["alloc", GIB, "arena", "alloc", 3 * GIB, "stats"], GPUSHARE_QUOTA_BYTES=2 * GIB,
+                     GPUSHARE_LEDGER=name, GPUSHARE_HBM_BROKER=sock, GPUSHARE_HBM_TOKEN="big")
+        assert r.returncode == 0, r.stderr
+        assert out[0]["err"] == 0 and out[1]["on"] == 0
+        assert out[2]["err"] == 2 and out[3]["used"] == GIB
+        import time
+        for _ in range(50):
+            if b.closed_at is not None:
+                break
+            time.sleep(0.02)
+        assert b.closed_at is not None                           # the granules went back at once
     finally:
         cleanup(name)
