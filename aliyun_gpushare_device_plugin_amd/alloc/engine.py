@@ -643,7 +643,7 @@ class Allocator(NativeTable):
             if hbm is not None:
                 g = self.model.gpu(gpu_index)
                 tok = hbm.token(pod_uid or f"{gpu_index}-{time.time_ns()}", slot)
-                if hbm.grant(gpu_index, tok, U.quota_bytes(ctr_units, g.units, g.vram_bytes)):
+                if hbm.submit(gpu_index, tok, U.quota_bytes(ctr_units, g.units, g.vram_bytes)):
                     r.envs[const.ENV_HBM_TOKEN] = tok
         return r
 
@@ -962,7 +962,7 @@ class Allocator(NativeTable):
             if hbm is not None:
                 gg = self.model.gpu(g)
                 tok = hbm.token(u or f"{g}-{time.time_ns()}", 0)
-                if hbm.grant(g, tok, U.quota_bytes(units, gg.units, gg.vram_bytes)):
+                if hbm.submit(g, tok, U.quota_bytes(units, gg.units, gg.vram_bytes)):
                     extra += _pb_map_entry(0x0a, const.ENV_HBM_TOKEN, tok)
         body = _pb_ld(0x0a, base + extra)            # AllocateResponse.container_responses[0]
         return _Prepared(u, O.namespace(p), O.name(p), units, False, g, body,

@@ -135,8 +135,8 @@ class HBMBroker:
 
 class HBMGranter:
     """The device plugin's side (``--hbm-broker-dir``): grants each shared container its HBM on
-    its GPU's broker while the plugin prepares the container's Allocate answer (before the bind
-    when the extender labelled the pod, so off the kubelet's path), under a token derived from
+    its GPU's broker when the plugin prepares the container's Allocate answer (before the bind
+    when the extender labelled the pod), from a background thread, under a token derived from
     the pod UID and the container slot with a per-process secret. The same pod always gets the
     same token, so a re-prepared or replayed answer is byte-identical.
 
@@ -144,7 +144,8 @@ class HBMGranter:
     (the shim charges it to the container's ledger, and what the runtime still takes from the
     driver is charged on top, within the quota). Below 2 granules there is no arena. A broker
     that cannot be reached is skipped for ``backoff_s``: the answer then carries no token and the
-    pod allocates from the driver as without a broker."""
+    pod allocates from the driver as without a broker (a grant that fails after its answer went
+    out: the pod's TAKE times out at the broker and the pod uses the driver)."""
 
     def __init__(self, host_dir: str, fraction: float = 0.94, secret: bytes | None = None,
                  timeout_s: float = 0.2, backoff_s: float = 5.0):
@@ -156,6 +157,45 @@ class HBMGranter:
         self._granted: collections.OrderedDict = collections.OrderedDict()   # token -> bytes
         self._down_until: dict[int, float] = {}
         self.grants = self.failures = 0
+        import queue
+        self._q: "queue.Queue" = queue.Queue()
+        self._queued: set[str] = set()
+        self._idle = threading.Event()
+        self._idle.set()
+        threading.Thread(target=self._worker, name="hbm-granter", daemon=True).start()
+
+    def submit(self, gpu_index: int, token: str, quota_bytes: int) -> bool:
+        """Grant in the background; True = the answer carries the token. The answer is prepared
+        on the pod watch thread, which must not wait for a broker (its event loop can be inside
+        a scrub); the broker holds the pod's TAKE until the grant has arrived."""
+        nbytes = self.arena_bytes(quota_bytes)
+        if not nbytes:
+            return False
+        with self._mu:
+            if self._granted.get(token) == nbytes or token in self._queued:
+                return True
+            if self._down_until.get(gpu_index, 0.0) > time.monotonic():
+                return False
+            self._queued.add(token)
+            self._idle.clear()
+        self._q.put((gpu_index, token, quota_bytes))
+        return True
+
+    def flush(self, timeout: float = 5.0) -> bool:
+        """Wait until every submitted grant was sent (tests)."""
+        return self._idle.wait(timeout)
+
+    def _worker(self) -> None:
+        while True:
+            gpu_index, token, quota_bytes = self._q.get()
+            try:
+                self.grant(gpu_index, token, quota_bytes)
+            except Exception as e:  # noqa: BLE001 - the granter thread must survive
+                log.warning("hbm broker grant failed: %s", e)
+            with self._mu:
+                self._queued.discard(token)
+                if not self._queued:
+                    self._idle.set()
 
     def container_socket(self, gpu_index: int) -> str:
         return f"{const.HBM_BROKER_CONTAINER_DIR}/{socket_name(gpu_index)}"
@@ -174,8 +214,6 @@ class HBMGranter:
         with self._mu:
             if self._granted.get(token) == nbytes:
                 return True
-            if self._down_until.get(gpu_index, 0.0) > time.monotonic():
-                return False
         path = os.path.join(self.host_dir, socket_name(gpu_index)) + ".admin"
         try:
             r = _request(path, f"GRANT {token} {nbytes}", timeout=self.timeout_s)

@@ -634,15 +634,21 @@ def test_hbm_broker_grant_rides_in_the_prepared_answer(tmp_path):
         tok = got.envs[const.ENV_HBM_TOKEN]
         assert got.envs[const.ENV_HBM_BROKER] == f"{const.HBM_BROKER_CONTAINER_DIR}/hbm1.sock"
         assert any(m.container_path == const.HBM_BROKER_CONTAINER_DIR and m.host_path == str(hdir) for m in got.mounts)
-        # 16 of 64 GiB -> a 16 GiB quota; 94 % of it in whole granules = 15 GiB, granted once
+        # 16 of 64 GiB -> a 16 GiB quota; 94 % of it in whole granules = 15 GiB, granted once,
+        # off the thread that prepares the answer
+        assert al._hbm.flush()
         assert admin.grants == [(tok, 15 << 30)]
-        assert al._prepared(pod, "uid-h0", 1, 16).body == c.body and len(admin.grants) == 1
-        # GPU 0 has no broker: no token, and the failure is not retried on every answer
+        assert al._prepared(pod, "uid-h0", 1, 16).body == c.body
+        assert al._hbm.flush() and len(admin.grants) == 1
+        # GPU 0 has no broker: the first answer carries its token (the grant is not known to
+        # fail yet; the pod's TAKE would time out), later ones do not, and the broker is not
+        # asked again on every answer
         r0 = al._container_response(0, 16, 16, "uid-h1", 0, None)
-        assert const.ENV_HBM_TOKEN not in r0.envs and r0.envs[const.ENV_HBM_BROKER].endswith("hbm0.sock")
-        assert al._hbm.failures == 1
-        al._container_response(0, 16, 16, "uid-h2", 0, None)
-        assert al._hbm.failures == 1       # backed off: no second connect
+        assert r0.envs[const.ENV_HBM_BROKER].endswith("hbm0.sock")
+        assert al._hbm.flush() and al._hbm.failures == 1
+        r2 = al._container_response(0, 16, 16, "uid-h2", 0, None)
+        assert const.ENV_HBM_TOKEN not in r2.envs
+        assert al._hbm.flush() and al._hbm.failures == 1       # backed off: no second connect
         # too small for two granules: no arena, no grant
         small = al._container_response(1, 1, 1, "uid-h3", 0, None)
         assert const.ENV_HBM_TOKEN not in small.envs and len(admin.grants) == 1
