@@ -1,0 +1,105 @@
+"""``gpushare-hbm-brokers`` — run and supervise one HBM broker per GPU of the node.
+
+Each broker (``native/hbmbroker``, ``gpushare-hbm-broker``) holds its GPU's shareable HBM as VMM
+granules and lends each pod its own, zeroed between pods (``docs/HBM_TURNOVER.md``). The device
+plugin, started with ``--hbm-broker-dir`` on the same directory, grants every shared container its
+granules. GPU ``i`` of the plugin (its SMI order) gets the socket ``<dir>/hbm<i>.sock``, and the
+broker finds its HIP device by that GPU's PCI address, because HIP and SMI orders are not
+promised to agree.
+
+A broker that exits is started again after ``--restart-backoff`` seconds. Its pods lose their
+granules with it: the same blast radius as the GPU. Pods admitted meanwhile find no socket.
+Their TAKE fails, and they allocate from the driver under the quota shim.
+
+No counterpart in the reference (``pkg/gpu/nvidia/allocate.go:114-127`` leaves isolation and
+memory to cGPU).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import signal
+import sys
+import threading
+import time
+
+from ..device.smi import SMI
+from ..quota.hbmbroker import HBMBroker, socket_name
+from ..utils import log
+
+
+def build_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(prog="gpushare-hbm-brokers", description=__doc__.splitlines()[0])
+    p.add_argument("--dir", default="/var/run/gpushare/hbm", help="socket directory (the plugin's --hbm-broker-dir)")
+    p.add_argument("--smi-backend", default="auto")
+    p.add_argument("--gpu-indices", default="", help="comma-separated plugin GPU indices (default: all)")
+    p.add_argument("--reserve-gib", type=float, default=12.0,
+                   help="HBM each broker leaves to the driver (the pods' runtimes allocate some themselves)")
+    p.add_argument("--granule-mib", type=int, default=1024)
+    p.add_argument("--wait-s", type=float, default=30.0, help="how long a pod's TAKE waits for its granules")
+    p.add_argument("--restart-backoff", type=float, default=2.0)
+    return p
+
+
+class Supervisor:
+    def __init__(self, brokers: dict[int, HBMBroker], backoff_s: float = 2.0):
+        self.brokers, self.backoff_s = brokers, backoff_s
+        self.restarts = {i: 0 for i in brokers}
+        self._stop = threading.Event()
+
+    def start(self) -> None:
+        for i, b in self.brokers.items():
+            info = b.start()
+            log.info("hbm broker of GPU %d: %s granules of %s bytes at %s", i, info.get("granules"),
+                     info.get("granule_bytes"), b.socket_path)
+
+    def watch_once(self) -> None:
+        for i, b in self.brokers.items():
+            p = b.proc
+            if p is not None and p.poll() is None:
+                continue
+            rc = p.returncode if p is not None else None
+            log.warning("hbm broker of GPU %d exited (%s); starting it again", i, rc)
+            self.restarts[i] += 1
+            b.proc = None
+            try:
+                b.start()
+            except Exception as e:  # noqa: BLE001 - retried on the next pass
+                log.warning("hbm broker of GPU %d did not start: %s", i, e)
+
+    def run(self) -> None:
+        while not self._stop.wait(self.backoff_s):
+            self.watch_once()
+
+    def stop(self) -> None:
+        self._stop.set()
+        for b in self.brokers.values():
+            b.stop()
+
+
+def main(argv=None) -> int:
+    a = build_parser().parse_args(argv)
+    log.setup(buffered=True)
+    os.makedirs(a.dir, exist_ok=True)
+    want = {int(x) for x in a.gpu_indices.split(",") if x.strip()}
+    with SMI(a.smi_backend) as s:
+        gpus = [s.device(i) for i in range(s.count())]
+    brokers = {g.index: HBMBroker(os.path.join(a.dir, socket_name(g.index)), pci_bus_id=g.bdf,
+                                  reserve_gib=a.reserve_gib, granule_mib=a.granule_mib, wait_s=a.wait_s)
+               for g in gpus if not want or g.index in want}
+    if not brokers:
+        log.error("no GPU to run an HBM broker for")
+        return 1
+    sup = Supervisor(brokers, a.restart_backoff)
+    signal.signal(signal.SIGTERM, lambda *_: sup._stop.set())
+    signal.signal(signal.SIGINT, lambda *_: sup._stop.set())
+    try:
+        sup.start()
+        sup.run()
+    finally:
+        sup.stop()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -33,7 +33,8 @@ GRANULE = 1 << 30
 
 
 def broker_exe() -> str:
-    return ensure_built("hbmbroker")
+    """The broker binary (``GPUSHARE_HBM_BROKER_EXE`` overrides it: tests run a stand-in)."""
+    return os.environ.get("GPUSHARE_HBM_BROKER_EXE") or ensure_built("hbmbroker")
 
 
 def new_token() -> str:
@@ -67,9 +68,10 @@ class HBMBroker:
     (``attach``)."""
 
     def __init__(self, socket_path: str, device: int = 0, gib: float | None = None, reserve_gib: float = 16.0,
-                 granule_mib: int = 1024, wait_s: float = 30.0, env: dict | None = None):
+                 granule_mib: int = 1024, wait_s: float = 30.0, env: dict | None = None, pci_bus_id: str | None = None):
         self.socket_path = socket_path
         self.device, self.gib, self.reserve_gib = device, gib, reserve_gib
+        self.pci_bus_id = pci_bus_id
         self.granule_mib, self.wait_s = granule_mib, wait_s
         self.env = env
         self.proc: subprocess.Popen | None = None
@@ -84,8 +86,9 @@ class HBMBroker:
         return self.socket_path + ".admin"
 
     def start(self, timeout: float = 180.0) -> dict:
-        cmd = [broker_exe(), "--socket", self.socket_path, "--device", str(self.device),
-               "--granule-mib", str(self.granule_mib), "--wait-s", str(self.wait_s)]
+        cmd = [broker_exe(), "--socket", self.socket_path, "--granule-mib", str(self.granule_mib),
+               "--wait-s", str(self.wait_s)]
+        cmd += ["--pci-bus-id", self.pci_bus_id] if self.pci_bus_id else ["--device", str(self.device)]
         cmd += ["--gib", str(self.gib)] if self.gib else ["--reserve-gib", str(self.reserve_gib)]
         os.makedirs(os.path.dirname(self.socket_path) or ".", exist_ok=True)
         self.proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,

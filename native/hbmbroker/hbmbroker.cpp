@@ -22,7 +22,8 @@
 // waits (up to --wait-s) instead of failing: the pod's runtime may start before the retired pod
 // is gone, as it does on a node.
 //
-//   gpushare-hbm-broker --socket /run/gpushare/hbm0.sock [--device 0] [--gib N | --reserve-gib R]
+//   gpushare-hbm-broker --socket /run/gpushare/hbm0.sock [--device 0 | --pci-bus-id 0000:05:00.0]
+//                       [--gib N | --reserve-gib R]
 //                       [--granule-mib 1024] [--wait-s 30] [--grant-ttl-s 600]
 #include <hip/hip_runtime.h>
 
@@ -276,7 +277,7 @@ struct Broker {
 }  // namespace
 
 int main(int argc, char** argv) {
-  std::string sock;
+  std::string sock, pci;
   Broker b;
   double gib = 0, reserve_gib = 16;
   size_t gran_mib = 1024;
@@ -285,6 +286,7 @@ int main(int argc, char** argv) {
     const char* v = argv[i + 1];
     if (k == "--socket") sock = v;
     else if (k == "--device") b.device = std::atoi(v);
+    else if (k == "--pci-bus-id") pci = v;  // the GPU by PCI address (HIP and SMI orders differ)
     else if (k == "--gib") gib = std::atof(v);
     else if (k == "--reserve-gib") reserve_gib = std::atof(v);
     else if (k == "--granule-mib") gran_mib = std::strtoull(v, nullptr, 10);
@@ -296,11 +298,12 @@ int main(int argc, char** argv) {
     }
   }
   if (sock.empty()) {
-    std::fprintf(stderr, "usage: gpushare-hbm-broker --socket PATH [--device N] [--gib N | --reserve-gib N] "
+    std::fprintf(stderr, "usage: gpushare-hbm-broker --socket PATH [--device N | --pci-bus-id BDF] [--gib N | --reserve-gib N] "
                          "[--granule-mib 1024] [--wait-s 30]\n");
     return 2;
   }
   b.gran = gran_mib << 20;
+  if (!pci.empty()) CK(hipDeviceGetByPCIBusId(&b.device, pci.c_str()));
   CK(hipSetDevice(b.device));
   size_t fr = 0, tot = 0;
   CK(hipMemGetInfo(&fr, &tot));

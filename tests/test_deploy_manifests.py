@@ -34,9 +34,7 @@ def test_manifests_parse_and_have_kinds():
 
 
 def test_daemonset_flags_are_accepted_by_the_cli():
-    ds = [d for _, d in _docs() if d["kind"] == "DaemonSet"]
-    assert ds
-    cmd = ds[0]["spec"]["template"]["spec"]["containers"][0]["command"]
+    cmd = _ds()["containers"][0]["command"]
     cfg = config_from_args(build_parser().parse_args([a for a in cmd[1:] if a.startswith("--")]))
     assert cfg.memory_unit == const.GIB
     # the commented-out isolation flag is valid too
@@ -59,10 +57,29 @@ def test_demo_pods_use_the_plugin_contract():
     assert seen >= 4
 
 
-def _ds():
-    ds = [d for _, d in _docs() if d["kind"] == "DaemonSet"]
+def _ds(name="gpushare-device-plugin-ds"):
+    ds = [d for _, d in _docs() if d["kind"] == "DaemonSet" and d["metadata"]["name"] == name]
     assert len(ds) == 1
     return ds[0]["spec"]["template"]["spec"]
+
+
+def test_hbm_broker_daemonset_matches_the_plugin_flag():
+    """The opt-in broker DaemonSet: its flags are the launcher's, it serves the directory the
+    plugin's (commented) --hbm-broker-dir names, from a hostPath, privileged for /dev/kfd."""
+    from aliyun_gpushare_device_plugin_amd.cli import hbmbroker
+
+    spec = _ds("gpushare-hbm-broker-ds")
+    c = spec["containers"][0]
+    assert c["command"][0] == "gpushare-hbm-brokers" and c["securityContext"]["privileged"] is True
+    a = hbmbroker.build_parser().parse_args(c["command"][1:])
+    mounts = {m["mountPath"]: m for m in c["volumeMounts"]}
+    vols = {v["name"]: v for v in spec["volumes"]}
+    assert vols[mounts[a.dir]["name"]]["hostPath"]["path"] == a.dir
+    with open(os.path.join(ROOT, "deploy", "device-plugin-ds.yaml")) as f:
+        line = next(ln for ln in f if "--hbm-broker-dir=" in ln)
+    flag = line.split("#", 1)[1].strip().split()[1]
+    cfg = config_from_args(build_parser().parse_args([flag]))
+    assert cfg.hbm_broker_dir == a.dir
 
 
 def test_daemonset_can_open_kfd_and_render_nodes():

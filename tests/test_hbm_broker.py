@@ -113,3 +113,28 @@ def test_an_unknown_token_gets_no_arena(tmp_path):
         assert b.stat()["timeouts"] == 1
     finally:
         b.stop()
+
+
+def test_launcher_brings_up_the_broker_of_every_gpu_by_pci_address(tmp_path):
+    """The node launcher (``gpushare-hbm-brokers``) on the box: one broker per GPU of the SMI
+    enumeration, found by PCI address, answering on <dir>/hbm<index>.sock; a pod takes a grant
+    from it."""
+    from aliyun_gpushare_device_plugin_amd.cli import hbmbroker as cli
+    from aliyun_gpushare_device_plugin_amd.device.smi import SMI
+
+    with SMI("auto") as s:
+        gpus = [s.device(i) for i in range(s.count())]
+    d = tmp_path / "hbm"
+    d.mkdir()
+    brokers = {g.index: cli.HBMBroker(str(d / cli.socket_name(g.index)), pci_bus_id=g.bdf, gib=8)
+               for g in gpus[:1]}
+    sup = cli.Supervisor(brokers)
+    try:
+        sup.start()
+        b = brokers[gpus[0].index]
+        assert b.stat()["granules"] == 8
+        b.grant("e" * 32, 6 * GIB)
+        r = _result(_tenant(b, "e" * 32, "check"))
+        assert r["arena"] == 1 and r["nonzero"] == 0
+    finally:
+        sup.stop()
