@@ -65,7 +65,7 @@ ENV_SHIM_LOG = "GPUSHARE_SHIM_LOG"
 ENV_SHIM_LEDGER_DIR = "GPUSHARE_LEDGER_DIR"    # file-backed ledgers in a host-mounted directory
 LEDGER_CONTAINER_DIR = "/run/gpushare/ledger"
 # per-GPU HBM broker (native/hbmbroker): the socket directory mounted into shared containers,
-# the GPU's socket and the pod's one-time grant token
+# the GPU's socket and the pod's grant token
 ENV_HBM_BROKER = "GPUSHARE_HBM_BROKER"
 ENV_HBM_TOKEN = "GPUSHARE_HBM_TOKEN"
 HBM_BROKER_CONTAINER_DIR = "/run/gpushare/hbm"

@@ -3,7 +3,7 @@
 The broker holds a GPU's shareable HBM as VMM granules and lends each pod its own granules,
 zeroed between pods, so an admission never waits for amdgpu to wipe the HBM a retired pod freed.
 The granter (the device plugin at Allocate, or the bench acting for it) grants a pod's bytes
-under a one-time token on the broker's admin socket. The pod's quota shim takes the grant with
+under a per-pod token on the broker's admin socket. The pod's quota shim takes the grant with
 that token (``GPUSHARE_HBM_BROKER`` / ``GPUSHARE_HBM_TOKEN`` in its env) and serves the pod's
 ``hipMalloc`` from it.
 

@@ -9,7 +9,7 @@
 // Isolation: a pod receives ONLY the fds of its own granules (SCM_RIGHTS) and maps them into its
 // own address space; it cannot name another pod's granules. The amount is set by the granter
 // (the device plugin's Allocate, or the bench acting for it) on an admin socket that only root
-// can open, and a pod takes its grant with a one-time token.
+// can open, and a pod takes its grant with its token (again after a container restart).
 //
 // Protocol: one text line per connection's request.
 //   admin socket  <sock>.admin (0600):  "GRANT <token> <bytes>\n"  -> "OK <granules>\n" | "ERR ...\n"
@@ -88,6 +88,7 @@ struct Client {
   std::string in;
   // a pod: the granules it holds (indices), or the token it waits for
   std::vector<int> held;
+  std::string token;    // the grant it holds
   std::string waiting;  // token of a TAKE not yet served
   double wait_since = 0;
 };
@@ -102,11 +103,15 @@ struct Broker {
   char* base = nullptr;  // every granule mapped here, for the scrub
   hipStream_t stream = nullptr;
   std::deque<int> free_list;
+  // A grant belongs to the pod, not to one process: a TAKE holds it while its connection lives,
+  // and a restarted container (same env, same token) takes it again once the old process's
+  // granules are back. It expires grant_ttl_s after it was granted or last released.
   struct Grant {
     int granules;
     double at;
+    int holder = -1;  // fd of the connection holding it
   };
-  std::map<std::string, Grant> grants;  // token -> granules; dropped after grant_ttl_s untaken
+  std::map<std::string, Grant> grants;
   double grant_ttl_s = 600.0;
   unsigned long long expired = 0;
   std::map<int, Client> clients;
@@ -203,14 +208,15 @@ struct Broker {
     for (auto& o : order) {
       Client& c = clients[o.second];
       auto g = grants.find(c.waiting);
-      if (g == grants.end()) continue;           // grant not here yet
+      if (g == grants.end() || g->second.holder >= 0) continue;  // not granted yet, or held
       if (size_t(g->second.granules) > free_list.size()) break;  // keep arrival order: no overtaking
       std::vector<int> idx;
       for (int i = 0; i < g->second.granules; ++i) {
         idx.push_back(free_list.front());
         free_list.pop_front();
       }
-      grants.erase(g);
+      g->second.holder = o.second;
+      c.token = c.waiting;
       c.waiting.clear();
       c.held = idx;
       ++takes;
@@ -225,6 +231,11 @@ struct Broker {
       scrub(it->second.held);
       for (int i : it->second.held) free_list.push_back(i);
       ++releases;
+    }
+    auto g = it->second.token.empty() ? grants.end() : grants.find(it->second.token);
+    if (g != grants.end() && g->second.holder == fd) {
+      g->second.holder = -1;
+      g->second.at = now_s();
     }
     close(fd);
     clients.erase(it);
@@ -258,7 +269,9 @@ struct Broker {
         reply(fd, "ERR size\n");
         return;
       }
-      grants[tok] = Grant{n, now_s()};  // a repeated grant (a re-prepared answer) refreshes it
+      auto& gr = grants[tok];  // a repeated grant (a re-prepared answer) refreshes it
+      gr.granules = n;
+      gr.at = now_s();
       reply(fd, "OK " + std::to_string(n) + "\n");
       serve_waiting();
     } else if (c.admin && line == "STAT") {
@@ -364,7 +377,7 @@ int main(int argc, char** argv) {
     }
     // grants of pods that never started (deleted before admission) do not pile up
     for (auto it = b.grants.begin(); it != b.grants.end();) {
-      if (t - it->second.at > b.grant_ttl_s) {
+      if (it->second.holder < 0 && t - it->second.at > b.grant_ttl_s) {
         it = b.grants.erase(it);
         ++b.expired;
       } else {

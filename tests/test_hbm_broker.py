@@ -86,6 +86,17 @@ def test_the_next_pod_sees_only_zeros(broker):
     assert st["scrubbed_bytes"] >= 12 * GIB
 
 
+def test_a_restarted_container_takes_its_grant_again(broker):
+    """A grant belongs to the pod: after its process exits (a container restart keeps the env and
+    the token), the next process with the same token gets its granules back, zeroed."""
+    broker.grant("r" * 32, 6 * GIB)
+    first = _result(_tenant(broker, "r" * 32, "write"))
+    again = _result(_tenant(broker, "r" * 32, "check"), timeout=60)
+    assert first["arena"] == 1 and again["arena"] == 1 and again["nonzero"] == 0
+    st = broker.stat()
+    assert st["takes"] == 2 and st["timeouts"] == 0
+
+
 def test_a_pod_waits_for_granules_a_retiring_pod_holds(broker):
     broker.grant("c" * 32, 6 * GIB)
     holder = _tenant(broker, "c" * 32, "hold")
