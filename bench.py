@@ -958,7 +958,9 @@ def main():
     retired = gather(fleet.retired_bytes if fleet is not None else 0)
     rel = [x for r in gather(fleet.release_bytes_s if fleet is not None else []) for x in r]
     per_rank = gather(dict(done, rank=rank, gpu=local, binding=binding,
-                           pods_live=len(fleet.pods) if fleet is not None else None))
+                           pods_live=len(fleet.pods) if fleet is not None else None,
+                           broker=broker.stat() if broker is not None else None,
+                           broker_error=broker_error))
     by_size: dict = {}
     phases: dict = {}
     for d in gather(fleet.phase_ms if fleet is not None else {}):
@@ -1103,10 +1105,13 @@ def main():
             # bytes-weighted over the retirements: sum(bytes held) / sum(stop -> GPU has room again)
             "amdgpu_release_GBps": round(sum(b for b, _ in rel) / sum(t for _, t in rel) / 1e9, 1) if rel else None,
         }
-        # pods' HBM from the per-GPU broker (--hbm-broker): rank 0's broker counters
-        res["hbm_broker"] = broker.stat() if broker is not None else None
-        if broker_error:
-            res["hbm_broker_error"] = broker_error
+        # pods' HBM from the per-GPU brokers (--hbm-broker): each GPU's broker counters
+        brokers = {str(r["gpu"]): r["broker"] for r in per_rank}
+        res["hbm_broker"] = brokers.get(str(local))
+        res["hbm_broker_by_gpu"] = brokers if len(brokers) > 1 else None
+        errs = {str(r["gpu"]): r["broker_error"] for r in per_rank if r.get("broker_error")}
+        if errs:
+            res["hbm_broker_error"] = errs
         if topo_report is not None:
             res["topology"] = topo_report
             if use_gpu:
