@@ -76,6 +76,7 @@ class HBMBroker:
         self.env = env
         self.proc: subprocess.Popen | None = None
         self.info: dict = {}
+        self.last_stderr = ""
 
     @classmethod
     def attach(cls, socket_path: str) -> "HBMBroker":
@@ -122,10 +123,12 @@ class HBMBroker:
     def stat(self) -> dict:
         return json.loads(_request(self.admin_path, "STAT"))
 
-    def stop(self) -> None:
+    def stop(self) -> int | None:
+        """Stop the broker; returns its exit status (SIGTERM ends it cleanly: 0). Its stderr is
+        kept in ``last_stderr``."""
         p = self.proc
         if p is None:
-            return
+            return None
         if p.poll() is None:
             p.terminate()
             try:
@@ -133,7 +136,12 @@ class HBMBroker:
             except subprocess.TimeoutExpired:
                 p.kill()
                 p.wait()
+        try:
+            self.last_stderr = p.stderr.read() if p.stderr else ""
+        except (OSError, ValueError):
+            self.last_stderr = ""
         self.proc = None
+        return p.returncode
 
 
 class HBMGranter:

@@ -149,3 +149,39 @@ def test_launcher_brings_up_the_broker_of_every_gpu_by_pci_address(tmp_path):
         assert r["arena"] == 1 and r["nonzero"] == 0
     finally:
         sup.stop()
+
+
+def test_broker_under_asan(tmp_path, monkeypatch):
+    """The broker built with ASan+UBSan (host code: it is compiled by g++, the scrub is a HIP
+    runtime memset), through grants, takes, a waiting take and releases, against the real HIP
+    runtime. Built beforehand: ``python native/build.py hbmbroker --sanitize asan``."""
+    from aliyun_gpushare_device_plugin_amd.quota.hbmbroker import HBMBroker
+    from aliyun_gpushare_device_plugin_amd.utils.native import NATIVE_DIR
+
+    exe = os.path.join(NATIVE_DIR, "asan", "gpushare-hbm-broker")
+    if not os.path.exists(exe):
+        pytest.skip("ASan broker not built")
+    monkeypatch.setenv("GPUSHARE_HBM_BROKER_EXE", exe)
+    monkeypatch.setenv("ASAN_OPTIONS", "detect_leaks=0:halt_on_error=1")
+    monkeypatch.setenv("UBSAN_OPTIONS", "halt_on_error=1:print_stacktrace=1")
+    b = HBMBroker(str(tmp_path / "hbm.sock"), device=0, gib=8, wait_s=20)
+    b.start()
+    rc = None
+    try:
+        b.grant("s" * 32, 6 * GIB)
+        holder = _tenant(b, "s" * 32, "hold")
+        assert json.loads(holder.stdout.readline())["arena"] == 1
+        b.grant("t" * 32, 6 * GIB)
+        waiter = _tenant(b, "t" * 32, "check")
+        time.sleep(1.0)
+        holder.stdin.write("\n")
+        holder.stdin.flush()
+        holder.wait(60)
+        r = _result(waiter)
+        assert r["arena"] == 1 and r["nonzero"] == 0
+        st = b.stat()
+        assert st["takes"] == 2 and st["releases"] == 2
+    finally:
+        rc = b.stop()
+    assert rc == 0, b.last_stderr[-3000:]
+    assert "AddressSanitizer" not in b.last_stderr and "runtime error" not in b.last_stderr
