@@ -163,8 +163,23 @@ hipError_t hipMemAddressReserve(void** p, size_t n, size_t al, void* addr, unsig
   *p = m; return 0;
 }
 hipError_t hipMemAddressFree(void* p, size_t n) { munmap(p, n); return 0; }
-hipError_t hipMemMap(void* p, size_t n, size_t off, uint64_t h, unsigned long long fl) { return (h & IMPORTED) ? 0 : 1; }
+hipError_t hipMemMap(void* p, size_t n, size_t off, uint64_t h, unsigned long long fl) { return 0; }
 hipError_t hipMemUnmap(void* p, size_t n) { return 0; }
 hipError_t hipMemSetAccess(void* p, size_t n, const void* d, size_t c) { return 0; }
 hipError_t hipGetDevice(int* d) { *d = 0; return 0; }
 hipError_t hipDeviceSynchronize(void) { return 0; }
+/* what the HBM broker (native/hbmbroker) needs besides the above: exported handles are memfds,
+   the scrub (hipMemsetAsync) is counted, not performed (the reserved range is not accessible) */
+hipError_t hipMemGetAllocationGranularity(size_t* g, const void* prop, int opt) { *g = 4096; return 0; }
+hipError_t hipMemExportToShareableHandle(void* out, uint64_t h, int type, unsigned long long fl) {
+  int fd = (int)syscall(SYS_memfd_create, "fake-vram", 0);
+  if (fd < 0) return 1;
+  *(int*)out = fd; return 0;
+}
+static size_t g_memset_bytes = 0;
+hipError_t hipMemsetAsync(void* p, int v, size_t n, void* s) { __atomic_add_fetch(&g_memset_bytes, n, __ATOMIC_RELAXED); return 0; }
+hipError_t hipStreamCreateWithFlags(void** s, unsigned f) { *s = (void*)0x1; return 0; }
+hipError_t hipStreamSynchronize(void* s) { return 0; }
+hipError_t hipSetDevice(int d) { return 0; }
+hipError_t hipDeviceGetByPCIBusId(int* d, const char* bdf) { *d = 0; return 0; }
+const char* hipGetErrorString(hipError_t e) { return "fake hip error"; }
