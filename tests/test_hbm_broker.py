@@ -56,6 +56,17 @@ def broker(tmp_path):
     b.stop()
 
 
+def _settled(broker, timeout=5.0) -> dict:
+    """The broker's counters once no released granule is quarantined any more (a retired
+    tenant's references drop when the kernel has torn its process down)."""
+    deadline = time.time() + timeout
+    st = broker.stat()
+    while st["quarantined"] and time.time() < deadline:
+        time.sleep(0.02)
+        st = broker.stat()
+    return st
+
+
 def _tenant(broker, token, mode, **kw):
     from aliyun_gpushare_device_plugin_amd.utils.native import ensure_built
 
@@ -81,7 +92,7 @@ def test_the_next_pod_sees_only_zeros(broker):
     assert broker.grant("b" * 32, 6 * GIB) == 6
     b = _result(_tenant(broker, "b" * 32, "check"))
     assert b["arena"] == 1 and b["nonzero"] == 0
-    st = broker.stat()
+    st = _settled(broker)
     assert st["takes"] == 2 and st["releases"] == 2 and st["free"] == st["granules"]
     assert st["scrubbed_bytes"] >= 12 * GIB
 
@@ -185,3 +196,36 @@ def test_broker_under_asan(tmp_path, monkeypatch):
         rc = b.stop()
     assert rc == 0, b.last_stderr[-3000:]
     assert "AddressSanitizer" not in b.last_stderr and "runtime error" not in b.last_stderr
+
+
+def test_granules_a_tenant_still_refers_to_are_not_lent_again(broker):
+    """A tenant that keeps its granules' dma-buf fds (or hands them to another process) after
+    its connection ends must not share them with the next pod: the broker sees the references
+    (the dma-buf's fdinfo count), keeps the granules out of the free list, and scrubs and lends
+    them only once the last reference is gone."""
+    import socket
+
+    broker.grant("q" * 32, 2 * GIB)
+    s = socket.socket(socket.AF_UNIX)
+    s.settimeout(10)
+    s.connect(broker.socket_path)
+    s.sendall(b"TAKE " + b"q" * 32 + b"\n")
+    head = b""
+    while not head.endswith(b"\n"):
+        head += s.recv(1)
+    assert head.decode().startswith("FDS 2 ")
+    _, fds, _, _ = socket.recv_fds(s, 1, 200)
+    assert len(fds) == 2
+    s.close()                                    # released, but the fds are still held here
+    deadline = time.time() + 5
+    while broker.stat()["releases"] < 1 and time.time() < deadline:
+        time.sleep(0.05)
+    st = broker.stat()
+    assert st["quarantined"] == 2 and st["free"] == st["granules"] - 2
+    for fd in fds:
+        os.close(fd)
+    deadline = time.time() + 5
+    while broker.stat()["quarantined"] and time.time() < deadline:
+        time.sleep(0.05)
+    st = broker.stat()
+    assert st["quarantined"] == 0 and st["free"] == st["granules"] and st["quarantined_total"] == 2
