@@ -59,6 +59,16 @@ def _arena_release():
         return None
     f.restype = ctypes.c_int
     r = f()
+    if r == -1:
+        # still live in the arena: torch's BLAS workspaces outlive empty_cache()
+        import torch
+
+        try:
+            torch._C._cuda_clearCublasWorkspaces()
+        except (AttributeError, RuntimeError):
+            pass
+        torch.cuda.empty_cache()
+        r = f()
     return None if r == 0 else r == 1
 
 
