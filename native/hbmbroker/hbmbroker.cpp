@@ -8,39 +8,65 @@
 //
 // Isolation: a pod receives ONLY the fds of its own granules (SCM_RIGHTS) and maps them into its
 // own address space; it cannot name another pod's granules. The amount is set by the granter
-// (the device plugin's Allocate, or the bench acting for it) on an admin socket that only root
-// can open, and a pod takes its grant with its token (again after a container restart).
+// (the device plugin) on an admin socket that lives outside every directory mounted into a
+// container (mode 0600, and the peer's SO_PEERCRED uid must be the broker's or root); a pod takes
+// its grant with its token (again after a container restart).
 //
-// Protocol: one text line per connection's request.
-//   admin socket  <sock>.admin (0600):  "GRANT <token> <bytes>\n"  -> "OK <granules>\n" | "ERR ...\n"
-//                                       "STAT\n"                   -> one JSON line
-//   pod socket    <sock>       (0666):  "TAKE <token>\n"           -> "FDS <n> <granule bytes>\n",
-//                                        then n fds (batches of <= 200, one byte each); the
-//                                        connection stays open: its end (close, exit, crash)
-//                                        returns the granules, which are scrubbed first.
-// A TAKE whose grant has not arrived yet, or whose granules are still held by a retiring pod,
-// waits (up to --wait-s) instead of failing: the pod's runtime may start before the retired pod
-// is gone, as it does on a node.
+// Protocol: one text line per request.
+//   admin socket (--admin-socket, 0600):
+//     "GRANT <token> <bytes>\n" -> "OK <granules>\n" | "ERR ...\n"   (a repeated grant refreshes it)
+//     "REVOKE <token>\n"        -> "OK <held>\n": the token can never be taken again; a process
+//                                  holding it keeps its granules until its connection ends
+//     "LIST\n"                  -> one JSON line {"boot": .., "grants": {token: granules, ..}}
+//     "STAT\n"                  -> one JSON line of counters, with this process's "boot" id
+//   pod socket (--socket, 0666):
+//     "TAKE <token>\n"          -> "FDS <n> <granule bytes>\n", then n fds (batches of <= 200,
+//                                  one byte each); the connection stays open: its end (close,
+//                                  exit, crash) returns the granules, which are scrubbed first.
+// A TAKE whose granules are still held by a retiring pod waits (up to --wait-s), and one whose
+// grant has not arrived yet waits up to --ungranted-wait-s (a broker that just restarted is
+// re-granted by the plugin within a poll interval): the pod's runtime may start before the
+// retired pod is gone, or before the plugin has seen this broker, as on a booting node.
 //
-//   gpushare-hbm-broker --socket /run/gpushare/hbm0.sock [--device 0 | --pci-bus-id 0000:05:00.0]
-//                       [--gib N | --reserve-gib R]
-//                       [--granule-mib 1024] [--wait-s 30] [--grant-ttl-s 600]
+// The boot id changes with every start. The plugin polls STAT, and on a new boot id it re-grants
+// every live pod's token: a broker restart loses no grant that a pod still needs.
+//
+// Scrubs are asynchronous: a released pod's granules are zeroed by hipMemsetAsync on the broker's
+// stream and lent again once the stream's event has completed, so GRANT, TAKE and STAT are
+// served while the GPU zeroes.
+//
+// Release policy (--release-policy): before a released granule is lent again, "refs" waits until
+// no reference to its dma-buf is left outside the broker (fdinfo "count:"), "exit" waits until
+// the holding process has exited (pidfd), "trust" lends it at once (tests only). The default
+// "auto" is refs where the kernel reports the count, else exit.
+//
+//   gpushare-hbm-broker --socket /run/gpushare/hbm/gpu0/hbm0.sock
+//                       --admin-socket /run/gpushare/hbm/admin/hbm0.sock
+//                       [--device 0 | --pci-bus-id 0000:05:00.0] [--gib N | --reserve-gib R]
+//                       [--granule-mib 1024] [--wait-s 30] [--ungranted-wait-s 10]
+//                       [--grant-ttl-s 0] [--max-clients 1024] [--max-per-peer 8]
+//                       [--request-timeout-s 2] [--release-policy auto]
 #include <hip/hip_runtime.h>
 
+#include <fcntl.h>
 #include <poll.h>
 #include <signal.h>
 #include <sys/socket.h>
 #include <sys/stat.h>
+#include <sys/syscall.h>
 #include <sys/un.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <cerrno>
 #include <chrono>
+#include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <map>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -65,7 +91,7 @@ volatile sig_atomic_t g_stop = 0;
 void on_signal(int) { g_stop = 1; }
 
 int listen_unix(const std::string& path, mode_t mode) {
-  int s = socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  int s = socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC | SOCK_NONBLOCK, 0);
   sockaddr_un a{};
   a.sun_family = AF_UNIX;
   if (path.size() >= sizeof a.sun_path) {
@@ -74,7 +100,11 @@ int listen_unix(const std::string& path, mode_t mode) {
   }
   std::memcpy(a.sun_path, path.c_str(), path.size() + 1);
   unlink(path.c_str());
-  if (bind(s, reinterpret_cast<sockaddr*>(&a), sizeof a) || listen(s, 64)) {
+  // created with the final mode: no window in which the admin socket is open to everyone
+  mode_t old = umask(0777 & ~mode);
+  int rc = bind(s, reinterpret_cast<sockaddr*>(&a), sizeof a);
+  umask(old);
+  if (rc || listen(s, 128)) {
     std::perror(path.c_str());
     std::exit(2);
   }
@@ -82,46 +112,108 @@ int listen_unix(const std::string& path, mode_t mode) {
   return s;
 }
 
+std::string boot_id() {
+  unsigned char b[8] = {0};
+  int fd = open("/dev/urandom", O_RDONLY | O_CLOEXEC);
+  if (fd < 0 || read(fd, b, sizeof b) != ssize_t(sizeof b)) {
+    uint64_t t = uint64_t(now_s() * 1e9) ^ (uint64_t(getpid()) << 40);
+    std::memcpy(b, &t, sizeof b);
+  }
+  if (fd >= 0) close(fd);
+  char s[17];
+  for (int i = 0; i < 8; ++i) std::snprintf(s + 2 * i, 3, "%02x", b[i]);
+  return s;
+}
+
+int pidfd_of(pid_t pid) {
+#ifdef SYS_pidfd_open
+  if (pid > 0) return int(syscall(SYS_pidfd_open, pid, 0));
+#endif
+  (void)pid;
+  return -1;
+}
+
+bool exited(int pidfd) {  // a pidfd polls readable once its process has exited
+  pollfd p{pidfd, POLLIN, 0};
+  return poll(&p, 1, 0) > 0;
+}
+
+bool valid_token(const char* t) {
+  size_t n = std::strlen(t);
+  if (n == 0 || n > 128) return false;
+  for (size_t i = 0; i < n; ++i) {
+    char c = t[i];
+    if (!((c >= '0' && c <= '9') || (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || c == '-' || c == '_'))
+      return false;
+  }
+  return true;
+}
+
 struct Client {
   int fd = -1;
   bool admin = false;
   std::string in;
+  double since = 0;       // connected at
+  bool asked = false;     // a complete request line has arrived
+  pid_t pid = 0;          // SO_PEERCRED (0: the peer is in another PID namespace)
+  uid_t uid = 0;
+  int pidfd = -1;         // release policy "exit": the holder's process, opened at its TAKE
   // a pod: the granules it holds (indices), or the token it waits for
   std::vector<int> held;
-  std::string token;    // the grant it holds
-  std::string waiting;  // token of a TAKE not yet served
+  std::string token;      // the grant it holds
+  std::string waiting;    // token of a TAKE not yet served
   double wait_since = 0;
 };
+
+enum Policy { kRefs, kExit, kTrust };
 
 struct Broker {
   int device = 0;
   size_t gran = 1ull << 30;
   int count = 0;
-  double wait_s = 30.0;
+  double wait_s = 30.0, ungranted_wait_s = 10.0, request_timeout_s = 2.0;
+  size_t max_clients = 1024, max_per_peer = 8;
+  Policy policy = kRefs;
+  std::string boot = boot_id();
   std::vector<hipMemGenericAllocationHandle_t> h;
   std::vector<int> fds;
   char* base = nullptr;  // every granule mapped here, for the scrub
   hipStream_t stream = nullptr;
   std::deque<int> free_list;
-  // granules whose dma-buf something besides the broker still refers to (a tenant kept an fd, or
-  // passed it on): not lent again until that reference is gone, then scrubbed again
-  std::vector<std::vector<int>> quarantine;  // by release: one tenant's granules go together
-  unsigned long long quarantined_total = 0;
+  // released granules being zeroed: lent again once their event has completed
+  struct Scrub {
+    std::vector<int> idx;
+    hipEvent_t ev;
+    double t0;
+  };
+  std::deque<Scrub> scrubbing;
+  // granules not lent again until their holder is really gone (see the release policy); one
+  // release's granules go together
+  struct Held {
+    std::vector<int> idx;
+    int pidfd = -1;  // kExit: the holder's process
+  };
+  std::vector<Held> quarantine;
+  unsigned long long quarantined_total = 0, lost = 0;
   std::vector<int> base_refs;  // each granule's references with no tenant (the broker's own export)
   // A grant belongs to the pod, not to one process: a TAKE holds it while its connection lives,
   // and a restarted container (same env, same token) takes it again once the old process's
-  // granules are back. It expires grant_ttl_s after it was granted or last released.
+  // granules are back. It lives until the plugin revokes it (or grant_ttl_s after it was
+  // granted or last released, when a TTL is set).
   struct Grant {
     int granules;
     double at;
     int holder = -1;  // fd of the connection holding it
   };
   std::map<std::string, Grant> grants;
-  double grant_ttl_s = 600.0;
+  std::set<std::string> revoked;
+  std::deque<std::string> revoked_order;  // bounded: the oldest revocations are forgotten
+  double grant_ttl_s = 0.0;
   unsigned long long expired = 0;
   std::map<int, Client> clients;
   // stats
-  unsigned long long takes = 0, releases = 0, refused = 0, timeouts = 0;
+  unsigned long long takes = 0, releases = 0, refused = 0, timeouts = 0, busy = 0, idle_dropped = 0,
+                     revokes = 0, peer_refused = 0;
   double scrub_s_total = 0, scrub_s_last = 0, setup_s = 0;
   unsigned long long scrubbed_bytes = 0;
 
@@ -161,9 +253,9 @@ struct Broker {
     setup_s = now_s() - t0;
   }
 
+  // zero the granules on the broker's stream; they are lent again from reap_scrubs()
   void scrub(const std::vector<int>& idx) {
     if (idx.empty()) return;
-    double t0 = now_s();
     std::vector<int> s(idx);
     std::sort(s.begin(), s.end());
     for (size_t i = 0; i < s.size();) {  // one memset per run of adjacent granules
@@ -172,13 +264,48 @@ struct Broker {
       CK(hipMemsetAsync(base + size_t(s[i]) * gran, 0, gran * (j - i), stream));
       i = j;
     }
-    CK(hipStreamSynchronize(stream));
-    scrub_s_last = now_s() - t0;
-    scrub_s_total += scrub_s_last;
-    scrubbed_bytes += gran * idx.size();
+    hipEvent_t ev;
+    CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    CK(hipEventRecord(ev, stream));
+    scrubbing.push_back({std::move(s), ev, now_s()});
   }
 
-  static void reply(int fd, const std::string& s) { (void)!send(fd, s.data(), s.size(), MSG_NOSIGNAL); }
+  // scrubs whose event has completed (they complete in stream order): granules back to the free list
+  bool reap_scrubs() {
+    bool any = false;
+    while (!scrubbing.empty()) {
+      hipError_t q = hipEventQuery(scrubbing.front().ev);
+      if (q == hipErrorNotReady) break;
+      if (q != hipSuccess) die("hipEventQuery(scrub)", q);
+      Scrub& s = scrubbing.front();
+      CK(hipEventDestroy(s.ev));
+      scrub_s_last = now_s() - s.t0;
+      scrub_s_total += scrub_s_last;
+      scrubbed_bytes += gran * s.idx.size();
+      for (int i : s.idx) free_list.push_back(i);
+      scrubbing.pop_front();
+      any = true;
+    }
+    return any;
+  }
+
+  static void reply(int fd, const std::string& s) {
+    // admin and pod replies are short (LIST aside) and the peer reads them at once; a peer that
+    // does not read is dropped by its request deadline, never waited for
+    size_t off = 0;
+    while (off < s.size()) {
+      ssize_t n = send(fd, s.data() + off, s.size() - off, MSG_NOSIGNAL);
+      if (n > 0) {
+        off += size_t(n);
+        continue;
+      }
+      if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
+        pollfd p{fd, POLLOUT, 0};
+        if (poll(&p, 1, 100) > 0) continue;
+      }
+      return;
+    }
+  }
 
   bool send_fds(int fd, const std::vector<int>& idx) {
     char head[64];
@@ -213,7 +340,9 @@ struct Broker {
       if (!kv.second.waiting.empty()) order.push_back({kv.second.wait_since, kv.first});
     std::sort(order.begin(), order.end());
     for (auto& o : order) {
-      Client& c = clients[o.second];
+      auto ci = clients.find(o.second);
+      if (ci == clients.end()) continue;
+      Client& c = ci->second;
       auto g = grants.find(c.waiting);
       if (g == grants.end() || g->second.holder >= 0) continue;  // not granted yet, or held
       if (size_t(g->second.granules) > free_list.size()) break;  // keep arrival order: no overtaking
@@ -223,6 +352,7 @@ struct Broker {
         free_list.pop_front();
       }
       g->second.holder = o.second;
+      if (policy == kExit && c.pidfd < 0) c.pidfd = pidfd_of(c.pid);  // while it is surely alive
       c.token = c.waiting;
       c.waiting.clear();
       c.held = idx;
@@ -233,7 +363,6 @@ struct Broker {
 
   // other references to granule i's dma-buf: the kernel's fdinfo "count" is the file's
   // reference count without procfs's own; the broker's exported fd is one of them. -1 = unknown
-  // (no such field: then the release is trusted, as before)
   int refs(int i) const {
     char path[64];
     std::snprintf(path, sizeof path, "/proc/self/fdinfo/%d", fds[i]);
@@ -250,54 +379,78 @@ struct Broker {
   // references beyond the broker's own: a tenant (or whoever it passed the fd to) still has it
   bool outside(int i) const {
     int r = refs(i);
-    return r >= 0 && size_t(i) < base_refs.size() && base_refs[i] >= 0 && r > base_refs[i];
+    return r < 0 || size_t(i) >= base_refs.size() || base_refs[i] < 0 || r > base_refs[i];
   }
 
-  void release(const std::vector<int>& idx) {
-    std::vector<int> clean, held;
-    for (int i : idx) (outside(i) ? held : clean).push_back(i);
+  // the granules a connection held; takes over `pfd` (the holder's pidfd, or -1)
+  void release(const std::vector<int>& idx, int pfd) {
+    if (policy == kTrust) {
+      if (pfd >= 0) close(pfd);
+      scrub(idx);
+      return;
+    }
+    if (policy == kExit) {
+      if (pfd < 0) {  // the holder cannot be followed: never lent again (fail closed)
+        lost += idx.size();
+        std::fprintf(stderr, "gpushare-hbm-broker: %zu granules of an untraceable holder are not lent again\n",
+                     idx.size());
+        return;
+      }
+      quarantined_total += idx.size();
+      quarantine.push_back({idx, pfd});
+      return;
+    }
+    if (pfd >= 0) close(pfd);
+    std::vector<int> clean, kept;
+    for (int i : idx) (outside(i) ? kept : clean).push_back(i);
     scrub(clean);
-    for (int i : clean) free_list.push_back(i);
-    if (!held.empty()) {
-      quarantined_total += held.size();
-      quarantine.push_back(std::move(held));
+    if (!kept.empty()) {
+      quarantined_total += kept.size();
+      quarantine.push_back({std::move(kept), -1});
     }
   }
 
   size_t quarantined() const {
     size_t n = 0;
-    for (auto& g : quarantine) n += g.size();
+    for (auto& g : quarantine) n += g.idx.size();
     return n;
   }
 
-  // quarantined granules whose last outside reference is gone: scrub (again) and lend. A
-  // release's granules lose their references together (the tenant's process teardown), so
-  // while the group's first one is still referenced the rest are not read.
-  bool sweep_quarantine() {
-    bool any = false;
-    std::vector<std::vector<int>> keep;
+  // quarantined granules whose holder is really gone: scrub (again) and lend. A release's
+  // granules lose their references together (the tenant's process teardown), so while the
+  // group's first one is still referenced the rest are not read.
+  void sweep_quarantine() {
+    std::vector<Held> keep;
     for (auto& g : quarantine) {
-      if (outside(g.front())) {
+      if (g.pidfd >= 0) {
+        if (!exited(g.pidfd)) {
+          keep.push_back(std::move(g));
+          continue;
+        }
+        close(g.pidfd);
+        scrub(g.idx);
+        continue;
+      }
+      if (outside(g.idx.front())) {
         keep.push_back(std::move(g));
         continue;
       }
       std::vector<int> back, still;
-      for (int i : g) (outside(i) ? still : back).push_back(i);
+      for (int i : g.idx) (outside(i) ? still : back).push_back(i);
       scrub(back);
-      for (int i : back) free_list.push_back(i);
-      any = any || !back.empty();
-      if (!still.empty()) keep.push_back(std::move(still));
+      if (!still.empty()) keep.push_back({std::move(still), -1});
     }
     quarantine.swap(keep);
-    return any;
   }
 
   void drop(int fd) {
     auto it = clients.find(fd);
     if (it == clients.end()) return;
     if (!it->second.held.empty()) {
-      release(it->second.held);
+      release(it->second.held, it->second.pidfd);
       ++releases;
+    } else if (it->second.pidfd >= 0) {
+      close(it->second.pidfd);
     }
     auto g = it->second.token.empty() ? grants.end() : grants.find(it->second.token);
     if (g != grants.end() && g->second.holder == fd) {
@@ -315,43 +468,109 @@ struct Broker {
     return m;
   }
 
+  const char* policy_name() const { return policy == kRefs ? "refs" : policy == kExit ? "exit" : "trust"; }
+
   std::string stat() const {
-    size_t held = 0, waiting = 0;
+    size_t held = 0, waiting = 0, scrub_n = 0;
     for (auto& kv : clients) {
       held += kv.second.held.size();
       waiting += !kv.second.waiting.empty();
     }
-    char b[1024];
+    for (auto& s : scrubbing) scrub_n += s.idx.size();
+    char b[1536];
     std::snprintf(b, sizeof b,
-                  "{\"device\": %d, \"granule_bytes\": %zu, \"granules\": %d, \"free\": %zu, \"held\": %zu, "
-                  "\"waiting\": %zu, \"grants\": %zu, \"takes\": %llu, \"releases\": %llu, \"refused\": %llu, "
-                  "\"timeouts\": %llu, \"expired\": %llu, \"quarantined\": %zu, \"quarantined_total\": %llu, "
-                  "\"held_refs_max\": %d, \"base_refs\": %d, \"scrubbed_bytes\": %llu, \"scrub_ms_total\": %.3f, \"scrub_ms_last\": %.3f, "
-                  "\"setup_ms\": %.1f}\n",
-                  device, gran, count, free_list.size(), held, waiting, grants.size(), takes, releases, refused,
-                  timeouts, expired, quarantined(), quarantined_total, held_refs_max(), base_refs.empty() ? -1 : base_refs[0], scrubbed_bytes, scrub_s_total * 1e3, scrub_s_last * 1e3, setup_s * 1e3);
+                  "{\"boot\": \"%s\", \"device\": %d, \"granule_bytes\": %zu, \"granules\": %d, \"free\": %zu, "
+                  "\"held\": %zu, \"scrubbing\": %zu, \"waiting\": %zu, \"grants\": %zu, \"takes\": %llu, "
+                  "\"releases\": %llu, \"refused\": %llu, \"revokes\": %llu, \"revoked\": %zu, \"timeouts\": %llu, "
+                  "\"expired\": %llu, \"busy\": %llu, \"idle_dropped\": %llu, \"peer_refused\": %llu, "
+                  "\"clients\": %zu, \"quarantined\": %zu, \"quarantined_total\": %llu, \"lost\": %llu, "
+                  "\"release_policy\": \"%s\", \"held_refs_max\": %d, \"base_refs\": %d, \"scrubbed_bytes\": %llu, "
+                  "\"scrub_ms_total\": %.3f, \"scrub_ms_last\": %.3f, \"setup_ms\": %.1f}\n",
+                  boot.c_str(), device, gran, count, free_list.size(), held, scrub_n, waiting, grants.size(), takes,
+                  releases, refused, revokes, revoked.size(), timeouts, expired, busy, idle_dropped, peer_refused,
+                  clients.size(), quarantined(), quarantined_total, lost, policy_name(), held_refs_max(),
+                  base_refs.empty() ? -1 : base_refs[0], scrubbed_bytes, scrub_s_total * 1e3, scrub_s_last * 1e3,
+                  setup_s * 1e3);
     return b;
+  }
+
+  std::string list() const {
+    std::string s = "{\"boot\": \"" + boot + "\", \"grants\": {";
+    bool first = true;
+    for (auto& kv : grants) {
+      s += (first ? "\"" : ", \"") + kv.first + "\": " + std::to_string(kv.second.granules);
+      first = false;
+    }
+    return s + "}}\n";
+  }
+
+  void remember_revoked(const std::string& t) {
+    if (revoked.insert(t).second) {
+      revoked_order.push_back(t);
+      while (revoked_order.size() > 65536) {
+        revoked.erase(revoked_order.front());
+        revoked_order.pop_front();
+      }
+    }
   }
 
   void on_line(int fd, const std::string& line) {
     Client& c = clients[fd];
+    c.asked = true;
     char tok[129] = {0};
     unsigned long long bytes = 0;
-    if (c.admin && std::sscanf(line.c_str(), "GRANT %128s %llu", tok, &bytes) == 2) {
-      int n = int((bytes + gran - 1) / gran);
-      if (n <= 0 || n > count) {
+    char extra = 0;
+    if (c.admin && std::sscanf(line.c_str(), "GRANT %128s %llu %c", tok, &bytes, &extra) == 2 && valid_token(tok)) {
+      // in granules, without overflow: bytes beyond the broker are refused before rounding
+      unsigned long long cap = (unsigned long long)count * (unsigned long long)gran;
+      if (bytes == 0 || bytes > cap) {
         ++refused;
         reply(fd, "ERR size\n");
         return;
       }
-      auto& gr = grants[tok];  // a repeated grant (a re-prepared answer) refreshes it
+      int n = int(bytes / gran + (bytes % gran ? 1 : 0));
+      auto& gr = grants[tok];  // a repeated grant (a re-prepared answer, a re-grant) refreshes it
       gr.granules = n;
       gr.at = now_s();
+      if (revoked.erase(tok)) revoked_order.erase(std::find(revoked_order.begin(), revoked_order.end(), std::string(tok)));
       reply(fd, "OK " + std::to_string(n) + "\n");
       serve_waiting();
+    } else if (c.admin && std::sscanf(line.c_str(), "REVOKE %128s %c", tok, &extra) == 1 && valid_token(tok)) {
+      std::string t(tok);
+      int held = 0;
+      auto g = grants.find(t);
+      if (g != grants.end()) {
+        if (g->second.holder >= 0) {
+          auto h = clients.find(g->second.holder);
+          if (h != clients.end()) {
+            h->second.token.clear();  // its end returns the granules, the grant is gone already
+            held = int(h->second.held.size());
+          }
+        }
+        grants.erase(g);
+      }
+      remember_revoked(t);
+      ++revokes;
+      std::vector<int> waiters;
+      for (auto& kv : clients)
+        if (kv.second.waiting == t) waiters.push_back(kv.first);
+      for (int w : waiters) {
+        reply(w, "ERR revoked\n");
+        drop(w);
+      }
+      reply(fd, "OK " + std::to_string(held) + "\n");
+    } else if (c.admin && line == "LIST") {
+      reply(fd, list());
     } else if (c.admin && line == "STAT") {
       reply(fd, stat());
-    } else if (!c.admin && c.held.empty() && c.waiting.empty() && std::sscanf(line.c_str(), "TAKE %128s", tok) == 1) {
+    } else if (!c.admin && c.held.empty() && c.waiting.empty() &&
+               std::sscanf(line.c_str(), "TAKE %128s %c", tok, &extra) == 1 && valid_token(tok)) {
+      if (revoked.count(tok)) {
+        ++refused;
+        reply(fd, "ERR revoked\n");
+        drop(fd);
+        return;
+      }
       c.waiting = tok;
       c.wait_since = now_s();
       serve_waiting();
@@ -360,12 +579,43 @@ struct Broker {
       reply(fd, "ERR request\n");
     }
   }
+
+  // one connection from a listener; false when there is none left to accept
+  bool accept_one(int ls, bool admin) {
+    int c = accept4(ls, nullptr, nullptr, SOCK_CLOEXEC | SOCK_NONBLOCK);
+    if (c < 0) return false;
+    ucred cr{};
+    socklen_t cl = sizeof cr;
+    bool have_cred = getsockopt(c, SOL_SOCKET, SO_PEERCRED, &cr, &cl) == 0;
+    if (admin && (!have_cred || (cr.uid != 0 && cr.uid != geteuid()))) {
+      ++peer_refused;  // the socket's mode already says this; the peer's credentials say it again
+      reply(c, "ERR peer\n");
+      close(c);
+      return true;
+    }
+    size_t same = 0;
+    if (!admin && have_cred && cr.pid > 0)
+      for (auto& kv : clients) same += !kv.second.admin && kv.second.pid == cr.pid;
+    if (clients.size() >= max_clients || same >= max_per_peer) {
+      ++busy;
+      reply(c, "ERR busy\n");
+      close(c);
+      return true;
+    }
+    Client& n = clients[c];
+    n.fd = c;
+    n.admin = admin;
+    n.since = now_s();
+    n.pid = have_cred ? cr.pid : 0;
+    n.uid = have_cred ? cr.uid : 0;
+    return true;
+  }
 };
 
 }  // namespace
 
 int main(int argc, char** argv) {
-  std::string sock, pci;
+  std::string sock, admin, pci, policy = "auto";
   Broker b;
   double gib = 0, reserve_gib = 16;
   size_t gran_mib = 1024;
@@ -373,23 +623,31 @@ int main(int argc, char** argv) {
     std::string k = argv[i];
     const char* v = argv[i + 1];
     if (k == "--socket") sock = v;
+    else if (k == "--admin-socket") admin = v;
     else if (k == "--device") b.device = std::atoi(v);
     else if (k == "--pci-bus-id") pci = v;  // the GPU by PCI address (HIP and SMI orders differ)
     else if (k == "--gib") gib = std::atof(v);
     else if (k == "--reserve-gib") reserve_gib = std::atof(v);
     else if (k == "--granule-mib") gran_mib = std::strtoull(v, nullptr, 10);
     else if (k == "--wait-s") b.wait_s = std::atof(v);
+    else if (k == "--ungranted-wait-s") b.ungranted_wait_s = std::atof(v);
     else if (k == "--grant-ttl-s") b.grant_ttl_s = std::atof(v);
+    else if (k == "--max-clients") b.max_clients = std::strtoull(v, nullptr, 10);
+    else if (k == "--max-per-peer") b.max_per_peer = std::strtoull(v, nullptr, 10);
+    else if (k == "--request-timeout-s") b.request_timeout_s = std::atof(v);
+    else if (k == "--release-policy") policy = v;
     else {
       std::fprintf(stderr, "gpushare-hbm-broker: unknown flag %s\n", k.c_str());
       return 2;
     }
   }
-  if (sock.empty()) {
-    std::fprintf(stderr, "usage: gpushare-hbm-broker --socket PATH [--device N | --pci-bus-id BDF] [--gib N | --reserve-gib N] "
-                         "[--granule-mib 1024] [--wait-s 30]\n");
+  if (sock.empty() || (policy != "auto" && policy != "refs" && policy != "exit" && policy != "trust")) {
+    std::fprintf(stderr, "usage: gpushare-hbm-broker --socket PATH [--admin-socket PATH] [--device N | --pci-bus-id BDF] "
+                         "[--gib N | --reserve-gib N] [--granule-mib 1024] [--wait-s 30] [--ungranted-wait-s 10] "
+                         "[--release-policy auto|refs|exit|trust]\n");
     return 2;
   }
+  if (admin.empty()) admin = sock + ".admin";
   b.gran = gran_mib << 20;
   if (!pci.empty()) CK(hipDeviceGetByPCIBusId(&b.device, pci.c_str()));
   CK(hipSetDevice(b.device));
@@ -398,32 +656,43 @@ int main(int argc, char** argv) {
   size_t total = gib > 0 ? size_t(gib * double(1ull << 30))
                          : (fr > size_t(reserve_gib * double(1ull << 30)) ? fr - size_t(reserve_gib * double(1ull << 30)) : 0);
   b.setup(total);
+  bool counted = !b.base_refs.empty() && b.base_refs[0] >= 0;
+  b.policy = policy == "refs" ? kRefs : policy == "exit" ? kExit : policy == "trust" ? kTrust : (counted ? kRefs : kExit);
+  if (b.policy == kRefs && !counted) {
+    std::fprintf(stderr, "gpushare-hbm-broker: --release-policy refs needs the dma-buf count in fdinfo, which this "
+                         "kernel does not report\n");
+    return 2;
+  }
   signal(SIGTERM, on_signal);
   signal(SIGINT, on_signal);
   signal(SIGPIPE, SIG_IGN);
   int pod_ls = listen_unix(sock, 0666);
-  int adm_ls = listen_unix(sock + ".admin", 0600);
-  std::printf("{\"ready\": true, \"socket\": \"%s\", \"granules\": %d, \"granule_bytes\": %zu, \"setup_ms\": %.1f}\n",
-              sock.c_str(), b.count, b.gran, b.setup_s * 1e3);
+  int adm_ls = listen_unix(admin, 0600);
+  std::printf("{\"ready\": true, \"boot\": \"%s\", \"socket\": \"%s\", \"admin_socket\": \"%s\", \"granules\": %d, "
+              "\"granule_bytes\": %zu, \"release_policy\": \"%s\", \"setup_ms\": %.1f}\n",
+              b.boot.c_str(), sock.c_str(), admin.c_str(), b.count, b.gran, b.policy_name(), b.setup_s * 1e3);
   std::fflush(stdout);
 
+  std::vector<pollfd> pf;
   while (!g_stop) {
-    std::vector<pollfd> pf{{pod_ls, POLLIN, 0}, {adm_ls, POLLIN, 0}};
+    pf.assign({{pod_ls, POLLIN, 0}, {adm_ls, POLLIN, 0}});
     for (auto& kv : b.clients) pf.push_back({kv.first, POLLIN, 0});
-    // a retired tenant's references drop when the kernel finishes tearing its process down:
-    // look often while granules wait for that, so the next pod's TAKE is not held up
-    int r = poll(pf.data(), pf.size(), b.quarantine.empty() ? 100 : 3);
-    if (r < 0) continue;
-    for (int k = 0; k < 2; ++k)
-      if (pf[k].revents & POLLIN) {
-        int c = accept4(pf[k].fd, nullptr, nullptr, SOCK_CLOEXEC);
-        if (c >= 0) b.clients[c].fd = c, b.clients[c].admin = (k == 1);
-      }
-    for (size_t k = 2; k < pf.size(); ++k) {
+    // scrubs complete on the GPU in a few ms, and a retired tenant's references drop when the
+    // kernel finishes tearing its process down: look often while granules wait for either
+    int timeout = !b.scrubbing.empty() ? 1 : !b.quarantine.empty() ? 3 : 100;
+    int r = poll(pf.data(), pf.size(), timeout);
+    if (r < 0 && errno != EINTR) break;
+    for (int k = 0; k < 2 && r > 0; ++k)
+      if (pf[k].revents & POLLIN)
+        for (int j = 0; j < 64 && b.accept_one(pf[k].fd, k == 1); ++j) {
+        }  // drain the backlog, bounded per pass
+    for (size_t k = 2; k < pf.size() && r > 0; ++k) {
       if (!pf[k].revents) continue;
       int fd = pf[k].fd;
+      if (!b.clients.count(fd)) continue;
       char buf[512];
       ssize_t n = recv(fd, buf, sizeof buf, 0);
+      if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) continue;
       if (n <= 0) {  // the pod is gone (or the admin hung up): scrub and return its granules
         b.drop(fd);
         b.serve_waiting();
@@ -442,29 +711,47 @@ int main(int argc, char** argv) {
         b.on_line(fd, line);
       }
     }
-    // TAKEs that waited too long are refused (their grant stays for a retry)
     double t = now_s();
-    std::vector<int> late;
-    for (auto& kv : b.clients)
-      if (!kv.second.waiting.empty() && t - kv.second.wait_since > b.wait_s) late.push_back(kv.first);
-    for (int fd : late) {
-      ++b.timeouts;
-      Broker::reply(fd, "ERR timeout\n");
-      b.drop(fd);
-    }
-    if (!b.quarantine.empty() && b.sweep_quarantine()) b.serve_waiting();
-    // grants of pods that never started (deleted before admission) do not pile up
-    for (auto it = b.grants.begin(); it != b.grants.end();) {
-      if (it->second.holder < 0 && t - it->second.at > b.grant_ttl_s) {
-        it = b.grants.erase(it);
-        ++b.expired;
-      } else {
-        ++it;
+    std::vector<int> late, idle;
+    for (auto& kv : b.clients) {
+      const Client& c = kv.second;
+      if (!c.waiting.empty()) {
+        // TAKEs that waited too long are refused (their grant stays for a retry); a TAKE with no
+        // grant at all gets a shorter deadline than one waiting for a retiring pod's granules
+        bool granted = b.grants.count(c.waiting) > 0;
+        if (t - c.wait_since > (granted ? b.wait_s : b.ungranted_wait_s)) late.push_back(kv.first);
+      } else if (!c.asked && t - c.since > b.request_timeout_s) {
+        idle.push_back(kv.first);  // connected, never asked: junk or a stuck peer
       }
     }
+    for (int fd : late) {
+      ++b.timeouts;
+      bool granted = b.grants.count(b.clients[fd].waiting) > 0;
+      Broker::reply(fd, granted ? "ERR timeout\n" : "ERR nogrant\n");
+      b.drop(fd);
+    }
+    for (int fd : idle) {
+      ++b.idle_dropped;
+      b.drop(fd);
+    }
+    bool back = b.reap_scrubs();
+    if (!b.quarantine.empty()) b.sweep_quarantine();
+    if (back || !late.empty()) b.serve_waiting();
+    // with a TTL, grants of pods that never started (deleted before admission) do not pile up;
+    // without one (the default) the plugin's revocations do that
+    if (b.grant_ttl_s > 0)
+      for (auto it = b.grants.begin(); it != b.grants.end();) {
+        if (it->second.holder < 0 && t - it->second.at > b.grant_ttl_s) {
+          it = b.grants.erase(it);
+          ++b.expired;
+        } else {
+          ++it;
+        }
+      }
   }
   for (auto it = b.clients.begin(); it != b.clients.end();) close((it++)->first);
+  if (!b.scrubbing.empty()) (void)hipStreamSynchronize(b.stream);
   unlink(sock.c_str());
-  unlink((sock + ".admin").c_str());
+  unlink(admin.c_str());
   return 0;
 }

@@ -183,3 +183,26 @@ hipError_t hipStreamSynchronize(void* s) { return 0; }
 hipError_t hipSetDevice(int d) { return 0; }
 hipError_t hipDeviceGetByPCIBusId(int* d, const char* bdf) { *d = 0; return 0; }
 const char* hipGetErrorString(hipError_t e) { return "fake hip error"; }
+/* events: hipEventRecord completes FAKE_HIP_EVENT_MS after it was recorded (0 = at once), so a
+   test can hold the broker's asynchronous scrub, or a stream-ordered free, in flight */
+#include <time.h>
+struct fake_event { double done_at; };
+static double fake_now(void) { struct timespec t; clock_gettime(CLOCK_MONOTONIC, &t); return t.tv_sec + t.tv_nsec * 1e-9; }
+hipError_t hipEventCreateWithFlags(void** e, unsigned f) {
+  struct fake_event* ev = calloc(1, sizeof *ev);
+  if (!ev) return 2;
+  *e = ev; return 0;
+}
+hipError_t hipEventCreate(void** e) { return hipEventCreateWithFlags(e, 0); }
+hipError_t hipEventRecord(void* e, void* s) {
+  const char* ms = getenv("FAKE_HIP_EVENT_MS");
+  ((struct fake_event*)e)->done_at = fake_now() + (ms ? atof(ms) : 0.0) / 1e3;
+  return 0;
+}
+hipError_t hipEventQuery(void* e) { return fake_now() >= ((struct fake_event*)e)->done_at ? 0 : 600; /* hipErrorNotReady */ }
+hipError_t hipEventSynchronize(void* e) {
+  double w = ((struct fake_event*)e)->done_at - fake_now();
+  if (w > 0) { struct timespec t = {(time_t)w, (long)((w - (time_t)w) * 1e9)}; nanosleep(&t, 0); }
+  return 0;
+}
+hipError_t hipEventDestroy(void* e) { free(e); return 0; }

@@ -1,6 +1,8 @@
 """The HBM broker's protocol on CPU: ``native/hbmbroker`` linked against the stub HIP runtime
-(tests/native/fake_hip.c, whose exported VMM handles are memfds). Grants, takes, waiting in
-arrival order, a container restart taking its grant again, timeouts, grant expiry, and hostile
+(tests/native/fake_hip.c, whose exported VMM handles are memfds and whose events complete after
+``FAKE_HIP_EVENT_MS``). Grants, takes, waiting in arrival order, a container restart taking its
+grant again, timeouts, REVOKE / LIST / boot id, the admin socket apart from the pod socket, caps
+on junk connections, scrubs that do not stall the event loop, the release policies, and hostile
 input on both sockets. The real runtime is covered by tests/test_hbm_broker.py on MI355X."""
 from __future__ import annotations
 
@@ -8,6 +10,7 @@ import json
 import os
 import socket
 import subprocess
+import sys
 import time
 
 import pytest
@@ -31,30 +34,36 @@ def broker_exe(tmp_path_factory):
     return str(exe), str(d)
 
 
+def _line(path, line, timeout=5.0):
+    s = socket.socket(socket.AF_UNIX)
+    s.settimeout(timeout)
+    s.connect(path)
+    s.sendall(line.encode() + b"\n")
+    out = b""
+    while not out.endswith(b"\n"):
+        c = s.recv(65536)
+        if not c:
+            break
+        out += c
+    s.close()
+    return out.decode().strip()
+
+
 class Broker:
-    def __init__(self, exe, path, gib=8, wait_s=1.0, ttl_s=600.0):
+    def __init__(self, exe, path, gib=8, wait_s=1.0, ttl_s=0.0, policy="trust", admin=None, extra=(), env=None):
         exe, libdir = exe
         self.path = path
+        self.admin_path = admin or path + ".admin"
         env = dict(os.environ, LD_LIBRARY_PATH=libdir, ASAN_OPTIONS="detect_leaks=0:halt_on_error=1",
-                   UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
-        self.p = subprocess.Popen([exe, "--socket", path, "--gib", str(gib), "--wait-s", str(wait_s),
-                                   "--grant-ttl-s", str(ttl_s)], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
-                                  text=True, env=env)
-        assert json.loads(self.p.stdout.readline())["ready"]
+                   UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1", **(env or {}))
+        self.p = subprocess.Popen([exe, "--socket", path, "--admin-socket", self.admin_path, "--gib", str(gib),
+                                   "--wait-s", str(wait_s), "--grant-ttl-s", str(ttl_s), "--release-policy", policy,
+                                   *extra], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
+        self.ready = json.loads(self.p.stdout.readline())
+        assert self.ready["ready"]
 
     def admin(self, line):
-        s = socket.socket(socket.AF_UNIX)
-        s.settimeout(5)
-        s.connect(self.path + ".admin")
-        s.sendall(line.encode() + b"\n")
-        out = b""
-        while not out.endswith(b"\n"):
-            c = s.recv(4096)
-            if not c:
-                break
-            out += c
-        s.close()
-        return out.decode().strip()
+        return _line(self.admin_path, line)
 
     def stat(self):
         return json.loads(self.admin("STAT"))
@@ -141,15 +150,194 @@ def test_takes_wait_for_granules_in_arrival_order(broker):
     second.close()
 
 
-def test_unknown_token_times_out_and_grants_expire(broker_exe, tmp_path):
-    b = Broker(broker_exe, str(tmp_path / "hbm1.sock"), wait_s=0.5, ttl_s=0.5)
+def test_ungranted_take_gets_a_short_deadline_and_a_late_grant_is_served(broker_exe, tmp_path):
+    b = Broker(broker_exe, str(tmp_path / "hbm1.sock"), wait_s=30.0, extra=("--ungranted-wait-s", "0.5"))
     try:
-        p = Pod(b.path, "never")
-        assert p.result()[0] == "ERR timeout"
+        t = time.monotonic()
+        assert Pod(b.path, "never").result()[0] == "ERR nogrant"               # not the 30 s of --wait-s
+        assert time.monotonic() - t < 3.0
+        p = Pod(b.path, "l" * 32)                                             # the grant comes after the TAKE
+        time.sleep(0.2)
+        assert b.admin(f"GRANT {'l' * 32} {GIB}") == "OK 1"
+        assert p.result()[0] == f"FDS 1 {GIB}"
+        p.close()
+        st = b.stat()
+        assert st["timeouts"] == 1 and st["takes"] == 1
+    finally:
+        b.stop()
+
+
+def test_grants_expire_only_with_a_ttl(broker_exe, tmp_path):
+    b = Broker(broker_exe, str(tmp_path / "hbm1.sock"), ttl_s=0.5)
+    try:
         b.admin(f"GRANT {'e' * 32} {GIB}")
         time.sleep(1.0)
         st = b.stat()
-        assert st["timeouts"] == 1 and st["expired"] == 1 and st["grants"] == 0
+        assert st["expired"] == 1 and st["grants"] == 0
+    finally:
+        b.stop()
+    b = Broker(broker_exe, str(tmp_path / "hbm2.sock"))                     # default: no TTL
+    try:
+        b.admin(f"GRANT {'e' * 32} {GIB}")
+        time.sleep(0.5)
+        assert b.stat()["grants"] == 1
+    finally:
+        b.stop()
+
+
+def test_revoke_list_and_boot_id(broker_exe, tmp_path):
+    b = Broker(broker_exe, str(tmp_path / "hbm0.sock"))
+    try:
+        boot = b.ready["boot"]
+        assert len(boot) == 16 and b.stat()["boot"] == boot
+        b.admin(f"GRANT {'r' * 32} {2 * GIB}")
+        b.admin(f"GRANT {'s' * 32} {GIB}")
+        assert json.loads(b.admin("LIST")) == {"boot": boot, "grants": {"r" * 32: 2, "s" * 32: 1}}
+        held = Pod(b.path, "r" * 32)
+        assert held.result()[0] == f"FDS 2 {GIB}"
+        waiter = Pod(b.path, "r" * 32)                   # a second process of the pod waits ...
+        time.sleep(0.2)
+        assert b.admin(f"REVOKE {'r' * 32}") == "OK 2"   # ... the pod is deleted: 2 granules still held
+        assert waiter.result()[0] == "ERR revoked"
+        assert Pod(b.path, "r" * 32).result()[0] == "ERR revoked"   # never taken again
+        assert json.loads(b.admin("LIST"))["grants"] == {"s" * 32: 1}
+        held.close()                                     # the holder exits: the granules come back
+        time.sleep(0.3)
+        st = b.stat()
+        assert st["free"] == 8 and st["held"] == 0 and st["revokes"] == 1 and st["revoked"] == 1
+        assert b.admin(f"REVOKE {'z' * 32}") == "OK 0"   # unknown tokens are revoked too
+        assert b.admin(f"GRANT {'r' * 32} {GIB}") == "OK 1"   # the granter may grant it again
+        p = Pod(b.path, "r" * 32)
+        assert p.result()[0] == f"FDS 1 {GIB}"
+        p.close()
+    finally:
+        b.stop()
+    b2 = Broker(broker_exe, str(tmp_path / "hbm0.sock"))     # a restart: a new boot id, no grants
+    try:
+        assert b2.ready["boot"] != boot and json.loads(b2.admin("LIST"))["grants"] == {}
+    finally:
+        b2.stop()
+
+
+def test_admin_socket_lives_apart_and_checks_the_peer(broker_exe):
+    import pathlib
+    import tempfile
+
+    root = pathlib.Path(tempfile.mkdtemp(prefix="gs-peer-", dir="/tmp"))   # reachable by another uid
+    os.chmod(root, 0o755)
+    pods = root / "gpu0"
+    adm = root / "admin"
+    pods.mkdir()
+    adm.mkdir(mode=0o700)
+    b = Broker(broker_exe, str(pods / "hbm0.sock"), admin=str(adm / "hbm0.sock"))
+    try:
+        assert sorted(os.listdir(pods)) == ["hbm0.sock"]                 # what a container mounts
+        assert oct(os.stat(adm / "hbm0.sock").st_mode & 0o777) == "0o600"
+        assert oct(os.stat(pods / "hbm0.sock").st_mode & 0o777) == "0o666"
+        assert b.admin(f"GRANT {'k' * 32} {GIB}") == "OK 1"               # root: accepted
+        if os.geteuid() == 0:
+            # another uid that reaches the socket anyway (mode opened up) is refused by SO_PEERCRED
+            os.chmod(adm / "hbm0.sock", 0o666)
+            os.chmod(adm, 0o755)
+            code = ("import socket,sys,time\ns=socket.socket(socket.AF_UNIX); s.connect(sys.argv[1]); time.sleep(0.2)\n"
+                    "try: s.sendall(b'GRANT " + "q" * 32 + " 1073741824\\n')\nexcept OSError: pass\n"
+                    "print(s.recv(64).decode().strip())")
+            out = subprocess.run([sys.executable, "-c", code, str(adm / "hbm0.sock")], capture_output=True, text=True,
+                                 user=65534, timeout=30)
+            assert out.stdout.strip() == "ERR peer", out
+            assert b.stat()["peer_refused"] == 1 and json.loads(b.admin("LIST"))["grants"] == {"k" * 32: 1}
+    finally:
+        b.stop()
+
+
+def test_junk_connections_do_not_delay_a_take(broker_exe, tmp_path):
+    """1,000 connections that never ask anything: the per-peer cap turns nearly all of them away
+    at once, the rest are dropped at the request deadline, and a legitimate TAKE from another
+    process is served within 50 ms meanwhile."""
+    b = Broker(broker_exe, str(tmp_path / "hbm0.sock"), extra=("--request-timeout-s", "1"))
+    try:
+        b.admin(f"GRANT {'t' * 32} {GIB}")
+        junk, connected = [], 0
+        for _ in range(1000):
+            s = socket.socket(socket.AF_UNIX)
+            s.setblocking(False)
+            try:
+                s.connect(b.path)
+                connected += 1
+            except (BlockingIOError, ConnectionRefusedError, OSError):
+                pass                                   # the listen backlog is full: refused by the kernel
+            junk.append(s)
+        time.sleep(0.3)
+        code = ("import socket,sys,time; t=time.perf_counter(); s=socket.socket(socket.AF_UNIX); "
+                "s.connect(sys.argv[1]); s.sendall(('TAKE '+'t'*32+'\\n').encode()); h=b''\n"
+                "while not h.endswith(b'\\n'): h+=s.recv(1)\n"
+                "print(h.decode().strip(), round((time.perf_counter()-t)*1e3,2))")
+        out = subprocess.run([sys.executable, "-c", code, b.path], capture_output=True, text=True, timeout=30)
+        head, ms = out.stdout.split()[:3], float(out.stdout.split()[-1])
+        assert " ".join(head) == f"FDS 1 {GIB}", out
+        assert ms < 50.0, ms
+        st = b.stat()
+        assert connected >= 500 and st["busy"] >= connected - 8 and st["clients"] <= 8 + 2
+        time.sleep(1.5)
+        assert b.stat()["idle_dropped"] >= 1
+        for s in junk:
+            s.close()
+    finally:
+        b.stop()
+
+
+def test_scrub_in_flight_does_not_stall_grant_take_or_stat(broker_exe, tmp_path):
+    """A release's scrub takes 1.5 s on the stub GPU (FAKE_HIP_EVENT_MS): GRANT, STAT and a TAKE
+    of free granules are answered meanwhile; the scrubbed granules come back after it."""
+    b = Broker(broker_exe, str(tmp_path / "hbm0.sock"), wait_s=10.0, env={"FAKE_HIP_EVENT_MS": "1500"})
+    try:
+        b.admin(f"GRANT {'a' * 32} {6 * GIB}")
+        p = Pod(b.path, "a" * 32)
+        assert p.result()[0] == f"FDS 6 {GIB}"
+        p.close()
+        time.sleep(0.1)
+        t = time.perf_counter()
+        st = b.stat()
+        assert st["scrubbing"] == 6 and st["free"] == 2
+        assert b.admin(f"GRANT {'b' * 32} {2 * GIB}") == "OK 2"
+        q = Pod(b.path, "b" * 32)
+        assert q.result()[0] == f"FDS 2 {GIB}"
+        assert time.perf_counter() - t < 0.5
+        r = Pod(b.path, "a" * 32)                          # needs the granules being scrubbed: waits
+        assert r.result()[0] == f"FDS 6 {GIB}"
+        assert time.perf_counter() - t > 1.0
+        st = b.stat()
+        assert st["scrubbing"] == 0 and st["scrubbed_bytes"] >= 6 * GIB
+        q.close()
+        r.close()
+    finally:
+        b.stop()
+
+
+def test_exit_policy_lends_only_after_the_holder_exits(broker_exe, tmp_path):
+    """Release policy "exit" (the default where the kernel does not count dma-buf references, as
+    with the stub's memfds): a holder that closes its connection but keeps running does not get
+    its granules lent to the next pod; they are lent once its process has exited."""
+    b = Broker(broker_exe, str(tmp_path / "hbm0.sock"), gib=2, policy="auto")
+    try:
+        assert b.ready["release_policy"] == "exit"
+        b.admin(f"GRANT {'o' * 32} {2 * GIB}")
+        b.admin(f"GRANT {'n' * 32} {2 * GIB}")
+        code = ("import socket,sys,time; s=socket.socket(socket.AF_UNIX); s.connect(sys.argv[1]); "
+                "s.sendall(('TAKE '+'o'*32+'\\n').encode()); h=b''\n"
+                "while not h.endswith(b'\\n'): h+=s.recv(1)\n"
+                "socket.recv_fds(s,1,200); s.close(); print('released', flush=True); sys.stdin.read()")
+        tenant = subprocess.Popen([sys.executable, "-c", code, b.path], stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                                  text=True)
+        assert tenant.stdout.readline().strip() == "released"      # connection closed, process alive
+        nxt = Pod(b.path, "n" * 32)
+        time.sleep(0.5)
+        st = b.stat()
+        assert st["quarantined"] == 2 and st["waiting"] == 1 and st["free"] == 0
+        tenant.stdin.close()
+        tenant.wait(10)
+        assert nxt.result()[0] == f"FDS 2 {GIB}"
+        nxt.close()
     finally:
         b.stop()
 
@@ -169,13 +357,21 @@ def test_hostile_input_ends_only_that_connection(broker):
 
     assert send(broker.path, b"GRANT abc 999999999999\n").startswith(b"ERR")   # no grants from a pod
     assert send(broker.path, b"STAT\n").startswith(b"ERR")                     # nor its counters
+    assert send(broker.path, b"LIST\n").startswith(b"ERR")                     # nor the tokens
+    assert send(broker.path, b"REVOKE abc\n").startswith(b"ERR")               # nor revocations
     assert send(broker.path, b"\x00\xff garbage\n").startswith(b"ERR")
+    assert send(broker.path, b"TAKE ../../etc\n").startswith(b"ERR")           # tokens are [A-Za-z0-9_-]
     assert send(broker.path, b"A" * 5000) == b""                               # over-long line: dropped
-    assert send(broker.path + ".admin", b"GRANT t 0\n").startswith(b"ERR")     # no empty grants
-    assert send(broker.path + ".admin", f"GRANT t {100 * GIB}\n".encode()).startswith(b"ERR")   # > the broker
-    assert broker.stat()["refused"] >= 5
+    adm = broker.admin_path
+    assert send(adm, b"GRANT t 0\n").startswith(b"ERR")                        # no empty grants
+    assert send(adm, f"GRANT t {100 * GIB}\n".encode()).startswith(b"ERR")    # > the broker
+    # bytes near 2^64 must not wrap into a small grant when rounded up to granules
+    assert send(adm, b"GRANT t 18446744073709551615\n").startswith(b"ERR size")
+    assert send(adm, b"GRANT t 18446744073709551000\n").startswith(b"ERR size")
+    assert send(adm, b"GRANT t 1 extra\n").startswith(b"ERR")
+    assert broker.stat()["refused"] >= 9
     broker.admin(f"GRANT {'k' * 32} {GIB}")                                    # still serving
     p = Pod(broker.path, "k" * 32)
     assert p.result()[0] == f"FDS 1 {GIB}"
     p.close()
-    assert oct(os.stat(broker.path + ".admin").st_mode & 0o777) == "0o600"
+    assert oct(os.stat(adm).st_mode & 0o777) == "0o600"
