@@ -133,6 +133,8 @@ class AllocatorOptions:
     # a container's quota granted as broker granules (quota/hbmbroker.py HBMGranter); None = off
     hbm_broker_dir: str | None = None
     hbm_broker_fraction: float = 0.94
+    # HBMGranter keyword arguments (poll_s, startup_grace_s, down_grace_s, revoke_grace_s, ...)
+    hbm_granter_args: dict = dataclasses.field(default_factory=dict)
 
 
 @dataclasses.dataclass
@@ -179,7 +181,7 @@ class Allocator(NativeTable):
         self.grants = PL.GrantBook()
         self.prestart_hooks: list = []          # run at PreStartContainer (after the placement pass)
         self._ledgers = self._ledger_dir(self.opts)
-        self._hbm = self._hbm_granter(self.opts)
+        self._hbm = self._hbm_granter(self.opts, live=self._hbm_live, on_readiness=self._hbm_readiness)
         self.podres = None
         self._overlay: dict[str, dict] = {}       # uid -> annotations written, not yet landed
         self._overlay_gen: dict[str, int] = {}
@@ -210,6 +212,9 @@ class Allocator(NativeTable):
         self._resp_tmpl: dict[tuple, api.ContainerAllocateResponse] = {}   # _container_response
         # answers prepared before the bind (PrebindWatch -> precompute), by (uid, gpu, units)
         self._precomputed: collections.OrderedDict = collections.OrderedDict()
+        # pods placed here but not bound yet: uid -> (pod, first seen, pre-bind watch gone at | None);
+        # candidates already (native_table.py precompute / expire_prebind)
+        self._prebind: dict[str, tuple] = {}
         self._tmpl_bytes: dict[tuple, bytes] = {}                          # _prepared
         self.native_rotate_bytes = 16 << 20       # rotate the native journal file past this
         self.native_prep_keep = 4096              # prepared answers kept for native claims past the current table
@@ -232,11 +237,47 @@ class Allocator(NativeTable):
             threading.Thread(target=self._prepare_loop, name="prepare-answers", daemon=True).start()
 
     @staticmethod
-    def _hbm_granter(opts: AllocatorOptions, secret: bytes | None = None):
+    def _hbm_granter(opts: AllocatorOptions, live=None, on_readiness=None):
         if not (opts.hbm_broker_dir and opts.shim is not None and opts.shim.enabled and not opts.disable_cgpu):
             return None
         from ..quota.hbmbroker import HBMGranter
-        return HBMGranter(opts.hbm_broker_dir, opts.hbm_broker_fraction, secret=secret)
+        return HBMGranter(opts.hbm_broker_dir, opts.hbm_broker_fraction, live=live, on_readiness=on_readiness,
+                          **opts.hbm_granter_args)
+
+    def _hbm_live(self) -> dict | None:
+        """The HBM tokens the pods on this node need (the granter's pod view): every gpu container
+        of every pod here with a GPU assignment (``ALIYUN_COM_GPU_MEM_IDX``), whether it is running
+        or still being admitted. None when the pod view is unavailable (nothing is revoked then)."""
+        hbm = self._hbm
+        if hbm is None:
+            return None
+        try:
+            pods = self.pods.node_pods()
+        except Exception:  # noqa: BLE001 - the granter retries on its next pass
+            return None
+        out = {}
+        for p in pods:
+            shape = self._info(p)[3]
+            idx = O.annotations(p).get(const.ENV_RESOURCE_INDEX) if shape else None
+            if idx is None or not idx.isdigit():
+                continue
+            g = int(idx)
+            dev = self.model.gpu(g)
+            if dev is None:
+                continue
+            u = O.uid(p)
+            for slot, units in enumerate(shape):
+                out[hbm.token(u, slot)] = (g, U.quota_bytes(units, dev.units, dev.vram_bytes))
+        return out
+
+    def _hbm_readiness(self) -> None:
+        """A GPU's broker went away for good or came back: answers prepared with (or without) its
+        token are re-prepared."""
+        with self._mu:
+            self._bump_gen()
+            self._fast = None
+            self._prep_cache.clear()
+        self._precomputed.clear()
 
     @staticmethod
     def _ledger_dir(opts: AllocatorOptions):
@@ -262,8 +303,13 @@ class Allocator(NativeTable):
             self.opts = dataclasses.replace(opts, async_patch=async_patch, journal_path=self.opts.journal_path)
             if opts.ledger_dir != ledger_dir:
                 self._ledgers = self._ledger_dir(self.opts)
-            # same secret across rebuilds: a re-prepared answer keeps its pod's token
-            self._hbm = self._hbm_granter(self.opts, self._hbm.secret if self._hbm is not None else None)
+            # the same granter across rebuilds (its grants and pod view stay); a new one only when
+            # the broker directory or the share changed
+            old = self._hbm
+            if old is None or (opts.hbm_broker_dir, opts.hbm_broker_fraction) != (old.host_dir, old.fraction):
+                if old is not None:
+                    old.stop()
+                self._hbm = self._hbm_granter(self.opts, live=self._hbm_live, on_readiness=self._hbm_readiness)
             self._pinfo.clear()
             self._bump_gen()
             self._fast = None
@@ -274,6 +320,8 @@ class Allocator(NativeTable):
 
     def close(self):
         self._stop.set()
+        if self._hbm is not None:
+            self._hbm.stop()
         if self._patch_q is not None:
             self._patch_q.put(None)
 
@@ -342,7 +390,7 @@ class Allocator(NativeTable):
                     del self._assigned[u]
 
     def _candidates(self, fresh: bool) -> list[dict]:
-        pods = self._view(A.dedupe_by_uid(self.pods.pending_pods(fresh=fresh), self.node))
+        pods = self._view(A.dedupe_by_uid(self.pods.pending_pods(fresh=fresh), self.node) + self._prebind_pods())
         now = time.monotonic()
         self._sweep_assigned(now)
         if fresh and self._tainted:   # forget a withheld reservation once its pod is gone
@@ -683,9 +731,10 @@ class Allocator(NativeTable):
             # exact bytes from the SMI-reported HBM size, so the shim needs no device query
             r.envs[const.ENV_SHIM_QUOTA_BYTES] = str(U.quota_bytes(ctr_units, g.units, g.vram_bytes))
             if self._hbm is not None:
-                # the GPU's HBM broker; the pod's token is per pod (_container_response / _prepared)
-                r.mounts.add(container_path=const.HBM_BROKER_CONTAINER_DIR, host_path=self._hbm.host_dir,
-                             read_only=False)
+                # the GPU's HBM broker: only that GPU's pod-socket directory (never the admin
+                # sockets); the pod's token is per pod (_container_response / _prepared)
+                r.mounts.add(container_path=const.HBM_BROKER_CONTAINER_DIR, host_path=self._hbm.mount_dir(gpu_index),
+                             read_only=True)
                 r.envs[const.ENV_HBM_BROKER] = self._hbm.container_socket(gpu_index)
         return r
 
@@ -838,6 +887,7 @@ class Allocator(NativeTable):
             ev.wait(0.5)
             ev.clear()
             try:
+                self.expire_prebind()
                 if self.native is not None and self._published == (getattr(src, "pending_version", None), self._gen):
                     # the cache hook already applied the change to the native table: a full
                     # rebuild now would only compete with the Allocate it made the table for

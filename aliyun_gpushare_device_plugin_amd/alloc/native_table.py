@@ -8,8 +8,12 @@ own candidate rules give (``docs/ALLOCATE_PATH.md``):
 * the pod-cache hook (``_on_pending`` / ``_publish_change``, on the watch thread) applies each
   change of the Pending set to the last table at once; a full rebuild (``Allocator._prepare``)
   covers everything else (engine generation changes, relists);
-* answers of pods the extender placed here are prepared before their bind (``precompute``,
-  fed by ``cluster/podcache.py`` PrebindWatch);
+* pods the extender placed here are candidates from before their bind (``precompute``, fed by
+  ``cluster/podcache.py`` PrebindWatch): their answers are prepared and published into the table
+  at once, so the kubelet's Allocate — whose own watch may deliver the bind before the plugin's —
+  finds its pod already there; a pre-bind pod whose bind does not come (deleted, placed
+  elsewhere, label moved) is withdrawn from the table after ``PREBIND_CONFIRM_S``
+  (``expire_prebind``);
 * the server's claims come back through ``_native_loop`` / ``_native_taken`` for the same
   bookkeeping as the engine's own answers (claimed set, grants, replay index, write-behind
   PATCH), and its journal file is compacted into the engine's.
@@ -297,22 +301,142 @@ class NativeTable:
 
     def precompute(self, pod: dict) -> None:
         """A pod placed on this node but not bound yet (``cluster/podcache.py`` PrebindWatch):
-        prepare its Allocate answer now, so the watch-thread hook only has to insert it when
-        the bind arrives — the kubelet's Allocate follows the same watch event."""
-        if self.native is None or not self.opts.fast_path or self.opts.compute_isolation == "cu":
-            return
+        prepare its Allocate answer now and publish it into the table as a candidate, in assume
+        time order, so the kubelet's Allocate finds it even when the kubelet's watch delivered
+        the bind before the plugin's (the pod is this node's assumed candidate from the moment
+        the extender placed it, ``allocate.go:63-89``). The bind, when the pod watch brings it,
+        replaces the entry in place."""
+        if (self.native is None or not self.opts.fast_path or self.opts.compute_isolation == "cu"
+                or not hasattr(self.pods, "pending_version")):
+            return                                    # (pre-bind candidates need the pod watch cache)
         assumed, _, _, shape = self._info(pod)
         if not assumed or len(shape) != 1:
             return
         u, g = O.uid(pod), A.gpu_id_from_annotation(pod)
+        if self.pods.get(u) is not None:
+            return                                    # the bind came first: the pod cache has it
         k = (u, g, shape[0])
-        if self.model.gpu(g) is None or k in self._precomputed or k in self._prep_cache or u in self._native_prep:
-            return                                    # prepared already (the bind came first)
-        c = self._prepared(pod, u, g, shape[0])
-        _native_blob(0, 0, 0, [c], [])                # fills c.frag: the table entry, encoded once
-        self._precomputed[k] = (c, time.monotonic())
-        while len(self._precomputed) > 1024:
-            self._precomputed.popitem(last=False)
+        if self.model.gpu(g) is None:
+            return
+        if k not in self._precomputed and k not in self._prep_cache and u not in self._native_prep:
+            c = self._prepared(pod, u, g, shape[0])
+            _native_blob(0, 0, 0, [c], [])            # fills c.frag: the table entry, encoded once
+            self._precomputed[k] = (c, time.monotonic())
+            while len(self._precomputed) > 1024:
+                self._precomputed.popitem(last=False)
+        with self._table_mu:
+            prev = self._prebind.get(u)
+            self._prebind[u] = (pod, prev[1] if prev is not None else time.monotonic(), None)
+            while len(self._prebind) > 1024:
+                self._prebind.pop(next(iter(self._prebind)))
+        self._publish_prebind(u)
+
+    # how long a pre-bind candidate whose pre-bind watch entry went away (bound, deleted, label
+    # moved: the watch does not say which) stays in the table waiting for the pod watch to show
+    # it bound here; and how long one that never went away is kept at all
+    PREBIND_CONFIRM_S = 2.0
+    PREBIND_TTL_S = 30.0
+
+    def prebind_gone(self, pod: dict) -> None:
+        """PrebindWatch: the pod left the unbound-and-labelled set — bound (here, the pod watch
+        will show it), deleted, placed elsewhere or relabelled. Its entry stays for
+        ``PREBIND_CONFIRM_S`` (``expire_prebind``)."""
+        u = O.uid(pod)
+        with self._table_mu:
+            e = self._prebind.get(u)
+            if e is not None and e[2] is None:
+                self._prebind[u] = (e[0], e[1], time.monotonic())
+
+    def _prebind_live(self, u: str, now: float) -> bool:
+        e = self._prebind.get(u)
+        if e is None:
+            return False
+        _, t0, gone = e
+        return now - t0 < self.PREBIND_TTL_S and (gone is None or now - gone < self.PREBIND_CONFIRM_S)
+
+    def _prebind_pods(self) -> list[dict]:
+        """Pre-bind candidates the pod cache does not have yet (the engine's ``_candidates``)."""
+        if not self._prebind:
+            return []
+        now = time.monotonic()
+        with self._table_mu:
+            items = list(self._prebind.items())
+        return [e[0] for u, e in items if self._prebind_live(u, now) and self.pods.get(u) is None]
+
+    def expire_prebind(self) -> None:
+        """Withdraw pre-bind candidates that the pod cache never showed bound here within their
+        window: their entries leave the table unless a native answer already claimed them (that
+        answer went to a pod of this node, and the claim stands, as any claim does). A pod the
+        cache has now is no longer pre-bind."""
+        if not self._prebind:
+            return
+        now = time.monotonic()
+        drop, bound = [], []
+        # (the pod cache's lock is never taken under _table_mu: the cache hook takes them the
+        # other way round)
+        with self._table_mu:
+            uids = list(self._prebind)
+        cached = {u for u in uids if self.pods.get(u) is not None}
+        with self._table_mu:
+            for u, e in list(self._prebind.items()):
+                if u in cached:
+                    bound.append(u)
+                elif not self._prebind_live(u, now):
+                    drop.append(u)
+            for u in bound + drop:
+                self._prebind.pop(u, None)
+        for u in drop:
+            if u in self._assigned:
+                log.warning("pod uid %s: answered before its bind, which never reached this node; its answer "
+                            "went to another pod of the same size (placement truth reconciles the annotations)", u)
+                continue
+            self.metrics.allocate_outcomes.inc(outcome="prebind_withdrawn")
+            self._publish_prebind(u, remove=True)
+
+    def _publish_prebind(self, u: str, remove: bool = False) -> None:
+        """Insert (or withdraw) pre-bind candidate ``u`` in the last published table, at the same
+        cache version: the table is what a full rebuild gives now (``_prepare`` takes the same
+        pre-bind set into its candidates)."""
+        nat = self.native
+        if nat is None or not self.opts.fast_path or self.opts.compute_isolation == "cu":
+            return
+        in_cache = self.pods.get(u) is not None        # before _table_mu (lock order: cache, then table)
+        with self._table_mu:
+            last = self._last_table
+            if last is None or last[1] != self._gen or time.time() < self.journal._legacy_until:
+                return                                # the prepare loop rebuilds (it takes the pre-bind set too)
+            version, gen, out, ats = last
+            idx = next((i for i, c in enumerate(out) if c.uid == u), None)
+            if remove:
+                if idx is None or in_cache:
+                    return
+                old = out[idx]
+                self._prep_cache.pop((old.uid, old.gpu, old.size), None)
+                out, ats = out[:idx] + out[idx + 1:], ats[:idx] + ats[idx + 1:]
+            else:
+                e = self._prebind.get(u)
+                if idx is not None or e is None or u in self._assigned or u in self._claims or u in self._tainted:
+                    return
+                p = self._view([e[0]])[0]
+                assumed, _, at, shape = self._info(p)
+                if not assumed or len(shape) != 1 or O.deleting(p):
+                    return
+                g = A.gpu_id_from_annotation(p)
+                k = (u, g, shape[0])
+                c = self._prep_cache.get(k) or self._take_precomputed(k) or self._prepared(p, u, g, shape[0])
+                self._prep_cache[k] = c
+                i = bisect.bisect_right(ats, at)
+                out, ats = out[:i] + (c,) + out[i:], ats[:i] + (at,) + ats[i:]
+                self._native_prep.pop(u, None)
+                self._native_prep[u] = c
+                for en in out:
+                    if en.uid != u:
+                        self._native_prep.pop(en.uid, None)
+                        self._native_prep[en.uid] = en
+                self._trim_native_prep(len(out))
+            nat.publish(_native_blob(version, gen, 1 if self.podres is not None else 0, list(out),
+                                     self.journal.replay_ids()))
+            self._last_table = (version, gen, out, ats)
 
     # the ledger directory a prepared answer names is kept for a grace period without a pod on
     # this node (quota/ledger.py collect, 60 s): a bind later than this gets a fresh answer

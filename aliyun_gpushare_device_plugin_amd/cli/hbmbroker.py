@@ -3,13 +3,17 @@
 Each broker (``native/hbmbroker``, ``gpushare-hbm-broker``) holds its GPU's shareable HBM as VMM
 granules and lends each pod its own, zeroed between pods (``docs/HBM_TURNOVER.md``). The device
 plugin, started with ``--hbm-broker-dir`` on the same directory, grants every shared container its
-granules. GPU ``i`` of the plugin (its SMI order) gets the socket ``<dir>/hbm<i>.sock``, and the
-broker finds its HIP device by that GPU's PCI address, because HIP and SMI orders are not
+granules. GPU ``i`` of the plugin (its SMI order) gets the pod socket ``<dir>/gpu<i>/hbm<i>.sock``
+and the admin socket ``<dir>/admin/hbm<i>.sock`` (``quota/hbmbroker.py`` has the layout), and
+the broker finds its HIP device by that GPU's PCI address, because HIP and SMI orders are not
 promised to agree.
 
-A broker that exits is started again after ``--restart-backoff`` seconds. Its pods lose their
-granules with it: the same blast radius as the GPU. Pods admitted meanwhile find no socket.
-Their TAKE fails, and they allocate from the driver under the quota shim.
+A broker that exits is started again after ``--restart-backoff`` seconds, with a new boot id: the
+plugin sees it on its next poll and grants the new instance every live pod's token again, so a
+container that restarts afterwards gets its granules. Pods that held granules of the dead broker
+keep what they mapped until they exit (docs/HBM_TURNOVER.md, exporter death). A pod whose first
+allocation comes while its broker is down waits for it (the shim retries the socket), within
+``GPUSHARE_HBM_WAIT_S``.
 
 No counterpart in the reference (``pkg/gpu/nvidia/allocate.go:114-127`` leaves isolation and
 memory to cGPU).
@@ -24,7 +28,7 @@ import threading
 import time
 
 from ..device.smi import SMI
-from ..quota.hbmbroker import HBMBroker, socket_name
+from ..quota.hbmbroker import HBMBroker
 from ..utils import log
 
 
@@ -37,6 +41,12 @@ def build_parser() -> argparse.ArgumentParser:
                    help="HBM each broker leaves to the driver (the pods' runtimes allocate some themselves)")
     p.add_argument("--granule-mib", type=int, default=1024)
     p.add_argument("--wait-s", type=float, default=30.0, help="how long a pod's TAKE waits for its granules")
+    p.add_argument("--ungranted-wait-s", type=float, default=10.0,
+                   help="how long a TAKE whose grant has not arrived waits (the plugin re-grants within a poll)")
+    p.add_argument("--release-policy", default="auto", choices=("auto", "refs", "exit"),
+                   help="when a released granule may be lent again (hbmbroker.cpp): refs = no dma-buf reference "
+                        "left outside the broker, exit = the holder's process is gone; auto = refs where the "
+                        "kernel counts them")
     p.add_argument("--restart-backoff", type=float, default=2.0)
     return p
 
@@ -81,11 +91,13 @@ def main(argv=None) -> int:
     a = build_parser().parse_args(argv)
     log.setup(buffered=True)
     os.makedirs(a.dir, exist_ok=True)
+    os.chmod(a.dir, 0o755)
     want = {int(x) for x in a.gpu_indices.split(",") if x.strip()}
     with SMI(a.smi_backend) as s:
         gpus = [s.device(i) for i in range(s.count())]
-    brokers = {g.index: HBMBroker(os.path.join(a.dir, socket_name(g.index)), pci_bus_id=g.bdf,
-                                  reserve_gib=a.reserve_gib, granule_mib=a.granule_mib, wait_s=a.wait_s)
+    extra = ["--ungranted-wait-s", str(a.ungranted_wait_s), "--release-policy", a.release_policy]
+    brokers = {g.index: HBMBroker.for_gpu(a.dir, g.index, pci_bus_id=g.bdf, reserve_gib=a.reserve_gib,
+                                          granule_mib=a.granule_mib, wait_s=a.wait_s, extra_args=extra)
                for g in gpus if not want or g.index in want}
     if not brokers:
         log.error("no GPU to run an HBM broker for")

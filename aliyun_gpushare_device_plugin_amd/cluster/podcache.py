@@ -157,10 +157,13 @@ class PrebindWatch:
     ``gpushare.amd.com/node=<node>``, ``spec.nodeName`` empty): ``on_pod(pod)`` for each, so the
     Allocate engine can prepare the pod's answer before the bind reaches the node's pod watch
     and, right behind it, the kubelet's Allocate. Pods placed by an extender that does not set
-    the label are simply never seen here (the answer is prepared at the bind, as before)."""
+    the label are simply never seen here (the answer is prepared at the bind, as before).
+    ``on_gone(pod)`` when a pod leaves that set (bound, deleted, relabelled: a watch's DELETED for
+    an object that stops matching carries its previous state, so which one is not known here)."""
 
-    def __init__(self, client: APIClient, node: str, on_pod, watch_timeout: int = 300):
+    def __init__(self, client: APIClient, node: str, on_pod, watch_timeout: int = 300, on_gone=None):
         self.client, self.node, self.on_pod, self.watch_timeout = client, node, on_pod, watch_timeout
+        self.on_gone = on_gone
         self._stop = threading.Event()
         self._conn: list = []
         self._thread = None
@@ -181,12 +184,15 @@ class PrebindWatch:
             try:
                 for ev in self.client.watch_pods("spec.nodeName=", None, self.watch_timeout, self._stop, self._conn,
                                                  label_selector=f"{const.POD_LABEL_NODE}={self.node}"):
-                    if ev.get("type") in ("ADDED", "MODIFIED") and not O.node_name(ev.get("object") or {}):
-                        self.events += 1
-                        try:
-                            self.on_pod(ev["object"])
-                        except Exception as e:  # noqa: BLE001 - preparing ahead is an optimisation
-                            log.V(2).info("prebind: %s", e)
+                    typ, obj = ev.get("type"), ev.get("object") or {}
+                    try:
+                        if typ in ("ADDED", "MODIFIED") and not O.node_name(obj):
+                            self.events += 1
+                            self.on_pod(obj)
+                        elif typ == "DELETED" and self.on_gone is not None:
+                            self.on_gone(obj)
+                    except Exception as e:  # noqa: BLE001 - preparing ahead is an optimisation
+                        log.V(2).info("prebind: %s", e)
                 backoff = 0.1
             except Exception as e:  # noqa: BLE001 - apiserver restart, expired watch
                 if self._stop.is_set():

@@ -162,9 +162,12 @@ def main() -> int:
     del hold, player
     torch.cuda.synchronize()
     torch.cuda.empty_cache()      # HBM back to the device now, not at process exit
+    # the broker arena (if any) is handed back first: its granules are on the ledger while it is
+    # mapped, so the ledger read before the release would count them as a residue
+    released = _arena_release()
     after = _shim_stats()
     _send({"event": "done", "gemms": gemms, "t": time.time(), "seconds": time.time() - t_start, "shim": st,
-           "used_after_release": (after or {}).get("used"), "arena_released": _arena_release()})
+           "used_after_release": (after or {}).get("used"), "arena_released": released})
     # everything is freed and reported: leave without the interpreter's and torch's teardown
     # (hundreds of ms). The kernel still tears the process down, and only then do its last
     # references to an HBM broker's granules go (the broker quarantines them until then)

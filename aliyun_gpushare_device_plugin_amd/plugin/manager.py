@@ -70,6 +70,7 @@ class PluginConfig:
     ledger_dir: str | None = None        # host dir for file-backed shim ledgers (usage metrics)
     hbm_broker_dir: str | None = None    # host dir of the per-GPU HBM broker sockets (quota/hbmbroker.py)
     hbm_broker_fraction: float = 0.94
+    hbm_granter_args: dict = dataclasses.field(default_factory=dict)   # HBMGranter timing (tests)
     ledger_scan_s: float = 10.0
     journal_path: str | None = None      # persisted allocation journal (alloc/journal.py)
     compute_isolation: str = "none"      # "cu": per-pod CU-slot masks (alloc/cuslots.py)
@@ -190,6 +191,7 @@ class SharedGPUManager:
                                 ledger_dir=cfg.ledger_dir if shim else None,
                                 hbm_broker_dir=cfg.hbm_broker_dir if shim else None,
                                 hbm_broker_fraction=cfg.hbm_broker_fraction,
+                                hbm_granter_args=dict(cfg.hbm_granter_args),
                                 journal_path=cfg.journal_path,
                                 compute_isolation=cfg.compute_isolation, placement_s=cfg.placement_s,
                                 identify=cfg.admission_identity)
@@ -206,7 +208,8 @@ class SharedGPUManager:
         if allocator.podres is None:
             allocator.set_pod_resources(self._pod_resources())
         if cfg.prebind_watch and cfg.pod_source == "watch" and self.client is not None:
-            self._prebind = PrebindWatch(self.client, cfg.node_name, allocator.precompute).start()
+            self._prebind = PrebindWatch(self.client, cfg.node_name, allocator.precompute,
+                                         on_gone=allocator.prebind_gone).start()
         self.model = model
         cls = self._server_class()
         kw = ({"fast_wait_us": cfg.native_fast_wait_us, "spin_us": cfg.native_spin_us}

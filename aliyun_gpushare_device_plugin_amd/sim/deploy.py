@@ -35,6 +35,7 @@ ENTRY_POINTS = {
     "gpushare-device-plugin-v2": "aliyun_gpushare_device_plugin_amd.cli.main",
     "gpushare-scheduler-extender": "aliyun_gpushare_device_plugin_amd.cli.extender",
     "kubectl-inspect-gpushare": "aliyun_gpushare_device_plugin_amd.cli.inspect",
+    "gpushare-hbm-brokers": "aliyun_gpushare_device_plugin_amd.cli.hbmbroker",
 }
 
 
@@ -79,12 +80,14 @@ def _rewrite(value: str, mounts: dict) -> str:
     return f"{flag}={target}" if eq else target
 
 
-def resolve(doc: dict, host_root: str, field_refs: dict, overrides: dict, skip_volumes=()) -> Container:
-    """The first container of a DaemonSet / Deployment: command with hostPath volumes mapped under
-    ``host_root`` (one directory per volume), env with downward-API ``fieldRef`` values from
+def resolve(doc: dict, host_root: str, field_refs: dict, overrides: dict, skip_volumes=(),
+            container: str | None = None) -> Container:
+    """A container of a DaemonSet / Deployment (the first, or the one named ``container``):
+    command with hostPath volumes mapped under ``host_root`` (one directory per volume, shared by
+    the pod's containers as a hostPath is), env with downward-API ``fieldRef`` values from
     ``field_refs``, and ``overrides`` ({flag: value or None to drop}) applied to the flags."""
     spec = pod_template(doc)["spec"]
-    c = spec["containers"][0]
+    c = spec["containers"][0] if container is None else next(x for x in spec["containers"] if x["name"] == container)
     vols = {v["name"]: v for v in spec.get("volumes", [])}
     mounts = {}
     for m in c.get("volumeMounts", []):

@@ -91,6 +91,14 @@ def parse():
     ap.add_argument("--hbm-broker-reserve-gib", type=float, default=12.0,
                     help="HBM the broker leaves to the driver (runtimes' own allocations); the plugin grants each "
                          "pod 94 %% of its quota in whole GiB, 269-270 GiB for a GPU's 4 pods")
+    ap.add_argument("--driver-path-steps", type=int, default=5,
+                    help="after the timed run (1 GPU, broker on): this many churn steps of the driver path "
+                         "(--no-hbm-broker) in a child run, reported as driver_path (0 = off)")
+    ap.add_argument("--stub-runtime", default=None,
+                    help="CPU rehearsal of the broker path: a directory with the stub HIP runtime "
+                         "(libamdhip64.so.7, tests/native/fake_hip.c), shim_driver and a gpushare-hbm-broker linked "
+                         "against it; every rank runs a stub broker and its pods are stub processes under the real "
+                         "quota shim that take their arenas from it")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -745,6 +753,101 @@ class PodFleet:
                 w["proc"].kill()
 
 
+class StubFleet:
+    """CPU rehearsal of the broker path (``--stub-runtime``): each admitted pod is a process of
+    the stub HIP runtime (``tests/native/shim_driver``) under the real quota shim, with the
+    Allocate answer's env. It takes its arena from this rank's stub broker at its first
+    allocation, holds ``fill`` of its quota, reports, and waits; stopping it ends the process
+    (its broker connection closes and the granules go back). No GEMMs: the rehearsal is about
+    every rank's broker serving every pod, not about throughput."""
+
+    def __init__(self, stub_dir: str, fill: float):
+        self.stub_dir, self.fill = stub_dir, fill
+        self.pods: dict[str, dict] = {}
+        self.ready_ms: list[float] = []
+        self.arenas = 0                       # pods whose allocations came from the broker arena
+        self.denied = self.held_bytes = self.released_residue = self.retired_bytes = 0
+        self.release_ms: list[float] = []
+        self.release_by_size: dict[int, list] = {}
+        self.release_bytes_s: list[tuple] = []
+        self.phase_ms: dict[str, list] = {"stop": [], "init": [], "room": [], "alloc": [], "hold": []}
+        self.trace = None
+
+    def start(self, rec: dict) -> float:
+        from aliyun_gpushare_device_plugin_amd import const
+
+        env = dict(os.environ, **rec["env"])
+        env.update(LD_PRELOAD=os.path.join(NATIVE, "libgpushare_hipquota.so"), LD_LIBRARY_PATH=self.stub_dir,
+                   FAKE_HIP_TOTAL_GIB="288", GPUSHARE_HBM_WAIT_S="30")
+        quota = int(env.get(const.ENV_SHIM_QUOTA_BYTES, 0))
+        t0 = time.perf_counter()
+        p = subprocess.Popen([os.path.join(self.stub_dir, "shim_driver"), "alloc", str(int(quota * self.fill)),
+                              "arena", "wait"], env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+        alloc = arena = None
+        for ln in p.stdout:
+            if ln.startswith("{"):
+                ev = json.loads(ln)
+                if ev["op"] == "alloc":
+                    alloc = ev
+                elif ev["op"] == "arena":
+                    arena = ev
+                    break
+        dt = time.perf_counter() - t0
+        if alloc is None or arena is None:
+            raise RuntimeError(f"stub pod {rec['uid']} exited before it reported (rc {p.poll()})")
+        self.denied += alloc["err"] != 0
+        self.arenas += arena["on"] == 1
+        held = int(quota * self.fill) if alloc["err"] == 0 else 0
+        self.held_bytes += held
+        self.pods[rec["uid"]] = {"proc": p, "size": rec["size"], "held": held, "arena": arena}
+        self.ready_ms.append(dt)
+        self.phase_ms["alloc"].append(dt)
+        return dt
+
+    def stop(self, uid: str):
+        w = self.pods.pop(uid, None)
+        if w is None:
+            return
+        t0 = time.perf_counter()
+        w["proc"].stdin.close()
+        w["proc"].wait(30)
+        self.phase_ms["stop"].append(time.perf_counter() - t0)
+        self.held_bytes -= w["held"]
+        self.retired_bytes += w["held"]
+
+    def oldest(self) -> str | None:
+        return next(iter(self.pods), None)
+
+    def gemms(self) -> int:
+        return 0
+
+    def close(self):
+        for uid in list(self.pods):
+            self.stop(uid)
+
+
+def driver_path_run(a) -> dict:
+    """A short child run of the driver path (``--no-hbm-broker``: every pod allocates fresh from
+    amdgpu, which wipes a retired pod's HBM first) with this run's pod shapes; its headline."""
+    import tempfile
+
+    out = os.path.join(tempfile.mkdtemp(prefix="gs-driver-", dir="/tmp"), "line.json")
+    cmd = [sys.executable, os.path.abspath(__file__), "--gpus", "1", "--steps", str(a.driver_path_steps), "--warmup", "1",
+           "--no-hbm-broker", "--compare-rtts", "", "--fill-orders", "", "--no-ref-churn", "--driver-path-steps", "0",
+           "--gemm", str(a.gemm), "--fill", str(a.fill), "--standby", str(a.standby), "--json-out", out]
+    t0 = time.perf_counter()
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+        with open(out) as f:
+            d = json.loads(f.read())
+    except Exception as e:  # noqa: BLE001 - a comparator, never fatal to the headline
+        return {"error": f"{type(e).__name__}: {e}"[:300]}
+    return {"value": d["value"], "unit": d["unit"], "steps": d["steps"], "ms_per_step": d["ms_per_step"],
+            "pod_ready_p50_ms": d.get("pod_ready_p50_ms"), "pod_phase_p50_ms": d.get("pod_phase_p50_ms"),
+            "allocate_p50_ms": d.get("allocate_p50_ms"), "failed_admissions": d.get("failed_admissions"),
+            "rc": r.returncode, "wall_s": round(time.perf_counter() - t0, 1)}
+
+
 def relaunch(n: int) -> int:
     """``bench.py --gpus N`` started without a launcher (no ``WORLD_SIZE``): run the same command
     as N ranks under ``torch.distributed.run`` in a child process and return its exit code. Called
@@ -794,6 +897,7 @@ def main():
     import torch.distributed as dist
 
     use_gpu = torch.cuda.is_available() and not a.no_gpu
+    stub = os.path.abspath(a.stub_runtime) if a.stub_runtime and not use_gpu else None
     binding = None
     ordinal = local
     if use_gpu:
@@ -834,29 +938,40 @@ def main():
             with SMI("auto") as s:
                 # every rank bound its plugin GPU above (bind_device), so the node has >= n GPUs
                 ref_spec = f"fake:{n}x{s.device(0).vram_total}B"
-        hbm_dir = tempfile.mkdtemp(prefix="gs-hbm-", dir="/tmp") if use_gpu and a.hbm_broker else None
-        cp = ControlPlane(n, smi, a.pod_source, a.plugin_mode, workdir, with_shim=use_gpu,
+        hbm_dir = tempfile.mkdtemp(prefix="gs-hbm-", dir="/tmp") if (use_gpu or stub) and a.hbm_broker else None
+        cp = ControlPlane(n, smi, a.pod_source, a.plugin_mode, workdir, with_shim=use_gpu or bool(stub),
                           ref_spec=None if a.no_ref_churn else ref_spec, hbm_dir=hbm_dir)
         info = {"units_per_gpu": cp.units_per_gpu, "gpu_count": cp.gpu_count, "hbm_dir": hbm_dir}
     info = bcast(info)
     units = info["units_per_gpu"]
     broker = None
     broker_error = None
-    if use_gpu and info.get("hbm_dir"):
-        from aliyun_gpushare_device_plugin_amd.quota.hbmbroker import HBMBroker, socket_name
+    if (use_gpu or stub) and info.get("hbm_dir"):
+        from aliyun_gpushare_device_plugin_amd.quota.hbmbroker import HBMBroker
 
-        # the broker of the plugin's GPU <local> (this rank's device, bound by PCI address)
-        broker = HBMBroker(os.path.join(info["hbm_dir"], socket_name(local)), device=ordinal,
-                           reserve_gib=a.hbm_broker_reserve_gib)
+        # the broker of the plugin's GPU <local> (this rank's device, bound by PCI address), in
+        # the node layout the plugin's --hbm-broker-dir names
+        kw = {}
+        if stub:
+            kw = dict(exe=os.path.join(stub, "gpushare-hbm-broker"),
+                      env=dict(os.environ, FAKE_HIP_TOTAL_GIB="288", LD_LIBRARY_PATH=stub))
+        broker = HBMBroker.for_gpu(info["hbm_dir"], local, device=ordinal, reserve_gib=a.hbm_broker_reserve_gib, **kw)
         try:
             broker.start()
         except Exception as e:  # noqa: BLE001 - reported in the line; the churn runs on the driver path
             broker_error = f"{type(e).__name__}: {e}"[:500]
             sys.stderr.write(f"bench: hbm broker unavailable, pods allocate from the driver: {broker_error}\n")
             broker = None
+    # every rank's broker listens before rank 0 fills the node: the plugin grants each pod while it
+    # prepares its answer (a grant that finds no broker is re-sent on the granter's next poll, and
+    # the pod's shim waits for its broker, but the fill should not depend on that)
+    barrier()
     # pod processes see their GPU through the Allocate response's ROCR_VISIBLE_DEVICES (UUID)
-    fleet = PodFleet(local, a.gemm, a.burst, a.fill, not smi.startswith("fake:"), a.standby,
-                     slack=int(a.room_slack_gib * (1 << 30)), ordinal=ordinal, broker=broker) if use_gpu else None
+    if use_gpu:
+        fleet = PodFleet(local, a.gemm, a.burst, a.fill, not smi.startswith("fake:"), a.standby,
+                         slack=int(a.room_slack_gib * (1 << 30)), ordinal=ordinal, broker=broker)
+    else:
+        fleet = StubFleet(stub, a.fill) if stub else None
     topo_report = cp_topo = None
     topo_failed = False
     problems: list = []
@@ -959,6 +1074,7 @@ def main():
     rel = [x for r in gather(fleet.release_bytes_s if fleet is not None else []) for x in r]
     per_rank = gather(dict(done, rank=rank, gpu=local, binding=binding,
                            pods_live=len(fleet.pods) if fleet is not None else None,
+                           arenas=getattr(fleet, "arenas", None),
                            broker=broker.stat() if broker is not None else None,
                            broker_error=broker_error))
     by_size: dict = {}
@@ -1004,7 +1120,7 @@ def main():
         for r in per_rank:
             if r["churned"] == 0:
                 problems.append(f"GPU {r['gpu']} (rank {r['rank']}): no admissions in the timed region")
-            if use_gpu and (r["started"] == 0 or not r["pods_live"]):
+            if (use_gpu or stub) and (r["started"] == 0 or not r["pods_live"]):
                 problems.append(f"GPU {r['gpu']} (rank {r['rank']}): no pod processes started")
         if n > 1 and (topo_report is None or "verdict" not in topo_report):
             problems.append("no topology verdict for a multi-GPU node")
@@ -1109,6 +1225,9 @@ def main():
         brokers = {str(r["gpu"]): r["broker"] for r in per_rank}
         res["hbm_broker"] = brokers.get(str(local))
         res["hbm_broker_by_gpu"] = brokers if len(brokers) > 1 else None
+        if stub:
+            # the CPU rehearsal: stub pods whose allocations came from their GPU's broker arena
+            res["stub_pods_with_arena_by_gpu"] = {str(r["gpu"]): r["arenas"] for r in per_rank}
         errs = {str(r["gpu"]): r["broker_error"] for r in per_rank if r.get("broker_error")}
         if errs:
             res["hbm_broker_error"] = errs
@@ -1125,11 +1244,6 @@ def main():
                         problems.append(f"rank of GPU {k} bound {b} but the plugin's topology row is {row}")
         if problems:
             res["run_problems"] = problems
-        line = json.dumps(res)
-        print(line, flush=True)
-        if a.json_out:
-            with open(a.json_out, "w") as f:
-                f.write(line + "\n")
     if fleet is not None:
         if fleet.trace is not None:              # per-pod cycle phases (GS_BENCH_POD_TRACE=<path>)
             with open(f"{os.environ['GS_BENCH_POD_TRACE']}.{rank}", "w") as f:
@@ -1145,6 +1259,16 @@ def main():
     import shutil
 
     shutil.rmtree(workdir, ignore_errors=True)
+    if rank == 0:
+        if world == 1 and use_gpu and broker is not None and a.driver_path_steps > 0:
+            # the same churn without the broker, after this run has handed every GPU byte back: what
+            # the broker buys, measured on the same box in the same line
+            res["driver_path"] = driver_path_run(a)
+        line = json.dumps(res)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                f.write(line + "\n")
     if topo_failed:
         # a broken topology export must not pass as a successful multi-GPU run
         sys.stderr.write("bench: topology verdict FAIL: " + "; ".join(topo_report["reasons"]) + "\n")

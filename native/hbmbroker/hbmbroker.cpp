@@ -217,40 +217,84 @@ struct Broker {
   double scrub_s_total = 0, scrub_s_last = 0, setup_s = 0;
   unsigned long long scrubbed_bytes = 0;
 
-  void setup(size_t total) {
-    CK(hipSetDevice(device));
-    hipMemAllocationProp p;
-    std::memset(&p, 0, sizeof p);
-    p.type = hipMemAllocationTypePinned;
-    p.requestedHandleType = hipMemHandleTypePosixFileDescriptor;
-    p.location.type = hipMemLocationTypeDevice;
-    p.location.id = device;
-    size_t mg = 0;
-    CK(hipMemGetAllocationGranularity(&mg, &p, hipMemAllocationGranularityMinimum));
-    if (mg && gran % mg) gran = (gran + mg - 1) / mg * mg;
-    count = int(total / gran);
-    double t0 = now_s();
-    h.resize(count);
-    fds.resize(count);
-    CK(hipMemAddressReserve(reinterpret_cast<void**>(&base), gran * count, 0, nullptr, 0));
-    for (int i = 0; i < count; ++i) {
-      CK(hipMemCreate(&h[i], gran, &p, 0));
-      CK(hipMemExportToShareableHandle(&fds[i], h[i], hipMemHandleTypePosixFileDescriptor, 0));
-      CK(hipMemMap(base + size_t(i) * gran, gran, 0, h[i], 0));
-      free_list.push_back(i);
-    }
+  hipMemAllocationProp prop_{};
+  int count_max = 0;          // granules the broker is sized for (its address range)
+  size_t reserve_bytes = 0;   // what it leaves to the driver
+  unsigned long long grown = 0;
+
+  hipMemAccessDesc rw() const {
     hipMemAccessDesc d;
     std::memset(&d, 0, sizeof d);
     d.location.type = hipMemLocationTypeDevice;
     d.location.id = device;
     d.flags = hipMemAccessFlagsProtReadWrite;
-    CK(hipMemSetAccess(base, gran * count, &d, 1));
+    return d;
+  }
+
+  // granule i: created, exported, mapped in the broker's range (not yet zeroed)
+  void add_granule(int i) {
+    CK(hipMemCreate(&h[i], gran, &prop_, 0));
+    CK(hipMemExportToShareableHandle(&fds[i], h[i], hipMemHandleTypePosixFileDescriptor, 0));
+    CK(hipMemMap(base + size_t(i) * gran, gran, 0, h[i], 0));
+  }
+
+  // `target` bytes of granules, as many of them as the device has free now (the rest is taken
+  // later, by grow(): after a broker restart, pods of the previous instance still hold theirs)
+  void setup(size_t target, size_t free_now) {
+    CK(hipSetDevice(device));
+    std::memset(&prop_, 0, sizeof prop_);
+    prop_.type = hipMemAllocationTypePinned;
+    prop_.requestedHandleType = hipMemHandleTypePosixFileDescriptor;
+    prop_.location.type = hipMemLocationTypeDevice;
+    prop_.location.id = device;
+    size_t mg = 0;
+    CK(hipMemGetAllocationGranularity(&mg, &prop_, hipMemAllocationGranularityMinimum));
+    if (mg && gran % mg) gran = (gran + mg - 1) / mg * mg;
+    count_max = int(target / gran);
+    count = std::min(count_max, int(free_now / gran));
+    double t0 = now_s();
+    h.resize(count_max);
+    fds.assign(count_max, -1);
+    base_refs.assign(count_max, -1);
+    CK(hipMemAddressReserve(reinterpret_cast<void**>(&base), gran * size_t(count_max), 0, nullptr, 0));
+    for (int i = 0; i < count; ++i) {
+      add_granule(i);
+      free_list.push_back(i);
+    }
+    hipMemAccessDesc d = rw();
+    if (count) CK(hipMemSetAccess(base, gran * count, &d, 1));
     CK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-    CK(hipMemsetAsync(base, 0, gran * count, stream));  // nobody sees what was there before
+    if (count) CK(hipMemsetAsync(base, 0, gran * count, stream));  // nobody sees what was there before
     CK(hipStreamSynchronize(stream));
-    base_refs.resize(count);
     for (int i = 0; i < count; ++i) base_refs[i] = refs(i);
     setup_s = now_s() - t0;
+  }
+
+  // take more of the device while the broker is short of its size: HBM that pods of a previous
+  // broker instance held comes back to the driver when they exit (the dma-buf imports keep it
+  // alive until then). New granules are zeroed like released ones before they are lent.
+  void grow() {
+    if (count >= count_max) return;
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr <= reserve_bytes) return;
+    int n = std::min(count_max - count, int((fr - reserve_bytes) / gran));
+    if (n <= 0) return;
+    hipMemAccessDesc d = rw();
+    std::vector<int> fresh;
+    for (int k = 0; k < n; ++k) {
+      int i = count;
+      if (hipMemCreate(&h[i], gran, &prop_, 0) != hipSuccess) break;   // raced: try again later
+      CK(hipMemExportToShareableHandle(&fds[i], h[i], hipMemHandleTypePosixFileDescriptor, 0));
+      CK(hipMemMap(base + size_t(i) * gran, gran, 0, h[i], 0));
+      CK(hipMemSetAccess(base + size_t(i) * gran, gran, &d, 1));
+      base_refs[i] = refs(i);
+      fresh.push_back(i);
+      ++count;
+    }
+    grown += fresh.size();
+    if (!fresh.empty())
+      std::fprintf(stderr, "gpushare-hbm-broker: grew by %zu granules to %d of %d\n", fresh.size(), count, count_max);
+    scrub(fresh);
   }
 
   // zero the granules on the broker's stream; they are lent again from reap_scrubs()
@@ -477,16 +521,17 @@ struct Broker {
       waiting += !kv.second.waiting.empty();
     }
     for (auto& s : scrubbing) scrub_n += s.idx.size();
-    char b[1536];
+    char b[2048];
     std::snprintf(b, sizeof b,
-                  "{\"boot\": \"%s\", \"device\": %d, \"granule_bytes\": %zu, \"granules\": %d, \"free\": %zu, "
+                  "{\"boot\": \"%s\", \"device\": %d, \"granule_bytes\": %zu, \"granules\": %d, \"granules_max\": %d, "
+                  "\"grown\": %llu, \"free\": %zu, "
                   "\"held\": %zu, \"scrubbing\": %zu, \"waiting\": %zu, \"grants\": %zu, \"takes\": %llu, "
                   "\"releases\": %llu, \"refused\": %llu, \"revokes\": %llu, \"revoked\": %zu, \"timeouts\": %llu, "
                   "\"expired\": %llu, \"busy\": %llu, \"idle_dropped\": %llu, \"peer_refused\": %llu, "
                   "\"clients\": %zu, \"quarantined\": %zu, \"quarantined_total\": %llu, \"lost\": %llu, "
                   "\"release_policy\": \"%s\", \"held_refs_max\": %d, \"base_refs\": %d, \"scrubbed_bytes\": %llu, "
                   "\"scrub_ms_total\": %.3f, \"scrub_ms_last\": %.3f, \"setup_ms\": %.1f}\n",
-                  boot.c_str(), device, gran, count, free_list.size(), held, scrub_n, waiting, grants.size(), takes,
+                  boot.c_str(), device, gran, count, count_max, grown, free_list.size(), held, scrub_n, waiting, grants.size(), takes,
                   releases, refused, revokes, revoked.size(), timeouts, expired, busy, idle_dropped, peer_refused,
                   clients.size(), quarantined(), quarantined_total, lost, policy_name(), held_refs_max(),
                   base_refs.empty() ? -1 : base_refs[0], scrubbed_bytes, scrub_s_total * 1e3, scrub_s_last * 1e3,
@@ -653,9 +698,12 @@ int main(int argc, char** argv) {
   CK(hipSetDevice(b.device));
   size_t fr = 0, tot = 0;
   CK(hipMemGetInfo(&fr, &tot));
-  size_t total = gib > 0 ? size_t(gib * double(1ull << 30))
-                         : (fr > size_t(reserve_gib * double(1ull << 30)) ? fr - size_t(reserve_gib * double(1ull << 30)) : 0);
-  b.setup(total);
+  b.reserve_bytes = size_t(reserve_gib * double(1ull << 30));
+  // sized for the device (or --gib); what is not free yet is taken as it comes back (grow)
+  size_t target = gib > 0 ? size_t(gib * double(1ull << 30)) : (tot > b.reserve_bytes ? tot - b.reserve_bytes : 0);
+  size_t free_now = gib > 0 ? target : (fr > b.reserve_bytes ? fr - b.reserve_bytes : 0);
+  if (gib > 0) b.reserve_bytes = fr > target ? fr - target : 0;
+  b.setup(target, std::min(target, free_now));
   bool counted = !b.base_refs.empty() && b.base_refs[0] >= 0;
   b.policy = policy == "refs" ? kRefs : policy == "exit" ? kExit : policy == "trust" ? kTrust : (counted ? kRefs : kExit);
   if (b.policy == kRefs && !counted) {
@@ -674,6 +722,7 @@ int main(int argc, char** argv) {
   std::fflush(stdout);
 
   std::vector<pollfd> pf;
+  double last_grow = now_s();
   while (!g_stop) {
     pf.assign({{pod_ls, POLLIN, 0}, {adm_ls, POLLIN, 0}});
     for (auto& kv : b.clients) pf.push_back({kv.first, POLLIN, 0});
@@ -736,6 +785,10 @@ int main(int argc, char** argv) {
     }
     bool back = b.reap_scrubs();
     if (!b.quarantine.empty()) b.sweep_quarantine();
+    if (b.count < b.count_max && t - last_grow > 1.0) {
+      last_grow = t;
+      b.grow();
+    }
     if (back || !late.empty()) b.serve_waiting();
     // with a TTL, grants of pods that never started (deleted before admission) do not pile up;
     // without one (the default) the plugin's revocations do that

@@ -1075,6 +1075,16 @@ REAL(hipError_t, hipMemUnmap, void*, size_t)
 REAL(hipError_t, hipMemSetAccess, void*, size_t, const hipMemAccessDesc*, size_t)
 REAL(hipError_t, hipGetDevice, int*)
 REAL(hipError_t, hipDeviceSynchronize)
+REAL(hipError_t, hipEventCreateWithFlags, hipEvent_t*, unsigned)
+REAL(hipError_t, hipEventRecord, hipEvent_t, hipStream_t)
+REAL(hipError_t, hipEventQuery, hipEvent_t)
+REAL(hipError_t, hipEventSynchronize, hipEvent_t)
+REAL(hipError_t, hipEventDestroy, hipEvent_t)
+REAL(hipError_t, hipStreamIsCapturing, hipStream_t, hipStreamCaptureStatus*)
+REAL(hipError_t, hipDeviceGetDefaultMemPool, hipMemPool_t*, int)
+REAL(hipError_t, hipMemGetAllocationPropertiesFromHandle, hipMemAllocationProp*, hipMemGenericAllocationHandle_t)
+REAL(hipError_t, hipMemExportToShareableHandle, void*, hipMemGenericAllocationHandle_t, hipMemAllocationHandleType,
+     unsigned long long)
 
 constexpr int kArenaMaxGranules = 1024;
 constexpr int kArenaMaxExt = 1 << 16;     // free extents
@@ -1104,6 +1114,7 @@ struct Arena {
   bool charged = false;  // the arena's size is on the pod's ledger
 };
 Arena g_arena;
+int g_dev = 0;  // the arena's device (HIP ordinal in this process)
 
 bool arena_configured() {
   static std::atomic<int> c{-1};
@@ -1188,7 +1199,31 @@ void arena_take() {
   auto access_f = real_hipMemSetAccess();
   auto getdev_f = real_hipGetDevice();
   if (s < 0 || !import_f || !reserve_f || !map_f || !access_f || !getdev_f) goto fail;
-  if (connect(s, reinterpret_cast<sockaddr*>(&sa), sizeof sa) != 0) goto fail;
+  {
+    // the broker may not be listening yet (a node booting, a broker restarting): its socket is
+    // missing or refuses; retry for GPUSHARE_HBM_WAIT_S (default 15 s), then use the driver
+    double wait_s = 15.0;
+    if (const char* w = getenv("GPUSHARE_HBM_WAIT_S")) wait_s = atof(w);
+    timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    bool logged = false;
+    while (connect(s, reinterpret_cast<sockaddr*>(&sa), sizeof sa) != 0) {
+      int err = errno;
+      clock_gettime(CLOCK_MONOTONIC, &t1);
+      double el = double(t1.tv_sec - t0.tv_sec) + double(t1.tv_nsec - t0.tv_nsec) * 1e-9;
+      if ((err != ENOENT && err != ECONNREFUSED && err != EAGAIN) || el >= wait_s) {
+        logf(1, "hbm broker %s: cannot connect (%s) after %.1f s: allocating from the driver", path, strerror(err), el);
+        goto fail;
+      }
+      if (!logged) logf(1, "hbm broker %s: not there yet (%s); waiting up to %.0f s", path, strerror(err), wait_s);
+      logged = true;
+      timespec nap{0, 50 * 1000 * 1000};
+      nanosleep(&nap, nullptr);
+      close(s);  // a fresh socket per attempt
+      s = socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+      if (s < 0) goto fail;
+    }
+  }
   {
     int n = snprintf(line, sizeof line, "TAKE %s\n", tok);
     if (send(s, line, n, MSG_NOSIGNAL) != n) goto fail;
@@ -1235,6 +1270,7 @@ void arena_take() {
     a.base = static_cast<char*>(base);
     a.size = size;
     a.gran = gran;
+    g_dev = dev;
   }
   // the arena counts against the pod's quota like any other HBM it holds: what the runtime
   // still takes from the driver (code objects, scratch) is charged on top of it
@@ -1288,6 +1324,30 @@ bool live_take(uint64_t off, uint64_t* len) {
   }
 }
 
+// take [start, start + len) out of free extent i (it lies inside it)
+bool arena_carve(int i, uint64_t start, uint64_t len) {
+  Arena& a = g_arena;
+  Ext e = a.ext[i];
+  uint64_t head = start - e.off, tail = e.off + e.len - (start + len);
+  if (head && tail && a.next >= kArenaMaxExt) return false;
+  if (!live_put(start, len)) return false;
+  if (head && tail) {  // split in two: shift the rest up by one
+    memmove(&a.ext[i + 2], &a.ext[i + 1], sizeof(Ext) * (a.next - i - 1));
+    a.ext[i] = {e.off, head};
+    a.ext[i + 1] = {start + len, tail};
+    ++a.next;
+  } else if (head) {
+    a.ext[i] = {e.off, head};
+  } else if (tail) {
+    a.ext[i] = {start + len, tail};
+  } else {
+    memmove(&a.ext[i], &a.ext[i + 1], sizeof(Ext) * (a.next - i - 1));
+    --a.next;
+  }
+  a.used += len;
+  return true;
+}
+
 // first fit; large blocks on 2 MiB boundaries (the CDNA4 TLB fragment), small ones on 4 KiB
 bool arena_alloc(uint64_t size, void** ptr) {
   Arena& a = g_arena;
@@ -1297,24 +1357,24 @@ bool arena_alloc(uint64_t size, void** ptr) {
     Ext e = a.ext[i];
     uint64_t start = (e.off + align - 1) & ~(align - 1);
     if (start + len > e.off + e.len) continue;
-    uint64_t head = start - e.off, tail = e.off + e.len - (start + len);
-    if (head && tail && a.next >= kArenaMaxExt) return false;
-    if (!live_put(start, len)) return false;
-    if (head && tail) {  // split in two: shift the rest up by one
-      memmove(&a.ext[i + 2], &a.ext[i + 1], sizeof(Ext) * (a.next - i - 1));
-      a.ext[i] = {e.off, head};
-      a.ext[i + 1] = {start + len, tail};
-      ++a.next;
-    } else if (head) {
-      a.ext[i] = {e.off, head};
-    } else if (tail) {
-      a.ext[i] = {start + len, tail};
-    } else {
-      memmove(&a.ext[i], &a.ext[i + 1], sizeof(Ext) * (a.next - i - 1));
-      --a.next;
-    }
-    a.used += len;
+    if (!arena_carve(i, start, len)) return false;
     *ptr = a.base + start;
+    return true;
+  }
+  return false;
+}
+
+// one whole granule (granule-aligned in the arena), last fit: the VMM windows' slots take
+// granules from the top while hipMalloc blocks fill from the bottom
+bool arena_take_granule(uint64_t* off) {
+  Arena& a = g_arena;
+  for (int i = a.next - 1; i >= 0; --i) {
+    Ext e = a.ext[i];
+    if (e.len < a.gran) continue;
+    uint64_t start = (e.off + e.len - a.gran) / a.gran * a.gran;
+    if (start < e.off) continue;
+    if (!arena_carve(i, start, a.gran)) return false;
+    *off = start;
     return true;
   }
   return false;
@@ -1349,6 +1409,38 @@ void arena_free(uint64_t off) {
   }  // else: the extent list is full and these bytes stay unusable until release (never seen)
 }
 
+// ---- stream-ordered frees (hipFreeAsync of arena blocks) ----
+// The block goes back to the free list once an event recorded on the freeing stream has
+// completed: the kernels that still use it were queued before the event.
+struct AsyncFree {
+  uint64_t off;
+  hipEvent_t ev;
+};
+constexpr int kMaxAsyncFree = 8192;
+AsyncFree g_afree[kMaxAsyncFree];
+int g_nafree = 0;  // g_arena.mu held
+
+// return completed stream-ordered frees to the free list (g_arena.mu held); `wait`: all of them
+void reap_async_frees(bool wait) {
+  auto query = real_hipEventQuery();
+  auto sync = real_hipEventSynchronize();
+  auto destroy = real_hipEventDestroy();
+  Depth d;
+  for (int i = 0; i < g_nafree;) {
+    hipError_t q = hipSuccess;
+    if (g_afree[i].ev) {
+      q = wait ? (sync ? sync(g_afree[i].ev) : hipSuccess) : (query ? query(g_afree[i].ev) : hipSuccess);
+      if (q == hipErrorNotReady) {
+        ++i;
+        continue;
+      }
+      if (destroy) (void)destroy(g_afree[i].ev);
+    }
+    arena_free(g_afree[i].off);
+    g_afree[i] = g_afree[--g_nafree];
+  }
+}
+
 // 1: served from the arena (*e set), 0: not the arena's (pass through)
 int arena_try_alloc(void** ptr, size_t size, hipError_t* e) {
   if (!arena_configured() || size == 0 || t_depth) return 0;
@@ -1359,7 +1451,12 @@ int arena_try_alloc(void** ptr, size_t size, hipError_t* e) {
     pthread_mutex_unlock(&a.mu);
     return 0;
   }
+  if (g_nafree) reap_async_frees(false);
   bool ok = arena_alloc(size, ptr);
+  if (!ok && g_nafree) {  // room that stream-ordered frees will give back: wait for them
+    reap_async_frees(true);
+    ok = arena_alloc(size, ptr);
+  }
   pthread_mutex_unlock(&a.mu);
   if (!ok) {
     if (ptr) *ptr = nullptr;
@@ -1376,6 +1473,252 @@ bool arena_owns(void* p) {
   Arena& a = g_arena;
   return a.state.load(std::memory_order_acquire) == 1 && static_cast<char*>(p) >= a.base &&
          static_cast<char*>(p) < a.base + a.size;
+}
+
+// ---- VMM from the arena (PyTorch's expandable segments) ----------------------------------------
+// A VMM user reserves a large VA range (hipMemAddressReserve), creates small physical handles
+// (hipMemCreate, 2 / 20 MiB pages for PyTorch) and maps them one after another into the range.
+// Physical handles of the arena cannot be cut into pages, so the shim lends whole granules:
+// a reservation of >= 1 GiB (a "window") is aligned to the granule, its granule-sized slots are
+// backed on demand by arena granules (unmapped from the arena's own range and mapped into the
+// slot), and the user's handles are stand-ins whose map is a no-op inside a backed slot. A slot
+// whose pages are all unmapped gives its granule back to the arena. When no granule is free, the
+// slot is served by real handles from the driver (charged to the quota as before).
+constexpr uint64_t kWinAlign = 1ull << 30;
+constexpr int kMaxWin = 64;
+constexpr uint64_t kVHandleMagic = 0x67737668616e646cull;  // "gsvhandl"
+
+struct Win {
+  char* base;
+  uint64_t size;
+  int nslots;
+  int32_t* slot_g;      // arena granule backing the slot, -1 none
+  uint64_t* slot_used;  // bytes of stand-in pages mapped in the slot (arena-backed slots)
+  uint32_t* slot_real;  // real (driver) pieces mapped in the slot
+};
+Win g_win[kMaxWin];
+int g_nwin = 0;
+
+struct VPiece {
+  char* va;
+  uint64_t len;
+  hipMemGenericAllocationHandle_t h;  // real handle (driver), or nullptr: inside an arena slot
+};
+struct VHandle {
+  uint64_t magic;
+  uint64_t size;
+  hipMemAllocationProp prop;
+  unsigned long long flags;
+  char* at;  // mapped at (nullptr: not mapped)
+  int npieces;
+  VPiece* pieces;
+};
+
+// stand-in handles and their mapped addresses: open addressing on the pointer / VA
+constexpr uint64_t kVCap = 1 << 17;
+uintptr_t* g_vh = nullptr;   // VHandle* set
+uintptr_t* g_vva = nullptr;  // VA -> VHandle* (pairs)
+uint64_t g_vh_n = 0, g_vva_n = 0, g_pending_bytes = 0;
+uint64_t g_vmm_arena_maps = 0, g_vmm_real_pieces = 0, g_vmm_creates = 0, g_slots_backed = 0;
+
+bool vtables() {
+  if (!g_vh) g_vh = static_cast<uintptr_t*>(calloc(kVCap, sizeof(uintptr_t)));
+  if (!g_vva) g_vva = static_cast<uintptr_t*>(calloc(2 * kVCap, sizeof(uintptr_t)));
+  return g_vh && g_vva;
+}
+uint64_t vslot(uintptr_t k) { return (k * 0x9E3779B97F4A7C15ull >> 17) & (kVCap - 1); }
+constexpr uintptr_t kTomb = ~uintptr_t(0);
+
+bool vh_put(VHandle* h) {
+  if (g_vh_n * 2 >= kVCap) return false;
+  uintptr_t k = reinterpret_cast<uintptr_t>(h);
+  for (uint64_t i = vslot(k);; i = (i + 1) & (kVCap - 1))
+    if (!g_vh[i] || g_vh[i] == kTomb) {
+      g_vh[i] = k;
+      ++g_vh_n;
+      return true;
+    }
+}
+bool vh_has(const void* p) {
+  if (!g_vh || !p) return false;
+  uintptr_t k = reinterpret_cast<uintptr_t>(p);
+  for (uint64_t i = vslot(k);; i = (i + 1) & (kVCap - 1)) {
+    if (!g_vh[i]) return false;
+    if (g_vh[i] == k) return true;
+  }
+}
+void vh_del(VHandle* h) {
+  uintptr_t k = reinterpret_cast<uintptr_t>(h);
+  for (uint64_t i = vslot(k);; i = (i + 1) & (kVCap - 1)) {
+    if (!g_vh[i]) return;
+    if (g_vh[i] == k) {
+      g_vh[i] = kTomb;
+      --g_vh_n;
+      return;
+    }
+  }
+}
+bool vva_put(char* va, VHandle* h) {
+  if (g_vva_n * 2 >= kVCap) return false;
+  uintptr_t k = reinterpret_cast<uintptr_t>(va);
+  for (uint64_t i = vslot(k);; i = (i + 1) & (kVCap - 1))
+    if (!g_vva[2 * i] || g_vva[2 * i] == kTomb) {
+      g_vva[2 * i] = k;
+      g_vva[2 * i + 1] = reinterpret_cast<uintptr_t>(h);
+      ++g_vva_n;
+      return true;
+    }
+}
+VHandle* vva_take(char* va) {
+  if (!g_vva) return nullptr;
+  uintptr_t k = reinterpret_cast<uintptr_t>(va);
+  for (uint64_t i = vslot(k);; i = (i + 1) & (kVCap - 1)) {
+    if (!g_vva[2 * i]) return nullptr;
+    if (g_vva[2 * i] == k) {
+      g_vva[2 * i] = kTomb;
+      --g_vva_n;
+      return reinterpret_cast<VHandle*>(g_vva[2 * i + 1]);
+    }
+  }
+}
+
+Win* win_of(const char* p, uint64_t len) {
+  for (int i = 0; i < g_nwin; ++i)
+    if (p >= g_win[i].base && p + len <= g_win[i].base + g_win[i].size) return &g_win[i];
+  return nullptr;
+}
+
+bool set_rw(char* va, uint64_t len, int dev) {
+  hipMemAccessDesc acc;
+  memset(&acc, 0, sizeof acc);
+  acc.location.type = hipMemLocationTypeDevice;
+  acc.location.id = dev;
+  acc.flags = hipMemAccessFlagsProtReadWrite;
+  auto f = real_hipMemSetAccess();
+  return f && f(va, len, &acc, 1) == hipSuccess;
+}
+
+// back slot s of window w with an arena granule (g_arena.mu held); false: none free (or the
+// broker's granule is not the slot size: then every page is the driver's)
+bool slot_back(Win& w, int s) {
+  Arena& a = g_arena;
+  uint64_t off;
+  if (a.state.load(std::memory_order_relaxed) != 1 || a.gran != kWinAlign || !arena_take_granule(&off)) return false;
+  int gi = int(off / a.gran);
+  auto un = real_hipMemUnmap();
+  auto map = real_hipMemMap();
+  char* slot = w.base + uint64_t(s) * kWinAlign;
+  Depth d;
+  if (!un || !map || un(a.base + off, a.gran) != hipSuccess) {
+    arena_free(off);
+    return false;
+  }
+  if (map(slot, a.gran, 0, a.h[gi], 0) != hipSuccess || !set_rw(slot, a.gran, g_dev)) {
+    // back where it was: the arena's own range keeps every granule it does not lend
+    if (map(a.base + off, a.gran, 0, a.h[gi], 0) == hipSuccess) set_rw(a.base + off, a.gran, g_dev);
+    arena_free(off);
+    return false;
+  }
+  w.slot_g[s] = gi;
+  w.slot_used[s] = 0;
+  ++g_slots_backed;
+  return true;
+}
+
+// the slot's last page is gone: its granule goes back to the arena (g_arena.mu held)
+void slot_return(Win& w, int s) {
+  Arena& a = g_arena;
+  int gi = w.slot_g[s];
+  if (gi < 0) return;
+  auto un = real_hipMemUnmap();
+  auto map = real_hipMemMap();
+  char* slot = w.base + uint64_t(s) * kWinAlign;
+  Depth d;
+  if (auto sync = real_hipDeviceSynchronize()) (void)sync();   // nothing may still use it when it moves
+  if (un) (void)un(slot, a.gran);
+  if (map && map(a.base + uint64_t(gi) * a.gran, a.gran, 0, a.h[gi], 0) == hipSuccess)
+    set_rw(a.base + uint64_t(gi) * a.gran, a.gran, g_dev);
+  arena_free(uint64_t(gi) * a.gran);
+  w.slot_g[s] = -1;
+  w.slot_used[s] = 0;
+}
+
+// bytes a new stand-in handle could still be given: free arena granules, unmapped room in the
+// backed slots, less what stand-ins created but not mapped yet will take (g_arena.mu held)
+uint64_t vmm_room() {
+  Arena& a = g_arena;
+  uint64_t room = a.size - a.used;
+  for (int i = 0; i < g_nwin; ++i)
+    for (int s = 0; s < g_win[i].nslots; ++s)
+      if (g_win[i].slot_g[s] >= 0) room += kWinAlign - g_win[i].slot_used[s];
+  return room > g_pending_bytes ? room - g_pending_bytes : 0;
+}
+
+hipError_t real_create_charged(hipMemGenericAllocationHandle_t* h, size_t size, const hipMemAllocationProp* prop,
+                               unsigned long long flags);
+
+// map stand-in `v` at [va, va + v->size) inside window `w` (g_arena.mu held)
+hipError_t vmm_map(Win& w, VHandle* v, char* va) {
+  uint64_t lo = uint64_t(va - w.base), hi = lo + v->size;
+  int s0 = int(lo / kWinAlign), s1 = int((hi - 1) / kWinAlign);
+  v->pieces = static_cast<VPiece*>(calloc(size_t(s1 - s0 + 1), sizeof(VPiece)));
+  if (!v->pieces) return hipErrorOutOfMemory;
+  v->npieces = 0;
+  v->at = va;  // (vmm_unmap undoes a partial map)
+  auto map = real_hipMemMap();
+  for (int s = s0; s <= s1; ++s) {
+    uint64_t plo = s == s0 ? lo : uint64_t(s) * kWinAlign;
+    uint64_t phi = s == s1 ? hi : uint64_t(s + 1) * kWinAlign;
+    VPiece& pc = v->pieces[v->npieces];
+    pc.va = w.base + plo;
+    pc.len = phi - plo;
+    pc.h = nullptr;
+    if (w.slot_g[s] < 0 && w.slot_real[s] == 0) slot_back(w, s);
+    if (w.slot_g[s] >= 0) {
+      w.slot_used[s] += pc.len;
+      ++g_vmm_arena_maps;
+    } else {
+      // the driver: a real handle of this piece's size, mapped in the slot (charged as any other)
+      hipError_t e = real_create_charged(&pc.h, pc.len, &v->prop, v->flags);
+      if (e == hipSuccess) {
+        Depth d;
+        e = map ? map(pc.va, pc.len, 0, pc.h, 0) : hipErrorNotInitialized;
+        if (e != hipSuccess) hipMemRelease(pc.h);
+      }
+      if (e != hipSuccess) return e;  // the caller undoes the pieces mapped so far
+      ++w.slot_real[s];
+      ++g_vmm_real_pieces;
+    }
+    ++v->npieces;
+  }
+  return hipSuccess;
+}
+
+// unmap stand-in `v` (g_arena.mu held); its real pieces are released with it (hipMemRelease)
+void vmm_unmap(VHandle* v) {
+  Win* w = v->at ? win_of(v->at, v->size) : nullptr;
+  auto un = real_hipMemUnmap();
+  for (int i = 0; i < v->npieces && w; ++i) {
+    VPiece& pc = v->pieces[i];
+    int s = int(uint64_t(pc.va - w->base) / kWinAlign);
+    if (pc.h) {
+      Depth d;
+      if (un) (void)un(pc.va, pc.len);
+      --w->slot_real[s];
+    } else if (w->slot_g[s] >= 0) {
+      w->slot_used[s] -= pc.len;
+      if (w->slot_used[s] == 0) slot_return(*w, s);
+    }
+  }
+  v->at = nullptr;
+}
+
+void vmm_release_pieces(VHandle* v) {
+  for (int i = 0; i < v->npieces; ++i)
+    if (v->pieces[i].h) hipMemRelease(v->pieces[i].h);   // the interposed release: uncharged
+  free(v->pieces);
+  v->pieces = nullptr;
+  v->npieces = 0;
 }
 }  // namespace
 
@@ -1397,7 +1740,8 @@ GS_EXPORT int gpushare_shim_arena_release() {
     pthread_mutex_unlock(&a.mu);
     return 0;
   }
-  if (a.nlive) {
+  if (g_nafree) reap_async_frees(true);
+  if (a.nlive) {  // (granules lent to VMM windows are live blocks too)
     pthread_mutex_unlock(&a.mu);
     return -1;
   }
@@ -1409,6 +1753,24 @@ GS_EXPORT int gpushare_shim_arena_release() {
   a.state.store(-1, std::memory_order_release);
   pthread_mutex_unlock(&a.mu);
   return 1;
+}
+
+// VMM from the arena: stand-ins created, pages mapped into arena slots, driver pieces, slots backed
+// by a granule so far, and granules lent to windows now
+GS_EXPORT int gpushare_shim_vmm_stats(uint64_t* creates, uint64_t* arena_maps, uint64_t* real_pieces,
+                                      uint64_t* slots_backed, uint64_t* slots_now) {
+  pthread_mutex_lock(&g_arena.mu);
+  uint64_t now = 0;
+  for (int i = 0; i < g_nwin; ++i)
+    for (int sl = 0; sl < g_win[i].nslots; ++sl) now += g_win[i].slot_g[sl] >= 0;
+  if (creates) *creates = g_vmm_creates;
+  if (arena_maps) *arena_maps = g_vmm_arena_maps;
+  if (real_pieces) *real_pieces = g_vmm_real_pieces;
+  if (slots_backed) *slots_backed = g_slots_backed;
+  if (slots_now) *slots_now = now;
+  int n = g_nwin;
+  pthread_mutex_unlock(&g_arena.mu);
+  return n;
 }
 
 // (size, used) of the arena; 0 when there is none
@@ -1434,15 +1796,44 @@ GS_EXPORT hipError_t hipMallocManaged(void** ptr, size_t size, unsigned int flag
   return guarded_alloc(ptr, size, [&] { return f(ptr, size, flags); });
 }
 
+namespace {
+// a stream under graph capture records its allocations into the graph: those stay the driver's
+bool capturing(hipStream_t stream) {
+  auto f = real_hipStreamIsCapturing();
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  Depth d;
+  return f && f(stream, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
+}
+}  // namespace
+
+// Stream-ordered allocations (PyTorch's cudaMallocAsync backend) come from the arena too: the
+// memory is there at once, and a stream-ordered free returns it once the stream got past it.
 GS_EXPORT hipError_t hipMallocAsync(void** ptr, size_t size, hipStream_t stream) {
   auto f = real_hipMallocAsync();
   if (!f) return hipErrorNotInitialized;
+  hipError_t ae;
+  if (arena_configured() && !capturing(stream) && arena_try_alloc(ptr, size, &ae)) return ae;
   return guarded_alloc(ptr, size, [&] { return f(ptr, size, stream); });
 }
 
+// from the device's default pool only: a pool the program made has attributes of its own
+// (IPC export, a release threshold it watches) that the arena does not give
 GS_EXPORT hipError_t hipMallocFromPoolAsync(void** ptr, size_t size, hipMemPool_t pool, hipStream_t stream) {
   auto f = real_hipMallocFromPoolAsync();
   if (!f) return hipErrorNotInitialized;
+  if (arena_configured() && !capturing(stream)) {
+    hipMemPool_t dflt = nullptr;
+    int dev = 0;
+    auto gd = real_hipGetDevice();
+    auto dp = real_hipDeviceGetDefaultMemPool();
+    bool is_default;
+    {
+      Depth d;
+      is_default = gd && dp && gd(&dev) == hipSuccess && dp(&dflt, dev) == hipSuccess && dflt == pool;
+    }
+    hipError_t ae;
+    if (is_default && arena_try_alloc(ptr, size, &ae)) return ae;
+  }
   return guarded_alloc(ptr, size, [&] { return f(ptr, size, pool, stream); });
 }
 
@@ -1514,6 +1905,30 @@ GS_EXPORT hipError_t hipFree(void* ptr) {
 GS_EXPORT hipError_t hipFreeAsync(void* ptr, hipStream_t stream) {
   auto f = real_hipFreeAsync();
   if (!f) return hipErrorNotInitialized;
+  if (ptr && arena_configured() && arena_owns(ptr)) {
+    uint64_t off = uint64_t(static_cast<char*>(ptr) - g_arena.base);
+    hipEvent_t ev = nullptr;
+    auto mk = real_hipEventCreateWithFlags();
+    auto rec = real_hipEventRecord();
+    bool ok;
+    {
+      Depth d;
+      ok = mk && rec && mk(&ev, hipEventDisableTiming) == hipSuccess;
+      if (ok && rec(ev, stream) != hipSuccess) {
+        if (auto de = real_hipEventDestroy()) (void)de(ev);
+        ok = false;
+      }
+      if (!ok) {  // no event: wait for the device instead, as a plain hipFree does
+        ev = nullptr;
+        if (auto dev_sync = real_hipDeviceSynchronize()) (void)dev_sync();
+      }
+    }
+    pthread_mutex_lock(&g_arena.mu);
+    if (g_nafree == kMaxAsyncFree) reap_async_frees(true);
+    g_afree[g_nafree++] = {off, ev};
+    pthread_mutex_unlock(&g_arena.mu);
+    return hipSuccess;
+  }
   if (!hip_active() || !ptr) return f(ptr, stream);
   hipError_t e;
   {
@@ -1524,11 +1939,16 @@ GS_EXPORT hipError_t hipFreeAsync(void* ptr, hipStream_t stream) {
   return e;
 }
 
-GS_EXPORT hipError_t hipMemCreate(hipMemGenericAllocationHandle_t* handle, size_t size,
-                                  const hipMemAllocationProp* prop, unsigned long long flags) {
+namespace {
+// the driver's hipMemCreate under the quota (hip mode charges here; kfd mode at the ioctl)
+hipError_t real_create_charged(hipMemGenericAllocationHandle_t* handle, size_t size, const hipMemAllocationProp* prop,
+                               unsigned long long flags) {
   auto f = real_hipMemCreate();
   if (!f) return hipErrorNotInitialized;
-  if (!hip_active()) return f(handle, size, prop, flags);
+  if (!hip_active()) {
+    Depth d;
+    return f(handle, size, prop, flags);
+  }
   uint64_t c = charge_of(size);
   if (c && !charge(c)) return deny(size);
   hipError_t e;
@@ -1544,9 +1964,291 @@ GS_EXPORT hipError_t hipMemCreate(hipMemGenericAllocationHandle_t* handle, size_
   return e;
 }
 
+// with a broker arena: VMM on the device is served from it (see "VMM from the arena")
+bool vmm_from_arena(const hipMemAllocationProp* prop) {
+  if (!arena_configured() || t_depth || !prop || prop->type != hipMemAllocationTypePinned ||
+      prop->location.type != hipMemLocationTypeDevice)
+    return false;
+  Arena& a = g_arena;
+  if (a.state.load(std::memory_order_acquire) == 0) {
+    pthread_mutex_lock(&a.mu);
+    if (a.state == 0) arena_take();
+    pthread_mutex_unlock(&a.mu);
+  }
+  return a.state.load(std::memory_order_acquire) == 1 && prop->location.id == g_dev;
+}
+}  // namespace
+
+GS_EXPORT hipError_t hipMemCreate(hipMemGenericAllocationHandle_t* handle, size_t size,
+                                  const hipMemAllocationProp* prop, unsigned long long flags) {
+  if (!real_hipMemCreate()) return hipErrorNotInitialized;
+  if (handle && size && vmm_from_arena(prop)) {
+    // a stand-in: its memory is decided where it is mapped (an arena slot, or the driver)
+    Arena& a = g_arena;
+    pthread_mutex_lock(&a.mu);
+    bool ok = vtables();
+    if (ok) {
+      uint64_t left = 0, quota = g.quota.load();
+      if (enabled() && quota) {
+        uint64_t used = g.ledger->total.load();
+        left = used >= quota ? 0 : quota - used;
+      }
+      ok = vmm_room() + left >= size;
+    }
+    VHandle* v = ok ? static_cast<VHandle*>(calloc(1, sizeof(VHandle))) : nullptr;
+    if (v) {
+      v->magic = kVHandleMagic;
+      v->size = size;
+      v->prop = *prop;
+      v->flags = flags;
+      if (!vh_put(v)) {
+        free(v);
+        v = nullptr;
+      }
+    }
+    if (v) {
+      g_pending_bytes += size;
+      ++g_vmm_creates;
+    }
+    pthread_mutex_unlock(&a.mu);
+    if (!v) {
+      logf(1, "vmm: deny a handle of %zu bytes (arena and quota full)", size);
+      return hipErrorOutOfMemory;  // what the driver says when memory is out: callers handle it
+    }
+    *handle = reinterpret_cast<hipMemGenericAllocationHandle_t>(v);
+    return hipSuccess;
+  }
+  return real_create_charged(handle, size, prop, flags);
+}
+
+GS_EXPORT hipError_t hipMemAddressReserve(void** ptr, size_t size, size_t alignment, void* addr,
+                                          unsigned long long flags) {
+  auto f = real_hipMemAddressReserve();
+  if (!f) return hipErrorNotInitialized;
+  bool window = arena_configured() && !t_depth && size >= kWinAlign && !addr;
+  if (window && alignment < kWinAlign) alignment = kWinAlign;  // slots on granule boundaries
+  hipError_t e;
+  {
+    Depth d;
+    e = f(ptr, size, alignment, addr, flags);
+  }
+  if (e != hipSuccess || !window || !ptr || !*ptr || reinterpret_cast<uintptr_t>(*ptr) % kWinAlign) return e;
+  pthread_mutex_lock(&g_arena.mu);
+  if (g_nwin < kMaxWin) {
+    Win& w = g_win[g_nwin];
+    w.base = static_cast<char*>(*ptr);
+    w.size = size;
+    w.nslots = int((size + kWinAlign - 1) / kWinAlign);
+    w.slot_g = static_cast<int32_t*>(malloc(sizeof(int32_t) * size_t(w.nslots)));
+    w.slot_used = static_cast<uint64_t*>(calloc(size_t(w.nslots), sizeof(uint64_t)));
+    w.slot_real = static_cast<uint32_t*>(calloc(size_t(w.nslots), sizeof(uint32_t)));
+    if (w.slot_g && w.slot_used && w.slot_real) {
+      for (int i = 0; i < w.nslots; ++i) w.slot_g[i] = -1;
+      ++g_nwin;
+    } else {
+      free(w.slot_g), free(w.slot_used), free(w.slot_real);
+    }
+  }
+  pthread_mutex_unlock(&g_arena.mu);
+  return e;
+}
+
+GS_EXPORT hipError_t hipMemAddressFree(void* ptr, size_t size) {
+  auto f = real_hipMemAddressFree();
+  if (!f) return hipErrorNotInitialized;
+  if (ptr && arena_configured() && !t_depth) {
+    pthread_mutex_lock(&g_arena.mu);
+    for (int i = 0; i < g_nwin; ++i) {
+      if (g_win[i].base != ptr) continue;
+      Win& w = g_win[i];
+      for (int sl = 0; sl < w.nslots; ++sl)
+        if (w.slot_g[sl] >= 0) slot_return(w, sl);   // pages the program never unmapped
+      free(w.slot_g), free(w.slot_used), free(w.slot_real);
+      g_win[i] = g_win[--g_nwin];
+      break;
+    }
+    pthread_mutex_unlock(&g_arena.mu);
+  }
+  Depth d;
+  return f(ptr, size);
+}
+
+GS_EXPORT hipError_t hipMemMap(void* ptr, size_t size, size_t offset, hipMemGenericAllocationHandle_t handle,
+                               unsigned long long flags) {
+  auto f = real_hipMemMap();
+  if (!f) return hipErrorNotInitialized;
+  if (t_depth || !arena_configured()) return f(ptr, size, offset, handle, flags);
+  pthread_mutex_lock(&g_arena.mu);
+  if (!vh_has(handle)) {
+    pthread_mutex_unlock(&g_arena.mu);
+    return f(ptr, size, offset, handle, flags);
+  }
+  VHandle* v = reinterpret_cast<VHandle*>(handle);
+  char* va = static_cast<char*>(ptr);
+  hipError_t e = hipErrorInvalidValue;
+  Win* w = va && !v->at && offset == 0 && size == v->size ? win_of(va, size) : nullptr;
+  if (w) {
+    e = vmm_map(*w, v, va);
+    if (e != hipSuccess) {
+      vmm_unmap(v);
+      vmm_release_pieces(v);
+    } else {
+      g_pending_bytes -= v->size;
+      vva_put(va, v);
+    }
+  } else if (va && !v->at && offset == 0 && size == v->size) {
+    // outside every window: the driver's memory for it, mapped where asked
+    VPiece* pc = static_cast<VPiece*>(calloc(1, sizeof(VPiece)));
+    if (pc) {
+      e = real_create_charged(&pc->h, size, &v->prop, v->flags);
+      if (e == hipSuccess) {
+        Depth d;
+        e = f(va, size, 0, pc->h, flags);
+        if (e != hipSuccess) hipMemRelease(pc->h);
+      }
+      if (e == hipSuccess) {
+        pc->va = va;
+        pc->len = size;
+        v->pieces = pc;
+        v->npieces = 1;
+        v->at = va;
+        g_pending_bytes -= v->size;
+        vva_put(va, v);
+        ++g_vmm_real_pieces;
+      } else {
+        free(pc);
+      }
+    } else {
+      e = hipErrorOutOfMemory;
+    }
+  }
+  pthread_mutex_unlock(&g_arena.mu);
+  return e;
+}
+
+GS_EXPORT hipError_t hipMemUnmap(void* ptr, size_t size) {
+  auto f = real_hipMemUnmap();
+  if (!f) return hipErrorNotInitialized;
+  if (t_depth || !arena_configured() || !g_vva) return f(ptr, size);
+  pthread_mutex_lock(&g_arena.mu);
+  // the program unmaps what it mapped, one handle's range at a time (or several at once)
+  char* va = static_cast<char*>(ptr);
+  char* end = va + size;
+  bool any = false;
+  while (va < end) {
+    VHandle* v = vva_take(va);
+    if (!v) break;
+    any = true;
+    if (win_of(v->at, v->size)) {
+      vmm_unmap(v);
+    } else {  // the driver piece mapped outside the windows
+      Depth d;
+      (void)f(v->at, v->size);
+      v->at = nullptr;
+    }
+    va += v->size;
+  }
+  pthread_mutex_unlock(&g_arena.mu);
+  if (any) return va == end ? hipSuccess : f(va, size_t(end - va));
+  return f(ptr, size);
+}
+
+GS_EXPORT hipError_t hipMemSetAccess(void* ptr, size_t size, const hipMemAccessDesc* desc, size_t count) {
+  auto f = real_hipMemSetAccess();
+  if (!f) return hipErrorNotInitialized;
+  if (t_depth || !arena_configured() || !ptr || !g_nwin) return f(ptr, size, desc, count);
+  pthread_mutex_lock(&g_arena.mu);
+  Win* w = win_of(static_cast<char*>(ptr), size);
+  if (!w) {
+    pthread_mutex_unlock(&g_arena.mu);
+    return f(ptr, size, desc, count);
+  }
+  // slot by slot: the driver's memory in the range (real pages, driver pieces) gets the access
+  // asked for, run by run; an arena slot is one granule mapping, read-write for this device
+  // since it was backed: only access for other devices is set, on the whole granule
+  bool local_rw = true;
+  for (size_t k = 0; k < count; ++k)
+    local_rw = local_rw && desc[k].location.type == hipMemLocationTypeDevice && desc[k].location.id == g_dev &&
+               desc[k].flags == hipMemAccessFlagsProtReadWrite;
+  char* lo = static_cast<char*>(ptr);
+  char* hi = lo + size;
+  char* run = nullptr;  // start of the current run of driver memory
+  hipError_t e = hipSuccess;
+  Depth d;
+  for (char* p = lo; p < hi && e == hipSuccess;) {
+    int s = int(uint64_t(p - w->base) / kWinAlign);
+    char* send = w->base + uint64_t(s + 1) * kWinAlign;
+    char* q = send < hi ? send : hi;
+    if (w->slot_g[s] >= 0) {
+      if (run) e = f(run, size_t(p - run), desc, count), run = nullptr;
+      if (e == hipSuccess && !local_rw) e = f(w->base + uint64_t(s) * kWinAlign, kWinAlign, desc, count);
+    } else if (!run) {
+      run = p;
+    }
+    p = q;
+  }
+  if (run && e == hipSuccess) e = f(run, size_t(hi - run), desc, count);
+  pthread_mutex_unlock(&g_arena.mu);
+  return e;
+}
+
+GS_EXPORT hipError_t hipMemGetAllocationPropertiesFromHandle(hipMemAllocationProp* prop,
+                                                             hipMemGenericAllocationHandle_t handle) {
+  auto f = real_hipMemGetAllocationPropertiesFromHandle();
+  if (!f) return hipErrorNotInitialized;
+  if (arena_configured() && g_vh) {
+    pthread_mutex_lock(&g_arena.mu);
+    bool mine = vh_has(handle);
+    if (mine && prop) *prop = reinterpret_cast<VHandle*>(handle)->prop;
+    pthread_mutex_unlock(&g_arena.mu);
+    if (mine) return prop ? hipSuccess : hipErrorInvalidValue;
+  }
+  return f(prop, handle);
+}
+
+GS_EXPORT hipError_t hipMemExportToShareableHandle(void* out, hipMemGenericAllocationHandle_t handle,
+                                                   hipMemAllocationHandleType type, unsigned long long flags) {
+  auto f = real_hipMemExportToShareableHandle();
+  if (!f) return hipErrorNotInitialized;
+  if (arena_configured() && g_vh) {
+    pthread_mutex_lock(&g_arena.mu);
+    bool mine = vh_has(handle);
+    pthread_mutex_unlock(&g_arena.mu);
+    // an arena page is part of a granule another pod had and will have: it is never exported
+    if (mine) return hipErrorNotSupported;
+  }
+  return f(out, handle, type, flags);
+}
+
 GS_EXPORT hipError_t hipMemRelease(hipMemGenericAllocationHandle_t handle) {
   auto f = real_hipMemRelease();
   if (!f) return hipErrorNotInitialized;
+  if (arena_configured() && g_vh) {
+    pthread_mutex_lock(&g_arena.mu);
+    if (vh_has(handle)) {
+      VHandle* v = reinterpret_cast<VHandle*>(handle);
+      if (v->at) {  // released while mapped: the mapping goes with it
+        char* at = v->at;
+        (void)vva_take(at);
+        if (win_of(at, v->size)) {
+          vmm_unmap(v);
+        } else if (auto un = real_hipMemUnmap()) {
+          Depth d;
+          (void)un(at, v->size);
+          v->at = nullptr;
+        }
+      } else if (!v->npieces) {
+        g_pending_bytes -= v->size;
+      }
+      vh_del(v);
+      pthread_mutex_unlock(&g_arena.mu);
+      vmm_release_pieces(v);
+      v->magic = 0;
+      free(v);
+      return hipSuccess;
+    }
+    pthread_mutex_unlock(&g_arena.mu);
+  }
   if (!hip_active()) return f(handle);
   hipError_t e;
   {
@@ -1574,8 +2276,18 @@ GS_EXPORT hipError_t hipMemGetInfo(size_t* free_b, size_t* total_b) {
   if (free_b && *free_b > left) *free_b = (size_t)left;
   if (total_b) *total_b = (size_t)quota;
   uint64_t asz = 0, aused = 0;
-  if (free_b && arena_configured() && gpushare_shim_arena_stats(&asz, &aused))
-    *free_b = (size_t)(asz - aused);  // with a broker arena, hipMalloc is served from the arena's rest
+  if (free_b && arena_configured() && gpushare_shim_arena_stats(&asz, &aused)) {
+    // with a broker arena: what its rest serves (every entry point allocates from it), plus what
+    // the quota still lets the driver give
+    uint64_t room = asz - aused;
+    pthread_mutex_lock(&g_arena.mu);
+    for (int i = 0; i < g_nwin; ++i)
+      for (int sl = 0; sl < g_win[i].nslots; ++sl)
+        if (g_win[i].slot_g[sl] >= 0) room += kWinAlign - g_win[i].slot_used[sl];
+    pthread_mutex_unlock(&g_arena.mu);
+    *free_b = (size_t)(room + *free_b);
+    if (*free_b > quota) *free_b = (size_t)quota;
+  }
   return e;
 }
 

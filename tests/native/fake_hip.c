@@ -16,6 +16,7 @@
 #include <stdio.h>
 #include <sys/syscall.h>
 #include <unistd.h>
+#include <time.h>
 typedef int hipError_t;
 struct kfd_alloc { uint64_t va, size, handle, mmap_offset; uint32_t gpu_id, flags; };
 struct kfd_free { uint64_t handle; };
@@ -89,7 +90,29 @@ int ioctl(int fd, unsigned long req, ...) {
    free range (map + unmap), issues the allocation ioctl, then maps that range MAP_FIXED and
    trims it. Whatever the process mapped inside the range meanwhile (the shim initialising
    inside that ioctl) is silently replaced. */
+/* FAKE_HIP_HELD_GIB / FAKE_HIP_HELD_MS: that much of the device is held by "another process"
+   (pods of a previous broker) until that many ms after start */
+static size_t g_held = 0;
+static double g_held_until = 0;
+static double fake_now(void);
+static void total_init(void) {     /* FAKE_HIP_TOTAL_GIB: the "device" size (default 16 GiB) */
+  static int done = 0;
+  if (__atomic_exchange_n(&done, 1, __ATOMIC_ACQ_REL)) return;
+  const char* tg = getenv("FAKE_HIP_TOTAL_GIB");
+  if (tg && atof(tg) > 0) g_total = (size_t)(atof(tg) * (double)(1ull << 30));
+  const char* hg = getenv("FAKE_HIP_HELD_GIB");
+  const char* hm = getenv("FAKE_HIP_HELD_MS");
+  if (hg && atof(hg) > 0) {
+    g_held = (size_t)(atof(hg) * (double)(1ull << 30));
+    __atomic_add_fetch(&g_used, g_held, __ATOMIC_ACQ_REL);
+    g_held_until = fake_now() + (hm ? atof(hm) : 0) / 1e3;
+  }
+}
+static void held_release(void) {
+  if (g_held && fake_now() >= g_held_until) { __atomic_fetch_sub(&g_used, g_held, __ATOMIC_ACQ_REL); g_held = 0; }
+}
 static int kfd(size_t n, uint64_t* h) {
+  total_init();
   struct kfd_alloc a = {0, n, 0, 0, 1, 1u /* VRAM */};
   const char* pf = getenv("FAKE_HIP_PROBE_FIXED");
   void* probe = NULL;
@@ -137,8 +160,8 @@ static void runtime_init(void) {
   const char* v = getenv("FAKE_HIP_INIT_KFD");
   if (v && *v == '1') { uint64_t h; kfd((size_t)2 << 20, &h); }
 }
-hipError_t hipMemGetInfo(size_t* f, size_t* t) { runtime_init(); *f = g_total - __atomic_load_n(&g_used, __ATOMIC_ACQUIRE); *t = g_total; return 0; }
-hipError_t hipDeviceTotalMem(size_t* b, int d) { *b = g_total; return 0; }
+hipError_t hipMemGetInfo(size_t* f, size_t* t) { total_init(); held_release(); runtime_init(); *f = g_total - __atomic_load_n(&g_used, __ATOMIC_ACQUIRE); *t = g_total; return 0; }
+hipError_t hipDeviceTotalMem(size_t* b, int d) { total_init(); *b = g_total; return 0; }
 hipError_t hipMemCreate(uint64_t* h, size_t n, const void* prop, unsigned long long fl) { return kfd(n, h); }
 hipError_t hipMemRelease_imported(uint64_t h);
 hipError_t hipMemRelease(uint64_t h) { if (h & (1ull << 62)) return hipMemRelease_imported(h); kfd_release(h); return 0; }
@@ -158,9 +181,13 @@ hipError_t hipMemImportFromShareableHandle(uint64_t* h, void* os, int type) {
 }
 hipError_t hipMemRelease_imported(uint64_t h) { close((int)(h & 0xffffffff)); return 0; }
 hipError_t hipMemAddressReserve(void** p, size_t n, size_t al, void* addr, unsigned long long fl) {
-  void* m = mmap(0, n, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+  if (al < 4096) al = 4096;
+  char* m = mmap(0, n + al, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
   if (m == MAP_FAILED) return 2;
-  *p = m; return 0;
+  char* a = (char*)(((uintptr_t)m + al - 1) / al * al);      /* honour the alignment: trim both ends */
+  if (a > m) munmap(m, (size_t)(a - m));
+  if (m + n + al > a + n) munmap(a + n, (size_t)(m + n + al - (a + n)));
+  *p = a; return 0;
 }
 hipError_t hipMemAddressFree(void* p, size_t n) { munmap(p, n); return 0; }
 hipError_t hipMemMap(void* p, size_t n, size_t off, uint64_t h, unsigned long long fl) { return 0; }
@@ -185,9 +212,8 @@ hipError_t hipDeviceGetByPCIBusId(int* d, const char* bdf) { *d = 0; return 0; }
 const char* hipGetErrorString(hipError_t e) { return "fake hip error"; }
 /* events: hipEventRecord completes FAKE_HIP_EVENT_MS after it was recorded (0 = at once), so a
    test can hold the broker's asynchronous scrub, or a stream-ordered free, in flight */
-#include <time.h>
 struct fake_event { double done_at; };
-static double fake_now(void) { struct timespec t; clock_gettime(CLOCK_MONOTONIC, &t); return t.tv_sec + t.tv_nsec * 1e-9; }
+static double fake_now(void) { struct timespec t; clock_gettime(CLOCK_MONOTONIC, &t); return t.tv_sec + t.tv_nsec * 1e-9; }  /* (declared above) */
 hipError_t hipEventCreateWithFlags(void** e, unsigned f) {
   struct fake_event* ev = calloc(1, sizeof *ev);
   if (!ev) return 2;
@@ -206,3 +232,8 @@ hipError_t hipEventSynchronize(void* e) {
   return 0;
 }
 hipError_t hipEventDestroy(void* e) { free(e); return 0; }
+/* stream capture never on; the default pool is a token (hipMallocFromPoolAsync = hipMallocAsync) */
+hipError_t hipStreamIsCapturing(void* s, int* st) { *st = 0; return 0; }
+hipError_t hipDeviceGetDefaultMemPool(void** pool, int dev) { *pool = (void*)0x1; return 0; }
+hipError_t hipMallocFromPoolAsync(void** p, size_t n, void* pool, void* s) { return hipMallocAsync(p, n, s); }
+hipError_t hipMemGetAllocationPropertiesFromHandle(void* prop, uint64_t h) { return 1; }

@@ -44,6 +44,16 @@ hipError_t hipMalloc(void**, size_t); hipError_t hipFree(void*);
 hipError_t hipMemGetInfo(size_t*, size_t*); hipError_t hipMallocAsync(void**, size_t, void*);
 hipError_t hipFreeAsync(void*, void*); hipError_t hipMemCreate(uint64_t*, size_t, const void*, unsigned long long);
 hipError_t hipMemRelease(uint64_t); hipError_t hipMemPoolTrimTo(void*, size_t); int fake_runtime_scratch(size_t);
+hipError_t hipMemAddressReserve(void**, size_t, size_t, void*, unsigned long long); hipError_t hipMemAddressFree(void*, size_t);
+hipError_t hipMemMap(void*, size_t, size_t, uint64_t, unsigned long long); hipError_t hipMemUnmap(void*, size_t);
+hipError_t hipMemSetAccess(void*, size_t, const void*, size_t);
+hipError_t hipMallocFromPoolAsync(void**, size_t, void*, void*); hipError_t hipDeviceGetDefaultMemPool(void**, int);
+/* hipMemAllocationProp / hipMemAccessDesc as laid out in hip/hip_runtime_api.h, driver_types.h */
+struct vprop { int type; int htype; struct { int type; int id; } loc; void* w32; unsigned char ct, rdma; unsigned short usage; };
+struct vaccess { struct { int type; int id; } loc; int flags; };
+/* VMM the way PyTorch's expandable segments use it: one reserved range, pages mapped one after another */
+static char* g_vbase = 0; static size_t g_vsize = 0, g_vcur = 0;
+static struct { char* va; uint64_t h; size_t n; } g_vpages[8192]; static int g_nv = 0;
 // "threads N ITERS SIZE": N threads each alloc+free SIZE bytes ITERS times (quota contention)
 struct targ { int iters; size_t n; int ok, denied; };
 static void* worker(void* v) {
@@ -68,7 +78,8 @@ int main(int argc, char** argv) {
       printf("{\"op\":\"arenarelease\",\"r\":%d}\n", f ? f() : -2); fflush(stdout); }
     else if (!strcmp(argv[i], "sleepms")) { fflush(stdout); usleep((useconds_t)atoi(argv[++i]) * 1000); }
     else if (!strcmp(argv[i], "async")) { size_t n = strtoull(argv[++i], 0, 10); void* p = 0; int e = hipMallocAsync(&p, n, 0);
-      printf("{\"op\":\"async\",\"n\":%zu,\"err\":%d,\"idx\":%d}\n", n, e, e ? -1 : np); if (!e) ptrs[np++] = p; }
+      printf("{\"op\":\"async\",\"n\":%zu,\"err\":%d,\"idx\":%d,\"p\":%llu}\n", n, e, e ? -1 : np,
+             (unsigned long long)(uintptr_t)p); if (!e) ptrs[np++] = p; }
     else if (!strcmp(argv[i], "vmm")) { size_t n = strtoull(argv[++i], 0, 10); uint64_t h = 0; int e = hipMemCreate(&h, n, 0, 0);
       printf("{\"op\":\"vmm\",\"n\":%zu,\"err\":%d}\n", n, e); if (!e) hipMemRelease(h); }
     else if (!strcmp(argv[i], "freeasync")) { int k = atoi(argv[++i]); int e = hipFreeAsync(ptrs[k], 0); ptrs[k] = 0;
@@ -135,6 +146,32 @@ int main(int argc, char** argv) {
       int r = ioctl(g_render_fd, req, &a); printf("{\"op\":\"prime\",\"err\":%d,\"fd\":%d}\n", r ? errno : 0, a.fd); }
     else if (!strcmp(argv[i], "sleep")) { usleep((useconds_t)(atof(argv[++i]) * 1e6)); }
     else if (!strcmp(argv[i], "crash")) { fflush(stdout); _exit(3); }
+    else if (!strcmp(argv[i], "vres")) { g_vsize = strtoull(argv[++i], 0, 10); void* b = 0;
+      int e = hipMemAddressReserve(&b, g_vsize, 0, 0, 0); g_vbase = (char*)b; g_vcur = 0;
+      printf("{\"op\":\"vres\",\"err\":%d,\"aligned\":%d}\n", e, (int)(((uintptr_t)b & ((1ull << 30) - 1)) == 0)); }
+    else if (!strcmp(argv[i], "vpage")) { size_t n = strtoull(argv[++i], 0, 10); uint64_t h = 0;
+      struct vprop pr; memset(&pr, 0, sizeof pr); pr.type = 1; pr.loc.type = 1; pr.loc.id = 0;
+      int e = hipMemCreate(&h, n, &pr, 0), me = -1, ae = -1;
+      if (!e) { me = hipMemMap(g_vbase + g_vcur, n, 0, h, 0);
+        struct vaccess ac; memset(&ac, 0, sizeof ac); ac.loc.type = 1; ac.flags = 3;
+        if (!me) { ae = hipMemSetAccess(g_vbase + g_vcur, n, &ac, 1); g_vpages[g_nv].va = g_vbase + g_vcur;
+          g_vpages[g_nv].h = h; g_vpages[g_nv].n = n; g_nv++; g_vcur += n; } else hipMemRelease(h); }
+      printf("{\"op\":\"vpage\",\"n\":%zu,\"err\":%d,\"map\":%d,\"access\":%d,\"idx\":%d}\n", n, e, me, ae, e || me ? -1 : g_nv - 1); }
+    else if (!strcmp(argv[i], "vdrop")) { int k = atoi(argv[++i]); int ue = hipMemUnmap(g_vpages[k].va, g_vpages[k].n);
+      int re = hipMemRelease(g_vpages[k].h); printf("{\"op\":\"vdrop\",\"unmap\":%d,\"release\":%d}\n", ue, re); }
+    else if (!strcmp(argv[i], "vfree")) { int e = hipMemAddressFree(g_vbase, g_vsize); printf("{\"op\":\"vfree\",\"err\":%d}\n", e); }
+    else if (!strcmp(argv[i], "vstats")) {
+      int (*f)(uint64_t*, uint64_t*, uint64_t*, uint64_t*, uint64_t*) =
+          (int (*)(uint64_t*, uint64_t*, uint64_t*, uint64_t*, uint64_t*))dlsym(RTLD_DEFAULT, "gpushare_shim_vmm_stats");
+      uint64_t c = 0, am = 0, rp = 0, sb = 0, sn = 0; int w = f ? f(&c, &am, &rp, &sb, &sn) : -2;
+      printf("{\"op\":\"vstats\",\"windows\":%d,\"creates\":%llu,\"arena_maps\":%llu,\"real_pieces\":%llu,"
+             "\"slots_backed\":%llu,\"slots_now\":%llu}\n", w, (unsigned long long)c, (unsigned long long)am,
+             (unsigned long long)rp, (unsigned long long)sb, (unsigned long long)sn); }
+    else if (!strcmp(argv[i], "poolasync")) { size_t n = strtoull(argv[++i], 0, 10); void* pool = 0; void* p = 0;
+      hipDeviceGetDefaultMemPool(&pool, 0); int e = hipMallocFromPoolAsync(&p, n, pool, 0);
+      printf("{\"op\":\"poolasync\",\"n\":%zu,\"err\":%d,\"idx\":%d,\"p\":%llu}\n", n, e, e ? -1 : np,
+             (unsigned long long)(uintptr_t)p); if (!e) ptrs[np++] = p; }
+    else if (!strcmp(argv[i], "wait")) { fflush(stdout); char b[256]; while (read(0, b, sizeof b) > 0) {} }  /* until stdin closes */
     fflush(stdout);
   }
   return 0;

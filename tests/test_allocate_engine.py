@@ -581,19 +581,24 @@ def test_prepared_body_is_the_container_response(tmp_path, shim, ledgers, disabl
 
 
 class _FakeBrokerAdmin:
-    """The admin socket of one GPU's HBM broker: records GRANTs and answers OK."""
+    """The admin socket of one GPU's HBM broker: records GRANTs / REVOKEs, answers OK, and STAT /
+    LIST with a fixed boot id."""
 
-    def __init__(self, path, ok=True):
+    def __init__(self, path, ok=True, boot="b00t"):
         import socket as _s
 
-        self.grants = []
-        self.ok = ok
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        self.grants, self.revokes = [], []
+        self.held: dict = {}
+        self.ok, self.boot = ok, boot
         self.ls = _s.socket(_s.AF_UNIX, _s.SOCK_STREAM)
         self.ls.bind(path)
         self.ls.listen(16)
         threading.Thread(target=self._serve, daemon=True).start()
 
     def _serve(self):
+        import json as _j
+
         while True:
             try:
                 c, _ = self.ls.accept()
@@ -605,27 +610,46 @@ class _FakeBrokerAdmin:
                 if not chunk:
                     break
                 buf += chunk
-            _, tok, nbytes = buf.decode().split()
-            self.grants.append((tok, int(nbytes)))
-            c.sendall(f"OK {int(nbytes) >> 30}\n".encode() if self.ok else b"ERR size\n")
+            w = buf.decode().split()
+            if w[:1] == ["STAT"]:
+                c.sendall((_j.dumps({"boot": self.boot}) + "\n").encode())
+            elif w[:1] == ["LIST"]:
+                c.sendall((_j.dumps({"boot": self.boot, "grants": self.held}) + "\n").encode())
+            elif w[:1] == ["REVOKE"]:
+                self.revokes.append(w[1])
+                self.held.pop(w[1], None)
+                c.sendall(b"OK 0\n")
+            else:
+                _, tok, nbytes = w
+                self.grants.append((tok, int(nbytes)))
+                if self.ok:
+                    self.held[tok] = int(nbytes) >> 30
+                c.sendall(f"OK {int(nbytes) >> 30}\n".encode() if self.ok else b"ERR size\n")
             c.close()
 
 
 def test_hbm_broker_grant_rides_in_the_prepared_answer(tmp_path):
-    """With --hbm-broker-dir the answer mounts the broker directory, names the GPU's socket and
-    carries the pod's token, granted on that GPU's broker while the answer is prepared; the
-    hand-encoded prepared answer and the field-by-field one stay equal, and a re-prepared answer
-    grants nothing new. An unreachable broker leaves the token out (the pod uses the driver)."""
+    """With --hbm-broker-dir the answer mounts only the GPU's pod-socket directory (read-only; the
+    admin sockets stay outside it), names the GPU's socket and carries the pod's token, granted on
+    that GPU's broker off the thread that prepares the answer; the hand-encoded prepared answer and
+    the field-by-field one stay equal, and a re-prepared answer grants nothing new. Tokens come
+    from the node secret (0600), so a new plugin instance derives the same ones. A GPU whose
+    broker never appears gets tokens during the start-up grace (the pod waits for it), then none
+    (the pod allocates from the driver at once)."""
+    import time as _t
+
     from aliyun_gpushare_device_plugin_amd.quota import hbmbroker
 
     model = DeviceModel([gpu(i, 64 << 30) for i in range(2)], const.GIB)
     src = StaticSource([])
     hdir = tmp_path / "hbm"
     hdir.mkdir()
-    admin = _FakeBrokerAdmin(str(hdir / (hbmbroker.socket_name(1) + ".admin")))
-    opts = AllocatorOptions(shim=ShimConfig(host_dir=str(tmp_path / "shim")), hbm_broker_dir=str(hdir))
+    admin = _FakeBrokerAdmin(hbmbroker.admin_socket(str(hdir), 1))
+    opts = AllocatorOptions(shim=ShimConfig(host_dir=str(tmp_path / "shim")), hbm_broker_dir=str(hdir),
+                            hbm_granter_args={"poll_s": 0.1, "startup_grace_s": 1.0, "down_grace_s": 0.5})
     al = Allocator(model, src, FakeClient(src), NODE, opts)
     try:
+        assert oct(os.stat(hbmbroker.secret_path(str(hdir))).st_mode & 0o777) == "0o600"
         pod = mkpod("h0", 16, 1, 10)
         c = al._prepared(pod, "uid-h0", 1, 16)
         got = api.AllocateResponse.FromString(c.body).container_responses[0]
@@ -633,24 +657,29 @@ def test_hbm_broker_grant_rides_in_the_prepared_answer(tmp_path):
         assert got == want
         tok = got.envs[const.ENV_HBM_TOKEN]
         assert got.envs[const.ENV_HBM_BROKER] == f"{const.HBM_BROKER_CONTAINER_DIR}/hbm1.sock"
-        assert any(m.container_path == const.HBM_BROKER_CONTAINER_DIR and m.host_path == str(hdir) for m in got.mounts)
-        # 16 of 64 GiB -> a 16 GiB quota; 94 % of it in whole granules = 15 GiB, granted once,
-        # off the thread that prepares the answer
+        mounts = [m for m in got.mounts if m.container_path == const.HBM_BROKER_CONTAINER_DIR]
+        assert len(mounts) == 1 and mounts[0].host_path == str(hdir / "gpu1") and mounts[0].read_only
+        # 16 of 64 GiB -> a 16 GiB quota; 94 % of it in whole granules = 15 GiB, granted once
         assert al._hbm.flush()
         assert admin.grants == [(tok, 15 << 30)]
         assert al._prepared(pod, "uid-h0", 1, 16).body == c.body
         assert al._hbm.flush() and len(admin.grants) == 1
-        # GPU 0 has no broker: the first answer carries its token (the grant is not known to
-        # fail yet; the pod's TAKE would time out), later ones do not, and the broker is not
-        # asked again on every answer
+        # the same node secret in another instance: the same token for the same pod and slot
+        g2 = hbmbroker.HBMGranter(str(hdir), start=False)
+        assert g2.token("uid-h0", 0) == tok and g2.token("uid-h0", 1) != tok
+        # GPU 0 has no broker: within the start-up grace its answers carry the token (the shim
+        # waits for the broker); once the grace is over they do not
         r0 = al._container_response(0, 16, 16, "uid-h1", 0, None)
-        assert r0.envs[const.ENV_HBM_BROKER].endswith("hbm0.sock")
-        assert al._hbm.flush() and al._hbm.failures == 1
+        assert const.ENV_HBM_TOKEN in r0.envs and r0.envs[const.ENV_HBM_BROKER].endswith("hbm0.sock")
+        _t.sleep(1.3)
+        assert al._hbm.reconcile_now()
         r2 = al._container_response(0, 16, 16, "uid-h2", 0, None)
         assert const.ENV_HBM_TOKEN not in r2.envs
-        assert al._hbm.flush() and al._hbm.failures == 1       # backed off: no second connect
+        r3 = al._container_response(1, 16, 16, "uid-h3", 0, None)      # GPU 1's broker is up
+        assert const.ENV_HBM_TOKEN in r3.envs
         # too small for two granules: no arena, no grant
-        small = al._container_response(1, 1, 1, "uid-h3", 0, None)
-        assert const.ENV_HBM_TOKEN not in small.envs and len(admin.grants) == 1
+        small = al._container_response(1, 1, 1, "uid-h4", 0, None)
+        assert const.ENV_HBM_TOKEN not in small.envs
+        assert al._hbm.flush() and {t for t, _ in admin.grants} == {tok, r3.envs[const.ENV_HBM_TOKEN]}
     finally:
         al.close()

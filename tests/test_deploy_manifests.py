@@ -36,7 +36,7 @@ def test_manifests_parse_and_have_kinds():
 def test_daemonset_flags_are_accepted_by_the_cli():
     cmd = _ds()["containers"][0]["command"]
     cfg = config_from_args(build_parser().parse_args([a for a in cmd[1:] if a.startswith("--")]))
-    assert cfg.memory_unit == const.GIB
+    assert cfg.memory_unit == const.GIB and cfg.hbm_broker_dir == "/var/run/gpushare/hbm"
     # the commented-out isolation flag is valid too
     assert config_from_args(build_parser().parse_args(["--compute-isolation=cu"])).compute_isolation == "cu"
 
@@ -63,23 +63,27 @@ def _ds(name="gpushare-device-plugin-ds"):
     return ds[0]["spec"]["template"]["spec"]
 
 
-def test_hbm_broker_daemonset_matches_the_plugin_flag():
-    """The opt-in broker DaemonSet: its flags are the launcher's, it serves the directory the
-    plugin's (commented) --hbm-broker-dir names, from a hostPath, privileged for /dev/kfd."""
+def test_hbm_brokers_ship_on_by_default_with_the_plugin():
+    """The default deployment runs what the bench measures: the brokers are a container of the
+    plugin's own DaemonSet (no opt-in), the plugin's --hbm-broker-dir names the directory they
+    serve, both containers mount it from the same hostPath, and the broker container is privileged
+    for /dev/kfd. Only the plugin and the brokers mount the whole directory: a shared container
+    gets its GPU's gpu<i>/ only (tests/test_allocate_engine.py), never admin/."""
     from aliyun_gpushare_device_plugin_amd.cli import hbmbroker
 
-    spec = _ds("gpushare-hbm-broker-ds")
-    c = spec["containers"][0]
-    assert c["command"][0] == "gpushare-hbm-brokers" and c["securityContext"]["privileged"] is True
-    a = hbmbroker.build_parser().parse_args(c["command"][1:])
-    mounts = {m["mountPath"]: m for m in c["volumeMounts"]}
+    ds = [d for _, d in _docs() if d["kind"] == "DaemonSet"]
+    assert [d["metadata"]["name"] for d in ds] == ["gpushare-device-plugin-ds"]   # one DaemonSet: the product
+    spec = _ds()
+    plugin, brokers = spec["containers"]
+    assert brokers["name"] == "hbm-brokers" and brokers["command"][0] == "gpushare-hbm-brokers"
+    assert brokers["securityContext"]["privileged"] is True
+    a = hbmbroker.build_parser().parse_args(brokers["command"][1:])
+    cfg = config_from_args(build_parser().parse_args([x for x in plugin["command"][1:] if x.startswith("--")]))
+    assert cfg.hbm_broker_dir == a.dir == "/var/run/gpushare/hbm"
     vols = {v["name"]: v for v in spec["volumes"]}
-    assert vols[mounts[a.dir]["name"]]["hostPath"]["path"] == a.dir
-    with open(os.path.join(ROOT, "deploy", "device-plugin-ds.yaml")) as f:
-        line = next(ln for ln in f if "--hbm-broker-dir=" in ln)
-    flag = line.split("#", 1)[1].strip().split()[1]
-    cfg = config_from_args(build_parser().parse_args([flag]))
-    assert cfg.hbm_broker_dir == a.dir
+    for c in (plugin, brokers):
+        m = {x["mountPath"]: x for x in c["volumeMounts"]}[a.dir]
+        assert vols[m["name"]]["hostPath"]["path"] == a.dir and not m.get("readOnly")
 
 
 def test_daemonset_can_open_kfd_and_render_nodes():

@@ -39,12 +39,12 @@ def _stop(p):
             p.kill()
 
 
-def test_shipped_manifests_run_a_node(hostroot):
+def test_shipped_manifests_run_a_node(hostroot, stub_runtime, native_shim):
     api = FakeAPIServer()
     api.start()
     client = APIClient(KubeConfig(api.url))
     client.create_node(make_node(NODE))
-    plugin = ext = None
+    plugin = ext = brokers = None
     kubelet = FakeKubelet(os.path.join(hostroot, "device-plugin"), APIClient(KubeConfig(api.url)), NODE).start()
     try:
         # ---- the DaemonSet, as the kubelet would start it on NODE
@@ -63,6 +63,14 @@ def test_shipped_manifests_run_a_node(hostroot):
         assert ct.host_path("/var/lib/kubelet/device-plugins") == kubelet.dir
         assert ct.env["NODE_NAME"] == NODE
         plugin = D.start(ct, os.path.join(hostroot, "plugin.log"))
+        # the DaemonSet's second container: one HBM broker per GPU (no GPU here: the brokers are the
+        # stub runtime's, over the same fake node the plugin sees)
+        bct = D.resolve(ds, hostroot, {"spec.nodeName": NODE}, {"--smi-backend": "fake:2x288G"}, skip_volumes=("sys",),
+                        container="hbm-brokers")
+        assert bct.host_path("/var/run/gpushare/hbm") == ct.host_path("/var/run/gpushare/hbm")   # one hostPath
+        bct.env.update(GPUSHARE_HBM_BROKER_EXE=os.path.join(stub_runtime, "gpushare-hbm-broker"),
+                       LD_LIBRARY_PATH=stub_runtime, FAKE_HIP_TOTAL_GIB="288")
+        brokers = D.start(bct, os.path.join(hostroot, "brokers.log"))
         assert kubelet.registered.wait(60), open(os.path.join(hostroot, "plugin.log")).read()[-3000:]
         assert D.wait_for(lambda: O.node_allocatable(client.get_node(NODE), const.RESOURCE_NAME) == 576, 30)
         # the probes the manifest declares (port remapped from 9400)
@@ -123,14 +131,53 @@ def test_shipped_manifests_run_a_node(hostroot):
         gpus = {O.annotations(client.get_pod("default", O.name(p)))[const.ENV_RESOURCE_INDEX] for p in pods}
         assert len(gpus) == 1
 
+        # ---- a 64 GiB pod (deploy/demo/llama-colocate.yaml) takes its HBM from its GPU's broker
+        from aliyun_gpushare_device_plugin_amd.quota import hbmbroker as hb
+
+        hdir = ct.host_path("/var/run/gpushare/hbm")
+        dep = next(d for d in D.load(os.path.join(ROOT, "deploy", "demo", "llama-colocate.yaml")) if d["kind"] == "Deployment")
+        tpl = D.pod_template(dep)
+        big = client.create_pod("default", {"apiVersion": "v1", "kind": "Pod",
+                                            "metadata": {"name": "llama-0", "namespace": "default"},
+                                            "spec": {**tpl["spec"], "schedulerName": "default-scheduler"}})
+        placed = []
+        assert D.wait_for(lambda: placed.append(sched.schedule(big, [NODE])) or placed[-1] == NODE, 10, 0.1)
+        adm = kubelet.admit(client.get_pod("default", "llama-0"))
+        assert adm.error is None, adm.error
+        r = adm.responses[0]
+        gi = int(r.envs[const.ENV_RESOURCE_INDEX])
+        tok = r.envs[const.ENV_HBM_TOKEN]
+        mounts = {m.container_path: m for m in r.mounts}
+        assert mounts[const.HBM_BROKER_CONTAINER_DIR].host_path == hb.pod_dir(hdir, gi)   # its GPU's sockets only
+        assert mounts[const.HBM_BROKER_CONTAINER_DIR].read_only
+        assert not any(m.host_path.startswith(hb.admin_dir(hdir)) for m in r.mounts)
+        st = {}
+        assert D.wait_for(lambda: st.update(hb.HBMBroker.attach(hb.pod_socket(hdir, gi), hb.admin_socket(hdir, gi))
+                                            .list()) or tok in st.get("grants", {}), 30, 0.2), \
+            open(os.path.join(hostroot, "brokers.log")).read()[-3000:]
+        # the container's process: the answer's env with its mounts resolved to host paths
+        env = dict(r.envs)
+        for k, v in list(env.items()):
+            for cpath, m in sorted(mounts.items(), key=lambda x: -len(x[0])):
+                if v == cpath or v.startswith(cpath.rstrip("/") + "/"):
+                    env[k] = m.host_path + v[len(cpath.rstrip("/")):]
+                    break
+        assert os.path.isfile(env["LD_PRELOAD"])
+        env.update(LD_LIBRARY_PATH=stub_runtime, FAKE_HIP_TOTAL_GIB="288")
+        p = subprocess.run([os.path.join(stub_runtime, "shim_driver"), "alloc", str(32 << 30), "arena"],
+                           env=dict(os.environ, **env), capture_output=True, text=True, timeout=60)
+        out = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+        assert '"op":"arena","on":1,"size":64424509440' in out[-1], (out, p.stderr[-2000:])   # 60 GiB: 94 % of 64
+
         # ---- kubectl-inspect-gpushare against the same apiserver
         r = subprocess.run([sys.executable, "-m", D.ENTRY_POINTS["kubectl-inspect-gpushare"], "--apiserver", api.url],
                            capture_output=True, text=True, timeout=60,
                            env=dict(os.environ, PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", "")))
         assert r.returncode == 0, r.stdout + r.stderr
-        assert NODE in r.stdout and "8/576" in r.stdout.replace(" ", ""), r.stdout
+        assert NODE in r.stdout and "72/576" in r.stdout.replace(" ", ""), r.stdout   # 4 x 2 + 64 GiB
     finally:
         _stop(ext)
+        _stop(brokers)
         _stop(plugin)
         kubelet.stop()
         api.stop()

@@ -375,3 +375,36 @@ def test_hostile_input_ends_only_that_connection(broker):
     assert p.result()[0] == f"FDS 1 {GIB}"
     p.close()
     assert oct(os.stat(adm).st_mode & 0o777) == "0o600"
+
+
+def test_a_restarted_broker_grows_back_when_old_tenants_exit(broker_exe, tmp_path):
+    """After a broker restart, pods of the previous instance still hold their granules (imported
+    dma-bufs keep the memory alive, measured on MI355X: docs/HBM_TURNOVER.md, exporter death).
+    The new broker starts with what is free and takes the rest once it is back (the stub holds
+    6 of 16 GiB for 1.5 s), zeroing the new granules before it lends them."""
+    exe, libdir = broker_exe
+    env = dict(os.environ, LD_LIBRARY_PATH=libdir, ASAN_OPTIONS="detect_leaks=0:halt_on_error=1",
+               FAKE_HIP_TOTAL_GIB="16", FAKE_HIP_HELD_GIB="6", FAKE_HIP_HELD_MS="1500")
+    path = str(tmp_path / "hbm0.sock")
+    p = subprocess.Popen([exe, "--socket", path, "--reserve-gib", "2", "--release-policy", "trust"],
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
+    try:
+        ready = json.loads(p.stdout.readline())
+        assert ready["granules"] == 8                       # 16 - 6 held - 2 reserve
+        st = json.loads(_line(path + ".admin", "STAT"))
+        assert st["granules_max"] == 14 and st["free"] == 8
+        t = time.monotonic() + 10
+        while time.monotonic() < t:
+            st = json.loads(_line(path + ".admin", "STAT"))
+            if st["granules"] == 14 and st["free"] == 14:
+                break
+            time.sleep(0.1)
+        assert st["granules"] == 14 and st["grown"] == 6 and st["free"] == 14, st
+        assert st["scrubbed_bytes"] >= 6 * GIB                # the new granules were zeroed first
+        assert _line(path + ".admin", f"GRANT {'g' * 32} {13 * GIB}") == "OK 13"
+        pod = Pod(path, "g" * 32)
+        assert pod.result()[0] == f"FDS 13 {GIB}"
+        pod.close()
+    finally:
+        p.terminate()
+        assert p.wait(10) == 0

@@ -31,19 +31,23 @@ def test_launcher_runs_one_broker_per_gpu_and_restarts_a_dead_one(tmp_path, monk
     d.mkdir()
     with SMI("fake:2x64G") as s:
         gpus = [s.device(i) for i in range(s.count())]
-    brokers = {g.index: cli.HBMBroker(str(d / cli.socket_name(g.index)), pci_bus_id=g.bdf) for g in gpus}
+    brokers = {g.index: cli.HBMBroker.for_gpu(str(d), g.index, pci_bus_id=g.bdf) for g in gpus}
     sup = cli.Supervisor(brokers, backoff_s=0.1)
     try:
         sup.start()
         for g in gpus:
-            args = json.loads((d / f"hbm{g.index}.sock.args").read_text().splitlines()[0])
+            args = json.loads((d / f"gpu{g.index}" / f"hbm{g.index}.sock.args").read_text().splitlines()[0])
             assert args[args.index("--pci-bus-id") + 1] == g.bdf        # by PCI address, not HIP order
+            # the pod socket in the GPU's own directory, the admin socket apart (never mounted)
+            assert args[args.index("--socket") + 1] == str(d / f"gpu{g.index}" / f"hbm{g.index}.sock")
+            assert args[args.index("--admin-socket") + 1] == str(d / "admin" / f"hbm{g.index}.sock")
+        assert oct(os.stat(d / "admin").st_mode & 0o777) == "0o700"
         brokers[1].proc.kill()
         brokers[1].proc.wait()
         sup.watch_once()
         assert sup.restarts == {0: 0, 1: 1}
         assert brokers[1].proc.poll() is None
-        assert len((d / "hbm1.sock.args").read_text().splitlines()) == 2
+        assert len((d / "gpu1" / "hbm1.sock.args").read_text().splitlines()) == 2
     finally:
         sup.stop()
     assert all(b.proc is None for b in brokers.values())

@@ -516,7 +516,7 @@ def test_broker_arena_serves_hipmalloc_from_the_granted_granules(stub, native_sh
         assert c2["err"] == 0 and c2["p"] == a3["p"]             # first fit reuses the freed range
         assert d1["err"] == 0 and d1["p"] == a3["p"] + 2 * GIB   # coalesced rest of it
         assert e1["err"] == 2                                    # 4 GiB arena full: out of memory
-        assert info["total"] == 8 * GIB and info["free"] == 512 * MIB
+        assert info["total"] == 8 * GIB and info["free"] == 512 * MIB + 4 * GIB   # the arena's rest + the quota's rest
         assert st["used"] == 4 * GIB                             # the arena is on the pod's ledger
         assert rel_live["r"] == -1 and rel["r"] == 1             # released only once nothing is live
         assert arena_after["on"] == 0
@@ -588,5 +588,85 @@ def test_broker_arena_larger_than_the_quota_is_not_used(stub, native_shim, tmp_p
                 break
             time.sleep(0.02)
         assert b.closed_at is not None                           # the granules went back at once
+    finally:
+        cleanup(name)
+
+
+def test_broker_arena_serves_stream_ordered_allocations(stub, native_shim, tmp_path):
+    """hipMallocAsync and hipMallocFromPoolAsync (the default pool: PyTorch's
+    cudaMallocAsync backend) come from the arena like hipMalloc; a hipFreeAsync'd block is reused
+    once its stream got past the free (an event), and an allocation that needs it waits for that
+    instead of going to the driver."""
+    sock = str(tmp_path / "hbm.sock")
+    FakeBroker(sock, granules=4)
+    name = ledger()
+    try:
+        out, r = run(stub, native_shim, ["async", 2 * GIB, "poolasync", GIB, "arena", "freeasync", 0,
+                                         "async", 2 * GIB, "arena", "stats", "info"],
+                     GPUSHARE_QUOTA_BYTES=8 * GIB, GPUSHARE_LEDGER=name, GPUSHARE_HBM_BROKER=sock,
+                     GPUSHARE_HBM_TOKEN="tok", FAKE_HIP_EVENT_MS=300)
+        assert r.returncode == 0, r.stderr
+        a2, p1, arena, _, again, arena2, st, info = out
+        assert a2["err"] == 0 and p1["err"] == 0
+        assert arena == {"op": "arena", "on": 1, "size": 4 * GIB, "used": 3 * GIB}
+        assert again["err"] == 0 and again["p"] == a2["p"]          # waited for the stream, reused
+        assert arena2["used"] == 3 * GIB
+        assert st["used"] == 4 * GIB and st["denied"] == 0           # the arena only: nothing from the driver
+        assert info["total"] == 8 * GIB and info["free"] == 5 * GIB  # the arena's rest + the quota's rest
+    finally:
+        cleanup(name)
+
+
+def test_broker_arena_serves_vmm_pages(stub, native_shim, tmp_path):
+    """VMM the way PyTorch's expandable segments use it (a large reserved
+    range, 20 MiB pages created and mapped one after another) is served from the arena: the
+    range is aligned to the granule, its slots are backed by arena granules on demand (a page may
+    straddle two), unmapping a slot's last page gives its granule back, and past the arena the
+    pages come from the driver, charged, until the quota is out."""
+    sock = str(tmp_path / "hbm.sock")
+    FakeBroker(sock, granules=4)
+    name = ledger()
+    page = 20 * MIB
+    n1 = 60                                          # 1.17 GiB: two slots
+    try:
+        args = ["alloc", MIB, "vres", 9 * GIB] + ["vpage", page] * n1 + ["vstats", "arena", "stats"]
+        args += sum((["vdrop", k] for k in range(n1)), []) + ["vstats", "arena"]
+        out, r = run(stub, native_shim, args, GPUSHARE_QUOTA_BYTES=8 * GIB, GPUSHARE_LEDGER=name,
+                     GPUSHARE_HBM_BROKER=sock, GPUSHARE_HBM_TOKEN="tok")
+        assert r.returncode == 0, r.stderr
+        vres = out[1]
+        assert vres == {"op": "vres", "err": 0, "aligned": 1}
+        pages = out[2:2 + n1]
+        assert all(p["err"] == 0 and p["map"] == 0 and p["access"] == 0 for p in pages)
+        vs, arena, st = out[2 + n1:5 + n1]
+        assert vs["windows"] == 1 and vs["creates"] == n1 and vs["real_pieces"] == 0
+        assert vs["arena_maps"] == n1 + 1 and vs["slots_now"] == 2     # one page straddles the slots
+        assert arena["used"] == 2 * GIB + MIB                          # two granules lent + the 1 MiB block
+        assert st["used"] == 4 * GIB                                   # only the arena's charge
+        drops = out[5 + n1:5 + 2 * n1]
+        assert all(d == {"op": "vdrop", "unmap": 0, "release": 0} for d in drops)
+        vs2, arena2 = out[5 + 2 * n1:]
+        assert vs2["slots_now"] == 0 and arena2["used"] == MIB          # granules back in the arena
+    finally:
+        cleanup(name)
+
+
+def test_broker_arena_vmm_spills_to_the_driver_within_the_quota(stub, native_shim, tmp_path):
+    sock = str(tmp_path / "hbm.sock")
+    FakeBroker(sock, granules=4)
+    name = ledger()
+    half = GIB // 2
+    try:
+        args = ["vres", 12 * GIB] + ["vpage", half] * 17 + ["vstats", "stats", "info"]
+        out, r = run(stub, native_shim, args, GPUSHARE_QUOTA_BYTES=8 * GIB, GPUSHARE_LEDGER=name,
+                     GPUSHARE_HBM_BROKER=sock, GPUSHARE_HBM_TOKEN="tok")
+        assert r.returncode == 0, r.stderr
+        pages = out[1:18]
+        ok = [p for p in pages if p["err"] == 0]
+        assert len(ok) == 16 and pages[16]["err"] == 2                 # 8 GiB: 4 arena + 4 driver, then OOM
+        assert all(p["map"] == 0 for p in ok)
+        vs, st, info = out[18:]
+        assert vs["slots_now"] == 4 and vs["real_pieces"] == 8          # 8 half-GiB driver pages
+        assert st["used"] == 8 * GIB and info["free"] == 0
     finally:
         cleanup(name)

@@ -828,3 +828,121 @@ def test_claims_are_swept_with_the_native_server_answering(tmp_path):
     finally:
         srv.stop()
         al.close()
+
+
+def _prebind_server(tmp_path):
+    srv, al, src = _server(tmp_path)
+    al.opts.fast_path = True
+    al.PREBIND_CONFIRM_S = 0.1
+    src.changed.set()
+    t = time.monotonic() + 5
+    while al._published != (src.pending_version, al._gen) and time.monotonic() < t:
+        time.sleep(0.002)
+    assert al._last_table is not None
+    return srv, al, src
+
+
+def _in_table(al, uid):
+    return any(c.uid == uid for c in al._last_table[2])
+
+
+def test_a_prebind_pod_is_answered_before_the_plugin_sees_its_bind(tmp_path):
+    """a pod the extender placed here (labelled, annotated, not bound yet) is
+    a candidate at once. The kubelet's Allocate, arriving before the plugin's pod watch shows the
+    bind, is answered from the table natively, without the watch wait."""
+    srv, al, src = _prebind_server(tmp_path)
+    ch, stub = _stub(srv)
+    try:
+        p = mkpod("pb", 2, 1, 10, node="")
+        al.precompute(p)
+        assert _in_table(al, "uid-pb") and src.get("uid-pb") is None
+        before = srv.stats()
+        r = stub.Allocate(_req("x1", "x2"))
+        st = srv.stats()
+        assert r.container_responses[0].envs[const.ENV_RESOURCE_INDEX] == "1"
+        assert st["fast"] == before["fast"] + 1 and st["watch_waits"] == before["watch_waits"]
+        t = time.monotonic() + 5
+        while "uid-pb" not in al._assigned and time.monotonic() < t:
+            time.sleep(0.01)
+        assert "uid-pb" in al._assigned                      # claimed: its ASSIGNED patch is queued
+        # the bind reaches the plugin: the claimed pod is no candidate, nothing is handed out twice
+        bound = json.loads(json.dumps(p))
+        bound["spec"]["nodeName"] = "node-a"
+        src.pods.append(bound)
+        al.expire_prebind()
+        assert "uid-pb" not in al._prebind
+    finally:
+        ch.close()
+        srv.stop()
+        al.close()
+
+
+def test_a_prebind_pod_whose_bind_fails_is_withdrawn_and_rearmed(tmp_path):
+    """The bind never reaches this node (deleted, placed elsewhere, label moved): the unclaimed
+    entry leaves the table after PREBIND_CONFIRM_S, so its reservation is never handed out (no
+    over-commit); the same pod placed here again is a candidate again and answered once."""
+    srv, al, src = _prebind_server(tmp_path)
+    ch, stub = _stub(srv)
+    try:
+        p = mkpod("nb", 3, 0, 10, node="")
+        al.precompute(p)
+        assert _in_table(al, "uid-nb")
+        al.prebind_gone(p)
+        assert _in_table(al, "uid-nb")                       # within the confirm window: still there
+        time.sleep(0.2)
+        al.expire_prebind()
+        assert not _in_table(al, "uid-nb") and "uid-nb" not in al._prebind
+        fast0 = srv.stats()["fast"]
+        try:
+            r = stub.Allocate(_req("y1", "y2", "y3"))
+            assert const.ENV_RESOURCE_INDEX not in r.container_responses[0].envs or \
+                r.container_responses[0].envs.get("GPUSHARE_POD_UID") != "uid-nb"
+        except grpc.RpcError:
+            pass                                             # the engine: no candidate of that size
+        assert srv.stats()["fast"] == fast0 and "uid-nb" not in al._assigned
+        # re-placed here (a new assume time): armed again, answered once
+        p2 = mkpod("nb", 3, 1, 20, node="")
+        al.precompute(p2)
+        assert _in_table(al, "uid-nb")
+        r = stub.Allocate(_req("z1", "z2", "z3"))
+        assert r.container_responses[0].envs[const.ENV_RESOURCE_INDEX] == "1"
+        assert srv.stats()["fast"] == fast0 + 1
+        fast1 = srv.stats()["fast"]
+        try:
+            stub.Allocate(_req("w1", "w2", "w3"))
+        except grpc.RpcError:
+            pass
+        assert srv.stats()["fast"] == fast1                  # not handed out twice
+    finally:
+        ch.close()
+        srv.stop()
+        al.close()
+
+
+def test_a_claimed_prebind_answer_stands_when_the_bind_fails(tmp_path):
+    """An entry a native answer already took went to a pod of this node (the kubelet admits only
+    pods bound here): the claim stands — the pod stays assigned and is never offered again."""
+    srv, al, src = _prebind_server(tmp_path)
+    ch, stub = _stub(srv)
+    try:
+        p = mkpod("cb", 1, 0, 10, node="")
+        al.precompute(p)
+        assert stub.Allocate(_req("c1")).container_responses[0].envs[const.ENV_RESOURCE_INDEX] == "0"
+        t = time.monotonic() + 5
+        while "uid-cb" not in al._assigned and time.monotonic() < t:
+            time.sleep(0.01)
+        al.prebind_gone(p)
+        time.sleep(0.2)
+        al.expire_prebind()
+        assert "uid-cb" in al._assigned and "uid-cb" not in al._prebind
+        al.precompute(p)                                     # a late pre-bind event: not armed again
+        fast = srv.stats()["fast"]
+        try:
+            stub.Allocate(_req("c2"))
+        except grpc.RpcError:
+            pass
+        assert srv.stats()["fast"] == fast
+    finally:
+        ch.close()
+        srv.stop()
+        al.close()

@@ -24,10 +24,35 @@
 #include <string>
 #include <vector>
 
+#include <link.h>
+
+#include <cstring>
+
 namespace {
+// the libamdhip64 this process has loaded (PyTorch loads its own copy RTLD_LOCAL: RTLD_DEFAULT
+// does not see it), else the system's
+void* hip_lib() {
+  static void* h = nullptr;
+  if (h) return h;
+  const char* path = nullptr;
+  dl_iterate_phdr(
+      [](dl_phdr_info* info, size_t, void* data) {
+        if (info->dlpi_name && std::strstr(info->dlpi_name, "libamdhip64.so")) {
+          *static_cast<const char**>(data) = info->dlpi_name;
+          return 1;
+        }
+        return 0;
+      },
+      &path);
+  if (path) h = dlopen(path, RTLD_NOLOAD | RTLD_LAZY);
+  if (!h) h = dlopen("libamdhip64.so.7", RTLD_LAZY);
+  return h;
+}
+
 template <class F>
 F sym(const char* n) {
-  return reinterpret_cast<F>(dlsym(RTLD_DEFAULT, n));
+  void* h = hip_lib();
+  return reinterpret_cast<F>(h ? dlsym(h, n) : nullptr);
 }
 
 struct Api {
@@ -86,7 +111,7 @@ extern "C" const char* vmm_semantics_probe(unsigned long long gran_mib) {
     return out.c_str();
   }
   int ver = 0;
-  if (A.version) A.version(&ver);
+  if (A.version) (void)A.version(&ver);
   rec("runtime_version", ver);
   A.setdev(0);
   size_t gran = size_t(gran_mib) << 20, page = 20ull << 20;
