@@ -207,16 +207,18 @@ class APIClient:
         return h
 
     def request(self, method: str, path: str, query: dict | None = None, body=None,
-                content_type: str = "application/json"):
+                content_type: str = "application/json", timeout: float | None = None):
+        """One request; ``timeout`` bounds each socket operation of this call (default: the
+        client's), e.g. a lease renewal that must give up before its renew deadline."""
         url = self._prefix + path
         if query:
             url += "?" + urllib.parse.urlencode({k: v for k, v in query.items() if v is not None})
         data = None if body is None else (body if isinstance(body, bytes) else json.dumps(body).encode())
-        r, raw = self._roundtrip(method, url, data, content_type)
+        r, raw = self._roundtrip(method, url, data, content_type, timeout)
         if r.status == 401 and self.cfg.reload_token(force=True):
             # rotated service-account token: retry once with the new one
             log.info("apiserver answered 401; retrying with the reloaded token")
-            r, raw = self._roundtrip(method, url, data, content_type)
+            r, raw = self._roundtrip(method, url, data, content_type, timeout)
         self.requests += 1
         self._local.n = getattr(self._local, "n", 0) + 1
         try:
@@ -228,9 +230,13 @@ class APIClient:
                            obj.get("message", "") if isinstance(obj, dict) else str(obj), obj)
         return obj
 
-    def _roundtrip(self, method, url, data, content_type):
+    def _roundtrip(self, method, url, data, content_type, timeout=None):
         for attempt in (0, 1):
             c = self._conn()
+            t = self.timeout if timeout is None else timeout
+            c.timeout = t
+            if c.sock is not None:
+                c.sock.settimeout(t)
             try:
                 c.request(method, url, body=data, headers=self._headers(content_type if data is not None else None))
                 r = c.getresponse()

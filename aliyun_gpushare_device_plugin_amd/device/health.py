@@ -27,7 +27,12 @@ Recovery never depends on one event arriving (the reference's "no way to recover
 a mark when it sees the reset itself:
 
 * "GPU reset in progress" (a pre-reset without its post-reset): Healthy again once the GPU is
-  present and answering SMI on ``settle_polls`` consecutive polls;
+  present *and working* on ``settle_polls`` consecutive polls. An MI355X stays enumerated in
+  sysfs and SMI during a mode-1 reset, so being listed proves nothing: the functional probe
+  (``SMI.probe``: amdgpu's gpu_metrics table, which the driver refuses while the GPU is in
+  reset) must succeed on each of those polls. A device that is listed but failing the probe
+  stays Unhealthy, and its count starts again; a backend with no probe falls back to presence;
+* a GPU that left the enumeration and came back is Healthy again once it passes the probe;
 * an ECC uncorrectable-error mark clears on an *observed* reset: a pre-reset event (then as
   above), the GPU leaving and re-joining the enumeration, or its UE counters going backwards
   (a reset cleared them) — the UE baseline restarts from the value read then.
@@ -149,6 +154,16 @@ class HealthMonitor:
                 self._set(idx, False, "GPU reset in progress")
             elif k == S.EV_POST_RESET:
                 if g is not None:
+                    try:
+                        working = self.smi.probe(ev.index) if ev.index >= 0 else None
+                    except S.SMIError:
+                        working = None
+                    if working is False:
+                        # the event came, the GPU does not work yet: the poll clears the mark once it does
+                        with self._lock:
+                            self._marks[g.uuid] = "reset"
+                            self._settle[g.uuid] = 0
+                        continue
                     with self._lock:
                         self._marks.pop(g.uuid, None)
                     self._ecc_baseline[g.uuid] = self._current_ecc(g.uuid, self._ecc_baseline.get(g.uuid, 0))
@@ -182,8 +197,16 @@ class HealthMonitor:
         except S.SMIError as e:
             log.warning("SMI refresh failed: %s", e)
             return
+        smi_index = {d.uuid: i for i, d in enumerate(self.smi.devices())} if self._marks else {}
         for g in self.model.gpus:
             d = present.get(g.uuid)
+            mark0 = self._marks.get(g.uuid)
+            working = None
+            if d is not None and mark0 is not None:
+                try:
+                    working = self.smi.probe(smi_index[g.uuid])
+                except (S.SMIError, KeyError):
+                    working = False
             with self._lock:
                 if d is None:
                     self._marks[g.uuid] = "gone"
@@ -191,7 +214,8 @@ class HealthMonitor:
                     mark, settled = "gone", 0
                 else:
                     mark = self._marks.get(g.uuid)
-                    settled = self._settle.get(g.uuid, 0) + 1 if mark == "reset" else 0
+                    # a poll counts towards the settle only when the GPU works, not just answers
+                    settled = (self._settle.get(g.uuid, 0) + 1 if working is not False else 0) if mark == "reset" else 0
                     if mark == "reset":
                         self._settle[g.uuid] = settled
             if d is None:
@@ -203,12 +227,18 @@ class HealthMonitor:
             last = self._ecc_last.get(g.uuid, d.ecc_ue)
             self._ecc_last[g.uuid] = d.ecc_ue
             why = None
+            if mark is not None and working is False:
+                # listed, but not working yet (still in reset): stays Unhealthy, the count restarts
+                self._set(g.index, False, "GPU reset in progress (enumerated, not answering the functional probe)",
+                          present=True)
+                continue
             if d.ecc_ue < last:
                 why = f"uncorrectable ECC counters went back ({last}->{d.ecc_ue}): reset observed"
             elif mark == "gone":
                 why = "device back"
             elif mark == "reset" and settled >= self.settle_polls:
-                why = f"answering SMI on {settled} polls after a reset (post-reset event not seen)"
+                why = (f"working on {settled} polls after a reset (post-reset event not seen)" if working
+                       else f"answering SMI on {settled} polls after a reset (post-reset event not seen; no probe here)")
             if why is not None:
                 # an observed reset: the UE baseline restarts from what the GPU reports now
                 with self._lock:

@@ -120,6 +120,7 @@ def _load():
             lib.gs_get_link.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_Link)]
             lib.gs_wait_event.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(_Event)]
             lib.gs_inject.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
+            lib.gs_probe.argtypes = [ctypes.c_void_p, ctypes.c_int]
             lib.gs_health_status.argtypes = [ctypes.c_void_p, ctypes.POINTER(_HealthStatus)]
             lib.gs_to_json.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t]
             if lib.gs_abi_version() != 2:
@@ -261,6 +262,14 @@ class SMI:
         if rc == 0:
             return None
         return Event(ev.index, ev.kind, ev.message.decode(errors="replace"))
+
+    def probe(self, i: int) -> bool | None:
+        """Is device ``i`` working, beyond being enumerated: True / False, None = no probe on
+        this backend (``gs_probe``: amdgpu's gpu_metrics, refused while the GPU is in reset)."""
+        rc = self._call(self._lib.gs_probe, int(i))
+        if rc == -2:
+            self._err(f"gs_probe({i})")
+        return None if rc < 0 else rc == 1
 
     def inject(self, cmd: str):
         if self._call(self._lib.gs_inject, cmd.encode()) != 0:

@@ -16,7 +16,11 @@ The algorithm is the one Kubernetes components use (client-go ``leaderelection``
   local time, so clock skew between hosts cannot hand the lease over early;
 * every write is a compare-and-swap on the Lease's ``resourceVersion`` (a lost race is a 409);
 * the leader renews every ``retry_s``; if it has not renewed for ``renew_s`` (< ``lease_s``),
-  it steps down before any other replica can consider the lease expired;
+  it steps down before any other replica can consider the lease expired. A renewal counts from
+  the moment it was *started* (a slow PUT must not extend the leader's own view of its term),
+  and each of its requests gives up after ``(renew_s - retry_s) / 2`` (client-go's
+  RenewDeadline), so a stalled apiserver cannot keep a stale leader serving;
+* a follower dates what it observed from the moment the GET *returned*, never earlier;
 * a graceful stop releases the lease (empty holder), so a follower takes over at its next try.
 """
 from __future__ import annotations
@@ -67,11 +71,13 @@ class LeaderElector:
         return {"holderIdentity": self.identity, "leaseDurationSeconds": max(1, int(round(self.lease_s))),
                 "acquireTime": acquire, "renewTime": _micro_time(), "leaseTransitions": transitions}
 
+    def _req(self, method: str, path: str, body=None):
+        return self.client.request(method, path, body=body, timeout=max(0.1, (self.renew_s - self.retry_s) / 2))
+
     def try_acquire_or_renew(self) -> bool:
         """One attempt; True when this replica holds the lease afterwards."""
-        now = self.clock()
         try:
-            lease = self.client.request("GET", self._path())
+            lease = self._req("GET", self._path())
         except APIError as e:
             if not e.not_found:
                 raise
@@ -79,14 +85,14 @@ class LeaderElector:
                     "metadata": {"name": self.name, "namespace": self.namespace},
                     "spec": self._spec(_micro_time(), 0)}
             try:
-                made = self.client.request("POST", f"/apis/coordination.k8s.io/v1/namespaces/{self.namespace}/leases",
-                                           body=body)
+                made = self._req("POST", f"/apis/coordination.k8s.io/v1/namespaces/{self.namespace}/leases", body=body)
             except APIError as e2:
                 if e2.status == 409:             # another replica created it first
                     return False
                 raise
-            self._see(made, now)
+            self._see(made, self.clock())
             return True
+        now = self.clock()                       # observed now that the GET has returned
         spec = lease.get("spec") or {}
         self._see(lease, now)
         holder = spec.get("holderIdentity") or ""
@@ -100,12 +106,12 @@ class LeaderElector:
         new["spec"] = self._spec(spec.get("acquireTime") if mine and spec.get("acquireTime") else _micro_time(),
                                  int(spec.get("leaseTransitions") or 0) + (0 if mine else 1))
         try:
-            upd = self.client.request("PUT", self._path(), body=new)
+            upd = self._req("PUT", self._path(), body=new)
         except APIError as e:
             if e.status == 409:                  # someone wrote it since the GET
                 return False
             raise
-        self._see(upd, now)
+        self._see(upd, self.clock())
         return True
 
     def _see(self, lease: dict, now: float) -> None:
@@ -146,6 +152,7 @@ class LeaderElector:
 
     def step(self) -> None:
         """One round of the loop (tests drive it directly)."""
+        started = self.clock()                   # a renewal's term counts from its start
         try:
             ok = self.try_acquire_or_renew()
         except Exception as e:  # noqa: BLE001 - apiserver unreachable: count it as a failed renew
@@ -153,7 +160,7 @@ class LeaderElector:
             ok = False
         now = self.clock()
         if ok:
-            self._last_renew = now
+            self._last_renew = started
             if not self._leader:
                 try:
                     self._set(True)

@@ -19,6 +19,10 @@
 #include <condition_variable>
 #include <cstdlib>
 #include <deque>
+#include <fcntl.h>
+#include <unistd.h>
+
+#include <cstring>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -174,11 +178,28 @@ struct LinkMatrix {
   const gs_link_t& at(int i, int j) const { return m[(size_t)i * n + j]; }
 };
 
+// Functional probe: amdgpu's gpu_metrics table, which the driver reads from the SMU and refuses
+// (EPERM/EBUSY) while the GPU is in reset or not initialised. 1 = answered, 0 = the file is there
+// and the read failed (enumerated but not functional), -1 = no such file (unknown here).
+int probe_gpu_metrics(const std::string& root, int render_minor) {
+  if (render_minor < 0) return -1;
+  std::string path = root + "/sys/class/drm/renderD" + std::to_string(render_minor) + "/device/gpu_metrics";
+  int fd = open(path.c_str(), O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return errno == ENOENT ? -1 : 0;
+  unsigned char hdr[64];
+  ssize_t n = read(fd, hdr, sizeof hdr);
+  close(fd);
+  // metrics_table_header: structure_size (u16), format_revision (u8), content_revision (u8)
+  return n >= 4 && (hdr[0] | hdr[1]) != 0 && hdr[2] != 0 ? 1 : 0;
+}
+
 // ---------------------------------------------------------------------------------------
 // backends
 // ---------------------------------------------------------------------------------------
 class Backend {
  public:
+  // is the device working, beyond being enumerated (see probe_gpu_metrics)
+  virtual int probe(const gs_device_t& d) { return probe_gpu_metrics("", d.render_minor); }
   virtual ~Backend() = default;
   virtual const char* name() const = 0;
   virtual bool enumerate(std::vector<gs_device_t>* devs, LinkMatrix* links, int* inaccessible) = 0;
@@ -233,6 +254,7 @@ class SysfsBackend : public Backend {
  public:
   explicit SysfsBackend(std::string root) : root_(std::move(root)) {}
   const char* name() const override { return "sysfs"; }
+  int probe(const gs_device_t& d) override { return probe_gpu_metrics(root_, d.render_minor); }
 
   // Enriches a device whose render minor is known from amdgpu's DRM sysfs.
   // Returns true when the RAS (ECC) counters were read.
@@ -805,6 +827,18 @@ class AmdSmiBackend : public Backend {
 class FakeBackend : public Backend {
  public:
   const char* name() const override { return "fake"; }
+  // "resetting I N": the device stays enumerated but fails the probe on its next N probes
+  int probe(const gs_device_t& d) override {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (size_t i = 0; i < all_.size(); ++i)
+      if (std::strcmp(all_[i].uuid, d.uuid) == 0) {
+        auto it = probe_fail_.find((int)i);
+        if (it == probe_fail_.end() || it->second <= 0) return 1;
+        --it->second;
+        return 0;
+      }
+    return -1;
+  }
   bool events_start(const std::vector<gs_device_t>& devs) override {
     events_note(true, (int)devs.size(), 0);  // injected events are always delivered
     return true;
@@ -924,7 +958,7 @@ class FakeBackend : public Backend {
     std::string op;
     int a = -1, b = -1;
     is >> op >> a;
-    if (op == "linkdown" || op == "linkup" || op == "ecc" || op == "vram") is >> b;
+    if (op == "linkdown" || op == "linkup" || op == "ecc" || op == "vram" || op == "resetting") is >> b;
     std::lock_guard<std::mutex> lk(mu_);
     if (a < 0 || a >= (int)all_.size()) {
       set_err("inject: bad device index in '" + cmd + "'");
@@ -950,6 +984,9 @@ class FakeBackend : public Backend {
       push(a, GS_EV_PRE_RESET, "GPU pre-reset");
     } else if (op == "silentreset") {  // a completed reset with no event at all: counters cleared
       all_[a].ecc_ue = 0;
+    } else if (op == "resetting") {  // a pre-reset, then the device enumerated but not working for b probes
+      probe_fail_[a] = b > 0 ? b : 1;
+      push(a, GS_EV_PRE_RESET, "GPU pre-reset");
     } else if (op == "ecc") {
       all_[a].ecc_ue += (uint64_t)(b > 0 ? b : 1);
       push(a, GS_EV_ECC_UE, "uncorrectable ECC error");
@@ -1011,6 +1048,7 @@ class FakeBackend : public Backend {
   std::vector<gs_device_t> all_;
   LinkMatrix base_links_;
   std::set<int> unplugged_;
+  std::map<int, int> probe_fail_;  // device -> probes still to fail ("resetting")
   std::set<std::pair<int, int>> down_;
   std::deque<gs_event_t> q_;
 };
@@ -1157,6 +1195,20 @@ int gs_health_status(const gs_handle* h, gs_health_status_t* out) {
 int gs_inject(gs_handle* h, const char* cmd) {
   if (!h || !cmd) return -1;
   return h->be->inject(cmd);
+}
+
+int gs_probe(gs_handle* h, int i) {
+  if (!h) return -1;
+  gs_device_t d;
+  {
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (i < 0 || i >= (int)h->devs.size()) {
+      set_err("device index out of range");
+      return -2;
+    }
+    d = h->devs[(size_t)i];
+  }
+  return h->be->probe(d);
 }
 
 int gs_to_json(const gs_handle* h, char* buf, size_t len) {

@@ -100,8 +100,12 @@ int gs_wait_event(gs_handle* h, int timeout_ms, gs_event_t* ev);
 // Fills *out with the backend's health-path status (see gs_health_status_t).
 int gs_health_status(const gs_handle* h, gs_health_status_t* out);
 // Fault injection (fake backend only): "unplug I", "replug I", "reset I", "ecc I N",
-// "vmfault I", "linkdown I J", "linkup I J", "thermal I".
+// "vmfault I", "linkdown I J", "linkup I J", "thermal I", "prereset I", "silentreset I",
+// "resetting I N" (a pre-reset, then enumerated but failing gs_probe N times).
 int gs_inject(gs_handle* h, const char* cmd);
+// Functional probe of device i beyond enumeration (amdgpu gpu_metrics, which the driver refuses
+// while the GPU is in reset): 1 working, 0 enumerated but not working, -1 unknown, -2 bad index.
+int gs_probe(gs_handle* h, int i);
 // Writes a JSON document describing all devices and the link matrix. Returns the number of
 // bytes needed (excluding NUL); writes at most len bytes.
 int gs_to_json(const gs_handle* h, char* buf, size_t len);

@@ -183,3 +183,43 @@ def test_cli_flags_and_manifest():
 def test_bad_timings_are_refused():
     with pytest.raises(ValueError):
         LeaderElector(None, "ns", "n", "x", lease_s=5, renew_s=6, retry_s=1)
+
+
+def test_a_slow_renewal_does_not_extend_the_leaders_term():
+    """ADVICE r4: the leader's renewal counts from when it started, not when its PUT returned;
+    a follower dates its observation from when its GET returned."""
+    clock = [100.0]
+
+    class SlowClient:
+        def __init__(self, inner, delay):
+            self.inner, self.delay = inner, delay
+            self.timeouts = []
+
+        def request(self, method, path, body=None, timeout=None):
+            self.timeouts.append(timeout)
+            r = self.inner.request(method, path, body=body)
+            clock[0] += self.delay                    # the request took this long
+            return r
+
+    api = FakeAPIServer()
+    api.start()
+    try:
+        from aliyun_gpushare_device_plugin_amd.cluster.client import APIClient, KubeConfig
+        from aliyun_gpushare_device_plugin_amd.extender.leader import LeaderElector
+
+        slow = SlowClient(APIClient(KubeConfig(api.url)), delay=4.0)
+        le = LeaderElector(slow, "kube-system", "x", "a", lease_s=15.0, renew_s=10.0, retry_s=2.0, clock=lambda: clock[0])
+        t0 = clock[0]
+        le.step()                                      # POST (create) took 4 s
+        assert le._leader and le._last_renew == t0
+        assert all(t == 4.0 for t in slow.timeouts)    # (renew 10 - retry 2) / 2
+        t1 = clock[0]
+        le.step()                                      # GET + PUT: 8 s, started at t1
+        assert le._last_renew == t1 and clock[0] - le._last_renew == 8.0
+        f = LeaderElector(SlowClient(APIClient(KubeConfig(api.url)), delay=3.0), "kube-system", "x", "b",
+                          lease_s=15.0, renew_s=10.0, retry_s=2.0, clock=lambda: clock[0])
+        before = clock[0]
+        assert f.try_acquire_or_renew() is False
+        assert f._observed_at == before + 3.0          # when the GET returned
+    finally:
+        api.stop()

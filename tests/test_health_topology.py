@@ -201,3 +201,59 @@ def test_ecc_mark_clears_on_a_pre_reset_without_post_reset():
         assert wait(lambda: health_by_gpu(kl, mgr.model)[1] == const.HEALTHY, timeout=3.0)
         time.sleep(0.6)                                 # re-baselined: the old UEs do not re-mark it
         assert health_by_gpu(kl, mgr.model)[1] == const.HEALTHY
+
+
+def test_a_gpu_enumerated_but_still_resetting_stays_unhealthy():
+    """an MI355X stays enumerated during a mode-1 reset, so presence alone must
+    not end a reset mark. Fake SMI "resetting 1 5": a pre-reset, then the GPU is listed but fails
+    the functional probe (amdgpu gpu_metrics) on its next 5 probes — it stays Unhealthy through
+    them, and recovers only after settle_polls (2) working polls."""
+    with SimCluster([("n", "fake:2x4G")], health_poll_s=0.2) as c:
+        mgr, kl = c.manager("n"), c.nodes["n"].kubelet
+        mgr.smi.inject("resetting 1 5")
+        assert wait(lambda: health_by_gpu(kl, mgr.model)[1] == const.UNHEALTHY)
+        time.sleep(0.2 * 4)                              # 4 polls: listed every time, probe failing
+        assert health_by_gpu(kl, mgr.model)[1] == const.UNHEALTHY
+        assert "not answering the functional probe" in mgr.model.gpu(1).reason
+        assert wait(lambda: health_by_gpu(kl, mgr.model)[1] == const.HEALTHY, timeout=6.0)
+        assert "working on 2 polls" in mgr.model.gpu(1).reason
+        assert health_by_gpu(kl, mgr.model)[0] == const.HEALTHY
+
+
+def test_a_post_reset_event_before_the_gpu_works_waits_for_the_probe():
+    from aliyun_gpushare_device_plugin_amd.device import smi as S
+
+    with SimCluster([("n", "fake:2x4G")], health_poll_s=0.2) as c:
+        mgr, kl = c.manager("n"), c.nodes["n"].kubelet
+        mgr.smi.inject("resetting 0 3")
+        assert wait(lambda: health_by_gpu(kl, mgr.model)[0] == const.UNHEALTHY)
+        mgr.health.handle_event(S.Event(0, S.EV_POST_RESET, "GPU post-reset"))   # early: probe still failing
+        assert mgr.model.gpu(0).healthy is False or "reset" in mgr.model.gpu(0).reason
+        assert wait(lambda: health_by_gpu(kl, mgr.model)[0] == const.HEALTHY, timeout=6.0)
+
+
+def test_probe_on_real_backends_reads_gpu_metrics(tmp_path):
+    """The functional probe on a sysfs tree: gpu_metrics readable with a header = working; the file
+    there but unreadable = not working; no file = unknown (presence decides, as before)."""
+    import ctypes
+
+    from aliyun_gpushare_device_plugin_amd.device import smi as S
+
+    lib = S._load()
+    root = tmp_path / "root"
+    node = root / "sys/class/kfd/kfd/topology/nodes/1"
+    node.mkdir(parents=True)
+    (node / "gpu_id").write_text("4242\n")
+    (node / "properties").write_text("simd_count 1024\narray_count 32\nlocal_mem_size 0\ndrm_render_minor 128\n"
+                                     "gfx_target_version 90500\nunique_id 77\nnum_xcc 8\ndomain 0\nlocation_id 1280\n")
+    dev = root / "sys/class/drm/renderD128/device"
+    dev.mkdir(parents=True)
+    (dev / "mem_info_vram_total").write_text(str(288 << 30))
+    with S.SMI(f"sysfs:{root}") as s:
+        assert s.count() == 1
+        assert s.probe(0) is None                                       # no gpu_metrics: unknown
+        (dev / "gpu_metrics").write_bytes(bytes([0x80, 0x00, 1, 8]) + bytes(124))
+        assert s.probe(0) is True
+        (dev / "gpu_metrics").write_bytes(b"")                         # the driver refused the read
+        assert s.probe(0) is False
+    assert ctypes is not None

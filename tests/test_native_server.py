@@ -251,6 +251,7 @@ import pathlib, tests.test_native_server as T
 tmp = pathlib.Path({str(tmp_path)!r})
 srv, al, src = T._server(tmp, [T.mkpod("p", 1, 0, 10)])
 T._hostile(srv, n_random=20)
+T._grpc_go_replay(srv)
 stubs = [T._stub(srv) for _ in range(4)]
 law = stubs[0][1].ListAndWatch(T.api.Empty())
 next(law)
@@ -944,5 +945,144 @@ def test_a_claimed_prebind_answer_stands_when_the_bind_fails(tmp_path):
         assert srv.stats()["fast"] == fast
     finally:
         ch.close()
+        srv.stop()
+        al.close()
+
+
+# ---- the kubelet's client: grpc-go's frames, replayed ------------------------------------------
+class GoClient:
+    """The kubelet's device-plugin client as grpc-go (1.5x) puts it on the wire, built from the
+    HTTP/2 (RFC 9113) and gRPC-over-HTTP/2 specs and grpc-go's documented transport behaviour:
+    the preface and an empty SETTINGS; a stream-0 WINDOW_UPDATE (its connection window) sent
+    before the server's SETTINGS are acknowledged; BDP-estimator PINGs carrying grpc-go's fixed
+    payload after data arrives; request HEADERS with ``te: trailers`` and a grpc-go user-agent;
+    per-stream and connection WINDOW_UPDATEs as data is consumed; and GOAWAY when it shuts down.
+    grpc-go itself is not available here, so parity with a real kubelet stays unpinned."""
+
+    BDP_PING = bytes([2, 4, 16, 16, 9, 14, 7, 7])       # grpc-go internal/transport bdp_estimator.go
+
+    def __init__(self, path):
+        import socket
+
+        self.s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        self.s.settimeout(10)
+        self.s.connect(path)
+        self.buf = b""
+        self.next_sid = 1
+        self.acked_settings = False
+        self.pings_acked = []
+        self.data = collections.defaultdict(bytes)      # stream -> gRPC-framed bytes received
+        self.ended = set()                              # streams the server ended (trailers)
+        self.goaway = None
+        self.s.sendall(_PREFACE + _frame(4, 0, 0) + _frame(8, 0, 0, (983041).to_bytes(4, "big")))
+
+    def _headers(self, path):
+        def lit(k, v):
+            return b"\x00" + bytes([len(k)]) + k + bytes([len(v)]) + v
+        hs = ((b":method", b"POST"), (b":scheme", b"http"), (b":path", path.encode()), (b":authority", b"localhost"),
+              (b"content-type", b"application/grpc"), (b"user-agent", b"grpc-go/1.59.0"), (b"te", b"trailers"),
+              (b"grpc-timeout", b"9999996u"))
+        return b"".join(lit(k, v) for k, v in hs)
+
+    def call(self, path, msg: bytes, end=True) -> int:
+        sid = self.next_sid
+        self.next_sid += 2
+        body = b"\x00" + len(msg).to_bytes(4, "big") + msg
+        self.s.sendall(_frame(1, 4, sid, self._headers(path)) + _frame(0, 1 if end else 0, sid, body))
+        return sid
+
+    def pump(self, until, timeout=5.0):
+        """Read frames (answering SETTINGS and PINGs as grpc-go does) until ``until()``."""
+        end = time.monotonic() + timeout
+        while not until():
+            if time.monotonic() > end:
+                raise AssertionError("timed out waiting for the server")
+            while len(self.buf) < 9 or len(self.buf) < 9 + int.from_bytes(self.buf[:3], "big"):
+                chunk = self.s.recv(65536)
+                if not chunk:
+                    raise ConnectionError("server closed the connection")
+                self.buf += chunk
+            n = int.from_bytes(self.buf[:3], "big")
+            typ, flags, sid = self.buf[3], self.buf[4], int.from_bytes(self.buf[5:9], "big") & 0x7FFFFFFF
+            payload, self.buf = self.buf[9:9 + n], self.buf[9 + n:]
+            if typ == 4 and not flags & 1:                       # the server's SETTINGS: ACK them
+                self.s.sendall(_frame(4, 1, 0))
+            elif typ == 4:
+                self.acked_settings = True
+            elif typ == 6 and flags & 1:                          # PING ACK
+                self.pings_acked.append(payload)
+            elif typ == 6:
+                self.s.sendall(_frame(6, 1, 0, payload))
+            elif typ == 0:
+                self.data[sid] += payload
+                if n:                                             # consumed: give the window back, BDP ping
+                    self.s.sendall(_frame(8, 0, sid, n.to_bytes(4, "big")) + _frame(8, 0, 0, n.to_bytes(4, "big")) +
+                                   _frame(6, 0, 0, self.BDP_PING))
+                if flags & 1:
+                    self.ended.add(sid)
+            elif typ == 1 and flags & 1:                          # trailers (END_STREAM)
+                self.ended.add(sid)
+            elif typ == 7:
+                self.goaway = payload
+
+    def messages(self, sid):
+        out, b = [], self.data[sid]
+        while len(b) >= 5 and len(b) >= 5 + int.from_bytes(b[1:5], "big"):
+            n = int.from_bytes(b[1:5], "big")
+            out.append(b[5:5 + n])
+            b = b[5 + n:]
+        return out
+
+    def goaway_and_close(self, last_sid=0):
+        self.s.sendall(_frame(7, 0, 0, last_sid.to_bytes(4, "big") + (0).to_bytes(4, "big") + b"client transport shutdown"))
+        self.s.close()
+
+
+def _grpc_go_replay(srv):
+    """The kubelet's session: register-time RPCs, a ListAndWatch that stays open across health
+    changes and Allocates, BDP PINGs, then a kubelet restart (GOAWAY, hang-up) and a new kubelet
+    whose ListAndWatch gets the current devices."""
+    c = GoClient(srv.socket)
+    opts = c.call("/v1beta1.DevicePlugin/GetDevicePluginOptions", b"")
+    c.pump(lambda: opts in c.ended and c.acked_settings)
+    assert api.DevicePluginOptions.FromString(c.messages(opts)[0]) == srv.options()
+    law = c.call("/v1beta1.DevicePlugin/ListAndWatch", b"")
+    c.pump(lambda: len(c.messages(law)) >= 1)
+    first = api.ListAndWatchResponse.FromString(c.messages(law)[0])
+    n = len(first.devices)
+    assert n > 0 and law not in c.ended
+    c.pump(lambda: c.BDP_PING in c.pings_acked)                   # the BDP ping is answered in kind
+    srv.model.set_health(0, False, "replay")
+    c.pump(lambda: len(c.messages(law)) >= 2)
+    second = api.ListAndWatchResponse.FromString(c.messages(law)[1])
+    assert sum(d.health == const.UNHEALTHY for d in second.devices) == n // 2
+    for k in range(3):
+        sid = c.call("/v1beta1.DevicePlugin/Allocate", _req(f"go-{k}").SerializeToString())
+        c.pump(lambda: sid in c.ended)
+        got = c.messages(sid)                                     # an answer, or trailers with an error
+        if got:
+            r = api.AllocateResponse.FromString(got[0])
+            assert r.container_responses[0].envs[const.ENV_RESOURCE_INDEX] in ("0", "1", "-1")   # -1: no pod to match
+    srv.model.set_health(0, True, "replay")
+    c.pump(lambda: len(c.messages(law)) >= 3)                     # the watch stayed open throughout
+    assert law not in c.ended
+    c.goaway_and_close()                                          # the kubelet restarts
+    time.sleep(0.2)
+    c2 = GoClient(srv.socket)
+    law2 = c2.call("/v1beta1.DevicePlugin/ListAndWatch", b"")
+    c2.pump(lambda: len(c2.messages(law2)) >= 1)
+    again = api.ListAndWatchResponse.FromString(c2.messages(law2)[0])
+    assert len(again.devices) == n and {d.health for d in again.devices} == {const.HEALTHY}
+    c2.goaway_and_close()
+
+
+def test_grpc_go_wire_replay(tmp_path):
+    """the native server with grpc-go's frame shapes (GoClient)."""
+    srv, al, src = _server(tmp_path, [mkpod(f"g{i}", 1, i % 2, 10 + i) for i in range(3)])
+    try:
+        _grpc_go_replay(srv)
+        st = srv.stats()
+        assert st["unknown"] == 0 and st["fast"] + st["forwarded_allocate"] >= 3
+    finally:
         srv.stop()
         al.close()
