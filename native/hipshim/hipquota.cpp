@@ -1075,6 +1075,7 @@ REAL(hipError_t, hipMemUnmap, void*, size_t)
 REAL(hipError_t, hipMemSetAccess, void*, size_t, const hipMemAccessDesc*, size_t)
 REAL(hipError_t, hipGetDevice, int*)
 REAL(hipError_t, hipDeviceSynchronize)
+REAL(hipError_t, hipRuntimeGetVersion, int*)
 REAL(hipError_t, hipEventCreateWithFlags, hipEvent_t*, unsigned)
 REAL(hipError_t, hipEventRecord, hipEvent_t, hipStream_t)
 REAL(hipError_t, hipEventQuery, hipEvent_t)
@@ -1180,6 +1181,7 @@ void arena_unmap_locked() {
 // called with g_arena.mu held, at the first allocation
 void arena_take() {
   Arena& a = g_arena;
+  (void)enabled();  // the shim's own init first (log level, quota): the arena is charged below
   a.state.store(-1, std::memory_order_relaxed);
   const char* path = getenv("GPUSHARE_HBM_BROKER");
   const char* tok = getenv("GPUSHARE_HBM_TOKEN");
@@ -1239,18 +1241,24 @@ void arena_take() {
   {
     Depth d;
     if (getdev_f(&dev) != hipSuccess) goto fail;
+    // How hipMemImportFromShareableHandle reads a POSIX fd differs by runtime: HIP 7.0 (the one
+    // PyTorch bundles, 7.0.51831) reads it through the osHandle pointer and crashes on a bare
+    // value; 7.1 and later take the fd as the pointer's value and refuse an address
+    // (profiles/r4/vmm_import_semantics.json). Keyed on the runtime's version, not on errors.
+    int rtv = 0;
+    auto ver_f = real_hipRuntimeGetVersion();
+    if (!ver_f || ver_f(&rtv) != hipSuccess) rtv = 0;
+    bool by_address = rtv > 0 && rtv < 70100000;
+    logf(1, "hbm broker: runtime %d: fds imported by %s", rtv, by_address ? "address" : "value");
     void* base = nullptr;
     uint64_t size = want * gran;
     if (reserve_f(&base, size, 0, nullptr, 0) != hipSuccess) goto fail;
     logf(2, "hbm broker: reserved %p + %llu", base, (unsigned long long)size);
     for (int i = 0; i < got; ++i) {
       logf(2, "hbm broker: import granule %d (fd %d)", i, fds[i]);
-      // The HIP 7.0 runtime (PyTorch's) reads the fd through the pointer, dies on a bare fd; the
-      // 7.2 runtime takes the fd as the pointer's value and refuses an address (invalid value).
-      hipError_t ie = import_f(&a.h[i], &fds[i], hipMemHandleTypePosixFileDescriptor);
-      if (ie == hipErrorInvalidValue)
-        ie = import_f(&a.h[i], reinterpret_cast<void*>(static_cast<intptr_t>(fds[i])),
-                      hipMemHandleTypePosixFileDescriptor);
+      hipError_t ie = by_address ? import_f(&a.h[i], &fds[i], hipMemHandleTypePosixFileDescriptor)
+                                 : import_f(&a.h[i], reinterpret_cast<void*>(static_cast<intptr_t>(fds[i])),
+                                            hipMemHandleTypePosixFileDescriptor);
       if (ie != hipSuccess ||
           map_f(static_cast<char*>(base) + uint64_t(i) * gran, gran, 0, a.h[i], 0) != hipSuccess) {
         logf(1, "hbm broker: import/map of granule %d failed", i);

@@ -172,9 +172,19 @@ int fake_runtime_scratch(size_t n) { uint64_t h; return kfd(n, &h); }
    runtime: the fd is the pointer's value, and an address (a pointer to the fd) is refused
    with hipErrorInvalidValue. */
 #define IMPORTED (1ull << 62)
+/* FAKE_HIP_VERSION (default 70253211, a 7.2 runtime): below 7.1 the import reads the fd through
+   the pointer as HIP 7.0 does (and "crashes" — exit 139 — on a bare value); from 7.1 on it takes
+   the pointer's value and refuses an address */
+static int fake_version(void) { const char* v = getenv("FAKE_HIP_VERSION"); return v ? atoi(v) : 70253211; }
+hipError_t hipRuntimeGetVersion(int* v) { *v = fake_version(); return 0; }
 hipError_t hipMemImportFromShareableHandle(uint64_t* h, void* os, int type) {
   uintptr_t fd = (uintptr_t)os;
-  if (fd > (1u << 20)) return 1;                     /* hipErrorInvalidValue */
+  if (fake_version() < 70100000) {
+    if (fd < (1u << 20)) _exit(139);                 /* HIP 7.0 dereferences a bare fd value */
+    fd = (uintptr_t)*(int*)os;
+  } else if (fd > (1u << 20)) {
+    return 1;                                        /* hipErrorInvalidValue */
+  }
   int d = dup((int)fd);
   if (d < 0) return 1;
   *h = IMPORTED | (uint64_t)d; return 0;

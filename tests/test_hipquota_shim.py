@@ -670,3 +670,21 @@ def test_broker_arena_vmm_spills_to_the_driver_within_the_quota(stub, native_shi
         assert st["used"] == 8 * GIB and info["free"] == 0
     finally:
         cleanup(name)
+
+
+@pytest.mark.parametrize("version,form", [(70051831, "address"), (70253211, "value")])
+def test_broker_fds_are_imported_the_way_the_runtime_reads_them(stub, native_shim, tmp_path, version, form):
+    """how a POSIX fd reaches hipMemImportFromShareableHandle is chosen by the
+    runtime's version, not by probing errors. The stub runtime behaves like HIP 7.0 (reads the fd
+    through the pointer, dies on a bare value) or 7.2 (takes the value, refuses an address)."""
+    sock = str(tmp_path / "hbm.sock")
+    FakeBroker(sock, granules=2)
+    name = ledger()
+    try:
+        out, r = run(stub, native_shim, ["alloc", GIB, "arena"], GPUSHARE_QUOTA_BYTES=4 * GIB, GPUSHARE_LEDGER=name,
+                     GPUSHARE_HBM_BROKER=sock, GPUSHARE_HBM_TOKEN="t", FAKE_HIP_VERSION=version, GPUSHARE_SHIM_LOG="2")
+        assert r.returncode == 0, r.stderr
+        assert out[1]["on"] == 1 and out[1]["size"] == 2 * GIB
+        assert f"fds imported by {form}" in r.stderr
+    finally:
+        cleanup(name)
