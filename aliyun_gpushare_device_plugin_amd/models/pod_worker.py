@@ -50,6 +50,19 @@ def _shim_stats() -> dict | None:
     return dict(zip(("used", "quota", "denied", "peak"), (v.value for v in vals)))
 
 
+def _arena_timing() -> dict | None:
+    """Where the quota shim's broker TAKE spent its time (ms), or None without an arena."""
+    try:
+        f = ctypes.CDLL(None).gpushare_shim_arena_timing
+    except AttributeError:
+        return None
+    f.argtypes = [ctypes.POINTER(ctypes.c_uint64)] * 3
+    vals = [ctypes.c_uint64() for _ in range(3)]
+    if not f(*(ctypes.byref(v) for v in vals)):
+        return None
+    return dict(zip(("connect", "wait", "map"), (round(v.value / 1e6, 3) for v in vals)))
+
+
 def _arena_release():
     """With an HBM broker arena (quota shim + GPUSHARE_HBM_BROKER), hand its granules back now
     that everything is freed, rather than at process exit. None without an arena."""
@@ -95,14 +108,18 @@ def main() -> int:
     t0 = time.perf_counter()
     torch.cuda.init()
     dev = torch.device("cuda", 0)
-    torch.empty(1, device=dev)                                 # context + runtime up
+    t_rt = time.perf_counter()
+    torch.empty(1, device=dev)                                 # context + runtime up (+ the arena's TAKE)
+    t_up = time.perf_counter()
     free, quota = torch.cuda.mem_get_info(dev)                 # = the pod's quota under the shim
+    take = _arena_timing()
     from .gemm_player import GemmPlayer
 
     if cmd.get("two_phase"):
         # the container is up before the GPU has room for its state (the driver may still be
         # wiping the HBM a retired pod freed): report, then allocate on "alloc"
-        _send({"event": "inited", "init_ms": round((time.perf_counter() - t0) * 1e3, 3)})
+        _send({"event": "inited", "init_ms": round((time.perf_counter() - t0) * 1e3, 3),
+               "runtime_ms": round((t_up - t_rt) * 1e3, 3), "take_ms": take})
         nxt = json.loads(sys.stdin.readline() or "{}")
         if nxt.get("cmd") != "alloc":
             return 0

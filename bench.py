@@ -672,8 +672,12 @@ class PodFleet:
         t0 = time.perf_counter()
         w["proc"].stdin.write(json.dumps({"cmd": "start", "env": env, "gemm": self.gemm, "burst": self.burst,
                                           "fill": self.fill, "two_phase": True}) + "\n")
-        self._wait(w, "inited")
+        inited = self._wait(w, "inited")
         t1 = time.perf_counter()
+        take = inited.get("take_ms") or {}
+        for k in ("connect", "wait", "map"):          # the broker TAKE inside init (shim timing)
+            if k in take:
+                self.phase_ms.setdefault(f"init_take_{k}", []).append(take[k] / 1e3)
         self._wait_room(int(env.get(const.ENV_SHIM_QUOTA_BYTES, 0)) * self.fill + 3 * self.gemm ** 2 * 2)
         t2 = time.perf_counter()
         free2 = self._vram_total - self._vram_used() if self._vram_used is not None else None

@@ -1116,6 +1116,15 @@ struct Arena {
 };
 Arena g_arena;
 int g_dev = 0;  // the arena's device (HIP ordinal in this process)
+// where a TAKE's time went (ns): connecting to the broker, waiting for its answer, importing and
+// mapping the granules (gpushare_shim_arena_timing)
+uint64_t g_take_connect_ns = 0, g_take_wait_ns = 0, g_take_map_ns = 0;
+
+uint64_t mono_ns() {
+  timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return uint64_t(t.tv_sec) * 1000000000ull + uint64_t(t.tv_nsec);
+}
 
 bool arena_configured() {
   static std::atomic<int> c{-1};
@@ -1163,6 +1172,41 @@ bool recv_fd_batch(int s, int* out, int* got, int want) {
   return true;
 }
 
+// one TAKE's import + map, shared by threads (granule i: its fd's handle, mapped at base + i * gran)
+struct ImportJob {
+  hipMemImportFromShareableHandle_t import_f;
+  hipMemMap_t map_f;
+  int* fds;
+  hipMemGenericAllocationHandle_t* h;
+  char* base;
+  uint64_t gran;
+  bool by_address;
+  std::atomic<int> next;
+  std::atomic<int> failed;  // granule + 1 of the first failure, 0 none
+  int n;
+};
+
+void* import_worker(void* p) {
+  ImportJob* j = static_cast<ImportJob*>(p);
+  Depth d;
+  for (;;) {
+    int i = j->next.fetch_add(1);
+    if (i >= j->n || j->failed.load(std::memory_order_relaxed)) break;
+    hipMemGenericAllocationHandle_t h = nullptr;
+    hipError_t ie = j->by_address
+                        ? j->import_f(&h, &j->fds[i], hipMemHandleTypePosixFileDescriptor)
+                        : j->import_f(&h, reinterpret_cast<void*>(static_cast<intptr_t>(j->fds[i])),
+                                      hipMemHandleTypePosixFileDescriptor);
+    if (ie == hipSuccess) j->h[i] = h;
+    if (ie != hipSuccess || j->map_f(j->base + uint64_t(i) * j->gran, j->gran, 0, h, 0) != hipSuccess) {
+      int none = 0;
+      j->failed.compare_exchange_strong(none, i + 1);
+      break;
+    }
+  }
+  return nullptr;
+}
+
 // unmap and release whatever of the arena is mapped (g_arena.mu held)
 void arena_unmap_locked() {
   Arena& a = g_arena;
@@ -1173,7 +1217,8 @@ void arena_unmap_locked() {
     if (auto fr = real_hipMemAddressFree()) (void)fr(a.base, a.size);
   }
   if (auto rel = real_hipMemRelease())
-    for (int i = 0; i < a.n; ++i) (void)rel(a.h[i]);
+    for (int i = 0; i < a.n; ++i)
+      if (a.h[i]) (void)rel(a.h[i]);
   a.n = 0;
   a.base = nullptr;
 }
@@ -1200,6 +1245,7 @@ void arena_take() {
   auto map_f = real_hipMemMap();
   auto access_f = real_hipMemSetAccess();
   auto getdev_f = real_hipGetDevice();
+  uint64_t t_start = mono_ns(), t_conn = 0, t_fds = 0;
   if (s < 0 || !import_f || !reserve_f || !map_f || !access_f || !getdev_f) goto fail;
   {
     // the broker may not be listening yet (a node booting, a broker restarting): its socket is
@@ -1226,6 +1272,7 @@ void arena_take() {
       if (s < 0) goto fail;
     }
   }
+  t_conn = mono_ns();
   {
     int n = snprintf(line, sizeof line, "TAKE %s\n", tok);
     if (send(s, line, n, MSG_NOSIGNAL) != n) goto fail;
@@ -1237,6 +1284,7 @@ void arena_take() {
   }
   while (got < (int)want)
     if (!recv_fd_batch(s, fds, &got, (int)want)) goto fail;
+  t_fds = mono_ns();
   logf(2, "hbm broker: %d fds of %llu bytes received", got, gran);
   {
     Depth d;
@@ -1254,21 +1302,28 @@ void arena_take() {
     uint64_t size = want * gran;
     if (reserve_f(&base, size, 0, nullptr, 0) != hipSuccess) goto fail;
     logf(2, "hbm broker: reserved %p + %llu", base, (unsigned long long)size);
-    for (int i = 0; i < got; ++i) {
-      logf(2, "hbm broker: import granule %d (fd %d)", i, fds[i]);
-      hipError_t ie = by_address ? import_f(&a.h[i], &fds[i], hipMemHandleTypePosixFileDescriptor)
-                                 : import_f(&a.h[i], reinterpret_cast<void*>(static_cast<intptr_t>(fds[i])),
-                                            hipMemHandleTypePosixFileDescriptor);
-      if (ie != hipSuccess ||
-          map_f(static_cast<char*>(base) + uint64_t(i) * gran, gran, 0, a.h[i], 0) != hipSuccess) {
-        logf(1, "hbm broker: import/map of granule %d failed", i);
-        goto fail;  // the process keeps what it mapped until exit; the broker reclaims at close
+    // import + map every granule; GPUSHARE_HBM_MAP_THREADS (default 1) threads share the work
+    ImportJob job{import_f, map_f, fds, a.h, static_cast<char*>(base), gran, by_address, {0}, {0}, got};
+    for (int i = 0; i < got; ++i) a.h[i] = nullptr;
+    int nt = int(env_u64("GPUSHARE_HBM_MAP_THREADS", 1));
+    nt = nt < 1 ? 1 : nt > 16 ? 16 : nt > got ? got : nt;
+    pthread_t th[16];
+    int started = 0;
+    for (int k = 1; k < nt; ++k)
+      if (pthread_create(&th[started], nullptr, import_worker, &job) == 0) ++started;
+    import_worker(&job);
+    for (int k = 0; k < started; ++k) pthread_join(th[k], nullptr);
+    a.n = got;  // (released at a failure: the ones imported)
+    for (int i = 0; i < got; ++i)
+      if (a.h[i]) {
+        close(fds[i]);
+        fds[i] = -1;
       }
-      logf(2, "hbm broker: mapped granule %d", i);
-      close(fds[i]);
-      fds[i] = -1;
-      a.n = i + 1;
+    if (job.failed.load()) {
+      logf(1, "hbm broker: import/map of granule %d failed", job.failed.load() - 1);
+      goto fail;  // the process keeps what it mapped until exit; the broker reclaims at close
     }
+    logf(2, "hbm broker: %d granules imported and mapped by %d threads", got, nt);
     hipMemAccessDesc acc;
     memset(&acc, 0, sizeof acc);
     acc.location.type = hipMemLocationTypeDevice;
@@ -1295,6 +1350,9 @@ void arena_take() {
   a.ext[0] = {0, a.size};
   a.next = 1;
   a.sock = s;
+  g_take_connect_ns = t_conn - t_start;
+  g_take_wait_ns = t_fds - t_conn;
+  g_take_map_ns = mono_ns() - t_fds;
   a.state.store(1, std::memory_order_release);  // base/size published before the state
   logf(1, "hbm broker: %d granules of %llu bytes mapped at %p", a.n, gran, a.base);
   return;
@@ -1779,6 +1837,16 @@ GS_EXPORT int gpushare_shim_vmm_stats(uint64_t* creates, uint64_t* arena_maps, u
   int n = g_nwin;
   pthread_mutex_unlock(&g_arena.mu);
   return n;
+}
+
+// where the arena's TAKE spent its time (ns): connect, the broker's answer (a grant not there
+// yet, granules still held by a retiring pod), import + map; 0 when there is no arena
+GS_EXPORT int gpushare_shim_arena_timing(uint64_t* connect_ns, uint64_t* wait_ns, uint64_t* map_ns) {
+  int on = g_arena.state.load(std::memory_order_acquire) == 1;
+  if (connect_ns) *connect_ns = g_take_connect_ns;
+  if (wait_ns) *wait_ns = g_take_wait_ns;
+  if (map_ns) *map_ns = g_take_map_ns;
+  return on;
 }
 
 // (size, used) of the arena; 0 when there is none

@@ -556,6 +556,7 @@ def test_broker_arena_under_sanitizers(stub, tmp_path, san):
     name = ledger()
     env = dict(os.environ, LD_PRELOAD=f"{rt}:{lib}", LD_LIBRARY_PATH=str(d), GPUSHARE_LEDGER=name,
                GPUSHARE_QUOTA_BYTES=str(4 * GIB), GPUSHARE_HBM_BROKER=sock, GPUSHARE_HBM_TOKEN="t",
+               GPUSHARE_HBM_MAP_THREADS="4",           # the granules imported and mapped by 2 threads
                ASAN_OPTIONS="detect_leaks=0:halt_on_error=1", UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1",
                TSAN_OPTIONS="halt_on_error=1:report_bugs=1")
     try:
