@@ -92,6 +92,8 @@ __asm__(".symver dlopen,dlopen@GLIBC_2.2.5");
 __asm__(".symver shm_open,shm_open@GLIBC_2.2.5");
 __asm__(".symver pthread_once,pthread_once@GLIBC_2.2.5");
 __asm__(".symver memcpy,memcpy@GLIBC_2.2.5");
+__asm__(".symver pthread_create,pthread_create@GLIBC_2.2.5");
+__asm__(".symver pthread_join,pthread_join@GLIBC_2.2.5");
 
 #undef hipGetDeviceProperties
 
