@@ -63,6 +63,21 @@ def _arena_timing() -> dict | None:
     return dict(zip(("connect", "wait", "map"), (round(v.value / 1e6, 3) for v in vals)))
 
 
+def _arena_stream() -> dict | None:
+    """A streaming TAKE after it returned: allocations that waited for granules the broker still
+    owed, the MORE batches and their import + map time, granules mapped of the grant."""
+    try:
+        f = ctypes.CDLL(None).gpushare_shim_arena_stream
+    except AttributeError:
+        return None
+    f.argtypes = [ctypes.POINTER(ctypes.c_uint64)] * 6
+    v = [ctypes.c_uint64() for _ in range(6)]
+    if not f(*(ctypes.byref(x) for x in v)):
+        return None
+    return {"waits": v[0].value, "wait_ms": round(v[1].value / 1e6, 3), "msgs": v[2].value,
+            "map_ms": round(v[3].value / 1e6, 3), "mapped": v[4].value, "granted": v[5].value}
+
+
 def _arena_release():
     """With an HBM broker arena (quota shim + GPUSHARE_HBM_BROKER), hand its granules back now
     that everything is freed, rather than at process exit. None without an arena."""
@@ -140,7 +155,8 @@ def main() -> int:
     player.synchronize()
     init_ms = (time.perf_counter() - t0) * 1e3
     _send({"event": "ready", "init_ms": round(init_ms, 3), "quota": quota, "free_at_start": free,
-           "held": hold_bytes + work, "hold_ms": round(hold_ms, 3), "hold_chunk_ms": chunk_ms, "shim": _shim_stats()})
+           "held": hold_bytes + work, "hold_ms": round(hold_ms, 3), "hold_chunk_ms": chunk_ms, "shim": _shim_stats(),
+           "stream": _arena_stream()})
 
     ctl: "queue.Queue" = queue.Queue()
 

@@ -694,6 +694,10 @@ class PodFleet:
         dt = t3 - t0
         for k, v in (("init", t1 - t0), ("room", t2 - t1), ("alloc", t3 - t2), ("hold", ev.get("hold_ms", 0) / 1e3)):
             self.phase_ms[k].append(v)
+        stream = ev.get("stream") or {}
+        for k in ("wait_ms", "map_ms"):               # a streaming TAKE: owed granules, inside "alloc"
+            if k in stream:
+                self.phase_ms.setdefault(f"alloc_more_{k[:-3]}", []).append(stream[k] / 1e3)
         if self.trace is not None:
             self.trace.append({"size": rec["size"], "init": t1 - t0, "room": t2 - t1, "alloc": t3 - t2,
                                "hold_chunk_ms": ev.get("hold_chunk_ms"),

@@ -23,6 +23,11 @@
 //     "TAKE <token>\n"          -> "FDS <n> <granule bytes>\n", then n fds (batches of <= 200,
 //                                  one byte each); the connection stays open: its end (close,
 //                                  exit, crash) returns the granules, which are scrubbed first.
+//     "TAKE <token> STREAM\n"   -> "FDS <k> <granule bytes> <n>\n" + k fds at once (k = what is
+//                                  free now, possibly 0), then "MORE <j> <granule bytes>\n" + j
+//                                  fds as granules come back, until all n are delivered: the pod
+//                                  maps the first granules while a retiring pod's are still being
+//                                  torn down, instead of waiting for all n.
 // A TAKE whose granules are still held by a retiring pod waits (up to --wait-s), and one whose
 // grant has not arrived yet waits up to --ungranted-wait-s (a broker that just restarted is
 // re-granted by the plugin within a poll interval): the pod's runtime may start before the
@@ -163,6 +168,8 @@ struct Client {
   std::string token;      // the grant it holds
   std::string waiting;    // token of a TAKE not yet served
   double wait_since = 0;
+  bool stream = false;    // TAKE ... STREAM: granules are delivered as they become free
+  int owed = 0;           // granules of its grant still to deliver (stream)
 };
 
 enum Policy { kRefs, kExit, kTrust };
@@ -213,7 +220,7 @@ struct Broker {
   std::map<int, Client> clients;
   // stats
   unsigned long long takes = 0, releases = 0, refused = 0, timeouts = 0, busy = 0, idle_dropped = 0,
-                     revokes = 0, peer_refused = 0;
+                     revokes = 0, peer_refused = 0, streamed = 0, more_msgs = 0;
   double scrub_s_total = 0, scrub_s_last = 0, setup_s = 0;
   unsigned long long scrubbed_bytes = 0;
 
@@ -351,9 +358,11 @@ struct Broker {
     }
   }
 
-  bool send_fds(int fd, const std::vector<int>& idx) {
-    char head[64];
-    int n = std::snprintf(head, sizeof head, "FDS %zu %zu\n", idx.size(), gran);
+  // the header ("FDS <k> <gran>[ <total>]" or "MORE <k> <gran>"), then the fds
+  bool send_fds(int fd, const std::vector<int>& idx, const char* verb = "FDS", int total = -1) {
+    char head[96];
+    int n = total >= 0 ? std::snprintf(head, sizeof head, "%s %zu %zu %d\n", verb, idx.size(), gran, total)
+                       : std::snprintf(head, sizeof head, "%s %zu %zu\n", verb, idx.size(), gran);
     if (send(fd, head, n, MSG_NOSIGNAL) != n) return false;
     for (size_t i = 0; i < idx.size(); i += 200) {
       size_t k = std::min<size_t>(200, idx.size() - i);
@@ -377,32 +386,62 @@ struct Broker {
     return true;
   }
 
-  // serve waiting TAKEs in arrival order while granules last
+  std::vector<int> pop_free(int n) {
+    std::vector<int> idx;
+    for (int i = 0; i < n && !free_list.empty(); ++i) {
+      idx.push_back(free_list.front());
+      free_list.pop_front();
+    }
+    return idx;
+  }
+
+  // serve TAKEs in arrival order while granules last: granules still owed to streaming takers
+  // and whole grants of plain TAKEs go to the earliest first, nobody overtakes a taker still
+  // short of granules. A streaming TAKE is accepted at once whatever is free (its first batch may
+  // be empty): it is then owed the rest, in the same order.
   void serve_waiting() {
     std::vector<std::pair<double, int>> order;
     for (auto& kv : clients)
-      if (!kv.second.waiting.empty()) order.push_back({kv.second.wait_since, kv.first});
+      if (!kv.second.waiting.empty() || kv.second.owed > 0) order.push_back({kv.second.wait_since, kv.first});
     std::sort(order.begin(), order.end());
+    bool blocked = false;  // an earlier taker is still short: later ones get nothing now
+    std::vector<int> dead;
     for (auto& o : order) {
       auto ci = clients.find(o.second);
       if (ci == clients.end()) continue;
       Client& c = ci->second;
+      if (c.owed > 0) {
+        if (blocked) continue;
+        std::vector<int> idx = pop_free(c.owed);
+        if (!idx.empty()) {
+          c.owed -= int(idx.size());
+          c.held.insert(c.held.end(), idx.begin(), idx.end());
+          ++more_msgs;
+          if (!send_fds(c.fd, idx, "MORE")) dead.push_back(o.second);
+        }
+        if (c.owed > 0) blocked = true;
+        continue;
+      }
       auto g = grants.find(c.waiting);
       if (g == grants.end() || g->second.holder >= 0) continue;  // not granted yet, or held
-      if (size_t(g->second.granules) > free_list.size()) break;  // keep arrival order: no overtaking
-      std::vector<int> idx;
-      for (int i = 0; i < g->second.granules; ++i) {
-        idx.push_back(free_list.front());
-        free_list.pop_front();
+      int n = g->second.granules;
+      if (!c.stream && (blocked || size_t(n) > free_list.size())) {
+        blocked = true;  // keep arrival order: no overtaking
+        continue;
       }
+      std::vector<int> idx = pop_free(blocked ? 0 : n);
       g->second.holder = o.second;
       if (policy == kExit && c.pidfd < 0) c.pidfd = pidfd_of(c.pid);  // while it is surely alive
       c.token = c.waiting;
       c.waiting.clear();
       c.held = idx;
+      c.owed = n - int(idx.size());
       ++takes;
-      if (!send_fds(c.fd, idx)) drop(o.second);
+      streamed += c.stream;
+      if (c.owed > 0) blocked = true;
+      if (!send_fds(c.fd, idx, "FDS", c.stream ? n : -1)) dead.push_back(o.second);
     }
+    for (int fd : dead) drop(fd);
   }
 
   // other references to granule i's dma-buf: the kernel's fdinfo "count" is the file's
@@ -515,23 +554,24 @@ struct Broker {
   const char* policy_name() const { return policy == kRefs ? "refs" : policy == kExit ? "exit" : "trust"; }
 
   std::string stat() const {
-    size_t held = 0, waiting = 0, scrub_n = 0;
+    size_t held = 0, waiting = 0, scrub_n = 0, owed = 0;
     for (auto& kv : clients) {
       held += kv.second.held.size();
       waiting += !kv.second.waiting.empty();
+      owed += size_t(kv.second.owed);
     }
     for (auto& s : scrubbing) scrub_n += s.idx.size();
     char b[2048];
     std::snprintf(b, sizeof b,
                   "{\"boot\": \"%s\", \"device\": %d, \"granule_bytes\": %zu, \"granules\": %d, \"granules_max\": %d, "
                   "\"grown\": %llu, \"free\": %zu, "
-                  "\"held\": %zu, \"scrubbing\": %zu, \"waiting\": %zu, \"grants\": %zu, \"takes\": %llu, "
+                  "\"held\": %zu, \"owed\": %zu, \"streamed\": %llu, \"more_msgs\": %llu, \"scrubbing\": %zu, \"waiting\": %zu, \"grants\": %zu, \"takes\": %llu, "
                   "\"releases\": %llu, \"refused\": %llu, \"revokes\": %llu, \"revoked\": %zu, \"timeouts\": %llu, "
                   "\"expired\": %llu, \"busy\": %llu, \"idle_dropped\": %llu, \"peer_refused\": %llu, "
                   "\"clients\": %zu, \"quarantined\": %zu, \"quarantined_total\": %llu, \"lost\": %llu, "
                   "\"release_policy\": \"%s\", \"held_refs_max\": %d, \"base_refs\": %d, \"scrubbed_bytes\": %llu, "
                   "\"scrub_ms_total\": %.3f, \"scrub_ms_last\": %.3f, \"setup_ms\": %.1f}\n",
-                  boot.c_str(), device, gran, count, count_max, grown, free_list.size(), held, scrub_n, waiting, grants.size(), takes,
+                  boot.c_str(), device, gran, count, count_max, grown, free_list.size(), held, owed, streamed, more_msgs, scrub_n, waiting, grants.size(), takes,
                   releases, refused, revokes, revoked.size(), timeouts, expired, busy, idle_dropped, peer_refused,
                   clients.size(), quarantined(), quarantined_total, lost, policy_name(), held_refs_max(),
                   base_refs.empty() ? -1 : base_refs[0], scrubbed_bytes, scrub_s_total * 1e3, scrub_s_last * 1e3,
@@ -557,6 +597,23 @@ struct Broker {
         revoked_order.pop_front();
       }
     }
+  }
+
+  // "TAKE <token>" or "TAKE <token> STREAM"
+  static bool take_line(const std::string& line, char* tok, bool* stream) {
+    char opt[16] = {0};
+    char extra = 0;
+    int k = std::sscanf(line.c_str(), "TAKE %128s %15s %c", tok, opt, &extra);
+    if (!valid_token(tok)) return false;
+    if (k == 1) {
+      *stream = false;
+      return true;
+    }
+    if (k == 2 && std::strcmp(opt, "STREAM") == 0) {
+      *stream = true;
+      return true;
+    }
+    return false;
   }
 
   void on_line(int fd, const std::string& line) {
@@ -589,6 +646,7 @@ struct Broker {
           auto h = clients.find(g->second.holder);
           if (h != clients.end()) {
             h->second.token.clear();  // its end returns the granules, the grant is gone already
+            h->second.owed = 0;       // and it is lent no more of them
             held = int(h->second.held.size());
           }
         }
@@ -608,8 +666,7 @@ struct Broker {
       reply(fd, list());
     } else if (c.admin && line == "STAT") {
       reply(fd, stat());
-    } else if (!c.admin && c.held.empty() && c.waiting.empty() &&
-               std::sscanf(line.c_str(), "TAKE %128s %c", tok, &extra) == 1 && valid_token(tok)) {
+    } else if (!c.admin && c.held.empty() && c.waiting.empty() && c.token.empty() && take_line(line, tok, &c.stream)) {
       if (revoked.count(tok)) {
         ++refused;
         reply(fd, "ERR revoked\n");

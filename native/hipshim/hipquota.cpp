@@ -67,6 +67,7 @@
 #include <errno.h>
 #include <fcntl.h>
 #include <link.h>
+#include <poll.h>
 #include <pthread.h>
 #include <signal.h>
 #include <stdarg.h>
@@ -1107,8 +1108,12 @@ struct Arena {
   std::atomic<int> state{0};  // 0 untried, 1 active, -1 off (no broker configured, failed or released)
   int sock = -1;
   char* base = nullptr;
-  uint64_t size = 0, gran = 0, used = 0;
-  int n = 0;
+  // size: the pod's grant (total granules; charged, and what hipMemGetInfo promises); vsize: the
+  // address range reserved for it. A streaming TAKE maps granules [0, n) and is owed [n, total)
+  uint64_t size = 0, vsize = 0, gran = 0, used = 0;
+  int n = 0, total = 0;
+  bool by_address = false;  // how this runtime imports a POSIX fd (see arena_take)
+  int map_threads = 1;
   hipMemGenericAllocationHandle_t h[kArenaMaxGranules];
   Ext* ext = nullptr;
   int next = 0;
@@ -1119,8 +1124,10 @@ struct Arena {
 Arena g_arena;
 int g_dev = 0;  // the arena's device (HIP ordinal in this process)
 // where a TAKE's time went (ns): connecting to the broker, waiting for its answer, importing and
-// mapping the granules (gpushare_shim_arena_timing)
+// mapping the granules (gpushare_shim_arena_timing); then, for a streaming TAKE, allocations that
+// waited for owed granules, importing and mapping those, and MORE messages received
 uint64_t g_take_connect_ns = 0, g_take_wait_ns = 0, g_take_map_ns = 0;
+uint64_t g_more_wait_ns = 0, g_more_map_ns = 0, g_more_msgs = 0, g_more_waits = 0;
 
 uint64_t mono_ns() {
   timespec t;
@@ -1209,19 +1216,48 @@ void* import_worker(void* p) {
   return nullptr;
 }
 
+// import fds[0..k) and map granule i at base + i * gran, by `nt` threads; h[i] set for each one
+// imported (nullptr otherwise). Returns 0, or the first failed granule + 1
+int import_and_map(int* fds, int k, hipMemGenericAllocationHandle_t* h, char* base, uint64_t gran, bool by_address,
+                   int nt) {
+  ImportJob job{real_hipMemImportFromShareableHandle(), real_hipMemMap(), fds, h, base, gran, by_address, {0}, {0}, k};
+  for (int i = 0; i < k; ++i) h[i] = nullptr;
+  if (!job.import_f || !job.map_f) return k > 0 ? 1 : 0;
+  nt = nt < 1 ? 1 : nt > 16 ? 16 : nt > k ? k : nt;
+  pthread_t th[16];
+  int started = 0;
+  for (int t = 1; t < nt; ++t)
+    if (pthread_create(&th[started], nullptr, import_worker, &job) == 0) ++started;
+  import_worker(&job);
+  for (int t = 0; t < started; ++t) pthread_join(th[t], nullptr);
+  return job.failed.load();
+}
+
+// read-write for device `dev`
+bool set_rw(char* va, uint64_t len, int dev) {
+  hipMemAccessDesc acc;
+  memset(&acc, 0, sizeof acc);
+  acc.location.type = hipMemLocationTypeDevice;
+  acc.location.id = dev;
+  acc.flags = hipMemAccessFlagsProtReadWrite;
+  auto f = real_hipMemSetAccess();
+  return f && f(va, len, &acc, 1) == hipSuccess;
+}
+
 // unmap and release whatever of the arena is mapped (g_arena.mu held)
 void arena_unmap_locked() {
   Arena& a = g_arena;
   Depth d;
   if (auto dev_sync = real_hipDeviceSynchronize()) (void)dev_sync();
   if (a.base) {
-    if (auto un = real_hipMemUnmap()) (void)un(a.base, a.size);
-    if (auto fr = real_hipMemAddressFree()) (void)fr(a.base, a.size);
+    if (auto un = real_hipMemUnmap())
+      if (a.n) (void)un(a.base, uint64_t(a.n) * a.gran);
+    if (auto fr = real_hipMemAddressFree()) (void)fr(a.base, a.vsize);
   }
   if (auto rel = real_hipMemRelease())
     for (int i = 0; i < a.n; ++i)
       if (a.h[i]) (void)rel(a.h[i]);
-  a.n = 0;
+  a.n = a.total = 0;
   a.base = nullptr;
 }
 
@@ -1240,8 +1276,11 @@ void arena_take() {
   char line[256];
   int fds[kArenaMaxGranules];
   int got = 0;
-  unsigned long long want = 0, gran = 0;
+  unsigned long long want = 0, gran = 0, total = 0;
   int dev = 0;
+  // streaming (the default): the broker answers at once with what is free and sends the rest as
+  // it comes back; GPUSHARE_HBM_STREAM=0 waits for the whole grant in one answer
+  bool stream = env_u64("GPUSHARE_HBM_STREAM", 1) != 0;
   auto import_f = real_hipMemImportFromShareableHandle();
   auto reserve_f = real_hipMemAddressReserve();
   auto map_f = real_hipMemMap();
@@ -1276,13 +1315,17 @@ void arena_take() {
   }
   t_conn = mono_ns();
   {
-    int n = snprintf(line, sizeof line, "TAKE %s\n", tok);
+    int n = snprintf(line, sizeof line, stream ? "TAKE %s STREAM\n" : "TAKE %s\n", tok);
     if (send(s, line, n, MSG_NOSIGNAL) != n) goto fail;
   }
-  if (!recv_line(s, line, sizeof line) || sscanf(line, "FDS %llu %llu", &want, &gran) != 2 || want == 0 ||
-      want > (unsigned long long)kArenaMaxGranules || gran == 0) {
-    logf(1, "hbm broker %s refused the grant: %s", path, line);
-    goto fail;
+  {
+    line[0] = 0;
+    int k = recv_line(s, line, sizeof line) ? sscanf(line, "FDS %llu %llu %llu", &want, &gran, &total) : 0;
+    if (k == 2) total = want;
+    if (k < 2 || total == 0 || want > total || total > (unsigned long long)kArenaMaxGranules || gran == 0) {
+      logf(1, "hbm broker %s refused the grant: %s", path, line);
+      goto fail;
+    }
   }
   while (got < (int)want)
     if (!recv_fd_batch(s, fds, &got, (int)want)) goto fail;
@@ -1301,40 +1344,30 @@ void arena_take() {
     bool by_address = rtv > 0 && rtv < 70100000;
     logf(1, "hbm broker: runtime %d: fds imported by %s", rtv, by_address ? "address" : "value");
     void* base = nullptr;
-    uint64_t size = want * gran;
-    if (reserve_f(&base, size, 0, nullptr, 0) != hipSuccess) goto fail;
-    logf(2, "hbm broker: reserved %p + %llu", base, (unsigned long long)size);
-    // import + map every granule; GPUSHARE_HBM_MAP_THREADS (default 1) threads share the work
-    ImportJob job{import_f, map_f, fds, a.h, static_cast<char*>(base), gran, by_address, {0}, {0}, got};
-    for (int i = 0; i < got; ++i) a.h[i] = nullptr;
+    uint64_t vsize = total * gran;
+    if (reserve_f(&base, vsize, 0, nullptr, 0) != hipSuccess) goto fail;
+    logf(2, "hbm broker: reserved %p + %llu", base, (unsigned long long)vsize);
+    // import + map the granules; GPUSHARE_HBM_MAP_THREADS (default 1) threads share the work
     int nt = int(env_u64("GPUSHARE_HBM_MAP_THREADS", 1));
-    nt = nt < 1 ? 1 : nt > 16 ? 16 : nt > got ? got : nt;
-    pthread_t th[16];
-    int started = 0;
-    for (int k = 1; k < nt; ++k)
-      if (pthread_create(&th[started], nullptr, import_worker, &job) == 0) ++started;
-    import_worker(&job);
-    for (int k = 0; k < started; ++k) pthread_join(th[k], nullptr);
+    int failed = import_and_map(fds, got, a.h, static_cast<char*>(base), gran, by_address, nt);
     a.n = got;  // (released at a failure: the ones imported)
     for (int i = 0; i < got; ++i)
       if (a.h[i]) {
         close(fds[i]);
         fds[i] = -1;
       }
-    if (job.failed.load()) {
-      logf(1, "hbm broker: import/map of granule %d failed", job.failed.load() - 1);
+    if (failed) {
+      logf(1, "hbm broker: import/map of granule %d failed", failed - 1);
       goto fail;  // the process keeps what it mapped until exit; the broker reclaims at close
     }
     logf(2, "hbm broker: %d granules imported and mapped by %d threads", got, nt);
-    hipMemAccessDesc acc;
-    memset(&acc, 0, sizeof acc);
-    acc.location.type = hipMemLocationTypeDevice;
-    acc.location.id = dev;
-    acc.flags = hipMemAccessFlagsProtReadWrite;
-    if (access_f(base, size, &acc, 1) != hipSuccess) goto fail;
+    if (got && !set_rw(static_cast<char*>(base), uint64_t(got) * gran, dev)) goto fail;
     a.base = static_cast<char*>(base);
-    a.size = size;
+    a.size = a.vsize = vsize;
     a.gran = gran;
+    a.total = int(total);
+    a.by_address = by_address;
+    a.map_threads = nt;
     g_dev = dev;
   }
   // the arena counts against the pod's quota like any other HBM it holds: what the runtime
@@ -1349,14 +1382,14 @@ void arena_take() {
   a.ext = static_cast<Ext*>(calloc(kArenaMaxExt, sizeof(Ext)));
   a.live = static_cast<Live*>(calloc(kArenaLiveCap, sizeof(Live)));
   if (!a.ext || !a.live) goto fail;
-  a.ext[0] = {0, a.size};
-  a.next = 1;
+  a.ext[0] = {0, uint64_t(a.n) * a.gran};
+  a.next = a.n ? 1 : 0;
   a.sock = s;
   g_take_connect_ns = t_conn - t_start;
   g_take_wait_ns = t_fds - t_conn;
   g_take_map_ns = mono_ns() - t_fds;
   a.state.store(1, std::memory_order_release);  // base/size published before the state
-  logf(1, "hbm broker: %d granules of %llu bytes mapped at %p", a.n, gran, a.base);
+  logf(1, "hbm broker: %d of %d granules of %llu bytes mapped at %p", a.n, a.total, gran, a.base);
   return;
 fail:
   for (int i = 0; i < got; ++i)
@@ -1448,11 +1481,9 @@ bool arena_take_granule(uint64_t* off) {
   return false;
 }
 
-void arena_free(uint64_t off) {
+// [off, off + len) is free again: into the sorted extent list, joined with its neighbours
+void ext_insert(uint64_t off, uint64_t len) {
   Arena& a = g_arena;
-  uint64_t len = 0;
-  if (!live_take(off, &len)) return;
-  a.used -= len;
   int lo = 0, hi = a.next;  // first extent after off
   while (lo < hi) {
     int mid = (lo + hi) / 2;
@@ -1475,6 +1506,104 @@ void arena_free(uint64_t off) {
     a.ext[lo] = {off, len};
     ++a.next;
   }  // else: the extent list is full and these bytes stay unusable until release (never seen)
+}
+
+void arena_free(uint64_t off) {
+  Arena& a = g_arena;
+  uint64_t len = 0;
+  if (!live_take(off, &len)) return;
+  a.used -= len;
+  ext_insert(off, len);
+}
+
+// ---- streaming TAKE: granules owed by the broker ----
+// The broker sends "MORE <k> <gran>" and k fds as granules come back (a retiring pod's, once its
+// process is gone and they are scrubbed). Each batch is mapped after the granules already there
+// and joins the free list. g_arena.mu held.
+
+// the broker will send no more (it went away, or sent something else): the grant shrinks to what
+// was delivered, and the ledger with it
+void arena_stream_end(const char* why) {
+  Arena& a = g_arena;
+  logf(1, "hbm broker: stream ended (%s) at %d of %d granules", why, a.n, a.total);
+  uint64_t owed = uint64_t(a.total - a.n) * a.gran;
+  a.total = a.n;
+  a.size -= owed;
+  if (a.charged) uncharge(owed);
+}
+
+// receive one batch if it arrives within `wait_ms` (0: only one already there); true if the
+// arena grew
+bool arena_more_locked(int wait_ms) {
+  Arena& a = g_arena;
+  if (a.n >= a.total || a.sock < 0) return false;
+  pollfd p{a.sock, POLLIN, 0};
+  uint64_t t0 = mono_ns();
+  int r = poll(&p, 1, wait_ms);
+  if (wait_ms > 0) g_more_wait_ns += mono_ns() - t0;
+  if (r <= 0) return false;
+  char line[128];
+  line[0] = 0;
+  unsigned long long k = 0, gran = 0;
+  if (!recv_line(a.sock, line, sizeof line) || sscanf(line, "MORE %llu %llu", &k, &gran) != 2 || gran != a.gran ||
+      k == 0 || k > (unsigned long long)(a.total - a.n)) {
+    arena_stream_end(line[0] ? line : "connection closed");
+    return false;
+  }
+  uint64_t t1 = mono_ns();
+  int fds[kArenaMaxGranules];
+  int got = 0;
+  while (got < int(k))
+    if (!recv_fd_batch(a.sock, fds, &got, int(k))) {
+      for (int i = 0; i < got; ++i) close(fds[i]);
+      arena_stream_end("fds lost");
+      return false;
+    }
+  Depth d;
+  char* at = a.base + uint64_t(a.n) * a.gran;
+  int failed = import_and_map(fds, got, a.h + a.n, at, a.gran, a.by_address, a.map_threads);
+  for (int i = 0; i < got; ++i) close(fds[i]);
+  if (failed || !set_rw(at, uint64_t(got) * a.gran, g_dev)) {
+    // keep none of this batch: what was mapped goes, the handles are released
+    auto un = real_hipMemUnmap();
+    auto rel = real_hipMemRelease();
+    for (int i = 0; i < got; ++i)
+      if (a.h[a.n + i]) {
+        if (un) (void)un(at + uint64_t(i) * a.gran, a.gran);
+        if (rel) (void)rel(a.h[a.n + i]);
+        a.h[a.n + i] = nullptr;
+      }
+    arena_stream_end("import/map failed");
+    return false;
+  }
+  ext_insert(uint64_t(a.n) * a.gran, uint64_t(got) * a.gran);
+  a.n += got;
+  ++g_more_msgs;
+  g_more_map_ns += mono_ns() - t1;
+  logf(2, "hbm broker: %d more granules, %d of %d mapped", got, a.n, a.total);
+  return true;
+}
+
+// an allocation of `need` bytes found no room: while the grant has granules still owed that
+// would make room, wait for them (GPUSHARE_HBM_MORE_WAIT_S, default 60 s); false: none came
+bool arena_wait_more(uint64_t need) {
+  Arena& a = g_arena;
+  if (a.n >= a.total || need > a.size - a.used) return false;
+  static double limit_s = -1;
+  if (limit_s < 0) {
+    const char* w = getenv("GPUSHARE_HBM_MORE_WAIT_S");
+    limit_s = w ? atof(w) : 60.0;
+  }
+  ++g_more_waits;
+  uint64_t deadline = mono_ns() + uint64_t(limit_s * 1e9);
+  while (a.n < a.total) {
+    if (arena_more_locked(100)) return true;
+    if (mono_ns() > deadline) {
+      logf(1, "hbm broker: %d granules still owed after %.0f s", a.total - a.n, limit_s);
+      return false;
+    }
+  }
+  return false;
 }
 
 // ---- stream-ordered frees (hipFreeAsync of arena blocks) ----
@@ -1520,11 +1649,14 @@ int arena_try_alloc(void** ptr, size_t size, hipError_t* e) {
     return 0;
   }
   if (g_nafree) reap_async_frees(false);
+  while (a.n < a.total && arena_more_locked(0)) {
+  }  // owed granules that have arrived
   bool ok = arena_alloc(size, ptr);
   if (!ok && g_nafree) {  // room that stream-ordered frees will give back: wait for them
     reap_async_frees(true);
     ok = arena_alloc(size, ptr);
   }
+  while (!ok && arena_wait_more(size)) ok = arena_alloc(size, ptr);  // room the broker still owes
   pthread_mutex_unlock(&a.mu);
   if (!ok) {
     if (ptr) *ptr = nullptr;
@@ -1559,6 +1691,8 @@ constexpr uint64_t kVHandleMagic = 0x67737668616e646cull;  // "gsvhandl"
 struct Win {
   char* base;
   uint64_t size;
+  char* vbase;     // the reservation it lies in (larger when the runtime ignored the alignment)
+  uint64_t vsize;
   int nslots;
   int32_t* slot_g;      // arena granule backing the slot, -1 none
   uint64_t* slot_used;  // bytes of stand-in pages mapped in the slot (arena-backed slots)
@@ -1656,22 +1790,17 @@ Win* win_of(const char* p, uint64_t len) {
   return nullptr;
 }
 
-bool set_rw(char* va, uint64_t len, int dev) {
-  hipMemAccessDesc acc;
-  memset(&acc, 0, sizeof acc);
-  acc.location.type = hipMemLocationTypeDevice;
-  acc.location.id = dev;
-  acc.flags = hipMemAccessFlagsProtReadWrite;
-  auto f = real_hipMemSetAccess();
-  return f && f(va, len, &acc, 1) == hipSuccess;
-}
-
 // back slot s of window w with an arena granule (g_arena.mu held); false: none free (or the
 // broker's granule is not the slot size: then every page is the driver's)
 bool slot_back(Win& w, int s) {
   Arena& a = g_arena;
   uint64_t off;
-  if (a.state.load(std::memory_order_relaxed) != 1 || a.gran != kWinAlign || !arena_take_granule(&off)) return false;
+  if (a.state.load(std::memory_order_relaxed) != 1 || a.gran != kWinAlign) return false;
+  while (a.n < a.total && arena_more_locked(0)) {
+  }
+  bool got = arena_take_granule(&off);
+  while (!got && arena_wait_more(a.gran)) got = arena_take_granule(&off);
+  if (!got) return false;
   int gi = int(off / a.gran);
   auto un = real_hipMemUnmap();
   auto map = real_hipMemMap();
@@ -1848,6 +1977,23 @@ GS_EXPORT int gpushare_shim_arena_timing(uint64_t* connect_ns, uint64_t* wait_ns
   if (connect_ns) *connect_ns = g_take_connect_ns;
   if (wait_ns) *wait_ns = g_take_wait_ns;
   if (map_ns) *map_ns = g_take_map_ns;
+  return on;
+}
+
+// a streaming TAKE after it returned: allocations that waited for owed granules (count, ns), the
+// MORE batches received and the ns spent importing + mapping them, granules mapped and granted
+GS_EXPORT int gpushare_shim_arena_stream(uint64_t* waits, uint64_t* wait_ns, uint64_t* msgs, uint64_t* map_ns,
+                                         uint64_t* mapped, uint64_t* granted) {
+  Arena& a = g_arena;
+  pthread_mutex_lock(&a.mu);
+  int on = a.state == 1;
+  if (waits) *waits = g_more_waits;
+  if (wait_ns) *wait_ns = g_more_wait_ns;
+  if (msgs) *msgs = g_more_msgs;
+  if (map_ns) *map_ns = g_more_map_ns;
+  if (mapped) *mapped = on ? uint64_t(a.n) : 0;
+  if (granted) *granted = on ? uint64_t(a.total) : 0;
+  pthread_mutex_unlock(&a.mu);
   return on;
 }
 
@@ -2106,16 +2252,36 @@ GS_EXPORT hipError_t hipMemAddressReserve(void** ptr, size_t size, size_t alignm
   bool window = arena_configured() && !t_depth && size >= kWinAlign && !addr;
   if (window && alignment < kWinAlign) alignment = kWinAlign;  // slots on granule boundaries
   hipError_t e;
+  char* vbase = nullptr;
+  uint64_t vsize = size;
   {
     Depth d;
     e = f(ptr, size, alignment, addr, flags);
+    vbase = e == hipSuccess && ptr ? static_cast<char*>(*ptr) : nullptr;
+    if (window && vbase && reinterpret_cast<uintptr_t>(vbase) % kWinAlign) {
+      // the runtime does not honour so large an alignment (HIP 7.x returns a 2 MiB-aligned range):
+      // reserve one granule more and use its aligned part; the whole reservation is freed with it
+      (void)real_hipMemAddressFree()(vbase, size);
+      void* big = nullptr;
+      if (f(&big, size + kWinAlign, 0, nullptr, flags) == hipSuccess && big) {
+        vbase = static_cast<char*>(big);
+        vsize = size + kWinAlign;
+        *ptr = reinterpret_cast<void*>((reinterpret_cast<uintptr_t>(big) + kWinAlign - 1) & ~uintptr_t(kWinAlign - 1));
+      } else {
+        window = false;  // no aligned range: an ordinary reservation, its pages from the driver
+        e = f(ptr, size, 0, addr, flags);
+        vbase = nullptr;
+      }
+    }
   }
-  if (e != hipSuccess || !window || !ptr || !*ptr || reinterpret_cast<uintptr_t>(*ptr) % kWinAlign) return e;
+  if (e != hipSuccess || !window || !ptr || !*ptr) return e;
   pthread_mutex_lock(&g_arena.mu);
   if (g_nwin < kMaxWin) {
     Win& w = g_win[g_nwin];
     w.base = static_cast<char*>(*ptr);
     w.size = size;
+    w.vbase = vbase;
+    w.vsize = vsize;
     w.nslots = int((size + kWinAlign - 1) / kWinAlign);
     w.slot_g = static_cast<int32_t*>(malloc(sizeof(int32_t) * size_t(w.nslots)));
     w.slot_used = static_cast<uint64_t*>(calloc(size_t(w.nslots), sizeof(uint64_t)));
@@ -2134,6 +2300,8 @@ GS_EXPORT hipError_t hipMemAddressReserve(void** ptr, size_t size, size_t alignm
 GS_EXPORT hipError_t hipMemAddressFree(void* ptr, size_t size) {
   auto f = real_hipMemAddressFree();
   if (!f) return hipErrorNotInitialized;
+  char* vbase = static_cast<char*>(ptr);
+  uint64_t vsize = size;
   if (ptr && arena_configured() && !t_depth) {
     pthread_mutex_lock(&g_arena.mu);
     for (int i = 0; i < g_nwin; ++i) {
@@ -2142,13 +2310,15 @@ GS_EXPORT hipError_t hipMemAddressFree(void* ptr, size_t size) {
       for (int sl = 0; sl < w.nslots; ++sl)
         if (w.slot_g[sl] >= 0) slot_return(w, sl);   // pages the program never unmapped
       free(w.slot_g), free(w.slot_used), free(w.slot_real);
+      vbase = w.vbase;
+      vsize = w.vsize;
       g_win[i] = g_win[--g_nwin];
       break;
     }
     pthread_mutex_unlock(&g_arena.mu);
   }
   Depth d;
-  return f(ptr, size);
+  return f(vbase, vsize);
 }
 
 GS_EXPORT hipError_t hipMemMap(void* ptr, size_t size, size_t offset, hipMemGenericAllocationHandle_t handle,

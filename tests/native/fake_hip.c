@@ -190,13 +190,19 @@ hipError_t hipMemImportFromShareableHandle(uint64_t* h, void* os, int type) {
   *h = IMPORTED | (uint64_t)d; return 0;
 }
 hipError_t hipMemRelease_imported(uint64_t h) { close((int)(h & 0xffffffff)); return 0; }
+/* FAKE_HIP_RESERVE_ALIGN_MAX=<bytes>: like HIP 7.x, a larger alignment is not honoured, and the
+   range is deliberately placed off any larger boundary */
 hipError_t hipMemAddressReserve(void** p, size_t n, size_t al, void* addr, unsigned long long fl) {
   if (al < 4096) al = 4096;
-  char* m = mmap(0, n + al, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+  const char* cap = getenv("FAKE_HIP_RESERVE_ALIGN_MAX");
+  size_t skew = 0;
+  if (cap && al > strtoull(cap, 0, 10)) { al = strtoull(cap, 0, 10); skew = al; }
+  char* m = mmap(0, n + al + skew, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
   if (m == MAP_FAILED) return 2;
   char* a = (char*)(((uintptr_t)m + al - 1) / al * al);      /* honour the alignment: trim both ends */
+  if (skew && ((uintptr_t)a % (1ull << 30)) == 0) a += skew;
   if (a > m) munmap(m, (size_t)(a - m));
-  if (m + n + al > a + n) munmap(a + n, (size_t)(m + n + al - (a + n)));
+  if (m + n + al + skew > a + n) munmap(a + n, (size_t)(m + n + al + skew - (a + n)));
   *p = a; return 0;
 }
 hipError_t hipMemAddressFree(void* p, size_t n) { munmap(p, n); return 0; }

@@ -453,13 +453,16 @@ def test_prime_export_of_charged_vram_is_refused(stub, native_shim, tmp_path):
 
 class FakeBroker:
     """The HBM broker's pod side (native/hbmbroker): answers one TAKE with ``granules`` fds, then
-    records when the pod's connection ends (its granules would be scrubbed and lent again)."""
+    records when the pod's connection ends (its granules would be scrubbed and lent again).
+    ``stream``: [(delay_s, k), ...] answers a streaming TAKE with ``granules - sum(k)`` at once
+    ("FDS <k0> <gran> <total>") and each k after its delay ("MORE <k> <gran>"); with ``hangup``
+    it closes the connection at the first delay instead (a broker that went away)."""
 
-    def __init__(self, path, granules=4, gran=GIB, refuse=False):
+    def __init__(self, path, granules=4, gran=GIB, refuse=False, stream=None, hangup=False):
         import socket
         import threading
 
-        self.granules, self.gran, self.refuse = granules, gran, refuse
+        self.granules, self.gran, self.refuse, self.stream, self.hangup = granules, gran, refuse, stream, hangup
         self.took = None
         self.closed_at = None
         self.ls = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
@@ -480,11 +483,26 @@ class FakeBroker:
             conn.sendall(b"ERR timeout\n")
             conn.close()
             return
-        fds = [os.open("/dev/null", os.O_RDONLY) for _ in range(self.granules)]
-        conn.sendall(f"FDS {self.granules} {self.gran}\n".encode())
-        socket.send_fds(conn, [b"f"], fds)
-        for fd in fds:
-            os.close(fd)
+        def send(head, k):
+            fds = [os.open("/dev/null", os.O_RDONLY) for _ in range(k)]
+            conn.sendall(head.encode())
+            if fds:
+                socket.send_fds(conn, [b"f"], fds)
+            for fd in fds:
+                os.close(fd)
+
+        if self.stream:
+            later = sum(k for _, k in self.stream)
+            send(f"FDS {self.granules - later} {self.gran} {self.granules}\n", self.granules - later)
+            for delay, k in self.stream:
+                time.sleep(delay)
+                if self.hangup:
+                    conn.close()
+                    self.closed_at = time.monotonic()
+                    return
+                send(f"MORE {k} {self.gran}\n", k)
+        else:
+            send(f"FDS {self.granules} {self.gran}\n", self.granules)
         while conn.recv(1):
             pass
         self.closed_at = time.monotonic()
@@ -509,7 +527,7 @@ def test_broker_arena_serves_hipmalloc_from_the_granted_granules(stub, native_sh
                      GPUSHARE_HBM_TOKEN="tok123")
         t_end = time.monotonic()
         assert r.returncode == 0, r.stderr
-        assert b.took == "TAKE tok123"
+        assert b.took == "TAKE tok123 STREAM"               # streaming is the default; this broker answers whole
         a3, b512, arena, _, c2, d1, e1, info, st, rel_live, _, rel, arena_after, late, st_after = out
         assert a3["err"] == 0 and b512["err"] == 0
         assert arena == {"op": "arena", "on": 1, "size": 4 * GIB, "used": 3 * GIB + 512 * MIB}
@@ -526,6 +544,68 @@ def test_broker_arena_serves_hipmalloc_from_the_granted_granules(stub, native_sh
         cleanup(name)
 
 
+def test_streaming_take_maps_the_first_granules_and_waits_for_the_rest(stub, native_shim, tmp_path):
+    """A streaming TAKE (the default): the broker answers at once with the 1 granule of 4 it has
+    free; the pod's runtime is up without waiting for the other 3. A 512 MiB allocation is served
+    from it; a 2 GiB one waits for the MORE batches (0.3 s, then 0.2 s) and lands contiguously
+    in the first granule's rest and the new ones; hipMemGetInfo reports the whole grant; the ledger holds the grant
+    from the start."""
+    import time
+
+    sock = str(tmp_path / "hbm.sock")
+    b = FakeBroker(sock, granules=4, stream=[(0.3, 1), (0.2, 2)])
+    name = ledger()
+    try:
+        t0 = time.monotonic()
+        out, r = run(stub, native_shim, ["alloc", 512 * MIB, "arena", "arenastream", "info", "stats", "alloc", 2 * GIB,
+                                         "arenastream", "alloc", 2 * GIB, "arena", "arenastream"],
+                     GPUSHARE_QUOTA_BYTES=8 * GIB, GPUSHARE_LEDGER=name, GPUSHARE_HBM_BROKER=sock,
+                     GPUSHARE_HBM_TOKEN="tok")
+        assert r.returncode == 0, r.stderr
+        assert b.took == "TAKE tok STREAM"
+        small, arena, s0, info, st, big, s1, last, arena2, s2 = out
+        assert small["err"] == 0 and arena == {"op": "arena", "on": 1, "size": 4 * GIB, "used": 512 * MIB}
+        assert s0["mapped"] == 1 and s0["granted"] == 4 and s0["waits"] == 0
+        assert info["free"] == 4 * GIB - 512 * MIB + 4 * GIB                # the grant's rest + the quota's rest
+        assert st["used"] == 4 * GIB                                         # the whole grant is charged
+        assert big["err"] == 0 and big["p"] == small["p"] + 512 * MIB       # the granules join the first one's rest
+        assert s1["mapped"] == 4 and s1["msgs"] == 2 and s1["waits"] >= 1 and s1["wait_ms"] >= 400
+        assert last["err"] == 2                                              # 1.5 GiB left of the grant: no wait
+        assert arena2["used"] == 2 * GIB + 512 * MIB and s2["mapped"] == 4
+        assert time.monotonic() - t0 < 10
+    finally:
+        cleanup(name)
+
+
+def test_plain_take_and_a_stream_that_ends_early(stub, native_shim, tmp_path):
+    """GPUSHARE_HBM_STREAM=0 asks for the whole grant in one answer. A stream whose broker goes
+    away before the rest comes shrinks the grant to what was delivered, and the ledger with it."""
+    sock = str(tmp_path / "hbm.sock")
+    b = FakeBroker(sock, granules=2)
+    name = ledger()
+    try:
+        out, r = run(stub, native_shim, ["alloc", GIB, "arena"], GPUSHARE_QUOTA_BYTES=4 * GIB, GPUSHARE_LEDGER=name,
+                     GPUSHARE_HBM_BROKER=sock, GPUSHARE_HBM_TOKEN="plain", GPUSHARE_HBM_STREAM="0")
+        assert r.returncode == 0, r.stderr
+        assert b.took == "TAKE plain" and out[1]["size"] == 2 * GIB
+    finally:
+        cleanup(name)
+    sock2 = str(tmp_path / "hbm2.sock")
+    FakeBroker(sock2, granules=4, stream=[(0.1, 3)], hangup=True)    # 1 granule, then gone
+    name = ledger()
+    try:
+        out, r = run(stub, native_shim, ["alloc", 512 * MIB, "alloc", 2 * GIB, "arena", "stats", "arenastream"],
+                     GPUSHARE_QUOTA_BYTES=8 * GIB, GPUSHARE_LEDGER=name, GPUSHARE_HBM_BROKER=sock2,
+                     GPUSHARE_HBM_TOKEN="short", GPUSHARE_HBM_MORE_WAIT_S="5")
+        assert r.returncode == 0, r.stderr
+        small, big, arena, st, s = out
+        assert small["err"] == 0 and big["err"] == 2                 # the rest never came: out of memory
+        assert arena["size"] == GIB and st["used"] == GIB            # grant and ledger shrank to 1 granule
+        assert s["granted"] == s["mapped"] == 1
+    finally:
+        cleanup(name)
+
+
 def test_broker_refusal_leaves_the_pod_on_the_driver(stub, native_shim, tmp_path):
     sock = str(tmp_path / "hbm.sock")
     b = FakeBroker(sock, refuse=True)
@@ -534,7 +614,7 @@ def test_broker_refusal_leaves_the_pod_on_the_driver(stub, native_shim, tmp_path
         out, r = run(stub, native_shim, ["alloc", GIB, "arena", "stats"], GPUSHARE_QUOTA_BYTES=4 * GIB,
                      GPUSHARE_LEDGER=name, GPUSHARE_HBM_BROKER=sock, GPUSHARE_HBM_TOKEN="nope")
         assert r.returncode == 0, r.stderr
-        assert b.took == "TAKE nope"
+        assert b.took == "TAKE nope STREAM"
         assert out[0]["err"] == 0 and out[1]["on"] == 0 and out[2]["used"] == GIB   # quota shim as before
     finally:
         cleanup(name)
@@ -566,7 +646,7 @@ def test_broker_arena_under_sanitizers(stub, tmp_path, san):
         out = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
         assert out[0]["ok"] == 8 * 300 and out[0]["denied"] == 0
         assert out[1] == {"op": "arena", "on": 1, "size": 2 * GIB, "used": 0}
-        assert out[2]["r"] == 1 and b.took == "TAKE t"
+        assert out[2]["r"] == 1 and b.took == "TAKE t STREAM"
     finally:
         cleanup(name)
 
@@ -618,12 +698,15 @@ def test_broker_arena_serves_stream_ordered_allocations(stub, native_shim, tmp_p
         cleanup(name)
 
 
-def test_broker_arena_serves_vmm_pages(stub, native_shim, tmp_path):
+@pytest.mark.parametrize("align_cap", [None, 2 * MIB])
+def test_broker_arena_serves_vmm_pages(stub, native_shim, tmp_path, align_cap):
     """VMM the way PyTorch's expandable segments use it (a large reserved
     range, 20 MiB pages created and mapped one after another) is served from the arena: the
     range is aligned to the granule, its slots are backed by arena granules on demand (a page may
     straddle two), unmapping a slot's last page gives its granule back, and past the arena the
-    pages come from the driver, charged, until the quota is out."""
+    pages come from the driver, charged, until the quota is out. ``align_cap``: the runtime
+    returns ranges aligned to 2 MiB only, whatever alignment is asked for (HIP 7.x on MI355X):
+    the shim reserves a granule more and uses the aligned part."""
     sock = str(tmp_path / "hbm.sock")
     FakeBroker(sock, granules=4)
     name = ledger()
@@ -632,8 +715,9 @@ def test_broker_arena_serves_vmm_pages(stub, native_shim, tmp_path):
     try:
         args = ["alloc", MIB, "vres", 9 * GIB] + ["vpage", page] * n1 + ["vstats", "arena", "stats"]
         args += sum((["vdrop", k] for k in range(n1)), []) + ["vstats", "arena"]
+        extra = {"FAKE_HIP_RESERVE_ALIGN_MAX": str(align_cap)} if align_cap else {}
         out, r = run(stub, native_shim, args, GPUSHARE_QUOTA_BYTES=8 * GIB, GPUSHARE_LEDGER=name,
-                     GPUSHARE_HBM_BROKER=sock, GPUSHARE_HBM_TOKEN="tok")
+                     GPUSHARE_HBM_BROKER=sock, GPUSHARE_HBM_TOKEN="tok", **extra)
         assert r.returncode == 0, r.stderr
         vres = out[1]
         assert vres == {"op": "vres", "err": 0, "aligned": 1}
