@@ -4,14 +4,20 @@ Layer map (re-designed for MI355X):
   L0 device/smi.py       -> native/gpuinfo (C++: librocm_smi64 + amdgpu/KFD sysfs)
   L1 device/model.py     physical GPU -> fake memory-unit devices
   L2 cluster/            apiserver client, node status, pod watch cache, kubelet client
-  L3 plugin/server.py    kubelet v1beta1 DevicePlugin gRPC server; alloc/ Allocate engine
+  L3 plugin/native_server.py -> native/dpserver (C++ HTTP/2 + gRPC: the kubelet v1beta1
+                         DevicePlugin service, Allocate answered from the engine's prepared
+                         table); plugin/server.py (grpcio alternative); alloc/ Allocate engine
   L4 plugin/manager.py   lifecycle (inotify, signals, restart), device/health.py
   L5 cli/main.py         flags / entry point
   L6 cli/inspect.py      kubectl-inspect-gpushare; cli/podgetter.py
-  quota/ + native/hipshim  per-container HBM quota (LD_PRELOAD HIP interposer)
+  quota/ + native/hipshim    per-container HBM quota (LD_PRELOAD shim at the KFD boundary),
+                             watchdog, dmem limits
+  quota/hbmbroker.py + native/hbmbroker   per-GPU HBM broker (VMM granules lent to pods) and
+                             the plugin's granter
+  extender/ + cli/extender.py  gpushare-scheduler-extender (filter / bind, HA leader election)
   ops/ + models/           HIP/CDNA4 kernels and the PyTorch-ROCm demo workloads
   parallel/                xGMI topology export, TP-group placement, RCCL demo
-  sim/                     fake apiserver / kubelet / extender for CPU-only end-to-end runs
+  sim/                     fake apiserver / kubelet and the multi-node harness for CPU-only runs
 """
 import os as _os
 

@@ -1882,9 +1882,14 @@ hipError_t vmm_map(Win& w, VHandle* v, char* va) {
         e = map ? map(pc.va, pc.len, 0, pc.h, 0) : hipErrorNotInitialized;
         if (e != hipSuccess) hipMemRelease(pc.h);
       }
-      if (e != hipSuccess) return e;  // the caller undoes the pieces mapped so far
+      if (e != hipSuccess) {
+        logf(1, "vmm: driver piece of %llu bytes at slot %d + %llu: error %d", (unsigned long long)pc.len, s,
+             (unsigned long long)(plo - uint64_t(s) * kWinAlign), int(e));
+        return e;  // the caller undoes the pieces mapped so far
+      }
       ++w.slot_real[s];
       ++g_vmm_real_pieces;
+      logf(2, "vmm: driver piece of %llu bytes mapped at +%llu", (unsigned long long)pc.len, (unsigned long long)plo);
     }
     ++v->npieces;
   }
@@ -2423,19 +2428,26 @@ GS_EXPORT hipError_t hipMemSetAccess(void* ptr, size_t size, const hipMemAccessD
   char* run = nullptr;  // start of the current run of driver memory
   hipError_t e = hipSuccess;
   Depth d;
+  auto set = [&](char* at, size_t n) {
+    hipError_t r = f(at, n, desc, count);
+    logf(2, "vmm: access +%llu, %zu bytes: %d", (unsigned long long)(at - w->base), n, int(r));
+    return r;
+  };
   for (char* p = lo; p < hi && e == hipSuccess;) {
     int s = int(uint64_t(p - w->base) / kWinAlign);
     char* send = w->base + uint64_t(s + 1) * kWinAlign;
     char* q = send < hi ? send : hi;
     if (w->slot_g[s] >= 0) {
-      if (run) e = f(run, size_t(p - run), desc, count), run = nullptr;
-      if (e == hipSuccess && !local_rw) e = f(w->base + uint64_t(s) * kWinAlign, kWinAlign, desc, count);
+      if (run) e = set(run, size_t(p - run)), run = nullptr;
+      if (e == hipSuccess && !local_rw) e = set(w->base + uint64_t(s) * kWinAlign, kWinAlign);
     } else if (!run) {
       run = p;
     }
     p = q;
   }
-  if (run && e == hipSuccess) e = f(run, size_t(hi - run), desc, count);
+  if (run && e == hipSuccess) e = set(run, size_t(hi - run));
+  if (e != hipSuccess)
+    logf(1, "vmm: access for window +%llu, %zu bytes: error %d", (unsigned long long)(lo - w->base), size, int(e));
   pthread_mutex_unlock(&g_arena.mu);
   return e;
 }

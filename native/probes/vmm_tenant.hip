@@ -88,7 +88,8 @@ int main(int argc, char** argv) {
   acc.flags = hipMemAccessFlagsProtReadWrite;
   std::vector<Page> pages;
   size_t want = size_t(double(total) * fill) / page;
-  int create_err = 0, map_err = 0;
+  int create_err = 0, map_err = 0, access_err = 0;
+  long fail_page = -1;
   for (size_t k = 0; k < want; ++k) {
     Page pg{static_cast<char*>(base) + k * page, nullptr};
     hipError_t e = hipMemCreate(&pg.h, page, &p, 0);
@@ -97,9 +98,14 @@ int main(int argc, char** argv) {
       break;
     }
     e = hipMemMap(pg.va, page, 0, pg.h, 0);
-    if (e == hipSuccess) e = hipMemSetAccess(pg.va, page, &acc, 1);
     if (e != hipSuccess) {
       map_err = e;
+    } else if ((e = hipMemSetAccess(pg.va, page, &acc, 1)) != hipSuccess) {
+      access_err = e;
+      (void)hipMemUnmap(pg.va, page);
+    }
+    if (e != hipSuccess) {
+      fail_page = long(k);
       (void)hipMemRelease(pg.h);
       break;
     }
@@ -123,8 +129,10 @@ int main(int argc, char** argv) {
   char st[1024];
   stats(st, sizeof st);
   std::printf("{\"phase\": \"filled\", \"total\": %zu, \"page\": %zu, \"pages\": %zu, \"want\": %zu, \"bytes\": %zu, "
-              "\"create_err\": %d, \"map_err\": %d, \"holes\": %zu, \"ok_fill\": %s, \"ok_refill\": %s, %s}\n",
-              total, page, pages.size(), want, pages.size() * page, create_err, map_err, holes, ok1 ? "true" : "false",
+              "\"create_err\": %d, \"map_err\": %d, \"access_err\": %d, \"fail_page\": %ld, \"base_mod_gib\": %zu, "
+              "\"holes\": %zu, \"ok_fill\": %s, \"ok_refill\": %s, %s}\n",
+              total, page, pages.size(), want, pages.size() * page, create_err, map_err, access_err, fail_page,
+              size_t(reinterpret_cast<uintptr_t>(base) % (1ull << 30)), holes, ok1 ? "true" : "false",
               ok2 ? "true" : "false", st);
   std::fflush(stdout);
   for (auto& pg : pages)

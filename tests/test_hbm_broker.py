@@ -127,7 +127,7 @@ def test_a_pod_waits_for_granules_a_retiring_pod_holds(broker, stream):
     if stream == "0":
         assert st["waiting"] == 1 and st["owed"] == 0
     else:
-        assert st["waiting"] == 0 and st["owed"] == 4 and st["held"] == 6 + 2 and st["streamed"] == 1
+        assert st["waiting"] == 0 and st["owed"] == 4 and st["held"] == 6 + 2 and st["streamed"] == 2
     holder.stdin.write("\n")
     holder.stdin.flush()
     holder.wait(60)
@@ -376,7 +376,8 @@ def test_vmm_pages_come_from_the_arena(tmp_path, fill):
                    GPUSHARE_HBM_BROKER=b.socket_path, GPUSHARE_HBM_TOKEN="v" * 32)
         r = subprocess.run([exe, str(fill)], env=env, capture_output=True, text=True, timeout=120)
         lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
-        print(json.dumps({"fill": fill, "lines": lines, "stderr": r.stderr[-1500:]}))
+        vmm_log = [x for x in r.stderr.splitlines() if "vmm:" in x or "error" in x.lower()]
+        print(json.dumps({"fill": fill, "lines": lines, "vmm_log": vmm_log[-40:], "stderr": r.stderr[-1500:]}))
         assert r.returncode == 0 and len(lines) == 2, r.stderr[-3000:]
         filled, released = lines
         assert filled["pages"] == filled["want"] and filled["create_err"] == 0 and filled["map_err"] == 0
