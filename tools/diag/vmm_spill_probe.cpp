@@ -11,6 +11,13 @@
 //              then driver pieces at +1 GiB as in "split"
 //   overres    like "imported", in a range reserved 1 GiB larger and used from its 1 GiB-aligned part
 //   both_rw    like "imported", with access set again on the whole slot 0 before the pieces
+//   offset12   20 MiB pages from +12 MiB, nothing mapped before them
+//
+// When an access fails the probe tries, in order, and counts which one worked: the same call
+// again ("retry"), after hipDeviceSynchronize ("sync"), and one call over everything mapped
+// since the start of the case ("span"); then it checks the page reads back what was written.
+// (Round 5, first run: plain and overres_plain pass; split, imported and overres fail the first
+// page after a 12 MiB piece; both_rw fails the piece and passes the pages.)
 //
 //   g++ -std=c++17 -O1 -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -o tools/diag/build/vmm_spill_probe \
 //       tools/diag/vmm_spill_probe.cpp -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib
@@ -51,7 +58,8 @@ struct Case {
   std::vector<std::pair<char*, size_t>> maps;
   void* res = nullptr;
   size_t res_size = 0;
-  int fd = -1;
+  char* first = nullptr;  // start of what the case mapped
+  int fails = 0, retry_ok = 0, sync_ok = 0, span_ok = 0, readback_bad = 0;
 
   void rec(const char* k, long v) {
     char b[96];
@@ -67,7 +75,25 @@ struct Case {
     hs.push_back(h);
     if ((e = hipMemMap(va, n, 0, h, 0)) != hipSuccess) return 200 + e;
     maps.push_back({va, n});
-    if ((e = rw(va, n)) != hipSuccess) return 300 + e;
+    if (!first) first = va;
+    if ((e = rw(va, n)) != hipSuccess) {
+      ++fails;
+      (void)hipGetLastError();
+      if (rw(va, n) == hipSuccess) {
+        ++retry_ok;
+      } else if ((void)hipDeviceSynchronize(), (void)hipGetLastError(), rw(va, n) == hipSuccess) {
+        ++sync_ok;
+      } else if ((void)hipGetLastError(), rw(first, size_t(va + n - first)) == hipSuccess) {
+        ++span_ok;
+      } else {
+        (void)hipGetLastError();
+        return 300 + e;
+      }
+    }
+    if (hipMemset(va, 0x3c, n) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return 400;
+    unsigned char b[64];
+    if (hipMemcpy(b, va + n - sizeof b, sizeof b, hipMemcpyDeviceToHost) != hipSuccess) return 500;
+    for (unsigned char x : b) readback_bad += x != 0x3c;
     return 0;
   }
   void cleanup() {
@@ -78,7 +104,7 @@ struct Case {
   }
 };
 
-std::string run(const char* name, bool split, bool imported, bool overres, bool both_rw) {
+std::string run(const char* name, bool split, bool imported, bool overres, bool both_rw, size_t start_off = 0) {
   Case c;
   c.name = name;
   size_t want = 4 * kGiB;
@@ -87,7 +113,7 @@ std::string run(const char* name, bool split, bool imported, bool overres, bool 
   char* base = static_cast<char*>(c.res);
   c.rec("reserve_mod_gib_mib", long((reinterpret_cast<uintptr_t>(base) % kGiB) / kMiB));
   if (overres) base = reinterpret_cast<char*>((reinterpret_cast<uintptr_t>(base) + kGiB - 1) & ~uintptr_t(kGiB - 1));
-  char* at = base;
+  char* at = base + start_off;
   if (imported) {
     auto p = prop(true);
     hipMemGenericAllocationHandle_t h = nullptr, hi = nullptr;
@@ -106,6 +132,7 @@ std::string run(const char* name, bool split, bool imported, bool overres, bool 
     c.rec("map_slot0", hipMemMap(base, kGiB, 0, hi, 0));
     c.maps.push_back({base, kGiB});
     c.rec("access_slot0", rw(base, kGiB));
+    c.first = base;
     if (both_rw) c.rec("access_slot0_again", rw(base, kGiB));
     at = base + kGiB;
   }
@@ -124,6 +151,11 @@ std::string run(const char* name, bool split, bool imported, bool overres, bool 
   }
   c.rec("pages_failed_at", failed_at);
   c.rec("pages_err", err);
+  c.rec("access_fails", c.fails);
+  c.rec("retry_ok", c.retry_ok);
+  c.rec("sync_ok", c.sync_ok);
+  c.rec("span_ok", c.span_ok);
+  c.rec("readback_bad", c.readback_bad);
   c.cleanup();
   return "\"" + c.name + "\": {" + c.out + "}";
 }
@@ -140,6 +172,8 @@ int main() {
   o += ", " + run("overres", true, true, true, false);
   o += ", " + run("both_rw", true, true, false, true);
   o += ", " + run("overres_plain", false, false, true, false);
+  o += ", " + run("offset12", false, false, false, false, 12 * kMiB);
+  o += ", " + run("split_again", true, false, false, false);
   std::puts((o + "}").c_str());
   return 0;
 }
