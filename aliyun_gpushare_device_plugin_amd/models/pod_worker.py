@@ -70,12 +70,14 @@ def _arena_stream() -> dict | None:
         f = ctypes.CDLL(None).gpushare_shim_arena_stream
     except AttributeError:
         return None
-    f.argtypes = [ctypes.POINTER(ctypes.c_uint64)] * 6
-    v = [ctypes.c_uint64() for _ in range(6)]
+    f.argtypes = [ctypes.POINTER(ctypes.c_uint64)] * 9
+    v = [ctypes.c_uint64() for _ in range(9)]
     if not f(*(ctypes.byref(x) for x in v)):
         return None
     return {"waits": v[0].value, "wait_ms": round(v[1].value / 1e6, 3), "msgs": v[2].value,
-            "map_ms": round(v[3].value / 1e6, 3), "mapped": v[4].value, "granted": v[5].value}
+            "map_ms": round(v[3].value / 1e6, 3), "mapped": v[4].value, "granted": v[5].value,
+            "first": v[6].value, "first_reserve_ms": round(v[7].value / 1e6, 3),
+            "first_access_ms": round(v[8].value / 1e6, 3)}
 
 
 def _arena_release():

@@ -1128,6 +1128,7 @@ int g_dev = 0;  // the arena's device (HIP ordinal in this process)
 // waited for owed granules, importing and mapping those, and MORE messages received
 uint64_t g_take_connect_ns = 0, g_take_wait_ns = 0, g_take_map_ns = 0;
 uint64_t g_more_wait_ns = 0, g_more_map_ns = 0, g_more_msgs = 0, g_more_waits = 0;
+uint64_t g_take_first = 0, g_take_reserve_ns = 0, g_take_access_ns = 0;  // the TAKE's first batch
 
 uint64_t mono_ns() {
   timespec t;
@@ -1345,7 +1346,10 @@ void arena_take() {
     logf(1, "hbm broker: runtime %d: fds imported by %s", rtv, by_address ? "address" : "value");
     void* base = nullptr;
     uint64_t vsize = total * gran;
+    uint64_t t_r = mono_ns();
     if (reserve_f(&base, vsize, 0, nullptr, 0) != hipSuccess) goto fail;
+    g_take_reserve_ns = mono_ns() - t_r;
+    g_take_first = uint64_t(got);
     logf(2, "hbm broker: reserved %p + %llu", base, (unsigned long long)vsize);
     // import + map the granules; GPUSHARE_HBM_MAP_THREADS (default 1) threads share the work
     int nt = int(env_u64("GPUSHARE_HBM_MAP_THREADS", 1));
@@ -1361,7 +1365,9 @@ void arena_take() {
       goto fail;  // the process keeps what it mapped until exit; the broker reclaims at close
     }
     logf(2, "hbm broker: %d granules imported and mapped by %d threads", got, nt);
+    uint64_t t_a = mono_ns();
     if (got && !set_rw(static_cast<char*>(base), uint64_t(got) * gran, dev)) goto fail;
+    g_take_access_ns = mono_ns() - t_a;
     a.base = static_cast<char*>(base);
     a.size = a.vsize = vsize;
     a.gran = gran;
@@ -1986,9 +1992,11 @@ GS_EXPORT int gpushare_shim_arena_timing(uint64_t* connect_ns, uint64_t* wait_ns
 }
 
 // a streaming TAKE after it returned: allocations that waited for owed granules (count, ns), the
-// MORE batches received and the ns spent importing + mapping them, granules mapped and granted
+// MORE batches received and the ns spent importing + mapping them, granules mapped and granted;
+// of the TAKE's first batch: its granules, and the ns of its address reservation and access
 GS_EXPORT int gpushare_shim_arena_stream(uint64_t* waits, uint64_t* wait_ns, uint64_t* msgs, uint64_t* map_ns,
-                                         uint64_t* mapped, uint64_t* granted) {
+                                         uint64_t* mapped, uint64_t* granted, uint64_t* first, uint64_t* reserve_ns,
+                                         uint64_t* access_ns) {
   Arena& a = g_arena;
   pthread_mutex_lock(&a.mu);
   int on = a.state == 1;
@@ -1998,6 +2006,9 @@ GS_EXPORT int gpushare_shim_arena_stream(uint64_t* waits, uint64_t* wait_ns, uin
   if (map_ns) *map_ns = g_more_map_ns;
   if (mapped) *mapped = on ? uint64_t(a.n) : 0;
   if (granted) *granted = on ? uint64_t(a.total) : 0;
+  if (first) *first = g_take_first;
+  if (reserve_ns) *reserve_ns = g_take_reserve_ns;
+  if (access_ns) *access_ns = g_take_access_ns;
   pthread_mutex_unlock(&a.mu);
   return on;
 }

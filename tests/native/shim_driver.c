@@ -75,11 +75,13 @@ int main(int argc, char** argv) {
       uint64_t sz = 0, used = 0; int on = f ? f(&sz, &used) : -2;
       printf("{\"op\":\"arena\",\"on\":%d,\"size\":%llu,\"used\":%llu}\n", on, (unsigned long long)sz, (unsigned long long)used); }
     else if (!strcmp(argv[i], "arenastream")) {
-      int (*f)(uint64_t*, uint64_t*, uint64_t*, uint64_t*, uint64_t*, uint64_t*) =
-          (int (*)(uint64_t*, uint64_t*, uint64_t*, uint64_t*, uint64_t*, uint64_t*))dlsym(RTLD_DEFAULT, "gpushare_shim_arena_stream");
-      uint64_t w = 0, wn = 0, m = 0, mn = 0, mp = 0, gr = 0; int on = f ? f(&w, &wn, &m, &mn, &mp, &gr) : -2;
-      printf("{\"op\":\"arenastream\",\"on\":%d,\"waits\":%llu,\"wait_ms\":%.1f,\"msgs\":%llu,\"mapped\":%llu,\"granted\":%llu}\n",
-             on, (unsigned long long)w, wn / 1e6, (unsigned long long)m, (unsigned long long)mp, (unsigned long long)gr); }
+      typedef uint64_t* P;
+      int (*f)(P, P, P, P, P, P, P, P, P) = (int (*)(P, P, P, P, P, P, P, P, P))dlsym(RTLD_DEFAULT, "gpushare_shim_arena_stream");
+      uint64_t w = 0, wn = 0, m = 0, mn = 0, mp = 0, gr = 0, fi = 0, rn = 0, an = 0;
+      int on = f ? f(&w, &wn, &m, &mn, &mp, &gr, &fi, &rn, &an) : -2;
+      printf("{\"op\":\"arenastream\",\"on\":%d,\"waits\":%llu,\"wait_ms\":%.1f,\"msgs\":%llu,\"mapped\":%llu,\"granted\":%llu,\"first\":%llu}\n",
+             on, (unsigned long long)w, wn / 1e6, (unsigned long long)m, (unsigned long long)mp, (unsigned long long)gr,
+             (unsigned long long)fi); }
     else if (!strcmp(argv[i], "arenarelease")) { int (*f)(void) = (int (*)(void))dlsym(RTLD_DEFAULT, "gpushare_shim_arena_release");
       printf("{\"op\":\"arenarelease\",\"r\":%d}\n", f ? f() : -2); fflush(stdout); }
     else if (!strcmp(argv[i], "sleepms")) { fflush(stdout); usleep((useconds_t)atoi(argv[++i]) * 1000); }
