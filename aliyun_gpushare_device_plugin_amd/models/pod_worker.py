@@ -74,10 +74,20 @@ def _arena_stream() -> dict | None:
     v = [ctypes.c_uint64() for _ in range(9)]
     if not f(*(ctypes.byref(x) for x in v)):
         return None
-    return {"waits": v[0].value, "wait_ms": round(v[1].value / 1e6, 3), "msgs": v[2].value,
-            "map_ms": round(v[3].value / 1e6, 3), "mapped": v[4].value, "granted": v[5].value,
-            "first": v[6].value, "first_reserve_ms": round(v[7].value / 1e6, 3),
-            "first_access_ms": round(v[8].value / 1e6, 3)}
+    out = {"waits": v[0].value, "wait_ms": round(v[1].value / 1e6, 3), "msgs": v[2].value,
+           "map_ms": round(v[3].value / 1e6, 3), "mapped": v[4].value, "granted": v[5].value,
+           "first": v[6].value, "first_reserve_ms": round(v[7].value / 1e6, 3),
+           "first_access_ms": round(v[8].value / 1e6, 3)}
+    try:
+        g = ctypes.CDLL(None).gpushare_shim_arena_first
+        g.argtypes = [ctypes.POINTER(ctypes.c_uint64)] * 2
+        w = [ctypes.c_uint64() for _ in range(2)]
+        if g(*(ctypes.byref(x) for x in w)):
+            out["first_import_ms"] = round(w[0].value / 1e6, 3)
+            out["first_map_ms"] = round(w[1].value / 1e6, 3)
+    except AttributeError:
+        pass
+    return out
 
 
 def _arena_release():

@@ -93,8 +93,6 @@ __asm__(".symver dlopen,dlopen@GLIBC_2.2.5");
 __asm__(".symver shm_open,shm_open@GLIBC_2.2.5");
 __asm__(".symver pthread_once,pthread_once@GLIBC_2.2.5");
 __asm__(".symver memcpy,memcpy@GLIBC_2.2.5");
-__asm__(".symver pthread_create,pthread_create@GLIBC_2.2.5");
-__asm__(".symver pthread_join,pthread_join@GLIBC_2.2.5");
 
 #undef hipGetDeviceProperties
 
@@ -1079,6 +1077,7 @@ REAL(hipError_t, hipMemSetAccess, void*, size_t, const hipMemAccessDesc*, size_t
 REAL(hipError_t, hipGetDevice, int*)
 REAL(hipError_t, hipDeviceSynchronize)
 REAL(hipError_t, hipRuntimeGetVersion, int*)
+REAL(hipError_t, hipGetLastError)
 REAL(hipError_t, hipEventCreateWithFlags, hipEvent_t*, unsigned)
 REAL(hipError_t, hipEventRecord, hipEvent_t, hipStream_t)
 REAL(hipError_t, hipEventQuery, hipEvent_t)
@@ -1113,7 +1112,6 @@ struct Arena {
   uint64_t size = 0, vsize = 0, gran = 0, used = 0;
   int n = 0, total = 0;
   bool by_address = false;  // how this runtime imports a POSIX fd (see arena_take)
-  int map_threads = 1;
   hipMemGenericAllocationHandle_t h[kArenaMaxGranules];
   Ext* ext = nullptr;
   int next = 0;
@@ -1129,6 +1127,7 @@ int g_dev = 0;  // the arena's device (HIP ordinal in this process)
 uint64_t g_take_connect_ns = 0, g_take_wait_ns = 0, g_take_map_ns = 0;
 uint64_t g_more_wait_ns = 0, g_more_map_ns = 0, g_more_msgs = 0, g_more_waits = 0;
 uint64_t g_take_first = 0, g_take_reserve_ns = 0, g_take_access_ns = 0;  // the TAKE's first batch
+uint64_t g_first_import_ns = 0, g_first_map_ns = 0;  // the process's first granule
 
 uint64_t mono_ns() {
   timespec t;
@@ -1182,56 +1181,34 @@ bool recv_fd_batch(int s, int* out, int* got, int want) {
   return true;
 }
 
-// one TAKE's import + map, shared by threads (granule i: its fd's handle, mapped at base + i * gran)
-struct ImportJob {
-  hipMemImportFromShareableHandle_t import_f;
-  hipMemMap_t map_f;
-  int* fds;
-  hipMemGenericAllocationHandle_t* h;
-  char* base;
-  uint64_t gran;
-  bool by_address;
-  std::atomic<int> next;
-  std::atomic<int> failed;  // granule + 1 of the first failure, 0 none
-  int n;
-};
-
-void* import_worker(void* p) {
-  ImportJob* j = static_cast<ImportJob*>(p);
-  Depth d;
-  for (;;) {
-    int i = j->next.fetch_add(1);
-    if (i >= j->n || j->failed.load(std::memory_order_relaxed)) break;
-    hipMemGenericAllocationHandle_t h = nullptr;
-    hipError_t ie = j->by_address
-                        ? j->import_f(&h, &j->fds[i], hipMemHandleTypePosixFileDescriptor)
-                        : j->import_f(&h, reinterpret_cast<void*>(static_cast<intptr_t>(j->fds[i])),
-                                      hipMemHandleTypePosixFileDescriptor);
-    if (ie == hipSuccess) j->h[i] = h;
-    if (ie != hipSuccess || j->map_f(j->base + uint64_t(i) * j->gran, j->gran, 0, h, 0) != hipSuccess) {
-      int none = 0;
-      j->failed.compare_exchange_strong(none, i + 1);
-      break;
-    }
-  }
-  return nullptr;
-}
-
-// import fds[0..k) and map granule i at base + i * gran, by `nt` threads; h[i] set for each one
-// imported (nullptr otherwise). Returns 0, or the first failed granule + 1
-int import_and_map(int* fds, int k, hipMemGenericAllocationHandle_t* h, char* base, uint64_t gran, bool by_address,
-                   int nt) {
-  ImportJob job{real_hipMemImportFromShareableHandle(), real_hipMemMap(), fds, h, base, gran, by_address, {0}, {0}, k};
+// import fds[0..k) and map granule i at base + i * gran; h[i] set for each one imported (nullptr
+// otherwise). Returns 0, or the failed granule + 1. One thread: HIP 7.x's hipMemMap into one
+// reservation from several threads at once failed (round 5, bench with 4 mapping threads: an
+// allocation in the pod then saw hipErrorInvalidValue)
+int import_and_map(int* fds, int k, hipMemGenericAllocationHandle_t* h, char* base, uint64_t gran, bool by_address) {
+  auto import_f = real_hipMemImportFromShareableHandle();
+  auto map_f = real_hipMemMap();
   for (int i = 0; i < k; ++i) h[i] = nullptr;
-  if (!job.import_f || !job.map_f) return k > 0 ? 1 : 0;
-  nt = nt < 1 ? 1 : nt > 16 ? 16 : nt > k ? k : nt;
-  pthread_t th[16];
-  int started = 0;
-  for (int t = 1; t < nt; ++t)
-    if (pthread_create(&th[started], nullptr, import_worker, &job) == 0) ++started;
-  import_worker(&job);
-  for (int t = 0; t < started; ++t) pthread_join(th[t], nullptr);
-  return job.failed.load();
+  if (!import_f || !map_f) return k > 0 ? 1 : 0;
+  Depth d;
+  for (int i = 0; i < k; ++i) {
+    uint64_t t0 = mono_ns();
+    hipError_t e = by_address ? import_f(&h[i], &fds[i], hipMemHandleTypePosixFileDescriptor)
+                              : import_f(&h[i], reinterpret_cast<void*>(static_cast<intptr_t>(fds[i])),
+                                         hipMemHandleTypePosixFileDescriptor);
+    uint64_t t1 = mono_ns();
+    if (e != hipSuccess) {
+      h[i] = nullptr;
+      return i + 1;
+    }
+    e = map_f(base + uint64_t(i) * gran, gran, 0, h[i], 0);
+    if (!g_first_import_ns) {  // the process's first import and map (the runtime's one-time work)
+      g_first_import_ns = t1 - t0;
+      g_first_map_ns = mono_ns() - t1;
+    }
+    if (e != hipSuccess) return i + 1;
+  }
+  return 0;
 }
 
 // read-write for device `dev`
@@ -1251,8 +1228,16 @@ void arena_unmap_locked() {
   Depth d;
   if (auto dev_sync = real_hipDeviceSynchronize()) (void)dev_sync();
   if (a.base) {
-    if (auto un = real_hipMemUnmap())
-      if (a.n) (void)un(a.base, uint64_t(a.n) * a.gran);
+    // one unmap per mapping: HIP unmaps one handle's mapping per call. Unmapping the whole range
+    // at once failed, and the imported handles then stayed mapped, keeping the broker's granules
+    // referenced until this process was torn down (tools/diag/dmabuf_ref_probe.cpp: with a
+    // per-mapping unmap and the release the references go at once)
+    if (auto un = real_hipMemUnmap()) {
+      int bad = 0;
+      for (int i = 0; i < a.n; ++i)
+        bad += un(a.base + uint64_t(i) * a.gran, a.gran) != hipSuccess;
+      if (bad) logf(1, "hbm broker: %d of %d granule unmaps failed", bad, a.n);
+    }
     if (auto fr = real_hipMemAddressFree()) (void)fr(a.base, a.vsize);
   }
   if (auto rel = real_hipMemRelease())
@@ -1351,9 +1336,7 @@ void arena_take() {
     g_take_reserve_ns = mono_ns() - t_r;
     g_take_first = uint64_t(got);
     logf(2, "hbm broker: reserved %p + %llu", base, (unsigned long long)vsize);
-    // import + map the granules; GPUSHARE_HBM_MAP_THREADS (default 1) threads share the work
-    int nt = int(env_u64("GPUSHARE_HBM_MAP_THREADS", 1));
-    int failed = import_and_map(fds, got, a.h, static_cast<char*>(base), gran, by_address, nt);
+    int failed = import_and_map(fds, got, a.h, static_cast<char*>(base), gran, by_address);
     a.n = got;  // (released at a failure: the ones imported)
     for (int i = 0; i < got; ++i)
       if (a.h[i]) {
@@ -1364,7 +1347,7 @@ void arena_take() {
       logf(1, "hbm broker: import/map of granule %d failed", failed - 1);
       goto fail;  // the process keeps what it mapped until exit; the broker reclaims at close
     }
-    logf(2, "hbm broker: %d granules imported and mapped by %d threads", got, nt);
+    logf(2, "hbm broker: %d granules imported and mapped", got);
     uint64_t t_a = mono_ns();
     if (got && !set_rw(static_cast<char*>(base), uint64_t(got) * gran, dev)) goto fail;
     g_take_access_ns = mono_ns() - t_a;
@@ -1373,7 +1356,6 @@ void arena_take() {
     a.gran = gran;
     a.total = int(total);
     a.by_address = by_address;
-    a.map_threads = nt;
     g_dev = dev;
   }
   // the arena counts against the pod's quota like any other HBM it holds: what the runtime
@@ -1567,7 +1549,7 @@ bool arena_more_locked(int wait_ms) {
     }
   Depth d;
   char* at = a.base + uint64_t(a.n) * a.gran;
-  int failed = import_and_map(fds, got, a.h + a.n, at, a.gran, a.by_address, a.map_threads);
+  int failed = import_and_map(fds, got, a.h + a.n, at, a.gran, a.by_address);
   for (int i = 0; i < got; ++i) close(fds[i]);
   if (failed || !set_rw(at, uint64_t(got) * a.gran, g_dev)) {
     // keep none of this batch: what was mapped goes, the handles are released
@@ -1727,7 +1709,7 @@ constexpr uint64_t kVCap = 1 << 17;
 uintptr_t* g_vh = nullptr;   // VHandle* set
 uintptr_t* g_vva = nullptr;  // VA -> VHandle* (pairs)
 uint64_t g_vh_n = 0, g_vva_n = 0, g_pending_bytes = 0;
-uint64_t g_vmm_arena_maps = 0, g_vmm_real_pieces = 0, g_vmm_creates = 0, g_slots_backed = 0;
+uint64_t g_vmm_arena_maps = 0, g_vmm_real_pieces = 0, g_vmm_creates = 0, g_slots_backed = 0, g_vmm_span_access = 0;
 
 bool vtables() {
   if (!g_vh) g_vh = static_cast<uintptr_t*>(calloc(kVCap, sizeof(uintptr_t)));
@@ -1789,6 +1771,60 @@ VHandle* vva_take(char* va) {
     }
   }
 }
+
+// where the run of mappings that ends at `at` without a hole begins, in window `w`: whole arena
+// slots and the driver pieces mapped in the other slots (g_arena.mu held)
+struct Span {
+  char* va;
+  uint64_t len;
+};
+int span_cmp(const void* x, const void* y) {
+  const char* a = static_cast<const Span*>(x)->va;
+  const char* b = static_cast<const Span*>(y)->va;
+  return a < b ? -1 : a > b;
+}
+char* mapped_run_start(Win& w, char* at) {
+  uint64_t cap = 256, n = 0;
+  Span* v = static_cast<Span*>(malloc(cap * sizeof(Span)));
+  for (uint64_t i = 0; v && g_vva && i < kVCap; ++i) {
+    uintptr_t k = g_vva[2 * i];
+    if (!k || k == kTomb) continue;
+    VHandle* h = reinterpret_cast<VHandle*>(g_vva[2 * i + 1]);
+    for (int j = 0; j < h->npieces; ++j) {
+      VPiece& pc = h->pieces[j];
+      if (!pc.h || pc.va < w.base || pc.va >= w.base + w.size) continue;
+      if (n == cap) {
+        Span* g = static_cast<Span*>(realloc(v, 2 * cap * sizeof(Span)));
+        if (!g) break;
+        v = g;
+        cap *= 2;
+      }
+      v[n++] = {pc.va, pc.len};
+    }
+  }
+  if (v) qsort(v, n, sizeof(Span), span_cmp);
+  char* cur = at;
+  while (v && cur > w.base) {
+    int s = int(uint64_t(cur - 1 - w.base) / kWinAlign);
+    char* st = w.base + uint64_t(s) * kWinAlign;
+    if (w.slot_g[s] >= 0) {  // an arena slot: one mapping of its whole granule
+      if (cur != st + kWinAlign) break;
+      cur = st;
+      continue;
+    }
+    uint64_t lo = 0, hi = n;  // the last driver piece starting below cur
+    while (lo < hi) {
+      uint64_t mid = (lo + hi) / 2;
+      if (v[mid].va < cur) lo = mid + 1;
+      else hi = mid;
+    }
+    if (lo == 0 || v[lo - 1].va + v[lo - 1].len != cur) break;
+    cur = v[lo - 1].va;
+  }
+  free(v);
+  return cur;
+}
+
 
 Win* win_of(const char* p, uint64_t len) {
   for (int i = 0; i < g_nwin; ++i)
@@ -2011,6 +2047,13 @@ GS_EXPORT int gpushare_shim_arena_stream(uint64_t* waits, uint64_t* wait_ns, uin
   if (access_ns) *access_ns = g_take_access_ns;
   pthread_mutex_unlock(&a.mu);
   return on;
+}
+
+// the process's first granule import and map (ns): the runtime's one-time work inside the TAKE
+GS_EXPORT int gpushare_shim_arena_first(uint64_t* import_ns, uint64_t* map_ns) {
+  if (import_ns) *import_ns = g_first_import_ns;
+  if (map_ns) *map_ns = g_first_map_ns;
+  return g_first_import_ns != 0;
 }
 
 // (size, used) of the arena; 0 when there is none
@@ -2442,6 +2485,20 @@ GS_EXPORT hipError_t hipMemSetAccess(void* ptr, size_t size, const hipMemAccessD
   auto set = [&](char* at, size_t n) {
     hipError_t r = f(at, n, desc, count);
     logf(2, "vmm: access +%llu, %zu bytes: %d", (unsigned long long)(at - w->base), n, int(r));
+    if (r != hipSuccess && local_rw) {
+      // HIP 7.x refuses, now and then, the access of a driver page mapped after a mapping of
+      // another size in the same range, while one call over the whole run of mappings ending at
+      // that page succeeds (tools/diag/vmm_spill_probe.cpp, profiles/r5/vmm_spill_probe_run*.json)
+      char* from = mapped_run_start(*w, at);
+      if (from < at) {
+        if (auto le = real_hipGetLastError()) (void)le();
+        r = f(from, size_t(at + n - from), desc, count);
+        ++g_vmm_span_access;
+        logf(1, "vmm: access of +%llu refused; over the run from +%llu (%llu bytes): %d",
+             (unsigned long long)(at - w->base), (unsigned long long)(from - w->base),
+             (unsigned long long)(at + n - from), int(r));
+      }
+    }
     return r;
   };
   for (char* p = lo; p < hi && e == hipSuccess;) {

@@ -208,7 +208,12 @@ hipError_t hipMemAddressReserve(void** p, size_t n, size_t al, void* addr, unsig
 hipError_t hipMemAddressFree(void* p, size_t n) { munmap(p, n); return 0; }
 hipError_t hipMemMap(void* p, size_t n, size_t off, uint64_t h, unsigned long long fl) { return 0; }
 hipError_t hipMemUnmap(void* p, size_t n) { return 0; }
-hipError_t hipMemSetAccess(void* p, size_t n, const void* d, size_t c) { return 0; }
+/* FAKE_HIP_ACCESS_REFUSE_SIZE=<bytes>: refuse an access call of exactly that size, as HIP 7.x
+   now and then refuses one driver page's access (hipErrorInvalidValue) */
+hipError_t hipMemSetAccess(void* p, size_t n, const void* d, size_t c) {
+  const char* r = getenv("FAKE_HIP_ACCESS_REFUSE_SIZE");
+  return r && strtoull(r, 0, 10) == n ? 1 : 0;
+}
 hipError_t hipGetDevice(int* d) { *d = 0; return 0; }
 hipError_t hipDeviceSynchronize(void) { return 0; }
 /* what the HBM broker (native/hbmbroker) needs besides the above: exported handles are memfds,

@@ -636,7 +636,6 @@ def test_broker_arena_under_sanitizers(stub, tmp_path, san):
     name = ledger()
     env = dict(os.environ, LD_PRELOAD=f"{rt}:{lib}", LD_LIBRARY_PATH=str(d), GPUSHARE_LEDGER=name,
                GPUSHARE_QUOTA_BYTES=str(4 * GIB), GPUSHARE_HBM_BROKER=sock, GPUSHARE_HBM_TOKEN="t",
-               GPUSHARE_HBM_MAP_THREADS="4",           # the granules imported and mapped by 2 threads
                ASAN_OPTIONS="detect_leaks=0:halt_on_error=1", UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1",
                TSAN_OPTIONS="halt_on_error=1:report_bugs=1")
     try:
@@ -736,16 +735,24 @@ def test_broker_arena_serves_vmm_pages(stub, native_shim, tmp_path, align_cap):
         cleanup(name)
 
 
-def test_broker_arena_vmm_spills_to_the_driver_within_the_quota(stub, native_shim, tmp_path):
+@pytest.mark.parametrize("refuse", [False, True])
+def test_broker_arena_vmm_spills_to_the_driver_within_the_quota(stub, native_shim, tmp_path, refuse):
+    """Past the arena, VMM pages come from the driver within the quota. ``refuse``: the runtime
+    refuses the access call of a single driver page (HIP 7.x does, now and then); the shim sets
+    it over the whole run of mappings ending at that page, which the runtime accepts."""
     sock = str(tmp_path / "hbm.sock")
     FakeBroker(sock, granules=4)
     name = ledger()
     half = GIB // 2
     try:
         args = ["vres", 12 * GIB] + ["vpage", half] * 17 + ["vstats", "stats", "info"]
+        extra = {"FAKE_HIP_ACCESS_REFUSE_SIZE": str(half), "GPUSHARE_SHIM_LOG": "1"} if refuse else {}
         out, r = run(stub, native_shim, args, GPUSHARE_QUOTA_BYTES=8 * GIB, GPUSHARE_LEDGER=name,
-                     GPUSHARE_HBM_BROKER=sock, GPUSHARE_HBM_TOKEN="tok")
+                     GPUSHARE_HBM_BROKER=sock, GPUSHARE_HBM_TOKEN="tok", **extra)
         assert r.returncode == 0, r.stderr
+        if refuse:   # each driver page: over the run from the window's start (4 arena slots, the pages before it)
+            spans = [ln for ln in r.stderr.splitlines() if "refused; over the run from +0 " in ln]
+            assert len(spans) == 8 and all(ln.endswith(": 0") for ln in spans), r.stderr
         pages = out[1:18]
         ok = [p for p in pages if p["err"] == 0]
         assert len(ok) == 16 and pages[16]["err"] == 2                 # 8 GiB: 4 arena + 4 driver, then OOM
