@@ -199,9 +199,11 @@ struct Broker {
   struct Held {
     std::vector<int> idx;
     int pidfd = -1;  // kExit: the holder's process
+    double t0 = 0;   // released at
   };
   std::vector<Held> quarantine;
   unsigned long long quarantined_total = 0, lost = 0;
+  double quarantine_s_last = 0, quarantine_s_max = 0;  // release -> the last reference gone
   std::vector<int> base_refs;  // each granule's references with no tenant (the broker's own export)
   // A grant belongs to the pod, not to one process: a TAKE holds it while its connection lives,
   // and a restarted container (same env, same token) takes it again once the old process's
@@ -480,7 +482,7 @@ struct Broker {
         return;
       }
       quarantined_total += idx.size();
-      quarantine.push_back({idx, pfd});
+      quarantine.push_back({idx, pfd, now_s()});
       return;
     }
     if (pfd >= 0) close(pfd);
@@ -489,8 +491,13 @@ struct Broker {
     scrub(clean);
     if (!kept.empty()) {
       quarantined_total += kept.size();
-      quarantine.push_back({std::move(kept), -1});
+      quarantine.push_back({std::move(kept), -1, now_s()});
     }
+  }
+
+  void quarantine_done(const Held& g) {
+    quarantine_s_last = now_s() - g.t0;
+    quarantine_s_max = std::max(quarantine_s_max, quarantine_s_last);
   }
 
   size_t quarantined() const {
@@ -511,6 +518,7 @@ struct Broker {
           continue;
         }
         close(g.pidfd);
+        quarantine_done(g);
         scrub(g.idx);
         continue;
       }
@@ -521,7 +529,8 @@ struct Broker {
       std::vector<int> back, still;
       for (int i : g.idx) (outside(i) ? still : back).push_back(i);
       scrub(back);
-      if (!still.empty()) keep.push_back({std::move(still), -1});
+      if (!still.empty()) keep.push_back({std::move(still), -1, g.t0});
+      else quarantine_done(g);
     }
     quarantine.swap(keep);
   }
@@ -569,11 +578,12 @@ struct Broker {
                   "\"releases\": %llu, \"refused\": %llu, \"revokes\": %llu, \"revoked\": %zu, \"timeouts\": %llu, "
                   "\"expired\": %llu, \"busy\": %llu, \"idle_dropped\": %llu, \"peer_refused\": %llu, "
                   "\"clients\": %zu, \"quarantined\": %zu, \"quarantined_total\": %llu, \"lost\": %llu, "
-                  "\"release_policy\": \"%s\", \"held_refs_max\": %d, \"base_refs\": %d, \"scrubbed_bytes\": %llu, "
+                  "\"release_policy\": \"%s\", \"quarantine_ms_last\": %.1f, \"quarantine_ms_max\": %.1f, \"held_refs_max\": %d, \"base_refs\": %d, \"scrubbed_bytes\": %llu, "
                   "\"scrub_ms_total\": %.3f, \"scrub_ms_last\": %.3f, \"setup_ms\": %.1f}\n",
                   boot.c_str(), device, gran, count, count_max, grown, free_list.size(), held, owed, streamed, more_msgs, scrub_n, waiting, grants.size(), takes,
                   releases, refused, revokes, revoked.size(), timeouts, expired, busy, idle_dropped, peer_refused,
-                  clients.size(), quarantined(), quarantined_total, lost, policy_name(), held_refs_max(),
+                  clients.size(), quarantined(), quarantined_total, lost, policy_name(), quarantine_s_last * 1e3,
+                  quarantine_s_max * 1e3, held_refs_max(),
                   base_refs.empty() ? -1 : base_refs[0], scrubbed_bytes, scrub_s_total * 1e3, scrub_s_last * 1e3,
                   setup_s * 1e3);
     return b;

@@ -83,6 +83,7 @@ def test_fast_path_defers_to_identity_on_ambiguity(server):
         assert int(adm.responses[0].envs[const.ENV_RESOURCE_INDEX]) == 1
         assert _fast_count(al) == 0
         assert al.metrics.allocate_outcomes.value(outcome="identified") == 1
+        c.wait_assigned(b)                     # b's ASSIGNED patch has landed in the pod cache
         assert _settle(al)
         adm = c.admit(a)                       # now unambiguous: fast
         assert int(adm.responses[0].envs[const.ENV_RESOURCE_INDEX]) == 0

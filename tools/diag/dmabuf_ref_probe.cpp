@@ -28,6 +28,8 @@
 #include <sys/wait.h>
 #include <unistd.h>
 
+#include <time.h>
+
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -123,19 +125,23 @@ int main() {
   pid_t child = fork();  // before any HIP call in either process
   if (child == 0) {      // the exporter (the broker's part)
     close(sp[0]);
-    hipMemGenericAllocationHandle_t h = nullptr;
-    int efd = -1;
+    hipMemGenericAllocationHandle_t h = nullptr, h2 = nullptr;
+    int efd = -1, efd2 = -1;
     if (hipSetDevice(0) != hipSuccess || hipMemCreate(&h, gran, &p, 0) != hipSuccess ||
-        hipMemExportToShareableHandle(&efd, h, hipMemHandleTypePosixFileDescriptor, 0) != hipSuccess)
+        hipMemExportToShareableHandle(&efd, h, hipMemHandleTypePosixFileDescriptor, 0) != hipSuccess ||
+        hipMemCreate(&h2, gran, &p, 0) != hipSuccess ||
+        hipMemExportToShareableHandle(&efd2, h2, hipMemHandleTypePosixFileDescriptor, 0) != hipSuccess)
       _exit(3);
     send_fd(sp[1], efd);
+    send_fd(sp[1], efd2);
     char b;
     if (read(sp[1], &b, 1) < 0) _exit(4);  // until the tenant is done
     _exit(0);
   }
   close(sp[1]);
   int fd = recv_fd(sp[0]);
-  if (fd < 0) return 3;
+  int fd2 = recv_fd(sp[0]);
+  if (fd < 0 || fd2 < 0) return 3;
   if (hipSetDevice(0) != hipSuccess) return 2;
   int rt = 0;
   (void)hipRuntimeGetVersion(&rt);
@@ -148,9 +154,17 @@ int main() {
                                                                  hipMemHandleTypePosixFileDescriptor);
   rec("import", e);
   rec("c1", count_of(fd));
+  rec("c_fd2_before", count_of(fd2));
   void* va = nullptr;
   rec("reserve", hipMemAddressReserve(&va, gran, 0, nullptr, 0));
+  auto now_us = [] {
+    timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return long(t.tv_sec) * 1000000 + t.tv_nsec / 1000;
+  };
+  long t0 = now_us();
   rec("map", hipMemMap(va, gran, 0, hi, 0));
+  rec("first_map_us", now_us() - t0);
   hipMemAccessDesc d;
   std::memset(&d, 0, sizeof d);
   d.location.type = hipMemLocationTypeDevice;
@@ -196,6 +210,30 @@ int main() {
   rec("prime_lookups", found);
   rec("gem_closed", closed);
   rec("c6", count_of(fd));
+  {
+    // a second granule into a fresh range: is the first map's cost once per process?
+    hipMemGenericAllocationHandle_t h2 = nullptr;
+    void* va2 = nullptr;
+    long a = now_us();
+    hipError_t ie = rt < 70100000 ? hipMemImportFromShareableHandle(&h2, &fd2, hipMemHandleTypePosixFileDescriptor)
+                                  : hipMemImportFromShareableHandle(
+                                        &h2, reinterpret_cast<void*>(static_cast<intptr_t>(fd2)),
+                                        hipMemHandleTypePosixFileDescriptor);
+    long b = now_us();
+    rec("second_import", ie);
+    rec("second_import_us", b - a);
+    (void)hipMemAddressReserve(&va2, gran, 0, nullptr, 0);
+    long c = now_us();
+    rec("second_map", hipMemMap(va2, gran, 0, h2, 0));
+    rec("second_map_us", now_us() - c);
+    long e2 = now_us();
+    rec("second_access", hipMemSetAccess(va2, gran, &d, 1));
+    rec("second_access_us", now_us() - e2);
+    (void)hipMemUnmap(va2, gran);
+    (void)hipMemRelease(h2);
+    (void)hipMemAddressFree(va2, gran);
+    rec("c_second_released", count_of(fd2));
+  }
   (void)hipMemAddressFree(va, gran);
   if (write(sp[0], "x", 1) != 1) rec("tell_exporter", -1);
   int st = 0;
