@@ -1,42 +1,74 @@
-// Who keeps a broker granule's dma-buf referenced after a tenant released it?
+// Who keeps a broker granule's dma-buf referenced after a tenant released it, and what does a
+// tenant's first import + map cost?
 //
 // The HBM broker lends a granule again only when no reference to its dma-buf is left outside the
-// broker (fdinfo "count"). Measured in round 4-5: a tenant's references stay until its process is
-// torn down, even after hipMemUnmap + hipMemRelease of the imported handle, so a replacement pod
-// waits for the retired pod's process teardown (~70-110 ms). This probe follows the count through
-// one import: a child process exports a 1 GiB handle and sends the fd (SCM_RIGHTS), as the broker
-// does, and stays alive; this process imports it, as a tenant does:
+// broker (fdinfo "count"). Round 5 measured, with the quota shim under PyTorch: after the tenant's
+// hipMemUnmap + hipMemRelease of its imported handles the references stay until the tenant's
+// process is torn down, so a replacement pod waits for that teardown. This probe follows the
+// count through one import: a child process exports 1 GiB handles and sends the fds
+// (SCM_RIGHTS), as the broker does, and stays alive; this process imports one, as a tenant does:
 //
-//   c0  exported fd only
-//   c1  after hipMemImportFromShareableHandle
-//   c2  after hipMemMap + hipMemSetAccess
-//   c3  after hipMemUnmap
-//   c4  after hipMemRelease of the imported handle
-//   c5  after hipDeviceSynchronize
-//   then, on every render-node fd of this process, DRM_IOCTL_PRIME_FD_TO_HANDLE of the dma-buf
-//   (the GEM handle this DRM file holds for it, if any) and DRM_IOCTL_GEM_CLOSE of that handle:
-//   c6  after those closes
+//   c0  received fd only              c3  after hipMemUnmap
+//   c1  after the import              c4  after hipMemRelease of the imported handle
+//   c2  after map + access + memset   c5  after hipDeviceSynchronize (and 300 ms later)
+//   then, on every render-node fd of this process, DRM_IOCTL_PRIME_FD_TO_HANDLE of the dma-buf and
+//   DRM_IOCTL_GEM_CLOSE of the handle it names: c6 after those closes
 //
-//   g++ -std=c++17 -O1 -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -o tools/diag/build/dmabuf_ref_probe \
-//       tools/diag/dmabuf_ref_probe.cpp -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib
-#include <hip/hip_runtime.h>
-
+// and times the first map in the process against a second granule's import / map / access.
+// "warm": a hipMalloc + hipMemset + sync first, so the runtime's own one-time device work is done
+// before the first map.
+//
+// Every HIP entry point is looked up in the libamdhip64 this process loaded: the system runtime
+// when built as an executable (PROBE_MAIN, linked with -lamdhip64), PyTorch's bundled runtime
+// when loaded from Python after `import torch` (tools/diag/dmabuf_ref_probe.py).
+//
+//   g++ -std=c++17 -O1 -DPROBE_MAIN -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -o tools/diag/build/dmabuf_ref_probe
+//       tools/diag/dmabuf_ref_probe.cpp -L/opt/rocm/lib -lamdhip64 -ldl -Wl,-rpath,/opt/rocm/lib
+//   g++ -std=c++17 -O1 -shared -fPIC -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include
+//       -o tools/diag/build/libdmabuf_ref_probe.so tools/diag/dmabuf_ref_probe.cpp -ldl
 #include <dirent.h>
+#include <dlfcn.h>
 #include <fcntl.h>
+#include <hip/hip_runtime.h>
+#include <link.h>
 #include <sys/ioctl.h>
 #include <sys/socket.h>
 #include <sys/wait.h>
-#include <unistd.h>
-
 #include <time.h>
+#include <unistd.h>
 
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
 
 namespace {
+void* hip_lib() {
+  static void* h = nullptr;
+  if (h) return h;
+  const char* path = nullptr;
+  dl_iterate_phdr(
+      [](dl_phdr_info* info, size_t, void* data) {
+        if (info->dlpi_name && std::strstr(info->dlpi_name, "libamdhip64.so")) {
+          *static_cast<const char**>(data) = info->dlpi_name;
+          return 1;
+        }
+        return 0;
+      },
+      &path);
+  if (path) h = dlopen(path, RTLD_NOLOAD | RTLD_LAZY);
+  if (!h) h = dlopen("libamdhip64.so.7", RTLD_LAZY);
+  return h;
+}
+template <class F>
+F sym(const char* n) {
+  void* h = hip_lib();
+  return reinterpret_cast<F>(h ? dlsym(h, n) : nullptr);
+}
+#define H(name) (sym<decltype(&name)>(#name))
+
 struct drm_prime_handle_ {
   uint32_t handle;
   uint32_t flags;
@@ -48,6 +80,13 @@ struct drm_gem_close_ {
 };
 constexpr unsigned long kPrimeFdToHandle = _IOWR('d', 0x2e, drm_prime_handle_);
 constexpr unsigned long kGemClose = _IOW('d', 0x09, drm_gem_close_);
+constexpr size_t kGran = 1ull << 30;
+
+long now_us() {
+  timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return long(t.tv_sec) * 1000000 + t.tv_nsec / 1000;
+}
 
 int count_of(int fd) {
   char path[64];
@@ -77,7 +116,6 @@ std::vector<int> render_fds() {
   closedir(d);
   return out;
 }
-}  // namespace
 
 void send_fd(int s, int fd) {
   char b = 'f';
@@ -112,76 +150,94 @@ int recv_fd(int s) {
   return fd;
 }
 
-int main() {
-  const size_t gran = 1ull << 30;
+hipMemAllocationProp shareable() {
   hipMemAllocationProp p;
   std::memset(&p, 0, sizeof p);
   p.type = hipMemAllocationTypePinned;
   p.requestedHandleType = hipMemHandleTypePosixFileDescriptor;
   p.location.type = hipMemLocationTypeDevice;
   p.location.id = 0;
+  return p;
+}
+
+std::string out;
+void rec(const char* k, long v) { out += std::string(out.size() > 1 ? ", \"" : "\"") + k + "\": " + std::to_string(v); }
+
+hipError_t import_fd(int rt, hipMemGenericAllocationHandle_t* h, int& fd) {
+  return rt < 70100000 ? H(hipMemImportFromShareableHandle)(h, &fd, hipMemHandleTypePosixFileDescriptor)
+                       : H(hipMemImportFromShareableHandle)(h, reinterpret_cast<void*>(static_cast<intptr_t>(fd)),
+                                                            hipMemHandleTypePosixFileDescriptor);
+}
+}  // namespace
+
+extern "C" const char* dmabuf_ref_probe(int warm) {
+  out = "{";
+  if (!H(hipMemMap)) return "{\"error\": \"no HIP runtime in this process\"}";
   int sp[2];
-  if (socketpair(AF_UNIX, SOCK_STREAM, 0, sp)) return 2;
-  pid_t child = fork();  // before any HIP call in either process
+  if (socketpair(AF_UNIX, SOCK_STREAM, 0, sp)) return "{\"error\": \"socketpair\"}";
+  pid_t child = fork();  // before this process's first HIP call
   if (child == 0) {      // the exporter (the broker's part)
     close(sp[0]);
-    hipMemGenericAllocationHandle_t h = nullptr, h2 = nullptr;
-    int efd = -1, efd2 = -1;
-    if (hipSetDevice(0) != hipSuccess || hipMemCreate(&h, gran, &p, 0) != hipSuccess ||
-        hipMemExportToShareableHandle(&efd, h, hipMemHandleTypePosixFileDescriptor, 0) != hipSuccess ||
-        hipMemCreate(&h2, gran, &p, 0) != hipSuccess ||
-        hipMemExportToShareableHandle(&efd2, h2, hipMemHandleTypePosixFileDescriptor, 0) != hipSuccess)
-      _exit(3);
-    send_fd(sp[1], efd);
-    send_fd(sp[1], efd2);
+    auto p = shareable();
+    hipMemGenericAllocationHandle_t h[2] = {nullptr, nullptr};
+    int efd[2] = {-1, -1};
+    if (H(hipSetDevice)(0) != hipSuccess) _exit(3);
+    for (int i = 0; i < 2; ++i)
+      if (H(hipMemCreate)(&h[i], kGran, &p, 0) != hipSuccess ||
+          H(hipMemExportToShareableHandle)(&efd[i], h[i], hipMemHandleTypePosixFileDescriptor, 0) != hipSuccess)
+        _exit(3);
+    send_fd(sp[1], efd[0]);
+    send_fd(sp[1], efd[1]);
     char b;
     if (read(sp[1], &b, 1) < 0) _exit(4);  // until the tenant is done
     _exit(0);
   }
   close(sp[1]);
-  int fd = recv_fd(sp[0]);
-  int fd2 = recv_fd(sp[0]);
-  if (fd < 0 || fd2 < 0) return 3;
-  if (hipSetDevice(0) != hipSuccess) return 2;
+  int fd = recv_fd(sp[0]), fd2 = recv_fd(sp[0]);
+  if (fd < 0 || fd2 < 0) return "{\"error\": \"no fds\"}";
+  (void)H(hipSetDevice)(0);
   int rt = 0;
-  (void)hipRuntimeGetVersion(&rt);
-  hipMemGenericAllocationHandle_t hi = nullptr;
-  std::string o = "{\"runtime_version\": " + std::to_string(rt);
-  auto rec = [&](const char* k, long v) { o += std::string(", \"") + k + "\": " + std::to_string(v); };
-  rec("c0", count_of(fd));
-  hipError_t e = rt < 70100000 ? hipMemImportFromShareableHandle(&hi, &fd, hipMemHandleTypePosixFileDescriptor)
-                               : hipMemImportFromShareableHandle(&hi, reinterpret_cast<void*>(static_cast<intptr_t>(fd)),
-                                                                 hipMemHandleTypePosixFileDescriptor);
-  rec("import", e);
-  rec("c1", count_of(fd));
-  rec("c_fd2_before", count_of(fd2));
-  void* va = nullptr;
-  rec("reserve", hipMemAddressReserve(&va, gran, 0, nullptr, 0));
-  auto now_us = [] {
-    timespec t;
-    clock_gettime(CLOCK_MONOTONIC, &t);
-    return long(t.tv_sec) * 1000000 + t.tv_nsec / 1000;
-  };
-  long t0 = now_us();
-  rec("map", hipMemMap(va, gran, 0, hi, 0));
-  rec("first_map_us", now_us() - t0);
+  (void)H(hipRuntimeGetVersion)(&rt);
+  rec("runtime_version", rt);
+  rec("warm", warm);
+  if (warm) {
+    void* m = nullptr;
+    long t = now_us();
+    rec("warm_malloc", sym<hipError_t (*)(void**, size_t)>("hipMalloc")(&m, 64 << 20));
+    rec("warm_memset", sym<hipError_t (*)(void*, int, size_t)>("hipMemset")(m, 0, 64 << 20));
+    rec("warm_sync", H(hipDeviceSynchronize)());
+    rec("warm_us", now_us() - t);
+    (void)H(hipFree)(m);
+  }
   hipMemAccessDesc d;
   std::memset(&d, 0, sizeof d);
   d.location.type = hipMemLocationTypeDevice;
   d.location.id = 0;
   d.flags = hipMemAccessFlagsProtReadWrite;
-  rec("access", hipMemSetAccess(va, gran, &d, 1));
-  rec("memset", hipMemset(va, 0, 4096));
-  rec("sync0", hipDeviceSynchronize());
+  hipMemGenericAllocationHandle_t hi = nullptr;
+  rec("c0", count_of(fd));
+  long t = now_us();
+  rec("import", import_fd(rt, &hi, fd));
+  rec("first_import_us", now_us() - t);
+  rec("c1", count_of(fd));
+  void* va = nullptr;
+  rec("reserve", H(hipMemAddressReserve)(&va, kGran, 0, nullptr, 0));
+  t = now_us();
+  rec("map", H(hipMemMap)(va, kGran, 0, hi, 0));
+  rec("first_map_us", now_us() - t);
+  t = now_us();
+  rec("access", H(hipMemSetAccess)(va, kGran, &d, 1));
+  rec("first_access_us", now_us() - t);
+  rec("memset", sym<hipError_t (*)(void*, int, size_t)>("hipMemset")(va, 0, 4096));
+  rec("sync0", H(hipDeviceSynchronize)());
   rec("c2", count_of(fd));
-  rec("unmap", hipMemUnmap(va, gran));
+  rec("unmap", H(hipMemUnmap)(va, kGran));
   rec("c3", count_of(fd));
-  rec("release_imported", hipMemRelease(hi));
+  rec("release_imported", H(hipMemRelease)(hi));
   rec("c4", count_of(fd));
-  rec("sync", hipDeviceSynchronize());
+  rec("sync", H(hipDeviceSynchronize)());
   rec("c5", count_of(fd));
   {
-    // left alone, does the count come down while the process lives?
     int c = count_of(fd), ms = 0;
     while (ms < 300 && count_of(fd) == c) {
       usleep(1000);
@@ -189,6 +245,25 @@ int main() {
     }
     rec("c5_after_wait", count_of(fd));
     rec("c5_wait_ms", ms);
+  }
+  {  // a second granule into a fresh range
+    hipMemGenericAllocationHandle_t h2 = nullptr;
+    void* va2 = nullptr;
+    t = now_us();
+    rec("second_import", import_fd(rt, &h2, fd2));
+    rec("second_import_us", now_us() - t);
+    (void)H(hipMemAddressReserve)(&va2, kGran, 0, nullptr, 0);
+    t = now_us();
+    rec("second_map", H(hipMemMap)(va2, kGran, 0, h2, 0));
+    rec("second_map_us", now_us() - t);
+    t = now_us();
+    rec("second_access", H(hipMemSetAccess)(va2, kGran, &d, 1));
+    rec("second_access_us", now_us() - t);
+    rec("c2_second", count_of(fd2));
+    (void)H(hipMemUnmap)(va2, kGran);
+    (void)H(hipMemRelease)(h2);
+    (void)H(hipMemAddressFree)(va2, kGran);
+    rec("c4_second", count_of(fd2));
   }
   std::vector<int> rfds = render_fds();
   rec("render_fds", long(rfds.size()));
@@ -201,8 +276,6 @@ int main() {
       rec("c_after_lookup", count_of(fd));
       drm_gem_close_ gc{ph.handle, 0};
       if (ioctl(r, kGemClose, &gc) == 0) ++closed;
-      // a second close of the same handle: if the lookup created a handle of its own, the first
-      // close removed it; if the import had one, it is gone as well now
       drm_gem_close_ gc2{ph.handle, 0};
       rec("second_close_rc", ioctl(r, kGemClose, &gc2));
     }
@@ -210,37 +283,21 @@ int main() {
   rec("prime_lookups", found);
   rec("gem_closed", closed);
   rec("c6", count_of(fd));
-  {
-    // a second granule into a fresh range: is the first map's cost once per process?
-    hipMemGenericAllocationHandle_t h2 = nullptr;
-    void* va2 = nullptr;
-    long a = now_us();
-    hipError_t ie = rt < 70100000 ? hipMemImportFromShareableHandle(&h2, &fd2, hipMemHandleTypePosixFileDescriptor)
-                                  : hipMemImportFromShareableHandle(
-                                        &h2, reinterpret_cast<void*>(static_cast<intptr_t>(fd2)),
-                                        hipMemHandleTypePosixFileDescriptor);
-    long b = now_us();
-    rec("second_import", ie);
-    rec("second_import_us", b - a);
-    (void)hipMemAddressReserve(&va2, gran, 0, nullptr, 0);
-    long c = now_us();
-    rec("second_map", hipMemMap(va2, gran, 0, h2, 0));
-    rec("second_map_us", now_us() - c);
-    long e2 = now_us();
-    rec("second_access", hipMemSetAccess(va2, gran, &d, 1));
-    rec("second_access_us", now_us() - e2);
-    (void)hipMemUnmap(va2, gran);
-    (void)hipMemRelease(h2);
-    (void)hipMemAddressFree(va2, gran);
-    rec("c_second_released", count_of(fd2));
-  }
-  (void)hipMemAddressFree(va, gran);
+  (void)H(hipMemAddressFree)(va, kGran);
   if (write(sp[0], "x", 1) != 1) rec("tell_exporter", -1);
   int st = 0;
   waitpid(child, &st, 0);
   rec("exporter_status", st);
   rec("c7_exporter_gone", count_of(fd));
   close(fd);
-  std::puts((o + "}").c_str());
+  close(fd2);
+  out += "}";
+  return out.c_str();
+}
+
+#ifdef PROBE_MAIN
+int main(int argc, char** argv) {
+  std::puts(dmabuf_ref_probe(argc > 1 ? std::atoi(argv[1]) : 0));
   return 0;
 }
+#endif
