@@ -81,6 +81,7 @@ struct drm_gem_close_ {
 constexpr unsigned long kPrimeFdToHandle = _IOWR('d', 0x2e, drm_prime_handle_);
 constexpr unsigned long kGemClose = _IOW('d', 0x09, drm_gem_close_);
 constexpr size_t kGran = 1ull << 30;
+constexpr int kFds = 5;
 
 long now_us() {
   timespec t;
@@ -179,22 +180,23 @@ extern "C" const char* dmabuf_ref_probe(int warm) {
   if (child == 0) {      // the exporter (the broker's part)
     close(sp[0]);
     auto p = shareable();
-    hipMemGenericAllocationHandle_t h[2] = {nullptr, nullptr};
-    int efd[2] = {-1, -1};
+    hipMemGenericAllocationHandle_t h[kFds] = {};
+    int efd[kFds];
     if (H(hipSetDevice)(0) != hipSuccess) _exit(3);
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < kFds; ++i)
       if (H(hipMemCreate)(&h[i], kGran, &p, 0) != hipSuccess ||
           H(hipMemExportToShareableHandle)(&efd[i], h[i], hipMemHandleTypePosixFileDescriptor, 0) != hipSuccess)
         _exit(3);
-    send_fd(sp[1], efd[0]);
-    send_fd(sp[1], efd[1]);
+    for (int i = 0; i < kFds; ++i) send_fd(sp[1], efd[i]);
     char b;
     if (read(sp[1], &b, 1) < 0) _exit(4);  // until the tenant is done
     _exit(0);
   }
   close(sp[1]);
-  int fd = recv_fd(sp[0]), fd2 = recv_fd(sp[0]);
-  if (fd < 0 || fd2 < 0) return "{\"error\": \"no fds\"}";
+  int fds[kFds];
+  for (int i = 0; i < kFds; ++i)
+    if ((fds[i] = recv_fd(sp[0])) < 0) return "{\"error\": \"no fds\"}";
+  int fd = fds[0], fd2 = fds[1];
   (void)H(hipSetDevice)(0);
   int rt = 0;
   (void)H(hipRuntimeGetVersion)(&rt);
@@ -265,6 +267,44 @@ extern "C" const char* dmabuf_ref_probe(int warm) {
     (void)H(hipMemAddressFree)(va2, kGran);
     rec("c4_second", count_of(fd2));
   }
+  {  // B: import, release, no map
+    hipMemGenericAllocationHandle_t hb = nullptr;
+    rec("b_c0", count_of(fds[2]));
+    rec("b_import", import_fd(rt, &hb, fds[2]));
+    rec("b_c1", count_of(fds[2]));
+    rec("b_release", H(hipMemRelease)(hb));
+    rec("b_c4", count_of(fds[2]));
+  }
+  {  // C: the full cycle, then a second release of the same handle
+    hipMemGenericAllocationHandle_t hc = nullptr;
+    void* vc = nullptr;
+    rec("c_import", import_fd(rt, &hc, fds[3]));
+    (void)H(hipMemAddressReserve)(&vc, kGran, 0, nullptr, 0);
+    rec("c_map", H(hipMemMap)(vc, kGran, 0, hc, 0));
+    rec("c_access", H(hipMemSetAccess)(vc, kGran, &d, 1));
+    rec("c_unmap", H(hipMemUnmap)(vc, kGran));
+    rec("c_release", H(hipMemRelease)(hc));
+    rec("c_c4", count_of(fds[3]));
+    rec("c_release_again", H(hipMemRelease)(hc));
+    (void)H(hipGetLastError)();
+    rec("c_c4_again", count_of(fds[3]));
+    (void)H(hipMemAddressFree)(vc, kGran);
+    rec("c_c_after_free", count_of(fds[3]));
+  }
+  {  // D: release while mapped, then unmap
+    hipMemGenericAllocationHandle_t hd = nullptr;
+    void* vd = nullptr;
+    rec("d_import", import_fd(rt, &hd, fds[4]));
+    (void)H(hipMemAddressReserve)(&vd, kGran, 0, nullptr, 0);
+    rec("d_map", H(hipMemMap)(vd, kGran, 0, hd, 0));
+    rec("d_access", H(hipMemSetAccess)(vd, kGran, &d, 1));
+    rec("d_release", H(hipMemRelease)(hd));
+    rec("d_c_released_mapped", count_of(fds[4]));
+    rec("d_unmap", H(hipMemUnmap)(vd, kGran));
+    rec("d_c4", count_of(fds[4]));
+    (void)H(hipMemAddressFree)(vd, kGran);
+    rec("d_c_after_free", count_of(fds[4]));
+  }
   std::vector<int> rfds = render_fds();
   rec("render_fds", long(rfds.size()));
   int closed = 0, found = 0;
@@ -289,8 +329,7 @@ extern "C" const char* dmabuf_ref_probe(int warm) {
   waitpid(child, &st, 0);
   rec("exporter_status", st);
   rec("c7_exporter_gone", count_of(fd));
-  close(fd);
-  close(fd2);
+  for (int i = 0; i < kFds; ++i) close(fds[i]);
   out += "}";
   return out.c_str();
 }
