@@ -33,6 +33,7 @@
 #include <link.h>
 #include <sys/ioctl.h>
 #include <sys/socket.h>
+#include <sys/stat.h>
 #include <sys/wait.h>
 #include <time.h>
 #include <unistd.h>
@@ -113,6 +114,24 @@ std::vector<int> render_fds() {
     if (n <= 0) continue;
     link[n] = 0;
     if (std::strstr(link, "/dev/dri/renderD")) out.push_back(std::atoi(e->d_name));
+  }
+  closedir(d);
+  return out;
+}
+
+// other fds of this process on the same file as `fd` (the runtime's own copies)
+std::vector<int> same_file_fds(int fd) {
+  std::vector<int> out;
+  struct stat a;
+  if (fstat(fd, &a)) return out;
+  DIR* d = opendir("/proc/self/fd");
+  if (!d) return out;
+  int self = dirfd(d);
+  while (dirent* e = readdir(d)) {
+    int f = std::atoi(e->d_name);
+    if (e->d_name[0] < '0' || e->d_name[0] > '9' || f == fd || f == self) continue;
+    struct stat b;
+    if (fstat(f, &b) == 0 && b.st_dev == a.st_dev && b.st_ino == a.st_ino) out.push_back(f);
   }
   closedir(d);
   return out;
@@ -240,6 +259,11 @@ extern "C" const char* dmabuf_ref_probe(int warm) {
   rec("sync", H(hipDeviceSynchronize)());
   rec("c5", count_of(fd));
   {
+    // does the runtime keep a copy of the fd? (checked again for case B below, then closed)
+    std::vector<int> dups = same_file_fds(fd);
+    rec("dup_fds_after_release", long(dups.size()));
+  }
+  {
     int c = count_of(fd), ms = 0;
     while (ms < 300 && count_of(fd) == c) {
       usleep(1000);
@@ -272,8 +296,13 @@ extern "C" const char* dmabuf_ref_probe(int warm) {
     rec("b_c0", count_of(fds[2]));
     rec("b_import", import_fd(rt, &hb, fds[2]));
     rec("b_c1", count_of(fds[2]));
+    rec("b_dups_while_imported", long(same_file_fds(fds[2]).size()));
     rec("b_release", H(hipMemRelease)(hb));
     rec("b_c4", count_of(fds[2]));
+    std::vector<int> dups = same_file_fds(fds[2]);
+    rec("b_dups_after_release", long(dups.size()));
+    for (int f : dups) close(f);
+    rec("b_c_after_closing_dups", count_of(fds[2]));
   }
   {  // C: the full cycle, then a second release of the same handle
     hipMemGenericAllocationHandle_t hc = nullptr;

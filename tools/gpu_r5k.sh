@@ -1,5 +1,5 @@
 set -o pipefail
-D=gpurun_out/r5k
+D=gpurun_out/r5l
 mkdir -p $D
 step() { local name=$1; shift; "$@"; local rc=$?; echo "$name rc=$rc" >> $D/steps.log; [ $rc -eq 0 ] || exit $rc; }
 step sys timeout -k 10 90 ./tools/diag/build/dmabuf_ref_probe 1 > $D/sys.json 2> $D/sys.err
