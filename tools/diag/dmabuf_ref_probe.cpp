@@ -38,6 +38,7 @@
 #include <time.h>
 #include <unistd.h>
 
+#include <cstdarg>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -180,6 +181,40 @@ hipMemAllocationProp shareable() {
   return p;
 }
 
+// ---- the runtime's KFD ioctls (this file's ioctl interposes libc's: in the executable, or in the
+// library when it is LD_PRELOADed) ----
+struct KRec {
+  unsigned nr;
+  uint64_t handle;
+  uint32_t gpu_id;
+  ino_t ino;
+  int kfd;
+  int rc;
+};
+KRec g_k[8192];
+int g_nk = 0;
+bool g_recording = false;
+
+constexpr unsigned long kfd_iowr(unsigned nr, unsigned size) {
+  return (3ul << 30) | ((unsigned long)size << 16) | ((unsigned long)'K' << 8) | nr;
+}
+constexpr unsigned long kfd_iow(unsigned nr, unsigned size) {
+  return (1ul << 30) | ((unsigned long)size << 16) | ((unsigned long)'K' << 8) | nr;
+}
+struct UnmapArgs {
+  uint64_t handle, device_ids_array_ptr;
+  uint32_t n_devices, n_success;
+};
+struct ImportArgs {
+  uint64_t va_addr, handle;
+  uint32_t gpu_id, dmabuf_fd;
+};
+
+ino_t ino_of(int fd) {
+  struct stat st;
+  return fstat(fd, &st) == 0 ? st.st_ino : 0;
+}
+
 std::string out;
 void rec(const char* k, long v) { out += std::string(out.size() > 1 ? ", \"" : "\"") + k + "\": " + std::to_string(v); }
 
@@ -188,7 +223,53 @@ hipError_t import_fd(int rt, hipMemGenericAllocationHandle_t* h, int& fd) {
                        : H(hipMemImportFromShareableHandle)(h, reinterpret_cast<void*>(static_cast<intptr_t>(fd)),
                                                             hipMemHandleTypePosixFileDescriptor);
 }
+// free the KFD objects the runtime made when it imported `fd` and has not freed: unmap them from
+// their GPU, then free them. Returns how many were freed (-1: none found)
+int free_leaked_imports(int fd, const char* tag) {
+  ino_t ino = ino_of(fd);
+  int freed = -1;
+  for (int i = 0; i < g_nk; ++i) {
+    if (g_k[i].nr != 0x1D || g_k[i].rc != 0 || g_k[i].ino != ino) continue;
+    bool gone = false;
+    for (int j = i + 1; j < g_nk; ++j) gone |= g_k[j].nr == 0x17 && g_k[j].handle == g_k[i].handle && g_k[j].rc == 0;
+    if (gone) continue;
+    if (freed < 0) freed = 0;
+    uint32_t dev = g_k[i].gpu_id;
+    UnmapArgs u{g_k[i].handle, reinterpret_cast<uint64_t>(&dev), 1, 0};
+    int ru = ioctl(g_k[i].kfd, kfd_iowr(0x19, sizeof(UnmapArgs)), &u);
+    uint64_t h = g_k[i].handle;
+    int rf = ioctl(g_k[i].kfd, kfd_iow(0x17, sizeof(uint64_t)), &h);
+    std::string k = std::string(tag) + "_unmap_rc";
+    rec(k.c_str(), ru);
+    k = std::string(tag) + "_free_rc";
+    rec(k.c_str(), rf);
+    freed += rf == 0;
+  }
+  return freed;
+}
 }  // namespace
+
+extern "C" int ioctl(int fd, unsigned long req, ...) {
+  va_list ap;
+  va_start(ap, req);
+  void* arg = va_arg(ap, void*);
+  va_end(ap);
+  static auto real = reinterpret_cast<int (*)(int, unsigned long, void*)>(dlsym(RTLD_NEXT, "ioctl"));
+  int rc = real(fd, req, arg);
+  unsigned nr = req & 0xff;
+  if (g_recording && ((req >> 8) & 0xff) == 'K' && g_nk < 8192 &&
+      (nr == 0x16 || nr == 0x17 || nr == 0x18 || nr == 0x19 || nr == 0x1D)) {
+    KRec& r = g_k[g_nk++];
+    r = KRec{nr, *static_cast<uint64_t*>(arg), 0, 0, fd, rc};
+    if (nr == 0x1D) {
+      auto* a = static_cast<ImportArgs*>(arg);
+      r.handle = a->handle;
+      r.gpu_id = a->gpu_id;
+      r.ino = ino_of(int(a->dmabuf_fd));
+    }
+  }
+  return rc;
+}
 
 extern "C" const char* dmabuf_ref_probe(int warm) {
   out = "{";
@@ -236,6 +317,7 @@ extern "C" const char* dmabuf_ref_probe(int warm) {
   d.location.id = 0;
   d.flags = hipMemAccessFlagsProtReadWrite;
   hipMemGenericAllocationHandle_t hi = nullptr;
+  g_recording = true;
   rec("c0", count_of(fd));
   long t = now_us();
   rec("import", import_fd(rt, &hi, fd));
@@ -303,6 +385,8 @@ extern "C" const char* dmabuf_ref_probe(int warm) {
     rec("b_dups_after_release", long(dups.size()));
     for (int f : dups) close(f);
     rec("b_c_after_closing_dups", count_of(fds[2]));
+    rec("b_leaked_freed", free_leaked_imports(fds[2], "b"));
+    rec("b_c_after_kfd_free", count_of(fds[2]));
   }
   {  // C: the full cycle, then a second release of the same handle
     hipMemGenericAllocationHandle_t hc = nullptr;
@@ -319,6 +403,8 @@ extern "C" const char* dmabuf_ref_probe(int warm) {
     rec("c_c4_again", count_of(fds[3]));
     (void)H(hipMemAddressFree)(vc, kGran);
     rec("c_c_after_free", count_of(fds[3]));
+    rec("c_leaked_freed", free_leaked_imports(fds[3], "c"));
+    rec("c_c_after_kfd_free", count_of(fds[3]));
   }
   {  // D: release while mapped, then unmap
     hipMemGenericAllocationHandle_t hd = nullptr;
@@ -350,6 +436,19 @@ extern "C" const char* dmabuf_ref_probe(int warm) {
     }
   }
   rec("prime_lookups", found);
+  {
+    int imports = 0, frees = 0, maps = 0, unmaps = 0;
+    for (int i = 0; i < g_nk; ++i) {
+      imports += g_k[i].nr == 0x1D;
+      frees += g_k[i].nr == 0x17;
+      maps += g_k[i].nr == 0x18;
+      unmaps += g_k[i].nr == 0x19;
+    }
+    rec("kfd_imports", imports);
+    rec("kfd_frees", frees);
+    rec("kfd_maps", maps);
+    rec("kfd_unmaps", unmaps);
+  }
   rec("gem_closed", closed);
   rec("c6", count_of(fd));
   (void)H(hipMemAddressFree)(va, kGran);
