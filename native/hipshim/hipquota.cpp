@@ -125,6 +125,21 @@ constexpr unsigned long kfd_ioc(unsigned dir, unsigned nr, unsigned size) {
 constexpr unsigned long kIocAlloc = kfd_ioc(3, 0x16, sizeof(KfdAllocArgs));  // AMDKFD_IOWR(0x16)
 constexpr unsigned long kIocFree = kfd_ioc(1, 0x17, sizeof(KfdFreeArgs));    // AMDKFD_IOW(0x17)
 static_assert(sizeof(KfdAllocArgs) == 40 && sizeof(KfdFreeArgs) == 8, "KFD uapi layout");
+struct KfdUnmapArgs {   // struct kfd_ioctl_unmap_memory_from_gpu_args
+  uint64_t handle;
+  uint64_t device_ids_array_ptr;
+  uint32_t n_devices;
+  uint32_t n_success;
+};
+struct KfdImportArgs {  // struct kfd_ioctl_import_dmabuf_args
+  uint64_t va_addr;
+  uint64_t handle;
+  uint32_t gpu_id;
+  uint32_t dmabuf_fd;
+};
+constexpr unsigned long kIocUnmap = kfd_ioc(3, 0x19, sizeof(KfdUnmapArgs));    // AMDKFD_IOWR(0x19)
+constexpr unsigned long kIocImport = kfd_ioc(3, 0x1D, sizeof(KfdImportArgs));  // AMDKFD_IOWR(0x1D)
+static_assert(sizeof(KfdUnmapArgs) == 24 && sizeof(KfdImportArgs) == 24, "KFD uapi layout");
 
 // ---- amdgpu DRM uapi (drm/amdgpu_drm.h, drm/drm.h) -----------------------------------------
 struct DrmGemCreateIn {   // union drm_amdgpu_gem_create: in {bo_size, alignment, domains, domain_flags}
@@ -981,6 +996,66 @@ void gem_fd_closed(int fd, uint64_t key) {
   release_client(key);
 }
 
+// ---- the runtime's KFD imports of broker granules ----
+// HIP 7.0 (the runtime PyTorch bundles) never frees the KFD object it creates when it imports a
+// dma-buf: after hipMemRelease the granule stays referenced until the process is torn down, and
+// the broker cannot lend it to the next pod before that (tools/diag/dmabuf_ref_probe.cpp,
+// profiles/r5/dmabuf_refs/). HIP 7.2 frees it at hipMemRelease. So the shim notes the imports the
+// runtime makes while the arena imports its granules, and at gpushare_shim_arena_release() frees
+// the ones a runtime older than 7.1 left behind.
+struct KfdImport {
+  uint64_t handle;
+  int kfd;
+  uint32_t gpu_id;
+  bool live;
+};
+constexpr int kMaxImports = 2048;
+KfdImport g_imports[kMaxImports];
+int g_nimports = 0;
+std::atomic<int> g_imports_live{0};
+pthread_mutex_t g_imp_mu = PTHREAD_MUTEX_INITIALIZER;
+thread_local bool t_importing = false;  // inside the arena's own import of a granule
+
+void import_note(int kfd, const KfdImportArgs* a) {
+  pthread_mutex_lock(&g_imp_mu);
+  if (g_nimports < kMaxImports) {
+    g_imports[g_nimports++] = {a->handle, kfd, a->gpu_id, true};
+    g_imports_live.fetch_add(1, std::memory_order_relaxed);
+  }
+  pthread_mutex_unlock(&g_imp_mu);
+}
+
+void import_forget(uint64_t handle) {
+  pthread_mutex_lock(&g_imp_mu);
+  for (int i = 0; i < g_nimports; ++i)
+    if (g_imports[i].live && g_imports[i].handle == handle) {
+      g_imports[i].live = false;
+      g_imports_live.fetch_sub(1, std::memory_order_relaxed);
+    }
+  pthread_mutex_unlock(&g_imp_mu);
+}
+
+// free the imports the runtime kept (after it released every arena handle); returns how many
+int imports_free_kept(ioctl_t f) {
+  int n = 0;
+  pthread_mutex_lock(&g_imp_mu);
+  for (int i = 0; i < g_nimports; ++i) {
+    KfdImport& m = g_imports[i];
+    if (!m.live) continue;
+    uint32_t dev = m.gpu_id;
+    KfdUnmapArgs u{m.handle, reinterpret_cast<uint64_t>(&dev), 1, 0};
+    (void)f(m.kfd, kIocUnmap, &u);  // mapped through VMM, not KFD: normally refused, harmless
+    KfdFreeArgs fr{m.handle};
+    if (f(m.kfd, kIocFree, &fr) == 0) ++n;
+    m.live = false;
+  }
+  g_nimports = 0;
+  g_imports_live.store(0, std::memory_order_relaxed);
+  pthread_mutex_unlock(&g_imp_mu);
+  return n;
+}
+
+int ioctl_body(ioctl_t f, int fd, unsigned long req, void* arg);
 }  // namespace
 
 // ---- interposed libc ioctl (kfd mode) ------------------------------------------------------
@@ -994,6 +1069,22 @@ GS_EXPORT int ioctl(int fd, unsigned long req, ...) {
     errno = ENOSYS;
     return -1;
   }
+  if (req == kIocImport && arg && t_importing) {
+    int r = f(fd, req, arg);
+    if (r == 0) import_note(fd, static_cast<KfdImportArgs*>(arg));
+    return r;
+  }
+  if (req == kIocFree && arg && g_imports_live.load(std::memory_order_relaxed) > 0) {
+    uint64_t h = static_cast<KfdFreeArgs*>(arg)->handle;
+    int r = ioctl_body(f, fd, req, arg);
+    if (r == 0) import_forget(h);
+    return r;
+  }
+  return ioctl_body(f, fd, req, arg);
+}
+
+namespace {
+int ioctl_body(ioctl_t f, int fd, unsigned long req, void* arg) {
   // Cheap filters first, and never the once-control while init() runs (the runtime may start
   // up underneath it and allocate through here: waiting on that init would deadlock).
   if ((req != kIocAlloc && req != kIocFree && req != kDrmGemCreate && req != kDrmGemClose &&
@@ -1017,6 +1108,7 @@ GS_EXPORT int ioctl(int fd, unsigned long req, ...) {
   }
   return r;
 }
+}  // namespace
 
 // ---- interposed libc close (render-node fds with charged GEM handles) ----------------------
 using close_t = int (*)(int);
@@ -1112,6 +1204,7 @@ struct Arena {
   uint64_t size = 0, vsize = 0, gran = 0, used = 0;
   int n = 0, total = 0;
   bool by_address = false;  // how this runtime imports a POSIX fd (see arena_take)
+  int rt_version = 0;       // hipRuntimeGetVersion
   hipMemGenericAllocationHandle_t h[kArenaMaxGranules];
   Ext* ext = nullptr;
   int next = 0;
@@ -1193,9 +1286,11 @@ int import_and_map(int* fds, int k, hipMemGenericAllocationHandle_t* h, char* ba
   Depth d;
   for (int i = 0; i < k; ++i) {
     uint64_t t0 = mono_ns();
+    t_importing = true;
     hipError_t e = by_address ? import_f(&h[i], &fds[i], hipMemHandleTypePosixFileDescriptor)
                               : import_f(&h[i], reinterpret_cast<void*>(static_cast<intptr_t>(fds[i])),
                                          hipMemHandleTypePosixFileDescriptor);
+    t_importing = false;
     uint64_t t1 = mono_ns();
     if (e != hipSuccess) {
       h[i] = nullptr;
@@ -1356,6 +1451,7 @@ void arena_take() {
     a.gran = gran;
     a.total = int(total);
     a.by_address = by_address;
+    a.rt_version = rtv;
     g_dev = dev;
   }
   // the arena counts against the pod's quota like any other HBM it holds: what the runtime
@@ -1990,6 +2086,12 @@ GS_EXPORT int gpushare_shim_arena_release() {
     return -1;
   }
   arena_unmap_locked();
+  if (a.rt_version > 0 && a.rt_version < 70100000 && env_u64("GPUSHARE_HBM_FREE_KEPT", 1)) {
+    // HIP 7.0 keeps the KFD imports of the released handles: free them, so the broker sees its
+    // granules' references gone now rather than at this process's teardown
+    int n = imports_free_kept(real_ioctl());
+    logf(1, "hbm broker: freed %d KFD imports the runtime kept", n);
+  }
   if (a.charged) uncharge(a.size);
   a.charged = false;
   close(a.sock);

@@ -23,6 +23,14 @@ struct kfd_free { uint64_t handle; };
 #define KIOC(dir, nr, sz) (((unsigned long)(dir) << 30) | ((unsigned long)(sz) << 16) | ((unsigned long)'K' << 8) | (nr))
 #define KFD_ALLOC KIOC(3, 0x16, sizeof(struct kfd_alloc))
 #define KFD_FREE KIOC(1, 0x17, sizeof(struct kfd_free))
+/* AMDKFD_IOC_IMPORT_DMABUF: the "kernel" keeps the dma-buf referenced (a dup of the fd) until the
+   import is freed (AMDKFD_IOC_FREE_MEMORY_OF_GPU of its handle) */
+struct kfd_import { uint64_t va, handle; uint32_t gpu_id, dmabuf_fd; };
+#define KFD_IMPORT KIOC(3, 0x1D, sizeof(struct kfd_import))
+#define IMPORT_HANDLE (1ull << 40)
+#define MAXIMP 4096
+static int g_imp_fd[MAXIMP];  /* fd + 1 of each live import, 0 none */
+static unsigned g_imp_next = 0;
 #define MAXH (1 << 20)
 static size_t g_total = (size_t)16 << 30, g_used = 0;
 static uint64_t g_sizes[MAXH];
@@ -77,6 +85,17 @@ int ioctl(int fd, unsigned long req, ...) {
     uint64_t h = __atomic_fetch_add(&g_next, 1, __ATOMIC_ACQ_REL) % MAXH;
     __atomic_store_n(&g_sizes[h], a->size, __ATOMIC_RELEASE);
     a->handle = h; return 0;
+  }
+  if (req == KFD_IMPORT) {
+    struct kfd_import* a = (struct kfd_import*)arg;
+    unsigned i = __atomic_fetch_add(&g_imp_next, 1, __ATOMIC_ACQ_REL) % MAXIMP;
+    g_imp_fd[i] = (int)a->dmabuf_fd + 1;
+    a->handle = IMPORT_HANDLE | i; return 0;
+  }
+  if (req == KFD_FREE && (((struct kfd_free*)arg)->handle & IMPORT_HANDLE)) {
+    unsigned i = (unsigned)(((struct kfd_free*)arg)->handle & (MAXIMP - 1));
+    if (g_imp_fd[i] <= 0) { errno = EINVAL; return -1; }
+    close(g_imp_fd[i] - 1); g_imp_fd[i] = 0; return 0;
   }
   if (req == KFD_FREE) {
     uint64_t h = ((struct kfd_free*)arg)->handle;
@@ -167,10 +186,12 @@ hipError_t hipMemRelease_imported(uint64_t h);
 hipError_t hipMemRelease(uint64_t h) { if (h & (1ull << 62)) return hipMemRelease_imported(h); kfd_release(h); return 0; }
 /* what ROCr does for a scratch-heavy dispatch: VRAM taken inside the runtime, no HIP call */
 int fake_runtime_scratch(size_t n) { uint64_t h; return kfd(n, &h); }
-/* HIP VMM for the shim's HBM-broker arena: imported handles keep a dup of the broker's fd (the
-   high bit marks them); the address range is a host reservation. Import follows the 7.2
-   runtime: the fd is the pointer's value, and an address (a pointer to the fd) is refused
-   with hipErrorInvalidValue. */
+/* HIP VMM for the shim's HBM-broker arena: an import goes through the KFD import ioctl with a dup
+   of the broker's fd (the "kernel" reference; the high bit marks the handle); the address range is
+   a host reservation. Import follows the 7.2 runtime: the fd is the pointer's value, and an
+   address (a pointer to the fd) is refused with hipErrorInvalidValue. Release frees the KFD
+   import from 7.1 on; below 7.1 it leaves it, as HIP 7.0 does (measured on MI355X,
+   profiles/r5/dmabuf_refs/), so the reference stays until the process exits. */
 #define IMPORTED (1ull << 62)
 /* FAKE_HIP_VERSION (default 70253211, a 7.2 runtime): below 7.1 the import reads the fd through
    the pointer as HIP 7.0 does (and "crashes" — exit 139 — on a bare value); from 7.1 on it takes
@@ -187,9 +208,15 @@ hipError_t hipMemImportFromShareableHandle(uint64_t* h, void* os, int type) {
   }
   int d = dup((int)fd);
   if (d < 0) return 1;
-  *h = IMPORTED | (uint64_t)d; return 0;
+  struct kfd_import a = {0, 0, 1, (uint32_t)d};
+  if (ioctl(3, KFD_IMPORT, &a)) { close(d); return 1; }
+  *h = IMPORTED | a.handle; return 0;
 }
-hipError_t hipMemRelease_imported(uint64_t h) { close((int)(h & 0xffffffff)); return 0; }
+int fake_live_imports(void) { int n = 0; for (int i = 0; i < MAXIMP; ++i) n += g_imp_fd[i] > 0; return n; }
+hipError_t hipMemRelease_imported(uint64_t h) {
+  if (fake_version() >= 70100000) { struct kfd_free f = {h & ~IMPORTED}; ioctl(3, KFD_FREE, &f); }
+  return 0;
+}
 /* FAKE_HIP_RESERVE_ALIGN_MAX=<bytes>: like HIP 7.x, a larger alignment is not honoured, and the
    range is deliberately placed off any larger boundary */
 hipError_t hipMemAddressReserve(void** p, size_t n, size_t al, void* addr, unsigned long long fl) {

@@ -82,6 +82,8 @@ int main(int argc, char** argv) {
       printf("{\"op\":\"arenastream\",\"on\":%d,\"waits\":%llu,\"wait_ms\":%.1f,\"msgs\":%llu,\"mapped\":%llu,\"granted\":%llu,\"first\":%llu}\n",
              on, (unsigned long long)w, wn / 1e6, (unsigned long long)m, (unsigned long long)mp, (unsigned long long)gr,
              (unsigned long long)fi); }
+    else if (!strcmp(argv[i], "imports")) { int (*f)(void) = (int (*)(void))dlsym(RTLD_DEFAULT, "fake_live_imports");
+      printf("{\"op\":\"imports\",\"live\":%d}\n", f ? f() : -2); }
     else if (!strcmp(argv[i], "arenarelease")) { int (*f)(void) = (int (*)(void))dlsym(RTLD_DEFAULT, "gpushare_shim_arena_release");
       printf("{\"op\":\"arenarelease\",\"r\":%d}\n", f ? f() : -2); fflush(stdout); }
     else if (!strcmp(argv[i], "sleepms")) { fflush(stdout); usleep((useconds_t)atoi(argv[++i]) * 1000); }

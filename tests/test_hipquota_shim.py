@@ -606,6 +606,32 @@ def test_plain_take_and_a_stream_that_ends_early(stub, native_shim, tmp_path):
         cleanup(name)
 
 
+@pytest.mark.parametrize("version,free_kept,left", [(70051831, "1", 0), (70051831, "0", 3), (70253211, "1", 0)])
+def test_arena_release_frees_the_kfd_imports_hip70_keeps(stub, native_shim, tmp_path, version, free_kept, left):
+    """HIP 7.0 (PyTorch's runtime) never frees the KFD import of a released handle, so a broker
+    granule stays referenced until the pod's process is torn down and the next pod waits for that
+    (measured on MI355X: profiles/r5/dmabuf_refs/); the stub runtime does the same below 7.1. At
+    gpushare_shim_arena_release() the shim frees the KFD imports the runtime kept (noted when it
+    made them, during the arena's own imports). GPUSHARE_HBM_FREE_KEPT=0 leaves the runtime's
+    behaviour; HIP 7.2 frees them itself. The broker side is on MI355X:
+    tests/test_hbm_broker.py::test_a_released_arena_comes_back_while_the_tenant_lives."""
+    sock = str(tmp_path / "hbm.sock")
+    FakeBroker(sock, granules=3)
+    name = ledger()
+    try:
+        out, r = run(stub, native_shim, ["alloc", GIB, "imports", "freeall", "arenarelease", "imports"],
+                     GPUSHARE_QUOTA_BYTES=4 * GIB, GPUSHARE_LEDGER=name, GPUSHARE_HBM_BROKER=sock, GPUSHARE_HBM_TOKEN="t",
+                     FAKE_HIP_VERSION=version, GPUSHARE_HBM_FREE_KEPT=free_kept, GPUSHARE_SHIM_LOG="1")
+        assert r.returncode == 0, r.stderr
+        a, live, _, rel, after = out
+        assert a["err"] == 0 and live["live"] == 3 and rel["r"] == 1
+        assert after["live"] == left, r.stderr
+        if version < 70100000 and free_kept == "1":
+            assert "freed 3 KFD imports the runtime kept" in r.stderr
+    finally:
+        cleanup(name)
+
+
 def test_broker_refusal_leaves_the_pod_on_the_driver(stub, native_shim, tmp_path):
     sock = str(tmp_path / "hbm.sock")
     b = FakeBroker(sock, refuse=True)
