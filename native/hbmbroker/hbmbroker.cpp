@@ -50,7 +50,7 @@
 //                       [--device 0 | --pci-bus-id 0000:05:00.0] [--gib N | --reserve-gib R]
 //                       [--granule-mib 1024] [--wait-s 30] [--ungranted-wait-s 10]
 //                       [--grant-ttl-s 0] [--max-clients 1024] [--max-per-peer 8]
-//                       [--request-timeout-s 2] [--release-policy auto]
+//                       [--request-timeout-s 2] [--release-policy auto] [--scrub-chunk 8]
 #include <hip/hip_runtime.h>
 
 #include <fcntl.h>
@@ -218,6 +218,7 @@ struct Broker {
   std::set<std::string> revoked;
   std::deque<std::string> revoked_order;  // bounded: the oldest revocations are forgotten
   double grant_ttl_s = 0.0;
+  int scrub_chunk = 8;  // granules per scrub event
   unsigned long long expired = 0;
   std::map<int, Client> clients;
   // stats
@@ -306,21 +307,27 @@ struct Broker {
     scrub(fresh);
   }
 
-  // zero the granules on the broker's stream; they are lent again from reap_scrubs()
+  // zero the granules on the broker's stream; they are lent again from reap_scrubs(), in chunks
+  // of scrub_chunk granules (an event each): a pod waiting for a retired pod's 128 granules gets
+  // the first ones after ~2 ms of zeroing, not after all of it
   void scrub(const std::vector<int>& idx) {
     if (idx.empty()) return;
     std::vector<int> s(idx);
     std::sort(s.begin(), s.end());
-    for (size_t i = 0; i < s.size();) {  // one memset per run of adjacent granules
-      size_t j = i + 1;
-      while (j < s.size() && s[j] == s[j - 1] + 1) ++j;
-      CK(hipMemsetAsync(base + size_t(s[i]) * gran, 0, gran * (j - i), stream));
-      i = j;
+    size_t step = scrub_chunk > 0 ? size_t(scrub_chunk) : s.size();
+    for (size_t c = 0; c < s.size(); c += step) {
+      size_t e = std::min(s.size(), c + step);
+      for (size_t i = c; i < e;) {  // one memset per run of adjacent granules
+        size_t j = i + 1;
+        while (j < e && s[j] == s[j - 1] + 1) ++j;
+        CK(hipMemsetAsync(base + size_t(s[i]) * gran, 0, gran * (j - i), stream));
+        i = j;
+      }
+      hipEvent_t ev;
+      CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+      CK(hipEventRecord(ev, stream));
+      scrubbing.push_back({std::vector<int>(s.begin() + long(c), s.begin() + long(e)), ev, now_s()});
     }
-    hipEvent_t ev;
-    CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    CK(hipEventRecord(ev, stream));
-    scrubbing.push_back({std::move(s), ev, now_s()});
   }
 
   // scrubs whose event has completed (they complete in stream order): granules back to the free list
@@ -748,6 +755,7 @@ int main(int argc, char** argv) {
     else if (k == "--max-per-peer") b.max_per_peer = std::strtoull(v, nullptr, 10);
     else if (k == "--request-timeout-s") b.request_timeout_s = std::atof(v);
     else if (k == "--release-policy") policy = v;
+    else if (k == "--scrub-chunk") b.scrub_chunk = std::atoi(v);
     else {
       std::fprintf(stderr, "gpushare-hbm-broker: unknown flag %s\n", k.c_str());
       return 2;

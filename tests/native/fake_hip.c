@@ -252,9 +252,25 @@ hipError_t hipMemExportToShareableHandle(void* out, uint64_t h, int type, unsign
   *(int*)out = fd; return 0;
 }
 static size_t g_memset_bytes = 0;
-hipError_t hipMemsetAsync(void* p, int v, size_t n, void* s) { __atomic_add_fetch(&g_memset_bytes, n, __ATOMIC_RELAXED); return 0; }
+/* FAKE_HIP_MEMSET_MS_PER_GIB: the stream zeroes at that pace, one memset after another; an event
+   recorded after them completes when they have */
+static double g_stream_busy = 0;
+static double fake_now(void);
+hipError_t hipMemsetAsync(void* p, int v, size_t n, void* s) {
+  __atomic_add_fetch(&g_memset_bytes, n, __ATOMIC_RELAXED);
+  const char* pace = getenv("FAKE_HIP_MEMSET_MS_PER_GIB");
+  if (pace) {
+    double t = fake_now(), start = g_stream_busy > t ? g_stream_busy : t;
+    g_stream_busy = start + (double)n / (double)(1ull << 30) * atof(pace) / 1e3;
+  }
+  return 0;
+}
 hipError_t hipStreamCreateWithFlags(void** s, unsigned f) { *s = (void*)0x1; return 0; }
-hipError_t hipStreamSynchronize(void* s) { return 0; }
+hipError_t hipStreamSynchronize(void* s) {
+  double w = g_stream_busy - fake_now();
+  if (w > 0) { struct timespec t = {(time_t)w, (long)((w - (time_t)w) * 1e9)}; nanosleep(&t, 0); }
+  return 0;
+}
 hipError_t hipSetDevice(int d) { return 0; }
 hipError_t hipDeviceGetByPCIBusId(int* d, const char* bdf) { *d = 0; return 0; }
 const char* hipGetErrorString(hipError_t e) { return "fake hip error"; }
@@ -270,7 +286,8 @@ hipError_t hipEventCreateWithFlags(void** e, unsigned f) {
 hipError_t hipEventCreate(void** e) { return hipEventCreateWithFlags(e, 0); }
 hipError_t hipEventRecord(void* e, void* s) {
   const char* ms = getenv("FAKE_HIP_EVENT_MS");
-  ((struct fake_event*)e)->done_at = fake_now() + (ms ? atof(ms) : 0.0) / 1e3;
+  double at = fake_now() + (ms ? atof(ms) : 0.0) / 1e3;
+  ((struct fake_event*)e)->done_at = g_stream_busy > at ? g_stream_busy : at;
   return 0;
 }
 hipError_t hipEventQuery(void* e) { return fake_now() >= ((struct fake_event*)e)->done_at ? 0 : 600; /* hipErrorNotReady */ }

@@ -194,6 +194,35 @@ def test_streaming_take_gets_what_is_free_at_once_and_the_rest_as_it_comes_back(
         p.close()
 
 
+@pytest.mark.parametrize("chunk", [2, 0])
+def test_a_released_pods_granules_are_lent_as_their_scrub_progresses(broker_exe, tmp_path, chunk):
+    """The broker zeroes a released pod's granules in chunks (--scrub-chunk, an event each): a
+    streaming taker gets the first ones once their chunk is zeroed, not after the whole release.
+    The stub GPU zeroes 100 ms per granule here; 6 granules come back, 4 are owed."""
+    b = Broker(broker_exe, str(tmp_path / "hbm0.sock"), extra=("--scrub-chunk", str(chunk)),
+               env={"FAKE_HIP_MEMSET_MS_PER_GIB": "100"})
+    try:
+        b.admin(f"GRANT {'h' * 32} {6 * GIB}")
+        b.admin(f"GRANT {'s' * 32} {6 * GIB}")
+        holder = Pod(b.path, "h" * 32)
+        assert holder.result()[0] == f"FDS 6 {GIB}"
+        st = StreamPod(b.path, "s" * 32)
+        assert st.result()[0] == f"FDS 2 {GIB} 6"
+        t0 = time.perf_counter()
+        holder.close()
+        got = []
+        while sum(n for n, _ in got) < 4:
+            head = st.more()[0]
+            got.append((int(head.split()[1]), time.perf_counter() - t0))
+        if chunk:
+            assert [n for n, _ in got] == [2, 2] and got[0][1] < 0.35 and 0.35 < got[1][1] < 0.8, got
+        else:
+            assert [n for n, _ in got] == [4] and got[0][1] > 0.55, got
+        st.close()
+    finally:
+        b.stop()
+
+
 def test_a_revoked_streamer_is_sent_no_more(broker):
     broker.admin(f"GRANT {'h' * 32} {7 * GIB}")
     broker.admin(f"GRANT {'r' * 32} {4 * GIB}")
