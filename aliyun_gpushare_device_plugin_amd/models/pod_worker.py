@@ -80,11 +80,12 @@ def _arena_stream() -> dict | None:
            "first_access_ms": round(v[8].value / 1e6, 3)}
     try:
         g = ctypes.CDLL(None).gpushare_shim_arena_first
-        g.argtypes = [ctypes.POINTER(ctypes.c_uint64)] * 2
-        w = [ctypes.c_uint64() for _ in range(2)]
+        g.argtypes = [ctypes.POINTER(ctypes.c_uint64)] * 3
+        w = [ctypes.c_uint64() for _ in range(3)]
         if g(*(ctypes.byref(x) for x in w)):
             out["first_import_ms"] = round(w[0].value / 1e6, 3)
             out["first_map_ms"] = round(w[1].value / 1e6, 3)
+            out["answer_ms"] = round(w[2].value / 1e6, 3)
     except AttributeError:
         pass
     return out

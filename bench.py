@@ -698,9 +698,9 @@ class PodFleet:
         for k in ("wait_ms", "map_ms"):               # a streaming TAKE: owed granules, inside "alloc"
             if k in stream:
                 self.phase_ms.setdefault(f"alloc_more_{k[:-3]}", []).append(stream[k] / 1e3)
-        for k in ("first_reserve_ms", "first_access_ms", "first_import_ms", "first_map_ms"):   # parts of init_take_map
-            if k in stream:
-                self.phase_ms.setdefault(f"init_take_{k[6:-3]}", []).append(stream[k] / 1e3)
+        for k in ("first_reserve_ms", "first_access_ms", "first_import_ms", "first_map_ms", "answer_ms"):
+            if k in stream:        # parts of init_take_map (first_*) and of init_take_wait (answer)
+                self.phase_ms.setdefault(f"init_take_{k[:-3]}", []).append(stream[k] / 1e3)
         if "first" in stream:      # a count, stored /1e3 so the line's ms conversion prints it as is
             self.phase_ms.setdefault("init_take_first_batch_granules", []).append(stream["first"] / 1e3)
         if self.trace is not None:

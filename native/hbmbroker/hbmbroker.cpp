@@ -225,6 +225,9 @@ struct Broker {
   unsigned long long takes = 0, releases = 0, refused = 0, timeouts = 0, busy = 0, idle_dropped = 0,
                      revokes = 0, peer_refused = 0, streamed = 0, more_msgs = 0;
   double scrub_s_total = 0, scrub_s_last = 0, setup_s = 0;
+  // where the event loop's time goes: the longest pass, a release's bookkeeping, enqueueing a
+  // scrub, and how long TAKEs waited to be answered
+  double loop_s_max = 0, release_s_max = 0, scrub_enqueue_s_max = 0, take_wait_s_last = 0, take_wait_s_max = 0;
   unsigned long long scrubbed_bytes = 0;
 
   hipMemAllocationProp prop_{};
@@ -312,6 +315,7 @@ struct Broker {
   // the first ones after ~2 ms of zeroing, not after all of it
   void scrub(const std::vector<int>& idx) {
     if (idx.empty()) return;
+    double t_enq = now_s();
     std::vector<int> s(idx);
     std::sort(s.begin(), s.end());
     size_t step = scrub_chunk > 0 ? size_t(scrub_chunk) : s.size();
@@ -328,6 +332,7 @@ struct Broker {
       CK(hipEventRecord(ev, stream));
       scrubbing.push_back({std::vector<int>(s.begin() + long(c), s.begin() + long(e)), ev, now_s()});
     }
+    scrub_enqueue_s_max = std::max(scrub_enqueue_s_max, now_s() - t_enq);
   }
 
   // scrubs whose event has completed (they complete in stream order): granules back to the free list
@@ -446,6 +451,8 @@ struct Broker {
       c.held = idx;
       c.owed = n - int(idx.size());
       ++takes;
+      take_wait_s_last = now_s() - c.wait_since;
+      take_wait_s_max = std::max(take_wait_s_max, take_wait_s_last);
       streamed += c.stream;
       if (c.owed > 0) blocked = true;
       if (!send_fds(c.fd, idx, "FDS", c.stream ? n : -1)) dead.push_back(o.second);
@@ -476,6 +483,12 @@ struct Broker {
 
   // the granules a connection held; takes over `pfd` (the holder's pidfd, or -1)
   void release(const std::vector<int>& idx, int pfd) {
+    double t0 = now_s();
+    release_inner(idx, pfd);
+    release_s_max = std::max(release_s_max, now_s() - t0);
+  }
+
+  void release_inner(const std::vector<int>& idx, int pfd) {
     if (policy == kTrust) {
       if (pfd >= 0) close(pfd);
       scrub(idx);
@@ -577,7 +590,7 @@ struct Broker {
       owed += size_t(kv.second.owed);
     }
     for (auto& s : scrubbing) scrub_n += s.idx.size();
-    char b[2048];
+    char b[4096];
     std::snprintf(b, sizeof b,
                   "{\"boot\": \"%s\", \"device\": %d, \"granule_bytes\": %zu, \"granules\": %d, \"granules_max\": %d, "
                   "\"grown\": %llu, \"free\": %zu, "
@@ -586,13 +599,16 @@ struct Broker {
                   "\"expired\": %llu, \"busy\": %llu, \"idle_dropped\": %llu, \"peer_refused\": %llu, "
                   "\"clients\": %zu, \"quarantined\": %zu, \"quarantined_total\": %llu, \"lost\": %llu, "
                   "\"release_policy\": \"%s\", \"quarantine_ms_last\": %.1f, \"quarantine_ms_max\": %.1f, \"held_refs_max\": %d, \"base_refs\": %d, \"scrubbed_bytes\": %llu, "
-                  "\"scrub_ms_total\": %.3f, \"scrub_ms_last\": %.3f, \"setup_ms\": %.1f}\n",
+                  "\"scrub_ms_total\": %.3f, \"scrub_ms_last\": %.3f, \"setup_ms\": %.1f, \"loop_ms_max\": %.3f, "
+                  "\"release_ms_max\": %.3f, \"scrub_enqueue_ms_max\": %.3f, \"take_wait_ms_last\": %.3f, "
+                  "\"take_wait_ms_max\": %.3f}\n",
                   boot.c_str(), device, gran, count, count_max, grown, free_list.size(), held, owed, streamed, more_msgs, scrub_n, waiting, grants.size(), takes,
                   releases, refused, revokes, revoked.size(), timeouts, expired, busy, idle_dropped, peer_refused,
                   clients.size(), quarantined(), quarantined_total, lost, policy_name(), quarantine_s_last * 1e3,
                   quarantine_s_max * 1e3, held_refs_max(),
                   base_refs.empty() ? -1 : base_refs[0], scrubbed_bytes, scrub_s_total * 1e3, scrub_s_last * 1e3,
-                  setup_s * 1e3);
+                  setup_s * 1e3, loop_s_max * 1e3, release_s_max * 1e3, scrub_enqueue_s_max * 1e3,
+                  take_wait_s_last * 1e3, take_wait_s_max * 1e3);
     return b;
   }
 
@@ -806,6 +822,7 @@ int main(int argc, char** argv) {
     int timeout = !b.scrubbing.empty() ? 1 : !b.quarantine.empty() ? 3 : 100;
     int r = poll(pf.data(), pf.size(), timeout);
     if (r < 0 && errno != EINTR) break;
+    double t_pass = now_s();
     for (int k = 0; k < 2 && r > 0; ++k)
       if (pf[k].revents & POLLIN)
         for (int j = 0; j < 64 && b.accept_one(pf[k].fd, k == 1); ++j) {
@@ -865,6 +882,7 @@ int main(int argc, char** argv) {
       b.grow();
     }
     if (back || !late.empty()) b.serve_waiting();
+    b.loop_s_max = std::max(b.loop_s_max, now_s() - t_pass);
     // with a TTL, grants of pods that never started (deleted before admission) do not pile up;
     // without one (the default) the plugin's revocations do that
     if (b.grant_ttl_s > 0)

@@ -1221,6 +1221,7 @@ uint64_t g_take_connect_ns = 0, g_take_wait_ns = 0, g_take_map_ns = 0;
 uint64_t g_more_wait_ns = 0, g_more_map_ns = 0, g_more_msgs = 0, g_more_waits = 0;
 uint64_t g_take_first = 0, g_take_reserve_ns = 0, g_take_access_ns = 0;  // the TAKE's first batch
 uint64_t g_first_import_ns = 0, g_first_map_ns = 0;  // the process's first granule
+uint64_t g_take_header_ns = 0;                       // TAKE sent -> the broker's answer line
 
 uint64_t mono_ns() {
   timespec t;
@@ -1401,7 +1402,9 @@ void arena_take() {
   }
   {
     line[0] = 0;
-    int k = recv_line(s, line, sizeof line) ? sscanf(line, "FDS %llu %llu %llu", &want, &gran, &total) : 0;
+    bool got_line = recv_line(s, line, sizeof line);
+    g_take_header_ns = mono_ns() - t_conn;
+    int k = got_line ? sscanf(line, "FDS %llu %llu %llu", &want, &gran, &total) : 0;
     if (k == 2) total = want;
     if (k < 2 || total == 0 || want > total || total > (unsigned long long)kArenaMaxGranules || gran == 0) {
       logf(1, "hbm broker %s refused the grant: %s", path, line);
@@ -2151,10 +2154,12 @@ GS_EXPORT int gpushare_shim_arena_stream(uint64_t* waits, uint64_t* wait_ns, uin
   return on;
 }
 
-// the process's first granule import and map (ns): the runtime's one-time work inside the TAKE
-GS_EXPORT int gpushare_shim_arena_first(uint64_t* import_ns, uint64_t* map_ns) {
+// the process's first granule import and map (ns): the runtime's one-time work inside the TAKE;
+// and how long the TAKE waited for the broker's answer line
+GS_EXPORT int gpushare_shim_arena_first(uint64_t* import_ns, uint64_t* map_ns, uint64_t* header_ns) {
   if (import_ns) *import_ns = g_first_import_ns;
   if (map_ns) *map_ns = g_first_map_ns;
+  if (header_ns) *header_ns = g_take_header_ns;
   return g_first_import_ns != 0;
 }
 
