@@ -1411,10 +1411,17 @@ void arena_take() {
       goto fail;
     }
   }
-  while (got < (int)want)
-    if (!recv_fd_batch(s, fds, &got, (int)want)) goto fail;
-  t_fds = mono_ns();
-  logf(2, "hbm broker: %d fds of %llu bytes received", got, gran);
+  {
+    uint64_t t_h = mono_ns();
+    int batches = 0;
+    while (got < (int)want) {
+      if (!recv_fd_batch(s, fds, &got, (int)want)) goto fail;
+      ++batches;
+    }
+    t_fds = mono_ns();
+    logf(1, "hbm broker: answer after %.3f ms; %d of %llu granules' fds in %d message(s), %.3f ms",
+         g_take_header_ns / 1e6, got, total, batches, (t_fds - t_h) / 1e6);
+  }
   {
     Depth d;
     if (getdev_f(&dev) != hipSuccess) goto fail;
