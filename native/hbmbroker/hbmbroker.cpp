@@ -228,6 +228,7 @@ struct Broker {
   // where the event loop's time goes: the longest pass, a release's bookkeeping, enqueueing a
   // scrub, and how long TAKEs waited to be answered
   double loop_s_max = 0, release_s_max = 0, scrub_enqueue_s_max = 0, take_wait_s_last = 0, take_wait_s_max = 0;
+  double send_s_max = 0, last_send_at = 0;  // sending a batch of fds; wall clock of the last one
   unsigned long long scrubbed_bytes = 0;
 
   hipMemAllocationProp prop_{};
@@ -374,6 +375,16 @@ struct Broker {
 
   // the header ("FDS <k> <gran>[ <total>]" or "MORE <k> <gran>"), then the fds
   bool send_fds(int fd, const std::vector<int>& idx, const char* verb = "FDS", int total = -1) {
+    double t0 = now_s();
+    bool ok = send_fds_inner(fd, idx, verb, total);
+    send_s_max = std::max(send_s_max, now_s() - t0);
+    timespec w;
+    clock_gettime(CLOCK_REALTIME, &w);
+    last_send_at = double(w.tv_sec) + double(w.tv_nsec) * 1e-9;
+    return ok;
+  }
+
+  bool send_fds_inner(int fd, const std::vector<int>& idx, const char* verb, int total) {
     char head[96];
     int n = total >= 0 ? std::snprintf(head, sizeof head, "%s %zu %zu %d\n", verb, idx.size(), gran, total)
                        : std::snprintf(head, sizeof head, "%s %zu %zu\n", verb, idx.size(), gran);
@@ -601,14 +612,14 @@ struct Broker {
                   "\"release_policy\": \"%s\", \"quarantine_ms_last\": %.1f, \"quarantine_ms_max\": %.1f, \"held_refs_max\": %d, \"base_refs\": %d, \"scrubbed_bytes\": %llu, "
                   "\"scrub_ms_total\": %.3f, \"scrub_ms_last\": %.3f, \"setup_ms\": %.1f, \"loop_ms_max\": %.3f, "
                   "\"release_ms_max\": %.3f, \"scrub_enqueue_ms_max\": %.3f, \"take_wait_ms_last\": %.3f, "
-                  "\"take_wait_ms_max\": %.3f}\n",
+                  "\"take_wait_ms_max\": %.3f, \"send_ms_max\": %.3f, \"last_send_at\": %.6f}\n",
                   boot.c_str(), device, gran, count, count_max, grown, free_list.size(), held, owed, streamed, more_msgs, scrub_n, waiting, grants.size(), takes,
                   releases, refused, revokes, revoked.size(), timeouts, expired, busy, idle_dropped, peer_refused,
                   clients.size(), quarantined(), quarantined_total, lost, policy_name(), quarantine_s_last * 1e3,
                   quarantine_s_max * 1e3, held_refs_max(),
                   base_refs.empty() ? -1 : base_refs[0], scrubbed_bytes, scrub_s_total * 1e3, scrub_s_last * 1e3,
                   setup_s * 1e3, loop_s_max * 1e3, release_s_max * 1e3, scrub_enqueue_s_max * 1e3,
-                  take_wait_s_last * 1e3, take_wait_s_max * 1e3);
+                  take_wait_s_last * 1e3, take_wait_s_max * 1e3, send_s_max * 1e3, last_send_at);
     return b;
   }
 

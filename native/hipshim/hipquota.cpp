@@ -1419,8 +1419,10 @@ void arena_take() {
       ++batches;
     }
     t_fds = mono_ns();
-    logf(1, "hbm broker: answer after %.3f ms; %d of %llu granules' fds in %d message(s), %.3f ms",
-         g_take_header_ns / 1e6, got, total, batches, (t_fds - t_h) / 1e6);
+    timespec w;
+    clock_gettime(CLOCK_REALTIME, &w);
+    logf(1, "hbm broker: answer after %.3f ms; %d of %llu granules' fds in %d message(s), %.3f ms; at %.6f",
+         g_take_header_ns / 1e6, got, total, batches, (t_fds - t_h) / 1e6, double(w.tv_sec) + w.tv_nsec * 1e-9);
   }
   {
     Depth d;
