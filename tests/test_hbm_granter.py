@@ -250,7 +250,7 @@ def test_broker_down_for_good_answers_lose_the_token_and_get_it_back(stub_runtim
         b = broker(stub_runtime, host)
         b.start()
         wait_for(lambda: g.submit(0, g.token("u3", 0), QUOTA), what="readiness")
-        assert len(calls) >= 2
+        wait_for(lambda: len(calls) >= 2, what="the engine told again")   # (at the end of that pass)
         assert g.flush() and set(b.list()["grants"]) >= {g.token("u1", 0), g.token("u3", 0)}
     finally:
         g.stop()
