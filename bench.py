@@ -275,6 +275,7 @@ class ControlPlane:
         self.ref_splits: list = []
         self.splits: list = []
         self.steps_done = 0                     # alternates which node is admitted first
+        self.mirror_s: list = []                # the reference-model node's step inside each churn step
         self.ref_failed = 0
         self.admit_lat: list[float] = []
         self.failed = 0
@@ -316,6 +317,13 @@ class ControlPlane:
     def _mirror(self, gpu: int, size: int) -> None:
         """The same churn step on the reference-model node: retire its oldest ``size`` pod
         (preferring GPU ``gpu``) and admit a same-size replacement through its plugin."""
+        t0 = time.perf_counter()
+        try:
+            self._mirror_step(gpu, size)
+        finally:
+            self.mirror_s.append(time.perf_counter() - t0)
+
+    def _mirror_step(self, gpu: int, size: int) -> None:
         cands = [(g, i) for g in [gpu] + [x for x in range(self.n) if x != gpu]
                  for i, (_, sz) in enumerate(self.ref_resident[g]) if sz == size]
         if not cands:
@@ -659,7 +667,9 @@ class PodFleet:
         starts right after its admission); its state is allocated once the GPU has room."""
         w = self.standby.pop(0)
         self._spawn()                                   # replenish while this one initialises
+        t_sb = time.perf_counter()
         self._wait(w, "standby")
+        self.phase_ms.setdefault("standby_wait", []).append(time.perf_counter() - t_sb)
         env = dict(rec["env"])
         env.pop("LD_PRELOAD", None)                     # preloaded since exec (same host path)
         if not self.visible_by_uuid:                    # modelled node (fake SMI): this rank's GPU
@@ -1044,6 +1054,7 @@ def main():
         cp.ref_splits.clear()
         cp.splits.clear()
         cp.ref_failed = 0
+        cp.mirror_s.clear()
         cp.cp_time = 0.0
         cp.failed = 0
         cp.fail_reasons.clear()
@@ -1200,6 +1211,9 @@ def main():
             # (init) -> physical room for its state (room) -> state allocated + first GEMM (alloc)
             "pod_phase_p50_ms": {k: ms(pct(v, 0.5)) for k, v in phases.items()},
             "control_plane_ms_per_admission": round(cp.cp_time / max(1, admissions) * 1e3, 3),
+            # the reference-model node's own churn step runs inside each timed step (the
+            # allocate_under_churn comparison): its share of ms_per_step
+            "reference_mirror_ms_per_step": round(sum(cp.mirror_s) / max(1, len(cp.mirror_s)) * 1e3, 3) if cp.mirror_s else None,
             "allocate_p50_ms_by_gpu": {str(g): ms(pct(v, 0.5)) for g, v in cp.alloc_lat_by_gpu.items()},
             # both plugins during the same timed churn (alternating admissions, same pod load)
             "allocate_under_churn": under_churn,
