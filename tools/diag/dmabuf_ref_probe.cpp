@@ -302,12 +302,17 @@ extern "C" const char* dmabuf_ref_probe(int warm) {
   (void)H(hipRuntimeGetVersion)(&rt);
   rec("runtime_version", rt);
   rec("warm", warm);
-  if (warm) {
+  if (warm) {  // bit 0: a hipMalloc first; bit 1: a hipMemset + sync on it as well
     void* m = nullptr;
     long t = now_us();
     rec("warm_malloc", sym<hipError_t (*)(void**, size_t)>("hipMalloc")(&m, 64 << 20));
-    rec("warm_memset", sym<hipError_t (*)(void*, int, size_t)>("hipMemset")(m, 0, 64 << 20));
-    rec("warm_sync", H(hipDeviceSynchronize)());
+    rec("warm_malloc_us", now_us() - t);
+    if (warm & 2) {
+      long t2 = now_us();
+      rec("warm_memset", sym<hipError_t (*)(void*, int, size_t)>("hipMemset")(m, 0, 64 << 20));
+      rec("warm_sync", H(hipDeviceSynchronize)());
+      rec("warm_memset_us", now_us() - t2);
+    }
     rec("warm_us", now_us() - t);
     (void)H(hipFree)(m);
   }
