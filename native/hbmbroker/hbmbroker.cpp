@@ -667,8 +667,9 @@ struct Broker {
     unsigned long long bytes = 0;
     char extra = 0;
     if (c.admin && std::sscanf(line.c_str(), "GRANT %128s %llu %c", tok, &bytes, &extra) == 2 && valid_token(tok)) {
-      // in granules, without overflow: bytes beyond the broker are refused before rounding
-      unsigned long long cap = (unsigned long long)count * (unsigned long long)gran;
+      // in granules, without overflow: bytes beyond the broker's size are refused before rounding
+      // (a broker still growing honours a grant up to its full size as its granules arrive)
+      unsigned long long cap = (unsigned long long)count_max * (unsigned long long)gran;
       if (bytes == 0 || bytes > cap) {
         ++refused;
         reply(fd, "ERR size\n");
@@ -801,10 +802,11 @@ int main(int argc, char** argv) {
   size_t fr = 0, tot = 0;
   CK(hipMemGetInfo(&fr, &tot));
   b.reserve_bytes = size_t(reserve_gib * double(1ull << 30));
-  // sized for the device (or --gib); what is not free yet is taken as it comes back (grow)
+  // sized for the device (or --gib); what is not free yet is taken as it comes back (grow): pods
+  // of a previous broker instance, or memory amdgpu is still wiping after another process
   size_t target = gib > 0 ? size_t(gib * double(1ull << 30)) : (tot > b.reserve_bytes ? tot - b.reserve_bytes : 0);
-  size_t free_now = gib > 0 ? target : (fr > b.reserve_bytes ? fr - b.reserve_bytes : 0);
-  if (gib > 0) b.reserve_bytes = fr > target ? fr - target : 0;
+  if (gib > 0) b.reserve_bytes = size_t(2) << 30;  // --gib: leave the driver a small margin while growing
+  size_t free_now = fr > b.reserve_bytes ? fr - b.reserve_bytes : 0;
   b.setup(target, std::min(target, free_now));
   bool counted = !b.base_refs.empty() && b.base_refs[0] >= 0;
   b.policy = policy == "refs" ? kRefs : policy == "exit" ? kExit : policy == "trust" ? kTrust : (counted ? kRefs : kExit);

@@ -55,12 +55,25 @@ else:
 """
 
 
+def _full(b, timeout=60.0):
+    """Start-up completes when the broker holds its full size: right after another test, amdgpu
+    may still be wiping that test's memory, and the broker takes it as it comes back (grow)."""
+    deadline = time.time() + timeout
+    st = b.stat()
+    while (st["granules"] < st["granules_max"] or st["scrubbing"]) and time.time() < deadline:
+        time.sleep(0.2)
+        st = b.stat()
+    assert st["granules"] == st["granules_max"], st
+    return b
+
+
 @pytest.fixture
 def broker(tmp_path):
     from aliyun_gpushare_device_plugin_amd.quota.hbmbroker import HBMBroker
 
     b = HBMBroker(str(tmp_path / "hbm.sock"), device=0, gib=8, wait_s=20)
     b.start()
+    _full(b)
     yield b
     b.stop()
 
@@ -196,7 +209,7 @@ def test_launcher_brings_up_the_broker_of_every_gpu_by_pci_address(tmp_path):
     sup = cli.Supervisor(brokers)
     try:
         sup.start()
-        b = brokers[gpus[0].index]
+        b = _full(brokers[gpus[0].index])
         assert b.stat()["granules"] == 8 and b.stat()["release_policy"] == "refs"
         assert b.socket_path == str(d / f"gpu{gpus[0].index}" / f"hbm{gpus[0].index}.sock")
         b.grant("e" * 32, 6 * GIB)
@@ -223,6 +236,7 @@ def test_broker_under_asan(tmp_path, monkeypatch):
     b.start()
     rc = None
     try:
+        _full(b)
         b.grant("s" * 32, 6 * GIB)
         holder = _tenant(b, "s" * 32, "hold")
         assert json.loads(holder.stdout.readline())["arena"] == 1
@@ -363,6 +377,7 @@ def test_pytorch_allocators_fill_their_quota_from_the_arena(tmp_path, conf):
     b = HBMBroker(str(tmp_path / "hbm.sock"), device=0, gib=32, wait_s=20)
     b.start()
     try:
+        _full(b)
         granted = b.grant("m" * 32, int(quota * 0.94) // GIB * GIB)
         r, delta, err = run(dict(base_env, GPUSHARE_HBM_BROKER=b.socket_path, GPUSHARE_HBM_TOKEN="m" * 32))
         unsupported = "expandable_segments not supported" in err
@@ -404,6 +419,7 @@ def test_vmm_pages_come_from_the_arena(tmp_path, fill):
     b = HBMBroker(str(tmp_path / "hbm.sock"), device=0, gib=32, wait_s=20)
     b.start()
     try:
+        _full(b)
         quota = 24 * GIB
         granted = b.grant("v" * 32, int(quota * 0.94) // GIB * GIB)
         env = dict(os.environ, LD_PRELOAD=ensure_built("hipshim"), GPUSHARE_QUOTA_BYTES=str(quota),
