@@ -468,6 +468,34 @@ def test_hostile_input_ends_only_that_connection(broker):
     assert oct(os.stat(adm).st_mode & 0o777) == "0o600"
 
 
+def test_a_sized_broker_grows_while_memory_comes_back_and_streams_grants_meanwhile(broker_exe, tmp_path):
+    """--gib N right after another process freed its memory (amdgpu still wiping it; the stub
+    holds 8 of 16 GiB for 1.5 s): the broker starts with what is free less a 2 GiB margin, grows to
+    N as the memory comes back, accepts grants up to N at once, and a streaming TAKE gets its
+    granules as they are created."""
+    exe, libdir = broker_exe
+    env = dict(os.environ, LD_LIBRARY_PATH=libdir, ASAN_OPTIONS="detect_leaks=0:halt_on_error=1",
+               FAKE_HIP_TOTAL_GIB="16", FAKE_HIP_HELD_GIB="8", FAKE_HIP_HELD_MS="1500")
+    path = str(tmp_path / "hbm0.sock")
+    p = subprocess.Popen([exe, "--socket", path, "--gib", "10", "--release-policy", "trust"],
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
+    try:
+        ready = json.loads(p.stdout.readline())
+        assert ready["granules"] == 6                       # 16 - 8 held - 2 margin
+        assert _line(path + ".admin", f"GRANT {'g' * 32} {9 * GIB}") == "OK 9"     # up to the full 10
+        assert _line(path + ".admin", f"GRANT {'x' * 32} {11 * GIB}") == "ERR size"
+        pod = StreamPod(path, "g" * 32)
+        assert pod.result()[0] == f"FDS 6 {GIB} 9"
+        head = pod.more(timeout=10)[0]                      # the rest once grown and zeroed
+        assert head == f"MORE 3 {GIB}", head
+        st = json.loads(_line(path + ".admin", "STAT"))
+        assert st["granules"] == 10 and st["grown"] == 4 and st["owed"] == 0, st
+        pod.close()
+    finally:
+        p.terminate()
+        assert p.wait(10) == 0
+
+
 def test_a_restarted_broker_grows_back_when_old_tenants_exit(broker_exe, tmp_path):
     """After a broker restart, pods of the previous instance still hold their granules (imported
     dma-bufs keep the memory alive, measured on MI355X: docs/HBM_TURNOVER.md, exporter death).
