@@ -55,6 +55,25 @@ else:
 """
 
 
+@pytest.fixture(scope="module", autouse=True)
+def _device_memory_back():
+    """Tests of other modules run in this pytest process, and PyTorch's caching allocator keeps
+    what they allocated (Llama-3-8B and friends: most of the GPU). The brokers here need it: hand
+    it back to the driver first (amdgpu then wipes it, and the brokers take it as it returns)."""
+    import gc
+
+    gc.collect()
+    try:
+        import torch
+
+        if torch.cuda.is_initialized():
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+    except ImportError:
+        pass
+    yield
+
+
 def _full(b, timeout=60.0):
     """Start-up completes when the broker holds its full size: right after another test, amdgpu
     may still be wiping that test's memory, and the broker takes it as it comes back (grow)."""
