@@ -4,7 +4,5 @@ set -o pipefail
 D=gpurun_out/r5prof
 mkdir -p $D
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $D/prof -o run -- python3 bench.py --gpus 1 --steps 10 --warmup 3 --driver-path-steps 0 --compare-rtts "" --fill-orders "" > $D/bench.json 2> $D/bench.err
+timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $D/prof -o run_%pid% -- python3 bench.py --gpus 1 --steps 10 --warmup 3 --driver-path-steps 0 --compare-rtts "" --fill-orders "" > $D/bench.json 2> $D/bench.err
 echo "prof rc=$?" >> $D/steps.log
-timeout -k 10 420 python bench.py --gpus 1 --steps 20 --warmup 5 > $D/bench_n1.json 2> $D/bench_n1.err
-echo "bench rc=$?" >> $D/steps.log
