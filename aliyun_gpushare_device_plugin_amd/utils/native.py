@@ -31,6 +31,12 @@ class NativeUnavailable(RuntimeError):
     pass
 
 
+def preload(*libs: str) -> str:
+    """LD_PRELOAD for a child process: ``libs`` first, then whatever this process already
+    preloads (a profiler, the host's own libraries), which the child keeps."""
+    return ":".join(x for x in (*libs, os.environ.get("LD_PRELOAD", "")) if x)
+
+
 def lib_path(target: str) -> str:
     """``GPUSHARE_NATIVE_VARIANT=asan|tsan`` selects a sanitizer build (native/build.py
     --sanitize) from ``_native/<variant>/``; the matching runtime must be LD_PRELOADed."""

@@ -634,7 +634,10 @@ class PodFleet:
         return read, total
 
     def _spawn(self):
-        env = dict(os.environ, LD_PRELOAD=os.path.join(NATIVE, "libgpushare_hipquota.so"),
+        # the shim first; whatever this process already preloads (a profiler, the host's own
+        # libraries) stays preloaded in the pods too
+        pre = ":".join(x for x in (os.path.join(NATIVE, "libgpushare_hipquota.so"), os.environ.get("LD_PRELOAD", "")) if x)
+        env = dict(os.environ, LD_PRELOAD=pre,
                    PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""), GS_POD_NICE="5")
         for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
                   "TORCHELASTIC_RUN_ID", "GROUP_RANK", "ROLE_RANK"):
@@ -800,7 +803,8 @@ class StubFleet:
         from aliyun_gpushare_device_plugin_amd import const
 
         env = dict(os.environ, **rec["env"])
-        env.update(LD_PRELOAD=os.path.join(NATIVE, "libgpushare_hipquota.so"), LD_LIBRARY_PATH=self.stub_dir,
+        env.update(LD_PRELOAD=":".join(x for x in (os.path.join(NATIVE, "libgpushare_hipquota.so"),
+                                                   os.environ.get("LD_PRELOAD", "")) if x), LD_LIBRARY_PATH=self.stub_dir,
                    FAKE_HIP_TOTAL_GIB="288", GPUSHARE_HBM_WAIT_S="30")
         quota = int(env.get(const.ENV_SHIM_QUOTA_BYTES, 0))
         t0 = time.perf_counter()

@@ -6,6 +6,7 @@ import sys
 import textwrap
 
 import pytest
+from aliyun_gpushare_device_plugin_amd.utils.native import preload
 
 from aliyun_gpushare_device_plugin_amd import const
 from aliyun_gpushare_device_plugin_amd.device import smi as S
@@ -143,7 +144,7 @@ def _probe(args, **env):
     """native/probes/shim_probe.hip under the shim (LD_PRELOAD, like a container process)."""
     from aliyun_gpushare_device_plugin_amd.utils.native import ensure_built
     exe = os.path.join(os.path.dirname(ensure_built("hipshim")), "shim_probe")
-    e = dict(os.environ, LD_PRELOAD=ensure_built("hipshim"), GPUSHARE_SHIM_LOG="1")
+    e = dict(os.environ, LD_PRELOAD=preload(ensure_built("hipshim")), GPUSHARE_SHIM_LOG="1")
     e.update({k: str(v) for k, v in env.items()})
     r = subprocess.run([exe, *map(str, args)], env=e, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -332,7 +333,7 @@ def test_shim_charges_render_node_gem_vram():
 
     with S.SMI("auto") as smi:
         minor = smi.device(0).render_minor
-    env = dict(os.environ, LD_PRELOAD=lib_path("hipshim"), GPUSHARE_QUOTA_BYTES=str(4 * GIB),
+    env = dict(os.environ, LD_PRELOAD=preload(lib_path("hipshim")), GPUSHARE_QUOTA_BYTES=str(4 * GIB),
                GPUSHARE_SHIM_LOG="1")
     r = subprocess.run([sys.executable, "-c", _GEM_CHILD, str(minor), str(2 * GIB), str(3 * GIB), str(GIB)],
                        env=env, capture_output=True, text=True, timeout=60)
@@ -431,7 +432,7 @@ def test_shim_gem_escapes_are_closed():
 
     with S.SMI("auto") as smi:
         minor = smi.device(0).render_minor
-    env = dict(os.environ, LD_PRELOAD=lib_path("hipshim"), GPUSHARE_QUOTA_BYTES=str(4 * GIB),
+    env = dict(os.environ, LD_PRELOAD=preload(lib_path("hipshim")), GPUSHARE_QUOTA_BYTES=str(4 * GIB),
                GPUSHARE_SHIM_LOG="1")
     r = subprocess.run([sys.executable, "-c", _GEM_ESCAPES, str(minor)], env=env, capture_output=True, text=True,
                        timeout=90)

@@ -5,6 +5,7 @@ import os
 import subprocess
 
 import pytest
+from aliyun_gpushare_device_plugin_amd.utils.native import preload
 
 from aliyun_gpushare_device_plugin_amd.device import smi as S
 from aliyun_gpushare_device_plugin_amd.utils.native import NATIVE_DIR
@@ -203,7 +204,7 @@ def test_gpuinfo_under_sanitizers(san):
     rt = subprocess.run(["gcc", f"-print-file-name=lib{san}.so"], capture_output=True, text=True).stdout.strip()
     if not os.path.exists(rt):
         pytest.skip(f"lib{san}.so not installed")
-    env = dict(os.environ, LD_PRELOAD=rt, GPUSHARE_NATIVE_VARIANT=san, PYTHONPATH=root,
+    env = dict(os.environ, LD_PRELOAD=preload(rt), GPUSHARE_NATIVE_VARIANT=san, PYTHONPATH=root,
                ASAN_OPTIONS="detect_leaks=0:halt_on_error=1", UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1",
                TSAN_OPTIONS="halt_on_error=1:report_signal_unsafe=0")
     r = subprocess.run([sys.executable, "-c", _SAN_SCRIPT], env=env, capture_output=True, text=True, timeout=180)

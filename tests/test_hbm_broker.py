@@ -14,6 +14,7 @@ import sys
 import time
 
 import pytest
+from aliyun_gpushare_device_plugin_amd.utils.native import preload
 
 pytestmark = pytest.mark.gpu
 
@@ -112,7 +113,7 @@ def _settled(broker, timeout=5.0) -> dict:
 def _tenant(broker, token, mode, extra_env=None, **kw):
     from aliyun_gpushare_device_plugin_amd.utils.native import ensure_built
 
-    env = dict(os.environ, LD_PRELOAD=ensure_built("hipshim"), GPUSHARE_QUOTA_BYTES=str(8 * GIB),
+    env = dict(os.environ, LD_PRELOAD=preload(ensure_built("hipshim")), GPUSHARE_QUOTA_BYTES=str(8 * GIB),
                GPUSHARE_HBM_BROKER=broker.socket_path, GPUSHARE_HBM_TOKEN=token, GPUSHARE_SHIM_LOG="1",
                PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""), **(extra_env or {}))
     return subprocess.Popen([sys.executable, "-c", TENANT, mode], env=env, stdin=subprocess.PIPE,
@@ -371,7 +372,7 @@ def test_pytorch_allocators_fill_their_quota_from_the_arena(tmp_path, conf):
     from aliyun_gpushare_device_plugin_amd.utils.native import ensure_built
 
     quota = 24 * GIB
-    base_env = dict(os.environ, LD_PRELOAD=ensure_built("hipshim"), GPUSHARE_QUOTA_BYTES=str(quota),
+    base_env = dict(os.environ, LD_PRELOAD=preload(ensure_built("hipshim")), GPUSHARE_QUOTA_BYTES=str(quota),
                     PYTORCH_HIP_ALLOC_CONF=conf, PYTORCH_CUDA_ALLOC_CONF=conf)
 
     def run(env):
@@ -441,7 +442,7 @@ def test_vmm_pages_come_from_the_arena(tmp_path, fill):
         _full(b)
         quota = 24 * GIB
         granted = b.grant("v" * 32, int(quota * 0.94) // GIB * GIB)
-        env = dict(os.environ, LD_PRELOAD=ensure_built("hipshim"), GPUSHARE_QUOTA_BYTES=str(quota),
+        env = dict(os.environ, LD_PRELOAD=preload(ensure_built("hipshim")), GPUSHARE_QUOTA_BYTES=str(quota),
                    GPUSHARE_HBM_BROKER=b.socket_path, GPUSHARE_HBM_TOKEN="v" * 32)
         r = subprocess.run([exe, str(fill)], env=env, capture_output=True, text=True, timeout=120)
         lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]

@@ -22,6 +22,7 @@ import time
 import uuid
 
 import pytest
+from aliyun_gpushare_device_plugin_amd.utils.native import preload
 
 from aliyun_gpushare_device_plugin_amd.cli import hbmbroker as cli
 from aliyun_gpushare_device_plugin_amd.quota import hbmbroker as hb
@@ -40,7 +41,7 @@ def broker(stub, host, gpu=0, gib=12, policy="exit"):
 def pod(stub, native_shim, host, token, args, gpu=0, wait_s=30, **extra_env):
     """A pod's container process: the stub runtime under the quota shim, its env as the plugin's
     answer gives it (host paths: no container here)."""
-    env = dict(os.environ, LD_PRELOAD=native_shim, LD_LIBRARY_PATH=stub, GPUSHARE_QUOTA_BYTES=str(QUOTA),
+    env = dict(os.environ, LD_PRELOAD=preload(native_shim), LD_LIBRARY_PATH=stub, GPUSHARE_QUOTA_BYTES=str(QUOTA),
                GPUSHARE_LEDGER=f"/gs-test-{uuid.uuid4().hex[:12]}", GPUSHARE_HBM_BROKER=hb.pod_socket(str(host), gpu),
                GPUSHARE_HBM_TOKEN=token, GPUSHARE_HBM_WAIT_S=str(wait_s), **{k: str(v) for k, v in extra_env.items()})
     return subprocess.Popen([os.path.join(stub, "shim_driver"), *map(str, args)], env=env, stdin=subprocess.PIPE,

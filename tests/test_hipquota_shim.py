@@ -12,6 +12,7 @@ import subprocess
 import uuid
 
 import pytest
+from aliyun_gpushare_device_plugin_amd.utils.native import preload
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 GIB = 1 << 30
@@ -178,7 +179,7 @@ def test_shared_ledger_across_processes(stub, native_shim):
     name = ledger()
     try:
         d, drv = stub
-        env = dict(os.environ, LD_PRELOAD=native_shim, LD_LIBRARY_PATH=str(d), GPUSHARE_LEDGER=name,
+        env = dict(os.environ, LD_PRELOAD=preload(native_shim), LD_LIBRARY_PATH=str(d), GPUSHARE_LEDGER=name,
                    GPUSHARE_QUOTA_BYTES=str(4 * GIB))
         holder = subprocess.Popen([str(drv), "alloc", str(3 * GIB), "sleep", "3"], env=env,
                                   stdout=subprocess.PIPE, text=True)
@@ -262,7 +263,7 @@ def test_file_backed_ledger_is_readable_by_the_plugin(stub, native_shim, tmp_pat
     uid = "0b6f1c2e-aaaa-bbbb-cccc-0123456789ab"
     name = ledger_name(uid, 0)
     d, drv = stub
-    env = dict(os.environ, LD_PRELOAD=native_shim, LD_LIBRARY_PATH=str(d), GPUSHARE_LEDGER=name,
+    env = dict(os.environ, LD_PRELOAD=preload(native_shim), LD_LIBRARY_PATH=str(d), GPUSHARE_LEDGER=name,
                GPUSHARE_LEDGER_DIR=str(tmp_path), GPUSHARE_QUOTA_BYTES=str(4 * GIB))
     holder = subprocess.Popen([str(drv), "alloc", str(3 * GIB), "alloc", str(2 * GIB), "sleep", "3"], env=env,
                               stdout=subprocess.PIPE, text=True)
@@ -301,7 +302,7 @@ def test_per_container_ledger_dirs_and_gc_after_sigkill(stub, native_shim, tmp_p
     for uid in ("uid-a", "uid-b"):
         lkey = ld.new_key(uid, 0)
         keys[uid] = lkey
-        env = dict(os.environ, LD_PRELOAD=native_shim, LD_LIBRARY_PATH=str(d), GPUSHARE_LEDGER=ledger_name(uid, 0),
+        env = dict(os.environ, LD_PRELOAD=preload(native_shim), LD_LIBRARY_PATH=str(d), GPUSHARE_LEDGER=ledger_name(uid, 0),
                    GPUSHARE_LEDGER_DIR=ld.create(lkey, uid), GPUSHARE_QUOTA_BYTES=str(4 * GIB))
         procs.append(subprocess.Popen([str(drv), "alloc", str(1 * GIB), "sleep", "30"], env=env,
                                       stdout=subprocess.PIPE, text=True))
@@ -640,7 +641,7 @@ def test_the_fd_table_is_grown_at_load(native_shim, reserve):
     import resource
 
     soft, _ = resource.getrlimit(resource.RLIMIT_NOFILE)
-    env = dict(os.environ, LD_PRELOAD=native_shim, GPUSHARE_SHIM_FD_RESERVE="1" if reserve else "0")
+    env = dict(os.environ, LD_PRELOAD=preload(native_shim), GPUSHARE_SHIM_FD_RESERVE="1" if reserve else "0")
     out = subprocess.run(["cat", "/proc/self/status"], env=env, capture_output=True, text=True, check=True).stdout
     size = int(next(ln.split()[1] for ln in out.splitlines() if ln.startswith("FDSize:")))
     if reserve and soft >= 256:
@@ -677,7 +678,7 @@ def test_broker_arena_under_sanitizers(stub, tmp_path, san):
     sock = str(tmp_path / "hbm.sock")
     b = FakeBroker(sock, granules=2)
     name = ledger()
-    env = dict(os.environ, LD_PRELOAD=f"{rt}:{lib}", LD_LIBRARY_PATH=str(d), GPUSHARE_LEDGER=name,
+    env = dict(os.environ, LD_PRELOAD=preload(rt, lib), LD_LIBRARY_PATH=str(d), GPUSHARE_LEDGER=name,
                GPUSHARE_QUOTA_BYTES=str(4 * GIB), GPUSHARE_HBM_BROKER=sock, GPUSHARE_HBM_TOKEN="t",
                ASAN_OPTIONS="detect_leaks=0:halt_on_error=1", UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1",
                TSAN_OPTIONS="halt_on_error=1:report_bugs=1")

@@ -14,6 +14,7 @@ import time
 
 import grpc
 import pytest
+from aliyun_gpushare_device_plugin_amd.utils.native import preload
 
 from aliyun_gpushare_device_plugin_amd import const
 from aliyun_gpushare_device_plugin_amd.alloc.engine import Allocator, AllocatorOptions, _native_blob
@@ -271,7 +272,7 @@ print(srv.stats()["fast"] + srv.stats()["forwarded"])
 srv.stop()
 print("SAN-OK")
 """
-    env = dict(os.environ, LD_PRELOAD=rt, GPUSHARE_NATIVE_VARIANT=san, PYTHONPATH=root,
+    env = dict(os.environ, LD_PRELOAD=preload(rt), GPUSHARE_NATIVE_VARIANT=san, PYTHONPATH=root,
                ASAN_OPTIONS="detect_leaks=0:halt_on_error=1", UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1",
                TSAN_OPTIONS="halt_on_error=1:report_signal_unsafe=0:ignore_noninstrumented_modules=1")
     r = subprocess.run([sys.executable, "-c", script], env=env, capture_output=True, text=True, timeout=300)

@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import json
 import os
+from aliyun_gpushare_device_plugin_amd.utils.native import preload
 import signal
 import subprocess
 import sys
@@ -60,7 +61,7 @@ def main() -> int:
     b = HBMBroker.for_gpu(d, 0, device=0, gib=16, wait_s=20)
     out["broker"] = b.start()
     b.grant("x" * 32, 8 * GIB)
-    env = dict(os.environ, LD_PRELOAD=ensure_built("hipshim"), GPUSHARE_QUOTA_BYTES=str(12 * GIB),
+    env = dict(os.environ, LD_PRELOAD=preload(ensure_built("hipshim")), GPUSHARE_QUOTA_BYTES=str(12 * GIB),
                GPUSHARE_HBM_BROKER=b.socket_path, GPUSHARE_HBM_TOKEN="x" * 32)
     t = subprocess.Popen([sys.executable, "-c", TENANT], env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE,
                          stderr=subprocess.PIPE, text=True)

@@ -8,6 +8,7 @@ sys.path.insert(0, os.path.join(os.getcwd(), "tests"))
 import test_hbm_broker as T
 from aliyun_gpushare_device_plugin_amd.quota.hbmbroker import HBMBroker
 
+from aliyun_gpushare_device_plugin_amd.utils.native import preload
 TENANT = r"""
 import ctypes, json, sys, time
 import torch
@@ -39,7 +40,7 @@ try:
     b.grant("y" * 32, 6 << 30)
     import subprocess
     from aliyun_gpushare_device_plugin_amd.utils.native import ensure_built
-    env = dict(os.environ, LD_PRELOAD=ensure_built("hipshim"), GPUSHARE_QUOTA_BYTES=str(8 << 30),
+    env = dict(os.environ, LD_PRELOAD=preload(ensure_built("hipshim")), GPUSHARE_QUOTA_BYTES=str(8 << 30),
                GPUSHARE_HBM_BROKER=b.socket_path, GPUSHARE_HBM_TOKEN="y" * 32)
     p = subprocess.Popen([sys.executable, "-c", TENANT], env=env, stdout=subprocess.PIPE, text=True)
     first = json.loads(p.stdout.readline())

@@ -24,7 +24,7 @@ def main():
     out = {}
     with SMI("auto") as s:
         out["idle"] = vram_used(s)
-        env = dict(os.environ, LD_PRELOAD=SHIM, PYTHONPATH=ROOT)
+        env = dict(os.environ, LD_PRELOAD=":".join(x for x in (SHIM, os.environ.get("LD_PRELOAD", "")) if x), PYTHONPATH=ROOT)
         p = subprocess.Popen([sys.executable, "-m", "aliyun_gpushare_device_plugin_amd.models.pod_worker"], env=env,
                              stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, bufsize=1)
         assert json.loads(p.stdout.readline())["event"] == "standby"

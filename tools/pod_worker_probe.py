@@ -14,7 +14,7 @@ SHIM = os.path.join(ROOT, "aliyun_gpushare_device_plugin_amd", "_native", "libgp
 
 
 def spawn():
-    env = dict(os.environ, LD_PRELOAD=SHIM, PYTHONPATH=ROOT)
+    env = dict(os.environ, LD_PRELOAD=":".join(x for x in (SHIM, os.environ.get("LD_PRELOAD", "")) if x), PYTHONPATH=ROOT)
     t = time.perf_counter()
     p = subprocess.Popen([sys.executable, "-m", "aliyun_gpushare_device_plugin_amd.models.pod_worker"], env=env,
                          stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, bufsize=1)
