@@ -4,5 +4,5 @@ set -o pipefail
 D=gpurun_out/r5prof
 mkdir -p $D
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $D/prof -o run_%pid% -- python3 bench.py --gpus 1 --steps 10 --warmup 3 --driver-path-steps 0 --compare-rtts "" --fill-orders "" > $D/bench.json 2> $D/bench.err
+GS_POD_CLEAN_EXIT=1 timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $D/prof -o run_%pid% -- python3 bench.py --gpus 1 --steps 10 --warmup 3 --driver-path-steps 0 --compare-rtts "" --fill-orders "" > $D/bench.json 2> $D/bench.err
 echo "prof rc=$?" >> $D/steps.log
