@@ -153,7 +153,8 @@ def build_dpserver(force=False, asan=False):
 
 def build_hbmbroker(force=False, asan=False):
     """gpushare-hbm-broker: lends each pod VMM granules of HBM it holds, scrubbed between pods
-    (docs/HBM_TURNOVER.md). Host code only: the scrub is hipMemsetAsync."""
+    (docs/HBM_TURNOVER.md). Host code built by g++; its scrub kernel (scrub.hip) is a gfx950 code
+    object it loads at start."""
     src = _src("hbmbroker", "hbmbroker.cpp")
     if not os.path.exists(src):
         return []
@@ -167,7 +168,12 @@ def build_hbmbroker(force=False, asan=False):
     os.makedirs(os.path.dirname(exe), exist_ok=True)
     if force or _newer(exe, [src]):
         _run([CXX, *flags, "-o", exe, src, f"-L{ROCM}/lib", "-lamdhip64", f"-Wl,-rpath,{ROCM}/lib", "-pthread"])
-    return [exe]
+    # its scrub kernel: a gfx950 code object next to the executable, loaded with hipModuleLoad
+    ksrc = _src("hbmbroker", "scrub.hip")
+    co = os.path.join(os.path.dirname(exe), "gpushare-hbm-scrub.co")
+    if os.path.exists(ksrc) and (force or _newer(co, [ksrc])):
+        _run([HIPCC, "--genco", f"--offload-arch={ARCH}", "-O3", "-o", co, ksrc])
+    return [exe, co] if os.path.exists(ksrc) else [exe]
 
 
 def build_kernels(force=False, asan=False, jobs=4):

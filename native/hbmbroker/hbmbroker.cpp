@@ -36,9 +36,10 @@
 // The boot id changes with every start. The plugin polls STAT, and on a new boot id it re-grants
 // every live pod's token: a broker restart loses no grant that a pod still needs.
 //
-// Scrubs are asynchronous: a released pod's granules are zeroed by hipMemsetAsync on the broker's
-// stream and lent again once the stream's event has completed, so GRANT, TAKE and STAT are
-// served while the GPU zeroes.
+// Scrubs are asynchronous: a released pod's granules are zeroed on the broker's stream by its
+// scrub kernel (scrub.hip: non-temporal 16 B stores; hipMemsetAsync if the code object is
+// missing), in chunks of --scrub-chunk granules with an event each, and each chunk is lent again
+// once its event has completed. GRANT, TAKE and STAT are served while the GPU zeroes.
 //
 // Release policy (--release-policy): before a released granule is lent again, "refs" waits until
 // no reference to its dma-buf is left outside the broker (fdinfo "count:"), "exit" waits until
@@ -51,6 +52,7 @@
 //                       [--granule-mib 1024] [--wait-s 30] [--ungranted-wait-s 10]
 //                       [--grant-ttl-s 0] [--max-clients 1024] [--max-per-peer 8]
 //                       [--request-timeout-s 2] [--release-policy auto] [--scrub-chunk 8]
+//                       [--scrub-kernel <dir of this executable>/gpushare-hbm-scrub.co]
 #include <hip/hip_runtime.h>
 
 #include <fcntl.h>
@@ -232,6 +234,11 @@ struct Broker {
   unsigned long long scrubbed_bytes = 0;
 
   hipMemAllocationProp prop_{};
+  // the scrub kernel (scrub.hip, a code object next to the executable): zeroes at HBM write
+  // bandwidth with non-temporal stores; hipMemsetAsync when it is not there
+  hipModule_t scrub_mod = nullptr;
+  hipFunction_t scrub_fn = nullptr;
+  std::string scrub_path;
   int count_max = 0;          // granules the broker is sized for (its address range)
   size_t reserve_bytes = 0;   // what it leaves to the driver
   unsigned long long grown = 0;
@@ -243,6 +250,29 @@ struct Broker {
     d.location.id = device;
     d.flags = hipMemAccessFlagsProtReadWrite;
     return d;
+  }
+
+  void load_scrub_kernel() {
+    if (scrub_path.empty() || access(scrub_path.c_str(), R_OK) != 0) return;
+    if (hipModuleLoad(&scrub_mod, scrub_path.c_str()) != hipSuccess ||
+        hipModuleGetFunction(&scrub_fn, scrub_mod, "gs_scrub") != hipSuccess) {
+      scrub_fn = nullptr;
+      (void)hipGetLastError();
+      std::fprintf(stderr, "gpushare-hbm-broker: scrub kernel %s not loaded: zeroing with hipMemsetAsync\n",
+                   scrub_path.c_str());
+    }
+  }
+
+  // zero [p, p + bytes) on the broker's stream
+  void zero(char* p, size_t bytes) {
+    if (scrub_fn && bytes % 16 == 0 && reinterpret_cast<uintptr_t>(p) % 16 == 0) {
+      uint64_t n16 = bytes / 16;
+      uint64_t blocks = std::min<uint64_t>(2048, (n16 + 255) / 256);  // 8 blocks of 4 waves per CU
+      void* args[] = {&p, &n16};
+      CK(hipModuleLaunchKernel(scrub_fn, unsigned(blocks), 1, 1, 256, 1, 1, 0, stream, args, nullptr));
+      return;
+    }
+    CK(hipMemsetAsync(p, 0, bytes, stream));
   }
 
   // granule i: created, exported, mapped in the broker's range (not yet zeroed)
@@ -278,7 +308,8 @@ struct Broker {
     hipMemAccessDesc d = rw();
     if (count) CK(hipMemSetAccess(base, gran * count, &d, 1));
     CK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-    if (count) CK(hipMemsetAsync(base, 0, gran * count, stream));  // nobody sees what was there before
+    load_scrub_kernel();
+    if (count) zero(base, gran * count);  // nobody sees what was there before
     CK(hipStreamSynchronize(stream));
     for (int i = 0; i < count; ++i) base_refs[i] = refs(i);
     setup_s = now_s() - t0;
@@ -325,7 +356,7 @@ struct Broker {
       for (size_t i = c; i < e;) {  // one memset per run of adjacent granules
         size_t j = i + 1;
         while (j < e && s[j] == s[j - 1] + 1) ++j;
-        CK(hipMemsetAsync(base + size_t(s[i]) * gran, 0, gran * (j - i), stream));
+        zero(base + size_t(s[i]) * gran, gran * (j - i));
         i = j;
       }
       hipEvent_t ev;
@@ -609,13 +640,14 @@ struct Broker {
                   "\"releases\": %llu, \"refused\": %llu, \"revokes\": %llu, \"revoked\": %zu, \"timeouts\": %llu, "
                   "\"expired\": %llu, \"busy\": %llu, \"idle_dropped\": %llu, \"peer_refused\": %llu, "
                   "\"clients\": %zu, \"quarantined\": %zu, \"quarantined_total\": %llu, \"lost\": %llu, "
-                  "\"release_policy\": \"%s\", \"quarantine_ms_last\": %.1f, \"quarantine_ms_max\": %.1f, \"held_refs_max\": %d, \"base_refs\": %d, \"scrubbed_bytes\": %llu, "
+                  "\"scrub_kernel\": \"%s\", \"release_policy\": \"%s\", \"quarantine_ms_last\": %.1f, \"quarantine_ms_max\": %.1f, \"held_refs_max\": %d, \"base_refs\": %d, \"scrubbed_bytes\": %llu, "
                   "\"scrub_ms_total\": %.3f, \"scrub_ms_last\": %.3f, \"setup_ms\": %.1f, \"loop_ms_max\": %.3f, "
                   "\"release_ms_max\": %.3f, \"scrub_enqueue_ms_max\": %.3f, \"take_wait_ms_last\": %.3f, "
                   "\"take_wait_ms_max\": %.3f, \"send_ms_max\": %.3f, \"last_send_at\": %.6f}\n",
                   boot.c_str(), device, gran, count, count_max, grown, free_list.size(), held, owed, streamed, more_msgs, scrub_n, waiting, grants.size(), takes,
                   releases, refused, revokes, revoked.size(), timeouts, expired, busy, idle_dropped, peer_refused,
-                  clients.size(), quarantined(), quarantined_total, lost, policy_name(), quarantine_s_last * 1e3,
+                  clients.size(), quarantined(), quarantined_total, lost, scrub_fn ? "gs_scrub" : "memset", policy_name(),
+                  quarantine_s_last * 1e3,
                   quarantine_s_max * 1e3, held_refs_max(),
                   base_refs.empty() ? -1 : base_refs[0], scrubbed_bytes, scrub_s_total * 1e3, scrub_s_last * 1e3,
                   setup_s * 1e3, loop_s_max * 1e3, release_s_max * 1e3, scrub_enqueue_s_max * 1e3,
@@ -784,6 +816,7 @@ int main(int argc, char** argv) {
     else if (k == "--request-timeout-s") b.request_timeout_s = std::atof(v);
     else if (k == "--release-policy") policy = v;
     else if (k == "--scrub-chunk") b.scrub_chunk = std::atoi(v);
+    else if (k == "--scrub-kernel") b.scrub_path = v;
     else {
       std::fprintf(stderr, "gpushare-hbm-broker: unknown flag %s\n", k.c_str());
       return 2;
@@ -796,6 +829,15 @@ int main(int argc, char** argv) {
     return 2;
   }
   if (admin.empty()) admin = sock + ".admin";
+  if (b.scrub_path.empty()) {  // default: next to this executable
+    char self[4096];
+    ssize_t n = readlink("/proc/self/exe", self, sizeof self - 1);
+    if (n > 0) {
+      self[n] = 0;
+      std::string dir(self);
+      b.scrub_path = dir.substr(0, dir.rfind('/') + 1) + "gpushare-hbm-scrub.co";
+    }
+  }
   b.gran = gran_mib << 20;
   if (!pci.empty()) CK(hipDeviceGetByPCIBusId(&b.device, pci.c_str()));
   CK(hipSetDevice(b.device));
@@ -821,8 +863,9 @@ int main(int argc, char** argv) {
   int pod_ls = listen_unix(sock, 0666);
   int adm_ls = listen_unix(admin, 0600);
   std::printf("{\"ready\": true, \"boot\": \"%s\", \"socket\": \"%s\", \"admin_socket\": \"%s\", \"granules\": %d, "
-              "\"granule_bytes\": %zu, \"release_policy\": \"%s\", \"setup_ms\": %.1f}\n",
-              b.boot.c_str(), sock.c_str(), admin.c_str(), b.count, b.gran, b.policy_name(), b.setup_s * 1e3);
+              "\"granule_bytes\": %zu, \"release_policy\": \"%s\", \"scrub_kernel\": \"%s\", \"setup_ms\": %.1f}\n",
+              b.boot.c_str(), sock.c_str(), admin.c_str(), b.count, b.gran, b.policy_name(),
+              b.scrub_fn ? "gs_scrub" : "memset", b.setup_s * 1e3);
   std::fflush(stdout);
 
   std::vector<pollfd> pf;
