@@ -501,7 +501,10 @@ class FakeBroker:
                     conn.close()
                     self.closed_at = time.monotonic()
                     return
-                send(f"MORE {k} {self.gran}\n", k)
+                try:
+                    send(f"MORE {k} {self.gran}\n", k)
+                except OSError:           # the pod already handed its arena back
+                    break
         else:
             send(f"FDS {self.granules} {self.gran}\n", self.granules)
         while conn.recv(1):
@@ -664,9 +667,13 @@ def test_broker_refusal_leaves_the_pod_on_the_driver(stub, native_shim, tmp_path
         cleanup(name)
 
 
+@pytest.mark.parametrize("mode", ["whole", "stream"])
 @pytest.mark.parametrize("san", ["asan", "tsan"])
-def test_broker_arena_under_sanitizers(stub, tmp_path, san):
-    """8 threads allocating and freeing from the broker arena at once, under ASan+UBSan / TSan."""
+def test_broker_arena_under_sanitizers(stub, tmp_path, san, mode):
+    """Threads allocating and freeing from the broker arena at once, under ASan+UBSan / TSan:
+    8 threads in a 2-granule arena, or ("stream") 3 threads of 1 GiB blocks in a 3-granule grant
+    of which 1 granule is there at first and 2 arrive 0.2 s later, so two threads wait for the
+    owed granules while the third allocates and frees."""
     import sys
     sys.path.insert(0, os.path.join(HERE, "..", "native"))
     import build as nb
@@ -676,19 +683,20 @@ def test_broker_arena_under_sanitizers(stub, tmp_path, san):
         pytest.skip(f"lib{san}.so not installed")
     d, drv = stub
     sock = str(tmp_path / "hbm.sock")
-    b = FakeBroker(sock, granules=2)
+    b = FakeBroker(sock, granules=2) if mode == "whole" else FakeBroker(sock, granules=3, stream=[(0.2, 2)])
     name = ledger()
     env = dict(os.environ, LD_PRELOAD=preload(rt, lib), LD_LIBRARY_PATH=str(d), GPUSHARE_LEDGER=name,
                GPUSHARE_QUOTA_BYTES=str(4 * GIB), GPUSHARE_HBM_BROKER=sock, GPUSHARE_HBM_TOKEN="t",
                ASAN_OPTIONS="detect_leaks=0:halt_on_error=1", UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1",
                TSAN_OPTIONS="halt_on_error=1:report_bugs=1")
     try:
-        r = subprocess.run([str(drv), "threads", "8", "300", str(64 * MIB), "arena", "arenarelease"], env=env,
+        nt, it, sz = (8, 300, 64 * MIB) if mode == "whole" else (3, 20, GIB)
+        r = subprocess.run([str(drv), "threads", str(nt), str(it), str(sz), "arena", "arenarelease"], env=env,
                            capture_output=True, text=True, timeout=120)
         assert r.returncode == 0, r.stderr[-3000:]
         out = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
-        assert out[0]["ok"] == 8 * 300 and out[0]["denied"] == 0
-        assert out[1] == {"op": "arena", "on": 1, "size": 2 * GIB, "used": 0}
+        assert out[0]["ok"] == nt * it and out[0]["denied"] == 0
+        assert out[1] == {"op": "arena", "on": 1, "size": (2 if mode == "whole" else 3) * GIB, "used": 0}
         assert out[2]["r"] == 1 and b.took == "TAKE t STREAM"
     finally:
         cleanup(name)
