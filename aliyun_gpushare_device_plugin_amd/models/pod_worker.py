@@ -147,7 +147,8 @@ def main() -> int:
         # the container is up before the GPU has room for its state (the driver may still be
         # wiping the HBM a retired pod freed): report, then allocate on "alloc"
         _send({"event": "inited", "init_ms": round((time.perf_counter() - t0) * 1e3, 3),
-               "runtime_ms": round((t_up - t_rt) * 1e3, 3), "take_ms": take})
+               "runtime_ms": round((t_up - t_rt) * 1e3, 3), "cuda_init_ms": round((t_rt - t0) * 1e3, 3),
+               "take_ms": take})
         nxt = json.loads(sys.stdin.readline() or "{}")
         if nxt.get("cmd") != "alloc":
             return 0

@@ -688,6 +688,9 @@ class PodFleet:
         inited = self._wait(w, "inited")
         t1 = time.perf_counter()
         take = inited.get("take_ms") or {}
+        for k, name in (("cuda_init_ms", "init_cuda_init"), ("runtime_ms", "init_first_alloc")):
+            if k in inited:       # torch.cuda.init(); the first allocation (the TAKE inside it)
+                self.phase_ms.setdefault(name, []).append(inited[k] / 1e3)
         for k in ("connect", "wait", "map"):          # the broker TAKE inside init (shim timing)
             if k in take:
                 self.phase_ms.setdefault(f"init_take_{k}", []).append(take[k] / 1e3)
