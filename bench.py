@@ -1205,6 +1205,9 @@ def main():
             "allocate_p50_ms": ms(pct(cp.alloc_lat, 0.5)),
             "allocate_p99_ms": ms(pct(cp.alloc_lat, 0.99)),
             "allocate_breakdown_p50_ms": breakdown(cp.splits),
+            # the slowest Allocate of the run, leg by leg: where its tail comes from
+            "allocate_slowest_ms": (lambda w: {"total": ms(sum(w)), **{k: ms(w[i]) for i, k in enumerate(
+                ("kubelet_to_handler", "handler", "handler_to_kubelet"))}})(max(cp.splits, key=sum)) if cp.splits else None,
             "plugin_allocate_p50_ms": ms(srv["p50"]) if srv else None,
             "plugin_allocate_p99_ms": ms(srv["p99"]) if srv else None,
             "plugin_allocate_phase_p50_ms": {k: ms(v) for k, v in srv["phases"].items() if v is not None}
