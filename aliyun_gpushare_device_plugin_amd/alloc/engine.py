@@ -182,6 +182,9 @@ class Allocator(NativeTable):
         self.prestart_hooks: list = []          # run at PreStartContainer (after the placement pass)
         self._ledgers = self._ledger_dir(self.opts)
         self._hbm = self._hbm_granter(self.opts, live=self._hbm_live, on_readiness=self._hbm_readiness)
+        if self._hbm is not None and not getattr(self, "_hbm_metrics", False):
+            self.metrics.registry.add_collector(lambda: self._hbm.exposition() if self._hbm is not None else "")
+            self._hbm_metrics = True
         self.podres = None
         self._overlay: dict[str, dict] = {}       # uid -> annotations written, not yet landed
         self._overlay_gen: dict[str, int] = {}
@@ -310,6 +313,9 @@ class Allocator(NativeTable):
                 if old is not None:
                     old.stop()
                 self._hbm = self._hbm_granter(self.opts, live=self._hbm_live, on_readiness=self._hbm_readiness)
+            if self._hbm is not None and not getattr(self, "_hbm_metrics", False):
+                self.metrics.registry.add_collector(lambda: self._hbm.exposition() if self._hbm is not None else "")
+                self._hbm_metrics = True
             self._pinfo.clear()
             self._bump_gen()
             self._fast = None

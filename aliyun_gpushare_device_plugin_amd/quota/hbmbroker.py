@@ -251,6 +251,7 @@ class _GPUState:
     absent: dict = dataclasses.field(default_factory=dict)   # token -> first time no live pod needed it
     reported: bool | None = None                              # readiness last told to on_readiness
     restarts: int = 0
+    stat: dict = dataclasses.field(default_factory=dict)      # the broker's last STAT
 
 
 class HBMGranter:
@@ -385,6 +386,41 @@ class HBMGranter:
                     "gpus": {str(i): {"up": st.up, "boot": st.boot, "held": len(st.sent), "restarts": st.restarts}
                              for i, st in sorted(self._gpus.items())}}
 
+    def exposition(self) -> str:
+        """The brokers' state as Prometheus text, from each broker's last STAT (one per poll):
+        granules by state, takes / releases / timeouts, bytes zeroed, quarantine and scrub
+        timings, and the granter's own grant counters."""
+        with self._mu:
+            gpus = {i: (st.up, dict(st.stat), st.restarts) for i, st in self._gpus.items()}
+            own = {"grants": self.grants, "failures": self.failures, "revokes": self.revokes, "regrants": self.regrants}
+        out = ["# HELP gpushare_hbm_broker_up 1 if the GPU's HBM broker answered the last poll\n"
+               "# TYPE gpushare_hbm_broker_up gauge\n"]
+        out += [f'gpushare_hbm_broker_up{{gpu="{i}"}} {int(up)}\n' for i, (up, _, _) in sorted(gpus.items())]
+        out.append("# HELP gpushare_hbm_broker_granules Granules of the GPU's HBM broker by state\n"
+                   "# TYPE gpushare_hbm_broker_granules gauge\n")
+        for i, (_, stat, _) in sorted(gpus.items()):
+            for state in ("granules", "granules_max", "free", "held", "owed", "scrubbing", "quarantined"):
+                if state in stat:
+                    out.append(f'gpushare_hbm_broker_granules{{gpu="{i}",state="{state}"}} {stat[state]}\n')
+        for name, key, help_ in (("takes", "takes", "TAKEs served"), ("releases", "releases", "connections that returned granules"),
+                                 ("timeouts", "timeouts", "TAKEs refused after waiting"),
+                                 ("scrubbed_bytes", "scrubbed_bytes", "bytes zeroed between pods"),
+                                 ("lost", "lost", "granules never lent again (untraceable holder)")):
+            out.append(f"# HELP gpushare_hbm_broker_{name}_total {help_}\n# TYPE gpushare_hbm_broker_{name}_total counter\n")
+            out += [f'gpushare_hbm_broker_{name}_total{{gpu="{i}"}} {stat[key]}\n'
+                    for i, (_, stat, _) in sorted(gpus.items()) if key in stat]
+        out.append("# HELP gpushare_hbm_broker_restarts_total Broker restarts seen (a new boot id)\n"
+                   "# TYPE gpushare_hbm_broker_restarts_total counter\n")
+        out += [f'gpushare_hbm_broker_restarts_total{{gpu="{i}"}} {r}\n' for i, (_, _, r) in sorted(gpus.items())]
+        for key in ("quarantine_ms_max", "take_wait_ms_max", "scrub_ms_last"):
+            out.append(f"# HELP gpushare_hbm_broker_{key} From the broker's STAT\n# TYPE gpushare_hbm_broker_{key} gauge\n")
+            out += [f'gpushare_hbm_broker_{key}{{gpu="{i}"}} {stat[key]}\n'
+                    for i, (_, stat, _) in sorted(gpus.items()) if key in stat]
+        out.append("# HELP gpushare_hbm_granter_total The plugin's grant traffic to the brokers\n"
+                   "# TYPE gpushare_hbm_granter_total counter\n")
+        out += [f'gpushare_hbm_granter_total{{op="{k}"}} {v}\n' for k, v in own.items()]
+        return "".join(out)
+
     # -- the granter thread ---------------------------------------------------------------
     def _admin(self, gpu: int, line: str) -> str:
         return _request(admin_socket(self.host_dir, gpu), line, timeout=self.timeout_s)
@@ -490,6 +526,7 @@ class HBMGranter:
     def _sync_gpu(self, gpu: int, st: _GPUState, want: dict, may_revoke: bool, now: float) -> None:
         try:
             stat = json.loads(self._admin(gpu, "STAT"))
+            st.stat = stat
             boot = stat.get("boot", "")
             if boot != st.boot:
                 held = json.loads(self._admin(gpu, "LIST")).get("grants", {})

@@ -86,6 +86,34 @@ def take(path, token):
     return s, h.decode().strip()
 
 
+def test_broker_state_is_exported_as_metrics(stub_runtime, native_shim, tmp_path):
+    """The plugin's /metrics carries each broker's state from its last STAT:
+    up, granules by state, takes / releases, and the granter's own grant counters."""
+    from aliyun_gpushare_device_plugin_amd.utils.metrics import Registry
+
+    host = tmp_path / "hbm"
+    b = broker(stub_runtime, host)
+    b.start()
+    g = hb.HBMGranter(str(host), poll_s=0.1, startup_grace_s=0.0, live=lambda: {})
+    try:
+        assert g.reconcile_now()                                   # the broker is seen: answers carry tokens
+        assert g.submit(0, g.token("m1", 0), QUOTA) and g.flush()
+        p = pod(stub_runtime, native_shim, host, g.token("m1", 0), ["alloc", GIB, "arena", "freeall", "arenarelease"])
+        assert p.wait(30) == 0
+        assert g.reconcile_now()
+        reg = Registry()
+        reg.add_collector(g.exposition)
+        text = reg.render()
+        assert 'gpushare_hbm_broker_up{gpu="0"} 1' in text
+        assert 'gpushare_hbm_broker_granules{gpu="0",state="granules"} 12' in text
+        assert 'gpushare_hbm_broker_takes_total{gpu="0"} 1' in text
+        assert 'gpushare_hbm_broker_releases_total{gpu="0"} 1' in text
+        assert 'gpushare_hbm_granter_total{op="grants"} 1' in text
+    finally:
+        g.stop()
+        b.stop()
+
+
 def test_plugin_before_broker_every_pod_takes_its_arena(stub_runtime, native_shim, tmp_path):
     host = tmp_path / "hbm"
     g = hb.HBMGranter(str(host), poll_s=0.2, startup_grace_s=60.0, live=lambda: {})
