@@ -1030,20 +1030,28 @@ def main():
 
     idle = os.environ.get("GS_BENCH_IDLE_RANK")   # test hook: this rank's pipeline does nothing
 
+    step_parts: dict[str, list] = {"stop": [], "admission": [], "start": [], "total": []}
+
     def cycle():
         if idle is not None and int(idle) == rank:
             return
         uid = None
+        t0 = time.perf_counter()
         if fleet is not None:
             uid = fleet.oldest()
             if uid is not None:
                 fleet.stop(uid)                  # the replacement's start waits for the HBM
+        t1 = time.perf_counter()
         rec = svc.churn(local, uid) if rank == 0 else client.churn(local, uid)
+        t2 = time.perf_counter()
         if rec is not None:
             done["churned"] += 1
             if fleet is not None:
                 fleet.start(rec)
                 done["started"] += 1
+        t3 = time.perf_counter()
+        for k, v in (("stop", t1 - t0), ("admission", t2 - t1), ("start", t3 - t2), ("total", t3 - t0)):
+            step_parts[k].append(v)
 
     # ---- warm-up: fill the node, start its pods, then W untimed churn cycles per GPU ----
     started = bcast(cp.fill() if rank == 0 else None)
@@ -1079,6 +1087,8 @@ def main():
             v.clear()
 
     done.update(churned=0, started=0)
+    for v in step_parts.values():
+        v.clear()
     barrier()
     g0 = fleet.gemms() if fleet is not None else 0
     t0 = time.perf_counter()
@@ -1094,6 +1104,10 @@ def main():
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         elapsed, gemm_flops = float(mx[0]), float(t[1])
+    parts_all: dict = {}
+    for d_ in gather(step_parts):
+        for k, v in d_.items():
+            parts_all.setdefault(k, []).extend(v)
     ready = gather(fleet.ready_ms if fleet is not None else [])
     ready_all = [x for r in ready for x in r]
     held = gather(fleet.held_bytes if fleet is not None else 0)
@@ -1224,6 +1238,10 @@ def main():
             # the reference-model node's own churn step runs inside each timed step (the
             # allocate_under_churn comparison): its share of ms_per_step
             "reference_mirror_ms_per_step": round(sum(cp.mirror_s) / max(1, len(cp.mirror_s)) * 1e3, 3) if cp.mirror_s else None,
+            # a timed step, part by part (mean over steps and GPUs): the retired pod's stop, the
+            # admission (rank 0's control plane, the reference mirror inside), the replacement's
+            # start (standby hand-over + ready)
+            "step_parts_mean_ms": {k: round(sum(v) / len(v) * 1e3, 3) for k, v in parts_all.items() if v},
             "allocate_p50_ms_by_gpu": {str(g): ms(pct(v, 0.5)) for g, v in cp.alloc_lat_by_gpu.items()},
             # both plugins during the same timed churn (alternating admissions, same pod load)
             "allocate_under_churn": under_churn,
