@@ -668,8 +668,15 @@ class PodFleet:
         """Hand the oldest standby its pod's env; return the ready latency (seconds). The pod's
         runtime comes up while the GPU may still be wiping a retired pod's HBM (as a container
         starts right after its admission); its state is allocated once the GPU has room."""
+        if not self.standby:                            # (the pool refills in the background)
+            self._spawn()
         w = self.standby.pop(0)
-        self._spawn()                                   # replenish while this one initialises
+        # replenish the pool off this pod's path (forking this large process costs tens of ms)
+        t_sp = time.perf_counter()
+        th = threading.Thread(target=self._spawn, daemon=True)
+        th.start()
+        self._spawners = [t for t in getattr(self, "_spawners", []) if t.is_alive()] + [th]
+        self.phase_ms.setdefault("standby_spawn", []).append(time.perf_counter() - t_sp)
         t_sb = time.perf_counter()
         self._wait(w, "standby")
         self.phase_ms.setdefault("standby_wait", []).append(time.perf_counter() - t_sb)
@@ -774,6 +781,8 @@ class PodFleet:
     def close(self):
         for uid in list(self.pods):
             self.stop(uid)
+        for t in getattr(self, "_spawners", []):
+            t.join(60)                                  # every standby started is in the pool
         for w in self.standby:
             try:
                 w["proc"].stdin.close()
