@@ -1243,6 +1243,7 @@ def main():
             # one churn cycle on a GPU: stop (old pod frees) -> admission -> new pod's runtime up
             # (init) -> physical room for its state (room) -> state allocated + first GEMM (alloc)
             "pod_phase_p50_ms": {k: ms(pct(v, 0.5)) for k, v in phases.items()},
+            "pod_phase_max_ms": {k: ms(max(v)) for k, v in phases.items() if v},
             "control_plane_ms_per_admission": round(cp.cp_time / max(1, admissions) * 1e3, 3),
             # the reference-model node's own churn step runs inside each timed step (the
             # allocate_under_churn comparison): its share of ms_per_step
