@@ -47,6 +47,11 @@ def build_parser() -> argparse.ArgumentParser:
                    help="when a released granule may be lent again (hbmbroker.cpp): refs = no dma-buf reference "
                         "left outside the broker, exit = the holder's process is gone; auto = refs where the "
                         "kernel counts them")
+    p.add_argument("--scrub-chunk", type=int, default=8,
+                   help="granules zeroed per scrub event: a released pod's granules are lent again chunk by chunk")
+    p.add_argument("--scrub-kernel", default="",
+                   help="the broker's scrub code object (default: gpushare-hbm-scrub.co next to the broker); "
+                        "without it the broker zeroes with hipMemsetAsync")
     p.add_argument("--restart-backoff", type=float, default=2.0)
     return p
 
@@ -95,7 +100,10 @@ def main(argv=None) -> int:
     want = {int(x) for x in a.gpu_indices.split(",") if x.strip()}
     with SMI(a.smi_backend) as s:
         gpus = [s.device(i) for i in range(s.count())]
-    extra = ["--ungranted-wait-s", str(a.ungranted_wait_s), "--release-policy", a.release_policy]
+    extra = ["--ungranted-wait-s", str(a.ungranted_wait_s), "--release-policy", a.release_policy,
+             "--scrub-chunk", str(a.scrub_chunk)]
+    if a.scrub_kernel:
+        extra += ["--scrub-kernel", a.scrub_kernel]
     brokers = {g.index: HBMBroker.for_gpu(a.dir, g.index, pci_bus_id=g.bdf, reserve_gib=a.reserve_gib,
                                           granule_mib=a.granule_mib, wait_s=a.wait_s, extra_args=extra)
                for g in gpus if not want or g.index in want}
