@@ -67,9 +67,11 @@ def parse():
     ap.add_argument("--burst", type=int, default=8, help="GEMMs between a pod process's control checks")
     ap.add_argument("--gemm", type=int, default=4096, help="GEMM M=N=K")
     ap.add_argument("--fill", type=float, default=0.85, help="fraction of its quota a pod process holds")
-    ap.add_argument("--standby", type=int, default=6,
+    ap.add_argument("--standby", type=int, default=9,
                     help="pre-started pod interpreters per GPU (images pulled, processes created, torch imported; "
-                         "each takes ~1.5 s of CPU, so the pool must cover the admission rate)")
+                         "each takes ~1.5 s of CPU, so the pool must cover the admission rate: at ~3.5 pods/s per "
+                         "GPU a pool of 6 ran dry, up to 445 ms of waiting in a step; 9 did not, "
+                         "profiles/r5/bench_n1_standby_ab/)")
     ap.add_argument("--no-gpu", action="store_true", help="control plane only (CPU)")
     ap.add_argument("--smi-backend", default=None, help="default: auto on GPU, fake:Nx288G on CPU")
     ap.add_argument("--pod-source", default="watch", choices=("watch", "list", "kubelet"))
