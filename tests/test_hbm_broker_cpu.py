@@ -223,6 +223,27 @@ def test_a_released_pods_granules_are_lent_as_their_scrub_progresses(broker_exe,
         b.stop()
 
 
+def test_a_streamer_that_leaves_while_owed_frees_its_place(broker):
+    """A streaming taker owed granules goes away: what it held is returned and scrubbed, what it
+    was owed is forgotten, and the next taker in line is served."""
+    broker.admin(f"GRANT {'h' * 32} {6 * GIB}")
+    broker.admin(f"GRANT {'s' * 32} {5 * GIB}")
+    broker.admin(f"GRANT {'n' * 32} {2 * GIB}")
+    holder = Pod(broker.path, "h" * 32)
+    assert holder.result()[0] == f"FDS 6 {GIB}"
+    st = StreamPod(broker.path, "s" * 32)
+    assert st.result()[0] == f"FDS 2 {GIB} 5"
+    nxt = Pod(broker.path, "n" * 32)                 # a plain TAKE of 2, behind the streamer's owed 3
+    time.sleep(0.2)
+    assert broker.stat()["owed"] == 3 and broker.stat()["waiting"] == 1
+    st.close()                                       # gone while owed: its 2 come back, its 3 are forgotten
+    assert nxt.result()[0] == f"FDS 2 {GIB}"
+    s = broker.stat()
+    assert s["owed"] == 0 and s["held"] == 6 + 2
+    holder.close()
+    nxt.close()
+
+
 def test_a_revoked_streamer_is_sent_no_more(broker):
     broker.admin(f"GRANT {'h' * 32} {7 * GIB}")
     broker.admin(f"GRANT {'r' * 32} {4 * GIB}")
