@@ -6,7 +6,8 @@ Lifecycle (JSON lines on stdin/stdout):
 
 * **standby** — the interpreter is up and torch is imported, but nothing has touched the GPU
   (the analogue of a container whose image is pulled and whose process is created). Prints
-  ``{"event": "standby"}``.
+  ``{"event": "standby"}``. Standbys are fresh interpreters, or children forked from one
+  interpreter that imported torch once (``--zygote``, ``zygote()``).
 * ``{"cmd": "start", "env": {...}, "gemm": 4096, "burst": 8, "fill": 0.85}`` — the pod was
   admitted: the Allocate env (quota, ledger, visible GPU) is applied *before* the HIP runtime
   initialises, so the shim (preloaded since exec, initialised lazily at the first KFD ioctl)
@@ -113,13 +114,76 @@ def _arena_release():
     return None if r == 0 else r == 1
 
 
-def main() -> int:
+def _nice() -> None:
     nice = int(os.environ.get("GS_POD_NICE", "0") or 0)
     if nice > 0:
         # a node runs its daemons (kubelet, device plugin) ahead of container workloads
         # (system-reserved CPU); the pod's start-up must not starve the plugin's watch
         os.nice(nice)
+
+
+def zygote(ctl_fd: int) -> int:
+    """Fork standby pod processes from one interpreter that imported torch once (``--zygote FD``).
+
+    Each request on the control socket ``ctl_fd`` carries two fds, the child's stdin and stdout.
+    The zygote forks, and the child serves them as a standby pod exactly as ``main`` does. The
+    zygote answers the child's pid. Nothing here touches the GPU: the child's HIP runtime starts
+    after its ``start`` command, with the pod's env. The zygote exits when the socket closes.
+    A fresh interpreter per standby costs ~1.5 s of CPU (the torch import). At 4 pods/s that is
+    6 cores taken from the pods starting at the same time; a fork costs milliseconds."""
+    import signal
+    import socket
+
+    _nice()
+    import torch  # noqa: F401
+
+    ctl = socket.socket(fileno=ctl_fd)
+    signal.signal(signal.SIGCHLD, signal.SIG_IGN)          # the kernel reaps the children
+    while True:
+        try:
+            msg, fds, _, _ = socket.recv_fds(ctl, 16, 2)
+        except OSError:
+            return 0
+        if not msg:
+            return 0
+        if len(fds) != 2:
+            for fd in fds:
+                os.close(fd)
+            continue
+        sys.stdout.flush()
+        pid = os.fork()
+        if pid == 0:
+            try:
+                ctl.close()
+                signal.signal(signal.SIGCHLD, signal.SIG_DFL)
+                os.dup2(fds[0], 0)
+                os.dup2(fds[1], 1)
+                for fd in fds:
+                    os.close(fd)
+                rc = _pod()
+            except BaseException:  # noqa: BLE001 - a child never returns into the zygote's loop
+                import traceback
+
+                traceback.print_exc()
+                rc = 1
+            sys.stdout.flush()
+            os._exit(rc or 0)
+        for fd in fds:
+            os.close(fd)
+        ctl.sendall(f"{pid}\n".encode())
+
+
+def main() -> int:
+    if len(sys.argv) > 2 and sys.argv[1] == "--zygote":
+        return zygote(int(sys.argv[2]))
+    _nice()
     import torch  # noqa: F401 - imported in standby: the expensive part of a process start
+
+    return _pod()
+
+
+def _pod() -> int:
+    import torch
 
     _send({"event": "standby", "pid": os.getpid()})
     line = sys.stdin.readline()

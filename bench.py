@@ -21,7 +21,8 @@ Scenario (one node with N = --gpus MI355X, one rank per GPU, rank 0 also hosts t
     is deleted, a same-size replacement is created, bin-packed by the extender, admitted by the
     kubelet through the plugin's Allocate, and its process starts under the shim and runs its
     first GEMM ("pod ready"). The interpreter of the replacement is pre-started (standby: torch
-    imported, GPU untouched — an image already pulled); HIP init, quota, HBM allocation and the
+    imported, GPU untouched — an image already pulled; forked from one interpreter that imported
+    torch once, so the pool does not take CPU from starting pods); HIP init, quota, HBM allocation and the
     first GEMM are inside the timed step. By default pods take their HBM from the GPU's HBM
     broker (native/hbmbroker, docs/HBM_TURNOVER.md): VMM granules lent per pod and scrubbed
     between pods, so an admission does not wait for amdgpu's wipe of the retired pod's HBM
@@ -72,6 +73,9 @@ def parse():
                          "each takes ~1.5 s of CPU, so the pool must cover the admission rate: at ~3.5 pods/s per "
                          "GPU a pool of 6 ran dry, up to 445 ms of waiting in a step; 9 did not, "
                          "profiles/r5/bench_n1_standby_ab/)")
+    ap.add_argument("--no-pod-zygote", action="store_true",
+                    help="start each standby as a fresh interpreter (~1.5 s of CPU each) instead of forking it "
+                         "from one that imported torch once")
     ap.add_argument("--no-gpu", action="store_true", help="control plane only (CPU)")
     ap.add_argument("--smi-backend", default=None, help="default: auto on GPU, fake:Nx288G on CPU")
     ap.add_argument("--pod-source", default="watch", choices=("watch", "list", "kubelet"))
@@ -584,13 +588,97 @@ class AdmissionClient:
         self.sock.close()
 
 
+class _Forked:
+    """A pod process the zygote forked: the part of ``subprocess.Popen`` the fleet uses. It is
+    the zygote's child, so it is watched through a pidfd; its exit status is not known here."""
+
+    def __init__(self, pid: int, stdin, stdout):
+        self.pid, self.stdin, self.stdout = pid, stdin, stdout
+        self.returncode = None
+        try:
+            self._pidfd = os.pidfd_open(pid)
+        except ProcessLookupError:
+            self._pidfd, self.returncode = None, 0
+
+    def _exited(self, timeout) -> bool:
+        import select
+
+        if self._pidfd is None:
+            return True
+        r, _, _ = select.select([self._pidfd], [], [], timeout)
+        if r:
+            os.close(self._pidfd)
+            self._pidfd, self.returncode = None, 0
+        return bool(r)
+
+    def poll(self):
+        self._exited(0)
+        return self.returncode
+
+    def wait(self, timeout=None):
+        if not self._exited(timeout):
+            raise subprocess.TimeoutExpired(f"pod {self.pid}", timeout)
+        return self.returncode
+
+    def kill(self):
+        try:
+            os.kill(self.pid, 9)
+        except ProcessLookupError:
+            pass
+
+
+class _Zygote:
+    """One interpreter that imported torch and forks the standby pod processes
+    (``pod_worker.zygote``): keeping the pool full costs a fork per pod, not a torch import
+    (~1.5 s of CPU) taken from the pods that are starting at the same time."""
+
+    def __init__(self, env: dict):
+        import socket
+
+        self._sock, theirs = socket.socketpair(socket.AF_UNIX, socket.SOCK_STREAM)
+        self._proc = subprocess.Popen([sys.executable, "-m", "aliyun_gpushare_device_plugin_amd.models.pod_worker",
+                                       "--zygote", str(theirs.fileno())], env=env, pass_fds=(theirs.fileno(),),
+                                      stdin=subprocess.DEVNULL, stdout=subprocess.DEVNULL)
+        theirs.close()
+        self._rd = self._sock.makefile("r")
+        self._lock = threading.Lock()
+
+    def fork(self) -> _Forked:
+        import socket
+
+        c_in, p_in = os.pipe()          # the pod reads its commands from c_in
+        p_out, c_out = os.pipe()        # and writes its events to c_out
+        try:
+            with self._lock:
+                socket.send_fds(self._sock, [b"F"], [c_in, c_out])
+                line = self._rd.readline()
+        finally:
+            os.close(c_in)
+            os.close(c_out)
+        if not line:
+            os.close(p_in)
+            os.close(p_out)
+            raise RuntimeError(f"the pod zygote exited (status {self._proc.poll()})")
+        return _Forked(int(line), os.fdopen(p_in, "w", buffering=1), os.fdopen(p_out, "r"))
+
+    def close(self):
+        try:
+            self._rd.close()                # the socket's fd closes with its last file object
+            self._sock.close()
+            self._proc.wait(30)
+        except Exception:  # noqa: BLE001
+            self._proc.kill()
+            self._proc.wait(10)
+
+
 class PodFleet:
     """The pod processes of this rank's GPU, plus one standby process (interpreter up, torch
     imported, GPU untouched) that becomes the next admitted pod."""
 
     def __init__(self, local: int, gemm: int, burst: int, fill: float, visible_by_uuid: bool, standby: int = 2,
-                 slack: int = 2 << 30, ordinal: int | None = None, broker=None):
+                 slack: int = 2 << 30, ordinal: int | None = None, broker=None, zygote: bool = True):
         self.local, self.gemm, self.burst, self.fill, self.slack = local, gemm, burst, fill, slack
+        self._zygote = _Zygote(self._pod_env()) if zygote else None
         self.broker = broker                  # HBMBroker: pods' HBM comes from it (no driver wipe on the path)
         self.ordinal = local if ordinal is None else ordinal     # this GPU's HIP ordinal (bind_device)
         self.visible_by_uuid = visible_by_uuid
@@ -635,7 +723,8 @@ class PodFleet:
                 return int(f.read())
         return read, total
 
-    def _spawn(self):
+    @staticmethod
+    def _pod_env() -> dict:
         # the shim first; whatever this process already preloads (a profiler, the host's own
         # libraries) stays preloaded in the pods too
         pre = ":".join(x for x in (os.path.join(NATIVE, "libgpushare_hipquota.so"), os.environ.get("LD_PRELOAD", "")) if x)
@@ -644,8 +733,15 @@ class PodFleet:
         for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
                   "TORCHELASTIC_RUN_ID", "GROUP_RANK", "ROLE_RANK"):
             env.pop(k, None)
-        p = subprocess.Popen([sys.executable, "-m", "aliyun_gpushare_device_plugin_amd.models.pod_worker"], env=env,
-                             stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, bufsize=1)
+        return env
+
+    def _spawn(self):
+        if self._zygote is not None:
+            p = self._zygote.fork()
+        else:
+            p = subprocess.Popen([sys.executable, "-m", "aliyun_gpushare_device_plugin_amd.models.pod_worker"],
+                                 env=self._pod_env(), stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True,
+                                 bufsize=1)
         q: "queue.Queue" = queue.Queue()
 
         def pump():
@@ -791,6 +887,8 @@ class PodFleet:
                 w["proc"].wait(30)
             except Exception:  # noqa: BLE001
                 w["proc"].kill()
+        if self._zygote is not None:
+            self._zygote.close()
 
 
 class StubFleet:
@@ -876,6 +974,8 @@ def driver_path_run(a) -> dict:
     cmd = [sys.executable, os.path.abspath(__file__), "--gpus", "1", "--steps", str(a.driver_path_steps), "--warmup", "1",
            "--no-hbm-broker", "--compare-rtts", "", "--fill-orders", "", "--no-ref-churn", "--driver-path-steps", "0",
            "--gemm", str(a.gemm), "--fill", str(a.fill), "--standby", str(a.standby), "--json-out", out]
+    if a.no_pod_zygote:
+        cmd.append("--no-pod-zygote")
     t0 = time.perf_counter()
     try:
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
@@ -1010,7 +1110,8 @@ def main():
     # pod processes see their GPU through the Allocate response's ROCR_VISIBLE_DEVICES (UUID)
     if use_gpu:
         fleet = PodFleet(local, a.gemm, a.burst, a.fill, not smi.startswith("fake:"), a.standby,
-                         slack=int(a.room_slack_gib * (1 << 30)), ordinal=ordinal, broker=broker)
+                         slack=int(a.room_slack_gib * (1 << 30)), ordinal=ordinal, broker=broker,
+                         zygote=not a.no_pod_zygote)
     else:
         fleet = StubFleet(stub, a.fill) if stub else None
     topo_report = cp_topo = None
@@ -1224,6 +1325,7 @@ def main():
                        "pods_per_gpu": 4, "gemm_mnk": a.gemm, "pod_fill": a.fill, "pod_source": a.pod_source,
                        "smi_backend": smi, "pod_processes": use_gpu, "hbm_broker": broker is not None,
                        "standby_interpreters_per_gpu": a.standby,
+                       "standby_forked_from_zygote": not a.no_pod_zygote,
                        # the plugin's gRPC server and the simulated kubelet's Allocate client
                        "grpc_server": "native" if native_server.available() else "python",
                        "kubelet_client": "native" if NativeUnaryClient.wanted() else "grpcio"},

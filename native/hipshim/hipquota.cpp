@@ -634,9 +634,9 @@ __attribute__((constructor)) void reserve_ledger_va() {
 // (a pod whose HIP runtime is up) each growth waits for an RCU grace period. Measured on MI355X:
 // receiving 60-120 granule fds at a TAKE took 115-210 ms, 30 (no growth) 0.014 ms. A table
 // grown here, at load time, never needs to grow for the arena. GPUSHARE_SHIM_FD_RESERVE=0 skips it.
-__attribute__((constructor)) void reserve_fd_table() {
-  const char* v = getenv("GPUSHARE_SHIM_FD_RESERVE");
-  if (v && !strcmp(v, "0")) return;
+// A forked child gets a table only as large as its highest open fd, so the child grows it again
+// right after the fork, while it is still single-threaded.
+void grow_fd_table() {
   rlimit rl;
   if (getrlimit(RLIMIT_NOFILE, &rl) != 0 || rl.rlim_cur < 256) return;
   long top = long(rl.rlim_cur > 2048 ? 2048 : rl.rlim_cur) - 1;
@@ -645,6 +645,13 @@ __attribute__((constructor)) void reserve_fd_table() {
   if (d < 0) return;
   if (syscall(SYS_dup3, d, top, O_CLOEXEC) == top) syscall(SYS_close, top);
   syscall(SYS_close, d);
+}
+
+__attribute__((constructor)) void reserve_fd_table() {
+  const char* v = getenv("GPUSHARE_SHIM_FD_RESERVE");
+  if (v && !strcmp(v, "0")) return;
+  grow_fd_table();
+  pthread_atfork(nullptr, nullptr, grow_fd_table);
 }
 
 void init() {

@@ -152,3 +152,30 @@ def test_bench_fails_when_a_gpu_does_no_work():
     d = parse(r.stdout)
     assert d["admissions"] == 3 and d["admissions_by_gpu"] == {"0": 3, "1": 0}
     assert any("GPU 1" in p for p in d["run_problems"]) and "run FAILED" in r.stderr
+
+
+def test_pod_zygote_forks_standby_pods_that_serve_their_own_pipes():
+    """The bench's standby pods are forked from one interpreter that imported torch once: each
+    child answers "standby" on its own pipe, with its own pid, and exits when its stdin closes.
+    Closing the zygote ends it. (CPU: the child is told nothing more than to go away.)"""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    env = dict(os.environ, PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    z = bench._Zygote(env)
+    try:
+        kids = [z.fork() for _ in range(3)]
+        pids = set()
+        for k in kids:
+            ev = json.loads(k.stdout.readline())
+            assert ev == {"event": "standby", "pid": k.pid}
+            pids.add(k.pid)
+        assert len(pids) == 3 and z._proc.pid not in pids
+        assert all(k.poll() is None for k in kids)
+        for k in kids:
+            k.stdin.close()
+            assert k.wait(30) == 0
+            assert k.stdout.read() == ""
+    finally:
+        z.close()
+    assert z._proc.returncode == 0

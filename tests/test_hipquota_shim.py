@@ -9,6 +9,7 @@ the HIP API. Real-hardware coverage of the same paths: tests/test_gpu_native.py 
 import json
 import os
 import subprocess
+import sys
 import uuid
 
 import pytest
@@ -651,6 +652,29 @@ def test_the_fd_table_is_grown_at_load(native_shim, reserve):
         assert size >= min(soft, 2048), size
     else:
         assert size < 256, size
+
+
+def test_a_forked_child_grows_its_fd_table_again(native_shim):
+    """fork() gives the child an fd table only as large as its highest open fd: a pod process
+    forked from a pre-started parent would grow it again at its TAKE, multi-threaded by then. The
+    shim grows it in the child right after the fork."""
+    import resource
+
+    soft, _ = resource.getrlimit(resource.RLIMIT_NOFILE)
+    if soft < 256:
+        pytest.skip("RLIMIT_NOFILE below 256")
+    code = ("import os\n"
+            "pid = os.fork()\n"
+            "if pid == 0:\n"
+            "    print([l.split()[1] for l in open('/proc/self/status') if l.startswith('FDSize:')][0], flush=True)\n"
+            "    os._exit(0)\n"
+            "os.waitpid(pid, 0)\n")
+    env = dict(os.environ, LD_PRELOAD=preload(native_shim))
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True).stdout
+    assert int(out.split()[0]) >= min(soft, 2048), out
+    env["GPUSHARE_SHIM_FD_RESERVE"] = "0"
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True).stdout
+    assert int(out.split()[0]) < 256, out
 
 
 def test_broker_refusal_leaves_the_pod_on_the_driver(stub, native_shim, tmp_path):
