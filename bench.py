@@ -69,10 +69,10 @@ def parse():
     ap.add_argument("--gemm", type=int, default=4096, help="GEMM M=N=K")
     ap.add_argument("--fill", type=float, default=0.85, help="fraction of its quota a pod process holds")
     ap.add_argument("--standby", type=int, default=9,
-                    help="pre-started pod interpreters per GPU (images pulled, processes created, torch imported; "
-                         "each takes ~1.5 s of CPU, so the pool must cover the admission rate: at ~3.5 pods/s per "
-                         "GPU a pool of 6 ran dry, up to 445 ms of waiting in a step; 9 did not, "
-                         "profiles/r5/bench_n1_standby_ab/)")
+                    help="pre-started pod processes per GPU (images pulled, processes created, torch imported). "
+                         "A fresh interpreter takes ~1.5 s of CPU (--no-pod-zygote), so the pool must cover the "
+                         "admission rate: at ~3.5 pods/s per GPU a pool of 6 ran dry, up to 445 ms of waiting in a "
+                         "step; 9 did not (profiles/r5/bench_n1_standby_ab/). Forked standbys take milliseconds")
     ap.add_argument("--no-pod-zygote", action="store_true",
                     help="start each standby as a fresh interpreter (~1.5 s of CPU each) instead of forking it "
                          "from one that imported torch once")
