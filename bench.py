@@ -640,6 +640,7 @@ class _Zygote:
                                        "--zygote", str(theirs.fileno())], env=env, pass_fds=(theirs.fileno(),),
                                       stdin=subprocess.DEVNULL, stdout=subprocess.DEVNULL)
         theirs.close()
+        self._sock.settimeout(120)      # a fork answers in milliseconds; the first waits for the torch import
         self._rd = self._sock.makefile("r")
         self._lock = threading.Lock()
 
