@@ -173,6 +173,19 @@ def zygote(ctl_fd: int) -> int:
         ctl.sendall(f"{pid}\n".encode())
 
 
+def _release_timing() -> dict | None:
+    """Where the quota shim's last arena release spent its time (ms), or None without the shim."""
+    try:
+        f = ctypes.CDLL(None).gpushare_shim_arena_release_timing
+    except AttributeError:
+        return None
+    f.argtypes = [ctypes.POINTER(ctypes.c_uint64)] * 5
+    v = [ctypes.c_uint64() for _ in range(5)]
+    if not f(*(ctypes.byref(x) for x in v)):
+        return None
+    return dict(zip(("sync", "unmap", "addr_free", "release", "kfd_free"), (round(x.value / 1e6, 3) for x in v)))
+
+
 def main() -> int:
     if len(sys.argv) > 2 and sys.argv[1] == "--zygote":
         return zygote(int(sys.argv[2]))
@@ -241,9 +254,11 @@ def _pod() -> int:
     def reader():
         for ln in sys.stdin:
             try:
-                ctl.put(json.loads(ln))
+                c = json.loads(ln)
             except ValueError:
                 continue
+            c["_t"] = time.perf_counter()
+            ctl.put(c)
         ctl.put({"cmd": "stop"})                                # parent went away
 
     threading.Thread(target=reader, daemon=True).start()
@@ -253,6 +268,7 @@ def _pod() -> int:
     burst_done = torch.cuda.Event(blocking=True)
     gemms = 1
     t_start = time.time()
+    t_asked = None
     while True:
         try:
             c = ctl.get_nowait()
@@ -262,23 +278,31 @@ def _pod() -> int:
             if c.get("cmd") == "stats":
                 _send({"event": "stats", "gemms": gemms, "t": time.time()})
             elif c.get("cmd") == "stop":
+                t_asked = c.get("_t", time.perf_counter())
                 break
             continue
         player.run(burst)
         burst_done.record(player.stream)
         burst_done.synchronize()
         gemms += burst
+    # where a stop's time goes: the rest of the burst in flight when it came, freeing, the arena
+    t_stop = time.perf_counter()
     player.release()
     st = _shim_stats()
     del hold, player
     torch.cuda.synchronize()
     torch.cuda.empty_cache()      # HBM back to the device now, not at process exit
+    t_freed = time.perf_counter()
     # the broker arena (if any) is handed back first: its granules are on the ledger while it is
     # mapped, so the ledger read before the release would count them as a residue
     released = _arena_release()
+    t_rel = time.perf_counter()
     after = _shim_stats()
     _send({"event": "done", "gemms": gemms, "t": time.time(), "seconds": time.time() - t_start, "shim": st,
-           "used_after_release": (after or {}).get("used"), "arena_released": released})
+           "used_after_release": (after or {}).get("used"), "arena_released": released,
+           "stop_ms": {"burst_in_flight": round((t_stop - (t_asked or t_stop)) * 1e3, 3), "free": round((t_freed - t_stop) * 1e3, 3),
+                       "arena_release": round((t_rel - t_freed) * 1e3, 3)},
+           "release_ms": _release_timing() if released else None})
     # everything is freed and reported: leave without the interpreter's and torch's teardown
     # (hundreds of ms). The kernel still tears the process down, and only then do its last
     # references to an HBM broker's granules go (the broker quarantines them until then)

@@ -857,6 +857,10 @@ class PodFleet:
         w["proc"].stdin.write('{"cmd":"stop"}\n')
         ev = self._wait(w, "done")                      # freed through KFD at this point
         self.phase_ms["stop"].append(time.perf_counter() - t0)
+        for k, v in (ev.get("stop_ms") or {}).items():  # inside the pod: burst in flight, free, arena
+            self.phase_ms.setdefault(f"stop_{k}", []).append(v / 1e3)
+        for k, v in (ev.get("release_ms") or {}).items():   # inside the shim's arena release
+            self.phase_ms.setdefault(f"stop_release_{k}", []).append(v / 1e3)
         threading.Thread(target=w["proc"].wait, daemon=True).start()   # reap the exit off the path
         self._stopped_at = (t0, w["size"], w["ready"].get("held", 0))
         self.retired_bytes += w["ready"].get("held", 0)

@@ -1344,11 +1344,17 @@ bool set_rw(char* va, uint64_t len, int dev) {
   return f && f(va, len, &acc, 1) == hipSuccess;
 }
 
+// where the last arena release spent its time (ns): device sync, unmaps, address free, handle
+// releases, the KFD frees of kept imports (gpushare_shim_arena_release_timing)
+uint64_t g_rel_ns[5];
+
 // unmap and release whatever of the arena is mapped (g_arena.mu held)
 void arena_unmap_locked() {
   Arena& a = g_arena;
   Depth d;
+  uint64_t t0 = mono_ns();
   if (auto dev_sync = real_hipDeviceSynchronize()) (void)dev_sync();
+  uint64_t t1 = mono_ns(), t2 = t1, t3 = t1;
   if (a.base) {
     // one unmap per mapping: HIP unmaps one handle's mapping per call. Unmapping the whole range
     // at once failed, and the imported handles then stayed mapped, keeping the broker's granules
@@ -1360,11 +1366,19 @@ void arena_unmap_locked() {
         bad += un(a.base + uint64_t(i) * a.gran, a.gran) != hipSuccess;
       if (bad) logf(1, "hbm broker: %d of %d granule unmaps failed", bad, a.n);
     }
+    t2 = mono_ns();
     if (auto fr = real_hipMemAddressFree()) (void)fr(a.base, a.vsize);
+    t3 = mono_ns();
   }
   if (auto rel = real_hipMemRelease())
     for (int i = 0; i < a.n; ++i)
       if (a.h[i]) (void)rel(a.h[i]);
+  uint64_t t4 = mono_ns();
+  g_rel_ns[0] = t1 - t0;
+  g_rel_ns[1] = t2 - t1;
+  g_rel_ns[2] = t3 - t2;
+  g_rel_ns[3] = t4 - t3;
+  g_rel_ns[4] = 0;
   a.n = a.total = 0;
   a.base = nullptr;
 }
@@ -2127,7 +2141,9 @@ GS_EXPORT int gpushare_shim_arena_release() {
   if (a.rt_version > 0 && a.rt_version < 70100000 && env_u64("GPUSHARE_HBM_FREE_KEPT", 1)) {
     // HIP 7.0 keeps the KFD imports of the released handles: free them, so the broker sees its
     // granules' references gone now rather than at this process's teardown
+    uint64_t t = mono_ns();
     int n = imports_free_kept(real_ioctl());
+    g_rel_ns[4] = mono_ns() - t;
     logf(1, "hbm broker: freed %d KFD imports the runtime kept", n);
   }
   if (a.charged) uncharge(a.size);
@@ -2136,6 +2152,18 @@ GS_EXPORT int gpushare_shim_arena_release() {
   a.sock = -1;
   a.state.store(-1, std::memory_order_release);
   pthread_mutex_unlock(&a.mu);
+  return 1;
+}
+
+GS_EXPORT int gpushare_shim_arena_release_timing(uint64_t* sync_ns, uint64_t* unmap_ns, uint64_t* addr_free_ns,
+                                                 uint64_t* release_ns, uint64_t* kfd_free_ns) {
+  pthread_mutex_lock(&g_arena.mu);
+  *sync_ns = g_rel_ns[0];
+  *unmap_ns = g_rel_ns[1];
+  *addr_free_ns = g_rel_ns[2];
+  *release_ns = g_rel_ns[3];
+  *kfd_free_ns = g_rel_ns[4];
+  pthread_mutex_unlock(&g_arena.mu);
   return 1;
 }
 
