@@ -649,6 +649,7 @@ class _Zygote:
 
         c_in, p_in = os.pipe()          # the pod reads its commands from c_in
         p_out, c_out = os.pipe()        # and writes its events to c_out
+        line = ""
         try:
             with self._lock:
                 socket.send_fds(self._sock, [b"F"], [c_in, c_out])
@@ -656,9 +657,10 @@ class _Zygote:
         finally:
             os.close(c_in)
             os.close(c_out)
+            if not line:                # no child: nothing will read or write the other ends
+                os.close(p_in)
+                os.close(p_out)
         if not line:
-            os.close(p_in)
-            os.close(p_out)
             raise RuntimeError(f"the pod zygote exited (status {self._proc.poll()})")
         return _Forked(int(line), os.fdopen(p_in, "w", buffering=1), os.fdopen(p_out, "r"))
 

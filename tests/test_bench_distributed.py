@@ -179,3 +179,25 @@ def test_pod_zygote_forks_standby_pods_that_serve_their_own_pipes():
     finally:
         z.close()
     assert z._proc.returncode == 0
+
+
+def test_a_dead_pod_zygote_fails_the_fork_loudly():
+    """A zygote that died answers no fork: the bench gets an error at once, not a hang."""
+    import pytest
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    env = dict(os.environ, PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    z = bench._Zygote(env)
+    try:
+        k = z.fork()
+        assert json.loads(k.stdout.readline())["event"] == "standby"
+        z._proc.kill()
+        z._proc.wait(30)
+        with pytest.raises((RuntimeError, OSError)):
+            z.fork()
+        k.stdin.close()
+        assert k.wait(30) == 0                # its forked standby is a process of its own
+    finally:
+        z.close()
