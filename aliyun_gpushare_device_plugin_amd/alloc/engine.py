@@ -241,11 +241,12 @@ class Allocator(NativeTable):
 
     @staticmethod
     def _hbm_granter(opts: AllocatorOptions, live=None, on_readiness=None):
-        if not (opts.hbm_broker_dir and opts.shim is not None and opts.shim.enabled and not opts.disable_cgpu):
+        # also on a cgpu-disabled node: there it holds the brokers at nothing (quota/hbmbroker.py)
+        if not (opts.hbm_broker_dir and opts.shim is not None and opts.shim.enabled):
             return None
         from ..quota.hbmbroker import HBMGranter
         return HBMGranter(opts.hbm_broker_dir, opts.hbm_broker_fraction, live=live, on_readiness=on_readiness,
-                          **opts.hbm_granter_args)
+                          disabled=opts.disable_cgpu, **opts.hbm_granter_args)
 
     def _hbm_live(self) -> dict | None:
         """The HBM tokens the pods on this node need (the granter's pod view): every gpu container
@@ -316,6 +317,8 @@ class Allocator(NativeTable):
             if self._hbm is not None and not getattr(self, "_hbm_metrics", False):
                 self.metrics.registry.add_collector(lambda: self._hbm.exposition() if self._hbm is not None else "")
                 self._hbm_metrics = True
+            if self._hbm is not None:
+                self._hbm.set_disabled(self.opts.disable_cgpu)
             self._pinfo.clear()
             self._bump_gen()
             self._fast = None
@@ -323,6 +326,25 @@ class Allocator(NativeTable):
         if self.native is not None:
             self._hook_pods(self.native)
         return self
+
+    def set_cgpu_disabled(self, disabled: bool) -> None:
+        """The node's ``cgpu.disable.isolation`` label changed while the plugin runs (the
+        reference reads it once, at start: ``podmanager.go:62-75``). Answers prepared from now on
+        carry ``CGPU_DISABLE=true`` and no shim (or the shim again), and the HBM brokers are sized
+        to nothing (or to the GPU again)."""
+        with self._mu:
+            if self.opts.disable_cgpu == disabled:
+                return
+            self.opts = dataclasses.replace(self.opts, disable_cgpu=disabled)
+            self._bump_gen()
+            self._fast = None
+            self._prep_cache.clear()
+            self._resp_tmpl.clear()
+            self._tmpl_bytes.clear()
+        self._precomputed.clear()
+        if self._hbm is not None:
+            self._hbm.set_disabled(disabled)
+        log.warning("cgpu isolation %s on this node", "disabled" if disabled else "enabled")
 
     def close(self):
         self._stop.set()

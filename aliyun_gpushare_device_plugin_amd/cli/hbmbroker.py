@@ -8,6 +8,11 @@ and the admin socket ``<dir>/admin/hbm<i>.sock`` (``quota/hbmbroker.py`` has the
 the broker finds its HIP device by that GPU's PCI address, because HIP and SMI orders are not
 promised to agree.
 
+Sizing: each broker is sized for its GPU less ``--reserve-gib``. With ``--start-empty`` (the
+DaemonSet) it holds nothing until the plugin's granter sizes it: the whole size, or nothing on a
+``cgpu.disable.isolation=true`` node (``SIZE``), so such a node's GPUs stay the driver's. Free
+granules go back to the driver when it runs short (``--low-water-gib``).
+
 A broker that exits is started again after ``--restart-backoff`` seconds, with a new boot id: the
 plugin sees it on its next poll and grants the new instance every live pod's token again, so a
 container that restarts afterwards gets its granules. Pods that held granules of the dead broker
@@ -53,6 +58,12 @@ def build_parser() -> argparse.ArgumentParser:
                    help="the broker's scrub code object (default: gpushare-hbm-scrub.co next to the broker); "
                         "without it the broker zeroes with hipMemsetAsync")
     p.add_argument("--restart-backoff", type=float, default=2.0)
+    p.add_argument("--start-empty", action="store_true",
+                   help="brokers hold nothing until the plugin sizes them (SIZE): on a cgpu.disable.isolation node "
+                        "they never take the GPU's HBM from the driver")
+    p.add_argument("--low-water-gib", type=float, default=-1.0,
+                   help="free granules go back to the driver when it has less than this free (default: half the "
+                        "reserve); the brokers grow again once it has more than the reserve")
     return p
 
 
@@ -102,6 +113,10 @@ def main(argv=None) -> int:
         gpus = [s.device(i) for i in range(s.count())]
     extra = ["--ungranted-wait-s", str(a.ungranted_wait_s), "--release-policy", a.release_policy,
              "--scrub-chunk", str(a.scrub_chunk)]
+    if a.start_empty:
+        extra.append("--start-empty")
+    if a.low_water_gib >= 0:
+        extra += ["--low-water-gib", str(a.low_water_gib)]
     if a.scrub_kernel:
         extra += ["--scrub-kernel", a.scrub_kernel]
     brokers = {g.index: HBMBroker.for_gpu(a.dir, g.index, pci_bus_id=g.bdf, reserve_gib=a.reserve_gib,

@@ -77,7 +77,10 @@ def build_parser() -> argparse.ArgumentParser:
                         "from them, so admissions do not wait for amdgpu to wipe a retired pod's HBM")
     p.add_argument("--hbm-broker-fraction", type=float, default=0.94,
                    help="share of a container's quota granted as broker granules (whole GiB, rounded down); the "
-                        "rest stays for what the runtime allocates from the driver")
+                        "rest of the quota is borrowed from granules no grant claims, or from the driver")
+    p.add_argument("--label-poll-interval", type=float, default=10.0,
+                   help="re-read the node's cgpu.disable.isolation label this often while running (0 = at start "
+                        "only, as the reference): a flip re-prepares answers and sizes the HBM brokers")
     p.add_argument("--journal-path", default=None,
                    help="persist recent Allocate decisions (JSON lines) so a retried admission of an "
                         "already-assigned, still-Pending pod is answered identically across plugin restarts")
@@ -155,7 +158,7 @@ def config_from_args(a) -> PluginConfig:
         rocr_visible=a.rocr_visible_devices, metrics_addr=a.metrics_addr, mps=_bool(a.mps),
         async_patch=not a.sync_patch, complete_swaps=not a.no_swap_completion,
         partition_aware=a.partition_aware, ledger_dir=a.ledger_dir, ledger_scan_s=a.ledger_scan_interval,
-        hbm_broker_dir=a.hbm_broker_dir, hbm_broker_fraction=a.hbm_broker_fraction,
+        hbm_broker_dir=a.hbm_broker_dir, hbm_broker_fraction=a.hbm_broker_fraction, label_poll_s=a.label_poll_interval,
         journal_path=a.journal_path, compute_isolation=a.compute_isolation,
         pod_resources_socket=a.pod_resources_socket, placement_s=a.placement_interval,
         admission_identity=a.admission_identity, quota_enforcement=a.quota_enforcement,

@@ -33,10 +33,11 @@ def patch_gpu_count(client: APIClient, node_name: str, gpu_count: int) -> bool:
     return True
 
 
-def cgpu_isolation_disabled(client: APIClient, node_name: str) -> bool:
+def cgpu_isolation_disabled(client: APIClient, node_name: str, quiet: bool = False) -> bool:
     node = client.get_node(node_name)
     if O.labels(node).get(const.NODE_LABEL_DISABLE_CGPU) == "true":
-        log.info("enable gpusharing mode and disable cgpu mode")
+        if not quiet:
+            log.info("enable gpusharing mode and disable cgpu mode")
         return True
     return False
 

@@ -93,6 +93,9 @@ class PluginConfig:
     native_fast_wait_us: int = 300       # native server: wait for a republished table (see native_server.py)
     prebind_watch: bool = True           # prepare answers of pods the extender placed here, before their bind
     native_spin_us: int = 0              # native server: busy-poll this long after a pod is published (0 = off)
+    # re-read the node's cgpu.disable.isolation label this often (0 = only at start, as the
+    # reference does): a flip re-prepares answers and sizes the HBM brokers to nothing / back
+    label_poll_s: float = 10.0
 
 
 class SharedGPUManager:
@@ -122,6 +125,7 @@ class SharedGPUManager:
         self.dmem = None
         self.enforcement = "off"             # effective HBM-share enforcement (see _enforcement)
         self._cgpu_disabled = False
+        self._label_thread = None
 
     # ------------------------------------------------------------------------------------
     def _kubelet_socket(self) -> str:
@@ -358,6 +362,28 @@ class SharedGPUManager:
         else:
             self.dmem.sync()                        # logs once that it is inactive
 
+    def _start_label_watch(self):
+        """Follow the node's ``cgpu.disable.isolation`` label while the plugin runs (the
+        reference reads it once, at start: ``podmanager.go:62-75``, ``server.go:43-78``)."""
+        if self.cfg.label_poll_s <= 0 or self.client is None or self._label_thread is not None:
+            return
+
+        def loop():
+            while not self._ledger_stop.wait(self.cfg.label_poll_s):
+                try:
+                    v = nodestatus.cgpu_isolation_disabled(self.client, self.cfg.node_name, quiet=True)
+                except Exception as e:  # noqa: BLE001 - the next poll tries again
+                    log.V(2).info("node label poll: %s", e)
+                    continue
+                if v != self._cgpu_disabled and self.allocator is not None:
+                    log.warning("node label %s=%s: %s", const.NODE_LABEL_DISABLE_CGPU, "true" if v else "(unset)",
+                                "quota isolation off, HBM brokers hold nothing" if v else "quota isolation back on")
+                    self._cgpu_disabled = v
+                    self.allocator.set_cgpu_disabled(v)
+
+        self._label_thread = threading.Thread(target=loop, name="node-label-watch", daemon=True)
+        self._label_thread.start()
+
     def _start_ledger_collector(self):
         """Export the quota shim's per-container ledgers (--ledger-dir) every ledger_scan_s and
         remove the ledger directories of containers whose pods no longer exist on this node."""
@@ -452,6 +478,7 @@ class SharedGPUManager:
                         log.warning("Failed to start device plugin due to %s", e)
                         return 2
                     self._start_health()
+                    self._start_label_watch()
                     self._start_ledger_collector()
                     self._start_dmem()
                     self._start_watchdog()

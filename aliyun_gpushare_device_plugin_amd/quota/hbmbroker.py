@@ -193,13 +193,23 @@ class HBMBroker:
         self.info = got
         return got
 
-    def grant(self, token: str, nbytes: int) -> int:
+    def grant(self, token: str, nbytes: int, limit: int | None = None) -> int:
         """Grant ``nbytes`` (rounded up to granules) to the pod holding ``token``; returns the
-        number of granules."""
-        r = _request(self.admin_path, f"GRANT {token} {int(nbytes)}")
+        number of granules. ``limit``: the pod's whole quota, up to which it may borrow granules
+        no grant claims beyond its grant (EXTEND); None = the grant only."""
+        line = f"GRANT {token} {int(nbytes)}" + (f" {int(limit)}" if limit else "")
+        r = _request(self.admin_path, line)
         if not r.startswith("OK "):
             raise RuntimeError(f"hbm broker refused the grant: {r!r}")
         return int(r.split()[1])
+
+    def size(self, granules: int | str) -> tuple[int, int]:
+        """How much of the GPU the broker may hold (``"max"``: all it is sized for; 0: nothing, a
+        cgpu-disabled node); returns (granules held now, target)."""
+        r = _request(self.admin_path, f"SIZE {granules}")
+        if not r.startswith("OK "):
+            raise RuntimeError(f"hbm broker refused the size: {r!r}")
+        return int(r.split()[1]), int(r.split()[2])
 
     def revoke(self, token: str) -> int:
         """The token can never be taken again; returns how many granules its holder still has."""
@@ -240,6 +250,7 @@ class _Want:
     gpu: int
     nbytes: int
     t: float                 # submitted at (monotonic)
+    quota: int = 0           # the container's whole quota: the grant's limit
 
 
 @dataclasses.dataclass
@@ -274,12 +285,19 @@ class HBMGranter:
       with a GPU assignment, or None when the pod view is unavailable (then nothing is revoked).
 
     The grant is ``fraction`` of the container's quota, rounded down to whole 1 GiB granules (the
-    shim charges it to the container's ledger). Below 2 granules there is no arena."""
+    shim charges it to the container's ledger). Below 2 granules there is no arena. The grant's
+    limit is the whole quota: the pod may borrow granules no grant claims beyond its grant, so it
+    can use all of its quota on a packed GPU (the driver serves what the broker cannot).
+
+    ``disabled`` (the node's ``cgpu.disable.isolation=true`` label, ``set_disabled``): no answer
+    carries a token, every grant is revoked and each broker is told to hold nothing (SIZE 0), so
+    the whole GPU is the driver's, as on the reference's cgpu-disabled nodes
+    (``podmanager.go:62-75``, ``allocate.go:125-127``); clearing it sizes them back (SIZE max)."""
 
     def __init__(self, host_dir: str, fraction: float = 0.94, secret: bytes | None = None,
                  timeout_s: float = 0.5, poll_s: float = 1.0, live=None, startup_grace_s: float = 120.0,
                  down_grace_s: float = 60.0, submit_ttl_s: float = 600.0, revoke_grace_s: float = 5.0,
-                 on_readiness=None, start: bool = True):
+                 on_readiness=None, start: bool = True, disabled: bool = False):
         self.host_dir = host_dir
         self.fraction = fraction
         self.secret = secret or load_secret(host_dir)
@@ -298,7 +316,8 @@ class HBMGranter:
         self._stop = threading.Event()
         self._full_passes = 0
         self._force_full = False
-        self.grants = self.failures = self.revokes = self.regrants = 0
+        self.disabled = disabled
+        self.grants = self.failures = self.revokes = self.regrants = self.resizes = 0
         self._thread = None
         if start:
             self._thread = threading.Thread(target=self._worker, name="hbm-granter", daemon=True)
@@ -332,14 +351,14 @@ class HBMGranter:
         """Record the grant and have the granter thread send it; True = the answer carries the
         token. Runs on the pod watch / prepare threads: never waits for a broker."""
         nbytes = self.arena_bytes(quota_bytes)
-        if not nbytes or not self.ready(gpu_index):
+        if not nbytes or self.disabled or not self.ready(gpu_index):
             return False
         with self._mu:
             w = self._submits.get(token)
             if w is not None and w.gpu == gpu_index and w.nbytes == nbytes:
                 w.t = time.monotonic()
                 return True
-            self._submits[token] = _Want(gpu_index, nbytes, time.monotonic())
+            self._submits[token] = _Want(gpu_index, nbytes, time.monotonic(), int(quota_bytes))
             st = self._gpus.get(gpu_index)
             if st is None or st.sent.get(token) != nbytes:
                 self._unsent.add(token)
@@ -379,10 +398,23 @@ class HBMGranter:
         self._stop.set()
         self._wake.set()
 
+    def set_disabled(self, disabled: bool) -> None:
+        """The node's cgpu.disable.isolation label changed: brokers are sized to nothing (and
+        every grant revoked) or back to the whole GPU on the next pass, started now."""
+        if disabled == self.disabled:
+            return
+        self.disabled = disabled
+        log.warning("hbm granter: %s", "cgpu isolation disabled on this node: brokers hold no HBM" if disabled
+                    else "cgpu isolation enabled again: brokers take the GPU's HBM back")
+        with self._mu:
+            self._force_full = True
+        self._wake.set()
+
     def stats(self) -> dict:
         with self._mu:
             return {"grants": self.grants, "failures": self.failures, "revokes": self.revokes,
-                    "regrants": self.regrants, "submitted": len(self._submits), "unsent": len(self._unsent),
+                    "regrants": self.regrants, "resizes": self.resizes, "disabled": self.disabled,
+                    "submitted": len(self._submits), "unsent": len(self._unsent),
                     "gpus": {str(i): {"up": st.up, "boot": st.boot, "held": len(st.sent), "restarts": st.restarts}
                              for i, st in sorted(self._gpus.items())}}
 
@@ -392,18 +424,24 @@ class HBMGranter:
         timings, and the granter's own grant counters."""
         with self._mu:
             gpus = {i: (st.up, dict(st.stat), st.restarts) for i, st in self._gpus.items()}
-            own = {"grants": self.grants, "failures": self.failures, "revokes": self.revokes, "regrants": self.regrants}
+            own = {"grants": self.grants, "failures": self.failures, "revokes": self.revokes, "regrants": self.regrants,
+                   "resizes": self.resizes}
         out = ["# HELP gpushare_hbm_broker_up 1 if the GPU's HBM broker answered the last poll\n"
                "# TYPE gpushare_hbm_broker_up gauge\n"]
         out += [f'gpushare_hbm_broker_up{{gpu="{i}"}} {int(up)}\n' for i, (up, _, _) in sorted(gpus.items())]
         out.append("# HELP gpushare_hbm_broker_granules Granules of the GPU's HBM broker by state\n"
                    "# TYPE gpushare_hbm_broker_granules gauge\n")
         for i, (_, stat, _) in sorted(gpus.items()):
-            for state in ("granules", "granules_max", "free", "held", "owed", "scrubbing", "quarantined"):
+            for state in ("granules", "granules_max", "target", "free", "held", "owed", "extra", "scrubbing",
+                          "quarantined"):
                 if state in stat:
                     out.append(f'gpushare_hbm_broker_granules{{gpu="{i}",state="{state}"}} {stat[state]}\n')
         for name, key, help_ in (("takes", "takes", "TAKEs served"), ("releases", "releases", "connections that returned granules"),
                                  ("timeouts", "timeouts", "TAKEs refused after waiting"),
+                                 ("extended", "extended", "granules lent beyond grants (EXTEND)"),
+                                 ("given_back", "given_back", "granules given back to the driver (SIZE, pressure)"),
+                                 ("pressure_given", "pressure_given", "granules given back because the driver ran short"),
+                                 ("ends", "ends", "streams ended with granules still owed (deadline, revocation)"),
                                  ("scrubbed_bytes", "scrubbed_bytes", "bytes zeroed between pods"),
                                  ("lost", "lost", "granules never lent again (untraceable holder)")):
             out.append(f"# HELP gpushare_hbm_broker_{name}_total {help_}\n# TYPE gpushare_hbm_broker_{name}_total counter\n")
@@ -447,18 +485,25 @@ class HBMGranter:
             self._wake.clear()
 
     def _want(self, now: float, live: dict | None) -> dict:
-        want: dict[str, tuple[int, int]] = {}
+        """token -> (gpu, grant bytes, quota bytes) of every grant live pods need (none while
+        the node is cgpu-disabled)."""
+        want: dict[str, tuple[int, int, int]] = {}
         with self._mu:
             for tok, w in list(self._submits.items()):
                 if now - w.t < self.submit_ttl_s or (live is not None and tok in live):
-                    want[tok] = (w.gpu, w.nbytes)
+                    want[tok] = (w.gpu, w.nbytes, w.quota)
                 else:
                     del self._submits[tok]
                     self._unsent.discard(tok)
         for tok, (gpu, quota) in (live or {}).items():
             nb = self.arena_bytes(quota)
             if nb:
-                want.setdefault(tok, (gpu, nb))
+                want.setdefault(tok, (gpu, nb, quota))
+        if self.disabled:
+            with self._mu:
+                self._submits.clear()
+                self._unsent.clear()
+            return {}
         return want
 
     def _push_unsent(self) -> None:
@@ -469,11 +514,11 @@ class HBMGranter:
             st = self._gpus.get(w.gpu)
             if st is None or not st.up:
                 continue                            # the next full pass contacts it
-            self._grant(w.gpu, st, tok, w.nbytes)
+            self._grant(w.gpu, st, tok, w.nbytes, w.quota)
 
-    def _grant(self, gpu: int, st: _GPUState, tok: str, nbytes: int) -> bool:
+    def _grant(self, gpu: int, st: _GPUState, tok: str, nbytes: int, quota: int = 0) -> bool:
         try:
-            r = self._admin(gpu, f"GRANT {tok} {nbytes}")
+            r = self._admin(gpu, f"GRANT {tok} {nbytes}" + (f" {quota}" if quota > nbytes else ""))
             ok = r.startswith("OK ")
         except OSError as e:
             r, ok = str(e), False
@@ -499,13 +544,14 @@ class HBMGranter:
             except Exception as e:  # noqa: BLE001 - no revocations without a pod view
                 log.V(2).info("hbm granter: no pod view (%s)", e)
         want = self._want(now, live)
-        gpus = {g for g, _ in want.values()} | set(self._gpus)
+        gpus = {w[0] for w in want.values()} | set(self._gpus)
         try:
             present = {int(n[3:]) for n in os.listdir(self.host_dir) if n.startswith("gpu") and n[3:].isdigit()}
         except OSError:
             present = set()
         gpus |= present
-        may_revoke = live is not None and now - self._t0 >= self.startup_grace_s
+        # a cgpu-disabled node revokes at once: no pod here may hold the brokers' HBM
+        may_revoke = self.disabled or (live is not None and now - self._t0 >= self.startup_grace_s)
         changed = False
         for gpu in sorted(gpus):
             with self._mu:
@@ -539,7 +585,7 @@ class HBMGranter:
                     st.boot = boot
                     st.sent = {t: n * GRANULE for t, n in held.items()}
                     st.absent.clear()
-                    for t, (g, nb) in want.items():
+                    for t, (g, nb, _q) in want.items():
                         if g == gpu and st.sent.get(t) != nb:
                             self._unsent.add(t)
         except (OSError, ValueError) as e:
@@ -551,9 +597,20 @@ class HBMGranter:
         with self._mu:
             st.up = True
             st.last_ok = now
-        for tok, (g, nb) in want.items():
+        # its size: the whole GPU (less its reserve), or nothing on a cgpu-disabled node
+        target = 0 if self.disabled else stat.get("granules_max")
+        if target is not None and "target" in stat and stat["target"] != target:
+            try:
+                r = self._admin(gpu, f"SIZE {target}")
+                if r.startswith("OK "):
+                    with self._mu:
+                        self.resizes += 1
+                    log.info("hbm broker of GPU %d sized to %s granules (holds %s)", gpu, target, r.split()[1])
+            except OSError as e:
+                log.V(2).info("hbm broker of GPU %d: size: %s", gpu, e)
+        for tok, (g, nb, q) in want.items():
             if g == gpu and st.sent.get(tok) != nb:
-                if not self._grant(gpu, st, tok, nb):
+                if not self._grant(gpu, st, tok, nb, q):
                     return
         if not may_revoke:
             return
@@ -562,7 +619,7 @@ class HBMGranter:
                 st.absent.pop(tok, None)
                 continue
             first = st.absent.setdefault(tok, now)
-            if now - first < self.revoke_grace_s:
+            if now - first < self.revoke_grace_s and not self.disabled:
                 continue
             try:
                 r = self._admin(gpu, f"REVOKE {tok}")

@@ -90,10 +90,16 @@ def build_gpuinfo(force=False, asan=False):
     return [lib, cli]
 
 
+def hipshim_sources():
+    """The quota shim's translation units (native/hipshim/shim.h lists what each one owns)."""
+    d = _src("hipshim")
+    return sorted(os.path.join(d, f) for f in os.listdir(d) if f.endswith(".cpp")) if os.path.isdir(d) else []
+
+
 def build_hipshim(force=False, asan=False):
     d = _src("hipshim")
-    src = _src("hipshim", "hipquota.cpp")
-    if not os.path.exists(src):
+    srcs = hipshim_sources()
+    if not srcs:
         return []
     lib = os.path.join(OUT, "libgpushare_hipquota.so")
     flags = ["-std=c++17", "-O2", "-fPIC", "-Wall", "-Wextra", "-Wno-unused-parameter",
@@ -103,7 +109,7 @@ def build_hipshim(force=False, asan=False):
         flags += SANITIZERS[san]
         lib = os.path.join(OUT, san, "libgpushare_hipquota.so")
     os.makedirs(os.path.dirname(lib), exist_ok=True)
-    if force or _newer(lib, [src] + _headers(d)):
+    if force or _newer(lib, srcs + _headers(d)):
         # Deliberately NOT linked against libamdhip64: the real entry points are resolved at
         # run time from whichever HIP runtime the process loaded (PyTorch bundles its own).
         # -static-libstdc++/-static-libgcc: the shim is preloaded into arbitrary tenant images,
@@ -112,8 +118,8 @@ def build_hipshim(force=False, asan=False):
         # pins its glibc symbol versions to the 2.2.5 baseline; libdl/librt/libpthread stay
         # NEEDED for images whose glibc predates their merge into libc (2.34).
         static = [] if san else ["-static-libstdc++", "-static-libgcc", "-fno-exceptions", "-fno-rtti"]
-        _run([CXX, *flags, "-shared", "-o", lib, src, *static, "-Wl,--no-as-needed", "-l:libdl.so.2", "-l:librt.so.1", "-l:libpthread.so.0",
-              "-Wl,--as-needed"])
+        _run([CXX, *flags, "-shared", "-o", lib, *srcs, *static, "-Wl,--no-as-needed", "-l:libdl.so.2", "-l:librt.so.1",
+              "-l:libpthread.so.0", "-Wl,--as-needed"])
     return [lib]
 
 

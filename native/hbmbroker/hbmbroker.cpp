@@ -14,24 +14,45 @@
 //
 // Protocol: one text line per request.
 //   admin socket (--admin-socket, 0600):
-//     "GRANT <token> <bytes>\n" -> "OK <granules>\n" | "ERR ...\n"   (a repeated grant refreshes it)
+//     "GRANT <token> <bytes> [<limit bytes>]\n" -> "OK <granules>\n" | "ERR ...\n" (a repeated
+//                                  grant refreshes it). <limit>: the pod's whole quota; it may
+//                                  borrow granules beyond its grant up to that (EXTEND below)
 //     "REVOKE <token>\n"        -> "OK <held>\n": the token can never be taken again; a process
-//                                  holding it keeps its granules until its connection ends
+//                                  holding it keeps its granules until its connection ends, and
+//                                  is sent "END\n" (no more granules)
+//     "SIZE <granules>|max\n"   -> "OK <granules> <target>\n": how much of the GPU the broker may
+//                                  hold. Free granules beyond it go back to the driver at once,
+//                                  lent ones when they come back; below it the broker grows as the
+//                                  driver has room (SIZE 0: a cgpu.disable.isolation node)
 //     "LIST\n"                  -> one JSON line {"boot": .., "grants": {token: granules, ..}}
 //     "STAT\n"                  -> one JSON line of counters, with this process's "boot" id
 //   pod socket (--socket, 0666):
 //     "TAKE <token>\n"          -> "FDS <n> <granule bytes>\n", then n fds (batches of <= 200,
 //                                  one byte each); the connection stays open: its end (close,
 //                                  exit, crash) returns the granules, which are scrubbed first.
-//     "TAKE <token> STREAM\n"   -> "FDS <k> <granule bytes> <n>\n" + k fds at once (k = what is
-//                                  free now, possibly 0), then "MORE <j> <granule bytes>\n" + j
-//                                  fds as granules come back, until all n are delivered: the pod
-//                                  maps the first granules while a retiring pod's are still being
-//                                  torn down, instead of waiting for all n.
+//     "TAKE <token> STREAM\n"   -> "FDS <k> <granule bytes> <n> <limit>\n" + k fds at once (k =
+//                                  what is free now, possibly 0), then "MORE <j> <granule bytes>\n"
+//                                  + j fds as granules come back, until all n are delivered: the
+//                                  pod maps the first granules while a retiring pod's are still
+//                                  being torn down, instead of waiting for all n. Owed granules
+//                                  that have not come within --wait-s are cancelled with "END\n".
+//     after a TAKE was served and nothing is owed:
+//     "EXTEND <k>\n"            -> "XFDS <j> <granule bytes>\n" + j fds, j <= k: granules beyond
+//                                  the grant, up to the grant's limit, from granules no grant
+//                                  has a claim on (j = 0 when there are none: the pod uses the
+//                                  driver). They return with the connection like the others.
+//     "AVAIL\n"                 -> "AVAIL <j>\n": what EXTEND could give now (hipMemGetInfo)
 // A TAKE whose granules are still held by a retiring pod waits (up to --wait-s), and one whose
 // grant has not arrived yet waits up to --ungranted-wait-s (a broker that just restarted is
 // re-granted by the plugin within a poll interval): the pod's runtime may start before the
 // retired pod is gone, or before the plugin has seen this broker, as on a booting node.
+//
+// Sizing: the broker is sized for the GPU less --reserve-gib (the pods' runtimes, and whatever
+// of their quota is not lent as granules, come from the driver). Every pod can use its whole
+// quota: its grant (a share of the quota) is lent at once, granules no grant claims can be
+// borrowed beyond it (EXTEND), and the driver serves the rest. Free granules are given back to the
+// driver when its free memory drops under --low-water-gib (default half the reserve), and the
+// broker grows again once the driver has more than the reserve free.
 //
 // The boot id changes with every start. The plugin polls STAT, and on a new boot id it re-grants
 // every live pod's token: a broker restart loses no grant that a pod still needs.
@@ -53,6 +74,9 @@
 //                       [--grant-ttl-s 0] [--max-clients 1024] [--max-per-peer 8]
 //                       [--request-timeout-s 2] [--release-policy auto] [--scrub-chunk 8]
 //                       [--scrub-kernel <dir of this executable>/gpushare-hbm-scrub.co]
+//                       [--start-empty] [--low-water-gib R/2]
+// --start-empty: hold nothing until the granter sends SIZE (the DaemonSet: the plugin knows
+// whether the node is cgpu-disabled, the broker does not).
 #include <hip/hip_runtime.h>
 
 #include <fcntl.h>
@@ -172,6 +196,7 @@ struct Client {
   double wait_since = 0;
   bool stream = false;    // TAKE ... STREAM: granules are delivered as they become free
   int owed = 0;           // granules of its grant still to deliver (stream)
+  int extra = 0;          // granules borrowed beyond the grant (EXTEND), part of `held`
 };
 
 enum Policy { kRefs, kExit, kTrust };
@@ -213,6 +238,7 @@ struct Broker {
   // granted or last released, when a TTL is set).
   struct Grant {
     int granules;
+    int limit;        // granules it may hold with what it borrows (EXTEND): the pod's quota
     double at;
     int holder = -1;  // fd of the connection holding it
   };
@@ -240,8 +266,14 @@ struct Broker {
   hipFunction_t scrub_fn = nullptr;
   std::string scrub_path;
   int count_max = 0;          // granules the broker is sized for (its address range)
+  int target = 0;             // granules it may hold now (SIZE; count_max unless told otherwise)
+  std::vector<char> present;  // granule i exists (created, exported, mapped)
   size_t reserve_bytes = 0;   // what it leaves to the driver
-  unsigned long long grown = 0;
+  size_t low_water_bytes = 0; // driver free memory under which free granules go back to it
+  double last_pressure = 0;
+  unsigned long long grown = 0, given_back = 0, pressure_given = 0, extends = 0, extended = 0, ends = 0;
+  int counted = -1;           // the kernel reports dma-buf references in fdinfo: 1 yes, 0 no, -1 not known yet
+  bool policy_auto = true;    // --release-policy auto: refs where counted, else exit
 
   hipMemAccessDesc rw() const {
     hipMemAccessDesc d;
@@ -280,11 +312,75 @@ struct Broker {
     CK(hipMemCreate(&h[i], gran, &prop_, 0));
     CK(hipMemExportToShareableHandle(&fds[i], h[i], hipMemHandleTypePosixFileDescriptor, 0));
     CK(hipMemMap(base + size_t(i) * gran, gran, 0, h[i], 0));
+    present[i] = 1;
   }
 
-  // `target` bytes of granules, as many of them as the device has free now (the rest is taken
-  // later, by grow(): after a broker restart, pods of the previous instance still hold theirs)
-  void setup(size_t target, size_t free_now) {
+  // granule i back to the driver (it is free: nobody holds it, it is not being scrubbed). The
+  // driver wipes it when the last reference to its memory is gone.
+  void destroy_granule(int i) {
+    if (!present[i]) return;
+    hipError_t e = hipMemUnmap(base + size_t(i) * gran, gran);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      std::fprintf(stderr, "gpushare-hbm-broker: unmap of granule %d: %s (kept out of the free list)\n", i,
+                   hipGetErrorString(e));
+      ++lost;
+      return;
+    }
+    (void)hipMemRelease(h[i]);
+    h[i] = nullptr;
+    close(fds[i]);
+    fds[i] = -1;
+    base_refs[i] = -1;
+    present[i] = 0;
+    --count;
+    ++given_back;
+  }
+
+  // whether the kernel reports a dma-buf's references in fdinfo ("count:"), read on a throwaway
+  // export of the smallest handle; -1 when even that cannot be had (the device is full)
+  int probe_counted() {
+    size_t mg = 0;
+    if (hipMemGetAllocationGranularity(&mg, &prop_, hipMemAllocationGranularityMinimum) != hipSuccess || !mg) mg = 2u << 20;
+    hipMemGenericAllocationHandle_t t = nullptr;
+    if (hipMemCreate(&t, mg, &prop_, 0) != hipSuccess) {
+      (void)hipGetLastError();
+      return -1;
+    }
+    int fd = -1, r = -1;
+    if (hipMemExportToShareableHandle(&fd, t, hipMemHandleTypePosixFileDescriptor, 0) == hipSuccess && fd >= 0) {
+      r = fd_refs(fd) >= 0 ? 1 : 0;
+      close(fd);
+    } else {
+      (void)hipGetLastError();
+    }
+    (void)hipMemRelease(t);
+    return r;
+  }
+
+  // the release policy once the kernel's reference count is known (at start, or at the first
+  // granule when the device was full then)
+  void settle_policy(int i) {
+    if (counted >= 0 || !present[i]) return;
+    counted = base_refs[i] >= 0 ? 1 : 0;
+    choose_policy();
+  }
+
+  void choose_policy() {
+    if (counted < 0) return;
+    if (policy_auto) {
+      policy = counted ? kRefs : kExit;
+    } else if (policy == kRefs && !counted) {
+      std::fprintf(stderr, "gpushare-hbm-broker: --release-policy refs needs the dma-buf count in fdinfo, which this "
+                           "kernel does not report\n");
+      std::exit(2);
+    }
+  }
+
+  // sized for `target` bytes; holds as much of it as the device has free now, or nothing with
+  // --start-empty (the rest is taken later, by grow(): after a broker restart, pods of the
+  // previous instance still hold theirs)
+  void setup(size_t target_bytes, size_t free_now, bool start_empty) {
     CK(hipSetDevice(device));
     std::memset(&prop_, 0, sizeof prop_);
     prop_.type = hipMemAllocationTypePinned;
@@ -294,17 +390,20 @@ struct Broker {
     size_t mg = 0;
     CK(hipMemGetAllocationGranularity(&mg, &prop_, hipMemAllocationGranularityMinimum));
     if (mg && gran % mg) gran = (gran + mg - 1) / mg * mg;
-    count_max = int(target / gran);
-    count = std::min(count_max, int(free_now / gran));
+    count_max = int(target_bytes / gran);
+    target = start_empty ? 0 : count_max;
+    int n0 = std::min(target, int(free_now / gran));
     double t0 = now_s();
-    h.resize(count_max);
+    h.assign(count_max, nullptr);
     fds.assign(count_max, -1);
     base_refs.assign(count_max, -1);
-    CK(hipMemAddressReserve(reinterpret_cast<void**>(&base), gran * size_t(count_max), 0, nullptr, 0));
-    for (int i = 0; i < count; ++i) {
+    present.assign(count_max, 0);
+    CK(hipMemAddressReserve(reinterpret_cast<void**>(&base), gran * size_t(std::max(count_max, 1)), 0, nullptr, 0));
+    for (int i = 0; i < n0; ++i) {
       add_granule(i);
       free_list.push_back(i);
     }
+    count = n0;
     hipMemAccessDesc d = rw();
     if (count) CK(hipMemSetAccess(base, gran * count, &d, 1));
     CK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
@@ -312,34 +411,90 @@ struct Broker {
     if (count) zero(base, gran * count);  // nobody sees what was there before
     CK(hipStreamSynchronize(stream));
     for (int i = 0; i < count; ++i) base_refs[i] = refs(i);
+    counted = count ? (base_refs[0] >= 0 ? 1 : 0) : probe_counted();
     setup_s = now_s() - t0;
   }
 
-  // take more of the device while the broker is short of its size: HBM that pods of a previous
+  // take more of the device while the broker is short of its target: HBM that pods of a previous
   // broker instance held comes back to the driver when they exit (the dma-buf imports keep it
-  // alive until then). New granules are zeroed like released ones before they are lent.
+  // alive until then), and what was given back under pressure or by SIZE is taken again once the
+  // driver has more than the reserve free. New granules are zeroed like released ones before
+  // they are lent.
   void grow() {
-    if (count >= count_max) return;
+    if (count >= target) return;
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr <= reserve_bytes) return;
-    int n = std::min(count_max - count, int((fr - reserve_bytes) / gran));
+    int n = std::min(target - count, int((fr - reserve_bytes) / gran));
     if (n <= 0) return;
     hipMemAccessDesc d = rw();
     std::vector<int> fresh;
-    for (int k = 0; k < n; ++k) {
-      int i = count;
-      if (hipMemCreate(&h[i], gran, &prop_, 0) != hipSuccess) break;   // raced: try again later
+    for (int i = 0; i < count_max && int(fresh.size()) < n; ++i) {
+      if (present[i]) continue;
+      if (hipMemCreate(&h[i], gran, &prop_, 0) != hipSuccess) {  // raced: try again later
+        (void)hipGetLastError();
+        break;
+      }
       CK(hipMemExportToShareableHandle(&fds[i], h[i], hipMemHandleTypePosixFileDescriptor, 0));
       CK(hipMemMap(base + size_t(i) * gran, gran, 0, h[i], 0));
       CK(hipMemSetAccess(base + size_t(i) * gran, gran, &d, 1));
+      present[i] = 1;
       base_refs[i] = refs(i);
+      settle_policy(i);
       fresh.push_back(i);
       ++count;
     }
     grown += fresh.size();
     if (!fresh.empty())
-      std::fprintf(stderr, "gpushare-hbm-broker: grew by %zu granules to %d of %d\n", fresh.size(), count, count_max);
+      std::fprintf(stderr, "gpushare-hbm-broker: grew by %zu granules to %d of %d\n", fresh.size(), count, target);
     scrub(fresh);
+  }
+
+  // granules no grant has a claim on: the broker's size less every grant (taken or not: a grant
+  // not taken yet is a pod about to start) and what is borrowed beyond grants. Only these are
+  // lent beyond a grant or given back under pressure, so a pod's owed granules always come.
+  long uncommitted() const {
+    long c = 0;
+    for (auto& g : grants) c += g.second.granules;
+    for (auto& kv : clients) c += kv.second.extra;
+    return long(std::min(count, target)) - c;
+  }
+
+  // what EXTEND may lend now: free granules no grant claims, and none while a taker waits
+  int lendable() const {
+    for (auto& kv : clients)
+      if (!kv.second.waiting.empty() || kv.second.owed > 0) return 0;
+    long u = std::min<long>(uncommitted(), long(free_list.size()));
+    return int(std::max(0L, u));
+  }
+
+  // free granules beyond the target go back to the driver
+  void shrink_to_target() {
+    while (count > target && !free_list.empty()) {
+      int i = free_list.back();
+      free_list.pop_back();
+      destroy_granule(i);
+    }
+  }
+
+  // the driver is short (pods' runtimes, their quota beyond the granules, processes without a
+  // grant): free granules no grant claims go back to it until it has --low-water-gib free again.
+  // grow() takes them back once the driver has more than the reserve free.
+  void relieve_pressure(double t) {
+    if (!low_water_bytes || free_list.empty() || t - last_pressure < 0.05) return;
+    last_pressure = t;
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr >= low_water_bytes) return;
+    long k = long((low_water_bytes - fr + gran - 1) / gran);
+    k = std::min<long>(k, std::min<long>(uncommitted(), long(free_list.size())));
+    for (long j = 0; j < k; ++j) {
+      int i = free_list.back();
+      free_list.pop_back();
+      destroy_granule(i);
+      ++pressure_given;
+    }
+    if (k > 0)
+      std::fprintf(stderr, "gpushare-hbm-broker: driver had %.2f GiB free: gave %ld granules back (%d held)\n",
+                   double(fr) / double(1ull << 30), k, count);
   }
 
   // zero the granules on the broker's stream; they are lent again from reap_scrubs(), in chunks
@@ -379,7 +534,10 @@ struct Broker {
       scrub_s_last = now_s() - s.t0;
       scrub_s_total += scrub_s_last;
       scrubbed_bytes += gran * s.idx.size();
-      for (int i : s.idx) free_list.push_back(i);
+      for (int i : s.idx) {
+        if (count > target) destroy_granule(i);  // SIZE asked for less while it was lent
+        else free_list.push_back(i);
+      }
       scrubbing.pop_front();
       any = true;
     }
@@ -404,10 +562,11 @@ struct Broker {
     }
   }
 
-  // the header ("FDS <k> <gran>[ <total>]" or "MORE <k> <gran>"), then the fds
-  bool send_fds(int fd, const std::vector<int>& idx, const char* verb = "FDS", int total = -1) {
+  // the header ("FDS <k> <gran>[ <total> <limit>]", "MORE <k> <gran>" or "XFDS <k> <gran>"), then
+  // the fds
+  bool send_fds(int fd, const std::vector<int>& idx, const char* verb = "FDS", int total = -1, int limit = -1) {
     double t0 = now_s();
-    bool ok = send_fds_inner(fd, idx, verb, total);
+    bool ok = send_fds_inner(fd, idx, verb, total, limit);
     send_s_max = std::max(send_s_max, now_s() - t0);
     timespec w;
     clock_gettime(CLOCK_REALTIME, &w);
@@ -415,9 +574,10 @@ struct Broker {
     return ok;
   }
 
-  bool send_fds_inner(int fd, const std::vector<int>& idx, const char* verb, int total) {
+  bool send_fds_inner(int fd, const std::vector<int>& idx, const char* verb, int total, int limit) {
     char head[96];
-    int n = total >= 0 ? std::snprintf(head, sizeof head, "%s %zu %zu %d\n", verb, idx.size(), gran, total)
+    int n = total >= 0 ? std::snprintf(head, sizeof head, "%s %zu %zu %d %d\n", verb, idx.size(), gran, total,
+                                       std::max(limit, total))
                        : std::snprintf(head, sizeof head, "%s %zu %zu\n", verb, idx.size(), gran);
     if (send(fd, head, n, MSG_NOSIGNAL) != n) return false;
     for (size_t i = 0; i < idx.size(); i += 200) {
@@ -497,16 +657,18 @@ struct Broker {
       take_wait_s_max = std::max(take_wait_s_max, take_wait_s_last);
       streamed += c.stream;
       if (c.owed > 0) blocked = true;
-      if (!send_fds(c.fd, idx, "FDS", c.stream ? n : -1)) dead.push_back(o.second);
+      if (!send_fds(c.fd, idx, "FDS", c.stream ? n : -1, g->second.limit)) dead.push_back(o.second);
     }
     for (int fd : dead) drop(fd);
   }
 
   // other references to granule i's dma-buf: the kernel's fdinfo "count" is the file's
   // reference count without procfs's own; the broker's exported fd is one of them. -1 = unknown
-  int refs(int i) const {
+  int refs(int i) const { return fds[i] < 0 ? -1 : fd_refs(fds[i]); }
+
+  static int fd_refs(int fd) {
     char path[64];
-    std::snprintf(path, sizeof path, "/proc/self/fdinfo/%d", fds[i]);
+    std::snprintf(path, sizeof path, "/proc/self/fdinfo/%d", fd);
     FILE* f = std::fopen(path, "r");
     if (!f) return -1;
     char line[256];
@@ -625,16 +787,19 @@ struct Broker {
   const char* policy_name() const { return policy == kRefs ? "refs" : policy == kExit ? "exit" : "trust"; }
 
   std::string stat() const {
-    size_t held = 0, waiting = 0, scrub_n = 0, owed = 0;
+    size_t held = 0, waiting = 0, scrub_n = 0, owed = 0, extra = 0;
     for (auto& kv : clients) {
       held += kv.second.held.size();
       waiting += !kv.second.waiting.empty();
       owed += size_t(kv.second.owed);
+      extra += size_t(kv.second.extra);
     }
     for (auto& s : scrubbing) scrub_n += s.idx.size();
     char b[4096];
-    std::snprintf(b, sizeof b,
+    int n = std::snprintf(b, sizeof b,
                   "{\"boot\": \"%s\", \"device\": %d, \"granule_bytes\": %zu, \"granules\": %d, \"granules_max\": %d, "
+                  "\"target\": %d, \"given_back\": %llu, \"pressure_given\": %llu, \"low_water_bytes\": %zu, "
+                  "\"extra\": %zu, \"extends\": %llu, \"extended\": %llu, \"uncommitted\": %ld, \"ends\": %llu, "
                   "\"grown\": %llu, \"free\": %zu, "
                   "\"held\": %zu, \"owed\": %zu, \"streamed\": %llu, \"more_msgs\": %llu, \"scrubbing\": %zu, \"waiting\": %zu, \"grants\": %zu, \"takes\": %llu, "
                   "\"releases\": %llu, \"refused\": %llu, \"revokes\": %llu, \"revoked\": %zu, \"timeouts\": %llu, "
@@ -644,7 +809,8 @@ struct Broker {
                   "\"scrub_ms_total\": %.3f, \"scrub_ms_last\": %.3f, \"setup_ms\": %.1f, \"loop_ms_max\": %.3f, "
                   "\"release_ms_max\": %.3f, \"scrub_enqueue_ms_max\": %.3f, \"take_wait_ms_last\": %.3f, "
                   "\"take_wait_ms_max\": %.3f, \"send_ms_max\": %.3f, \"last_send_at\": %.6f}\n",
-                  boot.c_str(), device, gran, count, count_max, grown, free_list.size(), held, owed, streamed, more_msgs, scrub_n, waiting, grants.size(), takes,
+                  boot.c_str(), device, gran, count, count_max, target, given_back, pressure_given, low_water_bytes,
+                  extra, extends, extended, uncommitted(), ends, grown, free_list.size(), held, owed, streamed, more_msgs, scrub_n, waiting, grants.size(), takes,
                   releases, refused, revokes, revoked.size(), timeouts, expired, busy, idle_dropped, peer_refused,
                   clients.size(), quarantined(), quarantined_total, lost, scrub_fn ? "gs_scrub" : "memset", policy_name(),
                   quarantine_s_last * 1e3,
@@ -652,7 +818,7 @@ struct Broker {
                   base_refs.empty() ? -1 : base_refs[0], scrubbed_bytes, scrub_s_total * 1e3, scrub_s_last * 1e3,
                   setup_s * 1e3, loop_s_max * 1e3, release_s_max * 1e3, scrub_enqueue_s_max * 1e3,
                   take_wait_s_last * 1e3, take_wait_s_max * 1e3, send_s_max * 1e3, last_send_at);
-    return b;
+    return n > 0 && size_t(n) < sizeof b ? std::string(b) : std::string("{}\n");
   }
 
   std::string list() const {
@@ -675,6 +841,33 @@ struct Broker {
     }
   }
 
+  // the words of a request line (single spaces; anything else is not a request)
+  static std::vector<std::string> words(const std::string& line) {
+    std::vector<std::string> w;
+    size_t i = 0;
+    while (i <= line.size()) {
+      size_t j = line.find(' ', i);
+      if (j == std::string::npos) j = line.size();
+      w.push_back(line.substr(i, j - i));
+      i = j + 1;
+    }
+    return w;
+  }
+
+  // decimal digits only, no overflow
+  static bool u64(const std::string& s, unsigned long long* v) {
+    if (s.empty() || s.size() > 20) return false;
+    unsigned long long x = 0;
+    for (char ch : s) {
+      if (ch < '0' || ch > '9') return false;
+      unsigned d = unsigned(ch - '0');
+      if (x > (~0ull - d) / 10) return false;
+      x = x * 10 + d;
+    }
+    *v = x;
+    return true;
+  }
+
   // "TAKE <token>" or "TAKE <token> STREAM"
   static bool take_line(const std::string& line, char* tok, bool* stream) {
     char opt[16] = {0};
@@ -692,13 +885,40 @@ struct Broker {
     return false;
   }
 
+  // "EXTEND <k>": granules beyond the grant for a holder that is owed nothing, up to its limit,
+  // from granules no grant claims; "XFDS 0" when there are none (the pod uses the driver)
+  void extend(int fd, Client& c, unsigned long long k) {
+    auto g = c.token.empty() ? grants.end() : grants.find(c.token);
+    int j = 0;
+    if (g != grants.end() && g->second.holder == fd) {
+      long room = long(g->second.limit) - long(c.held.size());
+      j = int(std::max(0L, std::min<long>({long(std::min<unsigned long long>(k, 1u << 20)), room, long(lendable())})));
+    }
+    std::vector<int> idx = pop_free(j);
+    c.held.insert(c.held.end(), idx.begin(), idx.end());
+    c.extra += int(idx.size());
+    ++extends;
+    extended += idx.size();
+    if (!send_fds(fd, idx, "XFDS")) drop(fd);
+  }
+
+  int avail(int fd, const Client& c) const {
+    auto g = c.token.empty() ? grants.end() : grants.find(c.token);
+    if (g == grants.end() || g->second.holder != fd || c.owed > 0) return 0;
+    return int(std::max(0L, std::min<long>(long(g->second.limit) - long(c.held.size()), long(lendable()))));
+  }
+
   void on_line(int fd, const std::string& line) {
     Client& c = clients[fd];
     c.asked = true;
     char tok[129] = {0};
-    unsigned long long bytes = 0;
-    char extra = 0;
-    if (c.admin && std::sscanf(line.c_str(), "GRANT %128s %llu %c", tok, &bytes, &extra) == 2 && valid_token(tok)) {
+    std::vector<std::string> w = words(line);
+    unsigned long long bytes = 0, limit = 0, k = 0;
+    std::string tk = w.size() > 1 ? w[1] : std::string();
+    bool tok_ok = tk.size() <= 128 && valid_token(tk.c_str());
+    if (tok_ok) std::memcpy(tok, tk.c_str(), tk.size() + 1);
+    if (c.admin && w[0] == "GRANT" && (w.size() == 3 || w.size() == 4) && tok_ok && u64(w[2], &bytes) &&
+        (w.size() == 3 || u64(w[3], &limit))) {
       // in granules, without overflow: bytes beyond the broker's size are refused before rounding
       // (a broker still growing honours a grant up to its full size as its granules arrive)
       unsigned long long cap = (unsigned long long)count_max * (unsigned long long)gran;
@@ -708,13 +928,20 @@ struct Broker {
         return;
       }
       int n = int(bytes / gran + (bytes % gran ? 1 : 0));
+      int lim = int(std::min<unsigned long long>(std::max(limit, bytes), cap) / gran);  // whole granules of the quota
       auto& gr = grants[tok];  // a repeated grant (a re-prepared answer, a re-grant) refreshes it
       gr.granules = n;
+      gr.limit = std::max(lim, n);
       gr.at = now_s();
       if (revoked.erase(tok)) revoked_order.erase(std::find(revoked_order.begin(), revoked_order.end(), std::string(tok)));
       reply(fd, "OK " + std::to_string(n) + "\n");
       serve_waiting();
-    } else if (c.admin && std::sscanf(line.c_str(), "REVOKE %128s %c", tok, &extra) == 1 && valid_token(tok)) {
+    } else if (c.admin && w[0] == "SIZE" && w.size() == 2 && (w[1] == "max" || u64(w[1], &k))) {
+      target = w[1] == "max" ? count_max : int(std::min<unsigned long long>(k, (unsigned long long)count_max));
+      shrink_to_target();
+      grow();
+      reply(fd, "OK " + std::to_string(count) + " " + std::to_string(target) + "\n");
+    } else if (c.admin && w[0] == "REVOKE" && w.size() == 2 && tok_ok) {
       std::string t(tok);
       int held = 0;
       auto g = grants.find(t);
@@ -723,8 +950,10 @@ struct Broker {
           auto h = clients.find(g->second.holder);
           if (h != clients.end()) {
             h->second.token.clear();  // its end returns the granules, the grant is gone already
-            h->second.owed = 0;       // and it is lent no more of them
+            h->second.owed = 0;       // and it is lent no more of them: it is told so
             held = int(h->second.held.size());
+            reply(h->first, "END\n");
+            ++ends;
           }
         }
         grants.erase(g);
@@ -743,6 +972,14 @@ struct Broker {
       reply(fd, list());
     } else if (c.admin && line == "STAT") {
       reply(fd, stat());
+    } else if (!c.admin && w[0] == "EXTEND" && w.size() == 2 && u64(w[1], &k) && k > 0 && !c.token.empty() &&
+               c.owed == 0 && c.waiting.empty()) {
+      extend(fd, c, k);
+    } else if (!c.admin && line == "AVAIL" && !c.token.empty() && c.waiting.empty()) {
+      reply(fd, "AVAIL " + std::to_string(avail(fd, c)) + "\n");
+    } else if (!c.admin && (w[0] == "EXTEND" || line == "AVAIL") && c.waiting.empty() && !c.held.empty()) {
+      // a holder whose grant was revoked: nothing more
+      reply(fd, w[0] == "EXTEND" ? "XFDS 0 " + std::to_string(gran) + "\n" : std::string("AVAIL 0\n"));
     } else if (!c.admin && c.held.empty() && c.waiting.empty() && c.token.empty() && take_line(line, tok, &c.stream)) {
       if (revoked.count(tok)) {
         ++refused;
@@ -796,10 +1033,20 @@ struct Broker {
 int main(int argc, char** argv) {
   std::string sock, admin, pci, policy = "auto";
   Broker b;
-  double gib = 0, reserve_gib = 16;
+  double gib = 0, reserve_gib = 16, low_water_gib = -1;
   size_t gran_mib = 1024;
-  for (int i = 1; i + 1 < argc; i += 2) {
+  bool start_empty = false;
+  for (int i = 1; i < argc; i += 2) {
     std::string k = argv[i];
+    if (k == "--start-empty") {
+      start_empty = true;
+      --i;
+      continue;
+    }
+    if (i + 1 >= argc) {
+      std::fprintf(stderr, "gpushare-hbm-broker: %s needs a value\n", k.c_str());
+      return 2;
+    }
     const char* v = argv[i + 1];
     if (k == "--socket") sock = v;
     else if (k == "--admin-socket") admin = v;
@@ -817,6 +1064,7 @@ int main(int argc, char** argv) {
     else if (k == "--release-policy") policy = v;
     else if (k == "--scrub-chunk") b.scrub_chunk = std::atoi(v);
     else if (k == "--scrub-kernel") b.scrub_path = v;
+    else if (k == "--low-water-gib") low_water_gib = std::atof(v);
     else {
       std::fprintf(stderr, "gpushare-hbm-broker: unknown flag %s\n", k.c_str());
       return 2;
@@ -825,7 +1073,7 @@ int main(int argc, char** argv) {
   if (sock.empty() || (policy != "auto" && policy != "refs" && policy != "exit" && policy != "trust")) {
     std::fprintf(stderr, "usage: gpushare-hbm-broker --socket PATH [--admin-socket PATH] [--device N | --pci-bus-id BDF] "
                          "[--gib N | --reserve-gib N] [--granule-mib 1024] [--wait-s 30] [--ungranted-wait-s 10] "
-                         "[--release-policy auto|refs|exit|trust]\n");
+                         "[--release-policy auto|refs|exit|trust] [--start-empty] [--low-water-gib N]\n");
     return 2;
   }
   if (admin.empty()) admin = sock + ".admin";
@@ -849,14 +1097,15 @@ int main(int argc, char** argv) {
   size_t target = gib > 0 ? size_t(gib * double(1ull << 30)) : (tot > b.reserve_bytes ? tot - b.reserve_bytes : 0);
   if (gib > 0) b.reserve_bytes = size_t(2) << 30;  // --gib: leave the driver a small margin while growing
   size_t free_now = fr > b.reserve_bytes ? fr - b.reserve_bytes : 0;
-  b.setup(target, std::min(target, free_now));
-  bool counted = !b.base_refs.empty() && b.base_refs[0] >= 0;
-  b.policy = policy == "refs" ? kRefs : policy == "exit" ? kExit : policy == "trust" ? kTrust : (counted ? kRefs : kExit);
-  if (b.policy == kRefs && !counted) {
-    std::fprintf(stderr, "gpushare-hbm-broker: --release-policy refs needs the dma-buf count in fdinfo, which this "
-                         "kernel does not report\n");
-    return 2;
-  }
+  b.low_water_bytes = size_t((low_water_gib >= 0 ? low_water_gib : double(b.reserve_bytes) / double(1ull << 30) / 2) *
+                             double(1ull << 30));
+  b.setup(target, std::min(target, free_now), start_empty);
+  // the release policy: auto = refs where the kernel counts a dma-buf's references. Known from the
+  // first granule, or a throwaway export when there is none; on a full device, at the first
+  // granule grown (nothing can be lent before it)
+  b.policy_auto = policy == "auto";
+  b.policy = policy == "refs" ? kRefs : policy == "exit" ? kExit : policy == "trust" ? kTrust : kRefs;
+  b.choose_policy();
   signal(SIGTERM, on_signal);
   signal(SIGINT, on_signal);
   signal(SIGPIPE, SIG_IGN);
@@ -909,10 +1158,12 @@ int main(int argc, char** argv) {
       }
     }
     double t = now_s();
-    std::vector<int> late, idle;
+    std::vector<int> late, idle, ended;
     for (auto& kv : b.clients) {
       const Client& c = kv.second;
-      if (!c.waiting.empty()) {
+      if (c.owed > 0 && t - c.wait_since > b.wait_s) {
+        ended.push_back(kv.first);   // owed granules that did not come in time: cancelled
+      } else if (!c.waiting.empty()) {
         // TAKEs that waited too long are refused (their grant stays for a retry); a TAKE with no
         // grant at all gets a shorter deadline than one waiting for a retiring pod's granules
         bool granted = b.grants.count(c.waiting) > 0;
@@ -931,13 +1182,22 @@ int main(int argc, char** argv) {
       ++b.idle_dropped;
       b.drop(fd);
     }
+    for (int fd : ended) {
+      // the shim takes any line but MORE as the end of its stream: its grant (and its ledger
+      // charge) shrinks to what it has, and it allocates the rest from the driver. A taker still
+      // owed granules no longer holds up the ones behind it.
+      ++b.ends;
+      b.clients[fd].owed = 0;
+      Broker::reply(fd, "END\n");
+    }
     bool back = b.reap_scrubs();
     if (!b.quarantine.empty()) b.sweep_quarantine();
-    if (b.count < b.count_max && t - last_grow > 1.0) {
+    if (b.count < b.target && t - last_grow > 1.0) {
       last_grow = t;
       b.grow();
     }
-    if (back || !late.empty()) b.serve_waiting();
+    b.relieve_pressure(t);
+    if (back || !late.empty() || !ended.empty()) b.serve_waiting();
     b.loop_s_max = std::max(b.loop_s_max, now_s() - t_pass);
     // with a TTL, grants of pods that never started (deleted before admission) do not pile up;
     // without one (the default) the plugin's revocations do that

@@ -113,6 +113,12 @@ int ioctl(int fd, unsigned long req, ...) {
    (pods of a previous broker) until that many ms after start */
 static size_t g_held = 0;
 static double g_held_until = 0;
+/* FAKE_HIP_LATE_GIB / FAKE_HIP_LATE_MS / FAKE_HIP_LATE_FOR_MS: "another process" takes that much
+   of the device that many ms after start, and gives it back after FOR_MS (0: keeps it) — driver
+   pressure on a broker that holds the rest */
+static size_t g_late = 0;
+static double g_late_at = 0, g_late_until = 0;
+static int g_late_state = 0;
 static double fake_now(void);
 static void total_init(void) {     /* FAKE_HIP_TOTAL_GIB: the "device" size (default 16 GiB) */
   static int done = 0;
@@ -126,12 +132,26 @@ static void total_init(void) {     /* FAKE_HIP_TOTAL_GIB: the "device" size (def
     __atomic_add_fetch(&g_used, g_held, __ATOMIC_ACQ_REL);
     g_held_until = fake_now() + (hm ? atof(hm) : 0) / 1e3;
   }
+  const char* lg = getenv("FAKE_HIP_LATE_GIB");
+  if (lg && atof(lg) > 0) {
+    const char* lm = getenv("FAKE_HIP_LATE_MS");
+    const char* lf = getenv("FAKE_HIP_LATE_FOR_MS");
+    g_late = (size_t)(atof(lg) * (double)(1ull << 30));
+    g_late_at = fake_now() + (lm ? atof(lm) : 0) / 1e3;
+    g_late_until = lf && atof(lf) > 0 ? g_late_at + atof(lf) / 1e3 : 0;
+  }
+}
+static void late_tick(void) {
+  double t = fake_now();
+  if (g_late_state == 0 && g_late && t >= g_late_at) { __atomic_add_fetch(&g_used, g_late, __ATOMIC_ACQ_REL); g_late_state = 1; }
+  if (g_late_state == 1 && g_late_until > 0 && t >= g_late_until) { __atomic_fetch_sub(&g_used, g_late, __ATOMIC_ACQ_REL); g_late_state = 2; }
 }
 static void held_release(void) {
   if (g_held && fake_now() >= g_held_until) { __atomic_fetch_sub(&g_used, g_held, __ATOMIC_ACQ_REL); g_held = 0; }
 }
 static int kfd(size_t n, uint64_t* h) {
   total_init();
+  late_tick();
   struct kfd_alloc a = {0, n, 0, 0, 1, 1u /* VRAM */};
   const char* pf = getenv("FAKE_HIP_PROBE_FIXED");
   void* probe = NULL;
@@ -179,7 +199,11 @@ static void runtime_init(void) {
   const char* v = getenv("FAKE_HIP_INIT_KFD");
   if (v && *v == '1') { uint64_t h; kfd((size_t)2 << 20, &h); }
 }
-hipError_t hipMemGetInfo(size_t* f, size_t* t) { total_init(); held_release(); runtime_init(); *f = g_total - __atomic_load_n(&g_used, __ATOMIC_ACQUIRE); *t = g_total; return 0; }
+hipError_t hipMemGetInfo(size_t* f, size_t* t) {
+  total_init(); held_release(); late_tick(); runtime_init();
+  size_t u = __atomic_load_n(&g_used, __ATOMIC_ACQUIRE);
+  *f = u < g_total ? g_total - u : 0; *t = g_total; return 0;
+}
 hipError_t hipDeviceTotalMem(size_t* b, int d) { total_init(); *b = g_total; return 0; }
 hipError_t hipMemCreate(uint64_t* h, size_t n, const void* prop, unsigned long long fl) { return kfd(n, h); }
 hipError_t hipMemRelease_imported(uint64_t h);
@@ -308,3 +332,14 @@ hipError_t hipStreamIsCapturing(void* s, int* st) { *st = 0; return 0; }
 hipError_t hipDeviceGetDefaultMemPool(void** pool, int dev) { *pool = (void*)0x1; return 0; }
 hipError_t hipMallocFromPoolAsync(void** p, size_t n, void* pool, void* s) { return hipMallocAsync(p, n, s); }
 hipError_t hipMemGetAllocationPropertiesFromHandle(void* prop, uint64_t h) { return 1; }
+/* what the runtime answers for arena memory (VMM mappings of imported dma-bufs), measured on MI355X
+   (profiles/r6/arena_probe.jsonl): hipIpcGetMemHandle refuses it; hipMemRetainAllocationHandle
+   hands out the mapping's handle — the broker's granule, which the caller could release */
+hipError_t hipIpcGetMemHandle(void* h, void* p) { return 1; }
+hipError_t hipIpcOpenMemHandle(void** p, char h[64], unsigned f) { return 1; }
+hipError_t hipIpcCloseMemHandle(void* p) { return 1; }
+hipError_t hipMemGetAddressRange(void** b, size_t* n, void* p) { if (b) *b = (void*)((uintptr_t)p & ~((1ull << 30) - 1)); if (n) *n = 1ull << 30; return 0; }
+hipError_t hipMemRetainAllocationHandle(uint64_t* h, void* p) { *h = IMPORTED | 1; return 0; }
+hipError_t hipStreamCreate(void** s) { *s = calloc(1, 8); return 0; }
+hipError_t hipStreamCreateWithPriority(void** s, unsigned f, int pr) { *s = calloc(1, 8); return 0; }
+hipError_t hipStreamDestroy(void* s) { return 0; }

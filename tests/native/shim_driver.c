@@ -12,6 +12,8 @@
 #include <sys/ioctl.h>
 #include <sys/stat.h>
 #include <sys/wait.h>
+#include <signal.h>
+#include <time.h>
 #include <unistd.h>
 static int g_render_fd = -1, g_dup_fd = -1, g_hold_pipe = -1;
 static pid_t g_hold_pid = -1;
@@ -65,6 +67,13 @@ static void* worker(void* v) {
   return 0;
 }
 typedef int (*stats_fn)(uint64_t*, uint64_t*, uint64_t*, uint64_t*);
+/* IPC (hip_runtime_api.h: hipIpcMemHandle_t is 64 bytes, passed by value to hipIpcOpenMemHandle) */
+typedef struct { char reserved[64]; } ipch_t;
+hipError_t hipIpcGetMemHandle(ipch_t*, void*); hipError_t hipIpcOpenMemHandle(void**, ipch_t, unsigned);
+hipError_t hipIpcCloseMemHandle(void*); hipError_t hipMemGetAddressRange(void**, size_t*, void*);
+hipError_t hipMemRetainAllocationHandle(uint64_t*, void*);
+static double now_ms(void) { struct timespec t; clock_gettime(CLOCK_MONOTONIC, &t); return t.tv_sec * 1e3 + t.tv_nsec / 1e6; }
+static void on_term(int sig) { (void)sig; const char m[] = "{\"op\":\"handled\"}\n"; ssize_t r = write(1, m, sizeof m - 1); (void)r; _exit(0); }
 int main(int argc, char** argv) {
   void* ptrs[4096]; int np = 0;
   for (int i = 1; i < argc; ++i) {
@@ -181,6 +190,45 @@ int main(int argc, char** argv) {
       hipDeviceGetDefaultMemPool(&pool, 0); int e = hipMallocFromPoolAsync(&p, n, pool, 0);
       printf("{\"op\":\"poolasync\",\"n\":%zu,\"err\":%d,\"idx\":%d,\"p\":%llu}\n", n, e, e ? -1 : np,
              (unsigned long long)(uintptr_t)p); if (!e) ptrs[np++] = p; }
+    else if (!strcmp(argv[i], "timefree")) { int k = atoi(argv[++i]); double t = now_ms(); int e = hipFree(ptrs[k]); ptrs[k] = 0;
+      printf("{\"op\":\"timefree\",\"err\":%d,\"ms\":%.3f}\n", e, now_ms() - t); }
+    else if (!strcmp(argv[i], "timealloc")) { size_t n = strtoull(argv[++i], 0, 10); void* p = 0; double t = now_ms();
+      int e = hipMalloc(&p, n); printf("{\"op\":\"timealloc\",\"err\":%d,\"ms\":%.3f,\"idx\":%d,\"p\":%llu}\n", e,
+      now_ms() - t, e ? -1 : np, (unsigned long long)(uintptr_t)p); if (!e) ptrs[np++] = p; }
+    else if (!strcmp(argv[i], "freestats")) { int (*f)(uint64_t*, uint64_t*, uint64_t*, uint64_t*) =
+        (int (*)(uint64_t*, uint64_t*, uint64_t*, uint64_t*))dlsym(RTLD_DEFAULT, "gpushare_shim_free_stats");
+      uint64_t d = 0, pe = 0, w = 0, st = 0; if (f) f(&d, &pe, &w, &st);
+      printf("{\"op\":\"freestats\",\"deferred\":%llu,\"pending\":%llu,\"device_waits\":%llu,\"streams\":%llu}\n",
+             (unsigned long long)d, (unsigned long long)pe, (unsigned long long)w, (unsigned long long)st); }
+    else if (!strcmp(argv[i], "extra")) { int (*f)(uint64_t*, uint64_t*, uint64_t*, uint64_t*, uint64_t*) =
+        (int (*)(uint64_t*, uint64_t*, uint64_t*, uint64_t*, uint64_t*))dlsym(RTLD_DEFAULT, "gpushare_shim_arena_extra");
+      uint64_t x = 0, xd = 0, da = 0, db = 0, lim = 0; int on = f ? f(&x, &xd, &da, &db, &lim) : -2;
+      printf("{\"op\":\"extra\",\"on\":%d,\"extends\":%llu,\"extended\":%llu,\"driver_allocs\":%llu,\"driver_bytes\":%llu,\"limit\":%llu}\n",
+             on, (unsigned long long)x, (unsigned long long)xd, (unsigned long long)da, (unsigned long long)db, (unsigned long long)lim); }
+    else if (!strcmp(argv[i], "ipcget")) { int k = atoi(argv[++i]); ipch_t h; memset(&h, 0, sizeof h);
+      int e = hipIpcGetMemHandle(&h, ptrs[k]); char hex[129]; for (int j = 0; j < 64; ++j) sprintf(hex + 2 * j, "%02x", (unsigned char)h.reserved[j]);
+      printf("{\"op\":\"ipcget\",\"err\":%d,\"handle\":\"%s\"}\n", e, hex); }
+    else if (!strcmp(argv[i], "ipcopen")) { const char* hex = argv[++i]; ipch_t h; memset(&h, 0, sizeof h);
+      for (int j = 0; j < 64 && hex[2 * j]; ++j) { unsigned v = 0; sscanf(hex + 2 * j, "%2x", &v); h.reserved[j] = (char)v; }
+      void* p = 0; int e = hipIpcOpenMemHandle(&p, h, 1);
+      printf("{\"op\":\"ipcopen\",\"err\":%d,\"idx\":%d,\"p\":%llu}\n", e, e ? -1 : np, (unsigned long long)(uintptr_t)p);
+      if (!e) ptrs[np++] = p; }
+    else if (!strcmp(argv[i], "ipcclose")) { int k = atoi(argv[++i]); int e = hipIpcCloseMemHandle(ptrs[k]); ptrs[k] = 0;
+      printf("{\"op\":\"ipcclose\",\"err\":%d}\n", e); }
+    else if (!strcmp(argv[i], "ipcstats")) { int (*f)(uint64_t*, uint64_t*, uint64_t*, uint64_t*) =
+        (int (*)(uint64_t*, uint64_t*, uint64_t*, uint64_t*))dlsym(RTLD_DEFAULT, "gpushare_shim_ipc_stats");
+      uint64_t ex = 0, sv = 0, op = 0, on = 0; if (f) f(&ex, &sv, &op, &on);
+      printf("{\"op\":\"ipcstats\",\"exports\":%llu,\"served\":%llu,\"opened\":%llu,\"open_now\":%llu}\n",
+             (unsigned long long)ex, (unsigned long long)sv, (unsigned long long)op, (unsigned long long)on); }
+    else if (!strcmp(argv[i], "range")) { int k = atoi(argv[++i]); size_t off = strtoull(argv[++i], 0, 10); void* b = 0; size_t n = 0;
+      int e = hipMemGetAddressRange(&b, &n, (char*)ptrs[k] + off);
+      printf("{\"op\":\"range\",\"err\":%d,\"base\":%llu,\"size\":%zu}\n", e, (unsigned long long)(uintptr_t)b, n); }
+    else if (!strcmp(argv[i], "retain")) { int k = atoi(argv[++i]); uint64_t h = 0; int e = hipMemRetainAllocationHandle(&h, ptrs[k]);
+      printf("{\"op\":\"retain\",\"err\":%d}\n", e); }
+    else if (!strcmp(argv[i], "forksleep")) { int ms = atoi(argv[++i]); fflush(stdout); pid_t c = fork();
+      if (c == 0) { usleep((useconds_t)ms * 1000); _exit(0); }
+      printf("{\"op\":\"forksleep\",\"pid\":%d}\n", (int)c); }
+    else if (!strcmp(argv[i], "sigterm_handler")) { signal(SIGTERM, on_term); printf("{\"op\":\"sigterm_handler\"}\n"); }
     else if (!strcmp(argv[i], "wait")) { fflush(stdout); char b[256]; while (read(0, b, sizeof b) > 0) {} }  /* until stdin closes */
     fflush(stdout);
   }

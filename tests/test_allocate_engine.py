@@ -590,6 +590,7 @@ class _FakeBrokerAdmin:
         os.makedirs(os.path.dirname(path), exist_ok=True)
         self.grants, self.revokes = [], []
         self.held: dict = {}
+        self.limits: dict = {}
         self.ok, self.boot = ok, boot
         self.ls = _s.socket(_s.AF_UNIX, _s.SOCK_STREAM)
         self.ls.bind(path)
@@ -620,7 +621,8 @@ class _FakeBrokerAdmin:
                 self.held.pop(w[1], None)
                 c.sendall(b"OK 0\n")
             else:
-                _, tok, nbytes = w
+                _, tok, nbytes = w[:3]
+                self.limits[tok] = int(w[3]) if len(w) > 3 else None     # the pod's whole quota
                 self.grants.append((tok, int(nbytes)))
                 if self.ok:
                     self.held[tok] = int(nbytes) >> 30
@@ -661,7 +663,7 @@ def test_hbm_broker_grant_rides_in_the_prepared_answer(tmp_path):
         assert len(mounts) == 1 and mounts[0].host_path == str(hdir / "gpu1") and mounts[0].read_only
         # 16 of 64 GiB -> a 16 GiB quota; 94 % of it in whole granules = 15 GiB, granted once
         assert al._hbm.flush()
-        assert admin.grants == [(tok, 15 << 30)]
+        assert admin.grants == [(tok, 15 << 30)] and admin.limits[tok] == 16 << 30   # may borrow up to the quota
         assert al._prepared(pod, "uid-h0", 1, 16).body == c.body
         assert al._hbm.flush() and len(admin.grants) == 1
         # the same node secret in another instance: the same token for the same pod and slot

@@ -175,6 +175,27 @@ def test_shipped_manifests_run_a_node(hostroot, stub_runtime, native_shim):
                            env=dict(os.environ, PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", "")))
         assert r.returncode == 0, r.stdout + r.stderr
         assert NODE in r.stdout and "72/576" in r.stdout.replace(" ", ""), r.stdout   # 4 x 2 + 64 GiB
+
+        # ---- the node is labelled cgpu.disable.isolation=true while running. The
+        # brokers (--start-empty: sized by the plugin) give their HBM back to the driver, answers carry
+        # CGPU_DISABLE and no shim; the label removed, the brokers take the GPU again
+        adm_b = hb.HBMBroker.attach(hb.pod_socket(hdir, gi), hb.admin_socket(hdir, gi))
+        assert adm_b.stat()["target"] == adm_b.stat()["granules_max"] == 276        # 288 less the 12 GiB reserve
+        client.patch_node(NODE, {"metadata": {"labels": {const.NODE_LABEL_DISABLE_CGPU: "true"}}})
+        assert D.wait_for(lambda: adm_b.stat()["target"] == 0 and adm_b.stat()["granules"] == 0, 40, 0.2), adm_b.stat()
+        assert adm_b.list()["grants"] == {}                                          # every grant revoked
+        off = client.create_pod("default", {"apiVersion": "v1", "kind": "Pod",
+                                            "metadata": {"name": "llama-1", "namespace": "default"},
+                                            "spec": {**tpl["spec"], "schedulerName": "default-scheduler"}})
+        placed = []
+        assert D.wait_for(lambda: placed.append(sched.schedule(off, [NODE])) or placed[-1] == NODE, 10, 0.1)
+        adm = kubelet.admit(client.get_pod("default", "llama-1"))
+        assert adm.error is None, adm.error
+        envs = adm.responses[0].envs
+        assert envs[const.ENV_CGPU_DISABLE] == "true" and "LD_PRELOAD" not in envs and const.ENV_HBM_TOKEN not in envs
+        client.patch_node(NODE, {"metadata": {"labels": {const.NODE_LABEL_DISABLE_CGPU: None}}})
+        assert D.wait_for(lambda: adm_b.stat()["target"] == 276 and adm_b.stat()["granules"] == 276, 40, 0.2), \
+            adm_b.stat()
     finally:
         _stop(ext)
         _stop(brokers)

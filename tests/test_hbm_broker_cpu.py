@@ -92,7 +92,7 @@ class Pod:
                 return head.decode(), []
             head += c
         head = head.decode().strip()
-        if not head.startswith("FDS "):
+        if head.split(" ")[0] not in ("FDS", "MORE", "XFDS"):
             return head, []
         n = int(head.split()[1])
         fds = []
@@ -177,11 +177,11 @@ def test_streaming_take_gets_what_is_free_at_once_and_the_rest_as_it_comes_back(
     t = time.perf_counter()
     st = StreamPod(broker.path, "s" * 32)
     head, fds = st.result()
-    assert head == f"FDS 2 {GIB} 4" and len(fds) == 2 and time.perf_counter() - t < 1.0   # no wait
+    assert head == f"FDS 2 {GIB} 4 4" and len(fds) == 2 and time.perf_counter() - t < 1.0   # no wait
     plain = Pod(broker.path, "p" * 32)           # arrives later: waits behind the streamer's owed 2
     time.sleep(0.1)
     late = StreamPod(broker.path, "q" * 32)      # a later streamer is accepted with nothing yet
-    assert late.result()[0] == f"FDS 0 {GIB} 1"
+    assert late.result()[0] == f"FDS 0 {GIB} 1 1"
     s = broker.stat()
     assert s["owed"] == 2 + 1 and s["waiting"] == 1 and s["streamed"] == 2 and s["free"] == 0
     holder.close()                               # 6 back: 2 owed to the streamer, then the plain 1, then 1 owed
@@ -207,7 +207,7 @@ def test_a_released_pods_granules_are_lent_as_their_scrub_progresses(broker_exe,
         holder = Pod(b.path, "h" * 32)
         assert holder.result()[0] == f"FDS 6 {GIB}"
         st = StreamPod(b.path, "s" * 32)
-        assert st.result()[0] == f"FDS 2 {GIB} 6"
+        assert st.result()[0] == f"FDS 2 {GIB} 6 6"
         t0 = time.perf_counter()
         holder.close()
         got = []
@@ -232,7 +232,7 @@ def test_a_streamer_that_leaves_while_owed_frees_its_place(broker):
     holder = Pod(broker.path, "h" * 32)
     assert holder.result()[0] == f"FDS 6 {GIB}"
     st = StreamPod(broker.path, "s" * 32)
-    assert st.result()[0] == f"FDS 2 {GIB} 5"
+    assert st.result()[0] == f"FDS 2 {GIB} 5 5"
     nxt = Pod(broker.path, "n" * 32)                 # a plain TAKE of 2, behind the streamer's owed 3
     time.sleep(0.2)
     assert broker.stat()["owed"] == 3 and broker.stat()["waiting"] == 1
@@ -250,8 +250,9 @@ def test_a_revoked_streamer_is_sent_no_more(broker):
     holder = Pod(broker.path, "h" * 32)
     assert holder.result()[0] == f"FDS 7 {GIB}"
     st = StreamPod(broker.path, "r" * 32)
-    assert st.result()[0] == f"FDS 1 {GIB} 4"
+    assert st.result()[0] == f"FDS 1 {GIB} 4 4"
     assert broker.admin(f"REVOKE {'r' * 32}") == "OK 1"
+    assert st.more(timeout=2)[0] == "END"            # told: the shim ends its stream at what it has
     holder.close()
     with pytest.raises(TimeoutError):
         st.more(timeout=0.5)
@@ -506,7 +507,7 @@ def test_a_sized_broker_grows_while_memory_comes_back_and_streams_grants_meanwhi
         assert _line(path + ".admin", f"GRANT {'g' * 32} {9 * GIB}") == "OK 9"     # up to the full 10
         assert _line(path + ".admin", f"GRANT {'x' * 32} {11 * GIB}") == "ERR size"
         pod = StreamPod(path, "g" * 32)
-        assert pod.result()[0] == f"FDS 6 {GIB} 9"
+        assert pod.result()[0] == f"FDS 6 {GIB} 9 9"
         head = pod.more(timeout=10)[0]                      # the rest once grown and zeroed
         assert head == f"MORE 3 {GIB}", head
         st = json.loads(_line(path + ".admin", "STAT"))
@@ -548,3 +549,150 @@ def test_a_restarted_broker_grows_back_when_old_tenants_exit(broker_exe, tmp_pat
     finally:
         p.terminate()
         assert p.wait(10) == 0
+
+
+class Holder(StreamPod):
+    """A pod's shim after its TAKE: asks for granules beyond its grant (EXTEND) and for what it
+    could still borrow (AVAIL) on the same connection."""
+
+    def ask(self, line, timeout=5.0):
+        self.s.sendall(line.encode() + b"\n")
+        return self.more(timeout)
+
+
+def test_extend_lends_only_granules_no_grant_claims_up_to_the_limit(broker):
+    """a pod may borrow granules beyond its grant, up to its quota (the
+    grant's limit), but only granules no grant claims: a grant not taken yet is a pod about to
+    start, and its granules must be there for it."""
+    assert broker.admin(f"GRANT {'a' * 32} {4 * GIB} {7 * GIB + 5}") == "OK 4"   # limit: 7 whole granules
+    assert broker.admin(f"GRANT {'b' * 32} {2 * GIB}") == "OK 2"                  # not taken yet
+    a = Holder(broker.path, "a" * 32)
+    assert a.result()[0] == f"FDS 4 {GIB} 4 7"
+    assert broker.stat()["uncommitted"] == 2
+    assert a.ask("AVAIL")[0] == "AVAIL 2"
+    head, fds = a.ask("EXTEND 5")
+    assert head == f"XFDS 2 {GIB}" and len(fds) == 2
+    assert a.ask("AVAIL")[0] == "AVAIL 0" and a.ask("EXTEND 1")[0] == f"XFDS 0 {GIB}"
+    b = Pod(broker.path, "b" * 32)
+    assert b.result()[0] == f"FDS 2 {GIB}"                   # the grant's granules were kept for it
+    st = broker.stat()
+    assert st["extra"] == 2 and st["extended"] == 2 and st["extends"] == 2 and st["held"] == 8 and st["free"] == 0
+    a.close()                                                # borrowed granules return with the rest
+    time.sleep(0.3)
+    st = broker.stat()
+    assert st["extra"] == 0 and st["free"] == 6 and st["held"] == 2
+    b.close()
+
+
+def test_extend_respects_the_limit_and_a_revoked_holder_gets_nothing(broker):
+    assert broker.admin(f"GRANT {'c' * 32} {2 * GIB} {3 * GIB}") == "OK 2"
+    c = Holder(broker.path, "c" * 32)
+    assert c.result()[0] == f"FDS 2 {GIB} 2 3"
+    assert c.ask("EXTEND 4")[0] == f"XFDS 1 {GIB}"           # 3 granules at most
+    assert c.ask("EXTEND 1")[0] == f"XFDS 0 {GIB}"
+    assert broker.admin(f"REVOKE {'c' * 32}") == "OK 3"
+    assert c.more()[0] == "END"
+    assert c.ask("EXTEND 1")[0] == f"XFDS 0 {GIB}" and c.ask("AVAIL")[0] == "AVAIL 0"
+    c.close()
+
+
+def test_owed_granules_that_never_come_are_cancelled_and_the_next_taker_is_answered(broker_exe, tmp_path):
+    """a streaming taker owed granules that never come back (a holder that keeps them)
+    must not hold up the takers behind it for ever: at --wait-s its stream is ended ("END": the
+    shim shrinks its grant to what it has and uses the driver for the rest), and the next taker
+    is served or ended in its turn."""
+    b = Broker(broker_exe, str(tmp_path / "hbm0.sock"), wait_s=1.0)
+    try:
+        b.admin(f"GRANT {'h' * 32} {6 * GIB}")
+        b.admin(f"GRANT {'s' * 32} {4 * GIB}")
+        b.admin(f"GRANT {'q' * 32} {1 * GIB}")
+        holder = Pod(b.path, "h" * 32)
+        assert holder.result()[0] == f"FDS 6 {GIB}"
+        t0 = time.monotonic()
+        s = StreamPod(b.path, "s" * 32)
+        assert s.result()[0] == f"FDS 2 {GIB} 4 4"
+        q = StreamPod(b.path, "q" * 32)
+        assert q.result()[0] == f"FDS 0 {GIB} 1 1"
+        assert s.more(timeout=3)[0] == "END" and 0.9 < time.monotonic() - t0 < 2.5
+        assert q.more(timeout=3)[0] == "END" and time.monotonic() - t0 < 3.5
+        st = b.stat()
+        assert st["ends"] == 2 and st["owed"] == 0 and st["held"] == 8
+        for p in (holder, s, q):
+            p.close()
+    finally:
+        b.stop()
+
+
+def test_size_gives_granules_back_and_takes_them_again(broker_exe, tmp_path):
+    """SIZE sets how much of the GPU the broker may hold (the plugin sends
+    SIZE 0 on a cgpu.disable.isolation node). Free granules go back to the driver at once, lent
+    ones when they come back; SIZE max grows it again."""
+    b = Broker(broker_exe, str(tmp_path / "hbm0.sock"))
+    try:
+        b.admin(f"GRANT {'a' * 32} {2 * GIB}")
+        a = Pod(b.path, "a" * 32)
+        assert a.result()[0] == f"FDS 2 {GIB}"
+        assert b.admin("SIZE 0") == "OK 2 0"                 # the 2 lent granules cannot go yet
+        st = b.stat()
+        assert st["granules"] == 2 and st["target"] == 0 and st["given_back"] == 6 and st["free"] == 0
+        a.close()
+        deadline = time.time() + 5
+        while b.stat()["granules"] and time.time() < deadline:
+            time.sleep(0.05)
+        assert b.stat()["granules"] == 0
+        assert b.admin("SIZE max") == "OK 8 8"               # taken again at once
+        deadline = time.time() + 5
+        while b.stat()["free"] < 8 and time.time() < deadline:
+            time.sleep(0.05)
+        st = b.stat()
+        assert st["free"] == 8 and st["scrubbed_bytes"] >= 10 * GIB   # new granules are zeroed first
+        assert b.admin("SIZE 3") == "OK 3 3" and b.stat()["free"] == 3
+        assert b.admin("SIZE -1").startswith("ERR") and b.admin("SIZE 99") == "OK 8 8"   # capped at its size
+    finally:
+        b.stop()
+
+
+def test_start_empty_holds_nothing_until_sized(broker_exe, tmp_path):
+    """--start-empty (the DaemonSet): nothing is held until the granter says how much, and the
+    release policy is still chosen from the kernel (a throwaway export: here the stub's memfds,
+    which fdinfo does not count, so "exit"); an explicit "refs" on such a kernel refuses to run
+    (the choice no longer depends on a granule 0 that may not exist)."""
+    b = Broker(broker_exe, str(tmp_path / "hbm0.sock"), policy="auto", extra=("--start-empty",))
+    try:
+        assert b.ready["granules"] == 0 and b.ready["release_policy"] == "exit"
+        assert b.stat()["target"] == 0
+        assert b.admin("SIZE max") == "OK 8 8"
+    finally:
+        b.stop()
+    exe, libdir = broker_exe
+    r = subprocess.run([exe, "--socket", str(tmp_path / "x.sock"), "--gib", "4", "--release-policy", "refs",
+                        "--start-empty"], env=dict(os.environ, LD_LIBRARY_PATH=libdir, ASAN_OPTIONS="detect_leaks=0"),
+                       capture_output=True, text=True, timeout=30)
+    assert r.returncode == 2 and "needs the dma-buf count" in r.stderr
+
+
+def test_driver_pressure_gives_free_granules_back_and_the_broker_grows_again(broker_exe, tmp_path):
+    """when the driver runs short (here "another process" takes 3 of the 4 GiB
+    the broker left it, for 1.5 s), free granules no grant claims go back to the driver until it
+    has --low-water-gib free; once it has more than the reserve again the broker grows back."""
+    b = Broker(broker_exe, str(tmp_path / "hbm0.sock"), gib=12, extra=("--low-water-gib", "3"),
+               env={"FAKE_HIP_TOTAL_GIB": "16", "FAKE_HIP_LATE_GIB": "3", "FAKE_HIP_LATE_MS": "600",
+                    "FAKE_HIP_LATE_FOR_MS": "1500"})
+    try:
+        b.admin(f"GRANT {'g' * 32} {4 * GIB}")
+        deadline = time.time() + 5
+        st = b.stat()
+        while st["pressure_given"] < 2 and time.time() < deadline:
+            time.sleep(0.05)
+            st = b.stat()
+        assert st["pressure_given"] == 2 and st["granules"] == 10, st   # driver: 1 -> 3 GiB free
+        deadline = time.time() + 8
+        while st["granules"] < 12 and time.time() < deadline:
+            time.sleep(0.1)
+            st = b.stat()
+        assert st["granules"] == 12 and st["grown"] >= 2, st
+        p = Pod(b.path, "g" * 32)                                        # the grant was never short
+        assert p.result()[0] == f"FDS 4 {GIB}"
+        p.close()
+    finally:
+        b.stop()

@@ -457,14 +457,18 @@ class FakeBroker:
     """The HBM broker's pod side (native/hbmbroker): answers one TAKE with ``granules`` fds, then
     records when the pod's connection ends (its granules would be scrubbed and lent again).
     ``stream``: [(delay_s, k), ...] answers a streaming TAKE with ``granules - sum(k)`` at once
-    ("FDS <k0> <gran> <total>") and each k after its delay ("MORE <k> <gran>"); with ``hangup``
-    it closes the connection at the first delay instead (a broker that went away)."""
+    ("FDS <k0> <gran> <total> <limit>") and each k after its delay ("MORE <k> <gran>"); with
+    ``hangup`` it closes the connection at the first delay instead (a broker that went away).
+    After that it answers EXTEND with up to ``extra`` granules beyond the grant (``limit``: the
+    pod's whole quota in granules, sent in the streaming header) and AVAIL with what is left."""
 
-    def __init__(self, path, granules=4, gran=GIB, refuse=False, stream=None, hangup=False):
+    def __init__(self, path, granules=4, gran=GIB, refuse=False, stream=None, hangup=False, extra=0, limit=None):
         import socket
         import threading
 
         self.granules, self.gran, self.refuse, self.stream, self.hangup = granules, gran, refuse, stream, hangup
+        self.extra, self.limit = extra, limit if limit is not None else granules + extra
+        self.requests = []
         self.took = None
         self.closed_at = None
         self.ls = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
@@ -493,9 +497,9 @@ class FakeBroker:
             for fd in fds:
                 os.close(fd)
 
-        if self.stream:
+        if self.stream is not None:
             later = sum(k for _, k in self.stream)
-            send(f"FDS {self.granules - later} {self.gran} {self.granules}\n", self.granules - later)
+            send(f"FDS {self.granules - later} {self.gran} {self.granules} {self.limit}\n", self.granules - later)
             for delay, k in self.stream:
                 time.sleep(delay)
                 if self.hangup:
@@ -508,8 +512,25 @@ class FakeBroker:
                     break
         else:
             send(f"FDS {self.granules} {self.gran}\n", self.granules)
-        while conn.recv(1):
-            pass
+        buf = b""
+        while True:
+            try:
+                c = conn.recv(1)
+            except OSError:
+                break
+            if not c:
+                break
+            buf += c
+            if not buf.endswith(b"\n"):
+                continue
+            line, buf = buf.decode().strip(), b""
+            self.requests.append(line)
+            if line.startswith("EXTEND "):
+                j = min(int(line.split()[1]), self.extra)
+                self.extra -= j
+                send(f"XFDS {j} {self.gran}\n", j)
+            elif line == "AVAIL":
+                conn.sendall(f"AVAIL {self.extra}\n".encode())
         self.closed_at = time.monotonic()
         conn.close()
 
@@ -538,9 +559,12 @@ def test_broker_arena_serves_hipmalloc_from_the_granted_granules(stub, native_sh
         assert arena == {"op": "arena", "on": 1, "size": 4 * GIB, "used": 3 * GIB + 512 * MIB}
         assert c2["err"] == 0 and c2["p"] == a3["p"]             # first fit reuses the freed range
         assert d1["err"] == 0 and d1["p"] == a3["p"] + 2 * GIB   # coalesced rest of it
-        assert e1["err"] == 2                                    # 4 GiB arena full: out of memory
-        assert info["total"] == 8 * GIB and info["free"] == 512 * MIB + 4 * GIB   # the arena's rest + the quota's rest
-        assert st["used"] == 4 * GIB                             # the arena is on the pod's ledger
+        # the 4 GiB arena is full and the broker lends nothing beyond the grant: the driver's, charged
+        assert e1["err"] == 0 and not a3["p"] <= e1["p"] < a3["p"] + 8 * GIB
+        assert b.requests == []                                  # a whole-grant answer has no limit beyond it
+        # what the pod can obtain: the arena's rest + the quota's rest (the stub's driver has room)
+        assert info["total"] == 8 * GIB and info["free"] == 512 * MIB + 3 * GIB
+        assert st["used"] == 5 * GIB                             # the arena (4) + the driver's 1
         assert rel_live["r"] == -1 and rel["r"] == 1             # released only once nothing is live
         assert arena_after["on"] == 0
         assert b.closed_at is not None and b.closed_at < t_end - 0.4   # handed back before exit
@@ -575,7 +599,7 @@ def test_streaming_take_maps_the_first_granules_and_waits_for_the_rest(stub, nat
         assert st["used"] == 4 * GIB                                         # the whole grant is charged
         assert big["err"] == 0 and big["p"] == small["p"] + 512 * MIB       # the granules join the first one's rest
         assert s1["mapped"] == 4 and s1["msgs"] == 2 and s1["waits"] >= 1 and s1["wait_ms"] >= 400
-        assert last["err"] == 2                                              # 1.5 GiB left of the grant: no wait
+        assert last["err"] == 0 and not small["p"] <= last["p"] < small["p"] + 8 * GIB   # 1.5 GiB left: the driver
         assert arena2["used"] == 2 * GIB + 512 * MIB and s2["mapped"] == 4
         assert time.monotonic() - t0 < 10
     finally:
@@ -604,8 +628,8 @@ def test_plain_take_and_a_stream_that_ends_early(stub, native_shim, tmp_path):
                      GPUSHARE_HBM_TOKEN="short", GPUSHARE_HBM_MORE_WAIT_S="5")
         assert r.returncode == 0, r.stderr
         small, big, arena, st, s = out
-        assert small["err"] == 0 and big["err"] == 2                 # the rest never came: out of memory
-        assert arena["size"] == GIB and st["used"] == GIB            # grant and ledger shrank to 1 granule
+        assert small["err"] == 0 and big["err"] == 0                 # the rest never came: the driver's
+        assert arena["size"] == GIB and st["used"] == 3 * GIB        # grant and ledger shrank to 1 granule
         assert s["granted"] == s["mapped"] == 1
     finally:
         cleanup(name)
@@ -855,4 +879,201 @@ def test_broker_fds_are_imported_the_way_the_runtime_reads_them(stub, native_shi
         assert out[1]["on"] == 1 and out[1]["size"] == 2 * GIB
         assert f"fds imported by {form}" in r.stderr
     finally:
+        cleanup(name)
+
+
+# ---- round 6: the whole quota usable, truthful free memory, frees that do not wait, IPC, fork and
+# exit hygiene ------------------------------------------------
+def test_extend_borrows_beyond_the_grant_then_the_driver_and_memgetinfo_tells_what_can_be_had(stub, native_shim,
+                                                                                                tmp_path):
+    """a pod can use its whole quota. Its grant is 4 granules of an 8 GiB quota
+    (limit 8); past the grant the shim asks the broker for granules beyond it (EXTEND, the broker
+    has 1 to lend), then uses the driver, charged to the same ledger. hipMemGetInfo reports what
+    the pod can actually obtain: the arena's rest plus the quota's rest bounded by the driver's
+    free memory and what the broker could lend (AVAIL), not the quota's rest alone."""
+    sock = str(tmp_path / "hbm.sock")
+    b = FakeBroker(sock, granules=4, stream=[], extra=1, limit=8)
+    name = ledger()
+    try:
+        out, r = run(stub, native_shim, ["alloc", 3 * GIB, "info", "alloc", 3 * GIB // 2, "extra", "alloc", GIB, "extra",
+                                         "arena", "stats", "info"],
+                     GPUSHARE_QUOTA_BYTES=8 * GIB, GPUSHARE_LEDGER=name, GPUSHARE_HBM_BROKER=sock,
+                     GPUSHARE_HBM_TOKEN="tok", FAKE_HIP_TOTAL_GIB=2)
+        assert r.returncode == 0, r.stderr
+        a3, info0, a15, x1, d1, x2, arena, st, info = out
+        # before: 1 GiB of the arena + min(4 GiB of quota, 2 GiB driver + 1 granule to borrow)
+        assert info0["free"] == GIB + 3 * GIB and info0["total"] == 8 * GIB
+        assert a15["err"] == 0 and a15["p"] == a3["p"] + 3 * GIB          # the borrowed granule joins the tail
+        assert x1["extends"] == 1 and x1["extended"] == 1 and x1["limit"] == 8 and x1["driver_allocs"] == 0
+        assert d1["err"] == 0 and not a3["p"] <= d1["p"] < a3["p"] + 8 * GIB   # nothing left to borrow: the driver
+        assert x2["driver_allocs"] == 1 and x2["driver_bytes"] == GIB
+        assert arena["size"] == 5 * GIB and arena["used"] == 3 * GIB + 3 * GIB // 2
+        assert st["used"] == 6 * GIB and st["denied"] == 0
+        # after: 0.5 GiB of the arena + min(2 GiB of quota, 1 GiB the driver still has + 0 to borrow)
+        assert info["free"] == GIB // 2 + GIB
+        assert b.requests == ["AVAIL", "EXTEND 1", "EXTEND 1", "AVAIL"]
+    finally:
+        cleanup(name)
+
+
+def test_extend_never_asks_beyond_the_quota_left(stub, native_shim, tmp_path):
+    sock = str(tmp_path / "hbm.sock")
+    b = FakeBroker(sock, granules=4, stream=[], extra=4, limit=8)
+    name = ledger()
+    try:
+        # 4.75 GiB quota: 4 granules charged, 0.75 GiB left, no whole granule to borrow
+        out, r = run(stub, native_shim, ["alloc", 4 * GIB, "alloc", GIB // 2, "extra", "stats"],
+                     GPUSHARE_QUOTA_BYTES=4 * GIB + 3 * GIB // 4, GPUSHARE_LEDGER=name, GPUSHARE_HBM_BROKER=sock,
+                     GPUSHARE_HBM_TOKEN="tok")
+        assert r.returncode == 0, r.stderr
+        a4, half, x, st = out
+        assert a4["err"] == 0 and half["err"] == 0 and x["extends"] == 0 and x["driver_allocs"] == 1
+        assert st["used"] == 4 * GIB + GIB // 2 and b.requests == []
+    finally:
+        cleanup(name)
+
+
+def test_hipfree_of_an_arena_block_does_not_wait_for_the_device(stub, native_shim, tmp_path):
+    """hipFree of an arena block used to synchronise the whole device. Now it
+    records an event on every stream of the device (and the null stream) and returns; the block is
+    reused once they have completed (here the stub's events complete 400 ms after they are
+    recorded), and an allocation that needs the room waits for them instead of going to the driver."""
+    sock = str(tmp_path / "hbm.sock")
+    FakeBroker(sock, granules=4)
+    name = ledger()
+    try:
+        out, r = run(stub, native_shim, ["alloc", 3 * GIB, "timefree", 0, "freestats", "arena", "timealloc", 4 * GIB,
+                                         "arena", "freestats", "extra"],
+                     GPUSHARE_QUOTA_BYTES=8 * GIB, GPUSHARE_LEDGER=name, GPUSHARE_HBM_BROKER=sock,
+                     GPUSHARE_HBM_TOKEN="tok", FAKE_HIP_EVENT_MS=400)
+        assert r.returncode == 0, r.stderr
+        a3, tf, fs, arena, ta, arena2, fs2, x = out
+        assert tf["err"] == 0 and tf["ms"] < 50, tf                        # returned without waiting
+        assert fs["deferred"] == 1 and fs["pending"] == 1 and fs["device_waits"] == 0
+        assert arena["used"] == 3 * GIB                                    # not reusable yet
+        assert ta["err"] == 0 and ta["p"] == a3["p"] and ta["ms"] >= 250   # waited for the events, from the arena
+        assert arena2["used"] == 4 * GIB and fs2["pending"] == 0 and x["driver_allocs"] == 0
+    finally:
+        cleanup(name)
+
+
+def test_arena_memory_is_shared_between_processes_through_ipc_handles(stub, native_shim, tmp_path):
+    """hipIpcGetMemHandle of arena memory (the runtime's own cannot export it)
+    gives a handle another process of the pod opens: the exporter's shim sends the fds of the
+    granules the allocation spans over its socket, the importer maps them (its import is freed again
+    at hipIpcCloseMemHandle). hipMemGetAddressRange answers with the allocation, not the granule;
+    hipMemRetainAllocationHandle gives no handle of arena memory (the broker's)."""
+    d, drv = stub
+    sock = str(tmp_path / "hbm.sock")
+    FakeBroker(sock, granules=4)
+    name = ledger()
+    env = dict(os.environ, LD_PRELOAD=native_shim, LD_LIBRARY_PATH=str(d), GPUSHARE_QUOTA_BYTES=str(8 * GIB),
+               GPUSHARE_LEDGER=name, GPUSHARE_HBM_BROKER=sock, GPUSHARE_HBM_TOKEN="tok")
+    args = ["alloc", 3 * GIB // 2, "alloc", 2 * GIB, "ipcget", 1, "range", 0, 12345, "range", 1, GIB + 7, "retain", 1,
+            "wait", "ipcstats"]
+    exp = subprocess.Popen([str(drv), *map(str, args)], env={k: str(v) for k, v in env.items()},
+                           stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        lines = [json.loads(exp.stdout.readline()) for _ in range(6)]
+        a0, a1, h, r0, r1, ret = lines
+        assert h["err"] == 0 and a1["err"] == 0
+        assert r0 == {"op": "range", "err": 0, "base": a0["p"], "size": 3 * GIB // 2}
+        assert r1 == {"op": "range", "err": 0, "base": a1["p"], "size": 2 * GIB}   # spans granules 1..3
+        assert ret["err"] == 1                                                     # hipErrorInvalidValue
+        out, r = run(stub, native_shim, ["ipcopen", h["handle"], "range", 0, 100, "ipcstats", "imports", "ipcclose", 0,
+                                         "ipcstats", "imports"], GPUSHARE_QUOTA_BYTES=4 * GIB)
+        assert r.returncode == 0, r.stderr
+        op, rng, st, imp, cl, st2, imp2 = out
+        assert op["err"] == 0 and rng["err"] == 0 and rng["base"] == op["p"] and rng["size"] == 2 * GIB
+        assert st["opened"] == 1 and st["open_now"] == 1 and imp["live"] == 3    # granules 1, 2, 3 of the exporter
+        assert cl["err"] == 0 and st2["open_now"] == 0 and imp2["live"] == 0
+        bad = h["handle"][:24] + "ffffffff" + h["handle"][32:]                    # an export that does not exist
+        out, r = run(stub, native_shim, ["ipcopen", bad])
+        assert out[0]["err"] != 0
+        exp.stdin.close()
+        tail = json.loads(exp.stdout.readline())
+        assert tail["exports"] == 1 and tail["served"] == 1
+        assert exp.wait(10) == 0
+    finally:
+        if exp.poll() is None:
+            exp.kill()
+        cleanup(name)
+
+
+def test_a_forked_child_does_not_keep_the_parents_granules(stub, native_shim, tmp_path):
+    """A child forked by a pod process (a data-loader worker) inherits the broker connection and
+    the granules' fds: it used to keep the parent's granules from the broker until it exited too.
+    The shim closes its copies in the child at the fork: the broker sees the connection end when
+    the parent exits."""
+    import time
+
+    sock = str(tmp_path / "hbm.sock")
+    b = FakeBroker(sock, granules=2)
+    name = ledger()
+    try:
+        t0 = time.monotonic()
+        out, r = run(stub, native_shim, ["alloc", GIB, "forksleep", 3000, "alloc", MIB],
+                     GPUSHARE_QUOTA_BYTES=4 * GIB, GPUSHARE_LEDGER=name, GPUSHARE_HBM_BROKER=sock, GPUSHARE_HBM_TOKEN="t")
+        assert r.returncode == 0 and out[2]["err"] == 0, r.stderr
+        for _ in range(100):
+            if b.closed_at is not None:
+                break
+            time.sleep(0.02)
+        assert b.closed_at is not None and b.closed_at - t0 < 2.5        # not the child's 3 s
+    finally:
+        cleanup(name)
+
+
+@pytest.mark.parametrize("case", ["sigterm", "handler", "exit", "off"])
+def test_fast_exit_hands_the_granules_back(stub, native_shim, tmp_path, case):
+    """a pod stopped the way the kubelet stops it (SIGTERM, default action) or
+    that just exits never calls gpushare_shim_arena_release(); the kernel would release its
+    imports of the broker's granules only once it has torn the process down (300-380 ms on
+    MI355X). The shim does it first: at SIGTERM it destroys the process's queues and frees the
+    imports, then lets the signal end the process; at the end of a normal exit likewise. A program
+    with its own SIGTERM handler keeps it; GPUSHARE_SHIM_FAST_EXIT=0 leaves it all to the kernel."""
+    import signal
+    import time
+
+    d, drv = stub
+    sock = str(tmp_path / "hbm.sock")
+    b = FakeBroker(sock, granules=2)
+    name = ledger()
+    env = {k: str(v) for k, v in dict(os.environ, LD_PRELOAD=native_shim, LD_LIBRARY_PATH=str(d),
+                                      GPUSHARE_QUOTA_BYTES=str(4 * GIB), GPUSHARE_LEDGER=name,
+                                      GPUSHARE_HBM_BROKER=sock, GPUSHARE_HBM_TOKEN="t", GPUSHARE_SHIM_LOG="1",
+                                      GPUSHARE_SHIM_FAST_EXIT="0" if case == "off" else "1").items()}
+    args = ["alloc", GIB, "wait"] if case != "exit" else ["alloc", GIB]
+    if case == "handler":
+        args = ["sigterm_handler"] + args
+    p = subprocess.Popen([str(drv), *map(str, args)], env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                         stderr=subprocess.PIPE, text=True)
+    try:
+        first = p.stdout.readline() if case != "handler" else (p.stdout.readline(), p.stdout.readline())[1]
+        assert json.loads(first)["err"] == 0
+        if case != "exit":
+            p.send_signal(signal.SIGTERM)
+        p.wait(20)                                   # stdin stays open: "wait" holds the process until the signal
+        out, err = p.stdout.read(), p.stderr.read()
+        if case in ("sigterm", "off"):
+            assert p.returncode == -signal.SIGTERM, err
+        else:
+            assert p.returncode == 0, err
+        fast = [ln for ln in err.splitlines() if "fast exit" in ln]
+        if case == "sigterm":
+            assert len(fast) == 1 and "fast exit (SIGTERM)" in fast[0] and "2 imports freed" in fast[0], err
+        elif case == "exit":
+            assert len(fast) == 1 and "fast exit (exit)" in fast[0] and "2 imports freed" in fast[0], err
+        else:
+            assert not fast, err
+        if case == "handler":
+            assert '"handled"' in out
+        for _ in range(100):
+            if b.closed_at is not None:
+                break
+            time.sleep(0.02)
+        assert b.closed_at is not None
+    finally:
+        if p.poll() is None:
+            p.kill()
         cleanup(name)
