@@ -418,7 +418,14 @@ class Allocator(NativeTable):
                     del self._assigned[u]
 
     def _candidates(self, fresh: bool) -> list[dict]:
-        pods = self._view(A.dedupe_by_uid(self.pods.pending_pods(fresh=fresh), self.node) + self._prebind_pods())
+        """Pending assumed pods in match order: assume time, then arrival — and every pod the
+        pod cache shows bound here before any pre-bind one (the kubelet admits only
+        bound pods, and the pod watch delivers binds in order, so an unbound pod older than a
+        bound one of the same size is one whose bind is still in flight, or failed: the
+        reference, which sees bound pods only, ``podmanager.go:228``, would pick the bound one)."""
+        pre = self._prebind_pods()
+        pre_u = {O.uid(p) for p in pre}
+        pods = self._view(A.dedupe_by_uid(self.pods.pending_pods(fresh=fresh), self.node) + pre)
         now = time.monotonic()
         self._sweep_assigned(now)
         if fresh and self._tainted:   # forget a withheld reservation once its pod is gone
@@ -431,12 +438,12 @@ class Allocator(NativeTable):
             u = O.uid(p)
             # a pod being deleted is never admitted by the kubelet
             if assumed and u not in self._assigned and u not in self._tainted and not O.deleting(p):
-                out.append((at, len(out), p))
-        out.sort(key=lambda e: (e[0], e[1]))      # assume time, then arrival order (stable)
+                out.append((1 if u in pre_u else 0, at, len(out), p))
+        out.sort(key=lambda e: e[:3])             # bound first, assume time, then arrival order (stable)
         if log.V(4):
-            for at, _, p in out:
+            for _, at, _, p in out:
                 log.info("candidate pod %s in ns %s with timestamp %d is found.", O.name(p), O.namespace(p), at)
-        return [p for _, _, p in out]
+        return [p for _, _, _, p in out]
 
     def _partial_state(self, c: _Claim, cands: list[dict], now: float) -> str:
         """"live": the claimed pod can still be continued; "stale": it exists but the claim
@@ -939,9 +946,10 @@ class Allocator(NativeTable):
             if not shape:
                 continue
             u, g = O.uid(p), A.gpu_id_from_annotation(p)
+            key = (0 if self.pods.get(u) is not None else 1, at)   # the table's order (see _candidates)
             if len(shape) > 1:
                 out.append(_Prepared(u, O.namespace(p), O.name(p), shape[0], True, g))
-                ats.append(at)
+                ats.append(key)
                 continue
             k = (u, g, shape[0])
             c = self._prep_cache.get(k) or self._take_precomputed(k)
@@ -951,7 +959,7 @@ class Allocator(NativeTable):
                 c = self._prepared(p, u, g, shape[0])
             keep[k] = c
             out.append(c)
-            ats.append(at)
+            ats.append(key)
         nat = self.native
         with self._mu:
             if gen != self._gen:          # reconfigured meanwhile: answers built from the old model

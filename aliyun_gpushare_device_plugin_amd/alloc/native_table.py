@@ -159,7 +159,8 @@ class NativeTable:
 
     def _publish_change(self, nat, version: int, pod: dict, gone: bool) -> str:
         """The table at ``version`` = the table at ``version - 1`` with ``pod`` removed and, if
-        it is a candidate now, placed in candidate order (assume time, then arrival) — what
+        it is a candidate now, placed in candidate order (bound before pre-bind, assume time,
+        then arrival; the table's keys are ``(pre-bind, assume time)``) — what
         ``_prepare`` would build: anything else that changes candidates (a taint, a placement
         overlay, a reconfigure) bumps the engine generation, and claims made since are marked
         taken in the server."""
@@ -188,6 +189,7 @@ class NativeTable:
                         c = (self._prep_cache.get(k) or self._take_precomputed(k)
                              or self._prepared(p, u, g, shape[0]))
                         self._prep_cache[k] = c
+            at = (0, at)                              # a pod of the pod cache: bound here
             keep_at = idx is not None and c is not None and ats[idx] == at
             if idx is not None:
                 old = out[idx]
@@ -425,8 +427,9 @@ class NativeTable:
                 k = (u, g, shape[0])
                 c = self._prep_cache.get(k) or self._take_precomputed(k) or self._prepared(p, u, g, shape[0])
                 self._prep_cache[k] = c
-                i = bisect.bisect_right(ats, at)
-                out, ats = out[:i] + (c,) + out[i:], ats[:i] + (at,) + ats[i:]
+                key = (1, at)                         # after every bound candidate (_candidates)
+                i = bisect.bisect_right(ats, key)
+                out, ats = out[:i] + (c,) + out[i:], ats[:i] + (key,) + ats[i:]
                 self._native_prep.pop(u, None)
                 self._native_prep[u] = c
                 for en in out:

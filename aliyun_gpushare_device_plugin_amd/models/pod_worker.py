@@ -19,6 +19,9 @@ Lifecycle (JSON lines on stdin/stdout):
   ``{"cmd": "stats"}`` answers ``{"event": "stats", "gemms": n, "t": ...}`` between bursts.
 * ``{"cmd": "stop"}`` — frees everything (its HBM is back on the device when ``done`` is
   printed, before the process exits), prints ``{"event": "done", ...}`` and exits 0.
+* ``{"cmd": "exit"}`` — the program just ends: a normal process exit (the C runtime's exit: atexit
+  handlers, library destructors) with nothing freed and no arena release, as a pod whose main
+  returns. A SIGTERM (the kubelet's stop) takes the default action: the process ends at once.
 
 The reference's demo pod is ``cheyang/gpu-player:v2`` (``demo/binpack-1/binpack-1.yaml:39``);
 ``player_main.py`` is the long-running container entry point, this is its benchable form.
@@ -280,6 +283,9 @@ def _pod() -> int:
             elif c.get("cmd") == "stop":
                 t_asked = c.get("_t", time.perf_counter())
                 break
+            elif c.get("cmd") == "exit":
+                sys.stdout.flush()
+                ctypes.CDLL(None).exit(0)       # (a forked standby has no interpreter to unwind into)
             continue
         player.run(burst)
         burst_done.record(player.stream)

@@ -100,6 +100,15 @@ def parse():
     ap.add_argument("--driver-path-steps", type=int, default=5,
                     help="after the timed run (1 GPU, broker on): this many churn steps of the driver path "
                          "(--no-hbm-broker) in a child run, reported as driver_path (0 = off)")
+    ap.add_argument("--tenant-stop", default="cooperative", choices=("cooperative", "sigterm", "exit"),
+                    help="how a retired pod's process ends: cooperative = it frees its HBM and hands its arena "
+                         "back (gpushare_shim_arena_release) before it exits; sigterm = the kubelet's stop, SIGTERM "
+                         "with the default action and nothing else; exit = its program ends (a normal exit, no "
+                         "release call)")
+    ap.add_argument("--comparator-steps", type=int, default=8,
+                    help="after the timed run (1 GPU, broker on): this many churn steps each of an unmodified tenant "
+                         "(--tenant-stop sigterm), of a normal exit (--tenant-stop exit) and of fresh standby "
+                         "interpreters (--no-pod-zygote), in child runs, reported in the line (0 = off)")
     ap.add_argument("--stub-runtime", default=None,
                     help="CPU rehearsal of the broker path: a directory with the stub HIP runtime "
                          "(libamdhip64.so.7, tests/native/fake_hip.c), shim_driver and a gpushare-hbm-broker linked "
@@ -626,6 +635,12 @@ class _Forked:
         except ProcessLookupError:
             pass
 
+    def terminate(self):
+        try:
+            os.kill(self.pid, 15)
+        except ProcessLookupError:
+            pass
+
 
 class _Zygote:
     """One interpreter that imported torch and forks the standby pod processes
@@ -679,8 +694,10 @@ class PodFleet:
     imported, GPU untouched) that becomes the next admitted pod."""
 
     def __init__(self, local: int, gemm: int, burst: int, fill: float, visible_by_uuid: bool, standby: int = 2,
-                 slack: int = 2 << 30, ordinal: int | None = None, broker=None, zygote: bool = True):
+                 slack: int = 2 << 30, ordinal: int | None = None, broker=None, zygote: bool = True,
+                 stop_mode: str = "cooperative"):
         self.local, self.gemm, self.burst, self.fill, self.slack = local, gemm, burst, fill, slack
+        self.stop_mode = stop_mode            # how a retired pod's process ends (--tenant-stop)
         self._zygote = _Zygote(self._pod_env()) if zygote else None
         self.broker = broker                  # HBMBroker: pods' HBM comes from it (no driver wipe on the path)
         self.ordinal = local if ordinal is None else ordinal     # this GPU's HIP ordinal (bind_device)
@@ -855,6 +872,8 @@ class PodFleet:
         w = self.pods.pop(uid, None)
         if w is None:
             return
+        if self.stop_mode != "cooperative":
+            return self._stop_uncooperative(w)
         t0 = time.perf_counter()
         w["proc"].stdin.write('{"cmd":"stop"}\n')
         ev = self._wait(w, "done")                      # freed through KFD at this point
@@ -872,6 +891,25 @@ class PodFleet:
         self.retired_gemms += ev["gemms"]
         self.held_bytes -= w["ready"].get("held", 0)
         self.denied += ((ev.get("shim") or {}).get("denied") or 0)
+
+    def _stop_uncooperative(self, w) -> None:
+        """A retired pod stopped as the kubelet stops a container (``sigterm``: SIGTERM, the default
+        action, no release call) or whose program just ends (``exit``: a normal exit without
+        freeing or releasing anything). The step's stop lasts until the process is gone; its HBM
+        comes back as the broker sees its granules' last references go."""
+        w["proc"].stdin.write('{"cmd":"stats"}\n')
+        gemms = self._wait(w, "stats")["gemms"]         # the work it did, asked between bursts
+        t0 = time.perf_counter()
+        if self.stop_mode == "sigterm":
+            w["proc"].terminate()
+        else:
+            w["proc"].stdin.write('{"cmd":"exit"}\n')
+        w["proc"].wait(60)
+        self.phase_ms["stop"].append(time.perf_counter() - t0)
+        self._stopped_at = (t0, w["size"], w["ready"].get("held", 0))
+        self.retired_bytes += w["ready"].get("held", 0)
+        self.retired_gemms += gemms
+        self.held_bytes -= w["ready"].get("held", 0)
 
     def oldest(self) -> str | None:
         return next(iter(self.pods), None)
@@ -972,28 +1010,42 @@ class StubFleet:
             self.stop(uid)
 
 
-def driver_path_run(a) -> dict:
-    """A short child run of the driver path (``--no-hbm-broker``: every pod allocates fresh from
-    amdgpu, which wipes a retired pod's HBM first) with this run's pod shapes; its headline."""
+def child_run(a, steps: int, *flags: str, tenant_stop: str | None = None, zygote: bool | None = None) -> dict:
+    """A short child run of this churn on 1 GPU with one thing changed (``flags``, the tenant's
+    stop, fresh standby interpreters); its headline. The comparators of the line: each measured on
+    the same box right after the main run handed every byte back."""
     import tempfile
 
-    out = os.path.join(tempfile.mkdtemp(prefix="gs-driver-", dir="/tmp"), "line.json")
-    cmd = [sys.executable, os.path.abspath(__file__), "--gpus", "1", "--steps", str(a.driver_path_steps), "--warmup", "1",
-           "--no-hbm-broker", "--compare-rtts", "", "--fill-orders", "", "--no-ref-churn", "--driver-path-steps", "0",
-           "--gemm", str(a.gemm), "--fill", str(a.fill), "--standby", str(a.standby), "--json-out", out]
-    if a.no_pod_zygote:
+    out = os.path.join(tempfile.mkdtemp(prefix="gs-child-", dir="/tmp"), "line.json")
+    stop = tenant_stop or a.tenant_stop
+    cmd = [sys.executable, os.path.abspath(__file__), "--gpus", "1", "--steps", str(steps), "--warmup", "1",
+           "--compare-rtts", "", "--fill-orders", "", "--no-ref-churn", "--driver-path-steps", "0",
+           "--comparator-steps", "0", "--gemm", str(a.gemm), "--fill", str(a.fill), "--standby", str(a.standby),
+           "--tenant-stop", stop, "--json-out", out, *flags]
+    if (a.no_pod_zygote if zygote is None else not zygote):
         cmd.append("--no-pod-zygote")
     t0 = time.perf_counter()
     try:
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=420)
         with open(out) as f:
             d = json.loads(f.read())
     except Exception as e:  # noqa: BLE001 - a comparator, never fatal to the headline
         return {"error": f"{type(e).__name__}: {e}"[:300]}
+    broker = d.get("hbm_broker") or {}
     return {"value": d["value"], "unit": d["unit"], "steps": d["steps"], "ms_per_step": d["ms_per_step"],
-            "pod_ready_p50_ms": d.get("pod_ready_p50_ms"), "pod_phase_p50_ms": d.get("pod_phase_p50_ms"),
-            "allocate_p50_ms": d.get("allocate_p50_ms"), "failed_admissions": d.get("failed_admissions"),
+            "pod_ready_p50_ms": d.get("pod_ready_p50_ms"), "pod_ready_p99_ms": d.get("pod_ready_p99_ms"),
+            "pod_phase_p50_ms": d.get("pod_phase_p50_ms"), "allocate_p50_ms": d.get("allocate_p50_ms"),
+            "failed_admissions": d.get("failed_admissions"), "quota_denials": d.get("quota_denials"),
+            "tenant_stop": d.get("config", {}).get("tenant_stop"),
+            "standby_forked_from_zygote": d.get("config", {}).get("standby_forked_from_zygote"),
+            "broker_quarantine_ms_max": broker.get("quarantine_ms_max"), "broker_ends": broker.get("ends"),
             "rc": r.returncode, "wall_s": round(time.perf_counter() - t0, 1)}
+
+
+def driver_path_run(a) -> dict:
+    """The driver path (``--no-hbm-broker``: every pod allocates fresh from amdgpu, which wipes a
+    retired pod's HBM first) with this run's pod shapes."""
+    return child_run(a, a.driver_path_steps, "--no-hbm-broker")
 
 
 def relaunch(n: int) -> int:
@@ -1118,7 +1170,7 @@ def main():
     if use_gpu:
         fleet = PodFleet(local, a.gemm, a.burst, a.fill, not smi.startswith("fake:"), a.standby,
                          slack=int(a.room_slack_gib * (1 << 30)), ordinal=ordinal, broker=broker,
-                         zygote=not a.no_pod_zygote)
+                         zygote=not a.no_pod_zygote, stop_mode=a.tenant_stop)
     else:
         fleet = StubFleet(stub, a.fill) if stub else None
     topo_report = cp_topo = None
@@ -1333,6 +1385,7 @@ def main():
                        "smi_backend": smi, "pod_processes": use_gpu, "hbm_broker": broker is not None,
                        "standby_interpreters_per_gpu": a.standby,
                        "standby_forked_from_zygote": not a.no_pod_zygote,
+                       "tenant_stop": a.tenant_stop,
                        # the plugin's gRPC server and the simulated kubelet's Allocate client
                        "grpc_server": "native" if native_server.available() else "python",
                        "kubelet_client": "native" if NativeUnaryClient.wanted() else "grpcio"},
@@ -1440,6 +1493,14 @@ def main():
             # the same churn without the broker, after this run has handed every GPU byte back: what
             # the broker buys, measured on the same box in the same line
             res["driver_path"] = driver_path_run(a)
+        if world == 1 and use_gpu and broker is not None and a.comparator_steps > 0:
+            # tenants that do nothing for the broker (the kubelet's SIGTERM, a
+            # program that just ends), and the harness's forked standbys against fresh interpreters
+            for key, stop in (("cooperative_tenant", "cooperative"), ("unmodified_tenant", "sigterm"),
+                              ("normal_exit_tenant", "exit")):
+                if stop != a.tenant_stop:
+                    res[key] = child_run(a, a.comparator_steps, tenant_stop=stop)
+            res["no_pod_zygote"] = child_run(a, a.comparator_steps, zygote=False)
         line = json.dumps(res)
         print(line, flush=True)
         if a.json_out:

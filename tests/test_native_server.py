@@ -950,6 +950,57 @@ def test_a_claimed_prebind_answer_stands_when_the_bind_fails(tmp_path):
         al.close()
 
 
+@pytest.mark.parametrize("path", ["native", "full"])
+def test_a_bound_pod_is_never_given_an_older_prebind_pods_entry(tmp_path, path):
+    """a pre-bind pod A (assumed earlier, its bind still in flight or failed) and a pod
+    B of the same size bound here. The kubelet admits only bound pods and the pod watch delivers
+    binds in order, so this Allocate is B's: it must get B's GPU, not A's entry (as the reference,
+    which sees bound pods only, ``podmanager.go:228``). Then A's bind lands and A is answered with
+    its own GPU. Both through the native table and through the engine's full path."""
+    srv, al, src = _prebind_server(tmp_path)
+    ch, stub = _stub(srv)
+    try:
+        a = mkpod("older", 2, 0, 10, node="")                 # GPU 0, assumed at 10, not bound yet
+        al.precompute(a)
+        b = mkpod("newer", 2, 1, 20)                          # GPU 1, assumed at 20, bound here
+        with src._lock:
+            src.pods.append(b)
+            src.version += 1
+            src.pending_version += 1
+        al.native.set_version(src.pending_version)            # what the pod-cache hook tells the server
+        if path == "native":
+            src.changed.set()                                 # the prepare loop rebuilds the table
+            t = time.monotonic() + 5
+            while al._published != (src.pending_version, al._gen) and time.monotonic() < t:
+                time.sleep(0.002)
+            order = [c.uid for c in al._last_table[2]]
+            assert order.index("uid-newer") < order.index("uid-older"), order
+            before = srv.stats()["fast"]
+            r = stub.Allocate(_req("b1", "b2"))
+            assert srv.stats()["fast"] == before + 1
+        else:
+            r = al.allocate(_req("b1", "b2"))
+        assert r.container_responses[0].envs[const.ENV_RESOURCE_INDEX] == "1"     # B's GPU
+        t = time.monotonic() + 5
+        while "uid-newer" not in al._assigned and time.monotonic() < t:
+            time.sleep(0.01)
+        assert "uid-newer" in al._assigned and "uid-older" not in al._assigned
+        bound = json.loads(json.dumps(a))                     # A's bind lands: its own GPU
+        bound["spec"]["nodeName"] = "node-a"
+        with src._lock:
+            src.pods.append(bound)
+            src.version += 1
+            src.pending_version += 1
+        al.native.set_version(src.pending_version)
+        src.changed.set()
+        r2 = al.allocate(_req("a1", "a2"))
+        assert r2.container_responses[0].envs[const.ENV_RESOURCE_INDEX] == "0"
+    finally:
+        ch.close()
+        srv.stop()
+        al.close()
+
+
 # ---- the kubelet's client: grpc-go's frames, replayed ------------------------------------------
 class GoClient:
     """The kubelet's device-plugin client as grpc-go (1.5x) puts it on the wire, built from the
