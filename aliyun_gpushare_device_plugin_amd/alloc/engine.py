@@ -218,6 +218,8 @@ class Allocator(NativeTable):
         # pods placed here but not bound yet: uid -> (pod, first seen, pre-bind watch gone at | None);
         # candidates already (native_table.py precompute / expire_prebind)
         self._prebind: dict[str, tuple] = {}
+        # per-pod timeline of the fast path, CLOCK_MONOTONIC ns (native_table.py ``pod_trace``)
+        self._ptrace: dict[str, dict] = {}
         self._tmpl_bytes: dict[tuple, bytes] = {}                          # _prepared
         self.native_rotate_bytes = 16 << 20       # rotate the native journal file past this
         self.native_prep_keep = 4096              # prepared answers kept for native claims past the current table
@@ -988,6 +990,9 @@ class Allocator(NativeTable):
                     self._last_table = (version, gen, () if legacy else tuple(out), () if legacy else tuple(ats))
                     self._published = (version, gen)
                     self.metrics.table_publish.observe(time.perf_counter() - tp, path="prepare")
+                    if not legacy:
+                        for c in out:
+                            self._mark(c.uid, "tab")
         self._prune_replay_index(src)
 
     def _prune_replay_index(self, src) -> None:
@@ -1149,6 +1154,8 @@ class Allocator(NativeTable):
             return self._err_response(req, pod_units)
 
         idx = claim.gpu_index
+        self._mark(claim.uid, "alloc_in", int(t0 * 1e9))     # perf_counter is CLOCK_MONOTONIC here
+        self._mark(claim.uid, "path", "full")
         if self.model.gpu(idx) is None:
             log.warning("Failed to find the dev for pod %s because it's not able to find dev with index %d",
                         O.name(claim.pod), idx)

@@ -150,8 +150,13 @@ class NativeTable:
         nat.set_version(version)
         if pod is not None:
             t = time.perf_counter()
+            u = O.uid(pod)
+            if not gone:
+                self._mark(u, "bind_seen")
             try:
                 kind = self._publish_change(nat, version, pod, gone)
+                if not gone:
+                    self._mark(u, "bind_pub" if kind else "bind_skip")
                 if kind:
                     self.metrics.table_publish.observe(time.perf_counter() - t, path=f"hook_{kind}")
             except Exception as e:  # noqa: BLE001 - the prepare loop republishes anyway
@@ -213,6 +218,37 @@ class NativeTable:
             self._published = (version, gen)
         return "add" if idx is None and c is not None else "other"
 
+    # ---- the per-pod timeline (``/debug/latency`` "pod_trace") ------------------------------
+    PTRACE_KEEP = 256
+
+    def _mark(self, u: str, key: str, t: int | None = None) -> None:
+        """First time ``key`` happened for pod ``u`` (CLOCK_MONOTONIC ns, comparable across the
+        node's processes): ``pre_seen`` / ``pre_pub`` (the pre-bind watch delivered the placed pod;
+        its entry is in the table), ``bind_seen`` / ``bind_pub`` (the pod watch delivered the bind;
+        the table has it as bound), ``tab`` (a full rebuild published it), ``alloc_in`` (its
+        Allocate reached the server) and the server's waits."""
+        tr = self._ptrace.get(u)
+        if tr is None:
+            tr = self._ptrace[u] = {}
+            while len(self._ptrace) > self.PTRACE_KEEP:
+                self._ptrace.pop(next(iter(self._ptrace)), None)
+        if key not in tr:
+            tr[key] = t if t is not None else time.monotonic_ns()
+
+    def pod_trace(self) -> list[dict]:
+        """The last pods' timelines, in ms relative to their Allocate's arrival (pods whose
+        Allocate came), oldest first."""
+        out = []
+        for u, tr in list(self._ptrace.items()):
+            t0 = tr.get("alloc_in")
+            if t0 is None:
+                continue
+            rec = {k: (v if isinstance(v, str) or k.endswith("_ns") else round((v - t0) / 1e6, 3))
+                   for k, v in tr.items() if k != "alloc_in"}
+            rec["uid"], rec["alloc_in_abs"] = u, t0
+            out.append(rec)
+        return out
+
     def _native_loop(self, nat) -> None:
         """Takes in the native server's claims as they happen; rotates its journal file once
         the engine's own journal holds everything it has."""
@@ -259,7 +295,13 @@ class NativeTable:
 
     def _native_taken(self, rec) -> None:
         """One native answer: the same claim and bookkeeping as the engine's fast path."""
-        uid, rb, t, hns = rec
+        uid, rb, t, hns = rec[:4]
+        if len(rec) > 4:                              # the server's own timeline of this answer
+            t_in, ww, tw = rec[4:7]
+            self._mark(uid, "alloc_in", t_in)
+            self._mark(uid, "watch_wait_ns", ww)
+            self._mark(uid, "table_wait_ns", tw)
+        self._mark(uid, "path", "native")
         pick = self._native_prep.get(uid)
         with self._mu:
             self._assigned[uid] = time.monotonic()
@@ -315,7 +357,9 @@ class NativeTable:
         if not assumed or len(shape) != 1:
             return
         u, g = O.uid(pod), A.gpu_id_from_annotation(pod)
+        self._mark(u, "pre_seen")
         if self.pods.get(u) is not None:
+            self._mark(u, "pre_after_bind")
             return                                    # the bind came first: the pod cache has it
         k = (u, g, shape[0])
         if self.model.gpu(g) is None:
@@ -326,12 +370,14 @@ class NativeTable:
             self._precomputed[k] = (c, time.monotonic())
             while len(self._precomputed) > 1024:
                 self._precomputed.popitem(last=False)
+            self._mark(u, "pre_prep")
         with self._table_mu:
             prev = self._prebind.get(u)
             self._prebind[u] = (pod, prev[1] if prev is not None else time.monotonic(), None)
             while len(self._prebind) > 1024:
                 self._prebind.pop(next(iter(self._prebind)))
-        self._publish_prebind(u)
+        how = self._publish_prebind(u)
+        self._mark(u, "pre_pub" if how == "pub" else f"pre_{how}")
 
     # how long a pre-bind candidate whose pre-bind watch entry went away (bound, deleted, label
     # moved: the watch does not say which) stays in the table waiting for the pod watch to show
@@ -395,34 +441,37 @@ class NativeTable:
             self.metrics.allocate_outcomes.inc(outcome="prebind_withdrawn")
             self._publish_prebind(u, remove=True)
 
-    def _publish_prebind(self, u: str, remove: bool = False) -> None:
+    def _publish_prebind(self, u: str, remove: bool = False) -> str:
         """Insert (or withdraw) pre-bind candidate ``u`` in the last published table, at the same
         cache version: the table is what a full rebuild gives now (``_prepare`` takes the same
-        pre-bind set into its candidates)."""
+        pre-bind set into its candidates). Returns what happened ("pub", or why not)."""
         nat = self.native
         if nat is None or not self.opts.fast_path or self.opts.compute_isolation == "cu":
-            return
+            return "off"
         in_cache = self.pods.get(u) is not None        # before _table_mu (lock order: cache, then table)
         with self._table_mu:
             last = self._last_table
             if last is None or last[1] != self._gen or time.time() < self.journal._legacy_until:
-                return                                # the prepare loop rebuilds (it takes the pre-bind set too)
+                # the prepare loop rebuilds (it takes the pre-bind set too)
+                return "no_table" if last is None else "gen" if last[1] != self._gen else "legacy"
             version, gen, out, ats = last
             idx = next((i for i, c in enumerate(out) if c.uid == u), None)
             if remove:
                 if idx is None or in_cache:
-                    return
+                    return "kept"
                 old = out[idx]
                 self._prep_cache.pop((old.uid, old.gpu, old.size), None)
                 out, ats = out[:idx] + out[idx + 1:], ats[:idx] + ats[idx + 1:]
             else:
                 e = self._prebind.get(u)
-                if idx is not None or e is None or u in self._assigned or u in self._claims or u in self._tainted:
-                    return
+                if idx is not None:
+                    return "present"
+                if e is None or u in self._assigned or u in self._claims or u in self._tainted:
+                    return "not_candidate"
                 p = self._view([e[0]])[0]
                 assumed, _, at, shape = self._info(p)
                 if not assumed or len(shape) != 1 or O.deleting(p):
-                    return
+                    return "not_candidate"
                 g = A.gpu_id_from_annotation(p)
                 k = (u, g, shape[0])
                 c = self._prep_cache.get(k) or self._take_precomputed(k) or self._prepared(p, u, g, shape[0])
@@ -440,6 +489,7 @@ class NativeTable:
             nat.publish(_native_blob(version, gen, 1 if self.podres is not None else 0, list(out),
                                      self.journal.replay_ids()))
             self._last_table = (version, gen, out, ats)
+        return "pub"
 
     # the ledger directory a prepared answer names is kept for a grace period without a pod on
     # this node (quota/ledger.py collect, 60 s): a bind later than this gets a fresh answer

@@ -278,7 +278,11 @@ class SharedGPUManager:
         if not stats:
             return {}
         skipped = {dict(k).get("why", ""): v for k, v in self.metrics.table_publish_skipped._v.items()}
-        return {"native_server": dict(stats(), table_hook_skipped=skipped)}
+        out = {"native_server": dict(stats(), table_hook_skipped=skipped)}
+        trace = getattr(self.allocator, "pod_trace", None)
+        if trace is not None:
+            out["pod_trace"] = trace()
+        return out
 
     def _pod_resources(self):
         from ..api.podresources import SOCKET, PodResourcesClient

@@ -121,7 +121,8 @@ class NativeFast:
         return self.lib.gs_dp_taken_pending(self.h)
 
     def taken_next(self, timeout_ms: int):
-        """(uid, AllocateRequest bytes, wall time, handler ns); () on timeout; None once stopped."""
+        """(uid, AllocateRequest bytes, wall time, handler ns, arrival CLOCK_MONOTONIC ns, watch-wait
+        ns, table-wait ns); () on timeout; None once stopped."""
         fn = self.lib.gs_dp_taken_poll if timeout_ms <= 0 else self.lib.gs_dp_taken_next
         n = fn(self.h, timeout_ms, self._buf, len(self._buf))
         if n == 0:
@@ -137,8 +138,7 @@ class NativeFast:
         (lr,) = struct.unpack_from("<I", b, 4 + lu)
         o = 8 + lu
         req = b[o:o + lr]
-        t, hns = struct.unpack_from("<dQ", b, o + lr)
-        return uid, req, t, hns
+        return (uid, req) + struct.unpack_from("<dQqQQ", b, o + lr)
 
     def journal_open(self, path: str, nbytes: int) -> None:
         if self.lib.gs_dp_fast_journal_open(self.h, path.encode(), nbytes) != 0:

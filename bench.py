@@ -208,6 +208,56 @@ def native_share(before: dict | None, after: dict | None) -> dict | None:
                                    for k, v in (a.get("table_hook_skipped") or {}).items()}}
 
 
+def pod_timeline(port: int, commits: dict) -> dict | None:
+    """Where each timed pod's Allocate fell in its pod's timeline (ms relative to the Allocate's
+    arrival at the plugin; CLOCK_MONOTONIC, shared by the node's processes): the extender's
+    commit (annotate+label PATCH, then bind), the plugin's pre-bind watch delivering the placed
+    pod and its table entry going live, the pod watch delivering the bind. The pods that waited
+    for the plugin's watch are listed whole, with the step that was still missing."""
+    import urllib.request
+
+    try:
+        with urllib.request.urlopen(f"http://127.0.0.1:{port}/debug/latency", timeout=5) as r:
+            trace = json.loads(r.read()).get("pod_trace") or []
+    except Exception:  # noqa: BLE001
+        return None
+    rows = []
+    for t in trace:
+        c = commits.get(t["uid"])
+        if c is None:
+            continue
+        row = dict(t)
+        tin = t.get("alloc_in_abs")                    # (the plugin's rows are relative already)
+        if tin is not None:
+            row["commit_start"] = round((c[0] - tin) / 1e6, 3)
+            row["commit_done"] = round((c[1] - tin) / 1e6, 3)
+        rows.append(row)
+    if not rows:
+        return None
+
+    def med(k):
+        xs = sorted(r[k] for r in rows if isinstance(r.get(k), (int, float)))
+        return xs[len(xs) // 2] if xs else None
+
+    waited = [r for r in rows if r.get("watch_wait_ns")]
+    causes: dict = {}
+    for r in waited:
+        if r.get("pre_pub") is not None and r["pre_pub"] <= 0:
+            why = "prebind_entry_live"                 # (a size or order mismatch, not the watch)
+        elif r.get("pre_seen") is None or r["pre_seen"] > 0:
+            why = "prebind_event_after_allocate"       # the plugin had not read the placed pod yet
+        elif r.get("pre_pub") is None:
+            why = "prebind_not_published:" + ",".join(k[4:] for k in r if k.startswith("pre_") and k not in ("pre_seen", "pre_prep"))
+        else:
+            why = "prebind_publish_after_allocate"     # read, still preparing / publishing
+        causes[why] = causes.get(why, 0) + 1
+    keys = ("commit_start", "commit_done", "pre_seen", "pre_prep", "pre_pub", "bind_seen", "bind_pub", "tab")
+    return {"pods": len(rows), "watch_waited": len(waited), "causes": causes,
+            "median_ms": {k: med(k) for k in keys},
+            "waited": [{k: r.get(k) for k in keys + ("watch_wait_ns", "table_wait_ns", "path") if r.get(k) is not None}
+                       for r in waited]}
+
+
 def transport_floor() -> float | None:
     """Kubelet-side round trip of an Allocate whose handler returns a prepared answer at once."""
     try:
@@ -296,6 +346,7 @@ class ControlPlane:
         self.failed = 0
         self.fail_reasons: list[str] = []
         self.cp_time = 0.0
+        self.commit_ns: dict[str, tuple] = {}    # uid -> CLOCK_MONOTONIC ns around the extender's commit
 
     def _record(self, pod, size, adm) -> tuple[int, dict] | None:
         from aliyun_gpushare_device_plugin_amd.cluster import objects as O
@@ -386,7 +437,10 @@ class ControlPlane:
         self.cluster.delete_pod(old)
         pod = self.cluster.create_pod(size)
         where = self.cluster.extender.decide(pod, [MAIN_NODE])
+        c0 = time.monotonic_ns()
         bpod = self.cluster.extender.commit(pod, where, time.time_ns()) if where else None
+        if bpod is not None:
+            self.commit_ns[O.uid(bpod)] = (c0, time.monotonic_ns())   # annotate+label PATCH, then bind
         if bpod is None:
             self.failed += 1
             self.fail_reasons.append(f"{size}GiB: unschedulable")
@@ -1245,6 +1299,7 @@ def main():
         cp.failed = 0
         cp.fail_reasons.clear()
         cp.native_before = native_stats(cp.metrics_port)
+        cp.commit_ns.clear()
         cp.plugin_latency(reset=True)
         if cp.ref_port:
             plugin_latency(cp.ref_port, reset=True)
@@ -1346,6 +1401,7 @@ def main():
             "plugin_allocate_p99_ms": ms(srv["p99"]) if srv else None,
             "allocate_breakdown_p50_ms": breakdown(cp.splits),
             "answered_by": native_share(getattr(cp, "native_before", None), native_stats(cp.metrics_port)),
+            "pod_timeline": pod_timeline(cp.metrics_port, cp.commit_ns),
             "native_table_publish": (srv or {}).get("table_publish"),
             "admissions": len(cp.alloc_lat), "pod_source": a.pod_source, "patch": "write-behind",
             "apiserver_round_trips_on_path": round_trips(srv)}}

@@ -228,6 +228,9 @@ struct Taken {
   std::string uid, req;
   double t;
   uint64_t handler_ns;
+  int64_t t_in;            // CLOCK_MONOTONIC ns the request was complete
+  uint64_t watch_wait_ns;  // waited for a table holding a pod of this size
+  uint64_t table_wait_ns;  // waited for the table to catch up with the pod cache
 };
 
 struct Counters {
@@ -557,13 +560,15 @@ bool fast_allocate(Conn* c, int32_t sid, const std::string& body, int64_t t_in) 
     s->n.stale++;
     return false;
   }
+  uint64_t tw = 0, ww = 0;
   if (!table_current(s)) {
     // the pod cache or the engine moved since the table was built: the engine republishes
     // within a few hundred microseconds (its prepare loop wakes on the same change)
     s->n.waited++;
     int64_t w0 = mono_ns();
     wait_for_table(s, lk, s->fast_wait_us, [&] { return table_current(s) || s->blocked > 0 || s->stopping.load(); });
-    s->n.wait_ns += (uint64_t)(mono_ns() - w0);
+    tw = (uint64_t)(mono_ns() - w0);
+    s->n.wait_ns += tw;
     if (!table_current(s)) {
       (s->blocked > 0 ? s->n.blocked : s->n.stale)++;
       return false;
@@ -577,9 +582,11 @@ bool fast_allocate(Conn* c, int32_t sid, const std::string& body, int64_t t_in) 
     // wait for the next table (a LIST on the engine's path is the alternative)
     s->n.watch_waits++;
     uint64_t v = s->cur_version;
+    int64_t w0 = mono_ns();
     wait_for_table(s, lk, s->watch_wait_us, [&] {
       return (s->cur_version != v && table_current(s)) || s->blocked > 0 || s->stopping.load();
     });
+    ww = (uint64_t)(mono_ns() - w0);
     if (table_current(s)) d = pick(s, crs[0], &en);
   }
   if (d != kOk) {
@@ -597,7 +604,7 @@ bool fast_allocate(Conn* c, int32_t sid, const std::string& body, int64_t t_in) 
   s->taken_uids.insert(en->uid);
   for (auto& id : crs[0]) s->answered_ids[id] = t_in;
   uint64_t hns = (uint64_t)(mono_ns() - t_in);
-  s->taken.push_back(Taken{en->uid, body, t, hns});
+  s->taken.push_back(Taken{en->uid, body, t, hns, t_in, ww, tw});
   std::string resp = en->body;
   s->n.fast++;
   s->n.lock_ns += (uint64_t)(l1 - l0);
@@ -1138,7 +1145,7 @@ int gs_dp_taken_next(gs_dp* s, int timeout_ms, uint8_t* buf, int cap) {
     return 0;
   if (s->taken.empty()) return -1;
   const Taken& t = s->taken.front();
-  size_t need = 4 + t.uid.size() + 4 + t.req.size() + 8 + 8;
+  size_t need = 4 + t.uid.size() + 4 + t.req.size() + 8 + 8 + 24;
   if ((size_t)cap < need) return -2;
   uint8_t* p = buf;
   uint32_t l = (uint32_t)t.uid.size();
@@ -1149,6 +1156,9 @@ int gs_dp_taken_next(gs_dp* s, int timeout_ms, uint8_t* buf, int cap) {
   memcpy(p, t.req.data(), l), p += l;
   memcpy(p, &t.t, 8), p += 8;
   memcpy(p, &t.handler_ns, 8), p += 8;
+  memcpy(p, &t.t_in, 8), p += 8;
+  memcpy(p, &t.watch_wait_ns, 8), p += 8;
+  memcpy(p, &t.table_wait_ns, 8), p += 8;
   // the engine now knows the claim; the uid stays in taken_uids (the table entry must not be
   // answered again) until the next publish no longer lists it
   s->taken.pop_front();

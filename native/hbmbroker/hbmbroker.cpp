@@ -211,7 +211,10 @@ struct Broker {
   std::string boot = boot_id();
   std::vector<hipMemGenericAllocationHandle_t> h;
   std::vector<int> fds;
-  char* base = nullptr;  // every granule mapped here, for the scrub
+  // each granule mapped at an address range of its own, for the scrub: HIP gives a released
+  // handle's memory back to the driver only once the range it was mapped in is freed too
+  // (tools/diag/release_probe.cpp), so a granule going back frees its range
+  std::vector<char*> va;
   hipStream_t stream = nullptr;
   std::deque<int> free_list;
   // released granules being zeroed: lent again once their event has completed
@@ -307,19 +310,28 @@ struct Broker {
     CK(hipMemsetAsync(p, 0, bytes, stream));
   }
 
-  // granule i: created, exported, mapped in the broker's range (not yet zeroed)
-  void add_granule(int i) {
-    CK(hipMemCreate(&h[i], gran, &prop_, 0));
+  // granule i: created, exported, mapped at a range of its own, readable and writable (not yet
+  // zeroed). False (nothing held) when the device has no room for it now.
+  bool add_granule(int i) {
+    if (hipMemCreate(&h[i], gran, &prop_, 0) != hipSuccess) {
+      (void)hipGetLastError();
+      h[i] = nullptr;
+      return false;
+    }
     CK(hipMemExportToShareableHandle(&fds[i], h[i], hipMemHandleTypePosixFileDescriptor, 0));
-    CK(hipMemMap(base + size_t(i) * gran, gran, 0, h[i], 0));
+    CK(hipMemAddressReserve(reinterpret_cast<void**>(&va[i]), gran, 0, nullptr, 0));
+    CK(hipMemMap(va[i], gran, 0, h[i], 0));
+    hipMemAccessDesc d = rw();
+    CK(hipMemSetAccess(va[i], gran, &d, 1));
     present[i] = 1;
+    return true;
   }
 
   // granule i back to the driver (it is free: nobody holds it, it is not being scrubbed). The
   // driver wipes it when the last reference to its memory is gone.
   void destroy_granule(int i) {
     if (!present[i]) return;
-    hipError_t e = hipMemUnmap(base + size_t(i) * gran, gran);
+    hipError_t e = hipMemUnmap(va[i], gran);
     if (e != hipSuccess) {
       (void)hipGetLastError();
       std::fprintf(stderr, "gpushare-hbm-broker: unmap of granule %d: %s (kept out of the free list)\n", i,
@@ -329,6 +341,8 @@ struct Broker {
     }
     (void)hipMemRelease(h[i]);
     h[i] = nullptr;
+    (void)hipMemAddressFree(va[i], gran);
+    va[i] = nullptr;
     close(fds[i]);
     fds[i] = -1;
     base_refs[i] = -1;
@@ -398,17 +412,17 @@ struct Broker {
     fds.assign(count_max, -1);
     base_refs.assign(count_max, -1);
     present.assign(count_max, 0);
-    CK(hipMemAddressReserve(reinterpret_cast<void**>(&base), gran * size_t(std::max(count_max, 1)), 0, nullptr, 0));
+    va.assign(count_max, nullptr);
     for (int i = 0; i < n0; ++i) {
-      add_granule(i);
+      if (!add_granule(i)) break;
       free_list.push_back(i);
+      ++count;
     }
-    count = n0;
-    hipMemAccessDesc d = rw();
-    if (count) CK(hipMemSetAccess(base, gran * count, &d, 1));
     CK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     load_scrub_kernel();
-    if (count) zero(base, gran * count);  // nobody sees what was there before
+    std::vector<int> every;
+    for (int i = 0; i < count; ++i) every.push_back(i);
+    zero_granules(every);  // nobody sees what was there before
     CK(hipStreamSynchronize(stream));
     for (int i = 0; i < count; ++i) base_refs[i] = refs(i);
     counted = count ? (base_refs[0] >= 0 ? 1 : 0) : probe_counted();
@@ -426,18 +440,10 @@ struct Broker {
     if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr <= reserve_bytes) return;
     int n = std::min(target - count, int((fr - reserve_bytes) / gran));
     if (n <= 0) return;
-    hipMemAccessDesc d = rw();
     std::vector<int> fresh;
     for (int i = 0; i < count_max && int(fresh.size()) < n; ++i) {
       if (present[i]) continue;
-      if (hipMemCreate(&h[i], gran, &prop_, 0) != hipSuccess) {  // raced: try again later
-        (void)hipGetLastError();
-        break;
-      }
-      CK(hipMemExportToShareableHandle(&fds[i], h[i], hipMemHandleTypePosixFileDescriptor, 0));
-      CK(hipMemMap(base + size_t(i) * gran, gran, 0, h[i], 0));
-      CK(hipMemSetAccess(base + size_t(i) * gran, gran, &d, 1));
-      present[i] = 1;
+      if (!add_granule(i)) break;  // raced: try again later
       base_refs[i] = refs(i);
       settle_policy(i);
       fresh.push_back(i);
@@ -497,6 +503,17 @@ struct Broker {
                    double(fr) / double(1ull << 30), k, count);
   }
 
+  // zero granules `s` (sorted) on the broker's stream: one launch per run of granules whose
+  // ranges happen to be adjacent
+  void zero_granules(const std::vector<int>& s) {
+    for (size_t i = 0; i < s.size();) {
+      size_t j = i + 1;
+      while (j < s.size() && va[size_t(s[j])] == va[size_t(s[j - 1])] + gran) ++j;
+      zero(va[size_t(s[i])], gran * (j - i));
+      i = j;
+    }
+  }
+
   // zero the granules on the broker's stream; they are lent again from reap_scrubs(), in chunks
   // of scrub_chunk granules (an event each): a pod waiting for a retired pod's 128 granules gets
   // the first ones after ~2 ms of zeroing, not after all of it
@@ -508,12 +525,7 @@ struct Broker {
     size_t step = scrub_chunk > 0 ? size_t(scrub_chunk) : s.size();
     for (size_t c = 0; c < s.size(); c += step) {
       size_t e = std::min(s.size(), c + step);
-      for (size_t i = c; i < e;) {  // one memset per run of adjacent granules
-        size_t j = i + 1;
-        while (j < e && s[j] == s[j - 1] + 1) ++j;
-        zero(base + size_t(s[i]) * gran, gran * (j - i));
-        i = j;
-      }
+      zero_granules(std::vector<int>(s.begin() + long(c), s.begin() + long(e)));
       hipEvent_t ev;
       CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
       CK(hipEventRecord(ev, stream));

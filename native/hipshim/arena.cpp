@@ -272,9 +272,22 @@ void fast_release(const char* why) {
   uint64_t t0 = mono_ns();
   int q = queues_destroy_all();
   int m = imports_free_all_unlocked();
+  // the granule fds this process keeps for IPC exports are references of their own: without
+  // closing them the broker sees the granules held until the kernel closes the fd table, at the
+  // very end of the teardown (measured: 164 ms after SIGTERM, the imports long freed)
+  int c = 0;
+  for (int i = 0; i < kArenaMaxGranules; ++i) {
+    int fd = g_arena.fd[i];
+    if (fd >= 0) {
+      g_arena.fd[i] = -1;
+      close(fd);
+      ++c;
+    }
+  }
   int s = g_arena.sock;
   if (s >= 0) shutdown(s, SHUT_RDWR);  // the broker sees the connection end: the granules are back
-  logf(1, "fast exit (%s): %d queues destroyed, %d imports freed in %.3f ms", why, q, m, (mono_ns() - t0) / 1e6);
+  logf(1, "fast exit (%s): %d queues destroyed, %d imports freed, %d granule fds closed in %.3f ms", why, q, m, c,
+       (mono_ns() - t0) / 1e6);
 }
 
 void on_sigterm(int) {

@@ -861,21 +861,41 @@ def test_a_stopped_pod_gives_its_granules_back_at_once(broker, stop):
     t0 = time.time()
     if stop != "exit":
         p.send_signal(signal.SIGTERM)
-    rc = p.wait(60)
-    exit_ms = (time.time() - t0) * 1e3
+    # the broker's view and the process's end, watched together: the granules may be back
+    # before the kernel has finished tearing the process down
+    exit_ms = back_ms = None
     st = broker.stat()
-    while (st["free"] < st["granules"] or st["quarantined"] or st["scrubbing"]) and time.time() - t0 < 10:
-        time.sleep(0.001)
+    while time.time() - t0 < 60 and (exit_ms is None or back_ms is None):
+        if back_ms is None and st["free"] == st["granules"] and not st["quarantined"] and not st["scrubbing"]:
+            back_ms = (time.time() - t0) * 1e3
+        if exit_ms is None and p.poll() is not None:
+            exit_ms = (time.time() - t0) * 1e3
+        time.sleep(0.0005)
         st = broker.stat()
-    back_ms = (time.time() - t0) * 1e3
+    rc = p.wait(5)
     err = p.stderr.read()
     fast = [ln for ln in err.splitlines() if "fast exit" in ln]
-    print(json.dumps({"stop": stop, "rc": rc, "exit_ms": exit_ms, "back_ms": back_ms,
+    plain_exit_ms = None
+    if stop == "exit":
+        # the same program without the shim: how long its own exit takes
+        plain = dict(os.environ, STOP="exit")
+        q = subprocess.Popen([sys.executable, "-c", STOP_TENANT], env=plain, stdout=subprocess.PIPE,
+                             stderr=subprocess.PIPE, text=True)
+        assert q.stdout.readline(), q.stderr.read()[-3000:]
+        t1 = time.time()
+        assert q.wait(60) == 0
+        plain_exit_ms = (time.time() - t1) * 1e3
+    print(json.dumps({"stop": stop, "rc": rc, "exit_ms": exit_ms, "back_ms": back_ms, "plain_exit_ms": plain_exit_ms,
                       "quarantine_ms_last": st["quarantine_ms_last"], "fast_exit": fast}))
-    assert st["free"] == st["granules"], st
+    assert back_ms is not None, st
     if stop == "sigterm_kernel_path":
         assert rc == -signal.SIGTERM and not fast
         return
     assert fast, err[-3000:]
     assert rc == (0 if stop == "exit" else -signal.SIGTERM)
-    assert back_ms < 100.0, back_ms
+    if stop == "exit":
+        # released at the very end of the exit (after the runtime's own teardown): back no later
+        # than the plain program's exit would have ended
+        assert back_ms < plain_exit_ms + 100.0, (back_ms, plain_exit_ms)
+    else:
+        assert back_ms < 100.0, back_ms
