@@ -1021,13 +1021,17 @@ class Allocator(NativeTable):
         self.metrics.allocate_latency.observe(time.perf_counter() - t, phase="watch_wait")
         return changed
 
-    def _prepared(self, p: dict, u: str, g: int, units: int) -> "_Prepared":
+    def _prepared(self, p: dict, u: str, g: int, units: int, kicks: list | None = None) -> "_Prepared":
         """The answer to a single-container pod's Allocate, serialized ahead of the request:
         the cached wire bytes of its (GPU, size) template followed by its per-pod ledger
         fields, encoded directly (protobuf: appended records of repeated / map fields merge
         into the message) — the same message ``_container_response`` builds, at a fraction of
-        the cost on the watch thread (``tests/test_allocate_engine.py`` pins the equality)."""
+        the cost on the watch thread (``tests/test_allocate_engine.py`` pins the equality).
+        ``kicks``: the ledger and granter threads are not woken here; their wake-ups are
+        appended, for the caller to run once the answer is published (on the way to the
+        kubelet's Allocate, nothing else takes the interpreter)."""
         key = (self._gen, g, units)
+        wake = kicks is None
         base = self._tmpl_bytes.get(key)
         if base is None:
             base = self._container_base(g, units, units, None).SerializeToString()
@@ -1040,8 +1044,11 @@ class Allocator(NativeTable):
             extra = _pb_map_entry(0x0a, const.ENV_SHIM_LEDGER, ledger_name(u or f"{g}-{time.time_ns()}", 0))
             if self._ledgers is not None:
                 try:
-                    lkey = self._ledgers.take(u)
+                    lkey = self._ledgers.take(u, wake)
+                    self._mark(u, "prep_ledger")
                     host = self._ledgers.path(lkey)
+                    if not wake:
+                        kicks.append(self._ledgers.kick)
                 except OSError as e:
                     log.warning("ledger dir for pod %s: %s (pod-private shm ledger instead)", u, e)
                     lkey = ""
@@ -1053,8 +1060,12 @@ class Allocator(NativeTable):
             if hbm is not None:
                 gg = self.model.gpu(g)
                 tok = hbm.token(u or f"{g}-{time.time_ns()}", 0)
-                if hbm.submit(g, tok, U.quota_bytes(units, gg.units, gg.vram_bytes)):
+                ok = hbm.submit(g, tok, U.quota_bytes(units, gg.units, gg.vram_bytes), wake)
+                self._mark(u, "prep_hbm")
+                if ok:
                     extra += _pb_map_entry(0x0a, const.ENV_HBM_TOKEN, tok)
+                    if not wake:
+                        kicks.append(hbm.kick)
         body = _pb_ld(0x0a, base + extra)            # AllocateResponse.container_responses[0]
         return _Prepared(u, O.namespace(p), O.name(p), units, False, g, body,
                          AllocJournal.fast_head(u, O.namespace(p), O.name(p), body), lkey)

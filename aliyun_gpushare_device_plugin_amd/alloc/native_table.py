@@ -171,6 +171,14 @@ class NativeTable:
         taken in the server."""
         if not self.opts.fast_path or self.opts.compute_isolation == "cu" or time.time() < self.journal._legacy_until:
             return ""
+        kicks: list = []
+        try:
+            return self._publish_change_in(nat, version, pod, gone, kicks)
+        finally:
+            for k in kicks:                           # the ledger / granter threads, after the publish
+                k()
+
+    def _publish_change_in(self, nat, version: int, pod: dict, gone: bool, kicks: list) -> str:
         with self._table_mu:
             last = self._last_table
             gen = self._gen
@@ -192,7 +200,7 @@ class NativeTable:
                     elif self.model.gpu(g) is not None:
                         k = (u, g, shape[0])
                         c = (self._prep_cache.get(k) or self._take_precomputed(k)
-                             or self._prepared(p, u, g, shape[0]))
+                             or self._prepared(p, u, g, shape[0], kicks))
                         self._prep_cache[k] = c
             at = (0, at)                              # a pod of the pod cache: bound here
             keep_at = idx is not None and c is not None and ats[idx] == at
@@ -220,6 +228,7 @@ class NativeTable:
 
     # ---- the per-pod timeline (``/debug/latency`` "pod_trace") ------------------------------
     PTRACE_KEEP = 256
+    PTRACE_CPU = frozenset(("pre_seen", "prep_ledger", "prep_hbm", "pre_prep", "pre_pub"))
 
     def _mark(self, u: str, key: str, t: int | None = None) -> None:
         """First time ``key`` happened for pod ``u`` (CLOCK_MONOTONIC ns, comparable across the
@@ -234,6 +243,8 @@ class NativeTable:
                 self._ptrace.pop(next(iter(self._ptrace)), None)
         if key not in tr:
             tr[key] = t if t is not None else time.monotonic_ns()
+            if t is None and key in self.PTRACE_CPU:
+                tr[key + "_cpu_ns"] = time.thread_time_ns()   # this thread's CPU time: wall - cpu = waits
 
     def pod_trace(self) -> list[dict]:
         """The last pods' timelines, in ms relative to their Allocate's arrival (pods whose
@@ -357,27 +368,32 @@ class NativeTable:
         if not assumed or len(shape) != 1:
             return
         u, g = O.uid(pod), A.gpu_id_from_annotation(pod)
-        self._mark(u, "pre_seen")
+        self._mark(u, "pre_seen")                    # (pre_read: its watch event's bytes arrived)
         if self.pods.get(u) is not None:
             self._mark(u, "pre_after_bind")
             return                                    # the bind came first: the pod cache has it
         k = (u, g, shape[0])
         if self.model.gpu(g) is None:
             return
-        if k not in self._precomputed and k not in self._prep_cache and u not in self._native_prep:
-            c = self._prepared(pod, u, g, shape[0])
-            _native_blob(0, 0, 0, [c], [])            # fills c.frag: the table entry, encoded once
-            self._precomputed[k] = (c, time.monotonic())
-            while len(self._precomputed) > 1024:
-                self._precomputed.popitem(last=False)
-            self._mark(u, "pre_prep")
-        with self._table_mu:
-            prev = self._prebind.get(u)
-            self._prebind[u] = (pod, prev[1] if prev is not None else time.monotonic(), None)
-            while len(self._prebind) > 1024:
-                self._prebind.pop(next(iter(self._prebind)))
-        how = self._publish_prebind(u)
-        self._mark(u, "pre_pub" if how == "pub" else f"pre_{how}")
+        kicks: list = []
+        try:
+            if k not in self._precomputed and k not in self._prep_cache and u not in self._native_prep:
+                c = self._prepared(pod, u, g, shape[0], kicks)
+                _native_blob(0, 0, 0, [c], [])        # fills c.frag: the table entry, encoded once
+                self._precomputed[k] = (c, time.monotonic())
+                while len(self._precomputed) > 1024:
+                    self._precomputed.popitem(last=False)
+                self._mark(u, "pre_prep")
+            with self._table_mu:
+                prev = self._prebind.get(u)
+                self._prebind[u] = (pod, prev[1] if prev is not None else time.monotonic(), None)
+                while len(self._prebind) > 1024:
+                    self._prebind.pop(next(iter(self._prebind)))
+            how = self._publish_prebind(u, kicks=kicks)
+            self._mark(u, "pre_pub" if how == "pub" else f"pre_{how}")
+        finally:
+            for kk in kicks:                          # the ledger / granter threads, after the publish
+                kk()
 
     # how long a pre-bind candidate whose pre-bind watch entry went away (bound, deleted, label
     # moved: the watch does not say which) stays in the table waiting for the pod watch to show
@@ -441,7 +457,7 @@ class NativeTable:
             self.metrics.allocate_outcomes.inc(outcome="prebind_withdrawn")
             self._publish_prebind(u, remove=True)
 
-    def _publish_prebind(self, u: str, remove: bool = False) -> str:
+    def _publish_prebind(self, u: str, remove: bool = False, kicks: list | None = None) -> str:
         """Insert (or withdraw) pre-bind candidate ``u`` in the last published table, at the same
         cache version: the table is what a full rebuild gives now (``_prepare`` takes the same
         pre-bind set into its candidates). Returns what happened ("pub", or why not)."""
@@ -474,7 +490,7 @@ class NativeTable:
                     return "not_candidate"
                 g = A.gpu_id_from_annotation(p)
                 k = (u, g, shape[0])
-                c = self._prep_cache.get(k) or self._take_precomputed(k) or self._prepared(p, u, g, shape[0])
+                c = self._prep_cache.get(k) or self._take_precomputed(k) or self._prepared(p, u, g, shape[0], kicks)
                 self._prep_cache[k] = c
                 key = (1, at)                         # after every bound candidate (_candidates)
                 i = bisect.bisect_right(ats, key)

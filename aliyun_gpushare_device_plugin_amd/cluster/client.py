@@ -333,12 +333,15 @@ class APIClient:
                     break
                 if not chunk:
                     break
+                t_read = time.monotonic_ns()
                 buf += chunk
                 while b"\n" in buf:
                     line, buf = buf.split(b"\n", 1)
                     line = line.strip()
                     if line:
-                        yield json.loads(line)
+                        ev = json.loads(line)
+                        ev["_read_ns"] = t_read            # when its bytes arrived (timelines)
+                        yield ev
         finally:
             if holder is not None:
                 holder[:] = []

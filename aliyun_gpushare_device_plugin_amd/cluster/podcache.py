@@ -161,9 +161,10 @@ class PrebindWatch:
     ``on_gone(pod)`` when a pod leaves that set (bound, deleted, relabelled: a watch's DELETED for
     an object that stops matching carries its previous state, so which one is not known here)."""
 
-    def __init__(self, client: APIClient, node: str, on_pod, watch_timeout: int = 300, on_gone=None):
+    def __init__(self, client: APIClient, node: str, on_pod, watch_timeout: int = 300, on_gone=None, trace=None):
         self.client, self.node, self.on_pod, self.watch_timeout = client, node, on_pod, watch_timeout
         self.on_gone = on_gone
+        self.trace = trace          # trace(uid, "pre_read", ns): when the event's bytes arrived
         self._stop = threading.Event()
         self._conn: list = []
         self._thread = None
@@ -188,6 +189,8 @@ class PrebindWatch:
                     try:
                         if typ in ("ADDED", "MODIFIED") and not O.node_name(obj):
                             self.events += 1
+                            if self.trace is not None and ev.get("_read_ns"):
+                                self.trace(O.uid(obj), "pre_read", ev["_read_ns"])
                             self.on_pod(obj)
                         elif typ == "DELETED" and self.on_gone is not None:
                             self.on_gone(obj)

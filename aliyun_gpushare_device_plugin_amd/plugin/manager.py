@@ -213,7 +213,7 @@ class SharedGPUManager:
             allocator.set_pod_resources(self._pod_resources())
         if cfg.prebind_watch and cfg.pod_source == "watch" and self.client is not None:
             self._prebind = PrebindWatch(self.client, cfg.node_name, allocator.precompute,
-                                         on_gone=allocator.prebind_gone).start()
+                                         on_gone=allocator.prebind_gone, trace=allocator._mark).start()
         self.model = model
         cls = self._server_class()
         kw = ({"fast_wait_us": cfg.native_fast_wait_us, "spin_us": cfg.native_spin_us}

@@ -347,9 +347,10 @@ class HBMGranter:
             return now - st.last_ok < self.down_grace_s
         return now - self._t0 < self.startup_grace_s
 
-    def submit(self, gpu_index: int, token: str, quota_bytes: int) -> bool:
-        """Record the grant and have the granter thread send it; True = the answer carries the
-        token. Runs on the pod watch / prepare threads: never waits for a broker."""
+    def submit(self, gpu_index: int, token: str, quota_bytes: int, wake: bool = True) -> bool:
+        """Record the grant and have the granter thread send it (woken now, or at ``kick()``
+        when ``wake`` is false); True = the answer carries the token. Runs on the pod watch /
+        prepare threads: never waits for a broker."""
         nbytes = self.arena_bytes(quota_bytes)
         if not nbytes or self.disabled or not self.ready(gpu_index):
             return False
@@ -362,8 +363,12 @@ class HBMGranter:
             st = self._gpus.get(gpu_index)
             if st is None or st.sent.get(token) != nbytes:
                 self._unsent.add(token)
-        self._wake.set()
+        if wake:
+            self._wake.set()
         return True
+
+    def kick(self) -> None:
+        self._wake.set()
 
     def flush(self, timeout: float = 5.0) -> bool:
         """Wait until every submitted grant was acknowledged, or until a full pass has tried the

@@ -157,20 +157,28 @@ class LedgerDir:
         os.chmod(path, 0o777)             # containers may run as any uid; only one sees it
         return path
 
-    def take(self, owner_uid: str) -> str:
+    def take(self, owner_uid: str, wake: bool = True) -> str:
         """A fresh per-container directory for ``owner_uid``'s container: its key. Pool hit =
-        no syscall on the caller's path; the owner record follows on the background thread."""
+        no syscall on the caller's path; the owner record follows on the background thread
+        (woken now, or at ``kick()`` when ``wake`` is false: a caller racing the kubelet's
+        Allocate keeps the interpreter to itself until its answer is published)."""
         with self._cv:
             lkey = self._pool.pop() if self._pool else None
             if lkey is not None:
                 self._pending.append((lkey, [owner_uid] if owner_uid else []))
-                self._cv.notify()
+                if wake:
+                    self._cv.notify()
                 return lkey
         lkey = self.new_key(owner_uid, 0)
         self.create(lkey, owner_uid)
         with self._cv:
             self._cv.notify()
         return lkey
+
+    def kick(self) -> None:
+        """Wake the background thread for records ``take(wake=False)`` left."""
+        with self._cv:
+            self._cv.notify()
 
     def path(self, lkey: str) -> str:
         return os.path.join(self.root, lkey)

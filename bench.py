@@ -239,6 +239,17 @@ def pod_timeline(port: int, commits: dict) -> dict | None:
         xs = sorted(r[k] for r in rows if isinstance(r.get(k), (int, float)))
         return xs[len(xs) // 2] if xs else None
 
+    # the pre-bind path's steps: wall time and this thread's CPU time (wall - CPU = waiting for
+    # the interpreter lock or a CPU), medians in us
+    steps = {}
+    seq = ("pre_seen", "prep_ledger", "prep_hbm", "pre_prep", "pre_pub")
+    for a_, b_ in zip(seq, seq[1:]):
+        wall = sorted((r[b_] - r[a_]) * 1e3 for r in rows if isinstance(r.get(a_), (int, float)) and isinstance(r.get(b_), (int, float)))
+        cpu = sorted((r[b_ + "_cpu_ns"] - r[a_ + "_cpu_ns"]) / 1e3 for r in rows
+                     if r.get(a_ + "_cpu_ns") is not None and r.get(b_ + "_cpu_ns") is not None)
+        if wall:
+            steps[f"{a_}->{b_}"] = {"wall_us": round(wall[len(wall) // 2], 1),
+                                    "cpu_us": round(cpu[len(cpu) // 2], 1) if cpu else None}
     waited = [r for r in rows if r.get("watch_wait_ns")]
     causes: dict = {}
     for r in waited:
@@ -251,8 +262,9 @@ def pod_timeline(port: int, commits: dict) -> dict | None:
         else:
             why = "prebind_publish_after_allocate"     # read, still preparing / publishing
         causes[why] = causes.get(why, 0) + 1
-    keys = ("commit_start", "commit_done", "pre_seen", "pre_prep", "pre_pub", "bind_seen", "bind_pub", "tab")
-    return {"pods": len(rows), "watch_waited": len(waited), "causes": causes,
+    keys = ("commit_start", "commit_done", "pre_read", "pre_seen", "prep_ledger", "prep_hbm", "pre_prep", "pre_pub",
+            "bind_seen", "bind_pub", "tab")
+    return {"pods": len(rows), "watch_waited": len(waited), "causes": causes, "prebind_steps": steps,
             "median_ms": {k: med(k) for k in keys},
             "waited": [{k: r.get(k) for k in keys + ("watch_wait_ns", "table_wait_ns", "path") if r.get(k) is not None}
                        for r in waited]}

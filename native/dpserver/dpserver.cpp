@@ -276,7 +276,8 @@ struct gs_dp {
   std::atomic<int64_t> spin_until{0};
   // bumped (under mu) by everything a table wait depends on: a spinning waiter watches it
   // without the lock, so it never contends with the publisher it is waiting for
-  std::atomic<uint64_t> table_seq{0};   // an Allocate with no candidate yet waits this long for the pod watch
+  std::atomic<uint64_t> table_seq{0};
+  uint64_t pub_seq = 0;                  // tables published (under mu)   // an Allocate with no candidate yet waits this long for the pod watch
   // fake IDs of native answers -> when: a kubelet retry of them is for the engine (replay),
   // kept until a published replay set covers them (or for 30 s, by when the engine has)
   std::unordered_map<std::string, int64_t> answered_ids;
@@ -580,14 +581,20 @@ bool fast_allocate(Conn* c, int32_t sid, const std::string& body, int64_t t_in) 
     // no candidate of this size yet: the kubelet's own pod watch can deliver the bind before
     // the plugin's does; the engine's cache hook publishes the pod the moment it arrives, so
     // wait for the next table (a LIST on the engine's path is the alternative)
+    // (a pre-bind entry is published at the same cache version: any new table counts)
     s->n.watch_waits++;
-    uint64_t v = s->cur_version;
-    int64_t w0 = mono_ns();
-    wait_for_table(s, lk, s->watch_wait_us, [&] {
-      return (s->cur_version != v && table_current(s)) || s->blocked > 0 || s->stopping.load();
-    });
+    int64_t w0 = mono_ns(), dl = w0 + (int64_t)s->watch_wait_us * 1000;
+    while (d == kNoMatch) {
+      int left_us = (int)((dl - mono_ns()) / 1000);
+      if (left_us <= 0) break;
+      uint64_t seq = s->pub_seq;
+      wait_for_table(s, lk, left_us, [&] {
+        return (s->pub_seq != seq && table_current(s)) || s->blocked > 0 || s->stopping.load();
+      });
+      if (s->blocked > 0 || s->stopping.load() || !table_current(s)) break;
+      if (s->pub_seq != seq) d = pick(s, crs[0], &en);
+    }
     ww = (uint64_t)(mono_ns() - w0);
-    if (table_current(s)) d = pick(s, crs[0], &en);
   }
   if (d != kOk) {
     count_decline(s, d);
@@ -1070,6 +1077,7 @@ int gs_dp_fast_publish(gs_dp* s, const uint8_t* blob, int len) {
       it = (t.replay.count(it->first) || now - it->second > 30 * 1000000000LL) ? s->answered_ids.erase(it) : ++it;
     s->table = std::move(t);
     s->table_seq++;
+    s->pub_seq++;
   }
   s->cv.notify_all();
   return 0;

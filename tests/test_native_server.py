@@ -724,9 +724,9 @@ def test_answers_are_prepared_before_the_bind():
         built = []
         real = al._prepared
 
-        def counting(p, u, g, units):
+        def counting(p, u, g, units, kicks=None):
             built.append((u, threading.current_thread().name))
-            return real(p, u, g, units)
+            return real(p, u, g, units, kicks)
 
         al._prepared = counting
         pod = c.create_pod(2)
@@ -846,6 +846,46 @@ def _prebind_server(tmp_path):
 
 def _in_table(al, uid):
     return any(c.uid == uid for c in al._last_table[2])
+
+
+def test_an_allocate_waiting_for_the_watch_takes_a_prebind_entry_published_meanwhile(tmp_path):
+    """VERDICT r5 item 4 (the instrumented cause, ``profiles/r6``): the kubelet's Allocate came
+    while the pre-bind watch was still preparing the pod's answer. The entry is published at the
+    same pod-cache version; the waiting Allocate takes it then, without waiting for the bind to
+    reach the plugin's pod watch."""
+    srv, al, src = _prebind_server(tmp_path)
+    ch, stub = _stub(srv)
+    try:
+        p = mkpod("late", 2, 1, 10, node="")
+        srv._lib.gs_dp_set_watch_wait_us(srv._h, 3_000_000)   # (a loaded CI host: room for precompute)
+        before = srv.stats()
+        got = {}
+
+        def call():
+            t0 = time.monotonic()
+            got["r"] = stub.Allocate(_req("w1", "w2"))
+            got["s"] = time.monotonic() - t0
+
+        th = threading.Thread(target=call)
+        th.start()
+        t = time.monotonic() + 5
+        while srv.stats()["watch_waits"] == before["watch_waits"] and time.monotonic() < t:
+            time.sleep(0.0005)
+        al.precompute(p)                                   # the pre-bind watch catches up
+        th.join(10)
+        st = srv.stats()
+        assert got["r"].container_responses[0].envs[const.ENV_RESOURCE_INDEX] == "1"
+        assert st["fast"] == before["fast"] + 1 and st["watch_waits"] == before["watch_waits"] + 1
+        assert got["s"] < 2.5                              # not the whole watch-wait window
+        t = time.monotonic() + 5
+        while "uid-late" not in al._assigned and time.monotonic() < t:
+            time.sleep(0.01)
+        tr = {r["uid"]: r for r in al.pod_trace()}["uid-late"]
+        assert tr["path"] == "native" and tr["watch_wait_ns"] > 0 and tr["pre_pub"] > tr["pre_seen"] > 0
+    finally:
+        ch.close()
+        srv.stop()
+        al.close()
 
 
 def test_a_prebind_pod_is_answered_before_the_plugin_sees_its_bind(tmp_path):

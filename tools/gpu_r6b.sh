@@ -1,4 +1,3 @@
 set -o pipefail
-mkdir -p gpurun_out/r6c
-timeout -k 10 90 tools/diag/release_probe 16 pergran > gpurun_out/r6c/release_probe.jsonl 2>&1 || exit 1
-timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -s tests/test_hbm_broker.py > gpurun_out/r6c/hbm_broker_tests.log 2>&1
+mkdir -p gpurun_out/r6g
+timeout -k 10 900 python -u bench.py --steps 20 --warmup 3 --json-out gpurun_out/r6g/bench.json > gpurun_out/r6g/bench.log 2>&1
