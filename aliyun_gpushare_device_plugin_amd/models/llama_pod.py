@@ -17,6 +17,54 @@ import sys
 import time
 
 
+def _shim() -> dict | None:
+    """The quota shim's ledger and arena counters (None without the shim): quota denials, the
+    broker arena's size and use, granules borrowed beyond the grant, allocations that went to
+    the driver."""
+    import ctypes
+
+    from .pod_worker import _shim_stats
+
+    st = _shim_stats()
+    if st is None:
+        return None
+    lib = ctypes.CDLL(None)
+    try:
+        f = lib.gpushare_shim_arena_stats
+        f.argtypes = [ctypes.POINTER(ctypes.c_uint64)] * 2
+        v = [ctypes.c_uint64() for _ in range(2)]
+        if f(*(ctypes.byref(x) for x in v)):
+            st.update(arena_bytes=v[0].value, arena_used=v[1].value)
+        g = lib.gpushare_shim_arena_extra
+        g.argtypes = [ctypes.POINTER(ctypes.c_uint64)] * 5
+        w = [ctypes.c_uint64() for _ in range(5)]
+        g(*(ctypes.byref(x) for x in w))
+        st.update(zip(("extends", "extended", "driver_allocs", "driver_bytes", "limit_granules"), (x.value for x in w)))
+        b = lib.gpushare_shim_arena_base
+        b.restype = ctypes.c_uint64
+        base = b()
+        if base:
+            st["arena_base_mod_mib"] = (base % (1 << 30)) >> 20
+    except AttributeError:
+        pass
+    return st
+
+
+def _evicted_ms() -> dict:
+    """KFD's per-GPU count of how long this process's queues were evicted (ms): memory a KFD
+    process maps being moved or validated by another process stops all of its queues."""
+    import glob
+
+    out = {}
+    for f in glob.glob(f"/sys/class/kfd/kfd/proc/{os.getpid()}/stats_*/evicted_ms"):
+        try:
+            with open(f) as fh:
+                out[f.split("/")[-2]] = int(fh.read().strip() or 0)
+        except (OSError, ValueError):
+            pass
+    return out
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=20.0)
@@ -46,7 +94,9 @@ def main(argv=None):
         print(json.dumps(kw), flush=True)
 
     free, total = torch.cuda.mem_get_info()
+    sh0 = _shim() or {}
     emit(event="start", quota_total=total, free=free, ld_preload=os.environ.get("LD_PRELOAD", ""),
+         shim_denied=sh0.get("denied"),                    # (the pod's ledger counts across its runs)
          container_units=os.environ.get("ALIYUN_COM_GPU_MEM_CONTAINER"),
          dev_units=os.environ.get("ALIYUN_COM_GPU_MEM_DEV"))
     cfg = LlamaConfig.llama3_8b(n_layers=a.layers)
@@ -66,14 +116,17 @@ def main(argv=None):
     emit(event="loaded", weight_bytes=model.weight_bytes(), params=cfg.n_params())
     if a.probe_quota:
         free, total = torch.cuda.mem_get_info()
+        d0 = (_shim() or {}).get("denied") or 0
         try:
             x = torch.empty(int(free * 1.5) // 2, dtype=torch.bfloat16, device="cuda")
             emit(event="quota_probe", over_quota_alloc="allowed")
             del x
         except torch.OutOfMemoryError:
-            emit(event="quota_probe", over_quota_alloc="denied")
+            emit(event="quota_probe", over_quota_alloc="denied",
+                 probe_denied=((_shim() or {}).get("denied") or 0) - d0)
         torch.cuda.empty_cache()
-    emit(event="ready")
+    ev0 = _evicted_ms()
+    emit(event="ready", evicted_ms=ev0)
     if a.start_file:
         while not os.path.exists(a.start_file):
             time.sleep(0.01)
@@ -109,7 +162,8 @@ def main(argv=None):
          peak_mem=torch.cuda.max_memory_allocated(), lat_p50_ms=q(0.5), lat_p99_ms=q(0.99),
          lat_max_ms=round(lat[-1] * 1e3, 2) if lat else None,
          cus=torch.cuda.get_device_properties(0).multi_processor_count,
-         cu_slots=os.environ.get("GPUSHARE_CU_SLOTS"))
+         cu_slots=os.environ.get("GPUSHARE_CU_SLOTS"), shim=_shim(),
+         evicted_ms={k: v - ev0.get(k, 0) for k, v in _evicted_ms().items()})
     return 0
 
 

@@ -161,6 +161,26 @@ class SimCluster:
                             admission_identity=self.admission_identity, grpc_server=self.grpc_server,
                             **self._kubelet_cfg(node))
 
+    def _thread_cfg(self, node: SimNode) -> PluginConfig:
+        """The in-process plugin's config: ``_plugin_cfg`` plus whatever the extra plugin
+        arguments (the command-line flags a process-mode plugin gets) set away from their
+        defaults, so both modes run the same plugin."""
+        cfg = self._plugin_cfg(node)
+        ov = self.node_overrides.get(node.name, {})
+        extra = list(ov["extra_args"] if "extra_args" in ov else self.extra_plugin_args)
+        if extra:
+            import dataclasses
+
+            from ..cli.main import build_parser, config_from_args
+
+            base = config_from_args(build_parser().parse_args([]))
+            over = config_from_args(build_parser().parse_args(extra))
+            for f in dataclasses.fields(cfg):
+                v = getattr(over, f.name)
+                if v != getattr(base, f.name):
+                    setattr(cfg, f.name, v)
+        return cfg
+
     def _podres(self, node: SimNode) -> str:
         return os.path.join(node.plugin_dir, "pod-resources.sock") if self.placement_truth else "none"
 
@@ -195,7 +215,7 @@ class SimCluster:
             node.proc = subprocess.Popen(args, env=self._child_env(), stdout=subprocess.DEVNULL,
                                          stderr=open(os.path.join(self.workdir, f"{node.name}.plugin.log"), "w"))
         else:
-            node.manager = SharedGPUManager(self._plugin_cfg(node), client=APIClient(KubeConfig(self.api_url)))
+            node.manager = SharedGPUManager(self._thread_cfg(node), client=APIClient(KubeConfig(self.api_url)))
             node.thread = threading.Thread(target=node.manager.run, kwargs={"install_signals": False},
                                            name=f"plugin-{node.name}", daemon=True)
             node.thread.start()

@@ -484,7 +484,12 @@ void arena_take() {
     void* base = nullptr;
     uint64_t vsize = limit * gran;  // the whole quota: granules beyond the grant map after it
     uint64_t t_r = mono_ns();
-    if (reserve_f(&base, vsize, 0, nullptr, 0) != hipSuccess) goto fail;
+    // aligned to the granule (GPUSHARE_ARENA_ALIGN_MIB overrides; 0 = the runtime's default), so
+    // the GPU's page tables can map each granule with the largest fragments its pages allow
+    uint64_t align = env_u64("GPUSHARE_ARENA_ALIGN_MIB", gran >> 20) << 20;
+    if (reserve_f(&base, vsize, align, nullptr, 0) != hipSuccess &&
+        (align == 0 || reserve_f(&base, vsize, 0, nullptr, 0) != hipSuccess))
+      goto fail;
     g_take_reserve_ns = mono_ns() - t_r;
     g_take_first = uint64_t(got);
     logf(2, "hbm broker: reserved %p + %llu", base, (unsigned long long)vsize);
@@ -1069,6 +1074,9 @@ GS_EXPORT int gpushare_shim_arena_first(uint64_t* import_ns, uint64_t* map_ns, u
 }
 
 // (size, used) of the arena; 0 when there is none
+// the arena's address (0 without one): tests and tools check its alignment
+GS_EXPORT uint64_t gpushare_shim_arena_base() { return reinterpret_cast<uint64_t>(g_arena.base); }
+
 GS_EXPORT int gpushare_shim_arena_stats(uint64_t* size, uint64_t* used) {
   Arena& a = g_arena;
   pthread_mutex_lock(&a.mu);

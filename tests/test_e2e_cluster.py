@@ -214,3 +214,17 @@ def test_children_arm_their_lifeline_after_exec():
     env["GPUSHARE_DIE_WITH_PARENT"] = "1"                     # not our parent: the child leaves quietly
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=60)
     assert r.returncode == 0 and r.stdout == ""
+
+
+def test_an_in_process_plugin_gets_the_extra_plugin_flags(tmp_path):
+    """The simulator's thread-mode plugin runs with the same flags a process-mode one is started
+    with: a tool passing ``--hbm-broker-dir`` (tools/bench_colocate.py) gets a plugin that grants
+    HBM, not one that silently ignores the flag."""
+    hdir = tmp_path / "hbm"
+    with SimCluster([("n", "fake:1x288G")], extra_plugin_args=["--hbm-broker-dir", str(hdir)],
+                    shim_host_dir=str(tmp_path / "shim")) as c:
+        m = c.manager("n")
+        assert m.cfg.hbm_broker_dir == str(hdir) and m.allocator._hbm is not None
+        _, where, adm = c.run_pod(16)
+        assert adm.error is None
+        assert adm.responses[0].envs[const.ENV_HBM_BROKER].endswith("hbm0.sock")
