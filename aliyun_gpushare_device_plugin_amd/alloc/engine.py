@@ -133,6 +133,8 @@ class AllocatorOptions:
     # a container's quota granted as broker granules (quota/hbmbroker.py HBMGranter); None = off
     hbm_broker_dir: str | None = None
     hbm_broker_fraction: float = 0.94
+    # the node's read-only comgr cache (quota/comgr_cache.py) on the host; None = off
+    comgr_cache_dir: str | None = None
     # HBMGranter keyword arguments (poll_s, startup_grace_s, down_grace_s, revoke_grace_s, ...)
     hbm_granter_args: dict = dataclasses.field(default_factory=dict)
 
@@ -773,6 +775,14 @@ class Allocator(NativeTable):
                 r.mounts.add(container_path=const.HBM_BROKER_CONTAINER_DIR, host_path=self._hbm.mount_dir(gpu_index),
                              read_only=True)
                 r.envs[const.ENV_HBM_BROKER] = self._hbm.container_socket(gpu_index)
+        if self.opts.comgr_cache_dir and not self.opts.disable_cgpu:
+            # code objects the runtime would build with comgr at the container's first stream:
+            # from the cache the DaemonSet's init container filled; read-only, so no pod can put
+            # code into another pod's runtime (a miss compiles as without the cache)
+            r.mounts.add(container_path=const.COMGR_CACHE_CONTAINER_DIR, host_path=self.opts.comgr_cache_dir,
+                         read_only=True)
+            r.envs[const.ENV_COMGR_CACHE] = "1"
+            r.envs[const.ENV_COMGR_CACHE_DIR] = const.COMGR_CACHE_CONTAINER_DIR
         return r
 
     def _plan_slots(self, claim: _Claim, pod_units: int) -> cuslots.SlotRun | None:

@@ -75,6 +75,10 @@ def build_parser() -> argparse.ArgumentParser:
                    help="host directory of the per-GPU HBM brokers' sockets (hbm<index>.sock, gpushare-hbm-broker): "
                         "every shared container gets a grant of broker granules and its quota shim serves hipMalloc "
                         "from them, so admissions do not wait for amdgpu to wipe a retired pod's HBM")
+    p.add_argument("--comgr-cache-dir", default=None,
+                   help="host directory of the node's comgr cache (filled by the DaemonSet's init container, "
+                        "gpushare-comgr-cache): mounted read-only into shared containers with AMD_COMGR_CACHE set, "
+                        "so their HIP runtime loads its blit kernels instead of compiling them at the first stream")
     p.add_argument("--hbm-broker-fraction", type=float, default=0.94,
                    help="share of a container's quota granted as broker granules (whole GiB, rounded down); the "
                         "rest of the quota is borrowed from granules no grant claims, or from the driver")
@@ -158,7 +162,7 @@ def config_from_args(a) -> PluginConfig:
         rocr_visible=a.rocr_visible_devices, metrics_addr=a.metrics_addr, mps=_bool(a.mps),
         async_patch=not a.sync_patch, complete_swaps=not a.no_swap_completion,
         partition_aware=a.partition_aware, ledger_dir=a.ledger_dir, ledger_scan_s=a.ledger_scan_interval,
-        hbm_broker_dir=a.hbm_broker_dir, hbm_broker_fraction=a.hbm_broker_fraction, label_poll_s=a.label_poll_interval,
+        hbm_broker_dir=a.hbm_broker_dir, hbm_broker_fraction=a.hbm_broker_fraction, comgr_cache_dir=a.comgr_cache_dir, label_poll_s=a.label_poll_interval,
         journal_path=a.journal_path, compute_isolation=a.compute_isolation,
         pod_resources_socket=a.pod_resources_socket, placement_s=a.placement_interval,
         admission_identity=a.admission_identity, quota_enforcement=a.quota_enforcement,

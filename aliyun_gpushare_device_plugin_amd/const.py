@@ -69,6 +69,11 @@ LEDGER_CONTAINER_DIR = "/run/gpushare/ledger"
 ENV_HBM_BROKER = "GPUSHARE_HBM_BROKER"
 ENV_HBM_TOKEN = "GPUSHARE_HBM_TOKEN"
 HBM_BROKER_CONTAINER_DIR = "/run/gpushare/hbm"
+# the node's trusted comgr cache (quota/comgr_cache.py): code objects the HIP runtimes build at a
+# process's first stream, compiled once by the DaemonSet's init container and mounted read-only
+ENV_COMGR_CACHE = "AMD_COMGR_CACHE"
+ENV_COMGR_CACHE_DIR = "AMD_COMGR_CACHE_DIR"
+COMGR_CACHE_CONTAINER_DIR = "/run/gpushare/comgr-cache"
 # container annotation (ContainerAllocateResponse.annotations): the host ledger directory key
 # of this container, so the plugin can map an answer back to its ledger (quota/ledger.py)
 CTR_ANNOTATION_LEDGER = "gpushare.amd.com/ledger"

@@ -70,6 +70,7 @@ class PluginConfig:
     ledger_dir: str | None = None        # host dir for file-backed shim ledgers (usage metrics)
     hbm_broker_dir: str | None = None    # host dir of the per-GPU HBM broker sockets (quota/hbmbroker.py)
     hbm_broker_fraction: float = 0.94
+    comgr_cache_dir: str | None = None   # host dir of the node's read-only comgr cache (quota/comgr_cache.py)
     hbm_granter_args: dict = dataclasses.field(default_factory=dict)   # HBMGranter timing (tests)
     ledger_scan_s: float = 10.0
     journal_path: str | None = None      # persisted allocation journal (alloc/journal.py)
@@ -195,6 +196,7 @@ class SharedGPUManager:
                                 ledger_dir=cfg.ledger_dir if shim else None,
                                 hbm_broker_dir=cfg.hbm_broker_dir if shim else None,
                                 hbm_broker_fraction=cfg.hbm_broker_fraction,
+                                comgr_cache_dir=cfg.comgr_cache_dir,
                                 hbm_granter_args=dict(cfg.hbm_granter_args),
                                 journal_path=cfg.journal_path,
                                 compute_isolation=cfg.compute_isolation, placement_s=cfg.placement_s,

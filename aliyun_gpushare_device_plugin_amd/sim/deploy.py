@@ -36,6 +36,7 @@ ENTRY_POINTS = {
     "gpushare-scheduler-extender": "aliyun_gpushare_device_plugin_amd.cli.extender",
     "kubectl-inspect-gpushare": "aliyun_gpushare_device_plugin_amd.cli.inspect",
     "gpushare-hbm-brokers": "aliyun_gpushare_device_plugin_amd.cli.hbmbroker",
+    "gpushare-comgr-cache": "aliyun_gpushare_device_plugin_amd.cli.comgrcache",
 }
 
 

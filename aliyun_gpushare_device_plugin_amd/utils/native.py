@@ -22,6 +22,7 @@ LIBS = {
     "dpserver": "libgpushare_dpserver.so",
     "kernels": "libgpushare_kernels.so",
     "hbmbroker": "gpushare-hbm-broker",
+    "comgrwarm": "gpushare-comgr-warm",
 }
 
 _lock = threading.Lock()
@@ -47,7 +48,7 @@ def lib_path(target: str) -> str:
 
 
 SOURCES = {"gpuinfo": "gpuinfo", "hipshim": "hipshim", "dpserver": "dpserver", "kernels": "kernels",
-           "hbmbroker": "hbmbroker"}   # native/<dir>
+           "hbmbroker": "hbmbroker", "comgrwarm": "comgrwarm"}   # native/<dir>
 
 
 def stale(target: str, path: str) -> bool:

@@ -114,6 +114,10 @@ def parse():
                          "(libamdhip64.so.7, tests/native/fake_hip.c), shim_driver and a gpushare-hbm-broker linked "
                          "against it; every rank runs a stub broker and its pods are stub processes under the real "
                          "quota shim that take their arenas from it")
+    ap.add_argument("--comgr-cache", action=argparse.BooleanOptionalAction, default=True,
+                    help="the DaemonSet's comgr cache (quota/comgr_cache.py): filled before the plugin starts, as its "
+                         "init container does, and mounted read-only into every pod (--comgr-cache-dir)")
+    ap.add_argument("--comgr-cache-dir", default=None, help="an already filled cache to use (the comparators' runs)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -301,7 +305,8 @@ class ControlPlane:
     """Rank 0's view of the node: fake cluster + the real plugin process."""
 
     def __init__(self, n_gpus: int, smi_spec: str, pod_source: str, plugin_mode: str, workdir: str,
-                 with_shim: bool, ref_spec: str | None = None, hbm_dir: str | None = None):
+                 with_shim: bool, ref_spec: str | None = None, hbm_dir: str | None = None,
+                 comgr_dir: str | None = None):
         from aliyun_gpushare_device_plugin_amd.sim.cluster import SimCluster
 
         self.n = n_gpus
@@ -315,6 +320,8 @@ class ControlPlane:
         if hbm_dir:
             # the plugin grants every pod its broker granules while it prepares the pod's answer
             extra += ["--hbm-broker-dir", hbm_dir]
+        if comgr_dir:
+            extra += ["--comgr-cache-dir", comgr_dir]       # the init container's cache, read-only in pods
         nodes = [(MAIN_NODE, smi_spec)]
         overrides = {}
         # the reference's cost model (LIST per Allocate + synchronous PATCH, allocate.go:63-152)
@@ -1087,7 +1094,10 @@ def child_run(a, steps: int, *flags: str, tenant_stop: str | None = None, zygote
     cmd = [sys.executable, os.path.abspath(__file__), "--gpus", "1", "--steps", str(steps), "--warmup", "1",
            "--compare-rtts", "", "--fill-orders", "", "--no-ref-churn", "--driver-path-steps", "0",
            "--comparator-steps", "0", "--gemm", str(a.gemm), "--fill", str(a.fill), "--standby", str(a.standby),
-           "--tenant-stop", stop, "--json-out", out, *flags]
+           "--tenant-stop", stop, "--json-out", out]
+    if a.comgr_cache and a.comgr_cache_dir:
+        cmd += ["--comgr-cache-dir", a.comgr_cache_dir]     # the same sealed cache (flags may turn it off)
+    cmd += list(flags)
     if (a.no_pod_zygote if zygote is None else not zygote):
         cmd.append("--no-pod-zygote")
     t0 = time.perf_counter()
@@ -1196,6 +1206,7 @@ def main():
     smi = a.smi_backend or ("auto" if use_gpu else f"fake:{n}x288G")
     cp = None
     info = None
+    comgr_info = {"prefilled": True} if a.comgr_cache_dir else None
     workdir = tempfile.mkdtemp(prefix="gs-bench-", dir="/tmp")
     if rank == 0:
         ref_spec = smi if smi.startswith("fake:") else None
@@ -1205,8 +1216,20 @@ def main():
                 # every rank bound its plugin GPU above (bind_device), so the node has >= n GPUs
                 ref_spec = f"fake:{n}x{s.device(0).vram_total}B"
         hbm_dir = tempfile.mkdtemp(prefix="gs-hbm-", dir="/tmp") if (use_gpu or stub) and a.hbm_broker else None
+        if use_gpu and a.comgr_cache and not a.comgr_cache_dir:
+            # what the DaemonSet's comgr-cache init container does before the plugin starts
+            from aliyun_gpushare_device_plugin_amd.quota import comgr_cache
+
+            cdir = tempfile.mkdtemp(prefix="gs-comgr-", dir="/tmp")
+            t_c = time.perf_counter()
+            w = comgr_cache.warm(cdir, ("system", "torch"), device=ordinal)
+            comgr_cache.seal(cdir)
+            a.comgr_cache_dir = cdir
+            comgr_info = {"files": w["files"], "bytes": w["bytes"], "fill_s": round(time.perf_counter() - t_c, 2),
+                          "runtimes": {k: bool(v.get("ok")) for k, v in w["runtimes"].items()}}
         cp = ControlPlane(n, smi, a.pod_source, a.plugin_mode, workdir, with_shim=use_gpu or bool(stub),
-                          ref_spec=None if a.no_ref_churn else ref_spec, hbm_dir=hbm_dir)
+                          ref_spec=None if a.no_ref_churn else ref_spec, hbm_dir=hbm_dir,
+                          comgr_dir=a.comgr_cache_dir if use_gpu and a.comgr_cache else None)
         info = {"units_per_gpu": cp.units_per_gpu, "gpu_count": cp.gpu_count, "hbm_dir": hbm_dir}
     info = bcast(info)
     units = info["units_per_gpu"]
@@ -1454,6 +1477,7 @@ def main():
                        "standby_interpreters_per_gpu": a.standby,
                        "standby_forked_from_zygote": not a.no_pod_zygote,
                        "tenant_stop": a.tenant_stop,
+                       "comgr_cache": comgr_info if a.comgr_cache and use_gpu else False,
                        # the plugin's gRPC server and the simulated kubelet's Allocate client
                        "grpc_server": "native" if native_server.available() else "python",
                        "kubelet_client": "native" if NativeUnaryClient.wanted() else "grpcio"},
@@ -1569,6 +1593,9 @@ def main():
                 if stop != a.tenant_stop:
                     res[key] = child_run(a, a.comparator_steps, tenant_stop=stop)
             res["no_pod_zygote"] = child_run(a, a.comparator_steps, zygote=False)
+            if a.comgr_cache:
+                # the same churn with every pod compiling its blit kernels itself
+                res["no_comgr_cache"] = child_run(a, a.comparator_steps, "--no-comgr-cache")
         line = json.dumps(res)
         print(line, flush=True)
         if a.json_out:

@@ -8,6 +8,7 @@ Targets
   hbmbroker gpushare-hbm-broker     (C++17 per-GPU HBM broker daemon over HIP VMM, host only)
   kernels   libgpushare_kernels.so   (hand-written HIP/CDNA4 kernels, hipcc --offload-arch=gfx950)
   probes    shim_probe               (HIP test helper run under the quota shim on hardware)
+  comgrwarm gpushare-comgr-warm      (the system HIP runtime's first-stream work: fills the node's comgr cache)
 
 Usage: python native/build.py [targets...] [--force] [--asan | --sanitize {asan,tsan}] [-j N]
 The build is incremental (mtime based) so ``__graft_entry__.build()`` stays cheap.
@@ -225,9 +226,21 @@ def build_probes(force=False, asan=False):
     return out
 
 
+def build_comgrwarm(force=False, asan=False):
+    """gpushare-comgr-warm (native/comgrwarm): the first-stream work of a HIP process against the
+    system runtime, run by the DaemonSet's init container to fill the node's comgr cache."""
+    src = os.path.join(_src("comgrwarm"), "comgr_warm.cpp")
+    exe = os.path.join(OUT, "gpushare-comgr-warm")
+    if asan or not os.path.isfile(src):
+        return []
+    if force or _newer(exe, [src]):
+        _run([HIPCC, "-std=c++17", "-O2", f"--offload-arch={ARCH}", "-o", exe, src])
+    return [exe]
+
+
 TARGETS = {"gpuinfo": build_gpuinfo, "hipshim": build_hipshim, "dpserver": build_dpserver,
            "hbmbroker": build_hbmbroker, "kernels": build_kernels,
-           "probes": build_probes}
+           "probes": build_probes, "comgrwarm": build_comgrwarm}
 
 
 def build(targets=None, force=False, asan=False, jobs=4):
