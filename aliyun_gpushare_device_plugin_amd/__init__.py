@@ -41,4 +41,24 @@ def _lifeline() -> None:
         _os._exit(0)
 
 
+def _cpus() -> None:
+    """``GPUSHARE_CPUS=3,7-8``: run this process on those CPUs (set here, before any thread
+    starts, so every thread keeps it). A node's daemons on CPUs of their own — the kubelet's
+    ``reservedSystemCPUs`` — keep the plugin's watch and Allocate path off the cores pod start-ups
+    saturate (sim/cluster.py ``daemon_cpus``, bench.py ``--reserved-cpus``)."""
+    spec = _os.environ.pop("GPUSHARE_CPUS", None)
+    if not spec:
+        return
+    cpus = set()
+    for part in spec.split(","):
+        lo, _, hi = part.partition("-")
+        if lo.strip():
+            cpus.update(range(int(lo), int(hi or lo) + 1))
+    try:
+        _os.sched_setaffinity(0, cpus)
+    except (OSError, ValueError):
+        pass
+
+
 _lifeline()
+_cpus()

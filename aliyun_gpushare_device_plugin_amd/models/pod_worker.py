@@ -118,6 +118,13 @@ def _arena_release():
 
 
 def _nice() -> None:
+    cpus = os.environ.get("GS_POD_CPUS", "")
+    if cpus:
+        # the node's pod CPUs: the ones its daemons do not have reserved (kubelet reservedSystemCPUs)
+        try:
+            os.sched_setaffinity(0, {int(c) for c in cpus.split(",") if c})
+        except (OSError, ValueError):
+            pass
     nice = int(os.environ.get("GS_POD_NICE", "0") or 0)
     if nice > 0:
         # a node runs its daemons (kubelet, device plugin) ahead of container workloads

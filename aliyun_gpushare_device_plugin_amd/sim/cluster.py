@@ -60,8 +60,11 @@ class SimCluster:
                  extra_plugin_args: list[str] | None = None, apiserver: str = "thread",
                  preferred_allocation: bool = False, compute_isolation: str = "none", kubelet: str = "thread",
                  placement_truth: bool = True, node_overrides: dict | None = None,
-                 admission_identity: bool = True, grpc_server: str = "auto"):
+                 admission_identity: bool = True, grpc_server: str = "auto", daemon_cpus: dict | None = None):
         self.node_specs = nodes
+        # process-mode children's CPUs, by role ("plugin", "apiserver", "kubelet": "3" / "6-7"), as a
+        # node reserves CPUs for its daemons (the package import applies GPUSHARE_CPUS)
+        self.daemon_cpus = dict(daemon_cpus or {})
         # kubelet: "thread" (FakeKubelet in this interpreter) or "process" (its own interpreter,
         # sim/kubelet_proc.py, so kubelet-side Allocate timing is not inflated by this process's GIL)
         self.kubelet_mode = kubelet
@@ -107,14 +110,15 @@ class SimCluster:
         self.api_proc = subprocess.Popen(
             [sys.executable, "-m", "aliyun_gpushare_device_plugin_amd.sim.apiserver", "--port", "0",
              "--latency-ms", str(self.apiserver_latency_s * 1e3)],
-            env=self._child_env(), stdout=subprocess.PIPE, text=True)
+            env=self._child_env("apiserver"), stdout=subprocess.PIPE, text=True)
         self.api_url = self.api_proc.stdout.readline().strip()
         if not self.api_url.startswith("http"):
             raise RuntimeError("fake apiserver process failed to start")
 
-    @staticmethod
-    def _child_env():
+    def _child_env(self, role: str = ""):
         env = dict(os.environ)
+        if self.daemon_cpus.get(role):
+            env["GPUSHARE_CPUS"] = str(self.daemon_cpus[role])
         env.setdefault("GPUSHARE_DEBUG", "1")      # simulator children: debug endpoints on
         # SIGTERM the child when the simulator dies (a killed test or bench leaves no fake
         # apiserver / kubelet / plugin behind); armed by the package import, after exec
@@ -130,7 +134,7 @@ class SimCluster:
             self.client.create_node(make_node(name))
             pdir = os.path.join(self.workdir, name)
             if self.kubelet_mode == "process" and self.pod_source != "kubelet":
-                kl = KubeletProcess(pdir, self.api_url, name, env=self._child_env()).start()
+                kl = KubeletProcess(pdir, self.api_url, name, env=self._child_env("kubelet")).start()
             else:
                 kl = FakeKubelet(pdir, APIClient(KubeConfig(self.api_url)), name).start()
                 if self.pod_source == "kubelet":
@@ -212,7 +216,8 @@ class SimCluster:
                 args += ["--" + k.replace("_", "-"), str(v)]
             ov = self.node_overrides.get(node.name, {})
             args += ov["extra_args"] if "extra_args" in ov else self.extra_plugin_args
-            node.proc = subprocess.Popen(args, env=self._child_env(), stdout=subprocess.DEVNULL,
+            role = f"plugin:{node.name}" if f"plugin:{node.name}" in self.daemon_cpus else "plugin"
+            node.proc = subprocess.Popen(args, env=self._child_env(role), stdout=subprocess.DEVNULL,
                                          stderr=open(os.path.join(self.workdir, f"{node.name}.plugin.log"), "w"))
         else:
             node.manager = SharedGPUManager(self._thread_cfg(node), client=APIClient(KubeConfig(self.api_url)))

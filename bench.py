@@ -45,6 +45,7 @@ import json
 import os
 import queue
 import subprocess
+import tempfile
 import sys
 import threading
 import time
@@ -118,6 +119,13 @@ def parse():
                     help="the DaemonSet's comgr cache (quota/comgr_cache.py): filled before the plugin starts, as its "
                          "init container does, and mounted read-only into every pod (--comgr-cache-dir)")
     ap.add_argument("--comgr-cache-dir", default=None, help="an already filled cache to use (the comparators' runs)")
+    ap.add_argument("--reserved-cpus", type=int, default=0,
+                    help="CPUs reserved for the device plugin, as a node reserves CPUs for its daemons (the kubelet's "
+                         "reservedSystemCPUs): its watch threads and the native server's connection threads run there, "
+                         "pod processes on the others; the simulated kubelet / apiserver are not pinned (0 = no "
+                         "reservation, the default: on the test boxes, where a CPU quota and not a cpuset bounds the "
+                         "job, 2 pinned CPUs cut the Allocates that wait for the watch to 1-2 of 20 but added one "
+                         "0.9-5.8 ms transport stall per run, profiles/r6/allocate_tail.md)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -306,7 +314,7 @@ class ControlPlane:
 
     def __init__(self, n_gpus: int, smi_spec: str, pod_source: str, plugin_mode: str, workdir: str,
                  with_shim: bool, ref_spec: str | None = None, hbm_dir: str | None = None,
-                 comgr_dir: str | None = None):
+                 comgr_dir: str | None = None, daemon_cpus: dict | None = None):
         from aliyun_gpushare_device_plugin_amd.sim.cluster import SimCluster
 
         self.n = n_gpus
@@ -336,7 +344,7 @@ class ControlPlane:
         self.cluster = SimCluster(nodes, plugin_mode=plugin_mode, pod_source=pod_source,
                                   apiserver="process", kubelet="process", gpu_indices=list(range(n_gpus)), health_poll_s=5.0,
                                   extra_plugin_args=extra, shim_host_dir=NATIVE if with_shim else None,
-                                  node_overrides=overrides)
+                                  node_overrides=overrides, daemon_cpus=daemon_cpus)
         self.cluster.start()
         from aliyun_gpushare_device_plugin_amd import const
         from aliyun_gpushare_device_plugin_amd.cluster import objects as O
@@ -763,6 +771,8 @@ class _Zygote:
 
 
 class PodFleet:
+    pod_cpus = ""          # GS_POD_CPUS for every pod process (cpu_split)
+
     """The pod processes of this rank's GPU, plus one standby process (interpreter up, torch
     imported, GPU untouched) that becomes the next admitted pod."""
 
@@ -823,6 +833,8 @@ class PodFleet:
         pre = ":".join(x for x in (os.path.join(NATIVE, "libgpushare_hipquota.so"), os.environ.get("LD_PRELOAD", "")) if x)
         env = dict(os.environ, LD_PRELOAD=pre,
                    PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""), GS_POD_NICE="5")
+        if PodFleet.pod_cpus:
+            env["GS_POD_CPUS"] = PodFleet.pod_cpus       # not the CPUs reserved for the node's daemons
         for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
                   "TORCHELASTIC_RUN_ID", "GROUP_RANK", "ROLE_RANK"):
             env.pop(k, None)
@@ -876,6 +888,10 @@ class PodFleet:
         if not self.visible_by_uuid:                    # modelled node (fake SMI): this rank's GPU
             env.pop("ROCR_VISIBLE_DEVICES", None)
             env["HIP_VISIBLE_DEVICES"] = str(self.ordinal)
+        # a fresh container's own, empty cache home: comgr keeps what a process compiles under
+        # $XDG_CACHE_HOME by default, which pods of one image never share (their blit kernels come
+        # from the node's read-only comgr cache when the plugin mounts one, --comgr-cache-dir)
+        env["XDG_CACHE_HOME"] = tempfile.mkdtemp(prefix="gs-pod-home-", dir="/tmp")
         from aliyun_gpushare_device_plugin_amd import const
 
         # with an HBM broker the plugin granted the pod its granules while it prepared the answer:
@@ -1083,6 +1099,17 @@ class StubFleet:
             self.stop(uid)
 
 
+def cpu_split(n_reserved: int) -> tuple[dict | None, str]:
+    """The node's CPU split (``--reserved-cpus``): daemons' CPUs by role (SimCluster
+    ``daemon_cpus``) and the pods' CPUs (GS_POD_CPUS), from this process's allowed set."""
+    allowed = sorted(os.sched_getaffinity(0))
+    if n_reserved <= 0 or len(allowed) < n_reserved + 4:
+        return None, ""
+    res = allowed[-n_reserved:]
+    return ({f"plugin:{MAIN_NODE}": ",".join(map(str, res))},
+            ",".join(map(str, allowed[:-n_reserved])))
+
+
 def child_run(a, steps: int, *flags: str, tenant_stop: str | None = None, zygote: bool | None = None) -> dict:
     """A short child run of this churn on 1 GPU with one thing changed (``flags``, the tenant's
     stop, fresh standby interpreters); its headline. The comparators of the line: each measured on
@@ -1094,7 +1121,7 @@ def child_run(a, steps: int, *flags: str, tenant_stop: str | None = None, zygote
     cmd = [sys.executable, os.path.abspath(__file__), "--gpus", "1", "--steps", str(steps), "--warmup", "1",
            "--compare-rtts", "", "--fill-orders", "", "--no-ref-churn", "--driver-path-steps", "0",
            "--comparator-steps", "0", "--gemm", str(a.gemm), "--fill", str(a.fill), "--standby", str(a.standby),
-           "--tenant-stop", stop, "--json-out", out]
+           "--tenant-stop", stop, "--json-out", out, "--reserved-cpus", str(a.reserved_cpus)]
     if a.comgr_cache and a.comgr_cache_dir:
         cmd += ["--comgr-cache-dir", a.comgr_cache_dir]     # the same sealed cache (flags may turn it off)
     cmd += list(flags)
@@ -1206,6 +1233,8 @@ def main():
     smi = a.smi_backend or ("auto" if use_gpu else f"fake:{n}x288G")
     cp = None
     info = None
+    daemon_cpus, pod_cpus = cpu_split(a.reserved_cpus) if use_gpu else (None, "")
+    PodFleet.pod_cpus = pod_cpus
     comgr_info = {"prefilled": True} if a.comgr_cache_dir else None
     workdir = tempfile.mkdtemp(prefix="gs-bench-", dir="/tmp")
     if rank == 0:
@@ -1229,7 +1258,8 @@ def main():
                           "runtimes": {k: bool(v.get("ok")) for k, v in w["runtimes"].items()}}
         cp = ControlPlane(n, smi, a.pod_source, a.plugin_mode, workdir, with_shim=use_gpu or bool(stub),
                           ref_spec=None if a.no_ref_churn else ref_spec, hbm_dir=hbm_dir,
-                          comgr_dir=a.comgr_cache_dir if use_gpu and a.comgr_cache else None)
+                          comgr_dir=a.comgr_cache_dir if use_gpu and a.comgr_cache else None,
+                          daemon_cpus=daemon_cpus)
         info = {"units_per_gpu": cp.units_per_gpu, "gpu_count": cp.gpu_count, "hbm_dir": hbm_dir}
     info = bcast(info)
     units = info["units_per_gpu"]
@@ -1478,6 +1508,7 @@ def main():
                        "standby_forked_from_zygote": not a.no_pod_zygote,
                        "tenant_stop": a.tenant_stop,
                        "comgr_cache": comgr_info if a.comgr_cache and use_gpu else False,
+                       "reserved_cpus": {"daemons": daemon_cpus, "pods": pod_cpus} if daemon_cpus else None,
                        # the plugin's gRPC server and the simulated kubelet's Allocate client
                        "grpc_server": "native" if native_server.available() else "python",
                        "kubelet_client": "native" if NativeUnaryClient.wanted() else "grpcio"},

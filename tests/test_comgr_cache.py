@@ -111,7 +111,10 @@ print(json.dumps({"first_stream_ms": ms, "ok": float(y.sum()) == 2.0 * (1 << 20)
 
 
 def _pod(cache_dir):
-    env = dict(os.environ)
+    import tempfile
+
+    # a fresh container: comgr's own default cache ($XDG_CACHE_HOME/comgr) starts empty
+    env = dict(os.environ, XDG_CACHE_HOME=tempfile.mkdtemp(prefix="pod-home-"))
     env.pop("AMD_COMGR_CACHE", None)
     env.pop("AMD_COMGR_CACHE_DIR", None)
     if cache_dir:
