@@ -775,6 +775,7 @@ class Allocator(NativeTable):
                 r.mounts.add(container_path=const.HBM_BROKER_CONTAINER_DIR, host_path=self._hbm.mount_dir(gpu_index),
                              read_only=True)
                 r.envs[const.ENV_HBM_BROKER] = self._hbm.container_socket(gpu_index)
+                r.envs[const.ENV_HIP_FORCE_DEV_KERNARG] = "0"
         if self.opts.comgr_cache_dir and not self.opts.disable_cgpu:
             # code objects the runtime would build with comgr at the container's first stream:
             # from the cache the DaemonSet's init container filled; read-only, so no pod can put

@@ -69,6 +69,10 @@ LEDGER_CONTAINER_DIR = "/run/gpushare/ledger"
 ENV_HBM_BROKER = "GPUSHARE_HBM_BROKER"
 ENV_HBM_TOKEN = "GPUSHARE_HBM_TOKEN"
 HBM_BROKER_CONTAINER_DIR = "/run/gpushare/hbm"
+# kernel arguments in host memory for a pod on broker memory: with the runtime's default (copied
+# into device memory) a hipGraph decode next to a neighbour on broker memory kept 9 % of its solo
+# rate, 22 % with this, and solo decode is not slower (profiles/r6/colocate_llama3_8b_x2_broker.json)
+ENV_HIP_FORCE_DEV_KERNARG = "HIP_FORCE_DEV_KERNARG"
 # the node's trusted comgr cache (quota/comgr_cache.py): code objects the HIP runtimes build at a
 # process's first stream, compiled once by the DaemonSet's init container and mounted read-only
 ENV_COMGR_CACHE = "AMD_COMGR_CACHE"

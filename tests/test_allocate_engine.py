@@ -659,6 +659,7 @@ def test_hbm_broker_grant_rides_in_the_prepared_answer(tmp_path):
         assert got == want
         tok = got.envs[const.ENV_HBM_TOKEN]
         assert got.envs[const.ENV_HBM_BROKER] == f"{const.HBM_BROKER_CONTAINER_DIR}/hbm1.sock"
+        assert got.envs[const.ENV_HIP_FORCE_DEV_KERNARG] == "0"     # (hipGraph next to a broker neighbour)
         mounts = [m for m in got.mounts if m.container_path == const.HBM_BROKER_CONTAINER_DIR]
         assert len(mounts) == 1 and mounts[0].host_path == str(hdir / "gpu1") and mounts[0].read_only
         # 16 of 64 GiB -> a 16 GiB quota; 94 % of it in whole granules = 15 GiB, granted once
