@@ -75,15 +75,25 @@ def _device_memory_back():
     yield
 
 
-def _full(b, timeout=60.0):
+def _full(b, timeout=60.0, slack=0):
     """Start-up completes when the broker holds its full size: right after another test, amdgpu
-    may still be wiping that test's memory, and the broker takes it as it comes back (grow)."""
+    may still be wiping that test's memory, and the broker takes it as it comes back (grow).
+    ``slack``: a broker sized for the whole GPU may stay up to that many granules short, held by
+    this pytest process's own runtime after the other GPU tests ran in it; it is done once it has
+    stopped growing for 3 s."""
     deadline = time.time() + timeout
     st = b.stat()
-    while (st["granules"] < st["granules_max"] or st["scrubbing"]) and time.time() < deadline:
+    last, since = st["granules"], time.time()
+    while time.time() < deadline:
+        if st["granules"] != last:
+            last, since = st["granules"], time.time()
+        done = st["granules"] == st["granules_max"] or (st["granules"] >= st["granules_max"] - slack
+                                                        and time.time() - since > 3.0)
+        if done and not st["scrubbing"]:
+            break
         time.sleep(0.2)
         st = b.stat()
-    assert st["granules"] == st["granules_max"], st
+    assert st["granules"] >= st["granules_max"] - slack, st
     return b
 
 
@@ -586,7 +596,7 @@ def test_every_pod_fills_97_percent_of_its_quota_at_the_daemonset_sizing(tmp_pat
     b.start()
     procs = []
     try:
-        _full(b, timeout=120)
+        _full(b, timeout=120, slack=4)
         st0 = b.stat()
         quotas = [32, 64, 64, 128]
         for i, q in enumerate(quotas):
@@ -657,8 +667,8 @@ def test_a_cgpu_disabled_node_leaves_the_whole_gpu_to_the_driver(tmp_path):
     b = HBMBroker(str(tmp_path / "hbm.sock"), device=0, gib=None, reserve_gib=12, wait_s=30)
     b.start()
     try:
-        _full(b, timeout=120)
-        full = b.stat()["granules_max"]
+        _full(b, timeout=120, slack=4)
+        full = b.stat()["granules"]
         assert b.size(0) == (0, 0)
         st = b.stat()
         assert st["granules"] == 0 and st["given_back"] >= full
