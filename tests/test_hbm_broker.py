@@ -679,11 +679,11 @@ def test_a_cgpu_disabled_node_leaves_the_whole_gpu_to_the_driver(tmp_path):
         print(json.dumps({"plain_pod": out, "broker": {k: st[k] for k in ("granules", "target", "given_back")}}))
         assert out["gib"] == 200
         held, target = b.size("max")
-        assert target == full
-        deadline = time.time() + 60
+        assert target == b.stat()["granules_max"]
+        deadline = time.time() + 60                       # back to what it held before the label
         while b.stat()["granules"] < full and time.time() < deadline:
             time.sleep(0.25)
-        assert b.stat()["granules"] == full
+        assert b.stat()["granules"] >= full
     finally:
         b.stop()
 
