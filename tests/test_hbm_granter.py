@@ -310,3 +310,5 @@ def test_bench_rehearsal_eight_ranks_with_stub_brokers(stub_runtime):
     # every pod started on every GPU (4 at the fill + the churn's replacements) had its arena
     assert d["stub_pods_with_arena_by_gpu"] == {str(i): 4 + d["admissions_by_gpu"][str(i)] for i in range(8)}
     assert d["quota_denials"] == 0
+    # the line explains itself per GPU: each GPU's broker STAT (above) and its Allocate p50
+    assert sorted(d["allocate_p50_ms_by_gpu"]) == [str(i) for i in range(8)]
