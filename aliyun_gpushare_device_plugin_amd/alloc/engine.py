@@ -222,6 +222,7 @@ class Allocator(NativeTable):
         self._prebind: dict[str, tuple] = {}
         # per-pod timeline of the fast path, CLOCK_MONOTONIC ns (native_table.py ``pod_trace``)
         self._ptrace: dict[str, dict] = {}
+        self._ptrace_mu = threading.Lock()
         self._tmpl_bytes: dict[tuple, bytes] = {}                          # _prepared
         self.native_rotate_bytes = 16 << 20       # rotate the native journal file past this
         self.native_prep_keep = 4096              # prepared answers kept for native claims past the current table

@@ -236,21 +236,26 @@ class NativeTable:
         its entry is in the table), ``bind_seen`` / ``bind_pub`` (the pod watch delivered the bind;
         the table has it as bound), ``tab`` (a full rebuild published it), ``alloc_in`` (its
         Allocate reached the server) and the server's waits."""
-        tr = self._ptrace.get(u)
-        if tr is None:
-            tr = self._ptrace[u] = {}
-            while len(self._ptrace) > self.PTRACE_KEEP:
-                self._ptrace.pop(next(iter(self._ptrace)), None)
-        if key not in tr:
-            tr[key] = t if t is not None else time.monotonic_ns()
-            if t is None and key in self.PTRACE_CPU:
-                tr[key + "_cpu_ns"] = time.thread_time_ns()   # this thread's CPU time: wall - cpu = waits
+        now = t if t is not None else time.monotonic_ns()
+        cpu = time.thread_time_ns() if t is None and key in self.PTRACE_CPU else None
+        with self._ptrace_mu:             # (the watch threads, the claim reader, the metrics endpoint)
+            tr = self._ptrace.get(u)
+            if tr is None:
+                tr = self._ptrace[u] = {}
+                while len(self._ptrace) > self.PTRACE_KEEP:
+                    self._ptrace.pop(next(iter(self._ptrace)), None)
+            if key not in tr:
+                tr[key] = now
+                if cpu is not None:
+                    tr[key + "_cpu_ns"] = cpu    # this thread's CPU time: wall - cpu = waits
 
     def pod_trace(self) -> list[dict]:
         """The last pods' timelines, in ms relative to their Allocate's arrival (pods whose
         Allocate came), oldest first."""
         out = []
-        for u, tr in list(self._ptrace.items()):
+        with self._ptrace_mu:
+            items = [(u, dict(tr)) for u, tr in self._ptrace.items()]
+        for u, tr in items:
             t0 = tr.get("alloc_in")
             if t0 is None:
                 continue

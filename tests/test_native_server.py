@@ -1178,3 +1178,37 @@ def test_grpc_go_wire_replay(tmp_path):
     finally:
         srv.stop()
         al.close()
+
+
+def test_the_pod_timeline_takes_marks_from_every_thread(tmp_path):
+    """The timeline is written by the watch threads, the claim reader and the cache hook, and read
+    by the metrics endpoint: concurrent marks past its bound and reads never raise."""
+    srv, al, src = _server(tmp_path)
+    try:
+        errs = []
+
+        def writer(k):
+            try:
+                for i in range(3000):
+                    al._mark(f"p{k}-{i}", "pre_seen")
+                    al._mark(f"p{k}-{i}", "alloc_in", time.monotonic_ns())
+            except Exception as e:  # noqa: BLE001
+                errs.append(e)
+
+        def reader():
+            try:
+                for _ in range(300):
+                    al.pod_trace()
+            except Exception as e:  # noqa: BLE001
+                errs.append(e)
+
+        ts = [threading.Thread(target=writer, args=(k,)) for k in range(4)] + [threading.Thread(target=reader)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(60)
+        assert not errs and len(al._ptrace) <= al.PTRACE_KEEP
+        assert all("alloc_in_abs" in r for r in al.pod_trace())
+    finally:
+        srv.stop()
+        al.close()
