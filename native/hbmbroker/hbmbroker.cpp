@@ -318,11 +318,24 @@ struct Broker {
       h[i] = nullptr;
       return false;
     }
-    CK(hipMemExportToShareableHandle(&fds[i], h[i], hipMemHandleTypePosixFileDescriptor, 0));
-    CK(hipMemAddressReserve(reinterpret_cast<void**>(&va[i]), gran, 0, nullptr, 0));
-    CK(hipMemMap(va[i], gran, 0, h[i], 0));
+    // a step that fails undoes the ones before it: the broker keeps running without this granule
+    // (a transient shortage of address space or of the runtime's bookkeeping), grow() retries later
     hipMemAccessDesc d = rw();
-    CK(hipMemSetAccess(va[i], gran, &d, 1));
+    bool mapped = false;
+    hipError_t e = hipMemExportToShareableHandle(&fds[i], h[i], hipMemHandleTypePosixFileDescriptor, 0);
+    if (e == hipSuccess) e = hipMemAddressReserve(reinterpret_cast<void**>(&va[i]), gran, 0, nullptr, 0);
+    if (e == hipSuccess) e = hipMemMap(va[i], gran, 0, h[i], 0), mapped = e == hipSuccess;
+    if (e == hipSuccess) e = hipMemSetAccess(va[i], gran, &d, 1);
+    if (e != hipSuccess) {
+      std::fprintf(stderr, "gpushare-hbm-broker: granule %d not added: %s\n", i, hipGetErrorString(e));
+      (void)hipGetLastError();
+      if (mapped) (void)hipMemUnmap(va[i], gran);
+      if (va[i]) (void)hipMemAddressFree(va[i], gran), va[i] = nullptr;
+      (void)hipMemRelease(h[i]);
+      h[i] = nullptr;
+      if (fds[i] >= 0) close(fds[i]), fds[i] = -1;
+      return false;
+    }
     present[i] = 1;
     return true;
   }
