@@ -18,18 +18,23 @@ from aliyun_gpushare_device_plugin_amd.sim.cluster import SimCluster
 SERVERS = ["python", "native"]    # grpcio + the engine's fast path; libgpushare_dpserver's table
 
 
-def _settle(al, timeout=5.0):
+def _settle(al, timeout=5.0, quiet=0.1):
     """Wait until the prepared answers match the pod cache (the engine's own table, or the one
-    published to the native server)."""
+    published to the native server) and the cache has not changed for ``quiet`` seconds (the fake
+    kubelet's own status updates of a just-bound pod come in after the bind)."""
     t = time.monotonic() + timeout
+    since, seen = time.monotonic(), None
     while time.monotonic() < t:
+        v = al.pods.pending_version
+        if v != seen:
+            since, seen = time.monotonic(), v
         if al.native is not None:
-            if al._published == (al.pods.pending_version, al._gen):
-                return True
+            current = al._published == (v, al._gen)
         else:
             f = al._fast
-            if f is not None and f.version == al.pods.pending_version and f.gen == al._gen:
-                return True
+            current = f is not None and f.version == v and f.gen == al._gen
+        if current and time.monotonic() - since >= quiet:
+            return True
         time.sleep(0.005)
     return False
 
