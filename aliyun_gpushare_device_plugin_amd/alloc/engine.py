@@ -777,10 +777,11 @@ class Allocator(NativeTable):
                              read_only=True)
                 r.envs[const.ENV_HBM_BROKER] = self._hbm.container_socket(gpu_index)
                 r.envs[const.ENV_HIP_FORCE_DEV_KERNARG] = "0"
-        if self.opts.comgr_cache_dir and not self.opts.disable_cgpu:
+        if self.opts.comgr_cache_dir and not self.opts.disable_cgpu and os.path.isdir(self.opts.comgr_cache_dir):
             # code objects the runtime would build with comgr at the container's first stream:
             # from the cache the DaemonSet's init container filled; read-only, so no pod can put
-            # code into another pod's runtime (a miss compiles as without the cache)
+            # code into another pod's runtime (a miss compiles as without the cache). A directory
+            # that is not there (no init container ran) is not mounted: the container would not start
             r.mounts.add(container_path=const.COMGR_CACHE_CONTAINER_DIR, host_path=self.opts.comgr_cache_dir,
                          read_only=True)
             r.envs[const.ENV_COMGR_CACHE] = "1"

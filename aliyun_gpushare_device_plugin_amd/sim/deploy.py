@@ -83,12 +83,14 @@ def _rewrite(value: str, mounts: dict) -> str:
 
 def resolve(doc: dict, host_root: str, field_refs: dict, overrides: dict, skip_volumes=(),
             container: str | None = None) -> Container:
-    """A container of a DaemonSet / Deployment (the first, or the one named ``container``):
+    """A container of a DaemonSet / Deployment (the first, or the one named ``container``, which
+    may be an init container):
     command with hostPath volumes mapped under ``host_root`` (one directory per volume, shared by
     the pod's containers as a hostPath is), env with downward-API ``fieldRef`` values from
     ``field_refs``, and ``overrides`` ({flag: value or None to drop}) applied to the flags."""
     spec = pod_template(doc)["spec"]
-    c = spec["containers"][0] if container is None else next(x for x in spec["containers"] if x["name"] == container)
+    c = spec["containers"][0] if container is None else next(
+        x for x in spec["containers"] + spec.get("initContainers", []) if x["name"] == container)
     vols = {v["name"]: v for v in spec.get("volumes", [])}
     mounts = {}
     for m in c.get("volumeMounts", []):

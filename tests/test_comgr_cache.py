@@ -37,13 +37,17 @@ def _answer(tmp_path, **opts):
 
 
 def test_the_answer_mounts_the_cache_read_only(tmp_path):
-    r = _answer(tmp_path, comgr_cache_dir="/var/lib/gpushare/comgr-cache")
+    cache = tmp_path / "comgr-cache"
+    cache.mkdir()
+    r = _answer(tmp_path, comgr_cache_dir=str(cache))
     m = [x for x in r.mounts if x.container_path == const.COMGR_CACHE_CONTAINER_DIR]
-    assert len(m) == 1 and m[0].host_path == "/var/lib/gpushare/comgr-cache" and m[0].read_only
+    assert len(m) == 1 and m[0].host_path == str(cache) and m[0].read_only
     assert r.envs[const.ENV_COMGR_CACHE] == "1"
     assert r.envs[const.ENV_COMGR_CACHE_DIR] == const.COMGR_CACHE_CONTAINER_DIR
-    # off unless configured, and off on a cgpu-disabled node (its pods get nothing of the plugin's)
-    for r in (_answer(tmp_path), _answer(tmp_path, comgr_cache_dir="/x", disable_cgpu=True)):
+    # off unless configured, off on a cgpu-disabled node (its pods get nothing of the plugin's), and
+    # off while the directory is not there (a hostPath mount of a missing path fails the container)
+    for r in (_answer(tmp_path), _answer(tmp_path, comgr_cache_dir=str(cache), disable_cgpu=True),
+              _answer(tmp_path, comgr_cache_dir=str(tmp_path / "missing"))):
         assert const.ENV_COMGR_CACHE not in r.envs
         assert not any(x.container_path == const.COMGR_CACHE_CONTAINER_DIR for x in r.mounts)
 

@@ -6,6 +6,7 @@ kube-scheduler's side follows the extender ConfigMap; the reference's bin-pack d
 module docstring of sim/deploy.py and asserted below to be nothing else."""
 import os
 import shutil
+import stat
 import subprocess
 import sys
 import tempfile
@@ -53,7 +54,15 @@ def test_shipped_manifests_run_a_node(hostroot, stub_runtime, native_shim):
         assert make_node(NODE)["metadata"]["labels"]["gpushare"] == "true"
         mport = D.free_port()
         overrides = {"--smi-backend": "fake:2x288G", "--metrics-addr": f"127.0.0.1:{mport}", "--apiserver": api.url}
+        # the init container first, to completion: it fills the comgr cache (no GPU here: nothing
+        # to warm) and seals it read-only where the plugin's flag names it
+        ict = D.resolve(ds, hostroot, {"spec.nodeName": NODE}, {}, container="comgr-cache")
+        init = D.start(ict, os.path.join(hostroot, "comgr-cache.log"))
+        assert init.wait(300) == 0, open(os.path.join(hostroot, "comgr-cache.log")).read()[-3000:]
+        cache = ict.host_path("/var/lib/gpushare/comgr-cache")
+        assert os.path.isdir(cache) and stat.S_IMODE(os.stat(cache).st_mode) == 0o555
         ct = D.resolve(ds, hostroot, {"spec.nodeName": NODE}, overrides, skip_volumes=("sys",))
+        assert f"--comgr-cache-dir={cache}" in ct.argv          # the same hostPath as the init container's
         # the kubelet socket directory is the binary's default (not written in the manifest): the
         # container sees it at that path through the device-plugin mount
         ct.argv.append("--device-plugin-dir=" + ct.host_path(const.DEVICE_PLUGIN_PATH))
@@ -151,6 +160,9 @@ def test_shipped_manifests_run_a_node(hostroot, stub_runtime, native_shim):
         assert mounts[const.HBM_BROKER_CONTAINER_DIR].host_path == hb.pod_dir(hdir, gi)   # its GPU's sockets only
         assert mounts[const.HBM_BROKER_CONTAINER_DIR].read_only
         assert not any(m.host_path.startswith(hb.admin_dir(hdir)) for m in r.mounts)
+        # the init container's comgr cache, read-only, with comgr pointed at it
+        assert mounts[const.COMGR_CACHE_CONTAINER_DIR].host_path == cache and mounts[const.COMGR_CACHE_CONTAINER_DIR].read_only
+        assert r.envs[const.ENV_COMGR_CACHE_DIR] == const.COMGR_CACHE_CONTAINER_DIR and r.envs[const.ENV_COMGR_CACHE] == "1"
         st = {}
         assert D.wait_for(lambda: st.update(hb.HBMBroker.attach(hb.pod_socket(hdir, gi), hb.admin_socket(hdir, gi))
                                             .list()) or tok in st.get("grants", {}), 30, 0.2), \
