@@ -267,6 +267,8 @@ struct Broker {
   // bandwidth with non-temporal stores; hipMemsetAsync when it is not there
   hipModule_t scrub_mod = nullptr;
   hipFunction_t scrub_fn = nullptr;
+  hipFunction_t scrub_n_fn = nullptr;  // gs_scrub_n: up to 8 ranges in one dispatch
+  unsigned long long scrub_dispatches = 0;
   std::string scrub_path;
   int count_max = 0;          // granules the broker is sized for (its address range)
   int target = 0;             // granules it may hold now (SIZE; count_max unless told otherwise)
@@ -295,8 +297,20 @@ struct Broker {
       (void)hipGetLastError();
       std::fprintf(stderr, "gpushare-hbm-broker: scrub kernel %s not loaded: zeroing with hipMemsetAsync\n",
                    scrub_path.c_str());
+      return;
+    }
+    if (hipModuleGetFunction(&scrub_n_fn, scrub_mod, "gs_scrub_n") != hipSuccess) {
+      scrub_n_fn = nullptr;  // an older code object: one dispatch per range
+      (void)hipGetLastError();
     }
   }
+
+  // the kernel argument of gs_scrub_n (scrub.hip ScrubSet)
+  struct ScrubSet {
+    void* p[8];
+    uint64_t n16[8];
+    uint32_t count;
+  };
 
   // zero [p, p + bytes) on the broker's stream
   void zero(char* p, size_t bytes) {
@@ -305,9 +319,30 @@ struct Broker {
       uint64_t blocks = std::min<uint64_t>(2048, (n16 + 255) / 256);  // 8 blocks of 4 waves per CU
       void* args[] = {&p, &n16};
       CK(hipModuleLaunchKernel(scrub_fn, unsigned(blocks), 1, 1, 256, 1, 1, 0, stream, args, nullptr));
+      ++scrub_dispatches;
       return;
     }
     CK(hipMemsetAsync(p, 0, bytes, stream));
+    ++scrub_dispatches;
+  }
+
+  // zero up to 8 ranges in one dispatch (gs_scrub_n), or one by one without it
+  void zero_ranges(char* const* p, const size_t* bytes, int count) {
+    bool ok = scrub_n_fn != nullptr && count > 1;
+    for (int k = 0; ok && k < count; ++k)
+      ok = bytes[k] % 16 == 0 && reinterpret_cast<uintptr_t>(p[k]) % 16 == 0;
+    if (!ok) {
+      for (int k = 0; k < count; ++k) zero(p[k], bytes[k]);
+      return;
+    }
+    ScrubSet s;
+    std::memset(&s, 0, sizeof s);
+    s.count = uint32_t(count);
+    for (int k = 0; k < count; ++k) s.p[k] = p[k], s.n16[k] = bytes[k] / 16;
+    unsigned blocks = 2048u / unsigned(count) * unsigned(count);  // a multiple of count: blocks per range equal
+    void* args[] = {&s};
+    CK(hipModuleLaunchKernel(scrub_n_fn, blocks, 1, 1, 256, 1, 1, 0, stream, args, nullptr));
+    ++scrub_dispatches;
   }
 
   // granule i: created, exported, mapped at a range of its own, readable and writable (not yet
@@ -519,12 +554,17 @@ struct Broker {
   // zero granules `s` (sorted) on the broker's stream: one launch per run of granules whose
   // ranges happen to be adjacent
   void zero_granules(const std::vector<int>& s) {
+    char* p[8];
+    size_t b[8];
+    int n = 0;
     for (size_t i = 0; i < s.size();) {
       size_t j = i + 1;
       while (j < s.size() && va[size_t(s[j])] == va[size_t(s[j - 1])] + gran) ++j;
-      zero(va[size_t(s[i])], gran * (j - i));
+      p[n] = va[size_t(s[i])], b[n] = gran * (j - i), ++n;
+      if (n == 8) zero_ranges(p, b, n), n = 0;
       i = j;
     }
+    if (n) zero_ranges(p, b, n);
   }
 
   // zero the granules on the broker's stream; they are lent again from reap_scrubs(), in chunks
@@ -830,14 +870,15 @@ struct Broker {
                   "\"releases\": %llu, \"refused\": %llu, \"revokes\": %llu, \"revoked\": %zu, \"timeouts\": %llu, "
                   "\"expired\": %llu, \"busy\": %llu, \"idle_dropped\": %llu, \"peer_refused\": %llu, "
                   "\"clients\": %zu, \"quarantined\": %zu, \"quarantined_total\": %llu, \"lost\": %llu, "
-                  "\"scrub_kernel\": \"%s\", \"release_policy\": \"%s\", \"quarantine_ms_last\": %.1f, \"quarantine_ms_max\": %.1f, \"held_refs_max\": %d, \"base_refs\": %d, \"scrubbed_bytes\": %llu, "
+                  "\"scrub_kernel\": \"%s\", \"scrub_dispatches\": %llu, \"release_policy\": \"%s\", \"quarantine_ms_last\": %.1f, \"quarantine_ms_max\": %.1f, \"held_refs_max\": %d, \"base_refs\": %d, \"scrubbed_bytes\": %llu, "
                   "\"scrub_ms_total\": %.3f, \"scrub_ms_last\": %.3f, \"setup_ms\": %.1f, \"loop_ms_max\": %.3f, "
                   "\"release_ms_max\": %.3f, \"scrub_enqueue_ms_max\": %.3f, \"take_wait_ms_last\": %.3f, "
                   "\"take_wait_ms_max\": %.3f, \"send_ms_max\": %.3f, \"last_send_at\": %.6f}\n",
                   boot.c_str(), device, gran, count, count_max, target, given_back, pressure_given, low_water_bytes,
                   extra, extends, extended, uncommitted(), ends, grown, free_list.size(), held, owed, streamed, more_msgs, scrub_n, waiting, grants.size(), takes,
                   releases, refused, revokes, revoked.size(), timeouts, expired, busy, idle_dropped, peer_refused,
-                  clients.size(), quarantined(), quarantined_total, lost, scrub_fn ? "gs_scrub" : "memset", policy_name(),
+                  clients.size(), quarantined(), quarantined_total, lost,
+                  scrub_n_fn ? "gs_scrub_n" : scrub_fn ? "gs_scrub" : "memset", scrub_dispatches, policy_name(),
                   quarantine_s_last * 1e3,
                   quarantine_s_max * 1e3, held_refs_max(),
                   base_refs.empty() ? -1 : base_refs[0], scrubbed_bytes, scrub_s_total * 1e3, scrub_s_last * 1e3,
