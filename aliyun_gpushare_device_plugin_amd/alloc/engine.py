@@ -221,8 +221,9 @@ class Allocator(NativeTable):
         # candidates already (native_table.py precompute / expire_prebind)
         self._prebind: dict[str, tuple] = {}
         # per-pod timeline of the fast path, CLOCK_MONOTONIC ns (native_table.py ``pod_trace``)
-        self._ptrace: dict[str, dict] = {}
-        self._ptrace_mu = threading.Lock()
+        self._ptrace: collections.OrderedDict = collections.OrderedDict()
+        # with each mark this thread's CPU time too (a syscall each): GPUSHARE_TRACE_CPU=1 (bench.py)
+        self._ptrace_cpu = os.environ.get("GPUSHARE_TRACE_CPU") == "1"
         self._tmpl_bytes: dict[tuple, bytes] = {}                          # _prepared
         self.native_rotate_bytes = 16 << 20       # rotate the native journal file past this
         self.native_prep_keep = 4096              # prepared answers kept for native claims past the current table

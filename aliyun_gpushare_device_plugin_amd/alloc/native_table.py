@@ -65,7 +65,10 @@ def _pb_varint(n: int) -> bytes:
 
 
 def _pb_ld(tag: int, b: bytes) -> bytes:
-    return bytes((tag,)) + _pb_varint(len(b)) + b
+    n = len(b)
+    if n < 0x80:                                      # (most fields: one length byte)
+        return bytes((tag, n)) + b
+    return bytes((tag,)) + _pb_varint(n) + b
 
 
 def _pb_map_entry(tag: int, k: str, v: str) -> bytes:
@@ -236,25 +239,27 @@ class NativeTable:
         its entry is in the table), ``bind_seen`` / ``bind_pub`` (the pod watch delivered the bind;
         the table has it as bound), ``tab`` (a full rebuild published it), ``alloc_in`` (its
         Allocate reached the server) and the server's waits."""
-        now = t if t is not None else time.monotonic_ns()
-        cpu = time.thread_time_ns() if t is None and key in self.PTRACE_CPU else None
-        with self._ptrace_mu:             # (the watch threads, the claim reader, the metrics endpoint)
-            tr = self._ptrace.get(u)
-            if tr is None:
-                tr = self._ptrace[u] = {}
-                while len(self._ptrace) > self.PTRACE_KEEP:
-                    self._ptrace.pop(next(iter(self._ptrace)), None)
-            if key not in tr:
-                tr[key] = now
-                if cpu is not None:
-                    tr[key + "_cpu_ns"] = cpu    # this thread's CPU time: wall - cpu = waits
+        # (the watch threads, the claim reader and the metrics endpoint share it: every step below
+        # is one operation of the ordered dict or the dict, so no lock is taken on the pre-bind path)
+        trace = self._ptrace
+        tr = trace.get(u)
+        if tr is None:
+            tr = trace.setdefault(u, {})
+            if len(trace) > self.PTRACE_KEEP:
+                try:
+                    trace.popitem(last=False)
+                except KeyError:
+                    pass
+        if key not in tr:
+            tr.setdefault(key, t if t is not None else time.monotonic_ns())
+            if t is None and self._ptrace_cpu and key in self.PTRACE_CPU:
+                tr.setdefault(key + "_cpu_ns", time.thread_time_ns())   # this thread's CPU time: wall - cpu = waits
 
     def pod_trace(self) -> list[dict]:
         """The last pods' timelines, in ms relative to their Allocate's arrival (pods whose
         Allocate came), oldest first."""
         out = []
-        with self._ptrace_mu:
-            items = [(u, dict(tr)) for u, tr in self._ptrace.items()]
+        items = [(u, dict(tr)) for u, tr in list(self._ptrace.items())]
         for u, tr in items:
             t0 = tr.get("alloc_in")
             if t0 is None:

@@ -36,7 +36,7 @@ class ShimConfig:
 
 def ledger_name(pod_uid: str, container_slot: int) -> str:
     """POSIX shm name shared by all processes of one container (quota is per container)."""
-    safe = "".join(ch for ch in pod_uid if ch.isalnum())[:40] or "anon"
+    safe = "".join(filter(str.isalnum, pod_uid))[:40] or "anon"
     return f"/gpushare-{safe}-{container_slot}"
 
 

@@ -1185,6 +1185,8 @@ def bind_device(smi_index: int) -> tuple[int, dict]:
 
 def main():
     a = parse()
+    # the plugin's per-pod timeline carries each pre-bind step's thread CPU time (pod_timeline)
+    os.environ.setdefault("GPUSHARE_TRACE_CPU", "1")
     n = a.gpus
     if "WORLD_SIZE" not in os.environ and n > 1:
         sys.exit(relaunch(n))
