@@ -787,6 +787,13 @@ class Allocator(NativeTable):
                          read_only=True)
             r.envs[const.ENV_COMGR_CACHE] = "1"
             r.envs[const.ENV_COMGR_CACHE_DIR] = const.COMGR_CACHE_CONTAINER_DIR
+            if (shim is not None and shim.enabled
+                    and os.path.exists(os.path.join(shim.host_dir, const.COMGR_ACTION_LIB_NAME))):
+                # the rest of the runtime's compile from the same cache (native/comgrcache),
+                # preloaded from the shim's directory after the shim
+                r.envs[const.ENV_LD_PRELOAD] = shim.container_lib + ":" + os.path.join(
+                    shim.container_dir, const.COMGR_ACTION_LIB_NAME)
+                r.envs[const.ENV_COMGR_ACTION_CACHE] = const.COMGR_CACHE_CONTAINER_DIR
         return r
 
     def _plan_slots(self, claim: _Claim, pod_units: int) -> cuslots.SlotRun | None:

@@ -180,13 +180,20 @@ def install_shim(dest_dir: str) -> str:
 
     from ..utils.native import ensure_built
 
-    src = ensure_built("hipshim")
+    from ..utils.native import NativeUnavailable
+
+    libs = [(ensure_built("hipshim"), const.SHIM_LIB_NAME)]
+    try:      # the comgr action cache goes next to it (answers preload it when the cache is mounted)
+        libs.append((ensure_built("comgrcache"), const.COMGR_ACTION_LIB_NAME))
+    except NativeUnavailable as e:
+        log.warning("comgr action cache not installed: %s", e)
     os.makedirs(dest_dir, exist_ok=True)
-    fd, tmp = tempfile.mkstemp(dir=dest_dir, prefix=".shim-")
-    os.close(fd)
-    shutil.copyfile(src, tmp)
-    os.chmod(tmp, 0o755)
-    os.replace(tmp, os.path.join(dest_dir, const.SHIM_LIB_NAME))
+    for src, name in libs:
+        fd, tmp = tempfile.mkstemp(dir=dest_dir, prefix=".shim-")
+        os.close(fd)
+        shutil.copyfile(src, tmp)
+        os.chmod(tmp, 0o755)
+        os.replace(tmp, os.path.join(dest_dir, name))
     log.info("installed quota shim into %s", dest_dir)
     return dest_dir
 

@@ -78,6 +78,9 @@ ENV_HIP_FORCE_DEV_KERNARG = "HIP_FORCE_DEV_KERNARG"
 ENV_COMGR_CACHE = "AMD_COMGR_CACHE"
 ENV_COMGR_CACHE_DIR = "AMD_COMGR_CACHE_DIR"
 COMGR_CACHE_CONTAINER_DIR = "/run/gpushare/comgr-cache"
+# the whole-pipeline cache in front of comgr (native/comgrcache), installed next to the shim
+COMGR_ACTION_LIB_NAME = "libgpushare_comgrcache.so"
+ENV_COMGR_ACTION_CACHE = "GPUSHARE_COMGR_ACTION_CACHE"
 # container annotation (ContainerAllocateResponse.annotations): the host ledger directory key
 # of this container, so the plugin can map an answer back to its ledger (quota/ledger.py)
 CTR_ANNOTATION_LEDGER = "gpushare.amd.com/ledger"

@@ -23,6 +23,8 @@ LIBS = {
     "kernels": "libgpushare_kernels.so",
     "hbmbroker": "gpushare-hbm-broker",
     "comgrwarm": "gpushare-comgr-warm",
+    "comgrcache": "libgpushare_comgrcache.so",
+    "comgrprobe": "gpushare-comgr-probe",
 }
 
 _lock = threading.Lock()
@@ -48,7 +50,9 @@ def lib_path(target: str) -> str:
 
 
 SOURCES = {"gpuinfo": "gpuinfo", "hipshim": "hipshim", "dpserver": "dpserver", "kernels": "kernels",
-           "hbmbroker": "hbmbroker", "comgrwarm": "comgrwarm"}   # native/<dir>
+           "hbmbroker": "hbmbroker", "comgrwarm": "comgrwarm", "comgrcache": "comgrcache",
+           "comgrprobe": "comgrcache"}   # native/<dir>
+BUILD_TARGET = {"comgrprobe": "comgrcache"}     # built by another target of native/build.py
 
 
 def stale(target: str, path: str) -> bool:
@@ -58,7 +62,7 @@ def stale(target: str, path: str) -> bool:
     try:
         built = os.path.getmtime(path)
         return any(os.path.getmtime(os.path.join(src, f)) > built for f in os.listdir(src)
-                   if f.endswith((".cpp", ".h", ".hip", ".hpp")))
+                   if f.endswith((".c", ".cpp", ".h", ".hip", ".hpp")))
     except OSError:
         return False
 
@@ -79,7 +83,8 @@ def ensure_built(target: str, auto_build: bool | None = None) -> str:
             if not os.path.exists(path) or stale(target, path):
                 variant = os.environ.get("GPUSHARE_NATIVE_VARIANT", "")
                 extra = ["--sanitize", variant] if variant else []
-                r = subprocess.run([sys.executable, BUILD_SCRIPT, target, *extra], capture_output=True, text=True)
+                r = subprocess.run([sys.executable, BUILD_SCRIPT, BUILD_TARGET.get(target, target), *extra],
+                                   capture_output=True, text=True)
                 if r.returncode != 0:
                     raise NativeUnavailable(f"building {target} failed:\n{r.stdout}\n{r.stderr}")
     if not os.path.exists(path):

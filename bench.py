@@ -788,6 +788,7 @@ class PodFleet:
         self.pods: dict[str, dict] = {}       # uid -> {"proc", "q", "size", "ready"}
         self.standby: list[dict] = []         # pre-started interpreters, oldest first
         self.ready_ms: list[float] = []
+        self.slowest: dict = {}
         self.retired_gemms = 0
         self.denied = 0
         self.held_bytes = 0
@@ -830,7 +831,11 @@ class PodFleet:
     def _pod_env() -> dict:
         # the shim first; whatever this process already preloads (a profiler, the host's own
         # libraries) stays preloaded in the pods too
-        pre = ":".join(x for x in (os.path.join(NATIVE, "libgpushare_hipquota.so"), os.environ.get("LD_PRELOAD", "")) if x)
+        # (and the comgr action cache, as answers preload it: inert unless the answer's env turns
+        # it on, i.e. the plugin mounts a comgr cache)
+        cc = os.path.join(NATIVE, "libgpushare_comgrcache.so")
+        pre = ":".join(x for x in (os.path.join(NATIVE, "libgpushare_hipquota.so"), cc if os.path.exists(cc) else "",
+                                   os.environ.get("LD_PRELOAD", "")) if x)
         env = dict(os.environ, LD_PRELOAD=pre,
                    PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""), GS_POD_NICE="5")
         if PodFleet.pod_cpus:
@@ -941,6 +946,11 @@ class PodFleet:
         self.pods[rec["uid"]] = w
         self.held_bytes += ev.get("held", 0)
         self.ready_ms.append(dt)
+        if dt > self.slowest.get("ready", 0) / 1e3:     # the slowest pod of the run, phase by phase
+            self.slowest = {"ready": dt * 1e3, "size_gib": rec["size"], "init": (t1 - t0) * 1e3,
+                            "cuda_init": inited.get("cuda_init_ms"), "first_alloc": inited.get("runtime_ms"),
+                            "take": {k: take[k] for k in ("connect", "wait", "map") if k in take},
+                            "room": (t2 - t1) * 1e3, "alloc": (t3 - t2) * 1e3}
         return dt
 
     def _wait_room(self, nbytes: float, limit_s: float = 30.0) -> None:
@@ -1137,7 +1147,8 @@ def child_run(a, steps: int, *flags: str, tenant_stop: str | None = None, zygote
     broker = d.get("hbm_broker") or {}
     return {"value": d["value"], "unit": d["unit"], "steps": d["steps"], "ms_per_step": d["ms_per_step"],
             "pod_ready_p50_ms": d.get("pod_ready_p50_ms"), "pod_ready_p99_ms": d.get("pod_ready_p99_ms"),
-            "pod_phase_p50_ms": d.get("pod_phase_p50_ms"), "allocate_p50_ms": d.get("allocate_p50_ms"),
+            "pod_phase_p50_ms": d.get("pod_phase_p50_ms"), "pod_phase_max_ms": d.get("pod_phase_max_ms"),
+            "pod_slowest_ms": d.get("pod_slowest_ms"), "allocate_p50_ms": d.get("allocate_p50_ms"),
             "failed_admissions": d.get("failed_admissions"), "quota_denials": d.get("quota_denials"),
             "tenant_stop": d.get("config", {}).get("tenant_stop"),
             "standby_forked_from_zygote": d.get("config", {}).get("standby_forked_from_zygote"),
@@ -1372,6 +1383,8 @@ def main():
             plugin_latency(cp.ref_port, reset=True)
     if fleet is not None:
         fleet.ready_ms.clear()
+        if hasattr(fleet, "slowest"):
+            fleet.slowest = {}
         fleet.release_ms.clear()
         fleet.release_by_size.clear()
         fleet.release_bytes_s.clear()
@@ -1403,6 +1416,7 @@ def main():
             parts_all.setdefault(k, []).extend(v)
     ready = gather(fleet.ready_ms if fleet is not None else [])
     ready_all = [x for r in ready for x in r]
+    slowest = max(gather(getattr(fleet, "slowest", {}) if fleet is not None else {}), key=lambda w: w.get("ready", 0))
     held = gather(fleet.held_bytes if fleet is not None else 0)
     denied = gather(fleet.denied if fleet is not None else 0)
     residue = gather(fleet.released_residue if fleet is not None else 0)
@@ -1533,6 +1547,7 @@ def main():
             # (init) -> physical room for its state (room) -> state allocated + first GEMM (alloc)
             "pod_phase_p50_ms": {k: ms(pct(v, 0.5)) for k, v in phases.items()},
             "pod_phase_max_ms": {k: ms(max(v)) for k, v in phases.items() if v},
+            "pod_slowest_ms": {k: round(v, 3) if isinstance(v, float) else v for k, v in slowest.items()} or None,
             "control_plane_ms_per_admission": round(cp.cp_time / max(1, admissions) * 1e3, 3),
             # the reference-model node's own churn step runs inside each timed step (the
             # allocate_under_churn comparison): its share of ms_per_step

@@ -9,6 +9,7 @@ Targets
   kernels   libgpushare_kernels.so   (hand-written HIP/CDNA4 kernels, hipcc --offload-arch=gfx950)
   probes    shim_probe               (HIP test helper run under the quota shim on hardware)
   comgrwarm gpushare-comgr-warm      (the system HIP runtime's first-stream work: fills the node's comgr cache)
+  comgrcache libgpushare_comgrcache.so (clang: action cache in front of comgr, preloaded into pods) + gpushare-comgr-probe
 
 Usage: python native/build.py [targets...] [--force] [--asan | --sanitize {asan,tsan}] [-j N]
 The build is incremental (mtime based) so ``__graft_entry__.build()`` stays cheap.
@@ -238,9 +239,40 @@ def build_comgrwarm(force=False, asan=False):
     return [exe]
 
 
+def build_comgrcache(force=False, asan=False):
+    """libgpushare_comgrcache.so (native/comgrcache): the whole-pipeline cache in front of comgr
+    that shared pods preload. Built with ROCm's clang: its dlsym must tail-call the C library's
+    (``__attribute__((musttail))``, which g++ 11 lacks). gpushare-comgr-probe: the runtime's blit
+    compile without a GPU (tests)."""
+    d = _src("comgrcache")
+    if not os.path.isdir(d):
+        return []
+    clang = os.path.join(ROCM, "llvm", "bin", "clang")
+    lib = os.path.join(OUT, "libgpushare_comgrcache.so")
+    srcs = [os.path.join(d, "comgr_dlsym.c"), os.path.join(d, "comgr_action_cache.cpp")]
+    san = _san(asan)
+    flags = ["-O2", "-fPIC", "-fvisibility=hidden", "-Wall", "-Wextra", f"-I{ROCM}/include"]
+    if san:
+        flags += SANITIZERS[san]
+        lib = os.path.join(OUT, san, "libgpushare_comgrcache.so")
+    os.makedirs(os.path.dirname(lib), exist_ok=True)
+    if force or _newer(lib, srcs):
+        import tempfile
+        with tempfile.TemporaryDirectory() as tmp:
+            objs = [os.path.join(tmp, "dlsym.o"), os.path.join(tmp, "cache.o")]
+            _run([clang, *flags, "-c", "-o", objs[0], srcs[0]])
+            _run([clang + "++", *flags, "-std=c++17", "-c", "-o", objs[1], srcs[1]])
+            _run([clang + "++", *flags, "-shared", "-o", lib, *objs, "-ldl"])
+    probe = os.path.join(os.path.dirname(lib), "gpushare-comgr-probe")
+    psrc = os.path.join(d, "comgr_probe.cpp")
+    if force or _newer(probe, [psrc]):
+        _run([CXX, "-std=c++17", "-O2", "-Wall", f"-I{ROCM}/include", "-o", probe, psrc, "-ldl"])
+    return [lib, probe]
+
+
 TARGETS = {"gpuinfo": build_gpuinfo, "hipshim": build_hipshim, "dpserver": build_dpserver,
            "hbmbroker": build_hbmbroker, "kernels": build_kernels,
-           "probes": build_probes, "comgrwarm": build_comgrwarm}
+           "probes": build_probes, "comgrwarm": build_comgrwarm, "comgrcache": build_comgrcache}
 
 
 def build(targets=None, force=False, asan=False, jobs=4):

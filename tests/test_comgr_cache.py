@@ -3,7 +3,8 @@
 CPU: the Allocate answer mounts the sealed cache read-only with comgr's two variables (and
 nothing on a cgpu-disabled node), sealing makes every entry read-only, a fill without a GPU
 still seals and exits 0, and the DaemonSet fills it in an init container before the plugin
-mounts it. GPU: a filled cache takes the runtime's blit-kernel compile off a process's first
+mounts it. GPU: a filled cache (comgr's own plus the whole-pipeline one,
+tests/test_comgr_action_cache.py) takes the runtime's blit-kernel compile off a process's first
 stream, a pod cannot write it, and a runtime it does not hold still starts (a miss compiles)."""
 import json
 import os
@@ -44,6 +45,16 @@ def test_the_answer_mounts_the_cache_read_only(tmp_path):
     assert len(m) == 1 and m[0].host_path == str(cache) and m[0].read_only
     assert r.envs[const.ENV_COMGR_CACHE] == "1"
     assert r.envs[const.ENV_COMGR_CACHE_DIR] == const.COMGR_CACHE_CONTAINER_DIR
+    # the whole-pipeline cache: preloaded after the shim when it is installed next to it
+    assert const.ENV_COMGR_ACTION_CACHE not in r.envs
+    assert r.envs[const.ENV_LD_PRELOAD] == os.path.join(const.SHIM_CONTAINER_DIR, const.SHIM_LIB_NAME)
+    (tmp_path / "shim").mkdir()
+    (tmp_path / "shim" / const.COMGR_ACTION_LIB_NAME).write_bytes(b"")
+    r = _answer(tmp_path, comgr_cache_dir=str(cache))
+    assert r.envs[const.ENV_COMGR_ACTION_CACHE] == const.COMGR_CACHE_CONTAINER_DIR
+    assert r.envs[const.ENV_LD_PRELOAD].split(":") == [
+        os.path.join(const.SHIM_CONTAINER_DIR, n) for n in (const.SHIM_LIB_NAME, const.COMGR_ACTION_LIB_NAME)]
+    assert const.ENV_COMGR_ACTION_CACHE not in _answer(tmp_path).envs
     # off unless configured, off on a cgpu-disabled node (its pods get nothing of the plugin's), and
     # off while the directory is not there (a hostPath mount of a missing path fails the container)
     for r in (_answer(tmp_path), _answer(tmp_path, comgr_cache_dir=str(cache), disable_cgpu=True),
@@ -110,7 +121,14 @@ if d:
         write = "allowed"
     except OSError:
         write = "denied"
-print(json.dumps({"first_stream_ms": ms, "ok": float(y.sum()) == 2.0 * (1 << 20), "write": write}))
+try:                                   # the whole-pipeline cache's counters, when it is preloaded
+    import ctypes
+    a = (ctypes.c_uint64 * 5)()
+    ctypes.CDLL(None).gpushare_comgr_cache_stats(a, 5)
+    actions = dict(zip(("hits", "misses", "stores", "bypassed", "errors"), a))
+except AttributeError:
+    actions = None
+print(json.dumps({"first_stream_ms": ms, "ok": float(y.sum()) == 2.0 * (1 << 20), "write": write, "actions": actions}))
 """
 
 
@@ -122,7 +140,7 @@ def _pod(cache_dir):
     env.pop("AMD_COMGR_CACHE", None)
     env.pop("AMD_COMGR_CACHE_DIR", None)
     if cache_dir:
-        env = comgr_cache.cache_env(cache_dir, env)
+        env = comgr_cache.cache_env(cache_dir, env, lib=comgr_cache.action_lib())
     r = subprocess.run([sys.executable, "-c", POD], capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     return json.loads(r.stdout.strip().splitlines()[-1])
@@ -149,10 +167,15 @@ def test_a_pod_loads_its_blit_kernels_from_the_sealed_cache_and_cannot_write_it(
     miss = _pod(empty)
     res = {"cache": {"files": w["files"], "bytes": w["bytes"]}, "plain_ms": [p["first_stream_ms"] for p in plain],
            "cached_ms": [c["first_stream_ms"] for c in cached], "miss_ms": miss["first_stream_ms"],
-           "write": [c["write"] for c in cached]}
+           "write": [c["write"] for c in cached], "actions": [c["actions"] for c in cached],
+           "action_entries": w["action_entries"]}
     print(json.dumps(res))
     assert all(p["ok"] for p in plain + cached) and miss["ok"]
     assert _snapshot(d) == before and os.listdir(empty) == []
     if os.geteuid() != 0:                    # (root ignores the mode bits; a container's mount is read-only)
         assert all(c["write"] == "denied" for c in cached) and miss["write"] == "denied"
-    assert min(c["first_stream_ms"] for c in cached) + 30.0 < min(p["first_stream_ms"] for p in plain), res
+    # every step of the runtime's compile from the cache (none compiled, none stored): the first
+    # stream keeps only the runtime's own queue and code-object set-up
+    assert w["action_entries"] >= 4 and all(c["actions"]["hits"] >= 4 and not c["actions"]["misses"]
+                                             and not c["actions"]["stores"] for c in cached), res
+    assert min(c["first_stream_ms"] for c in cached) + 80.0 < min(p["first_stream_ms"] for p in plain), res

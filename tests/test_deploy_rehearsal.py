@@ -169,12 +169,19 @@ def test_shipped_manifests_run_a_node(hostroot, stub_runtime, native_shim):
             open(os.path.join(hostroot, "brokers.log")).read()[-3000:]
         # the container's process: the answer's env with its mounts resolved to host paths
         env = dict(r.envs)
-        for k, v in list(env.items()):
+
+        def host(v):
             for cpath, m in sorted(mounts.items(), key=lambda x: -len(x[0])):
                 if v == cpath or v.startswith(cpath.rstrip("/") + "/"):
-                    env[k] = m.host_path + v[len(cpath.rstrip("/")):]
-                    break
-        assert os.path.isfile(env["LD_PRELOAD"])
+                    return m.host_path + v[len(cpath.rstrip("/")):]
+            return v
+        for k, v in list(env.items()):
+            env[k] = ":".join(host(x) for x in v.split(":")) if k == "LD_PRELOAD" else host(v)
+        # the shim, then the comgr action cache the plugin installed next to it (with the cache mounted)
+        pre = env["LD_PRELOAD"].split(":")
+        assert [os.path.basename(x) for x in pre] == [const.SHIM_LIB_NAME, const.COMGR_ACTION_LIB_NAME]
+        assert all(os.path.isfile(x) for x in pre)
+        assert env[const.ENV_COMGR_ACTION_CACHE] == cache
         env.update(LD_LIBRARY_PATH=stub_runtime, FAKE_HIP_TOTAL_GIB="288")
         p = subprocess.run([os.path.join(stub_runtime, "shim_driver"), "alloc", str(32 << 30), "arena"],
                            env=dict(os.environ, **env), capture_output=True, text=True, timeout=60)
