@@ -1267,7 +1267,8 @@ def main():
             w = comgr_cache.warm(cdir, ("system", "torch"), device=ordinal)
             comgr_cache.seal(cdir)
             a.comgr_cache_dir = cdir
-            comgr_info = {"files": w["files"], "bytes": w["bytes"], "fill_s": round(time.perf_counter() - t_c, 2),
+            comgr_info = {"files": w["files"], "bytes": w["bytes"], "action_entries": w.get("action_entries"),
+                          "fill_s": round(time.perf_counter() - t_c, 2),
                           "runtimes": {k: bool(v.get("ok")) for k, v in w["runtimes"].items()}}
         cp = ControlPlane(n, smi, a.pod_source, a.plugin_mode, workdir, with_shim=use_gpu or bool(stub),
                           ref_spec=None if a.no_ref_churn else ref_spec, hbm_dir=hbm_dir,
