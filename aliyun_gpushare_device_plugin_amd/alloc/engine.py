@@ -201,6 +201,7 @@ class Allocator(NativeTable):
         # fast path: prepared answers, engine-state generation, answers awaiting bookkeeping
         self._fast: _Fast | None = None
         self._gen = 0
+        self.gen_bumps: dict[str, int] = {}
         self._prep_cache: dict[tuple, _Prepared] = {}
         self._post: "collections.deque" = collections.deque()
         self._post_mu = threading.Lock()
@@ -284,7 +285,7 @@ class Allocator(NativeTable):
         """A GPU's broker went away for good or came back: answers prepared with (or without) its
         token are re-prepared."""
         with self._mu:
-            self._bump_gen()
+            self._bump_gen("hbm_readiness")
             self._fast = None
             self._prep_cache.clear()
         self._precomputed.clear()
@@ -326,7 +327,7 @@ class Allocator(NativeTable):
             if self._hbm is not None:
                 self._hbm.set_disabled(self.opts.disable_cgpu)
             self._pinfo.clear()
-            self._bump_gen()
+            self._bump_gen("reconfigure")
             self._fast = None
             self._prep_cache.clear()
         if self.native is not None:
@@ -342,7 +343,7 @@ class Allocator(NativeTable):
             if self.opts.disable_cgpu == disabled:
                 return
             self.opts = dataclasses.replace(self.opts, disable_cgpu=disabled)
-            self._bump_gen()
+            self._bump_gen("cgpu_disable")
             self._fast = None
             self._prep_cache.clear()
             self._resp_tmpl.clear()
@@ -359,9 +360,11 @@ class Allocator(NativeTable):
         if self._patch_q is not None:
             self._patch_q.put(None)
 
-    def _bump_gen(self) -> None:
+    def _bump_gen(self, why: str = "other") -> None:
         """A change of engine state the prepared answers depend on (caller holds ``_mu``): the
-        native table built before it is no longer served, and the prepare loop rebuilds."""
+        native table built before it is no longer served, and the prepare loop rebuilds.
+        ``gen_bumps`` counts them by cause (/debug/latency, the bench line)."""
+        self.gen_bumps[why] = self.gen_bumps.get(why, 0) + 1
         self._gen += 1
         nat = self.native
         if nat is not None:
@@ -516,7 +519,7 @@ class Allocator(NativeTable):
                 # never handed out again while the pod lives (no double booking of its HBM);
                 # its own admission, if it comes, is matched elsewhere or refused.
                 self._tainted[c.uid] = now
-                self._bump_gen()
+                self._bump_gen("claim_tainted")
                 self.metrics.allocate_outcomes.inc(outcome="claim_tainted")
                 log.warning("pod %s: %d/%d gpu containers answered from its reservation, then the kubelet moved on "
                             "(%s); reservation withheld", O.name(c.pod), c.next_container, len(c.shape),
@@ -656,7 +659,7 @@ class Allocator(NativeTable):
             self._claims.pop(c.uid, None)
             if self.pods.get(c.uid) is not None:
                 self._tainted[c.uid] = now
-                self._bump_gen()
+                self._bump_gen("claim_tainted")
                 self.metrics.allocate_outcomes.inc(outcome="claim_tainted")
         if u in self._tainted or u in self._claims or (u in self._assigned and done == 0):
             log.warning("admission identity: pod %s is being admitted but its reservation is no longer whole", O.name(p))
@@ -1339,7 +1342,7 @@ class Allocator(NativeTable):
                 if self._overlay_gen.get(job.uid) == job.gen:
                     self._overlay.pop(job.uid, None)
                     self._overlay_gen.pop(job.uid, None)
-                    self._bump_gen()
+                    self._bump_gen("placement_landed")
             return
         self.journal.landed(job.uid)
         with self._mu:
@@ -1457,7 +1460,8 @@ class Allocator(NativeTable):
             held = src.list()
             pods = self._view(A.dedupe_by_uid(self.pods.node_pods(), self.node))
             now = time.time()
-            fixes = PL.plan(pods, held, self.grants, now, self.opts.in_flight_s)
+            fixes = [f for f in PL.plan(pods, held, self.grants, now, self.opts.in_flight_s)
+                     if not self._patch_queued(f)]
             for f in fixes:
                 self._apply_fix(f)
             live = {O.uid(p) for p in pods}
@@ -1465,6 +1469,16 @@ class Allocator(NativeTable):
                               self.opts.in_flight_s)
             self._placed_at = t_pass
             return fixes
+
+    def _patch_queued(self, f: PL.Fix) -> bool:
+        """A holder fix that would only set ASSIGNED=true on a pod whose own answer's ASSIGNED
+        patch is still queued (write-behind): that patch says the same. Applying it anyway would
+        queue a second PATCH and retire the prepared table twice (placement overlay, then its
+        landing), and the next Allocates would wait for a rebuild."""
+        if f.reason != "holder" or f.ann or f.assigned is not True:
+            return False
+        with self._mu:
+            return f.uid in self._unpatched
 
     def settled(self, uid: str) -> bool:
         """The pod's annotations are known to tell where it runs: placement truth is on, a
@@ -1506,7 +1520,7 @@ class Allocator(NativeTable):
             gen = self._overlay_gen.get(f.uid, 0) + 1
             self._overlay_gen[f.uid] = gen
             self._overlay[f.uid] = dict(self._overlay.get(f.uid) or {}, **ann)
-            self._bump_gen()
+            self._bump_gen("placement_overlay")
             if f.assigned is True:
                 self._assigned[f.uid] = time.monotonic()
                 self._revoked.discard(f.uid)

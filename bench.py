@@ -217,7 +217,11 @@ def native_share(before: dict | None, after: dict | None) -> dict | None:
             "native_answer_mean_us": {k: round((a.get(f"{k}_ns", 0) - b.get(f"{k}_ns", 0)) / 1e3 / max(1, fast), 1)
                                       for k in ("lock", "journal", "answer")},
             "table_hook_skipped": {k: v - (b.get("table_hook_skipped") or {}).get(k, 0)
-                                   for k, v in (a.get("table_hook_skipped") or {}).items()}}
+                                   for k, v in (a.get("table_hook_skipped") or {}).items()},
+            # engine-state changes that retired the prepared table (each makes the next Allocates
+            # wait for a rebuild), by cause
+            "gen_bumps": {k: v - (b.get("gen_bumps") or {}).get(k, 0)
+                          for k, v in (a.get("gen_bumps") or {}).items() if v - (b.get("gen_bumps") or {}).get(k, 0)}}
 
 
 def pod_timeline(port: int, commits: dict) -> dict | None:
@@ -263,6 +267,7 @@ def pod_timeline(port: int, commits: dict) -> dict | None:
             steps[f"{a_}->{b_}"] = {"wall_us": round(wall[len(wall) // 2], 1),
                                     "cpu_us": round(cpu[len(cpu) // 2], 1) if cpu else None}
     waited = [r for r in rows if r.get("watch_wait_ns")]
+    table_waited = [r for r in rows if r.get("table_wait_ns") and not r.get("watch_wait_ns")]
     causes: dict = {}
     for r in waited:
         if r.get("pre_pub") is not None and r["pre_pub"] <= 0:
@@ -276,10 +281,15 @@ def pod_timeline(port: int, commits: dict) -> dict | None:
         causes[why] = causes.get(why, 0) + 1
     keys = ("commit_start", "commit_done", "pre_read", "pre_seen", "prep_ledger", "prep_hbm", "pre_prep", "pre_pub",
             "bind_seen", "bind_pub", "tab")
+    def whole(r):        # every mark of the pod (a pre_<reason> names why its pre-bind entry was not published)
+        extra = tuple(k for k in r if k.startswith("pre_") and k not in keys and not k.endswith("_cpu_ns"))
+        return {k: r.get(k) for k in keys + extra + ("watch_wait_ns", "table_wait_ns", "path") if r.get(k) is not None}
+
     return {"pods": len(rows), "watch_waited": len(waited), "causes": causes, "prebind_steps": steps,
             "median_ms": {k: med(k) for k in keys},
-            "waited": [{k: r.get(k) for k in keys + ("watch_wait_ns", "table_wait_ns", "path") if r.get(k) is not None}
-                       for r in waited]}
+            "waited": [whole(r) for r in waited],
+            # Allocates that found the pod but waited for its table entry (an answer being re-prepared)
+            "table_waited": [whole(r) for r in table_waited]}
 
 
 def transport_floor() -> float | None:

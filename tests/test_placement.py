@@ -382,3 +382,34 @@ def test_rehoming_a_claimed_pod_whose_patch_has_not_landed_rearms_it():
         assert r.container_responses[0].envs[const.ENV_RESOURCE_INDEX] == "1"
     finally:
         al.close()
+
+
+def test_a_holder_whose_own_assigned_patch_is_queued_is_left_to_that_patch():
+    """Right after an answer, the kubelet lists the pod holding its IDs while the pod still reads
+    ASSIGNED=false (the answer's write-behind PATCH is queued). Placement must not queue a second
+    ASSIGNED patch for it: that retired the prepared table twice per admission (a placement
+    overlay, then its landing) and the next Allocates waited for a rebuild. Once that patch has
+    failed for good (nothing queued) a pass fixes the annotation as before."""
+    from .test_allocate_engine import NODE
+
+    class Down(Client):
+        def patch_pod(self, *a, **k):                        # the ASSIGNED patch stays queued
+            raise RuntimeError("apiserver unreachable")
+
+    src = StaticSource([mkpod("a", 4, 0, 1)])
+    al = Allocator(DeviceModel([gpu(0, 8 << 30)], const.GIB), src, Down(src), NODE,
+                   AllocatorOptions(async_patch=True, fast_path=False, placement_s=0))
+    kl = Kubelet()
+    al.set_pod_resources(kl)
+    try:
+        assert kl.admit(al, _cur(src, "a")) == [0]
+        assert "uid-a" in al._unpatched and _ann(src, "a")[const.ENV_ASSIGNED_FLAG] == "false"
+        gen = al._gen
+        assert al.reconcile_placement() == [] and al._gen == gen and "uid-a" not in al._overlay
+        with al._mu:                                         # the queued patch gave up
+            al._unpatched.discard("uid-a")
+        fixes = al.reconcile_placement()
+        assert [(f.uid, f.reason, f.assigned) for f in fixes] == [("uid-a", "holder", True)]
+        assert al._overlay["uid-a"][const.ENV_ASSIGNED_FLAG] == "true"
+    finally:
+        al.close()
