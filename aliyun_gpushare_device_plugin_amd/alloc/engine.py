@@ -55,6 +55,7 @@ from __future__ import annotations
 import collections
 import contextlib
 import dataclasses
+import functools
 import os
 import threading
 import time
@@ -1084,12 +1085,18 @@ class Allocator(NativeTable):
             if hbm is not None:
                 gg = self.model.gpu(g)
                 tok = hbm.token(u or f"{g}-{time.time_ns()}", 0)
-                ok = hbm.submit(g, tok, U.quota_bytes(units, gg.units, gg.vram_bytes), wake)
+                qb = U.quota_bytes(units, gg.units, gg.vram_bytes)
+                if wake:
+                    ok = hbm.submit(g, tok, qb)
+                else:
+                    # the grant is recorded (and the granter woken) once the answer is published:
+                    # the pod's TAKE comes at its container's start, long after
+                    ok = hbm.grantable(g, qb)
+                    if ok:
+                        kicks.append(functools.partial(hbm.submit, g, tok, qb))
                 self._mark(u, "prep_hbm")
                 if ok:
                     extra += _pb_map_entry(0x0a, const.ENV_HBM_TOKEN, tok)
-                    if not wake:
-                        kicks.append(hbm.kick)
         body = _pb_ld(0x0a, base + extra)            # AllocateResponse.container_responses[0]
         return _Prepared(u, O.namespace(p), O.name(p), units, False, g, body,
                          AllocJournal.fast_head(u, O.namespace(p), O.name(p), body), lkey)

@@ -347,6 +347,10 @@ class HBMGranter:
             return now - st.last_ok < self.down_grace_s
         return now - self._t0 < self.startup_grace_s
 
+    def grantable(self, gpu_index: int, quota_bytes: int) -> bool:
+        """Whether ``submit`` would take this grant now (the answer carries the token)."""
+        return bool(self.arena_bytes(quota_bytes)) and not self.disabled and self.ready(gpu_index)
+
     def submit(self, gpu_index: int, token: str, quota_bytes: int, wake: bool = True) -> bool:
         """Record the grant and have the granter thread send it (woken now, or at ``kick()``
         when ``wake`` is false); True = the answer carries the token. Runs on the pod watch /
