@@ -12,7 +12,7 @@ build:                      ## native libs: SMI library + CLI, HIP quota shim, D
 	$(PY) -c "import __graft_entry__ as g; g.build()"
 
 build-san:                  ## host-side ASan+UBSan and TSan variants (_native/asan, _native/tsan)
-	$(PY) native/build.py gpuinfo hipshim dpserver hbmbroker --sanitize asan
+	$(PY) native/build.py gpuinfo hipshim dpserver hbmbroker comgrcache --sanitize asan
 	$(PY) native/build.py gpuinfo hipshim dpserver --sanitize tsan
 
 lint:                       ## byte-compile everything; reject tabs / trailing whitespace in sources

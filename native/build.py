@@ -260,7 +260,8 @@ def build_comgrcache(force=False, asan=False):
         import tempfile
         with tempfile.TemporaryDirectory() as tmp:
             objs = [os.path.join(tmp, "dlsym.o"), os.path.join(tmp, "cache.o")]
-            _run([clang, *flags, "-c", "-o", objs[0], srcs[0]])
+            # the dlsym thunk is never instrumented: a sanitizer runtime calls dlsym while it starts
+            _run([clang, *[f for f in flags if f not in SANITIZERS.get(san or "", [])], "-c", "-o", objs[0], srcs[0]])
             _run([clang + "++", *flags, "-std=c++17", "-c", "-o", objs[1], srcs[1]])
             _run([clang + "++", *flags, "-shared", "-o", lib, *objs, "-ldl"])
     probe = os.path.join(os.path.dirname(lib), "gpushare-comgr-probe")

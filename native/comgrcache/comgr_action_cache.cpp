@@ -46,7 +46,11 @@ namespace {
 using dlsym_fn = void* (*)(void*, const char*);
 dlsym_fn g_real_dlsym = nullptr;
 
-void resolve_real_dlsym() {
+// (not instrumented in a sanitizer build: a sanitizer runtime resolves its interceptors with dlsym
+// before its shadow memory exists)
+#define GS_NO_SANITIZE __attribute__((no_sanitize("address", "undefined", "thread")))
+
+GS_NO_SANITIZE void resolve_real_dlsym() {
   void* p = dlvsym(RTLD_NEXT, "dlsym", "GLIBC_2.34");
   if (p == nullptr) p = dlvsym(RTLD_NEXT, "dlsym", "GLIBC_2.2.5");
   if (p == nullptr) {
@@ -435,7 +439,7 @@ void* wrap(void* handle) {
 // cannot leave a noexcept frame) calls these two
 extern "C" __attribute__((visibility("hidden"))) void* gs_comgr_wrap(void* handle) { return wrap(handle); }
 
-extern "C" __attribute__((visibility("hidden"))) dlsym_fn gs_comgr_real_dlsym() {
+extern "C" __attribute__((visibility("hidden"))) GS_NO_SANITIZE dlsym_fn gs_comgr_real_dlsym() {
   dlsym_fn f = __atomic_load_n(&g_real_dlsym, __ATOMIC_ACQUIRE);
   if (__builtin_expect(f == nullptr, 0)) {
     resolve_real_dlsym();

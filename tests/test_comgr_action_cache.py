@@ -134,3 +134,41 @@ def test_dlsym_keeps_rtld_next_relative_to_the_real_caller(tmp_path):
                              env=dict(os.environ, LD_PRELOAD=pre, GPUSHARE_COMGR_ACTION_CACHE=str(tmp_path)))
     assert plain.stdout.strip() == "none"
     assert shimmed.stdout.strip() == "none"
+
+
+def test_the_cache_under_address_and_ub_sanitizers(tmp_path):
+    """The library built with -fsanitize=address,undefined (its dlsym thunk left plain: the
+    sanitizer runtime resolves its interceptors with dlsym before its shadow exists), through a
+    fill, hits, and corrupt, truncated and foreign entries."""
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "native"))
+    import build as nb
+
+    lib = nb.build_comgrcache(asan="asan")[0]
+    clang = os.path.join(nb.ROCM, "llvm", "bin", "clang")
+    rt = subprocess.run([clang, "-print-file-name=libclang_rt.asan-x86_64.so"], capture_output=True,
+                        text=True).stdout.strip()
+    if not os.path.exists(rt):
+        pytest.skip("clang's ASan runtime is not installed")
+    d = tmp_path / "cache"
+    d.mkdir()
+    san = {"LD_PRELOAD": f"{rt}:{lib}", "ASAN_OPTIONS": "detect_leaks=0:halt_on_error=1",
+           "UBSAN_OPTIONS": "halt_on_error=1:print_stacktrace=1"}
+
+    def run(write=False):
+        env = dict(os.environ, GPUSHARE_COMGR_ACTION_CACHE=str(d), **san)
+        if write:
+            env["GPUSHARE_COMGR_ACTION_CACHE_WRITE"] = "1"
+        r = subprocess.run([PROBE, "", "1"], capture_output=True, text=True, timeout=300, env=env)
+        assert r.returncode == 0, r.stderr[-3000:]
+        assert "AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr[-3000:]
+        return json.loads(r.stdout.strip().splitlines()[-1])
+
+    digest = run(write=True)["exe_digest"]
+    assert run()["cache"]["hits"] == 4
+    entries = _entries(d)
+    (d / entries[0]).write_bytes((d / entries[0]).read_bytes()[:-9])          # short by the checksum
+    (d / entries[1]).write_bytes(b"GSCA0001" + b"\xff" * 64)                  # a count far past the end
+    (d / entries[2]).write_bytes(b"")
+    assert run()["exe_digest"] == digest
