@@ -361,6 +361,11 @@ class Allocator(NativeTable):
         if self._patch_q is not None:
             self._patch_q.put(None)
 
+    def gen_bump_counts(self) -> dict[str, int]:
+        """``gen_bumps``, copied under the engine lock (the debug endpoint's thread)."""
+        with self._mu:
+            return dict(self.gen_bumps)
+
     def _bump_gen(self, why: str = "other") -> None:
         """A change of engine state the prepared answers depend on (caller holds ``_mu``): the
         native table built before it is no longer served, and the prepare loop rebuilds.

@@ -281,7 +281,8 @@ class SharedGPUManager:
             return {}
         skipped = {dict(k).get("why", ""): v for k, v in self.metrics.table_publish_skipped._v.items()}
         out = {"native_server": dict(stats(), table_hook_skipped=skipped,
-                                     gen_bumps=dict(getattr(self.allocator, "gen_bumps", {})))}
+                                     gen_bumps=self.allocator.gen_bump_counts()
+                                     if hasattr(self.allocator, "gen_bump_counts") else {})}
         trace = getattr(self.allocator, "pod_trace", None)
         if trace is not None:
             out["pod_trace"] = trace()
