@@ -14,7 +14,9 @@ import sys
 import time
 
 TENANT = r"""
-import ctypes, json, os, sys, torch
+import ctypes, json, os, sys
+if os.environ.get("GS_CPU"): os.sched_setaffinity(0, {int(os.environ["GS_CPU"])})
+import torch
 x = torch.full((6 << 30,), 7, dtype=torch.uint8, device="cuda")
 y = torch.randn(4096, 4096, device="cuda")
 for _ in range(20):
@@ -34,24 +36,61 @@ os._exit(0)
 """
 
 STARTER = r"""
-import json, sys, time
+import json, os, sys, threading, time
+if os.environ.get("GS_CPU"): os.sched_setaffinity(0, {int(x) for x in os.environ["GS_CPU"].split(",")})
 import torch
+NAMES = {"16": "ioctl", "0": "read", "257": "openat", "9": "mmap", "11": "munmap", "3": "close", "202": "futex",
+         "10": "mprotect", "262": "newfstatat", "17": "pread64", "89": "readlink", "217": "getdents64", "7": "poll"}
+tid = threading.get_native_id()
+samples, stop = [], threading.Event()
+def sampler():                     # what the starting thread is doing, every 100 us: on a CPU or in a syscall
+    path = f"/proc/self/task/{tid}/syscall"
+    while not stop.is_set():
+        try:
+            with open(path) as f:
+                samples.append(f.read().split()[:3])
+        except OSError:
+            pass
+        time.sleep(0.0001)
 sys.stdout.write("go\n"); sys.stdout.flush()
 sys.stdin.readline()
+import resource
+def cg():                          # the job's cgroup CPU accounting (throttling under a CPU quota)
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            return {k: int(v) for k, v in (ln.split() for ln in f)}
+    except OSError:
+        return {}
+th = threading.Thread(target=sampler, daemon=True); th.start()
+c0, r0 = cg(), resource.getrusage(resource.RUSAGE_THREAD)
 t2 = time.perf_counter()
 torch.cuda.init()
 t3 = time.perf_counter()
+c1, r1 = cg(), resource.getrusage(resource.RUSAGE_THREAD)
+stop.set(); th.join()
+where = {}
+for f in samples:
+    k = "cpu" if f and f[0] == "running" else (NAMES.get(f[0], "sys" + f[0]) + (" " + f[2] if f[0] == "16" and len(f) > 2 else "")) if f else "?"
+    where[k] = where.get(k, 0) + 1
 z = torch.zeros(1 << 20, device="cuda")
 torch.cuda.synchronize()
 t4 = time.perf_counter()
-print(json.dumps({"cuda_init_ms": round((t3 - t2) * 1e3, 1), "first_alloc_ms": round((t4 - t3) * 1e3, 1)}), flush=True)
+n = max(1, sum(where.values()))
+print(json.dumps({"cuda_init_ms": round((t3 - t2) * 1e3, 1), "first_alloc_ms": round((t4 - t3) * 1e3, 1),
+                  "init_where_pct": {k: round(100 * v / n, 1) for k, v in sorted(where.items(), key=lambda x: -x[1])},
+                  "init_thread_cpu_ms": round((r1.ru_utime + r1.ru_stime - r0.ru_utime - r0.ru_stime) * 1e3, 1),
+                  "init_nvcsw": r1.ru_nvcsw - r0.ru_nvcsw, "init_nivcsw": r1.ru_nivcsw - r0.ru_nivcsw,
+                  "cgroup_during_init": {k: c1[k] - c0.get(k, 0) for k in c1 if k in ("usage_usec", "nr_throttled", "throttled_usec", "nr_periods")}}), flush=True)
 """
 
 
-def trial(mode: str, when: str, pause_s: float) -> dict:
-    st = subprocess.Popen([sys.executable, "-c", STARTER], stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+def trial(mode: str, when: str, pause_s: float, cpus: tuple = ("", "")) -> dict:
+    import os
+    st = subprocess.Popen([sys.executable, "-c", STARTER], stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True,
+                          env=dict(os.environ, GS_CPU=cpus[1]))
     assert st.stdout.readline().strip() == "go"
-    t = subprocess.Popen([sys.executable, "-c", TENANT], stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+    t = subprocess.Popen([sys.executable, "-c", TENANT], stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True,
+                         env=dict(os.environ, GS_CPU=cpus[0]))
     assert json.loads(t.stdout.readline())["ready"]
     t0 = time.perf_counter()
     t.stdin.write(mode + "\n")
@@ -67,7 +106,7 @@ def trial(mode: str, when: str, pause_s: float) -> dict:
     r = json.loads(st.stdout.readline())
     st.wait(60)
     t.wait(60)
-    return dict(r, mode=mode, when=when, pause_s=pause_s, leave_ms=round((t_ack - t0) * 1e3, 1),
+    return dict(r, mode=mode, when=when, pause_s=pause_s, cpus=list(cpus), leave_ms=round((t_ack - t0) * 1e3, 1),
                 go_after_ack_ms=round((t_go - t_ack) * 1e3, 1))
 
 
@@ -76,7 +115,14 @@ def main():
     ap.add_argument("--trials", type=int, default=3)
     ap.add_argument("--modes", default="exit,free,reset")
     ap.add_argument("--whens", default="ack,reaped")
+    ap.add_argument("--pin", default="", help="'T/S' CPU lists for tenant / starter, ';'-separated variants")
     a = ap.parse_args()
+    if a.pin:                      # placement variants only: reaped order, no pause
+        for i in range(a.trials):
+            for v in a.pin.split(";"):
+                tc, sc = v.split("/")
+                print(json.dumps(dict(trial("exit", "reaped", 0.0, (tc, sc)), trial=i)), flush=True)
+        return
     for i in range(a.trials):
         for mode in a.modes.split(","):
             for when in a.whens.split(","):
