@@ -17,14 +17,20 @@ TENANT = r"""
 import ctypes, json, os, sys
 if os.environ.get("GS_CPU"): os.sched_setaffinity(0, {int(os.environ["GS_CPU"])})
 import torch
-x = torch.full((6 << 30,), 7, dtype=torch.uint8, device="cuda")
-y = torch.randn(4096, 4096, device="cuda")
-for _ in range(20):
-    y = y @ y.T / 4096.0
-torch.cuda.synchronize()
+kind = os.environ.get("GS_TENANT", "full")     # what the tenant did with the GPU before it leaves
+if kind == "initonly":
+    torch.cuda.init()
+elif kind == "small":
+    x = torch.ones(1 << 20, device="cuda"); x.add_(1); torch.cuda.synchronize()
+else:
+    x = torch.full((6 << 30,), 7, dtype=torch.uint8, device="cuda")
+    y = torch.randn(4096, 4096, device="cuda")
+    for _ in range(20):
+        y = y @ y.T / 4096.0
+    torch.cuda.synchronize()
 print(json.dumps({"ready": True}), flush=True)
 mode = sys.stdin.readline().strip()
-if mode in ("free", "reset"):
+if mode in ("free", "reset") and kind == "full":
     del x, y
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
@@ -61,24 +67,42 @@ def cg():                          # the job's cgroup CPU accounting (throttling
             return {k: int(v) for k, v in (ln.split() for ln in f)}
     except OSError:
         return {}
+def cpustat():                     # system-wide jiffies: irq, softirq, steal (a VM's host takes the vCPUs)
+    with open("/proc/stat") as f:
+        v = [int(x) for x in f.readline().split()[1:]]
+    return {"user": v[0], "system": v[2], "idle": v[3], "iowait": v[4], "irq": v[5], "softirq": v[6], "steal": v[7]}
 th = threading.Thread(target=sampler, daemon=True); th.start()
+s0 = cpustat()
 c0, r0 = cg(), resource.getrusage(resource.RUSAGE_THREAD)
+# ROCr's hsa_init through ctypes (the interpreter lock is released, so the sampler runs during it;
+# torch.cuda.init() keeps the lock), then the rest of torch.cuda.init()
+import ctypes, glob
+hsa = ctypes.CDLL((glob.glob(os.path.join(os.path.dirname(torch.__file__), "lib", "libhsa-runtime64.so*")) or ["libhsa-runtime64.so.1"])[0])
 t2 = time.perf_counter()
+hsa.hsa_init()
+t_hsa = time.perf_counter()
 torch.cuda.init()
 t3 = time.perf_counter()
 c1, r1 = cg(), resource.getrusage(resource.RUSAGE_THREAD)
+s1 = cpustat()
 stop.set(); th.join()
 where = {}
 for f in samples:
-    k = "cpu" if f and f[0] == "running" else (NAMES.get(f[0], "sys" + f[0]) + (" " + f[2] if f[0] == "16" and len(f) > 2 else "")) if f else "?"
+    if f and f[0] == "257" and len(f) > 2:          # openat: the path, read from this process's memory
+        try:
+            f = ["257", "", ctypes.string_at(int(f[2], 16), 120).split(b"\0")[0].decode(errors="replace")]
+        except (ValueError, OSError):
+            pass
+    k = "runnable" if f and f[0] == "running" else (NAMES.get(f[0], "sys" + f[0]) + (" " + f[2] if f[0] in ("16", "257") and len(f) > 2 else "")) if f else "?"
     where[k] = where.get(k, 0) + 1
 z = torch.zeros(1 << 20, device="cuda")
 torch.cuda.synchronize()
 t4 = time.perf_counter()
 n = max(1, sum(where.values()))
-print(json.dumps({"cuda_init_ms": round((t3 - t2) * 1e3, 1), "first_alloc_ms": round((t4 - t3) * 1e3, 1),
+print(json.dumps({"cuda_init_ms": round((t3 - t2) * 1e3, 1), "hsa_init_ms": round((t_hsa - t2) * 1e3, 1), "first_alloc_ms": round((t4 - t3) * 1e3, 1),
                   "init_where_pct": {k: round(100 * v / n, 1) for k, v in sorted(where.items(), key=lambda x: -x[1])},
                   "init_thread_cpu_ms": round((r1.ru_utime + r1.ru_stime - r0.ru_utime - r0.ru_stime) * 1e3, 1),
+                  "system_jiffies_during_init": {k: s1[k] - s0[k] for k in s1},
                   "init_nvcsw": r1.ru_nvcsw - r0.ru_nvcsw, "init_nivcsw": r1.ru_nivcsw - r0.ru_nivcsw,
                   "cgroup_during_init": {k: c1[k] - c0.get(k, 0) for k in c1 if k in ("usage_usec", "nr_throttled", "throttled_usec", "nr_periods")}}), flush=True)
 """
@@ -115,8 +139,16 @@ def main():
     ap.add_argument("--trials", type=int, default=3)
     ap.add_argument("--modes", default="exit,free,reset")
     ap.add_argument("--whens", default="ack,reaped")
+    ap.add_argument("--tenants", default="", help="tenant kinds to compare (initonly,small,full): reaped order")
     ap.add_argument("--pin", default="", help="'T/S' CPU lists for tenant / starter, ';'-separated variants")
     a = ap.parse_args()
+    if a.tenants:
+        import os
+        for i in range(a.trials):
+            for k in a.tenants.split(","):
+                os.environ["GS_TENANT"] = k
+                print(json.dumps(dict(trial("exit", "reaped", 0.0), tenant=k, trial=i)), flush=True)
+        return
     if a.pin:                      # placement variants only: reaped order, no pause
         for i in range(a.trials):
             for v in a.pin.split(";"):
