@@ -203,6 +203,7 @@ class Allocator(NativeTable):
         self._fast: _Fast | None = None
         self._gen = 0
         self.gen_bumps: dict[str, int] = {}
+        self.placement_log: list[dict] = []
         self._prep_cache: dict[tuple, _Prepared] = {}
         self._post: "collections.deque" = collections.deque()
         self._post_mu = threading.Lock()
@@ -364,7 +365,7 @@ class Allocator(NativeTable):
     def gen_bump_counts(self) -> dict[str, int]:
         """``gen_bumps``, copied under the engine lock (the debug endpoint's thread)."""
         with self._mu:
-            return dict(self.gen_bumps)
+            return dict(self.gen_bumps, **({"last_fixes": list(self.placement_log)} if self.placement_log else {}))
 
     def _bump_gen(self, why: str = "other") -> None:
         """A change of engine state the prepared answers depend on (caller holds ``_mu``): the
@@ -1525,6 +1526,11 @@ class Allocator(NativeTable):
         elif f.assigned is False:
             ann[const.ENV_ASSIGNED_FLAG] = "false"
         self.metrics.allocate_outcomes.inc(outcome=f"placement_{f.reason}")
+        with self._mu:        # the last fixes, for /debug/latency (why a prepared table was retired)
+            self.placement_log.append({"uid": f.uid, "reason": f.reason, "ann": sorted(f.ann), "assigned": f.assigned,
+                                       "unpatched": f.uid in self._unpatched, "answered": f.uid in self._assigned,
+                                       "t": round(time.monotonic(), 3)})
+            del self.placement_log[:-16]
         log.warning("placement: pod %s/%s %s -> %s", f.ns, f.name,
                     "holds its containers' grants" if f.reason == "holder" else "reservation re-homed",
                     {k: v for k, v in ann.items() if k != const.ENV_RESOURCE_ASSUME_TIME})

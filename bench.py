@@ -221,7 +221,11 @@ def native_share(before: dict | None, after: dict | None) -> dict | None:
             # engine-state changes that retired the prepared table (each makes the next Allocates
             # wait for a rebuild), by cause
             "gen_bumps": {k: v - (b.get("gen_bumps") or {}).get(k, 0)
-                          for k, v in (a.get("gen_bumps") or {}).items() if v - (b.get("gen_bumps") or {}).get(k, 0)}}
+                          for k, v in (a.get("gen_bumps") or {}).items()
+                          if k != "last_fixes" and v - (b.get("gen_bumps") or {}).get(k, 0)},
+            # the placement fixes behind them (the plugin's last 16, newest last)
+            "placement_fixes": [f for f in (a.get("gen_bumps") or {}).get("last_fixes", [])
+                                if f not in (b.get("gen_bumps") or {}).get("last_fixes", [])]}
 
 
 def pod_timeline(port: int, commits: dict) -> dict | None:
