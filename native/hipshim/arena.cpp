@@ -974,6 +974,14 @@ using namespace gs;
 
 // Hand the arena back to the broker now (the pod is retiring and freed everything). Returns 1 if
 // released, 0 if there is no arena, -1 if allocations are still live in it.
+// The fast exit on demand, for a process about to end (probes): every queue destroyed, every
+// noted import (and, with GPUSHARE_SHIM_FREE_ALLOCS_AT_EXIT=1, every KFD allocation) freed. The
+// process must not touch the GPU afterwards.
+GS_EXPORT int gpushare_shim_fast_exit_release() {
+  fast_release("api");
+  return 0;
+}
+
 GS_EXPORT int gpushare_shim_arena_release() {
   Arena& a = g_arena;
   pthread_mutex_lock(&a.mu);

@@ -108,6 +108,9 @@ struct Lingering {                               // clients whose charged fd clo
 Lingering g_linger;
 
 // ---- KFD boundary --------------------------------------------------------------------------
+bool free_allocs_at_exit();
+void alloc_note(int kfd, uint64_t handle, uint32_t gpu_id);
+
 int kfd_alloc(ioctl_t f, int fd, unsigned long req, KfdAllocArgs* a) {
   if (!g.quota.load(std::memory_order_relaxed)) set_quota_from_device_bytes(kfd_vram_bytes(a->gpu_id));
   uint64_t c = a->size;
@@ -125,6 +128,7 @@ int kfd_alloc(ioctl_t f, int fd, unsigned long req, KfdAllocArgs* a) {
     return r;
   }
   track(a->handle, c);
+  if (free_allocs_at_exit()) alloc_note(fd, a->handle, a->gpu_id);
   logf(2, "kfd alloc %llu bytes (flags 0x%x) -> handle 0x%llx, used %llu", (unsigned long long)c, a->flags,
        (unsigned long long)a->handle, (unsigned long long)g.ledger->total.load());
   return r;
@@ -406,6 +410,22 @@ void import_note(int kfd, const KfdImportArgs* a, int tag) {
   pthread_mutex_unlock(&g_imp_mu);
 }
 
+// every KFD allocation too (tag kTagAlloc), when GPUSHARE_SHIM_FREE_ALLOCS_AT_EXIT=1: the fast exit
+// then frees the process's own buffers as well, before the kernel's release of the process
+constexpr int kTagAlloc = 3;
+bool free_allocs_at_exit() {
+  static int v = -1;
+  if (v < 0) v = env_u64("GPUSHARE_SHIM_FREE_ALLOCS_AT_EXIT", 0) ? 1 : 0;
+  return v == 1;
+}
+
+void alloc_note(int kfd, uint64_t handle, uint32_t gpu_id) {
+  KfdImportArgs a{};
+  a.handle = handle;
+  a.gpu_id = gpu_id;
+  import_note(kfd, &a, kTagAlloc);
+}
+
 void import_forget(uint64_t handle) {
   pthread_mutex_lock(&g_imp_mu);
   int n = g_nimports.load(std::memory_order_relaxed);
@@ -576,7 +596,14 @@ int ioctl_body(ioctl_t f, int fd, unsigned long req, void* arg) {
   if ((req != kIocAlloc && req != kIocFree && req != kDrmGemCreate && req != kDrmGemClose &&
        req != kDrmPrimeHandleToFd) || !arg || env_mode() != kModeKfd || g_initializing.load(std::memory_order_acquire))
     return f(fd, req, arg);
-  if (req == kIocAlloc && !(static_cast<KfdAllocArgs*>(arg)->flags & kKfdVram)) return f(fd, req, arg);
+  if (req == kIocAlloc && !(static_cast<KfdAllocArgs*>(arg)->flags & kKfdVram)) {
+    int r = f(fd, req, arg);
+    if (r == 0 && free_allocs_at_exit()) {
+      auto* a = static_cast<KfdAllocArgs*>(arg);
+      alloc_note(fd, a->handle, a->gpu_id);
+    }
+    return r;
+  }
   if ((req == kDrmGemClose || req == kDrmPrimeHandleToFd) && g_gem_live.load(std::memory_order_relaxed) <= 0)
     return f(fd, req, arg);
   if (!enabled()) return f(fd, req, arg);

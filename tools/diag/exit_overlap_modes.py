@@ -37,6 +37,9 @@ if mode in ("free", "reset") and kind == "full":
 if mode == "reset":
     lib = next(ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64" in ln)
     ctypes.CDLL(lib).hipDeviceReset()
+if mode in ("shimfast", "shimfastall"):   # the quota shim's fast exit: queues (and buffers) freed here
+    torch.cuda.synchronize()
+    ctypes.CDLL(None).gpushare_shim_fast_exit_release()
 print(json.dumps({"leaving": True}), flush=True)
 os._exit(0)
 """
@@ -113,8 +116,13 @@ def trial(mode: str, when: str, pause_s: float, cpus: tuple = ("", "")) -> dict:
     st = subprocess.Popen([sys.executable, "-c", STARTER], stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True,
                           env=dict(os.environ, GS_CPU=cpus[1]))
     assert st.stdout.readline().strip() == "go"
+    tenv = dict(os.environ, GS_CPU=cpus[0])
+    if mode.startswith("shim"):                # the tenant under the quota shim (kfd mode)
+        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        tenv.update(LD_PRELOAD=os.path.join(root, "aliyun_gpushare_device_plugin_amd", "_native", "libgpushare_hipquota.so"),
+                    GPUSHARE_QUOTA_BYTES=str(200 << 30), GPUSHARE_SHIM_FREE_ALLOCS_AT_EXIT="1" if mode == "shimfastall" else "0")
     t = subprocess.Popen([sys.executable, "-c", TENANT], stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True,
-                         env=dict(os.environ, GS_CPU=cpus[0]))
+                         env=tenv)
     assert json.loads(t.stdout.readline())["ready"]
     t0 = time.perf_counter()
     t.stdin.write(mode + "\n")

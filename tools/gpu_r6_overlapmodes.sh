@@ -1,3 +1,3 @@
 set -o pipefail
-O=gpurun_out/r6om7; mkdir -p $O
-timeout -k 10 500 python -u tools/diag/exit_overlap_modes.py --trials 3 --tenants initonly,small,full > $O/tenants.jsonl 2> $O/tenants.err
+O=gpurun_out/r6om8; mkdir -p $O
+timeout -k 10 600 python -u tools/diag/exit_overlap_modes.py --trials 3 --modes shim,shimfast,shimfastall --whens reaped > $O/shimfast.jsonl 2> $O/shimfast.err
