@@ -225,7 +225,19 @@ def native_share(before: dict | None, after: dict | None) -> dict | None:
                           if k != "last_fixes" and v - (b.get("gen_bumps") or {}).get(k, 0)},
             # the placement fixes behind them (the plugin's last 16, newest last)
             "placement_fixes": [f for f in (a.get("gen_bumps") or {}).get("last_fixes", [])
-                                if f not in (b.get("gen_bumps") or {}).get("last_fixes", [])]}
+                                if f not in (b.get("gen_bumps") or {}).get("last_fixes", [])],
+            # the plugin's cyclic-GC collections in the window, by generation, and their time
+            # (plugin/manager.py time_gc; max_us is over the plugin's life)
+            "plugin_gc": _gc_delta(b.get("gc"), a.get("gc"))}
+
+
+def _gc_delta(b: dict | None, a: dict | None) -> dict | None:
+    if not a:
+        return None
+    b = b or {"collections": [0, 0, 0], "ns": [0, 0, 0]}
+    return {"collections": [x - y for x, y in zip(a["collections"], b["collections"])],
+            "us": [round((x - y) / 1e3, 1) for x, y in zip(a["ns"], b["ns"])],
+            "max_us": round(a.get("max_ns", 0) / 1e3, 1)}
 
 
 def pod_timeline(port: int, commits: dict) -> dict | None:
