@@ -50,13 +50,54 @@ def _shim() -> dict | None:
     return st
 
 
+_KFD_PROC: list = []
+
+
+def _kfd_proc_dir() -> str | None:
+    """This process's directory under ``/sys/class/kfd/kfd/proc``. KFD names it by the pid in the
+    host's namespace, which is not ``os.getpid()`` inside a container; the process is then found
+    by its PASID: the amdgpu VM that KFD took over is the one of the render node the runtime
+    opened, and that file's fdinfo names it (``pasid:``)."""
+    import glob
+
+    if _KFD_PROC:
+        return _KFD_PROC[0]
+    d = f"/sys/class/kfd/kfd/proc/{os.getpid()}"
+    if os.path.isdir(d):
+        _KFD_PROC.append(d)
+        return d
+    pasids = set()
+    for fd in os.listdir("/proc/self/fd"):
+        try:
+            if not os.readlink(f"/proc/self/fd/{fd}").startswith("/dev/dri/renderD"):
+                continue
+            with open(f"/proc/self/fdinfo/{fd}") as fh:
+                for line in fh:
+                    if line.startswith("pasid:"):
+                        pasids.add(line.split(":", 1)[1].strip())
+        except OSError:
+            continue
+    for p in glob.glob("/sys/class/kfd/kfd/proc/*/pasid"):
+        try:
+            with open(p) as fh:
+                if fh.read().strip() in pasids:
+                    _KFD_PROC.append(os.path.dirname(p))
+                    return _KFD_PROC[0]
+        except OSError:
+            continue
+    return None
+
+
 def _evicted_ms() -> dict:
     """KFD's per-GPU count of how long this process's queues were evicted (ms): memory a KFD
     process maps being moved or validated by another process stops all of its queues."""
     import glob
 
     out = {}
-    for f in glob.glob(f"/sys/class/kfd/kfd/proc/{os.getpid()}/stats_*/evicted_ms"):
+    d = _kfd_proc_dir()
+    if d is None:
+        return out
+    for f in glob.glob(f"{d}/stats_*/evicted_ms"):
         try:
             with open(f) as fh:
                 out[f.split("/")[-2]] = int(fh.read().strip() or 0)
@@ -77,6 +118,8 @@ def main(argv=None):
     ap.add_argument("--mode", default="prefill", choices=("prefill", "decode"))
     ap.add_argument("--decode-window", type=int, default=256, help="decode steps before rewinding to the prompt")
     ap.add_argument("--eager", action="store_true", help="decode: launch kernel by kernel instead of a hipGraph")
+    ap.add_argument("--stream-priority", default=os.environ.get("GPUSHARE_STREAM_PRIORITY", "normal"),
+                    choices=("normal", "high"), help="decode: the priority of the stream the steps run on")
     ap.add_argument("--graph", action="store_true",
                     help="decode: replay a hipGraph even under CU slots (default: eager when GPUSHARE_CU_SLOTS is "
                          "set, since graph replay in a CU-masked pod stalls next to a busy neighbour: "
@@ -106,7 +149,7 @@ def main(argv=None):
     if a.mode == "decode":
         from .llama_serve import LlamaServer
 
-        srv = LlamaServer(model, a.batch, a.seq + a.decode_window + 1)
+        srv = LlamaServer(model, a.batch, a.seq + a.decode_window + 1, priority=a.stream_priority)
         srv.prefill(tok)
         if not a.eager:
             srv.capture()
@@ -126,7 +169,7 @@ def main(argv=None):
                  probe_denied=((_shim() or {}).get("denied") or 0) - d0)
         torch.cuda.empty_cache()
     ev0 = _evicted_ms()
-    emit(event="ready", evicted_ms=ev0)
+    emit(event="ready", evicted_ms=ev0, kfd_proc=_kfd_proc_dir())
     if a.start_file:
         while not os.path.exists(a.start_file):
             time.sleep(0.01)

@@ -25,8 +25,17 @@ from .llama import LlamaModel
 
 
 class LlamaServer:
-    def __init__(self, model: LlamaModel, batch: int, max_ctx: int, gemm: str = "skinny"):
+    def __init__(self, model: LlamaModel, batch: int, max_ctx: int, gemm: str = "skinny",
+                 priority: str = "normal"):
         c = self.cfg = model.cfg
+        # "high": decode steps (eager or graph replay) go to a high-priority stream, so the
+        # hardware queue scheduler dispatches their workgroups ahead of a co-located pod's
+        # normal-priority work as CUs free up (a decode step is hundreds of small kernels, each
+        # of which otherwise waits behind the neighbour's in-flight GEMM)
+        if priority not in ("normal", "high"):
+            raise ValueError("priority must be 'normal' or 'high'")
+        self.stream = (torch.cuda.Stream(model.device, priority=torch.cuda.Stream.priority_range()[1])
+                       if priority == "high" and str(model.device).startswith("cuda") else None)
         if gemm not in ("skinny", "hipblaslt") or (gemm == "skinny" and batch > 64):
             raise ValueError("gemm must be 'skinny' (batch <= 64) or 'hipblaslt'")
         self.gemm = gemm
@@ -148,7 +157,7 @@ class LlamaServer:
         self.tok.copy_(save[0])
         self.pos.copy_(save[1])
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with torch.cuda.graph(g, stream=self.stream):
             self.logits = self._step()
         self.tok.copy_(save[0])
         self.pos.copy_(save[1])
@@ -166,6 +175,16 @@ class LlamaServer:
         if self.host_len + 1 > self.max_ctx:
             raise RuntimeError("context full")
         self.host_len += 1
+        if self.stream is not None:
+            cur = torch.cuda.current_stream(self.model.device)
+            self.stream.wait_stream(cur)
+            with torch.cuda.stream(self.stream):
+                out = self._replay_or_step(use_graph)
+            cur.wait_stream(self.stream)
+            return out
+        return self._replay_or_step(use_graph)
+
+    def _replay_or_step(self, use_graph: bool) -> torch.Tensor:
         if use_graph:
             if self.graph is None:
                 self.capture()

@@ -83,6 +83,29 @@ def test_decode_steps_match_full_recompute_and_graph_matches_eager():
     assert graph.host_len == 43 and int(graph.pos[0]) == 43
 
 
+@pytest.mark.parametrize("use_graph", [False, True])
+def test_high_priority_stream_steps_match_the_normal_ones(use_graph):
+    """Decode steps on a high-priority stream (``priority="high"``, eager or graph replay) give
+    the same tokens and logits as on the current stream, and the caller's stream sees them."""
+    from aliyun_gpushare_device_plugin_amd.models.llama_serve import LlamaServer
+
+    model = _small_model()
+    torch.manual_seed(1)
+    prompt = torch.randint(0, model.cfg.vocab, (4, 33), device="cuda")
+    hi, lo = LlamaServer(model, 4, 128, priority="high"), LlamaServer(model, 4, 128)
+    assert hi.stream is not None and hi.stream.priority == torch.cuda.Stream.priority_range()[1]
+    assert lo.stream is None
+    hi.prefill(prompt)
+    lo.prefill(prompt)
+    for _ in range(4):
+        a = hi.step(use_graph=use_graph).float().clone()      # read on the caller's stream, no sync
+        b = lo.step(use_graph=use_graph).float()
+        assert (a - b).abs().max().item() <= 1e-2 * b.abs().max().item()
+        assert torch.equal(hi.tok, lo.tok)
+    with pytest.raises(ValueError):
+        LlamaServer(model, 4, 128, priority="urgent")
+
+
 _SKINNY_SHAPES = [(1, 256, 512), (7, 512, 4096), (16, 1024, 1024), (32, 4096, 4096),
                   (33, 6144, 4096), (64, 256, 14336), (32, 4096, 14336), (5, 192, 96)]
 

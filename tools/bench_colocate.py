@@ -150,6 +150,8 @@ def run_mode(args, isolation: str, hbm_dir: str | None = None, broker=None) -> d
         if name not in args.arena_pods:               # (experiments) this pod allocates from the driver
             env.pop("GPUSHARE_HBM_TOKEN", None)
             env.pop("GPUSHARE_HBM_BROKER", None)
+        if args.kernarg != "answer":                  # (experiments) override the answer's setting
+            env["HIP_FORCE_DEV_KERNARG"] = "1" if args.kernarg == "device" else "0"
     if args.split_brokers and broker is not None and env_b.get("GPUSHARE_HBM_TOKEN"):
         # (experiment) pod B's granules from a second broker process on the same GPU
         from aliyun_gpushare_device_plugin_amd.quota.hbmbroker import HBMBroker
@@ -164,7 +166,8 @@ def run_mode(args, isolation: str, hbm_dir: str | None = None, broker=None) -> d
         run_mode.second = b2
     extra_b = ["--batch", str(args.batch_b)] if args.batch_b else []
     extra_a = (["--mode", args.mode_a] + (["--seq", str(args.seq_a)] if args.seq_a else [])
-               + (["--eager"] if args.decode_eager else []))
+               + (["--eager"] if args.decode_eager else [])
+               + (["--stream-priority", args.priority_a] if args.mode_a == "decode" else []))
     solo = run_pods([("llama-a", env_a, ["--probe-quota"] + extra_a)], args.seconds, args)[0]
     both = run_pods([("llama-a", env_a, extra_a), ("llama-b", env_b, extra_b)], args.seconds, args)
     solo_b = run_pods([("llama-b", env_b, extra_b)], args.seconds, args)[0] if args.batch_b else None
@@ -247,6 +250,11 @@ def main():
                     help="with --hbm-broker: which pods take their arena (experiments: a, b, ab, none)")
     ap.add_argument("--split-brokers", action="store_true",
                     help="(experiment) pod B takes its granules from a second broker process")
+    ap.add_argument("--priority-a", default="normal", choices=("normal", "high"),
+                    help="decode pod A's stream priority (its steps, eager or graph replay)")
+    ap.add_argument("--kernarg", default="answer", choices=("answer", "device", "host"),
+                    help="(diagnosis) kernel arguments in device or host memory for both pods, "
+                         "instead of what the Allocate answer sets")
     ap.add_argument("--profile-dir", default=None, help="(diagnosis) run the colocated pod A under rocprofv3")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
