@@ -153,6 +153,9 @@ def main(argv=None):
         srv.prefill(tok)
         if not a.eager:
             srv.capture()
+        if srv.stream is not None:                    # every step on it, no per-step hand-off
+            torch.cuda.synchronize()
+            torch.cuda.set_stream(srv.stream)
     else:
         model.forward(tok)
     torch.cuda.synchronize()

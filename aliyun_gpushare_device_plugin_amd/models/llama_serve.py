@@ -175,7 +175,8 @@ class LlamaServer:
         if self.host_len + 1 > self.max_ctx:
             raise RuntimeError("context full")
         self.host_len += 1
-        if self.stream is not None:
+        if self.stream is not None and torch.cuda.current_stream(self.model.device) != self.stream:
+            # (a caller that made self.stream its current stream pays no hand-off per step)
             cur = torch.cuda.current_stream(self.model.device)
             self.stream.wait_stream(cur)
             with torch.cuda.stream(self.stream):

@@ -102,6 +102,11 @@ def test_high_priority_stream_steps_match_the_normal_ones(use_graph):
         b = lo.step(use_graph=use_graph).float()
         assert (a - b).abs().max().item() <= 1e-2 * b.abs().max().item()
         assert torch.equal(hi.tok, lo.tok)
+    with torch.cuda.stream(hi.stream):                 # the caller on the server's own stream
+        a = hi.step(use_graph=use_graph).float().clone()
+    b = lo.step(use_graph=use_graph).float()
+    torch.cuda.synchronize()
+    assert (a - b).abs().max().item() <= 1e-2 * b.abs().max().item()
     with pytest.raises(ValueError):
         LlamaServer(model, 4, 128, priority="urgent")
 
